@@ -1,0 +1,138 @@
+/*
+ * tw_whisper.h — C-ABI of the MI355X (gfx950) Whisper batch-transcription hot path.
+ *
+ * The reference (crmorton/Turbo-Whisper-Workspace) has no native code: its hot path is the
+ * Hugging Face ASR pipeline it builds in AudioProcessingPipeline.load_transcription_model
+ * (/root/reference/vocalis/core/audio_pipeline.py:171-208) and calls at exactly one site
+ * (:351-358). The arithmetic it executes lives in transformers ($TF =
+ * site-packages/transformers, 5.15.0 here; reference pins 4.54.1). Each entry point below
+ * replaces one stage of that executed path and cites it. The Python host layer
+ * (turbo-whisper-workspace_amd/twamd) binds these symbols with ctypes and mirrors the reference's
+ * callable / AudioProcessingPipeline interface on top of them.
+ *
+ * Conventions: plain pointers to DEVICE memory (HBM) unless noted, sizes in elements, bf16 passed
+ * as raw uint16_t, `stream` is a hipStream_t (NULL = legacy default stream). Every function
+ * returns 0 on success, nonzero on failure; tw_last_error() describes the failure (thread-local).
+ * No function allocates, frees or synchronises: all are hipGraph-capturable.
+ */
+#ifndef TW_WHISPER_H
+#define TW_WHISPER_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TW_ABI_VERSION 1
+
+/* GEMM epilogues (tw_gemm_bf16). out/ldo are interpreted per epilogue. */
+#define TW_EPI_BF16 0         /* out bf16[M][ldo] = acc + bias                                  */
+#define TW_EPI_GELU_BF16 1    /* out bf16 = gelu_erf(acc + bias)             (fc1, conv1)       */
+#define TW_EPI_RESID_F32 2    /* out f32[M][ldo] += acc + bias               (o-proj, fc2)      */
+#define TW_EPI_GELU_POS_F32 3 /* out f32 = gelu(acc+bias) + aux[m % aux_rows][n] (conv2 + pos)  */
+#define TW_EPI_F32 4          /* out f32 = acc + bias                        (proj_out logits)  */
+#define TW_EPI_CROSSKV 5      /* out bf16 scattered to [layer][k|v][b][head][s][64]             */
+
+/* Decoder per-row state (tw_logits_select), int32[TW_STATE_STRIDE] per batch row. */
+#define TW_STATE_STRIDE 8
+#define TW_ST_NGEN 0     /* tokens generated so far in this decode pass                         */
+#define TW_ST_LAST 1     /* last generated token                                                */
+#define TW_ST_PENULT 2   /* penultimate generated token                                         */
+#define TW_ST_LASTTS 3   /* last generated timestamp token id, -1 if none                       */
+#define TW_ST_FINISHED 4 /* 1 once EOS was produced or max length reached                       */
+#define TW_ST_LANG 5     /* language id chosen by mode-1 selection                              */
+
+typedef struct TwSelectParams {
+  int32_t V;                  /* vocabulary size                                                 */
+  int32_t eos;                /* eos_token_id (50257 multilingual)                               */
+  int32_t pad;                /* pad_token_id (== eos for Whisper)                               */
+  int32_t ts_begin;           /* no_timestamps_token_id + 1                                      */
+  int32_t no_timestamps;      /* <|notimestamps|>                                               */
+  int32_t max_initial_ts;     /* max_initial_timestamp_index, -1 = None                         */
+  int32_t use_timestamps;     /* WhisperTimeStampLogitsProcessor active (return_timestamps)     */
+  int32_t max_new;            /* finish after this many generated tokens (max_length - begin)   */
+  int32_t mode;               /* 0 = generation step, 1 = language detection argmax in [lo,hi)  */
+  int32_t lo, hi;             /* mode 1 range (language token ids)                              */
+  int32_t n_begin_suppress;   /* <= 8                                                            */
+  int32_t begin_suppress[8];  /* begin_suppress_tokens (e.g. 220, eos)                          */
+} TwSelectParams;
+
+/* ---- runtime ------------------------------------------------------------------------------- */
+int tw_version(void);
+const char* tw_last_error(void);
+
+/* Seeded synthetic parameters (bf16-exact values). as_f32: write f32 instead of bf16.
+ * Replaces: loading `openai/whisper-*` weights through transformers.pipeline
+ * (/root/reference/vocalis/core/audio_pipeline.py:195-200) when no checkpoint is on disk. */
+int tw_fill_synth(void* out, long n, uint64_t seed, uint32_t tensor_id, float scale, float offset, int as_f32,
+                  void* stream);
+/* out[i] = bf16(in[i] * scale) (checkpoint conversion; q-projection 0.125 fold). */
+int tw_f32_to_bf16(const float* in, uint16_t* out, long n, float scale, void* stream);
+
+/* ---- front end ------------------------------------------------------------------------------ */
+/* Log-mel of n_chunks 30-s windows: wave f32[n_chunks][480000] -> feats f32[n_chunks][n_mels][3000].
+ * basis_cos/basis_sin: f32[400][224] periodic-Hann-windowed DFT basis (cols >= 201 zero);
+ * mel_fb: f32[224][ceil32(n_mels)] slaney filterbank (rows >= 201, cols >= n_mels zero);
+ * maxkeys: u32[n_chunks] workspace. Replaces WhisperFeatureExtractor._torch_extract_fbank_features
+ * ($TF/models/whisper/feature_extraction_whisper.py:135-168), run on the host CPU by the reference. */
+int tw_logmel(const float* wave, int n_chunks, const float* basis_cos, const float* basis_sin, const float* mel_fb,
+              int n_mels, float* feats, uint32_t* maxkeys, void* stream);
+
+/* conv1 im2col with the seek-window slice: out bf16[R*3000][kpad], k = j*n_mels + c, value
+ * feats[row_map[r]][c][seek[r] + t + j - 1] inside [0, 3000 - seek[r]), else 0. row_map/seek may
+ * be NULL (identity / 0). Replaces _get_input_segment ($TF/models/whisper/generation_whisper.py:
+ * 1831-1850) + the Conv1d(k3,p1) input of WhisperEncoder.forward ($TF/.../modeling_whisper.py:618). */
+int tw_im2col_conv1(const float* feats, int n_mels, const int* row_map, const int* seek, int R, int kpad,
+                    uint16_t* out, void* stream);
+/* conv2 im2col (k3, stride 2, pad 1): h1 bf16[R*3000][D] -> out bf16[R*1500][3D], k = j*D + c.
+ * Replaces the Conv1d(k3,s2,p1) input of modeling_whisper.py:619. */
+int tw_im2col_conv2(const uint16_t* h1, int R, int D, uint16_t* out, void* stream);
+
+/* ---- dense ops ------------------------------------------------------------------------------ */
+/* C = A[M][K] . W[N][K]^T (bf16, f32 accumulate) with epilogue `epi` (TW_EPI_*). K % 64 == 0.
+ * kv_geom = {S, B, D, H} for TW_EPI_CROSSKV, else NULL. Replaces nn.Linear / Conv1d of
+ * $TF/models/whisper/modeling_whisper.py:279-282,309 (q,k,v,o), :375-376,444-445 (fc1, fc2),
+ * :566-567 (conv stem), :970,1080 (tied proj_out) and the cross-attention K/V projections
+ * cached by EncoderDecoderCache (:312-335). */
+int tw_gemm_bf16(const uint16_t* A, const uint16_t* W, int M, int N, int K, int lda, int ldw, int epi, void* out,
+                 int ldo, const float* bias, const float* aux, int aux_rows, const int* kv_geom, void* stream);
+/* out bf16[M][D] = LayerNorm(x f32[M][D]) (eps, affine). Replaces nn.LayerNorm (modeling_whisper.py
+ * :371,377,434,443,446,573,682). */
+int tw_layernorm(const float* x, const float* gamma, const float* beta, int M, int D, float eps, uint16_t* out,
+                 void* stream);
+
+/* ---- attention ------------------------------------------------------------------------------ */
+/* Encoder self-attention. qkv bf16[B*S][3*H*64] (q pre-scaled by 64^-0.5) -> out bf16[B*S][H*64].
+ * Replaces WhisperAttention + eager_attention_forward/SDPA for the encoder
+ * (modeling_whisper.py:215-238, 241-356). */
+int tw_attn_encoder(const uint16_t* qkv, int B, int S, int H, uint16_t* out, void* stream);
+/* Decoder self-attention for one new token per row: appends k,v of qkv bf16[B][3D] at pos[b] into
+ * k_cache/v_cache bf16[B][H][max_pos][64] (this layer) and attends over 0..pos[b].
+ * Replaces the causal self-attention + DynamicCache.update of modeling_whisper.py:312-335,448-505. */
+int tw_attn_decode_self(const uint16_t* qkv, int B, int H, int max_pos, const int* pos, uint16_t* k_cache,
+                        uint16_t* v_cache, uint16_t* out, void* stream);
+/* Decoder cross-attention for one query per row over the cached encoder K/V of this layer,
+ * cross_kv bf16[2][Bt][H][S][64]; row b reads slot row_map[b] (NULL = b). */
+int tw_attn_decode_cross(const uint16_t* q, int B, int H, int S, int Bt, const int* row_map, const uint16_t* cross_kv,
+                         uint16_t* out, void* stream);
+
+/* ---- decoder glue --------------------------------------------------------------------------- */
+/* x f32[B][D] = embed_tokens[ids[b]] + embed_positions[pos[b]] (modeling_whisper.py:737,753-762). */
+int tw_embed_decoder(const uint16_t* tok_emb, const uint16_t* pos_emb, const int* ids, const int* pos, int B, int D,
+                     float* x, void* stream);
+/* Whisper logits processors + greedy argmax for B rows of f32 logits (see TwSelectParams; state
+ * int32[B][TW_STATE_STRIDE]; tokens_out int32[B][ld_tokens] receives token n_gen; next_ids int32[B];
+ * pos int32[B] (may be NULL) is incremented so a captured decode step can be replayed unchanged).
+ * `params` is a HOST pointer (passed by value to the kernel). suppress_bits: u32[ceil(V/32)] or NULL.
+ * Replaces GenerationMixin._sample's selection step ($TF/generation/utils.py:2876-2941) with
+ * SuppressTokensAtBegin / SuppressTokens / WhisperTimeStamp processors
+ * ($TF/generation/logits_process.py:1816-2047) and detect_language's argmax
+ * ($TF/models/whisper/generation_whisper.py:1664-1671). */
+int tw_logits_select(const float* logits, int B, int ld_logits, const uint32_t* suppress_bits,
+                     const TwSelectParams* params, int* state, int* tokens_out, int ld_tokens, int* next_ids,
+                     int* pos, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TW_WHISPER_H */

@@ -1,0 +1,386 @@
+"""CPU ORACLE (test infrastructure only) — numpy restatement of the reference's Whisper hot path.
+
+NOT product code: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker. The product path (turbo-whisper-workspace_amd/twamd) never
+imports it and has no CPU fallback.
+
+What it restates (the reference executes transformers 5.15.0 here; it pins 4.54.1 / >=4.30.0,
+see SURVEY.md §8c), float32 / float64 numpy:
+  log-mel            WhisperFeatureExtractor._torch_extract_fbank_features
+                     ($TF/models/whisper/feature_extraction_whisper.py:135-168), mel_filter_bank
+                     ($TF/audio_utils.py:638-729)
+  encoder            WhisperEncoder.forward ($TF/models/whisper/modeling_whisper.py:592-646),
+                     WhisperEncoderLayer (:360-413), WhisperAttention (:241-356)
+  decoder step       WhisperDecoder.forward / WhisperDecoderLayer (:690-795, 416-505), tied proj_out
+  processors         SuppressTokensAtBegin / SuppressTokens / WhisperTimeStamp
+                     ($TF/generation/logits_process.py:1816-2047)
+  greedy loop        GenerationMixin._sample ($TF/generation/utils.py:2783-2941)
+  seek loop          WhisperGenerationMixin.generate / generate_with_fallback / _retrieve_segment
+                     ($TF/models/whisper/generation_whisper.py:785-903, 970-1116, 1977-2074)
+  synthetic weights  tw_fill_synth (turbo-whisper-workspace_amd/csrc/tw_runtime.hip)
+
+Pinning: tests/test_oracle_golden.py checks every function above against golden vectors that
+tests/golden/make_golden.py produced by running transformers itself on the same seeded weights.
+"""
+from __future__ import annotations
+
+import math
+import zlib
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+# ----------------------------------------------------------------------------- synthetic parameters
+_M64 = (1 << 64) - 1
+
+
+def synth_uniform(seed: int, tensor_id: int, n: int, scale: float, offset: float) -> np.ndarray:
+    """Bit-exact numpy restatement of k_fill_synth: bf16-rounded uniform(-1,1)*scale+offset, as f32."""
+    idx = np.arange(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z0 = (np.uint64((seed * 0x9E3779B97F4A7C15) & _M64)
+              ^ np.uint64(((tensor_id + 1) * 0xD1B54A32D192ED03) & _M64))
+        z = z0 + idx * np.uint64(0x9E3779B97F4A7C15)
+        z ^= z >> np.uint64(30)
+        z *= np.uint64(0xBF58476D1CE4E5B9)
+        z ^= z >> np.uint64(27)
+        z *= np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    s = (z >> np.uint64(40)).astype(np.int64) - 8388608
+    u = (2 * s + 1).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    v = (u * np.float32(scale)).astype(np.float32) + np.float32(offset)
+    v = v.astype(np.float32)
+    bits = v.view(np.uint32).astype(np.uint64)
+    rnd = (bits + np.uint64(0x7FFF) + ((bits >> np.uint64(16)) & np.uint64(1))) >> np.uint64(16)
+    return (rnd.astype(np.uint32) << np.uint32(16)).view(np.float32)
+
+
+def param_shapes(D: int, L_enc: int, L_dec: int, F: int, n_mels: int, V: int,
+                 n_src: int = 1500, n_tgt: int = 448) -> List[Tuple[str, Tuple[int, ...]]]:
+    out = [("model.encoder.conv1.weight", (D, n_mels, 3)), ("model.encoder.conv1.bias", (D,)),
+           ("model.encoder.conv2.weight", (D, D, 3)), ("model.encoder.conv2.bias", (D,)),
+           ("model.encoder.embed_positions.weight", (n_src, D))]
+
+    def attn(p):
+        out.extend([(f"{p}.k_proj.weight", (D, D)), (f"{p}.v_proj.weight", (D, D)), (f"{p}.v_proj.bias", (D,)),
+                    (f"{p}.q_proj.weight", (D, D)), (f"{p}.q_proj.bias", (D,)),
+                    (f"{p}.out_proj.weight", (D, D)), (f"{p}.out_proj.bias", (D,))])
+
+    def ln(p):
+        out.extend([(f"{p}.weight", (D,)), (f"{p}.bias", (D,))])
+
+    def mlp(p):
+        out.extend([(f"{p}.fc1.weight", (F, D)), (f"{p}.fc1.bias", (F,)),
+                    (f"{p}.fc2.weight", (D, F)), (f"{p}.fc2.bias", (D,))])
+
+    for i in range(L_enc):
+        p = f"model.encoder.layers.{i}"
+        attn(f"{p}.self_attn"); ln(f"{p}.self_attn_layer_norm"); mlp(p); ln(f"{p}.final_layer_norm")
+    ln("model.encoder.layer_norm")
+    out += [("model.decoder.embed_tokens.weight", (V, D)), ("model.decoder.embed_positions.weight", (n_tgt, D))]
+    for i in range(L_dec):
+        p = f"model.decoder.layers.{i}"
+        attn(f"{p}.self_attn"); ln(f"{p}.self_attn_layer_norm")
+        attn(f"{p}.encoder_attn"); ln(f"{p}.encoder_attn_layer_norm")
+        mlp(p); ln(f"{p}.final_layer_norm")
+    ln("model.decoder.layer_norm")
+    return out
+
+
+def synth_spec(name: str, shape: Tuple[int, ...], D: int) -> Tuple[int, float, float]:
+    tid = zlib.crc32(name.encode()) & 0xFFFFFFFF
+    if "layer_norm" in name:
+        return (tid, 0.2, 1.0) if name.endswith("weight") else (tid, 0.1, 0.0)
+    if name.endswith("embed_tokens.weight"):
+        return tid, (3.0 ** 0.5) * 2.0 / (D ** 0.5), 0.0
+    if name.endswith("embed_positions.weight"):
+        return tid, 0.5, 0.0
+    if name.endswith("bias"):
+        return tid, 0.05, 0.0
+    fan_in = int(np.prod(shape[1:]))
+    return tid, (3.0 / fan_in) ** 0.5, 0.0
+
+
+def synth_state_dict(D, L_enc, L_dec, F, n_mels, V, seed) -> Dict[str, np.ndarray]:
+    sd = {}
+    for name, shape in param_shapes(D, L_enc, L_dec, F, n_mels, V):
+        tid, scale, off = synth_spec(name, shape, D)
+        sd[name] = synth_uniform(seed, tid, int(np.prod(shape)), scale, off).reshape(shape)
+    return sd
+
+
+# ----------------------------------------------------------------------------- log-mel
+def _hz_to_mel(f):
+    f = np.asarray(f, np.float64)
+    return np.where(f >= 1000.0, 15.0 + np.log(np.maximum(f, 1e-300) / 1000.0) * (27.0 / np.log(6.4)), 3.0 * f / 200.0)
+
+
+def _mel_to_hz(m):
+    m = np.asarray(m, np.float64)
+    return np.where(m >= 15.0, 1000.0 * np.exp(np.log(6.4) / 27.0 * (m - 15.0)), 200.0 * m / 3.0)
+
+
+def mel_filters(n_mels: int) -> np.ndarray:
+    pts = _mel_to_hz(np.linspace(_hz_to_mel(0.0), _hz_to_mel(8000.0), n_mels + 2))
+    fft = np.linspace(0, 8000, 201)
+    diff = np.diff(pts)
+    slopes = pts[None, :] - fft[:, None]
+    fb = np.maximum(0.0, np.minimum(-slopes[:, :-2] / diff[:-1], slopes[:, 2:] / diff[1:]))
+    return fb * (2.0 / (pts[2: n_mels + 2] - pts[:n_mels]))[None, :]
+
+
+def log_mel(wave: np.ndarray, n_mels: int) -> np.ndarray:
+    """One 30-s window (padded/truncated to 480000) -> f32 [n_mels][3000]."""
+    x = np.zeros(480000, np.float64)
+    w = np.asarray(wave, np.float32)[:480000]
+    x[: len(w)] = w
+    xp = np.pad(x, (200, 200), mode="reflect")
+    idx = np.arange(3001)[:, None] * 160 + np.arange(400)[None, :]
+    n = np.arange(400)
+    win = 0.5 - 0.5 * np.cos(2 * np.pi * n / 400)
+    spec = np.fft.rfft(xp[idx] * win[None, :], axis=1)          # [3001][201]
+    mag = (np.abs(spec[:-1]) ** 2).T                               # [201][3000]
+    mel = mel_filters(n_mels).T.astype(np.float32).astype(np.float64) @ mag
+    ls = np.log10(np.maximum(mel, 1e-10))
+    ls = np.maximum(ls, ls.max() - 8.0)
+    return ((ls + 4.0) / 4.0).astype(np.float32)
+
+
+# ----------------------------------------------------------------------------- model
+def _gelu(x):
+    from scipy.special import erf
+
+    return 0.5 * x * (1.0 + erf(x / np.sqrt(2.0)))
+
+
+def _ln(x, g, b, eps=1e-5):
+    m = x.mean(-1, keepdims=True)
+    v = ((x - m) ** 2).mean(-1, keepdims=True)
+    return (x - m) / np.sqrt(v + eps) * g + b
+
+
+def _softmax(x):
+    x = x - x.max(-1, keepdims=True)
+    e = np.exp(x)
+    return e / e.sum(-1, keepdims=True)
+
+
+class WhisperOracle:
+    """fp32 numpy Whisper with the HF parameter names."""
+
+    def __init__(self, sd: Dict[str, np.ndarray], heads: int):
+        self.sd = {k: np.asarray(v, np.float32) for k, v in sd.items()}
+        self.H = heads
+        self.D = self.sd["model.encoder.conv1.bias"].shape[0]
+        self.L_enc = sum(1 for k in sd if k.startswith("model.encoder.layers.") and k.endswith("fc1.bias"))
+        self.L_dec = sum(1 for k in sd if k.startswith("model.decoder.layers.") and k.endswith("fc1.bias"))
+
+    def _lin(self, x, p, bias=True):
+        y = x @ self.sd[f"{p}.weight"].T
+        if bias and f"{p}.bias" in self.sd:
+            y = y + self.sd[f"{p}.bias"]
+        return y
+
+    def _mha(self, xq, xkv, p, k=None, v=None):
+        """Multi-head attention; q scaled by head_dim^-0.5 before QK^T (modeling_whisper.py:309)."""
+        H, hd = self.H, self.D // self.H
+        q = self._lin(xq, f"{p}.q_proj") * (hd ** -0.5)
+        if k is None:
+            k = self._lin(xkv, f"{p}.k_proj", bias=False)
+            v = self._lin(xkv, f"{p}.v_proj")
+        T, S = q.shape[0], k.shape[0]
+        qh = q.reshape(T, H, hd).transpose(1, 0, 2)
+        kh = k.reshape(S, H, hd).transpose(1, 0, 2)
+        vh = v.reshape(S, H, hd).transpose(1, 0, 2)
+        o = _softmax(qh @ kh.transpose(0, 2, 1)) @ vh
+        return self._lin(o.transpose(1, 0, 2).reshape(T, self.D), f"{p}.out_proj")
+
+    def conv_stem(self, feats: np.ndarray) -> np.ndarray:
+        """feats [n_mels][3000] -> x [1500][D] (gelu(conv1) -> gelu(conv2) -> + positions)."""
+        sd = self.sd
+
+        def conv(x, w, b, stride):
+            C, T = x.shape
+            xp = np.pad(x, ((0, 0), (1, 1)))
+            To = (T + 2 - 3) // stride + 1
+            cols = np.stack([xp[:, j: j + stride * (To - 1) + 1: stride] for j in range(3)], 0)  # [3][C][To]
+            return np.einsum("ocj,jct->ot", w, cols, optimize=True) + b[:, None]
+
+        h = _gelu(conv(feats.astype(np.float32), sd["model.encoder.conv1.weight"], sd["model.encoder.conv1.bias"], 1))
+        h = _gelu(conv(h.astype(np.float32), sd["model.encoder.conv2.weight"], sd["model.encoder.conv2.bias"], 2))
+        return (h.T + sd["model.encoder.embed_positions.weight"]).astype(np.float32)
+
+    def encode(self, feats: np.ndarray) -> np.ndarray:
+        x = self.conv_stem(feats)
+        for i in range(self.L_enc):
+            p = f"model.encoder.layers.{i}"
+            sd = self.sd
+            h = _ln(x, sd[f"{p}.self_attn_layer_norm.weight"], sd[f"{p}.self_attn_layer_norm.bias"])
+            x = x + self._mha(h, h, f"{p}.self_attn")
+            h = _ln(x, sd[f"{p}.final_layer_norm.weight"], sd[f"{p}.final_layer_norm.bias"])
+            x = x + self._lin(_gelu(self._lin(h, f"{p}.fc1")), f"{p}.fc2")
+            x = x.astype(np.float32)
+        return _ln(x, self.sd["model.encoder.layer_norm.weight"], self.sd["model.encoder.layer_norm.bias"]).astype(np.float32)
+
+    def new_cache(self, enc: np.ndarray) -> dict:
+        cross = []
+        for i in range(self.L_dec):
+            p = f"model.decoder.layers.{i}.encoder_attn"
+            cross.append((self._lin(enc, f"{p}.k_proj", bias=False), self._lin(enc, f"{p}.v_proj")))
+        return {"self": [(np.zeros((0, self.D), np.float32), np.zeros((0, self.D), np.float32))
+                         for _ in range(self.L_dec)], "cross": cross, "len": 0}
+
+    def decoder_step(self, token: int, cache: dict) -> np.ndarray:
+        """One token at position cache['len'] -> f32 logits [V] (updates cache)."""
+        sd, t = self.sd, cache["len"]
+        x = (sd["model.decoder.embed_tokens.weight"][token] + sd["model.decoder.embed_positions.weight"][t])[None, :]
+        for i in range(self.L_dec):
+            p = f"model.decoder.layers.{i}"
+            h = _ln(x, sd[f"{p}.self_attn_layer_norm.weight"], sd[f"{p}.self_attn_layer_norm.bias"])
+            kk, vv = cache["self"][i]
+            kk = np.concatenate([kk, self._lin(h, f"{p}.self_attn.k_proj", bias=False)], 0)
+            vv = np.concatenate([vv, self._lin(h, f"{p}.self_attn.v_proj")], 0)
+            cache["self"][i] = (kk, vv)
+            x = x + self._mha(h, None, f"{p}.self_attn", kk, vv)
+            h = _ln(x, sd[f"{p}.encoder_attn_layer_norm.weight"], sd[f"{p}.encoder_attn_layer_norm.bias"])
+            ck, cv = cache["cross"][i]
+            x = x + self._mha(h, None, f"{p}.encoder_attn", ck, cv)
+            h = _ln(x, sd[f"{p}.final_layer_norm.weight"], sd[f"{p}.final_layer_norm.bias"])
+            x = x + self._lin(_gelu(self._lin(h, f"{p}.fc1")), f"{p}.fc2")
+        cache["len"] = t + 1
+        h = _ln(x, sd["model.decoder.layer_norm.weight"], sd["model.decoder.layer_norm.bias"])
+        return (h @ sd["model.decoder.embed_tokens.weight"].T)[0].astype(np.float32)
+
+
+# ----------------------------------------------------------------------------- generation
+class GenCfg:
+    """The generation fields the Whisper greedy path reads (plain ints, no product imports)."""
+
+    def __init__(self, V, eot, sot, lang_begin, n_lang, transcribe, translate, notimestamps, suppress_tokens,
+                 begin_suppress_tokens, max_initial_timestamp_index=50, max_length=448, multilingual=True):
+        self.V, self.eot, self.sot = V, eot, sot
+        self.lang_begin, self.n_lang = lang_begin, n_lang
+        self.transcribe, self.translate, self.notimestamps = transcribe, translate, notimestamps
+        self.ts_begin = notimestamps + 1
+        self.suppress = list(suppress_tokens)
+        self.begin_suppress = list(begin_suppress_tokens)
+        self.mit = max_initial_timestamp_index
+        self.max_length = max_length
+        self.multilingual = multilingual
+
+
+def process_logits(scores: np.ndarray, sampled: Sequence[int], g: GenCfg, use_ts: bool) -> np.ndarray:
+    """The processor chain of _retrieve_logit_processors applied to one row (f32)."""
+    s = scores.astype(np.float32).copy()
+    n = len(sampled)
+    if n == 0 and g.begin_suppress:
+        s[g.begin_suppress] = -np.inf
+    if g.suppress:
+        s[g.suppress] = -np.inf
+    if use_ts:
+        tb = g.ts_begin
+        s[g.notimestamps] = -np.inf
+        last_ts = n >= 1 and sampled[-1] >= tb
+        pen_ts = n < 2 or sampled[-2] >= tb
+        if last_ts:
+            if pen_ts:
+                s[tb:] = -np.inf
+            else:
+                s[: g.eot] = -np.inf
+        tss = [t for t in sampled if t >= tb]
+        if tss:
+            tl = tss[-1] if (last_ts and not pen_ts) else tss[-1] + 1
+            s[tb:tl] = -np.inf
+        if n == 0:
+            s[:tb] = -np.inf
+            if g.mit is not None:
+                s[tb + g.mit + 1:] = -np.inf
+        with np.errstate(divide="ignore", invalid="ignore"):
+            m = np.max(s)
+            lp = s - (m + np.log(np.sum(np.exp(s - m)))) if np.isfinite(m) else s
+            ts_lp = lp[tb:]
+            mt = np.max(ts_lp)
+            ts_lse = mt + np.log(np.sum(np.exp(ts_lp - mt))) if np.isfinite(mt) else -np.inf
+            if ts_lse > np.max(lp[:tb]):
+                s[:tb] = -np.inf
+    return s
+
+
+def greedy_pass(model: WhisperOracle, enc: np.ndarray, prompt: Sequence[int], max_new: int, g: GenCfg,
+                use_ts: bool, logits_out: Optional[list] = None) -> List[int]:
+    """_sample for one row: returns the generated tokens (incl. the EOS), or up to max_new."""
+    cache = model.new_cache(enc)
+    for t in prompt[:-1]:
+        model.decoder_step(t, cache)
+    logits = model.decoder_step(prompt[-1], cache)
+    out: List[int] = []
+    while True:
+        s = process_logits(logits, out, g, use_ts)
+        if logits_out is not None:
+            logits_out.append((logits.copy(), s))
+        tok = int(np.argmax(s))
+        out.append(tok)
+        if tok == g.eot or len(out) >= max_new:
+            return out
+        logits = model.decoder_step(tok, cache)
+
+
+def detect_language(model: WhisperOracle, enc: np.ndarray, g: GenCfg) -> int:
+    cache = model.new_cache(enc)
+    lg = model.decoder_step(g.sot, cache)
+    m = np.full_like(lg, -np.inf)
+    m[g.lang_begin: g.lang_begin + g.n_lang] = lg[g.lang_begin: g.lang_begin + g.n_lang]
+    return int(np.argmax(m))
+
+
+def retrieve_segment(seq, seek_num_frames, tb):
+    ts = [t >= tb for t in seq]
+    single = ts[-2:] == [False, True]
+    pairs = [i + 1 for i in range(len(seq) - 1) if ts[i] and ts[i + 1]]
+    if pairs:
+        if single:
+            return list(seq), seek_num_frames
+        end = pairs[-1] + 1
+        return list(seq[:end]), (seq[end - 2] - tb) * 2
+    return list(seq), seek_num_frames
+
+
+def generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, task: Optional[str] = "transcribe",
+             language: Optional[int] = None, return_timestamps: bool = True, max_new_tokens: Optional[int] = None,
+             encoder_cache: Optional[dict] = None) -> Tuple[List[int], int]:
+    """Short-form WhisperGenerationMixin.generate for ONE 3000-frame window, num_beams=1.
+    Returns (final token sequence, language id)."""
+    feats = np.asarray(feats, np.float32)
+
+    def enc_at(seek):
+        seg = np.zeros_like(feats)
+        seg[:, : 3000 - seek] = feats[:, seek:]
+        if encoder_cache is not None and seek in encoder_cache:
+            return encoder_cache[seek]
+        e = model.encode(seg)
+        if encoder_cache is not None:
+            encoder_cache[seek] = e
+        return e
+
+    prompt = [g.sot]
+    lang = None
+    if g.multilingual:
+        lang = language if language is not None else detect_language(model, enc_at(0), g)
+        prompt.append(lang)
+        if task is not None:
+            prompt.append(g.transcribe if task == "transcribe" else g.translate)
+        elif language is not None:
+            prompt.append(g.transcribe)
+    if not return_timestamps:
+        prompt.append(g.notimestamps)
+    P = len(prompt)
+    max_new = max_new_tokens if max_new_tokens is not None else min(g.max_length + P, 448) - P
+    seek, out = 0, []
+    while seek < 3000:
+        seq = greedy_pass(model, enc_at(seek), prompt, max_new, g, return_timestamps)
+        if seq and seq[-1] == g.eot:
+            seq = seq[:-1]
+        toks, off = retrieve_segment(seq, 3000 - seek, g.ts_begin)
+        out += toks
+        seek += off
+    return out, lang

@@ -1,0 +1,235 @@
+"""Generate the golden vectors that pin oracle/ and the host logic to the reference's executed code.
+
+Runs transformers (5.15.0 here; the reference's hot path is transformers' Whisper, not vendored in
+/root/reference) on CPU in float32 with the seeded synthetic weights of oracle/whisper_oracle.py and an
+in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores small fixtures:
+
+  logmel.npz        WhisperFeatureExtractor features (128 and 80 mels) of synthetic clips, subsampled
+  model.npz         test-mini encoder output rows, teacher-forced decoder logits top-k, generate() tokens
+  pipeline.json     AutomaticSpeechRecognitionPipeline outputs with the reference's call kwargs
+                    (vocalis/core/audio_pipeline.py:351-358, num_beams=1 for greedy parity) and 30-s mode
+  decode_asr.json   tokenizer._decode_asr on seeded random strided token sequences
+
+Usage: python tests/golden/make_golden.py   (≈1-2 min on 8 CPU cores)
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "turbo-whisper-workspace_amd"))
+
+from oracle import whisper_oracle as wo  # noqa: E402
+from twamd.config import PRESETS, GenerationSettings  # noqa: E402
+from twamd.synth_audio import silence, speech_like, white_noise  # noqa: E402
+from twamd.tokenizer import special_token_strings, synthetic_vocab  # noqa: E402
+
+SEED = 1234
+DIMS = PRESETS["test-mini"]
+
+
+def hf_tokenizer(st):
+    from tokenizers import AddedToken
+    from transformers import WhisperTokenizer
+
+    toks = synthetic_vocab(st)
+    vocab = {t: i for i, t in enumerate(toks[: st.eot])}
+    spec = special_token_strings(st)
+    add = [spec[i] for i in range(st.eot + 1, st.timestamp_begin)]
+    tk = WhisperTokenizer(vocab=vocab, merges=[], additional_special_tokens=add, pad_token="<|endoftext|>")
+    tk.add_tokens([AddedToken(spec[i], special=False, normalized=False) for i in range(st.timestamp_begin, st.vocab)])
+    assert tk.convert_tokens_to_ids("<|notimestamps|>") == st.notimestamps
+    assert sorted(tk.all_special_ids) == st.special_ids()
+    return tk
+
+
+def hf_model(dims, sd_np, gen):
+    from transformers import WhisperConfig, WhisperForConditionalGeneration
+
+    st = gen.special
+    cfg = WhisperConfig(vocab_size=dims.vocab, num_mel_bins=dims.n_mels, encoder_layers=dims.encoder_layers,
+                        encoder_attention_heads=dims.heads, decoder_layers=dims.decoder_layers,
+                        decoder_attention_heads=dims.heads, d_model=dims.d_model, encoder_ffn_dim=dims.ffn,
+                        decoder_ffn_dim=dims.ffn, max_source_positions=1500, max_target_positions=448,
+                        pad_token_id=st.eot, bos_token_id=st.eot, eos_token_id=st.eot,
+                        decoder_start_token_id=st.sot, begin_suppress_tokens=None, suppress_tokens=None)
+    cfg._attn_implementation = "eager"
+    m = WhisperForConditionalGeneration(cfg).eval()
+    sd = {k: torch.from_numpy(v.copy()) for k, v in sd_np.items()}
+    sd["proj_out.weight"] = sd["model.decoder.embed_tokens.weight"]
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    assert all(k == "proj_out.weight" for k in missing), missing
+    gc = m.generation_config
+    gc.decoder_start_token_id = st.sot
+    gc.eos_token_id = st.eot
+    gc.pad_token_id = st.eot
+    gc.bos_token_id = st.eot
+    gc.no_timestamps_token_id = st.notimestamps
+    gc.lang_to_id = st.lang_to_id()
+    gc.task_to_id = {"transcribe": st.transcribe, "translate": st.translate}
+    gc.is_multilingual = st.is_multilingual
+    gc.suppress_tokens = list(gen.suppress_tokens)
+    gc.begin_suppress_tokens = list(gen.begin_suppress_tokens)
+    gc.max_initial_timestamp_index = gen.max_initial_timestamp_index
+    gc.max_length = 448
+    gc.forced_decoder_ids = None
+    return m
+
+
+def clips():
+    return {"speech30": speech_like(30.0, 1234), "noise12": white_noise(12.3, 7), "zeros30": silence(30.0),
+            "speech45": speech_like(45.0, 99)}
+
+
+def make_logmel(out):
+    from transformers import WhisperFeatureExtractor
+
+    res = {}
+    for n_mels in (128, 80):
+        fe = WhisperFeatureExtractor(feature_size=n_mels)
+        for name, x in clips().items():
+            if n_mels == 80 and name != "speech30":
+                continue
+            f = fe(x, sampling_rate=16000, return_tensors="np")["input_features"][0]
+            res[f"feat{n_mels}_{name}_sub"] = f[:, ::15].astype(np.float32)
+            res[f"feat{n_mels}_{name}_rowsum"] = f.sum(axis=1).astype(np.float64)
+    np.savez_compressed(os.path.join(out, "logmel.npz"), **res)
+
+
+def make_model(out):
+    from transformers import WhisperFeatureExtractor
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    st = gen.special
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    cl = clips()
+    feats = np.stack([fe(cl[k], sampling_rate=16000, return_tensors="np")["input_features"][0]
+                      for k in ("speech30", "noise12")])
+    res = {}
+    with torch.no_grad():
+        enc = m.model.encoder(torch.from_numpy(feats)).last_hidden_state.numpy()
+    res["enc_rows_idx"] = np.array([0, 1, 750, 1499])
+    res["enc_rows"] = enc[:, [0, 1, 750, 1499]].astype(np.float32)
+    res["enc_mean"] = enc.mean(axis=(1, 2))
+    res["enc_std"] = enc.std(axis=(1, 2))
+    # generate (short-form, timestamps, greedy) for both clips
+    with torch.no_grad():
+        gen_out = m.generate(torch.from_numpy(feats), task="transcribe", return_timestamps=True, num_beams=1,
+                             max_new_tokens=40, return_segments=True)
+    seqs = gen_out["sequences"].numpy()
+    res["gen_sequences"] = seqs
+    # detected language + teacher-forced logits along the first segment pass of clip 0
+    with torch.no_grad():
+        lang = m.detect_language(input_features=torch.from_numpy(feats)).numpy()
+    res["gen_lang"] = lang
+    first = gen_out["segments"][0][0]["result"]
+    full = first["sequences"] if isinstance(first, dict) else first
+    full = full.numpy().reshape(-1)
+    res["tf_input_ids"] = full[:24]
+    with torch.no_grad():
+        lg = m(input_features=torch.from_numpy(feats[:1]), decoder_input_ids=torch.from_numpy(full[None, :24])).logits[0]
+    lg = lg.numpy()
+    top = np.argsort(-lg, axis=1, kind="stable")[:, :16]
+    res["tf_top_idx"] = top
+    res["tf_top_val"] = np.take_along_axis(lg, top, 1).astype(np.float32)
+    res["tf_lse"] = (np.log(np.exp(lg - lg.max(1, keepdims=True)).sum(1)) + lg.max(1)).astype(np.float64)
+    res["tf_ts_slice"] = lg[:, st.timestamp_begin: st.timestamp_begin + 64].astype(np.float32)
+    np.savez_compressed(os.path.join(out, "model.npz"), **res)
+
+
+def make_pipeline(out):
+    from transformers import AutomaticSpeechRecognitionPipeline, WhisperFeatureExtractor
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    tk = hf_tokenizer(gen.special)
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    pipe = AutomaticSpeechRecognitionPipeline(model=m, feature_extractor=fe, tokenizer=tk, device=-1)
+    audio = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)])  # 75 s
+    cases = []
+    for name, kw in [
+        ("ref_60_5", dict(chunk_length_s=60, stride_length_s=5, batch_size=32)),
+        ("mode_30_0", dict(chunk_length_s=30, stride_length_s=0, batch_size=2)),
+        ("short_nochunk", dict()),
+    ]:
+        x = audio if name != "short_nochunk" else audio[: 20 * 16000]
+        r = pipe(x.copy(), generate_kwargs={"task": "transcribe", "num_beams": 1, "max_new_tokens": 40},
+                 return_timestamps=True, **kw)
+        cases.append({"name": name, "kwargs": kw, "n_samples": int(len(x)), "output": _jsonable(r)})
+    with open(os.path.join(out, "pipeline.json"), "w") as f:
+        json.dump({"seed": SEED, "dims": "test-mini", "audio": "speech_like(40,5)+white_noise(35,11)",
+                   "cases": cases}, f, indent=1)
+
+
+def make_decode_asr(out):
+    from transformers.models.whisper.tokenization_whisper import _decode_asr
+
+    gen = GenerationSettings.default(PRESETS["large-v3-turbo"])
+    st = gen.special
+    tk = hf_tokenizer(st)
+    rng = np.random.Generator(np.random.PCG64(2024))
+    cases = []
+    for ci in range(40):
+        n_chunks = int(rng.integers(1, 5))
+        chunk_len, left, right = (60.0, 5.0, 5.0) if ci % 2 == 0 else (30.0, 0.0, 0.0)
+        outputs = []
+        for k in range(n_chunks):
+            toks = []
+            t = int(rng.integers(0, 50))
+            if ci % 5 == 3:
+                toks.append(st.lang_begin + int(rng.integers(0, 5)))
+            for _ in range(int(rng.integers(0, 6))):
+                toks.append(st.timestamp_begin + t)
+                toks += [int(v) for v in rng.integers(256, 3000, size=int(rng.integers(0, 6)))]
+                t = min(1500, t + int(rng.integers(0, 400)))
+                toks.append(st.timestamp_begin + t)
+                if rng.random() < 0.3:
+                    t = min(1500, t + int(rng.integers(0, 50)))
+            if rng.random() < 0.3:
+                toks += [int(v) for v in rng.integers(256, 3000, size=3)]
+            if rng.random() < 0.4:
+                toks += [st.eot] * int(rng.integers(1, 3))
+            is_first, is_last = k == 0, k == n_chunks - 1
+            stride = (chunk_len if not is_last else chunk_len * float(rng.uniform(0.3, 1.0)),
+                      0.0 if is_first else left, 0.0 if is_last else right)
+            outputs.append({"tokens": toks, "stride": stride})
+        rt = bool(ci % 7 != 6)
+        hf_outs = [{"tokens": torch.tensor([o["tokens"]], dtype=torch.long), "stride": o["stride"]} for o in outputs]
+        text, opt = _decode_asr(tk, hf_outs, return_timestamps=rt, return_language=(ci % 5 == 3),
+                                time_precision=0.02)
+        cases.append({"outputs": outputs, "return_timestamps": rt, "return_language": ci % 5 == 3,
+                      "text": text, "optional": _jsonable(opt)})
+    with open(os.path.join(out, "decode_asr.json"), "w") as f:
+        json.dump(cases, f)
+
+
+def _jsonable(x):
+    if isinstance(x, dict):
+        return {k: _jsonable(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_jsonable(v) for v in x]
+    if isinstance(x, (np.floating, np.integer)):
+        return x.item()
+    return x
+
+
+if __name__ == "__main__":
+    torch.manual_seed(0)
+    torch.set_num_threads(max(1, os.cpu_count() or 1))
+    which = sys.argv[1:] or ["logmel", "model", "pipeline", "decode_asr"]
+    for w in which:
+        globals()[f"make_{w}"](HERE)
+        print("wrote", w)

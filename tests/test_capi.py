@@ -1,0 +1,60 @@
+"""The C-ABI boundary: libtwhip.so builds, loads, and exports exactly what include/tw_whisper.h declares.
+CPU only (no compute calls)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "tw_whisper.h")
+LIB = os.path.join(ROOT, "turbo-whisper-workspace_amd", "twamd", "libtwhip.so")
+
+
+def _declared():
+    src = open(HDR).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(tw_\w+)\s*\(", src, flags=re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib_path():
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "turbo-whisper-workspace_amd", "csrc"), "-j8"], check=True,
+                       capture_output=True)
+    return LIB
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    assert "tw_gemm_bf16" in names and "tw_logits_select" in names and len(names) >= 14
+
+
+def test_library_exports_every_declared_symbol(lib_path):
+    out = subprocess.run(["nm", "-D", "--defined-only", lib_path], check=True, capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (tw_\w+)", out))
+    missing = [n for n in _declared() if n not in exported]
+    assert not missing, missing
+
+
+def test_library_loads_and_binding_matches(lib_path):
+    import torch  # noqa: F401  (HIP runtime first, as the product loads it)
+    from twamd import _lib
+
+    lib = ctypes.CDLL(lib_path)
+    assert lib.tw_version() == 1
+    assert sorted(_lib.EXPORTED) == _declared()
+    assert set(_lib._SIGS) == set(_declared())
+    bound = _lib.load(lib_path)
+    assert bound.tw_version() == 1
+
+
+def test_errors_are_reported_not_raised_in_c(lib_path):
+    import torch  # noqa: F401
+    from twamd import _lib
+
+    _lib.load(lib_path)
+    with pytest.raises(_lib.TwError, match="K % 64"):
+        _lib.call("tw_gemm_bf16", 1, 1, 16, 16, 48, 48, 48, 0, 1, 16, None, None, 0, None, None)
+    with pytest.raises(_lib.TwError, match="null"):
+        _lib.call("tw_logmel", None, 1, None, None, None, 80, None, None, None)

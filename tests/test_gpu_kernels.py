@@ -1,0 +1,240 @@
+"""Per-kernel parity of libtwhip.so on the MI355X, called through the C-ABI.
+
+Integer/bit work (synthetic weights, logits selection) must be exact; floating-point kernels are compared
+with a float32 reference of the same op on the same (bf16-exact) inputs — the oracle for log-mel, torch fp32
+for GEMM / LayerNorm / attention — with the tolerance stated in each test."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import whisper_oracle as wo
+from twamd import _lib
+from twamd.frontend import dft_basis, mel_table
+from twamd.synth_audio import silence, speech_like, white_noise
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def S():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def rand_bf16(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return bf(torch.randn(*shape, generator=g) * scale).to(DEV)
+
+
+def test_fill_synth_bit_exact_vs_oracle():
+    for n, scale, off, as_f32 in ((100003, 0.05, 0.0, 0), (4097, 0.2, 1.0, 1)):
+        t = torch.empty(n, dtype=torch.float32 if as_f32 else torch.bfloat16, device=DEV)
+        _lib.call("tw_fill_synth", t.data_ptr(), n, 1234, 987654321, scale, off, as_f32, S())
+        ref = wo.synth_uniform(1234, 987654321, n, scale, off)
+        got = t.float().cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("n_mels", [128, 80])
+def test_logmel_vs_oracle(n_mels):
+    clips = [speech_like(30.0, 1234), white_noise(12.3, 7), silence(30.0), speech_like(45.0, 99)]
+    B = len(clips)
+    wave = np.zeros((B, 480000), np.float32)
+    for i, c in enumerate(clips):
+        wave[i, : min(len(c), 480000)] = c[:480000]
+    c, s = dft_basis()
+    w = torch.from_numpy(wave).to(DEV)
+    feats = torch.empty(B, n_mels, 3000, device=DEV)
+    mk = torch.empty(B, dtype=torch.int32, device=DEV)
+    bc, bs, fb = (torch.from_numpy(a).to(DEV) for a in (c, s, mel_table(n_mels)))
+    _lib.call("tw_logmel", w.data_ptr(), B, bc.data_ptr(), bs.data_ptr(), fb.data_ptr(), n_mels, feats.data_ptr(),
+              mk.data_ptr(), S())
+    got = feats.cpu().numpy()
+    for i, cl in enumerate(clips):
+        ref = wo.log_mel(cl, n_mels)
+        # f32 DFT-by-MFMA vs float64 FFT: |diff| <= 1e-4 on the (x+4)/4-scaled log10 features
+        np.testing.assert_allclose(got[i], ref, atol=1e-4, rtol=0)
+
+
+EPIS = [_lib.TW_EPI_BF16, _lib.TW_EPI_GELU_BF16, _lib.TW_EPI_RESID_F32, _lib.TW_EPI_F32]
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 384, 256), (1500, 1280, 1280), (24, 1280, 1280), (7, 51866, 384),
+                                   (32, 5120, 1280), (129, 200, 64)])
+@pytest.mark.parametrize("epi", EPIS)
+def test_gemm_vs_torch(M, N, K, epi):
+    A = rand_bf16(M, K, seed=1)
+    W = rand_bf16(N, K, scale=K ** -0.5, seed=2)
+    bias = torch.randn(N, device=DEV) * 0.1
+    ref = A.float() @ W.float().t() + bias
+    if epi in (_lib.TW_EPI_BF16, _lib.TW_EPI_GELU_BF16):
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    else:
+        out = torch.randn(M, N, device=DEV) if epi == _lib.TW_EPI_RESID_F32 else torch.empty(M, N, device=DEV)
+    base = out.clone()
+    _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, K, K, epi, out.data_ptr(), N, bias.data_ptr(),
+              None, 0, None, S())
+    if epi == _lib.TW_EPI_GELU_BF16:
+        ref = torch.nn.functional.gelu(ref)
+    if epi == _lib.TW_EPI_RESID_F32:
+        ref = base + ref
+    tol = 2e-2 if out.dtype == torch.bfloat16 else 2e-3  # bf16 output rounding / f32 accumulation order
+    torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
+
+
+def test_gemm_gelu_pos_and_crosskv():
+    M, N, K = 3000, 256, 768
+    A = rand_bf16(M, K, seed=3)
+    W = rand_bf16(N, K, scale=K ** -0.5, seed=4)
+    bias = torch.randn(N, device=DEV) * 0.1
+    pos = torch.randn(1500, N, device=DEV)
+    out = torch.empty(M, N, device=DEV)
+    _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, K, K, _lib.TW_EPI_GELU_POS_F32, out.data_ptr(), N,
+              bias.data_ptr(), pos.data_ptr(), 1500, None, S())
+    ref = torch.nn.functional.gelu(A.float() @ W.float().t() + bias) + pos.repeat(2, 1)
+    torch.testing.assert_close(out, ref, atol=2e-3, rtol=2e-3)
+    # cross-KV scatter: [B*S][L*2*D] -> [L][2][B][H][S][64]
+    B, Sx, D, H, L = 2, 1500, 256, 4, 2
+    A = rand_bf16(B * Sx, D, seed=5)
+    W = rand_bf16(L * 2 * D, D, scale=D ** -0.5, seed=6)
+    bias = torch.randn(L * 2 * D, device=DEV) * 0.1
+    out = torch.empty(L, 2, B, H, Sx, 64, dtype=torch.bfloat16, device=DEV)
+    geom = (ctypes.c_int * 4)(Sx, B, D, H)
+    _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), B * Sx, L * 2 * D, D, D, D, _lib.TW_EPI_CROSSKV,
+              out.data_ptr(), L * 2 * D, bias.data_ptr(), None, 0, geom, S())
+    ref = (A.float() @ W.float().t() + bias).view(B, Sx, L, 2, H, 64).permute(2, 3, 0, 4, 1, 5)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_layernorm_vs_torch():
+    for M, D in ((3000, 1280), (5, 384), (33, 256)):
+        x = torch.randn(M, D, device=DEV) * 3 + 1
+        g = torch.randn(D, device=DEV)
+        b = torch.randn(D, device=DEV)
+        out = torch.empty(M, D, dtype=torch.bfloat16, device=DEV)
+        _lib.call("tw_layernorm", x.data_ptr(), g.data_ptr(), b.data_ptr(), M, D, 1e-5, out.data_ptr(), S())
+        ref = torch.nn.functional.layer_norm(x, (D,), g, b, 1e-5)
+        torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=1e-2)
+
+
+def _ref_attn(q, k, v):  # [B,H,S,64] fp32, q already scaled
+    return torch.softmax(q @ k.transpose(-1, -2), dim=-1) @ v
+
+
+@pytest.mark.parametrize("B,S,H", [(2, 1500, 4), (1, 100, 2), (1, 1500, 20)])
+def test_encoder_attention_vs_torch(B, S, H):
+    D = H * 64
+    qkv = rand_bf16(B * S, 3 * D, seed=7)
+    qkv[:, :D] = bf(qkv[:, :D].float() * 0.125 * 3)  # scaled q with some dynamic range
+    out = torch.empty(B * S, D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_attn_encoder", qkv.data_ptr(), B, S, H, out.data_ptr(), S())
+    t = qkv.float().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = _ref_attn(t[0], t[1], t[2]).permute(0, 2, 1, 3).reshape(B * S, D)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_encoder_attention_online_softmax_rescale():
+    """Force the running max to jump in a late key tile (rule 26: exercise the rescale branch)."""
+    B, S, H = 1, 1500, 1
+    D = 64
+    qkv = rand_bf16(B * S, 3 * D, scale=0.3, seed=8)
+    qkv[1400, D:2 * D] = bf(qkv[:, :D].float().mean(0) * 0 + 4.0)  # one dominant key in the last tile
+    out = torch.empty(B * S, D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_attn_encoder", qkv.data_ptr(), B, S, H, out.data_ptr(), S())
+    t = qkv.float().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = _ref_attn(t[0], t[1], t[2]).permute(0, 2, 1, 3).reshape(B * S, D)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_decode_attention_self_and_cross():
+    B, H, T = 3, 4, 448
+    D = H * 64
+    kc = torch.zeros(B, H, T, 64, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    pos = torch.tensor([0, 5, 447], dtype=torch.int32, device=DEV)
+    kc[:, :, :447] = rand_bf16(B, H, 447, 64, seed=9)
+    vc[:, :, :447] = rand_bf16(B, H, 447, 64, seed=10)
+    qkv = rand_bf16(B, 3 * D, seed=11)
+    out = torch.empty(B, D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_attn_decode_self", qkv.data_ptr(), B, H, T, pos.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+              out.data_ptr(), S())
+    q = qkv.float().view(B, 3, H, 64)
+    for b in range(B):
+        p = int(pos[b])
+        assert torch.equal(kc[b, :, p], qkv[b, D:2 * D].view(H, 64))
+        k = kc[b, :, : p + 1].float()
+        v = vc[b, :, : p + 1].float()
+        ref = _ref_attn(q[b, 0][:, None, :], k, v)[:, 0].reshape(D)
+        torch.testing.assert_close(out[b].float(), ref, atol=1e-2, rtol=1e-2)
+    # cross
+    Sx, Bt = 1500, 3
+    ckv = rand_bf16(2, Bt, H, Sx, 64, seed=12)
+    qx = rand_bf16(B, D, seed=13)
+    rm = torch.tensor([2, 0, 1], dtype=torch.int32, device=DEV)
+    _lib.call("tw_attn_decode_cross", qx.data_ptr(), B, H, Sx, Bt, rm.data_ptr(), ckv.data_ptr(), out.data_ptr(), S())
+    for b in range(B):
+        s = int(rm[b])
+        ref = _ref_attn(qx[b].float().view(H, 1, 64), ckv[0, s].float(), ckv[1, s].float())[:, 0].reshape(D)
+        torch.testing.assert_close(out[b].float(), ref, atol=1e-2, rtol=1e-2)
+
+
+def _params(V, st, mode=0, max_new=100, use_ts=1):
+    p = _lib.TwSelectParams()
+    p.V, p.eos, p.pad, p.ts_begin, p.no_timestamps = V, st.eot, st.eot, st.timestamp_begin, st.notimestamps
+    p.max_initial_ts, p.use_timestamps, p.max_new, p.mode = 50, use_ts, max_new, mode
+    p.lo, p.hi = st.lang_begin, st.lang_end
+    p.n_begin_suppress = 2
+    p.begin_suppress[0], p.begin_suppress[1] = 220, st.eot
+    return p
+
+
+def test_logits_select_matches_oracle_processors():
+    from twamd.config import GenerationSettings, PRESETS
+
+    gen = GenerationSettings.default(PRESETS["large-v3-turbo"])
+    st = gen.special
+    V = 51866
+    g = wo.GenCfg(V, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate, st.notimestamps,
+                  gen.suppress_tokens, gen.begin_suppress_tokens)
+    bits = np.zeros((V + 31) // 32, np.uint32)
+    for t in gen.suppress_tokens:
+        bits[t >> 5] |= np.uint32(1 << (t & 31))
+    sup = torch.from_numpy(bits.view(np.int32)).to(DEV)
+    rng = np.random.default_rng(5)
+    tb = st.timestamp_begin
+    histories = [[], [tb + 3], [tb + 3, 400], [tb + 3, 400, tb + 20], [tb + 3, 400, tb + 20, tb + 20],
+                 [tb + 3, 400, 401], [tb, 7000, tb + 1500], [500, 600], [tb + 10, tb + 10]]
+    for trial in range(6):
+        B = len(histories)
+        logits = rng.standard_normal((B, V)).astype(np.float32) * (1 + trial)
+        if trial == 5:
+            logits[:, tb:] += 3.0  # push the timestamp log-prob rule
+        state = np.zeros((B, 8), np.int32)
+        for b, h in enumerate(histories):
+            n = len(h)
+            tss = [t for t in h if t >= tb]
+            state[b] = [n, h[-1] if n else -1, h[-2] if n > 1 else -1, tss[-1] if tss else -1, 0, 0, 0, 0]
+        lt = torch.from_numpy(logits).to(DEV)
+        stt = torch.from_numpy(state).to(DEV)
+        toks = torch.zeros(B, 448, dtype=torch.int32, device=DEV)
+        ids = torch.zeros(B, dtype=torch.int32, device=DEV)
+        p = _params(V, st)
+        _lib.call("tw_logits_select", lt.data_ptr(), B, V, sup.data_ptr(), ctypes.byref(p), stt.data_ptr(),
+                  toks.data_ptr(), 448, ids.data_ptr(), None, S())
+        got = ids.cpu().numpy()
+        for b, h in enumerate(histories):
+            s = wo.process_logits(logits[b], h, g, True)
+            assert got[b] == int(np.argmax(s)), (trial, b, h)
+            assert int(toks[b, len(h)]) == got[b]
+        # language mode
+        p = _params(V, st, mode=1)
+        stt.zero_()
+        _lib.call("tw_logits_select", lt.data_ptr(), B, V, sup.data_ptr(), ctypes.byref(p), stt.data_ptr(),
+                  None, 448, ids.data_ptr(), None, S())
+        ref = st.lang_begin + logits[:, st.lang_begin: st.lang_end].argmax(1)
+        assert np.array_equal(ids.cpu().numpy(), ref)

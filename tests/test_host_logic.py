@@ -1,0 +1,148 @@
+"""Host-side logic of the drop-in (CPU): chunk windows, seek-segment bookkeeping, _decode_asr stitching and
+the full TurboTranscriber.__call__ flow with the oracle standing in for the GPU engine."""
+import json
+import os
+
+import numpy as np
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as hs
+
+from oracle import whisper_oracle as wo
+from twamd import audio
+from twamd.config import PRESETS, GenerationSettings, SpecialTokens
+from twamd.frontend import chunk_windows, dft_basis, mel_filterbank, mel_table
+from twamd.pipeline import TurboTranscriber
+from twamd.segments import retrieve_segment, strip_generated
+from twamd.synth_audio import speech_like, white_noise
+from twamd.tokenizer import WhisperVocab, decode_asr
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_special_token_layouts():
+    for v, tb in ((51866, 50365), (51865, 50364), (51864, 50363)):
+        st = SpecialTokens.for_vocab(v)
+        assert st.timestamp_begin == tb and st.timestamp_begin + 1501 == v
+    st = SpecialTokens.for_vocab(51866)
+    assert st.lang_to_id()["<|en|>"] == 50259 and st.lang_to_id()["<|yue|>"] == 50358
+    assert (st.translate, st.transcribe, st.notimestamps) == (50359, 50360, 50364)
+
+
+def test_decode_asr_matches_transformers():
+    cases = json.load(open(os.path.join(G, "decode_asr.json")))
+    vocab = WhisperVocab.synthetic(SpecialTokens.for_vocab(51866))
+    for c in cases:
+        outs = [{"tokens": o["tokens"], "stride": tuple(o["stride"])} for o in c["outputs"]]
+        text, opt = decode_asr(vocab, outs, return_timestamps=c["return_timestamps"],
+                               return_language=c["return_language"])
+        assert text == c["text"]
+        got = json.loads(json.dumps(opt))
+        assert got == c["optional"]
+
+
+@given(n=hs.integers(0, 3_000_000), chunk=hs.sampled_from([30, 60, 10.5]), stride=hs.sampled_from([0, 5, 2.5, None]))
+@settings(max_examples=200, deadline=None)
+def test_chunk_windows_match_chunk_iter(n, chunk, stride):
+    from transformers.pipelines.automatic_speech_recognition import chunk_iter
+
+    class FE:  # records chunk lengths instead of featurising
+        sampling_rate = 16000
+
+        def __call__(self, chunk, **kw):
+            class R(dict):
+                def to(self, dtype):
+                    return self
+            return R(n=len(chunk))
+
+    sl = chunk / 6 if stride is None else stride
+    cl, st_ = int(round(chunk * 16000)), int(round(sl * 16000))
+    if cl < 2 * st_:
+        return
+    ref = [(it["stride"], it["is_last"]) for it in chunk_iter(np.zeros(n, np.float32), FE(), cl, st_, st_)]
+    got = [((w.length, w.stride_left, w.stride_right), w.is_last)
+           for w in chunk_windows(n, chunk, stride)]
+    assert got == ref
+
+
+@given(seq=hs.lists(hs.sampled_from([5, 6, 7, 100, 101, 150, 50257]), max_size=30))
+@settings(max_examples=300, deadline=None)
+def test_retrieve_segment_matches_oracle(seq):
+    seq = strip_generated(seq, 50257)
+    a = retrieve_segment(seq, 0, 3000, 100)
+    b = wo.retrieve_segment(seq, 3000, 100)
+    assert a == b
+    assert a[0] == list(seq[: len(a[0])])
+
+
+def test_strip_generated():
+    assert strip_generated([1, 2, 50257, 50257, 50257], 50257) == [1, 2]
+    assert strip_generated([1, 2, 50257], 50257) == [1, 2]
+    assert strip_generated([1, 2], 50257) == [1, 2]
+
+
+def test_frontend_tables():
+    fb = mel_filterbank(128)
+    from transformers.audio_utils import mel_filter_bank
+
+    ref = mel_filter_bank(201, 128, 0.0, 8000.0, 16000, norm="slaney", mel_scale="slaney")
+    np.testing.assert_allclose(fb, ref, rtol=1e-12, atol=1e-15)
+    c, s = dft_basis()
+    assert c.shape == (400, 224) and not c[:, 201:].any() and not s[:, 201:].any()
+    t = mel_table(80)
+    assert t.shape == (224, 96) and not t[201:].any() and not t[:, 80:].any()
+
+
+def test_wav_roundtrip(tmp_path):
+    x = speech_like(1.5, 3)
+    p = str(tmp_path / "a.wav")
+    audio.write_wav(p, x)
+    y = audio.load_input(p)
+    np.testing.assert_allclose(y, x, atol=1.0 / 32767)
+    y2 = audio.load_input({"array": x, "sampling_rate": 16000})
+    np.testing.assert_array_equal(y2, x)
+    y3 = audio.load_input({"raw": np.stack([x, x]), "sampling_rate": 32000})
+    assert abs(len(y3) - len(x) // 2) <= 1
+
+
+class _OracleTranscriber(TurboTranscriber):
+    """TurboTranscriber whose per-window model work is the fp32 oracle (CPU test of the host flow)."""
+
+    def __init__(self, dims):
+        gen = GenerationSettings.default(dims)
+        self.gen = gen
+        self.vocab = WhisperVocab.synthetic(gen.special)
+        self.sampling_rate = 16000
+        st = gen.special
+        self.g = wo.GenCfg(dims.vocab, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate,
+                           st.notimestamps, gen.suppress_tokens, gen.begin_suppress_tokens)
+        sd = wo.synth_state_dict(dims.d_model, dims.encoder_layers, dims.decoder_layers, dims.ffn, dims.n_mels,
+                                 dims.vocab, 1234)
+        self.m = wo.WhisperOracle(sd, dims.heads)
+        self.n_mels = dims.n_mels
+
+        class _E:
+            class d:
+                max_source_positions = 1500
+        self.engine = _E()
+
+    def transcribe_windows(self, wav, windows, task, lang_id, return_timestamps, max_new_tokens=None):
+        out = []
+        for w in windows:
+            f = wo.log_mel(wav[w.start: w.start + min(w.length, 480000)], self.n_mels)
+            toks, _ = wo.generate(self.m, f, self.g, task=task, language=lang_id,
+                                  return_timestamps=return_timestamps, max_new_tokens=max_new_tokens)
+            out.append(toks)
+        return out
+
+
+@pytest.mark.slow
+def test_pipeline_host_flow_matches_transformers_pipeline():
+    gold = json.load(open(os.path.join(G, "pipeline.json")))
+    tr = _OracleTranscriber(PRESETS["test-mini"])
+    x = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)])
+    for case in gold["cases"]:
+        xx = x if case["name"] != "short_nochunk" else x[: 20 * 16000]
+        r = tr(xx, generate_kwargs={"task": "transcribe", "num_beams": 1, "max_new_tokens": 40},
+               return_timestamps=True, **case["kwargs"])
+        assert json.loads(json.dumps(r)) == case["output"], case["name"]

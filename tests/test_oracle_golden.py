@@ -1,0 +1,90 @@
+"""Pin the CPU oracle (oracle/whisper_oracle.py) against golden vectors produced by transformers itself
+(tests/golden/make_golden.py, same seeded weights). CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import whisper_oracle as wo
+from twamd.config import PRESETS, GenerationSettings
+from twamd.synth_audio import silence, speech_like, white_noise
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+D = PRESETS["test-mini"]
+
+
+def _clips():
+    return {"speech30": speech_like(30.0, 1234), "noise12": white_noise(12.3, 7), "zeros30": silence(30.0),
+            "speech45": speech_like(45.0, 99)}
+
+
+@pytest.fixture(scope="module")
+def golden_model():
+    return np.load(os.path.join(G, "model.npz"))
+
+
+@pytest.fixture(scope="module")
+def oracle_model():
+    sd = wo.synth_state_dict(D.d_model, D.encoder_layers, D.decoder_layers, D.ffn, D.n_mels, D.vocab, 1234)
+    return wo.WhisperOracle(sd, D.heads)
+
+
+@pytest.fixture(scope="module")
+def gcfg():
+    gen = GenerationSettings.default(D)
+    st = gen.special
+    return wo.GenCfg(D.vocab, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate,
+                     st.notimestamps, gen.suppress_tokens, gen.begin_suppress_tokens)
+
+
+def test_synth_uniform_is_bf16_exact_and_bounded():
+    v = wo.synth_uniform(1234, 77, 100000, 0.05, 0.0)
+    assert np.all(np.abs(v) <= 0.05 * (1 + 2 ** -8))  # bf16 rounding may step just past the scale
+    assert np.all((v.view(np.uint32) & 0xFFFF) == 0)      # bf16-representable
+    assert abs(float(v.std()) - 0.05 / np.sqrt(3)) < 1e-3
+    assert not np.array_equal(v, wo.synth_uniform(1235, 77, 100000, 0.05, 0.0))
+
+
+@pytest.mark.parametrize("n_mels,name", [(128, "speech30"), (128, "noise12"), (128, "zeros30"), (128, "speech45"),
+                                         (80, "speech30")])
+def test_logmel_matches_feature_extractor(n_mels, name):
+    g = np.load(os.path.join(G, "logmel.npz"))
+    f = wo.log_mel(_clips()[name], n_mels)
+    assert f.shape == (n_mels, 3000)
+    np.testing.assert_allclose(f[:, ::15], g[f"feat{n_mels}_{name}_sub"], atol=2e-5, rtol=0)
+    np.testing.assert_allclose(f.sum(axis=1), g[f"feat{n_mels}_{name}_rowsum"], rtol=1e-5, atol=1e-3)
+
+
+def test_encoder_matches_transformers(golden_model, oracle_model):
+    feats = wo.log_mel(speech_like(30.0, 1234), 128)
+    enc = oracle_model.encode(feats)
+    np.testing.assert_allclose(enc[golden_model["enc_rows_idx"]], golden_model["enc_rows"][0], atol=2e-3, rtol=0)
+    assert abs(enc.mean() - golden_model["enc_mean"][0]) < 1e-4
+    assert abs(enc.std() - golden_model["enc_std"][0]) < 1e-4
+
+
+def test_teacher_forced_logits_match(golden_model, oracle_model):
+    feats = wo.log_mel(speech_like(30.0, 1234), 128)
+    enc = oracle_model.encode(feats)
+    cache = oracle_model.new_cache(enc)
+    ids = golden_model["tf_input_ids"]
+    for t, tok in enumerate(ids):
+        lg = oracle_model.decoder_step(int(tok), cache)
+        top = golden_model["tf_top_idx"][t]
+        np.testing.assert_allclose(lg[top], golden_model["tf_top_val"][t], atol=2e-3)
+        assert int(np.argmax(lg)) == int(top[0])
+        m = lg.max()
+        assert abs(float(m + np.log(np.exp(lg - m).sum())) - golden_model["tf_lse"][t]) < 2e-3
+
+
+def test_language_detection_and_generate_match(golden_model, oracle_model, gcfg):
+    clips = _clips()
+    for i, name in enumerate(("speech30", "noise12")):
+        feats = wo.log_mel(clips[name], 128)
+        toks, lang = wo.generate(oracle_model, feats, gcfg, task="transcribe", return_timestamps=True,
+                                 max_new_tokens=40)
+        assert lang == int(golden_model["gen_lang"][i])
+        ref = [int(t) for t in golden_model["gen_sequences"][i]]
+        while ref and ref[-1] == gcfg.eot:
+            ref.pop()
+        assert toks == ref, (name, toks, ref)

@@ -1,0 +1,278 @@
+// Whisper attention on CDNA4.
+//
+// (1) Encoder self-attention (non-causal, S = 1500, 64-wide heads): replaces WhisperAttention +
+//     eager/SDPA attention ($TF/models/whisper/modeling_whisper.py:215-238, 241-356) for the encoder.
+//     Flash-style: one wave = 32 queries, a workgroup = 4 waves = 128 queries of one (batch, head).
+//     The score tile is computed SWAPPED, S^T = K.Q^T with v_mfma_f32_32x32x16_bf16, so each lane holds
+//     16 keys of ONE query: the online-softmax max/sum is lane-local plus one xor-32 shuffle. The f32
+//     accumulator is then converted pairwise to bf16 and used in place as the B operand of O^T = V^T.P^T
+//     (no LDS round trip for P). K tiles are staged row-major with an XOR chunk swizzle; V tiles are
+//     staged transposed ([d][key], row stride 68) so the A operand of the PV product is two
+//     conflict-free ds_read_b64 per fragment. Keys past S are masked to -inf in the last tile.
+//     q is already multiplied by head_dim^-0.5 (folded into the q projection, exact: 0.125 = 2^-3).
+//
+// (2) Decoder single-token attention over the self KV cache (causal by construction: keys 0..t)
+//     and over the cached cross K/V (1500 keys): memory-bound, one workgroup per (batch row, head),
+//     8-lane groups read one 128-byte key/value row per step (coalesced 16 B per lane).
+#include "tw_common.h"
+#include "../../include/tw_whisper.h"
+
+#define EA_KT 64           // keys per tile
+#define EA_VS 68           // transposed-V LDS row stride (bf16): conflict-free ds_read_b64
+#define EA_LOG2E 1.4426950408889634f
+
+__device__ inline int ka_off(int key, int chunk) { return key * 64 + ((chunk ^ (key & 7)) << 3); }
+
+__global__ __launch_bounds__(256) void k_attn_encoder(const bf16_t* __restrict__ qkv, int S, int H, int D,
+                                                      bf16_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) bf16_t ks[EA_KT * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t vts[64 * EA_VS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int ld = 3 * D;
+  const bf16_t* base = qkv + (size_t)b * S * ld;
+  const int q0 = blockIdx.x * 128 + wid * 32;
+
+  // Q^T fragments (B operand): lane holds Q[q = lr][d = 16 s + 8 lh + j]
+  bf16x8 qf[4];
+  {
+    int qi = min(q0 + lr, S - 1);
+    const bf16_t* qp = base + (size_t)qi * ld + h * 64 + 8 * lh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+  }
+  f32x16 o0 = {0}, o1 = {0};   // O^T for d in [0,32) and [32,64): row = d, col = query
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int ntile = (S + EA_KT - 1) / EA_KT;
+  for (int kt = 0; kt < ntile; ++kt) {
+    const int k0 = kt * EA_KT;
+    __syncthreads();  // previous tile fully consumed
+    // stage K (row-major, swizzled) and V^T: 64 keys x 8 chunks = 512 chunks, 2 per thread
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int c = tid + 256 * i;
+      int key = c >> 3, ch = c & 7;
+      int kk = min(k0 + key, S - 1);
+      const bf16_t* rowp = base + (size_t)kk * ld + h * 64 + ch * 8;
+      uint4 kv = *(const uint4*)(rowp + D);
+      uint4 vv = *(const uint4*)(rowp + 2 * D);
+      *(uint4*)(ks + ka_off(key, ch)) = kv;
+      const bf16_t* ve = (const bf16_t*)&vv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vts[(ch * 8 + e) * EA_VS + key] = ve[e];
+    }
+    __syncthreads();
+
+    // S^T = K . Q^T for key halves 0..31 and 32..63
+    f32x16 s0 = {0}, s1 = {0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 ka = *(const bf16x8*)(ks + ka_off(lr, 2 * s + lh));
+      bf16x8 kb = *(const bf16x8*)(ks + ka_off(32 + lr, 2 * s + lh));
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[s], s1, 0, 0, 0);
+    }
+    // mask keys >= S; scale into log2 domain
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      int key = (r & 3) + 8 * (r >> 2) + 4 * lh;
+      float a = (k0 + key < S) ? s0[r] * EA_LOG2E : -INFINITY;
+      float c = (k0 + 32 + key < S) ? s1[r] * EA_LOG2E : -INFINITY;
+      s0[r] = a; s1[r] = c;
+      tmax = fmaxf(tmax, fmaxf(a, c));
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_run, tmax);
+    const float alpha = (m_run == -INFINITY) ? 0.f : exp2f(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = exp2f(s0[r] - m_new);
+      s1[r] = exp2f(s1[r] - m_new);
+      psum += s0[r] + s1[r];
+    }
+    psum += __shfl_xor(psum, 32, 64);
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+
+    // O^T += V^T . P^T ; B operand = P^T registers 8s..8s+7 (keys 16s + 8(j>>2) + 4lh + (j&3))
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float pv = half ? s1[8 * s + j] : s0[8 * s + j];
+          pb[j] = (__bf16)pv;
+        }
+        const int kbase = half * 32 + 16 * s + 4 * lh;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const bf16_t* vp = vts + (db * 32 + lr) * EA_VS + kbase;
+          bf16x4 lo = *(const bf16x4*)(vp);
+          bf16x4 hi = *(const bf16x4*)(vp + 8);
+          bf16x8 va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          if (db == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o0, 0, 0, 0);
+          else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o1, 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  const int q = q0 + lr;
+  if (q < S) {
+    const float inv = 1.f / l_run;
+    bf16_t* op = out + ((size_t)b * S + q) * D + h * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * lh;
+      uint2 w0, w1;
+      w0.x = pack_bf16x2(o0[4 * g] * inv, o0[4 * g + 1] * inv);
+      w0.y = pack_bf16x2(o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
+      w1.x = pack_bf16x2(o1[4 * g] * inv, o1[4 * g + 1] * inv);
+      w1.y = pack_bf16x2(o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
+      *(uint2*)(op + d) = w0;
+      *(uint2*)(op + 32 + d) = w1;
+    }
+  }
+}
+
+extern "C" int tw_attn_encoder(const bf16_t* qkv, int B, int S, int H, bf16_t* out, void* stream) {
+  TW_REQUIRE(qkv && out && B > 0 && S > 0 && H > 0, "tw_attn_encoder: bad args");
+  const int D = H * 64;
+  hipLaunchKernelGGL(k_attn_encoder, dim3(tw_cdiv(S, 128), H, B), dim3(256), 0, (hipStream_t)stream, qkv, S, H, D,
+                     out);
+  return tw_check_launch("tw_attn_encoder");
+}
+
+// ------------------------------------------------------------------------------------------------
+// Decoder: one query per (row, head) against a [n_keys][64] K block and V block.
+// ------------------------------------------------------------------------------------------------
+// Block = 256 threads. Phase 1: 8-lane groups compute q.k for one key row each (32 keys per pass).
+// Phase 2: softmax over <= max_keys scores held in LDS. Phase 3: groups accumulate p.v over their
+// keys (8 dims per lane), then an LDS reduction over the 32 groups.
+#define DA_MAXK 1536
+
+__device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf16_t* K, const bf16_t* V, int nkeys,
+                                  float* sc /*[DA_MAXK] LDS*/, float* part /*[32][64] LDS*/, float* red /*[8]*/,
+                                  float* outv /*[64] f32 LDS*/) {
+  const int tid = threadIdx.x, g = tid >> 3, gl = tid & 7;
+  float qv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) qv[e] = qf[gl * 8 + e];
+  for (int key = g; key < nkeys; key += 32) {
+    uint4 kk = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
+    const bf16_t* ke = (const bf16_t*)&kk;
+    float d = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
+    d += __shfl_xor(d, 1, 64);
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 4, 64);
+    if (gl == 0) sc[key] = d;
+  }
+  __syncthreads();
+  float mx = -INFINITY;
+  for (int i = tid; i < nkeys; i += 256) mx = fmaxf(mx, sc[i]);
+  mx = wave_max(mx);
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float sum = 0.f;
+  for (int i = tid; i < nkeys; i += 256) {
+    float p = __expf(sc[i] - mx);
+    sc[i] = p;
+    sum += p;
+  }
+  sum = wave_sum(sum);
+  __syncthreads();
+  if ((tid & 63) == 0) red[4 + (tid >> 6)] = sum;
+  __syncthreads();
+  const float inv = 1.f / (red[4] + red[5] + red[6] + red[7]);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int key = g; key < nkeys; key += 32) {
+    uint4 vv = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
+    const bf16_t* ve = (const bf16_t*)&vv;
+    const float p = sc[key];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += p * bf16_to_f32(ve[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[g * 64 + gl * 8 + e] = acc[e];
+  __syncthreads();
+  if (tid < 64) {
+    float v = 0.f;
+    for (int gg = 0; gg < 32; ++gg) v += part[gg * 64 + tid];
+    outv[tid] = v * inv;
+  }
+  __syncthreads();
+}
+
+// Self-attention step: qkv [B][3D] bf16 (q pre-scaled), appends k,v at position pos[b] into the cache
+// (layout [B][H][max_pos][64] for K and V of this layer) and attends over positions 0..pos[b].
+__global__ __launch_bounds__(256) void k_attn_decode_self(const bf16_t* __restrict__ qkv, int D, int max_pos,
+                                                          const int* __restrict__ pos, bf16_t* __restrict__ kc,
+                                                          bf16_t* __restrict__ vc, bf16_t* __restrict__ out) {
+  __shared__ float sc[DA_MAXK];
+  __shared__ float part[32 * 64];
+  __shared__ float qf[64];
+  __shared__ float outv[64];
+  __shared__ float red[8];
+  const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x;
+  const int t = pos[b];
+  const bf16_t* row = qkv + (size_t)b * 3 * D + h * 64;
+  bf16_t* K = kc + ((size_t)b * H + h) * max_pos * 64;
+  bf16_t* V = vc + ((size_t)b * H + h) * max_pos * 64;
+  if (threadIdx.x < 64) {
+    qf[threadIdx.x] = bf16_to_f32(row[threadIdx.x]);
+    K[(size_t)t * 64 + threadIdx.x] = row[D + threadIdx.x];
+    V[(size_t)t * 64 + threadIdx.x] = row[2 * D + threadIdx.x];
+  }
+  __threadfence_block();
+  __syncthreads();
+  dec_attend(qf, K, V, t + 1, sc, part, red, outv);
+  if (threadIdx.x < 64) out[(size_t)b * D + h * 64 + threadIdx.x] = f32_to_bf16(outv[threadIdx.x]);
+}
+
+// Cross-attention step: q [B][D] bf16 (pre-scaled); cross K/V layout [kv][Bt][H][S][64] for this layer,
+// batch row b reads block row_map[b] (the encoder batch slot holding that row's audio window).
+__global__ __launch_bounds__(256) void k_attn_decode_cross(const bf16_t* __restrict__ q, int D, int S, int Bt,
+                                                           const int* __restrict__ row_map,
+                                                           const bf16_t* __restrict__ ckv, bf16_t* __restrict__ out) {
+  __shared__ float sc[DA_MAXK];
+  __shared__ float part[32 * 64];
+  __shared__ float qf[64];
+  __shared__ float outv[64];
+  __shared__ float red[8];
+  const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x;
+  const int slot = row_map ? row_map[b] : b;
+  if (threadIdx.x < 64) qf[threadIdx.x] = bf16_to_f32(q[(size_t)b * D + h * 64 + threadIdx.x]);
+  __syncthreads();
+  const bf16_t* K = ckv + (((size_t)0 * Bt + slot) * H + h) * S * 64;
+  const bf16_t* V = ckv + (((size_t)1 * Bt + slot) * H + h) * S * 64;
+  dec_attend(qf, K, V, S, sc, part, red, outv);
+  if (threadIdx.x < 64) out[(size_t)b * D + h * 64 + threadIdx.x] = f32_to_bf16(outv[threadIdx.x]);
+}
+
+extern "C" int tw_attn_decode_self(const bf16_t* qkv, int B, int H, int max_pos, const int* pos, bf16_t* k_cache,
+                                   bf16_t* v_cache, bf16_t* out, void* stream) {
+  TW_REQUIRE(qkv && pos && k_cache && v_cache && out && B > 0 && H > 0, "tw_attn_decode_self: bad args");
+  TW_REQUIRE(max_pos <= DA_MAXK, "tw_attn_decode_self: max_pos %d > %d", max_pos, DA_MAXK);
+  hipLaunchKernelGGL(k_attn_decode_self, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos, pos,
+                     k_cache, v_cache, out);
+  return tw_check_launch("tw_attn_decode_self");
+}
+
+extern "C" int tw_attn_decode_cross(const bf16_t* q, int B, int H, int S, int Bt, const int* row_map,
+                                    const bf16_t* cross_kv, bf16_t* out, void* stream) {
+  TW_REQUIRE(q && cross_kv && out && B > 0 && H > 0 && S > 0 && S <= DA_MAXK, "tw_attn_decode_cross: bad args");
+  hipLaunchKernelGGL(k_attn_decode_cross, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt, row_map,
+                     cross_kv, out);
+  return tw_check_launch("tw_attn_decode_cross");
+}

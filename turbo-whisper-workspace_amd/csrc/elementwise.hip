@@ -1,0 +1,115 @@
+// Row-wise and data-movement kernels of the Whisper hot path:
+//   LayerNorm (nn.LayerNorm eps 1e-5, $TF/models/whisper/modeling_whisper.py:371,377,434,443,446,573,682)
+//   conv-stem im2col (Conv1d k3 p1 / k3 s2 p1, :566-567) incl. the seek-window slice + zero pad of
+//     WhisperGenerationMixin._get_input_segment ($TF/models/whisper/generation_whisper.py:1831-1850)
+//   decoder token + learned-position embedding (:737,753-762)
+#include "tw_common.h"
+#include "../../include/tw_whisper.h"
+
+// One wave per row, f32 in -> bf16 out (the GEMM A operand). Two-pass mean / variance in registers.
+__global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, const float* __restrict__ g,
+                                                   const float* __restrict__ bta, int M, int D, float eps,
+                                                   bf16_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* xr = x + (size_t)row * D;
+  // three streaming passes over the row (the re-reads hit L1/L2); no runtime-indexed register array
+  float s = 0.f;
+  for (int c = lane; c < D; c += 64) s += xr[c];
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+  for (int c = lane; c < D; c += 64) { float d = xr[c] - mean; q += d * d; }
+  const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+  bf16_t* orow = out + (size_t)row * D;
+  for (int c = lane; c < D; c += 64) orow[c] = f32_to_bf16((xr[c] - mean) * rstd * g[c] + bta[c]);
+}
+
+extern "C" int tw_layernorm(const float* x, const float* gamma, const float* beta, int M, int D, float eps, bf16_t* out,
+                            void* stream) {
+  TW_REQUIRE(x && gamma && beta && out && M > 0, "tw_layernorm: bad args");
+  TW_REQUIRE(D % 64 == 0 && D <= 4096, "tw_layernorm: D=%d must be a multiple of 64 and <= 4096", D);
+  hipLaunchKernelGGL(k_layernorm, dim3(tw_cdiv(M, 4)), dim3(256), 0, (hipStream_t)stream, x, gamma, beta, M, D, eps,
+                     out);
+  return tw_check_launch("tw_layernorm");
+}
+
+// conv1 im2col: A[r*3000 + t][k], k = j*n_mels + c (kw-major, weights reordered to match),
+// value = seg[c][t + j - 1] where seg = feats[row_map[r]][:, seek[r]:] zero-padded to 3000 frames.
+__global__ void k_im2col_conv1(const float* __restrict__ feats, int n_mels, const int* __restrict__ row_map,
+                               const int* __restrict__ seek, int R, int kpad, bf16_t* __restrict__ out) {
+  const long total = (long)R * 3000 * kpad;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (; i < total; i += stride) {
+    const int k = (int)(i % kpad);
+    const long m = i / kpad;
+    const int r = (int)(m / 3000), t = (int)(m - (long)r * 3000);
+    float v = 0.f;
+    if (k < 3 * n_mels) {
+      const int j = k / n_mels, c = k - j * n_mels;
+      const int sk = seek ? seek[r] : 0;
+      const int u = t + j - 1;
+      if (u >= 0 && u < 3000 - sk) {
+        const int chunk = row_map ? row_map[r] : r;
+        v = feats[((size_t)chunk * n_mels + c) * 3000 + sk + u];
+      }
+    }
+    out[i] = f32_to_bf16(v);
+  }
+}
+
+extern "C" int tw_im2col_conv1(const float* feats, int n_mels, const int* row_map, const int* seek, int R, int kpad,
+                               bf16_t* out, void* stream) {
+  TW_REQUIRE(feats && out && R > 0 && kpad >= 3 * n_mels && kpad % 64 == 0, "tw_im2col_conv1: bad args");
+  long total = (long)R * 3000 * kpad;
+  unsigned grid = tw_cdiv(total, 256);
+  if (grid > 16384) grid = 16384;
+  hipLaunchKernelGGL(k_im2col_conv1, dim3(grid), dim3(256), 0, (hipStream_t)stream, feats, n_mels, row_map, seek, R,
+                     kpad, out);
+  return tw_check_launch("tw_im2col_conv1");
+}
+
+// conv2 im2col (stride 2): A[r*1500 + t][j*D + c] = h1[r*3000 + 2t + j - 1][c], zero outside [0, 3000).
+__global__ void k_im2col_conv2(const bf16_t* __restrict__ h1, int R, int D, bf16_t* __restrict__ out) {
+  const int cpr = 3 * D / 8;  // 16-byte chunks per output row
+  const long total = (long)R * 1500 * cpr;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (; i < total; i += stride) {
+    const int ch = (int)(i % cpr);
+    const long m = i / cpr;
+    const int r = (int)(m / 1500), t = (int)(m - (long)r * 1500);
+    const int k = ch * 8, j = k / D, c = k - j * D;
+    const int u = 2 * t + j - 1;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (u >= 0 && u < 3000) v = *(const uint4*)(h1 + ((size_t)r * 3000 + u) * D + c);
+    *(uint4*)(out + (size_t)m * 3 * D + k) = v;
+  }
+}
+
+extern "C" int tw_im2col_conv2(const bf16_t* h1, int R, int D, bf16_t* out, void* stream) {
+  TW_REQUIRE(h1 && out && R > 0 && D % 8 == 0, "tw_im2col_conv2: bad args");
+  long total = (long)R * 1500 * (3 * D / 8);
+  unsigned grid = tw_cdiv(total, 256);
+  if (grid > 16384) grid = 16384;
+  hipLaunchKernelGGL(k_im2col_conv2, dim3(grid), dim3(256), 0, (hipStream_t)stream, h1, R, D, out);
+  return tw_check_launch("tw_im2col_conv2");
+}
+
+// x[b][:] = embed_tokens[ids[b]] + embed_positions[pos[b]]  (f32 residual stream)
+__global__ void k_embed_decoder(const bf16_t* __restrict__ tok_emb, const bf16_t* __restrict__ pos_emb,
+                                const int* __restrict__ ids, const int* __restrict__ pos, int D,
+                                float* __restrict__ x) {
+  const int b = blockIdx.x;
+  const bf16_t* te = tok_emb + (size_t)ids[b] * D;
+  const bf16_t* pe = pos_emb + (size_t)pos[b] * D;
+  for (int c = threadIdx.x; c < D; c += blockDim.x) x[(size_t)b * D + c] = bf16_to_f32(te[c]) + bf16_to_f32(pe[c]);
+}
+
+extern "C" int tw_embed_decoder(const bf16_t* tok_emb, const bf16_t* pos_emb, const int* ids, const int* pos, int B,
+                                int D, float* x, void* stream) {
+  TW_REQUIRE(tok_emb && pos_emb && ids && pos && x && B > 0 && D > 0, "tw_embed_decoder: bad args");
+  hipLaunchKernelGGL(k_embed_decoder, dim3(B), dim3(256), 0, (hipStream_t)stream, tok_emb, pos_emb, ids, pos, D, x);
+  return tw_check_launch("tw_embed_decoder");
+}

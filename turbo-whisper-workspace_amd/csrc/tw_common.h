@@ -1,0 +1,75 @@
+// Shared device/host helpers for the MI355X (gfx950) Whisper hot path.
+// Storage conventions: bf16 tensors are raw uint16 (no HIP bf16 class types cross the C-ABI),
+// f32 everywhere else. Every C-ABI entry returns 0 on success or a nonzero tw error code;
+// tw_last_error() gives the message (see include/tw_whisper.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;  // MFMA bf16 operand fragment (8 elems, 4 VGPRs)
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+
+#define TW_WAVE 64
+
+// ---- bf16 <-> f32 (round-to-nearest-even; NaN kept NaN) --------------------------------------
+__host__ __device__ inline float bf16_to_f32(bf16_t h) {
+  union { uint32_t u; float f; } v; v.u = ((uint32_t)h) << 16; return v.f;
+}
+__host__ __device__ inline bf16_t f32_to_bf16(float f) {
+  union { uint32_t u; float f; } v; v.f = f;
+  uint32_t u = v.u;
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+__device__ inline uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+
+// ---- exact-erf GELU (ACT2FN["gelu"] = nn.GELU() = 0.5 x (1 + erf(x/sqrt2))) -----------------
+__device__ inline float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+// ---- wave reductions (64 lanes) ----------------------------------------------------------------
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ inline float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- order-preserving float <-> uint key (for atomicMax over signed floats) ----------------------
+__device__ inline uint32_t f32_order_key(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ inline float f32_from_order_key(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+
+// ---- error plumbing -------------------------------------------------------------------------------
+enum {
+  TW_OK = 0,
+  TW_ERR_ARG = 1,     // bad shape / null pointer / unsupported size
+  TW_ERR_LAUNCH = 2,  // hipGetLastError after launch
+};
+void tw_set_error(const char* fmt, ...);
+int tw_check_launch(const char* what);
+
+#define TW_REQUIRE(cond, ...)            \
+  do {                                   \
+    if (!(cond)) {                       \
+      tw_set_error(__VA_ARGS__);         \
+      return TW_ERR_ARG;                 \
+    }                                    \
+  } while (0)
+
+static inline unsigned tw_cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }

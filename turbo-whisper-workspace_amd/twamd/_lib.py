@@ -1,0 +1,106 @@
+"""ctypes binding of libtwhip.so, the C-ABI declared in include/tw_whisper.h.
+
+The library must be built (`make -C turbo-whisper-workspace_amd/csrc`, or `__graft_entry__.build()`).
+There is deliberately no fallback: if the HIP library is missing every engine entry point raises.
+torch is imported first so that libtwhip.so binds to the HIP runtime torch already loaded
+(both carry SONAME libamdhip64.so.7; the dynamic linker reuses the loaded one).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before ours)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtwhip.so")
+
+TW_EPI_BF16 = 0
+TW_EPI_GELU_BF16 = 1
+TW_EPI_RESID_F32 = 2
+TW_EPI_GELU_POS_F32 = 3
+TW_EPI_F32 = 4
+TW_EPI_CROSSKV = 5
+
+TW_STATE_STRIDE = 8
+TW_ST_NGEN, TW_ST_LAST, TW_ST_PENULT, TW_ST_LASTTS, TW_ST_FINISHED, TW_ST_LANG = 0, 1, 2, 3, 4, 5
+
+# every symbol include/tw_whisper.h declares (tests check the .so exports all of them)
+EXPORTED = (
+    "tw_version", "tw_last_error", "tw_fill_synth", "tw_f32_to_bf16", "tw_logmel", "tw_im2col_conv1",
+    "tw_im2col_conv2", "tw_gemm_bf16", "tw_layernorm", "tw_attn_encoder", "tw_attn_decode_self",
+    "tw_attn_decode_cross", "tw_embed_decoder", "tw_logits_select",
+)
+
+
+class TwSelectParams(ctypes.Structure):
+    _fields_ = [
+        ("V", ctypes.c_int32), ("eos", ctypes.c_int32), ("pad", ctypes.c_int32), ("ts_begin", ctypes.c_int32),
+        ("no_timestamps", ctypes.c_int32), ("max_initial_ts", ctypes.c_int32), ("use_timestamps", ctypes.c_int32),
+        ("max_new", ctypes.c_int32), ("mode", ctypes.c_int32), ("lo", ctypes.c_int32), ("hi", ctypes.c_int32),
+        ("n_begin_suppress", ctypes.c_int32), ("begin_suppress", ctypes.c_int32 * 8),
+    ]
+
+
+class TwError(RuntimeError):
+    pass
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_F = ctypes.c_float
+_U64 = ctypes.c_uint64
+_U32 = ctypes.c_uint32
+
+_SIGS = {
+    "tw_version": ([], _I),
+    "tw_last_error": ([], ctypes.c_char_p),
+    "tw_fill_synth": ([_P, _L, _U64, _U32, _F, _F, _I, _P], _I),
+    "tw_f32_to_bf16": ([_P, _P, _L, _F, _P], _I),
+    "tw_logmel": ([_P, _I, _P, _P, _P, _I, _P, _P, _P], _I),
+    "tw_im2col_conv1": ([_P, _I, _P, _P, _I, _I, _P, _P], _I),
+    "tw_im2col_conv2": ([_P, _I, _I, _P, _P], _I),
+    "tw_gemm_bf16": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _P], _I),
+    "tw_layernorm": ([_P, _P, _P, _I, _I, _F, _P, _P], _I),
+    "tw_attn_encoder": ([_P, _I, _I, _I, _P, _P], _I),
+    "tw_attn_decode_self": ([_P, _I, _I, _I, _P, _P, _P, _P, _P], _I),
+    "tw_attn_decode_cross": ([_P, _I, _I, _I, _I, _P, _P, _P, _P], _I),
+    "tw_embed_decoder": ([_P, _P, _P, _P, _I, _I, _P, _P], _I),
+    "tw_logits_select": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), _P, _P, _I, _P, _P, _P], _I),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) and type the library; raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise TwError(f"HIP library not built: {path} (run `make -C turbo-whisper-workspace_amd/csrc`)")
+    lib = ctypes.CDLL(path)
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args) -> None:
+    """Invoke a tw_* entry point and turn a nonzero return into TwError(tw_last_error())."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise TwError(f"{name} failed ({rc}): {lib.tw_last_error().decode(errors='replace')}")
+
+
+def ptr(t) -> int:
+    """Device (or host) address of a torch tensor, or 0 for None."""
+    return 0 if t is None else t.data_ptr()
+
+
+def stream_handle(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

@@ -1,0 +1,159 @@
+"""Model dimensions, special-token layout and generation settings of the Whisper hot path.
+
+The reference never states these itself: it names a hub checkpoint
+(`openai/whisper-large-v3`, /root/reference/vocalis/core/audio_pipeline.py:171) and lets
+transformers resolve `config.json` / `generation_config.json`. Real checkpoints are not on disk
+here, so the values are restated from the public Whisper model cards (dims) and from transformers'
+Whisper generation logic ($TF/models/whisper/generation_whisper.py). When a local checkpoint
+directory is given, `GenerationSettings.from_checkpoint` reads its own generation_config.json.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+from typing import Dict, List, Optional
+
+# Whisper language codes in token order (<|en|> = first language token). 99 for v1/v2 vocabularies,
+# the v3 vocabulary (51866) adds "yue" as the 100th.
+LANGUAGE_CODES: List[str] = (
+    "en zh de es ru ko fr ja pt tr pl ca nl ar sv it id hi fi vi he uk el ms cs ro da hu ta no th ur hr bg "
+    "lt la mi ml cy sk te fa lv bn sr az sl kn et mk br eu is hy ne mn bs kk sq sw gl mr pa si km sn yo so "
+    "af oc ka be tg sd gu am yi lo uz fo ht ps tk nn mt sa lb my bo tl mg as tt haw ln ha ba jw su yue"
+).split()
+
+
+@dataclasses.dataclass(frozen=True)
+class WhisperDims:
+    """Architecture hyper-parameters (WhisperConfig fields)."""
+
+    name: str
+    d_model: int
+    encoder_layers: int
+    decoder_layers: int
+    heads: int
+    ffn: int
+    n_mels: int
+    vocab: int
+    max_source_positions: int = 1500
+    max_target_positions: int = 448
+
+    @property
+    def head_dim(self) -> int:
+        return self.d_model // self.heads
+
+    def validate(self) -> None:
+        if self.d_model % 64 or self.head_dim != 64:
+            raise ValueError(f"{self.name}: head_dim must be 64 (d_model={self.d_model}, heads={self.heads})")
+        if self.ffn % 128 or self.d_model % 128:
+            raise ValueError(f"{self.name}: d_model/ffn must be multiples of 128")
+
+
+PRESETS: Dict[str, WhisperDims] = {
+    # BASELINE.json configs[1..4]: openai/whisper-large-v3-turbo
+    "large-v3-turbo": WhisperDims("large-v3-turbo", 1280, 32, 4, 20, 5120, 128, 51866),
+    # reference default model name (audio_pipeline.py:171)
+    "large-v3": WhisperDims("large-v3", 1280, 32, 32, 20, 5120, 128, 51866),
+    # BASELINE.json configs[0]: whisper-tiny.en (English-only vocabulary)
+    "tiny.en": WhisperDims("tiny.en", 384, 4, 4, 6, 1536, 80, 51864),
+    "tiny": WhisperDims("tiny", 384, 4, 4, 6, 1536, 80, 51865),
+    "base": WhisperDims("base", 512, 6, 6, 8, 2048, 80, 51865),
+    # small synthetic config used by the parity tests (multilingual v3 vocabulary, 128 mels)
+    "test-mini": WhisperDims("test-mini", 256, 2, 2, 4, 1024, 128, 51866),
+}
+
+
+@dataclasses.dataclass(frozen=True)
+class SpecialTokens:
+    """Token-id layout of a Whisper vocabulary (derived from its size, as the checkpoints lay it out)."""
+
+    vocab: int
+    eot: int
+    sot: int
+    lang_begin: int
+    n_languages: int
+    translate: int
+    transcribe: int
+    startoflm: int
+    startofprev: int
+    nospeech: int
+    notimestamps: int
+    is_multilingual: bool
+
+    @property
+    def timestamp_begin(self) -> int:
+        return self.notimestamps + 1
+
+    @property
+    def lang_end(self) -> int:
+        return self.lang_begin + self.n_languages
+
+    def lang_to_id(self) -> Dict[str, int]:
+        return {f"<|{c}|>": self.lang_begin + i for i, c in enumerate(LANGUAGE_CODES[: self.n_languages])}
+
+    def special_ids(self) -> List[int]:
+        """ids the tokenizer reports in all_special_ids (everything between eot and the timestamps)."""
+        return list(range(self.eot, self.timestamp_begin))
+
+    @staticmethod
+    def for_vocab(vocab: int) -> "SpecialTokens":
+        if vocab == 51866:  # v3: 100 languages
+            n_lang, eot, multi = 100, 50257, True
+        elif vocab == 51865:  # v1/v2 multilingual: 99 languages
+            n_lang, eot, multi = 99, 50257, True
+        elif vocab == 51864:  # English-only (.en): same 99 language tokens, never prompted
+            n_lang, eot, multi = 99, 50256, False
+        else:
+            raise ValueError(f"unsupported Whisper vocabulary size {vocab}")
+        sot = eot + 1
+        lb = sot + 1
+        translate = lb + n_lang
+        transcribe = translate + 1
+        startoflm = transcribe + 1
+        startofprev = startoflm + 1
+        nospeech = startofprev + 1
+        notimestamps = nospeech + 1
+        st = SpecialTokens(vocab, eot, sot, lb, n_lang, translate, transcribe, startoflm, startofprev, nospeech,
+                           notimestamps, multi)
+        if st.timestamp_begin + 1501 != vocab:
+            raise AssertionError(f"timestamp layout mismatch for vocab {vocab}")
+        return st
+
+
+@dataclasses.dataclass
+class GenerationSettings:
+    """The generation_config fields the Whisper path reads (greedy decode, timestamps)."""
+
+    special: SpecialTokens
+    suppress_tokens: List[int]
+    begin_suppress_tokens: List[int]
+    max_initial_timestamp_index: Optional[int] = 50
+    max_length: int = 448
+    max_new_tokens: Optional[int] = None
+    num_beams: int = 1
+
+    @staticmethod
+    def default(dims: WhisperDims) -> "GenerationSettings":
+        st = SpecialTokens.for_vocab(dims.vocab)
+        # Whisper checkpoints suppress a fixed list of punctuation / symbol tokens plus the
+        # control tokens below (translate, transcribe, startoflm, startofprev, nospeech) and sot.
+        # The synthetic default keeps that structure with a short symbol list.
+        sym = [1, 2, 7, 8, 9, 10, 14, 25, 26, 27, 28, 29, 31, 58, 59, 60, 61, 62, 63, 90, 91, 92, 93]
+        ctrl = [st.translate, st.transcribe, st.startoflm, st.startofprev, st.nospeech]
+        return GenerationSettings(special=st, suppress_tokens=sorted(set(sym + [st.sot] + ctrl)),
+                                  begin_suppress_tokens=[220, st.eot])
+
+    @staticmethod
+    def from_checkpoint(path: str, dims: WhisperDims) -> "GenerationSettings":
+        gs = GenerationSettings.default(dims)
+        fn = os.path.join(path, "generation_config.json")
+        if os.path.exists(fn):
+            with open(fn) as f:
+                cfg = json.load(f)
+            if cfg.get("suppress_tokens") is not None:
+                gs.suppress_tokens = list(cfg["suppress_tokens"])
+            if cfg.get("begin_suppress_tokens") is not None:
+                gs.begin_suppress_tokens = list(cfg["begin_suppress_tokens"])
+            gs.max_initial_timestamp_index = cfg.get("max_initial_timestamp_index", gs.max_initial_timestamp_index)
+            gs.max_length = cfg.get("max_length", gs.max_length)
+        return gs

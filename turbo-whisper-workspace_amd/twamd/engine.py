@@ -1,0 +1,371 @@
+"""WhisperEngine: HBM-resident weights and activations, and the hot path as a sequence of C-ABI calls.
+
+Stage map (reference executed path -> this engine):
+  WhisperFeatureExtractor (host CPU in the reference)            -> logmel()          tw_logmel
+  WhisperEncoder.forward  (modeling_whisper.py:592-646)          -> encode()          im2col + GEMM + LN + attention
+  cross-attention K/V of EncoderDecoderCache (:312-335)          -> encode()          one stacked GEMM (CROSSKV)
+  detect_language + _sample loop (generation_whisper.py:1610-1673,
+    $TF/generation/utils.py:2783-2941)                          -> decode_pass()     decoder step + tw_logits_select
+  seek loop of WhisperGenerationMixin.generate (:785-903)         -> generate()        host bookkeeping (segments.py)
+
+Every compute stage is a HIP kernel from libtwhip.so; torch only provides device allocations, the
+stream, and (optionally) hipGraph capture of the per-token decoder step.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import GenerationSettings, WhisperDims
+from .frontend import CHUNK_SAMPLES, N_FRAMES, dft_basis, mel_table
+from .segments import retrieve_segment, strip_generated
+from .weights import PackedWeights
+
+LN_EPS = 1e-5
+S_ENC = 1500
+
+
+@dataclasses.dataclass
+class PassResult:
+    tokens: List[List[int]]      # generated tokens per row (as _sample returns them, before stripping)
+    lang_ids: Optional[List[int]]
+
+
+class WhisperEngine:
+    def __init__(self, weights: PackedWeights, gen: GenerationSettings, max_batch: int = 24,
+                 device: str = "cuda", use_graphs: bool = True):
+        _lib.load()
+        d = weights.dims
+        d.validate()
+        self.d, self.w, self.gen = d, weights, gen
+        self.max_batch = max_batch
+        self.device = torch.device(device)
+        self.use_graphs = use_graphs
+        self.stream = torch.cuda.current_stream(self.device)
+        D, F, H, V, B = d.d_model, d.ffn, d.heads, d.vocab, max_batch
+        dev, bf, f32, i32 = self.device, torch.bfloat16, torch.float32, torch.int32
+        c, s = dft_basis()
+        self.basis_cos = torch.from_numpy(c).to(dev)
+        self.basis_sin = torch.from_numpy(s).to(dev)
+        self.mel_fb = torch.from_numpy(mel_table(d.n_mels)).to(dev)
+        # front end
+        self.wave = torch.zeros(B, CHUNK_SAMPLES, dtype=f32, device=dev)
+        self.feats = torch.zeros(B, d.n_mels, N_FRAMES, dtype=f32, device=dev)
+        self.maxkeys = torch.zeros(B, dtype=torch.int32, device=dev)
+        # encoder activations
+        M3, M15 = B * N_FRAMES, B * S_ENC
+        self.a1 = torch.empty(M3, weights.kpad1, dtype=bf, device=dev)
+        self.h1 = torch.empty(M3, D, dtype=bf, device=dev)
+        self.a2 = torch.empty(M15, 3 * D, dtype=bf, device=dev)
+        self.x = torch.empty(M15, D, dtype=f32, device=dev)
+        self.hln = torch.empty(M15, D, dtype=bf, device=dev)
+        self.qkv = torch.empty(M15, 3 * D, dtype=bf, device=dev)
+        self.att = torch.empty(M15, D, dtype=bf, device=dev)
+        self.ffn = torch.empty(M15, F, dtype=bf, device=dev)
+        self.cross_kv = torch.empty(d.decoder_layers, 2, B, H, S_ENC, 64, dtype=bf, device=dev)
+        # decoder state
+        T = d.max_target_positions
+        self.kcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=bf, device=dev)
+        self.vcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=bf, device=dev)
+        self.xd = torch.empty(B, D, dtype=f32, device=dev)
+        self.hd = torch.empty(B, D, dtype=bf, device=dev)
+        self.qkvd = torch.empty(B, 3 * D, dtype=bf, device=dev)
+        self.qd = torch.empty(B, D, dtype=bf, device=dev)
+        self.attd = torch.empty(B, D, dtype=bf, device=dev)
+        self.ffnd = torch.empty(B, F, dtype=bf, device=dev)
+        self.logits = torch.empty(B, V, dtype=f32, device=dev)
+        self.state = torch.zeros(B, _lib.TW_STATE_STRIDE, dtype=i32, device=dev)
+        self.tokens = torch.zeros(B, T, dtype=i32, device=dev)
+        self.ids = torch.zeros(B, dtype=i32, device=dev)
+        self.pos = torch.zeros(B, dtype=i32, device=dev)
+        self.row_map = torch.zeros(B, dtype=i32, device=dev)
+        self.seek = torch.zeros(B, dtype=i32, device=dev)
+        self.suppress_bits = torch.zeros((V + 31) // 32, dtype=torch.int32, device=dev)
+        self.set_suppress_tokens(gen.suppress_tokens)
+        self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+
+    def set_suppress_tokens(self, tokens: Sequence[int]) -> None:
+        """SuppressTokensLogitsProcessor's list as a device bitmask (in place: captured graphs stay valid)."""
+        V = self.d.vocab
+        bits = np.zeros((V + 31) // 32, np.uint32)
+        for t in tokens:
+            if 0 <= t < V:
+                bits[t >> 5] |= np.uint32(1 << (t & 31))
+        self.suppress_bits.copy_(torch.from_numpy(bits.view(np.int32)))
+        self.gen.suppress_tokens = list(tokens)
+
+    # ------------------------------------------------------------------ helpers
+    @property
+    def _s(self) -> int:
+        return self.stream.cuda_stream
+
+    def _gemm(self, A, W, M, N, K, epi, out, bias=None, aux=None, aux_rows=0, kv_geom=None, lda=None, ldw=None,
+              ldo=None):
+        rec = self._begin_timer(("gemm_skinny" if M <= 32 else "gemm_tile", epi), 2.0 * M * N * K)
+        _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, lda or K, ldw or K, epi, out.data_ptr(),
+                  ldo or N, _lib.ptr(bias), _lib.ptr(aux), aux_rows, kv_geom, self._s)
+        self._end_timer(rec)
+
+    # per-launch HIP-event timing of kernel families (bench roofline; off by default)
+    timers: Optional[dict] = None
+
+    def _begin_timer(self, key, work):
+        if self.timers is None:
+            return None
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(self.stream)
+        return (key, work, a, b)
+
+    def _end_timer(self, rec):
+        if rec is None:
+            return
+        key, work, a, b = rec
+        b.record(self.stream)
+        self.timers.setdefault(key, []).append((work, a, b))
+
+    def timer_summary(self) -> dict:
+        """{family: (launches, total_work, total_ms)} after a synchronize."""
+        torch.cuda.synchronize(self.device)
+        out = {}
+        for k, lst in (self.timers or {}).items():
+            out[k] = (len(lst), sum(w for w, _, _ in lst), sum(a.elapsed_time(b) for _, a, b in lst))
+        return out
+
+    def _ln(self, x, g, b, M, out):
+        _lib.call("tw_layernorm", x.data_ptr(), g.data_ptr(), b.data_ptr(), M, self.d.d_model, LN_EPS,
+                  out.data_ptr(), self._s)
+
+    # ------------------------------------------------------------------ front end
+    def logmel(self, n: int) -> None:
+        """feats[:n] = log-mel of wave[:n] (each row one 30-s window, zero padded)."""
+        _lib.call("tw_logmel", self.wave.data_ptr(), n, self.basis_cos.data_ptr(), self.basis_sin.data_ptr(),
+                  self.mel_fb.data_ptr(), self.d.n_mels, self.feats.data_ptr(), self.maxkeys.data_ptr(), self._s)
+
+    # ------------------------------------------------------------------ encoder
+    def encode(self, R: int, row_map=True, seek=True) -> None:
+        """Encoder over R windows: slot r reads feats[row_map[r]][:, seek[r]:] (zero padded to 3000),
+        then projects every decoder layer's cross-attention K/V into cross_kv (batch stride R)."""
+        d, w = self.d, self.w
+        D, F, H = d.d_model, d.ffn, d.heads
+        M3, M15 = R * N_FRAMES, R * S_ENC
+        _lib.call("tw_im2col_conv1", self.feats.data_ptr(), d.n_mels, self.row_map.data_ptr() if row_map else None,
+                  self.seek.data_ptr() if seek else None, R, w.kpad1, self.a1.data_ptr(), self._s)
+        self._gemm(self.a1, w.conv1_w, M3, D, w.kpad1, _lib.TW_EPI_GELU_BF16, self.h1, bias=w.conv1_b)
+        _lib.call("tw_im2col_conv2", self.h1.data_ptr(), R, D, self.a2.data_ptr(), self._s)
+        self._gemm(self.a2, w.conv2_w, M15, D, 3 * D, _lib.TW_EPI_GELU_POS_F32, self.x, bias=w.conv2_b,
+                   aux=w.pos_enc, aux_rows=S_ENC)
+        for L in w.enc:
+            self._ln(self.x, L.ln1_g, L.ln1_b, M15, self.hln)
+            self._gemm(self.hln, L.wqkv, M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv)
+            rec = self._begin_timer(("attn_encoder", 0), 4.0 * S_ENC * S_ENC * 64 * H * R)
+            _lib.call("tw_attn_encoder", self.qkv.data_ptr(), R, S_ENC, H, self.att.data_ptr(), self._s)
+            self._end_timer(rec)
+            self._gemm(self.att, L.wo, M15, D, D, _lib.TW_EPI_RESID_F32, self.x, bias=L.bo)
+            self._ln(self.x, L.ln2_g, L.ln2_b, M15, self.hln)
+            self._gemm(self.hln, L.w1, M15, F, D, _lib.TW_EPI_GELU_BF16, self.ffn, bias=L.b1)
+            self._gemm(self.ffn, L.w2, M15, D, F, _lib.TW_EPI_RESID_F32, self.x, bias=L.b2)
+        self._ln(self.x, w.enc_ln_g, w.enc_ln_b, M15, self.hln)  # encoder last_hidden_state (bf16)
+        geom = (ctypes.c_int * 4)(S_ENC, R, D, H)
+        self._gemm(self.hln, w.wkv_x, M15, d.decoder_layers * 2 * D, D, _lib.TW_EPI_CROSSKV, self.cross_kv,
+                   bias=w.bkv_x, kv_geom=geom)
+
+    def encoder_output(self, R: int) -> torch.Tensor:
+        """Encoder last_hidden_state of the last encode() (bf16 view [R][1500][D])."""
+        return self.hln[: R * S_ENC].view(R, S_ENC, self.d.d_model)
+
+    # ------------------------------------------------------------------ decoder
+    def decoder_step(self, R: int, with_logits: bool = True) -> None:
+        """One token per row: ids[b] at position pos[b] -> logits[b] (f32)."""
+        d, w = self.d, self.w
+        D, F, H, T = d.d_model, d.ffn, d.heads, d.max_target_positions
+        _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), self.ids.data_ptr(),
+                  self.pos.data_ptr(), R, D, self.xd.data_ptr(), self._s)
+        xkv_stride = 2 * R * H * S_ENC * 64
+        for li, L in enumerate(w.dec):
+            self._ln(self.xd, L.ln1_g, L.ln1_b, R, self.hd)
+            self._gemm(self.hd, L.wqkv, R, 3 * D, D, _lib.TW_EPI_BF16, self.qkvd, bias=L.bqkv)
+            _lib.call("tw_attn_decode_self", self.qkvd.data_ptr(), R, H, T, self.pos.data_ptr(),
+                      self.kcache[li].data_ptr(), self.vcache[li].data_ptr(), self.attd.data_ptr(), self._s)
+            self._gemm(self.attd, L.wo, R, D, D, _lib.TW_EPI_RESID_F32, self.xd, bias=L.bo)
+            self._ln(self.xd, L.ln2_g, L.ln2_b, R, self.hd)
+            self._gemm(self.hd, L.wq_x, R, D, D, _lib.TW_EPI_BF16, self.qd, bias=L.bq_x)
+            ckv = self.cross_kv.data_ptr() + li * xkv_stride * 2  # bytes: bf16
+            _lib.call("tw_attn_decode_cross", self.qd.data_ptr(), R, H, S_ENC, R, None, ckv, self.attd.data_ptr(),
+                      self._s)
+            self._gemm(self.attd, L.wo_x, R, D, D, _lib.TW_EPI_RESID_F32, self.xd, bias=L.bo_x)
+            self._ln(self.xd, L.ln3_g, L.ln3_b, R, self.hd)
+            self._gemm(self.hd, L.w1, R, F, D, _lib.TW_EPI_GELU_BF16, self.ffnd, bias=L.b1)
+            self._gemm(self.ffnd, L.w2, R, D, F, _lib.TW_EPI_RESID_F32, self.xd, bias=L.b2)
+        if with_logits:
+            self._ln(self.xd, w.dec_ln_g, w.dec_ln_b, R, self.hd)
+            self._gemm(self.hd, w.emb, R, d.vocab, D, _lib.TW_EPI_F32, self.logits)
+
+    def _select_params(self, mode: int, max_new: int, use_timestamps: bool = True) -> _lib.TwSelectParams:
+        st, g = self.gen.special, self.gen
+        p = _lib.TwSelectParams()
+        p.V, p.eos, p.pad = self.d.vocab, st.eot, st.eot
+        p.ts_begin, p.no_timestamps = st.timestamp_begin, st.notimestamps
+        p.max_initial_ts = -1 if g.max_initial_timestamp_index is None else g.max_initial_timestamp_index
+        p.use_timestamps = int(use_timestamps)
+        p.max_new, p.mode = max_new, mode
+        p.lo, p.hi = st.lang_begin, st.lang_end
+        bs = list(g.begin_suppress_tokens or [])
+        p.n_begin_suppress = len(bs)
+        for i, t in enumerate(bs):
+            p.begin_suppress[i] = t
+        return p
+
+    def _select(self, R: int, params: _lib.TwSelectParams, tokens: bool = True) -> None:
+        _lib.call("tw_logits_select", self.logits.data_ptr(), R, self.d.vocab, self.suppress_bits.data_ptr(),
+                  ctypes.byref(params), self.state.data_ptr(), self.tokens.data_ptr() if tokens else None,
+                  self.tokens.shape[1], self.ids.data_ptr(), self.pos.data_ptr(), self._s)
+
+    def _gen_step(self, R: int, params) -> None:
+        self.decoder_step(R)
+        self._select(R, params)
+
+    def decode_pass(self, R: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
+                    check_every: int = 8, use_timestamps: bool = True) -> PassResult:
+        """Greedy decode of R rows from the prompt [SOT, (lang), *tail] (the init tokens of
+        _retrieve_init_tokens; the language is detected from the SOT step when lang_ids is None on a
+        multilingual model). Returns the generated tokens of every row."""
+        st = self.gen.special
+        dev = self.device
+        self.state[:R].zero_()
+        self.state[:R, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
+        self.pos[:R] = 0
+        self.ids[:R] = st.sot
+        detected = None
+        prompt_rest: List = []  # per-position token ids after SOT (int, or per-row list)
+        if st.is_multilingual:
+            prompt_rest.append(None if lang_ids is None else list(lang_ids))
+        prompt_rest.extend(int(t) for t in tail)
+        for k, tok in enumerate(prompt_rest):
+            if k == 0 and st.is_multilingual and lang_ids is None:
+                self.decoder_step(R)
+                self._select(R, self._select_params(1, max_new), tokens=False)  # ids <- lang, pos += 1
+                detected = self.state[:R, _lib.TW_ST_LANG].tolist()
+                continue
+            self.decoder_step(R, with_logits=False)
+            if isinstance(tok, list):
+                self.ids[:R] = torch.as_tensor(tok, dtype=torch.int32, device=dev)
+            else:
+                self.ids[:R] = tok
+            self.pos[:R] = k + 1
+        # last prompt token -> first generated token
+        params = self._select_params(0, max_new, use_timestamps)
+        self._gen_step(R, params)
+        steps = 1
+        graph = self._graph_for(R, params) if self.use_graphs else None
+        while steps < max_new:
+            n = min(check_every, max_new - steps)
+            for _ in range(n):
+                if graph is not None:
+                    graph.replay()
+                else:
+                    self._gen_step(R, params)
+            steps += n
+            if bool(self.state[:R, _lib.TW_ST_FINISHED].all().item()):
+                break
+        ngen = self.state[:R, _lib.TW_ST_NGEN].tolist()
+        toks = self.tokens[:R].tolist()
+        return PassResult([toks[r][: ngen[r]] for r in range(R)], detected if lang_ids is None else list(lang_ids))
+
+    def _graph_for(self, R: int, params) -> Optional[torch.cuda.CUDAGraph]:
+        key = (R, params.max_new, params.use_timestamps)
+        g = self._graphs.get(key)
+        if g is not None:
+            return g
+        g = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream(self.device)
+        cap.wait_stream(self.stream)
+        # capture on a side stream: the C-ABI calls launch on self.stream, so swap it for capture
+        saved = self.stream
+        try:
+            self.stream = cap
+            with torch.cuda.stream(cap):
+                # state is mutated by capture-time launches? no: capture records, it does not execute.
+                with torch.cuda.graph(g, stream=cap):
+                    self._gen_step(R, params)
+        finally:
+            self.stream = saved
+        self.stream.wait_stream(cap)
+        self._graphs[key] = g
+        return g
+
+    # ------------------------------------------------------------------ seek loop
+    def prompt_tail(self, task: Optional[str], return_timestamps: bool, language_given: bool = False) -> List[int]:
+        """Init tokens after SOT/lang (_retrieve_init_tokens, generation_whisper.py:1455-1608)."""
+        st = self.gen.special
+        tail: List[int] = []
+        if task is not None:
+            if not st.is_multilingual:
+                raise ValueError("Cannot specify `task` or `language` for an English-only model.")
+            if task not in ("transcribe", "translate"):
+                raise ValueError(f"The `{task}` task is not supported. The task should be one of "
+                                 "`['translate', 'transcribe']`")
+            tail.append(st.transcribe if task == "transcribe" else st.translate)
+        elif st.is_multilingual and language_given:
+            tail.append(st.transcribe)  # language given without a task: transcribe
+        if not return_timestamps:
+            tail.append(st.notimestamps)
+        return tail
+
+    def max_new_for(self, prompt_len: int, max_new_tokens: Optional[int] = None) -> int:
+        """_set_max_new_tokens_and_length (generation_whisper.py:1920-1950) for one seek pass."""
+        g, T = self.gen, self.d.max_target_positions
+        mnt = max_new_tokens if max_new_tokens is not None else g.max_new_tokens
+        if mnt is not None:
+            if mnt + prompt_len > T:
+                raise ValueError(f"prompt length {prompt_len} + max_new_tokens {mnt} exceeds {T}")
+            return mnt
+        return min(g.max_length + prompt_len, T) - prompt_len
+
+    def generate(self, n_chunks: int, task: Optional[str] = "transcribe", lang_ids: Optional[Sequence[int]] = None,
+                 max_new_tokens: Optional[int] = None, return_timestamps: bool = True,
+                 max_passes: Optional[int] = None) -> List[List[int]]:
+        """Whisper short-form generate() over feats[:n_chunks] (each 3000 frames): language
+        detection, the seek loop and segment extraction, returning for every chunk the concatenated
+        segment tokens (what generate() returns before padding)."""
+        st = self.gen.special
+        tail = self.prompt_tail(task, return_timestamps, language_given=lang_ids is not None)
+        prompt_len = 1 + (1 if st.is_multilingual else 0) + len(tail)
+        max_new = self.max_new_for(prompt_len, max_new_tokens)
+        seek = [0] * n_chunks
+        segs: List[List[int]] = [[] for _ in range(n_chunks)]
+        # language: given, or detected on the first pass (seek == 0, the whole 30-s window) as
+        # _retrieve_init_tokens -> detect_language does before the seek loop
+        langs: List[Optional[int]] = list(lang_ids) if lang_ids is not None else [None] * n_chunks
+        passes = 0
+        while any(s < N_FRAMES for s in seek):
+            rows = [i for i in range(n_chunks) if seek[i] < N_FRAMES]
+            for b0 in range(0, len(rows), self.max_batch):
+                part = rows[b0: b0 + self.max_batch]
+                R = len(part)
+                self.row_map[:R] = torch.as_tensor(part, dtype=torch.int32, device=self.device)
+                self.seek[:R] = torch.as_tensor([seek[i] for i in part], dtype=torch.int32, device=self.device)
+                self.encode(R)
+                part_langs = [langs[i] for i in part]
+                known = all(lg is not None for lg in part_langs) or not st.is_multilingual
+                res = self.decode_pass(R, tail, part_langs if (known and st.is_multilingual) else None, max_new,
+                                       use_timestamps=return_timestamps)
+                for j, i in enumerate(part):
+                    if not known:
+                        langs[i] = res.lang_ids[j]
+                    seq = strip_generated(res.tokens[j], st.eot)
+                    seg_tokens, offset = retrieve_segment(seq, seek[i], N_FRAMES - seek[i], st.timestamp_begin)
+                    segs[i].extend(seg_tokens)
+                    seek[i] += offset
+            passes += 1
+            if max_passes is not None and passes >= max_passes:
+                break
+            if passes >= 4 * N_FRAMES:  # a zero seek advance would loop forever (as generate() would)
+                raise RuntimeError("seek loop made no progress")
+        self.last_langs = langs
+        return segs

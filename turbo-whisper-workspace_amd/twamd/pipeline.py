@@ -1,0 +1,147 @@
+"""TurboTranscriber: the drop-in for the ASR callable the reference builds and calls.
+
+Reference: AudioProcessingPipeline.load_transcription_model stores
+`transformers.pipeline("automatic-speech-recognition", ...)` in `self.transcription_model`
+(/root/reference/vocalis/core/audio_pipeline.py:171-208) and `transcribe` calls it as
+    outputs = self.transcription_model(audio_path, chunk_length_s=60, batch_size=512|32,
+                                       stride_length_s=5, generate_kwargs={"task": task},
+                                       return_timestamps=return_timestamps)      (:351-358)
+TurboTranscriber.__call__ accepts the same arguments and returns the same dict
+({"text": str, "chunks": [{"timestamp": (start, end), "text": str}, ...]}), following
+AutomaticSpeechRecognitionPipeline preprocess / _forward / postprocess
+($TF/pipelines/automatic_speech_recognition.py:345-710) with every numeric stage on the GPU engine.
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Dict, List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from . import audio
+from .config import PRESETS, GenerationSettings, WhisperDims
+from .engine import WhisperEngine
+from .frontend import CHUNK_SAMPLES, SAMPLE_RATE, Window, chunk_windows, time_precision
+from .segments import pad_right
+from .tokenizer import LANGUAGE_NAMES, WhisperVocab, decode_asr
+from .weights import build_weights
+
+_NAME_TO_CODE = {v: k for k, v in LANGUAGE_NAMES.items()}
+
+
+class TurboTranscriber:
+    """Callable with the HF ASR pipeline signature, backed by WhisperEngine (HIP)."""
+
+    def __init__(self, engine: WhisperEngine, vocab: WhisperVocab, sampling_rate: int = SAMPLE_RATE):
+        self.engine = engine
+        self.vocab = vocab
+        self.sampling_rate = sampling_rate
+        self.gen = engine.gen
+
+    # -------------------------------------------------------------- construction
+    @staticmethod
+    def from_pretrained(model: str = "large-v3-turbo", checkpoint: Optional[str] = None, seed: int = 1234,
+                        max_batch: int = 24, device: str = "cuda", use_graphs: bool = True) -> "TurboTranscriber":
+        """`model`: a preset name (synthetic seeded weights) or, via `checkpoint`, a LOCAL Hugging Face
+        Whisper directory (config.json, *.safetensors, vocab.json, generation_config.json)."""
+        if checkpoint is None and model not in PRESETS and os.path.isdir(model):
+            checkpoint = model
+        if checkpoint is not None:
+            dims = _dims_from_checkpoint(checkpoint)
+            gen = GenerationSettings.from_checkpoint(checkpoint, dims)
+            vocab = WhisperVocab.from_checkpoint(checkpoint, gen.special)
+        else:
+            key = model.split("/")[-1].replace("whisper-", "")
+            if key not in PRESETS:
+                raise ValueError(f"unknown model {model!r}: give a preset ({sorted(PRESETS)}) or a local checkpoint dir")
+            dims = PRESETS[key]
+            gen = GenerationSettings.default(dims)
+            vocab = WhisperVocab.synthetic(gen.special)
+        weights = build_weights(dims, seed=seed, checkpoint=checkpoint)
+        eng = WhisperEngine(weights, gen, max_batch=max_batch, device=device, use_graphs=use_graphs)
+        return TurboTranscriber(eng, vocab)
+
+    # -------------------------------------------------------------- call
+    def __call__(self, inputs: Union[str, bytes, np.ndarray, dict], *, chunk_length_s: float = 0,
+                 stride_length_s=None, batch_size: int = 1, generate_kwargs: Optional[Dict[str, Any]] = None,
+                 return_timestamps: Union[bool, str] = False, return_language: bool = False, **kwargs) -> dict:
+        if return_timestamps == "word":
+            raise NotImplementedError("word-level timestamps (cross-attention DTW) are not on the GPU path yet")
+        if return_timestamps == "char":
+            raise ValueError("Whisper cannot return `char` timestamps, only word level or segment level timestamps.")
+        gk = dict(generate_kwargs or {})
+        gk.update({k: kwargs.pop(k) for k in list(kwargs) if k in ("max_new_tokens", "language", "task", "num_beams")})
+        num_beams = gk.pop("num_beams", 1)
+        if num_beams not in (None, 1):
+            raise NotImplementedError("beam search is not implemented; the engine decodes greedily (num_beams=1)")
+        task = gk.pop("task", None)
+        language = gk.pop("language", None)
+        max_new_tokens = gk.pop("max_new_tokens", None)
+        st = self.gen.special
+        if not st.is_multilingual and (task is not None or language is not None):
+            raise ValueError("Cannot specify `task` or `language` for an English-only model.")
+
+        wav = audio.load_input(inputs, self.sampling_rate)
+        if chunk_length_s:
+            windows = list(chunk_windows(len(wav), chunk_length_s, stride_length_s, self.sampling_rate))
+            with_stride = True
+        else:
+            if len(wav) > CHUNK_SAMPLES:
+                raise NotImplementedError("long-form (> 30 s without chunk_length_s) sequential decoding is not "
+                                          "implemented; pass chunk_length_s")
+            windows = [Window(0, len(wav), 0, 0, True)]
+            with_stride = False
+        lang_id = None
+        if language is not None:
+            code = language.lower()
+            code = _NAME_TO_CODE.get(code, code)
+            tok = f"<|{code}|>"
+            lt = st.lang_to_id()
+            if tok not in lt:
+                raise ValueError(f"Unsupported language: {language}.")
+            lang_id = lt[tok]
+        outputs = self.transcribe_windows(wav, windows, task=task, lang_id=lang_id, return_timestamps=bool(return_timestamps),
+                                          max_new_tokens=max_new_tokens)
+        model_outputs = []
+        for w, toks in zip(windows, outputs):
+            o = {"tokens": toks}
+            if with_stride:
+                sr = self.sampling_rate
+                o["stride"] = (w.length / sr, w.stride_left / sr, w.stride_right / sr)
+            model_outputs.append(o)
+        text, optional = decode_asr(self.vocab, model_outputs, return_timestamps=bool(return_timestamps),
+                                    return_language=return_language,
+                                    time_precision=time_precision(self.engine.d.max_source_positions))
+        return {"text": text, **optional}
+
+    def transcribe_windows(self, wav: np.ndarray, windows: Sequence[Window], task: Optional[str],
+                           lang_id: Optional[int], return_timestamps: bool,
+                           max_new_tokens: Optional[int] = None) -> List[List[int]]:
+        """Log-mel + generate for every window; returns per-window token sequences (generate() output,
+        right-padded with the pad token within each engine batch, as the HF batch output is)."""
+        eng = self.engine
+        out: List[List[int]] = []
+        B = eng.max_batch
+        for b0 in range(0, len(windows), B):
+            part = windows[b0: b0 + B]
+            host = np.zeros((len(part), CHUNK_SAMPLES), np.float32)
+            for j, w in enumerate(part):
+                seg = wav[w.start: w.start + min(w.length, CHUNK_SAMPLES)]  # feature extractor truncation
+                host[j, : len(seg)] = seg
+            eng.wave[: len(part)].copy_(torch.from_numpy(host), non_blocking=False)
+            eng.logmel(len(part))
+            seqs = eng.generate(len(part), task=task, lang_ids=None if lang_id is None else [lang_id] * len(part),
+                                max_new_tokens=max_new_tokens, return_timestamps=return_timestamps)
+            out.extend(pad_right(seqs, self.gen.special.eot))
+        return out
+
+
+def _dims_from_checkpoint(path: str) -> WhisperDims:
+    import json
+
+    with open(os.path.join(path, "config.json")) as f:
+        c = json.load(f)
+    return WhisperDims(os.path.basename(os.path.normpath(path)), c["d_model"], c["encoder_layers"], c["decoder_layers"],
+                       c["encoder_attention_heads"], c["encoder_ffn_dim"], c["num_mel_bins"], c["vocab_size"],
+                       c.get("max_source_positions", 1500), c.get("max_target_positions", 448))

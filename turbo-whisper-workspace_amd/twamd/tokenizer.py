@@ -1,0 +1,282 @@
+"""Whisper token decoding and the ASR pipeline's chunk stitching (host CPU, after the GPU passes).
+
+* `WhisperVocab`: byte-level BPE id -> text (GPT-2 byte<->unicode table; the tokenizer's
+  `decoders.ByteLevel()`, $TF/models/whisper/tokenization_whisper.py:239-251), built from a local
+  checkpoint's vocab.json / added tokens or from the deterministic synthetic vocabulary.
+* `decode_asr` restates `_decode_asr` ($TF/models/whisper/tokenization_whisper.py:901-1150) for
+  return_timestamps in {False, True} and `_find_longest_common_sequence` (:1153-1270), driven by
+  AutomaticSpeechRecognitionPipeline.postprocess (:600-710 of automatic_speech_recognition.py:
+  stride samples -> seconds, time_precision = 30 / max_source_positions).
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .config import LANGUAGE_CODES, SpecialTokens
+
+# Whisper's LANGUAGES code -> name table (only the codes are needed to recognise language tokens;
+# names are what _decode_asr stores in chunk["language"])
+LANGUAGE_NAMES = {
+    "en": "english", "zh": "chinese", "de": "german", "es": "spanish", "ru": "russian", "ko": "korean",
+    "fr": "french", "ja": "japanese", "pt": "portuguese", "tr": "turkish", "pl": "polish", "ca": "catalan",
+    "nl": "dutch", "ar": "arabic", "sv": "swedish", "it": "italian", "id": "indonesian", "hi": "hindi",
+    "fi": "finnish", "vi": "vietnamese", "he": "hebrew", "uk": "ukrainian", "el": "greek", "ms": "malay",
+    "cs": "czech", "ro": "romanian", "da": "danish", "hu": "hungarian", "ta": "tamil", "no": "norwegian",
+    "th": "thai", "ur": "urdu", "hr": "croatian", "bg": "bulgarian", "lt": "lithuanian", "la": "latin",
+    "mi": "maori", "ml": "malayalam", "cy": "welsh", "sk": "slovak", "te": "telugu", "fa": "persian",
+    "lv": "latvian", "bn": "bengali", "sr": "serbian", "az": "azerbaijani", "sl": "slovenian", "kn": "kannada",
+    "et": "estonian", "mk": "macedonian", "br": "breton", "eu": "basque", "is": "icelandic", "hy": "armenian",
+    "ne": "nepali", "mn": "mongolian", "bs": "bosnian", "kk": "kazakh", "sq": "albanian", "sw": "swahili",
+    "gl": "galician", "mr": "marathi", "pa": "punjabi", "si": "sinhala", "km": "khmer", "sn": "shona",
+    "yo": "yoruba", "so": "somali", "af": "afrikaans", "oc": "occitan", "ka": "georgian", "be": "belarusian",
+    "tg": "tajik", "sd": "sindhi", "gu": "gujarati", "am": "amharic", "yi": "yiddish", "lo": "lao",
+    "uz": "uzbek", "fo": "faroese", "ht": "haitian creole", "ps": "pashto", "tk": "turkmen", "nn": "nynorsk",
+    "mt": "maltese", "sa": "sanskrit", "lb": "luxembourgish", "my": "myanmar", "bo": "tibetan", "tl": "tagalog",
+    "mg": "malagasy", "as": "assamese", "tt": "tatar", "haw": "hawaiian", "ln": "lingala", "ha": "hausa",
+    "ba": "bashkir", "jw": "javanese", "su": "sundanese", "yue": "cantonese",
+}
+
+
+def bytes_to_unicode() -> Dict[int, str]:
+    """GPT-2 reversible byte <-> printable-unicode table."""
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) + list(range(ord("®"), ord("ÿ") + 1))
+    cs = bs[:]
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return dict(zip(bs, [chr(c) for c in cs]))
+
+
+def special_token_strings(st: SpecialTokens) -> Dict[int, str]:
+    out = {st.eot: "<|endoftext|>", st.sot: "<|startoftranscript|>"}
+    for i, code in enumerate(LANGUAGE_CODES[: st.n_languages]):
+        out[st.lang_begin + i] = f"<|{code}|>"
+    out.update({st.translate: "<|translate|>", st.transcribe: "<|transcribe|>", st.startoflm: "<|startoflm|>",
+                st.startofprev: "<|startofprev|>", st.nospeech: "<|nospeech|>" if st.vocab == 51866 else "<|nocaptions|>",
+                st.notimestamps: "<|notimestamps|>"})
+    for i in range(1501):
+        out[st.timestamp_begin + i] = f"<|{i * 0.02:.2f}|>"
+    return out
+
+
+def synthetic_vocab(st: SpecialTokens) -> List[str]:
+    """Deterministic byte-level vocabulary of size st.vocab: ids < 256 are the 256 byte symbols, text ids
+    up to eot are unique letter strings (even ids carry the 'Ġ' = space prefix), then the specials."""
+    b2u = bytes_to_unicode()
+    base = [b2u[b] for b in sorted(b2u, key=lambda x: list(b2u).index(x))]
+    toks: List[str] = list(base)
+    letters = "abcdefghijklmnopqrstuvwxyz"
+    for i in range(256, st.eot):
+        n, s = i, ""
+        while n:
+            s += letters[n % 26]
+            n //= 26
+        toks.append(("Ġ" + s) if i % 2 == 0 else s)
+    spec = special_token_strings(st)
+    for i in range(st.eot, st.vocab):
+        toks.append(spec[i])
+    return toks
+
+
+class WhisperVocab:
+    """id -> token string table plus byte-level decoding."""
+
+    def __init__(self, id_to_token: Sequence[str], special: SpecialTokens):
+        self.id_to_token = list(id_to_token)
+        self.special = special
+        self.byte_decoder = {v: k for k, v in bytes_to_unicode().items()}
+        self.all_special_ids = set(special.special_ids())
+
+    @staticmethod
+    def synthetic(special: SpecialTokens) -> "WhisperVocab":
+        return WhisperVocab(synthetic_vocab(special), special)
+
+    @staticmethod
+    def from_checkpoint(path: str, special: SpecialTokens) -> "WhisperVocab":
+        with open(os.path.join(path, "vocab.json"), encoding="utf-8") as f:
+            vocab = json.load(f)
+        toks = [""] * special.vocab
+        for t, i in vocab.items():
+            if i < special.vocab:
+                toks[i] = t
+        added = os.path.join(path, "added_tokens.json")
+        if os.path.exists(added):
+            with open(added, encoding="utf-8") as f:
+                for t, i in json.load(f).items():
+                    if i < special.vocab:
+                        toks[i] = t
+        for i, t in special_token_strings(special).items():
+            if not toks[i]:
+                toks[i] = t
+        return WhisperVocab(toks, special)
+
+    def decode(self, ids: Sequence[int]) -> str:
+        """tokenizer.decode(ids) for text tokens (specials render as their strings)."""
+        text = "".join(self.id_to_token[i] for i in ids)
+        data = bytearray()
+        out = []
+        for ch in text:
+            b = self.byte_decoder.get(ch)
+            if b is None:  # special-token characters outside the byte table
+                if data:
+                    out.append(data.decode("utf-8", errors="replace"))
+                    data = bytearray()
+                out.append(ch)
+            else:
+                data.append(b)
+        if data:
+            out.append(data.decode("utf-8", errors="replace"))
+        return "".join(out)
+
+
+def find_longest_common_sequence(sequences: List[List[int]]) -> List[int]:
+    """Greedy overlap merge of consecutive token runs (the pipeline's stride stitching)."""
+    left = sequences[0]
+    left_len = len(left)
+    total: List[int] = []
+    for right in sequences[1:]:
+        best = 0.0
+        best_idx = (left_len, left_len, 0, 0)
+        right_len = len(right)
+        la = np.asarray(left)
+        ra = np.asarray(right)
+        for i in range(1, left_len + right_len):
+            eps = i / 10000.0
+            ls, le = max(0, left_len - i), min(left_len, left_len + right_len - i)
+            rs, re_ = max(0, i - left_len), min(right_len, i)
+            matches = int(np.sum(la[ls:le] == ra[rs:re_])) if le > ls else 0
+            matching = matches / i + eps
+            if matches > 1 and matching > best:
+                best = matching
+                best_idx = (ls, le, rs, re_)
+        ls, le, rs, re_ = best_idx
+        lmid = (le + ls) // 2
+        rmid = (re_ + rs) // 2
+        total.extend(left[:lmid])
+        left = right[rmid:]
+        left_len = len(left)
+    total.extend(left)
+    return total
+
+
+def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps: bool, return_language: bool = False,
+               time_precision: float = 0.02, segment_size: int = 1500) -> Tuple[str, dict]:
+    """outputs: [{"tokens": [ids...], "stride": (chunk_len_s, left_s, right_s) optional}, ...] in chunk order."""
+    st = vocab.special
+    last_language = None
+
+    def new_chunk():
+        return {"language": last_language, "timestamp": [None, None], "text": ""}
+
+    chunks = []
+    chunk = new_chunk()
+    time_offset = 0.0
+    timestamp_begin = st.timestamp_begin
+    previous_tokens: List[List[int]] = []
+    skip = False
+    right_stride_start = None
+    special_ids = vocab.all_special_ids
+    for output in outputs:
+        token_ids = list(output["tokens"])
+        # _strip_prompt: a leading <|startofprev|> prompt is cut up to <|startoftranscript|>
+        if token_ids and token_ids[0] == st.startofprev:
+            token_ids = token_ids[token_ids.index(st.sot):] if st.sot in token_ids else []
+        last_timestamp = None
+        first_timestamp = timestamp_begin
+        cur_max_timestamp = 0.0
+        prev_segments_len = 0.0
+        penultimate_timestamp = 0.0
+        if "stride" in output:
+            chunk_len, stride_left, stride_right = output["stride"]
+            time_offset -= stride_left
+            right_stride_start = chunk_len - stride_right
+            if stride_left:
+                first_timestamp = stride_left / time_precision + timestamp_begin
+            if stride_right:
+                for token in reversed(token_ids):
+                    if token >= timestamp_begin:
+                        if last_timestamp is not None and (token - timestamp_begin) * time_precision < right_stride_start:
+                            break
+                        last_timestamp = token
+        current_tokens: List[int] = []
+        for i, token in enumerate(token_ids):
+            if token in special_ids:
+                text = vocab.id_to_token[token][2:-2]
+                language = LANGUAGE_NAMES.get(text)
+                if language is not None:
+                    if last_language and language != last_language and not return_timestamps:
+                        previous_tokens.append(current_tokens)
+                        resolved = find_longest_common_sequence(previous_tokens)
+                        chunk["text"] = vocab.decode(resolved)
+                        chunks.append(chunk)
+                        previous_tokens = []
+                        current_tokens = []
+                        chunk = new_chunk()
+                    chunk["language"] = language
+                    last_language = language
+            elif token >= timestamp_begin:
+                timestamp = float((token - timestamp_begin) * time_precision)
+                if timestamp < cur_max_timestamp:
+                    last_was_single_ending = i >= 2 and not (
+                        token_ids[i - 1] >= timestamp_begin and token_ids[i - 2] >= timestamp_begin)
+                    if last_was_single_ending:
+                        prev_segments_len += time_precision * segment_size
+                    else:
+                        cur_max_timestamp = penultimate_timestamp
+                        prev_segments_len += penultimate_timestamp
+                penultimate_timestamp = cur_max_timestamp
+                cur_max_timestamp = timestamp
+                time = (token - timestamp_begin) * time_precision + time_offset + prev_segments_len
+                time = round(time, 2)
+                if last_timestamp and token >= last_timestamp:
+                    skip = True
+                elif skip or (previous_tokens and token < first_timestamp):
+                    skip = False
+                elif chunk["timestamp"][0] is None:
+                    chunk["timestamp"][0] = time
+                else:
+                    if time == chunk["timestamp"][0]:
+                        pass
+                    else:
+                        chunk["timestamp"][1] = time
+                        previous_tokens.append(current_tokens)
+                        resolved = find_longest_common_sequence(previous_tokens)
+                        chunk["text"] = vocab.decode(resolved)
+                        chunks.append(chunk)
+                        previous_tokens = []
+                        current_tokens = []
+                        chunk = new_chunk()
+            else:
+                current_tokens.append(token)
+        if "stride" in output:
+            time_offset += chunk_len - stride_right
+        if current_tokens:
+            previous_tokens.append(current_tokens)
+        elif not any(p for p in previous_tokens):
+            chunk = new_chunk()
+            previous_tokens = []
+            current_tokens = []
+    if previous_tokens:
+        resolved = find_longest_common_sequence(previous_tokens)
+        chunk["text"] = vocab.decode(resolved)
+        chunks.append(chunk)
+    full_text = "".join(c["text"] for c in chunks)
+    if return_timestamps or return_language:
+        for c in chunks:
+            if not return_timestamps:
+                c.pop("timestamp")
+            else:
+                c["timestamp"] = tuple(c["timestamp"])
+            if not return_language:
+                c.pop("language")
+        optional = {"chunks": chunks}
+    else:
+        optional = {}
+    return full_text, optional
