@@ -126,28 +126,28 @@ def _ref_attn(q, k, v):  # [B,H,S,64] fp32, q already scaled
     return torch.softmax(q @ k.transpose(-1, -2), dim=-1) @ v
 
 
-@pytest.mark.parametrize("B,S,H", [(2, 1500, 4), (1, 100, 2), (1, 1500, 20)])
-def test_encoder_attention_vs_torch(B, S, H):
+@pytest.mark.parametrize("B,L,H", [(2, 1500, 4), (1, 100, 2), (1, 1500, 20)])
+def test_encoder_attention_vs_torch(B, L, H):
     D = H * 64
-    qkv = rand_bf16(B * S, 3 * D, seed=7)
+    qkv = rand_bf16(B * L, 3 * D, seed=7)
     qkv[:, :D] = bf(qkv[:, :D].float() * 0.125 * 3)  # scaled q with some dynamic range
-    out = torch.empty(B * S, D, dtype=torch.bfloat16, device=DEV)
-    _lib.call("tw_attn_encoder", qkv.data_ptr(), B, S, H, out.data_ptr(), S())
-    t = qkv.float().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
-    ref = _ref_attn(t[0], t[1], t[2]).permute(0, 2, 1, 3).reshape(B * S, D)
+    out = torch.empty(B * L, D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_attn_encoder", qkv.data_ptr(), B, L, H, out.data_ptr(), S())
+    t = qkv.float().view(B, L, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = _ref_attn(t[0], t[1], t[2]).permute(0, 2, 1, 3).reshape(B * L, D)
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
 def test_encoder_attention_online_softmax_rescale():
     """Force the running max to jump in a late key tile (rule 26: exercise the rescale branch)."""
-    B, S, H = 1, 1500, 1
+    B, L, H = 1, 1500, 1
     D = 64
-    qkv = rand_bf16(B * S, 3 * D, scale=0.3, seed=8)
+    qkv = rand_bf16(B * L, 3 * D, scale=0.3, seed=8)
     qkv[1400, D:2 * D] = bf(qkv[:, :D].float().mean(0) * 0 + 4.0)  # one dominant key in the last tile
-    out = torch.empty(B * S, D, dtype=torch.bfloat16, device=DEV)
-    _lib.call("tw_attn_encoder", qkv.data_ptr(), B, S, H, out.data_ptr(), S())
-    t = qkv.float().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
-    ref = _ref_attn(t[0], t[1], t[2]).permute(0, 2, 1, 3).reshape(B * S, D)
+    out = torch.empty(B * L, D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_attn_encoder", qkv.data_ptr(), B, L, H, out.data_ptr(), S())
+    t = qkv.float().view(B, L, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = _ref_attn(t[0], t[1], t[2]).permute(0, 2, 1, 3).reshape(B * L, D)
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
