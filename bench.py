@@ -161,7 +161,7 @@ def cpu_baseline(dims, gen, T, threads):
     from oracle import hf_baseline
     from twamd.synth_audio import speech_like
 
-    threads = threads or min(32, os.cpu_count() or 1)
+    threads = threads or min(16, os.cpu_count() or 1)  # the GPU box grants 16 host cores
     g = copy.deepcopy(gen)
     g.suppress_tokens = list(gen.suppress_tokens) + [gen.special.eot]
     try:

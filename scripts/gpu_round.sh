@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU-box session: parity tests, the bench line, a rocprofv3 kernel-trace summary and the two
+# PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic. Every GPU step has its own time limit and the
+# chain stops at the first failure.  usage: bash scripts/gpu_round.sh TAG [skip_tests]
+set -u
+TAG=${1:-r01}
+SKIP_TESTS=${2:-0}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # step NAME TIMEOUT CMD...
+  local name=$1 to=$2; shift 2
+  echo "[$(date +%T)] $name" 
+  timeout -k 10 $to "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc"; tail -4 $OUT/$name.log
+  if [ $rc -ne 0 ] && [ $rc -ne 5 ]; then echo "STOP after $name"; exit $rc; fi
+}
+if [ "$SKIP_TESTS" != "1" ]; then
+  step tests 900 python -m pytest tests -q -m gpu -x -p no:cacheprovider
+fi
+step bench 900 python bench.py --steps 5 --warmup 2
+grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
+step prof_kt 600 rocprofv3 --kernel-trace --stats -T -d $OUT/kt -o kt --output-format csv -- python bench.py --profile-only --steps 2 --warmup 1
+step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/pmc_fetch -o pmc --output-format csv -- python bench.py --profile-only --steps 1 --warmup 0
+step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/pmc_write -o pmc --output-format csv -- python bench.py --profile-only --steps 1 --warmup 0
+python scripts/summarize_prof.py $OUT > $OUT/summary.txt 2>&1
+echo done
