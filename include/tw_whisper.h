@@ -42,6 +42,10 @@ extern "C" {
 #define TW_ST_FINISHED 4 /* 1 once EOS was produced or max length reached                       */
 #define TW_ST_LANG 5     /* language id chosen by mode-1 selection                              */
 
+/* tw_logits_select workspace: f32[B][TW_SELECT_WS_PER_ROW] (TW_SELECT_CHUNKS vocab chunks per row). */
+#define TW_SELECT_CHUNKS 16
+#define TW_SELECT_WS_PER_ROW 128
+
 typedef struct TwSelectParams {
   int32_t V;                  /* vocabulary size                                                 */
   int32_t eos;                /* eos_token_id (50257 multilingual)                               */
@@ -96,6 +100,20 @@ int tw_im2col_conv2(const uint16_t* h1, int R, int D, uint16_t* out, void* strea
  * cached by EncoderDecoderCache (:312-335). */
 int tw_gemm_bf16(const uint16_t* A, const uint16_t* W, int M, int N, int K, int lda, int ldw, int epi, void* out,
                  int ldo, const float* bias, const float* aux, int aux_rows, const int* kv_geom, void* stream);
+/* Selects the large-M GEMM kernel of tw_gemm_bf16: 1 = 256x256 LDS-DMA kernel (default), 0 = the
+ * 128x128 register-staged kernel (kept for A/B measurement). Process-wide; returns 0. */
+int tw_gemm_set_variant(int big);
+/* Split-K partial product for the decoder step (M <= 32 rows, K % 32 == 0): part f32[splits][M][ldp]
+ * receives the `splits` partial sums of A . W^T over consecutive K ranges (no bias). Used for the
+ * d_model-wide projections (self/cross out_proj, fc2) whose residual add is done by
+ * tw_resid_layernorm, which sums the partials. Replaces the same nn.Linear calls as tw_gemm_bf16. */
+int tw_gemm_bf16_partial(const uint16_t* A, const uint16_t* W, int M, int N, int K, int lda, int ldw, int splits,
+                         float* part, int ldp, void* stream);
+/* Decoder residual update + LayerNorm, one row per block: x f32[M][D] += bias + sum_p parts[p] (parts
+ * f32[nparts][M][D]); then, if gamma != NULL, out bf16[M][D] = LayerNorm(x). Replaces the residual adds
+ * of WhisperDecoderLayer.forward (modeling_whisper.py:468-505) + the following pre-LayerNorm. */
+int tw_resid_layernorm(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
+                       const float* beta, int M, int D, float eps, uint16_t* out, void* stream);
 /* out bf16[M][D] = LayerNorm(x f32[M][D]) (eps, affine). Replaces nn.LayerNorm (modeling_whisper.py
  * :371,377,434,443,446,573,682). */
 int tw_layernorm(const float* x, const float* gamma, const float* beta, int M, int D, float eps, uint16_t* out,
@@ -122,7 +140,8 @@ int tw_embed_decoder(const uint16_t* tok_emb, const uint16_t* pos_emb, const int
                      float* x, void* stream);
 /* Whisper logits processors + greedy argmax for B rows of f32 logits (see TwSelectParams; state
  * int32[B][TW_STATE_STRIDE]; tokens_out int32[B][ld_tokens] receives token n_gen; next_ids int32[B];
- * pos int32[B] (may be NULL) is incremented so a captured decode step can be replayed unchanged).
+ * pos int32[B] (may be NULL) is incremented so a captured decode step can be replayed unchanged;
+ * workspace f32[B][TW_SELECT_WS_PER_ROW]).
  * `params` is a HOST pointer (passed by value to the kernel). suppress_bits: u32[ceil(V/32)] or NULL.
  * Replaces GenerationMixin._sample's selection step ($TF/generation/utils.py:2876-2941) with
  * SuppressTokensAtBegin / SuppressTokens / WhisperTimeStamp processors
@@ -130,7 +149,7 @@ int tw_embed_decoder(const uint16_t* tok_emb, const uint16_t* pos_emb, const int
  * ($TF/models/whisper/generation_whisper.py:1664-1671). */
 int tw_logits_select(const float* logits, int B, int ld_logits, const uint32_t* suppress_bits,
                      const TwSelectParams* params, int* state, int* tokens_out, int ld_tokens, int* next_ids,
-                     int* pos, void* stream);
+                     int* pos, float* workspace, void* stream);
 
 #ifdef __cplusplus
 }

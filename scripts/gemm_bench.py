@@ -1,0 +1,67 @@
+"""A/B timing of the large-M GEMM kernels on the encoder shapes (B=24 windows: M = 36000 rows).
+Interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24); random operands.
+
+    python scripts/gemm_bench.py [--rounds 5]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "turbo-whisper-workspace_amd")]
+import torch  # noqa: E402
+
+from twamd import _lib  # noqa: E402
+
+SHAPES = [  # name, M, N, K, epi
+    ("qkv", 36000, 3840, 1280, _lib.TW_EPI_BF16),
+    ("o-proj", 36000, 1280, 1280, _lib.TW_EPI_RESID_F32),
+    ("fc1", 36000, 5120, 1280, _lib.TW_EPI_GELU_BF16),
+    ("fc2", 36000, 1280, 5120, _lib.TW_EPI_RESID_F32),
+    ("conv2", 36000, 1280, 3840, _lib.TW_EPI_F32),
+    ("xkv", 36000, 10240, 1280, _lib.TW_EPI_BF16),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    _lib.load()
+    s = torch.cuda.current_stream().cuda_stream
+    for name, M, N, K, epi in SHAPES:
+        A = (torch.randn(M, K, device="cuda") * 0.5).to(torch.bfloat16)
+        W = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+        bias = torch.randn(N, device="cuda")
+        if epi in (_lib.TW_EPI_BF16, _lib.TW_EPI_GELU_BF16):
+            out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+        else:
+            out = torch.zeros(M, N, device="cuda")
+        res = {0: [], 1: []}
+        outs = {}
+        for r in range(a.rounds):
+            for v in (0, 1):
+                _lib.call("tw_gemm_set_variant", v)
+                if epi == _lib.TW_EPI_RESID_F32:
+                    out.zero_()
+                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                st.record()
+                for _ in range(a.iters):
+                    _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, K, K, epi, out.data_ptr(), N,
+                              bias.data_ptr(), None, 0, None, s)
+                en.record()
+                torch.cuda.synchronize()
+                res[v].append(st.elapsed_time(en) / a.iters)
+                if r == 0:
+                    outs[v] = out.float().clone() / (a.iters if epi == _lib.TW_EPI_RESID_F32 else 1)
+        fl = 2.0 * M * N * K
+        err = (outs[0] - outs[1]).abs().max().item()
+        print(f"{name:7s} M={M} N={N} K={K}: " + "  ".join(
+            f"v{v}: med {sorted(t)[len(t) // 2]:.3f} ms min {min(t):.3f} ms = {fl / min(t) / 1e9:.0f} TF/s"
+            for v, t in res.items()) + f"  max|v0-v1|={err:.3g}", flush=True)
+    _lib.call("tw_gemm_set_variant", 1)
+
+
+if __name__ == "__main__":
+    main()

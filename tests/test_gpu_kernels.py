@@ -87,6 +87,39 @@ def test_gemm_vs_torch(M, N, K, epi):
     torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
 
 
+@pytest.mark.parametrize("M,N,K,splits", [(24, 1280, 1280, 4), (24, 1280, 5120, 4), (1, 384, 1536, 3),
+                                          (17, 200, 96, 1), (32, 1280, 1280, 16)])
+def test_gemm_partial_splitk_vs_torch(M, N, K, splits):
+    A = rand_bf16(M, K, seed=21)
+    W = rand_bf16(N, K, scale=K ** -0.5, seed=22)
+    part = torch.full((splits, M, N), float("nan"), device=DEV)
+    _lib.call("tw_gemm_bf16_partial", A.data_ptr(), W.data_ptr(), M, N, K, K, K, splits, part.data_ptr(), N, S())
+    ref = A.float() @ W.float().t()
+    torch.testing.assert_close(part.sum(0), ref, atol=2e-3, rtol=2e-3)  # f32 accumulation order only
+    # each split is the product over its own K range (consecutive 32-deep steps)
+    ns = K // 32
+    for y in range(splits):
+        lo = 32 * (y * ns // splits)
+        hi = 32 * ((y + 1) * ns // splits)
+        torch.testing.assert_close(part[y], A[:, lo:hi].float() @ W[:, lo:hi].float().t(), atol=2e-3, rtol=2e-3)
+
+
+@pytest.mark.parametrize("M,D,nparts", [(24, 1280, 4), (5, 384, 0), (3, 256, 2)])
+def test_resid_layernorm_vs_torch(M, D, nparts):
+    x = torch.randn(M, D, device=DEV) * 3 + 1
+    parts = torch.randn(max(nparts, 1), M, D, device=DEV)
+    bias = torch.randn(D, device=DEV) if nparts else None
+    g = torch.randn(D, device=DEV)
+    b = torch.randn(D, device=DEV)
+    out = torch.empty(M, D, dtype=torch.bfloat16, device=DEV)
+    xr = x + (bias + parts[:nparts].sum(0) if nparts else 0)
+    _lib.call("tw_resid_layernorm", x.data_ptr(), parts.data_ptr(), nparts, _lib.ptr(bias), g.data_ptr(), b.data_ptr(),
+              M, D, 1e-5, out.data_ptr(), S())
+    torch.testing.assert_close(x, xr, atol=1e-5, rtol=1e-5)
+    ref = torch.nn.functional.layer_norm(xr, (D,), g, b, 1e-5)
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=1e-2)
+
+
 def test_gemm_gelu_pos_and_crosskv():
     M, N, K = 3000, 256, 768
     A = rand_bf16(M, K, seed=3)
@@ -224,8 +257,9 @@ def test_logits_select_matches_oracle_processors():
         toks = torch.zeros(B, 448, dtype=torch.int32, device=DEV)
         ids = torch.zeros(B, dtype=torch.int32, device=DEV)
         p = _params(V, st)
+        ws = torch.empty(B, _lib.TW_SELECT_WS_PER_ROW, device=DEV)
         _lib.call("tw_logits_select", lt.data_ptr(), B, V, sup.data_ptr(), ctypes.byref(p), stt.data_ptr(),
-                  toks.data_ptr(), 448, ids.data_ptr(), None, S())
+                  toks.data_ptr(), 448, ids.data_ptr(), None, ws.data_ptr(), S())
         got = ids.cpu().numpy()
         for b, h in enumerate(histories):
             s = wo.process_logits(logits[b], h, g, True)
@@ -235,6 +269,6 @@ def test_logits_select_matches_oracle_processors():
         p = _params(V, st, mode=1)
         stt.zero_()
         _lib.call("tw_logits_select", lt.data_ptr(), B, V, sup.data_ptr(), ctypes.byref(p), stt.data_ptr(),
-                  None, 448, ids.data_ptr(), None, S())
+                  None, 448, ids.data_ptr(), None, ws.data_ptr(), S())
         ref = st.lang_begin + logits[:, st.lang_begin: st.lang_end].argmax(1)
         assert np.array_equal(ids.cpu().numpy(), ref)

@@ -158,6 +158,7 @@ extern "C" int tw_attn_encoder(const bf16_t* qkv, int B, int S, int H, bf16_t* o
 // Phase 2: softmax over <= max_keys scores held in LDS. Phase 3: groups accumulate p.v over their
 // keys (8 dims per lane), then an LDS reduction over the 32 groups.
 #define DA_MAXK 1536
+#define DA_UNR 8  // key rows of loads in flight per 8-lane group
 
 __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf16_t* K, const bf16_t* V, int nkeys,
                                   float* sc /*[DA_MAXK] LDS*/, float* part /*[32][64] LDS*/, float* red /*[8]*/,
@@ -166,16 +167,28 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
   float qv[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) qv[e] = qf[gl * 8 + e];
-  for (int key = g; key < nkeys; key += 32) {
-    uint4 kk = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
-    const bf16_t* ke = (const bf16_t*)&kk;
-    float d = 0.f;
+  // pass 1: scores. Iteration it covers keys it*32 .. it*32+31 (4 KB contiguous per block); DA_UNR
+  // iterations of loads are issued before any is consumed (keys past the end re-read the last row).
+  const int nit = (nkeys + 31) >> 5;
+  for (int it0 = 0; it0 < nit; it0 += DA_UNR) {
+    uint4 kk[DA_UNR];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
-    d += __shfl_xor(d, 1, 64);
-    d += __shfl_xor(d, 2, 64);
-    d += __shfl_xor(d, 4, 64);
-    if (gl == 0) sc[key] = d;
+    for (int u = 0; u < DA_UNR; ++u) {
+      const int key = min((it0 + u) * 32 + g, nkeys - 1);
+      kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < DA_UNR; ++u) {
+      const bf16_t* ke = (const bf16_t*)&kk[u];
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      const int key = (it0 + u) * 32 + g;
+      if (gl == 0 && key < nkeys) sc[key] = d;
+    }
   }
   __syncthreads();
   float mx = -INFINITY;
@@ -195,19 +208,30 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
   if ((tid & 63) == 0) red[4 + (tid >> 6)] = sum;
   __syncthreads();
   const float inv = 1.f / (red[4] + red[5] + red[6] + red[7]);
+  // pass 2: P.V with the same access pattern
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int key = g; key < nkeys; key += 32) {
-    uint4 vv = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
-    const bf16_t* ve = (const bf16_t*)&vv;
-    const float p = sc[key];
+  for (int it0 = 0; it0 < nit; it0 += DA_UNR) {
+    uint4 vv[DA_UNR];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] += p * bf16_to_f32(ve[e]);
+    for (int u = 0; u < DA_UNR; ++u) {
+      const int key = min((it0 + u) * 32 + g, nkeys - 1);
+      vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < DA_UNR; ++u) {
+      const int key = (it0 + u) * 32 + g;
+      const float p = key < nkeys ? sc[key] : 0.f;
+      const bf16_t* ve = (const bf16_t*)&vv[u];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += p * bf16_to_f32(ve[e]);
+    }
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) part[g * 64 + gl * 8 + e] = acc[e];
   __syncthreads();
   if (tid < 64) {
     float v = 0.f;
+#pragma unroll 8
     for (int gg = 0; gg < 32; ++gg) v += part[gg * 64 + tid];
     outv[tid] = v * inv;
   }

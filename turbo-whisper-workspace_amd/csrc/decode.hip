@@ -32,64 +32,89 @@ __device__ inline void lse_merge(float& m, float& s, float m2, float s2) {
   else s = s + s2 * __expf(m2 - m);
 }
 
-__global__ __launch_bounds__(256) void k_logits_select(const float* __restrict__ logits, int ld_logits,
-                                                       const uint32_t* __restrict__ suppress_bits, TwSelectParams p,
-                                                       int* __restrict__ state, int* __restrict__ tokens_out,
-                                                       int ld_tokens, int* __restrict__ next_ids,
-                                                       int* __restrict__ pos) {
-  __shared__ Best sb_text[4], sb_ts[4];
-  __shared__ float sm_ts[4], ss_ts[4];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  int* st = state + b * TW_STATE_STRIDE;
-  const float* row = logits + (size_t)b * ld_logits;
-  const int n_gen = st[TW_ST_NGEN], last = st[TW_ST_LAST], penult = st[TW_ST_PENULT], last_ts = st[TW_ST_LASTTS];
-  const int V = p.V, tsb = p.ts_begin;
+// Partial record of one vocab chunk of one row (8 words).
+struct SelPart {
+  float bt_v; int bt_i;   // best text (or mode-1) candidate
+  float bs_v; int bs_i;   // best timestamp candidate
+  float m_ts, s_ts;       // logsumexp state over the timestamp logits
+  float pad0, pad1;
+};
 
-  // ---- per-row mask parameters (WhisperTimeStampLogitsProcessor.__call__) ----
-  int mask_ts_all = 0, mask_text_lt_eos = 0, ts_lo_block = tsb, ts_hi_block = tsb;  // masked [tsb, ts_hi_block)
-  int init_step = (n_gen == 0);
+// Row-constant masks of WhisperTimeStampLogitsProcessor.__call__ for this step.
+struct RowMask {
+  int init_step, mask_ts_all, mask_text_lt_eos, ts_hi_block;
+};
+__device__ inline RowMask row_mask(const int* st, const TwSelectParams& p) {
+  const int n_gen = st[TW_ST_NGEN], last = st[TW_ST_LAST], penult = st[TW_ST_PENULT], last_ts = st[TW_ST_LASTTS];
+  const int tsb = p.ts_begin;
+  RowMask r{n_gen == 0, 0, 0, tsb};
   if (p.mode == 0 && p.use_timestamps) {
     const bool last_was_ts = n_gen >= 1 && last >= tsb;
     const bool penult_was_ts = n_gen < 2 || penult >= tsb;
     if (last_was_ts) {
-      if (penult_was_ts) mask_ts_all = 1;
-      else mask_text_lt_eos = 1;
+      if (penult_was_ts) r.mask_ts_all = 1;
+      else r.mask_text_lt_eos = 1;
     }
-    if (last_ts >= 0) ts_hi_block = (last_was_ts && !penult_was_ts) ? last_ts : last_ts + 1;
+    if (last_ts >= 0) r.ts_hi_block = (last_was_ts && !penult_was_ts) ? last_ts : last_ts + 1;
   }
+  return r;
+}
 
+// grid (B, TW_SELECT_CHUNKS): chunk c of row b scans vocab [c*V/NC, (c+1)*V/NC) with float4 loads where aligned.
+__global__ __launch_bounds__(256) void k_select_partial(const float* __restrict__ logits, int ld_logits,
+                                                        const uint32_t* __restrict__ suppress_bits, TwSelectParams p,
+                                                        const int* __restrict__ state, SelPart* __restrict__ ws) {
+  __shared__ SelPart sp[4];
+  const int b = blockIdx.x, c = blockIdx.y, NC = gridDim.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const RowMask rm = row_mask(state + b * TW_STATE_STRIDE, p);
+  const float* row = logits + (size_t)b * ld_logits;
+  const int V = p.V, tsb = p.ts_begin;
+  const int v0 = (int)((long)c * V / NC), v1 = (int)((long)(c + 1) * V / NC);
   Best bt{-INFINITY, 0x7fffffff}, bs{-INFINITY, 0x7fffffff};
   float m_ts = -INFINITY, s_ts = 0.f;
-  for (int v = tid; v < V; v += 256) {
-    float x = row[v];
-    bool masked = false;
-    if (p.mode == 1) {
-      masked = (v < p.lo || v >= p.hi);
-    } else {
-      if (init_step)
-        for (int i = 0; i < p.n_begin_suppress; ++i) masked |= (v == p.begin_suppress[i]);
-      if (suppress_bits) masked |= (suppress_bits[v >> 5] >> (v & 31)) & 1u;
-      if (p.use_timestamps) {
-        masked |= (v == p.no_timestamps);
-        if (v >= tsb) {
-          masked |= mask_ts_all;
-          masked |= (v >= ts_lo_block && v < ts_hi_block);
-          if (init_step && p.max_initial_ts >= 0) masked |= (v > tsb + p.max_initial_ts);
-        } else {
-          masked |= mask_text_lt_eos && (v < p.eos);
-          masked |= init_step;
+  // 4 loads in flight per thread; indices clamped into the chunk (duplicates are dropped by `ok`)
+  for (int base = v0 + tid; base < v1; base += 4 * 256) {
+    float xs[4];
+    uint32_t sb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int v = min(base + 256 * u, v1 - 1);
+      xs[u] = row[v];
+      sb[u] = suppress_bits ? suppress_bits[v >> 5] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int v = base + 256 * u;
+      const bool ok = v < v1;
+      float x = xs[u];
+      bool masked;
+      if (p.mode == 1) {
+        masked = (v < p.lo || v >= p.hi);
+      } else {
+        masked = (sb[u] >> (v & 31)) & 1u;
+        if (rm.init_step)
+          for (int i = 0; i < p.n_begin_suppress; ++i) masked |= (v == p.begin_suppress[i]);
+        if (p.use_timestamps) {
+          masked |= (v == p.no_timestamps);
+          if (v >= tsb) {
+            masked |= rm.mask_ts_all || (v < rm.ts_hi_block);
+            if (rm.init_step && p.max_initial_ts >= 0) masked |= (v > tsb + p.max_initial_ts);
+          } else {
+            masked |= (rm.mask_text_lt_eos && v < p.eos) || rm.init_step;
+          }
         }
       }
-    }
-    if (masked) x = -INFINITY;
-    if (v < tsb || !p.use_timestamps || p.mode == 1) {
-      bt = best_of(bt, Best{x, v});
-    } else {
-      bs = best_of(bs, Best{x, v});
-      if (x != -INFINITY) lse_merge(m_ts, s_ts, x, 1.f);
+      if (masked) x = -INFINITY;
+      if (!ok) continue;
+      if (v < tsb || !p.use_timestamps || p.mode == 1) {
+        bt = best_of(bt, Best{x, v});
+      } else {
+        bs = best_of(bs, Best{x, v});
+        if (x != -INFINITY) lse_merge(m_ts, s_ts, x, 1.f);
+      }
     }
   }
-  // wave + block reductions
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     Best ot{__shfl_xor(bt.v, o, 64), __shfl_xor(bt.i, o, 64)};
@@ -99,15 +124,47 @@ __global__ __launch_bounds__(256) void k_logits_select(const float* __restrict__
     float m2 = __shfl_xor(m_ts, o, 64), s2 = __shfl_xor(s_ts, o, 64);
     lse_merge(m_ts, s_ts, m2, s2);
   }
-  if (lane == 0) { sb_text[wid] = bt; sb_ts[wid] = bs; sm_ts[wid] = m_ts; ss_ts[wid] = s_ts; }
+  if (lane == 0) sp[wid] = SelPart{bt.v, bt.i, bs.v, bs.i, m_ts, s_ts, 0.f, 0.f};
   __syncthreads();
-  if (tid != 0) return;
-  if (pos) pos[b] += 1;  // the next decoder step writes its K/V one position later
-  for (int w = 1; w < 4; ++w) {
-    bt = best_of(bt, sb_text[w]);
-    bs = best_of(bs, sb_ts[w]);
-    lse_merge(m_ts, s_ts, sm_ts[w], ss_ts[w]);
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w) {
+      bt = best_of(bt, Best{sp[w].bt_v, sp[w].bt_i});
+      bs = best_of(bs, Best{sp[w].bs_v, sp[w].bs_i});
+      lse_merge(m_ts, s_ts, sp[w].m_ts, sp[w].s_ts);
+    }
+    ws[b * NC + c] = SelPart{bt.v, bt.i, bs.v, bs.i, m_ts, s_ts, 0.f, 0.f};
   }
+}
+
+// grid B, one wave: merge the row's chunk records (in chunk order: ties keep the first index), then
+// the selection rule of the timestamp processor, the pad-after-EOS / stopping rule of _sample, and
+// the processor state update.
+__global__ __launch_bounds__(64) void k_select_final(const SelPart* __restrict__ ws, int NC, TwSelectParams p,
+                                                     int* __restrict__ state, int* __restrict__ tokens_out,
+                                                     int ld_tokens, int* __restrict__ next_ids,
+                                                     int* __restrict__ pos) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  Best bt{-INFINITY, 0x7fffffff}, bs{-INFINITY, 0x7fffffff};
+  float m_ts = -INFINITY, s_ts = 0.f;
+  for (int c = lane; c < NC; c += 64) {
+    const SelPart r = ws[b * NC + c];
+    bt = best_of(bt, Best{r.bt_v, r.bt_i});
+    bs = best_of(bs, Best{r.bs_v, r.bs_i});
+    lse_merge(m_ts, s_ts, r.m_ts, r.s_ts);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Best ot{__shfl_xor(bt.v, o, 64), __shfl_xor(bt.i, o, 64)};
+    Best os{__shfl_xor(bs.v, o, 64), __shfl_xor(bs.i, o, 64)};
+    bt = best_of(bt, ot);
+    bs = best_of(bs, os);
+    float m2 = __shfl_xor(m_ts, o, 64), s2 = __shfl_xor(s_ts, o, 64);
+    lse_merge(m_ts, s_ts, m2, s2);
+  }
+  if (lane != 0) return;
+  int* st = state + b * TW_STATE_STRIDE;
+  const int n_gen = st[TW_ST_NGEN], last = st[TW_ST_LAST];
+  if (pos) pos[b] += 1;  // the next decoder step writes its K/V one position later
   int sel;
   if (p.mode == 1) {
     sel = bt.i;
@@ -129,18 +186,23 @@ __global__ __launch_bounds__(256) void k_logits_select(const float* __restrict__
   if (next_ids) next_ids[b] = tok;
   st[TW_ST_PENULT] = last;
   st[TW_ST_LAST] = tok;
-  if (tok >= tsb && p.use_timestamps) st[TW_ST_LASTTS] = tok;
+  if (tok >= p.ts_begin && p.use_timestamps) st[TW_ST_LASTTS] = tok;
   st[TW_ST_NGEN] = n_gen + 1;
   if (!finished && (tok == p.eos || n_gen + 1 >= p.max_new)) st[TW_ST_FINISHED] = 1;
 }
 
 extern "C" int tw_logits_select(const float* logits, int B, int ld_logits, const uint32_t* suppress_bits,
                                 const TwSelectParams* params, int* state, int* tokens_out, int ld_tokens,
-                                int* next_ids, int* pos, void* stream) {
-  TW_REQUIRE(logits && params && state && B > 0, "tw_logits_select: bad args");
+                                int* next_ids, int* pos, float* workspace, void* stream) {
+  TW_REQUIRE(logits && params && state && workspace && B > 0, "tw_logits_select: bad args");
   TW_REQUIRE(params->V > 0 && params->V <= ld_logits, "tw_logits_select: V=%d ld=%d", params->V, ld_logits);
   TW_REQUIRE(params->n_begin_suppress >= 0 && params->n_begin_suppress <= 8, "tw_logits_select: begin_suppress");
-  hipLaunchKernelGGL(k_logits_select, dim3(B), dim3(256), 0, (hipStream_t)stream, logits, ld_logits, suppress_bits,
-                     *params, state, tokens_out, ld_tokens, next_ids, pos);
+  static_assert(sizeof(SelPart) * TW_SELECT_CHUNKS == sizeof(float) * TW_SELECT_WS_PER_ROW, "workspace size");
+  hipStream_t s = (hipStream_t)stream;
+  SelPart* ws = (SelPart*)workspace;
+  hipLaunchKernelGGL(k_select_partial, dim3(B, TW_SELECT_CHUNKS), dim3(256), 0, s, logits, ld_logits, suppress_bits,
+                     *params, state, ws);
+  hipLaunchKernelGGL(k_select_final, dim3(B), dim3(64), 0, s, ws, TW_SELECT_CHUNKS, *params, state, tokens_out,
+                     ld_tokens, next_ids, pos);
   return tw_check_launch("tw_logits_select");
 }

@@ -113,3 +113,93 @@ extern "C" int tw_embed_decoder(const bf16_t* tok_emb, const bf16_t* pos_emb, co
   hipLaunchKernelGGL(k_embed_decoder, dim3(B), dim3(256), 0, (hipStream_t)stream, tok_emb, pos_emb, ids, pos, D, x);
   return tw_check_launch("tw_embed_decoder");
 }
+
+// Decoder residual update + LayerNorm, one block per row:
+//   x[row] += bias + sum_p parts[p][row]   (the split-K partial sums of the previous projection,
+//                                           tw_gemm_bf16_partial; nparts = 0 and bias = NULL: no update)
+//   out[row] = bf16(LayerNorm(x[row]))      (gamma = NULL: residual update only)
+// Restates the residual adds of WhisperDecoderLayer.forward ($TF/models/whisper/modeling_whisper.py:
+// 468-505) fused with the next pre-LayerNorm (:434,443,446,682).
+#define RLN_MAXV 4  // float4 chunks per thread: D <= 4096
+// All loads are unconditional (index clamped into the row, result discarded): a guarded load per
+// element makes hipcc wait vmcnt(0) per element, a chain of L2 round trips.
+__global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const float* __restrict__ parts, int nparts,
+                                                  long part_stride, const float* __restrict__ bias,
+                                                  const float* __restrict__ g, const float* __restrict__ bta, int D,
+                                                  float eps, bf16_t* __restrict__ out) {
+  __shared__ float red[8];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int nc = D >> 2;
+  float* xr = x + (size_t)row * D;
+  const float* pr = parts ? parts + (size_t)row * D : nullptr;
+  float4 v[RLN_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < RLN_MAXV; ++i) {
+    const int c = min(tid + 256 * i, nc - 1);
+    float4 a = ((const float4*)xr)[c];
+    if (bias) {
+      const float4 bb = ((const float4*)bias)[c];
+      a.x += bb.x; a.y += bb.y; a.z += bb.z; a.w += bb.w;
+    }
+    if (nparts > 0) {
+      float4 q[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) q[p] = ((const float4*)(pr + min(p, nparts - 1) * part_stride))[c];
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        if (p < nparts) { a.x += q[p].x; a.y += q[p].y; a.z += q[p].z; a.w += q[p].w; }
+      for (int p = 4; p < nparts; ++p) {
+        const float4 qq = ((const float4*)(pr + p * part_stride))[c];
+        a.x += qq.x; a.y += qq.y; a.z += qq.z; a.w += qq.w;
+      }
+    }
+    v[i] = a;
+    if (tid + 256 * i < nc) s += (a.x + a.y) + (a.z + a.w);
+  }
+  if (nparts > 0 || bias) {
+#pragma unroll
+    for (int i = 0; i < RLN_MAXV; ++i)
+      if (tid + 256 * i < nc) ((float4*)xr)[tid + 256 * i] = v[i];
+  }
+  if (!g) return;
+  s = wave_sum(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < RLN_MAXV; ++i) {
+    if (tid + 256 * i < nc) {
+      const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+      q += (a * a + b * b) + (c * c + d * d);
+    }
+  }
+  q = wave_sum(q);
+  if ((tid & 63) == 0) red[4 + (tid >> 6)] = q;
+  __syncthreads();
+  const float rstd = rsqrtf((red[4] + red[5] + red[6] + red[7]) / (float)D + eps);
+  bf16_t* orow = out + (size_t)row * D;
+#pragma unroll
+  for (int i = 0; i < RLN_MAXV; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nc) {
+      const float4 gg = ((const float4*)g)[c], bb = ((const float4*)bta)[c];
+      uint2 w;
+      w.x = pack_bf16x2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
+      w.y = pack_bf16x2((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+      ((uint2*)orow)[c] = w;
+    }
+  }
+}
+
+extern "C" int tw_resid_layernorm(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
+                                  const float* beta, int M, int D, float eps, uint16_t* out, void* stream) {
+  TW_REQUIRE(x && M > 0 && D > 0 && D % 4 == 0 && D <= 1024 * RLN_MAXV, "tw_resid_layernorm: bad args (D %% 4, D <= %d)",
+             1024 * RLN_MAXV);
+  TW_REQUIRE(nparts >= 0 && (nparts == 0 || parts), "tw_resid_layernorm: parts");
+  TW_REQUIRE(!gamma || (beta && out), "tw_resid_layernorm: gamma without beta/out");
+  hipLaunchKernelGGL(k_resid_ln, dim3(M), dim3(256), 0, (hipStream_t)stream, x, parts, nparts, (long)M * D, bias, gamma,
+                     beta, D, eps, out);
+  return tw_check_launch("tw_resid_layernorm");
+}

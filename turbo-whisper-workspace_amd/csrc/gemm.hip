@@ -159,35 +159,235 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(const bf16_t* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------------
-// Skinny kernel (M <= 32): weight streaming GEMV-like MFMA
+// Large-M kernel, 256 x 256 x 64 tiles (encoder projections, FFN, conv stem, cross-K/V)
 // ------------------------------------------------------------------------------------------------
-// Block = 4 waves = 16 output columns. Wave w handles the K range [w*K/4, (w+1)*K/4) for two
-// 16-row M tiles (rows 0..15 and 16..31) with v_mfma_f32_16x16x32_bf16:
+// 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns a 128 x 64 sub-tile = 8 x 4 accumulators of
+// v_mfma_f32_16x16x32_bf16 (128 accumulator registers). One workgroup per CU (128 KiB LDS: two
+// buffers of the A and W tiles). Tiles are staged HBM/L2 -> LDS by global_load_lds_dwordx4 (LDS-DMA,
+// no VGPR round trip): one wave-instruction moves 8 rows x 128 B; the LDS image is lane-linear, so the
+// bank swizzle is applied on the SOURCE chunk (chunk ^ swz(row)) and undone on the ds_read_b128
+// address (same involution). swz(r) = (r >> 1) & 7 makes every 16x16x32 fragment read conflict-free.
+// K loop: issue tile t+1's DMA, run tile t's 64 MFMAs per wave, then one vmcnt(0) + barrier.
+// Epilogue: accumulators go through LDS (64-row halves, padded rows) so every global load/store of the
+// fused epilogue (bias, GELU, residual f32 read-modify-write, positional add, cross-K/V scatter) is a
+// 16-byte (f32) or 8-byte (bf16) access of 4 consecutive columns.
+#define GB_BM 256
+#define GB_BN 256
+#define GB_BK 64
+#define GB_EPI_LD 68  // f32 row stride of the epilogue staging image (64 + 4: conflict-free writes)
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ inline int gb_swz(int r) { return (r >> 1) & 7; }
+
+// epilogue of 4 consecutive columns n..n+3 of row m (v already includes the bias)
+template <int EPI>
+__device__ inline void epi_store4(const EpiArgs& ea, int m, int n, int N, float4 v) {
+  if (n + 3 >= N) {  // ragged right edge (tests only: the model's N are multiples of 256)
+    const float t[4] = {v.x, v.y, v.z, v.w};
+    EpiArgs e2 = ea;
+    e2.bias = nullptr;
+    for (int q = 0; q < 4; ++q)
+      if (n + q < N) epi_store<EPI>(e2, m, n + q, t[q]);
+    return;
+  }
+  if constexpr (EPI == TW_EPI_BF16 || EPI == TW_EPI_GELU_BF16) {
+    if constexpr (EPI == TW_EPI_GELU_BF16) {
+      v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+    }
+    uint2 w;
+    w.x = pack_bf16x2(v.x, v.y);
+    w.y = pack_bf16x2(v.z, v.w);
+    *(uint2*)((bf16_t*)ea.out + (size_t)m * ea.ldo + n) = w;
+  } else if constexpr (EPI == TW_EPI_RESID_F32) {
+    float4* o = (float4*)((float*)ea.out + (size_t)m * ea.ldo + n);
+    float4 x = *o;
+    x.x += v.x; x.y += v.y; x.z += v.z; x.w += v.w;
+    *o = x;
+  } else if constexpr (EPI == TW_EPI_GELU_POS_F32) {
+    const float4 a = *(const float4*)(ea.aux + (size_t)(m % ea.aux_rows) * ea.ldo + n);
+    float4 o;
+    o.x = gelu_erf(v.x) + a.x; o.y = gelu_erf(v.y) + a.y; o.z = gelu_erf(v.z) + a.z; o.w = gelu_erf(v.w) + a.w;
+    *(float4*)((float*)ea.out + (size_t)m * ea.ldo + n) = o;
+  } else if constexpr (EPI == TW_EPI_F32) {
+    *(float4*)((float*)ea.out + (size_t)m * ea.ldo + n) = v;
+  } else if constexpr (EPI == TW_EPI_CROSSKV) {
+    const int D = ea.kv_D, S = ea.kv_S;
+    int l = n / (2 * D), rem = n - l * 2 * D;
+    int kv = rem / D, hd = rem - kv * D;
+    int h = hd >> 6, d = hd & 63;
+    int b = m / S, s = m - b * S;
+    size_t idx = ((((size_t)(l * 2 + kv) * ea.kv_B + b) * ea.kv_H + h) * S + s) * 64 + d;
+    uint2 w;
+    w.x = pack_bf16x2(v.x, v.y);
+    w.y = pack_bf16x2(v.z, v.w);
+    *(uint2*)((bf16_t*)ea.out + idx) = w;
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                     int M, int N, int K, int lda, int ldw, EpiArgs ea) {
+  // [buf][A | W][256 rows x 64 k] bf16 = 128 KiB for the K loop; 8 x [64][68] f32 = 136 KiB after it
+  __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 64 * GB_EPI_LD * 2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntm = (M + GB_BM - 1) / GB_BM, ntn = (N + GB_BN - 1) / GB_BN;
+  const int nwg = ntm * ntn;
+  // XCD-aware bijective remap: blocks b, b+8, ... (one XCD under round-robin dispatch) take consecutive
+  // tile ids, so the N-tiles of one A row-panel are computed out of one L2.
+  const int orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int tm = wgid / ntn, tn = wgid - tm * ntn;
+  const int m0 = tm * GB_BM, n0 = tn * GB_BN;
+
+  // DMA assignment: wave w issues instructions i = 0..3 for A and for W; instruction (w, i) fills tile
+  // rows 8(4w+i) .. 8(4w+i)+7. Lane l: row 8(4w+i) + (l>>3), LDS chunk slot l&7 <- global chunk
+  // (l&7) ^ swz(row).
+  const bf16_t* ga[4];
+  const bf16_t* gw[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (4 * wid + i) + (lane >> 3);
+    const int ch = (lane & 7) ^ gb_swz(row);
+    ga[i] = A + (size_t)min(m0 + row, M - 1) * lda + ch * 8;
+    gw[i] = W + (size_t)min(n0 + row, N - 1) * ldw + ch * 8;
+  }
+  auto stage = [&](int buf, int k0) {
+    bf16_t* As = smem + buf * 2 * GB_BM * GB_BK;
+    bf16_t* Ws = As + GB_BM * GB_BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rb = 8 * (4 * wid + i) * GB_BK;  // wave-uniform LDS base of this instruction
+      __builtin_amdgcn_global_load_lds((const void*)(ga[i] + k0), (lds_void_t*)(As + rb), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(gw[i] + k0), (lds_void_t*)(Ws + rb), 16, 0, 0);
+    }
+  };
+
+  const int wr = wid >> 2, wc = wid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / GB_BK;
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * GB_BK);
+    const bf16_t* As = smem + cur * 2 * GB_BM * GB_BK;
+    const bf16_t* Ws = As + GB_BM * GB_BK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int kc = 4 * kk + fq;
+      bf16x8 bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wc * 64 + j * 16 + fr;
+        bfr[j] = *(const bf16x8*)(Ws + col * GB_BK + ((kc ^ gb_swz(col)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = wr * 128 + i * 16 + fr;
+        const bf16x8 af = *(const bf16x8*)(As + row * GB_BK + ((kc ^ gb_swz(row)) << 3));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // vmcnt(0) (tile kt+1 landed) + lgkmcnt(0) + barrier
+  }
+
+  // ---- epilogue through LDS: each wave stages 64 of its 128 rows at a time in its own
+  // [64][GB_EPI_LD] f32 image (8 images = 136 KiB, the LDS the K loop used plus 8 KiB), then reads
+  // back 4 consecutive columns per lane (16 lanes x 16 B per row) for vectorised global I/O.
+  const int ncol0 = n0 + wc * 64;
+  const int rc = (lane & 15) * 4;  // this lane's 4 columns in the read-back phase
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ea.bias) {
+    const int n = ncol0 + rc;
+    bias4.x = ea.bias[min(n, N - 1)];
+    bias4.y = ea.bias[min(n + 1, N - 1)];
+    bias4.z = ea.bias[min(n + 2, N - 1)];
+    bias4.w = ea.bias[min(n + 3, N - 1)];
+  }
+  float* wimg = (float*)smem + wid * (64 * GB_EPI_LD);
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int ib = 4 * half;
+    if (half) __syncthreads();  // (first pass: the K loop ended on a barrier)
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wimg[(ii * 16 + fq * 4 + r) * GB_EPI_LD + j * 16 + fr] = acc[ib + ii][j][r];
+    __syncthreads();
+    const int mrow0 = m0 + wr * 128 + ib * 16;
+#pragma unroll 4
+    for (int rr = 0; rr < 16; ++rr) {
+      const int lr = rr * 4 + (lane >> 4);  // 4 rows per wave-instruction
+      const int m = mrow0 + lr;
+      float4 v = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
+      v.x += bias4.x; v.y += bias4.y; v.z += bias4.z; v.w += bias4.w;
+      if (m < M && ncol0 + rc < N) epi_store4<EPI>(ea, m, ncol0 + rc, N, v);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Skinny kernel (M <= 32): weight-streaming MFMA GEMV for the decoder step
+// ------------------------------------------------------------------------------------------------
+// Block = NW waves = 16 output columns; the K range is cut into NW * gridDim.y slices of 32-deep
+// steps (wave w of block row y takes slice y*NW + w). Each wave streams its slice of the 16 weight
+// rows straight to VGPRs (every weight byte is read exactly once per step: this path is HBM-bound)
+// with 8 steps of loads in flight, and runs v_mfma_f32_16x16x32_bf16 on two 16-row M tiles:
 //   A lane l: A[row = l&15][k = 8(l>>4)+j]   B lane l: W[col = l&15][k = 8(l>>4)+j]
 //   C lane l: col = l&15, row = (l>>4)*4 + reg
-template <int EPI>
-__global__ __launch_bounds__(256) void k_gemm_skinny(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
-                                                     int M, int N, int K, int lda, int ldw, EpiArgs ea) {
-  __shared__ float red[4][32][17];
+// The NW partial sums meet in LDS. gridDim.y > 1 (split-K over blocks, used for the N = d_model
+// projections whose 80 column groups alone cannot fill 256 CUs): each block row writes its f32 partial
+// to part[y][M][ldo] and the consumer (tw_resid_layernorm) adds the partials, bias and residual.
+#define TW_EPI_PARTIAL 100
+
+template <int EPI, int NW, bool TWO>
+__global__ __launch_bounds__(NW * 64) void k_gemm_skinny(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                         int M, int N, int K, int lda, int ldw, EpiArgs ea) {
+  __shared__ float red[NW][32][17];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int n0 = blockIdx.x * 16;
-  const int kq = K / 4;               // K % 128 == 0 guaranteed by host
-  const int kb = wid * kq;
+  const int nsl = NW * gridDim.y, gw = blockIdx.y * NW + wid;
+  const int ns = K >> 5;
+  const int s0 = (int)((long)gw * ns / nsl), s1 = (int)((long)(gw + 1) * ns / nsl);
   const int col = min(n0 + (lane & 15), N - 1);
   const int ksub = 8 * (lane >> 4);
   const int ar0 = min(lane & 15, M - 1), ar1 = min(16 + (lane & 15), M - 1);
-  const bf16_t* wp = W + (size_t)col * ldw + kb + ksub;
-  const bf16_t* ap0 = A + (size_t)ar0 * lda + kb + ksub;
-  const bf16_t* ap1 = A + (size_t)ar1 * lda + kb + ksub;
+  const bf16_t* wp = W + (size_t)col * ldw + ksub;
+  const bf16_t* ap0 = A + (size_t)ar0 * lda + ksub;
+  const bf16_t* ap1 = A + (size_t)ar1 * lda + ksub;
   f32x4 c0 = {0}, c1 = {0};
-  const bool two = M > 16;
-#pragma unroll 4
-  for (int k = 0; k < kq; k += 32) {
-    bf16x8 bw = *(const bf16x8*)(wp + k);
-    bf16x8 a0 = *(const bf16x8*)(ap0 + k);
+  int s = s0;
+  for (; s + 8 <= s1; s += 8) {
+    bf16x8 bw[8], a0[8], a1[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      bw[u] = *(const bf16x8*)(wp + 32 * (s + u));
+      a0[u] = *(const bf16x8*)(ap0 + 32 * (s + u));
+      if (TWO) a1[u] = *(const bf16x8*)(ap1 + 32 * (s + u));
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], bw[u], c0, 0, 0, 0);
+      if (TWO) c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], bw[u], c1, 0, 0, 0);
+    }
+  }
+  for (; s < s1; ++s) {
+    bf16x8 bw = *(const bf16x8*)(wp + 32 * s);
+    bf16x8 a0 = *(const bf16x8*)(ap0 + 32 * s);
     c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bw, c0, 0, 0, 0);
-    if (two) {
-      bf16x8 a1 = *(const bf16x8*)(ap1 + k);
+    if (TWO) {
+      bf16x8 a1 = *(const bf16x8*)(ap1 + 32 * s);
       c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bw, c1, 0, 0, 0);
     }
   }
@@ -195,27 +395,71 @@ __global__ __launch_bounds__(256) void k_gemm_skinny(const bf16_t* __restrict__ 
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     red[wid][rb + r][cc] = c0[r];
-    red[wid][16 + rb + r][cc] = c1[r];
+    if (TWO) red[wid][16 + rb + r][cc] = c1[r];
   }
   __syncthreads();
-  for (int e = tid; e < 32 * 16; e += 256) {
+  const int rows = TWO ? 32 : 16;
+  for (int e = tid; e < rows * 16; e += NW * 64) {
     int m = e >> 4, c = e & 15;
     int n = n0 + c;
     if (m < M && n < N) {
-      float v = red[0][m][c] + red[1][m][c] + red[2][m][c] + red[3][m][c];
-      epi_store<EPI>(ea, m, n, v);
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v += red[w][m][c];
+      if constexpr (EPI == TW_EPI_PARTIAL) {
+        ((float*)ea.out)[((size_t)blockIdx.y * M + m) * ea.ldo + n] = v;
+      } else {
+        epi_store<EPI>(ea, m, n, v);
+      }
     }
   }
+}
+
+template <int EPI, int NW>
+static void launch_skinny_nw(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int ldw,
+                             const EpiArgs& ea, int splits, hipStream_t s) {
+  dim3 grid(tw_cdiv(N, 16), splits);
+  if (M > 16)
+    hipLaunchKernelGGL((k_gemm_skinny<EPI, NW, true>), grid, dim3(NW * 64), 0, s, A, W, M, N, K, lda, ldw, ea);
+  else
+    hipLaunchKernelGGL((k_gemm_skinny<EPI, NW, false>), grid, dim3(NW * 64), 0, s, A, W, M, N, K, lda, ldw, ea);
+}
+
+// Waves per block: enough column-group x K-slice waves to put ~4 waves on every CU, while every wave keeps
+// at least two 32-deep steps.
+template <int EPI>
+static void launch_skinny(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int ldw,
+                          const EpiArgs& ea, int splits, hipStream_t s) {
+  const long nb = tw_cdiv(N, 16) * (long)splits;
+  const int ns = K / 32;
+  int nw = 4;
+  while (nb * nw < 1024 && nw < 16 && ns >= 2 * 2 * nw * splits) nw *= 2;
+  if (nw == 4) launch_skinny_nw<EPI, 4>(A, W, M, N, K, lda, ldw, ea, splits, s);
+  else if (nw == 8) launch_skinny_nw<EPI, 8>(A, W, M, N, K, lda, ldw, ea, splits, s);
+  else launch_skinny_nw<EPI, 16>(A, W, M, N, K, lda, ldw, ea, splits, s);
+}
+
+// Large-M kernel selection (1 = 256x256 LDS-DMA kernel, 0 = 128x128 register-staged kernel);
+// tw_gemm_set_variant() switches it for A/B measurement.
+static int tw_gemm_big_enabled = 1;
+extern "C" int tw_gemm_set_variant(int big) {
+  tw_gemm_big_enabled = big ? 1 : 0;
+  return 0;
 }
 
 template <int EPI>
 static int launch_gemm(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int ldw, const EpiArgs& ea,
                        hipStream_t s) {
-  if (M <= 32 && K % 128 == 0) {
-    hipLaunchKernelGGL(k_gemm_skinny<EPI>, dim3(tw_cdiv(N, 16)), dim3(256), 0, s, A, W, M, N, K, lda, ldw, ea);
+  if (M <= 32) {
+    launch_skinny<EPI>(A, W, M, N, K, lda, ldw, ea, 1, s);
   } else {
-    unsigned nwg = tw_cdiv(M, G_BM) * tw_cdiv(N, G_BN);
-    hipLaunchKernelGGL(k_gemm_tile<EPI>, dim3(nwg), dim3(256), 0, s, A, W, M, N, K, lda, ldw, ea);
+    if (tw_gemm_big_enabled) {
+      unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
+      hipLaunchKernelGGL(k_gemm_big<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
+    } else {
+      unsigned nwg = tw_cdiv(M, G_BM) * tw_cdiv(N, G_BN);
+      hipLaunchKernelGGL(k_gemm_tile<EPI>, dim3(nwg), dim3(256), 0, s, A, W, M, N, K, lda, ldw, ea);
+    }
   }
   return tw_check_launch("tw_gemm_bf16");
 }
@@ -244,4 +488,17 @@ extern "C" int tw_gemm_bf16(const bf16_t* A, const bf16_t* W, int M, int N, int 
       return launch_gemm<TW_EPI_CROSSKV>(A, W, M, N, K, lda, ldw, ea, s);
     default: tw_set_error("tw_gemm_bf16: unknown epilogue %d", epi); return TW_ERR_ARG;
   }
+}
+
+extern "C" int tw_gemm_bf16_partial(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int ldw,
+                                    int splits, float* part, int ldp, void* stream) {
+  TW_REQUIRE(A && W && part, "tw_gemm_bf16_partial: null pointer");
+  TW_REQUIRE(M > 0 && M <= 32 && N > 0 && K > 0 && K % 32 == 0, "tw_gemm_bf16_partial: M=%d N=%d K=%d (M <= 32, K %% 32)",
+             M, N, K);
+  TW_REQUIRE(splits >= 1 && splits <= 16 && splits <= K / 32, "tw_gemm_bf16_partial: splits=%d", splits);
+  TW_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && lda >= K && ldw >= K && ldp >= N, "tw_gemm_bf16_partial: lda=%d ldw=%d ldp=%d",
+             lda, ldw, ldp);
+  EpiArgs ea{part, ldp, nullptr, nullptr, 0, 0, 0, 0, 0};
+  launch_skinny<TW_EPI_PARTIAL>(A, W, M, N, K, lda, ldw, ea, splits, (hipStream_t)stream);
+  return tw_check_launch("tw_gemm_bf16_partial");
 }

@@ -21,6 +21,8 @@ TW_EPI_GELU_POS_F32 = 3
 TW_EPI_F32 = 4
 TW_EPI_CROSSKV = 5
 
+TW_SELECT_CHUNKS = 16
+TW_SELECT_WS_PER_ROW = 128
 TW_STATE_STRIDE = 8
 TW_ST_NGEN, TW_ST_LAST, TW_ST_PENULT, TW_ST_LASTTS, TW_ST_FINISHED, TW_ST_LANG = 0, 1, 2, 3, 4, 5
 
@@ -28,7 +30,8 @@ TW_ST_NGEN, TW_ST_LAST, TW_ST_PENULT, TW_ST_LASTTS, TW_ST_FINISHED, TW_ST_LANG =
 EXPORTED = (
     "tw_version", "tw_last_error", "tw_fill_synth", "tw_f32_to_bf16", "tw_logmel", "tw_im2col_conv1",
     "tw_im2col_conv2", "tw_gemm_bf16", "tw_layernorm", "tw_attn_encoder", "tw_attn_decode_self",
-    "tw_attn_decode_cross", "tw_embed_decoder", "tw_logits_select",
+    "tw_attn_decode_cross", "tw_embed_decoder", "tw_logits_select", "tw_gemm_bf16_partial", "tw_resid_layernorm",
+    "tw_gemm_set_variant",
 )
 
 
@@ -66,7 +69,10 @@ _SIGS = {
     "tw_attn_decode_self": ([_P, _I, _I, _I, _P, _P, _P, _P, _P], _I),
     "tw_attn_decode_cross": ([_P, _I, _I, _I, _I, _P, _P, _P, _P], _I),
     "tw_embed_decoder": ([_P, _P, _P, _P, _I, _I, _P, _P], _I),
-    "tw_logits_select": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), _P, _P, _I, _P, _P, _P], _I),
+    "tw_logits_select": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), _P, _P, _I, _P, _P, _P, _P], _I),
+    "tw_gemm_bf16_partial": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P], _I),
+    "tw_gemm_set_variant": ([_I], _I),
+    "tw_resid_layernorm": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
 }
 
 _lib = None

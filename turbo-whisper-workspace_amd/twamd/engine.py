@@ -28,6 +28,7 @@ from .weights import PackedWeights
 
 LN_EPS = 1e-5
 S_ENC = 1500
+DEC_SPLITS = 4   # split-K factor of the decoder's d_model-wide projections (out_proj, fc2)
 
 
 @dataclasses.dataclass
@@ -79,6 +80,8 @@ class WhisperEngine:
         self.attd = torch.empty(B, D, dtype=bf, device=dev)
         self.ffnd = torch.empty(B, F, dtype=bf, device=dev)
         self.logits = torch.empty(B, V, dtype=f32, device=dev)
+        self.parts = torch.empty(DEC_SPLITS, B, D, dtype=f32, device=dev)   # split-K partials (decoder)
+        self.sel_ws = torch.empty(B, _lib.TW_SELECT_WS_PER_ROW, dtype=f32, device=dev)
         self.state = torch.zeros(B, _lib.TW_STATE_STRIDE, dtype=i32, device=dev)
         self.tokens = torch.zeros(B, T, dtype=i32, device=dev)
         self.ids = torch.zeros(B, dtype=i32, device=dev)
@@ -180,30 +183,47 @@ class WhisperEngine:
         return self.hln[: R * S_ENC].view(R, S_ENC, self.d.d_model)
 
     # ------------------------------------------------------------------ decoder
+    def _partial(self, A, W, M, N, K):
+        """parts[:DEC_SPLITS, :M] = split-K partial sums of A . W^T (decoder; residual add in _resid_ln)."""
+        rec = self._begin_timer(("gemm_skinny", "partial"), 2.0 * M * N * K)
+        _lib.call("tw_gemm_bf16_partial", A.data_ptr(), W.data_ptr(), M, N, K, K, K, DEC_SPLITS, self.parts.data_ptr(),
+                  N, self._s)
+        self._end_timer(rec)
+
+    def _resid_ln(self, R, nparts, bias, g, b):
+        """xd += bias + sum(parts[:nparts]); hd = LayerNorm(xd) (one fused launch)."""
+        _lib.call("tw_resid_layernorm", self.xd.data_ptr(), self.parts.data_ptr() if nparts else None, nparts,
+                  _lib.ptr(bias), _lib.ptr(g), _lib.ptr(b), R, self.d.d_model, LN_EPS, _lib.ptr(self.hd), self._s)
+
     def decoder_step(self, R: int, with_logits: bool = True) -> None:
-        """One token per row: ids[b] at position pos[b] -> logits[b] (f32)."""
+        """One token per row: ids[b] at position pos[b] -> logits[b] (f32).
+
+        Residual stream xd stays f32; every d_model-wide projection (self/cross out_proj, fc2) is a split-K
+        partial product whose sum, bias and residual add are folded into the next LayerNorm launch."""
         d, w = self.d, self.w
         D, F, H, T = d.d_model, d.ffn, d.heads, d.max_target_positions
         _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), self.ids.data_ptr(),
                   self.pos.data_ptr(), R, D, self.xd.data_ptr(), self._s)
         xkv_stride = 2 * R * H * S_ENC * 64
+        nparts, pbias = 0, None
         for li, L in enumerate(w.dec):
-            self._ln(self.xd, L.ln1_g, L.ln1_b, R, self.hd)
+            self._resid_ln(R, nparts, pbias, L.ln1_g, L.ln1_b)
             self._gemm(self.hd, L.wqkv, R, 3 * D, D, _lib.TW_EPI_BF16, self.qkvd, bias=L.bqkv)
             _lib.call("tw_attn_decode_self", self.qkvd.data_ptr(), R, H, T, self.pos.data_ptr(),
                       self.kcache[li].data_ptr(), self.vcache[li].data_ptr(), self.attd.data_ptr(), self._s)
-            self._gemm(self.attd, L.wo, R, D, D, _lib.TW_EPI_RESID_F32, self.xd, bias=L.bo)
-            self._ln(self.xd, L.ln2_g, L.ln2_b, R, self.hd)
+            self._partial(self.attd, L.wo, R, D, D)
+            self._resid_ln(R, DEC_SPLITS, L.bo, L.ln2_g, L.ln2_b)
             self._gemm(self.hd, L.wq_x, R, D, D, _lib.TW_EPI_BF16, self.qd, bias=L.bq_x)
             ckv = self.cross_kv.data_ptr() + li * xkv_stride * 2  # bytes: bf16
             _lib.call("tw_attn_decode_cross", self.qd.data_ptr(), R, H, S_ENC, R, None, ckv, self.attd.data_ptr(),
                       self._s)
-            self._gemm(self.attd, L.wo_x, R, D, D, _lib.TW_EPI_RESID_F32, self.xd, bias=L.bo_x)
-            self._ln(self.xd, L.ln3_g, L.ln3_b, R, self.hd)
+            self._partial(self.attd, L.wo_x, R, D, D)
+            self._resid_ln(R, DEC_SPLITS, L.bo_x, L.ln3_g, L.ln3_b)
             self._gemm(self.hd, L.w1, R, F, D, _lib.TW_EPI_GELU_BF16, self.ffnd, bias=L.b1)
-            self._gemm(self.ffnd, L.w2, R, D, F, _lib.TW_EPI_RESID_F32, self.xd, bias=L.b2)
+            self._partial(self.ffnd, L.w2, R, D, F)
+            nparts, pbias = DEC_SPLITS, L.b2
         if with_logits:
-            self._ln(self.xd, w.dec_ln_g, w.dec_ln_b, R, self.hd)
+            self._resid_ln(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b)
             self._gemm(self.hd, w.emb, R, d.vocab, D, _lib.TW_EPI_F32, self.logits)
 
     def _select_params(self, mode: int, max_new: int, use_timestamps: bool = True) -> _lib.TwSelectParams:
@@ -224,7 +244,7 @@ class WhisperEngine:
     def _select(self, R: int, params: _lib.TwSelectParams, tokens: bool = True) -> None:
         _lib.call("tw_logits_select", self.logits.data_ptr(), R, self.d.vocab, self.suppress_bits.data_ptr(),
                   ctypes.byref(params), self.state.data_ptr(), self.tokens.data_ptr() if tokens else None,
-                  self.tokens.shape[1], self.ids.data_ptr(), self.pos.data_ptr(), self._s)
+                  self.tokens.shape[1], self.ids.data_ptr(), self.pos.data_ptr(), self.sel_ws.data_ptr(), self._s)
 
     def _gen_step(self, R: int, params) -> None:
         self.decoder_step(R)
