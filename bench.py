@@ -66,17 +66,13 @@ def main():
     eng.set_suppress_tokens(list(gen.suppress_tokens) + [gen.special.eot])  # fixed decode length
     audio = workload(B, 30.0, seed=1234 + 1000 * rank)
     eng.wave[:B].copy_(torch.from_numpy(audio))
-    gather_buf = torch.zeros(world * B, 1 + T, dtype=torch.int32, device=eng.device) if world > 1 else None
+    from twamd import dist as twd
 
     def step():
         eng.logmel(B)
         seqs = eng.generate(B, task="transcribe", max_new_tokens=T, max_passes=1)
-        if world > 1:
-            loc = torch.zeros(B, 1 + T, dtype=torch.int32)
-            for i, s in enumerate(seqs):
-                loc[i, 0] = len(s)
-                loc[i, 1: 1 + len(s)] = torch.as_tensor(s[:T], dtype=torch.int32)
-            dist.all_gather_into_tensor(gather_buf, loc.to(eng.device))
+        if world > 1:  # rank r holds windows [rB, (r+1)B): one RCCL all-gather of the token arrays
+            seqs, _ = twd.gather_tokens(seqs, eng.last_langs, world * B)
         return seqs
 
     for _ in range(a.warmup):

@@ -1,0 +1,161 @@
+"""Chunk data parallelism (twamd.dist) on CPU: world_size-2 gloo process groups over 127.0.0.1.
+
+The engine itself needs the GPU, so the per-rank window work is a deterministic stand-in that turns each window's
+samples into a valid Whisper token sequence; what is under test is the sharding, the waveform broadcast, the
+all-gather reassembly and the stitched transcript, which must equal the single-process result exactly."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from twamd import dist as twd
+from twamd.config import GenerationSettings, PRESETS
+from twamd.frontend import chunk_windows, time_precision
+from twamd.tokenizer import WhisperVocab, decode_asr
+
+ST = GenerationSettings.default(PRESETS["large-v3-turbo"]).special
+
+
+def fake_windows(wav, windows):
+    """Deterministic per-window 'generate' output: <ts> text... <ts> pairs derived from the samples."""
+    out = []
+    for w in windows:
+        seg = wav[w.start: w.start + min(w.length, 480000)]
+        h = int(abs(float(seg[::997].sum())) * 1000) % 5000
+        n = 1 + h % 7
+        toks = [ST.timestamp_begin]
+        for i in range(n):
+            toks.append(300 + (h + 37 * i) % 20000)
+        toks.append(ST.timestamp_begin + 50 + h % 1400)
+        out.append(toks)
+    return out
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, ws, port, n_samples, chunk, stride, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        rng = np.random.default_rng(3)
+        wav = rng.standard_normal(n_samples).astype(np.float32) if rank == 0 else None
+        wav = twd.broadcast_waveform(wav)
+        windows = list(chunk_windows(len(wav), chunk, stride, 16000))
+        seqs = twd.transcribe_sharded(fake_windows, wav, windows)
+        langs = [None] * len(windows)
+        lo, hi = twd.shard_range(len(windows), ws, rank)
+        g_seqs, g_langs = twd.gather_tokens(seqs[lo:hi], [rank] * (hi - lo), len(windows))
+        q.put((rank, seqs, g_langs, float(wav.sum())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_samples,chunk,stride", [(3600 * 16000 // 10, 30, 0), (200 * 16000, 60, 5),
+                                                     (16000 * 20, 30, 0)])
+def test_two_rank_gather_equals_single_process(n_samples, chunk, stride):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_samples, chunk, stride, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(3)
+    wav = rng.standard_normal(n_samples).astype(np.float32)
+    windows = list(chunk_windows(len(wav), chunk, stride, 16000))
+    ref = fake_windows(wav, windows)
+    sizes = twd.shard_sizes(len(windows), 2)
+    for rank, seqs, g_langs, wsum in res:
+        assert wsum == pytest.approx(float(wav.sum()))
+        assert seqs == ref
+        assert g_langs == [0] * sizes[0] + [1] * sizes[1]
+    # the stitched transcript is the single-process one
+    vocab = WhisperVocab.synthetic(ST)
+    mo = [{"tokens": t, "stride": (w.length / 16000, w.stride_left / 16000, w.stride_right / 16000)}
+          for w, t in zip(windows, res[0][1])]
+    mo_ref = [{"tokens": t, "stride": (w.length / 16000, w.stride_left / 16000, w.stride_right / 16000)}
+              for w, t in zip(windows, ref)]
+    assert decode_asr(vocab, mo, True, False, time_precision(1500)) == decode_asr(vocab, mo_ref, True, False,
+                                                                                  time_precision(1500))
+
+
+def test_shard_ranges_cover_in_order():
+    for n in (0, 1, 7, 24, 120, 121):
+        for ws in (1, 2, 3, 8):
+            rs = [twd.shard_range(n, ws, r) for r in range(ws)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(ws - 1))
+            assert max(twd.shard_sizes(n, ws)) - min(twd.shard_sizes(n, ws)) <= 1
+
+
+def test_pack_unpack_roundtrip_and_limits():
+    seqs = [[1, 2, 3], [], list(range(448))]
+    arr = twd.pack_tokens(seqs, [5, None, 7], 4)
+    s2, l2 = twd.unpack_tokens(arr, 3)
+    assert s2 == seqs and l2 == [5, None, 7]
+    with pytest.raises(ValueError):
+        twd.pack_tokens([list(range(449))], None, 1)
+    with pytest.raises(ValueError):
+        twd.pack_tokens([[1], [2]], None, 1)
+
+
+class _RecordingASR:
+    def __init__(self):
+        self.calls = []
+
+    def __call__(self, inputs, **kw):
+        rank, ws = twd.world()
+        wav = np.asarray(inputs, np.float32) if rank == 0 else None
+        wav = twd.broadcast_waveform(wav)
+        windows = list(chunk_windows(len(wav), kw["chunk_length_s"], kw.get("stride_length_s"), 16000))
+        seqs = twd.transcribe_sharded(fake_windows, wav, windows)
+        self.calls.append(kw)
+        return seqs
+
+
+def _serve_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        fe = twd.RankZeroFrontend(_RecordingASR())
+        if rank == 0:
+            rng = np.random.default_rng(9)
+            outs = [fe(rng.standard_normal(16000 * s).astype(np.float32), chunk_length_s=30, stride_length_s=0)
+                    for s in (95, 40)]
+            fe.close()
+            q.put((0, outs))
+        else:
+            q.put((rank, fe.follow()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rank_zero_frontend_serves_followers():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_serve_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res[1] == 2
+    rng = np.random.default_rng(9)
+    for s, out in zip((95, 40), res[0]):
+        wav = rng.standard_normal(16000 * s).astype(np.float32)
+        assert out == fake_windows(wav, list(chunk_windows(len(wav), 30, 0, 16000)))

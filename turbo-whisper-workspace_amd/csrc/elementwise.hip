@@ -6,29 +6,56 @@
 #include "tw_common.h"
 #include "../../include/tw_whisper.h"
 
-// One wave per row, f32 in -> bf16 out (the GEMM A operand). Two-pass mean / variance in registers.
+// One wave per row, f32 in -> bf16 out (the GEMM A operand). The row is read once with 16-byte loads and
+// kept in registers (D <= 64 * 4 * LN_MAXC); mean and variance are two wave reductions over it.
+#define LN_MAXC 16
 __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, const float* __restrict__ g,
                                                    const float* __restrict__ bta, int M, int D, float eps,
                                                    bf16_t* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
-  const float* xr = x + (size_t)row * D;
-  // three streaming passes over the row (the re-reads hit L1/L2); no runtime-indexed register array
+  const int nc = D >> 2;
+  const float4* xr = (const float4*)(x + (size_t)row * D);
+  float4 v[LN_MAXC];
   float s = 0.f;
-  for (int c = lane; c < D; c += 64) s += xr[c];
+#pragma unroll
+  for (int i = 0; i < LN_MAXC; ++i) {
+    const int c = lane + 64 * i;
+    if (64 * i < nc) {  // wave-uniform trip bound; the lane index is clamped, not branched on
+      v[i] = xr[min(c, nc - 1)];
+      if (c < nc) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+  }
   const float mean = wave_sum(s) / (float)D;
   float q = 0.f;
-  for (int c = lane; c < D; c += 64) { float d = xr[c] - mean; q += d * d; }
+#pragma unroll
+  for (int i = 0; i < LN_MAXC; ++i) {
+    const int c = lane + 64 * i;
+    if (64 * i < nc && c < nc) {
+      const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, d = v[i].w - mean;
+      q += (a * a + b * b) + (cc * cc + d * d);
+    }
+  }
   const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
-  bf16_t* orow = out + (size_t)row * D;
-  for (int c = lane; c < D; c += 64) orow[c] = f32_to_bf16((xr[c] - mean) * rstd * g[c] + bta[c]);
+  uint2* orow = (uint2*)(out + (size_t)row * D);
+#pragma unroll
+  for (int i = 0; i < LN_MAXC; ++i) {
+    const int c = lane + 64 * i;
+    if (64 * i < nc && c < nc) {
+      const float4 gg = ((const float4*)g)[c], bb = ((const float4*)bta)[c];
+      uint2 w;
+      w.x = pack_bf16x2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
+      w.y = pack_bf16x2((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+      orow[c] = w;
+    }
+  }
 }
 
 extern "C" int tw_layernorm(const float* x, const float* gamma, const float* beta, int M, int D, float eps, bf16_t* out,
                             void* stream) {
   TW_REQUIRE(x && gamma && beta && out && M > 0, "tw_layernorm: bad args");
-  TW_REQUIRE(D % 64 == 0 && D <= 4096, "tw_layernorm: D=%d must be a multiple of 64 and <= 4096", D);
+  TW_REQUIRE(D % 4 == 0 && D <= 256 * LN_MAXC, "tw_layernorm: D=%d must be a multiple of 4 and <= %d", D, 256 * LN_MAXC);
   hipLaunchKernelGGL(k_layernorm, dim3(tw_cdiv(M, 4)), dim3(256), 0, (hipStream_t)stream, x, gamma, beta, M, D, eps,
                      out);
   return tw_check_launch("tw_layernorm");

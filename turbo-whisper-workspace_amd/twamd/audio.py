@@ -112,6 +112,17 @@ def load_input(inputs: Union[str, bytes, np.ndarray, dict], sr_out: int = TARGET
     raise TypeError(f"We expect a numpy ndarray or torch tensor as input, got `{type(inputs)}`")
 
 
+def duration_seconds(path: str) -> float:
+    """Duration of an audio file (the reference's get_audio_duration, vocalis/core/audio_utils.py:78-98, via
+    librosa; here from the decoded stream)."""
+    with open(path, "rb") as f:
+        data = f.read()
+    if data[:4] == b"RIFF":
+        x, sr = decode_wav(data)
+        return x.shape[0] / float(sr)
+    raise ValueError("duration: unsupported container")
+
+
 def write_wav(path_or_buf, x: np.ndarray, sr: int = TARGET_SR) -> None:
     """16-bit PCM mono WAV writer (test fixtures, examples)."""
     pcm = np.clip(np.round(np.asarray(x, np.float64) * 32767.0), -32768, 32767).astype("<i2").tobytes()

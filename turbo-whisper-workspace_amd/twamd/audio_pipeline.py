@@ -1,0 +1,163 @@
+"""AudioProcessingPipeline surface of the transcription hot path (§8b).
+
+Two ways to use it:
+
+1. Inside the reference (the drop-in): `install(vocalis.core.audio_pipeline)` replaces
+   `AudioProcessingPipeline.load_transcription_model` (/root/reference/vocalis/core/audio_pipeline.py:171-208) so
+   the callable it caches in `_PIPELINE_CACHE['transcription_model']` is a `TurboTranscriber` instead of
+   `transformers.pipeline(...)`. `transcribe` (:323-369), `process_audio` (:567-688), diarization, the LLM helpers
+   and `POST /api/transcribe` (vocalis/api/main.py:89-131) stay the reference's own code.
+2. Standalone: `AudioProcessingPipeline` below mirrors the reference class's transcription surface with the same
+   names, arguments, result schema and error conventions, for deployments without the reference package.
+   Diarization stays a host-CPU concern (north_star): pass `diarize_fn(audio_path, num_speakers) -> [segments]`
+   to run one; without it the reference's no-diarization merge branch applies (alternating speakers, :709-720).
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Any, Callable, Dict, List, Optional
+
+from . import audio
+from .pipeline import TurboTranscriber
+
+# process-wide model cache, as the reference's module-level _PIPELINE_CACHE (:28-32)
+_PIPELINE_CACHE: Dict[str, Any] = {"transcription_model": None, "diarization_model": None}
+
+DEFAULT_MODEL = "openai/whisper-large-v3"  # the reference's default name (:171)
+
+
+def _engine_options() -> Dict[str, Any]:
+    """Engine construction from the environment (the reference reads LLM_MODEL etc. the same way):
+    TW_CHECKPOINT = local HF Whisper directory (no hub access offline), TW_MAX_BATCH, TW_SEED, TW_DEVICE."""
+    return {"checkpoint": os.environ.get("TW_CHECKPOINT") or None,
+            "max_batch": int(os.environ.get("TW_MAX_BATCH", "24")),
+            "seed": int(os.environ.get("TW_SEED", "1234")),
+            "device": os.environ.get("TW_DEVICE", "cuda")}
+
+
+def build_transcriber(model_name: str = DEFAULT_MODEL, **overrides) -> TurboTranscriber:
+    opts = _engine_options()
+    opts.update(overrides)
+    return TurboTranscriber.from_pretrained(model_name, **opts)
+
+
+def load_transcription_model(self, model_name: str = DEFAULT_MODEL) -> bool:
+    """Replacement body of AudioProcessingPipeline.load_transcription_model (:171-208): same cache protocol,
+    same return convention (True, or False after printing the error)."""
+    cache = getattr(self, "_tw_cache", _PIPELINE_CACHE)
+    if cache.get("transcription_model") is not None:
+        self.transcription_model = cache["transcription_model"]
+        print(f"Using cached transcription model: {model_name}")
+        return True
+    try:
+        print(f"Loading MI355X transcription engine for {model_name}...")
+        self.transcription_model = build_transcriber(model_name)
+        cache["transcription_model"] = self.transcription_model
+        return True
+    except Exception as e:  # the reference's convention: print, return False
+        print(f"Error loading transcription model: {e}")
+        return False
+
+
+def install(reference_module) -> None:
+    """Patch the reference's AudioProcessingPipeline (module `vocalis.core.audio_pipeline` or the root
+    `audio_pipeline`) so its transcription callable is the MI355X engine. Its own _PIPELINE_CACHE is used."""
+    cls = reference_module.AudioProcessingPipeline
+    cache = reference_module._PIPELINE_CACHE
+
+    def _load(self, model_name: str = DEFAULT_MODEL) -> bool:
+        self._tw_cache = cache
+        return load_transcription_model(self, model_name)
+
+    _load.__doc__ = load_transcription_model.__doc__
+    cls.load_transcription_model = _load
+
+
+class AudioProcessingPipeline:
+    """Standalone mirror of the reference class's transcription surface."""
+
+    def __init__(self, diarize_fn: Optional[Callable[[str, int], List[Dict[str, Any]]]] = None,
+                 transcriber: Optional[TurboTranscriber] = None):
+        self.transcription_model = transcriber
+        self.diarize_fn = diarize_fn
+        if transcriber is not None and _PIPELINE_CACHE["transcription_model"] is None:
+            _PIPELINE_CACHE["transcription_model"] = transcriber
+
+    load_transcription_model = load_transcription_model
+
+    def transcribe(self, audio_path: str, task: str = "transcribe", return_timestamps: bool = True,
+                   batch_size: int = 512) -> Dict[str, Any]:
+        """:323-369 — the reference's exact call (chunk_length_s=60, stride_length_s=5) on the engine."""
+        if self.transcription_model is None:
+            if not self.load_transcription_model():
+                return {"error": "Failed to load transcription model"}
+        try:
+            return self.transcription_model(audio_path, chunk_length_s=60, batch_size=batch_size, stride_length_s=5,
+                                            generate_kwargs={"task": task}, return_timestamps=return_timestamps)
+        except Exception as e:
+            print(f"Error during transcription: {e}")
+            return {"error": f"Transcription error: {str(e)}"}
+
+    def _merge_transcription_with_diarization(self, transcription, diarization_segments):
+        """:690-726. With no diarization segments: alternating speakers over the transcript chunks, whose
+        `start`/`end` keys HF chunks do not carry (the reference reads them with .get(..., 0))."""
+        if isinstance(transcription, dict) and "segments" in transcription:
+            segs = transcription["segments"]
+        elif isinstance(transcription, dict) and "chunks" in transcription:
+            segs = transcription["chunks"]
+        else:
+            segs = transcription
+        if not diarization_segments:
+            return [{"speaker": f"Speaker {i % 2}", "text": s.get("text", ""), "start": s.get("start", 0),
+                     "end": s.get("end", 0)} for i, s in enumerate(segs)]
+        # the reference hands these to SpeakerDiarizer.create_transcript_with_speakers (vocalis/core/diar.py:
+        # 184-247), which reads seg['start'] and so raises KeyError on HF chunks; reproduced as-is
+        return [{"speaker": _speaker_at(diarization_segments, s["start"], s["end"]), "text": s.get("text", ""),
+                 "start": s["start"], "end": s["end"]} for s in segs]
+
+    def process_audio(self, audio_path: str, task: str = "transcribe",
+                      segmentation_model: str = "pyannote/segmentation-3.0",
+                      embedding_model: str = "3dspeaker_speech_eres2net_sv_en_voxceleb_16k.onnx|25.3MB",
+                      num_speakers: int = 2, threshold: float = 0.5) -> Dict[str, Any]:
+        """:567-688 — transcription + (host) diarization + merge; same result keys and error convention."""
+        start_time = time.time()
+        processing_times: Dict[str, float] = {}
+        try:
+            t0 = time.time()
+            transcription = self.transcribe(audio_path, task)
+            processing_times["transcription"] = time.time() - t0
+            if isinstance(transcription, dict) and "error" in transcription:
+                return transcription
+            text = transcription.get("text", "")
+            segments = transcription.get("chunks", [])
+            if not segments and "segments" in transcription:
+                segments = transcription["segments"]
+            if not segments:
+                segments = [{"text": text, "start": 0, "end": 0}]
+            t0 = time.time()
+            diarization_segments = self.diarize_fn(audio_path, num_speakers) if self.diarize_fn else []
+            processing_times["diarization"] = time.time() - t0
+            merged_segments = self._merge_transcription_with_diarization(transcription, diarization_segments)
+            try:
+                duration = audio.duration_seconds(audio_path)
+            except Exception:
+                duration = max([s.get("end", 0) for s in merged_segments]) if merged_segments else 0
+            processing_times["total"] = time.time() - start_time
+            return {"text": text, "segments": segments, "diarization_segments": diarization_segments,
+                    "merged_segments": merged_segments, "duration": duration, "processing_times": processing_times}
+        except Exception as e:
+            import traceback
+
+            traceback.print_exc()
+            return {"error": f"Processing error: {str(e)}"}
+
+
+def _speaker_at(diar, start, end) -> str:
+    best, ov = "Unknown", 0.0
+    for d in diar:
+        ds, de = (d["start"], d["end"]) if isinstance(d, dict) else (d.start, d.end)
+        o = min(end, de) - max(start, ds)
+        if o > ov:
+            ov, best = o, (d["speaker"] if isinstance(d, dict) else d.speaker)
+    return best

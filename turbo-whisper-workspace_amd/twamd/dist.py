@@ -1,0 +1,157 @@
+"""Chunk data parallelism: one process per GPU, 30-s windows sharded over ranks, one all-gather.
+
+The reference has no multi-GPU path (it hard-codes cuda:0, /root/reference/vocalis/core/audio_pipeline.py:191);
+SURVEY.md §8e adds exactly one strategy for it. Windows are independent until `_decode_asr` stitches them
+($TF/models/whisper/tokenization_whisper.py:901-1150), so:
+
+  * `shard_range`      contiguous, order-preserving ranges: rank r takes windows [r*n/W, (r+1)*n/W)
+  * each rank runs its windows through its own engine (weights replicated; no data-path collective)
+  * `gather_tokens`    ONE all_gather_into_tensor of an int32 [n_local_max, 2 + T] array per rank
+                       (col 0 = number of tokens, col 1 = language id or -1, then the tokens, pad -1)
+  * rank order = window order, so the gathered rows are already the global window list for stitching.
+
+With the nccl backend (= RCCL on ROCm) the gather runs over xGMI from device tensors; with gloo (CPU tests)
+from host tensors. Messages are tiny (1 h of audio = 120 windows x 450 x 4 B = 216 KB): latency-bound.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+MAX_TOKENS = 448  # max_target_positions: no window can return more tokens
+
+
+def world() -> Tuple[int, int]:
+    """(rank, world_size) of the default group, (0, 1) when torch.distributed is not initialised."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def shard_range(n: int, world_size: int, rank: int) -> Tuple[int, int]:
+    """[lo, hi) of the windows rank `rank` processes (r*n/W .. (r+1)*n/W)."""
+    if world_size < 1 or not 0 <= rank < world_size:
+        raise ValueError(f"bad rank {rank} / world {world_size}")
+    return rank * n // world_size, (rank + 1) * n // world_size
+
+
+def shard_sizes(n: int, world_size: int) -> List[int]:
+    return [shard_range(n, world_size, r)[1] - shard_range(n, world_size, r)[0] for r in range(world_size)]
+
+
+def pack_tokens(seqs: Sequence[Sequence[int]], langs: Optional[Sequence[Optional[int]]], rows: int,
+                width: int = MAX_TOKENS) -> np.ndarray:
+    """int32 [rows, 2 + width]: (len, lang, tokens..., -1 pad). rows >= len(seqs)."""
+    if len(seqs) > rows:
+        raise ValueError(f"{len(seqs)} sequences do not fit {rows} rows")
+    out = np.full((rows, 2 + width), -1, np.int32)
+    for i, s in enumerate(seqs):
+        if len(s) > width:
+            raise ValueError(f"window {i}: {len(s)} tokens > {width}")
+        out[i, 0] = len(s)
+        lg = None if langs is None else langs[i]
+        out[i, 1] = -1 if lg is None else int(lg)
+        out[i, 2: 2 + len(s)] = np.asarray(s, np.int32)
+    return out
+
+
+def unpack_tokens(arr: np.ndarray, n: int) -> Tuple[List[List[int]], List[Optional[int]]]:
+    seqs, langs = [], []
+    for i in range(n):
+        k = int(arr[i, 0])
+        seqs.append([int(t) for t in arr[i, 2: 2 + k]])
+        langs.append(None if arr[i, 1] < 0 else int(arr[i, 1]))
+    return seqs, langs
+
+
+def gather_tokens(local_seqs: Sequence[Sequence[int]], local_langs: Optional[Sequence[Optional[int]]], n_total: int,
+                  device: Optional[torch.device] = None, group=None,
+                  width: int = MAX_TOKENS) -> Tuple[List[List[int]], List[Optional[int]]]:
+    """All-gather every rank's window results; returns all n_total windows in global order (on every rank).
+
+    `device`: where the collective's buffers live (a cuda device for RCCL, cpu for gloo; default: cuda when
+    the default backend is nccl)."""
+    rank, ws = world()
+    if ws == 1:
+        return [list(s) for s in local_seqs], list(local_langs) if local_langs is not None else [None] * len(
+            local_seqs)
+    sizes = shard_sizes(n_total, ws)
+    if len(local_seqs) != sizes[rank]:
+        raise ValueError(f"rank {rank} holds {len(local_seqs)} windows, its shard has {sizes[rank]}")
+    rows = max(max(sizes), 1)
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+            else torch.device("cpu")
+    loc = torch.from_numpy(pack_tokens(local_seqs, local_langs, rows, width)).to(device)
+    allt = torch.empty(ws * rows, 2 + width, dtype=torch.int32, device=device)
+    dist.all_gather_into_tensor(allt, loc, group=group)
+    arr = allt.cpu().numpy()
+    seqs: List[List[int]] = []
+    langs: List[Optional[int]] = []
+    for r in range(ws):
+        s, lg = unpack_tokens(arr[r * rows:], sizes[r])
+        seqs.extend(s)
+        langs.extend(lg)
+    return seqs, langs
+
+
+def broadcast_waveform(wav: Optional[np.ndarray], device: Optional[torch.device] = None, src: int = 0,
+                       group=None) -> np.ndarray:
+    """Rank `src` holds the decoded 16 kHz waveform; every rank returns a copy (length first, then samples)."""
+    rank, ws = world()
+    if ws == 1:
+        return wav
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+            else torch.device("cpu")
+    n = torch.tensor([0 if wav is None else len(wav)], dtype=torch.int64, device=device)
+    dist.broadcast(n, src=src, group=group)
+    buf = torch.empty(int(n.item()), dtype=torch.float32, device=device)
+    if rank == src:
+        buf.copy_(torch.from_numpy(np.ascontiguousarray(wav, np.float32)))
+    dist.broadcast(buf, src=src, group=group)
+    return buf.cpu().numpy()
+
+
+def transcribe_sharded(run_windows, wav: np.ndarray, windows: Sequence, device: Optional[torch.device] = None,
+                       group=None) -> List[List[int]]:
+    """Every rank calls this with the same `windows` (chunk_iter windows over `wav`); each rank runs
+    `run_windows(wav, windows[lo:hi]) -> List[List[int]]` on its own shard, then the results are all-gathered
+    into the global window order."""
+    rank, ws = world()
+    lo, hi = shard_range(len(windows), ws, rank)
+    local = run_windows(wav, list(windows[lo:hi])) if hi > lo else []
+    seqs, _ = gather_tokens(local, None, len(windows), device=device, group=group)
+    return seqs
+
+
+class RankZeroFrontend:
+    """Serving on N GPUs: rank 0 owns the request surface (AudioProcessingPipeline / POST /api/transcribe) and
+    calls this like the single-GPU callable; the other ranks sit in `follow()`. Each call broadcasts the call's
+    keyword arguments, then every rank enters the SPMD TurboTranscriber.__call__ (rank 0 decodes the input and
+    broadcasts the waveform, windows are sharded, token arrays all-gathered)."""
+
+    def __init__(self, transcriber, group=None):
+        self.transcriber = transcriber
+        self.group = group
+
+    def __call__(self, inputs, **kwargs):
+        dist.broadcast_object_list([kwargs], src=0, group=self.group)
+        return self.transcriber(inputs, **kwargs)
+
+    def close(self) -> None:
+        dist.broadcast_object_list([None], src=0, group=self.group)
+
+    def follow(self) -> int:
+        """Loop of ranks != 0 until rank 0 calls close(); returns the number of calls served."""
+        n = 0
+        while True:
+            box = [None]
+            dist.broadcast_object_list(box, src=0, group=self.group)
+            if box[0] is None:
+                return n
+            self.transcriber(None, **box[0])
+            n += 1

@@ -19,7 +19,7 @@ from typing import Any, Dict, List, Optional, Sequence, Union
 import numpy as np
 import torch
 
-from . import audio
+from . import audio, dist
 from .config import PRESETS, GenerationSettings, WhisperDims
 from .engine import WhisperEngine
 from .frontend import CHUNK_SAMPLES, SAMPLE_RATE, Window, chunk_windows, time_precision
@@ -82,7 +82,10 @@ class TurboTranscriber:
         if not st.is_multilingual and (task is not None or language is not None):
             raise ValueError("Cannot specify `task` or `language` for an English-only model.")
 
-        wav = audio.load_input(inputs, self.sampling_rate)
+        rank, world = dist.world()
+        wav = audio.load_input(inputs, self.sampling_rate) if rank == 0 else None
+        if world > 1:  # SPMD: every rank calls with the same arguments; rank 0 decoded the input
+            wav = dist.broadcast_waveform(wav)
         if chunk_length_s:
             windows = list(chunk_windows(len(wav), chunk_length_s, stride_length_s, self.sampling_rate))
             with_stride = True
@@ -101,8 +104,13 @@ class TurboTranscriber:
             if tok not in lt:
                 raise ValueError(f"Unsupported language: {language}.")
             lang_id = lt[tok]
-        outputs = self.transcribe_windows(wav, windows, task=task, lang_id=lang_id, return_timestamps=bool(return_timestamps),
-                                          max_new_tokens=max_new_tokens)
+
+        def run(w, ws):
+            return self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=bool(return_timestamps),
+                                           max_new_tokens=max_new_tokens)
+
+        # one window shard per rank + one all-gather of the token arrays (twamd.dist); plain call on 1 GPU
+        outputs = dist.transcribe_sharded(run, wav, windows) if world > 1 else run(wav, windows)
         model_outputs = []
         for w, toks in zip(windows, outputs):
             o = {"tokens": toks}
