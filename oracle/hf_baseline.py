@@ -69,15 +69,17 @@ def build_pipeline(dims, gen, seed: int = 1234, threads: Optional[int] = None):
 
 
 def time_reference(dims, gen, audio: np.ndarray, max_new_tokens: int, threads: int, seed: int = 1234,
-                   num_beams: int = 1, one_pass: bool = False) -> dict:
-    """Wall time of the reference call on `audio` (reference kwargs: chunk 60 / stride 5 / batch 32).
-    one_pass: generation_config.force_unique_generate_call (a single seek pass per window)."""
+                   num_beams: int = 1, one_pass: bool = False, chunk_length_s: float = 60,
+                   stride_length_s: float = 5) -> dict:
+    """Wall time of the ASR pipeline call on `audio` (default: the reference kwargs chunk 60 / stride 5 /
+    batch 32, vocalis/core/audio_pipeline.py:351-358). one_pass: generation_config.force_unique_generate_call
+    (a single seek pass per window)."""
     pipe = build_pipeline(dims, gen, seed, threads)
     if one_pass:
         pipe.generation_config.force_unique_generate_call = True
     t0 = time.perf_counter()
     with torch.no_grad():
-        out = pipe(audio.copy(), chunk_length_s=60, batch_size=32, stride_length_s=5,
+        out = pipe(audio.copy(), chunk_length_s=chunk_length_s, batch_size=32, stride_length_s=stride_length_s,
                    generate_kwargs={"task": "transcribe", "num_beams": num_beams, "max_new_tokens": max_new_tokens},
                    return_timestamps=True)
     wall = time.perf_counter() - t0

@@ -19,10 +19,11 @@ step() {  # step NAME TIMEOUT CMD...
 if [ "$SKIP_TESTS" != "1" ]; then
   step tests 900 python -m pytest tests -q -m gpu -x -p no:cacheprovider
 fi
-step bench 900 python bench.py --steps 5 --warmup 2
-grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
 step prof_kt 600 rocprofv3 --kernel-trace --stats -T -d $OUT/kt -o kt --output-format csv -- python bench.py --profile-only --steps 2 --warmup 1
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/pmc_fetch -o pmc --output-format csv -- python bench.py --profile-only --steps 1 --warmup 0
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/pmc_write -o pmc --output-format csv -- python bench.py --profile-only --steps 1 --warmup 0
 python scripts/summarize_prof.py $OUT > $OUT/summary.txt 2>&1
+cp $OUT/traffic.json profiles/${TAG}_traffic.json   # bench.py reads the newest profiles/*traffic.json
+step bench 900 python bench.py --steps 5 --warmup 2
+grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
 echo done

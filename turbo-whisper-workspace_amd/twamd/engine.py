@@ -109,16 +109,18 @@ class WhisperEngine:
 
     def _gemm(self, A, W, M, N, K, epi, out, bias=None, aux=None, aux_rows=0, kv_geom=None, lda=None, ldw=None,
               ldo=None):
-        rec = self._begin_timer(("gemm_skinny" if M <= 32 else "gemm_tile", epi), 2.0 * M * N * K)
+        rec = self._begin_timer(("gemm_skinny" if M <= 32 else "gemm_big", epi), 2.0 * M * N * K)
         _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, lda or K, ldw or K, epi, out.data_ptr(),
                   ldo or N, _lib.ptr(bias), _lib.ptr(aux), aux_rows, kv_geom, self._s)
         self._end_timer(rec)
 
-    # per-launch HIP-event timing of kernel families (bench roofline; off by default)
+    # per-launch HIP-event timing of kernel families (bench roofline; off by default). timer_families: the
+    # family names (key[0]) to time, None = all.
     timers: Optional[dict] = None
+    timer_families: Optional[set] = None
 
     def _begin_timer(self, key, work):
-        if self.timers is None:
+        if self.timers is None or (self.timer_families is not None and key[0] not in self.timer_families):
             return None
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
@@ -215,8 +217,10 @@ class WhisperEngine:
             self._resid_ln(R, DEC_SPLITS, L.bo, L.ln2_g, L.ln2_b)
             self._gemm(self.hd, L.wq_x, R, D, D, _lib.TW_EPI_BF16, self.qd, bias=L.bq_x)
             ckv = self.cross_kv.data_ptr() + li * xkv_stride * 2  # bytes: bf16
+            rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2)  # K+V bytes read
             _lib.call("tw_attn_decode_cross", self.qd.data_ptr(), R, H, S_ENC, R, None, ckv, self.attd.data_ptr(),
                       self._s)
+            self._end_timer(rec)
             self._partial(self.attd, L.wo_x, R, D, D)
             self._resid_ln(R, DEC_SPLITS, L.bo_x, L.ln3_g, L.ln3_b)
             self._gemm(self.hd, L.w1, R, F, D, _lib.TW_EPI_GELU_BF16, self.ffnd, bias=L.b1)
