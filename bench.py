@@ -68,15 +68,15 @@ def main():
     eng.wave[:B].copy_(torch.from_numpy(audio))
     from twamd import dist as twd
 
-    def step():
-        eng.logmel(B)
-        seqs = eng.generate(B, task="transcribe", max_new_tokens=T, max_passes=1)
-        if world > 1:  # rank r holds windows [rB, (r+1)B): one RCCL all-gather of the token arrays
-            seqs, _ = twd.gather_tokens(seqs, eng.last_langs, world * B)
-        return seqs
+    def run(n_steps):
+        """n_steps batches of B windows through the engine's two-slot pipeline (the encoder of batch k+1 runs on
+        a second HIP stream beside the decode of batch k); every rank then all-gathers each batch's tokens."""
+        res = eng.run_batches([B] * n_steps, task="transcribe", max_new_tokens=T, max_passes=1)
+        if world > 1:  # rank r holds windows [rB, (r+1)B) of each batch: one RCCL all-gather per batch
+            res = [twd.gather_tokens(seqs, lg, world * B)[0] for seqs, lg in zip(res, eng.batch_langs)]
+        return res[-1] if res else []
 
-    for _ in range(a.warmup):
-        step()
+    run(a.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -84,8 +84,7 @@ def main():
     # timed region (the encoder is not graph-captured; ~0.3 us per event against 0.2-1 ms per launch)
     eng.timers, eng.timer_families = {}, {"gemm_big"}
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        seqs = step()
+    seqs = run(a.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

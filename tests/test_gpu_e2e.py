@@ -144,3 +144,28 @@ def test_graph_replay_equals_eager(tr):
     b = eng.generate(2, task="transcribe", max_new_tokens=30)
     eng.use_graphs = True
     assert a == b
+
+
+def test_pipelined_batches_equal_sequential(tr):
+    """run_batches (encoder of batch k+1 on the second stream beside the decode of batch k) returns exactly what
+    per-batch synchronous generate() returns."""
+    eng = tr.engine
+    clips = [speech_like(30.0, 1234), white_noise(12.3, 7), speech_like(30.0, 99)]
+    hosts = []
+    for k in range(3):
+        h = np.zeros((2, 480000), np.float32)
+        a, b = clips[k][:480000], clips[(k + 1) % 3][:480000]
+        h[0, : len(a)] = a
+        h[1, : len(b)] = b
+        hosts.append(h)
+    seq_ref = []
+    for h in hosts:
+        eng.wave[:2].copy_(torch.from_numpy(h))
+        eng.logmel(2)
+        seq_ref.append(eng.generate(2, task="transcribe", max_new_tokens=30))
+
+    def load(k):
+        eng.wave[:2].copy_(torch.from_numpy(hosts[k]))
+
+    got = eng.run_batches([2, 2, 2], load=load, task="transcribe", max_new_tokens=30)
+    assert got == seq_ref

@@ -158,6 +158,17 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(const bf16_t* __restrict__
     }
 }
 
+// Large-M kernel selection (1 = 256x256 LDS-DMA kernel, 0 = 128x128 register-staged kernel);
+// tw_gemm_set_variant() switches it for A/B measurement.
+static int tw_gemm_big_enabled = 1;
+static int tw_tune_skinny_nw = 0;  // 0 = heuristic; 4 / 8 / 16 force the skinny kernel's waves per block
+extern "C" int tw_gemm_set_variant(int big) {
+  tw_gemm_big_enabled = big & 1;
+  const int nw = (big >> 8) & 0xff;
+  tw_tune_skinny_nw = (nw == 4 || nw == 8 || nw == 16) ? nw : 0;
+  return 0;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Large-M kernel, 256 x 256 x 64 tiles (encoder projections, FFN, conv stem, cross-K/V)
 // ------------------------------------------------------------------------------------------------
@@ -433,18 +444,12 @@ static void launch_skinny(const bf16_t* A, const bf16_t* W, int M, int N, int K,
   const long nb = tw_cdiv(N, 16) * (long)splits;
   const int ns = K / 32;
   int nw = 4;
-  while (nb * nw < 1024 && nw < 16 && ns >= 2 * 2 * nw * splits) nw *= 2;
+  // at most 8 waves (17 KiB LDS): a 16-wave block (35 KiB) cannot co-reside with a k_gemm_big workgroup
+  while (nb * nw < 1024 && nw < 8 && ns >= 2 * 2 * nw * splits) nw *= 2;
+  if (tw_tune_skinny_nw) nw = tw_tune_skinny_nw;
   if (nw == 4) launch_skinny_nw<EPI, 4>(A, W, M, N, K, lda, ldw, ea, splits, s);
   else if (nw == 8) launch_skinny_nw<EPI, 8>(A, W, M, N, K, lda, ldw, ea, splits, s);
   else launch_skinny_nw<EPI, 16>(A, W, M, N, K, lda, ldw, ea, splits, s);
-}
-
-// Large-M kernel selection (1 = 256x256 LDS-DMA kernel, 0 = 128x128 register-staged kernel);
-// tw_gemm_set_variant() switches it for A/B measurement.
-static int tw_gemm_big_enabled = 1;
-extern "C" int tw_gemm_set_variant(int big) {
-  tw_gemm_big_enabled = big ? 1 : 0;
-  return 0;
 }
 
 template <int EPI>

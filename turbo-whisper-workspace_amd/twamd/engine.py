@@ -26,9 +26,55 @@ from .frontend import CHUNK_SAMPLES, N_FRAMES, dft_basis, mel_table
 from .segments import retrieve_segment, strip_generated
 from .weights import PackedWeights
 
+import functools
+
 LN_EPS = 1e-5
 S_ENC = 1500
 DEC_SPLITS = 4   # split-K factor of the decoder's d_model-wide projections (out_proj, fc2)
+
+
+def on_engine_streams(fn):
+    """Public engine calls run on the engine's own streams: ordered after the caller's current stream on entry,
+    and the caller's stream waits for the engine's decoder stream on exit (so torch ops the caller issues on
+    its stream see the results). Nested calls are already on the engine stream."""
+
+    @functools.wraps(fn)
+    def wrapper(self, *args, **kwargs):
+        cur = torch.cuda.current_stream(self.device)
+        if cur.cuda_stream in self._own_streams:
+            return fn(self, *args, **kwargs)
+        self.stream.wait_stream(cur)
+        try:
+            with torch.cuda.stream(self.stream):
+                return fn(self, *args, **kwargs)
+        finally:
+            cur.wait_stream(self.stream)
+
+    return wrapper
+
+
+@dataclasses.dataclass
+class DecView:
+    """Decoder rows [r0, r0 + n) of the engine batch: views of the per-row decoder buffers, their own split-K
+    partial buffer and the HIP stream their steps launch on. The full batch is one view; the generation loop
+    splits it into chains that run concurrently (each chain's kernels are latency-bound, so two chains fill
+    each other's gaps)."""
+    r0: int
+    n: int
+    stream: torch.cuda.Stream
+    xd: torch.Tensor
+    hd: torch.Tensor
+    qkvd: torch.Tensor
+    qd: torch.Tensor
+    attd: torch.Tensor
+    ffnd: torch.Tensor
+    logits: torch.Tensor
+    parts: torch.Tensor
+    sel_ws: torch.Tensor
+    state: torch.Tensor
+    tokens: torch.Tensor
+    ids: torch.Tensor
+    pos: torch.Tensor
 
 
 @dataclasses.dataclass
@@ -47,7 +93,12 @@ class WhisperEngine:
         self.max_batch = max_batch
         self.device = torch.device(device)
         self.use_graphs = use_graphs
-        self.stream = torch.cuda.current_stream(self.device)
+        # a high-priority decoder stream and a default-priority stream for the front end + encoder: the
+        # MFMA-bound encoder of the next window batch fills the CUs the latency-bound decode of this one leaves idle,
+        # and the dispatcher serves the decoder's small grids first
+        self.stream = torch.cuda.Stream(self.device, priority=-1)
+        self.enc_stream = torch.cuda.Stream(self.device, priority=0)
+        self._enc_ev = [torch.cuda.Event(), torch.cuda.Event()]
         D, F, H, V, B = d.d_model, d.ffn, d.heads, d.vocab, max_batch
         dev, bf, f32, i32 = self.device, torch.bfloat16, torch.float32, torch.int32
         c, s = dft_basis()
@@ -56,7 +107,8 @@ class WhisperEngine:
         self.mel_fb = torch.from_numpy(mel_table(d.n_mels)).to(dev)
         # front end
         self.wave = torch.zeros(B, CHUNK_SAMPLES, dtype=f32, device=dev)
-        self.feats = torch.zeros(B, d.n_mels, N_FRAMES, dtype=f32, device=dev)
+        self.feats_buf = torch.zeros(2, B, d.n_mels, N_FRAMES, dtype=f32, device=dev)  # [slot]
+        self.feats = self.feats_buf[0]
         self.maxkeys = torch.zeros(B, dtype=torch.int32, device=dev)
         # encoder activations
         M3, M15 = B * N_FRAMES, B * S_ENC
@@ -68,7 +120,10 @@ class WhisperEngine:
         self.qkv = torch.empty(M15, 3 * D, dtype=bf, device=dev)
         self.att = torch.empty(M15, D, dtype=bf, device=dev)
         self.ffn = torch.empty(M15, F, dtype=bf, device=dev)
-        self.cross_kv = torch.empty(d.decoder_layers, 2, B, H, S_ENC, 64, dtype=bf, device=dev)
+        # cross-attention K/V of the encoded windows, one buffer per pipeline slot
+        self.cross_kv_buf = torch.empty(2, d.decoder_layers, 2, B, H, S_ENC, 64, dtype=bf, device=dev)
+        self.cross_kv = self.cross_kv_buf[0]
+        self._slot = 0  # slot the decoder reads
         # decoder state
         T = d.max_target_positions
         self.kcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=bf, device=dev)
@@ -90,7 +145,13 @@ class WhisperEngine:
         self.seek = torch.zeros(B, dtype=i32, device=dev)
         self.suppress_bits = torch.zeros((V + 31) // 32, dtype=torch.int32, device=dev)
         self.set_suppress_tokens(gen.suppress_tokens)
+        # concurrent decode chains in the generation loop (measured: two 12-row chains on two streams run no faster
+        # than one 24-row chain on MI355X, so one by default)
+        self.n_chains = 1
+        self._chain_streams = [torch.cuda.Stream(self.device, priority=-1) for _ in range(self.n_chains)]
+        self._own_streams = {x.cuda_stream for x in [self.stream, self.enc_stream] + self._chain_streams}
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        self._chain_cache: Dict[tuple, List[DecView]] = {}
 
     def set_suppress_tokens(self, tokens: Sequence[int]) -> None:
         """SuppressTokensLogitsProcessor's list as a device bitmask (in place: captured graphs stay valid)."""
@@ -108,30 +169,32 @@ class WhisperEngine:
         return self.stream.cuda_stream
 
     def _gemm(self, A, W, M, N, K, epi, out, bias=None, aux=None, aux_rows=0, kv_geom=None, lda=None, ldw=None,
-              ldo=None):
-        rec = self._begin_timer(("gemm_skinny" if M <= 32 else "gemm_big", epi), 2.0 * M * N * K)
+              ldo=None, stream=None):
+        st = stream or self.stream
+        rec = self._begin_timer(("gemm_skinny" if M <= 32 else "gemm_big", epi), 2.0 * M * N * K, st)
         _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, lda or K, ldw or K, epi, out.data_ptr(),
-                  ldo or N, _lib.ptr(bias), _lib.ptr(aux), aux_rows, kv_geom, self._s)
-        self._end_timer(rec)
+                  ldo or N, _lib.ptr(bias), _lib.ptr(aux), aux_rows, kv_geom, st.cuda_stream)
+        self._end_timer(rec, st)
 
     # per-launch HIP-event timing of kernel families (bench roofline; off by default). timer_families: the
     # family names (key[0]) to time, None = all.
     timers: Optional[dict] = None
     timer_families: Optional[set] = None
 
-    def _begin_timer(self, key, work):
+    def _begin_timer(self, key, work, stream=None):
+        """HIP events on the stream the kernel is launched on."""
         if self.timers is None or (self.timer_families is not None and key[0] not in self.timer_families):
             return None
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
-        a.record(self.stream)
+        a.record(stream or self.stream)
         return (key, work, a, b)
 
-    def _end_timer(self, rec):
+    def _end_timer(self, rec, stream=None):
         if rec is None:
             return
         key, work, a, b = rec
-        b.record(self.stream)
+        b.record(stream or self.stream)
         self.timers.setdefault(key, []).append((work, a, b))
 
     def timer_summary(self) -> dict:
@@ -142,93 +205,141 @@ class WhisperEngine:
             out[k] = (len(lst), sum(w for w, _, _ in lst), sum(a.elapsed_time(b) for _, a, b in lst))
         return out
 
-    def _ln(self, x, g, b, M, out):
+    def _ln(self, x, g, b, M, out, stream=None):
         _lib.call("tw_layernorm", x.data_ptr(), g.data_ptr(), b.data_ptr(), M, self.d.d_model, LN_EPS,
-                  out.data_ptr(), self._s)
+                  out.data_ptr(), (stream or self.stream).cuda_stream)
+
+    # ------------------------------------------------------------------ streams / slots
+    def _enc_begin(self, sync: bool):
+        """Front-end/encoder work goes to enc_stream. sync: it is ordered after everything already queued on the
+        decoder stream (host writes of wave/row_map/seek made there), and _enc_end makes the decoder stream wait
+        for it; async (pipelined prefetch): independent of the decoder stream."""
+        if sync:
+            self.enc_stream.wait_stream(self.stream)
+        return self.enc_stream
+
+    def _enc_end(self, sync: bool, slot: int):
+        self._enc_ev[slot].record(self.enc_stream)
+        if sync:
+            self.stream.wait_stream(self.enc_stream)
+
+    def _view(self, r0: int = 0, n: Optional[int] = None, stream=None, parts=None) -> DecView:
+        n = self.max_batch - r0 if n is None else n
+        sl = slice(r0, r0 + n)
+        return DecView(r0, n, stream or self.stream, self.xd[sl], self.hd[sl], self.qkvd[sl], self.qd[sl],
+                       self.attd[sl], self.ffnd[sl], self.logits[sl],
+                       self.parts if parts is None else parts, self.sel_ws[sl], self.state[sl], self.tokens[sl],
+                       self.ids[sl], self.pos[sl])
+
+    def use_slot(self, slot: int) -> None:
+        """Point the decoder at the cross-K/V (and feature) buffers of pipeline slot `slot`."""
+        self._slot = slot
+        self.cross_kv = self.cross_kv_buf[slot]
+        self.feats = self.feats_buf[slot]
 
     # ------------------------------------------------------------------ front end
-    def logmel(self, n: int) -> None:
-        """feats[:n] = log-mel of wave[:n] (each row one 30-s window, zero padded)."""
+    @on_engine_streams
+    def logmel(self, n: int, slot: Optional[int] = None, sync: bool = True) -> None:
+        """feats[slot][:n] = log-mel of wave[:n] (each row one 30-s window, zero padded)."""
+        slot = self._slot if slot is None else slot
+        st = self._enc_begin(sync)
         _lib.call("tw_logmel", self.wave.data_ptr(), n, self.basis_cos.data_ptr(), self.basis_sin.data_ptr(),
-                  self.mel_fb.data_ptr(), self.d.n_mels, self.feats.data_ptr(), self.maxkeys.data_ptr(), self._s)
+                  self.mel_fb.data_ptr(), self.d.n_mels, self.feats_buf[slot].data_ptr(), self.maxkeys.data_ptr(),
+                  st.cuda_stream)
+        self._enc_end(sync, slot)
 
     # ------------------------------------------------------------------ encoder
-    def encode(self, R: int, row_map=True, seek=True) -> None:
-        """Encoder over R windows: slot r reads feats[row_map[r]][:, seek[r]:] (zero padded to 3000),
-        then projects every decoder layer's cross-attention K/V into cross_kv (batch stride R)."""
+    @on_engine_streams
+    def encode(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True) -> None:
+        """Encoder over R windows: slot r reads feats[slot][row_map[r]][:, seek[r]:] (zero padded to 3000), then
+        projects every decoder layer's cross-attention K/V into cross_kv_buf[slot] (batch stride R). Runs on
+        enc_stream (see _enc_begin for `sync`)."""
         d, w = self.d, self.w
+        slot = self._slot if slot is None else slot
         D, F, H = d.d_model, d.ffn, d.heads
         M3, M15 = R * N_FRAMES, R * S_ENC
-        _lib.call("tw_im2col_conv1", self.feats.data_ptr(), d.n_mels, self.row_map.data_ptr() if row_map else None,
-                  self.seek.data_ptr() if seek else None, R, w.kpad1, self.a1.data_ptr(), self._s)
-        self._gemm(self.a1, w.conv1_w, M3, D, w.kpad1, _lib.TW_EPI_GELU_BF16, self.h1, bias=w.conv1_b)
-        _lib.call("tw_im2col_conv2", self.h1.data_ptr(), R, D, self.a2.data_ptr(), self._s)
+        st = self._enc_begin(sync)
+        s = st.cuda_stream
+        _lib.call("tw_im2col_conv1", self.feats_buf[slot].data_ptr(), d.n_mels,
+                  self.row_map.data_ptr() if row_map else None, self.seek.data_ptr() if seek else None, R, w.kpad1,
+                  self.a1.data_ptr(), s)
+        self._gemm(self.a1, w.conv1_w, M3, D, w.kpad1, _lib.TW_EPI_GELU_BF16, self.h1, bias=w.conv1_b, stream=st)
+        _lib.call("tw_im2col_conv2", self.h1.data_ptr(), R, D, self.a2.data_ptr(), s)
         self._gemm(self.a2, w.conv2_w, M15, D, 3 * D, _lib.TW_EPI_GELU_POS_F32, self.x, bias=w.conv2_b,
-                   aux=w.pos_enc, aux_rows=S_ENC)
+                   aux=w.pos_enc, aux_rows=S_ENC, stream=st)
         for L in w.enc:
-            self._ln(self.x, L.ln1_g, L.ln1_b, M15, self.hln)
-            self._gemm(self.hln, L.wqkv, M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv)
-            rec = self._begin_timer(("attn_encoder", 0), 4.0 * S_ENC * S_ENC * 64 * H * R)
-            _lib.call("tw_attn_encoder", self.qkv.data_ptr(), R, S_ENC, H, self.att.data_ptr(), self._s)
-            self._end_timer(rec)
-            self._gemm(self.att, L.wo, M15, D, D, _lib.TW_EPI_RESID_F32, self.x, bias=L.bo)
-            self._ln(self.x, L.ln2_g, L.ln2_b, M15, self.hln)
-            self._gemm(self.hln, L.w1, M15, F, D, _lib.TW_EPI_GELU_BF16, self.ffn, bias=L.b1)
-            self._gemm(self.ffn, L.w2, M15, D, F, _lib.TW_EPI_RESID_F32, self.x, bias=L.b2)
-        self._ln(self.x, w.enc_ln_g, w.enc_ln_b, M15, self.hln)  # encoder last_hidden_state (bf16)
+            self._ln(self.x, L.ln1_g, L.ln1_b, M15, self.hln, stream=st)
+            self._gemm(self.hln, L.wqkv, M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv, stream=st)
+            rec = self._begin_timer(("attn_encoder", 0), 4.0 * S_ENC * S_ENC * 64 * H * R, st)
+            _lib.call("tw_attn_encoder", self.qkv.data_ptr(), R, S_ENC, H, self.att.data_ptr(), s)
+            self._end_timer(rec, st)
+            self._gemm(self.att, L.wo, M15, D, D, _lib.TW_EPI_RESID_F32, self.x, bias=L.bo, stream=st)
+            self._ln(self.x, L.ln2_g, L.ln2_b, M15, self.hln, stream=st)
+            self._gemm(self.hln, L.w1, M15, F, D, _lib.TW_EPI_GELU_BF16, self.ffn, bias=L.b1, stream=st)
+            self._gemm(self.ffn, L.w2, M15, D, F, _lib.TW_EPI_RESID_F32, self.x, bias=L.b2, stream=st)
+        self._ln(self.x, w.enc_ln_g, w.enc_ln_b, M15, self.hln, stream=st)  # encoder last_hidden_state (bf16)
         geom = (ctypes.c_int * 4)(S_ENC, R, D, H)
-        self._gemm(self.hln, w.wkv_x, M15, d.decoder_layers * 2 * D, D, _lib.TW_EPI_CROSSKV, self.cross_kv,
-                   bias=w.bkv_x, kv_geom=geom)
+        self._gemm(self.hln, w.wkv_x, M15, d.decoder_layers * 2 * D, D, _lib.TW_EPI_CROSSKV, self.cross_kv_buf[slot],
+                   bias=w.bkv_x, kv_geom=geom, stream=st)
+        self._enc_end(sync, slot)
 
     def encoder_output(self, R: int) -> torch.Tensor:
         """Encoder last_hidden_state of the last encode() (bf16 view [R][1500][D])."""
         return self.hln[: R * S_ENC].view(R, S_ENC, self.d.d_model)
 
     # ------------------------------------------------------------------ decoder
-    def _partial(self, A, W, M, N, K):
-        """parts[:DEC_SPLITS, :M] = split-K partial sums of A . W^T (decoder; residual add in _resid_ln)."""
-        rec = self._begin_timer(("gemm_skinny", "partial"), 2.0 * M * N * K)
-        _lib.call("tw_gemm_bf16_partial", A.data_ptr(), W.data_ptr(), M, N, K, K, K, DEC_SPLITS, self.parts.data_ptr(),
-                  N, self._s)
-        self._end_timer(rec)
+    def _partial(self, A, W, M, N, K, v: DecView):
+        """v.parts[:DEC_SPLITS, :M] = split-K partial sums of A . W^T (decoder; residual add in _resid_ln)."""
+        rec = self._begin_timer(("gemm_skinny", "partial"), 2.0 * M * N * K, v.stream)
+        _lib.call("tw_gemm_bf16_partial", A.data_ptr(), W.data_ptr(), M, N, K, K, K, DEC_SPLITS, v.parts.data_ptr(),
+                  N, v.stream.cuda_stream)
+        self._end_timer(rec, v.stream)
 
-    def _resid_ln(self, R, nparts, bias, g, b):
+    def _resid_ln(self, R, nparts, bias, g, b, v: DecView):
         """xd += bias + sum(parts[:nparts]); hd = LayerNorm(xd) (one fused launch)."""
-        _lib.call("tw_resid_layernorm", self.xd.data_ptr(), self.parts.data_ptr() if nparts else None, nparts,
-                  _lib.ptr(bias), _lib.ptr(g), _lib.ptr(b), R, self.d.d_model, LN_EPS, _lib.ptr(self.hd), self._s)
+        _lib.call("tw_resid_layernorm", v.xd.data_ptr(), v.parts.data_ptr() if nparts else None, nparts,
+                  _lib.ptr(bias), _lib.ptr(g), _lib.ptr(b), R, self.d.d_model, LN_EPS, _lib.ptr(v.hd),
+                  v.stream.cuda_stream)
 
-    def decoder_step(self, R: int, with_logits: bool = True) -> None:
-        """One token per row: ids[b] at position pos[b] -> logits[b] (f32).
+    @on_engine_streams
+    def decoder_step(self, R: int, with_logits: bool = True, v: Optional[DecView] = None, r_enc: Optional[int] = None
+                     ) -> None:
+        """One token per row of view v (default: rows 0..R-1): ids[b] at position pos[b] -> logits[b] (f32).
+        r_enc: the batch size the current cross-K/V was encoded with (its batch stride; default R).
 
         Residual stream xd stays f32; every d_model-wide projection (self/cross out_proj, fc2) is a split-K
         partial product whose sum, bias and residual add are folded into the next LayerNorm launch."""
         d, w = self.d, self.w
+        v = v or self._view()
+        r_enc = R if r_enc is None else r_enc
         D, F, H, T = d.d_model, d.ffn, d.heads, d.max_target_positions
-        _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), self.ids.data_ptr(),
-                  self.pos.data_ptr(), R, D, self.xd.data_ptr(), self._s)
-        xkv_stride = 2 * R * H * S_ENC * 64
+        st = v.stream
+        s = st.cuda_stream
+        _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), v.ids.data_ptr(), v.pos.data_ptr(), R, D,
+                  v.xd.data_ptr(), s)
+        xkv_stride = 2 * r_enc * H * S_ENC * 64
         nparts, pbias = 0, None
         for li, L in enumerate(w.dec):
-            self._resid_ln(R, nparts, pbias, L.ln1_g, L.ln1_b)
-            self._gemm(self.hd, L.wqkv, R, 3 * D, D, _lib.TW_EPI_BF16, self.qkvd, bias=L.bqkv)
-            _lib.call("tw_attn_decode_self", self.qkvd.data_ptr(), R, H, T, self.pos.data_ptr(),
-                      self.kcache[li].data_ptr(), self.vcache[li].data_ptr(), self.attd.data_ptr(), self._s)
-            self._partial(self.attd, L.wo, R, D, D)
-            self._resid_ln(R, DEC_SPLITS, L.bo, L.ln2_g, L.ln2_b)
-            self._gemm(self.hd, L.wq_x, R, D, D, _lib.TW_EPI_BF16, self.qd, bias=L.bq_x)
-            ckv = self.cross_kv.data_ptr() + li * xkv_stride * 2  # bytes: bf16
-            rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2)  # K+V bytes read
-            _lib.call("tw_attn_decode_cross", self.qd.data_ptr(), R, H, S_ENC, R, None, ckv, self.attd.data_ptr(),
-                      self._s)
-            self._end_timer(rec)
-            self._partial(self.attd, L.wo_x, R, D, D)
-            self._resid_ln(R, DEC_SPLITS, L.bo_x, L.ln3_g, L.ln3_b)
-            self._gemm(self.hd, L.w1, R, F, D, _lib.TW_EPI_GELU_BF16, self.ffnd, bias=L.b1)
-            self._partial(self.ffnd, L.w2, R, D, F)
+            self._resid_ln(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
+            self._gemm(v.hd, L.wqkv, R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, bias=L.bqkv, stream=st)
+            _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
+                      self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
+            self._partial(v.attd, L.wo, R, D, D, v)
+            self._resid_ln(R, DEC_SPLITS, L.bo, L.ln2_g, L.ln2_b, v)
+            self._gemm(v.hd, L.wq_x, R, D, D, _lib.TW_EPI_BF16, v.qd, bias=L.bq_x, stream=st)
+            # this layer's [k|v][r_enc][H][S][64] block, advanced to the view's first row (bytes: bf16)
+            ckv = self.cross_kv.data_ptr() + (li * xkv_stride + v.r0 * H * S_ENC * 64) * 2
+            rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
+            _lib.call("tw_attn_decode_cross", v.qd.data_ptr(), R, H, S_ENC, r_enc, None, ckv, v.attd.data_ptr(), s)
+            self._end_timer(rec, st)
+            self._partial(v.attd, L.wo_x, R, D, D, v)
+            self._resid_ln(R, DEC_SPLITS, L.bo_x, L.ln3_g, L.ln3_b, v)
+            self._gemm(v.hd, L.w1, R, F, D, _lib.TW_EPI_GELU_BF16, v.ffnd, bias=L.b1, stream=st)
+            self._partial(v.ffnd, L.w2, R, D, F, v)
             nparts, pbias = DEC_SPLITS, L.b2
         if with_logits:
-            self._resid_ln(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b)
-            self._gemm(self.hd, w.emb, R, d.vocab, D, _lib.TW_EPI_F32, self.logits)
+            self._resid_ln(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
+            self._gemm(v.hd, w.emb, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, stream=st)
 
     def _select_params(self, mode: int, max_new: int, use_timestamps: bool = True) -> _lib.TwSelectParams:
         st, g = self.gen.special, self.gen
@@ -245,15 +356,17 @@ class WhisperEngine:
             p.begin_suppress[i] = t
         return p
 
-    def _select(self, R: int, params: _lib.TwSelectParams, tokens: bool = True) -> None:
-        _lib.call("tw_logits_select", self.logits.data_ptr(), R, self.d.vocab, self.suppress_bits.data_ptr(),
-                  ctypes.byref(params), self.state.data_ptr(), self.tokens.data_ptr() if tokens else None,
-                  self.tokens.shape[1], self.ids.data_ptr(), self.pos.data_ptr(), self.sel_ws.data_ptr(), self._s)
+    def _select(self, R: int, params: _lib.TwSelectParams, tokens: bool = True, v: Optional[DecView] = None) -> None:
+        v = v or self._view()
+        _lib.call("tw_logits_select", v.logits.data_ptr(), R, self.d.vocab, self.suppress_bits.data_ptr(),
+                  ctypes.byref(params), v.state.data_ptr(), v.tokens.data_ptr() if tokens else None,
+                  v.tokens.shape[1], v.ids.data_ptr(), v.pos.data_ptr(), v.sel_ws.data_ptr(), v.stream.cuda_stream)
 
-    def _gen_step(self, R: int, params) -> None:
-        self.decoder_step(R)
-        self._select(R, params)
+    def _gen_step(self, R: int, params, v: Optional[DecView] = None, r_enc: Optional[int] = None) -> None:
+        self.decoder_step(R, v=v, r_enc=r_enc)
+        self._select(R, params, v=v)
 
+    @on_engine_streams
     def decode_pass(self, R: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
                     check_every: int = 8, use_timestamps: bool = True) -> PassResult:
         """Greedy decode of R rows from the prompt [SOT, (lang), *tail] (the init tokens of
@@ -261,6 +374,7 @@ class WhisperEngine:
         multilingual model). Returns the generated tokens of every row."""
         st = self.gen.special
         dev = self.device
+        self.stream.wait_event(self._enc_ev[self._slot])  # the cross-K/V of this slot is written
         self.state[:R].zero_()
         self.state[:R, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
         self.pos[:R] = 0
@@ -286,40 +400,54 @@ class WhisperEngine:
         params = self._select_params(0, max_new, use_timestamps)
         self._gen_step(R, params)
         steps = 1
-        graph = self._graph_for(R, params) if self.use_graphs else None
+        # generation loop: the rows split into chains on their own high-priority streams, each replaying its
+        # captured decode step; the chains' latency-bound kernels run concurrently
+        chains = self._chains(R)
+        graphs = [self._graph_for(R, params, i, c) for i, c in enumerate(chains)] if self.use_graphs else None
+        for c in chains:
+            c.stream.wait_stream(self.stream)
         while steps < max_new:
             n = min(check_every, max_new - steps)
             for _ in range(n):
-                if graph is not None:
-                    graph.replay()
-                else:
-                    self._gen_step(R, params)
+                for i, c in enumerate(chains):
+                    if graphs is not None:
+                        with torch.cuda.stream(c.stream):
+                            graphs[i].replay()
+                    else:
+                        self._gen_step(c.n, params, v=c, r_enc=R)
             steps += n
+            for c in chains:
+                self.stream.wait_stream(c.stream)
             if bool(self.state[:R, _lib.TW_ST_FINISHED].all().item()):
                 break
         ngen = self.state[:R, _lib.TW_ST_NGEN].tolist()
         toks = self.tokens[:R].tolist()
         return PassResult([toks[r][: ngen[r]] for r in range(R)], detected if lang_ids is None else list(lang_ids))
 
-    def _graph_for(self, R: int, params) -> Optional[torch.cuda.CUDAGraph]:
-        key = (R, params.max_new, params.use_timestamps)
+    def _chains(self, R: int) -> List[DecView]:
+        """Contiguous row ranges of [0, R), one per decode chain (each with its own partial-sum buffer)."""
+        key = ("chains", R)
+        if key not in self._chain_cache:
+            k = max(1, min(self.n_chains, R // 4))
+            views = []
+            for i in range(k):
+                r0, r1 = i * R // k, (i + 1) * R // k
+                parts = torch.empty(DEC_SPLITS, r1 - r0, self.d.d_model, dtype=torch.float32, device=self.device)
+                views.append(self._view(r0, r1 - r0, self._chain_streams[i], parts))
+            self._chain_cache[key] = views
+        return self._chain_cache[key]
+
+    def _graph_for(self, R: int, params, i: int, v: DecView) -> Optional[torch.cuda.CUDAGraph]:
+        key = (R, params.max_new, params.use_timestamps, self._slot, i)
         g = self._graphs.get(key)
         if g is not None:
             return g
         g = torch.cuda.CUDAGraph()
-        cap = torch.cuda.Stream(self.device)
-        cap.wait_stream(self.stream)
-        # capture on a side stream: the C-ABI calls launch on self.stream, so swap it for capture
-        saved = self.stream
-        try:
-            self.stream = cap
-            with torch.cuda.stream(cap):
-                # state is mutated by capture-time launches? no: capture records, it does not execute.
-                with torch.cuda.graph(g, stream=cap):
-                    self._gen_step(R, params)
-        finally:
-            self.stream = saved
-        self.stream.wait_stream(cap)
+        v.stream.wait_stream(self.stream)
+        with torch.cuda.stream(v.stream):
+            with torch.cuda.graph(g, stream=v.stream):  # records, does not execute
+                self._gen_step(v.n, params, v=v, r_enc=R)
+        self.stream.wait_stream(v.stream)
         self._graphs[key] = g
         return g
 
@@ -351,12 +479,21 @@ class WhisperEngine:
             return mnt
         return min(g.max_length + prompt_len, T) - prompt_len
 
+    @on_engine_streams
     def generate(self, n_chunks: int, task: Optional[str] = "transcribe", lang_ids: Optional[Sequence[int]] = None,
                  max_new_tokens: Optional[int] = None, return_timestamps: bool = True,
-                 max_passes: Optional[int] = None) -> List[List[int]]:
-        """Whisper short-form generate() over feats[:n_chunks] (each 3000 frames): language
+                 max_passes: Optional[int] = None, slot: Optional[int] = None,
+                 pre_encoded: bool = False) -> List[List[int]]:
+        """Whisper short-form generate() over feats[slot][:n_chunks] (each 3000 frames): language
         detection, the seek loop and segment extraction, returning for every chunk the concatenated
-        segment tokens (what generate() returns before padding)."""
+        segment tokens (what generate() returns before padding).
+
+        pre_encoded: the first seek pass (all chunks, seek 0, n_chunks <= max_batch) was already encoded into
+        this slot by encode(n_chunks, row_map=False, seek=False, slot=slot, sync=False) (pipelined prefetch)."""
+        if slot is not None:
+            self.use_slot(slot)
+        if pre_encoded and n_chunks > self.max_batch:
+            raise ValueError("pre_encoded needs n_chunks <= max_batch")
         st = self.gen.special
         tail = self.prompt_tail(task, return_timestamps, language_given=lang_ids is not None)
         prompt_len = 1 + (1 if st.is_multilingual else 0) + len(tail)
@@ -365,16 +502,17 @@ class WhisperEngine:
         segs: List[List[int]] = [[] for _ in range(n_chunks)]
         # language: given, or detected on the first pass (seek == 0, the whole 30-s window) as
         # _retrieve_init_tokens -> detect_language does before the seek loop
-        langs: List[Optional[int]] = list(lang_ids) if lang_ids is not None else [None] * n_chunks
+        langs: List[Optional[int]] = list(lang_ids)[:n_chunks] if lang_ids is not None else [None] * n_chunks
         passes = 0
         while any(s < N_FRAMES for s in seek):
             rows = [i for i in range(n_chunks) if seek[i] < N_FRAMES]
             for b0 in range(0, len(rows), self.max_batch):
                 part = rows[b0: b0 + self.max_batch]
                 R = len(part)
-                self.row_map[:R] = torch.as_tensor(part, dtype=torch.int32, device=self.device)
-                self.seek[:R] = torch.as_tensor([seek[i] for i in part], dtype=torch.int32, device=self.device)
-                self.encode(R)
+                if not (pre_encoded and passes == 0):
+                    self.row_map[:R] = torch.as_tensor(part, dtype=torch.int32, device=self.device)
+                    self.seek[:R] = torch.as_tensor([seek[i] for i in part], dtype=torch.int32, device=self.device)
+                    self.encode(R)
                 part_langs = [langs[i] for i in part]
                 known = all(lg is not None for lg in part_langs) or not st.is_multilingual
                 res = self.decode_pass(R, tail, part_langs if (known and st.is_multilingual) else None, max_new,
@@ -393,3 +531,33 @@ class WhisperEngine:
                 raise RuntimeError("seek loop made no progress")
         self.last_langs = langs
         return segs
+
+    @on_engine_streams
+    def run_batches(self, sizes: Sequence[int], load=None, **gen_kwargs) -> List[List[List[int]]]:
+        """generate() over consecutive window batches with a two-slot software pipeline: while batch k decodes on
+        the decoder stream, batch k+1's log-mel + encoder + cross-K/V run on enc_stream into the other slot.
+        sizes[k] = windows in batch k (<= max_batch); load(k) fills wave[:sizes[k]] for batch k (queued on
+        enc_stream; None = the waveforms are already resident). Returns generate()'s output per batch."""
+        if any(n < 1 or n > self.max_batch for n in sizes):
+            raise ValueError(f"batch sizes must be in [1, {self.max_batch}]")
+
+        def prefetch(k):
+            with torch.cuda.stream(self.enc_stream):
+                if load is not None:
+                    load(k)
+                self.logmel(sizes[k], slot=k % 2, sync=False)
+                self.encode(sizes[k], row_map=False, seek=False, slot=k % 2, sync=False)
+
+        # the first prefetch is ordered after whatever the caller queued on the decoder stream
+        self.enc_stream.wait_stream(self.stream)
+        out = []
+        self.batch_langs = []
+        if sizes:
+            prefetch(0)
+        for k, n in enumerate(sizes):
+            if k + 1 < len(sizes):
+                prefetch(k + 1)  # runs beside the decode of batch k
+            out.append(self.generate(n, slot=k % 2, pre_encoded=True, **gen_kwargs))
+            self.batch_langs.append(self.last_langs)
+        self.use_slot(0)
+        return out

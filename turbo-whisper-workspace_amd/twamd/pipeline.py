@@ -127,20 +127,25 @@ class TurboTranscriber:
                            lang_id: Optional[int], return_timestamps: bool,
                            max_new_tokens: Optional[int] = None) -> List[List[int]]:
         """Log-mel + generate for every window; returns per-window token sequences (generate() output,
-        right-padded with the pad token within each engine batch, as the HF batch output is)."""
+        right-padded with the pad token within each engine batch, as the HF batch output is). Batches of
+        max_batch windows go through WhisperEngine.run_batches: batch k+1 is encoded while batch k decodes."""
         eng = self.engine
-        out: List[List[int]] = []
         B = eng.max_batch
-        for b0 in range(0, len(windows), B):
-            part = windows[b0: b0 + B]
+        parts = [windows[b0: b0 + B] for b0 in range(0, len(windows), B)]
+
+        def load(k):  # called on the engine's encoder stream
+            part = parts[k]
             host = np.zeros((len(part), CHUNK_SAMPLES), np.float32)
             for j, w in enumerate(part):
                 seg = wav[w.start: w.start + min(w.length, CHUNK_SAMPLES)]  # feature extractor truncation
                 host[j, : len(seg)] = seg
-            eng.wave[: len(part)].copy_(torch.from_numpy(host), non_blocking=False)
-            eng.logmel(len(part))
-            seqs = eng.generate(len(part), task=task, lang_ids=None if lang_id is None else [lang_id] * len(part),
-                                max_new_tokens=max_new_tokens, return_timestamps=return_timestamps)
+            eng.wave[: len(part)].copy_(torch.from_numpy(host))
+
+        res = eng.run_batches([len(p) for p in parts], load=load, task=task,
+                              lang_ids=None if lang_id is None else [lang_id] * B, max_new_tokens=max_new_tokens,
+                              return_timestamps=return_timestamps)
+        out: List[List[int]] = []
+        for seqs in res:
             out.extend(pad_right(seqs, self.gen.special.eot))
         return out
 
