@@ -125,6 +125,9 @@ int tw_layernorm(const float* x, const float* gamma, const float* beta, int M, i
  * Replaces WhisperAttention + eager_attention_forward/SDPA for the encoder
  * (modeling_whisper.py:215-238, 241-356). */
 int tw_attn_encoder(const uint16_t* qkv, int B, int S, int H, uint16_t* out, void* stream);
+/* Measurement knob (process-wide, returns 0): encoder attention kernel of tw_attn_encoder. 8 (default) =
+ * k_attn_enc2 with 8 waves / 256 queries per workgroup, 4 = the same with 4 waves, 0 = the first kernel. */
+int tw_attn_set_variant(int variant);
 /* Decoder self-attention for one new token per row: appends k,v of qkv bf16[B][3D] at pos[b] into
  * k_cache/v_cache bf16[B][H][max_pos][64] (this layer) and attends over 0..pos[b].
  * Replaces the causal self-attention + DynamicCache.update of modeling_whisper.py:312-335,448-505. */

@@ -159,13 +159,16 @@ def _ref_attn(q, k, v):  # [B,H,S,64] fp32, q already scaled
     return torch.softmax(q @ k.transpose(-1, -2), dim=-1) @ v
 
 
-@pytest.mark.parametrize("B,L,H", [(2, 1500, 4), (1, 100, 2), (1, 1500, 20)])
-def test_encoder_attention_vs_torch(B, L, H):
+@pytest.mark.parametrize("variant", [8, 9, 4, 0])
+@pytest.mark.parametrize("B,L,H", [(2, 1500, 4), (1, 100, 2), (1, 1500, 20), (3, 1500, 5)])
+def test_encoder_attention_vs_torch(B, L, H, variant):
+    _lib.call("tw_attn_set_variant", variant)
     D = H * 64
     qkv = rand_bf16(B * L, 3 * D, seed=7)
     qkv[:, :D] = bf(qkv[:, :D].float() * 0.125 * 3)  # scaled q with some dynamic range
     out = torch.empty(B * L, D, dtype=torch.bfloat16, device=DEV)
     _lib.call("tw_attn_encoder", qkv.data_ptr(), B, L, H, out.data_ptr(), S())
+    _lib.call("tw_attn_set_variant", 8)
     t = qkv.float().view(B, L, 3, H, 64).permute(2, 0, 3, 1, 4)
     ref = _ref_attn(t[0], t[1], t[2]).permute(0, 2, 1, 3).reshape(B * L, D)
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)

@@ -143,11 +143,192 @@ __global__ __launch_bounds__(256) void k_attn_encoder(const bf16_t* __restrict__
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_attn_enc2: the same algorithm restructured for CDNA4 throughput
+//   * NW waves x 32 queries per workgroup (NW = 8: 256 queries share every staged K/V tile);
+//   * K/V tiles double-buffered in LDS, register-staged one tile ahead (loads for tile t+1 are issued before
+//     tile t's MFMAs and written after them), ONE barrier per 64-key tile;
+//   * V stays row-major in LDS (16-byte writes) and the V^T fragments of the PV product are read with
+//     ds_read_b64_tr_b16 (hardware transpose); chunk swizzles make the K row reads (chunk ^ ((key>>1)&7)) and
+//     the V transposed reads (chunk ^ (((key>>1)&1)<<2)) bank-conflict free (checked numerically against the
+//     gfx950 bank rules);
+//   * XCD-aware 1-D grid: the query blocks of one (batch, head) run on one XCD, sharing its L2 copy of K/V.
+// ------------------------------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(4))) short short4_t;
+typedef __attribute__((ext_vector_type(8))) short short8_t;
+typedef __attribute__((address_space(3))) short4_t lds_short4_t;
+
+__device__ inline int k2_off(int key, int ch) { return key * 64 + ((ch ^ ((key >> 1) & 7)) << 3); }        // elements
+__device__ inline int v2_off(int key, int ch) { return key * 64 + ((ch ^ (((key >> 1) & 1) << 2)) << 3); } // elements
+
+template <int NW, int WPS>
+__global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc2(const bf16_t* __restrict__ qkv, int S, int H, int D, int nqb,
+                                                          int nwork, bf16_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) bf16_t kbuf[2][EA_KT * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t vbuf[2][EA_KT * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  // XCD-aware bijective remap of the 1-D grid (blocks b, b+8, ... share an XCD under round-robin dispatch)
+  const int orig = blockIdx.x;
+  const int q8 = nwork / 8, r8 = nwork % 8, xcd = orig % 8;
+  const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int qb = work % nqb, bh = work / nqb;
+  const int h = bh % H, b = bh / H;
+  const int ld = 3 * D;
+  const bf16_t* base = qkv + (size_t)b * S * ld + h * 64;
+  const int q0 = qb * (NW * 32) + wid * 32;
+
+  bf16x8 qf[4];  // Q^T fragments (B operand): lane holds Q[q = lr][d = 16 s + 8 lh + j]
+  {
+    const bf16_t* qp = base + (size_t)min(q0 + lr, S - 1) * ld + 8 * lh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+  }
+  // staging: tile = 64 keys x 8 chunks (16 B) of K and of V = 512 chunk pairs; NW*64 threads
+  constexpr int CPT = 512 / (NW * 64);  // chunks per thread (1 for NW = 8, 2 for NW = 4)
+  uint4 rk[CPT], rv[CPT];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + NW * 64 * i;
+      const int key = c >> 3, ch = c & 7;
+      const bf16_t* rp = base + (size_t)min(k0 + key, S - 1) * ld + ch * 8;
+      rk[i] = *(const uint4*)(rp + D);
+      rv[i] = *(const uint4*)(rp + 2 * D);
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + NW * 64 * i;
+      const int key = c >> 3, ch = c & 7;
+      *(uint4*)(&kbuf[buf][k2_off(key, ch)]) = rk[i];
+      *(uint4*)(&vbuf[buf][v2_off(key, ch)]) = rv[i];
+    }
+  };
+
+  f32x16 o0 = {0}, o1 = {0};  // O^T for d in [0,32) and [32,64): row = d, col = query
+  float m_run = -INFINITY, l_run = 0.f;
+  const int ntile = (S + EA_KT - 1) / EA_KT;
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int kt = 0; kt < ntile; ++kt) {
+    const int cur = kt & 1, k0 = kt * EA_KT;
+    if (kt + 1 < ntile) gload(k0 + EA_KT);
+    const bf16_t* ks = kbuf[cur];
+    const bf16_t* vs = vbuf[cur];
+    // S^T = K . Q^T for key halves 0..31 and 32..63
+    f32x16 s0 = {0}, s1 = {0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 ka = *(const bf16x8*)(ks + k2_off(lr, 2 * s + lh));
+      const bf16x8 kb = *(const bf16x8*)(ks + k2_off(32 + lr, 2 * s + lh));
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[s], s1, 0, 0, 0);
+    }
+    // online softmax in raw score units (q carries head_dim^-0.5); exponent = (s - m) * log2e as ONE fma into
+    // the bare v_exp_f32 (__builtin_amdgcn_exp2f: no denormal range fix-up; arguments are <= 0 and a flushed
+    // underflow is exact enough for softmax). The O/l rescale runs only when some row's max grew in this tile.
+    float tmax = -INFINITY;
+    if (k0 + EA_KT > S) {  // last tile: keys >= S masked
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (k0 + key >= S) s0[r] = -INFINITY;
+        if (k0 + 32 + key >= S) s1[r] = -INFINITY;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, fmaxf(s0[r], s1[r]));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    if (__any(tmax > m_run)) {
+      const float m_new = fmaxf(m_run, tmax);
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * EA_LOG2E);  // first tile: exp2(-inf) = 0
+      l_run *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      m_run = m_new;
+    }
+    const float mb = m_run * EA_LOG2E;
+    float psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], EA_LOG2E, -mb));
+      s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], EA_LOG2E, -mb));
+      psum += s0[r] + s1[r];
+    }
+    psum += __shfl_xor(psum, 32, 64);
+    l_run += psum;
+    // O^T += V^T . P^T. B operand = P^T registers 8s..8s+7 of the key half (element j of lane half lh = key
+    // 16 s + 8 (j >> 2) + 4 lh + (j & 3)); A operand = V^T with the same key order, two transposed reads:
+    // lane 4q+p of each 16-lane group addresses V[row q][4p .. 4p+3] of its 4-key x 16-d block.
+    const int gq = (lane & 15) >> 2, gp = lane & 3, gd = ((lane >> 4) & 1) * 16;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = (__bf16)(half ? s1[8 * s + j] : s0[8 * s + j]);
+        const int kb = half * 32 + 16 * s + 4 * lh + gq;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const int d = db * 32 + gd + 4 * gp;
+          const int ch = d >> 3, wi = d & 7;
+          const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4_t*)(vs + v2_off(kb, ch) + wi));
+          const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4_t*)(vs + v2_off(kb + 8, ch) + wi));
+          const short8_t v8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          const bf16x8 va = __builtin_bit_cast(bf16x8, v8);
+          if (db == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o0, 0, 0, 0);
+          else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o1, 0, 0, 0);
+        }
+      }
+    }
+    if (kt + 1 < ntile) swrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  const int q = q0 + lr;
+  if (q < S) {
+    const float inv = 1.f / l_run;
+    bf16_t* op = out + ((size_t)b * S + q) * D + h * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * lh;
+      uint2 w0, w1;
+      w0.x = pack_bf16x2(o0[4 * g] * inv, o0[4 * g + 1] * inv);
+      w0.y = pack_bf16x2(o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
+      w1.x = pack_bf16x2(o1[4 * g] * inv, o1[4 * g + 1] * inv);
+      w1.y = pack_bf16x2(o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
+      *(uint2*)(op + d) = w0;
+      *(uint2*)(op + 32 + d) = w1;
+    }
+  }
+}
+
+static int tw_attn_variant = 8;  // 0 = k_attn_encoder, 4 / 8 = k_attn_enc2<NW>, 9 = <8> at 2 workgroups per CU
+extern "C" int tw_attn_set_variant(int v) {
+  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9) ? v : 8;
+  return 0;
+}
+
 extern "C" int tw_attn_encoder(const bf16_t* qkv, int B, int S, int H, bf16_t* out, void* stream) {
   TW_REQUIRE(qkv && out && B > 0 && S > 0 && H > 0, "tw_attn_encoder: bad args");
   const int D = H * 64;
-  hipLaunchKernelGGL(k_attn_encoder, dim3(tw_cdiv(S, 128), H, B), dim3(256), 0, (hipStream_t)stream, qkv, S, H, D,
-                     out);
+  hipStream_t st = (hipStream_t)stream;
+  if (tw_attn_variant == 0) {
+    hipLaunchKernelGGL(k_attn_encoder, dim3(tw_cdiv(S, 128), H, B), dim3(256), 0, st, qkv, S, H, D, out);
+  } else if (tw_attn_variant == 4) {
+    const int nqb = tw_cdiv(S, 128), nwork = nqb * H * B;
+    hipLaunchKernelGGL((k_attn_enc2<4, 2>), dim3(nwork), dim3(256), 0, st, qkv, S, H, D, nqb, nwork, out);
+  } else if (tw_attn_variant == 9) {
+    const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
+    hipLaunchKernelGGL((k_attn_enc2<8, 4>), dim3(nwork), dim3(512), 0, st, qkv, S, H, D, nqb, nwork, out);
+  } else {
+    const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
+    hipLaunchKernelGGL((k_attn_enc2<8, 2>), dim3(nwork), dim3(512), 0, st, qkv, S, H, D, nqb, nwork, out);
+  }
   return tw_check_launch("tw_attn_encoder");
 }
 

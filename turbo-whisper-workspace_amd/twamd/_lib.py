@@ -31,7 +31,7 @@ EXPORTED = (
     "tw_version", "tw_last_error", "tw_fill_synth", "tw_f32_to_bf16", "tw_logmel", "tw_im2col_conv1",
     "tw_im2col_conv2", "tw_gemm_bf16", "tw_layernorm", "tw_attn_encoder", "tw_attn_decode_self",
     "tw_attn_decode_cross", "tw_embed_decoder", "tw_logits_select", "tw_gemm_bf16_partial", "tw_resid_layernorm",
-    "tw_gemm_set_variant",
+    "tw_gemm_set_variant", "tw_attn_set_variant",
 )
 
 
@@ -72,6 +72,7 @@ _SIGS = {
     "tw_logits_select": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), _P, _P, _I, _P, _P, _P, _P], _I),
     "tw_gemm_bf16_partial": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P], _I),
     "tw_gemm_set_variant": ([_I], _I),
+    "tw_attn_set_variant": ([_I], _I),
     "tw_resid_layernorm": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
 }
 
