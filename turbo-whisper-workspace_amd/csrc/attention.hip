@@ -358,6 +358,7 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
       const int key = min((it0 + u) * 32 + g, nkeys - 1);
       kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
     }
+    __builtin_amdgcn_sched_barrier(0);  // all DA_UNR loads in flight before the first is consumed
 #pragma unroll
     for (int u = 0; u < DA_UNR; ++u) {
       const bf16_t* ke = (const bf16_t*)&kk[u];
@@ -398,6 +399,7 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
       const int key = min((it0 + u) * 32 + g, nkeys - 1);
       vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < DA_UNR; ++u) {
       const int key = (it0 + u) * 32 + g;
