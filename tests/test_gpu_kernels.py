@@ -64,10 +64,12 @@ def test_logmel_vs_oracle(n_mels):
 EPIS = [_lib.TW_EPI_BF16, _lib.TW_EPI_GELU_BF16, _lib.TW_EPI_RESID_F32, _lib.TW_EPI_F32]
 
 
+@pytest.mark.parametrize("variant", [2, 1])
 @pytest.mark.parametrize("M,N,K", [(300, 384, 256), (1500, 1280, 1280), (24, 1280, 1280), (7, 51866, 384),
-                                   (32, 5120, 1280), (129, 200, 64)])
+                                   (32, 5120, 1280), (129, 200, 64), (600, 512, 192), (257, 768, 3840)])
 @pytest.mark.parametrize("epi", EPIS)
-def test_gemm_vs_torch(M, N, K, epi):
+def test_gemm_vs_torch(M, N, K, epi, variant):
+    _lib.call("tw_gemm_set_variant", variant)
     A = rand_bf16(M, K, seed=1)
     W = rand_bf16(N, K, scale=K ** -0.5, seed=2)
     bias = torch.randn(N, device=DEV) * 0.1
@@ -79,6 +81,7 @@ def test_gemm_vs_torch(M, N, K, epi):
     base = out.clone()
     _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, K, K, epi, out.data_ptr(), N, bias.data_ptr(),
               None, 0, None, S())
+    _lib.call("tw_gemm_set_variant", 1)
     if epi == _lib.TW_EPI_GELU_BF16:
         ref = torch.nn.functional.gelu(ref)
     if epi == _lib.TW_EPI_RESID_F32:
