@@ -271,39 +271,32 @@ class GenCfg:
 
 def process_logits(scores: np.ndarray, sampled: Sequence[int], g: GenCfg, use_ts: bool) -> np.ndarray:
     """The processor chain of _retrieve_logit_processors applied to one row (f32)."""
-    s = scores.astype(np.float32).copy()
-    n = len(sampled)
-    if n == 0 and g.begin_suppress:
-        s[g.begin_suppress] = -np.inf
-    if g.suppress:
-        s[g.suppress] = -np.inf
-    if use_ts:
-        tb = g.ts_begin
-        s[g.notimestamps] = -np.inf
-        last_ts = n >= 1 and sampled[-1] >= tb
-        pen_ts = n < 2 or sampled[-2] >= tb
-        if last_ts:
-            if pen_ts:
-                s[tb:] = -np.inf
-            else:
-                s[: g.eot] = -np.inf
-        tss = [t for t in sampled if t >= tb]
-        if tss:
-            tl = tss[-1] if (last_ts and not pen_ts) else tss[-1] + 1
-            s[tb:tl] = -np.inf
-        if n == 0:
-            s[:tb] = -np.inf
-            if g.mit is not None:
-                s[tb + g.mit + 1:] = -np.inf
-        with np.errstate(divide="ignore", invalid="ignore"):
-            m = np.max(s)
-            lp = s - (m + np.log(np.sum(np.exp(s - m)))) if np.isfinite(m) else s
-            ts_lp = lp[tb:]
-            mt = np.max(ts_lp)
-            ts_lse = mt + np.log(np.sum(np.exp(ts_lp - mt))) if np.isfinite(mt) else -np.inf
-            if ts_lse > np.max(lp[:tb]):
-                s[:tb] = -np.inf
+    if not use_ts:
+        s = scores.astype(np.float32).copy()
+        if len(sampled) == 0 and g.begin_suppress:
+            s[g.begin_suppress] = -np.inf
+        if g.suppress:
+            s[g.suppress] = -np.inf
+        return s
+    s = process_logits_no_rule(scores, sampled, g)
+    margin = _ts_rule_margin(s, g.ts_begin)
+    if margin > 0:  # "if sum of probability over timestamps is above any other token, sample timestamp"
+        s[: g.ts_begin] = -np.inf
     return s
+
+
+def _ts_rule_margin(s: np.ndarray, tb: int) -> float:
+    """logsumexp(timestamp log-probs) - max(text log-probs) of processed scores s (WhisperTimeStampLogits-
+    Processor, logits_process.py:2041-2045); > 0 forces a timestamp."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        m = np.max(s)
+        if not np.isfinite(m):
+            return -np.inf
+        lp = s - (m + np.log(np.sum(np.exp(s - m))))
+        ts_lp = lp[tb:]
+        mt = np.max(ts_lp)
+        ts_lse = mt + np.log(np.sum(np.exp(ts_lp - mt))) if np.isfinite(mt) else -np.inf
+        return float(ts_lse - np.max(lp[:tb]))
 
 
 def greedy_pass(model: WhisperOracle, enc: np.ndarray, prompt: Sequence[int], max_new: int, g: GenCfg,
@@ -384,3 +377,117 @@ def generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, task: Optional[
         out += toks
         seek += off
     return out, lang
+
+
+# ----------------------------------------------------------------------------- tolerant greedy replay
+def decision_ok(scores: np.ndarray, sampled: Sequence[int], g: GenCfg, use_ts: bool, tok: int, tau: float) -> bool:
+    """Is `tok` a greedy choice of the f32 reference at this step within tolerance `tau` (in logits)?
+
+    The exact argmax of the processed scores always is. Otherwise `tok` must trail the f32 choice by at most tau on
+    the processed scores; or, when the timestamp rule (timestamp log-prob mass vs the best text log-prob) is itself
+    within tau of flipping, trail the best token of its own class (timestamp / text) by at most tau."""
+    s = process_logits(scores, sampled, g, use_ts)
+    best = int(np.argmax(s))
+    if tok == best or (np.isfinite(s[tok]) and s[tok] >= s[best] - tau):
+        return True
+    if use_ts:
+        pre = process_logits_no_rule(scores, sampled, g)
+        tb = g.ts_begin
+        if abs(_ts_rule_margin(pre, tb)) <= tau and np.isfinite(pre[tok]):
+            cls = pre[tb:] if tok >= tb else pre[:tb]
+            return bool(pre[tok] >= np.max(cls) - tau)
+    return False
+
+
+def process_logits_no_rule(scores: np.ndarray, sampled: Sequence[int], g: GenCfg) -> np.ndarray:
+    """process_logits with timestamps on, minus the final log-sum-exp rule."""
+    s = scores.astype(np.float32).copy()
+    n = len(sampled)
+    if n == 0 and g.begin_suppress:
+        s[g.begin_suppress] = -np.inf
+    if g.suppress:
+        s[g.suppress] = -np.inf
+    tb = g.ts_begin
+    s[g.notimestamps] = -np.inf
+    last_ts = n >= 1 and sampled[-1] >= tb
+    pen_ts = n < 2 or sampled[-2] >= tb
+    if last_ts:
+        if pen_ts:
+            s[tb:] = -np.inf
+        else:
+            s[: g.eot] = -np.inf
+    tss = [t for t in sampled if t >= tb]
+    if tss:
+        tl = tss[-1] if (last_ts and not pen_ts) else tss[-1] + 1
+        s[tb:tl] = -np.inf
+    if n == 0:
+        s[:tb] = -np.inf
+        if g.mit is not None:
+            s[tb + g.mit + 1:] = -np.inf
+    return s
+
+
+def replay_generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, passes: Sequence[Sequence[int]],
+                    lang: Optional[int], task: Optional[str] = "transcribe", return_timestamps: bool = True,
+                    max_new_tokens: Optional[int] = None, tau: float = 0.3) -> dict:
+    """Follow a device decode of ONE window (its raw per-seek-pass token lists and detected language) through the
+    f32 reference, checking every decision with decision_ok. Returns {"ok", "decisions", "exact", "first_bad"}."""
+    feats = np.asarray(feats, np.float32)
+    stats = {"ok": True, "decisions": 0, "exact": 0, "first_bad": None}
+
+    def enc_at(seek):
+        seg = np.zeros_like(feats)
+        seg[:, : 3000 - seek] = feats[:, seek:]
+        return model.encode(seg)
+
+    def check(scores, sampled, tok, use_ts):
+        stats["decisions"] += 1
+        if int(np.argmax(process_logits(scores, sampled, g, use_ts))) == tok:
+            stats["exact"] += 1
+            return
+        if not decision_ok(scores, sampled, g, use_ts, tok, tau) and stats["first_bad"] is None:
+            stats["ok"] = False
+            stats["first_bad"] = (len(sampled), tok, sampled[-5:])
+
+    prompt = [g.sot]
+    if g.multilingual:
+        if lang is None:
+            raise ValueError("multilingual replay needs the device's language id")
+        cache = model.new_cache(enc_at(0))
+        lg = model.decoder_step(g.sot, cache)
+        ml = np.full_like(lg, -np.inf)
+        ml[g.lang_begin: g.lang_begin + g.n_lang] = lg[g.lang_begin: g.lang_begin + g.n_lang]
+        stats["decisions"] += 1
+        if int(np.argmax(ml)) == lang:
+            stats["exact"] += 1
+        elif not ml[lang] >= np.max(ml) - tau:
+            stats["ok"], stats["first_bad"] = False, ("language", lang, int(np.argmax(ml)))
+        prompt.append(lang)
+        if task is not None:
+            prompt.append(g.transcribe if task == "transcribe" else g.translate)
+    if not return_timestamps:
+        prompt.append(g.notimestamps)
+    P = len(prompt)
+    max_new = max_new_tokens if max_new_tokens is not None else min(g.max_length + P, 448) - P
+    seek = 0
+    for seq_raw in passes:
+        if seek >= 3000:
+            stats["ok"], stats["first_bad"] = False, ("extra pass", seek, None)
+            break
+        cache = model.new_cache(enc_at(seek))
+        for t in prompt[:-1]:
+            model.decoder_step(t, cache)
+        logits = model.decoder_step(prompt[-1], cache)
+        out: List[int] = []
+        for tok in seq_raw:
+            check(logits, out, int(tok), return_timestamps)
+            out.append(int(tok))
+            if tok == g.eot or len(out) >= max_new:
+                break
+            logits = model.decoder_step(int(tok), cache)
+        seq = out[:-1] if out and out[-1] == g.eot else out
+        _, off = retrieve_segment(seq, 3000 - seek, g.ts_begin)
+        seek += off
+    if seek < 3000:
+        stats["ok"], stats["first_bad"] = False, ("missing pass", seek, None)
+    return stats

@@ -500,6 +500,7 @@ class WhisperEngine:
         max_new = self.max_new_for(prompt_len, max_new_tokens)
         seek = [0] * n_chunks
         segs: List[List[int]] = [[] for _ in range(n_chunks)]
+        passes_raw: List[List[List[int]]] = [[] for _ in range(n_chunks)]  # every seek pass's raw tokens
         # language: given, or detected on the first pass (seek == 0, the whole 30-s window) as
         # _retrieve_init_tokens -> detect_language does before the seek loop
         langs: List[Optional[int]] = list(lang_ids)[:n_chunks] if lang_ids is not None else [None] * n_chunks
@@ -520,6 +521,7 @@ class WhisperEngine:
                 for j, i in enumerate(part):
                     if not known:
                         langs[i] = res.lang_ids[j]
+                    passes_raw[i].append(list(res.tokens[j]))
                     seq = strip_generated(res.tokens[j], st.eot)
                     seg_tokens, offset = retrieve_segment(seq, seek[i], N_FRAMES - seek[i], st.timestamp_begin)
                     segs[i].extend(seg_tokens)
@@ -530,6 +532,7 @@ class WhisperEngine:
             if passes >= 4 * N_FRAMES:  # a zero seek advance would loop forever (as generate() would)
                 raise RuntimeError("seek loop made no progress")
         self.last_langs = langs
+        self.last_passes = passes_raw
         return segs
 
     @on_engine_streams
@@ -552,6 +555,7 @@ class WhisperEngine:
         self.enc_stream.wait_stream(self.stream)
         out = []
         self.batch_langs = []
+        self.batch_passes = []
         if sizes:
             prefetch(0)
         for k, n in enumerate(sizes):
@@ -559,5 +563,6 @@ class WhisperEngine:
                 prefetch(k + 1)  # runs beside the decode of batch k
             out.append(self.generate(n, slot=k % 2, pre_encoded=True, **gen_kwargs))
             self.batch_langs.append(self.last_langs)
+            self.batch_passes.append(self.last_passes)
         self.use_slot(0)
         return out

@@ -147,6 +147,9 @@ class TurboTranscriber:
         out: List[List[int]] = []
         for seqs in res:
             out.extend(pad_right(seqs, self.gen.special.eot))
+        # per-window record of the last call (languages, raw tokens of every seek pass) for diagnostics/tests
+        self.last_window_langs = [lg for bl in eng.batch_langs for lg in bl]
+        self.last_window_passes = [p for bp in eng.batch_passes for p in bp]
         return out
 
 
