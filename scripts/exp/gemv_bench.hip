@@ -136,6 +136,38 @@ __global__ __launch_bounds__(256) void v4(const bf16_t* Ap, const bf16_t* Wp, in
     }
 }
 
+
+// V5: packed W, row-major A [M][K] (as the decoder's LN / attention kernels write it); split-K over 4 waves
+__global__ __launch_bounds__(256) void v5(const bf16_t* A, const bf16_t* Wp, int M, int N, int K, float* out) {
+  __shared__ float red[4][32][17];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = blockIdx.x, n0 = g * 16, ns = K >> 5, s0 = wid * ns / 4, s1 = (wid + 1) * ns / 4;
+  const bf16_t* wp = Wp + ((size_t)g * ns) * 512 + lane * 8;
+  const int ksub = 8 * (lane >> 4);
+  const bf16_t* ap0 = A + (size_t)min(lane & 15, M - 1) * K + ksub;
+  const bf16_t* ap1 = A + (size_t)min(16 + (lane & 15), M - 1) * K + ksub;
+  f32x4 c0 = {0}, c1 = {0};
+  int s = s0;
+  for (; s + 8 <= s1; s += 8) {
+    bf16x8 bw[8], a0[8], a1[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { bw[u] = *(const bf16x8*)(wp + 512 * (s + u)); a0[u] = *(const bf16x8*)(ap0 + 32 * (s + u)); a1[u] = *(const bf16x8*)(ap1 + 32 * (s + u)); }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], bw[u], c0, 0, 0, 0); c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], bw[u], c1, 0, 0, 0); }
+  }
+  for (; s < s1; ++s) {
+    bf16x8 bw = *(const bf16x8*)(wp + 512 * s), a0 = *(const bf16x8*)(ap0 + 32 * s), a1 = *(const bf16x8*)(ap1 + 32 * s);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bw, c0, 0, 0, 0); c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bw, c1, 0, 0, 0);
+  }
+  const int cc = lane & 15, rb = (lane >> 4) * 4;
+  for (int r = 0; r < 4; ++r) { red[wid][rb + r][cc] = c0[r]; red[wid][16 + rb + r][cc] = c1[r]; }
+  __syncthreads();
+  for (int e = tid; e < 32 * 16; e += 256) {
+    int m = e >> 4, c = e & 15, n = n0 + c;
+    if (m < M && n < N) out[(size_t)m * N + n] = red[0][m][c] + red[1][m][c] + red[2][m][c] + red[3][m][c];
+  }
+}
+
 template <typename F>
 float time_graph(F launch, hipStream_t s, int n) {
   hipGraph_t g; hipGraphExec_t ge;
@@ -176,12 +208,13 @@ int main() {
     auto L2 = [&]() { hipLaunchKernelGGL(v2, dim3(N / 16), dim3(256), 0, s, Ap, Wp + (size_t)(it++ % copies) * wn, M, N, K, out); };
     auto L3 = [&]() { hipLaunchKernelGGL(v3<8>, dim3((N / 16 + 3) / 4), dim3(256), 0, s, Ap, Wp + (size_t)(it++ % copies) * wn, M, N, K, out); };
     auto L3b = [&]() { hipLaunchKernelGGL(v3<16>, dim3((N / 16 + 3) / 4), dim3(256), 0, s, Ap, Wp + (size_t)(it++ % copies) * wn, M, N, K, out); };
+    auto L5 = [&]() { hipLaunchKernelGGL(v5, dim3(N / 16), dim3(256), 0, s, A, Wp + (size_t)(it++ % copies) * wn, M, N, K, out); };
     auto L4 = [&]() { hipLaunchKernelGGL(v4, dim3((N / 16 + 3) / 4), dim3(256), (K / 32) * 2048, s, Ap, Wp + (size_t)(it++ % copies) * wn, M, N, K, out); };
     const int n = 4 * copies;
-    float t1 = time_graph(L1, s, n), t2 = time_graph(L2, s, n), t3 = time_graph(L3, s, n), t3b = time_graph(L3b, s, n), t4 = time_graph(L4, s, n);
+    float t1 = time_graph(L1, s, n), t2 = time_graph(L2, s, n), t3 = time_graph(L3, s, n), t3b = time_graph(L3b, s, n), t4 = K <= 2048 ? time_graph(L4, s, n) : 0.f, t5 = time_graph(L5, s, n);
     double gb = wn * 2 / 1e3;
-    printf("%-8s N=%6d K=%5d copies=%d | v1 rowmajor %7.2f us %6.0f GB/s | v2 packed splitK %7.2f us %6.0f | v3 packed fullK u8 %7.2f us %6.0f | u16 %7.2f us %6.0f | v4 A in LDS %7.2f us %6.0f\n",
-           sh.name, N, K, copies, t1, gb / t1, t2, gb / t2, t3, gb / t3, t3b, gb / t3b, t4, gb / t4);
+    printf("%-8s N=%6d K=%5d copies=%d | v1 rowmajor %7.2f us %6.0f GB/s | v2 packed splitK %7.2f us %6.0f | v3 packed fullK u8 %7.2f us %6.0f | u16 %7.2f us %6.0f | v4 A in LDS %7.2f us %6.0f | v5 packedW rowA %7.2f us %6.0f\n",
+           sh.name, N, K, copies, t1, gb / t1, t2, gb / t2, t3, gb / t3, t3b, gb / t3b, t4, gb / t4, t5, gb / t5);
     CK(hipFree(W)); CK(hipFree(Wp)); CK(hipFree(A)); CK(hipFree(Ap)); CK(hipFree(out));
   }
   return 0;
