@@ -100,9 +100,9 @@ int tw_im2col_conv2(const uint16_t* h1, int R, int D, uint16_t* out, void* strea
  * cached by EncoderDecoderCache (:312-335). */
 int tw_gemm_bf16(const uint16_t* A, const uint16_t* W, int M, int N, int K, int lda, int ldw, int epi, void* out,
                  int ldo, const float* bias, const float* aux, int aux_rows, const int* kv_geom, void* stream);
-/* Measurement knob (process-wide, returns 0). Bit 0 selects the large-M GEMM kernel of tw_gemm_bf16:
- * 1 = 256x256 LDS-DMA kernel (default), 0 = the 128x128 register-staged kernel (kept for A/B).
- * Bits 8..15: 4, 8 or 16 force the skinny (M <= 32) kernel's waves per block; 0 = heuristic. */
+/* Measurement knob (process-wide, returns 0). Bits 0..2 select the large-M GEMM kernel of tw_gemm_bf16:
+ * 1 = 256x256 2-stage BK=64 LDS-DMA (default), 0 = 128x128 register-staged, 3 = 256x256 counted-vmcnt + setprio,
+ * 4 = 256x128 3-stage ring. Bits 8..15: 4, 8 or 16 force the skinny (M <= 32) kernel's waves per block. */
 int tw_gemm_set_variant(int big);
 /* Split-K partial product for the decoder step (M <= 32 rows, K % 32 == 0): part f32[splits][M][ldp]
  * receives the `splits` partial sums of A . W^T over consecutive K ranges (no bias). Used for the

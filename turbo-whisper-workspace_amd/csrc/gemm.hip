@@ -158,12 +158,14 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(const bf16_t* __restrict__
     }
 }
 
-// Large-M kernel selection: 2 = k_gemm_pipe (256x256, 4-stage BK=32 DMA ring), 1 = k_gemm_big (256x256,
-// 2-stage BK=64), 0 = k_gemm_tile (128x128 register-staged); tw_gemm_set_variant() switches it for A/B.
+// Large-M kernel selection (tw_gemm_set_variant, for A/B measurement): 1 = k_gemm_big (256x256, 2-stage BK=64
+// LDS-DMA; default), 0 = k_gemm_tile (128x128 register-staged), 3 = k_gemm_ns<256, 2 stages> (counted vmcnt,
+// raw barrier, setprio), 4 = k_gemm_ns<BN=128, 3 stages>. Measured on the encoder shapes (scripts/gemm_bench.py,
+// random operands): 1 ~ 3 (641-1079 TF/s), 4 is 12-18% slower, a 4-stage BK=32 ring was 6% slower.
 static int tw_gemm_big_enabled = 1;
 static int tw_tune_skinny_nw = 0;  // 0 = heuristic; 4 / 8 / 16 force the skinny kernel's waves per block
 extern "C" int tw_gemm_set_variant(int big) {
-  tw_gemm_big_enabled = big & 3;
+  tw_gemm_big_enabled = big & 7;
   const int nw = (big >> 8) & 0xff;
   tw_tune_skinny_nw = (nw == 4 || nw == 8 || nw == 16) ? nw : 0;
   return 0;
@@ -349,102 +351,116 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_gemm_pipe: 256 x 256 tiles, BK = 32, a 4-stage LDS-DMA ring (3 K-steps in flight)
+// k_gemm_ns: 256 x BN tiles, BK = 64, an NST-stage LDS-DMA ring (NST - 1 K-steps in flight), counted vmcnt +
+// one raw barrier per K-step, optional s_setprio(1) around the MFMA cluster. BN = 128 makes a 3-stage ring fit
+// (3 x 48 KiB) so the DMA of a K-step has two K-steps of MFMAs to land instead of one.
 // ------------------------------------------------------------------------------------------------
-// Same wave layout, fragments and epilogue as k_gemm_big, but the K loop keeps the DMA of the next THREE
-// 32-deep K-steps in flight instead of one 64-deep step: per step each wave issues 4 global_load_lds_dwordx4
-// (2 for A, 2 for W), waits with a COUNTED vmcnt for the step it is about to read (never vmcnt(0) inside the
-// loop), passes one raw s_barrier (which also retires the reads of the stage the new DMA overwrites) and runs
-// 32 MFMAs. Rows are 64 B; swz(r) = (r >> 1) & 3 on the 16-byte chunk keeps the fragment reads conflict-free.
-#define GP_BK 32
-#define GP_STAGES 4
-
-__device__ inline int gp_swz(int r) { return (r >> 1) & 3; }
-
-template <int N_AFTER>
-__device__ inline void gp_wait_barrier() {
-  // tile t's 4 DMA instructions of this wave are done when at most 4 * N_AFTER newer ones are outstanding;
-  // the barrier then publishes every wave's part of tile t (and orders the LDS reads around it)
-  if constexpr (N_AFTER == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-  else if constexpr (N_AFTER == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+template <int N_AFTER, int PER_STEP>
+__device__ inline void ns_wait_barrier() {
+  // this wave's DMA of the K-step about to be read is complete when at most N_AFTER * PER_STEP newer
+  // instructions are outstanding
+  if constexpr (N_AFTER * PER_STEP == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N_AFTER * PER_STEP == 5) asm volatile("s_waitcnt vmcnt(5)\n\ts_barrier" ::: "memory");
+  else if constexpr (N_AFTER * PER_STEP == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+  else if constexpr (N_AFTER * PER_STEP == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  else if constexpr (N_AFTER * PER_STEP == 10) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+  else if constexpr (N_AFTER * PER_STEP == 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+  else if constexpr (N_AFTER * PER_STEP == 16) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  else static_assert(N_AFTER * PER_STEP == 0, "unsupported vmcnt");
 }
 
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void k_gemm_pipe(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
-                                                      int M, int N, int K, int lda, int ldw, EpiArgs ea) {
-  // [stage][A | W][256 rows x 32 k] bf16 = 128 KiB for the K loop; 8 x [64][68] f32 = 136 KiB after it
-  __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 64 * GB_EPI_LD * 2];
+template <int EPI, int BN, int NST, bool PRIO>
+__global__ __launch_bounds__(512, 1) void k_gemm_ns(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                    int M, int N, int K, int lda, int ldw, EpiArgs ea) {
+  constexpr int WN = BN / 4, NT = WN / 16;                    // per-wave columns, 16-wide n-tiles
+  constexpr int STAGE = (GB_BM + BN) * GB_BK;                   // bf16 elements per stage
+  constexpr int IA = GB_BM * GB_BK / (8 * 512), IB = BN * GB_BK / (8 * 512);  // DMA instructions per wave
+  constexpr int EPI_LD = WN + 4;
+  constexpr int SMEM = (NST * STAGE * 2 > 8 * 64 * EPI_LD * 4) ? NST * STAGE * 2 : 8 * 64 * EPI_LD * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SMEM];
+  bf16_t* smem = (bf16_t*)smem_raw;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int ntm = (M + GB_BM - 1) / GB_BM, ntn = (N + GB_BN - 1) / GB_BN;
+  const int ntm = (M + GB_BM - 1) / GB_BM, ntn = (N + BN - 1) / BN;
   const int nwg = ntm * ntn;
   const int orig = blockIdx.x;
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   const int tm = wgid / ntn, tn = wgid - tm * ntn;
-  const int m0 = tm * GB_BM, n0 = tn * GB_BN;
+  const int m0 = tm * GB_BM, n0 = tn * BN;
 
-  // DMA assignment: wave w issues instructions i = 0, 1 for A and for W; instruction (w, i) fills tile rows
-  // 16 (2w + i) .. +15 (1 KiB = 16 rows x 64 B). Lane l: row 16(2w+i) + (l>>2), LDS chunk slot l&3 <- global
-  // chunk (l&3) ^ swz(row).
-  const bf16_t* ga[2];
-  const bf16_t* gw[2];
+  const bf16_t* ga[IA];
+  const bf16_t* gw[IB];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 16 * (2 * wid + i) + (lane >> 2);
-    const int ch = (lane & 3) ^ gp_swz(row);
-    ga[i] = A + (size_t)min(m0 + row, M - 1) * lda + ch * 8;
-    gw[i] = W + (size_t)min(n0 + row, N - 1) * ldw + ch * 8;
+  for (int i = 0; i < IA; ++i) {
+    const int row = 8 * (IA * wid + i) + (lane >> 3);
+    ga[i] = A + (size_t)min(m0 + row, M - 1) * lda + ((lane & 7) ^ gb_swz(row)) * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    const int row = 8 * (IB * wid + i) + (lane >> 3);
+    gw[i] = W + (size_t)min(n0 + row, N - 1) * ldw + ((lane & 7) ^ gb_swz(row)) * 8;
   }
   auto stage = [&](int st, int k0) {
-    bf16_t* As = smem + st * 2 * GB_BM * GP_BK;
-    bf16_t* Ws = As + GB_BM * GP_BK;
+    bf16_t* As = smem + st * STAGE;
+    bf16_t* Ws = As + GB_BM * GB_BK;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int rb = 16 * (2 * wid + i) * GP_BK;  // wave-uniform LDS base of this instruction
-      __builtin_amdgcn_global_load_lds((const void*)(ga[i] + k0), (lds_void_t*)(As + rb), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(gw[i] + k0), (lds_void_t*)(Ws + rb), 16, 0, 0);
-    }
+    for (int i = 0; i < IA; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(ga[i] + k0), (lds_void_t*)(As + 8 * (IA * wid + i) * GB_BK), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < IB; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(gw[i] + k0), (lds_void_t*)(Ws + 8 * (IB * wid + i) * GB_BK), 16, 0, 0);
   };
 
   const int wr = wid >> 2, wc = wid & 3;
   const int fr = lane & 15, fq = lane >> 4;
-  f32x4 acc[8][4];
+  f32x4 acc[8][NT];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / GP_BK;
+  const int nk = K / GB_BK;
 #pragma unroll
-  for (int t = 0; t < GP_STAGES - 1; ++t)
-    if (t < nk) stage(t, t * GP_BK);
+  for (int t = 0; t < NST - 1; ++t)
+    if (t < nk) stage(t, t * GB_BK);
   for (int kt = 0; kt < nk; ++kt) {
-    const int after = min(GP_STAGES - 2, nk - 1 - kt);
-    if (after == 2) gp_wait_barrier<2>();
-    else if (after == 1) gp_wait_barrier<1>();
-    else gp_wait_barrier<0>();
-    if (kt + GP_STAGES - 1 < nk) stage((kt + GP_STAGES - 1) % GP_STAGES, (kt + GP_STAGES - 1) * GP_BK);
-    const bf16_t* As = smem + (kt % GP_STAGES) * 2 * GB_BM * GP_BK;
-    const bf16_t* Ws = As + GB_BM * GP_BK;
-    bf16x8 bfr[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = wc * 64 + j * 16 + fr;
-      bfr[j] = *(const bf16x8*)(Ws + col * GP_BK + ((fq ^ gp_swz(col)) << 3));
+    const int after = min(NST - 2, nk - 1 - kt);
+    if constexpr (NST == 3) {
+      if (after == 1) ns_wait_barrier<1, IA + IB>();
+      else ns_wait_barrier<0, IA + IB>();
+    } else {
+      ns_wait_barrier<0, IA + IB>();
     }
+    if (kt + NST - 1 < nk) stage((kt + NST - 1) % NST, (kt + NST - 1) * GB_BK);
+    const bf16_t* As = smem + (kt % NST) * STAGE;
+    const bf16_t* Ws = As + GB_BM * GB_BK;
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = wr * 128 + i * 16 + fr;
-      const bf16x8 af = *(const bf16x8*)(As + row * GP_BK + ((fq ^ gp_swz(row)) << 3));
+    for (int kk = 0; kk < 2; ++kk) {
+      const int kc = 4 * kk + fq;
+      bf16x8 bfr[NT];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < NT; ++j) {
+        const int col = wc * WN + j * 16 + fr;
+        bfr[j] = *(const bf16x8*)(Ws + col * GB_BK + ((kc ^ gb_swz(col)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = wr * 128 + i * 16 + fr;
+        const bf16x8 af = *(const bf16x8*)(As + row * GB_BK + ((kc ^ gb_swz(row)) << 3));
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+      }
     }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // LDS is reused by the epilogue
 
-  const int ncol0 = n0 + wc * 64;
-  const int rc = (lane & 15) * 4;
+  // epilogue through LDS (as k_gemm_big): per wave 64 rows x WN cols at a time, read back 4 cols per lane
+  constexpr int LPR = WN / 4;           // lanes per row in the read-back
+  constexpr int RPI = 64 / LPR;         // rows per wave-instruction
+  const int ncol0 = n0 + wc * WN;
+  const int rc = (lane % LPR) * 4;
   float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (ea.bias) {
     const int n = ncol0 + rc;
@@ -453,7 +469,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_pipe(const bf16_t* __restrict__
     bias4.z = ea.bias[min(n + 2, N - 1)];
     bias4.w = ea.bias[min(n + 3, N - 1)];
   }
-  float* wimg = (float*)smem + wid * (64 * GB_EPI_LD);
+  float* wimg = (float*)smem + wid * (64 * EPI_LD);
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int ib = 4 * half;
@@ -461,16 +477,16 @@ __global__ __launch_bounds__(512, 1) void k_gemm_pipe(const bf16_t* __restrict__
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NT; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) wimg[(ii * 16 + fq * 4 + r) * GB_EPI_LD + j * 16 + fr] = acc[ib + ii][j][r];
+        for (int r = 0; r < 4; ++r) wimg[(ii * 16 + fq * 4 + r) * EPI_LD + j * 16 + fr] = acc[ib + ii][j][r];
     __syncthreads();
     const int mrow0 = m0 + wr * 128 + ib * 16;
 #pragma unroll 4
-    for (int rr = 0; rr < 16; ++rr) {
-      const int lr = rr * 4 + (lane >> 4);
+    for (int rr = 0; rr < 64 / RPI; ++rr) {
+      const int lr = rr * RPI + lane / LPR;
       const int m = mrow0 + lr;
-      float4 v = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
+      float4 v = *(const float4*)(wimg + lr * EPI_LD + rc);
       v.x += bias4.x; v.y += bias4.y; v.z += bias4.z; v.w += bias4.w;
       if (m < M && ncol0 + rc < N) epi_store4<EPI>(ea, m, ncol0 + rc, N, v);
     }
@@ -587,9 +603,15 @@ static int launch_gemm(const bf16_t* A, const bf16_t* W, int M, int N, int K, in
   if (M <= 32) {
     launch_skinny<EPI>(A, W, M, N, K, lda, ldw, ea, 1, s);
   } else {
-    if (tw_gemm_big_enabled == 2 && K % GP_BK == 0) {
-      unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
-      hipLaunchKernelGGL(k_gemm_pipe<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
+    if (tw_gemm_big_enabled >= 3) {
+      const int v = tw_gemm_big_enabled;
+      if (v == 3) {  // 256x256, 2 stages, counted-vmcnt loop, setprio
+        unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, 256);
+        hipLaunchKernelGGL((k_gemm_ns<EPI, 256, 2, true>), dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
+      } else {  // 256x128, 3 stages
+        unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, 128);
+        hipLaunchKernelGGL((k_gemm_ns<EPI, 128, 3, false>), dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
+      }
     } else if (tw_gemm_big_enabled) {
       unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
       hipLaunchKernelGGL(k_gemm_big<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
