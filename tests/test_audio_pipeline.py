@@ -92,3 +92,31 @@ def test_install_patches_reference_class(monkeypatch):
     assert a.load_transcription_model() is True and b.load_transcription_model() is True
     assert built == ["openai/whisper-large-v3"]          # built once, then served from the module cache
     assert a.transcription_model is b.transcription_model is mod._PIPELINE_CACHE["transcription_model"]
+
+
+def test_overlapped_diarization_same_result_and_concurrent(tmp_path):
+    """BASELINE config 4: the host diarizer runs beside the (GPU) transcription; results are identical."""
+    import threading
+    import time
+
+    started = threading.Event()
+
+    class SlowASR(FakeASR):
+        def __call__(self, inputs, **kw):
+            assert started.wait(5), "diarizer did not start before transcription finished"
+            time.sleep(0.2)
+            return super().__call__(inputs, **kw)
+
+    def diar(path, n):
+        started.set()
+        time.sleep(0.2)
+        return []
+
+    p = _wav(tmp_path)
+    seq = ap.AudioProcessingPipeline(transcriber=FakeASR(), diarize_fn=lambda a, n: []).process_audio(p)
+    t0 = time.time()
+    ovl = ap.AudioProcessingPipeline(transcriber=SlowASR(), diarize_fn=diar, overlap_diarization=True).process_audio(p)
+    wall = time.time() - t0
+    assert wall < 0.39  # 0.2 s + 0.2 s, overlapped
+    for k in ("text", "segments", "diarization_segments", "merged_segments", "duration"):
+        assert ovl[k] == seq[k]

@@ -78,9 +78,12 @@ class AudioProcessingPipeline:
     """Standalone mirror of the reference class's transcription surface."""
 
     def __init__(self, diarize_fn: Optional[Callable[[str, int], List[Dict[str, Any]]]] = None,
-                 transcriber: Optional[TurboTranscriber] = None):
+                 transcriber: Optional[TurboTranscriber] = None, overlap_diarization: bool = False):
         self.transcription_model = transcriber
         self.diarize_fn = diarize_fn
+        # BASELINE config 4: run the host-CPU diarizer concurrently with the GPU transcription (the reference runs
+        # them back to back, :589-624); results are identical, only processing_times change
+        self.overlap_diarization = overlap_diarization
         if transcriber is not None and _PIPELINE_CACHE["transcription_model"] is None:
             _PIPELINE_CACHE["transcription_model"] = transcriber
 
@@ -124,6 +127,14 @@ class AudioProcessingPipeline:
         start_time = time.time()
         processing_times: Dict[str, float] = {}
         try:
+            diar_future = None
+            if self.overlap_diarization and self.diarize_fn:
+                import concurrent.futures
+
+                pool = concurrent.futures.ThreadPoolExecutor(max_workers=1)
+                t_d = time.time()
+                diar_future = pool.submit(self.diarize_fn, audio_path, num_speakers)
+                pool.shutdown(wait=False)
             t0 = time.time()
             transcription = self.transcribe(audio_path, task)
             processing_times["transcription"] = time.time() - t0
@@ -135,9 +146,13 @@ class AudioProcessingPipeline:
                 segments = transcription["segments"]
             if not segments:
                 segments = [{"text": text, "start": 0, "end": 0}]
-            t0 = time.time()
-            diarization_segments = self.diarize_fn(audio_path, num_speakers) if self.diarize_fn else []
-            processing_times["diarization"] = time.time() - t0
+            if diar_future is not None:
+                diarization_segments = diar_future.result()
+                processing_times["diarization"] = time.time() - t_d
+            else:
+                t0 = time.time()
+                diarization_segments = self.diarize_fn(audio_path, num_speakers) if self.diarize_fn else []
+                processing_times["diarization"] = time.time() - t0
             merged_segments = self._merge_transcription_with_diarization(transcription, diarization_segments)
             try:
                 duration = audio.duration_seconds(audio_path)
