@@ -1,0 +1,62 @@
+/*
+ * tw_audio.h — C-ABI of the native audio ingest in front of the transcription hot path.
+ *
+ * The reference reads every input through ffmpeg: transformers' ffmpeg_read
+ * ($TF/pipelines/audio_utils.py:9-45, called from AutomaticSpeechRecognitionPipeline.preprocess,
+ * $TF/pipelines/automatic_speech_recognition.py:345-356) pipes the file bytes through
+ * `ffmpeg -i pipe:0 -ac 1 -ar 16000 -f f32le`, i.e. container decode -> downmix to mono -> libswresample's
+ * default resampler -> float32. This image has no ffmpeg, so these two stages are native here:
+ *
+ *   tw_flac_probe / tw_flac_decode   FLAC container + frame decode on HOST memory (multi-threaded over frames),
+ *                                    bit-exact PCM (checked against the stream's own STREAMINFO MD5)
+ *   tw_resample_pcm_i32 / _f32       downmix + polyphase resample on the GPU (DEVICE memory, `stream`), the
+ *                                    libswresample default filter restated (Kaiser-windowed sinc, see
+ *                                    twamd/audio.py: swr_filter_bank)
+ *
+ * Conventions as tw_whisper.h: 0 = success, nonzero = failure with tw_last_error() set.
+ */
+#ifndef TW_AUDIO_H
+#define TW_AUDIO_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct TwFlacInfo {
+  int32_t sample_rate;     /* Hz (STREAMINFO)                                                          */
+  int32_t channels;        /* 1..8                                                                     */
+  int32_t bits_per_sample; /* 4..32                                                                    */
+  int32_t min_blocksize;   /* samples per channel                                                      */
+  int32_t max_blocksize;
+  int32_t reserved;
+  int64_t total_samples;   /* per channel; 0 = unknown (tw_flac_decode then refuses the stream)        */
+  int64_t audio_offset;    /* byte offset of the first frame                                           */
+  uint8_t md5[16];         /* MD5 of the unencoded PCM (interleaved, little-endian, ceil(bps/8) bytes) */
+} TwFlacInfo;
+
+/* Parse the "fLaC" marker and the metadata blocks (STREAMINFO required). HOST memory. */
+int tw_flac_probe(const uint8_t* data, int64_t size, TwFlacInfo* info);
+
+/* Decode every frame into out = int32[out_frames][channels] (interleaved, HOST memory, sample values as coded,
+ * i.e. in [-2^(bps-1), 2^(bps-1))). out_frames must be >= info.total_samples. Frames are verified with their
+ * CRC-8 header and CRC-16 footer; a damaged frame is an error (no concealment). n_threads <= 0 = hardware
+ * concurrency. *frames_decoded receives the samples per channel written. */
+int tw_flac_decode(const uint8_t* data, int64_t size, int32_t* out, int64_t out_frames, int32_t n_threads,
+                   int64_t* frames_decoded);
+
+/* Polyphase resampling y[n] = sum_i taps[ph][i] * x[idx + i - center], idx = floor(n*down/up),
+ * ph = (n*down) % up, center = (ntaps-1)/2, x reflected at both ends (x[-k] = x[k], x[n_in-1+k] = x[n_in-1-k]).
+ * taps: f32[up][ntaps] DEVICE. y: f32[n_out] DEVICE.
+ *   _i32: x[t] = scale * mean_c pcm[t][c]   (pcm int32[n_in][channels], DEVICE)  — decode output as-is
+ *   _f32: x[t] = mean_c x_in[t][c]           (f32[n_in][channels], DEVICE)
+ * up == down == 1 with ntaps == 1 is a plain downmix/convert. */
+int tw_resample_pcm_i32(const int32_t* pcm, int64_t n_in, int32_t channels, float scale, int32_t up, int32_t down,
+                        const float* taps, int32_t ntaps, float* y, int64_t n_out, void* stream);
+int tw_resample_pcm_f32(const float* x, int64_t n_in, int32_t channels, int32_t up, int32_t down, const float* taps,
+                        int32_t ntaps, float* y, int64_t n_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,132 @@
+"""Native audio ingest, CPU side: the FLAC decoder in libtwhip.so (host code) and the
+resampler's filter design. The GPU resampler is tested in tests/test_gpu_audio.py.
+
+Pins: the reference's own example file (examples/Test1/ChrisAndAlexDiTest.flac, libFLAC 1.4.2, 192 kHz 16-bit
+mono) must decode to PCM whose MD5 equals its STREAMINFO MD5 (runs where /root/reference exists); streams from
+the oracle's FLAC writer (oracle/audio_oracle.py) cover every subframe type, stereo mode, bit depth and blocking
+strategy and must round-trip exactly."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import audio_oracle as ao
+from twamd import audio
+from twamd.synth_audio import speech_like
+
+REF_FLAC = "/root/reference/examples/Test1/ChrisAndAlexDiTest.flac"
+
+
+def _pcm(n, ch, bps, seed):
+    """Speech-like integer PCM with some structure (LPC has something to predict) and full-scale peaks."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / 16000.0
+    cols = []
+    for c in range(ch):
+        x = 0.6 * speech_like(n / 16000.0 + 0.01, seed + c)[:n] + 0.05 * rng.standard_normal(n)
+        x += 0.2 * np.sin(2 * np.pi * (220 + 30 * c) * t)
+        cols.append(x)
+    x = np.clip(np.stack(cols, 1), -1, 1)
+    lim = (1 << (bps - 1)) - 1
+    return np.round(x * lim).astype(np.int32)
+
+
+def _roundtrip(pcm, bps, threads=1, **kw):
+    data = ao.flac_encode(pcm, 44100, bps, **kw)
+    fl = audio.decode_flac(data, threads=threads)
+    np.testing.assert_array_equal(fl.pcm, pcm.reshape(len(pcm), -1))
+    assert audio.pcm_md5(fl.pcm, bps) == fl.md5
+    return data
+
+
+@pytest.mark.skipif(not os.path.exists(REF_FLAC), reason="reference example not present")
+@pytest.mark.parametrize("threads", [1, 4])
+def test_reference_example_md5(threads):
+    data = open(REF_FLAC, "rb").read()
+    fl = audio.decode_flac(data, threads=threads)
+    assert (fl.sample_rate, fl.bits_per_sample, fl.pcm.shape) == (192000, 16, (3788416, 1))
+    assert audio.pcm_md5(fl.pcm, 16) == fl.md5 == bytes.fromhex("ad59c8238990b312513c3de75bda098e")
+    assert abs(audio.duration_seconds(REF_FLAC) - 19.731333) < 1e-5  # output.json's last timestamp is 19.74
+
+
+@pytest.mark.parametrize("kind", ["verbatim", "constant", "fixed0", "fixed1", "fixed2", "fixed3", "fixed4",
+                                  "lpc1", "lpc8", "lpc12", "lpc32"])
+def test_subframe_kinds_mono16(kind):
+    pcm = _pcm(5000, 1, 16, 3)
+    if kind == "constant":
+        pcm[:] = -1234
+    _roundtrip(pcm, 16, blocksizes=(1152,), subframe_kinds=(kind,))
+
+
+@pytest.mark.parametrize("mode", [0, 8, 9, 10])
+@pytest.mark.parametrize("bps", [16, 24])
+def test_stereo_decorrelation(mode, bps):
+    _roundtrip(_pcm(6000, 2, bps, 5), bps, blocksizes=(2048,), subframe_kinds=("lpc10", "fixed2"),
+               stereo_modes=(mode,))
+
+
+@pytest.mark.parametrize("bps", [8, 12, 20])
+def test_bit_depths(bps):
+    _roundtrip(_pcm(3000, 1, bps, 7), bps, blocksizes=(576,), subframe_kinds=("lpc6", "fixed3", "verbatim"))
+
+
+def test_multichannel_wasted_bits_and_escapes():
+    pcm = _pcm(4000, 3, 16, 9) & ~7  # three trailing zero bits in every sample -> wasted-bits subframes
+    _roundtrip(pcm, 16, blocksizes=(1024,), subframe_kinds=("lpc4", "fixed1", "verbatim"),
+               opts={"escape_parts": (1, 3), "porder": 3})
+    _roundtrip(_pcm(3000, 1, 16, 10), 16, blocksizes=(1000,), subframe_kinds=("fixed2",),
+               opts={"rice_method": 1, "porder": 0})
+
+
+def test_variable_blocking_and_odd_sizes():
+    _roundtrip(_pcm(9000, 2, 16, 11), 16, blocksizes=(4096, 192, 1000, 256, 333), subframe_kinds=("lpc8",),
+               stereo_modes=(10, 8, 0, 9), variable=True)
+    _roundtrip(_pcm(70, 1, 16, 12), 16, blocksizes=(4096,), subframe_kinds=("lpc8",))  # one short frame
+
+
+def test_threaded_decode_matches_sequential():
+    pcm = _pcm(16000 * 24, 2, 16, 13)
+    data = ao.flac_encode(pcm, 48000, 16, blocksizes=(4096,), subframe_kinds=("verbatim",), stereo_modes=(0, 10))
+    assert len(data) > 4 * 256 * 1024  # large enough for the decoder to split it
+    a = audio.decode_flac(data, threads=1).pcm
+    b = audio.decode_flac(data, threads=8).pcm
+    np.testing.assert_array_equal(a, pcm)
+    np.testing.assert_array_equal(b, pcm)
+
+
+def test_damaged_and_truncated_streams_raise():
+    pcm = _pcm(8000, 1, 16, 14)
+    data = bytearray(ao.flac_encode(pcm, 16000, 16, blocksizes=(1024,), subframe_kinds=("lpc8",)))
+    bad = bytearray(data)
+    bad[len(bad) // 2] ^= 0x10
+    with pytest.raises(ValueError, match="corrupt|decoded"):
+        audio.decode_flac(bytes(bad))
+    with pytest.raises(ValueError):
+        audio.decode_flac(bytes(data[: len(data) - 300]))
+    with pytest.raises(ValueError, match="not a FLAC"):
+        audio.decode_flac(b"RIFF" + bytes(60))
+
+
+@pytest.mark.parametrize("rates", [(192000, 16000), (44100, 16000), (48000, 16000), (8000, 16000),
+                                   (22050, 16000), (16000, 16000)])
+def test_filter_bank_matches_oracle_design(rates):
+    up, down, taps = audio.swr_filter_bank(*rates)
+    if rates[0] == rates[1]:
+        assert (up, down, taps.tolist()) == (1, 1, [[1.0]])
+        return
+    ou, od, ob = ao.swr_taps(*rates)
+    assert (up, down) == (ou, od) and taps.shape == ob.shape
+    np.testing.assert_allclose(taps, ob, rtol=0, atol=2e-7)
+    if rates == (192000, 16000):
+        assert taps.shape == (1, 396)  # ceil(32 / (0.97 / 12))
+
+
+def test_flac_needs_gpu_to_resample_on_cpu():
+    """No CPU resampler in the product: FLAC (decoded on the host) still resamples on the GPU."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    data = ao.flac_encode(_pcm(4000, 1, 16, 15), 44100, 16, blocksizes=(1024,))
+    with pytest.raises(RuntimeError, match="GPU"):
+        audio.load_input(data)

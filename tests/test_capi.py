@@ -1,4 +1,5 @@
-"""The C-ABI boundary: libtwhip.so builds, loads, and exports exactly what include/tw_whisper.h declares.
+"""The C-ABI boundary: libtwhip.so builds, loads, and exports exactly what include/tw_whisper.h and
+include/tw_audio.h declare.
 CPU only (no compute calls)."""
 import ctypes
 import os
@@ -8,12 +9,12 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HDR = os.path.join(ROOT, "include", "tw_whisper.h")
+HDRS = [os.path.join(ROOT, "include", h) for h in ("tw_whisper.h", "tw_audio.h")]
 LIB = os.path.join(ROOT, "turbo-whisper-workspace_amd", "twamd", "libtwhip.so")
 
 
 def _declared():
-    src = open(HDR).read()
+    src = "".join(open(h).read() for h in HDRS)
     return sorted(set(re.findall(r"^(?:int|const char\*)\s+(tw_\w+)\s*\(", src, flags=re.M)))
 
 

@@ -113,7 +113,7 @@ extern "C" int tw_logmel(const float* wave, int n_chunks, const float* basis_cos
   TW_REQUIRE(n_chunks > 0 && n_mels > 0 && n_mels <= 128, "tw_logmel: n_chunks=%d n_mels=%d", n_chunks, n_mels);
   hipStream_t s = (hipStream_t)stream;
   int mp = (n_mels + 31) / 32 * 32;
-  hipMemsetAsync(maxkeys, 0, sizeof(uint32_t) * n_chunks, s);
+  (void)hipMemsetAsync(maxkeys, 0, sizeof(uint32_t) * n_chunks, s);
   size_t lds = sizeof(float) * 32 * (LM_XS + LM_PS);
   hipLaunchKernelGGL(k_logmel, dim3(tw_cdiv(LM_FRAMES, 32), n_chunks), dim3(256), lds, s, wave, basis_cos, basis_sin,
                      mel_fb, n_mels, mp, feats, maxkeys);

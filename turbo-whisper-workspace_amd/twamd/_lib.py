@@ -1,4 +1,4 @@
-"""ctypes binding of libtwhip.so, the C-ABI declared in include/tw_whisper.h.
+"""ctypes binding of libtwhip.so, the C-ABI declared in include/tw_whisper.h and include/tw_audio.h.
 
 The library must be built (`make -C turbo-whisper-workspace_amd/csrc`, or `__graft_entry__.build()`).
 There is deliberately no fallback: if the HIP library is missing every engine entry point raises.
@@ -26,12 +26,13 @@ TW_SELECT_WS_PER_ROW = 128
 TW_STATE_STRIDE = 8
 TW_ST_NGEN, TW_ST_LAST, TW_ST_PENULT, TW_ST_LASTTS, TW_ST_FINISHED, TW_ST_LANG = 0, 1, 2, 3, 4, 5
 
-# every symbol include/tw_whisper.h declares (tests check the .so exports all of them)
+# every symbol include/tw_whisper.h + include/tw_audio.h declare (tests check the .so exports all of them)
 EXPORTED = (
     "tw_version", "tw_last_error", "tw_fill_synth", "tw_f32_to_bf16", "tw_logmel", "tw_im2col_conv1",
     "tw_im2col_conv2", "tw_gemm_bf16", "tw_layernorm", "tw_attn_encoder", "tw_attn_decode_self",
     "tw_attn_decode_cross", "tw_embed_decoder", "tw_logits_select", "tw_gemm_bf16_partial", "tw_resid_layernorm",
     "tw_gemm_set_variant", "tw_attn_set_variant",
+    "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
 )
 
 
@@ -41,6 +42,14 @@ class TwSelectParams(ctypes.Structure):
         ("no_timestamps", ctypes.c_int32), ("max_initial_ts", ctypes.c_int32), ("use_timestamps", ctypes.c_int32),
         ("max_new", ctypes.c_int32), ("mode", ctypes.c_int32), ("lo", ctypes.c_int32), ("hi", ctypes.c_int32),
         ("n_begin_suppress", ctypes.c_int32), ("begin_suppress", ctypes.c_int32 * 8),
+    ]
+
+
+class TwFlacInfo(ctypes.Structure):
+    _fields_ = [
+        ("sample_rate", ctypes.c_int32), ("channels", ctypes.c_int32), ("bits_per_sample", ctypes.c_int32),
+        ("min_blocksize", ctypes.c_int32), ("max_blocksize", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("total_samples", ctypes.c_int64), ("audio_offset", ctypes.c_int64), ("md5", ctypes.c_uint8 * 16),
     ]
 
 
@@ -74,6 +83,10 @@ _SIGS = {
     "tw_gemm_set_variant": ([_I], _I),
     "tw_attn_set_variant": ([_I], _I),
     "tw_resid_layernorm": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
+    "tw_flac_probe": ([_P, ctypes.c_int64, ctypes.POINTER(TwFlacInfo)], _I),
+    "tw_flac_decode": ([_P, ctypes.c_int64, _P, ctypes.c_int64, _I, ctypes.POINTER(ctypes.c_int64)], _I),
+    "tw_resample_pcm_i32": ([_P, ctypes.c_int64, _I, _F, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),
+    "tw_resample_pcm_f32": ([_P, ctypes.c_int64, _I, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),
 }
 
 _lib = None

@@ -1,25 +1,127 @@
-"""Audio ingest for the transcriber (host side, before the GPU path).
+"""Audio ingest for the transcriber (host decode + GPU resample, before the log-mel).
 
 Mirrors the input handling of AutomaticSpeechRecognitionPipeline.preprocess
-($TF/pipelines/automatic_speech_recognition.py:345-420): a path is read as bytes, bytes are decoded
-to mono f32 at 16 kHz (the reference shells out to ffmpeg, $TF/pipelines/audio_utils.py:9-45, which
-this image does not have), dicts carry {"raw"|"array", "sampling_rate"} and are resampled when the
-rate differs, multi-channel arrays are averaged to mono.
+($TF/pipelines/automatic_speech_recognition.py:345-420): a path is read as bytes, bytes are decoded to mono f32
+at 16 kHz (the reference shells out to `ffmpeg -ac 1 -ar 16000 -f f32le`, $TF/pipelines/audio_utils.py:9-45,
+which this image does not have), dicts carry {"raw"|"array", "sampling_rate"} and are resampled when the rate
+differs, multi-channel arrays are averaged to mono.
 
-Decoders here: RIFF/WAVE (PCM 8/16/24/32-bit, IEEE float 32/64). Resampling uses a polyphase
-windowed-sinc filter (scipy.signal.resample_poly); ffmpeg's resampler is not bit-reproducible,
-so no reference value is claimed for resampled input.
+Containers: FLAC (native multi-threaded decoder in libtwhip.so, include/tw_audio.h; bit-exact, verifiable
+against the stream's STREAMINFO MD5) and RIFF/WAVE (PCM 8/16/24/32-bit, IEEE float 32/64).
+Resampling runs on the GPU (tw_resample_pcm_*) with libswresample's default filter restated in
+swr_filter_bank. There is no CPU resampler in the product: resampling without a GPU raises.
 """
 from __future__ import annotations
 
+import ctypes
 import io
+import math
 import struct
-from fractions import Fraction
-from typing import Tuple, Union
+from typing import NamedTuple, Tuple, Union
 
 import numpy as np
 
 TARGET_SR = 16000
+
+
+class FlacStream(NamedTuple):
+    pcm: np.ndarray  # int32 [frames, channels], sample values as coded
+    sample_rate: int
+    bits_per_sample: int
+    md5: bytes  # STREAMINFO MD5 of the unencoded PCM
+
+
+def _flac_lib():
+    from . import _lib
+
+    return _lib, _lib.load()
+
+
+def flac_probe(data: bytes):
+    _lib, lib = _flac_lib()
+    info = _lib.TwFlacInfo()
+    buf = ctypes.c_char_p(data)
+    if lib.tw_flac_probe(buf, len(data), ctypes.byref(info)) != 0:
+        raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    return info
+
+
+def decode_flac(data: bytes, threads: int = 0) -> FlacStream:
+    """FLAC bytes -> int32 PCM through the native decoder (frame CRCs checked; no concealment)."""
+    _lib, lib = _flac_lib()
+    info = flac_probe(data)
+    pcm = np.empty((int(info.total_samples), int(info.channels)), np.int32)
+    got = ctypes.c_int64()
+    if lib.tw_flac_decode(ctypes.c_char_p(data), len(data), pcm.ctypes.data, pcm.shape[0], int(threads),
+                          ctypes.byref(got)) != 0:
+        raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    return FlacStream(pcm, int(info.sample_rate), int(info.bits_per_sample), bytes(info.md5))
+
+
+def pcm_md5(pcm: np.ndarray, bits_per_sample: int) -> bytes:
+    """FLAC's STREAMINFO checksum definition: MD5 over interleaved little-endian samples of ceil(bps/8) bytes."""
+    import hashlib
+
+    nb = (bits_per_sample + 7) // 8
+    raw = np.ascontiguousarray(pcm, dtype="<i4").view(np.uint8).reshape(-1, 4)[:, :nb]
+    return hashlib.md5(np.ascontiguousarray(raw).tobytes()).digest()
+
+
+def swr_filter_bank(sr_in: int, sr_out: int, filter_size: int = 32, cutoff: float = 0.97,
+                    kaiser_beta: float = 9.0) -> Tuple[int, int, np.ndarray]:
+    """libswresample's default resampler design (what `ffmpeg -ar 16000` runs): exact rational phases
+    up/down = sr_out/sr_in reduced, Kaiser-windowed sinc of filter_length = ceil(filter_size / factor) taps with
+    factor = min(up/down * cutoff, 1), each phase normalised by the sum of phase 0.
+    Returns (up, down, taps f32[up][ntaps]); tap i of phase ph sits at offset (i - center) - ph/up input samples,
+    center = (ntaps - 1) // 2."""
+    g = math.gcd(int(sr_in), int(sr_out))
+    up, down = int(sr_out) // g, int(sr_in) // g
+    if up == down:
+        return 1, 1, np.ones((1, 1), np.float32)
+    factor = min(up / down * cutoff, 1.0)
+    T = max(int(math.ceil(filter_size / factor)), 1)
+    center = (T - 1) // 2
+    i = np.arange(T, dtype=np.float64)[None, :]
+    ph = np.arange(up, dtype=np.float64)[:, None]
+    x = np.pi * ((i - center) - ph / up) * factor
+    with np.errstate(invalid="ignore", divide="ignore"):
+        y = np.where(x == 0, 1.0, np.sin(x) / np.where(x == 0, 1.0, x))
+    w = 2.0 * x / (factor * T * np.pi)
+    y = y * np.i0(kaiser_beta * np.sqrt(np.maximum(1.0 - w * w, 0.0)))
+    y = y / y[0].sum()
+    return up, down, y.astype(np.float32)
+
+
+def resample_device(x: np.ndarray, sr_in: int, sr_out: int = TARGET_SR, scale: float = 1.0,
+                    device=None):
+    """Downmix + resample on the GPU: x is int32 PCM [frames, ch] (times `scale`) or float [frames] /
+    [frames, ch]. Returns a float32 torch tensor [n_out] on `device` (default: the current GPU)."""
+    import torch
+
+    from . import _lib
+
+    if not torch.cuda.is_available():
+        raise RuntimeError("resampling runs on the GPU (tw_resample_pcm_*); no GPU is visible")
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    up, down, taps = swr_filter_bank(sr_in, sr_out)
+    x = np.asarray(x)
+    if x.ndim == 1:
+        x = x[:, None]
+    n_in, ch = x.shape
+    n_out = -(-n_in * up // down)
+    with torch.cuda.device(dev):
+        xd = torch.from_numpy(np.ascontiguousarray(x)).to(dev, non_blocking=False)
+        td = torch.from_numpy(taps).to(dev)
+        y = torch.empty(n_out, dtype=torch.float32, device=dev)
+        st = _lib.stream_handle()
+        if x.dtype == np.int32:
+            _lib.call("tw_resample_pcm_i32", xd.data_ptr(), n_in, ch, float(scale), up, down, td.data_ptr(),
+                      taps.shape[1], y.data_ptr(), n_out, st)
+        else:
+            xd = xd.float()
+            _lib.call("tw_resample_pcm_f32", xd.data_ptr(), n_in, ch, up, down, td.data_ptr(), taps.shape[1],
+                      y.data_ptr(), n_out, st)
+    return y
 
 
 def decode_wav(data: bytes) -> Tuple[np.ndarray, int]:
@@ -63,26 +165,26 @@ def decode_wav(data: bytes) -> Tuple[np.ndarray, int]:
     return x[: n * ch].reshape(n, ch), sr
 
 
-def resample(x: np.ndarray, sr_in: int, sr_out: int = TARGET_SR) -> np.ndarray:
+def resample(x: np.ndarray, sr_in: int, sr_out: int = TARGET_SR, device=None) -> np.ndarray:
+    """Mono/multi-channel float -> mono float32 at sr_out (GPU when the rates differ)."""
     if sr_in == sr_out:
-        return x.astype(np.float32, copy=False)
-    from scipy.signal import resample_poly
-
-    fr = Fraction(sr_out, sr_in).limit_denominator(1000)
-    return resample_poly(x.astype(np.float64), fr.numerator, fr.denominator).astype(np.float32)
+        x = np.asarray(x, np.float32)
+        return x if x.ndim == 1 else x.mean(axis=1, dtype=np.float32)
+    return resample_device(np.asarray(x, np.float32), sr_in, sr_out, device=device).cpu().numpy()
 
 
-def decode_bytes(data: bytes, sr_out: int = TARGET_SR) -> np.ndarray:
+def decode_bytes(data: bytes, sr_out: int = TARGET_SR, device=None) -> np.ndarray:
     if data[:4] == b"RIFF":
         x, sr = decode_wav(data)
-        return resample(x.mean(axis=1) if x.shape[1] > 1 else x[:, 0], sr, sr_out)
+        return resample(x.mean(axis=1) if x.shape[1] > 1 else x[:, 0], sr, sr_out, device)
     if data[:4] == b"fLaC":
-        raise NotImplementedError("FLAC decoding is not implemented yet (the reference relies on ffmpeg); "
-                                  "convert to WAV or pass a decoded array")
-    raise ValueError("unrecognised audio container (supported: RIFF/WAVE)")
+        fl = decode_flac(data)
+        scale = 2.0 ** -(fl.bits_per_sample - 1)  # ffmpeg's s16/s32 -> flt conversion of the coded samples
+        return resample_device(fl.pcm, fl.sample_rate, sr_out, scale=scale, device=device).cpu().numpy()
+    raise ValueError("unrecognised audio container (supported: FLAC, RIFF/WAVE)")
 
 
-def load_input(inputs: Union[str, bytes, np.ndarray, dict], sr_out: int = TARGET_SR) -> np.ndarray:
+def load_input(inputs: Union[str, bytes, np.ndarray, dict], sr_out: int = TARGET_SR, device=None) -> np.ndarray:
     """Any pipeline input -> mono float32 at sr_out."""
     if isinstance(inputs, str):
         if inputs.startswith("http://") or inputs.startswith("https://"):
@@ -90,7 +192,7 @@ def load_input(inputs: Union[str, bytes, np.ndarray, dict], sr_out: int = TARGET
         with open(inputs, "rb") as f:
             inputs = f.read()
     if isinstance(inputs, (bytes, bytearray)):
-        return decode_bytes(bytes(inputs), sr_out)
+        return decode_bytes(bytes(inputs), sr_out, device)
     if isinstance(inputs, dict):
         d = dict(inputs)
         if not ("sampling_rate" in d and ("raw" in d or "array" in d)):
@@ -101,7 +203,7 @@ def load_input(inputs: Union[str, bytes, np.ndarray, dict], sr_out: int = TARGET
         arr = np.asarray(arr, dtype=np.float32)
         if arr.ndim != 1:
             arr = arr.mean(axis=0)
-        return resample(arr, int(d["sampling_rate"]), sr_out)
+        return resample(arr, int(d["sampling_rate"]), sr_out, device)
     if hasattr(inputs, "cpu") and hasattr(inputs, "numpy"):  # torch tensor
         inputs = inputs.cpu().numpy()
     if isinstance(inputs, np.ndarray):
@@ -120,6 +222,9 @@ def duration_seconds(path: str) -> float:
     if data[:4] == b"RIFF":
         x, sr = decode_wav(data)
         return x.shape[0] / float(sr)
+    if data[:4] == b"fLaC":
+        info = flac_probe(data)
+        return int(info.total_samples) / float(info.sample_rate)
     raise ValueError("duration: unsupported container")
 
 

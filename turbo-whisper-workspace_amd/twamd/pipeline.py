@@ -83,7 +83,8 @@ class TurboTranscriber:
             raise ValueError("Cannot specify `task` or `language` for an English-only model.")
 
         rank, world = dist.world()
-        wav = audio.load_input(inputs, self.sampling_rate) if rank == 0 else None
+        dev = getattr(self.engine, "device", None)
+        wav = audio.load_input(inputs, self.sampling_rate, dev) if rank == 0 else None
         if world > 1:  # SPMD: every rank calls with the same arguments; rank 0 decoded the input
             wav = dist.broadcast_waveform(wav)
         if chunk_length_s:
