@@ -32,6 +32,8 @@ extern "C" {
 #define TW_EPI_GELU_POS_F32 3 /* out f32 = gelu(acc+bias) + aux[m % aux_rows][n] (conv2 + pos)  */
 #define TW_EPI_F32 4          /* out f32 = acc + bias                        (proj_out logits)  */
 #define TW_EPI_CROSSKV 5      /* out bf16 scattered to [layer][k|v][b][head][s][64]             */
+#define TW_EPI_GELU_PACKED 6  /* tw_gemv_packed: out = packed activation (below) of gelu(acc+bias) (fc1 -> fc2) */
+#define TW_EPI_PARTIAL_F32 100 /* tw_gemv_packed: out f32[splits][M][ldo] split-K partials (no bias)          */
 
 /* Decoder per-row state (tw_logits_select), int32[TW_STATE_STRIDE] per batch row. */
 #define TW_STATE_STRIDE 8
@@ -128,6 +130,34 @@ int tw_attn_encoder(const uint16_t* qkv, int B, int S, int H, uint16_t* out, voi
 /* Measurement knob (process-wide, returns 0): encoder attention kernel of tw_attn_encoder. 8 (default) =
  * k_attn_enc2 with 8 waves / 256 queries per workgroup, 4 = the same with 4 waves, 0 = the first kernel. */
 int tw_attn_set_variant(int variant);
+
+/* ---- packed decoder GEMV ------------------------------------------------------------------------- */
+/* The decoder step's projections (M <= 32 rows: $TF/models/whisper/modeling_whisper.py:279-282, 375-376, and the
+ * tied proj_out :970) read every weight byte once per token, so their layout is chosen for the HBM stream:
+ *   packed weight      bf16 [ceil(N/16)][K/32][64][8]: (n, k) at ((n/16*K/32 + k/32)*64 + n%16 + 16*(k/8%4))*8 + k%8
+ *   packed activation  bf16 [K/32][2][64][8]:          (m, k) at ((k/32*2 + m/16)*64 + m%16 + 16*(k/8%4))*8 + k%8
+ * i.e. each (16 columns or rows) x (32-deep step) MFMA operand fragment is 1 KiB contiguous; pad columns are zero,
+ * activation rows M..31 are never written (keep them finite, e.g. zeroed once).
+ * tw_pack_weight: W bf16[N][ldw] -> Wp packed weight (setup time).
+ * tw_gemv_packed: out = epi(A . W^T); A packed activation (a_packed = 1) or row-major [M][lda]; epi TW_EPI_BF16,
+ *   TW_EPI_F32 (row-major [M][ldo]), TW_EPI_GELU_PACKED (packed activation, N % 32 == 0) or TW_EPI_PARTIAL_F32
+ *   (splits > 1 allowed; bias ignored). */
+int tw_pack_weight(const uint16_t* W, int N, int K, int ldw, uint16_t* Wp, void* stream);
+int tw_gemv_packed(const uint16_t* A, int a_packed, int lda, const uint16_t* Wp, int M, int N, int K, int epi,
+                   void* out, int ldo, const float* bias, int splits, void* stream);
+/* tw_resid_layernorm with the normalised rows written as a packed activation (M <= 32, D % 32 == 0). */
+int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
+                              const float* beta, int M, int D, float eps, uint16_t* out, void* stream);
+
+/* ---- streams ---------------------------------------------------------------------------------------- */
+/* A HIP stream whose kernels run only on the CUs whose bits are set in mask = uint32[words] (hipExtStream-
+ * CreateWithCUMask; the mask belongs to the stream's hardware queue, so hipGraph replays on it are confined too).
+ * On MI355X bit i selects CU i/8 of XCD i%8 (measured with scripts/exp/cumask_probe.hip), and an XCD left with
+ * no bit falls back to all of its CUs, so a balanced mask sets the same number of bits for every XCD. The engine
+ * uses it to give the decoder of window batch k CUs of its own while batch k+1 is encoded (twamd/engine.py).
+ * Setup-time calls: they allocate, are not capturable, and tw_stream_destroy synchronises the stream. */
+int tw_stream_create_masked(const uint32_t* mask, int32_t words, void** stream_out);
+int tw_stream_destroy(void* stream);
 /* Decoder self-attention for one new token per row: appends k,v of qkv bf16[B][3D] at pos[b] into
  * k_cache/v_cache bf16[B][H][max_pos][64] (this layer) and attends over 0..pos[b].
  * Replaces the causal self-attention + DynamicCache.update of modeling_whisper.py:312-335,448-505. */

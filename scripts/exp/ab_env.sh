@@ -1,0 +1,9 @@
+# A/B of environment settings on the bench: bash scripts/exp/ab_env.sh "VAR=a" "VAR=b" [reps]
+set -e
+reps=${3:-2}
+for i in $(seq 1 $reps); do
+  for e in "$1" "$2"; do
+    env $e timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/ab.log 2>&1
+    echo "$e $(tail -1 gpurun_out/ab.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['achieved'])")"
+  done
+done

@@ -64,7 +64,7 @@ def test_logmel_vs_oracle(n_mels):
 EPIS = [_lib.TW_EPI_BF16, _lib.TW_EPI_GELU_BF16, _lib.TW_EPI_RESID_F32, _lib.TW_EPI_F32]
 
 
-@pytest.mark.parametrize("variant", [1, 3, 4, 0])
+@pytest.mark.parametrize("variant", [1, 5, 3, 4, 0])
 @pytest.mark.parametrize("M,N,K", [(300, 384, 256), (1500, 1280, 1280), (24, 1280, 1280), (7, 51866, 384),
                                    (32, 5120, 1280), (129, 200, 64), (600, 512, 192), (257, 768, 3840)])
 @pytest.mark.parametrize("epi", EPIS)
@@ -278,3 +278,105 @@ def test_logits_select_matches_oracle_processors():
                   None, 448, ids.data_ptr(), None, ws.data_ptr(), S())
         ref = st.lang_begin + logits[:, st.lang_begin: st.lang_end].argmax(1)
         assert np.array_equal(ids.cpu().numpy(), ref)
+
+
+# ---- packed decoder GEMV (include/tw_whisper.h "packed" layouts), restated here with torch index math
+def _act_index(M, K):
+    m = torch.arange(M).view(M, 1)
+    k = torch.arange(K).view(1, K)
+    return (((k // 32) * 2 + m // 16) * 64 + m % 16 + 16 * ((k // 8) % 4)) * 8 + k % 8
+
+
+def pack_act(x):
+    M, K = x.shape
+    out = torch.zeros(K * 32, dtype=x.dtype, device=x.device)
+    out[_act_index(M, K).to(x.device).reshape(-1)] = x.reshape(-1)
+    return out
+
+
+def unpack_act(p, M, K):
+    return p[_act_index(M, K).to(p.device).reshape(-1)].view(M, K)
+
+
+def pack_w(W):
+    N, K = W.shape
+    G = (N + 15) // 16
+    n = torch.arange(N).view(N, 1)
+    k = torch.arange(K).view(1, K)
+    idx = ((n // 16 * (K // 32) + k // 32) * 64 + n % 16 + 16 * ((k // 8) % 4)) * 8 + k % 8
+    out = torch.zeros(G * 16 * K, dtype=W.dtype, device=W.device)
+    out[idx.to(W.device).reshape(-1)] = W.reshape(-1)
+    return out
+
+
+@pytest.mark.parametrize("N,K", [(100, 64), (1280, 1280), (51866, 384)])
+def test_pack_weight_layout(N, K):
+    W = rand_bf16(N, K, seed=31)
+    Wp = torch.full((((N + 15) // 16) * 16 * K,), float("nan"), dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_pack_weight", W.data_ptr(), N, K, K, Wp.data_ptr(), S())
+    assert torch.equal(Wp.view(torch.int16), pack_w(W).view(torch.int16))  # bit-exact, pad columns zero
+
+
+GEMV_CASES = [  # M, N, K, epi, splits
+    (24, 1280, 1280, _lib.TW_EPI_BF16, 1), (24, 3840, 1280, _lib.TW_EPI_BF16, 1), (7, 1280, 1280, _lib.TW_EPI_BF16, 1),
+    (24, 5120, 1280, _lib.TW_EPI_GELU_PACKED, 1), (13, 1536, 384, _lib.TW_EPI_GELU_PACKED, 1),
+    (24, 1280, 5120, _lib.TW_EPI_PARTIAL_F32, 4), (24, 1280, 1280, _lib.TW_EPI_PARTIAL_F32, 4),
+    (1, 384, 1536, _lib.TW_EPI_PARTIAL_F32, 3), (24, 51866, 1280, _lib.TW_EPI_F32, 1), (5, 51864, 384, _lib.TW_EPI_F32, 1),
+]
+
+
+@pytest.mark.parametrize("a_packed", [1, 0])
+@pytest.mark.parametrize("M,N,K,epi,splits", GEMV_CASES)
+def test_gemv_packed_vs_torch(M, N, K, epi, splits, a_packed):
+    A = rand_bf16(M, K, seed=41)
+    W = rand_bf16(N, K, scale=K ** -0.5, seed=42)
+    bias = torch.randn(N, device=DEV) * 0.1
+    Wp = pack_w(W)
+    Ain = pack_act(A) if a_packed else A
+    ref = A.float() @ W.float().t()
+    if epi == _lib.TW_EPI_PARTIAL_F32:
+        out = torch.full((splits, M, N), float("nan"), device=DEV)
+        _lib.call("tw_gemv_packed", Ain.data_ptr(), a_packed, K, Wp.data_ptr(), M, N, K, epi, out.data_ptr(), N, None,
+                  splits, S())
+        torch.testing.assert_close(out.sum(0), ref, atol=2e-3, rtol=2e-3)  # f32 accumulation order only
+        return
+    if epi == _lib.TW_EPI_GELU_PACKED:
+        out = torch.zeros(N * 32, dtype=torch.bfloat16, device=DEV)
+        _lib.call("tw_gemv_packed", Ain.data_ptr(), a_packed, K, Wp.data_ptr(), M, N, K, epi, out.data_ptr(), 0,
+                  bias.data_ptr(), 1, S())
+        got = unpack_act(out, M, N).float()
+        torch.testing.assert_close(got, torch.nn.functional.gelu(ref + bias), atol=2e-2, rtol=2e-2)  # bf16 output
+        full = _act_index(32, N).to(DEV)[M:].reshape(-1)
+        assert not out[full].float().abs().sum()  # rows M..31 untouched
+        return
+    dt = torch.bfloat16 if epi == _lib.TW_EPI_BF16 else torch.float32
+    out = torch.full((M, N), float("nan"), dtype=dt, device=DEV)
+    _lib.call("tw_gemv_packed", Ain.data_ptr(), a_packed, K, Wp.data_ptr(), M, N, K, epi, out.data_ptr(), N,
+              bias.data_ptr(), 1, S())
+    tol = 2e-2 if dt == torch.bfloat16 else 2e-3
+    torch.testing.assert_close(out.float(), ref + bias, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("M,D,nparts", [(24, 1280, 4), (5, 384, 0), (17, 256, 2)])
+def test_resid_layernorm_packed_vs_torch(M, D, nparts):
+    x = torch.randn(M, D, device=DEV) * 3 + 1
+    parts = torch.randn(max(nparts, 1), M, D, device=DEV)
+    bias = torch.randn(D, device=DEV) if nparts else None
+    g = torch.randn(D, device=DEV)
+    b = torch.randn(D, device=DEV)
+    out = torch.zeros(D * 32, dtype=torch.bfloat16, device=DEV)
+    xr = x + (bias + parts[:nparts].sum(0) if nparts else 0)
+    _lib.call("tw_resid_layernorm_packed", x.data_ptr(), parts.data_ptr(), nparts, _lib.ptr(bias), g.data_ptr(),
+              b.data_ptr(), M, D, 1e-5, out.data_ptr(), S())
+    torch.testing.assert_close(x, xr, atol=1e-5, rtol=1e-5)
+    ref = torch.nn.functional.layer_norm(xr, (D,), g, b, 1e-5)
+    torch.testing.assert_close(unpack_act(out, M, D).float(), ref, atol=3e-2, rtol=1e-2)
+    # same bits as the row-major kernel
+    rm = torch.empty(M, D, dtype=torch.bfloat16, device=DEV)
+    x2 = torch.randn(M, D, device=DEV)
+    x3 = x2.clone()
+    _lib.call("tw_resid_layernorm", x2.data_ptr(), parts.data_ptr(), nparts, _lib.ptr(bias), g.data_ptr(), b.data_ptr(),
+              M, D, 1e-5, rm.data_ptr(), S())
+    _lib.call("tw_resid_layernorm_packed", x3.data_ptr(), parts.data_ptr(), nparts, _lib.ptr(bias), g.data_ptr(),
+              b.data_ptr(), M, D, 1e-5, out.data_ptr(), S())
+    assert torch.equal(unpack_act(out, M, D).view(torch.int16), rm.view(torch.int16))

@@ -426,6 +426,7 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
 __global__ __launch_bounds__(256) void k_attn_decode_self(const bf16_t* __restrict__ qkv, int D, int max_pos,
                                                           const int* __restrict__ pos, bf16_t* __restrict__ kc,
                                                           bf16_t* __restrict__ vc, bf16_t* __restrict__ out) {
+  TW_DEC_PRIO();
   __shared__ float sc[DA_MAXK];
   __shared__ float part[32 * 64];
   __shared__ float qf[64];
@@ -452,6 +453,7 @@ __global__ __launch_bounds__(256) void k_attn_decode_self(const bf16_t* __restri
 __global__ __launch_bounds__(256) void k_attn_decode_cross(const bf16_t* __restrict__ q, int D, int S, int Bt,
                                                            const int* __restrict__ row_map,
                                                            const bf16_t* __restrict__ ckv, bf16_t* __restrict__ out) {
+  TW_DEC_PRIO();
   __shared__ float sc[DA_MAXK];
   __shared__ float part[32 * 64];
   __shared__ float qf[64];

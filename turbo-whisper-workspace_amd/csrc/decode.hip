@@ -64,6 +64,7 @@ __device__ inline RowMask row_mask(const int* st, const TwSelectParams& p) {
 __global__ __launch_bounds__(256) void k_select_partial(const float* __restrict__ logits, int ld_logits,
                                                         const uint32_t* __restrict__ suppress_bits, TwSelectParams p,
                                                         const int* __restrict__ state, SelPart* __restrict__ ws) {
+  TW_DEC_PRIO();
   __shared__ SelPart sp[4];
   const int b = blockIdx.x, c = blockIdx.y, NC = gridDim.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -143,6 +144,7 @@ __global__ __launch_bounds__(64) void k_select_final(const SelPart* __restrict__
                                                      int* __restrict__ state, int* __restrict__ tokens_out,
                                                      int ld_tokens, int* __restrict__ next_ids,
                                                      int* __restrict__ pos) {
+  TW_DEC_PRIO();
   const int b = blockIdx.x, lane = threadIdx.x;
   Best bt{-INFINITY, 0x7fffffff}, bs{-INFINITY, 0x7fffffff};
   float m_ts = -INFINITY, s_ts = 0.f;

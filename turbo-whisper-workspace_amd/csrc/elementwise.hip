@@ -128,6 +128,7 @@ extern "C" int tw_im2col_conv2(const bf16_t* h1, int R, int D, bf16_t* out, void
 __global__ void k_embed_decoder(const bf16_t* __restrict__ tok_emb, const bf16_t* __restrict__ pos_emb,
                                 const int* __restrict__ ids, const int* __restrict__ pos, int D,
                                 float* __restrict__ x) {
+  TW_DEC_PRIO();
   const int b = blockIdx.x;
   const bf16_t* te = tok_emb + (size_t)ids[b] * D;
   const bf16_t* pe = pos_emb + (size_t)pos[b] * D;
@@ -150,10 +151,12 @@ extern "C" int tw_embed_decoder(const bf16_t* tok_emb, const bf16_t* pos_emb, co
 #define RLN_MAXV 4  // float4 chunks per thread: D <= 4096
 // All loads are unconditional (index clamped into the row, result discarded): a guarded load per
 // element makes hipcc wait vmcnt(0) per element, a chain of L2 round trips.
+template <bool PACKED>
 __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const float* __restrict__ parts, int nparts,
                                                   long part_stride, const float* __restrict__ bias,
                                                   const float* __restrict__ g, const float* __restrict__ bta, int D,
                                                   float eps, bf16_t* __restrict__ out) {
+  TW_DEC_PRIO();
   __shared__ float red[8];
   const int row = blockIdx.x, tid = threadIdx.x;
   const int nc = D >> 2;
@@ -215,7 +218,11 @@ __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const f
       uint2 w;
       w.x = pack_bf16x2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
       w.y = pack_bf16x2((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
-      ((uint2*)orow)[c] = w;
+      if constexpr (PACKED) {
+        *(uint2*)(out + tw_pack_act_idx(row, 4 * c)) = w;  // 4 columns = half a 16-byte fragment chunk
+      } else {
+        ((uint2*)orow)[c] = w;
+      }
     }
   }
 }
@@ -226,7 +233,18 @@ extern "C" int tw_resid_layernorm(float* x, const float* parts, int nparts, cons
              1024 * RLN_MAXV);
   TW_REQUIRE(nparts >= 0 && (nparts == 0 || parts), "tw_resid_layernorm: parts");
   TW_REQUIRE(!gamma || (beta && out), "tw_resid_layernorm: gamma without beta/out");
-  hipLaunchKernelGGL(k_resid_ln, dim3(M), dim3(256), 0, (hipStream_t)stream, x, parts, nparts, (long)M * D, bias, gamma,
-                     beta, D, eps, out);
+  hipLaunchKernelGGL(k_resid_ln<false>, dim3(M), dim3(256), 0, (hipStream_t)stream, x, parts, nparts, (long)M * D, bias,
+                     gamma, beta, D, eps, out);
   return tw_check_launch("tw_resid_layernorm");
+}
+
+extern "C" int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias,
+                                         const float* gamma, const float* beta, int M, int D, float eps, uint16_t* out,
+                                         void* stream) {
+  TW_REQUIRE(x && gamma && beta && out && M > 0 && M <= 32 && D > 0 && D % 32 == 0 && D <= 1024 * RLN_MAXV,
+             "tw_resid_layernorm_packed: bad args (M <= 32, D %% 32, gamma/beta/out required)");
+  TW_REQUIRE(nparts >= 0 && (nparts == 0 || parts), "tw_resid_layernorm_packed: parts");
+  hipLaunchKernelGGL(k_resid_ln<true>, dim3(M), dim3(256), 0, (hipStream_t)stream, x, parts, nparts, (long)M * D, bias,
+                     gamma, beta, D, eps, out);
+  return tw_check_launch("tw_resid_layernorm_packed");
 }

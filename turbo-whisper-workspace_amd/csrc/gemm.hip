@@ -14,6 +14,9 @@
 // Skinny path (decoder, M <= 32 rows): one wave owns 16 output columns and a K-slice; the 4 waves of a
 // block split K and reduce through LDS; weights are streamed straight to VGPRs (each weight byte is
 // read exactly once per step) with v_mfma_f32_16x16x32_bf16.
+#include <algorithm>
+#include <type_traits>
+
 #include "tw_common.h"
 #include "../../include/tw_whisper.h"
 
@@ -164,10 +167,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(const bf16_t* __restrict__
 // random operands): 1 ~ 3 (641-1079 TF/s), 4 is 12-18% slower, a 4-stage BK=32 ring was 6% slower.
 static int tw_gemm_big_enabled = 1;
 static int tw_tune_skinny_nw = 0;  // 0 = heuristic; 4 / 8 / 16 force the skinny kernel's waves per block
+static int tw_tune_gemv_kw = 0;    // 0 = heuristic; 1 / 2 / 4 / 8 force the packed GEMV's K-slices per column group
 extern "C" int tw_gemm_set_variant(int big) {
   tw_gemm_big_enabled = big & 7;
   const int nw = (big >> 8) & 0xff;
   tw_tune_skinny_nw = (nw == 4 || nw == 8 || nw == 16) ? nw : 0;
+  const int kw = (big >> 16) & 0xff;
+  tw_tune_gemv_kw = (kw == 1 || kw == 2 || kw == 4 || kw == 8) ? kw : 0;
   return 0;
 }
 
@@ -236,6 +242,40 @@ __device__ inline void epi_store4(const EpiArgs& ea, int m, int n, int N, float4
     w.y = pack_bf16x2(v.z, v.w);
     *(uint2*)((bf16_t*)ea.out + idx) = w;
   }
+}
+
+// epilogue of 8 consecutive columns n..n+7 of row m (v already includes the bias): one 16-byte store for the bf16
+// outputs (a wave's epilogue is store-issue bound: half the instructions of two 8-byte stores)
+template <int EPI>
+__device__ inline void epi_store8(const EpiArgs& ea, int m, int n, int N, float4 v0, float4 v1) {
+  if constexpr (EPI == TW_EPI_BF16 || EPI == TW_EPI_GELU_BF16 || EPI == TW_EPI_CROSSKV) {
+    if (n + 7 < N) {
+      if constexpr (EPI == TW_EPI_GELU_BF16) {
+        v0.x = gelu_erf(v0.x); v0.y = gelu_erf(v0.y); v0.z = gelu_erf(v0.z); v0.w = gelu_erf(v0.w);
+        v1.x = gelu_erf(v1.x); v1.y = gelu_erf(v1.y); v1.z = gelu_erf(v1.z); v1.w = gelu_erf(v1.w);
+      }
+      uint4 w;
+      w.x = pack_bf16x2(v0.x, v0.y);
+      w.y = pack_bf16x2(v0.z, v0.w);
+      w.z = pack_bf16x2(v1.x, v1.y);
+      w.w = pack_bf16x2(v1.z, v1.w);
+      size_t idx;
+      if constexpr (EPI == TW_EPI_CROSSKV) {  // 8 | 64: the group stays inside one head's 64 contiguous dims
+        const int D = ea.kv_D, S = ea.kv_S;
+        int l = n / (2 * D), rem = n - l * 2 * D;
+        int kv = rem / D, hd = rem - kv * D;
+        int h = hd >> 6, d = hd & 63;
+        int b = m / S, s2 = m - b * S;
+        idx = ((((size_t)(l * 2 + kv) * ea.kv_B + b) * ea.kv_H + h) * S + s2) * 64 + d;
+      } else {
+        idx = (size_t)m * ea.ldo + n;
+      }
+      *(uint4*)((bf16_t*)ea.out + idx) = w;
+      return;
+    }
+  }
+  epi_store4<EPI>(ea, m, n, N, v0);
+  if (n + 4 < N) epi_store4<EPI>(ea, m, n + 4, N, v1);
 }
 
 template <int EPI>
@@ -494,6 +534,199 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ns(const bf16_t* __restrict__ A
 }
 
 // ------------------------------------------------------------------------------------------------
+// k_gemm_8p: 256 x 256 x 64 tiles, 8 waves in two ping-pong groups, 4 phases per K-tile
+// (cdna_hip_programming.md §5 "The 256² 8-phase template": the structure, not its code).
+// LDS holds two K-tiles, each as four 16 KiB half-tiles A0 | A1 | B0 | B1 (rows 0-127 / 128-255 of the A and W
+// tiles). Phase p of K-tile t computes one C-quadrant (A half, B half) = (0,0), (0,1), (1,1), (1,0): every wave
+// owns a 64 x 32 piece of each quadrant (rows 64*wr + 128*mh, cols 32*wc + 128*nh), i.e. 16 MFMAs per phase, and
+// re-reads only the operand half that changed. Each phase also stages one half-tile of K-tile t+1 (A0, B0, B1,
+// A1 — the order K-tile t+1 first needs them), so two phases of MFMAs cover every DMA. Waits are counted
+// (vmcnt never 0 inside the loop), barriers raw; waves 4-7 run one barrier behind waves 0-3, so on each SIMD
+// one wave's MFMA cluster (at raised priority) overlaps the other wave's ds_reads and DMA issue.
+//   RAW: a half-tile is waited for (vmcnt) before the first barrier of the phase before the one that reads it.
+//   WAR: a half-tile is restaged >= 2 phases after its last ds_read (A0 4, B0 2, B1 4, A1 4).
+// ------------------------------------------------------------------------------------------------
+template <int N>
+__device__ inline void p8_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                    int M, int N, int K, int lda, int ldw, EpiArgs ea) {
+  // K loop: 2 buffers x 4 half-tiles x 16 KiB = 128 KiB; epilogue: 8 x [64][68] f32 = 136 KiB (one array: a
+  // second __shared__ object makes hipcc drain vmcnt before every ds_read)
+  __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 64 * GB_EPI_LD * 2];
+  constexpr int HT = 128 * GB_BK;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntm = (M + GB_BM - 1) / GB_BM, ntn = (N + GB_BN - 1) / GB_BN;
+  const int nwg = ntm * ntn;
+  const int orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int tm = wgid / ntn, tn = wgid - tm * ntn;
+  const int m0 = tm * GB_BM, n0 = tn * GB_BN;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // DMA: half-tile h (0 A0, 1 A1, 2 B0, 3 B1), wave instruction i = 0,1 fills rows 8(2*wid+i) .. +7
+  const bf16_t* gsrc[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = 8 * (2 * wid + i) + (lane >> 3);
+      const int ch = (lane & 7) ^ gb_swz(row);
+      gsrc[h][i] = h < 2 ? A + (size_t)min(m0 + 128 * h + row, M - 1) * lda + ch * 8
+                         : W + (size_t)min(n0 + 128 * (h - 2) + row, N - 1) * ldw + ch * 8;
+    }
+  auto stage = [&](int buf, int h, int k0) {
+    bf16_t* dst = smem + (buf * 4 + h) * HT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(gsrc[h][i] + k0), (lds_void_t*)(dst + 8 * (2 * wid + i) * GB_BK),
+                                       16, 0, 0);
+  };
+
+  bf16x8 af[4][2], bfr[2][2];
+  auto readA = [&](int buf, int mh) {
+    const bf16_t* As = smem + (buf * 4 + mh) * HT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int row = 64 * wr + 16 * i + fr, kc = 4 * kk + fq;
+        af[i][kk] = *(const bf16x8*)(As + row * GB_BK + ((kc ^ gb_swz(row)) << 3));
+      }
+  };
+  auto readB = [&](int buf, int nh) {
+    const bf16_t* Bs = smem + (buf * 4 + 2 + nh) * HT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int row = 32 * wc + 16 * j + fr, kc = 4 * kk + fq;
+        bfr[j][kk] = *(const bf16x8*)(Bs + row * GB_BK + ((kc ^ gb_swz(row)) << 3));
+      }
+  };
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto mfma_q = [&](auto MH, auto NH) {
+    constexpr int mh = decltype(MH)::value, nh = decltype(NH)::value;
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mh][nh][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bfr[j][kk], acc[mh][nh][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+
+  const int nk = K / GB_BK;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage(0, h, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // ping-pong: group 1 one barrier behind
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1, nb = buf ^ 1, kn = (t + 1) * GB_BK;
+    const bool nxt = t + 1 < nk;
+    // phase 1: quadrant (A0, B0)
+    readB(buf, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    readA(buf, 0);
+    if (nxt) {
+      stage(nb, 0, kn);
+      p8_vmcnt<4>();  // B1 of tile t (staged in phase 3 of t-1)
+    } else {
+      p8_vmcnt<2>();
+    }
+    mfma_q(I0{}, I0{});
+    // phase 2: (A0, B1)
+    readB(buf, 1);
+    if (nxt) {
+      stage(nb, 2, kn);
+      p8_vmcnt<4>();  // A1 of tile t (phase 4 of t-1)
+    } else {
+      p8_vmcnt<0>();
+    }
+    mfma_q(I0{}, I1{});
+    // phase 3: (A1, B1)
+    readA(buf, 1);
+    if (nxt) stage(nb, 3, kn);
+    mfma_q(I1{}, I1{});
+    // phase 4: (A1, B0)
+    readB(buf, 0);
+    if (nxt) {
+      stage(nb, 1, kn);
+      p8_vmcnt<4>();  // A0, B0 of tile t+1 (phases 1, 2 of t)
+    }
+    mfma_q(I1{}, I0{});
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // realign the groups
+  __syncthreads();
+
+  // epilogue through LDS: per wave two 64-row halves (mh) of [64][64] f32 (cols = its two 32-col chunks), read
+  // back 8 consecutive columns per lane (8 lanes per row) for 16-byte global stores
+  const int rc = (lane & 7) * 8;
+  const int ncol = n0 + (rc < 32 ? 32 * wc + rc : 128 + 32 * wc + rc - 32);
+  float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+  if (ea.bias) {
+    b0.x = ea.bias[min(ncol, N - 1)];
+    b0.y = ea.bias[min(ncol + 1, N - 1)];
+    b0.z = ea.bias[min(ncol + 2, N - 1)];
+    b0.w = ea.bias[min(ncol + 3, N - 1)];
+    b1.x = ea.bias[min(ncol + 4, N - 1)];
+    b1.y = ea.bias[min(ncol + 5, N - 1)];
+    b1.z = ea.bias[min(ncol + 6, N - 1)];
+    b1.w = ea.bias[min(ncol + 7, N - 1)];
+  }
+  float* wimg = (float*)smem + wid * (64 * GB_EPI_LD);
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh) {
+    if (mh) __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            wimg[(i * 16 + fq * 4 + r) * GB_EPI_LD + nh * 32 + j * 16 + fr] = acc[mh][nh][i][j][r];
+    __syncthreads();
+    const int mrow0 = m0 + 128 * mh + 64 * wr;
+#pragma unroll 4
+    for (int rr = 0; rr < 8; ++rr) {
+      const int lr = rr * 8 + (lane >> 3);
+      const int m = mrow0 + lr;
+      float4 v0 = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
+      float4 v1 = *(const float4*)(wimg + lr * GB_EPI_LD + rc + 4);
+      v0.x += b0.x; v0.y += b0.y; v0.z += b0.z; v0.w += b0.w;
+      v1.x += b1.x; v1.y += b1.y; v1.z += b1.z; v1.w += b1.w;
+      if (m < M && ncol < N) epi_store8<EPI>(ea, m, ncol, N, v0, v1);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Skinny kernel (M <= 32): weight-streaming MFMA GEMV for the decoder step
 // ------------------------------------------------------------------------------------------------
 // Block = NW waves = 16 output columns; the K range is cut into NW * gridDim.y slices of 32-deep
@@ -510,6 +743,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ns(const bf16_t* __restrict__ A
 template <int EPI, int NW, bool TWO>
 __global__ __launch_bounds__(NW * 64) void k_gemm_skinny(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                          int M, int N, int K, int lda, int ldw, EpiArgs ea) {
+  TW_DEC_PRIO();
   __shared__ float red[NW][32][17];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int n0 = blockIdx.x * 16;
@@ -597,13 +831,149 @@ static void launch_skinny(const bf16_t* A, const bf16_t* W, int M, int N, int K,
   else launch_skinny_nw<EPI, 16>(A, W, M, N, K, lda, ldw, ea, splits, s);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Packed decoder GEMV (M <= 32): weights pre-arranged in MFMA fragment order (tw_pack_weight), activations either
+// in the packed activation layout (written by tw_resid_layernorm_packed / the GELU_PACKED epilogue) or row-major.
+// Every wave-load is one contiguous 1 KiB fragment (weights: the whole read is one HBM stream per wave), instead
+// of 16 rows x 64 B. Block = 4 (or KW = 8: 8) waves = GPB column groups x KW K-slices; gridDim.y = split-K over
+// blocks for the PARTIAL epilogue (partials summed by the consumer, tw_resid_layernorm*).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pack_weight(const bf16_t* __restrict__ W, int N, int K, int ldw,
+                                                     bf16_t* __restrict__ Wp, long nchunks) {
+  const long c = (long)blockIdx.x * 256 + threadIdx.x;
+  if (c >= nchunks) return;
+  const int lane = (int)(c & 63);
+  const long rest = c >> 6;
+  const int ns = K >> 5;
+  const int st = (int)(rest % ns), g = (int)(rest / ns);
+  const int n = g * 16 + (lane & 15), k = st * 32 + 8 * (lane >> 4);
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (n < N) v = *(const uint4*)(W + (size_t)n * ldw + k);
+  *(uint4*)(Wp + c * 8) = v;
+}
+
+template <int EPI, int KW, int U, bool APACK, bool TWO>
+__global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __restrict__ A, int lda,
+                                                               const bf16_t* __restrict__ Wp, int M, int N, int K,
+                                                               EpiArgs ea) {
+  TW_DEC_PRIO();
+  constexpr int NW = KW > 4 ? KW : 4, GPB = NW / KW;
+  __shared__ float red[NW][32][17];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int gl = wid / KW, kw = wid - gl * KW;
+  const int g = blockIdx.x * GPB + gl;
+  const int ngroups = (N + 15) >> 4, ns = K >> 5;
+  const int nsl = KW * gridDim.y, sl = blockIdx.y * KW + kw;
+  const int s0 = (int)((long)sl * ns / nsl), s1 = (int)((long)(sl + 1) * ns / nsl);
+  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+  if (g < ngroups) {
+    const bf16_t* wp = Wp + (size_t)g * ns * 512 + lane * 8;
+    const bf16_t* ap;
+    const bf16_t* ap1 = nullptr;
+    if constexpr (APACK) {
+      ap = A + lane * 8;  // step s, m-tile t at + s*1024 + t*512
+    } else {
+      ap = A + (size_t)min(lane & 15, M - 1) * lda + 8 * (lane >> 4);
+      ap1 = A + (size_t)min(16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4);
+    }
+    auto ldA0 = [&](int st) -> bf16x8 {
+      return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024) : *(const bf16x8*)(ap + 32 * st);
+    };
+    auto ldA1 = [&](int st) -> bf16x8 {
+      return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024 + 512) : *(const bf16x8*)(ap1 + 32 * st);
+    };
+    int st = s0;
+    for (; st + U <= s1; st += U) {
+      bf16x8 bw[U], a0[U], a1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        bw[u] = *(const bf16x8*)(wp + (size_t)(st + u) * 512);
+        a0[u] = ldA0(st + u);
+        if (TWO) a1[u] = ldA1(st + u);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], bw[u], c0, 0, 0, 0);
+        if (TWO) c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], bw[u], c1, 0, 0, 0);
+      }
+    }
+    for (; st < s1; ++st) {
+      const bf16x8 bw = *(const bf16x8*)(wp + (size_t)st * 512);
+      c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ldA0(st), bw, c0, 0, 0, 0);
+      if (TWO) c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ldA1(st), bw, c1, 0, 0, 0);
+    }
+  }
+  const int cc = lane & 15, rb = (lane >> 4) * 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[wid][rb + r][cc] = c0[r];
+    if (TWO) red[wid][16 + rb + r][cc] = c1[r];
+  }
+  __syncthreads();
+  constexpr int ROWS = TWO ? 32 : 16;
+  for (int e = tid; e < GPB * ROWS * 16; e += NW * 64) {
+    const int gg = e / (ROWS * 16), rem = e - gg * ROWS * 16;
+    const int m = rem >> 4, c = rem & 15;
+    const int n = (blockIdx.x * GPB + gg) * 16 + c;
+    if (m < M && n < N) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < KW; ++w) v += red[gg * KW + w][m][c];
+      if constexpr (EPI == TW_EPI_PARTIAL) {
+        ((float*)ea.out)[((size_t)blockIdx.y * M + m) * ea.ldo + n] = v;
+      } else if constexpr (EPI == TW_EPI_GELU_PACKED) {
+        if (ea.bias) v += ea.bias[n];
+        ((bf16_t*)ea.out)[tw_pack_act_idx(m, n)] = f32_to_bf16(gelu_erf(v));
+      } else {
+        epi_store<EPI>(ea, m, n, v);
+      }
+    }
+  }
+}
+
+template <int EPI, int KW, int U, bool APACK>
+static void launch_gemv_p3(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea, int splits,
+                           hipStream_t s) {
+  constexpr int NW = KW > 4 ? KW : 4, GPB = NW / KW;
+  dim3 grid(tw_cdiv(tw_cdiv(N, 16), GPB), splits);
+  if (M > 16)
+    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, true>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea);
+  else
+    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, false>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea);
+}
+
+template <int EPI, bool APACK>
+static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea, int splits,
+                           hipStream_t s) {
+  // K-slices per column group: enough waves to put ~4 on every CU while each keeps >= 4 steps
+  const long groups = tw_cdiv(N, 16) * (long)splits;
+  const int steps = K / 32 / splits;
+  int kw = 1;
+  while (groups * kw < 1024 && kw < 8 && steps >= 8 * kw) kw *= 2;
+  if (tw_tune_gemv_kw) kw = tw_tune_gemv_kw;
+  if (kw == 1) launch_gemv_p3<EPI, 1, 16, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
+  else if (kw == 2) launch_gemv_p3<EPI, 2, 8, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
+  else if (kw == 4) launch_gemv_p3<EPI, 4, 8, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
+  else launch_gemv_p3<EPI, 8, 8, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
+}
+
+template <int EPI>
+static void launch_gemv_p(const bf16_t* A, int a_packed, int lda, const bf16_t* Wp, int M, int N, int K,
+                          const EpiArgs& ea, int splits, hipStream_t s) {
+  if (a_packed) launch_gemv_p2<EPI, true>(A, lda, Wp, M, N, K, ea, splits, s);
+  else launch_gemv_p2<EPI, false>(A, lda, Wp, M, N, K, ea, splits, s);
+}
+
 template <int EPI>
 static int launch_gemm(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int ldw, const EpiArgs& ea,
                        hipStream_t s) {
   if (M <= 32) {
     launch_skinny<EPI>(A, W, M, N, K, lda, ldw, ea, 1, s);
   } else {
-    if (tw_gemm_big_enabled >= 3) {
+    if (tw_gemm_big_enabled == 5) {
+      unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
+      hipLaunchKernelGGL(k_gemm_8p<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
+    } else if (tw_gemm_big_enabled >= 3) {
       const int v = tw_gemm_big_enabled;
       if (v == 3) {  // 256x256, 2 stages, counted-vmcnt loop, setprio
         unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, 256);
@@ -660,4 +1030,40 @@ extern "C" int tw_gemm_bf16_partial(const bf16_t* A, const bf16_t* W, int M, int
   EpiArgs ea{part, ldp, nullptr, nullptr, 0, 0, 0, 0, 0};
   launch_skinny<TW_EPI_PARTIAL>(A, W, M, N, K, lda, ldw, ea, splits, (hipStream_t)stream);
   return tw_check_launch("tw_gemm_bf16_partial");
+}
+
+extern "C" int tw_pack_weight(const bf16_t* W, int N, int K, int ldw, bf16_t* Wp, void* stream) {
+  TW_REQUIRE(W && Wp && N > 0 && K > 0 && K % 32 == 0 && ldw >= K && ldw % 8 == 0,
+             "tw_pack_weight: N=%d K=%d ldw=%d (K %% 32, ldw %% 8)", N, K, ldw);
+  const long nchunks = (long)tw_cdiv(N, 16) * (K / 32) * 64;
+  hipLaunchKernelGGL(k_pack_weight, dim3(tw_cdiv(nchunks, 256)), dim3(256), 0, (hipStream_t)stream, W, N, K, ldw, Wp,
+                     nchunks);
+  return tw_check_launch("tw_pack_weight");
+}
+
+extern "C" int tw_gemv_packed(const bf16_t* A, int a_packed, int lda, const bf16_t* Wp, int M, int N, int K, int epi,
+                              void* out, int ldo, const float* bias, int splits, void* stream) {
+  TW_REQUIRE(A && Wp && out, "tw_gemv_packed: null pointer");
+  TW_REQUIRE(M > 0 && M <= 32 && N > 0 && K > 0 && K % 32 == 0, "tw_gemv_packed: M=%d N=%d K=%d (M <= 32, K %% 32)", M,
+             N, K);
+  TW_REQUIRE(a_packed || (lda >= K && lda % 8 == 0), "tw_gemv_packed: lda=%d", lda);
+  TW_REQUIRE(splits >= 1 && splits <= 16 && splits <= K / 32, "tw_gemv_packed: splits=%d", splits);
+  TW_REQUIRE(splits == 1 || epi == TW_EPI_PARTIAL_F32, "tw_gemv_packed: split-K needs the PARTIAL epilogue");
+  EpiArgs ea{out, ldo, bias, nullptr, 0, 0, 0, 0, 0};
+  hipStream_t s = (hipStream_t)stream;
+  switch (epi) {
+    case TW_EPI_BF16: launch_gemv_p<TW_EPI_BF16>(A, a_packed, lda, Wp, M, N, K, ea, splits, s); break;
+    case TW_EPI_F32: launch_gemv_p<TW_EPI_F32>(A, a_packed, lda, Wp, M, N, K, ea, splits, s); break;
+    case TW_EPI_GELU_PACKED:
+      TW_REQUIRE(N % 32 == 0, "tw_gemv_packed: GELU_PACKED needs N %% 32 (it is the next GEMV's K)");
+      launch_gemv_p<TW_EPI_GELU_PACKED>(A, a_packed, lda, Wp, M, N, K, ea, splits, s);
+      break;
+    case TW_EPI_PARTIAL_F32:
+      TW_REQUIRE(ldo >= N, "tw_gemv_packed: ldo=%d < N", ldo);
+      ea.bias = nullptr;
+      launch_gemv_p<TW_EPI_PARTIAL>(A, a_packed, lda, Wp, M, N, K, ea, splits, s);
+      break;
+    default: tw_set_error("tw_gemv_packed: unsupported epilogue %d", epi); return TW_ERR_ARG;
+  }
+  return tw_check_launch("tw_gemv_packed");
 }

@@ -69,6 +69,27 @@ __device__ inline float f32_from_order_key(uint32_t k) {
   return __uint_as_float(u);
 }
 
+// Decoder kernels raise their waves' issue priority so that, sharing CUs with the encoder GEMM of the next
+// window batch, their (latency-bound) instructions are picked first. Compile-time knob for A/B builds.
+#ifndef TW_DEC_PRIORITY
+#define TW_DEC_PRIORITY 3
+#endif
+#define TW_DEC_PRIO()                                        \
+  do {                                                       \
+    if (TW_DEC_PRIORITY) __builtin_amdgcn_s_setprio(TW_DEC_PRIORITY); \
+  } while (0)
+
+// Decoder fragment layouts (include/tw_whisper.h "packed" formats), M <= 32 activation rows:
+//   activation [K/32][2][64][8] bf16: element (m, k) at ((k/32 * 2 + m/16) * 64 + (m%16) + 16*((k/8)%4)) * 8 + k%8,
+//     i.e. step s = k/32, m-tile t = m/16 is the 16x32 A fragment of v_mfma_f32_16x16x32_bf16 (1 KiB contiguous)
+//   weight     [N/16][K/32][64][8] bf16: element (n, k) at ((n/16 * K/32 + k/32) * 64 + (n%16) + 16*((k/8)%4)) * 8 + k%8
+__host__ __device__ inline size_t tw_pack_act_idx(int m, int k) {
+  return ((size_t)((k >> 5) * 2 + (m >> 4)) * 64 + (m & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
+}
+__host__ __device__ inline size_t tw_pack_w_idx(int n, int k, int K) {
+  return ((size_t)((n >> 4) * (K >> 5) + (k >> 5)) * 64 + (n & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
+}
+
 // ---- error plumbing -------------------------------------------------------------------------------
 enum {
   TW_OK = 0,

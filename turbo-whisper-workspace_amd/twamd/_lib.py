@@ -12,7 +12,8 @@ import os
 
 import torch  # noqa: F401  (load torch's HIP runtime before ours)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtwhip.so")
+# TW_LIB selects another in-tree build of the same sources (A/B builds with different compile-time options)
+LIB_PATH = os.environ.get("TW_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtwhip.so")
 
 TW_EPI_BF16 = 0
 TW_EPI_GELU_BF16 = 1
@@ -20,6 +21,8 @@ TW_EPI_RESID_F32 = 2
 TW_EPI_GELU_POS_F32 = 3
 TW_EPI_F32 = 4
 TW_EPI_CROSSKV = 5
+TW_EPI_GELU_PACKED = 6
+TW_EPI_PARTIAL_F32 = 100
 
 TW_SELECT_CHUNKS = 16
 TW_SELECT_WS_PER_ROW = 128
@@ -32,7 +35,7 @@ EXPORTED = (
     "tw_im2col_conv2", "tw_gemm_bf16", "tw_layernorm", "tw_attn_encoder", "tw_attn_decode_self",
     "tw_attn_decode_cross", "tw_embed_decoder", "tw_logits_select", "tw_gemm_bf16_partial", "tw_resid_layernorm",
     "tw_gemm_set_variant", "tw_attn_set_variant",
-    "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
+    "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_stream_create_masked", "tw_stream_destroy", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
 )
 
 
@@ -83,6 +86,11 @@ _SIGS = {
     "tw_gemm_set_variant": ([_I], _I),
     "tw_attn_set_variant": ([_I], _I),
     "tw_resid_layernorm": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
+    "tw_pack_weight": ([_P, _I, _I, _I, _P, _P], _I),
+    "tw_gemv_packed": ([_P, _I, _I, _P, _I, _I, _I, _I, _P, _I, _P, _I, _P], _I),
+    "tw_resid_layernorm_packed": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
+    "tw_stream_create_masked": ([_P, _I, ctypes.POINTER(ctypes.c_void_p)], _I),
+    "tw_stream_destroy": ([_P], _I),
     "tw_flac_probe": ([_P, ctypes.c_int64, ctypes.POINTER(TwFlacInfo)], _I),
     "tw_flac_decode": ([_P, ctypes.c_int64, _P, ctypes.c_int64, _I, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_resample_pcm_i32": ([_P, ctypes.c_int64, _I, _F, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes
 import dataclasses
+import os
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -75,6 +76,8 @@ class DecView:
     tokens: torch.Tensor
     ids: torch.Tensor
     pos: torch.Tensor
+    hp: Optional[torch.Tensor] = None  # packed-activation LayerNorm output (tw_gemv_packed A operand), <= 32 rows
+    fp: Optional[torch.Tensor] = None  # packed-activation fc1 output (fc2's A operand)
 
 
 @dataclasses.dataclass
@@ -85,8 +88,13 @@ class PassResult:
 
 class WhisperEngine:
     def __init__(self, weights: PackedWeights, gen: GenerationSettings, max_batch: int = 24,
-                 device: str = "cuda", use_graphs: bool = True):
+                 device: str = "cuda", use_graphs: bool = True, dec_cus: Optional[int] = None):
         _lib.load()
+        # kernel-variant overrides for A/B measurement (defaults are the measured-best kernels)
+        if os.environ.get("TW_GEMM_VARIANT"):
+            _lib.call("tw_gemm_set_variant", int(os.environ["TW_GEMM_VARIANT"], 0))
+        if os.environ.get("TW_ATTN_VARIANT"):
+            _lib.call("tw_attn_set_variant", int(os.environ["TW_ATTN_VARIANT"], 0))
         d = weights.dims
         d.validate()
         self.d, self.w, self.gen = d, weights, gen
@@ -96,8 +104,16 @@ class WhisperEngine:
         # a high-priority decoder stream and a default-priority stream for the front end + encoder: the
         # MFMA-bound encoder of the next window batch fills the CUs the latency-bound decode of this one leaves idle,
         # and the dispatcher serves the decoder's small grids first
-        self.stream = torch.cuda.Stream(self.device, priority=-1)
-        self.enc_stream = torch.cuda.Stream(self.device, priority=0)
+        # dec_cus > 0 partitions the chip instead: the decoder streams own dec_cus CUs of every XCD, the encoder
+        # stream the rest (hipExtStreamCreateWithCUMask; see tw_stream_create_masked)
+        self.dec_cus = int(os.environ.get("TW_DEC_CUS", "0")) if dec_cus is None else int(dec_cus)
+        self._masked: List[int] = []
+        if self.dec_cus > 0:
+            self.stream = self._masked_stream(range(0, 8 * self.dec_cus))
+            self.enc_stream = self._masked_stream(range(8 * self.dec_cus, self._n_cus()))
+        else:
+            self.stream = torch.cuda.Stream(self.device, priority=-1)
+            self.enc_stream = torch.cuda.Stream(self.device, priority=0)
         self._enc_ev = [torch.cuda.Event(), torch.cuda.Event()]
         D, F, H, V, B = d.d_model, d.ffn, d.heads, d.vocab, max_batch
         dev, bf, f32, i32 = self.device, torch.bfloat16, torch.float32, torch.int32
@@ -148,10 +164,56 @@ class WhisperEngine:
         # concurrent decode chains in the generation loop (measured: two 12-row chains on two streams run no faster
         # than one 24-row chain on MI355X, so one by default)
         self.n_chains = 1
-        self._chain_streams = [torch.cuda.Stream(self.device, priority=-1) for _ in range(self.n_chains)]
+        self._chain_streams = [self._masked_stream(range(0, 8 * self.dec_cus)) if self.dec_cus > 0 else
+                               torch.cuda.Stream(self.device, priority=-1) for _ in range(self.n_chains)]
         self._own_streams = {x.cuda_stream for x in [self.stream, self.enc_stream] + self._chain_streams}
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self._chain_cache: Dict[tuple, List[DecView]] = {}
+        # decoder projections in the packed fragment layout (tw_pack_weight; +~342 MB at large-v3-turbo): every
+        # wave-load of the per-token GEMVs is one contiguous 1 KiB fragment. TW_DEC_PACKED=0 keeps the row-major
+        # skinny GEMM path (A/B measurement).
+        self.packed_decoder = os.environ.get("TW_DEC_PACKED", "1") != "0"
+        self.dec_p: List[Dict[str, torch.Tensor]] = []
+        self.emb_p: Optional[torch.Tensor] = None
+        if self.packed_decoder:
+            with torch.cuda.device(self.device):
+                self.dec_p = [{k: self._pack(getattr(L, k)) for k in ("wqkv", "wo", "wq_x", "wo_x", "w1", "w2")}
+                              for L in weights.dec]
+                self.emb_p = self._pack(weights.emb)
+                torch.cuda.synchronize(self.device)
+
+    def _pack(self, W: torch.Tensor) -> torch.Tensor:
+        N, K = W.shape
+        Wp = torch.empty((N + 15) // 16 * 16 * K, dtype=torch.bfloat16, device=self.device)
+        _lib.call("tw_pack_weight", W.data_ptr(), N, K, K, Wp.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        return Wp
+
+    def _gemv(self, A, a_packed: bool, Wp, M, N, K, epi, out, v: DecView, bias=None, splits=1, ldo=None):
+        rec = self._begin_timer(("gemv_packed", epi), 2.0 * M * N * K, v.stream)
+        _lib.call("tw_gemv_packed", A.data_ptr(), int(a_packed), K, Wp.data_ptr(), M, N, K, epi, out.data_ptr(),
+                  ldo if ldo is not None else N, _lib.ptr(bias), splits, v.stream.cuda_stream)
+        self._end_timer(rec, v.stream)
+
+    def _resid_ln_p(self, R, nparts, bias, g, b, v: DecView):
+        """xd += bias + sum(parts[:nparts]); hp = LayerNorm(xd) as a packed activation."""
+        _lib.call("tw_resid_layernorm_packed", v.xd.data_ptr(), v.parts.data_ptr() if nparts else None, nparts,
+                  _lib.ptr(bias), _lib.ptr(g), _lib.ptr(b), R, self.d.d_model, LN_EPS, v.hp.data_ptr(),
+                  v.stream.cuda_stream)
+
+    def _n_cus(self) -> int:
+        return torch.cuda.get_device_properties(self.device).multi_processor_count
+
+    def _masked_stream(self, bits) -> torch.cuda.ExternalStream:
+        """A stream confined to the CUs of `bits` (bit i = CU i//8 of XCD i%8 on MI355X)."""
+        n = self._n_cus()
+        mask = (ctypes.c_uint32 * ((n + 31) // 32))()
+        for b in bits:
+            mask[b // 32] |= 1 << (b % 32)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.call("tw_stream_create_masked", mask, len(mask), ctypes.byref(h))
+        self._masked.append(h.value)
+        return torch.cuda.ExternalStream(h.value, device=self.device)
 
     def set_suppress_tokens(self, tokens: Sequence[int]) -> None:
         """SuppressTokensLogitsProcessor's list as a device bitmask (in place: captured graphs stay valid)."""
@@ -225,11 +287,20 @@ class WhisperEngine:
 
     def _view(self, r0: int = 0, n: Optional[int] = None, stream=None, parts=None) -> DecView:
         n = self.max_batch - r0 if n is None else n
+        if stream is None and parts is None:  # the default views are cached: graphs capture their buffers
+            key = ("view", r0, n)
+            if key not in self._chain_cache:
+                self._chain_cache[key] = self._view(r0, n, self.stream, self.parts)
+            return self._chain_cache[key]
         sl = slice(r0, r0 + n)
+        hp = fp = None
+        if self.packed_decoder and n <= 32:  # per-view packed scratch (rows 0..n-1 of the view; pad rows zero)
+            hp = torch.zeros(32 * self.d.d_model, dtype=torch.bfloat16, device=self.device)
+            fp = torch.zeros(32 * self.d.ffn, dtype=torch.bfloat16, device=self.device)
         return DecView(r0, n, stream or self.stream, self.xd[sl], self.hd[sl], self.qkvd[sl], self.qd[sl],
                        self.attd[sl], self.ffnd[sl], self.logits[sl],
                        self.parts if parts is None else parts, self.sel_ws[sl], self.state[sl], self.tokens[sl],
-                       self.ids[sl], self.pos[sl])
+                       self.ids[sl], self.pos[sl], hp, fp)
 
     def use_slot(self, slot: int) -> None:
         """Point the decoder at the cross-K/V (and feature) buffers of pipeline slot `slot`."""
@@ -310,11 +381,18 @@ class WhisperEngine:
         Residual stream xd stays f32; every d_model-wide projection (self/cross out_proj, fc2) is a split-K
         partial product whose sum, bias and residual add are folded into the next LayerNorm launch."""
         d, w = self.d, self.w
+        if v is None and self.packed_decoder and R > 32:  # the packed layout holds 32 rows: one pass per 32
+            r_enc = R if r_enc is None else r_enc
+            for r0 in range(0, R, 32):
+                self.decoder_step(min(32, R - r0), with_logits, self._view(r0, min(32, R - r0)), r_enc)
+            return
         v = v or self._view()
         r_enc = R if r_enc is None else r_enc
         D, F, H, T = d.d_model, d.ffn, d.heads, d.max_target_positions
         st = v.stream
         s = st.cuda_stream
+        if v.hp is not None:
+            return self._decoder_step_packed(R, with_logits, v, r_enc)
         _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), v.ids.data_ptr(), v.pos.data_ptr(), R, D,
                   v.xd.data_ptr(), s)
         xkv_stride = 2 * r_enc * H * S_ENC * 64
@@ -340,6 +418,40 @@ class WhisperEngine:
         if with_logits:
             self._resid_ln(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
             self._gemm(v.hd, w.emb, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, stream=st)
+
+    def _decoder_step_packed(self, R: int, with_logits: bool, v: DecView, r_enc: int) -> None:
+        """decoder_step on the packed-GEMV path: LayerNorm outputs and fc1's GELU output are packed activations,
+        attention outputs stay row-major, the d_model-wide projections are split-K partials (as decoder_step)."""
+        d, w = self.d, self.w
+        D, F, H, T = d.d_model, d.ffn, d.heads, d.max_target_positions
+        st = v.stream
+        s = st.cuda_stream
+        _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), v.ids.data_ptr(), v.pos.data_ptr(), R, D,
+                  v.xd.data_ptr(), s)
+        xkv_stride = 2 * r_enc * H * S_ENC * 64
+        nparts, pbias = 0, None
+        PART, K4 = _lib.TW_EPI_PARTIAL_F32, DEC_SPLITS
+        for li, L in enumerate(w.dec):
+            P = self.dec_p[li]
+            self._resid_ln_p(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
+            self._gemv(v.hp, True, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
+            _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
+                      self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
+            self._gemv(v.attd, False, P["wo"], R, D, D, PART, v.parts, v, splits=K4)
+            self._resid_ln_p(R, K4, L.bo, L.ln2_g, L.ln2_b, v)
+            self._gemv(v.hp, True, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
+            ckv = self.cross_kv.data_ptr() + (li * xkv_stride + v.r0 * H * S_ENC * 64) * 2
+            rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
+            _lib.call("tw_attn_decode_cross", v.qd.data_ptr(), R, H, S_ENC, r_enc, None, ckv, v.attd.data_ptr(), s)
+            self._end_timer(rec, st)
+            self._gemv(v.attd, False, P["wo_x"], R, D, D, PART, v.parts, v, splits=K4)
+            self._resid_ln_p(R, K4, L.bo_x, L.ln3_g, L.ln3_b, v)
+            self._gemv(v.hp, True, P["w1"], R, F, D, _lib.TW_EPI_GELU_PACKED, v.fp, v, bias=L.b1)
+            self._gemv(v.fp, True, P["w2"], R, D, F, PART, v.parts, v, splits=K4)
+            nparts, pbias = K4, L.b2
+        if with_logits:
+            self._resid_ln_p(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
+            self._gemv(v.hp, True, self.emb_p, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, v)
 
     def _select_params(self, mode: int, max_new: int, use_timestamps: bool = True) -> _lib.TwSelectParams:
         st, g = self.gen.special, self.gen
@@ -429,6 +541,10 @@ class WhisperEngine:
         key = ("chains", R)
         if key not in self._chain_cache:
             k = max(1, min(self.n_chains, R // 4))
+            if self.packed_decoder:
+                k = max(k, (R + 31) // 32)
+                while len(self._chain_streams) < k:
+                    self._chain_streams.append(self._chain_streams[0])  # one stream: the chains run in turn
             views = []
             for i in range(k):
                 r0, r1 = i * R // k, (i + 1) * R // k
