@@ -645,14 +645,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // ping-pong: group 1 one barrier behind
-  for (int t = 0; t < nk; ++t) {
+  // one K-tile = 4 phases; NXT: stage K-tile t+1 (compile-time, so the steady-state loop has no branches)
+  auto ktile = [&](int t, auto NXT) {
+    constexpr bool nxt = decltype(NXT)::value;
     const int buf = t & 1, nb = buf ^ 1, kn = (t + 1) * GB_BK;
-    const bool nxt = t + 1 < nk;
     // phase 1: quadrant (A0, B0)
     readB(buf, 0);
     __builtin_amdgcn_sched_barrier(0);
     readA(buf, 0);
-    if (nxt) {
+    if constexpr (nxt) {
       stage(nb, 0, kn);
       p8_vmcnt<4>();  // B1 of tile t (staged in phase 3 of t-1)
     } else {
@@ -661,7 +662,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
     mfma_q(I0{}, I0{});
     // phase 2: (A0, B1)
     readB(buf, 1);
-    if (nxt) {
+    if constexpr (nxt) {
       stage(nb, 2, kn);
       p8_vmcnt<4>();  // A1 of tile t (phase 4 of t-1)
     } else {
@@ -670,16 +671,20 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
     mfma_q(I0{}, I1{});
     // phase 3: (A1, B1)
     readA(buf, 1);
-    if (nxt) stage(nb, 3, kn);
+    if constexpr (nxt) stage(nb, 3, kn);
     mfma_q(I1{}, I1{});
     // phase 4: (A1, B0)
     readB(buf, 0);
-    if (nxt) {
+    if constexpr (nxt) {
       stage(nb, 1, kn);
       p8_vmcnt<4>();  // A0, B0 of tile t+1 (phases 1, 2 of t)
     }
     mfma_q(I1{}, I0{});
-  }
+  };
+  using BT = std::integral_constant<bool, true>;
+  using BF = std::integral_constant<bool, false>;
+  for (int t = 0; t + 1 < nk; ++t) ktile(t, BT{});
+  ktile(nk - 1, BF{});
   if (wr == 0) __builtin_amdgcn_s_barrier();  // realign the groups
   __syncthreads();
 
@@ -724,6 +729,210 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
       if (m < M && ncol < N) epi_store8<EPI>(ea, m, ncol, N, v0, v1);
     }
   }
+}
+
+// k_gemm_8pp: k_gemm_8p made persistent — one block per CU loops over tiles (virtual ids b, b + G, ...; G % 8 == 0
+// keeps a block on one XCD's share of the bijective remap). The whole grid is resident after one dispatch round,
+// so the command processor is free to dispatch other queues' kernels (the decoder step beside the encoder) instead
+// of feeding this kernel's thousands of workgroups. The next tile's K-tile 0 lands in buffer 0 during the epilogue;
+// the epilogue images move to [64 KiB, 132 KiB) and run in four 32-row passes.
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm_8pp(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                     int M, int N, int K, int lda, int ldw, EpiArgs ea) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 64 * GB_EPI_LD * 2];
+  constexpr int HT = 128 * GB_BK;
+  constexpr int EPI_BASE = 64 * 1024 / 4;  // f32 offset of the epilogue images
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntm = (M + GB_BM - 1) / GB_BM, ntn = (N + GB_BN - 1) / GB_BN;
+  const int nwg = ntm * ntn;
+  const int q8 = nwg / 8, r8 = nwg % 8;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  auto tile_origin = [&](int vid, int& m0, int& n0) {
+    const int xcd = vid % 8;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + vid / 8;
+    const int tm = wgid / ntn;
+    m0 = tm * GB_BM;
+    n0 = (wgid - tm * ntn) * GB_BN;
+  };
+  const bf16_t* gsrc[4][2];
+  auto set_src = [&](int m0, int n0) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = 8 * (2 * wid + i) + (lane >> 3);
+        const int ch = (lane & 7) ^ gb_swz(row);
+        gsrc[h][i] = h < 2 ? A + (size_t)min(m0 + 128 * h + row, M - 1) * lda + ch * 8
+                           : W + (size_t)min(n0 + 128 * (h - 2) + row, N - 1) * ldw + ch * 8;
+      }
+  };
+  auto stage = [&](int buf, int h, int k0) {
+    bf16_t* dst = smem + (buf * 4 + h) * HT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(gsrc[h][i] + k0), (lds_void_t*)(dst + 8 * (2 * wid + i) * GB_BK),
+                                       16, 0, 0);
+  };
+  bf16x8 af[4][2], bfr[2][2];
+  auto readA = [&](int buf, int mh) {
+    const bf16_t* As = smem + (buf * 4 + mh) * HT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int row = 64 * wr + 16 * i + fr, kc = 4 * kk + fq;
+        af[i][kk] = *(const bf16x8*)(As + row * GB_BK + ((kc ^ gb_swz(row)) << 3));
+      }
+  };
+  auto readB = [&](int buf, int nh) {
+    const bf16_t* Bs = smem + (buf * 4 + 2 + nh) * HT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int row = 32 * wc + 16 * j + fr, kc = 4 * kk + fq;
+        bfr[j][kk] = *(const bf16x8*)(Bs + row * GB_BK + ((kc ^ gb_swz(row)) << 3));
+      }
+  };
+  f32x4 acc[2][2][4][2];
+  auto mfma_q = [&](auto MH, auto NH) {
+    constexpr int mh = decltype(MH)::value, nh = decltype(NH)::value;
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mh][nh][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bfr[j][kk], acc[mh][nh][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  auto ktile = [&](int t, auto NXT) {
+    constexpr bool nxt = decltype(NXT)::value;
+    const int buf = t & 1, nb = buf ^ 1, kn = (t + 1) * GB_BK;
+    readB(buf, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    readA(buf, 0);
+    if constexpr (nxt) {
+      stage(nb, 0, kn);
+      p8_vmcnt<4>();
+    } else {
+      p8_vmcnt<2>();
+    }
+    mfma_q(I0{}, I0{});
+    readB(buf, 1);
+    if constexpr (nxt) {
+      stage(nb, 2, kn);
+      p8_vmcnt<4>();
+    } else {
+      p8_vmcnt<0>();
+    }
+    mfma_q(I0{}, I1{});
+    readA(buf, 1);
+    if constexpr (nxt) stage(nb, 3, kn);
+    mfma_q(I1{}, I1{});
+    readB(buf, 0);
+    if constexpr (nxt) {
+      stage(nb, 1, kn);
+      p8_vmcnt<4>();
+    }
+    mfma_q(I1{}, I0{});
+  };
+  using BT = std::integral_constant<bool, true>;
+  using BF = std::integral_constant<bool, false>;
+  const int nk = K / GB_BK;
+  const int rc = (lane & 7) * 8;
+  float* wimg = (float*)smem + EPI_BASE + wid * (32 * GB_EPI_LD);
+
+  int vid = blockIdx.x, m0, n0;
+  tile_origin(vid, m0, n0);
+  set_src(m0, n0);
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage(0, h, 0);
+  while (true) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K-tile 0 (and the previous tile's stores)
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();
+    for (int t = 0; t + 1 < nk; ++t) ktile(t, BT{});
+    ktile(nk - 1, BF{});
+    if (wr == 0) __builtin_amdgcn_s_barrier();
+    __syncthreads();
+    const int cm0 = m0, cn0 = n0;
+    const int nvid = vid + gridDim.x;
+    const bool more = nvid < nwg;
+    if (more) {
+      tile_origin(nvid, m0, n0);
+      set_src(m0, n0);
+#pragma unroll
+      for (int h = 0; h < 4; ++h) stage(0, h, 0);
+    }
+    const int ncol = cn0 + (rc < 32 ? 32 * wc + rc : 128 + 32 * wc + rc - 32);
+    float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+    if (ea.bias) {
+      b0.x = ea.bias[min(ncol, N - 1)];
+      b0.y = ea.bias[min(ncol + 1, N - 1)];
+      b0.z = ea.bias[min(ncol + 2, N - 1)];
+      b0.w = ea.bias[min(ncol + 3, N - 1)];
+      b1.x = ea.bias[min(ncol + 4, N - 1)];
+      b1.y = ea.bias[min(ncol + 5, N - 1)];
+      b1.z = ea.bias[min(ncol + 6, N - 1)];
+      b1.w = ea.bias[min(ncol + 7, N - 1)];
+    }
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih) {
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+          for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                wimg[(i2 * 16 + fq * 4 + r) * GB_EPI_LD + nh * 32 + j * 16 + fr] = acc[mh][nh][2 * ih + i2][j][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int mrow0 = cm0 + 128 * mh + 64 * wr + 32 * ih;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int lr = rr * 8 + (lane >> 3);
+          const int m = mrow0 + lr;
+          float4 v0 = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
+          float4 v1 = *(const float4*)(wimg + lr * GB_EPI_LD + rc + 4);
+          v0.x += b0.x; v0.y += b0.y; v0.z += b0.z; v0.w += b0.w;
+          v1.x += b1.x; v1.y += b1.y; v1.z += b1.z; v1.w += b1.w;
+          if (m < M && ncol < N) epi_store8<EPI>(ea, m, ncol, N, v0, v1);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    if (!more) break;
+    vid = nvid;
+    __syncthreads();
+  }
+}
+
+static int tw_num_cus() {
+  static int cus = 0;  // one device per process (the engine's)
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 8) cus = 256;
+  }
+  return cus;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -973,6 +1182,10 @@ static int launch_gemm(const bf16_t* A, const bf16_t* W, int M, int N, int K, in
     if (tw_gemm_big_enabled == 5) {
       unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
       hipLaunchKernelGGL(k_gemm_8p<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
+    } else if (tw_gemm_big_enabled == 6) {
+      unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
+      const unsigned grid = std::min<unsigned>(nwg, (unsigned)(tw_num_cus() & ~7));
+      hipLaunchKernelGGL(k_gemm_8pp<EPI>, dim3(grid), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
     } else if (tw_gemm_big_enabled >= 3) {
       const int v = tw_gemm_big_enabled;
       if (v == 3) {  // 256x256, 2 stages, counted-vmcnt loop, setprio

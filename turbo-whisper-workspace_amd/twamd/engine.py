@@ -114,6 +114,10 @@ class WhisperEngine:
         else:
             self.stream = torch.cuda.Stream(self.device, priority=-1)
             self.enc_stream = torch.cuda.Stream(self.device, priority=0)
+            # TW_ENC_RESERVE=r keeps the encoder off r CUs of every XCD (the decoder stream stays unmasked)
+            reserve = int(os.environ.get("TW_ENC_RESERVE", "0"))
+            if reserve > 0:
+                self.enc_stream = self._masked_stream(range(8 * reserve, self._n_cus()))
         self._enc_ev = [torch.cuda.Event(), torch.cuda.Event()]
         D, F, H, V, B = d.d_model, d.ffn, d.heads, d.vocab, max_batch
         dev, bf, f32, i32 = self.device, torch.bfloat16, torch.float32, torch.int32
@@ -672,10 +676,14 @@ class WhisperEngine:
         out = []
         self.batch_langs = []
         self.batch_passes = []
+        overlap = os.environ.get("TW_OVERLAP", "1") != "0"  # 0: encoder and decoder strictly in turn (A/B)
         if sizes:
             prefetch(0)
         for k, n in enumerate(sizes):
-            if k + 1 < len(sizes):
+            if not overlap and k > 0:
+                self.enc_stream.wait_stream(self.stream)
+                prefetch(k)
+            if overlap and k + 1 < len(sizes):
                 prefetch(k + 1)  # runs beside the decode of batch k
             out.append(self.generate(n, slot=k % 2, pre_encoded=True, **gen_kwargs))
             self.batch_langs.append(self.last_langs)
