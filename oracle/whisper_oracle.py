@@ -249,7 +249,7 @@ class WhisperOracle:
             x = x + self._lin(_gelu(self._lin(h, f"{p}.fc1")), f"{p}.fc2")
         cache["len"] = t + 1
         h = _ln(x, sd["model.decoder.layer_norm.weight"], sd["model.decoder.layer_norm.bias"])
-        return (h @ sd["model.decoder.embed_tokens.weight"].T)[0].astype(np.float32)
+        return (sd["model.decoder.embed_tokens.weight"] @ h[0]).astype(np.float32)  # tied proj_out (row-major GEMV)
 
 
 # ----------------------------------------------------------------------------- generation
@@ -318,6 +318,96 @@ def greedy_pass(model: WhisperOracle, enc: np.ndarray, prompt: Sequence[int], ma
         logits = model.decoder_step(tok, cache)
 
 
+def _log_softmax32(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.float32)
+    m = np.max(x)
+    return (x - (m + np.log(np.sum(np.exp(x - m), dtype=np.float32)))).astype(np.float32)
+
+
+def _topk_desc(x: np.ndarray, k: int) -> np.ndarray:
+    """Indices of the k largest values, descending; ties -> lower index first."""
+    if x.size <= 4 * k:
+        return np.argsort(-x, kind="stable")[:k]
+    kth = np.partition(x, x.size - k)[x.size - k]
+    cand = np.nonzero(x >= kth)[0]  # every value tied with the k-th is a candidate
+    return cand[np.lexsort((cand, -x[cand]))][:k]
+
+
+def beam_pass(model: WhisperOracle, enc: np.ndarray, prompt: Sequence[int], max_new: int, g: GenCfg, use_ts: bool,
+              num_beams: int, length_penalty: float = 1.0) -> List[int]:
+    """GenerationMixin._beam_search ($TF/generation/utils.py:3208-3512) for ONE window with the Whisper processor
+    chain, early_stopping=False (GenerationConfig default), one EOS id: K = 2 * num_beams continuations per step
+    (:3277-3282) from log_softmax(f32 logits) + processors (:3381-3382) + the running beam scores; running beams =
+    best K non-finished (:3131-3151); finished beams = best of the previous and the just-finished top-num_beams
+    candidates scored sum/len**length_penalty (:3153-3206); stop when no running beam can beat the worst finished
+    one (:3008-3053) or every candidate hit a stopping criterion (EOS / max_length, :3055-3073). Returns the
+    generated tokens of the best finished beam (with its EOS if it ended on one)."""
+    nb, K, V = num_beams, 2 * num_beams, g.V
+    P = len(prompt)
+    max_length = P + max_new
+    base = model.new_cache(enc)
+    for t in prompt[:-1]:
+        model.decoder_step(t, base)
+    logits0 = model.decoder_step(prompt[-1], base)
+
+    def clone(c):
+        return {"self": [(k.copy(), v.copy()) for k, v in c["self"]], "cross": c["cross"], "len": c["len"]}
+
+    caches = [clone(base) for _ in range(nb)]
+    logits = [logits0] * nb
+    run_tok: List[List[int]] = [[] for _ in range(nb)]
+    run_score = np.full(nb, -1e9, np.float32)
+    run_score[0] = 0.0
+    fin_score = np.full(nb, -1e9, np.float32)
+    fin_seq: List[Optional[List[int]]] = [None] * nb
+    fin_flag = np.zeros(nb, bool)
+    unsatisfied = True
+    cur_len = P
+    while True:
+        acc = np.empty(nb * V, np.float32)
+        for b in range(nb):
+            lp = process_logits(_log_softmax32(logits[b]), run_tok[b], g, use_ts)
+            acc[b * V:(b + 1) * V] = lp + run_score[b]
+        top = _topk_desc(acc, K)
+        sc = acc[top].astype(np.float32)
+        src, tok = top // V, top % V
+        hits = (tok == g.eot) | (cur_len + 1 >= max_length)
+        # e. running beams for the next step
+        rsc = (sc + hits.astype(np.float32) * np.float32(-1e9)).astype(np.float32)
+        order = _topk_desc(rsc, nb)
+        # f. finished beams
+        cand = (sc / np.float32((cur_len + 1 - P) ** length_penalty)).astype(np.float32)
+        if not unsatisfied:
+            cand = cand + np.float32(-1e9)
+        just = hits & (np.arange(K) < nb)
+        cand = np.where(just, cand, cand + np.float32(-1e9)).astype(np.float32)
+        merged = np.concatenate([fin_score, cand])
+        msel = _topk_desc(merged, nb)
+        new_seq, new_flag = [], []
+        for i in msel:
+            if i < nb:
+                new_seq.append(fin_seq[i])
+                new_flag.append(fin_flag[i])
+            else:
+                c = i - nb
+                new_seq.append(run_tok[src[c]] + [int(tok[c])])
+                new_flag.append(bool(just[c]))
+        fin_score, fin_seq, fin_flag = merged[msel].astype(np.float32), new_seq, np.array(new_flag)
+        # g. reorder running beams (and their caches)
+        new_caches = [clone(caches[src[c]]) for c in order]
+        run_tok = [run_tok[src[c]] + [int(tok[c])] for c in order]
+        run_score = rsc[order].astype(np.float32)
+        cur_len += 1
+        best_possible = run_score[0] / np.float32((cur_len - P) ** length_penalty)
+        worst = np.where(fin_flag, np.min(fin_score), np.float32(-1e9))
+        unsatisfied = unsatisfied and bool(np.any(best_possible > worst))
+        if not unsatisfied or bool(np.all(hits)):
+            break
+        caches = new_caches
+        logits = [model.decoder_step(run_tok[j][-1], caches[j]) for j in range(nb)]
+    return list(fin_seq[0])
+
+
 def detect_language(model: WhisperOracle, enc: np.ndarray, g: GenCfg) -> int:
     cache = model.new_cache(enc)
     lg = model.decoder_step(g.sot, cache)
@@ -340,9 +430,9 @@ def retrieve_segment(seq, seek_num_frames, tb):
 
 def generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, task: Optional[str] = "transcribe",
              language: Optional[int] = None, return_timestamps: bool = True, max_new_tokens: Optional[int] = None,
-             encoder_cache: Optional[dict] = None) -> Tuple[List[int], int]:
-    """Short-form WhisperGenerationMixin.generate for ONE 3000-frame window, num_beams=1.
-    Returns (final token sequence, language id)."""
+             encoder_cache: Optional[dict] = None, num_beams: int = 1) -> Tuple[List[int], int]:
+    """Short-form WhisperGenerationMixin.generate for ONE 3000-frame window (greedy, or beam search with
+    num_beams > 1). Returns (final token sequence, language id)."""
     feats = np.asarray(feats, np.float32)
 
     def enc_at(seek):
@@ -370,7 +460,10 @@ def generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, task: Optional[
     max_new = max_new_tokens if max_new_tokens is not None else min(g.max_length + P, 448) - P
     seek, out = 0, []
     while seek < 3000:
-        seq = greedy_pass(model, enc_at(seek), prompt, max_new, g, return_timestamps)
+        if num_beams > 1:
+            seq = beam_pass(model, enc_at(seek), prompt, max_new, g, return_timestamps, num_beams)
+        else:
+            seq = greedy_pass(model, enc_at(seek), prompt, max_new, g, return_timestamps)
         if seq and seq[-1] == g.eot:
             seq = seq[:-1]
         toks, off = retrieve_segment(seq, 3000 - seek, g.ts_begin)

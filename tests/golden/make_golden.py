@@ -9,6 +9,8 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
   pipeline.json     AutomaticSpeechRecognitionPipeline outputs with the reference's call kwargs
                     (vocalis/core/audio_pipeline.py:351-358, num_beams=1 for greedy parity) and 30-s mode
   decode_asr.json   tokenizer._decode_asr on seeded random strided token sequences
+  beam.json         generate(num_beams=5) token sequences (the pipeline's default decode, asr:160-163) of
+                    test-mini on three windows, with and without timestamps and with a max_length stop
 
 Usage: python tests/golden/make_golden.py   (≈1-2 min on 8 CPU cores)
 """
@@ -214,6 +216,29 @@ def make_decode_asr(out):
                       "text": text, "optional": _jsonable(opt)})
     with open(os.path.join(out, "decode_asr.json"), "w") as f:
         json.dump(cases, f)
+
+
+def make_beam(out):
+    from transformers import WhisperFeatureExtractor
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    cl = clips()
+    names = ["speech30", "noise12", "zeros30"]
+    feats = np.stack([fe(cl[k], sampling_rate=16000, return_tensors="np")["input_features"][0] for k in names])
+    cases = []
+    for ts, mnt in ((True, 40), (False, 40), (True, 9)):
+        with torch.no_grad():
+            o = m.generate(torch.from_numpy(feats), task="transcribe", return_timestamps=ts, num_beams=5,
+                           max_new_tokens=mnt)
+        seqs = o["sequences"] if isinstance(o, dict) else o
+        cases.append({"return_timestamps": ts, "max_new_tokens": mnt, "clips": names,
+                      "sequences": seqs.numpy().tolist()})
+    with open(os.path.join(out, "beam.json"), "w") as f:
+        json.dump({"seed": SEED, "dims": "test-mini", "num_beams": 5, "cases": cases}, f)
 
 
 def _jsonable(x):

@@ -88,3 +88,21 @@ def test_language_detection_and_generate_match(golden_model, oracle_model, gcfg)
         while ref and ref[-1] == gcfg.eot:
             ref.pop()
         assert toks == ref, (name, toks, ref)
+
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_beam_search_matches_transformers(oracle_model, gcfg, case):
+    """The oracle's restatement of _beam_search (num_beams=5, the ASR pipeline's default) reproduces
+    transformers' generate() token-for-token (tests/golden/beam.json)."""
+    import json
+
+    gold = json.load(open(os.path.join(G, "beam.json")))
+    c = gold["cases"][case]
+    cl = _clips()
+    for name, ref in zip(c["clips"], c["sequences"]):
+        feats = wo.log_mel(cl[name][:480000], D.n_mels)
+        got, _ = wo.generate(oracle_model, feats, gcfg, task="transcribe", return_timestamps=c["return_timestamps"],
+                             max_new_tokens=c["max_new_tokens"], num_beams=gold["num_beams"])
+        while ref and ref[-1] == gcfg.eot:
+            ref = ref[:-1]
+        assert got == ref, (name, got[:20], ref[:20])
