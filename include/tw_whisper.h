@@ -131,6 +131,41 @@ int tw_attn_encoder(const uint16_t* qkv, int B, int S, int H, uint16_t* out, voi
  * k_attn_enc2 with 8 waves / 256 queries per workgroup, 4 = the same with 4 waves, 0 = the first kernel. */
 int tw_attn_set_variant(int variant);
 
+/* ---- beam search ------------------------------------------------------------------------------ */
+/* GenerationMixin._beam_search ($TF/generation/utils.py:3208-3512) with the Whisper processor chain, for W windows
+ * of num_beams rows each (row = w * num_beams + j), early_stopping=False, one EOS id. One call per generated token:
+ * per row the log_softmax of the f32 logits, the processors (as tw_logits_select) and the top 2*num_beams
+ * continuations; per window the running beams, the finished beams (score / len**length_penalty) and the
+ * early-stop heuristic. It rewrites the running token histories (tokens), the processor state, ids and pos of
+ * every row, and src_rows (the row whose self-attention K/V each new running beam continues: tw_kv_reorder).
+ * TwBeamState holds DEVICE arrays; win[w] = {improvement possible, done, tokens generated, unused}. Initialise
+ * run_score to {0, -1e9, ...} per window, fin_score to -1e9, fin_flag/fin_len to 0, win to {1, 0, 0, 0}.
+ * The best hypothesis of window w is finished slot 0: fin_tokens[w*nb][0 .. fin_len[w*nb]). */
+typedef struct TwBeamParams {
+  int32_t num_beams;     /* 2 .. 8                                                      */
+  int32_t max_new;       /* max_length - prompt length                                   */
+  float length_penalty;  /* generation_config.length_penalty (1.0)                       */
+  int32_t ld_tokens;     /* row stride of tokens / fin_tokens (<= 448)                   */
+} TwBeamParams;
+typedef struct TwBeamState {
+  float* run_score;      /* f32[R]   running beam scores (descending within a window)    */
+  float* fin_score;      /* f32[R]                                                        */
+  int32_t* fin_flag;     /* i32[R]                                                        */
+  int32_t* fin_len;      /* i32[R]                                                        */
+  int32_t* fin_tokens;   /* i32[R][ld_tokens]                                             */
+  int32_t* win;          /* i32[W][4]                                                     */
+  int32_t* src_rows;     /* i32[R]   out                                                  */
+} TwBeamState;
+/* workspace: tw_beam_workspace_bytes(R) bytes of device memory. */
+size_t tw_beam_workspace_bytes(int rows);
+int tw_beam_step(const float* logits, int W, int ld_logits, const uint32_t* suppress_bits,
+                 const TwSelectParams* params, const TwBeamParams* beam, const TwBeamState* bstate, int* state,
+                 int* tokens, int* ids, int* pos, void* workspace, void* stream);
+/* caches bf16[layers][rows_cap][H][T][64]: rows 0..R-1 take positions [0, pos[r]) of row src_rows[r]; scratch has
+ * the caches' shape. */
+int tw_kv_reorder(uint16_t* k_cache, uint16_t* v_cache, uint16_t* k_scratch, uint16_t* v_scratch, int layers,
+                  int rows_cap, int H, int T, int R, const int* src_rows, const int* pos, void* stream);
+
 /* ---- packed decoder GEMV ------------------------------------------------------------------------- */
 /* The decoder step's projections (M <= 32 rows: $TF/models/whisper/modeling_whisper.py:279-282, 375-376, and the
  * tied proj_out :970) read every weight byte once per token, so their layout is chosen for the HBM stream:

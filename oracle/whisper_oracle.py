@@ -333,33 +333,25 @@ def _topk_desc(x: np.ndarray, k: int) -> np.ndarray:
     return cand[np.lexsort((cand, -x[cand]))][:k]
 
 
-def beam_pass(model: WhisperOracle, enc: np.ndarray, prompt: Sequence[int], max_new: int, g: GenCfg, use_ts: bool,
-              num_beams: int, length_penalty: float = 1.0) -> List[int]:
+def beam_search_core(first_logits: np.ndarray, step_fn, P: int, max_new: int, g: GenCfg, use_ts: bool,
+                     num_beams: int, length_penalty: float = 1.0) -> Tuple[List[int], dict]:
     """GenerationMixin._beam_search ($TF/generation/utils.py:3208-3512) for ONE window with the Whisper processor
     chain, early_stopping=False (GenerationConfig default), one EOS id: K = 2 * num_beams continuations per step
     (:3277-3282) from log_softmax(f32 logits) + processors (:3381-3382) + the running beam scores; running beams =
     best K non-finished (:3131-3151); finished beams = best of the previous and the just-finished top-num_beams
     candidates scored sum/len**length_penalty (:3153-3206); stop when no running beam can beat the worst finished
-    one (:3008-3053) or every candidate hit a stopping criterion (EOS / max_length, :3055-3073). Returns the
-    generated tokens of the best finished beam (with its EOS if it ended on one)."""
+    one (:3008-3053) or every candidate hit a stopping criterion (EOS / max_length, :3055-3073).
+    first_logits: f32[V] after the prompt; step_fn(src_beams, tokens) -> f32[nb][V]: reorder the beams' decoder
+    caches to src_beams, feed tokens, return the next logits. Returns (generated tokens of the best finished beam,
+    with its EOS if it ended on one; a trace dict of the final finished/running beams)."""
     nb, K, V = num_beams, 2 * num_beams, g.V
-    P = len(prompt)
     max_length = P + max_new
-    base = model.new_cache(enc)
-    for t in prompt[:-1]:
-        model.decoder_step(t, base)
-    logits0 = model.decoder_step(prompt[-1], base)
-
-    def clone(c):
-        return {"self": [(k.copy(), v.copy()) for k, v in c["self"]], "cross": c["cross"], "len": c["len"]}
-
-    caches = [clone(base) for _ in range(nb)]
-    logits = [logits0] * nb
+    logits = [first_logits] * nb
     run_tok: List[List[int]] = [[] for _ in range(nb)]
     run_score = np.full(nb, -1e9, np.float32)
     run_score[0] = 0.0
     fin_score = np.full(nb, -1e9, np.float32)
-    fin_seq: List[Optional[List[int]]] = [None] * nb
+    fin_seq: List[List[int]] = [[] for _ in range(nb)]
     fin_flag = np.zeros(nb, bool)
     unsatisfied = True
     cur_len = P
@@ -393,8 +385,8 @@ def beam_pass(model: WhisperOracle, enc: np.ndarray, prompt: Sequence[int], max_
                 new_seq.append(run_tok[src[c]] + [int(tok[c])])
                 new_flag.append(bool(just[c]))
         fin_score, fin_seq, fin_flag = merged[msel].astype(np.float32), new_seq, np.array(new_flag)
-        # g. reorder running beams (and their caches)
-        new_caches = [clone(caches[src[c]]) for c in order]
+        # g. reorder the running beams
+        srcs = [int(src[c]) for c in order]
         run_tok = [run_tok[src[c]] + [int(tok[c])] for c in order]
         run_score = rsc[order].astype(np.float32)
         cur_len += 1
@@ -403,9 +395,31 @@ def beam_pass(model: WhisperOracle, enc: np.ndarray, prompt: Sequence[int], max_
         unsatisfied = unsatisfied and bool(np.any(best_possible > worst))
         if not unsatisfied or bool(np.all(hits)):
             break
-        caches = new_caches
-        logits = [model.decoder_step(run_tok[j][-1], caches[j]) for j in range(nb)]
-    return list(fin_seq[0])
+        logits = step_fn(srcs, [t[-1] for t in run_tok])
+    trace = {"fin_score": fin_score, "fin_seq": fin_seq, "fin_flag": fin_flag, "run_tok": run_tok,
+             "run_score": run_score, "steps": cur_len - P}
+    return list(fin_seq[0]), trace
+
+
+def beam_pass(model: WhisperOracle, enc: np.ndarray, prompt: Sequence[int], max_new: int, g: GenCfg, use_ts: bool,
+              num_beams: int, length_penalty: float = 1.0) -> List[int]:
+    """beam_search_core driven by the oracle decoder (one KV cache per beam, reordered like the model's cache)."""
+    base = model.new_cache(enc)
+    for t in prompt[:-1]:
+        model.decoder_step(t, base)
+    logits0 = model.decoder_step(prompt[-1], base)
+
+    def clone(c):
+        return {"self": [(k.copy(), v.copy()) for k, v in c["self"]], "cross": c["cross"], "len": c["len"]}
+
+    caches = [clone(base) for _ in range(num_beams)]
+
+    def step(srcs, toks):
+        new = [clone(caches[s]) for s in srcs]
+        caches[:] = new
+        return [model.decoder_step(t, c) for t, c in zip(toks, caches)]
+
+    return beam_search_core(logits0, step, len(prompt), max_new, g, use_ts, num_beams, length_penalty)[0]
 
 
 def detect_language(model: WhisperOracle, enc: np.ndarray, g: GenCfg) -> int:

@@ -237,8 +237,21 @@ def make_beam(out):
         seqs = o["sequences"] if isinstance(o, dict) else o
         cases.append({"return_timestamps": ts, "max_new_tokens": mnt, "clips": names,
                       "sequences": seqs.numpy().tolist()})
+    # the ASR pipeline with the reference's call and its default decode (num_beams=5)
+    from transformers import AutomaticSpeechRecognitionPipeline
+
+    tk = hf_tokenizer(gen.special)
+    pipe = AutomaticSpeechRecognitionPipeline(model=m, feature_extractor=fe, tokenizer=tk, device=-1)
+    audio = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)])  # 75 s
+    pcases = []
+    for name, kw in [("ref_60_5", dict(chunk_length_s=60, stride_length_s=5, batch_size=32)),
+                     ("mode_30_0", dict(chunk_length_s=30, stride_length_s=0, batch_size=2))]:
+        r = pipe(audio.copy(), generate_kwargs={"task": "transcribe", "num_beams": 5, "max_new_tokens": 40},
+                 return_timestamps=True, **kw)
+        pcases.append({"name": name, "kwargs": kw, "output": _jsonable(r)})
     with open(os.path.join(out, "beam.json"), "w") as f:
-        json.dump({"seed": SEED, "dims": "test-mini", "num_beams": 5, "cases": cases}, f)
+        json.dump({"seed": SEED, "dims": "test-mini", "num_beams": 5, "cases": cases,
+                   "pipeline_audio": "speech_like(40,5)+white_noise(35,11)", "pipeline": pcases}, f)
 
 
 def _jsonable(x):

@@ -15,7 +15,7 @@ LIB = os.path.join(ROOT, "turbo-whisper-workspace_amd", "twamd", "libtwhip.so")
 
 def _declared():
     src = "".join(open(h).read() for h in HDRS)
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(tw_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|size_t|const char\*)\s+(tw_\w+)\s*\(", src, flags=re.M)))
 
 
 @pytest.fixture(scope="module")

@@ -1,0 +1,166 @@
+"""Beam search on the MI355X (tw_beam_step + tw_kv_reorder, WhisperEngine.beam_pass) against the oracle's
+restatement of transformers' _beam_search (oracle/whisper_oracle.py: beam_search_core, itself pinned token-for-token
+to transformers generate(num_beams=5) by tests/test_oracle_golden.py)."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import whisper_oracle as wo
+from twamd import _lib
+from twamd.config import PRESETS, GenerationSettings
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _gcfg(dims):
+    gen = GenerationSettings.default(dims)
+    st = gen.special
+    return gen, wo.GenCfg(dims.vocab, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate,
+                          st.notimestamps, gen.suppress_tokens, gen.begin_suppress_tokens)
+
+
+def _synthetic_logits(history, V, tsb, eot, salt):
+    """Deterministic logits for a beam's token history: seeded Gaussian plus a few boosted tokens, with EOS and
+    timestamps likely enough that beams finish and the timestamp rules act."""
+    h = hash((salt,) + tuple(history)) & 0xFFFFFFFF
+    rng = np.random.default_rng(h)
+    x = rng.standard_normal(V).astype(np.float32) * 2.0
+    x[rng.integers(0, tsb, 6)] += 7.0
+    x[tsb + rng.integers(0, 60, 3)] += 6.5
+    x[eot] += 5.0 + 0.4 * len(history)
+    return x
+
+
+@pytest.mark.parametrize("nb,W,use_ts,max_new", [(5, 3, True, 24), (2, 4, True, 30), (5, 2, False, 16),
+                                                 (3, 3, True, 5)])
+def test_beam_step_matches_oracle_core(nb, W, use_ts, max_new):
+    d = PRESETS["test-mini"]
+    gen, g = _gcfg(d)
+    st = gen.special
+    V, T, R = d.vocab, 448, W * nb
+    P = 3
+    # device state
+    logits = torch.empty(R, V, device=DEV)
+    state = torch.zeros(R, _lib.TW_STATE_STRIDE, dtype=torch.int32, device=DEV)
+    state[:, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
+    tokens = torch.zeros(R, T, dtype=torch.int32, device=DEV)
+    ids = torch.zeros(R, dtype=torch.int32, device=DEV)
+    pos = torch.full((R,), P, dtype=torch.int32, device=DEV)
+    run_score = torch.full((W, nb), -1e9, device=DEV)
+    run_score[:, 0] = 0
+    fin_score = torch.full((R,), -1e9, device=DEV)
+    fin_flag = torch.zeros(R, dtype=torch.int32, device=DEV)
+    fin_len = torch.zeros(R, dtype=torch.int32, device=DEV)
+    fin_tokens = torch.zeros(R, T, dtype=torch.int32, device=DEV)
+    win = torch.tensor([[1, 0, 0, 0]] * W, dtype=torch.int32, device=DEV)
+    src_rows = torch.zeros(R, dtype=torch.int32, device=DEV)
+    ws = torch.empty(int(_lib.load().tw_beam_workspace_bytes(R)), dtype=torch.uint8, device=DEV)
+    bits = np.zeros((V + 31) // 32, np.uint32)
+    for t in gen.suppress_tokens:
+        bits[t >> 5] |= np.uint32(1 << (t & 31))
+    sup = torch.from_numpy(bits.view(np.int32)).to(DEV)
+    bs_ = list(gen.begin_suppress_tokens)[:8]
+    sel = _lib.TwSelectParams(V, st.eot, st.eot, st.timestamp_begin, st.notimestamps, 50, int(use_ts), max_new, 0, 0, 0,
+                              len(bs_), (ctypes.c_int32 * 8)(*(bs_ + [0] * (8 - len(bs_)))))
+    bp = _lib.TwBeamParams(nb, max_new, 1.0, T)
+    bst = _lib.TwBeamState(run_score.data_ptr(), fin_score.data_ptr(), fin_flag.data_ptr(), fin_len.data_ptr(),
+                           fin_tokens.data_ptr(), win.data_ptr(), src_rows.data_ptr())
+    tsb = st.timestamp_begin
+    # GPU loop: logits of every row from its history (window salt w)
+    hist = [[] for _ in range(R)]
+    steps = 0
+    while steps < max_new:
+        host = np.stack([_synthetic_logits(hist[r], V, tsb, st.eot, r // nb) for r in range(R)])
+        logits.copy_(torch.from_numpy(host))
+        _lib.call("tw_beam_step", logits.data_ptr(), W, V, sup.data_ptr(), ctypes.byref(sel), ctypes.byref(bp),
+                  ctypes.byref(bst), state.data_ptr(), tokens.data_ptr(), ids.data_ptr(), pos.data_ptr(),
+                  ws.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        steps += 1
+        tk = tokens.cpu().numpy()
+        hist = [list(tk[r, :steps]) for r in range(R)]
+        assert (pos.cpu().numpy() == P + steps).all()
+        if bool(win[:, 1].all().item()):
+            break
+    # oracle: the same logits function, per window
+    for w in range(W):
+        first = _synthetic_logits([], V, tsb, st.eot, w)
+
+        def step(srcs, toks, _st={"h": [[] for _ in range(nb)]}):
+            _st["h"] = [_st["h"][s] + [t] for s, t in zip(srcs, toks)]
+            return [_synthetic_logits(h, V, tsb, st.eot, w) for h in _st["h"]]
+
+        ref, tr = wo.beam_search_core(first, step, P, max_new, g, use_ts, nb)
+        got = fin_tokens[w * nb, : int(fin_len[w * nb])].tolist()
+        assert got == ref, (w, got, ref)
+        np.testing.assert_allclose(fin_score.view(W, nb)[w].cpu().numpy(), tr["fin_score"], rtol=1e-5, atol=1e-4)
+        assert [bool(x) for x in fin_flag.view(W, nb)[w].cpu().numpy()] == [bool(x) for x in tr["fin_flag"]]
+
+
+def test_kv_reorder_matches_gather():
+    L, cap, H, T, R = 2, 12, 3, 40, 10
+    k = torch.randn(L, cap, H, T, 64, device=DEV).to(torch.bfloat16)
+    v = torch.randn(L, cap, H, T, 64, device=DEV).to(torch.bfloat16)
+    k0, v0 = k.clone(), v.clone()
+    src = torch.tensor([0, 0, 1, 4, 4, 5, 9, 2, 8, 3], dtype=torch.int32, device=DEV)
+    pos = torch.full((R,), 17, dtype=torch.int32, device=DEV)
+    ks, vs = torch.empty_like(k), torch.empty_like(v)
+    _lib.call("tw_kv_reorder", k.data_ptr(), v.data_ptr(), ks.data_ptr(), vs.data_ptr(), L, cap, H, T, R, src.data_ptr(),
+              pos.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    sl = src.long()
+    assert torch.equal(k[:, :R, :, :17], k0[:, sl, :, :17]) and torch.equal(v[:, :R, :, :17], v0[:, sl, :, :17])
+    assert torch.equal(k[:, :R, :, 17:], k0[:, :R, :, 17:])  # positions past pos untouched
+    assert torch.equal(k[:, R:], k0[:, R:])
+
+
+@pytest.fixture(scope="module")
+def mini():
+    from twamd.pipeline import TurboTranscriber
+
+    return TurboTranscriber.from_pretrained("test-mini", seed=1234, max_batch=3, max_beams=5)
+
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_engine_beam_search_matches_transformers(mini, case):
+    """generate(num_beams=5) on the engine vs transformers' own beam search (tests/golden/beam.json)."""
+    from twamd.synth_audio import silence, speech_like, white_noise
+
+    gold = json.load(open(os.path.join(G, "beam.json")))
+    c = gold["cases"][case]
+    clips = {"speech30": speech_like(30.0, 1234), "noise12": white_noise(12.3, 7), "zeros30": silence(30.0)}
+    eng = mini.engine
+    host = np.zeros((3, 480000), np.float32)
+    for i, name in enumerate(c["clips"]):
+        x = clips[name][:480000]
+        host[i, : len(x)] = x
+    eng.wave[:3].copy_(torch.from_numpy(host))
+    eng.logmel(3)
+    seqs = eng.generate(3, task="transcribe", max_new_tokens=c["max_new_tokens"],
+                        return_timestamps=c["return_timestamps"], num_beams=5)
+    for got, ref in zip(seqs, c["sequences"]):
+        while ref and ref[-1] == 50257:
+            ref = ref[:-1]
+        assert list(got) == ref
+
+
+@pytest.mark.parametrize("name", ["ref_60_5", "mode_30_0"])
+def test_pipeline_beam5_matches_transformers_pipeline(mini, name):
+    """The drop-in callable with the reference's call and the ASR pipeline's default num_beams=5 reproduces the
+    transformers pipeline's output (tests/golden/beam.json)."""
+    from twamd.synth_audio import speech_like, white_noise
+
+    gold = json.load(open(os.path.join(G, "beam.json")))
+    case = next(c for c in gold["pipeline"] if c["name"] == name)
+    audio = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)])
+    kw = {k: v for k, v in case["kwargs"].items()}
+    r = mini(audio, generate_kwargs={"task": "transcribe", "num_beams": 5, "max_new_tokens": 40},
+             return_timestamps=True, **kw)
+    ref = case["output"]
+    assert r["text"] == ref["text"]
+    assert [(tuple(c["timestamp"]), c["text"]) for c in r["chunks"]] == \
+        [(tuple(c["timestamp"]), c["text"]) for c in ref["chunks"]]

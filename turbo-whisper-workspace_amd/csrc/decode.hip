@@ -208,3 +208,467 @@ extern "C" int tw_logits_select(const float* logits, int B, int ld_logits, const
                      ld_tokens, next_ids, pos);
   return tw_check_launch("tw_logits_select");
 }
+
+// =================================================================================================
+// Beam search (num_beams > 1): GenerationMixin._beam_search ($TF/generation/utils.py:3208-3512) with the same Whisper
+// processor chain, early_stopping=False, one EOS id. Rows are window-major: row = w * nb + j.
+//   k_beam_partial  grid (R, NC): per vocab chunk of a row, the log-sum-exp of the raw logits (log_softmax), the
+//                   timestamp-rule statistics of k_select_partial, and the top-K masked text and timestamp
+//                   candidates (K = 2 nb continuations per window, :3277-3282)
+//   k_beam_step     grid W: per window, the row candidates (the timestamp rule removes the text ones when it fires),
+//                   the window's top-K by accumulated log-prob (:3316-3349), running beams for the next step
+//                   (:3131-3151), finished beams (:3153-3206), the early-stop heuristic (:3008-3073); then it
+//                   reorders the running token histories, the processor state, ids/pos, and writes the row each
+//                   new running beam continues (for the self-attention K/V reorder, tw_kv_reorder)
+// =================================================================================================
+struct Cand {
+  float v;
+  int i;
+};
+__device__ inline bool cand_better(float v, int i, const Cand& c) { return v > c.v || (v == c.v && i < c.i); }
+
+template <int K>
+__device__ inline void cand_insert(Cand (&L)[K], float v, int i) {
+  if (!cand_better(v, i, L[K - 1])) return;
+#pragma unroll
+  for (int j = K - 1; j > 0; --j) {
+    if (cand_better(v, i, L[j - 1])) {
+      L[j] = L[j - 1];
+    } else {
+      L[j] = Cand{v, i};
+      return;
+    }
+  }
+  L[0] = Cand{v, i};
+}
+
+// K rounds of wave argmax over the lanes' sorted lists: out (LDS, K entries) = the wave's top-K, descending.
+template <int K>
+__device__ inline void wave_topk(Cand (&L)[K], Cand* out, int lane) {
+  for (int r = 0; r < K; ++r) {
+    float bv = L[0].v;
+    int bi = L[0].i, bl = lane;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64), ol = __shfl_xor(bl, o, 64);
+      if (ov > bv || (ov == bv && (oi < bi || (oi == bi && ol < bl)))) {
+        bv = ov;
+        bi = oi;
+        bl = ol;
+      }
+    }
+    if (lane == 0) out[r] = Cand{bv, bi};
+    if (lane == bl) {  // pop the head
+#pragma unroll
+      for (int j = 0; j < K - 1; ++j) L[j] = L[j + 1];
+      L[K - 1] = Cand{-INFINITY, 0x7fffffff};
+    }
+  }
+}
+
+template <int K>
+struct BeamPart {
+  Cand t[K];  // top-K masked text candidates (logit value)
+  Cand s[K];  // top-K masked timestamp candidates
+  float m_all, s_all, m_ts, s_ts;
+};
+
+template <int K>
+__global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ logits, int ld_logits,
+                                                      const uint32_t* __restrict__ suppress_bits, TwSelectParams p,
+                                                      const int* __restrict__ state, BeamPart<K>* __restrict__ ws) {
+  TW_DEC_PRIO();
+  __shared__ Cand wl[2][4][K];
+  __shared__ float wst[4][4];
+  const int b = blockIdx.x, c = blockIdx.y, NC = gridDim.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const RowMask rm = row_mask(state + b * TW_STATE_STRIDE, p);
+  const float* row = logits + (size_t)b * ld_logits;
+  const int V = p.V, tsb = p.ts_begin;
+  const int v0 = (int)((long)c * V / NC), v1 = (int)((long)(c + 1) * V / NC);
+  Cand T[K], S[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) T[j] = S[j] = Cand{-INFINITY, 0x7fffffff};
+  float m_all = -INFINITY, s_all = 0.f, m_ts = -INFINITY, s_ts = 0.f;
+  for (int v = v0 + tid; v < v1; v += 256) {
+    const float x = row[v];
+    lse_merge(m_all, s_all, x, 1.f);
+    bool masked = (suppress_bits ? (suppress_bits[v >> 5] >> (v & 31)) & 1u : 0u);
+    if (rm.init_step)
+      for (int i = 0; i < p.n_begin_suppress; ++i) masked |= (v == p.begin_suppress[i]);
+    if (p.use_timestamps) {
+      masked |= (v == p.no_timestamps);
+      if (v >= tsb) {
+        masked |= rm.mask_ts_all || (v < rm.ts_hi_block);
+        if (rm.init_step && p.max_initial_ts >= 0) masked |= (v > tsb + p.max_initial_ts);
+      } else {
+        masked |= (rm.mask_text_lt_eos && v < p.eos) || rm.init_step;
+      }
+    }
+    if (masked) continue;
+    if (v < tsb || !p.use_timestamps) {
+      cand_insert<K>(T, x, v);
+    } else {
+      cand_insert<K>(S, x, v);
+      lse_merge(m_ts, s_ts, x, 1.f);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float m2 = __shfl_xor(m_all, o, 64), s2 = __shfl_xor(s_all, o, 64);
+    lse_merge(m_all, s_all, m2, s2);
+    m2 = __shfl_xor(m_ts, o, 64);
+    s2 = __shfl_xor(s_ts, o, 64);
+    lse_merge(m_ts, s_ts, m2, s2);
+  }
+  wave_topk<K>(T, wl[0][wid], lane);
+  wave_topk<K>(S, wl[1][wid], lane);
+  if (lane == 0) {
+    wst[wid][0] = m_all;
+    wst[wid][1] = s_all;
+    wst[wid][2] = m_ts;
+    wst[wid][3] = s_ts;
+  }
+  __syncthreads();
+  if (wid != 0) return;
+  BeamPart<K>* out = ws + (size_t)b * NC + c;
+  for (int l = 0; l < 2; ++l) {  // merge the 4 wave lists: lane q holds entry q (4K <= 64), K rounds of argmax
+    Cand mine = lane < 4 * K ? wl[l][lane / K][lane % K] : Cand{-INFINITY, 0x7fffffff};
+    bool used = false;
+    for (int r = 0; r < K; ++r) {
+      float bv = used ? -INFINITY : mine.v;
+      int bi = used ? 0x7fffffff : mine.i, bl = lane;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64), ol = __shfl_xor(bl, o, 64);
+        if (ov > bv || (ov == bv && (oi < bi || (oi == bi && ol < bl)))) {
+          bv = ov;
+          bi = oi;
+          bl = ol;
+        }
+      }
+      if (lane == bl) used = true;
+      if (lane == 0) {
+        if (l == 0) out->t[r] = Cand{bv, bi};
+        else out->s[r] = Cand{bv, bi};
+      }
+    }
+  }
+  if (lane == 0) {
+    float ma = wst[0][0], sa = wst[0][1], mt = wst[0][2], st2 = wst[0][3];
+    for (int w = 1; w < 4; ++w) {
+      lse_merge(ma, sa, wst[w][0], wst[w][1]);
+      lse_merge(mt, st2, wst[w][2], wst[w][3]);
+    }
+    out->m_all = ma;
+    out->s_all = sa;
+    out->m_ts = mt;
+    out->s_ts = st2;
+  }
+}
+
+#define TW_BEAM_MAXNB 8
+#define TW_BEAM_MAXT 448
+
+template <int K>
+__global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict__ ws, int NC, TwSelectParams p,
+                                                   TwBeamParams bp, TwBeamState bs, int* __restrict__ state,
+                                                   int* __restrict__ tokens, int* __restrict__ ids,
+                                                   int* __restrict__ pos) {
+  TW_DEC_PRIO();
+  __shared__ Cand rc[TW_BEAM_MAXNB][K];  // row candidates: accumulated log-prob, token
+  __shared__ int old_tok[TW_BEAM_MAXNB][TW_BEAM_MAXT];
+  __shared__ int old_fin[TW_BEAM_MAXNB][TW_BEAM_MAXT];
+  __shared__ int old_st[TW_BEAM_MAXNB][TW_STATE_STRIDE];
+  __shared__ int old_flen[TW_BEAM_MAXNB];
+  __shared__ int s_src[TW_BEAM_MAXNB], s_tok[TW_BEAM_MAXNB], f_from[TW_BEAM_MAXNB], f_flag[TW_BEAM_MAXNB];
+  __shared__ float s_score[TW_BEAM_MAXNB], f_score[TW_BEAM_MAXNB];
+  __shared__ int c_beam[2 * K], c_tok[2 * K];
+  const int w = blockIdx.x, nb = bp.num_beams, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ldt = bp.ld_tokens;
+  int* win = bs.win + 4 * w;
+  const int t = win[2];
+  const float NEG = -1.0e9f;
+
+  // 1. per row (one wave each): merge the chunk records, apply the timestamp rule, score the candidates
+  if (wid < nb) {
+    const int row = w * nb + wid;
+    const BeamPart<K>* parts = ws + (size_t)row * NC;
+    float m_all = -INFINITY, s_all = 0.f, m_ts = -INFINITY, s_ts = 0.f;
+    for (int c = lane; c < NC; c += 64) {
+      lse_merge(m_all, s_all, parts[c].m_all, parts[c].s_all);
+      lse_merge(m_ts, s_ts, parts[c].m_ts, parts[c].s_ts);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      float m2 = __shfl_xor(m_all, o, 64), s2 = __shfl_xor(s_all, o, 64);
+      lse_merge(m_all, s_all, m2, s2);
+      m2 = __shfl_xor(m_ts, o, 64);
+      s2 = __shfl_xor(s_ts, o, 64);
+      lse_merge(m_ts, s_ts, m2, s2);
+    }
+    // top-K of the text list and of the timestamp list over the NC chunk lists (<= 4 entries per lane)
+    Cand top[2][K];
+    for (int l = 0; l < 2; ++l) {
+      Cand mine[4];
+      bool used[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = lane + 64 * q;
+        mine[q] = e < NC * K ? (l == 0 ? parts[e / K].t[e % K] : parts[e / K].s[e % K]) : Cand{-INFINITY, 0x7fffffff};
+        used[q] = false;
+      }
+      for (int r = 0; r < K; ++r) {
+        float bv = -INFINITY;
+        int bi = 0x7fffffff, bq = -1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (!used[q] && cand_better(mine[q].v, mine[q].i, Cand{bv, bi})) {
+            bv = mine[q].v;
+            bi = mine[q].i;
+            bq = q;
+          }
+        int bl = lane;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const float ov = __shfl_xor(bv, o, 64);
+          const int oi = __shfl_xor(bi, o, 64), ol = __shfl_xor(bl, o, 64);
+          if (ov > bv || (ov == bv && (oi < bi || (oi == bi && ol < bl)))) {
+            bv = ov;
+            bi = oi;
+            bl = ol;
+          }
+        }
+        if (lane == bl && bq >= 0) used[bq] = true;
+        top[l][r] = Cand{bv, bi};
+      }
+    }
+    if (lane == 0) {
+      const float lse_all = m_all + __logf(s_all);
+      const float lse_ts = (m_ts == -INFINITY) ? -INFINITY : m_ts + __logf(s_ts);
+      // WhisperTimeStampLogitsProcessor: timestamp mass above every text token -> text tokens -inf
+      const bool fires = p.use_timestamps && lse_ts > top[0][0].v;
+      const float run = bs.run_score[row];
+      int a = 0, bb = 0;
+      for (int k = 0; k < K; ++k) {
+        Cand pick;
+        if (fires) {
+          pick = top[1][bb++];
+        } else if (cand_better(top[0][a].v, top[0][a].i, top[1][bb])) {
+          pick = top[0][a++];
+        } else {
+          pick = top[1][bb++];
+        }
+        rc[wid][k] = Cand{pick.v == -INFINITY ? -INFINITY : run + (pick.v - lse_all), pick.i};
+      }
+    }
+  }
+  // stage the old running histories, finished histories and processor states of the window
+  for (int e = tid; e < nb * TW_BEAM_MAXT; e += blockDim.x) {
+    const int j = e / TW_BEAM_MAXT, q = e % TW_BEAM_MAXT;
+    const int row = w * nb + j;
+    old_tok[j][q] = q < t ? tokens[(size_t)row * ldt + q] : 0;
+    old_fin[j][q] = q < bs.fin_len[row] ? bs.fin_tokens[(size_t)row * ldt + q] : 0;
+  }
+  if (tid < nb * TW_STATE_STRIDE) old_st[tid / TW_STATE_STRIDE][tid % TW_STATE_STRIDE] = state[(w * nb) * TW_STATE_STRIDE + tid];
+  if (tid < nb) old_flen[tid] = bs.fin_len[w * nb + tid];
+  __syncthreads();
+
+  // 2. the window's beam bookkeeping (one thread: nb * K <= 128 candidates)
+  if (tid == 0) {
+    const int V = p.V;
+    float csc[2 * K];
+    // top-K over all beams' candidates by accumulated log-prob; ties -> lower flat index beam * V + token
+    bool taken[TW_BEAM_MAXNB][K];
+    for (int j = 0; j < nb; ++j)
+      for (int k = 0; k < K; ++k) taken[j][k] = false;
+    for (int c = 0; c < K; ++c) {
+      int bj = -1, bk = -1;
+      float bv = -INFINITY;
+      long bf = 0x7fffffffffffffffL;
+      for (int j = 0; j < nb; ++j)
+        for (int k = 0; k < K; ++k) {
+          if (taken[j][k]) continue;
+          const float v = rc[j][k].v;
+          const long f = (long)j * V + rc[j][k].i;
+          if (bj < 0 || v > bv || (v == bv && f < bf)) {
+            bj = j;
+            bk = k;
+            bv = v;
+            bf = f;
+          }
+          break;  // each row list is sorted: only its first untaken entry can win
+        }
+      taken[bj][bk] = true;
+      c_beam[c] = bj;
+      c_tok[c] = rc[bj][bk].i;
+      csc[c] = bv;
+    }
+    bool hits[2 * K];
+    bool all_hit = true;
+    for (int c = 0; c < K; ++c) {
+      hits[c] = c_tok[c] == p.eos || t + 1 >= bp.max_new;
+      all_hit = all_hit && hits[c];
+    }
+    // e. running beams for the next step: best nb of the non-finished continuations
+    float rsc[2 * K];
+    bool rsel[2 * K];
+    for (int c = 0; c < K; ++c) {
+      rsc[c] = csc[c] + (hits[c] ? NEG : 0.f);
+      rsel[c] = false;
+    }
+    for (int j = 0; j < nb; ++j) {
+      int bc = -1;
+      for (int c = 0; c < K; ++c)
+        if (!rsel[c] && (bc < 0 || rsc[c] > rsc[bc])) bc = c;
+      rsel[bc] = true;
+      s_src[j] = c_beam[bc];
+      s_tok[j] = c_tok[bc];
+      s_score[j] = rsc[bc];
+    }
+    // f. finished beams: previous best nb merged with the just-finished top-nb continuations
+    const int unsat_prev = win[0];
+    const float lp_div = __powf((float)(t + 1), bp.length_penalty);
+    float merged[TW_BEAM_MAXNB + 2 * K];
+    for (int q = 0; q < nb; ++q) merged[q] = bs.fin_score[w * nb + q];
+    for (int c = 0; c < K; ++c) {
+      float v = csc[c] / lp_div;
+      if (!unsat_prev) v += NEG;
+      const bool just = hits[c] && c < nb;
+      if (!just) v += NEG;
+      merged[nb + c] = v;
+    }
+    bool msel[TW_BEAM_MAXNB + 2 * K];
+    for (int e = 0; e < nb + K; ++e) msel[e] = false;
+    float min_fin = INFINITY;
+    bool all_fin = true;
+    for (int q = 0; q < nb; ++q) {
+      int be = -1;
+      for (int e = 0; e < nb + K; ++e)
+        if (!msel[e] && (be < 0 || merged[e] > merged[be])) be = e;
+      msel[be] = true;
+      f_from[q] = be;
+      f_score[q] = merged[be];
+      f_flag[q] = be < nb ? bs.fin_flag[w * nb + be] : (hits[be - nb] && be - nb < nb);
+      min_fin = fminf(min_fin, merged[be]);
+      all_fin = all_fin && f_flag[q];
+    }
+    // g. early-stop heuristic (early_stopping=False: best running score at the current length)
+    const float best_possible = s_score[0] / __powf((float)(t + 1), bp.length_penalty);
+    bool any_better = false;
+    for (int q = 0; q < nb; ++q) any_better = any_better || best_possible > (f_flag[q] ? min_fin : NEG);
+    const int unsat = unsat_prev && any_better;
+    win[0] = unsat;
+    win[1] = (!unsat || all_hit) ? 1 : 0;
+    win[2] = t + 1;
+  }
+  __syncthreads();
+
+  // 3. apply: running histories, state, ids, pos, the K/V source rows; finished histories
+  for (int e = tid; e < nb * (t + 1); e += blockDim.x) {
+    const int j = e / (t + 1), q = e % (t + 1);
+    tokens[(size_t)(w * nb + j) * ldt + q] = q < t ? old_tok[s_src[j]][q] : s_tok[j];
+  }
+  for (int e = tid; e < nb * TW_BEAM_MAXT; e += blockDim.x) {
+    const int qs = e / TW_BEAM_MAXT, q = e % TW_BEAM_MAXT;
+    const int from = f_from[qs];
+    int len, v;
+    if (from < nb) {
+      len = old_flen[from];
+      v = q < len ? old_fin[from][q] : 0;
+    } else {
+      const int c = from - nb;
+      len = t + 1;
+      v = q < t ? old_tok[c_beam[c]][q] : c_tok[c];
+    }
+    if (q < len) bs.fin_tokens[(size_t)(w * nb + qs) * ldt + q] = v;
+  }
+  if (tid < nb) {
+    const int j = tid, row = w * nb + j, src = s_src[j], tok = s_tok[j];
+    int* st = state + row * TW_STATE_STRIDE;
+    st[TW_ST_NGEN] = t + 1;
+    st[TW_ST_PENULT] = old_st[src][TW_ST_LAST];
+    st[TW_ST_LAST] = tok;
+    st[TW_ST_LASTTS] = (p.use_timestamps && tok >= p.ts_begin) ? tok : old_st[src][TW_ST_LASTTS];
+    st[TW_ST_FINISHED] = 0;
+    ids[row] = tok;
+    pos[row] += 1;
+    bs.src_rows[row] = w * nb + src;
+    bs.run_score[row] = s_score[j];
+    const int from = f_from[j];
+    bs.fin_score[row] = f_score[j];
+    bs.fin_flag[row] = f_flag[j];
+    bs.fin_len[row] = from < nb ? old_flen[from] : t + 1;
+  }
+}
+
+template <int K>
+static int launch_beam(const float* logits, int W, int ld_logits, const uint32_t* suppress_bits,
+                       const TwSelectParams* p, const TwBeamParams* bp, TwBeamState bs, int* state, int* tokens,
+                       int* ids, int* pos, void* workspace, hipStream_t s) {
+  const int R = W * bp->num_beams;
+  BeamPart<K>* ws = (BeamPart<K>*)workspace;
+  hipLaunchKernelGGL(k_beam_partial<K>, dim3(R, TW_SELECT_CHUNKS), dim3(256), 0, s, logits, ld_logits, suppress_bits,
+                     *p, state, ws);
+  hipLaunchKernelGGL(k_beam_step<K>, dim3(W), dim3(512), 0, s, ws, TW_SELECT_CHUNKS, *p, *bp, bs, state, tokens, ids,
+                     pos);
+  return tw_check_launch("tw_beam_step");
+}
+
+extern "C" size_t tw_beam_workspace_bytes(int rows) {
+  return (size_t)rows * TW_SELECT_CHUNKS * sizeof(BeamPart<2 * TW_BEAM_MAXNB>);
+}
+
+extern "C" int tw_beam_step(const float* logits, int W, int ld_logits, const uint32_t* suppress_bits,
+                            const TwSelectParams* params, const TwBeamParams* bp, const TwBeamState* bs, int* state,
+                            int* tokens, int* ids, int* pos, void* workspace, void* stream) {
+  TW_REQUIRE(logits && params && bp && bs && state && tokens && ids && pos && workspace && W > 0,
+             "tw_beam_step: null argument");
+  TW_REQUIRE(bp->num_beams >= 2 && bp->num_beams <= TW_BEAM_MAXNB, "tw_beam_step: num_beams=%d (2..%d)",
+             bp->num_beams, TW_BEAM_MAXNB);
+  TW_REQUIRE(bp->ld_tokens <= TW_BEAM_MAXT && bp->max_new >= 1 && bp->max_new <= bp->ld_tokens,
+             "tw_beam_step: ld_tokens=%d max_new=%d", bp->ld_tokens, bp->max_new);
+  TW_REQUIRE(params->mode == 0 && params->V <= ld_logits, "tw_beam_step: params");
+  hipStream_t s = (hipStream_t)stream;
+  switch (bp->num_beams) {
+    case 2: return launch_beam<4>(logits, W, ld_logits, suppress_bits, params, bp, *bs, state, tokens, ids, pos, workspace, s);
+    case 3: return launch_beam<6>(logits, W, ld_logits, suppress_bits, params, bp, *bs, state, tokens, ids, pos, workspace, s);
+    case 4: return launch_beam<8>(logits, W, ld_logits, suppress_bits, params, bp, *bs, state, tokens, ids, pos, workspace, s);
+    case 5: return launch_beam<10>(logits, W, ld_logits, suppress_bits, params, bp, *bs, state, tokens, ids, pos, workspace, s);
+    case 6: return launch_beam<12>(logits, W, ld_logits, suppress_bits, params, bp, *bs, state, tokens, ids, pos, workspace, s);
+    case 7: return launch_beam<14>(logits, W, ld_logits, suppress_bits, params, bp, *bs, state, tokens, ids, pos, workspace, s);
+    default: return launch_beam<16>(logits, W, ld_logits, suppress_bits, params, bp, *bs, state, tokens, ids, pos, workspace, s);
+  }
+}
+
+// Self-attention K/V reorder after a beam step: row r continues row src_rows[r]; positions [0, pos[r]) move.
+// Two passes through scratch (same layout as the caches) so a permutation never reads a row it already overwrote.
+__global__ __launch_bounds__(256) void k_kv_reorder(bf16_t* __restrict__ cache, bf16_t* __restrict__ scratch,
+                                                    const int* __restrict__ src_rows, const int* __restrict__ pos,
+                                                    int rows_cap, int H, int T, int phase) {
+  const int r = blockIdx.x, lh = blockIdx.y, l = lh / H, h = lh - l * H;
+  const int s = src_rows[r];
+  if (s == r) return;
+  const int n = pos[r] * 64 / 8;  // uint4 chunks of the valid positions
+  const size_t dst_off = (((size_t)l * rows_cap + r) * H + h) * (size_t)T * 64;
+  const size_t src_off = (((size_t)l * rows_cap + s) * H + h) * (size_t)T * 64;
+  const uint4* from = (const uint4*)(phase == 0 ? cache + src_off : scratch + dst_off);
+  uint4* to = (uint4*)(phase == 0 ? scratch + dst_off : cache + dst_off);
+  for (int e = threadIdx.x; e < n; e += 256) to[e] = from[e];
+}
+
+extern "C" int tw_kv_reorder(uint16_t* k_cache, uint16_t* v_cache, uint16_t* k_scratch, uint16_t* v_scratch, int layers,
+                             int rows_cap, int H, int T, int R, const int* src_rows, const int* pos, void* stream) {
+  TW_REQUIRE(k_cache && v_cache && k_scratch && v_scratch && src_rows && pos && R > 0 && R <= rows_cap,
+             "tw_kv_reorder: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  for (int phase = 0; phase < 2; ++phase) {
+    hipLaunchKernelGGL(k_kv_reorder, dim3(R, layers * H), dim3(256), 0, s, (bf16_t*)k_cache, (bf16_t*)k_scratch,
+                       src_rows, pos, rows_cap, H, T, phase);
+    hipLaunchKernelGGL(k_kv_reorder, dim3(R, layers * H), dim3(256), 0, s, (bf16_t*)v_cache, (bf16_t*)v_scratch,
+                       src_rows, pos, rows_cap, H, T, phase);
+  }
+  return tw_check_launch("tw_kv_reorder");
+}

@@ -35,7 +35,7 @@ EXPORTED = (
     "tw_im2col_conv2", "tw_gemm_bf16", "tw_layernorm", "tw_attn_encoder", "tw_attn_decode_self",
     "tw_attn_decode_cross", "tw_embed_decoder", "tw_logits_select", "tw_gemm_bf16_partial", "tw_resid_layernorm",
     "tw_gemm_set_variant", "tw_attn_set_variant",
-    "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_stream_create_masked", "tw_stream_destroy", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
+    "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_stream_create_masked", "tw_stream_destroy", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
 )
 
 
@@ -46,6 +46,17 @@ class TwSelectParams(ctypes.Structure):
         ("max_new", ctypes.c_int32), ("mode", ctypes.c_int32), ("lo", ctypes.c_int32), ("hi", ctypes.c_int32),
         ("n_begin_suppress", ctypes.c_int32), ("begin_suppress", ctypes.c_int32 * 8),
     ]
+
+
+class TwBeamParams(ctypes.Structure):
+    _fields_ = [("num_beams", ctypes.c_int32), ("max_new", ctypes.c_int32), ("length_penalty", ctypes.c_float),
+                ("ld_tokens", ctypes.c_int32)]
+
+
+class TwBeamState(ctypes.Structure):
+    _fields_ = [("run_score", ctypes.c_void_p), ("fin_score", ctypes.c_void_p), ("fin_flag", ctypes.c_void_p),
+                ("fin_len", ctypes.c_void_p), ("fin_tokens", ctypes.c_void_p), ("win", ctypes.c_void_p),
+                ("src_rows", ctypes.c_void_p)]
 
 
 class TwFlacInfo(ctypes.Structure):
@@ -86,6 +97,10 @@ _SIGS = {
     "tw_gemm_set_variant": ([_I], _I),
     "tw_attn_set_variant": ([_I], _I),
     "tw_resid_layernorm": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
+    "tw_beam_workspace_bytes": ([_I], ctypes.c_size_t),
+    "tw_beam_step": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), ctypes.POINTER(TwBeamParams),
+                      ctypes.POINTER(TwBeamState), _P, _P, _P, _P, _P, _P], _I),
+    "tw_kv_reorder": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P], _I),
     "tw_pack_weight": ([_P, _I, _I, _I, _P, _P], _I),
     "tw_gemv_packed": ([_P, _I, _I, _P, _I, _I, _I, _I, _P, _I, _P, _I, _P], _I),
     "tw_resid_layernorm_packed": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),

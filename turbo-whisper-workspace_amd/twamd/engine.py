@@ -88,7 +88,7 @@ class PassResult:
 
 class WhisperEngine:
     def __init__(self, weights: PackedWeights, gen: GenerationSettings, max_batch: int = 24,
-                 device: str = "cuda", use_graphs: bool = True, dec_cus: Optional[int] = None):
+                 device: str = "cuda", use_graphs: bool = True, dec_cus: Optional[int] = None, max_beams: int = 1):
         _lib.load()
         # kernel-variant overrides for A/B measurement (defaults are the measured-best kernels)
         if os.environ.get("TW_GEMM_VARIANT"):
@@ -99,6 +99,9 @@ class WhisperEngine:
         d.validate()
         self.d, self.w, self.gen = d, weights, gen
         self.max_batch = max_batch
+        # decoder rows: windows x beams (beam search decodes num_beams rows per window against one cross-K/V)
+        self.max_beams = max(1, int(max_beams))
+        self.max_rows = max_batch * self.max_beams
         self.device = torch.device(device)
         self.use_graphs = use_graphs
         # a high-priority decoder stream and a default-priority stream for the front end + encoder: the
@@ -144,8 +147,9 @@ class WhisperEngine:
         self.cross_kv_buf = torch.empty(2, d.decoder_layers, 2, B, H, S_ENC, 64, dtype=bf, device=dev)
         self.cross_kv = self.cross_kv_buf[0]
         self._slot = 0  # slot the decoder reads
-        # decoder state
+        # decoder state (max_rows = max_batch * max_beams rows)
         T = d.max_target_positions
+        B = self.max_rows
         self.kcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=bf, device=dev)
         self.vcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=bf, device=dev)
         self.xd = torch.empty(B, D, dtype=f32, device=dev)
@@ -161,8 +165,11 @@ class WhisperEngine:
         self.tokens = torch.zeros(B, T, dtype=i32, device=dev)
         self.ids = torch.zeros(B, dtype=i32, device=dev)
         self.pos = torch.zeros(B, dtype=i32, device=dev)
-        self.row_map = torch.zeros(B, dtype=i32, device=dev)
-        self.seek = torch.zeros(B, dtype=i32, device=dev)
+        self.row_map = torch.zeros(max_batch, dtype=i32, device=dev)
+        self.seek = torch.zeros(max_batch, dtype=i32, device=dev)
+        self.dec_row_map = torch.zeros(B, dtype=i32, device=dev)  # decoder row -> cross-K/V row (beam search)
+        self._use_dec_row_map = False
+        self._beam: Optional[dict] = None  # beam-search buffers, allocated on first use
         self.suppress_bits = torch.zeros((V + 31) // 32, dtype=torch.int32, device=dev)
         self.set_suppress_tokens(gen.suppress_tokens)
         # concurrent decode chains in the generation loop (measured: two 12-row chains on two streams run no faster
@@ -290,7 +297,7 @@ class WhisperEngine:
             self.stream.wait_stream(self.enc_stream)
 
     def _view(self, r0: int = 0, n: Optional[int] = None, stream=None, parts=None) -> DecView:
-        n = self.max_batch - r0 if n is None else n
+        n = self.max_rows - r0 if n is None else n
         if stream is None and parts is None:  # the default views are cached: graphs capture their buffers
             key = ("view", r0, n)
             if key not in self._chain_cache:
@@ -409,10 +416,9 @@ class WhisperEngine:
             self._partial(v.attd, L.wo, R, D, D, v)
             self._resid_ln(R, DEC_SPLITS, L.bo, L.ln2_g, L.ln2_b, v)
             self._gemm(v.hd, L.wq_x, R, D, D, _lib.TW_EPI_BF16, v.qd, bias=L.bq_x, stream=st)
-            # this layer's [k|v][r_enc][H][S][64] block, advanced to the view's first row (bytes: bf16)
-            ckv = self.cross_kv.data_ptr() + (li * xkv_stride + v.r0 * H * S_ENC * 64) * 2
+            ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
             rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
-            _lib.call("tw_attn_decode_cross", v.qd.data_ptr(), R, H, S_ENC, r_enc, None, ckv, v.attd.data_ptr(), s)
+            _lib.call("tw_attn_decode_cross", v.qd.data_ptr(), R, H, S_ENC, r_enc, rmap, ckv, v.attd.data_ptr(), s)
             self._end_timer(rec, st)
             self._partial(v.attd, L.wo_x, R, D, D, v)
             self._resid_ln(R, DEC_SPLITS, L.bo_x, L.ln3_g, L.ln3_b, v)
@@ -444,9 +450,9 @@ class WhisperEngine:
             self._gemv(v.attd, False, P["wo"], R, D, D, PART, v.parts, v, splits=K4)
             self._resid_ln_p(R, K4, L.bo, L.ln2_g, L.ln2_b, v)
             self._gemv(v.hp, True, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
-            ckv = self.cross_kv.data_ptr() + (li * xkv_stride + v.r0 * H * S_ENC * 64) * 2
+            ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
             rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
-            _lib.call("tw_attn_decode_cross", v.qd.data_ptr(), R, H, S_ENC, r_enc, None, ckv, v.attd.data_ptr(), s)
+            _lib.call("tw_attn_decode_cross", v.qd.data_ptr(), R, H, S_ENC, r_enc, rmap, ckv, v.attd.data_ptr(), s)
             self._end_timer(rec, st)
             self._gemv(v.attd, False, P["wo_x"], R, D, D, PART, v.parts, v, splits=K4)
             self._resid_ln_p(R, K4, L.bo_x, L.ln3_g, L.ln3_b, v)
@@ -456,6 +462,15 @@ class WhisperEngine:
         if with_logits:
             self._resid_ln_p(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
             self._gemv(v.hp, True, self.emb_p, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, v)
+
+    def _cross_ptrs(self, li: int, xkv_stride: int, v: DecView):
+        """This layer's [k|v][r_enc][H][S][64] block and the row map for the view's rows: identity rows start at
+        the view's first row; with beam search every row reads its window's slot through dec_row_map."""
+        H = self.d.heads
+        base = self.cross_kv.data_ptr() + li * xkv_stride * 2
+        if self._use_dec_row_map:
+            return base, self.dec_row_map.data_ptr() + 4 * v.r0
+        return base + v.r0 * H * S_ENC * 64 * 2, None
 
     def _select_params(self, mode: int, max_new: int, use_timestamps: bool = True) -> _lib.TwSelectParams:
         st, g = self.gen.special, self.gen
@@ -540,6 +555,102 @@ class WhisperEngine:
         toks = self.tokens[:R].tolist()
         return PassResult([toks[r][: ngen[r]] for r in range(R)], detected if lang_ids is None else list(lang_ids))
 
+    def _beam_buffers(self, R: int) -> dict:
+        if self._beam is None or self._beam["rows"] < R:
+            dev, d = self.device, self.d
+            T = d.max_target_positions
+            ws_bytes = int(_lib.load().tw_beam_workspace_bytes(self.max_rows))
+            self._beam = {
+                "rows": self.max_rows,
+                "run_score": torch.zeros(self.max_rows, dtype=torch.float32, device=dev),
+                "fin_score": torch.zeros(self.max_rows, dtype=torch.float32, device=dev),
+                "fin_flag": torch.zeros(self.max_rows, dtype=torch.int32, device=dev),
+                "fin_len": torch.zeros(self.max_rows, dtype=torch.int32, device=dev),
+                "fin_tokens": torch.zeros(self.max_rows, T, dtype=torch.int32, device=dev),
+                "win": torch.zeros(self.max_batch, 4, dtype=torch.int32, device=dev),
+                "src_rows": torch.zeros(self.max_rows, dtype=torch.int32, device=dev),
+                "ws": torch.empty(ws_bytes, dtype=torch.uint8, device=dev),
+                "kscr": torch.empty_like(self.kcache),
+                "vscr": torch.empty_like(self.vcache),
+            }
+        return self._beam
+
+    @on_engine_streams
+    def beam_pass(self, W: int, num_beams: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
+                  use_timestamps: bool = True, check_every: int = 8, length_penalty: float = 1.0,
+                  enc_row0: int = 0, r_enc: Optional[int] = None) -> PassResult:
+        """Beam-search decode (GenerationMixin._beam_search, $TF/generation/utils.py:3208-3512) of W windows with
+        num_beams rows each (row = w * num_beams + j, all reading window w's cross-K/V): the prompt as
+        decode_pass (language detected from the SOT step when lang_ids is None), then per token one decoder step
+        over all rows, tw_beam_step and the self-attention K/V reorder. Returns the best finished hypothesis of
+        every window (with its EOS when it ended on one). enc_row0 / r_enc: the windows' first row and the batch
+        the cross-K/V slot was encoded with (default 0 / W)."""
+        nb, R = num_beams, W * num_beams
+        r_enc = W if r_enc is None else r_enc
+        if R > self.max_rows:
+            raise ValueError(f"{W} windows x {nb} beams > {self.max_rows} decoder rows (construct with max_beams)")
+        st = self.gen.special
+        dev = self.device
+        T = self.d.max_target_positions
+        bb = self._beam_buffers(R)
+        self.stream.wait_event(self._enc_ev[self._slot])
+        self.dec_row_map[:R] = enc_row0 + torch.arange(R, dtype=torch.int32, device=dev) // nb
+        self._use_dec_row_map = True
+        try:
+            self.state[:R].zero_()
+            self.state[:R, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
+            self.pos[:R] = 0
+            self.ids[:R] = st.sot
+            detected = None
+            prompt_rest: List = []
+            if st.is_multilingual:
+                prompt_rest.append(None if lang_ids is None else [int(x) for x in lang_ids for _ in range(nb)])
+            prompt_rest.extend(int(t) for t in tail)
+            for k, tok in enumerate(prompt_rest):
+                if k == 0 and st.is_multilingual and lang_ids is None:
+                    self.decoder_step(R, r_enc=r_enc)
+                    self._select(R, self._select_params(1, max_new), tokens=False)  # ids <- lang, pos += 1
+                    detected = self.state[:R:nb, _lib.TW_ST_LANG].tolist()
+                    continue
+                self.decoder_step(R, with_logits=False, r_enc=r_enc)
+                if isinstance(tok, list):
+                    self.ids[:R] = torch.as_tensor(tok, dtype=torch.int32, device=dev)
+                else:
+                    self.ids[:R] = tok
+                self.pos[:R] = k + 1
+            bb["run_score"][:R].view(W, nb).fill_(-1e9)
+            bb["run_score"][:R].view(W, nb)[:, 0] = 0.0
+            bb["fin_score"][:R] = -1e9
+            bb["fin_flag"][:R] = 0
+            bb["fin_len"][:R] = 0
+            bb["win"][:W] = torch.tensor([1, 0, 0, 0], dtype=torch.int32, device=dev)
+            self.state[:R, _lib.TW_ST_NGEN] = 0
+            sel = self._select_params(0, max_new, use_timestamps)
+            bp = _lib.TwBeamParams(nb, max_new, float(length_penalty), T)
+            bst = _lib.TwBeamState(bb["run_score"].data_ptr(), bb["fin_score"].data_ptr(), bb["fin_flag"].data_ptr(),
+                                   bb["fin_len"].data_ptr(), bb["fin_tokens"].data_ptr(), bb["win"].data_ptr(),
+                                   bb["src_rows"].data_ptr())
+            s = self.stream.cuda_stream
+            L, H = self.d.decoder_layers, self.d.heads
+            steps = 0
+            while steps < max_new:
+                self.decoder_step(R, r_enc=r_enc)
+                _lib.call("tw_beam_step", self.logits.data_ptr(), W, self.d.vocab, self.suppress_bits.data_ptr(),
+                          ctypes.byref(sel), ctypes.byref(bp), ctypes.byref(bst), self.state.data_ptr(),
+                          self.tokens.data_ptr(), self.ids.data_ptr(), self.pos.data_ptr(), bb["ws"].data_ptr(), s)
+                _lib.call("tw_kv_reorder", self.kcache.data_ptr(), self.vcache.data_ptr(), bb["kscr"].data_ptr(),
+                          bb["vscr"].data_ptr(), L, self.max_rows, H, T, R, bb["src_rows"].data_ptr(),
+                          self.pos.data_ptr(), s)
+                steps += 1
+                if steps % check_every == 0 or steps >= max_new:
+                    if bool(bb["win"][:W, 1].all().item()):
+                        break
+            flen = bb["fin_len"][:R:nb].tolist()
+            ftok = bb["fin_tokens"][:R:nb].tolist()
+        finally:
+            self._use_dec_row_map = False
+        return PassResult([ftok[w][: flen[w]] for w in range(W)], detected if lang_ids is None else list(lang_ids))
+
     def _chains(self, R: int) -> List[DecView]:
         """Contiguous row ranges of [0, R), one per decode chain (each with its own partial-sum buffer)."""
         key = ("chains", R)
@@ -603,7 +714,7 @@ class WhisperEngine:
     def generate(self, n_chunks: int, task: Optional[str] = "transcribe", lang_ids: Optional[Sequence[int]] = None,
                  max_new_tokens: Optional[int] = None, return_timestamps: bool = True,
                  max_passes: Optional[int] = None, slot: Optional[int] = None,
-                 pre_encoded: bool = False) -> List[List[int]]:
+                 pre_encoded: bool = False, num_beams: int = 1) -> List[List[int]]:
         """Whisper short-form generate() over feats[slot][:n_chunks] (each 3000 frames): language
         detection, the seek loop and segment extraction, returning for every chunk the concatenated
         segment tokens (what generate() returns before padding).
@@ -627,8 +738,11 @@ class WhisperEngine:
         passes = 0
         while any(s < N_FRAMES for s in seek):
             rows = [i for i in range(n_chunks) if seek[i] < N_FRAMES]
-            for b0 in range(0, len(rows), self.max_batch):
-                part = rows[b0: b0 + self.max_batch]
+            per = self.max_batch if num_beams == 1 else min(self.max_batch, self.max_rows // num_beams)
+            if per < 1:
+                raise ValueError(f"num_beams={num_beams} > the engine's {self.max_rows} decoder rows")
+            for b0 in range(0, len(rows), per):
+                part = rows[b0: b0 + per]
                 R = len(part)
                 if not (pre_encoded and passes == 0):
                     self.row_map[:R] = torch.as_tensor(part, dtype=torch.int32, device=self.device)
@@ -636,8 +750,13 @@ class WhisperEngine:
                     self.encode(R)
                 part_langs = [langs[i] for i in part]
                 known = all(lg is not None for lg in part_langs) or not st.is_multilingual
-                res = self.decode_pass(R, tail, part_langs if (known and st.is_multilingual) else None, max_new,
-                                       use_timestamps=return_timestamps)
+                given = part_langs if (known and st.is_multilingual) else None
+                if num_beams > 1:  # pre-encoded first pass: this part's windows sit at encoder rows b0..
+                    pre = pre_encoded and passes == 0
+                    res = self.beam_pass(R, num_beams, tail, given, max_new, use_timestamps=return_timestamps,
+                                         enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R)
+                else:
+                    res = self.decode_pass(R, tail, given, max_new, use_timestamps=return_timestamps)
                 for j, i in enumerate(part):
                     if not known:
                         langs[i] = res.lang_ids[j]

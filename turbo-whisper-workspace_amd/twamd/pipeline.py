@@ -42,7 +42,8 @@ class TurboTranscriber:
     # -------------------------------------------------------------- construction
     @staticmethod
     def from_pretrained(model: str = "large-v3-turbo", checkpoint: Optional[str] = None, seed: int = 1234,
-                        max_batch: int = 24, device: str = "cuda", use_graphs: bool = True) -> "TurboTranscriber":
+                        max_batch: int = 24, device: str = "cuda", use_graphs: bool = True,
+                        max_beams: int = 1) -> "TurboTranscriber":
         """`model`: a preset name (synthetic seeded weights) or, via `checkpoint`, a LOCAL Hugging Face
         Whisper directory (config.json, *.safetensors, vocab.json, generation_config.json)."""
         if checkpoint is None and model not in PRESETS and os.path.isdir(model):
@@ -59,7 +60,7 @@ class TurboTranscriber:
             gen = GenerationSettings.default(dims)
             vocab = WhisperVocab.synthetic(gen.special)
         weights = build_weights(dims, seed=seed, checkpoint=checkpoint)
-        eng = WhisperEngine(weights, gen, max_batch=max_batch, device=device, use_graphs=use_graphs)
+        eng = WhisperEngine(weights, gen, max_batch=max_batch, device=device, use_graphs=use_graphs, max_beams=max_beams)
         return TurboTranscriber(eng, vocab)
 
     # -------------------------------------------------------------- call
@@ -72,9 +73,9 @@ class TurboTranscriber:
             raise ValueError("Whisper cannot return `char` timestamps, only word level or segment level timestamps.")
         gk = dict(generate_kwargs or {})
         gk.update({k: kwargs.pop(k) for k in list(kwargs) if k in ("max_new_tokens", "language", "task", "num_beams")})
-        num_beams = gk.pop("num_beams", 1)
-        if num_beams not in (None, 1):
-            raise NotImplementedError("beam search is not implemented; the engine decodes greedily (num_beams=1)")
+        num_beams = int(gk.pop("num_beams", 1) or 1)
+        if num_beams < 1 or num_beams > 8:
+            raise ValueError(f"num_beams={num_beams}: the engine supports 1 (greedy) to 8 beams")
         task = gk.pop("task", None)
         language = gk.pop("language", None)
         max_new_tokens = gk.pop("max_new_tokens", None)
@@ -108,7 +109,7 @@ class TurboTranscriber:
 
         def run(w, ws):
             return self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=bool(return_timestamps),
-                                           max_new_tokens=max_new_tokens)
+                                           max_new_tokens=max_new_tokens, num_beams=num_beams)
 
         # one window shard per rank + one all-gather of the token arrays (twamd.dist); plain call on 1 GPU
         outputs = dist.transcribe_sharded(run, wav, windows) if world > 1 else run(wav, windows)
@@ -126,7 +127,7 @@ class TurboTranscriber:
 
     def transcribe_windows(self, wav: np.ndarray, windows: Sequence[Window], task: Optional[str],
                            lang_id: Optional[int], return_timestamps: bool,
-                           max_new_tokens: Optional[int] = None) -> List[List[int]]:
+                           max_new_tokens: Optional[int] = None, num_beams: int = 1) -> List[List[int]]:
         """Log-mel + generate for every window; returns per-window token sequences (generate() output,
         right-padded with the pad token within each engine batch, as the HF batch output is). Batches of
         max_batch windows go through WhisperEngine.run_batches: batch k+1 is encoded while batch k decodes."""
@@ -144,7 +145,7 @@ class TurboTranscriber:
 
         res = eng.run_batches([len(p) for p in parts], load=load, task=task,
                               lang_ids=None if lang_id is None else [lang_id] * B, max_new_tokens=max_new_tokens,
-                              return_timestamps=return_timestamps)
+                              return_timestamps=return_timestamps, num_beams=num_beams)
         out: List[List[int]] = []
         for seqs in res:
             out.extend(pad_right(seqs, self.gen.special.eot))
