@@ -126,12 +126,13 @@ class _OracleTranscriber(TurboTranscriber):
                 max_source_positions = 1500
         self.engine = _E()
 
-    def transcribe_windows(self, wav, windows, task, lang_id, return_timestamps, max_new_tokens=None):
+    def transcribe_windows(self, wav, windows, task, lang_id, return_timestamps, max_new_tokens=None, num_beams=1):
         out = []
         for w in windows:
             f = wo.log_mel(wav[w.start: w.start + min(w.length, 480000)], self.n_mels)
             toks, _ = wo.generate(self.m, f, self.g, task=task, language=lang_id,
-                                  return_timestamps=return_timestamps, max_new_tokens=max_new_tokens)
+                                  return_timestamps=return_timestamps, max_new_tokens=max_new_tokens,
+                                  num_beams=num_beams)
             out.append(toks)
         return out
 
