@@ -181,8 +181,9 @@ class WhisperOracle:
             y = y + self.sd[f"{p}.bias"]
         return y
 
-    def _mha(self, xq, xkv, p, k=None, v=None):
-        """Multi-head attention; q scaled by head_dim^-0.5 before QK^T (modeling_whisper.py:309)."""
+    def _mha(self, xq, xkv, p, k=None, v=None, probs_out=None):
+        """Multi-head attention; q scaled by head_dim^-0.5 before QK^T (modeling_whisper.py:309).
+        probs_out: list that receives the attention probabilities [H][T][S]."""
         H, hd = self.H, self.D // self.H
         q = self._lin(xq, f"{p}.q_proj") * (hd ** -0.5)
         if k is None:
@@ -192,7 +193,10 @@ class WhisperOracle:
         qh = q.reshape(T, H, hd).transpose(1, 0, 2)
         kh = k.reshape(S, H, hd).transpose(1, 0, 2)
         vh = v.reshape(S, H, hd).transpose(1, 0, 2)
-        o = _softmax(qh @ kh.transpose(0, 2, 1)) @ vh
+        pr = _softmax(qh @ kh.transpose(0, 2, 1))
+        if probs_out is not None:
+            probs_out.append(pr)
+        o = pr @ vh
         return self._lin(o.transpose(1, 0, 2).reshape(T, self.D), f"{p}.out_proj")
 
     def conv_stem(self, feats: np.ndarray) -> np.ndarray:
@@ -244,7 +248,10 @@ class WhisperOracle:
             x = x + self._mha(h, None, f"{p}.self_attn", kk, vv)
             h = _ln(x, sd[f"{p}.encoder_attn_layer_norm.weight"], sd[f"{p}.encoder_attn_layer_norm.bias"])
             ck, cv = cache["cross"][i]
-            x = x + self._mha(h, None, f"{p}.encoder_attn", ck, cv)
+            rec = [] if "xattn" in cache else None
+            x = x + self._mha(h, None, f"{p}.encoder_attn", ck, cv, probs_out=rec)
+            if rec is not None:  # cross-attention probabilities of this step, [H][S], per layer
+                cache["xattn"].setdefault(t, {})[i] = rec[0][:, 0, :]
             h = _ln(x, sd[f"{p}.final_layer_norm.weight"], sd[f"{p}.final_layer_norm.bias"])
             x = x + self._lin(_gelu(self._lin(h, f"{p}.fc1")), f"{p}.fc2")
         cache["len"] = t + 1
@@ -300,9 +307,12 @@ def _ts_rule_margin(s: np.ndarray, tb: int) -> float:
 
 
 def greedy_pass(model: WhisperOracle, enc: np.ndarray, prompt: Sequence[int], max_new: int, g: GenCfg,
-                use_ts: bool, logits_out: Optional[list] = None) -> List[int]:
-    """_sample for one row: returns the generated tokens (incl. the EOS), or up to max_new."""
+                use_ts: bool, logits_out: Optional[list] = None, xattn: Optional[dict] = None) -> List[int]:
+    """_sample for one row: returns the generated tokens (incl. the EOS), or up to max_new.
+    xattn: dict that receives the cross-attention probabilities of every fed position ({pos: {layer: [H][S]}})."""
     cache = model.new_cache(enc)
+    if xattn is not None:
+        cache["xattn"] = xattn
     for t in prompt[:-1]:
         model.decoder_step(t, cache)
     logits = model.decoder_step(prompt[-1], cache)
@@ -422,6 +432,82 @@ def beam_pass(model: WhisperOracle, enc: np.ndarray, prompt: Sequence[int], max_
     return beam_search_core(logits0, step, len(prompt), max_new, g, use_ts, num_beams, length_penalty)[0]
 
 
+# ----------------------------------------------------------------------------- token-level timestamps
+def median_filter(x: np.ndarray, width: int) -> np.ndarray:
+    """_median_filter ($TF/models/whisper/generation_whisper.py:43-61): reflect-pad the last axis by width//2, the
+    middle of the sorted window (NaN sorts last, as torch.sort)."""
+    pad = width // 2
+    if x.shape[-1] <= pad:
+        return x
+    xp = np.pad(x, [(0, 0)] * (x.ndim - 1) + [(pad, pad)], mode="reflect")
+    win = np.lib.stride_tricks.sliding_window_view(xp, width, axis=-1)
+    return np.sort(win, axis=-1)[..., pad]
+
+
+def dynamic_time_warping(matrix: np.ndarray):
+    """_dynamic_time_warping (generation_whisper.py:64-114), restated: float32 cost table, ties resolved to the
+    horizontal move, backtrace from the corner. Returns (text_indices, time_indices)."""
+    n, m = matrix.shape
+    cost = np.full((n + 1, m + 1), np.inf, np.float32)
+    trace = -np.ones((n + 1, m + 1), np.float32)
+    cost[0, 0] = 0
+    for j in range(1, m + 1):
+        for i in range(1, n + 1):
+            c0, c1, c2 = cost[i - 1, j - 1], cost[i - 1, j], cost[i, j - 1]
+            if c0 < c1 and c0 < c2:
+                c, t = c0, 0
+            elif c1 < c0 and c1 < c2:
+                c, t = c1, 1
+            else:
+                c, t = c2, 2
+            cost[i, j] = matrix[i - 1, j - 1] + c
+            trace[i, j] = t
+    i, j = n, m
+    trace[0, :] = 2
+    trace[:, 0] = 1
+    ti, tj = [], []
+    while i > 0 or j > 0:
+        ti.append(i - 1)
+        tj.append(j - 1)
+        if trace[i, j] == 0:
+            i -= 1
+            j -= 1
+        elif trace[i, j] == 1:
+            i -= 1
+        else:
+            j -= 1
+    return np.array(ti[::-1]), np.array(tj[::-1])
+
+
+def token_timestamps(weights: np.ndarray, num_input_ids: int, num_frames: Optional[int], median_width: int = 7,
+                     time_precision: float = 0.02) -> np.ndarray:
+    """_extract_token_timestamps (generation_whisper.py:241-380) for ONE sequence, num_beams=1.
+    weights: f32 [heads][rows][1500], the alignment heads' cross-attention of every fed token (prompt rows first);
+    returns f32 timestamps of length rows + 1."""
+    heads, rows, _ = weights.shape
+    ts = np.zeros(rows + 1, np.float32)
+    w = weights.astype(np.float32)
+    if num_frames is not None:
+        # generate() passes num_frames as a per-sample tensor (attention_mask.sum - seek): the weights are cropped
+        # once for the batch (:316-323) and once more per sample (:353-354); only a negative value (a seek past the
+        # audio end, e.g. -390 // 2) makes the second crop bite
+        w = w[..., : num_frames // 2]
+        w = w[..., : num_frames // 2]
+    w = w[:, num_input_ids:, :]
+    if w.shape[1] == 0:
+        return ts
+    with np.errstate(invalid="ignore", divide="ignore"):
+        std = w.std(axis=-2, keepdims=True)
+        mean = w.mean(axis=-2, keepdims=True)
+        w = ((w - mean) / std).astype(np.float32)
+    w = median_filter(w, median_width)
+    mat = w.mean(axis=0)
+    text_idx, time_idx = dynamic_time_warping(-mat.astype(np.float64))
+    jumps = np.pad(np.diff(text_idx), (1, 0), constant_values=1).astype(bool)
+    jump_times = time_idx[jumps] * time_precision
+    return np.concatenate([np.zeros(num_input_ids), jump_times, [jump_times[-1]]]).astype(np.float32)
+
+
 def detect_language(model: WhisperOracle, enc: np.ndarray, g: GenCfg) -> int:
     cache = model.new_cache(enc)
     lg = model.decoder_step(g.sot, cache)
@@ -444,9 +530,12 @@ def retrieve_segment(seq, seek_num_frames, tb):
 
 def generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, task: Optional[str] = "transcribe",
              language: Optional[int] = None, return_timestamps: bool = True, max_new_tokens: Optional[int] = None,
-             encoder_cache: Optional[dict] = None, num_beams: int = 1) -> Tuple[List[int], int]:
+             encoder_cache: Optional[dict] = None, num_beams: int = 1, alignment_heads=None,
+             num_frames: Optional[int] = None, median_width: int = 7):
     """Short-form WhisperGenerationMixin.generate for ONE 3000-frame window (greedy, or beam search with
-    num_beams > 1). Returns (final token sequence, language id)."""
+    num_beams > 1). Returns (final token sequence, language id); with alignment_heads (greedy only) also the
+    token-level timestamps of return_token_timestamps=True (the top-level "token_timestamps": every pass's DTW
+    times of the kept tokens, no seek offset; segments add seek * 0.01 s) and per pass the seek offset."""
     feats = np.asarray(feats, np.float32)
 
     def enc_at(seek):
@@ -473,16 +562,30 @@ def generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, task: Optional[
     P = len(prompt)
     max_new = max_new_tokens if max_new_tokens is not None else min(g.max_length + P, 448) - P
     seek, out = 0, []
+    tts: List[float] = []
+    pass_seeks: List[int] = []
     while seek < 3000:
+        xattn = {} if alignment_heads is not None else None
         if num_beams > 1:
             seq = beam_pass(model, enc_at(seek), prompt, max_new, g, return_timestamps, num_beams)
         else:
-            seq = greedy_pass(model, enc_at(seek), prompt, max_new, g, return_timestamps)
+            seq = greedy_pass(model, enc_at(seek), prompt, max_new, g, return_timestamps, xattn=xattn)
+        raw_ts = None
+        if xattn is not None:
+            rows = P + len(seq) - 1  # every fed position: the prompt and all generated tokens but the last
+            w = np.stack([np.stack([xattn[t][l][h] for t in range(rows)]) for l, h in alignment_heads])
+            nf = None if num_frames is None else num_frames - seek
+            raw_ts = token_timestamps(w, P, nf, median_width)
         if seq and seq[-1] == g.eot:
             seq = seq[:-1]
         toks, off = retrieve_segment(seq, 3000 - seek, g.ts_begin)
         out += toks
+        if raw_ts is not None:
+            tts += [float(x) for x in raw_ts[P: P + len(toks)]]
+            pass_seeks += [seek] * len(toks)
         seek += off
+    if alignment_heads is not None:
+        return out, lang, tts, pass_seeks
     return out, lang
 
 

@@ -9,6 +9,9 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
   pipeline.json     AutomaticSpeechRecognitionPipeline outputs with the reference's call kwargs
                     (vocalis/core/audio_pipeline.py:351-358, num_beams=1 for greedy parity) and 30-s mode
   decode_asr.json   tokenizer._decode_asr on seeded random strided token sequences
+  word.npz/.json    token-level timestamps (cross-attention DTW) of generate(return_token_timestamps=True) and
+                    the pipeline's return_timestamps="word" output, plus HF's _median_filter / _dynamic_time_warping
+                    on seeded random matrices
   beam.json         generate(num_beams=5) token sequences (the pipeline's default decode, asr:160-163) of
                     test-mini on three windows, with and without timestamps and with a max_length stop
 
@@ -252,6 +255,50 @@ def make_beam(out):
     with open(os.path.join(out, "beam.json"), "w") as f:
         json.dump({"seed": SEED, "dims": "test-mini", "num_beams": 5, "cases": cases,
                    "pipeline_audio": "speech_like(40,5)+white_noise(35,11)", "pipeline": pcases}, f)
+
+
+ALIGN_HEADS_MINI = [[1, 0], [1, 1], [1, 2], [1, 3]]  # test-mini: every head of the upper half of the decoder
+
+
+def make_word(out):
+    from transformers import AutomaticSpeechRecognitionPipeline, WhisperFeatureExtractor
+    from transformers.models.whisper.generation_whisper import _dynamic_time_warping, _median_filter
+
+    res = {}
+    rng = np.random.default_rng(77)
+    for k, (n, m) in enumerate(((5, 40), (17, 300), (1, 9), (30, 30))):
+        mat = rng.standard_normal((n, m))
+        ti, tj = _dynamic_time_warping(mat)
+        res[f"dtw{k}_in"], res[f"dtw{k}_text"], res[f"dtw{k}_time"] = mat, ti, tj
+    x = rng.standard_normal((2, 3, 11, 50)).astype(np.float32)
+    res["median_in"], res["median_out"] = x, _median_filter(torch.from_numpy(x), 7).numpy()
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    m.generation_config.alignment_heads = ALIGN_HEADS_MINI
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    cl = clips()
+    for name in ("speech30", "noise12"):
+        f = fe(cl[name], sampling_rate=16000, return_tensors="pt", return_attention_mask=True)
+        with torch.no_grad():
+            o = m.generate(f["input_features"], attention_mask=f["attention_mask"], task="transcribe",
+                           return_timestamps=True, return_token_timestamps=True, max_new_tokens=40)
+        res[f"gen_{name}_seq"] = o["sequences"].numpy()
+        res[f"gen_{name}_ts"] = o["token_timestamps"].numpy()
+    np.savez_compressed(os.path.join(out, "word.npz"), **res)
+    tk = hf_tokenizer(gen.special)
+    pipe = AutomaticSpeechRecognitionPipeline(model=m, feature_extractor=fe, tokenizer=tk, device=-1)
+    audio = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)])  # 75 s
+    cases = []
+    for name, x, kw in (("single_20s", audio[: 20 * 16000], {}),
+                        ("mode_30_0", audio, dict(chunk_length_s=30, stride_length_s=0, batch_size=8))):
+        r = pipe(x.copy(), generate_kwargs={"task": "transcribe", "num_beams": 1, "max_new_tokens": 40},
+                 return_timestamps="word", **kw)
+        cases.append({"name": name, "kwargs": kw, "n_samples": int(len(x)), "output": _jsonable(r)})
+    with open(os.path.join(out, "word.json"), "w") as f:
+        json.dump({"seed": SEED, "dims": "test-mini", "alignment_heads": ALIGN_HEADS_MINI,
+                   "audio": "speech_like(40,5)+white_noise(35,11)", "cases": cases}, f)
 
 
 def _jsonable(x):

@@ -106,3 +106,25 @@ def test_beam_search_matches_transformers(oracle_model, gcfg, case):
         while ref and ref[-1] == gcfg.eot:
             ref = ref[:-1]
         assert got == ref, (name, got[:20], ref[:20])
+
+
+def test_dtw_and_median_filter_match_transformers():
+    z = np.load(os.path.join(G, "word.npz"))
+    for k in range(4):
+        ti, tj = wo.dynamic_time_warping(z[f"dtw{k}_in"])
+        assert np.array_equal(ti, z[f"dtw{k}_text"]) and np.array_equal(tj, z[f"dtw{k}_time"])
+    np.testing.assert_array_equal(wo.median_filter(z["median_in"], 7), z["median_out"])
+
+
+@pytest.mark.parametrize("name", ["speech30", "noise12"])
+def test_token_timestamps_match_transformers(oracle_model, gcfg, name):
+    """generate(return_token_timestamps=True): cross-attention of the alignment heads -> normalise -> median filter
+    -> DTW, per seek pass (tests/golden/word.npz)."""
+    z = np.load(os.path.join(G, "word.npz"))
+    x = _clips()[name]
+    feats = wo.log_mel(x[:480000], D.n_mels)
+    nf = min(480000, len(x)) // 160 + (1 if min(480000, len(x)) % 160 else 0)
+    toks, _, tts, _ = wo.generate(oracle_model, feats, gcfg, task="transcribe", return_timestamps=True,
+                                  max_new_tokens=40, alignment_heads=[(1, 0), (1, 1), (1, 2), (1, 3)], num_frames=nf)
+    assert toks == z[f"gen_{name}_seq"][0].tolist()
+    np.testing.assert_allclose(tts, z[f"gen_{name}_ts"][0], atol=1e-6)
