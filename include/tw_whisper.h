@@ -202,6 +202,17 @@ int tw_attn_decode_self(const uint16_t* qkv, int B, int H, int max_pos, const in
  * cross_kv bf16[2][Bt][H][S][64]; row b reads slot row_map[b] (NULL = b). */
 int tw_attn_decode_cross(const uint16_t* q, int B, int H, int S, int Bt, const int* row_map, const uint16_t* cross_kv,
                          uint16_t* out, void* stream);
+/* The same plus the attention probabilities of selected heads (token-level timestamps, the cross_attentions of
+ * WhisperGenerationMixin._extract_token_timestamps, $TF/models/whisper/generation_whisper.py:241-380):
+ * probs f32[B][n_steps][n_slots][S] receives, for every head h with bit h of head_mask set (H <= 32), row b's
+ * probabilities at step pos[b] - pos0 into slot slot0 + (set bits of head_mask below h), when 0 <= step < n_steps. */
+int tw_attn_decode_cross_probs(const uint16_t* q, int B, int H, int S, int Bt, const int* row_map,
+                               const uint16_t* cross_kv, uint16_t* out, float* probs, uint32_t head_mask, int slot0,
+                               int n_slots, const int* pos, int pos0, int n_steps, void* stream);
+/* Host memory: dynamic time warping of matrix f64[n][m] (the cost, i.e. minus the smoothed attention) as
+ * _dynamic_time_warping (generation_whisper.py:64-114); text_idx / time_idx int32[n + m] receive the path,
+ * *path_len its length. */
+int tw_dtw(const double* matrix, int n, int m, int* text_idx, int* time_idx, int* path_len);
 
 /* ---- decoder glue --------------------------------------------------------------------------- */
 /* x f32[B][D] = embed_tokens[ids[b]] + embed_positions[pos[b]] (modeling_whisper.py:737,753-762). */

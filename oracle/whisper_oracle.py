@@ -307,10 +307,14 @@ def _ts_rule_margin(s: np.ndarray, tb: int) -> float:
 
 
 def greedy_pass(model: WhisperOracle, enc: np.ndarray, prompt: Sequence[int], max_new: int, g: GenCfg,
-                use_ts: bool, logits_out: Optional[list] = None, xattn: Optional[dict] = None) -> List[int]:
+                use_ts: bool, logits_out: Optional[list] = None, xattn: Optional[dict] = None,
+                cache_out: Optional[list] = None) -> List[int]:
     """_sample for one row: returns the generated tokens (incl. the EOS), or up to max_new.
-    xattn: dict that receives the cross-attention probabilities of every fed position ({pos: {layer: [H][S]}})."""
+    xattn: dict that receives the cross-attention probabilities of every fed position ({pos: {layer: [H][S]}}).
+    cache_out: receives the row's KV cache (a batch keeps feeding pad tokens to finished rows)."""
     cache = model.new_cache(enc)
+    if cache_out is not None:
+        cache_out.append(cache)
     if xattn is not None:
         cache["xattn"] = xattn
     for t in prompt[:-1]:
@@ -587,6 +591,79 @@ def generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, task: Optional[
     if alignment_heads is not None:
         return out, lang, tts, pass_seeks
     return out, lang
+
+
+def generate_batch_word(model: WhisperOracle, feats_list: Sequence[np.ndarray], g: GenCfg, alignment_heads,
+                        num_frames: Sequence[int], task: Optional[str] = "transcribe", language: Optional[int] = None,
+                        max_new_tokens: Optional[int] = None, median_width: int = 7, forced=None):
+    """generate(return_timestamps=True, return_token_timestamps=True) over a BATCH of windows (greedy), as the
+    ASR pipeline's batched forward runs it: every seek pass decodes the batch's active rows together, and
+    _extract_token_timestamps runs over the pass's padded batch -- rows that hit EOS keep being fed the pad
+    token (= EOS) until the longest row ends, and those pad positions take part in the per-head standardization
+    over tokens. ($TF/models/whisper/generation_whisper.py:241-400 over the batch of generate_with_fallback.)
+    Returns per window (segment tokens, language id, token timestamps incl. the seek offsets).
+
+    forced: optional per window (language id, [raw tokens of every seek pass]) of a device decode; the passes are
+    then teacher-forced instead of decoded greedily (token-level timestamps of the device's own tokens, for inputs
+    where bf16 took the other side of a greedy near-tie)."""
+    n = len(feats_list)
+    feats_list = [np.asarray(f, np.float32) for f in feats_list]
+
+    def enc_at(i, seek):
+        seg = np.zeros_like(feats_list[i])
+        seg[:, : 3000 - seek] = feats_list[i][:, seek:]
+        return model.encode(seg)
+
+    langs: List[Optional[int]] = [None] * n
+    prompts = []
+    for i in range(n):
+        prompt = [g.sot]
+        if g.multilingual:
+            if forced is not None:
+                langs[i] = forced[i][0]
+            else:
+                langs[i] = language if language is not None else detect_language(model, enc_at(i, 0), g)
+            prompt.append(langs[i])
+            prompt.append(g.transcribe if (task or "transcribe") == "transcribe" else g.translate)
+        prompts.append(prompt)
+    P = len(prompts[0])
+    max_new = max_new_tokens if max_new_tokens is not None else min(g.max_length + P, 448) - P
+    seek = [0] * n
+    outs: List[List[int]] = [[] for _ in range(n)]
+    tts: List[List[float]] = [[] for _ in range(n)]
+    npass = [0] * n
+    while any(s < 3000 for s in seek):
+        act = [i for i in range(n) if seek[i] < 3000]
+        seqs, xs, caches = {}, {}, {}
+        for i in act:
+            xs[i], co = {}, []
+            if forced is not None:
+                raw = list(forced[i][1][npass[i]])
+                raw = raw[: raw.index(g.eot) + 1] if g.eot in raw else raw
+                cache = model.new_cache(enc_at(i, seek[i]))
+                cache["xattn"] = xs[i]
+                for t in prompts[i] + raw[:-1]:
+                    model.decoder_step(t, cache)
+                seqs[i], caches[i] = raw, cache
+            else:
+                seqs[i] = greedy_pass(model, enc_at(i, seek[i]), prompts[i], max_new, g, True, xattn=xs[i],
+                                      cache_out=co)
+                caches[i] = co[0]
+            npass[i] += 1
+        L = max(len(seqs[i]) for i in act)
+        rows = P + L - 1
+        for i in act:  # pad rows: the finished row is fed EOS (its own last token, then the pad token)
+            for _ in range(L - len(seqs[i])):
+                model.decoder_step(g.eot, caches[i])
+            w = np.stack([np.stack([xs[i][t][l][h] for t in range(rows)]) for l, h in alignment_heads])
+            raw_ts = token_timestamps(w, P, num_frames[i] - seek[i], median_width)
+            seq = seqs[i][:-1] if seqs[i][-1] == g.eot else seqs[i]
+            toks, off = retrieve_segment(seq, 3000 - seek[i], g.ts_begin)
+            outs[i] += toks
+            o = np.float32(seek[i] * 0.02 / 2)
+            tts[i] += [float(np.float32(x) + o) for x in raw_ts[P: P + len(toks)]]
+            seek[i] += off
+    return [(outs[i], langs[i], tts[i]) for i in range(n)]
 
 
 # ----------------------------------------------------------------------------- tolerant greedy replay

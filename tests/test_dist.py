@@ -35,6 +35,12 @@ def fake_windows(wav, windows):
     return out
 
 
+def fake_timed_windows(wav, windows):
+    """(tokens, per-token float32 times) pairs, as the word-timestamp path returns them."""
+    return [(t, [float(np.float32(0.02 * (i + 1) + 1e-3 * (j % 7))) for i in range(len(t))])
+            for j, t in enumerate(fake_windows(wav, windows))]
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -55,7 +61,8 @@ def _worker(rank, ws, port, n_samples, chunk, stride, q):
         langs = [None] * len(windows)
         lo, hi = twd.shard_range(len(windows), ws, rank)
         g_seqs, g_langs = twd.gather_tokens(seqs[lo:hi], [rank] * (hi - lo), len(windows))
-        q.put((rank, seqs, g_langs, float(wav.sum())))
+        timed = twd.transcribe_sharded(fake_timed_windows, wav, windows, timed=True)
+        q.put((rank, seqs, g_langs, float(wav.sum()), timed))
     finally:
         dist.destroy_process_group()
 
@@ -78,9 +85,15 @@ def test_two_rank_gather_equals_single_process(n_samples, chunk, stride):
     windows = list(chunk_windows(len(wav), chunk, stride, 16000))
     ref = fake_windows(wav, windows)
     sizes = twd.shard_sizes(len(windows), 2)
-    for rank, seqs, g_langs, wsum in res:
+    sizes = twd.shard_sizes(len(windows), 2)
+    ref_timed = []
+    for r in range(2):  # each rank's stand-in numbers its windows from 0
+        lo, hi = twd.shard_range(len(windows), 2, r)
+        ref_timed += fake_timed_windows(wav, windows[lo:hi])
+    for rank, seqs, g_langs, wsum, timed in res:
         assert wsum == pytest.approx(float(wav.sum()))
         assert seqs == ref
+        assert timed == ref_timed  # float32 times travel bit-exactly
         assert g_langs == [0] * sizes[0] + [1] * sizes[1]
     # the stitched transcript is the single-process one
     vocab = WhisperVocab.synthetic(ST)

@@ -126,7 +126,21 @@ class _OracleTranscriber(TurboTranscriber):
                 max_source_positions = 1500
         self.engine = _E()
 
-    def transcribe_windows(self, wav, windows, task, lang_id, return_timestamps, max_new_tokens=None, num_beams=1):
+    def transcribe_windows(self, wav, windows, task, lang_id, return_timestamps, max_new_tokens=None, num_beams=1,
+                           word_timestamps=False, num_frames=None):
+        if word_timestamps:  # batches of `word_batch` windows, as the HF pipeline's batch_size groups them
+            out, self.last_window_token_timestamps = [], []
+            B = getattr(self, "word_batch", 1)
+            heads = getattr(self, "alignment_heads", None) or self.gen.alignment_heads
+            for b0 in range(0, len(windows), B):
+                feats = [wo.log_mel(wav[w.start: w.start + min(w.length, 480000)], self.n_mels)
+                         for w in windows[b0: b0 + B]]
+                for toks, _, tts in wo.generate_batch_word(self.m, feats, self.g, heads, num_frames[b0: b0 + B],
+                                                           task=task, language=lang_id,
+                                                           max_new_tokens=max_new_tokens):
+                    out.append(toks)
+                    self.last_window_token_timestamps.append(tts)
+            return out
         out = []
         for w in windows:
             f = wo.log_mel(wav[w.start: w.start + min(w.length, 480000)], self.n_mels)
@@ -146,4 +160,19 @@ def test_pipeline_host_flow_matches_transformers_pipeline():
         xx = x if case["name"] != "short_nochunk" else x[: 20 * 16000]
         r = tr(xx, generate_kwargs={"task": "transcribe", "num_beams": 1, "max_new_tokens": 40},
                return_timestamps=True, **case["kwargs"])
+        assert json.loads(json.dumps(r)) == case["output"], case["name"]
+
+
+@pytest.mark.slow
+def test_pipeline_word_timestamps_host_flow_matches_transformers():
+    """return_timestamps="word" through the host flow (num_frames per window, per-token times, LCS merge with
+    times, word collation) with the batched oracle as the model: equals the transformers ASR pipeline output."""
+    gold = json.load(open(os.path.join(G, "word.json")))
+    tr = _OracleTranscriber(PRESETS["test-mini"])
+    tr.alignment_heads = [tuple(h) for h in gold["alignment_heads"]]
+    x = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)])
+    for case in gold["cases"]:
+        tr.word_batch = case["kwargs"].get("batch_size", 1)
+        r = tr(x[: case["n_samples"]], generate_kwargs={"task": "transcribe", "num_beams": 1, "max_new_tokens": 40},
+               return_timestamps="word", **case["kwargs"])
         assert json.loads(json.dumps(r)) == case["output"], case["name"]

@@ -450,9 +450,30 @@ __global__ __launch_bounds__(256) void k_attn_decode_self(const bf16_t* __restri
 
 // Cross-attention step: q [B][D] bf16 (pre-scaled); cross K/V layout [kv][Bt][H][S][64] for this layer,
 // batch row b reads block row_map[b] (the encoder batch slot holding that row's audio window).
+extern "C" int tw_attn_decode_self(const bf16_t* qkv, int B, int H, int max_pos, const int* pos, bf16_t* k_cache,
+                                   bf16_t* v_cache, bf16_t* out, void* stream) {
+  TW_REQUIRE(qkv && pos && k_cache && v_cache && out && B > 0 && H > 0, "tw_attn_decode_self: bad args");
+  TW_REQUIRE(max_pos <= DA_MAXK, "tw_attn_decode_self: max_pos %d > %d", max_pos, DA_MAXK);
+  hipLaunchKernelGGL(k_attn_decode_self, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos, pos,
+                     k_cache, v_cache, out);
+  return tw_check_launch("tw_attn_decode_self");
+}
+
+// Optional output for token-level timestamps (return_timestamps="word"): the attention probabilities of the
+// alignment heads, probs[b][pos[b] - pos0][slot][S] f32 for the heads whose bit is set in head_mask (slot = slot0 +
+// the set bits below h), written only for 0 <= pos[b] - pos0 < n_steps (the generated tokens as they are fed back).
+struct XProbs {
+  float* probs;
+  const int* pos;
+  unsigned head_mask;
+  int slot0, n_slots, pos0, n_steps;
+};
+
+template <bool PROBS>
 __global__ __launch_bounds__(256) void k_attn_decode_cross(const bf16_t* __restrict__ q, int D, int S, int Bt,
                                                            const int* __restrict__ row_map,
-                                                           const bf16_t* __restrict__ ckv, bf16_t* __restrict__ out) {
+                                                           const bf16_t* __restrict__ ckv, bf16_t* __restrict__ out,
+                                                           XProbs xp) {
   TW_DEC_PRIO();
   __shared__ float sc[DA_MAXK];
   __shared__ float part[32 * 64];
@@ -467,21 +488,36 @@ __global__ __launch_bounds__(256) void k_attn_decode_cross(const bf16_t* __restr
   const bf16_t* V = ckv + (((size_t)1 * Bt + slot) * H + h) * S * 64;
   dec_attend(qf, K, V, S, sc, part, red, outv);
   if (threadIdx.x < 64) out[(size_t)b * D + h * 64 + threadIdx.x] = f32_to_bf16(outv[threadIdx.x]);
-}
-
-extern "C" int tw_attn_decode_self(const bf16_t* qkv, int B, int H, int max_pos, const int* pos, bf16_t* k_cache,
-                                   bf16_t* v_cache, bf16_t* out, void* stream) {
-  TW_REQUIRE(qkv && pos && k_cache && v_cache && out && B > 0 && H > 0, "tw_attn_decode_self: bad args");
-  TW_REQUIRE(max_pos <= DA_MAXK, "tw_attn_decode_self: max_pos %d > %d", max_pos, DA_MAXK);
-  hipLaunchKernelGGL(k_attn_decode_self, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos, pos,
-                     k_cache, v_cache, out);
-  return tw_check_launch("tw_attn_decode_self");
+  if constexpr (PROBS) {
+    if ((xp.head_mask >> h) & 1u) {
+      const int k = xp.pos[b] - xp.pos0;
+      if (k >= 0 && k < xp.n_steps) {
+        const int sl = xp.slot0 + __popc(xp.head_mask & ((1u << h) - 1u));
+        const float inv = 1.f / (red[4] + red[5] + red[6] + red[7]);  // dec_attend's softmax denominator
+        float* dst = xp.probs + (((size_t)b * xp.n_steps + k) * xp.n_slots + sl) * S;
+        for (int i = threadIdx.x; i < S; i += 256) dst[i] = sc[i] * inv;
+      }
+    }
+  }
 }
 
 extern "C" int tw_attn_decode_cross(const bf16_t* q, int B, int H, int S, int Bt, const int* row_map,
                                     const bf16_t* cross_kv, bf16_t* out, void* stream) {
   TW_REQUIRE(q && cross_kv && out && B > 0 && H > 0 && S > 0 && S <= DA_MAXK, "tw_attn_decode_cross: bad args");
-  hipLaunchKernelGGL(k_attn_decode_cross, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt, row_map,
-                     cross_kv, out);
+  hipLaunchKernelGGL(k_attn_decode_cross<false>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt,
+                     row_map, cross_kv, out, XProbs{});
   return tw_check_launch("tw_attn_decode_cross");
+}
+
+extern "C" int tw_attn_decode_cross_probs(const bf16_t* q, int B, int H, int S, int Bt, const int* row_map,
+                                          const bf16_t* cross_kv, bf16_t* out, float* probs, uint32_t head_mask,
+                                          int slot0, int n_slots, const int* pos, int pos0, int n_steps,
+                                          void* stream) {
+  TW_REQUIRE(q && cross_kv && out && probs && pos && B > 0 && H > 0 && H <= 32 && S > 0 && S <= DA_MAXK,
+             "tw_attn_decode_cross_probs: bad args");
+  TW_REQUIRE(slot0 >= 0 && slot0 + __builtin_popcount(head_mask) <= n_slots && n_steps > 0,
+             "tw_attn_decode_cross_probs: slots");
+  hipLaunchKernelGGL(k_attn_decode_cross<true>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt,
+                     row_map, cross_kv, out, XProbs{probs, pos, head_mask, slot0, n_slots, pos0, n_steps});
+  return tw_check_launch("tw_attn_decode_cross_probs");
 }

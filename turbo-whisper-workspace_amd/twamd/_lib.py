@@ -35,7 +35,7 @@ EXPORTED = (
     "tw_im2col_conv2", "tw_gemm_bf16", "tw_layernorm", "tw_attn_encoder", "tw_attn_decode_self",
     "tw_attn_decode_cross", "tw_embed_decoder", "tw_logits_select", "tw_gemm_bf16_partial", "tw_resid_layernorm",
     "tw_gemm_set_variant", "tw_attn_set_variant",
-    "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_stream_create_masked", "tw_stream_destroy", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
+    "tw_dtw", "tw_attn_decode_cross_probs", "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_stream_create_masked", "tw_stream_destroy", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
 )
 
 
@@ -97,6 +97,8 @@ _SIGS = {
     "tw_gemm_set_variant": ([_I], _I),
     "tw_attn_set_variant": ([_I], _I),
     "tw_resid_layernorm": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
+    "tw_dtw": ([_P, _I, _I, _P, _P, _P], _I),
+    "tw_attn_decode_cross_probs": ([_P, _I, _I, _I, _I, _P, _P, _P, _P, _U32, _I, _I, _P, _I, _I, _P], _I),
     "tw_beam_workspace_bytes": ([_I], ctypes.c_size_t),
     "tw_beam_step": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), ctypes.POINTER(TwBeamParams),
                       ctypes.POINTER(TwBeamState), _P, _P, _P, _P, _P, _P], _I),

@@ -12,7 +12,7 @@ from __future__ import annotations
 import dataclasses
 import json
 import os
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 # Whisper language codes in token order (<|en|> = first language token). 99 for v1/v2 vocabularies,
 # the v3 vocabulary (51866) adds "yue" as the 100th.
@@ -131,6 +131,10 @@ class GenerationSettings:
     max_length: int = 448
     max_new_tokens: Optional[int] = None
     num_beams: int = 1
+    # token-level timestamps (return_timestamps="word"): cross-attention heads used for DTW and the median filter
+    # width (generation_config.alignment_heads, config.median_filter_width)
+    alignment_heads: Optional[List[Tuple[int, int]]] = None
+    median_filter_width: int = 7
 
     @staticmethod
     def default(dims: WhisperDims) -> "GenerationSettings":
@@ -140,8 +144,11 @@ class GenerationSettings:
         # The synthetic default keeps that structure with a short symbol list.
         sym = [1, 2, 7, 8, 9, 10, 14, 25, 26, 27, 28, 29, 31, 58, 59, 60, 61, 62, 63, 90, 91, 92, 93]
         ctrl = [st.translate, st.transcribe, st.startoflm, st.startofprev, st.nospeech]
+        # no published alignment heads for synthetic weights: every head of the upper half of the decoder (the
+        # default of openai/whisper's model.py when a checkpoint ships none)
+        heads = [(l, h) for l in range(dims.decoder_layers // 2, dims.decoder_layers) for h in range(dims.heads)]
         return GenerationSettings(special=st, suppress_tokens=sorted(set(sym + [st.sot] + ctrl)),
-                                  begin_suppress_tokens=[220, st.eot])
+                                  begin_suppress_tokens=[220, st.eot], alignment_heads=heads)
 
     @staticmethod
     def from_checkpoint(path: str, dims: WhisperDims) -> "GenerationSettings":
@@ -156,4 +163,10 @@ class GenerationSettings:
                 gs.begin_suppress_tokens = list(cfg["begin_suppress_tokens"])
             gs.max_initial_timestamp_index = cfg.get("max_initial_timestamp_index", gs.max_initial_timestamp_index)
             gs.max_length = cfg.get("max_length", gs.max_length)
+            if cfg.get("alignment_heads"):
+                gs.alignment_heads = [(int(a), int(b)) for a, b in cfg["alignment_heads"]]
+        cfn = os.path.join(path, "config.json")
+        if os.path.exists(cfn):
+            with open(cfn) as f:
+                gs.median_filter_width = int(json.load(f).get("median_filter_width", gs.median_filter_width))
         return gs

@@ -117,15 +117,22 @@ def broadcast_waveform(wav: Optional[np.ndarray], device: Optional[torch.device]
 
 
 def transcribe_sharded(run_windows, wav: np.ndarray, windows: Sequence, device: Optional[torch.device] = None,
-                       group=None) -> List[List[int]]:
+                       group=None, timed: bool = False) -> List:
     """Every rank calls this with the same `windows` (chunk_iter windows over `wav`); each rank runs
     `run_windows(wav, windows[lo:hi]) -> List[List[int]]` on its own shard, then the results are all-gathered
-    into the global window order."""
+    into the global window order. `timed`: run_windows returns (tokens, per-token times) pairs (word
+    timestamps); the times are gathered too and the pairs are returned."""
     rank, ws = world()
     lo, hi = shard_range(len(windows), ws, rank)
     local = run_windows(wav, list(windows[lo:hi])) if hi > lo else []
-    seqs, _ = gather_tokens(local, None, len(windows), device=device, group=group)
-    return seqs
+    if not timed:
+        seqs, _ = gather_tokens(local, None, len(windows), device=device, group=group)
+        return seqs
+    # word timestamps: (tokens, per-token float32 times); the times travel as their int32 bit patterns
+    seqs, _ = gather_tokens([t for t, _ in local], None, len(windows), device=device, group=group)
+    bits = [np.asarray(ts, dtype=np.float32).view(np.int32).tolist() for _, ts in local]
+    tsb, _ = gather_tokens(bits, None, len(windows), device=device, group=group)
+    return [(s, np.asarray(b, dtype=np.int32).view(np.float32).tolist()) for s, b in zip(seqs, tsb)]
 
 
 class RankZeroFrontend:

@@ -21,7 +21,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, alignment
 from .config import GenerationSettings, WhisperDims
 from .frontend import CHUNK_SAMPLES, N_FRAMES, dft_basis, mel_table
 from .segments import retrieve_segment, strip_generated
@@ -84,6 +84,7 @@ class DecView:
 class PassResult:
     tokens: List[List[int]]      # generated tokens per row (as _sample returns them, before stripping)
     lang_ids: Optional[List[int]]
+    token_ts: Optional[List[np.ndarray]] = None  # per row, token-level times (prompt zeros first; word timestamps)
 
 
 class WhisperEngine:
@@ -170,6 +171,8 @@ class WhisperEngine:
         self.dec_row_map = torch.zeros(B, dtype=i32, device=dev)  # decoder row -> cross-K/V row (beam search)
         self._use_dec_row_map = False
         self._beam: Optional[dict] = None  # beam-search buffers, allocated on first use
+        self._align: Optional[dict] = None  # token-level timestamps: alignment-head attention recording
+        self._align_buf: Optional[torch.Tensor] = None
         self.suppress_bits = torch.zeros((V + 31) // 32, dtype=torch.int32, device=dev)
         self.set_suppress_tokens(gen.suppress_tokens)
         # concurrent decode chains in the generation loop (measured: two 12-row chains on two streams run no faster
@@ -418,7 +421,7 @@ class WhisperEngine:
             self._gemm(v.hd, L.wq_x, R, D, D, _lib.TW_EPI_BF16, v.qd, bias=L.bq_x, stream=st)
             ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
             rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
-            _lib.call("tw_attn_decode_cross", v.qd.data_ptr(), R, H, S_ENC, r_enc, rmap, ckv, v.attd.data_ptr(), s)
+            self._cross_attend(li, R, r_enc, rmap, ckv, v)
             self._end_timer(rec, st)
             self._partial(v.attd, L.wo_x, R, D, D, v)
             self._resid_ln(R, DEC_SPLITS, L.bo_x, L.ln3_g, L.ln3_b, v)
@@ -452,7 +455,7 @@ class WhisperEngine:
             self._gemv(v.hp, True, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
             ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
             rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
-            _lib.call("tw_attn_decode_cross", v.qd.data_ptr(), R, H, S_ENC, r_enc, rmap, ckv, v.attd.data_ptr(), s)
+            self._cross_attend(li, R, r_enc, rmap, ckv, v)
             self._end_timer(rec, st)
             self._gemv(v.attd, False, P["wo_x"], R, D, D, PART, v.parts, v, splits=K4)
             self._resid_ln_p(R, K4, L.bo_x, L.ln3_g, L.ln3_b, v)
@@ -462,6 +465,47 @@ class WhisperEngine:
         if with_logits:
             self._resid_ln_p(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
             self._gemv(v.hp, True, self.emb_p, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, v)
+
+    def _cross_attend(self, li: int, R: int, r_enc: int, rmap, ckv, v: DecView) -> None:
+        """Cross-attention of the view's rows; with token-level timestamps requested (self._align) the alignment
+        heads of this layer also write their attention probabilities."""
+        H, s = self.d.heads, v.stream.cuda_stream
+        al = self._align
+        if al is not None and li in al["layers"]:
+            mask, slot0 = al["layers"][li]
+            row_stride = al["n_steps"] * al["n_slots"] * S_ENC * 4
+            _lib.call("tw_attn_decode_cross_probs", v.qd.data_ptr(), R, H, S_ENC, r_enc, rmap, ckv, v.attd.data_ptr(),
+                      al["buf"].data_ptr() + v.r0 * row_stride, mask, slot0, al["n_slots"], v.pos.data_ptr(),
+                      al["pos0"], al["n_steps"], s)
+        else:
+            _lib.call("tw_attn_decode_cross", v.qd.data_ptr(), R, H, S_ENC, r_enc, rmap, ckv, v.attd.data_ptr(), s)
+
+    def _align_setup(self, R: int, pos0: int, n_steps: int) -> None:
+        heads = self.gen.alignment_heads
+        if not heads:
+            raise ValueError("token-level timestamps need generation alignment_heads")
+        layers: Dict[int, tuple] = {}
+        slot = 0
+        for li in sorted({l for l, _ in heads}):
+            hs = sorted({h for l, h in heads if l == li})
+            layers[li] = (sum(1 << h for h in hs), slot)
+            slot += len(hs)
+        order = [(l, h) for l in sorted(layers) for h in sorted({hh for ll, hh in heads if ll == l})]
+        shape = (self.max_rows, n_steps, slot, S_ENC)
+        buf = self._align_buf if getattr(self, "_align_buf", None) is not None else None
+        if buf is None or buf.numel() < int(np.prod(shape)):
+            buf = torch.empty(int(np.prod(shape)), dtype=torch.float32, device=self.device)
+            self._align_buf = buf
+        # slot order inside the buffer -> the order of generation_config.alignment_heads
+        perm = [order.index((l, h)) for l, h in heads]
+        self._align = {"layers": layers, "n_slots": slot, "pos0": pos0, "n_steps": n_steps, "buf": buf, "perm": perm}
+
+    def _align_weights(self, R: int, n_rows: int) -> np.ndarray:
+        """f32 [R][alignment heads][n_rows][S] of the generated tokens fed so far (steps 0 .. n_rows-1)."""
+        al = self._align
+        b = al["buf"][: R * al["n_steps"] * al["n_slots"] * S_ENC].view(R, al["n_steps"], al["n_slots"], S_ENC)
+        w = b[:, :n_rows].permute(0, 2, 1, 3)[:, al["perm"]].float().cpu().numpy()
+        return w
 
     def _cross_ptrs(self, li: int, xkv_stride: int, v: DecView):
         """This layer's [k|v][r_enc][H][S][64] block and the row map for the view's rows: identity rows start at
@@ -499,10 +543,31 @@ class WhisperEngine:
 
     @on_engine_streams
     def decode_pass(self, R: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
-                    check_every: int = 8, use_timestamps: bool = True) -> PassResult:
+                    check_every: int = 8, use_timestamps: bool = True, align: bool = False,
+                    num_frames: Optional[Sequence[int]] = None) -> PassResult:
         """Greedy decode of R rows from the prompt [SOT, (lang), *tail] (the init tokens of
         _retrieve_init_tokens; the language is detected from the SOT step when lang_ids is None on a
-        multilingual model). Returns the generated tokens of every row."""
+        multilingual model). Returns the generated tokens of every row; with align, also every row's token-level
+        timestamps (alignment-head cross-attention of the fed tokens -> DTW; num_frames: the rows' valid frames
+        minus their seek, as generate() passes them)."""
+        if align:
+            P = 1 + (1 if self.gen.special.is_multilingual else 0) + len(tail)
+            self._align_setup(R, P, max_new)
+            try:
+                res = self.decode_pass(R, tail, lang_ids, max_new, check_every, use_timestamps)
+                st = self.gen.special
+                real = [(t.index(st.eot) + 1) if st.eot in t else len(t) for t in res.tokens]
+                rows = max(real) - 1 if real else 0
+                w = self._align_weights(R, rows) if rows > 0 else None
+                res.token_ts = []
+                for r in range(R):
+                    nf = None if num_frames is None else int(num_frames[r])
+                    ts = (alignment.token_timestamps(w[r], 0, nf, self.gen.median_filter_width) if w is not None
+                          else np.zeros(1, np.float32))
+                    res.token_ts.append(np.concatenate([np.zeros(P, np.float32), ts]))
+                return res
+            finally:
+                self._align = None
         st = self.gen.special
         dev = self.device
         self.stream.wait_event(self._enc_ev[self._slot])  # the cross-K/V of this slot is written
@@ -669,7 +734,9 @@ class WhisperEngine:
         return self._chain_cache[key]
 
     def _graph_for(self, R: int, params, i: int, v: DecView) -> Optional[torch.cuda.CUDAGraph]:
-        key = (R, params.max_new, params.use_timestamps, self._slot, i)
+        al = self._align
+        key = (R, params.max_new, params.use_timestamps, self._slot, i,
+               None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()))
         g = self._graphs.get(key)
         if g is not None:
             return g
@@ -714,7 +781,8 @@ class WhisperEngine:
     def generate(self, n_chunks: int, task: Optional[str] = "transcribe", lang_ids: Optional[Sequence[int]] = None,
                  max_new_tokens: Optional[int] = None, return_timestamps: bool = True,
                  max_passes: Optional[int] = None, slot: Optional[int] = None,
-                 pre_encoded: bool = False, num_beams: int = 1) -> List[List[int]]:
+                 pre_encoded: bool = False, num_beams: int = 1, word_timestamps: bool = False,
+                 num_frames: Optional[Sequence[int]] = None) -> List[List[int]]:
         """Whisper short-form generate() over feats[slot][:n_chunks] (each 3000 frames): language
         detection, the seek loop and segment extraction, returning for every chunk the concatenated
         segment tokens (what generate() returns before padding).
@@ -735,6 +803,11 @@ class WhisperEngine:
         # language: given, or detected on the first pass (seek == 0, the whole 30-s window) as
         # _retrieve_init_tokens -> detect_language does before the seek loop
         langs: List[Optional[int]] = list(lang_ids)[:n_chunks] if lang_ids is not None else [None] * n_chunks
+        if word_timestamps and num_beams > 1:
+            raise NotImplementedError("word-level timestamps with beam search are not implemented (greedy only)")
+        # word timestamps: per chunk the segments' token times (segment token_timestamps of generate(), i.e. the
+        # pass's DTW times of the kept tokens + seek * 0.01 s); num_frames: the chunks' valid feature frames
+        tts: List[List[float]] = [[] for _ in range(n_chunks)]
         passes = 0
         while any(s < N_FRAMES for s in seek):
             rows = [i for i in range(n_chunks) if seek[i] < N_FRAMES]
@@ -751,12 +824,14 @@ class WhisperEngine:
                 part_langs = [langs[i] for i in part]
                 known = all(lg is not None for lg in part_langs) or not st.is_multilingual
                 given = part_langs if (known and st.is_multilingual) else None
+                nf_part = None if num_frames is None else [int(num_frames[i]) - seek[i] for i in part]
                 if num_beams > 1:  # pre-encoded first pass: this part's windows sit at encoder rows b0..
                     pre = pre_encoded and passes == 0
                     res = self.beam_pass(R, num_beams, tail, given, max_new, use_timestamps=return_timestamps,
                                          enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R)
                 else:
-                    res = self.decode_pass(R, tail, given, max_new, use_timestamps=return_timestamps)
+                    res = self.decode_pass(R, tail, given, max_new, use_timestamps=return_timestamps,
+                                           align=word_timestamps, num_frames=nf_part)
                 for j, i in enumerate(part):
                     if not known:
                         langs[i] = res.lang_ids[j]
@@ -764,6 +839,10 @@ class WhisperEngine:
                     seq = strip_generated(res.tokens[j], st.eot)
                     seg_tokens, offset = retrieve_segment(seq, seek[i], N_FRAMES - seek[i], st.timestamp_begin)
                     segs[i].extend(seg_tokens)
+                    if word_timestamps:
+                        raw = res.token_ts[j][prompt_len: prompt_len + len(seg_tokens)]
+                        off = np.float32(seek[i] * 0.02 / 2)  # time_offset = seek * time_precision / input_stride
+                        tts[i].extend(float(np.float32(x) + off) for x in raw)
                     seek[i] += offset
             passes += 1
             if max_passes is not None and passes >= max_passes:
@@ -772,10 +851,12 @@ class WhisperEngine:
                 raise RuntimeError("seek loop made no progress")
         self.last_langs = langs
         self.last_passes = passes_raw
+        self.last_token_timestamps = tts if word_timestamps else None
         return segs
 
     @on_engine_streams
-    def run_batches(self, sizes: Sequence[int], load=None, **gen_kwargs) -> List[List[List[int]]]:
+    def run_batches(self, sizes: Sequence[int], load=None, batch_kwargs: Optional[Sequence[dict]] = None,
+                    **gen_kwargs) -> List[List[List[int]]]:
         """generate() over consecutive window batches with a two-slot software pipeline: while batch k decodes on
         the decoder stream, batch k+1's log-mel + encoder + cross-K/V run on enc_stream into the other slot.
         sizes[k] = windows in batch k (<= max_batch); load(k) fills wave[:sizes[k]] for batch k (queued on
@@ -795,6 +876,7 @@ class WhisperEngine:
         out = []
         self.batch_langs = []
         self.batch_passes = []
+        self.batch_token_timestamps = []
         overlap = os.environ.get("TW_OVERLAP", "1") != "0"  # 0: encoder and decoder strictly in turn (A/B)
         if sizes:
             prefetch(0)
@@ -804,8 +886,10 @@ class WhisperEngine:
                 prefetch(k)
             if overlap and k + 1 < len(sizes):
                 prefetch(k + 1)  # runs beside the decode of batch k
-            out.append(self.generate(n, slot=k % 2, pre_encoded=True, **gen_kwargs))
+            kw = dict(gen_kwargs, **(batch_kwargs[k] if batch_kwargs else {}))
+            out.append(self.generate(n, slot=k % 2, pre_encoded=True, **kw))
             self.batch_langs.append(self.last_langs)
             self.batch_passes.append(self.last_passes)
+            self.batch_token_timestamps.append(self.last_token_timestamps)
         self.use_slot(0)
         return out

@@ -67,8 +67,7 @@ class TurboTranscriber:
     def __call__(self, inputs: Union[str, bytes, np.ndarray, dict], *, chunk_length_s: float = 0,
                  stride_length_s=None, batch_size: int = 1, generate_kwargs: Optional[Dict[str, Any]] = None,
                  return_timestamps: Union[bool, str] = False, return_language: bool = False, **kwargs) -> dict:
-        if return_timestamps == "word":
-            raise NotImplementedError("word-level timestamps (cross-attention DTW) are not on the GPU path yet")
+        word = return_timestamps == "word"
         if return_timestamps == "char":
             raise ValueError("Whisper cannot return `char` timestamps, only word level or segment level timestamps.")
         gk = dict(generate_kwargs or {})
@@ -76,6 +75,8 @@ class TurboTranscriber:
         num_beams = int(gk.pop("num_beams", 1) or 1)
         if num_beams < 1 or num_beams > 8:
             raise ValueError(f"num_beams={num_beams}: the engine supports 1 (greedy) to 8 beams")
+        if word and num_beams > 1:
+            raise NotImplementedError("word-level timestamps with beam search are not implemented (greedy only)")
         task = gk.pop("task", None)
         language = gk.pop("language", None)
         max_new_tokens = gk.pop("max_new_tokens", None)
@@ -108,26 +109,38 @@ class TurboTranscriber:
             lang_id = lt[tok]
 
         def run(w, ws):
+            if word:  # token times ride along as floats after the tokens (one all-gather carries both)
+                nf = [min(x.length, CHUNK_SAMPLES) // 160 + (1 if min(x.length, CHUNK_SAMPLES) % 160 else 0)
+                      for x in ws]
+                toks = self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=True,
+                                               max_new_tokens=max_new_tokens, num_beams=num_beams,
+                                               word_timestamps=True, num_frames=nf)
+                return [(t, ts) for t, ts in zip(toks, self.last_window_token_timestamps)]
             return self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=bool(return_timestamps),
                                            max_new_tokens=max_new_tokens, num_beams=num_beams)
 
         # one window shard per rank + one all-gather of the token arrays (twamd.dist); plain call on 1 GPU
-        outputs = dist.transcribe_sharded(run, wav, windows) if world > 1 else run(wav, windows)
+        outputs = dist.transcribe_sharded(run, wav, windows, timed=word) if world > 1 else run(wav, windows)
         model_outputs = []
         for w, toks in zip(windows, outputs):
-            o = {"tokens": toks}
+            if word:
+                toks, tts = toks
+                o = {"tokens": toks, "token_timestamps": tts}
+            else:
+                o = {"tokens": toks}
             if with_stride:
                 sr = self.sampling_rate
                 o["stride"] = (w.length / sr, w.stride_left / sr, w.stride_right / sr)
             model_outputs.append(o)
-        text, optional = decode_asr(self.vocab, model_outputs, return_timestamps=bool(return_timestamps),
+        text, optional = decode_asr(self.vocab, model_outputs, return_timestamps="word" if word else bool(return_timestamps),
                                     return_language=return_language,
                                     time_precision=time_precision(self.engine.d.max_source_positions))
         return {"text": text, **optional}
 
     def transcribe_windows(self, wav: np.ndarray, windows: Sequence[Window], task: Optional[str],
                            lang_id: Optional[int], return_timestamps: bool,
-                           max_new_tokens: Optional[int] = None, num_beams: int = 1) -> List[List[int]]:
+                           max_new_tokens: Optional[int] = None, num_beams: int = 1, word_timestamps: bool = False,
+                           num_frames: Optional[Sequence[int]] = None) -> List[List[int]]:
         """Log-mel + generate for every window; returns per-window token sequences (generate() output,
         right-padded with the pad token within each engine batch, as the HF batch output is). Batches of
         max_batch windows go through WhisperEngine.run_batches: batch k+1 is encoded while batch k decodes."""
@@ -143,7 +156,11 @@ class TurboTranscriber:
                 host[j, : len(seg)] = seg
             eng.wave[: len(part)].copy_(torch.from_numpy(host))
 
-        res = eng.run_batches([len(p) for p in parts], load=load, task=task,
+        bkw = None
+        if word_timestamps:
+            bkw = [{"word_timestamps": True, "num_frames": list(num_frames[b0: b0 + B])}
+                   for b0 in range(0, len(windows), B)]
+        res = eng.run_batches([len(p) for p in parts], load=load, batch_kwargs=bkw, task=task,
                               lang_ids=None if lang_id is None else [lang_id] * B, max_new_tokens=max_new_tokens,
                               return_timestamps=return_timestamps, num_beams=num_beams)
         out: List[List[int]] = []
@@ -152,6 +169,8 @@ class TurboTranscriber:
         # per-window record of the last call (languages, raw tokens of every seek pass) for diagnostics/tests
         self.last_window_langs = [lg for bl in eng.batch_langs for lg in bl]
         self.last_window_passes = [p for bp in eng.batch_passes for p in bp]
+        if word_timestamps:  # per window the concatenated segments' token times (not padded, as the pipeline's)
+            self.last_window_token_timestamps = [t for bt in eng.batch_token_timestamps for t in bt]
         return out
 
 

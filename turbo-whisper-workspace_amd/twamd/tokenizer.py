@@ -136,12 +136,19 @@ class WhisperVocab:
         return "".join(out)
 
 
-def find_longest_common_sequence(sequences: List[List[int]]) -> List[int]:
-    """Greedy overlap merge of consecutive token runs (the pipeline's stride stitching)."""
+def find_longest_common_sequence(sequences: List[List[int]], token_timestamp_sequences=None):
+    """Greedy overlap merge of consecutive token runs (the pipeline's stride stitching,
+    $TF/models/whisper/tokenization_whisper.py:1153-1270). With token_timestamp_sequences (word timestamps) a match
+    also needs the left token's (start, end) <= the right one's, the timestamps are split the same way, and the
+    result is (tokens, timestamps)."""
     left = sequences[0]
     left_len = len(left)
     total: List[int] = []
-    for right in sequences[1:]:
+    with_ts = bool(token_timestamp_sequences)
+    if with_ts:
+        left_ts = token_timestamp_sequences[0]
+        total_ts: list = []
+    for seq_idx, right in enumerate(sequences[1:]):
         best = 0.0
         best_idx = (left_len, left_len, 0, 0)
         right_len = len(right)
@@ -151,7 +158,12 @@ def find_longest_common_sequence(sequences: List[List[int]]) -> List[int]:
             eps = i / 10000.0
             ls, le = max(0, left_len - i), min(left_len, left_len + right_len - i)
             rs, re_ = max(0, i - left_len), min(right_len, i)
-            matches = int(np.sum(la[ls:le] == ra[rs:re_])) if le > ls else 0
+            if with_ts:
+                rts = token_timestamp_sequences[seq_idx + 1]
+                matches = sum(1 for k in range(le - ls)
+                              if left[ls + k] == right[rs + k] and tuple(left_ts[ls + k]) <= tuple(rts[rs + k]))
+            else:
+                matches = int(np.sum(la[ls:le] == ra[rs:re_])) if le > ls else 0
             matching = matches / i + eps
             if matches > 1 and matching > best:
                 best = matching
@@ -162,13 +174,104 @@ def find_longest_common_sequence(sequences: List[List[int]]) -> List[int]:
         total.extend(left[:lmid])
         left = right[rmid:]
         left_len = len(left)
+        if with_ts:
+            total_ts.extend(left_ts[:lmid])
+            left_ts = token_timestamp_sequences[seq_idx + 1][rmid:]
     total.extend(left)
-    return total
+    if token_timestamp_sequences is None:
+        return total
+    if with_ts:
+        total_ts.extend(left_ts)
+        return total, total_ts
+    return total, []
 
 
-def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps: bool, return_language: bool = False,
+_PUNCT = "!\"#$%&'()*+,-./:;<=>?@[\\]^_`{|}~"
+
+
+def _split_tokens_on_unicode(vocab: "WhisperVocab", tokens: List[int]):
+    """tokenization_whisper.py:1315-1344: cut wherever the decoded prefix is complete unicode."""
+    decoded_full = vocab.decode(tokens)
+    rep = "\ufffd"
+    words, word_tokens, token_indices = [], [], []
+    cur, cur_idx = [], []
+    offset = 0
+    for k, tok in enumerate(tokens):
+        cur.append(tok)
+        cur_idx.append(k)
+        dec = vocab.decode(cur)
+        if rep not in dec or offset + dec.index(rep) >= len(decoded_full) or decoded_full[offset + dec.index(rep)] == rep:
+            words.append(dec)
+            word_tokens.append(cur)
+            token_indices.append(cur_idx)
+            cur, cur_idx = [], []
+            offset += len(dec)
+    return words, word_tokens, token_indices
+
+
+def _split_tokens_on_spaces(vocab: "WhisperVocab", tokens: List[int]):
+    """:1347-1368: subwords start a new word on a leading space, a punctuation mark or a special token."""
+    subwords, sub_tokens, sub_idx = _split_tokens_on_unicode(vocab, tokens)
+    words, word_tokens, token_indices = [], [], []
+    for sw, stoks, sidx in zip(subwords, sub_tokens, sub_idx):
+        special = stoks[0] >= vocab.special.eot
+        if special or sw.startswith(" ") or sw.strip() in _PUNCT or not words:
+            words.append(sw)
+            word_tokens.append(list(stoks))
+            token_indices.append(list(sidx))
+        else:
+            words[-1] = words[-1] + sw
+            word_tokens[-1].extend(stoks)
+            token_indices[-1].extend(sidx)
+    return words, word_tokens, token_indices
+
+
+def _merge_punctuations(words, tokens, indices, prepended="\"'“¡¿([{-", appended="\"'.。,，!！?？:：”)]}、"):
+    """:1371-1404."""
+    i, j = len(words) - 2, len(words) - 1
+    while i >= 0:
+        if words[i].startswith(" ") and words[i].strip() in prepended:
+            words[j] = words[i] + words[j]
+            tokens[j] = tokens[i] + tokens[j]
+            indices[j] = indices[i] + indices[j]
+            words[i], tokens[i], indices[i] = "", [], []
+        else:
+            j = i
+        i -= 1
+    i, j = 0, 1
+    while j < len(words):
+        if not words[i].endswith(" ") and words[j] in appended:
+            words[i] += words[j]
+            tokens[i] += tokens[j]
+            indices[i] += indices[j]
+            words[j], tokens[j], indices[j] = "", [], []
+        else:
+            i = j
+        j += 1
+    words[:] = [w for w in words if w]
+    tokens[:] = [t for t in tokens if t]
+    indices[:] = [x for x in indices if x]
+
+
+def collate_word_timestamps(vocab: "WhisperVocab", tokens: List[int], token_timestamps, language: Optional[str],
+                            return_language: bool) -> List[dict]:
+    """_collate_word_timestamps + _combine_tokens_into_words (:1273-1312)."""
+    language = language or "english"
+    if language in {"chinese", "japanese", "thai", "lao", "myanmar", "cantonese"}:
+        words, wtoks, idx = _split_tokens_on_unicode(vocab, tokens)
+    else:
+        words, wtoks, idx = _split_tokens_on_spaces(vocab, tokens)
+    _merge_punctuations(words, wtoks, idx)
+    extra = {"language": language} if return_language else {}
+    return [{"text": w, "timestamp": (token_timestamps[ix[0]][0], token_timestamps[ix[-1]][1]), **extra}
+            for w, ix in zip(words, idx)]
+
+
+def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps, return_language: bool = False,
                time_precision: float = 0.02, segment_size: int = 1500) -> Tuple[str, dict]:
-    """outputs: [{"tokens": [ids...], "stride": (chunk_len_s, left_s, right_s) optional}, ...] in chunk order."""
+    """outputs: [{"tokens": [ids...], "stride": (chunk_len_s, left_s, right_s) optional,
+    "token_timestamps": [s...] (return_timestamps="word")}, ...] in chunk order."""
+    word = return_timestamps == "word"
     st = vocab.special
     last_language = None
 
@@ -180,6 +283,7 @@ def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps: 
     time_offset = 0.0
     timestamp_begin = st.timestamp_begin
     previous_tokens: List[List[int]] = []
+    previous_token_timestamps: list = []
     skip = False
     right_stride_start = None
     special_ids = vocab.all_special_ids
@@ -188,6 +292,7 @@ def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps: 
         # _strip_prompt: a leading <|startofprev|> prompt is cut up to <|startoftranscript|>
         if token_ids and token_ids[0] == st.startofprev:
             token_ids = token_ids[token_ids.index(st.sot):] if st.sot in token_ids else []
+        token_timestamps = list(output["token_timestamps"]) if word else None
         last_timestamp = None
         first_timestamp = timestamp_begin
         cur_max_timestamp = 0.0
@@ -206,6 +311,7 @@ def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps: 
                             break
                         last_timestamp = token
         current_tokens: List[int] = []
+        current_token_timestamps: list = []
         for i, token in enumerate(token_ids):
             if token in special_ids:
                 text = vocab.id_to_token[token][2:-2]
@@ -247,25 +353,41 @@ def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps: 
                     else:
                         chunk["timestamp"][1] = time
                         previous_tokens.append(current_tokens)
-                        resolved = find_longest_common_sequence(previous_tokens)
+                        if word:
+                            previous_token_timestamps.append(current_token_timestamps)
+                        resolved, resolved_ts = find_longest_common_sequence(previous_tokens, previous_token_timestamps)
                         chunk["text"] = vocab.decode(resolved)
+                        if word:
+                            chunk["words"] = collate_word_timestamps(vocab, resolved, resolved_ts, last_language,
+                                                                     return_language)
                         chunks.append(chunk)
                         previous_tokens = []
                         current_tokens = []
+                        previous_token_timestamps = []
+                        current_token_timestamps = []
                         chunk = new_chunk()
             else:
                 current_tokens.append(token)
+                if word:
+                    start = round(0.0 + time_offset, 2) if i == 0 else round(token_timestamps[i - 1] + time_offset, 2)
+                    current_token_timestamps.append((start, round(token_timestamps[i] + time_offset, 2)))
         if "stride" in output:
             time_offset += chunk_len - stride_right
         if current_tokens:
             previous_tokens.append(current_tokens)
+            if word:
+                previous_token_timestamps.append(current_token_timestamps)
         elif not any(p for p in previous_tokens):
             chunk = new_chunk()
             previous_tokens = []
             current_tokens = []
+            previous_token_timestamps = []
+            current_token_timestamps = []
     if previous_tokens:
-        resolved = find_longest_common_sequence(previous_tokens)
+        resolved, resolved_ts = find_longest_common_sequence(previous_tokens, previous_token_timestamps)
         chunk["text"] = vocab.decode(resolved)
+        if word:
+            chunk["words"] = collate_word_timestamps(vocab, resolved, resolved_ts, last_language, return_language)
         chunks.append(chunk)
     full_text = "".join(c["text"] for c in chunks)
     if return_timestamps or return_language:
@@ -276,7 +398,10 @@ def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps: 
                 c["timestamp"] = tuple(c["timestamp"])
             if not return_language:
                 c.pop("language")
-        optional = {"chunks": chunks}
+        if word:
+            optional = {"chunks": [w for c in chunks for w in c["words"]]}
+        else:
+            optional = {"chunks": chunks}
     else:
         optional = {}
     return full_text, optional
