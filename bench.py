@@ -27,6 +27,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense bf16
+FP8_DENSE_PEAK_TFLOPS = 5000.0    # MI355X_MICROARCH.md: ~5 PF dense fp8 (MX-scaled e4m3)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -35,7 +36,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=24)
+    ap.add_argument("--config", choices=("c2", "c5"), default="c2",
+                    help="c2: bf16, 24 windows/GPU (BASELINE configs[1]); c5: MX fp8 encoder + bf16 decoder, "
+                         "64 windows/GPU (configs[4])")
+    ap.add_argument("--batch", type=int, default=0, help="windows per GPU (default 24 for c2, 64 for c5)")
     ap.add_argument("--decode-tokens", type=int, default=128)
     ap.add_argument("--model", default="large-v3-turbo")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -60,9 +64,12 @@ def main():
 
     dims = PRESETS[a.model]
     gen = GenerationSettings.default(dims)
-    B, T = a.batch, a.decode_tokens
+    fp8 = a.config == "c5"
+    B, T = (a.batch or (64 if fp8 else 24)), a.decode_tokens
     w = build_weights(dims, seed=1234)
-    eng = WhisperEngine(w, gen, max_batch=B, device=f"cuda:{local}")
+    eng = WhisperEngine(w, gen, max_batch=B, device=f"cuda:{local}", enc_fp8=fp8)
+    dom = "gemm_mx" if fp8 else "gemm_big"
+    peak = FP8_DENSE_PEAK_TFLOPS if fp8 else BF16_DENSE_PEAK_TFLOPS
     eng.set_suppress_tokens(list(gen.suppress_tokens) + [gen.special.eot])  # fixed decode length
     audio = workload(B, 30.0, seed=1234 + 1000 * rank)
     eng.wave[:B].copy_(torch.from_numpy(audio))
@@ -82,7 +89,7 @@ def main():
         dist.barrier()
     # HIP events around every launch of the dominant kernel (k_gemm_big) on the engine stream, inside the
     # timed region (the encoder is not graph-captured; ~0.3 us per event against 0.2-1 ms per launch)
-    eng.timers, eng.timer_families = {}, {"gemm_big"}
+    eng.timers, eng.timer_families = {}, {dom}
     t0 = time.perf_counter()
     seqs = run(a.steps)
     torch.cuda.synchronize()
@@ -113,11 +120,11 @@ def main():
     families = {f"{k[0]}<{k[1]}>": {"launches": v[0], "tflop": round(v[1] / 1e12, 3), "ms": round(v[2], 3),
                                     "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 1) if v[2] > 0 else None}
                 for k, v in fam.items()}
-    traffic, traffic_src = measured_traffic("k_gemm_big")
+    traffic, traffic_src = measured_traffic("k_" + dom, fp8)
 
     # secondary (HBM-bound) kernel: decoder cross-attention, timed on one eager decode pass outside the timed
     # region (the timed decode steps replay a hipGraph, which has no room for events)
-    dec = decode_cross_roofline(eng, B, traffic_lookup=measured_traffic("k_attn_decode_cross"))
+    dec = decode_cross_roofline(eng, B, traffic_lookup=measured_traffic("k_attn_decode_cross", fp8))
 
     out = {
         "metric": "real-time factor (audio-sec/wall-sec) Whisper-v3-turbo, 30s chunks, 1/2/4/8 GPU",
@@ -130,15 +137,18 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "fp8-e4m3 (MX) encoder projections + bf16" if fp8 else "bf16",
         "data": "synthetic (seeded speech-like 16 kHz audio, 10% silent windows; seeded synthetic weights)",
-        "config": {"workload": f"whisper-{a.model} bf16, batch={B} x 30s windows per GPU, greedy, "
+        "config": {"workload": f"whisper-{a.model} {'MX-fp8 encoder + bf16 decoder' if fp8 else 'bf16'}, "
+                               f"batch={B} x 30s windows per GPU, greedy, "
                                f"{T} new tokens/window (EOS suppressed), timestamps on, language detected",
                    "global_batch": world * B, "seq_len": 3000, "parallelism": f"chunk-dp{world}",
                    "decode_tokens_per_window": T, "mean_tokens_out": float(np.mean(n_tok))},
-        "roofline": {"bound": "mfma", "kernel": "k_gemm_big (all encoder/conv/cross-KV projections, bf16 MFMA)",
-                     "achieved": round(achieved, 1), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": traffic,
+        "roofline": {"bound": "mfma",
+                     "kernel": ("k_gemm_mx (encoder q/k/v/o + fc1/fc2, MX fp8 MFMA)" if fp8 else
+                                "k_gemm_big (all encoder/conv/cross-KV projections, bf16 MFMA)"),
+                     "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": traffic,
                      "traffic_source": traffic_src, "launches_per_step": n_l // a.steps,
                      "avg_launch_ms": round(avg_ms, 4), "flop_per_launch": work / n_l},
         "roofline_decode": dec,
@@ -153,12 +163,14 @@ def main():
         dist.destroy_process_group()
 
 
-def measured_traffic(kernel: str):
+def measured_traffic(kernel: str, c5: bool = False):
     """HBM bytes per launch of `kernel` from the newest rocprofv3 PMC summary under profiles/
-    (scripts/summarize_prof.py: 2*FETCH_SIZE + WRITE_SIZE per launch), or (None, None)."""
+    (scripts/summarize_prof.py: 2*FETCH_SIZE + WRITE_SIZE per launch), or (None, None). Config-5 runs
+    (--config c5) write *_c5_traffic.json; each config reads only its own."""
     import glob
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json")), key=os.path.getmtime)
+    files = [f for f in files if ("_c5_" in os.path.basename(f)) == c5]
     for f in reversed(files):
         try:
             with open(f) as fh:

@@ -33,6 +33,7 @@ extern "C" {
 #define TW_EPI_F32 4          /* out f32 = acc + bias                        (proj_out logits)  */
 #define TW_EPI_CROSSKV 5      /* out bf16 scattered to [layer][k|v][b][head][s][64]             */
 #define TW_EPI_GELU_PACKED 6  /* tw_gemv_packed: out = packed activation (below) of gelu(acc+bias) (fc1 -> fc2) */
+#define TW_EPI_GELU_MX 7      /* tw_gemm_mx: out fp8 e4m3[M][ldo] + e8m0 scales of gelu(acc+bias) (fc1 -> fc2) */
 #define TW_EPI_PARTIAL_F32 100 /* tw_gemv_packed: out f32[splits][M][ldo] split-K partials (no bias)          */
 
 /* Decoder per-row state (tw_logits_select), int32[TW_STATE_STRIDE] per batch row. */
@@ -121,6 +122,26 @@ int tw_resid_layernorm(float* x, const float* parts, int nparts, const float* bi
  * :371,377,434,443,446,573,682). */
 int tw_layernorm(const float* x, const float* gamma, const float* beta, int M, int D, float eps, uint16_t* out,
                  void* stream);
+
+/* ---- MX fp8 encoder (BASELINE config 5: fp8 MFMA encoder + bf16 decoder) --------------------- */
+/* MX block format: e4m3fn elements [rows][K] (row-major bytes), e8m0 scales [K/128][rows_pad][4] bytes (byte
+ * (k/32)%4 of row r's dword for K-step k/128; rows_pad >= rows, a multiple of 256 for GEMM operands). Scale
+ * s = E - 8 + (absmax mantissa > 1.75) (E = biased f32 exponent of the 32-block's absmax; s = 1 for E < 9),
+ * element = e4m3_rne(clamp(x * 2^(127-s), +-448)). The arithmetic they replace is the same nn.Linear of the encoder as tw_gemm_bf16
+ * (modeling_whisper.py:279-282,309 q/k/v/o, :375-376 fc1/fc2), at reduced operand precision. */
+/* C = A . W^T on v_mfma_scale_f32_16x16x128_f8f6f4, f32 accumulate. K % 128 == 0, lda/ldw in bytes (% 16),
+ * Mp / Np the scale row pads of A / W (multiples of 256). epi: TW_EPI_BF16, TW_EPI_RESID_F32, TW_EPI_F32, or
+ * TW_EPI_GELU_MX (out fp8[M][ldo] + sout scales [N/128][sout_rows][4]; N % 256 == 0). */
+int tw_gemm_mx(const uint8_t* A, const uint8_t* Sa, const uint8_t* W, const uint8_t* Sw, int M, int N, int K, int lda,
+               int ldw, int Mp, int Np, int epi, void* out, int ldo, const float* bias, uint8_t* sout, int sout_rows,
+               void* stream);
+/* bf16 src[rows][ld] -> MX fp8 dst[rows][K] + scales (K % 128 == 0). Encoder weights once at load; the
+ * attention output before out_proj (modeling_whisper.py:350-356). */
+int tw_quant_mx(const uint16_t* src, int rows, int K, int ld, uint8_t* dst, uint8_t* scales, int rows_pad,
+                void* stream);
+/* LayerNorm (as tw_layernorm) with the MX quantisation of its output fused into the store (D % 128 == 0). */
+int tw_layernorm_mx(const float* x, const float* gamma, const float* beta, int M, int D, float eps, uint8_t* out,
+                    uint8_t* scales, int rows_pad, void* stream);
 
 /* ---- attention ------------------------------------------------------------------------------ */
 /* Encoder self-attention. qkv bf16[B*S][3*H*64] (q pre-scaled by 64^-0.5) -> out bf16[B*S][H*64].

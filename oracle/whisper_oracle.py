@@ -165,6 +165,65 @@ def _softmax(x):
     return e / e.sum(-1, keepdims=True)
 
 
+# ----------------------------------------------------------------------------- MX fp8 (BASELINE config 5)
+# Not in the reference: config 5 ("fp8 MFMA encoder + bf16 decoder") runs the encoder projections of
+# modeling_whisper.py:279-282,309,375-376 on OCP MX fp8 operands. This restates the format the kernels use
+# (turbo-whisper-workspace_amd/csrc/tw_common.h "MX fp8"): e4m3fn elements, one e8m0 scale per 32 K elements,
+# s = E(absmax) - 8 (+1 when the absmax mantissa exceeds 1.75, so nothing saturates; 1 for E < 9),
+# element = rne_e4m3(clip(x * 2^(127-s), +-448)).
+
+def e4m3_rne(y: np.ndarray) -> np.ndarray:
+    """Round |y| <= 448 to the nearest OCP e4m3fn value (ties to even), as float64."""
+    y = np.asarray(y, np.float64)
+    _, ex = np.frexp(y)                      # y = m * 2^ex, m in [0.5, 1): floor(log2|y|) = ex - 1
+    e = np.maximum(ex - 1, -6)               # subnormals share the exponent -6
+    step = np.ldexp(1.0, e - 3)              # 3 mantissa bits
+    return np.round(y / step) * step         # np.round: half to even
+
+
+def mx_quant(x: np.ndarray):
+    """x [..., K] (K % 32 == 0) -> (elements e4m3 as float64 [..., K], scale bytes uint8 [..., K/32])."""
+    x = np.asarray(x, np.float32)
+    xb = x.reshape(x.shape[:-1] + (x.shape[-1] // 32, 32))
+    amax = np.abs(xb).max(-1).astype(np.float32)
+    u = amax.view(np.uint32).astype(np.int64)
+    E = (u >> 23) & 0xFF
+    s = np.where(E < 9, 1, E - 8 + ((u & 0x7FFFFF) > 0x600000)).astype(np.uint8)
+    inv = np.ldexp(1.0, 127 - s.astype(np.int64))[..., None]
+    q = e4m3_rne(np.clip(xb.astype(np.float64) * inv, -448.0, 448.0))
+    return q.reshape(x.shape), s
+
+
+def mx_dequant(q: np.ndarray, s: np.ndarray) -> np.ndarray:
+    qb = q.reshape(q.shape[:-1] + (q.shape[-1] // 32, 32))
+    return (qb * np.ldexp(1.0, s.astype(np.int64) - 127)[..., None]).reshape(q.shape)
+
+
+def mx_round(x: np.ndarray) -> np.ndarray:
+    """Quantise-dequantise: the value an MX fp8 GEMM operand carries, float32."""
+    return mx_dequant(*mx_quant(x)).astype(np.float32)
+
+
+def e4m3_bytes(q: np.ndarray) -> np.ndarray:
+    """e4m3fn encoding (uint8) of exactly representable float64 values (|q| <= 448)."""
+    q = np.asarray(q, np.float64)
+    sign = (q < 0) | ((q == 0) & np.signbit(q))
+    a = np.abs(q)
+    _, ex = np.frexp(a)
+    e = np.maximum(ex - 1, -6)
+    mant = np.round(a / np.ldexp(1.0, e - 3)).astype(np.int64)  # 8..15 normal, 0..7 subnormal
+    normal = mant >= 8
+    code = np.where(normal, ((e + 7) << 3) | (mant - 8), mant)
+    return (code | (sign.astype(np.int64) << 7)).astype(np.uint8)
+
+
+def bf16_round(x: np.ndarray) -> np.ndarray:
+    """float32 -> nearest bf16 (ties to even), returned as float32."""
+    u = np.asarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return u.astype(np.uint32).view(np.float32)
+
+
 class WhisperOracle:
     """fp32 numpy Whisper with the HF parameter names."""
 
@@ -225,6 +284,35 @@ class WhisperOracle:
             x = x + self._lin(_gelu(self._lin(h, f"{p}.fc1")), f"{p}.fc2")
             x = x.astype(np.float32)
         return _ln(x, self.sd["model.encoder.layer_norm.weight"], self.sd["model.encoder.layer_norm.bias"]).astype(np.float32)
+
+    def _lin_mx(self, xq, p, scale=1.0):
+        """nn.Linear on MX operands: mx_round(x) . mx_round(scale * W)^T + scale * b (scale: the 2^-3 folded into
+        the packed q rows, exact in MX)."""
+        w = mx_round(self.sd[f"{p}.weight"] * np.float32(scale))
+        y = xq.astype(np.float64) @ w.T.astype(np.float64)
+        if f"{p}.bias" in self.sd:
+            y = y + self.sd[f"{p}.bias"] * np.float32(scale)
+        return y.astype(np.float32)
+
+    def encode_mx(self, feats: np.ndarray) -> np.ndarray:
+        """The config-5 encoder: conv stem, attention core and LayerNorms as encode(); the q/k/v/o and fc1/fc2
+        projections on MX fp8 operands quantised where the GPU quantises them (LayerNorm output f32, attention
+        output after its bf16 store, GELU(fc1) f32)."""
+        sd, H, hd = self.sd, self.H, self.D // self.H
+        x = self.conv_stem(feats)
+        for i in range(self.L_enc):
+            p = f"model.encoder.layers.{i}"
+            h = mx_round(_ln(x, sd[f"{p}.self_attn_layer_norm.weight"], sd[f"{p}.self_attn_layer_norm.bias"]))
+            q = self._lin_mx(h, f"{p}.self_attn.q_proj", hd ** -0.5)
+            k = self._lin_mx(h, f"{p}.self_attn.k_proj")
+            v = self._lin_mx(h, f"{p}.self_attn.v_proj")
+            T = q.shape[0]
+            qh, kh, vh = (t.reshape(T, H, hd).transpose(1, 0, 2) for t in (q, k, v))
+            o = (_softmax(qh @ kh.transpose(0, 2, 1)) @ vh).transpose(1, 0, 2).reshape(T, self.D)
+            x = x + self._lin_mx(mx_round(bf16_round(o)), f"{p}.self_attn.out_proj")
+            h = mx_round(_ln(x, sd[f"{p}.final_layer_norm.weight"], sd[f"{p}.final_layer_norm.bias"]))
+            x = (x + self._lin_mx(mx_round(_gelu(self._lin_mx(h, f"{p}.fc1"))), f"{p}.fc2")).astype(np.float32)
+        return _ln(x, sd["model.encoder.layer_norm.weight"], sd["model.encoder.layer_norm.bias"]).astype(np.float32)
 
     def new_cache(self, enc: np.ndarray) -> dict:
         cross = []
@@ -716,16 +804,17 @@ def process_logits_no_rule(scores: np.ndarray, sampled: Sequence[int], g: GenCfg
 
 def replay_generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, passes: Sequence[Sequence[int]],
                     lang: Optional[int], task: Optional[str] = "transcribe", return_timestamps: bool = True,
-                    max_new_tokens: Optional[int] = None, tau: float = 0.3) -> dict:
+                    max_new_tokens: Optional[int] = None, tau: float = 0.3, mx: bool = False) -> dict:
     """Follow a device decode of ONE window (its raw per-seek-pass token lists and detected language) through the
-    f32 reference, checking every decision with decision_ok. Returns {"ok", "decisions", "exact", "first_bad"}."""
+    f32 reference, checking every decision with decision_ok. Returns {"ok", "decisions", "exact", "first_bad"}.
+    mx: the reference encoder is encode_mx (config 5's MX fp8 projections)."""
     feats = np.asarray(feats, np.float32)
     stats = {"ok": True, "decisions": 0, "exact": 0, "first_bad": None}
 
     def enc_at(seek):
         seg = np.zeros_like(feats)
         seg[:, : 3000 - seek] = feats[:, seek:]
-        return model.encode(seg)
+        return model.encode_mx(seg) if mx else model.encode(seg)
 
     def check(scores, sampled, tok, use_ts):
         stats["decisions"] += 1

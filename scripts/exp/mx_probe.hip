@@ -1,0 +1,122 @@
+// Probe of v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3) operand/scale lane maps and of v_cvt_pk_fp8_f32
+// rounding/saturation, with exact data. Prints which hypothesis matches.
+//   hipcc --offload-arch=gfx950 -O2 scripts/exp/mx_probe.hip -o scripts/exp/mx_probe && ./scripts/exp/mx_probe
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+__global__ void k_mfma(const unsigned char* a, const unsigned char* b, const int* sa, const int* sb, float* c) {
+  const int l = threadIdx.x;
+  i32x8 av, bv;
+  memcpy(&av, a + 32 * l, 32);
+  memcpy(&bv, b + 32 * l, 32);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, acc, 0, 0, 0, sa[l], 0, sb[l]);
+  for (int r = 0; r < 4; ++r) c[4 * l + r] = acc[r];
+}
+
+__global__ void k_cvt(const float* x, unsigned char* q, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (2 * i + 1 >= n) return;
+  const int w = __builtin_amdgcn_cvt_pk_fp8_f32(x[2 * i], x[2 * i + 1], 0, false);
+  q[2 * i] = w & 0xff;
+  q[2 * i + 1] = (w >> 8) & 0xff;
+}
+
+static double fp8_dec(unsigned char b) {
+  int s = b >> 7, e = (b >> 3) & 15, m = b & 7;
+  double v = e == 0 ? (m / 8.0) * ldexp(1.0, -6) : (1 + m / 8.0) * ldexp(1.0, e - 7);
+  return s ? -v : v;
+}
+// reference RNE + saturate to +-448
+static unsigned char fp8_enc(double x) {
+  unsigned char s = x < 0 ? 0x80 : 0;
+  double a = fabs(x);
+  if (a >= 448.0) return s | 0x7e;
+  int best = 0;
+  double bd = 1e300;
+  for (int b = 0; b < 0x7f; ++b) {
+    double d = fabs(fp8_dec(b) - a);
+    if (d < bd || (d == bd && (b & 1) == 0)) { bd = d; best = b; }
+  }
+  return s | best;
+}
+
+int main() {
+  srand(7);
+  unsigned char A[64 * 32], B[64 * 32];
+  for (int i = 0; i < 64 * 32; ++i) {
+    int v;
+    do v = rand() & 0xff; while ((v & 0x7f) == 0x7f || ((v >> 3) & 15) > 9 || ((v >> 3) & 15) < 4);
+    A[i] = v;
+    do v = rand() & 0xff; while ((v & 0x7f) == 0x7f || ((v >> 3) & 15) > 9 || ((v >> 3) & 15) < 4);
+    B[i] = v;
+  }
+  int SA[64], SB[64];
+  for (int l = 0; l < 64; ++l) { SA[l] = 127 + (rand() % 5) - 2; SB[l] = 127 + (rand() % 5) - 2; }
+  unsigned char *dA, *dB; int *dsa, *dsb; float* dC;
+  hipMalloc(&dA, sizeof A); hipMalloc(&dB, sizeof B); hipMalloc(&dsa, 256); hipMalloc(&dsb, 256); hipMalloc(&dC, 1024);
+  hipMemcpy(dA, A, sizeof A, hipMemcpyHostToDevice); hipMemcpy(dB, B, sizeof B, hipMemcpyHostToDevice);
+  float C[256];
+  for (int pass = 0; pass < 2; ++pass) {
+    int sa[64], sb[64];
+    for (int l = 0; l < 64; ++l) { sa[l] = pass ? SA[l] : 127; sb[l] = pass ? SB[l] : 127; }
+    hipMemcpy(dsa, sa, 256, hipMemcpyHostToDevice); hipMemcpy(dsb, sb, 256, hipMemcpyHostToDevice);
+    k_mfma<<<1, 64>>>(dA, dB, dsa, dsb, dC);
+    hipMemcpy(C, dC, 1024, hipMemcpyDeviceToHost);
+    // hypotheses for lane l, byte j: H1 k = 32*(l/16) + j ; H2 k = 16*(l/16) + j (j<16), 64 + 16*(l/16) + j-16
+    for (int h = 0; h < 2; ++h) {
+      double Am[16][128], Bm[128][16], Sa[16][128], Sb[128][16];
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 32; ++j) {
+          int k = h == 0 ? 32 * (l / 16) + j : (j < 16 ? 16 * (l / 16) + j : 64 + 16 * (l / 16) + j - 16);
+          Am[l % 16][k] = fp8_dec(A[32 * l + j]);
+          Bm[k][l % 16] = fp8_dec(B[32 * l + j]);
+          Sa[l % 16][k] = ldexp(1.0, sa[l] - 127);
+          Sb[k][l % 16] = ldexp(1.0, sb[l] - 127);
+        }
+      double maxerr = 0;
+      for (int l = 0; l < 64; ++l)
+        for (int r = 0; r < 4; ++r) {
+          int row = (l >> 4) * 4 + r, col = l & 15;
+          double ref = 0;
+          for (int k = 0; k < 128; ++k) ref += Am[row][k] * Sa[row][k] * Bm[k][col] * Sb[k][col];
+          double e = fabs(ref - C[4 * l + r]) / (1e-6 + fabs(ref));
+          if (e > maxerr) maxerr = e;
+        }
+      printf("pass %d (%s scales) hypothesis H%d: max rel err %.3g %s\n", pass, pass ? "random" : "unit", h + 1, maxerr,
+             maxerr < 1e-5 ? "MATCH" : "");
+    }
+  }
+  // conversion: RNE + saturation
+  const int n = 4096;
+  float* x = (float*)malloc(n * 4);
+  for (int i = 0; i < n; ++i) {
+    double u = (rand() / (double)RAND_MAX) * 2 - 1;
+    x[i] = (float)(u * ldexp(1.0, (rand() % 26) - 14));
+  }
+  x[0] = 448.f; x[1] = 449.f; x[2] = 470.f; x[3] = 500.f; x[4] = 1e6f; x[5] = -1e6f; x[6] = 0.f; x[7] = -0.f;
+  x[8] = 1.0625f; x[9] = 1.1875f;  // ties
+  float* dx; unsigned char* dq;
+  hipMalloc(&dx, n * 4); hipMalloc(&dq, n);
+  hipMemcpy(dx, x, n * 4, hipMemcpyHostToDevice);
+  k_cvt<<<n / 128, 64>>>(dx, dq, n);
+  unsigned char q[4096];
+  hipMemcpy(q, dq, n, hipMemcpyDeviceToHost);
+  int bad = 0, bad_inrange = 0;
+  for (int i = 0; i < n; ++i) {
+    unsigned char r = fp8_enc(x[i]);
+    if (r != q[i]) {
+      ++bad;
+      if (fabs(x[i]) < 448.0) ++bad_inrange;
+      if (bad <= 12) printf("cvt mismatch x=%g hw=0x%02x (%g) ref=0x%02x (%g)\n", x[i], q[i], fp8_dec(q[i]), r, fp8_dec(r));
+    }
+  }
+  printf("cvt: %d mismatches (%d with |x| < 448) of %d\n", bad, bad_inrange, n);
+  return 0;
+}

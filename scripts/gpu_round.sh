@@ -1,10 +1,12 @@
 #!/bin/bash
 # One GPU-box session: parity tests, the bench line, a rocprofv3 kernel-trace summary and the two
 # PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic. Every GPU step has its own time limit and the
-# chain stops at the first failure.  usage: bash scripts/gpu_round.sh TAG [skip_tests]
+# chain stops at the first failure.  usage: [BENCH_ARGS="--config c5"] bash scripts/gpu_round.sh TAG [skip_tests]
+# (a config-5 TAG must contain "_c5": bench.py reads profiles/*_c5_traffic.json for it)
 set -u
 TAG=${1:-r01}
 SKIP_TESTS=${2:-0}
+BA=${BENCH_ARGS:-}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -19,11 +21,11 @@ step() {  # step NAME TIMEOUT CMD...
 if [ "$SKIP_TESTS" != "1" ]; then
   step tests 900 python -m pytest tests -q -m gpu -x -p no:cacheprovider
 fi
-step prof_kt 600 rocprofv3 --kernel-trace --stats -T -d $OUT/kt -o kt --output-format csv -- python bench.py --profile-only --steps 2 --warmup 1
-step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/pmc_fetch -o pmc --output-format csv -- python bench.py --profile-only --steps 1 --warmup 0
-step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/pmc_write -o pmc --output-format csv -- python bench.py --profile-only --steps 1 --warmup 0
+step prof_kt 600 rocprofv3 --kernel-trace --stats -T -d $OUT/kt -o kt --output-format csv -- python bench.py $BA --profile-only --steps 2 --warmup 1
+step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/pmc_fetch -o pmc --output-format csv -- python bench.py $BA --profile-only --steps 1 --warmup 0
+step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/pmc_write -o pmc --output-format csv -- python bench.py $BA --profile-only --steps 1 --warmup 0
 python scripts/summarize_prof.py $OUT > $OUT/summary.txt 2>&1
 cp $OUT/traffic.json profiles/${TAG}_traffic.json   # bench.py reads the newest profiles/*traffic.json
-step bench 900 python bench.py --steps 5 --warmup 2
+step bench 900 python bench.py $BA --steps 5 --warmup 2
 grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
 echo done

@@ -1,0 +1,152 @@
+"""MX fp8 encoder kernels (BASELINE config 5) on the MI355X, through the C-ABI, against the oracle's restatement of
+the MX format (oracle/whisper_oracle.py mx_quant, itself pinned to torch.float8_e4m3fn in test_mx_oracle.py).
+
+Bit-exact where the input is bit-identical (bf16 -> MX quantisation); the GEMM against float64 products of the same
+quantised operands (only f32 accumulation order differs: 2e-6 of sum |a*w|); the fused producers (LayerNorm,
+GELU epilogue) quantise f32 values the GPU computes in a different order than numpy, so an element may land on
+the other side of a rounding tie: at most 0.5 % of the bytes differ, each by one e4m3 step."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import whisper_oracle as wo
+from twamd import _lib
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def S():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def pad256(n):
+    return (n + 255) // 256 * 256
+
+
+def quant_gpu(x_bf16, rows_pad=None):
+    rows, K = x_bf16.shape
+    rp = rows_pad or pad256(rows)
+    q = torch.empty(rows, K, dtype=torch.uint8, device=DEV)
+    s = torch.zeros(K // 128, rp, 4, dtype=torch.uint8, device=DEV)
+    _lib.call("tw_quant_mx", x_bf16.data_ptr(), rows, K, x_bf16.shape[1], q.data_ptr(), s.data_ptr(), rp, S())
+    return q, s
+
+
+def scales_rowmajor(s, rows):
+    """[K/128][rows_pad][4] -> [rows][K/32]"""
+    return s[:, :rows, :].permute(1, 0, 2).reshape(rows, -1).cpu().numpy()
+
+
+def decode_e4m3(b):
+    b = b.astype(np.int64)
+    sgn = np.where(b >> 7, -1.0, 1.0)
+    e, m = (b >> 3) & 15, b & 7
+    v = np.where(e == 0, m / 8.0 * 2.0 ** -6, (1 + m / 8.0) * np.ldexp(1.0, e - 7))
+    return sgn * v
+
+
+def dequant(q, s_rm):
+    return wo.mx_dequant(decode_e4m3(q), s_rm)
+
+
+def test_quant_mx_bit_exact_vs_oracle():
+    g = torch.Generator().manual_seed(3)
+    rows, K = 333, 1280
+    x = torch.randn(rows, K, generator=g) * torch.exp2(torch.randint(-20, 12, (rows, 1), generator=g).float())
+    x[5, 64:96] = 0.0                       # an all-zero block
+    x[7, :32] = 1e-38                       # tiny block (scale floor)
+    x[9, 100] = 3.0e4                       # one large element
+    x[11, 200:232] = torch.linspace(-448, 448, 32)
+    xb = x.to(torch.bfloat16).to(DEV)
+    q, s = quant_gpu(xb)
+    rq, rs = wo.mx_quant(xb.float().cpu().numpy())
+    assert np.array_equal(scales_rowmajor(s, rows), rs)
+    assert np.array_equal(q.cpu().numpy(), wo.e4m3_bytes(rq))
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 512, 1280), (1500, 1280, 1280), (257, 768, 1024), (600, 1280, 5120)])
+@pytest.mark.parametrize("epi", [_lib.TW_EPI_F32, _lib.TW_EPI_RESID_F32, _lib.TW_EPI_BF16])
+def test_gemm_mx_vs_float64(M, N, K, epi):
+    g = torch.Generator().manual_seed(M + N + K)
+    A = (torch.randn(M, K, generator=g)).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = torch.randn(N, generator=g).to(DEV)
+    Aq, As = quant_gpu(A)
+    Wq, Ws = quant_gpu(W)
+    Mp, Np = As.shape[1], Ws.shape[1]
+    if epi == _lib.TW_EPI_BF16:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    else:
+        out = torch.randn(M, N, generator=g).to(DEV) if epi == _lib.TW_EPI_RESID_F32 else torch.empty(M, N, device=DEV)
+    before = out.float().cpu().numpy().copy()
+    _lib.call("tw_gemm_mx", Aq.data_ptr(), As.data_ptr(), Wq.data_ptr(), Ws.data_ptr(), M, N, K, K, K, Mp, Np, epi,
+              out.data_ptr(), N, bias.data_ptr(), None, 0, S())
+    a = dequant(Aq.cpu().numpy(), scales_rowmajor(As, M))
+    w = dequant(Wq.cpu().numpy(), scales_rowmajor(Ws, N))
+    ref = a @ w.T + bias.cpu().numpy()[None, :].astype(np.float64)
+    mag = np.abs(a) @ np.abs(w).T + 1.0
+    got = out.float().cpu().numpy().astype(np.float64)
+    if epi == _lib.TW_EPI_RESID_F32:
+        got = got - before
+    tol = 2e-6 * mag + (4e-3 * np.abs(ref) if epi == _lib.TW_EPI_BF16 else 0)
+    assert np.all(np.abs(got - ref) <= tol + 1e-6), float(np.max(np.abs(got - ref) - tol))
+
+
+def _byte_agreement(got_q, got_s, ref_q, ref_s):
+    """fraction of elements whose (scale, byte) differ, and that every difference is at most one e4m3 step"""
+    gv = dequant(got_q, got_s)
+    rv = wo.mx_dequant(ref_q, ref_s)
+    diff = gv != rv
+    step = np.ldexp(1.0, np.floor(np.log2(np.maximum(np.abs(rv), 1e-30))).astype(np.int64) - 3)
+    step = np.maximum(step, np.repeat(np.ldexp(1.0, ref_s.astype(np.int64) - 127 - 9), 32, axis=-1))
+    assert np.all(np.abs(gv - rv)[diff] <= 2.0001 * step[diff]), "an MX element differs by more than one step"
+    return diff.mean()
+
+
+def test_gemm_mx_gelu_epilogue_quantises_like_oracle():
+    M, N, K = 700, 1024, 1280
+    g = torch.Generator().manual_seed(11)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    Aq, As = quant_gpu(A)
+    Wq, Ws = quant_gpu(W)
+    Mp = As.shape[1]
+    out = torch.empty(M, N, dtype=torch.uint8, device=DEV)
+    so = torch.zeros(N // 128, Mp, 4, dtype=torch.uint8, device=DEV)
+    _lib.call("tw_gemm_mx", Aq.data_ptr(), As.data_ptr(), Wq.data_ptr(), Ws.data_ptr(), M, N, K, K, K, Mp,
+              Ws.shape[1], _lib.TW_EPI_GELU_MX, out.data_ptr(), N, bias.data_ptr(), so.data_ptr(), Mp, S())
+    a = dequant(Aq.cpu().numpy(), scales_rowmajor(As, M))
+    w = dequant(Wq.cpu().numpy(), scales_rowmajor(Ws, N))
+    h = wo._gelu(a @ w.T + bias.cpu().numpy()[None, :]).astype(np.float32)
+    rq, rs = wo.mx_quant(h)
+    frac = _byte_agreement(out.cpu().numpy(), scales_rowmajor(so, M), rq, rs)
+    assert frac < 5e-3, frac
+
+
+@pytest.mark.parametrize("M,D", [(1500, 1280), (37, 384), (300, 256)])
+def test_layernorm_mx_vs_oracle(M, D):
+    g = torch.Generator().manual_seed(M * D)
+    x = (torch.randn(M, D, generator=g) * 3 + 0.5).to(DEV)
+    gam = (1 + 0.2 * torch.randn(D, generator=g)).to(DEV)
+    bet = (0.1 * torch.randn(D, generator=g)).to(DEV)
+    rp = pad256(M)
+    q = torch.empty(M, D, dtype=torch.uint8, device=DEV)
+    s = torch.zeros(D // 128, rp, 4, dtype=torch.uint8, device=DEV)
+    _lib.call("tw_layernorm_mx", x.data_ptr(), gam.data_ptr(), bet.data_ptr(), M, D, 1e-5, q.data_ptr(), s.data_ptr(),
+              rp, S())
+    ref = wo._ln(x.cpu().numpy().astype(np.float64), gam.cpu().numpy(), bet.cpu().numpy()).astype(np.float32)
+    rq, rs = wo.mx_quant(ref)
+    frac = _byte_agreement(q.cpu().numpy(), scales_rowmajor(s, M), rq, rs)
+    assert frac < 5e-3, frac
+
+
+def test_gemm_mx_rejects_bad_shapes():
+    z = torch.zeros(256 * 128, dtype=torch.uint8, device=DEV)
+    with pytest.raises(_lib.TwError, match="K % 128"):
+        _lib.call("tw_gemm_mx", z.data_ptr(), z.data_ptr(), z.data_ptr(), z.data_ptr(), 16, 16, 96, 96, 96, 256, 256,
+                  _lib.TW_EPI_F32, z.data_ptr(), 16, None, None, 0, S())
+    with pytest.raises(_lib.TwError, match="multiples of 256"):
+        _lib.call("tw_gemm_mx", z.data_ptr(), z.data_ptr(), z.data_ptr(), z.data_ptr(), 300, 16, 128, 128, 128, 256,
+                  256, _lib.TW_EPI_F32, z.data_ptr(), 16, None, None, 0, S())

@@ -27,6 +27,8 @@ struct EpiArgs {
   const float* aux;   // EPI_GELU_POS_F32: positional table [aux_rows][N]
   int aux_rows;
   int kv_S, kv_B, kv_D, kv_H;  // EPI_CROSSKV scatter geometry
+  uint8_t* sout;      // EPI_GELU_MX: e8m0 scales of the fp8 output, [N/128][s_rows][4]
+  int s_rows;
 };
 
 template <int EPI>
@@ -1279,4 +1281,187 @@ extern "C" int tw_gemv_packed(const bf16_t* A, int a_packed, int lda, const bf16
     default: tw_set_error("tw_gemv_packed: unsupported epilogue %d", epi); return TW_ERR_ARG;
   }
   return tw_check_launch("tw_gemv_packed");
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_gemm_mx: the encoder projections in MX fp8 (BASELINE config 5). C[M][N] = A[M][K] . W[N][K]^T with e4m3
+// operands and one e8m0 scale per 32 K elements of every A row and W row (tw_common.h "MX fp8"), on
+// v_mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate per clock: MI355X_MICROARCH.md § Matrix cores).
+// The structure is k_gemm_big's with BK = 128 elements: a K-step row is still 128 bytes, so the LDS-DMA staging,
+// the bank swizzle and the 24 ds_read_b128 per wave per K-step are unchanged, while one K-step now covers twice
+// the K (32 MFMAs of 16x16x128 per wave instead of 64 of 16x16x32). The K-step's scales (one dword per tile row:
+// 1 KiB for A, 1 KiB for W, contiguous in HBM) ride along by LDS-DMA from waves 0 and 1; lane l of a fragment
+// (row l % 16, K block l / 16 of the 16x16x128 operand, lane map checked by scripts/exp/mx_probe.hip) reads its
+// own scale byte with one ds_read_u8.
+// ------------------------------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+#define MX_BK 128                                  // K elements (= bytes) per K-step
+#define MX_TILE (GB_BM * MX_BK)                    // 32 KiB: one operand tile of one K-step
+#define MX_STAGE (2 * MX_TILE + 2 * GB_BM * 4)     // A | W | A scales | W scales = 66 KiB
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm_mx(const uint8_t* __restrict__ A, const uint8_t* __restrict__ W,
+                                                    const uint8_t* __restrict__ Sa, const uint8_t* __restrict__ Sw,
+                                                    int M, int N, int K, int lda, int ldw, int Mp, int Np,
+                                                    EpiArgs ea) {
+  // K loop: 2 x 66 KiB; epilogue: 8 x [64][68] f32 = 136 KiB (one array: see cdna_hip_programming.md §5 trap (a))
+  __shared__ __attribute__((aligned(16))) uint8_t smem[8 * 64 * GB_EPI_LD * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntm = (M + GB_BM - 1) / GB_BM, ntn = (N + GB_BN - 1) / GB_BN;
+  const int nwg = ntm * ntn;
+  const int orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int tm = wgid / ntn, tn = wgid - tm * ntn;
+  const int m0 = tm * GB_BM, n0 = tn * GB_BN;
+
+  const uint8_t* ga[4];
+  const uint8_t* gw[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (4 * wid + i) + (lane >> 3);
+    const int ch = (lane & 7) ^ gb_swz(row);
+    ga[i] = A + (size_t)min(m0 + row, M - 1) * lda + ch * 16;
+    gw[i] = W + (size_t)min(n0 + row, N - 1) * ldw + ch * 16;
+  }
+  // scales of K-step kt: rows m0..m0+255 of [K/128][Mp][4] are 1 KiB contiguous (Mp, Np: multiples of 256)
+  const uint8_t* gs = wid == 0 ? Sa + (size_t)m0 * 4 + lane * 16 : Sw + (size_t)n0 * 4 + lane * 16;
+  const size_t gs_step = (size_t)(wid == 0 ? Mp : Np) * 4;
+  auto stage = [&](int buf, int kt) {
+    uint8_t* As = smem + buf * MX_STAGE;
+    uint8_t* Ws = As + MX_TILE;
+    const int k0 = kt * MX_BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rb = 8 * (4 * wid + i) * MX_BK;
+      __builtin_amdgcn_global_load_lds((const void*)(ga[i] + k0), (lds_void_t*)(As + rb), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(gw[i] + k0), (lds_void_t*)(Ws + rb), 16, 0, 0);
+    }
+    if (wid < 2)
+      __builtin_amdgcn_global_load_lds((const void*)(gs + kt * gs_step), (lds_void_t*)(As + 2 * MX_TILE + wid * 1024),
+                                       16, 0, 0);
+  };
+
+  const int wr = wid >> 2, wc = wid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / MX_BK;
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    const uint8_t* As = smem + cur * MX_STAGE;
+    const uint8_t* Ws = As + MX_TILE;
+    const uint8_t* SAs = As + 2 * MX_TILE;
+    const uint8_t* SWs = SAs + 1024;
+    i32x8 bfr[4];
+    int sb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = wc * 64 + j * 16 + fr;
+      const uint8_t* p = Ws + col * MX_BK;
+      const int4 lo = *(const int4*)(p + (((2 * fq) ^ gb_swz(col)) << 4));
+      const int4 hi = *(const int4*)(p + (((2 * fq + 1) ^ gb_swz(col)) << 4));
+      bfr[j] = (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      sb[j] = SWs[col * 4 + fq];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = wr * 128 + i * 16 + fr;
+      const uint8_t* p = As + row * MX_BK;
+      const int4 lo = *(const int4*)(p + (((2 * fq) ^ gb_swz(row)) << 4));
+      const int4 hi = *(const int4*)(p + (((2 * fq + 1) ^ gb_swz(row)) << 4));
+      const i32x8 af = (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      const int sa = SAs[row * 4 + fq];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[j], acc[i][j], 0, 0, 0, sa, 0, sb[j]);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue through LDS, as k_gemm_big (4 consecutive columns per lane in the read-back)
+  const int ncol0 = n0 + wc * 64;
+  const int rc = (lane & 15) * 4;
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ea.bias) {
+    const int n = ncol0 + rc;
+    bias4.x = ea.bias[min(n, N - 1)];
+    bias4.y = ea.bias[min(n + 1, N - 1)];
+    bias4.z = ea.bias[min(n + 2, N - 1)];
+    bias4.w = ea.bias[min(n + 3, N - 1)];
+  }
+  float* wimg = (float*)smem + wid * (64 * GB_EPI_LD);
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int ib = 4 * half;
+    if (half) __syncthreads();
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wimg[(ii * 16 + fq * 4 + r) * GB_EPI_LD + j * 16 + fr] = acc[ib + ii][j][r];
+    __syncthreads();
+    const int mrow0 = m0 + wr * 128 + ib * 16;
+#pragma unroll 4
+    for (int rr = 0; rr < 16; ++rr) {
+      const int lr = rr * 4 + (lane >> 4);
+      const int m = mrow0 + lr;
+      float4 v = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
+      v.x += bias4.x; v.y += bias4.y; v.z += bias4.z; v.w += bias4.w;
+      if constexpr (EPI == TW_EPI_GELU_MX) {
+        // fc1 -> fc2 operand: GELU, then MX-quantise; the 8 lanes of a 32-column block share one scale
+        // (N % 256 == 0 is checked on the host, so every lane of the group is inside N)
+        v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+        const uint32_t sbyte = mx_scale_byte(mx_group8_max(abs4max(v.x, v.y, v.z, v.w)));
+        const uint32_t w = mx_pack4(v.x, v.y, v.z, v.w, mx_inv_scale(sbyte));
+        if (m < M) {
+          *(uint32_t*)((uint8_t*)ea.out + (size_t)m * ea.ldo + ncol0 + rc) = w;
+          if ((lane & 7) == 0) ea.sout[tw_mx_sidx(m, (ncol0 + rc) >> 5, ea.s_rows)] = (uint8_t)sbyte;
+        }
+      } else {
+        if (m < M && ncol0 + rc < N) epi_store4<EPI>(ea, m, ncol0 + rc, N, v);
+      }
+    }
+  }
+}
+
+template <int EPI>
+static void launch_gemm_mx(const uint8_t* A, const uint8_t* Sa, const uint8_t* W, const uint8_t* Sw, int M, int N,
+                           int K, int lda, int ldw, int Mp, int Np, const EpiArgs& ea, hipStream_t s) {
+  const unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
+  hipLaunchKernelGGL(k_gemm_mx<EPI>, dim3(nwg), dim3(512), 0, s, A, W, Sa, Sw, M, N, K, lda, ldw, Mp, Np, ea);
+}
+
+extern "C" int tw_gemm_mx(const uint8_t* A, const uint8_t* Sa, const uint8_t* W, const uint8_t* Sw, int M, int N,
+                          int K, int lda, int ldw, int Mp, int Np, int epi, void* out, int ldo, const float* bias,
+                          uint8_t* sout, int sout_rows, void* stream) {
+  TW_REQUIRE(A && Sa && W && Sw && out, "tw_gemm_mx: null pointer");
+  TW_REQUIRE(M > 0 && N > 0 && K > 0 && K % MX_BK == 0, "tw_gemm_mx: M=%d N=%d K=%d (K %% 128 required)", M, N, K);
+  TW_REQUIRE(lda % 16 == 0 && ldw % 16 == 0 && lda >= K && ldw >= K, "tw_gemm_mx: lda=%d ldw=%d", lda, ldw);
+  TW_REQUIRE(Mp % GB_BM == 0 && Mp >= M && Np % GB_BN == 0 && Np >= N,
+             "tw_gemm_mx: scale row pads Mp=%d Np=%d must be multiples of 256 covering M=%d N=%d", Mp, Np, M, N);
+  EpiArgs ea{out, ldo, bias, nullptr, 0, 0, 0, 0, 0, nullptr, 0};
+  hipStream_t s = (hipStream_t)stream;
+  switch (epi) {
+    case TW_EPI_BF16: launch_gemm_mx<TW_EPI_BF16>(A, Sa, W, Sw, M, N, K, lda, ldw, Mp, Np, ea, s); break;
+    case TW_EPI_RESID_F32: launch_gemm_mx<TW_EPI_RESID_F32>(A, Sa, W, Sw, M, N, K, lda, ldw, Mp, Np, ea, s); break;
+    case TW_EPI_F32: launch_gemm_mx<TW_EPI_F32>(A, Sa, W, Sw, M, N, K, lda, ldw, Mp, Np, ea, s); break;
+    case TW_EPI_GELU_MX:
+      TW_REQUIRE(sout && sout_rows >= M && N % GB_BN == 0 && ldo >= N && ldo % 4 == 0,
+                 "tw_gemm_mx: GELU_MX needs scale output (sout_rows %d >= M), N %% 256 (N=%d), ldo %% 4", sout_rows, N);
+      ea.sout = sout;
+      ea.s_rows = sout_rows;
+      launch_gemm_mx<TW_EPI_GELU_MX>(A, Sa, W, Sw, M, N, K, lda, ldw, Mp, Np, ea, s);
+      break;
+    default: tw_set_error("tw_gemm_mx: unsupported epilogue %d", epi); return TW_ERR_ARG;
+  }
+  return tw_check_launch("tw_gemm_mx");
 }

@@ -59,6 +59,43 @@ __device__ inline float wave_max(float v) {
   return v;
 }
 
+// ---- MX fp8 (BASELINE config 5: fp8 MFMA encoder) -----------------------------------------------
+// OCP MX block format for the encoder GEMM operands: e4m3fn elements, one e8m0 scale per 32 consecutive K
+// elements of a row (the block v_mfma_scale_f32_16x16x128_f8f6f4 consumes). Scale byte s = E - 8, plus one
+// when the absmax mantissa exceeds 1.75 (E = biased f32 exponent of the block's absmax; s = 1 for E < 9): the
+// OCP shared exponent floor(log2 amax) - emax(e4m3), raised by one where it would push the block's largest
+// elements past 448 = 1.75 * 2^8, so no element saturates; element = e4m3_rne(clamp(x * 2^(127 - s), +-448)).
+// oracle/whisper_oracle.py mx_quant restates this bit for bit.
+// Scale layout in HBM: [K/128][rows_pad][4] bytes (one dword per row per 128-deep K-step: a GEMM tile's scales
+// of one K-step are one contiguous 1 KiB run), byte (k/32) % 4.
+__host__ __device__ inline size_t tw_mx_sidx(int m, int kb, int rows_pad) {
+  return ((size_t)(kb >> 2) * rows_pad + m) * 4 + (kb & 3);
+}
+__device__ inline uint32_t mx_scale_byte(float amax) {
+  const uint32_t u = __float_as_uint(amax), e = (u >> 23) & 0xffu;
+  return e < 9u ? 1u : e - 8u + ((u & 0x7fffffu) > 0x600000u ? 1u : 0u);
+}
+__device__ inline float mx_inv_scale(uint32_t s) { return __uint_as_float((254u - s) << 23); }  // 2^(127 - s)
+__device__ inline uint32_t mx_pack4(float a, float b, float c, float d, float inv) {
+  a = fminf(fmaxf(a * inv, -448.f), 448.f);
+  b = fminf(fmaxf(b * inv, -448.f), 448.f);
+  c = fminf(fmaxf(c * inv, -448.f), 448.f);
+  d = fminf(fmaxf(d * inv, -448.f), 448.f);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+// absmax over the 8 consecutive lanes (xor 1, 2, 4) that hold one 32-element block as 4 values each
+__device__ inline float mx_group8_max(float v) {
+  v = fmaxf(v, __shfl_xor(v, 1, 64));
+  v = fmaxf(v, __shfl_xor(v, 2, 64));
+  v = fmaxf(v, __shfl_xor(v, 4, 64));
+  return v;
+}
+__device__ inline float abs4max(float a, float b, float c, float d) {
+  return fmaxf(fmaxf(fabsf(a), fabsf(b)), fmaxf(fabsf(c), fabsf(d)));
+}
+
 // ---- order-preserving float <-> uint key (for atomicMax over signed floats) ----------------------
 __device__ inline uint32_t f32_order_key(float f) {
   uint32_t u = __float_as_uint(f);

@@ -31,6 +31,10 @@ import functools
 
 LN_EPS = 1e-5
 S_ENC = 1500
+
+
+def _pad256(n: int) -> int:
+    return (n + 255) // 256 * 256
 DEC_SPLITS = 4   # split-K factor of the decoder's d_model-wide projections (out_proj, fc2)
 
 
@@ -89,7 +93,8 @@ class PassResult:
 
 class WhisperEngine:
     def __init__(self, weights: PackedWeights, gen: GenerationSettings, max_batch: int = 24,
-                 device: str = "cuda", use_graphs: bool = True, dec_cus: Optional[int] = None, max_beams: int = 1):
+                 device: str = "cuda", use_graphs: bool = True, dec_cus: Optional[int] = None, max_beams: int = 1,
+                 enc_fp8: Optional[bool] = None):
         _lib.load()
         # kernel-variant overrides for A/B measurement (defaults are the measured-best kernels)
         if os.environ.get("TW_GEMM_VARIANT"):
@@ -145,6 +150,22 @@ class WhisperEngine:
         self.att = torch.empty(M15, D, dtype=bf, device=dev)
         self.ffn = torch.empty(M15, F, dtype=bf, device=dev)
         # cross-attention K/V of the encoded windows, one buffer per pipeline slot
+        # BASELINE config 5: the encoder projections on MX fp8 operands (tw_gemm_mx); TW_ENC_FP8=1 turns it on
+        self.enc_fp8 = (os.environ.get("TW_ENC_FP8", "0") == "1") if enc_fp8 is None else bool(enc_fp8)
+        self.enc_mx: List[Dict[str, tuple]] = []
+        if self.enc_fp8:
+            u8 = torch.uint8
+            self.m15p = _pad256(M15)
+            self.hq = torch.empty(M15, D, dtype=u8, device=dev)
+            self.hq_s = torch.zeros(D // 128, self.m15p, 4, dtype=u8, device=dev)
+            self.attq = torch.empty(M15, D, dtype=u8, device=dev)
+            self.attq_s = torch.zeros(D // 128, self.m15p, 4, dtype=u8, device=dev)
+            self.ffnq = torch.empty(M15, F, dtype=u8, device=dev)
+            self.ffnq_s = torch.zeros(F // 128, self.m15p, 4, dtype=u8, device=dev)
+            with torch.cuda.device(self.device):
+                self.enc_mx = [{k: self._quant_weight(getattr(L, k)) for k in ("wqkv", "wo", "w1", "w2")}
+                               for L in weights.enc]
+                torch.cuda.synchronize(self.device)
         self.cross_kv_buf = torch.empty(2, d.decoder_layers, 2, B, H, S_ENC, 64, dtype=bf, device=dev)
         self.cross_kv = self.cross_kv_buf[0]
         self._slot = 0  # slot the decoder reads
@@ -195,6 +216,26 @@ class WhisperEngine:
                               for L in weights.dec]
                 self.emb_p = self._pack(weights.emb)
                 torch.cuda.synchronize(self.device)
+
+    def _quant_weight(self, W: torch.Tensor) -> tuple:
+        """bf16 [N][K] -> (fp8 [N][K], e8m0 scales [K/128][Np][4], Np) in the MX layout of tw_gemm_mx."""
+        N, K = W.shape
+        Np = _pad256(N)
+        q = torch.empty(N, K, dtype=torch.uint8, device=self.device)
+        sc = torch.zeros(K // 128, Np, 4, dtype=torch.uint8, device=self.device)
+        _lib.call("tw_quant_mx", W.data_ptr(), N, K, K, q.data_ptr(), sc.data_ptr(), Np,
+                  torch.cuda.current_stream(self.device).cuda_stream)
+        return q, sc, Np
+
+    def _gemm_mx(self, A, As, Wt, M, N, K, epi, out, bias=None, sout=None, stream=None):
+        """MX fp8 GEMM: A fp8 [M][K] + scales As [K/128][m15p][4]; Wt = _quant_weight(W)."""
+        st = stream or self.stream
+        Wq, Ws, Np = Wt
+        rec = self._begin_timer(("gemm_mx", epi), 2.0 * M * N * K, st)
+        _lib.call("tw_gemm_mx", A.data_ptr(), As.data_ptr(), Wq.data_ptr(), Ws.data_ptr(), M, N, K, K, K, self.m15p,
+                  Np, epi, out.data_ptr(), N, _lib.ptr(bias), _lib.ptr(sout), self.m15p if sout is not None else 0,
+                  st.cuda_stream)
+        self._end_timer(rec, st)
 
     def _pack(self, W: torch.Tensor) -> torch.Tensor:
         N, K = W.shape
@@ -352,7 +393,9 @@ class WhisperEngine:
         _lib.call("tw_im2col_conv2", self.h1.data_ptr(), R, D, self.a2.data_ptr(), s)
         self._gemm(self.a2, w.conv2_w, M15, D, 3 * D, _lib.TW_EPI_GELU_POS_F32, self.x, bias=w.conv2_b,
                    aux=w.pos_enc, aux_rows=S_ENC, stream=st)
-        for L in w.enc:
+        if self.enc_fp8:
+            self._encode_layers_mx(R, st)
+        for L in ([] if self.enc_fp8 else w.enc):
             self._ln(self.x, L.ln1_g, L.ln1_b, M15, self.hln, stream=st)
             self._gemm(self.hln, L.wqkv, M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv, stream=st)
             rec = self._begin_timer(("attn_encoder", 0), 4.0 * S_ENC * S_ENC * 64 * H * R, st)
@@ -367,6 +410,32 @@ class WhisperEngine:
         self._gemm(self.hln, w.wkv_x, M15, d.decoder_layers * 2 * D, D, _lib.TW_EPI_CROSSKV, self.cross_kv_buf[slot],
                    bias=w.bkv_x, kv_geom=geom, stream=st)
         self._enc_end(sync, slot)
+
+    def _encode_layers_mx(self, R: int, st) -> None:
+        """The 32 encoder layers of config 5: LayerNorms emit MX fp8 (tw_layernorm_mx), q/k/v/o and fc1/fc2 run on
+        tw_gemm_mx, the attention core stays bf16 (its output is quantised once for out_proj), fc1's GELU output is
+        quantised in its epilogue."""
+        d, w = self.d, self.w
+        D, F, H = d.d_model, d.ffn, d.heads
+        M15, s = R * S_ENC, st.cuda_stream
+        for L, Q in zip(w.enc, self.enc_mx):
+            _lib.call("tw_layernorm_mx", self.x.data_ptr(), L.ln1_g.data_ptr(), L.ln1_b.data_ptr(), M15, D, LN_EPS,
+                      self.hq.data_ptr(), self.hq_s.data_ptr(), self.m15p, s)
+            self._gemm_mx(self.hq, self.hq_s, Q["wqkv"], M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv,
+                          stream=st)
+            rec = self._begin_timer(("attn_encoder", 0), 4.0 * S_ENC * S_ENC * 64 * H * R, st)
+            _lib.call("tw_attn_encoder", self.qkv.data_ptr(), R, S_ENC, H, self.att.data_ptr(), s)
+            self._end_timer(rec, st)
+            _lib.call("tw_quant_mx", self.att.data_ptr(), M15, D, D, self.attq.data_ptr(), self.attq_s.data_ptr(),
+                      self.m15p, s)
+            self._gemm_mx(self.attq, self.attq_s, Q["wo"], M15, D, D, _lib.TW_EPI_RESID_F32, self.x, bias=L.bo,
+                          stream=st)
+            _lib.call("tw_layernorm_mx", self.x.data_ptr(), L.ln2_g.data_ptr(), L.ln2_b.data_ptr(), M15, D, LN_EPS,
+                      self.hq.data_ptr(), self.hq_s.data_ptr(), self.m15p, s)
+            self._gemm_mx(self.hq, self.hq_s, Q["w1"], M15, F, D, _lib.TW_EPI_GELU_MX, self.ffnq, bias=L.b1,
+                          sout=self.ffnq_s, stream=st)
+            self._gemm_mx(self.ffnq, self.ffnq_s, Q["w2"], M15, D, F, _lib.TW_EPI_RESID_F32, self.x, bias=L.b2,
+                          stream=st)
 
     def encoder_output(self, R: int) -> torch.Tensor:
         """Encoder last_hidden_state of the last encode() (bf16 view [R][1500][D])."""

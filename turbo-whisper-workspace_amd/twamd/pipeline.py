@@ -43,9 +43,10 @@ class TurboTranscriber:
     @staticmethod
     def from_pretrained(model: str = "large-v3-turbo", checkpoint: Optional[str] = None, seed: int = 1234,
                         max_batch: int = 24, device: str = "cuda", use_graphs: bool = True,
-                        max_beams: int = 1) -> "TurboTranscriber":
+                        max_beams: int = 1, enc_fp8: Optional[bool] = None) -> "TurboTranscriber":
         """`model`: a preset name (synthetic seeded weights) or, via `checkpoint`, a LOCAL Hugging Face
-        Whisper directory (config.json, *.safetensors, vocab.json, generation_config.json)."""
+        Whisper directory (config.json, *.safetensors, vocab.json, generation_config.json). enc_fp8: run the encoder
+        projections on MX fp8 (BASELINE config 5; default: env TW_ENC_FP8)."""
         if checkpoint is None and model not in PRESETS and os.path.isdir(model):
             checkpoint = model
         if checkpoint is not None:
@@ -60,7 +61,8 @@ class TurboTranscriber:
             gen = GenerationSettings.default(dims)
             vocab = WhisperVocab.synthetic(gen.special)
         weights = build_weights(dims, seed=seed, checkpoint=checkpoint)
-        eng = WhisperEngine(weights, gen, max_batch=max_batch, device=device, use_graphs=use_graphs, max_beams=max_beams)
+        eng = WhisperEngine(weights, gen, max_batch=max_batch, device=device, use_graphs=use_graphs, max_beams=max_beams,
+                            enc_fp8=enc_fp8)
         return TurboTranscriber(eng, vocab)
 
     # -------------------------------------------------------------- call
