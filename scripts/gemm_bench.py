@@ -21,6 +21,9 @@ SHAPES = [  # name, M, N, K, epi
     ("conv2", 36000, 1280, 3840, _lib.TW_EPI_F32),
     ("xkv", 36000, 10240, 1280, _lib.TW_EPI_BF16),
 ]
+if os.environ.get("GEMM_BENCH_B"):  # windows per batch (config 5: 64)
+    _M = int(os.environ["GEMM_BENCH_B"]) * 1500
+    SHAPES = [(n, _M, N, K, e) for n, _, N, K, e in SHAPES]
 
 
 def main():
@@ -38,7 +41,24 @@ def main():
             out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
         else:
             out = torch.zeros(M, N, device="cuda")
-        res = {1: [], 5: [], "blas": []}
+        res = {1: [], 5: [], "blas": [], "mx": []}
+        mx = name not in ("conv2", "xkv")  # the MX fp8 encoder GEMM (config 5) on the layer shapes
+        if mx:
+            Mp, Np = (M + 255) // 256 * 256, (N + 255) // 256 * 256
+            Aq = torch.empty(M, K, dtype=torch.uint8, device="cuda")
+            As = torch.zeros(K // 128, Mp, 4, dtype=torch.uint8, device="cuda")
+            Wq = torch.empty(N, K, dtype=torch.uint8, device="cuda")
+            Ws = torch.zeros(K // 128, Np, 4, dtype=torch.uint8, device="cuda")
+            _lib.call("tw_quant_mx", A.data_ptr(), M, K, K, Aq.data_ptr(), As.data_ptr(), Mp, s)
+            _lib.call("tw_quant_mx", W.data_ptr(), N, K, K, Wq.data_ptr(), Ws.data_ptr(), Np, s)
+            mepi = _lib.TW_EPI_GELU_MX if epi == _lib.TW_EPI_GELU_BF16 else epi
+            if mepi == _lib.TW_EPI_GELU_MX:
+                mout = torch.empty(M, N, dtype=torch.uint8, device="cuda")
+                mso = torch.zeros(N // 128, Mp, 4, dtype=torch.uint8, device="cuda")
+            else:
+                mout, mso = out, None
+        else:
+            del res["mx"]
         outs = {}
         for r in range(a.rounds):
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -62,6 +82,16 @@ def main():
                 res[v].append(st.elapsed_time(en) / a.iters)
                 if r == 0:
                     outs[v] = out.float().clone() / (a.iters if epi == _lib.TW_EPI_RESID_F32 else 1)
+            if mx:
+                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                st.record()
+                for _ in range(a.iters):
+                    _lib.call("tw_gemm_mx", Aq.data_ptr(), As.data_ptr(), Wq.data_ptr(), Ws.data_ptr(), M, N, K, K, K,
+                              Mp, Np, mepi, mout.data_ptr(), N, bias.data_ptr(), _lib.ptr(mso), Mp if mso is not None
+                              else 0, s)
+                en.record()
+                torch.cuda.synchronize()
+                res["mx"].append(st.elapsed_time(en) / a.iters)
         fl = 2.0 * M * N * K
         err = max((outs[1] - outs[v]).abs().max().item() for v in (5,))
         print(f"{name:7s} M={M} N={N} K={K}: " + "  ".join(

@@ -213,9 +213,7 @@ __device__ inline void epi_store4(const EpiArgs& ea, int m, int n, int N, float4
     return;
   }
   if constexpr (EPI == TW_EPI_BF16 || EPI == TW_EPI_GELU_BF16) {
-    if constexpr (EPI == TW_EPI_GELU_BF16) {
-      v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
-    }
+    if constexpr (EPI == TW_EPI_GELU_BF16) v = gelu_erf4(v);
     uint2 w;
     w.x = pack_bf16x2(v.x, v.y);
     w.y = pack_bf16x2(v.z, v.w);
@@ -227,8 +225,8 @@ __device__ inline void epi_store4(const EpiArgs& ea, int m, int n, int N, float4
     *o = x;
   } else if constexpr (EPI == TW_EPI_GELU_POS_F32) {
     const float4 a = *(const float4*)(ea.aux + (size_t)(m % ea.aux_rows) * ea.ldo + n);
-    float4 o;
-    o.x = gelu_erf(v.x) + a.x; o.y = gelu_erf(v.y) + a.y; o.z = gelu_erf(v.z) + a.z; o.w = gelu_erf(v.w) + a.w;
+    float4 o = gelu_erf4(v);
+    o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
     *(float4*)((float*)ea.out + (size_t)m * ea.ldo + n) = o;
   } else if constexpr (EPI == TW_EPI_F32) {
     *(float4*)((float*)ea.out + (size_t)m * ea.ldo + n) = v;
@@ -253,8 +251,8 @@ __device__ inline void epi_store8(const EpiArgs& ea, int m, int n, int N, float4
   if constexpr (EPI == TW_EPI_BF16 || EPI == TW_EPI_GELU_BF16 || EPI == TW_EPI_CROSSKV) {
     if (n + 7 < N) {
       if constexpr (EPI == TW_EPI_GELU_BF16) {
-        v0.x = gelu_erf(v0.x); v0.y = gelu_erf(v0.y); v0.z = gelu_erf(v0.z); v0.w = gelu_erf(v0.w);
-        v1.x = gelu_erf(v1.x); v1.y = gelu_erf(v1.y); v1.z = gelu_erf(v1.z); v1.w = gelu_erf(v1.w);
+        v0 = gelu_erf4(v0);
+        v1 = gelu_erf4(v1);
       }
       uint4 w;
       w.x = pack_bf16x2(v0.x, v0.y);
@@ -1419,7 +1417,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_mx(const uint8_t* __restrict__ 
       if constexpr (EPI == TW_EPI_GELU_MX) {
         // fc1 -> fc2 operand: GELU, then MX-quantise; the 8 lanes of a 32-column block share one scale
         // (N % 256 == 0 is checked on the host, so every lane of the group is inside N)
-        v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+        v = gelu_erf4(v);
         const uint32_t sbyte = mx_scale_byte(mx_group8_max(abs4max(v.x, v.y, v.z, v.w)));
         const uint32_t w = mx_pack4(v.x, v.y, v.z, v.w, mx_inv_scale(sbyte));
         if (m < M) {

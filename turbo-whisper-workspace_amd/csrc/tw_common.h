@@ -47,6 +47,38 @@ __device__ inline float erf_fast(float x) {
 }
 __device__ inline float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 
+// The same GELU on two values with packed f32 VALU (v_pk_fma_f32 / v_pk_mul_f32: two results per issue, the f32
+// vector peak): the GEMM epilogues evaluate it with no MFMA beside them (one workgroup per CU), so their cost is
+// pure VALU issue. Same operations and rounding order as gelu_erf, up to the final 0.5x(1+erf) = fma(0.5x, erf, 0.5x).
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+__device__ inline f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 u = x * 0.70710678118654752f;
+  const f32x2 z = __builtin_elementwise_abs(u);
+  const f32x2 d = z * 0.3275911f + 1.0f;
+  f32x2 t;
+  t.x = __builtin_amdgcn_rcpf(d.x);
+  t.y = __builtin_amdgcn_rcpf(d.y);
+  f32x2 p = t * 1.061405429f + -1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t + -0.284496736f;
+  p = p * t + 0.254829592f;
+  p = p * t;
+  const f32x2 q = (-z * z) * 1.4426950408889634f;
+  f32x2 e;
+  e.x = __builtin_amdgcn_exp2f(q.x);
+  e.y = __builtin_amdgcn_exp2f(q.y);
+  const f32x2 a = 1.0f - p * e;
+  f32x2 erf;
+  erf.x = copysignf(a.x, u.x);
+  erf.y = copysignf(a.y, u.y);
+  const f32x2 hx = x * 0.5f;
+  return hx * erf + hx;
+}
+__device__ inline float4 gelu_erf4(float4 v) {
+  const f32x2 a = gelu_erf2((f32x2){v.x, v.y}), b = gelu_erf2((f32x2){v.z, v.w});
+  return make_float4(a.x, a.y, b.x, b.y);
+}
+
 // ---- wave reductions (64 lanes) ----------------------------------------------------------------
 __device__ inline float wave_sum(float v) {
 #pragma unroll
