@@ -148,6 +148,10 @@ int tw_layernorm_mx(const float* x, const float* gamma, const float* beta, int M
  * Replaces WhisperAttention + eager_attention_forward/SDPA for the encoder
  * (modeling_whisper.py:215-238, 241-356). */
 int tw_attn_encoder(const uint16_t* qkv, int B, int S, int H, uint16_t* out, void* stream);
+/* tw_attn_encoder with the output stored as MX fp8 (out e4m3[B*S][H*64], scales [H*64/128][rows_pad][4]; format:
+ * "MX fp8 encoder" above), the out_proj operand of the config-5 encoder (modeling_whisper.py:350-356). H even. */
+int tw_attn_encoder_mx(const uint16_t* qkv, int B, int S, int H, uint8_t* out, uint8_t* scales, int rows_pad,
+                       void* stream);
 /* Measurement knob (process-wide, returns 0): encoder attention kernel of tw_attn_encoder. 8 (default) =
  * k_attn_enc2 with 8 waves / 256 queries per workgroup, 4 = the same with 4 waves, 0 = the first kernel. */
 int tw_attn_set_variant(int variant);

@@ -296,8 +296,8 @@ class WhisperOracle:
 
     def encode_mx(self, feats: np.ndarray) -> np.ndarray:
         """The config-5 encoder: conv stem, attention core and LayerNorms as encode(); the q/k/v/o and fc1/fc2
-        projections on MX fp8 operands quantised where the GPU quantises them (LayerNorm output f32, attention
-        output after its bf16 store, GELU(fc1) f32)."""
+        projections on MX fp8 operands quantised where the GPU quantises them (LayerNorm output, attention output
+        and GELU(fc1), each from f32)."""
         sd, H, hd = self.sd, self.H, self.D // self.H
         x = self.conv_stem(feats)
         for i in range(self.L_enc):
@@ -309,7 +309,7 @@ class WhisperOracle:
             T = q.shape[0]
             qh, kh, vh = (t.reshape(T, H, hd).transpose(1, 0, 2) for t in (q, k, v))
             o = (_softmax(qh @ kh.transpose(0, 2, 1)) @ vh).transpose(1, 0, 2).reshape(T, self.D)
-            x = x + self._lin_mx(mx_round(bf16_round(o)), f"{p}.self_attn.out_proj")
+            x = x + self._lin_mx(mx_round(o), f"{p}.self_attn.out_proj")
             h = mx_round(_ln(x, sd[f"{p}.final_layer_norm.weight"], sd[f"{p}.final_layer_norm.bias"]))
             x = (x + self._lin_mx(mx_round(_gelu(self._lin_mx(h, f"{p}.fc1"))), f"{p}.fc2")).astype(np.float32)
         return _ln(x, sd["model.encoder.layer_norm.weight"], sd["model.encoder.layer_norm.bias"]).astype(np.float32)

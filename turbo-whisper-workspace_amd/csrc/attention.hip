@@ -161,9 +161,13 @@ typedef __attribute__((address_space(3))) short4_t lds_short4_t;
 __device__ inline int k2_off(int key, int ch) { return key * 64 + ((ch ^ ((key >> 1) & 7)) << 3); }        // elements
 __device__ inline int v2_off(int key, int ch) { return key * 64 + ((ch ^ (((key >> 1) & 1) << 2)) << 3); } // elements
 
-template <int NW, int WPS>
+// MXO (config 5): the output is stored as MX fp8 for the fp8 out_proj (tw_common.h "MX fp8": one scale per 32 of the
+// head's 64 dims; a lane pair (lr, lr + 32) holds one query's 32-dim block in o0 / o1) instead of bf16.
+template <int NW, int WPS, bool MXO = false>
 __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc2(const bf16_t* __restrict__ qkv, int S, int H, int D, int nqb,
-                                                          int nwork, bf16_t* __restrict__ out) {
+                                                          int nwork, bf16_t* __restrict__ out,
+                                                          uint8_t* __restrict__ qout = nullptr,
+                                                          uint8_t* __restrict__ qscale = nullptr, int rows_pad = 0) {
   __shared__ __attribute__((aligned(16))) bf16_t kbuf[2][EA_KT * 64];
   __shared__ __attribute__((aligned(16))) bf16_t vbuf[2][EA_KT * 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -290,6 +294,36 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc2(const bf16_t* __rest
   }
 
   const int q = q0 + lr;
+  if constexpr (MXO) {
+    const float inv = 1.f / l_run;
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      o0[r] *= inv;
+      o1[r] *= inv;
+      a0 = fmaxf(a0, fabsf(o0[r]));
+      a1 = fmaxf(a1, fabsf(o1[r]));
+    }
+    a0 = fmaxf(a0, __shfl_xor(a0, 32, 64));
+    a1 = fmaxf(a1, __shfl_xor(a1, 32, 64));
+    const uint32_t s0b = mx_scale_byte(a0), s1b = mx_scale_byte(a1);
+    const float i0 = mx_inv_scale(s0b), i1 = mx_inv_scale(s1b);
+    if (q < S) {
+      const size_t row = (size_t)b * S + q;
+      uint8_t* op = qout + row * D + h * 64;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 8 * g + 4 * lh;
+        *(uint32_t*)(op + d) = mx_pack4(o0[4 * g], o0[4 * g + 1], o0[4 * g + 2], o0[4 * g + 3], i0);
+        *(uint32_t*)(op + 32 + d) = mx_pack4(o1[4 * g], o1[4 * g + 1], o1[4 * g + 2], o1[4 * g + 3], i1);
+      }
+      if (lh == 0) {
+        qscale[tw_mx_sidx((int)row, 2 * h, rows_pad)] = (uint8_t)s0b;
+        qscale[tw_mx_sidx((int)row, 2 * h + 1, rows_pad)] = (uint8_t)s1b;
+      }
+    }
+    return;
+  }
   if (q < S) {
     const float inv = 1.f / l_run;
     bf16_t* op = out + ((size_t)b * S + q) * D + h * 64;
@@ -330,6 +364,18 @@ extern "C" int tw_attn_encoder(const bf16_t* qkv, int B, int S, int H, bf16_t* o
     hipLaunchKernelGGL((k_attn_enc2<8, 2>), dim3(nwork), dim3(512), 0, st, qkv, S, H, D, nqb, nwork, out);
   }
   return tw_check_launch("tw_attn_encoder");
+}
+
+extern "C" int tw_attn_encoder_mx(const bf16_t* qkv, int B, int S, int H, uint8_t* out, uint8_t* scales, int rows_pad,
+                                  void* stream) {
+  TW_REQUIRE(qkv && out && scales && B > 0 && S > 0 && H > 0, "tw_attn_encoder_mx: bad args");
+  TW_REQUIRE(H % 2 == 0 && rows_pad >= B * S, "tw_attn_encoder_mx: H=%d (even: the 128-wide scale groups), rows_pad %d",
+             H, rows_pad);
+  const int D = H * 64;
+  const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
+  hipLaunchKernelGGL((k_attn_enc2<8, 2, true>), dim3(nwork), dim3(512), 0, (hipStream_t)stream, qkv, S, H, D, nqb,
+                     nwork, nullptr, out, scales, rows_pad);
+  return tw_check_launch("tw_attn_encoder_mx");
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -413,8 +413,8 @@ class WhisperEngine:
 
     def _encode_layers_mx(self, R: int, st) -> None:
         """The 32 encoder layers of config 5: LayerNorms emit MX fp8 (tw_layernorm_mx), q/k/v/o and fc1/fc2 run on
-        tw_gemm_mx, the attention core stays bf16 (its output is quantised once for out_proj), fc1's GELU output is
-        quantised in its epilogue."""
+        tw_gemm_mx, the attention core stays bf16 and stores its output as MX fp8 (tw_attn_encoder_mx), fc1's GELU
+        output is quantised in its epilogue."""
         d, w = self.d, self.w
         D, F, H = d.d_model, d.ffn, d.heads
         M15, s = R * S_ENC, st.cuda_stream
@@ -424,10 +424,9 @@ class WhisperEngine:
             self._gemm_mx(self.hq, self.hq_s, Q["wqkv"], M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv,
                           stream=st)
             rec = self._begin_timer(("attn_encoder", 0), 4.0 * S_ENC * S_ENC * 64 * H * R, st)
-            _lib.call("tw_attn_encoder", self.qkv.data_ptr(), R, S_ENC, H, self.att.data_ptr(), s)
+            _lib.call("tw_attn_encoder_mx", self.qkv.data_ptr(), R, S_ENC, H, self.attq.data_ptr(),
+                      self.attq_s.data_ptr(), self.m15p, s)
             self._end_timer(rec, st)
-            _lib.call("tw_quant_mx", self.att.data_ptr(), M15, D, D, self.attq.data_ptr(), self.attq_s.data_ptr(),
-                      self.m15p, s)
             self._gemm_mx(self.attq, self.attq_s, Q["wo"], M15, D, D, _lib.TW_EPI_RESID_F32, self.x, bias=L.bo,
                           stream=st)
             _lib.call("tw_layernorm_mx", self.x.data_ptr(), L.ln2_g.data_ptr(), L.ln2_b.data_ptr(), M15, D, LN_EPS,
