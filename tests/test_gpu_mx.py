@@ -156,16 +156,16 @@ def test_attn_encoder_mx_store_matches_bf16_kernel():
     """tw_attn_encoder_mx quantises the same attention output tw_attn_encoder stores as bf16: against the MX
     quantisation of that bf16 output, elements differ only where the bf16 rounding crossed an e4m3 rounding
     boundary (at most one step, a few % of elements)."""
-    B, S, H = 2, 1500, 4
+    B, L, H = 2, 1500, 4
     D = H * 64
     g = torch.Generator().manual_seed(5)
-    qkv = (torch.randn(B * S, 3 * D, generator=g) * 0.8).to(torch.bfloat16).to(DEV)
-    ref = torch.empty(B * S, D, dtype=torch.bfloat16, device=DEV)
-    _lib.call("tw_attn_encoder", qkv.data_ptr(), B, S, H, ref.data_ptr(), S())
-    rp = pad256(B * S)
-    q = torch.empty(B * S, D, dtype=torch.uint8, device=DEV)
+    qkv = (torch.randn(B * L, 3 * D, generator=g) * 0.8).to(torch.bfloat16).to(DEV)
+    ref = torch.empty(B * L, D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_attn_encoder", qkv.data_ptr(), B, L, H, ref.data_ptr(), S())
+    rp = pad256(B * L)
+    q = torch.empty(B * L, D, dtype=torch.uint8, device=DEV)
     s = torch.zeros(D // 128, rp, 4, dtype=torch.uint8, device=DEV)
-    _lib.call("tw_attn_encoder_mx", qkv.data_ptr(), B, S, H, q.data_ptr(), s.data_ptr(), rp, S())
+    _lib.call("tw_attn_encoder_mx", qkv.data_ptr(), B, L, H, q.data_ptr(), s.data_ptr(), rp, S())
     rq, rs = wo.mx_quant(ref.float().cpu().numpy())
-    frac = _byte_agreement(q.cpu().numpy(), scales_rowmajor(s, B * S), rq, rs)
+    frac = _byte_agreement(q.cpu().numpy(), scales_rowmajor(s, B * L), rq, rs)
     assert frac < 0.03, frac
