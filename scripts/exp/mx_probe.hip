@@ -80,7 +80,7 @@ int main() {
           Sa[l % 16][k] = ldexp(1.0, sa[l] - 127);
           Sb[k][l % 16] = ldexp(1.0, sb[l] - 127);
         }
-      double maxerr = 0;
+      double maxerr = 0, maxabs = 0, maxref = 0;
       for (int l = 0; l < 64; ++l)
         for (int r = 0; r < 4; ++r) {
           int row = (l >> 4) * 4 + r, col = l & 15;
@@ -88,9 +88,53 @@ int main() {
           for (int k = 0; k < 128; ++k) ref += Am[row][k] * Sa[row][k] * Bm[k][col] * Sb[k][col];
           double e = fabs(ref - C[4 * l + r]) / (1e-6 + fabs(ref));
           if (e > maxerr) maxerr = e;
+          maxabs = fmax(maxabs, fabs(ref - C[4 * l + r]));
+          maxref = fmax(maxref, fabs(ref));
         }
-      printf("pass %d (%s scales) hypothesis H%d: max rel err %.3g %s\n", pass, pass ? "random" : "unit", h + 1, maxerr,
-             maxerr < 1e-5 ? "MATCH" : "");
+      printf("pass %d (%s scales) hypothesis H%d: max rel err %.3g, max abs err %.3g of max |C| %.3g %s\n", pass,
+             pass ? "random" : "unit", h + 1, maxerr, maxabs, maxref, maxabs < 1e-6 * maxref ? "MATCH" : "");
+    }
+  }
+  // scale impulses: A all ones (B lane l bytes = w(l/16) in {1,2,4,8}) with lane L's A scale x2, and the mirror
+  // for B. dC[r][c] = sum over the K set the scale of lane L covers; H1 (lane l holds k = 32(l/16)+j) predicts
+  // dC = 32 w(block) on the rows/cols of lane L's row l%16 and nowhere else.
+  {
+    const unsigned char w8[4] = {0x38, 0x40, 0x48, 0x50};  // 1, 2, 4, 8
+    unsigned char Ao[64 * 32], Bw[64 * 32];
+    for (int l = 0; l < 64; ++l)
+      for (int j = 0; j < 32; ++j) { Ao[32 * l + j] = 0x38; Bw[32 * l + j] = w8[l / 16]; }
+    for (int side = 0; side < 2; ++side) {
+      hipMemcpy(dA, side == 0 ? Ao : Bw, sizeof Ao, hipMemcpyHostToDevice);
+      hipMemcpy(dB, side == 0 ? Bw : Ao, sizeof Ao, hipMemcpyHostToDevice);
+      int one[64];
+      for (int l = 0; l < 64; ++l) one[l] = 127;
+      hipMemcpy(dsa, one, 256, hipMemcpyHostToDevice); hipMemcpy(dsb, one, 256, hipMemcpyHostToDevice);
+      float base[256];
+      k_mfma<<<1, 64>>>(dA, dB, dsa, dsb, dC);
+      hipMemcpy(base, dC, 1024, hipMemcpyDeviceToHost);
+      int ok = 1;
+      for (int L = 0; L < 64; ++L) {
+        int sc[64];
+        for (int l = 0; l < 64; ++l) sc[l] = (l == L) ? 128 : 127;
+        hipMemcpy(side == 0 ? dsa : dsb, sc, 256, hipMemcpyHostToDevice);
+        k_mfma<<<1, 64>>>(dA, dB, dsa, dsb, dC);
+        hipMemcpy(C, dC, 1024, hipMemcpyDeviceToHost);
+        hipMemcpy(side == 0 ? dsa : dsb, one, 256, hipMemcpyHostToDevice);
+        char desc[512]; int n = 0; desc[0] = 0;
+        int good = 1;
+        for (int l = 0; l < 64; ++l)
+          for (int r = 0; r < 4; ++r) {
+            const int row = (l >> 4) * 4 + r, col = l & 15;
+            const float d = C[4 * l + r] - base[4 * l + r];
+            const int mine = side == 0 ? (row == (L & 15)) : (col == (L & 15));
+            const float expect = mine ? 32.f * (1 << (L / 16)) : 0.f;
+            if (d != expect) good = 0;
+            if (d != 0 && n < 400) n += snprintf(desc + n, 512 - n, " (%d,%d)=%g", row, col, d);
+          }
+        if (!good || L < 2 || L == 17 || L == 63) printf("%s-scale lane %2d %s:%.200s\n", side ? "B" : "A", L, good ? "H1" : "??", desc);
+        ok &= good;
+      }
+      printf("%s-scale map H1 (lane l -> row/col l%%16, K block l/16): %s\n", side ? "B" : "A", ok ? "CONFIRMED" : "NO");
     }
   }
   // conversion: RNE + saturation

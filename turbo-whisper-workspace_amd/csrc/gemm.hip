@@ -551,6 +551,7 @@ __device__ inline void p8_vmcnt() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
   else static_assert(N == 0, "unsupported vmcnt");
 }
 
@@ -1431,11 +1432,241 @@ __global__ __launch_bounds__(512, 1) void k_gemm_mx(const uint8_t* __restrict__ 
   }
 }
 
+// k_gemm_8p_mx: k_gemm_8p's 8-phase ping-pong schedule on MX fp8 operands (the default tw_gemm_mx kernel).
+// A K-tile is 128 fp8 elements = 128 bytes per row, so the four half-tiles are the same 16 KiB and the per-phase
+// ds_reads the same count (a 16x16x128 fragment is 32 bytes = two ds_read_b128), while each phase issues 8
+// v_mfma_scale_f32_16x16x128_f8f6f4 (32 cycles) where the bf16 kernel issued 16 16x16x32 (16 cycles): the same
+// MFMA time per phase for twice the K. Scales: per K-tile 1 KiB of A and 1 KiB of W scale dwords, one 4-byte
+// LDS-DMA per wave (waves 0-3: A rows 64w..64w+63, waves 4-7: W rows), staged with half-tile A0 in phase 1 and read
+// into registers (12 bytes per lane) in phase 1 of the K-tile that uses them: WAR distance 4 phases; the vmcnt
+// counts of phases 1 and 2 grow by that one DMA (5 instead of 4).
+#define MX8_SC (8 * 128 * MX_BK)  // byte offset of the scale area: after 2 buffers x 4 half-tiles of 16 KiB
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict__ A, const uint8_t* __restrict__ W,
+                                                       const uint8_t* __restrict__ Sa, const uint8_t* __restrict__ Sw,
+                                                       int M, int N, int K, int lda, int ldw, int Mp, int Np,
+                                                       EpiArgs ea) {
+  // K loop: 128 KiB of half-tiles + 2 x 2 KiB scales; epilogue: 8 x [64][68] f32 = 136 KiB (one array)
+  __shared__ __attribute__((aligned(16))) uint8_t smem[8 * 64 * GB_EPI_LD * 4];
+  constexpr int HT = 128 * MX_BK;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntm = (M + GB_BM - 1) / GB_BM, ntn = (N + GB_BN - 1) / GB_BN;
+  const int nwg = ntm * ntn;
+  const int orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int tm = wgid / ntn, tn = wgid - tm * ntn;
+  const int m0 = tm * GB_BM, n0 = tn * GB_BN;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  const uint8_t* gsrc[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = 8 * (2 * wid + i) + (lane >> 3);
+      const int ch = (lane & 7) ^ gb_swz(row);
+      gsrc[h][i] = h < 2 ? A + (size_t)min(m0 + 128 * h + row, M - 1) * lda + ch * 16
+                         : W + (size_t)min(n0 + 128 * (h - 2) + row, N - 1) * ldw + ch * 16;
+    }
+  // scale DMA: wave w < 4 -> A scale dwords of rows 64w + lane, w >= 4 -> W rows 64(w-4) + lane
+  const uint8_t* gsc = wid < 4 ? Sa + (size_t)(m0 + 64 * wid + lane) * 4 : Sw + (size_t)(n0 + 64 * (wid - 4) + lane) * 4;
+  const size_t gsc_step = (size_t)(wid < 4 ? Mp : Np) * 4;
+  auto stage = [&](int buf, int h, int kt) {
+    uint8_t* dst = smem + (buf * 4 + h) * HT;
+    const int k0 = kt * MX_BK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(gsrc[h][i] + k0), (lds_void_t*)(dst + 8 * (2 * wid + i) * MX_BK),
+                                       16, 0, 0);
+  };
+  auto stage_sc = [&](int buf, int kt) {
+    __builtin_amdgcn_global_load_lds((const void*)(gsc + kt * gsc_step),
+                                     (lds_void_t*)(smem + MX8_SC + buf * 2048 + wid * 256), 4, 0, 0);
+  };
+
+  i32x8 af[4], bfr[2];
+  int sa[2][4], sb[2][2];
+  auto frag = [&](const uint8_t* base, int row) {
+    const uint8_t* p = base + row * MX_BK;
+    const int4 lo = *(const int4*)(p + (((2 * fq) ^ gb_swz(row)) << 4));
+    const int4 hi = *(const int4*)(p + (((2 * fq + 1) ^ gb_swz(row)) << 4));
+    return (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  };
+  auto readA = [&](int buf, int mh) {
+    const uint8_t* As = smem + (buf * 4 + mh) * HT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag(As, 64 * wr + 16 * i + fr);
+  };
+  auto readB = [&](int buf, int nh) {
+    const uint8_t* Bs = smem + (buf * 4 + 2 + nh) * HT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bfr[j] = frag(Bs, 32 * wc + 16 * j + fr);
+  };
+  auto readS = [&](int buf) {  // this lane's scale bytes: (tile row, K block fq) of every fragment of the K-tile
+    const uint8_t* S = smem + MX8_SC + buf * 2048;
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sa[mh][i] = S[(128 * mh + 64 * wr + 16 * i + fr) * 4 + fq];
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) sb[nh][j] = S[1024 + (128 * nh + 32 * wc + 16 * j + fr) * 4 + fq];
+  };
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto mfma_q = [&](auto MH, auto NH) {
+    constexpr int mh = decltype(MH)::value, nh = decltype(NH)::value;
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[mh][nh][i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[mh][nh][i][j], 0, 0, 0,
+                                                                             sa[mh][i], 0, sb[nh][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+
+  const int nk = K / MX_BK;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage(0, h, 0);
+  stage_sc(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+  auto ktile = [&](int t, auto NXT) {
+    constexpr bool nxt = decltype(NXT)::value;
+    const int buf = t & 1, nb = buf ^ 1;
+    // phase 1: quadrant (A0, B0); this K-tile's scales into registers
+    readB(buf, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    readA(buf, 0);
+    readS(buf);
+    if constexpr (nxt) {
+      stage(nb, 0, t + 1);
+      stage_sc(nb, t + 1);
+      p8_vmcnt<5>();  // B1 of tile t (phase 3 of t-1)
+    } else {
+      p8_vmcnt<2>();
+    }
+    mfma_q(I0{}, I0{});
+    // phase 2: (A0, B1)
+    readB(buf, 1);
+    if constexpr (nxt) {
+      stage(nb, 2, t + 1);
+      p8_vmcnt<5>();  // A1 of tile t (phase 4 of t-1)
+    } else {
+      p8_vmcnt<0>();
+    }
+    mfma_q(I0{}, I1{});
+    // phase 3: (A1, B1)
+    readA(buf, 1);
+    if constexpr (nxt) stage(nb, 3, t + 1);
+    mfma_q(I1{}, I1{});
+    // phase 4: (A1, B0)
+    readB(buf, 0);
+    if constexpr (nxt) {
+      stage(nb, 1, t + 1);
+      p8_vmcnt<4>();  // A0 + scales, B0 of tile t+1 (phases 1, 2 of t)
+    }
+    mfma_q(I1{}, I0{});
+  };
+  using BT = std::integral_constant<bool, true>;
+  using BF = std::integral_constant<bool, false>;
+  for (int t = 0; t + 1 < nk; ++t) ktile(t, BT{});
+  ktile(nk - 1, BF{});
+  if (wr == 0) __builtin_amdgcn_s_barrier();
+  __syncthreads();
+
+  // epilogue as k_gemm_8p: 8 consecutive columns per lane, 8 lanes per 64-column row
+  const int rc = (lane & 7) * 8;
+  const int ncol = n0 + (rc < 32 ? 32 * wc + rc : 128 + 32 * wc + rc - 32);
+  float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+  if (ea.bias) {
+    b0.x = ea.bias[min(ncol, N - 1)];
+    b0.y = ea.bias[min(ncol + 1, N - 1)];
+    b0.z = ea.bias[min(ncol + 2, N - 1)];
+    b0.w = ea.bias[min(ncol + 3, N - 1)];
+    b1.x = ea.bias[min(ncol + 4, N - 1)];
+    b1.y = ea.bias[min(ncol + 5, N - 1)];
+    b1.z = ea.bias[min(ncol + 6, N - 1)];
+    b1.w = ea.bias[min(ncol + 7, N - 1)];
+  }
+  float* wimg = (float*)smem + wid * (64 * GB_EPI_LD);
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh) {
+    if (mh) __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            wimg[(i * 16 + fq * 4 + r) * GB_EPI_LD + nh * 32 + j * 16 + fr] = acc[mh][nh][i][j][r];
+    __syncthreads();
+    const int mrow0 = m0 + 128 * mh + 64 * wr;
+#pragma unroll 4
+    for (int rr = 0; rr < 8; ++rr) {
+      const int lr = rr * 8 + (lane >> 3);
+      const int m = mrow0 + lr;
+      float4 v0 = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
+      float4 v1 = *(const float4*)(wimg + lr * GB_EPI_LD + rc + 4);
+      v0.x += b0.x; v0.y += b0.y; v0.z += b0.z; v0.w += b0.w;
+      v1.x += b1.x; v1.y += b1.y; v1.z += b1.z; v1.w += b1.w;
+      if constexpr (EPI == TW_EPI_GELU_MX) {
+        // a 32-column block is 4 lanes x 8 columns (lanes 0-3 / 4-7 of the row's 8): absmax over xor 1, 2
+        v0 = gelu_erf4(v0);
+        v1 = gelu_erf4(v1);
+        float a = fmaxf(abs4max(v0.x, v0.y, v0.z, v0.w), abs4max(v1.x, v1.y, v1.z, v1.w));
+        a = fmaxf(a, __shfl_xor(a, 1, 64));
+        a = fmaxf(a, __shfl_xor(a, 2, 64));
+        const uint32_t sbyte = mx_scale_byte(a);
+        const float inv = mx_inv_scale(sbyte);
+        uint2 w;
+        w.x = mx_pack4(v0.x, v0.y, v0.z, v0.w, inv);
+        w.y = mx_pack4(v1.x, v1.y, v1.z, v1.w, inv);
+        if (m < M) {
+          *(uint2*)((uint8_t*)ea.out + (size_t)m * ea.ldo + ncol) = w;
+          if ((lane & 3) == 0) ea.sout[tw_mx_sidx(m, ncol >> 5, ea.s_rows)] = (uint8_t)sbyte;
+        }
+      } else {
+        if (m < M && ncol < N) epi_store8<EPI>(ea, m, ncol, N, v0, v1);
+      }
+    }
+  }
+}
+
+// tw_gemm_mx kernel choice (tw_gemm_mx_set_variant, A/B measurement): 8 = k_gemm_8p_mx (default), 1 = k_gemm_mx
+static int tw_gemm_mx_variant = 8;
+extern "C" int tw_gemm_mx_set_variant(int v) {
+  tw_gemm_mx_variant = (v == 1) ? 1 : 8;
+  return 0;
+}
+
 template <int EPI>
 static void launch_gemm_mx(const uint8_t* A, const uint8_t* Sa, const uint8_t* W, const uint8_t* Sw, int M, int N,
                            int K, int lda, int ldw, int Mp, int Np, const EpiArgs& ea, hipStream_t s) {
   const unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
-  hipLaunchKernelGGL(k_gemm_mx<EPI>, dim3(nwg), dim3(512), 0, s, A, W, Sa, Sw, M, N, K, lda, ldw, Mp, Np, ea);
+  if (tw_gemm_mx_variant == 1)
+    hipLaunchKernelGGL(k_gemm_mx<EPI>, dim3(nwg), dim3(512), 0, s, A, W, Sa, Sw, M, N, K, lda, ldw, Mp, Np, ea);
+  else
+    hipLaunchKernelGGL(k_gemm_8p_mx<EPI>, dim3(nwg), dim3(512), 0, s, A, W, Sa, Sw, M, N, K, lda, ldw, Mp, Np, ea);
 }
 
 extern "C" int tw_gemm_mx(const uint8_t* A, const uint8_t* Sa, const uint8_t* W, const uint8_t* Sw, int M, int N,
