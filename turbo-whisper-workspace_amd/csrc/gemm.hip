@@ -1289,9 +1289,11 @@ extern "C" int tw_gemv_packed(const bf16_t* A, int a_packed, int lda, const bf16
 // The structure is k_gemm_big's with BK = 128 elements: a K-step row is still 128 bytes, so the LDS-DMA staging,
 // the bank swizzle and the 24 ds_read_b128 per wave per K-step are unchanged, while one K-step now covers twice
 // the K (32 MFMAs of 16x16x128 per wave instead of 64 of 16x16x32). The K-step's scales (one dword per tile row:
-// 1 KiB for A, 1 KiB for W, contiguous in HBM) ride along by LDS-DMA from waves 0 and 1; lane l of a fragment
-// (row l % 16, K block l / 16 of the 16x16x128 operand, lane map checked by scripts/exp/mx_probe.hip) reads its
-// own scale byte with one ds_read_u8.
+// 1 KiB for A, 1 KiB for W, contiguous in HBM) ride along by LDS-DMA from waves 0 and 1. Lane map of the
+// 16x16x128 f8 operand, measured by scripts/exp/mx_probe.hip: lane l (row l % 16, group g = l / 16) holds K bytes
+// [16g, 16g+16) in its first 16 bytes and [64+16g, 64+16g+16) in its last 16, while its scale VGPR scales K block
+// g = [32g, 32g+32) of row l % 16 (the hardware pairs them up: block g's bytes sit in lane groups 2(g%2), 2(g%2)+1).
+// So a lane reads 16-byte chunks g and g+4 of the K-step row, and its own scale byte with one ds_read_u8.
 // ------------------------------------------------------------------------------------------------
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 #define MX_BK 128                                  // K elements (= bytes) per K-step
@@ -1365,8 +1367,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_mx(const uint8_t* __restrict__ 
     for (int j = 0; j < 4; ++j) {
       const int col = wc * 64 + j * 16 + fr;
       const uint8_t* p = Ws + col * MX_BK;
-      const int4 lo = *(const int4*)(p + (((2 * fq) ^ gb_swz(col)) << 4));
-      const int4 hi = *(const int4*)(p + (((2 * fq + 1) ^ gb_swz(col)) << 4));
+      const int4 lo = *(const int4*)(p + ((fq ^ gb_swz(col)) << 4));
+      const int4 hi = *(const int4*)(p + (((fq + 4) ^ gb_swz(col)) << 4));
       bfr[j] = (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
       sb[j] = SWs[col * 4 + fq];
     }
@@ -1374,8 +1376,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_mx(const uint8_t* __restrict__ 
     for (int i = 0; i < 8; ++i) {
       const int row = wr * 128 + i * 16 + fr;
       const uint8_t* p = As + row * MX_BK;
-      const int4 lo = *(const int4*)(p + (((2 * fq) ^ gb_swz(row)) << 4));
-      const int4 hi = *(const int4*)(p + (((2 * fq + 1) ^ gb_swz(row)) << 4));
+      const int4 lo = *(const int4*)(p + ((fq ^ gb_swz(row)) << 4));
+      const int4 hi = *(const int4*)(p + (((fq + 4) ^ gb_swz(row)) << 4));
       const i32x8 af = (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
       const int sa = SAs[row * 4 + fq];
 #pragma unroll
@@ -1490,8 +1492,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
   int sa[2][4], sb[2][2];
   auto frag = [&](const uint8_t* base, int row) {
     const uint8_t* p = base + row * MX_BK;
-    const int4 lo = *(const int4*)(p + (((2 * fq) ^ gb_swz(row)) << 4));
-    const int4 hi = *(const int4*)(p + (((2 * fq + 1) ^ gb_swz(row)) << 4));
+    const int4 lo = *(const int4*)(p + ((fq ^ gb_swz(row)) << 4));
+    const int4 hi = *(const int4*)(p + (((fq + 4) ^ gb_swz(row)) << 4));
     return (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
   };
   auto readA = [&](int buf, int mh) {
@@ -1653,7 +1655,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
 }
 
 // tw_gemm_mx kernel choice (tw_gemm_mx_set_variant, A/B measurement): 8 = k_gemm_8p_mx (default), 1 = k_gemm_mx
-static int tw_gemm_mx_variant = 8;
+static int tw_gemm_mx_variant = 1;  // 8 = k_gemm_8p_mx (WIP, wrong results)
 extern "C" int tw_gemm_mx_set_variant(int v) {
   tw_gemm_mx_variant = (v == 1) ? 1 : 8;
   return 0;

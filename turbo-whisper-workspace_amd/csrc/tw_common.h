@@ -49,7 +49,7 @@ __device__ inline float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x
 
 // The same GELU on two values with packed f32 VALU (v_pk_fma_f32 / v_pk_mul_f32: two results per issue, the f32
 // vector peak): the GEMM epilogues evaluate it with no MFMA beside them (one workgroup per CU), so their cost is
-// pure VALU issue. Same operations and rounding order as gelu_erf, up to the final 0.5x(1+erf) = fma(0.5x, erf, 0.5x).
+// pure VALU issue. Same operations and rounding order as gelu_erf (bit-identical results).
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 __device__ inline f32x2 gelu_erf2(f32x2 x) {
   const f32x2 u = x * 0.70710678118654752f;
@@ -72,7 +72,7 @@ __device__ inline f32x2 gelu_erf2(f32x2 x) {
   erf.x = copysignf(a.x, u.x);
   erf.y = copysignf(a.y, u.y);
   const f32x2 hx = x * 0.5f;
-  return hx * erf + hx;
+  return hx * (erf + 1.0f);  // (0.5x)(1+erf) exactly as gelu_erf rounds it
 }
 __device__ inline float4 gelu_erf4(float4 v) {
   const f32x2 a = gelu_erf2((f32x2){v.x, v.y}), b = gelu_erf2((f32x2){v.z, v.w});
