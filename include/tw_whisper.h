@@ -135,6 +135,9 @@ int tw_layernorm(const float* x, const float* gamma, const float* beta, int M, i
 int tw_gemm_mx(const uint8_t* A, const uint8_t* Sa, const uint8_t* W, const uint8_t* Sw, int M, int N, int K, int lda,
                int ldw, int Mp, int Np, int epi, void* out, int ldo, const float* bias, uint8_t* sout, int sout_rows,
                void* stream);
+/* Measurement knob (process-wide, returns 0): tw_gemm_mx's kernel, 0 = chosen by shape (default),
+ * 1 = k_gemm_mx (2-stage), 8 = k_gemm_8p_mx (8-phase ping-pong). */
+int tw_gemm_mx_set_variant(int v);
 /* bf16 src[rows][ld] -> MX fp8 dst[rows][K] + scales (K % 128 == 0). Encoder weights once at load; the
  * attention output before out_proj (modeling_whisper.py:350-356). */
 int tw_quant_mx(const uint16_t* src, int rows, int K, int ld, uint8_t* dst, uint8_t* scales, int rows_pad,

@@ -41,7 +41,7 @@ def main():
             out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
         else:
             out = torch.zeros(M, N, device="cuda")
-        res = {1: [], 5: [], "blas": [], "mx": []}
+        res = {1: [], 5: [], "blas": [], "mx1": [], "mx8": []}
         mx = name not in ("conv2", "xkv")  # the MX fp8 encoder GEMM (config 5) on the layer shapes
         if mx:
             Mp, Np = (M + 255) // 256 * 256, (N + 255) // 256 * 256
@@ -58,7 +58,7 @@ def main():
             else:
                 mout, mso = out, None
         else:
-            del res["mx"]
+            del res["mx1"], res["mx8"]
         outs = {}
         for r in range(a.rounds):
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -82,7 +82,10 @@ def main():
                 res[v].append(st.elapsed_time(en) / a.iters)
                 if r == 0:
                     outs[v] = out.float().clone() / (a.iters if epi == _lib.TW_EPI_RESID_F32 else 1)
-            if mx:
+            for mv in ((1, 8) if mx else ()):  # forced kernels (0 = by shape is restored below)
+                _lib.call("tw_gemm_mx_set_variant", mv)
+                if epi == _lib.TW_EPI_RESID_F32:
+                    out.zero_()
                 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 st.record()
                 for _ in range(a.iters):
@@ -91,13 +94,18 @@ def main():
                               else 0, s)
                 en.record()
                 torch.cuda.synchronize()
-                res["mx"].append(st.elapsed_time(en) / a.iters)
+                res[f"mx{mv}"].append(st.elapsed_time(en) / a.iters)
+                if r == 0:
+                    outs[f"mx{mv}"] = mout.float().clone() / (a.iters if epi == _lib.TW_EPI_RESID_F32 else 1)
         fl = 2.0 * M * N * K
         err = max((outs[1] - outs[v]).abs().max().item() for v in (5,))
+        if mx:
+            err = max(err, (outs["mx1"] - outs["mx8"]).abs().max().item())
         print(f"{name:7s} M={M} N={N} K={K}: " + "  ".join(
             f"{v}: med {sorted(t)[len(t) // 2]:.3f} ms min {min(t):.3f} ms = {fl / min(t) / 1e9:.0f} TF/s"
-            for v, t in res.items()) + f"  max|v1-vX|={err:.3g}", flush=True)
+            for v, t in res.items()) + f"  max|v1-v5|,|mx1-mx8|={err:.3g}", flush=True)
     _lib.call("tw_gemm_set_variant", 1)
+    _lib.call("tw_gemm_mx_set_variant", 0)
 
 
 if __name__ == "__main__":

@@ -65,9 +65,16 @@ def test_quant_mx_bit_exact_vs_oracle():
     assert np.array_equal(q.cpu().numpy(), wo.e4m3_bytes(rq))
 
 
+@pytest.fixture(params=[1, 8], ids=["k_gemm_mx", "k_gemm_8p_mx"])
+def mx_variant(request):
+    _lib.call("tw_gemm_mx_set_variant", request.param)
+    yield request.param
+    _lib.call("tw_gemm_mx_set_variant", 0)
+
+
 @pytest.mark.parametrize("M,N,K", [(300, 512, 1280), (1500, 1280, 1280), (257, 768, 1024), (600, 1280, 5120)])
 @pytest.mark.parametrize("epi", [_lib.TW_EPI_F32, _lib.TW_EPI_RESID_F32, _lib.TW_EPI_BF16])
-def test_gemm_mx_vs_float64(M, N, K, epi):
+def test_gemm_mx_vs_float64(M, N, K, epi, mx_variant):
     g = torch.Generator().manual_seed(M + N + K)
     A = (torch.randn(M, K, generator=g)).to(torch.bfloat16).to(DEV)
     W = (torch.randn(N, K, generator=g) * K ** -0.5).to(torch.bfloat16).to(DEV)
@@ -107,7 +114,7 @@ def _byte_agreement(got_q, got_s, ref_q, ref_s):
     return diff.mean()
 
 
-def test_gemm_mx_gelu_epilogue_quantises_like_oracle():
+def test_gemm_mx_gelu_epilogue_quantises_like_oracle(mx_variant):
     M, N, K = 700, 1024, 1280
     g = torch.Generator().manual_seed(11)
     A = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)

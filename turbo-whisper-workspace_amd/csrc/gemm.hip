@@ -244,6 +244,22 @@ __device__ inline void epi_store4(const EpiArgs& ea, int m, int n, int N, float4
   }
 }
 
+// the second f32 operand of a RESID / GELU_POS epilogue for 4 columns n..n+3 of row m (zeros when the group is
+// ragged: that path re-reads it element-wise in epi_store4)
+template <int EPI>
+__device__ inline float4 epi_addend(const EpiArgs& ea, int m, int n, bool full) {
+  if (!full) return make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (EPI == TW_EPI_RESID_F32) return *(const float4*)((const float*)ea.out + (size_t)m * ea.ldo + n);
+  else return *(const float4*)(ea.aux + (size_t)(m % ea.aux_rows) * ea.ldo + n);
+}
+// epi_store4 for a full group whose second operand `a` was loaded ahead
+template <int EPI>
+__device__ inline void epi_store4_pre(const EpiArgs& ea, int m, int n, float4 v, float4 a) {
+  if constexpr (EPI == TW_EPI_GELU_POS_F32) v = gelu_erf4(v);
+  v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+  *(float4*)((float*)ea.out + (size_t)m * ea.ldo + n) = v;
+}
+
 // epilogue of 8 consecutive columns n..n+7 of row m (v already includes the bias): one 16-byte store for the bf16
 // outputs (a wave's epilogue is store-issue bound: half the instructions of two 8-byte stores)
 template <int EPI>
@@ -367,9 +383,21 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ 
     bias4.w = ea.bias[min(n + 3, N - 1)];
   }
   float* wimg = (float*)smem + wid * (64 * GB_EPI_LD);
+  // epilogues that read a second f32 operand (RESID: the residual stream it updates in place; GELU_POS: the
+  // positional table) load it ahead: rows rr and rr + 8 of a half share a register slot, so a half costs two
+  // dependent HBM round trips instead of sixteen (the compiler cannot hoist a load above the previous row's store
+  // to the same buffer), and the first eight loads fly while the accumulators are staged through LDS.
+  constexpr bool PRE = EPI == TW_EPI_RESID_F32 || EPI == TW_EPI_GELU_POS_F32;
+  const bool full = ncol0 + rc + 3 < N;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int ib = 4 * half;
+    const int mrow0 = m0 + wr * 128 + ib * 16;
+    float4 ad[8];
+    if constexpr (PRE) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ad[q] = epi_addend<EPI>(ea, min(mrow0 + q * 4 + (lane >> 4), M - 1), ncol0 + rc, full);
+    }
     if (half) __syncthreads();  // (first pass: the K loop ended on a barrier)
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii)
@@ -378,14 +406,29 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ 
 #pragma unroll
         for (int r = 0; r < 4; ++r) wimg[(ii * 16 + fq * 4 + r) * GB_EPI_LD + j * 16 + fr] = acc[ib + ii][j][r];
     __syncthreads();
-    const int mrow0 = m0 + wr * 128 + ib * 16;
+    if constexpr (PRE) {
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int lr = rr * 4 + (lane >> 4);  // 4 rows per wave-instruction
+        const int m = mrow0 + lr;
+        float4 v = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
+        v.x += bias4.x; v.y += bias4.y; v.z += bias4.z; v.w += bias4.w;
+        if (full) {
+          if (m < M) epi_store4_pre<EPI>(ea, m, ncol0 + rc, v, ad[rr & 7]);
+        } else if (m < M && ncol0 + rc < N) {
+          epi_store4<EPI>(ea, m, ncol0 + rc, N, v);
+        }
+        if (rr < 8) ad[rr] = epi_addend<EPI>(ea, min(m + 32, M - 1), ncol0 + rc, full);
+      }
+    } else {
 #pragma unroll 4
-    for (int rr = 0; rr < 16; ++rr) {
-      const int lr = rr * 4 + (lane >> 4);  // 4 rows per wave-instruction
-      const int m = mrow0 + lr;
-      float4 v = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
-      v.x += bias4.x; v.y += bias4.y; v.z += bias4.z; v.w += bias4.w;
-      if (m < M && ncol0 + rc < N) epi_store4<EPI>(ea, m, ncol0 + rc, N, v);
+      for (int rr = 0; rr < 16; ++rr) {
+        const int lr = rr * 4 + (lane >> 4);
+        const int m = mrow0 + lr;
+        float4 v = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
+        v.x += bias4.x; v.y += bias4.y; v.z += bias4.z; v.w += bias4.w;
+        if (m < M && ncol0 + rc < N) epi_store4<EPI>(ea, m, ncol0 + rc, N, v);
+      }
     }
   }
 }
@@ -546,6 +589,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ns(const bf16_t* __restrict__ A
 //   RAW: a half-tile is waited for (vmcnt) before the first barrier of the phase before the one that reads it.
 //   WAR: a half-tile is restaged >= 2 phases after its last ds_read (A0 4, B0 2, B1 4, A1 4).
 // ------------------------------------------------------------------------------------------------
+// Buffer descriptor from values the compiler can prove wave-uniform (readfirstlane'd base halves and size): the
+// descriptor then lives in SGPRs and every buffer op through it is one instruction, not a waterfall loop.
+__device__ inline __amdgpu_buffer_rsrc_t tw_uniform_rsrc(const void* p, int bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
 template <int N>
 __device__ inline void p8_vmcnt() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -573,23 +625,32 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
   const int wr = wid >> 2, wc = wid & 3;
   const int fr = lane & 15, fq = lane >> 4;
 
-  // DMA: half-tile h (0 A0, 1 A1, 2 B0, 3 B1), wave instruction i = 0,1 fills rows 8(2*wid+i) .. +7
-  const bf16_t* gsrc[4][2];
+  // DMA: half-tile h (0 A0, 1 A1, 2 B0, 3 B1), wave instruction i = 0,1 fills rows 8(2*wid+i) .. +7.
+  // buffer_load ... lds through one descriptor per half-tile (wave-uniform base = the half-tile's first row,
+  // num_records = its rows inside M / N): the per-lane part is a 32-bit row/chunk offset (4 VGPRs instead of 8
+  // 64-bit pointers, so the kernel stays under 196 VGPRs and a decoder wave can co-reside on every SIMD), the
+  // K offset rides in soffset, and rows past M / N read as zeros (their outputs are never stored).
+  __amdgpu_buffer_rsrc_t rs[4];
 #pragma unroll
-  for (int h = 0; h < 4; ++h)
+  for (int h = 0; h < 4; ++h) {
+    const int r0 = (h < 2 ? m0 : n0) + 128 * (h & 1), lim = h < 2 ? M : N, ld = h < 2 ? lda : ldw;
+    const int rows = max(0, min(128, lim - r0));
+    rs[h] = tw_uniform_rsrc((h < 2 ? A : W) + (size_t)r0 * ld, rows * ld * 2);
+  }
+  unsigned voff[2][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = 8 * (2 * wid + i) + (lane >> 3);
-      const int ch = (lane & 7) ^ gb_swz(row);
-      gsrc[h][i] = h < 2 ? A + (size_t)min(m0 + 128 * h + row, M - 1) * lda + ch * 8
-                         : W + (size_t)min(n0 + 128 * (h - 2) + row, N - 1) * ldw + ch * 8;
-    }
+  for (int i = 0; i < 2; ++i) {
+    const int row = 8 * (2 * wid + i) + (lane >> 3);
+    const int ch = (lane & 7) ^ gb_swz(row);
+    voff[0][i] = (unsigned)(row * lda + ch * 8) * 2u;
+    voff[1][i] = (unsigned)(row * ldw + ch * 8) * 2u;
+  }
   auto stage = [&](int buf, int h, int k0) {
     bf16_t* dst = smem + (buf * 4 + h) * HT;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(gsrc[h][i] + k0), (lds_void_t*)(dst + 8 * (2 * wid + i) * GB_BK),
-                                       16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs[h], (lds_void_t*)(dst + 8 * (2 * wid + i) * GB_BK), 16,
+                                               voff[h >> 1][i], (unsigned)k0 * 2u, 0, 0);
   };
 
   bf16x8 af[4][2], bfr[2][2];
@@ -705,8 +766,21 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
     b1.w = ea.bias[min(ncol + 7, N - 1)];
   }
   float* wimg = (float*)smem + wid * (64 * GB_EPI_LD);
+  // RESID / GELU_POS: second operand loaded ahead, rows rr and rr + 4 sharing a slot (see k_gemm_big)
+  constexpr bool PRE = EPI == TW_EPI_RESID_F32 || EPI == TW_EPI_GELU_POS_F32;
+  const bool full = ncol + 7 < N;
 #pragma unroll
   for (int mh = 0; mh < 2; ++mh) {
+    const int mrow0 = m0 + 128 * mh + 64 * wr;
+    float4 ad[4][2];
+    if constexpr (PRE) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int mq = min(mrow0 + q * 8 + (lane >> 3), M - 1);
+        ad[q][0] = epi_addend<EPI>(ea, mq, ncol, full);
+        ad[q][1] = epi_addend<EPI>(ea, mq, ncol + 4, full);
+      }
+    }
     if (mh) __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -718,8 +792,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
           for (int r = 0; r < 4; ++r)
             wimg[(i * 16 + fq * 4 + r) * GB_EPI_LD + nh * 32 + j * 16 + fr] = acc[mh][nh][i][j][r];
     __syncthreads();
-    const int mrow0 = m0 + 128 * mh + 64 * wr;
-#pragma unroll 4
+#pragma unroll
     for (int rr = 0; rr < 8; ++rr) {
       const int lr = rr * 8 + (lane >> 3);
       const int m = mrow0 + lr;
@@ -727,7 +800,23 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
       float4 v1 = *(const float4*)(wimg + lr * GB_EPI_LD + rc + 4);
       v0.x += b0.x; v0.y += b0.y; v0.z += b0.z; v0.w += b0.w;
       v1.x += b1.x; v1.y += b1.y; v1.z += b1.z; v1.w += b1.w;
-      if (m < M && ncol < N) epi_store8<EPI>(ea, m, ncol, N, v0, v1);
+      if constexpr (PRE) {
+        if (full) {
+          if (m < M) {
+            epi_store4_pre<EPI>(ea, m, ncol, v0, ad[rr & 3][0]);
+            epi_store4_pre<EPI>(ea, m, ncol + 4, v1, ad[rr & 3][1]);
+          }
+        } else if (m < M && ncol < N) {
+          epi_store8<EPI>(ea, m, ncol, N, v0, v1);
+        }
+        if (rr < 4) {
+          const int mq = min(m + 32, M - 1);
+          ad[rr][0] = epi_addend<EPI>(ea, mq, ncol, full);
+          ad[rr][1] = epi_addend<EPI>(ea, mq, ncol + 4, full);
+        }
+      } else {
+        if (m < M && ncol < N) epi_store8<EPI>(ea, m, ncol, N, v0, v1);
+      }
     }
   }
 }
@@ -1434,7 +1523,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_mx(const uint8_t* __restrict__ 
   }
 }
 
-// k_gemm_8p_mx: k_gemm_8p's 8-phase ping-pong schedule on MX fp8 operands (the default tw_gemm_mx kernel).
+// k_gemm_8p_mx: k_gemm_8p's 8-phase ping-pong schedule on MX fp8 operands (tw_gemm_mx's FFN-shape kernel).
 // A K-tile is 128 fp8 elements = 128 bytes per row, so the four half-tiles are the same 16 KiB and the per-phase
 // ds_reads the same count (a 16x16x128 fragment is 32 bytes = two ds_read_b128), while each phase issues 8
 // v_mfma_scale_f32_16x16x128_f8f6f4 (32 cycles) where the bf16 kernel issued 16 16x16x32 (16 cycles): the same
@@ -1654,18 +1743,25 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
   }
 }
 
-// tw_gemm_mx kernel choice (tw_gemm_mx_set_variant, A/B measurement): 8 = k_gemm_8p_mx (default), 1 = k_gemm_mx
-static int tw_gemm_mx_variant = 1;  // 8 = k_gemm_8p_mx (WIP, wrong results)
+// tw_gemm_mx kernel choice: 0 = by shape (default), 1 = k_gemm_mx, 8 = k_gemm_8p_mx (tw_gemm_mx_set_variant, A/B).
+// Measured (scripts/gemm_bench.py, B = 24 and 64 windows): the 8-phase kernel wins on the long-K / wide-N FFN
+// shapes (fc1 +10-14 %, fc2 +14-18 %) and on o_proj at M = 96000 (+11 %); the 2-stage kernel on qkv (+3-5 %) and
+// on o_proj at M = 36000 (+2 %).
+static int tw_gemm_mx_variant = 0;
 extern "C" int tw_gemm_mx_set_variant(int v) {
-  tw_gemm_mx_variant = (v == 1) ? 1 : 8;
+  tw_gemm_mx_variant = (v == 1 || v == 8) ? v : 0;
   return 0;
+}
+static inline bool mx_use_8p(int M, int N, int K) {
+  if (tw_gemm_mx_variant) return tw_gemm_mx_variant == 8;
+  return N >= 4096 || K >= 4096 || (N <= 1280 && M >= 65536);
 }
 
 template <int EPI>
 static void launch_gemm_mx(const uint8_t* A, const uint8_t* Sa, const uint8_t* W, const uint8_t* Sw, int M, int N,
                            int K, int lda, int ldw, int Mp, int Np, const EpiArgs& ea, hipStream_t s) {
   const unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
-  if (tw_gemm_mx_variant == 1)
+  if (!mx_use_8p(M, N, K))
     hipLaunchKernelGGL(k_gemm_mx<EPI>, dim3(nwg), dim3(512), 0, s, A, W, Sa, Sw, M, N, K, lda, ldw, Mp, Np, ea);
   else
     hipLaunchKernelGGL(k_gemm_8p_mx<EPI>, dim3(nwg), dim3(512), 0, s, A, W, Sa, Sw, M, N, K, lda, ldw, Mp, Np, ea);

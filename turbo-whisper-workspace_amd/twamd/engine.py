@@ -84,6 +84,47 @@ class DecView:
     fp: Optional[torch.Tensor] = None  # packed-activation fc1 output (fc2's A operand)
 
 
+class _EncoderPump:
+    """Paced queueing of a pipelined encoder prefetch (run_batches). ROCm's launch call costs ~60 us of host time
+    once a queue holds more than a few ms of pending work (~7 us otherwise; measured with rocprofv3
+    --hip-runtime-trace), and a decode step is 49 launches replayed node by node from the host: queueing the whole
+    next-batch encoder up front made every launch of the overlapped decode steps slow (2.8 ms per step instead of
+    ~0.5). The pump instead queues the encoder one chunk (conv stem / layer) at a time, keeping at most `ahead`
+    chunks pending on enc_stream, and is called from the decode loop between steps."""
+
+    def __init__(self, eng: "WhisperEngine", steps, ahead: int = 2):
+        self.eng, self.steps, self.ahead = eng, steps, ahead
+        self.pending: List[torch.cuda.Event] = []
+        self.done = False
+
+    def __call__(self) -> bool:
+        """Queue chunks while fewer than `ahead` are unfinished; True if anything was queued."""
+        queued = False
+        while not self.done:
+            while self.pending and self.pending[0].query():
+                self.pending.pop(0)
+            if len(self.pending) >= self.ahead:
+                break
+            self._one()
+            queued = True
+        return queued
+
+    def _one(self) -> None:
+        try:
+            next(self.steps)
+        except StopIteration:
+            self.done = True
+            return
+        ev = torch.cuda.Event()
+        ev.record(self.eng.enc_stream)
+        self.pending.append(ev)
+
+    def drain(self) -> None:
+        while not self.done:
+            self._one()
+        self.pending.clear()
+
+
 @dataclasses.dataclass
 class PassResult:
     tokens: List[List[int]]      # generated tokens per row (as _sample returns them, before stripping)
@@ -99,6 +140,8 @@ class WhisperEngine:
         # kernel-variant overrides for A/B measurement (defaults are the measured-best kernels)
         if os.environ.get("TW_GEMM_VARIANT"):
             _lib.call("tw_gemm_set_variant", int(os.environ["TW_GEMM_VARIANT"], 0))
+        if os.environ.get("TW_GEMM_MX_VARIANT"):
+            _lib.call("tw_gemm_mx_set_variant", int(os.environ["TW_GEMM_MX_VARIANT"], 0))
         if os.environ.get("TW_ATTN_VARIANT"):
             _lib.call("tw_attn_set_variant", int(os.environ["TW_ATTN_VARIANT"], 0))
         d = weights.dims
@@ -204,6 +247,8 @@ class WhisperEngine:
         self._own_streams = {x.cuda_stream for x in [self.stream, self.enc_stream] + self._chain_streams}
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self._chain_cache: Dict[tuple, List[DecView]] = {}
+        self._pump: Optional[_EncoderPump] = None  # paced next-batch encoder (run_batches)
+        self.dec_ahead = int(os.environ.get("TW_DEC_AHEAD", "2"))  # decode steps queued ahead while pumping
         # decoder projections in the packed fragment layout (tw_pack_weight; +~342 MB at large-v3-turbo): every
         # wave-load of the per-token GEMVs is one contiguous 1 KiB fragment. TW_DEC_PACKED=0 keeps the row-major
         # skinny GEMM path (A/B measurement).
@@ -327,6 +372,10 @@ class WhisperEngine:
                   out.data_ptr(), (stream or self.stream).cuda_stream)
 
     # ------------------------------------------------------------------ streams / slots
+    def _pump_drain(self) -> None:
+        if self._pump is not None:
+            self._pump.drain()
+
     def _enc_begin(self, sync: bool):
         """Front-end/encoder work goes to enc_stream. sync: it is ordered after everything already queued on the
         decoder stream (host writes of wave/row_map/seek made there), and _enc_end makes the decoder stream wait
@@ -380,6 +429,13 @@ class WhisperEngine:
         """Encoder over R windows: slot r reads feats[slot][row_map[r]][:, seek[r]:] (zero padded to 3000), then
         projects every decoder layer's cross-attention K/V into cross_kv_buf[slot] (batch stride R). Runs on
         enc_stream (see _enc_begin for `sync`)."""
+        self._pump_drain()  # a paced prefetch shares the encoder's activation buffers: queue all of it first
+        for _ in self._encode_steps(R, row_map, seek, slot, sync):
+            pass
+
+    def _encode_steps(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True):
+        """encode() as a generator that yields after the conv stem and after every layer, so a pipelined prefetch
+        can queue the encoder a layer at a time (run_batches' _EncoderPump). Every launch names enc_stream."""
         d, w = self.d, self.w
         slot = self._slot if slot is None else slot
         D, F, H = d.d_model, d.ffn, d.heads
@@ -393,8 +449,9 @@ class WhisperEngine:
         _lib.call("tw_im2col_conv2", self.h1.data_ptr(), R, D, self.a2.data_ptr(), s)
         self._gemm(self.a2, w.conv2_w, M15, D, 3 * D, _lib.TW_EPI_GELU_POS_F32, self.x, bias=w.conv2_b,
                    aux=w.pos_enc, aux_rows=S_ENC, stream=st)
+        yield
         if self.enc_fp8:
-            self._encode_layers_mx(R, st)
+            yield from self._encode_layers_mx(R, st)
         for L in ([] if self.enc_fp8 else w.enc):
             self._ln(self.x, L.ln1_g, L.ln1_b, M15, self.hln, stream=st)
             self._gemm(self.hln, L.wqkv, M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv, stream=st)
@@ -405,13 +462,14 @@ class WhisperEngine:
             self._ln(self.x, L.ln2_g, L.ln2_b, M15, self.hln, stream=st)
             self._gemm(self.hln, L.w1, M15, F, D, _lib.TW_EPI_GELU_BF16, self.ffn, bias=L.b1, stream=st)
             self._gemm(self.ffn, L.w2, M15, D, F, _lib.TW_EPI_RESID_F32, self.x, bias=L.b2, stream=st)
+            yield
         self._ln(self.x, w.enc_ln_g, w.enc_ln_b, M15, self.hln, stream=st)  # encoder last_hidden_state (bf16)
         geom = (ctypes.c_int * 4)(S_ENC, R, D, H)
         self._gemm(self.hln, w.wkv_x, M15, d.decoder_layers * 2 * D, D, _lib.TW_EPI_CROSSKV, self.cross_kv_buf[slot],
                    bias=w.bkv_x, kv_geom=geom, stream=st)
         self._enc_end(sync, slot)
 
-    def _encode_layers_mx(self, R: int, st) -> None:
+    def _encode_layers_mx(self, R: int, st):
         """The 32 encoder layers of config 5: LayerNorms emit MX fp8 (tw_layernorm_mx), q/k/v/o and fc1/fc2 run on
         tw_gemm_mx, the attention core stays bf16 and stores its output as MX fp8 (tw_attn_encoder_mx), fc1's GELU
         output is quantised in its epilogue."""
@@ -435,6 +493,7 @@ class WhisperEngine:
                           sout=self.ffnq_s, stream=st)
             self._gemm_mx(self.ffnq, self.ffnq_s, Q["w2"], M15, D, F, _lib.TW_EPI_RESID_F32, self.x, bias=L.b2,
                           stream=st)
+            yield
 
     def encoder_output(self, R: int) -> torch.Tensor:
         """Encoder last_hidden_state of the last encode() (bf16 view [R][1500][D])."""
@@ -670,6 +729,7 @@ class WhisperEngine:
         graphs = [self._graph_for(R, params, i, c) for i, c in enumerate(chains)] if self.use_graphs else None
         for c in chains:
             c.stream.wait_stream(self.stream)
+        pump, inflight = self._pump, []
         while steps < max_new:
             n = min(check_every, max_new - steps)
             for _ in range(n):
@@ -679,6 +739,15 @@ class WhisperEngine:
                             graphs[i].replay()
                     else:
                         self._gen_step(c.n, params, v=c, r_enc=R)
+                if pump is not None:  # keep both queues shallow: <= dec_ahead steps, <= pump.ahead encoder chunks
+                    ev = torch.cuda.Event()
+                    ev.record(chains[-1].stream)
+                    inflight.append(ev)
+                    while len(inflight) > self.dec_ahead:
+                        if inflight[0].query():
+                            inflight.pop(0)
+                        elif not pump():
+                            inflight.pop(0).synchronize()
             steps += n
             for c in chains:
                 self.stream.wait_stream(c.stream)
@@ -939,6 +1008,14 @@ class WhisperEngine:
                 self.logmel(sizes[k], slot=k % 2, sync=False)
                 self.encode(sizes[k], row_map=False, seek=False, slot=k % 2, sync=False)
 
+        def prefetch_steps(k):  # the same work as prefetch(k), queued chunk by chunk by an _EncoderPump
+            with torch.cuda.stream(self.enc_stream):
+                if load is not None:
+                    load(k)
+                self.logmel(sizes[k], slot=k % 2, sync=False)
+            yield
+            yield from self._encode_steps(sizes[k], row_map=False, seek=False, slot=k % 2, sync=False)
+
         # the first prefetch is ordered after whatever the caller queued on the decoder stream
         self.enc_stream.wait_stream(self.stream)
         out = []
@@ -946,6 +1023,7 @@ class WhisperEngine:
         self.batch_passes = []
         self.batch_token_timestamps = []
         overlap = os.environ.get("TW_OVERLAP", "1") != "0"  # 0: encoder and decoder strictly in turn (A/B)
+        paced = os.environ.get("TW_PACED", "1") != "0"  # 0: queue the next batch's encoder up front (A/B)
         if sizes:
             prefetch(0)
         for k, n in enumerate(sizes):
@@ -953,9 +1031,17 @@ class WhisperEngine:
                 self.enc_stream.wait_stream(self.stream)
                 prefetch(k)
             if overlap and k + 1 < len(sizes):
-                prefetch(k + 1)  # runs beside the decode of batch k
+                if paced:  # runs beside the decode of batch k, queued between its decode steps
+                    self._pump = _EncoderPump(self, prefetch_steps(k + 1))
+                    self._pump()
+                else:
+                    prefetch(k + 1)
             kw = dict(gen_kwargs, **(batch_kwargs[k] if batch_kwargs else {}))
-            out.append(self.generate(n, slot=k % 2, pre_encoded=True, **kw))
+            try:
+                out.append(self.generate(n, slot=k % 2, pre_encoded=True, **kw))
+            finally:
+                self._pump_drain()
+                self._pump = None
             self.batch_langs.append(self.last_langs)
             self.batch_passes.append(self.last_passes)
             self.batch_token_timestamps.append(self.last_token_timestamps)
