@@ -96,12 +96,17 @@ def main():
     # HIP events around every launch of the dominant kernel (k_gemm_big) on the engine stream, inside the
     # timed region (the encoder is not graph-captured; ~0.3 us per event against 0.2-1 ms per launch)
     eng.timers, eng.timer_families = ({}, {dom}) if os.environ.get("TW_BENCH_TIMERS", "1") != "0" else (None, None)
+    if eng.hostprof is not None:
+        eng.hostprof.update(replay=0.0, pump=0.0, wait=0.0, steps=0)
     t0 = time.perf_counter()
     seqs = run(a.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if eng.hostprof is not None and rank == 0:  # TW_HOSTPROF=1: host seconds in graph replay / pump / waits
+        print("hostprof", json.dumps({k: round(v, 4) for k, v in eng.hostprof.items()}), "wall", round(dt, 4),
+              file=sys.stderr)
     fam = eng.timer_summary()
     eng.timers, eng.timer_families = None, None
     if world > 1:

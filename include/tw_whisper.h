@@ -258,6 +258,18 @@ int tw_embed_decoder(const uint16_t* tok_emb, const uint16_t* pos_emb, const int
 int tw_logits_select(const float* logits, int B, int ld_logits, const uint32_t* suppress_bits,
                      const TwSelectParams* params, int* state, int* tokens_out, int ld_tokens, int* next_ids,
                      int* pos, float* workspace, void* stream);
+/* tw_logits_select (mode 0, next_ids and pos required) fused with the head of the next decoder step: the chosen
+ * token is embedded at the row's incremented position into x f32[B][D] (as tw_embed_decoder) and the first decoder
+ * layer's self_attn_layer_norm (gamma, beta, eps) is written to out bf16 — row-major [B][D], or the packed
+ * activation layout when packed != 0 (B <= 32, D % 32 == 0; as tw_resid_layernorm_packed). max_pos = rows of
+ * pos_emb (a position past it, after the last step, reads the last row; that embedding is never consumed).
+ * Same results as tw_logits_select + tw_embed_decoder + tw_resid_layernorm[_packed](nparts 0) in two launches
+ * instead of four (the step's graph starts at the first layer's q/k/v projection). */
+int tw_logits_select_embed(const float* logits, int B, int ld_logits, const uint32_t* suppress_bits,
+                           const TwSelectParams* params, int* state, int* tokens_out, int ld_tokens, int* next_ids,
+                           int* pos, float* workspace, const uint16_t* tok_emb, const uint16_t* pos_emb, int D,
+                           int max_pos, float* x, const float* gamma, const float* beta, float eps, uint16_t* out,
+                           int packed, void* stream);
 
 #ifdef __cplusplus
 }

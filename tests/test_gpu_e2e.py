@@ -165,6 +165,24 @@ def test_graph_replay_equals_eager(tr):
     assert a == b
 
 
+@pytest.mark.parametrize("graphs", [True, False], ids=["graphs", "eager"])
+def test_fused_select_embed_equals_separate_launches(tr, graphs):
+    """tw_logits_select_embed (selection + the next step's embedding + layer 0's LayerNorm in one launch, the
+    default greedy step) decodes exactly what the separate select / embed / LayerNorm launches decode."""
+    eng = tr.engine
+    _load(tr, [speech_like(30.0, 21), white_noise(30.0, 5), speech_like(17.0, 8)])
+    eng.use_graphs = graphs
+    try:
+        eng.fused_select = True
+        a = eng.generate(3, task="transcribe", max_new_tokens=40, return_timestamps=True)
+        eng.fused_select = False
+        b = eng.generate(3, task="transcribe", max_new_tokens=40, return_timestamps=True)
+    finally:
+        eng.fused_select = True
+        eng.use_graphs = True
+    assert a == b
+
+
 def test_pipelined_batches_equal_sequential(tr):
     """run_batches (encoder of batch k+1 on the second stream beside the decode of batch k) returns exactly what
     per-batch synchronous generate() returns."""

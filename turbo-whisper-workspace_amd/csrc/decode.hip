@@ -137,15 +137,13 @@ __global__ __launch_bounds__(256) void k_select_partial(const float* __restrict_
   }
 }
 
-// grid B, one wave: merge the row's chunk records (in chunk order: ties keep the first index), then
-// the selection rule of the timestamp processor, the pad-after-EOS / stopping rule of _sample, and
-// the processor state update.
-__global__ __launch_bounds__(64) void k_select_final(const SelPart* __restrict__ ws, int NC, TwSelectParams p,
-                                                     int* __restrict__ state, int* __restrict__ tokens_out,
-                                                     int ld_tokens, int* __restrict__ next_ids,
-                                                     int* __restrict__ pos) {
-  TW_DEC_PRIO();
-  const int b = blockIdx.x, lane = threadIdx.x;
+// One wave per row: merge the row's chunk records (in chunk order: ties keep the first index), then the
+// selection rule of the timestamp processor, the pad-after-EOS / stopping rule of _sample, and the processor
+// state update. Lane 0 returns the token fed to the next step (tok) and the row's next position (npos).
+__device__ inline void select_final_row(const SelPart* __restrict__ ws, int NC, const TwSelectParams& p,
+                                        int* __restrict__ state, int* __restrict__ tokens_out, int ld_tokens,
+                                        int* __restrict__ next_ids, int* __restrict__ pos, int b, int lane,
+                                        int& tok_out, int& npos) {
   Best bt{-INFINITY, 0x7fffffff}, bs{-INFINITY, 0x7fffffff};
   float m_ts = -INFINITY, s_ts = 0.f;
   for (int c = lane; c < NC; c += 64) {
@@ -166,12 +164,14 @@ __global__ __launch_bounds__(64) void k_select_final(const SelPart* __restrict__
   if (lane != 0) return;
   int* st = state + b * TW_STATE_STRIDE;
   const int n_gen = st[TW_ST_NGEN], last = st[TW_ST_LAST];
-  if (pos) pos[b] += 1;  // the next decoder step writes its K/V one position later
+  npos = 0;
+  if (pos) npos = pos[b] += 1;  // the next decoder step writes its K/V one position later
   int sel;
   if (p.mode == 1) {
     sel = bt.i;
     st[TW_ST_LANG] = sel;
     if (next_ids) next_ids[b] = sel;
+    tok_out = sel;
     return;
   }
   if (p.use_timestamps) {
@@ -191,6 +191,68 @@ __global__ __launch_bounds__(64) void k_select_final(const SelPart* __restrict__
   if (tok >= p.ts_begin && p.use_timestamps) st[TW_ST_LASTTS] = tok;
   st[TW_ST_NGEN] = n_gen + 1;
   if (!finished && (tok == p.eos || n_gen + 1 >= p.max_new)) st[TW_ST_FINISHED] = 1;
+  tok_out = tok;
+}
+
+// grid B, one wave per row
+__global__ __launch_bounds__(64) void k_select_final(const SelPart* __restrict__ ws, int NC, TwSelectParams p,
+                                                     int* __restrict__ state, int* __restrict__ tokens_out,
+                                                     int ld_tokens, int* __restrict__ next_ids,
+                                                     int* __restrict__ pos) {
+  TW_DEC_PRIO();
+  int tok, npos;
+  select_final_row(ws, NC, p, state, tokens_out, ld_tokens, next_ids, pos, blockIdx.x, threadIdx.x, tok, npos);
+}
+
+// k_select_final fused with the head of the NEXT decoder step (grid B, 256 threads per row): wave 0 selects the
+// token, then the block embeds it at the row's next position (embed_tokens + embed_positions, f32 residual
+// stream x, as k_embed_decoder) and writes the first layer's self_attn_layer_norm output (as k_resid_ln with no
+// partials). Replaces three launches per generated token with one; the results are those of the three.
+#define SFE_MAXV 4  // float4 chunks per thread: D <= 4096
+template <bool PACKED>
+__global__ __launch_bounds__(256) void k_select_final_embed(const SelPart* __restrict__ ws, int NC, TwSelectParams p,
+                                                            int* __restrict__ state, int* __restrict__ tokens_out,
+                                                            int ld_tokens, int* __restrict__ next_ids,
+                                                            int* __restrict__ pos, const bf16_t* __restrict__ tok_emb,
+                                                            const bf16_t* __restrict__ pos_emb, int D, int max_pos,
+                                                            float* __restrict__ x, const float* __restrict__ g,
+                                                            const float* __restrict__ bta, float eps,
+                                                            bf16_t* __restrict__ out) {
+  TW_DEC_PRIO();
+  __shared__ float red[8];
+  __shared__ int sh[2];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid < 64) {
+    int tok = 0, npos = 0;
+    select_final_row(ws, NC, p, state, tokens_out, ld_tokens, next_ids, pos, b, tid, tok, npos);
+    if (tid == 0) {
+      sh[0] = tok;
+      sh[1] = min(npos, max_pos - 1);  // (past the last step: the embedding is never consumed)
+    }
+  }
+  __syncthreads();
+  const bf16_t* te = tok_emb + (size_t)sh[0] * D;
+  const bf16_t* pe = pos_emb + (size_t)sh[1] * D;
+  float* xr = x + (size_t)b * D;
+  const int nc = D >> 2;
+  float4 v[SFE_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < SFE_MAXV; ++i) {
+    const int c = min(tid + 256 * i, nc - 1);
+    const uint2 t = ((const uint2*)te)[c], q = ((const uint2*)pe)[c];
+    float4 a;
+    a.x = bf16_to_f32((bf16_t)(t.x & 0xffff)) + bf16_to_f32((bf16_t)(q.x & 0xffff));
+    a.y = bf16_to_f32((bf16_t)(t.x >> 16)) + bf16_to_f32((bf16_t)(q.x >> 16));
+    a.z = bf16_to_f32((bf16_t)(t.y & 0xffff)) + bf16_to_f32((bf16_t)(q.y & 0xffff));
+    a.w = bf16_to_f32((bf16_t)(t.y >> 16)) + bf16_to_f32((bf16_t)(q.y >> 16));
+    v[i] = a;
+    if (tid + 256 * i < nc) {
+      ((float4*)xr)[tid + 256 * i] = a;
+      s += (a.x + a.y) + (a.z + a.w);
+    }
+  }
+  tw_row_ln_store<PACKED>(v, s, b, D, eps, g, bta, out, red);
 }
 
 extern "C" int tw_logits_select(const float* logits, int B, int ld_logits, const uint32_t* suppress_bits,
@@ -207,6 +269,31 @@ extern "C" int tw_logits_select(const float* logits, int B, int ld_logits, const
   hipLaunchKernelGGL(k_select_final, dim3(B), dim3(64), 0, s, ws, TW_SELECT_CHUNKS, *params, state, tokens_out,
                      ld_tokens, next_ids, pos);
   return tw_check_launch("tw_logits_select");
+}
+
+extern "C" int tw_logits_select_embed(const float* logits, int B, int ld_logits, const uint32_t* suppress_bits,
+                                      const TwSelectParams* params, int* state, int* tokens_out, int ld_tokens,
+                                      int* next_ids, int* pos, float* workspace, const uint16_t* tok_emb,
+                                      const uint16_t* pos_emb, int D, int max_pos, float* x, const float* gamma,
+                                      const float* beta, float eps, uint16_t* out, int packed, void* stream) {
+  TW_REQUIRE(logits && params && state && workspace && next_ids && pos && B > 0, "tw_logits_select_embed: bad args");
+  TW_REQUIRE(params->mode == 0, "tw_logits_select_embed: greedy token selection (mode 0) only");
+  TW_REQUIRE(params->V > 0 && params->V <= ld_logits, "tw_logits_select_embed: V=%d ld=%d", params->V, ld_logits);
+  TW_REQUIRE(params->n_begin_suppress >= 0 && params->n_begin_suppress <= 8, "tw_logits_select_embed: begin_suppress");
+  TW_REQUIRE(tok_emb && pos_emb && x && gamma && beta && out && max_pos > 0, "tw_logits_select_embed: embed/LN args");
+  TW_REQUIRE(D > 0 && D % 4 == 0 && D <= 1024 * SFE_MAXV && (!packed || (B <= 32 && D % 32 == 0)),
+             "tw_logits_select_embed: D=%d B=%d packed=%d", D, B, packed);
+  hipStream_t s = (hipStream_t)stream;
+  SelPart* ws = (SelPart*)workspace;
+  hipLaunchKernelGGL(k_select_partial, dim3(B, TW_SELECT_CHUNKS), dim3(256), 0, s, logits, ld_logits, suppress_bits,
+                     *params, state, ws);
+  if (packed)
+    hipLaunchKernelGGL(k_select_final_embed<true>, dim3(B), dim3(256), 0, s, ws, TW_SELECT_CHUNKS, *params, state,
+                       tokens_out, ld_tokens, next_ids, pos, tok_emb, pos_emb, D, max_pos, x, gamma, beta, eps, out);
+  else
+    hipLaunchKernelGGL(k_select_final_embed<false>, dim3(B), dim3(256), 0, s, ws, TW_SELECT_CHUNKS, *params, state,
+                       tokens_out, ld_tokens, next_ids, pos, tok_emb, pos_emb, D, max_pos, x, gamma, beta, eps, out);
+  return tw_check_launch("tw_logits_select_embed");
 }
 
 // =================================================================================================

@@ -193,38 +193,7 @@ __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const f
       if (tid + 256 * i < nc) ((float4*)xr)[tid + 256 * i] = v[i];
   }
   if (!g) return;
-  s = wave_sum(s);
-  if ((tid & 63) == 0) red[tid >> 6] = s;
-  __syncthreads();
-  const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)D;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < RLN_MAXV; ++i) {
-    if (tid + 256 * i < nc) {
-      const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
-      q += (a * a + b * b) + (c * c + d * d);
-    }
-  }
-  q = wave_sum(q);
-  if ((tid & 63) == 0) red[4 + (tid >> 6)] = q;
-  __syncthreads();
-  const float rstd = rsqrtf((red[4] + red[5] + red[6] + red[7]) / (float)D + eps);
-  bf16_t* orow = out + (size_t)row * D;
-#pragma unroll
-  for (int i = 0; i < RLN_MAXV; ++i) {
-    const int c = tid + 256 * i;
-    if (c < nc) {
-      const float4 gg = ((const float4*)g)[c], bb = ((const float4*)bta)[c];
-      uint2 w;
-      w.x = pack_bf16x2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
-      w.y = pack_bf16x2((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
-      if constexpr (PACKED) {
-        *(uint2*)(out + tw_pack_act_idx(row, 4 * c)) = w;  // 4 columns = half a 16-byte fragment chunk
-      } else {
-        ((uint2*)orow)[c] = w;
-      }
-    }
-  }
+  tw_row_ln_store<PACKED>(v, s, row, D, eps, g, bta, out, red);
 }
 
 extern "C" int tw_resid_layernorm(float* x, const float* parts, int nparts, const float* bias, const float* gamma,

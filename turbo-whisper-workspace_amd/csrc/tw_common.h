@@ -159,6 +159,49 @@ __host__ __device__ inline size_t tw_pack_w_idx(int n, int k, int K) {
   return ((size_t)((n >> 4) * (K >> 5) + (k >> 5)) * 64 + (n & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
 }
 
+// ---- decoder row LayerNorm (one 256-thread block per row) ----------------------------------------
+// The row's d_model values sit as float4 chunks c = tid + 256 i in v[i] (valid for c < D/4), s = this thread's
+// partial sum of them. Writes bf16(LayerNorm(row) * g + bta) row-major (out + row * D) or in the packed
+// activation layout. red: 8 floats of LDS. Shared by k_resid_ln and the fused select/embed/LN tail.
+template <bool PACKED, int NV>
+__device__ inline void tw_row_ln_store(const float4 (&v)[NV], float s, int row, int D, float eps,
+                                       const float* __restrict__ g, const float* __restrict__ bta,
+                                       bf16_t* __restrict__ out, float* red) {
+  const int tid = threadIdx.x, nc = D >> 2;
+  s = wave_sum(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    if (tid + 256 * i < nc) {
+      const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+      q += (a * a + b * b) + (c * c + d * d);
+    }
+  }
+  q = wave_sum(q);
+  if ((tid & 63) == 0) red[4 + (tid >> 6)] = q;
+  __syncthreads();
+  const float rstd = rsqrtf((red[4] + red[5] + red[6] + red[7]) / (float)D + eps);
+  bf16_t* orow = out + (size_t)row * D;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nc) {
+      const float4 gg = ((const float4*)g)[c], bb = ((const float4*)bta)[c];
+      uint2 w;
+      w.x = pack_bf16x2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
+      w.y = pack_bf16x2((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+      if constexpr (PACKED) {
+        *(uint2*)(out + tw_pack_act_idx(row, 4 * c)) = w;  // 4 columns = half a 16-byte fragment chunk
+      } else {
+        ((uint2*)orow)[c] = w;
+      }
+    }
+  }
+}
+
 // ---- error plumbing -------------------------------------------------------------------------------
 enum {
   TW_OK = 0,

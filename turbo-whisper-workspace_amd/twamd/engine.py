@@ -16,6 +16,7 @@ from __future__ import annotations
 import ctypes
 import dataclasses
 import os
+import time
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -248,7 +249,12 @@ class WhisperEngine:
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self._chain_cache: Dict[tuple, List[DecView]] = {}
         self._pump: Optional[_EncoderPump] = None  # paced next-batch encoder (run_batches)
-        self.dec_ahead = int(os.environ.get("TW_DEC_AHEAD", "2"))  # decode steps queued ahead while pumping
+        self.dec_ahead = int(os.environ.get("TW_DEC_AHEAD", "2"))
+        # greedy steps end with the fused select + next-step embedding + first LayerNorm (tw_logits_select_embed):
+        # 47 launches per token instead of 49. TW_FUSED_SELECT=0: the separate kernels (A/B)
+        self.fused_select = os.environ.get("TW_FUSED_SELECT", "1") != "0"
+        self.hostprof = ({"replay": 0.0, "pump": 0.0, "wait": 0.0, "steps": 0}
+                         if os.environ.get("TW_HOSTPROF") == "1" else None)  # decode steps queued ahead while pumping
         # decoder projections in the packed fragment layout (tw_pack_weight; +~342 MB at large-v3-turbo): every
         # wave-load of the per-token GEMVs is one contiguous 1 KiB fragment. TW_DEC_PACKED=0 keeps the row-major
         # skinny GEMM path (A/B measurement).
@@ -514,10 +520,12 @@ class WhisperEngine:
                   v.stream.cuda_stream)
 
     @on_engine_streams
-    def decoder_step(self, R: int, with_logits: bool = True, v: Optional[DecView] = None, r_enc: Optional[int] = None
-                     ) -> None:
+    def decoder_step(self, R: int, with_logits: bool = True, v: Optional[DecView] = None, r_enc: Optional[int] = None,
+                     pre_embedded: bool = False) -> None:
         """One token per row of view v (default: rows 0..R-1): ids[b] at position pos[b] -> logits[b] (f32).
         r_enc: the batch size the current cross-K/V was encoded with (its batch stride; default R).
+        pre_embedded: the view's xd and first-layer LayerNorm output already hold this step's input (written by the
+        previous step's fused select, _select(embed_next=True)); the step starts at layer 0's q/k/v projection.
 
         Residual stream xd stays f32; every d_model-wide projection (self/cross out_proj, fc2) is a split-K
         partial product whose sum, bias and residual add are folded into the next LayerNorm launch."""
@@ -525,7 +533,7 @@ class WhisperEngine:
         if v is None and self.packed_decoder and R > 32:  # the packed layout holds 32 rows: one pass per 32
             r_enc = R if r_enc is None else r_enc
             for r0 in range(0, R, 32):
-                self.decoder_step(min(32, R - r0), with_logits, self._view(r0, min(32, R - r0)), r_enc)
+                self.decoder_step(min(32, R - r0), with_logits, self._view(r0, min(32, R - r0)), r_enc, pre_embedded)
             return
         v = v or self._view()
         r_enc = R if r_enc is None else r_enc
@@ -533,13 +541,15 @@ class WhisperEngine:
         st = v.stream
         s = st.cuda_stream
         if v.hp is not None:
-            return self._decoder_step_packed(R, with_logits, v, r_enc)
-        _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), v.ids.data_ptr(), v.pos.data_ptr(), R, D,
-                  v.xd.data_ptr(), s)
+            return self._decoder_step_packed(R, with_logits, v, r_enc, pre_embedded)
+        if not pre_embedded:
+            _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), v.ids.data_ptr(), v.pos.data_ptr(), R,
+                      D, v.xd.data_ptr(), s)
         xkv_stride = 2 * r_enc * H * S_ENC * 64
         nparts, pbias = 0, None
         for li, L in enumerate(w.dec):
-            self._resid_ln(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
+            if li or not pre_embedded:
+                self._resid_ln(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
             self._gemm(v.hd, L.wqkv, R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, bias=L.bqkv, stream=st)
             _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
                       self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
@@ -559,21 +569,24 @@ class WhisperEngine:
             self._resid_ln(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
             self._gemm(v.hd, w.emb, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, stream=st)
 
-    def _decoder_step_packed(self, R: int, with_logits: bool, v: DecView, r_enc: int) -> None:
+    def _decoder_step_packed(self, R: int, with_logits: bool, v: DecView, r_enc: int, pre_embedded: bool = False
+                             ) -> None:
         """decoder_step on the packed-GEMV path: LayerNorm outputs and fc1's GELU output are packed activations,
         attention outputs stay row-major, the d_model-wide projections are split-K partials (as decoder_step)."""
         d, w = self.d, self.w
         D, F, H, T = d.d_model, d.ffn, d.heads, d.max_target_positions
         st = v.stream
         s = st.cuda_stream
-        _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), v.ids.data_ptr(), v.pos.data_ptr(), R, D,
-                  v.xd.data_ptr(), s)
+        if not pre_embedded:
+            _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), v.ids.data_ptr(), v.pos.data_ptr(), R,
+                      D, v.xd.data_ptr(), s)
         xkv_stride = 2 * r_enc * H * S_ENC * 64
         nparts, pbias = 0, None
         PART, K4 = _lib.TW_EPI_PARTIAL_F32, DEC_SPLITS
         for li, L in enumerate(w.dec):
             P = self.dec_p[li]
-            self._resid_ln_p(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
+            if li or not pre_embedded:
+                self._resid_ln_p(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
             self._gemv(v.hp, True, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
             _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
                       self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
@@ -658,15 +671,42 @@ class WhisperEngine:
             p.begin_suppress[i] = t
         return p
 
-    def _select(self, R: int, params: _lib.TwSelectParams, tokens: bool = True, v: Optional[DecView] = None) -> None:
+    def _select(self, R: int, params: _lib.TwSelectParams, tokens: bool = True, v: Optional[DecView] = None,
+                embed_next: bool = False) -> None:
+        """Processors + greedy selection for the view's rows; embed_next: also the head of the next step (the chosen
+        token's embedding into xd and layer 0's self_attn_layer_norm into the view's LN buffer, one fused launch)."""
         v = v or self._view()
+        if embed_next:
+            L0 = self.w.dec[0]
+            packed = v.hp is not None
+            _lib.call("tw_logits_select_embed", v.logits.data_ptr(), R, self.d.vocab, self.suppress_bits.data_ptr(),
+                      ctypes.byref(params), v.state.data_ptr(), v.tokens.data_ptr() if tokens else None,
+                      v.tokens.shape[1], v.ids.data_ptr(), v.pos.data_ptr(), v.sel_ws.data_ptr(),
+                      self.w.emb.data_ptr(), self.w.pos_dec.data_ptr(), self.d.d_model, self.d.max_target_positions,
+                      v.xd.data_ptr(), L0.ln1_g.data_ptr(), L0.ln1_b.data_ptr(), LN_EPS,
+                      (v.hp if packed else v.hd).data_ptr(), int(packed), v.stream.cuda_stream)
+            return
         _lib.call("tw_logits_select", v.logits.data_ptr(), R, self.d.vocab, self.suppress_bits.data_ptr(),
                   ctypes.byref(params), v.state.data_ptr(), v.tokens.data_ptr() if tokens else None,
                   v.tokens.shape[1], v.ids.data_ptr(), v.pos.data_ptr(), v.sel_ws.data_ptr(), v.stream.cuda_stream)
 
-    def _gen_step(self, R: int, params, v: Optional[DecView] = None, r_enc: Optional[int] = None) -> None:
-        self.decoder_step(R, v=v, r_enc=r_enc)
-        self._select(R, params, v=v)
+    def _embed_head(self, v: DecView) -> None:
+        """The head of a decoder step alone (embedding + layer 0's self_attn_layer_norm) for view v: primes a chain
+        whose captured steps run pre_embedded."""
+        L0 = self.w.dec[0]
+        _lib.call("tw_embed_decoder", self.w.emb.data_ptr(), self.w.pos_dec.data_ptr(), v.ids.data_ptr(),
+                  v.pos.data_ptr(), v.n, self.d.d_model, v.xd.data_ptr(), v.stream.cuda_stream)
+        if v.hp is not None:
+            self._resid_ln_p(v.n, 0, None, L0.ln1_g, L0.ln1_b, v)
+        else:
+            self._resid_ln(v.n, 0, None, L0.ln1_g, L0.ln1_b, v)
+
+    def _gen_step(self, R: int, params, v: Optional[DecView] = None, r_enc: Optional[int] = None,
+                  fused: bool = False) -> None:
+        """One generated token. fused: the step starts pre-embedded and ends by embedding its token for the next
+        step (tw_logits_select_embed); only for a view whose previous step did the same or that was primed."""
+        self.decoder_step(R, v=v, r_enc=r_enc, pre_embedded=fused)
+        self._select(R, params, v=v, embed_next=fused)
 
     @on_engine_streams
     def decode_pass(self, R: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
@@ -726,19 +766,31 @@ class WhisperEngine:
         # generation loop: the rows split into chains on their own high-priority streams, each replaying its
         # captured decode step; the chains' latency-bound kernels run concurrently
         chains = self._chains(R)
-        graphs = [self._graph_for(R, params, i, c) for i, c in enumerate(chains)] if self.use_graphs else None
+        fused = self.fused_select
+        graphs = ([self._graph_for(R, params, i, c, fused) for i, c in enumerate(chains)] if self.use_graphs
+                  else None)
         for c in chains:
             c.stream.wait_stream(self.stream)
+            if fused and max_new > 1:
+                with torch.cuda.stream(c.stream):
+                    self._embed_head(c)
         pump, inflight = self._pump, []
+        hp = self.hostprof  # optional host-time accounting (TW_HOSTPROF=1): replay / pump / wait seconds
+        clk = time.perf_counter
         while steps < max_new:
             n = min(check_every, max_new - steps)
             for _ in range(n):
+                t0 = clk() if hp is not None else 0.0
                 for i, c in enumerate(chains):
                     if graphs is not None:
                         with torch.cuda.stream(c.stream):
                             graphs[i].replay()
                     else:
-                        self._gen_step(c.n, params, v=c, r_enc=R)
+                        self._gen_step(c.n, params, v=c, r_enc=R, fused=fused)
+                if hp is not None:
+                    t1 = clk()
+                    hp["replay"] += t1 - t0
+                    hp["steps"] += 1
                 if pump is not None:  # keep both queues shallow: <= dec_ahead steps, <= pump.ahead encoder chunks
                     ev = torch.cuda.Event()
                     ev.record(chains[-1].stream)
@@ -746,8 +798,16 @@ class WhisperEngine:
                     while len(inflight) > self.dec_ahead:
                         if inflight[0].query():
                             inflight.pop(0)
-                        elif not pump():
-                            inflight.pop(0).synchronize()
+                        else:
+                            tp = clk() if hp is not None else 0.0
+                            queued = pump()
+                            if hp is not None:
+                                hp["pump"] += clk() - tp
+                            if not queued:
+                                tw = clk() if hp is not None else 0.0
+                                inflight.pop(0).synchronize()
+                                if hp is not None:
+                                    hp["wait"] += clk() - tw
             steps += n
             for c in chains:
                 self.stream.wait_stream(c.stream)
@@ -870,9 +930,9 @@ class WhisperEngine:
             self._chain_cache[key] = views
         return self._chain_cache[key]
 
-    def _graph_for(self, R: int, params, i: int, v: DecView) -> Optional[torch.cuda.CUDAGraph]:
+    def _graph_for(self, R: int, params, i: int, v: DecView, fused: bool = False) -> Optional[torch.cuda.CUDAGraph]:
         al = self._align
-        key = (R, params.max_new, params.use_timestamps, self._slot, i,
+        key = (R, params.max_new, params.use_timestamps, self._slot, i, fused,
                None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()))
         g = self._graphs.get(key)
         if g is not None:
@@ -881,7 +941,7 @@ class WhisperEngine:
         v.stream.wait_stream(self.stream)
         with torch.cuda.stream(v.stream):
             with torch.cuda.graph(g, stream=v.stream):  # records, does not execute
-                self._gen_step(v.n, params, v=v, r_enc=R)
+                self._gen_step(v.n, params, v=v, r_enc=R, fused=fused)
         self.stream.wait_stream(v.stream)
         self._graphs[key] = g
         return g
