@@ -138,6 +138,10 @@ int tw_gemm_mx(const uint8_t* A, const uint8_t* Sa, const uint8_t* W, const uint
 /* Measurement knob (process-wide, returns 0): tw_gemm_mx's kernel, 0 = chosen by shape (default),
  * 1 = k_gemm_mx (2-stage), 8 = k_gemm_8p_mx (8-phase ping-pong). */
 int tw_gemm_mx_set_variant(int v);
+/* Measurement knob (process-wide, returns 0): tile rows per group of the large-M GEMM tile order (0 = by shape,
+ * the default: 8 for N >= 2560, else 1; 1 = row-major: one A row panel against every W column panel in turn).
+ * Applies to tw_gemm_bf16 and tw_gemm_mx. */
+int tw_gemm_set_group(int group_m);
 /* bf16 src[rows][ld] -> MX fp8 dst[rows][K] + scales (K % 128 == 0). Encoder weights once at load; the
  * attention output before out_proj (modeling_whisper.py:350-356). */
 int tw_quant_mx(const uint16_t* src, int rows, int K, int ld, uint8_t* dst, uint8_t* scales, int rows_pad,

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
     _lib.load()
+    if os.environ.get("GEMM_BENCH_GROUP"):  # tile rows per group of the large-M tile order (tw_gemm_set_group)
+        _lib.call("tw_gemm_set_group", int(os.environ["GEMM_BENCH_GROUP"]))
     s = torch.cuda.current_stream().cuda_stream
     for name, M, N, K, epi in SHAPES:
         A = (torch.randn(M, K, device="cuda") * 0.5).to(torch.bfloat16)

@@ -29,7 +29,24 @@ struct EpiArgs {
   int kv_S, kv_B, kv_D, kv_H;  // EPI_CROSSKV scatter geometry
   uint8_t* sout;      // EPI_GELU_MX: e8m0 scales of the fp8 output, [N/128][s_rows][4]
   int s_rows;
+  int group_m;        // large-M kernels: tile rows per group of the tile order (tw_tile_grouped); <= 1 row-major
 };
+
+// Tile (tm, tn) of tile id `wgid` (after the XCD remap, which hands each XCD a contiguous id range) in grouped
+// order: groups of gm tile rows, walked down the group's rows first. The ~32 tiles one XCD runs at once then span
+// gm A row panels x 32/gm W column panels instead of 1 x 32, so each K-step's operand slices are shared by more
+// of the XCD's CUs through its L2 (row-major order re-streams every W panel once per A row panel).
+__device__ inline void tw_tile_grouped(int wgid, int ntm, int ntn, int gm, int& tm, int& tn) {
+  if (gm <= 1) {
+    tm = wgid / ntn;
+    tn = wgid - tm * ntn;
+    return;
+  }
+  const int per = gm * ntn, g = wgid / per, first = g * gm;
+  const int rows = min(ntm - first, gm), l = wgid - g * per;
+  tm = first + l % rows;
+  tn = l / rows;
+}
 
 template <int EPI>
 __device__ inline void epi_store(const EpiArgs& ea, int m, int n, float v) {
@@ -78,7 +95,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(const bf16_t* __restrict__
   const int orig = blockIdx.x;
   const int q = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
-  const int tm = wgid / ntn, tn = wgid - tm * ntn;
+  int tm, tn;
+  tw_tile_grouped(wgid, ntm, ntn, ea.group_m, tm, tn);
   const int m0 = tm * G_BM, n0 = tn * G_BN;
 
   // staging assignment: 4 chunks of A + 4 chunks of W per thread (16 B each)
@@ -168,6 +186,18 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tile(const bf16_t* __restrict__
 // raw barrier, setprio), 4 = k_gemm_ns<BN=128, 3 stages>. Measured on the encoder shapes (scripts/gemm_bench.py,
 // random operands): 1 ~ 3 (641-1079 TF/s), 4 is 12-18% slower, a 4-stage BK=32 ring was 6% slower.
 static int tw_gemm_big_enabled = 1;
+// tw_tile_grouped rows per group for the large-M kernels (tw_gemm_set_group; 0 = by shape). Measured
+// (scripts/gemm_bench.py, M = 36000, groups 1/4/8/16): 8 gains 2-7 % on the wide-N shapes (q/k/v, fc1, cross-K/V:
+// >= 15 column tiles), while the 5-column-tile shapes (o_proj, fc2, conv2) are best row-major.
+static int tw_gemm_group_m = 0;
+extern "C" int tw_gemm_set_group(int gm) {
+  tw_gemm_group_m = gm < 0 ? 0 : (gm > 64 ? 64 : gm);
+  return 0;
+}
+static inline int tw_group_for(int N) {
+  if (tw_gemm_group_m > 0) return tw_gemm_group_m;
+  return (N + 255) / 256 >= 10 ? 8 : 1;
+}
 static int tw_tune_skinny_nw = 0;  // 0 = heuristic; 4 / 8 / 16 force the skinny kernel's waves per block
 static int tw_tune_gemv_kw = 0;    // 0 = heuristic; 1 / 2 / 4 / 8 force the packed GEMV's K-slices per column group
 extern "C" int tw_gemm_set_variant(int big) {
@@ -307,7 +337,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ 
   const int orig = blockIdx.x;
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int tm = wgid / ntn, tn = wgid - tm * ntn;
+  int tm, tn;
+  tw_tile_grouped(wgid, ntm, ntn, ea.group_m, tm, tn);
   const int m0 = tm * GB_BM, n0 = tn * GB_BN;
 
   // DMA assignment: wave w issues instructions i = 0..3 for A and for W; instruction (w, i) fills tile
@@ -468,7 +499,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ns(const bf16_t* __restrict__ A
   const int orig = blockIdx.x;
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int tm = wgid / ntn, tn = wgid - tm * ntn;
+  int tm, tn;
+  tw_tile_grouped(wgid, ntm, ntn, ea.group_m, tm, tn);
   const int m0 = tm * GB_BM, n0 = tn * BN;
 
   const bf16_t* ga[IA];
@@ -620,7 +652,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
   const int orig = blockIdx.x;
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int tm = wgid / ntn, tn = wgid - tm * ntn;
+  int tm, tn;
+  tw_tile_grouped(wgid, ntm, ntn, ea.group_m, tm, tn);
   const int m0 = tm * GB_BM, n0 = tn * GB_BN;
   const int wr = wid >> 2, wc = wid & 3;
   const int fr = lane & 15, fq = lane >> 4;
@@ -841,9 +874,10 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8pp(const bf16_t* __restrict__ 
   auto tile_origin = [&](int vid, int& m0, int& n0) {
     const int xcd = vid % 8;
     const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + vid / 8;
-    const int tm = wgid / ntn;
+    int tm, tn;
+    tw_tile_grouped(wgid, ntm, ntn, ea.group_m, tm, tn);
     m0 = tm * GB_BM;
-    n0 = (wgid - tm * ntn) * GB_BN;
+    n0 = tn * GB_BN;
   };
   const bf16_t* gsrc[4][2];
   auto set_src = [&](int m0, int n0) {
@@ -1303,6 +1337,7 @@ extern "C" int tw_gemm_bf16(const bf16_t* A, const bf16_t* W, int M, int N, int 
   TW_REQUIRE(M > 0 && N > 0 && K > 0 && K % G_BK == 0, "tw_gemm_bf16: M=%d N=%d K=%d (K %% 64 required)", M, N, K);
   TW_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && lda >= K && ldw >= K, "tw_gemm_bf16: lda=%d ldw=%d", lda, ldw);
   EpiArgs ea{out, ldo, bias, aux, aux_rows, 0, 0, 0, 0};
+  ea.group_m = tw_group_for(N);
   hipStream_t s = (hipStream_t)stream;
   switch (epi) {
     case TW_EPI_BF16: return launch_gemm<TW_EPI_BF16>(A, W, M, N, K, lda, ldw, ea, s);
@@ -1402,7 +1437,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_mx(const uint8_t* __restrict__ 
   const int orig = blockIdx.x;
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int tm = wgid / ntn, tn = wgid - tm * ntn;
+  int tm, tn;
+  tw_tile_grouped(wgid, ntm, ntn, ea.group_m, tm, tn);
   const int m0 = tm * GB_BM, n0 = tn * GB_BN;
 
   const uint8_t* ga[4];
@@ -1546,7 +1582,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
   const int orig = blockIdx.x;
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int tm = wgid / ntn, tn = wgid - tm * ntn;
+  int tm, tn;
+  tw_tile_grouped(wgid, ntm, ntn, ea.group_m, tm, tn);
   const int m0 = tm * GB_BM, n0 = tn * GB_BN;
   const int wr = wid >> 2, wc = wid & 3;
   const int fr = lane & 15, fq = lane >> 4;
@@ -1776,6 +1813,7 @@ extern "C" int tw_gemm_mx(const uint8_t* A, const uint8_t* Sa, const uint8_t* W,
   TW_REQUIRE(Mp % GB_BM == 0 && Mp >= M && Np % GB_BN == 0 && Np >= N,
              "tw_gemm_mx: scale row pads Mp=%d Np=%d must be multiples of 256 covering M=%d N=%d", Mp, Np, M, N);
   EpiArgs ea{out, ldo, bias, nullptr, 0, 0, 0, 0, 0, nullptr, 0};
+  ea.group_m = tw_group_for(N);
   hipStream_t s = (hipStream_t)stream;
   switch (epi) {
     case TW_EPI_BF16: launch_gemm_mx<TW_EPI_BF16>(A, Sa, W, Sw, M, N, K, lda, ldw, Mp, Np, ea, s); break;
