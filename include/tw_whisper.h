@@ -160,7 +160,8 @@ int tw_attn_encoder(const uint16_t* qkv, int B, int S, int H, uint16_t* out, voi
 int tw_attn_encoder_mx(const uint16_t* qkv, int B, int S, int H, uint8_t* out, uint8_t* scales, int rows_pad,
                        void* stream);
 /* Measurement knob (process-wide, returns 0): encoder attention kernel of tw_attn_encoder. 8 (default) =
- * k_attn_enc2 with 8 waves / 256 queries per workgroup, 4 = the same with 4 waves, 0 = the first kernel. */
+ * k_attn_enc2 with 8 waves / 256 queries per workgroup, 4 = the same with 4 waves, 0 = the first kernel.
+ * + 0x100: tw_attn_decode_cross in two passes (scores, softmax, P.V) instead of the one-pass online softmax. */
 int tw_attn_set_variant(int variant);
 
 /* ---- beam search ------------------------------------------------------------------------------ */

@@ -222,6 +222,30 @@ def test_decode_attention_self_and_cross():
         torch.testing.assert_close(out[b].float(), ref, atol=1e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("Sx", [1500, 33, 7])
+@pytest.mark.parametrize("two_pass", [False, True], ids=["online", "two_pass"])
+def test_attn_decode_cross_variants(Sx, two_pass):
+    """tw_attn_decode_cross (one-pass online softmax, the default; and the two-pass form) vs fp32 attention, with
+    key counts that leave 8-lane groups without keys (7) or with one partial chunk (33)."""
+    B, H, Bt = 3, 4, 3
+    D = H * 64
+    ckv = rand_bf16(2, Bt, H, Sx, 64, seed=Sx)
+    qx = (rand_bf16(B, D, seed=Sx + 1).float() * 4).to(torch.bfloat16)  # peaked softmax
+    rm = torch.tensor([1, 2, 0], dtype=torch.int32, device=DEV)
+    out = torch.empty(B, D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_attn_set_variant", 8 | (0x100 if two_pass else 0))
+    try:
+        _lib.call("tw_attn_decode_cross", qx.data_ptr(), B, H, Sx, Bt, rm.data_ptr(), ckv.data_ptr(), out.data_ptr(),
+                  S())
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("tw_attn_set_variant", 8)
+    for b in range(B):
+        s = int(rm[b])
+        ref = _ref_attn(qx[b].float().view(H, 1, 64), ckv[0, s].float(), ckv[1, s].float())[:, 0].reshape(D)
+        torch.testing.assert_close(out[b].float(), ref, atol=1e-2, rtol=1e-2)
+
+
 def _params(V, st, mode=0, max_new=100, use_ts=1):
     p = _lib.TwSelectParams()
     p.V, p.eos, p.pad, p.ts_begin, p.no_timestamps = V, st.eot, st.eot, st.timestamp_begin, st.notimestamps

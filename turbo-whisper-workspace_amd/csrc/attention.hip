@@ -342,7 +342,11 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc2(const bf16_t* __rest
 }
 
 static int tw_attn_variant = 8;  // 0 = k_attn_encoder, 4 / 8 = k_attn_enc2<NW>, 9 = <8> at 2 workgroups per CU
+// decoder cross-attention: 1 = one pass with an online softmax (default), 0 = two passes (scores, then P.V)
+static int tw_dec_cross_1p = 1;
 extern "C" int tw_attn_set_variant(int v) {
+  tw_dec_cross_1p = (v & 0x100) ? 0 : 1;  // bit 8: the two-pass decoder cross-attention (A/B)
+  v &= 0xff;
   tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9) ? v : 8;
   return 0;
 }
@@ -467,6 +471,83 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
   __syncthreads();
 }
 
+// dec_attend in ONE pass over the keys (flash-decoding's online softmax per 8-lane group): each group loads the K
+// and the V row of its keys together (DA_UNR keys = 16 x 16-byte loads in flight per lane), rescales its running
+// (max, sum, P.V) once per DA_UNR keys, and the 32 groups' states are merged through LDS at the end. The two-pass
+// form streams all of K, then (after a block-wide softmax) all of V: two load ramps and three barriers between
+// them on an HBM-bound kernel. Same softmax up to f32 rounding (the rescaling order differs).
+__device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const bf16_t* K, const bf16_t* V, int nkeys,
+                                     float* part /*[32][64] LDS*/, float* gml /*[32][2] LDS*/,
+                                     float* outv /*[64] f32 LDS*/) {
+  const int tid = threadIdx.x, g = tid >> 3, gl = tid & 7;
+  float qv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) qv[e] = qf[gl * 8 + e];
+  float m = -INFINITY, l = 0.f;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int nit = (nkeys + 31) >> 5;
+  for (int it0 = 0; it0 < nit; it0 += DA_UNR) {
+    uint4 kk[DA_UNR], vv[DA_UNR];
+#pragma unroll
+    for (int u = 0; u < DA_UNR; ++u) {
+      const int key = min((it0 + u) * 32 + g, nkeys - 1);
+      kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
+      vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // all 2 x DA_UNR loads in flight before the first is consumed
+    float sv[DA_UNR];
+    float bm = m;
+#pragma unroll
+    for (int u = 0; u < DA_UNR; ++u) {
+      const bf16_t* ke = (const bf16_t*)&kk[u];
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      sv[u] = (it0 + u) * 32 + g < nkeys ? d : -INFINITY;
+      bm = fmaxf(bm, sv[u]);
+    }
+    if (bm == -INFINITY) continue;  // (no key of this group yet: short self-attention rows only)
+    const float sc = __expf(m - bm);  // 0 on the group's first keys (m = -inf)
+    l *= sc;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= sc;
+#pragma unroll
+    for (int u = 0; u < DA_UNR; ++u) {
+      const float p = __expf(sv[u] - bm);  // 0 for the masked keys
+      l += p;
+      const bf16_t* ve = (const bf16_t*)&vv[u];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += p * bf16_to_f32(ve[e]);
+    }
+    m = bm;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[g * 64 + gl * 8 + e] = acc[e];
+  if (gl == 0) {
+    gml[2 * g] = m;
+    gml[2 * g + 1] = l;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float M = -INFINITY;
+#pragma unroll 8
+    for (int gg = 0; gg < 32; ++gg) M = fmaxf(M, gml[2 * gg]);
+    float v = 0.f, tot = 0.f;
+#pragma unroll 8
+    for (int gg = 0; gg < 32; ++gg) {
+      const float mg = gml[2 * gg];
+      const float w = mg == -INFINITY ? 0.f : __expf(mg - M);
+      tot += w * gml[2 * gg + 1];
+      v += w * part[gg * 64 + tid];
+    }
+    outv[tid] = v / tot;
+  }
+  __syncthreads();
+}
+
 // Self-attention step: qkv [B][3D] bf16 (q pre-scaled), appends k,v at position pos[b] into the cache
 // (layout [B][H][max_pos][64] for K and V of this layer) and attends over positions 0..pos[b].
 __global__ __launch_bounds__(256) void k_attn_decode_self(const bf16_t* __restrict__ qkv, int D, int max_pos,
@@ -519,7 +600,7 @@ template <bool PROBS>
 __global__ __launch_bounds__(256) void k_attn_decode_cross(const bf16_t* __restrict__ q, int D, int S, int Bt,
                                                            const int* __restrict__ row_map,
                                                            const bf16_t* __restrict__ ckv, bf16_t* __restrict__ out,
-                                                           XProbs xp) {
+                                                           XProbs xp, int one_pass) {
   TW_DEC_PRIO();
   __shared__ float sc[DA_MAXK];
   __shared__ float part[32 * 64];
@@ -532,7 +613,8 @@ __global__ __launch_bounds__(256) void k_attn_decode_cross(const bf16_t* __restr
   __syncthreads();
   const bf16_t* K = ckv + (((size_t)0 * Bt + slot) * H + h) * S * 64;
   const bf16_t* V = ckv + (((size_t)1 * Bt + slot) * H + h) * S * 64;
-  dec_attend(qf, K, V, S, sc, part, red, outv);
+  if (!PROBS && one_pass) dec_attend_1p(qf, K, V, S, part, sc, outv);  // (the probabilities need the two passes)
+  else dec_attend(qf, K, V, S, sc, part, red, outv);
   if (threadIdx.x < 64) out[(size_t)b * D + h * 64 + threadIdx.x] = f32_to_bf16(outv[threadIdx.x]);
   if constexpr (PROBS) {
     if ((xp.head_mask >> h) & 1u) {
@@ -551,7 +633,7 @@ extern "C" int tw_attn_decode_cross(const bf16_t* q, int B, int H, int S, int Bt
                                     const bf16_t* cross_kv, bf16_t* out, void* stream) {
   TW_REQUIRE(q && cross_kv && out && B > 0 && H > 0 && S > 0 && S <= DA_MAXK, "tw_attn_decode_cross: bad args");
   hipLaunchKernelGGL(k_attn_decode_cross<false>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt,
-                     row_map, cross_kv, out, XProbs{});
+                     row_map, cross_kv, out, XProbs{}, tw_dec_cross_1p);
   return tw_check_launch("tw_attn_decode_cross");
 }
 
@@ -564,6 +646,6 @@ extern "C" int tw_attn_decode_cross_probs(const bf16_t* q, int B, int H, int S, 
   TW_REQUIRE(slot0 >= 0 && slot0 + __builtin_popcount(head_mask) <= n_slots && n_steps > 0,
              "tw_attn_decode_cross_probs: slots");
   hipLaunchKernelGGL(k_attn_decode_cross<true>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt,
-                     row_map, cross_kv, out, XProbs{probs, pos, head_mask, slot0, n_slots, pos0, n_steps});
+                     row_map, cross_kv, out, XProbs{probs, pos, head_mask, slot0, n_slots, pos0, n_steps}, 0);
   return tw_check_launch("tw_attn_decode_cross_probs");
 }

@@ -324,6 +324,75 @@ __device__ inline void epi_store8(const EpiArgs& ea, int m, int n, int N, float4
   if (n + 4 < N) epi_store4<EPI>(ea, m, n + 4, N, v1);
 }
 
+// Epilogue of one wave's 128 x 64 sub-tile (rows mw0.., columns ncol0..) held as 8 x 4 16x16 MFMA accumulators,
+// through the wave's own [64][GB_EPI_LD] f32 LDS image `wimg` (shared by k_gemm_big and k_gemm_h; every wave of the
+// block calls it: it holds block barriers). The caller's K loop must have ended on a barrier.
+template <int EPI>
+__device__ inline void gemm_epi_128x64(const f32x4 (&acc)[8][4], float* wimg, int lane, int mw0, int ncol0, int M,
+                                       int N, const EpiArgs& ea) {
+  const int fr = lane & 15, fq = lane >> 4;
+  // ---- epilogue through LDS: each wave stages 64 of its 128 rows at a time in its own
+  // [64][GB_EPI_LD] f32 image (k_gemm_big: 8 images = 136 KiB, the K loop's LDS plus 8 KiB), then reads
+  // back 4 consecutive columns per lane (16 lanes x 16 B per row) for vectorised global I/O.
+  const int rc = (lane & 15) * 4;  // this lane's 4 columns in the read-back phase
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ea.bias) {
+    const int n = ncol0 + rc;
+    bias4.x = ea.bias[min(n, N - 1)];
+    bias4.y = ea.bias[min(n + 1, N - 1)];
+    bias4.z = ea.bias[min(n + 2, N - 1)];
+    bias4.w = ea.bias[min(n + 3, N - 1)];
+  }
+  // epilogues that read a second f32 operand (RESID: the residual stream it updates in place; GELU_POS: the
+  // positional table) load it ahead: rows rr and rr + 8 of a half share a register slot, so a half costs two
+  // dependent HBM round trips instead of sixteen (the compiler cannot hoist a load above the previous row's store
+  // to the same buffer), and the first eight loads fly while the accumulators are staged through LDS.
+  constexpr bool PRE = EPI == TW_EPI_RESID_F32 || EPI == TW_EPI_GELU_POS_F32;
+  const bool full = ncol0 + rc + 3 < N;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int ib = 4 * half;
+    const int mrow0 = mw0 + ib * 16;
+    float4 ad[8];
+    if constexpr (PRE) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ad[q] = epi_addend<EPI>(ea, min(mrow0 + q * 4 + (lane >> 4), M - 1), ncol0 + rc, full);
+    }
+    if (half) __syncthreads();  // (first pass: the K loop ended on a barrier)
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wimg[(ii * 16 + fq * 4 + r) * GB_EPI_LD + j * 16 + fr] = acc[ib + ii][j][r];
+    __syncthreads();
+    if constexpr (PRE) {
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int lr = rr * 4 + (lane >> 4);  // 4 rows per wave-instruction
+        const int m = mrow0 + lr;
+        float4 v = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
+        v.x += bias4.x; v.y += bias4.y; v.z += bias4.z; v.w += bias4.w;
+        if (full) {
+          if (m < M) epi_store4_pre<EPI>(ea, m, ncol0 + rc, v, ad[rr & 7]);
+        } else if (m < M && ncol0 + rc < N) {
+          epi_store4<EPI>(ea, m, ncol0 + rc, N, v);
+        }
+        if (rr < 8) ad[rr] = epi_addend<EPI>(ea, min(m + 32, M - 1), ncol0 + rc, full);
+      }
+    } else {
+#pragma unroll 4
+      for (int rr = 0; rr < 16; ++rr) {
+        const int lr = rr * 4 + (lane >> 4);
+        const int m = mrow0 + lr;
+        float4 v = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
+        v.x += bias4.x; v.y += bias4.y; v.z += bias4.z; v.w += bias4.w;
+        if (m < M && ncol0 + rc < N) epi_store4<EPI>(ea, m, ncol0 + rc, N, v);
+      }
+    }
+  }
+}
+
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                      int M, int N, int K, int lda, int ldw, EpiArgs ea) {
@@ -400,68 +469,96 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ 
     __syncthreads();  // vmcnt(0) (tile kt+1 landed) + lgkmcnt(0) + barrier
   }
 
-  // ---- epilogue through LDS: each wave stages 64 of its 128 rows at a time in its own
-  // [64][GB_EPI_LD] f32 image (8 images = 136 KiB, the LDS the K loop used plus 8 KiB), then reads
-  // back 4 consecutive columns per lane (16 lanes x 16 B per row) for vectorised global I/O.
-  const int ncol0 = n0 + wc * 64;
-  const int rc = (lane & 15) * 4;  // this lane's 4 columns in the read-back phase
-  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (ea.bias) {
-    const int n = ncol0 + rc;
-    bias4.x = ea.bias[min(n, N - 1)];
-    bias4.y = ea.bias[min(n + 1, N - 1)];
-    bias4.z = ea.bias[min(n + 2, N - 1)];
-    bias4.w = ea.bias[min(n + 3, N - 1)];
+  gemm_epi_128x64<EPI>(acc, (float*)smem + wid * (64 * GB_EPI_LD), lane, m0 + wr * 128, n0 + wc * 64, M, N, ea);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_gemm_h: 256 x 128 x 32 tiles, 256 threads = 4 waves (2 M x 2 N, each a 128 x 64 sub-tile exactly as a
+// k_gemm_big wave), a 3-stage LDS-DMA ring of 24 KiB stages (two K-steps of DMA in flight behind the one being
+// computed), and TWO workgroups per CU (72 KiB LDS each). The point is the epilogue: with one 256 x 256 block per
+// CU every CU reaches its epilogue at the same moment (the grid runs in lock-step rounds), so the output stores
+// (and the residual reads) of all 256 CUs contend for HBM while the MFMAs idle, and then the K loops contend for L2
+// while HBM idles. Two resident blocks per CU drift apart after the first round: one block's epilogue runs beside
+// the other's K loop. BK = 32: a row is 64 B (4 16-byte chunks), swizzle chunk ^ ((row >> 2) & 3) makes the
+// 16-lane groups of a ds_read_b128 fragment read hit 16 distinct 16-byte bank groups.
+// ------------------------------------------------------------------------------------------------
+#define GH_BN 128
+#define GH_BK 32
+#define GH_ST 3
+#define GH_STAGE ((GB_BM + GH_BN) * GH_BK)  // bf16 elements per stage (A rows then W rows)
+__device__ inline int gh_swz(int r) { return (r >> 2) & 3; }
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void k_gemm_h(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                   int M, int N, int K, int lda, int ldw, EpiArgs ea) {
+  // 3 x 24 KiB ring; after the K loop 4 x [64][68] f32 epilogue images (69.6 KB) reuse it
+  __shared__ __attribute__((aligned(16))) bf16_t smem[GH_ST * GH_STAGE];
+  static_assert(4 * 64 * GB_EPI_LD * 4 <= GH_ST * GH_STAGE * 2, "epilogue images exceed the ring");
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntm = (M + GB_BM - 1) / GB_BM, ntn = (N + GH_BN - 1) / GH_BN;
+  const int nwg = ntm * ntn;
+  const int orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  int tm, tn;
+  tw_tile_grouped(wgid, ntm, ntn, ea.group_m, tm, tn);
+  const int m0 = tm * GB_BM, n0 = tn * GH_BN;
+
+  // DMA: a stage is 384 rows x 64 B (A rows 0..255, W rows 256..383) = 24 wave-instructions of 16 rows; wave w
+  // issues instructions t = 6w .. 6w+5. Lane l: row 16t + (l >> 2), LDS chunk slot l & 3 <- global chunk
+  // (l & 3) ^ swz(row) (rows past M / N are clamped: their outputs are never stored).
+  const bf16_t* src[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int t = wid * 6 + i, r = 16 * t + (lane >> 2);
+    const int ch = (lane & 3) ^ gh_swz(r);
+    src[i] = r < GB_BM ? A + (size_t)min(m0 + r, M - 1) * lda + ch * 8
+                       : W + (size_t)min(n0 + r - GB_BM, N - 1) * ldw + ch * 8;
   }
-  float* wimg = (float*)smem + wid * (64 * GB_EPI_LD);
-  // epilogues that read a second f32 operand (RESID: the residual stream it updates in place; GELU_POS: the
-  // positional table) load it ahead: rows rr and rr + 8 of a half share a register slot, so a half costs two
-  // dependent HBM round trips instead of sixteen (the compiler cannot hoist a load above the previous row's store
-  // to the same buffer), and the first eight loads fly while the accumulators are staged through LDS.
-  constexpr bool PRE = EPI == TW_EPI_RESID_F32 || EPI == TW_EPI_GELU_POS_F32;
-  const bool full = ncol0 + rc + 3 < N;
+  auto stage = [&](int buf, int k0) {
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    const int ib = 4 * half;
-    const int mrow0 = m0 + wr * 128 + ib * 16;
-    float4 ad[8];
-    if constexpr (PRE) {
+    for (int i = 0; i < 6; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src[i] + k0),
+                                       (lds_void_t*)(smem + buf * GH_STAGE + (wid * 6 + i) * 16 * GH_BK), 16, 0, 0);
+  };
+
+  const int wr = wid >> 1, wc = wid & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  f32x4 acc[8][4];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) ad[q] = epi_addend<EPI>(ea, min(mrow0 + q * 4 + (lane >> 4), M - 1), ncol0 + rc, full);
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / GH_BK;
+  stage(0, 0);
+  if (nk > 1) stage(1, GH_BK);
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // K-step kt landed (this wave's DMA: all but the newest stage; everyone's: the barrier), and every wave is
+    // past K-step kt-1, whose buffer the DMA below refills
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + 2 < nk) stage(cur == 0 ? 2 : cur - 1, (kt + 2) * GH_BK);
+    const bf16_t* As = smem + cur * GH_STAGE;
+    const bf16_t* Ws = As + GB_BM * GH_BK;
+    bf16x8 bfr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = wc * 64 + j * 16 + fr;
+      bfr[j] = *(const bf16x8*)(Ws + col * GH_BK + ((fq ^ gh_swz(col)) << 3));
     }
-    if (half) __syncthreads();  // (first pass: the K loop ended on a barrier)
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
+    for (int i = 0; i < 8; ++i) {
+      const int row = wr * 128 + i * 16 + fr;
+      const bf16x8 af = *(const bf16x8*)(As + row * GH_BK + ((fq ^ gh_swz(row)) << 3));
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) wimg[(ii * 16 + fq * 4 + r) * GB_EPI_LD + j * 16 + fr] = acc[ib + ii][j][r];
-    __syncthreads();
-    if constexpr (PRE) {
-#pragma unroll
-      for (int rr = 0; rr < 16; ++rr) {
-        const int lr = rr * 4 + (lane >> 4);  // 4 rows per wave-instruction
-        const int m = mrow0 + lr;
-        float4 v = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
-        v.x += bias4.x; v.y += bias4.y; v.z += bias4.z; v.w += bias4.w;
-        if (full) {
-          if (m < M) epi_store4_pre<EPI>(ea, m, ncol0 + rc, v, ad[rr & 7]);
-        } else if (m < M && ncol0 + rc < N) {
-          epi_store4<EPI>(ea, m, ncol0 + rc, N, v);
-        }
-        if (rr < 8) ad[rr] = epi_addend<EPI>(ea, min(m + 32, M - 1), ncol0 + rc, full);
-      }
-    } else {
-#pragma unroll 4
-      for (int rr = 0; rr < 16; ++rr) {
-        const int lr = rr * 4 + (lane >> 4);
-        const int m = mrow0 + lr;
-        float4 v = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
-        v.x += bias4.x; v.y += bias4.y; v.z += bias4.z; v.w += bias4.w;
-        if (m < M && ncol0 + rc < N) epi_store4<EPI>(ea, m, ncol0 + rc, N, v);
-      }
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
     }
+    cur = cur == 2 ? 0 : cur + 1;
   }
+  __syncthreads();  // every wave's last ds_reads are done before the ring becomes epilogue images
+  gemm_epi_128x64<EPI>(acc, (float*)smem + wid * (64 * GB_EPI_LD), lane, m0 + wr * 128, n0 + wc * 64, M, N, ea);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1303,7 +1400,10 @@ static int launch_gemm(const bf16_t* A, const bf16_t* W, int M, int N, int K, in
   if (M <= 32) {
     launch_skinny<EPI>(A, W, M, N, K, lda, ldw, ea, 1, s);
   } else {
-    if (tw_gemm_big_enabled == 5) {
+    if (tw_gemm_big_enabled == 7) {
+      unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GH_BN);
+      hipLaunchKernelGGL(k_gemm_h<EPI>, dim3(nwg), dim3(256), 0, s, A, W, M, N, K, lda, ldw, ea);
+    } else if (tw_gemm_big_enabled == 5) {
       unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
       hipLaunchKernelGGL(k_gemm_8p<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
     } else if (tw_gemm_big_enabled == 6) {
