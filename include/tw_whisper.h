@@ -161,7 +161,8 @@ int tw_attn_encoder_mx(const uint16_t* qkv, int B, int S, int H, uint8_t* out, u
                        void* stream);
 /* Measurement knob (process-wide, returns 0): encoder attention kernel of tw_attn_encoder. 8 (default) =
  * k_attn_enc2 with 8 waves / 256 queries per workgroup, 4 = the same with 4 waves, 0 = the first kernel.
- * + 0x100: tw_attn_decode_cross in two passes (scores, softmax, P.V) instead of the one-pass online softmax. */
+ * + 0x100: tw_attn_decode_cross in two passes (scores, softmax, P.V) instead of the one-pass online softmax.
+ * + 0x200: the one-pass tw_attn_decode_cross with 512 threads (64 key groups) per (row, head) instead of 256. */
 int tw_attn_set_variant(int variant);
 
 /* ---- beam search ------------------------------------------------------------------------------ */

@@ -223,17 +223,17 @@ def test_decode_attention_self_and_cross():
 
 
 @pytest.mark.parametrize("Sx", [1500, 33, 7])
-@pytest.mark.parametrize("two_pass", [False, True], ids=["online", "two_pass"])
-def test_attn_decode_cross_variants(Sx, two_pass):
-    """tw_attn_decode_cross (one-pass online softmax, the default; and the two-pass form) vs fp32 attention, with
-    key counts that leave 8-lane groups without keys (7) or with one partial chunk (33)."""
+@pytest.mark.parametrize("mode", [0, 0x200, 0x100], ids=["online256", "online512", "two_pass"])
+def test_attn_decode_cross_variants(Sx, mode):
+    """tw_attn_decode_cross (one-pass online softmax over 32 key groups, the default; over 64 groups; and the two-pass
+    form) vs fp32 attention, with key counts that leave 8-lane groups without keys (7) or with one partial chunk (33)."""
     B, H, Bt = 3, 4, 3
     D = H * 64
     ckv = rand_bf16(2, Bt, H, Sx, 64, seed=Sx)
     qx = (rand_bf16(B, D, seed=Sx + 1).float() * 4).to(torch.bfloat16)  # peaked softmax
     rm = torch.tensor([1, 2, 0], dtype=torch.int32, device=DEV)
     out = torch.empty(B, D, dtype=torch.bfloat16, device=DEV)
-    _lib.call("tw_attn_set_variant", 8 | (0x100 if two_pass else 0))
+    _lib.call("tw_attn_set_variant", 8 | mode)
     try:
         _lib.call("tw_attn_decode_cross", qx.data_ptr(), B, H, Sx, Bt, rm.data_ptr(), ckv.data_ptr(), out.data_ptr(),
                   S())

@@ -344,8 +344,10 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc2(const bf16_t* __rest
 static int tw_attn_variant = 8;  // 0 = k_attn_encoder, 4 / 8 = k_attn_enc2<NW>, 9 = <8> at 2 workgroups per CU
 // decoder cross-attention: 1 = one pass with an online softmax (default), 0 = two passes (scores, then P.V)
 static int tw_dec_cross_1p = 1;
+static int tw_dec_cross_ng = 32;  // 8-lane key groups per one-pass block (64 measured 3% slower in the bench)
 extern "C" int tw_attn_set_variant(int v) {
   tw_dec_cross_1p = (v & 0x100) ? 0 : 1;  // bit 8: the two-pass decoder cross-attention (A/B)
+  tw_dec_cross_ng = (v & 0x200) ? 64 : 32;  // bit 9: one-pass with 512 threads (64 key groups) instead of 256
   v &= 0xff;
   tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9) ? v : 8;
   return 0;
@@ -476,8 +478,10 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
 // (max, sum, P.V) once per DA_UNR keys, and the 32 groups' states are merged through LDS at the end. The two-pass
 // form streams all of K, then (after a block-wide softmax) all of V: two load ramps and three barriers between
 // them on an HBM-bound kernel. Same softmax up to f32 rounding (the rescaling order differs).
+// NG = 8-lane groups per block (32: 256 threads; 64: 512 threads, half the serial load round trips per group).
+template <int NG>
 __device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const bf16_t* K, const bf16_t* V, int nkeys,
-                                     float* part /*[32][64] LDS*/, float* gml /*[32][2] LDS*/,
+                                     float* part /*[NG][64] LDS*/, float* gml /*[NG][2] LDS*/,
                                      float* outv /*[64] f32 LDS*/) {
   const int tid = threadIdx.x, g = tid >> 3, gl = tid & 7;
   float qv[8];
@@ -485,12 +489,12 @@ __device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const 
   for (int e = 0; e < 8; ++e) qv[e] = qf[gl * 8 + e];
   float m = -INFINITY, l = 0.f;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int nit = (nkeys + 31) >> 5;
+  const int nit = (nkeys + NG - 1) / NG;
   for (int it0 = 0; it0 < nit; it0 += DA_UNR) {
     uint4 kk[DA_UNR], vv[DA_UNR];
 #pragma unroll
     for (int u = 0; u < DA_UNR; ++u) {
-      const int key = min((it0 + u) * 32 + g, nkeys - 1);
+      const int key = min((it0 + u) * NG + g, nkeys - 1);
       kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
       vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
     }
@@ -506,7 +510,7 @@ __device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const 
       d += __shfl_xor(d, 1, 64);
       d += __shfl_xor(d, 2, 64);
       d += __shfl_xor(d, 4, 64);
-      sv[u] = (it0 + u) * 32 + g < nkeys ? d : -INFINITY;
+      sv[u] = (it0 + u) * NG + g < nkeys ? d : -INFINITY;
       bm = fmaxf(bm, sv[u]);
     }
     if (bm == -INFINITY) continue;  // (no key of this group yet: short self-attention rows only)
@@ -534,10 +538,10 @@ __device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const 
   if (tid < 64) {
     float M = -INFINITY;
 #pragma unroll 8
-    for (int gg = 0; gg < 32; ++gg) M = fmaxf(M, gml[2 * gg]);
+    for (int gg = 0; gg < NG; ++gg) M = fmaxf(M, gml[2 * gg]);
     float v = 0.f, tot = 0.f;
 #pragma unroll 8
-    for (int gg = 0; gg < 32; ++gg) {
+    for (int gg = 0; gg < NG; ++gg) {
       const float mg = gml[2 * gg];
       const float w = mg == -INFINITY ? 0.f : __expf(mg - M);
       tot += w * gml[2 * gg + 1];
@@ -596,14 +600,14 @@ struct XProbs {
   int slot0, n_slots, pos0, n_steps;
 };
 
-template <bool PROBS>
-__global__ __launch_bounds__(256) void k_attn_decode_cross(const bf16_t* __restrict__ q, int D, int S, int Bt,
+template <bool PROBS, int NG = 32>
+__global__ __launch_bounds__(NG * 8) void k_attn_decode_cross(const bf16_t* __restrict__ q, int D, int S, int Bt,
                                                            const int* __restrict__ row_map,
                                                            const bf16_t* __restrict__ ckv, bf16_t* __restrict__ out,
                                                            XProbs xp, int one_pass) {
   TW_DEC_PRIO();
   __shared__ float sc[DA_MAXK];
-  __shared__ float part[32 * 64];
+  __shared__ float part[NG * 64];
   __shared__ float qf[64];
   __shared__ float outv[64];
   __shared__ float red[8];
@@ -613,8 +617,8 @@ __global__ __launch_bounds__(256) void k_attn_decode_cross(const bf16_t* __restr
   __syncthreads();
   const bf16_t* K = ckv + (((size_t)0 * Bt + slot) * H + h) * S * 64;
   const bf16_t* V = ckv + (((size_t)1 * Bt + slot) * H + h) * S * 64;
-  if (!PROBS && one_pass) dec_attend_1p(qf, K, V, S, part, sc, outv);  // (the probabilities need the two passes)
-  else dec_attend(qf, K, V, S, sc, part, red, outv);
+  if (!PROBS && one_pass) dec_attend_1p<NG>(qf, K, V, S, part, sc, outv);  // (the probabilities need the two passes)
+  else if constexpr (NG == 32) dec_attend(qf, K, V, S, sc, part, red, outv);
   if (threadIdx.x < 64) out[(size_t)b * D + h * 64 + threadIdx.x] = f32_to_bf16(outv[threadIdx.x]);
   if constexpr (PROBS) {
     if ((xp.head_mask >> h) & 1u) {
@@ -632,8 +636,12 @@ __global__ __launch_bounds__(256) void k_attn_decode_cross(const bf16_t* __restr
 extern "C" int tw_attn_decode_cross(const bf16_t* q, int B, int H, int S, int Bt, const int* row_map,
                                     const bf16_t* cross_kv, bf16_t* out, void* stream) {
   TW_REQUIRE(q && cross_kv && out && B > 0 && H > 0 && S > 0 && S <= DA_MAXK, "tw_attn_decode_cross: bad args");
-  hipLaunchKernelGGL(k_attn_decode_cross<false>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt,
-                     row_map, cross_kv, out, XProbs{}, tw_dec_cross_1p);
+  if (tw_dec_cross_ng == 64 && tw_dec_cross_1p)
+    hipLaunchKernelGGL((k_attn_decode_cross<false, 64>), dim3(H, B), dim3(512), 0, (hipStream_t)stream, q, H * 64, S,
+                       Bt, row_map, cross_kv, out, XProbs{}, 1);
+  else
+    hipLaunchKernelGGL(k_attn_decode_cross<false>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt,
+                       row_map, cross_kv, out, XProbs{}, tw_dec_cross_1p);
   return tw_check_launch("tw_attn_decode_cross");
 }
 

@@ -139,7 +139,12 @@ class WhisperEngine:
                  enc_fp8: Optional[bool] = None):
         _lib.load()
         # kernel-variant overrides for A/B measurement (defaults are the measured-best kernels)
-        if os.environ.get("TW_GEMM_VARIANT"):
+        # Large-M GEMM kernel per encoder context (tw_gemm_set_variant): the 8-phase ping-pong k_gemm_8p (5) is 6-19 %
+        # faster than k_gemm_big (1) on every encoder shape when it has the GPU to itself (scripts/gemm_bench.py), but
+        # beside a running decode it slows the latency-bound decoder kernels more than it gains (bench step 117.1 vs
+        # 113.4 ms). An encoder that runs alone uses 5, one queued beside a decode (run_batches' overlap) uses 1.
+        self._gemm_variant_fixed = bool(os.environ.get("TW_GEMM_VARIANT"))
+        if self._gemm_variant_fixed:
             _lib.call("tw_gemm_set_variant", int(os.environ["TW_GEMM_VARIANT"], 0))
         if os.environ.get("TW_GEMM_MX_VARIANT"):
             _lib.call("tw_gemm_mx_set_variant", int(os.environ["TW_GEMM_MX_VARIANT"], 0))
@@ -433,17 +438,36 @@ class WhisperEngine:
 
     # ------------------------------------------------------------------ encoder
     @on_engine_streams
-    def encode(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True) -> None:
+    def encode(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True,
+               alone: bool = True) -> None:
         """Encoder over R windows: slot r reads feats[slot][row_map[r]][:, seek[r]:] (zero padded to 3000), then
         projects every decoder layer's cross-attention K/V into cross_kv_buf[slot] (batch stride R). Runs on
         enc_stream (see _enc_begin for `sync`)."""
         self._pump_drain()  # a paced prefetch shares the encoder's activation buffers: queue all of it first
-        for _ in self._encode_steps(R, row_map, seek, slot, sync):
+        for _ in self._encode_steps(R, row_map, seek, slot, sync, alone=alone):
             pass
 
-    def _encode_steps(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True):
+    def _set_gemm_context(self, alone: bool) -> None:
+        """Large-M GEMM kernel for the encoder chunk about to be queued (see __init__): 5 alone, 1 beside a decode."""
+        if not self._gemm_variant_fixed:
+            _lib.call("tw_gemm_set_variant", 5 if alone else 1)
+
+    def _encode_steps(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True,
+                      alone: bool = True):
         """encode() as a generator that yields after the conv stem and after every layer, so a pipelined prefetch
-        can queue the encoder a layer at a time (run_batches' _EncoderPump). Every launch names enc_stream."""
+        can queue the encoder a layer at a time (run_batches' _EncoderPump). Every launch names enc_stream.
+        alone: no decode runs beside this encoder (picks the large-M GEMM kernel, re-applied after every yield)."""
+        chunks = self._encode_chunks(R, row_map, seek, slot, sync)
+        while True:
+            self._set_gemm_context(alone)  # before each chunk is queued: the decode loop runs between chunks
+            try:
+                next(chunks)
+            except StopIteration:
+                break
+            yield
+        self._set_gemm_context(True)
+
+    def _encode_chunks(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True):
         d, w = self.d, self.w
         slot = self._slot if slot is None else slot
         D, F, H = d.d_model, d.ffn, d.heads
@@ -1063,12 +1087,12 @@ class WhisperEngine:
         if any(n < 1 or n > self.max_batch for n in sizes):
             raise ValueError(f"batch sizes must be in [1, {self.max_batch}]")
 
-        def prefetch(k):
+        def prefetch(k, alone=True):
             with torch.cuda.stream(self.enc_stream):
                 if load is not None:
                     load(k)
                 self.logmel(sizes[k], slot=k % 2, sync=False)
-                self.encode(sizes[k], row_map=False, seek=False, slot=k % 2, sync=False)
+                self.encode(sizes[k], row_map=False, seek=False, slot=k % 2, sync=False, alone=alone)
 
         def prefetch_steps(k):  # the same work as prefetch(k), queued chunk by chunk by an _EncoderPump
             with torch.cuda.stream(self.enc_stream):
@@ -1076,7 +1100,7 @@ class WhisperEngine:
                     load(k)
                 self.logmel(sizes[k], slot=k % 2, sync=False)
             yield
-            yield from self._encode_steps(sizes[k], row_map=False, seek=False, slot=k % 2, sync=False)
+            yield from self._encode_steps(sizes[k], row_map=False, seek=False, slot=k % 2, sync=False, alone=False)
 
         # the first prefetch is ordered after whatever the caller queued on the decoder stream
         self.enc_stream.wait_stream(self.stream)
@@ -1097,7 +1121,7 @@ class WhisperEngine:
                     self._pump = _EncoderPump(self, prefetch_steps(k + 1))
                     self._pump()
                 else:
-                    prefetch(k + 1)
+                    prefetch(k + 1, alone=False)
             kw = dict(gen_kwargs, **(batch_kwargs[k] if batch_kwargs else {}))
             try:
                 out.append(self.generate(n, slot=k % 2, pre_encoded=True, **kw))
