@@ -164,6 +164,8 @@ int tw_attn_encoder_mx(const uint16_t* qkv, int B, int S, int H, uint8_t* out, u
  * + 0x100: tw_attn_decode_cross in two passes (scores, softmax, P.V) instead of the one-pass online softmax.
  * + 0x200: the one-pass tw_attn_decode_cross with 512 threads (64 key groups) per (row, head) instead of 256. */
 int tw_attn_set_variant(int variant);
+/* Decoder residual+LayerNorm kernel (A/B): 0 = one wave per row when D == 1280 (default), 1 = the 4-wave block form. */
+int tw_ln_set_variant(int variant);
 
 /* ---- beam search ------------------------------------------------------------------------------ */
 /* GenerationMixin._beam_search ($TF/generation/utils.py:3208-3512) with the Whisper processor chain, for W windows

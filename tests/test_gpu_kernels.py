@@ -107,8 +107,17 @@ def test_gemm_partial_splitk_vs_torch(M, N, K, splits):
         torch.testing.assert_close(part[y], A[:, lo:hi].float() @ W[:, lo:hi].float().t(), atol=2e-3, rtol=2e-3)
 
 
-@pytest.mark.parametrize("M,D,nparts", [(24, 1280, 4), (5, 384, 0), (3, 256, 2)])
-def test_resid_layernorm_vs_torch(M, D, nparts):
+@pytest.mark.parametrize("M,D,nparts", [(24, 1280, 4), (2, 1280, 6), (5, 384, 0), (3, 256, 2)])
+@pytest.mark.parametrize("lnv", [0, 1], ids=["wave", "block"])
+def test_resid_layernorm_vs_torch(M, D, nparts, lnv):
+    _lib.call("tw_ln_set_variant", lnv)
+    try:
+        _test_resid_layernorm_vs_torch(M, D, nparts)
+    finally:
+        _lib.call("tw_ln_set_variant", 0)
+
+
+def _test_resid_layernorm_vs_torch(M, D, nparts):
     x = torch.randn(M, D, device=DEV) * 3 + 1
     parts = torch.randn(max(nparts, 1), M, D, device=DEV)
     bias = torch.randn(D, device=DEV) if nparts else None
@@ -382,7 +391,16 @@ def test_gemv_packed_vs_torch(M, N, K, epi, splits, a_packed):
 
 
 @pytest.mark.parametrize("M,D,nparts", [(24, 1280, 4), (5, 384, 0), (17, 256, 2)])
-def test_resid_layernorm_packed_vs_torch(M, D, nparts):
+@pytest.mark.parametrize("lnv", [0, 1], ids=["wave", "block"])
+def test_resid_layernorm_packed_vs_torch(M, D, nparts, lnv):
+    _lib.call("tw_ln_set_variant", lnv)
+    try:
+        _test_resid_layernorm_packed_vs_torch(M, D, nparts)
+    finally:
+        _lib.call("tw_ln_set_variant", 0)
+
+
+def _test_resid_layernorm_packed_vs_torch(M, D, nparts):
     x = torch.randn(M, D, device=DEV) * 3 + 1
     parts = torch.randn(max(nparts, 1), M, D, device=DEV)
     bias = torch.randn(D, device=DEV) if nparts else None

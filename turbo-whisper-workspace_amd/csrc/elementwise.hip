@@ -196,14 +196,99 @@ __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const f
   tw_row_ln_store<PACKED>(v, s, row, D, eps, g, bta, out, red);
 }
 
+// k_resid_ln for D = 256 * NV with ONE wave per row: every lane holds NV float4 chunks (c = lane + 64 i), both
+// LayerNorm reductions are wave shuffles, no LDS round trip or block barrier. A decode step runs 13 of these on 24
+// rows; the 4-wave form spends most of its ~6.8 us in its two barrier-separated reductions (tw_ln_set_variant(1)
+// restores it for A/B).
+template <bool PACKED, int NV>
+__global__ __launch_bounds__(64) void k_resid_ln_w(float* __restrict__ x, const float* __restrict__ parts, int nparts,
+                                                   long part_stride, const float* __restrict__ bias,
+                                                   const float* __restrict__ g, const float* __restrict__ bta, int D,
+                                                   float eps, bf16_t* __restrict__ out) {
+  TW_DEC_PRIO();
+  const int row = blockIdx.x, lane = threadIdx.x;
+  float* xr = x + (size_t)row * D;
+  const float* pr = parts ? parts + (size_t)row * D : nullptr;
+  float4 v[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = ((const float4*)xr)[lane + 64 * i];
+  if (bias) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const float4 bb = ((const float4*)bias)[lane + 64 * i];
+      v[i].x += bb.x; v[i].y += bb.y; v[i].z += bb.z; v[i].w += bb.w;
+    }
+  }
+  if (nparts > 0) {
+    float4 q[4][NV];  // all partial loads in flight together (clamped part index, unused ones discarded)
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int i = 0; i < NV; ++i) q[p][i] = ((const float4*)(pr + min(p, nparts - 1) * part_stride))[lane + 64 * i];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      if (p < nparts)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          v[i].x += q[p][i].x; v[i].y += q[p][i].y; v[i].z += q[p][i].z; v[i].w += q[p][i].w;
+        }
+    for (int p = 4; p < nparts; ++p)
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const float4 qq = ((const float4*)(pr + p * part_stride))[lane + 64 * i];
+        v[i].x += qq.x; v[i].y += qq.y; v[i].z += qq.z; v[i].w += qq.w;
+      }
+  }
+  if (nparts > 0 || bias) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) ((float4*)xr)[lane + 64 * i] = v[i];
+  }
+  if (!g) return;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  const float mean = wave_sum(s) / (float)D;
+  float q2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+    q2 += (a * a + b * b) + (c * c + d * d);
+  }
+  const float rstd = rsqrtf(wave_sum(q2) / (float)D + eps);
+  bf16_t* orow = out + (size_t)row * D;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + 64 * i;
+    const float4 gg = ((const float4*)g)[c], bb = ((const float4*)bta)[c];
+    uint2 w;
+    w.x = pack_bf16x2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
+    w.y = pack_bf16x2((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+    if constexpr (PACKED) {
+      *(uint2*)(out + tw_pack_act_idx(row, 4 * c)) = w;
+    } else {
+      ((uint2*)orow)[c] = w;
+    }
+  }
+}
+
+static int tw_ln_variant = 0;  // 0: one wave per row when D == 1280, 1: always the 4-wave k_resid_ln
+extern "C" int tw_ln_set_variant(int v) {
+  tw_ln_variant = v == 1 ? 1 : 0;
+  return 0;
+}
+
 extern "C" int tw_resid_layernorm(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
                                   const float* beta, int M, int D, float eps, uint16_t* out, void* stream) {
   TW_REQUIRE(x && M > 0 && D > 0 && D % 4 == 0 && D <= 1024 * RLN_MAXV, "tw_resid_layernorm: bad args (D %% 4, D <= %d)",
              1024 * RLN_MAXV);
   TW_REQUIRE(nparts >= 0 && (nparts == 0 || parts), "tw_resid_layernorm: parts");
   TW_REQUIRE(!gamma || (beta && out), "tw_resid_layernorm: gamma without beta/out");
-  hipLaunchKernelGGL(k_resid_ln<false>, dim3(M), dim3(256), 0, (hipStream_t)stream, x, parts, nparts, (long)M * D, bias,
-                     gamma, beta, D, eps, out);
+  if (D == 1280 && tw_ln_variant == 0)
+    hipLaunchKernelGGL((k_resid_ln_w<false, 5>), dim3(M), dim3(64), 0, (hipStream_t)stream, x, parts, nparts,
+                       (long)M * D, bias, gamma, beta, D, eps, out);
+  else
+    hipLaunchKernelGGL(k_resid_ln<false>, dim3(M), dim3(256), 0, (hipStream_t)stream, x, parts, nparts, (long)M * D,
+                       bias, gamma, beta, D, eps, out);
   return tw_check_launch("tw_resid_layernorm");
 }
 
@@ -213,7 +298,11 @@ extern "C" int tw_resid_layernorm_packed(float* x, const float* parts, int npart
   TW_REQUIRE(x && gamma && beta && out && M > 0 && M <= 32 && D > 0 && D % 32 == 0 && D <= 1024 * RLN_MAXV,
              "tw_resid_layernorm_packed: bad args (M <= 32, D %% 32, gamma/beta/out required)");
   TW_REQUIRE(nparts >= 0 && (nparts == 0 || parts), "tw_resid_layernorm_packed: parts");
-  hipLaunchKernelGGL(k_resid_ln<true>, dim3(M), dim3(256), 0, (hipStream_t)stream, x, parts, nparts, (long)M * D, bias,
-                     gamma, beta, D, eps, out);
+  if (D == 1280 && tw_ln_variant == 0)
+    hipLaunchKernelGGL((k_resid_ln_w<true, 5>), dim3(M), dim3(64), 0, (hipStream_t)stream, x, parts, nparts,
+                       (long)M * D, bias, gamma, beta, D, eps, out);
+  else
+    hipLaunchKernelGGL(k_resid_ln<true>, dim3(M), dim3(256), 0, (hipStream_t)stream, x, parts, nparts, (long)M * D,
+                       bias, gamma, beta, D, eps, out);
   return tw_check_launch("tw_resid_layernorm_packed");
 }

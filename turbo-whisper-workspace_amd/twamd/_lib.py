@@ -35,7 +35,7 @@ EXPORTED = (
     "tw_version", "tw_last_error", "tw_fill_synth", "tw_f32_to_bf16", "tw_logmel", "tw_im2col_conv1",
     "tw_im2col_conv2", "tw_gemm_bf16", "tw_layernorm", "tw_attn_encoder", "tw_attn_decode_self",
     "tw_attn_decode_cross", "tw_embed_decoder", "tw_logits_select", "tw_gemm_bf16_partial", "tw_resid_layernorm",
-    "tw_gemm_set_variant", "tw_attn_set_variant",
+    "tw_gemm_set_variant", "tw_attn_set_variant", "tw_ln_set_variant",
     "tw_dtw", "tw_attn_decode_cross_probs", "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_stream_create_masked", "tw_stream_destroy", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
     "tw_gemm_mx", "tw_quant_mx", "tw_layernorm_mx", "tw_attn_encoder_mx", "tw_gemm_mx_set_variant", "tw_logits_select_embed", "tw_gemm_set_group",
 )
@@ -106,6 +106,7 @@ _SIGS = {
     "tw_logits_select_embed": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), _P, _P, _I, _P, _P, _P, _P, _P, _I,
                                 _I, _P, _P, _P, _F, _P, _I, _P], _I),
     "tw_attn_set_variant": ([_I], _I),
+    "tw_ln_set_variant": ([_I], _I),
     "tw_resid_layernorm": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
     "tw_dtw": ([_P, _I, _I, _P, _P, _P], _I),
     "tw_attn_decode_cross_probs": ([_P, _I, _I, _I, _I, _P, _P, _P, _P, _U32, _I, _I, _P, _I, _I, _P], _I),

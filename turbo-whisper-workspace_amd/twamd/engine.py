@@ -150,6 +150,8 @@ class WhisperEngine:
             _lib.call("tw_gemm_mx_set_variant", int(os.environ["TW_GEMM_MX_VARIANT"], 0))
         if os.environ.get("TW_GEMM_GROUP"):
             _lib.call("tw_gemm_set_group", int(os.environ["TW_GEMM_GROUP"], 0))
+        if os.environ.get("TW_LN_VARIANT"):
+            _lib.call("tw_ln_set_variant", int(os.environ["TW_LN_VARIANT"], 0))
         if os.environ.get("TW_ATTN_VARIANT"):
             _lib.call("tw_attn_set_variant", int(os.environ["TW_ATTN_VARIANT"], 0))
         d = weights.dims
