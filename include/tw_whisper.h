@@ -104,8 +104,11 @@ int tw_im2col_conv2(const uint16_t* h1, int R, int D, uint16_t* out, void* strea
 int tw_gemm_bf16(const uint16_t* A, const uint16_t* W, int M, int N, int K, int lda, int ldw, int epi, void* out,
                  int ldo, const float* bias, const float* aux, int aux_rows, const int* kv_geom, void* stream);
 /* Measurement knob (process-wide, returns 0). Bits 0..2 select the large-M GEMM kernel of tw_gemm_bf16:
- * 1 = 256x256 2-stage BK=64 LDS-DMA (default), 0 = 128x128 register-staged, 3 = 256x256 counted-vmcnt + setprio,
- * 4 = 256x128 3-stage ring. Bits 8..15: 4, 8 or 16 force the skinny (M <= 32) kernel's waves per block. */
+ * 1 = 256x256 2-stage BK=64 LDS-DMA (default; the engine switches to 5 for an encoder that runs without a decode
+ * beside it), 0 = 128x128 register-staged, 3 = 256x256 counted-vmcnt + setprio, 4 = 256x128 3-stage ring,
+ * 5 = 8-phase ping-pong, 6 = persistent 8-phase, 7 = 256x128 two blocks per CU. Bits 8..15: 4, 8 or 16 force the
+ * skinny (M <= 32) kernel's waves per block; bits 16..23: 1/2/4/8 force the packed GEMV's K-slices; bit 24: the
+ * packed GEMV of N >= 16384 (proj_out) reads its weights through the caches instead of non-temporally. */
 int tw_gemm_set_variant(int big);
 /* Split-K partial product for the decoder step (M <= 32 rows, K % 32 == 0): part f32[splits][M][ldp]
  * receives the `splits` partial sums of A . W^T over consecutive K ranges (no bias). Used for the
@@ -162,7 +165,8 @@ int tw_attn_encoder_mx(const uint16_t* qkv, int B, int S, int H, uint8_t* out, u
 /* Measurement knob (process-wide, returns 0): encoder attention kernel of tw_attn_encoder. 8 (default) =
  * k_attn_enc2 with 8 waves / 256 queries per workgroup, 4 = the same with 4 waves, 0 = the first kernel.
  * + 0x100: tw_attn_decode_cross in two passes (scores, softmax, P.V) instead of the one-pass online softmax.
- * + 0x200: the one-pass tw_attn_decode_cross with 512 threads (64 key groups) per (row, head) instead of 256. */
+ * + 0x200: the one-pass tw_attn_decode_cross with 512 threads (64 key groups) per (row, head) instead of 256.
+ * + (s + 1) << 12: cross K/V of encoder slots >= s read non-temporally (0: every slot, the default; 0xff << 12: none). */
 int tw_attn_set_variant(int variant);
 /* Decoder residual+LayerNorm kernel (A/B): 0 = one wave per row when D == 1280 (default), 1 = the 4-wave block form. */
 int tw_ln_set_variant(int variant);

@@ -344,9 +344,15 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc2(const bf16_t* __rest
 static int tw_attn_variant = 8;  // 0 = k_attn_encoder, 4 / 8 = k_attn_enc2<NW>, 9 = <8> at 2 workgroups per CU
 // decoder cross-attention: 1 = one pass with an online softmax (default), 0 = two passes (scores, then P.V)
 static int tw_dec_cross_1p = 1;
+// Encoder slots >= this read their cross K/V with non-temporal loads. The 737 MB of cross K/V a decode step streams
+// (B = 24) cannot stay in the 256 MB Infinity Cache anyway; read nt it stops evicting what can (the decoder weights,
+// the encoder's operands): cross-attention 40.1 -> 35.2 us per launch, bench step 111.1 -> 109.0 ms.
+static int tw_dec_cross_nt = 0;
 static int tw_dec_cross_ng = 32;  // 8-lane key groups per one-pass block (64 measured 3% slower in the bench)
 extern "C" int tw_attn_set_variant(int v) {
   tw_dec_cross_1p = (v & 0x100) ? 0 : 1;  // bit 8: the two-pass decoder cross-attention (A/B)
+  // bits 12-19: 0 = every slot's cross K/V read non-temporally (default), else 1 + the first slot read so (0xff: none)
+  tw_dec_cross_nt = (v >> 12) & 0xff ? ((v >> 12) & 0xff) - 1 : 0;
   tw_dec_cross_ng = (v & 0x200) ? 64 : 32;  // bit 9: one-pass with 512 threads (64 key groups) instead of 256
   v &= 0xff;
   tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9) ? v : 8;
@@ -479,7 +485,7 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
 // form streams all of K, then (after a block-wide softmax) all of V: two load ramps and three barriers between
 // them on an HBM-bound kernel. Same softmax up to f32 rounding (the rescaling order differs).
 // NG = 8-lane groups per block (32: 256 threads; 64: 512 threads, half the serial load round trips per group).
-template <int NG>
+template <int NG, bool NT = false>
 __device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const bf16_t* K, const bf16_t* V, int nkeys,
                                      float* part /*[NG][64] LDS*/, float* gml /*[NG][2] LDS*/,
                                      float* outv /*[64] f32 LDS*/) {
@@ -495,8 +501,16 @@ __device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const 
 #pragma unroll
     for (int u = 0; u < DA_UNR; ++u) {
       const int key = min((it0 + u) * NG + g, nkeys - 1);
-      kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
-      vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
+      if constexpr (NT) {
+        typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+        const u32x4_nt a = __builtin_nontemporal_load((const u32x4_nt*)(K + (size_t)key * 64 + gl * 8));
+        const u32x4_nt c = __builtin_nontemporal_load((const u32x4_nt*)(V + (size_t)key * 64 + gl * 8));
+        kk[u] = make_uint4(a.x, a.y, a.z, a.w);
+        vv[u] = make_uint4(c.x, c.y, c.z, c.w);
+      } else {
+        kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
+        vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);  // all 2 x DA_UNR loads in flight before the first is consumed
     float sv[DA_UNR];
@@ -604,7 +618,7 @@ template <bool PROBS, int NG = 32>
 __global__ __launch_bounds__(NG * 8) void k_attn_decode_cross(const bf16_t* __restrict__ q, int D, int S, int Bt,
                                                            const int* __restrict__ row_map,
                                                            const bf16_t* __restrict__ ckv, bf16_t* __restrict__ out,
-                                                           XProbs xp, int one_pass) {
+                                                           XProbs xp, int one_pass, int tw_nt_from = 1 << 30) {
   TW_DEC_PRIO();
   __shared__ float sc[DA_MAXK];
   __shared__ float part[NG * 64];
@@ -617,7 +631,8 @@ __global__ __launch_bounds__(NG * 8) void k_attn_decode_cross(const bf16_t* __re
   __syncthreads();
   const bf16_t* K = ckv + (((size_t)0 * Bt + slot) * H + h) * S * 64;
   const bf16_t* V = ckv + (((size_t)1 * Bt + slot) * H + h) * S * 64;
-  if (!PROBS && one_pass) dec_attend_1p<NG>(qf, K, V, S, part, sc, outv);  // (the probabilities need the two passes)
+  if (!PROBS && one_pass && slot >= tw_nt_from) dec_attend_1p<NG, true>(qf, K, V, S, part, sc, outv);
+  else if (!PROBS && one_pass) dec_attend_1p<NG>(qf, K, V, S, part, sc, outv);  // (probabilities: two passes)
   else if constexpr (NG == 32) dec_attend(qf, K, V, S, sc, part, red, outv);
   if (threadIdx.x < 64) out[(size_t)b * D + h * 64 + threadIdx.x] = f32_to_bf16(outv[threadIdx.x]);
   if constexpr (PROBS) {
@@ -638,10 +653,10 @@ extern "C" int tw_attn_decode_cross(const bf16_t* q, int B, int H, int S, int Bt
   TW_REQUIRE(q && cross_kv && out && B > 0 && H > 0 && S > 0 && S <= DA_MAXK, "tw_attn_decode_cross: bad args");
   if (tw_dec_cross_ng == 64 && tw_dec_cross_1p)
     hipLaunchKernelGGL((k_attn_decode_cross<false, 64>), dim3(H, B), dim3(512), 0, (hipStream_t)stream, q, H * 64, S,
-                       Bt, row_map, cross_kv, out, XProbs{}, 1);
+                       Bt, row_map, cross_kv, out, XProbs{}, 1, tw_dec_cross_nt);
   else
     hipLaunchKernelGGL(k_attn_decode_cross<false>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt,
-                       row_map, cross_kv, out, XProbs{}, tw_dec_cross_1p);
+                       row_map, cross_kv, out, XProbs{}, tw_dec_cross_1p, tw_dec_cross_nt);
   return tw_check_launch("tw_attn_decode_cross");
 }
 
@@ -654,6 +669,6 @@ extern "C" int tw_attn_decode_cross_probs(const bf16_t* q, int B, int H, int S, 
   TW_REQUIRE(slot0 >= 0 && slot0 + __builtin_popcount(head_mask) <= n_slots && n_steps > 0,
              "tw_attn_decode_cross_probs: slots");
   hipLaunchKernelGGL(k_attn_decode_cross<true>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt,
-                     row_map, cross_kv, out, XProbs{probs, pos, head_mask, slot0, n_slots, pos0, n_steps}, 0);
+                     row_map, cross_kv, out, XProbs{probs, pos, head_mask, slot0, n_slots, pos0, n_steps}, 0, 1 << 30);
   return tw_check_launch("tw_attn_decode_cross_probs");
 }

@@ -198,12 +198,15 @@ static inline int tw_group_for(int N) {
   if (tw_gemm_group_m > 0) return tw_gemm_group_m;
   return (N + 255) / 256 >= 10 ? 8 : 1;
 }
+// packed GEMVs with N >= this (proj_out) read their weights non-temporally: bench step -1 ms (109.2 vs 110.3)
+static int tw_gemv_nt_min_n = 16384;
 static int tw_tune_skinny_nw = 0;  // 0 = heuristic; 4 / 8 / 16 force the skinny kernel's waves per block
 static int tw_tune_gemv_kw = 0;    // 0 = heuristic; 1 / 2 / 4 / 8 force the packed GEMV's K-slices per column group
 extern "C" int tw_gemm_set_variant(int big) {
   tw_gemm_big_enabled = big & 7;
   const int nw = (big >> 8) & 0xff;
   tw_tune_skinny_nw = (nw == 4 || nw == 8 || nw == 16) ? nw : 0;
+  tw_gemv_nt_min_n = (big & 0x1000000) ? (1 << 30) : 16384;  // bit 24: proj_out weights through the caches (A/B)
   const int kw = (big >> 16) & 0xff;
   tw_tune_gemv_kw = (kw == 1 || kw == 2 || kw == 4 || kw == 8) ? kw : 0;
   return 0;
@@ -1282,7 +1285,9 @@ __global__ __launch_bounds__(256) void k_pack_weight(const bf16_t* __restrict__ 
   *(uint4*)(Wp + c * 8) = v;
 }
 
-template <int EPI, int KW, int U, bool APACK, bool TWO>
+// NTW: weight fragments read with non-temporal loads (proj_out: 133 MB streamed once per step, kept out of the
+// caches so that the layer weights can stay in them).
+template <int EPI, int KW, int U, bool APACK, bool TWO, bool NTW = false>
 __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __restrict__ A, int lda,
                                                                const bf16_t* __restrict__ Wp, int M, int N, int K,
                                                                EpiArgs ea) {
@@ -1317,7 +1322,13 @@ __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __r
       bf16x8 bw[U], a0[U], a1[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        bw[u] = *(const bf16x8*)(wp + (size_t)(st + u) * 512);
+        if constexpr (NTW) {
+          typedef short s16x8_nt __attribute__((ext_vector_type(8)));
+          const s16x8_nt t = __builtin_nontemporal_load((const s16x8_nt*)(wp + (size_t)(st + u) * 512));
+          bw[u] = __builtin_bit_cast(bf16x8, t);
+        } else {
+          bw[u] = *(const bf16x8*)(wp + (size_t)(st + u) * 512);
+        }
         a0[u] = ldA0(st + u);
         if (TWO) a1[u] = ldA1(st + u);
       }
@@ -1361,16 +1372,17 @@ __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __r
   }
 }
 
-template <int EPI, int KW, int U, bool APACK>
+template <int EPI, int KW, int U, bool APACK, bool NTW = false>
 static void launch_gemv_p3(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea, int splits,
                            hipStream_t s) {
   constexpr int NW = KW > 4 ? KW : 4, GPB = NW / KW;
   dim3 grid(tw_cdiv(tw_cdiv(N, 16), GPB), splits);
   if (M > 16)
-    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, true>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea);
+    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, true, NTW>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea);
   else
-    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, false>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea);
+    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, false, NTW>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea);
 }
+
 
 template <int EPI, bool APACK>
 static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea, int splits,
@@ -1381,7 +1393,8 @@ static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
   int kw = 1;
   while (groups * kw < 1024 && kw < 8 && steps >= 8 * kw) kw *= 2;
   if (tw_tune_gemv_kw) kw = tw_tune_gemv_kw;
-  if (kw == 1) launch_gemv_p3<EPI, 1, 16, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
+  if (kw == 1 && N >= tw_gemv_nt_min_n) launch_gemv_p3<EPI, 1, 16, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
+  else if (kw == 1) launch_gemv_p3<EPI, 1, 16, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
   else if (kw == 2) launch_gemv_p3<EPI, 2, 8, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
   else if (kw == 4) launch_gemv_p3<EPI, 4, 8, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
   else launch_gemv_p3<EPI, 8, 8, APACK>(A, lda, Wp, M, N, K, ea, splits, s);

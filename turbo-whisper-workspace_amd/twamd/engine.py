@@ -259,6 +259,7 @@ class WhisperEngine:
         self._chain_cache: Dict[tuple, List[DecView]] = {}
         self._pump: Optional[_EncoderPump] = None  # paced next-batch encoder (run_batches)
         self.dec_ahead = int(os.environ.get("TW_DEC_AHEAD", "2"))
+        self.pump_ahead = int(os.environ.get("TW_PUMP_AHEAD", "2"))  # encoder chunks pending beside a decode
         # greedy steps end with the fused select + next-step embedding + first LayerNorm (tw_logits_select_embed):
         # 47 launches per token instead of 49. TW_FUSED_SELECT=0: the separate kernels (A/B)
         self.fused_select = os.environ.get("TW_FUSED_SELECT", "1") != "0"
@@ -1120,7 +1121,7 @@ class WhisperEngine:
                 prefetch(k)
             if overlap and k + 1 < len(sizes):
                 if paced:  # runs beside the decode of batch k, queued between its decode steps
-                    self._pump = _EncoderPump(self, prefetch_steps(k + 1))
+                    self._pump = _EncoderPump(self, prefetch_steps(k + 1), ahead=self.pump_ahead)
                     self._pump()
                 else:
                     prefetch(k + 1, alone=False)
