@@ -131,11 +131,12 @@ def main():
     families = {f"{k[0]}<{k[1]}>": {"launches": v[0], "tflop": round(v[1] / 1e12, 3), "ms": round(v[2], 3),
                                     "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 1) if v[2] > 0 else None}
                 for k, v in fam.items()}
-    traffic, traffic_src = measured_traffic("k_" + dom, fp8)
+    # the bf16 family runs as k_gemm_big beside a decode and as k_gemm_8p alone (engine._set_gemm_context)
+    traffic, traffic_src = measured_traffic(("k_" + dom,) if fp8 else ("k_gemm_big", "k_gemm_8p"), fp8)
 
     # secondary (HBM-bound) kernel: decoder cross-attention, timed on one eager decode pass outside the timed
     # region (the timed decode steps replay a hipGraph, which has no room for events)
-    dec = decode_cross_roofline(eng, B, traffic_lookup=measured_traffic("k_attn_decode_cross", fp8))
+    dec = decode_cross_roofline(eng, B, traffic_lookup=measured_traffic(("k_attn_decode_cross",), fp8))
 
     out = {
         "metric": "real-time factor (audio-sec/wall-sec) Whisper-v3-turbo, 30s chunks, 1/2/4/8 GPU",
@@ -158,7 +159,7 @@ def main():
                    "decode_tokens_per_window": T, "mean_tokens_out": float(np.mean(n_tok))},
         "roofline": {"bound": "mfma",
                      "kernel": ("k_gemm_mx (encoder q/k/v/o + fc1/fc2, MX fp8 MFMA)" if fp8 else
-                                "k_gemm_big (all encoder/conv/cross-KV projections, bf16 MFMA)"),
+                                "k_gemm_big / k_gemm_8p (all encoder/conv/cross-KV projections, bf16 MFMA)"),
                      "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "traffic_source": traffic_src, "launches_per_step": n_l // a.steps,
@@ -175,10 +176,11 @@ def main():
         dist.destroy_process_group()
 
 
-def measured_traffic(kernel: str, c5: bool = False):
-    """HBM bytes per launch of `kernel` from the newest rocprofv3 PMC summary under profiles/
-    (scripts/summarize_prof.py: 2*FETCH_SIZE + WRITE_SIZE per launch), or (None, None). Config-5 runs
-    (--config c5) write *_c5_traffic.json; each config reads only its own."""
+def measured_traffic(kernels, c5: bool = False):
+    """HBM bytes per launch of the `kernels` (names of one family, launch-weighted together) from the newest
+    rocprofv3 PMC summary under profiles/ that has any of them (scripts/summarize_prof.py: 2*FETCH_SIZE + WRITE_SIZE
+    per launch), or (None, None). Config-5 runs (--config c5) write *_c5_traffic.json; each config reads only its
+    own."""
     import glob
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json")), key=os.path.getmtime)
@@ -189,8 +191,10 @@ def measured_traffic(kernel: str, c5: bool = False):
                 d = json.load(fh)
         except (OSError, ValueError):
             continue
-        if kernel in d and d[kernel].get("hbm_bytes"):
-            return d[kernel]["hbm_bytes"], os.path.relpath(f, ROOT)
+        hit = [d[k] for k in kernels if k in d and d[k].get("hbm_bytes") and d[k].get("launches")]
+        if hit:
+            n = sum(h["launches"] for h in hit)
+            return sum(h["hbm_bytes"] * h["launches"] for h in hit) / n, os.path.relpath(f, ROOT)
     return None, None
 
 
