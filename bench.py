@@ -183,7 +183,9 @@ def measured_traffic(kernels, c5: bool = False):
     own."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json")), key=os.path.getmtime)
+    # newest = the latest round tag (profiles/rNN<x>_..., names sort by round); file mtimes do not survive the copy
+    # to the GPU box reliably
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json")), key=os.path.basename)
     files = [f for f in files if ("_c5_" in os.path.basename(f)) == c5]
     for f in reversed(files):
         try:
