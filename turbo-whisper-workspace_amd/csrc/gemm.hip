@@ -228,6 +228,9 @@ extern "C" int tw_gemm_set_variant(int big) {
 #define GB_BM 256
 #define GB_BN 256
 #define GB_BK 64
+#ifndef GB_A_POL
+#define GB_A_POL 0  // cache policy of k_gemm_big's activation-operand DMA (experiment builds: 2 = nt)
+#endif
 #define GB_EPI_LD 68  // f32 row stride of the epilogue staging image (64 + 4: conflict-free writes)
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -431,7 +434,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int rb = 8 * (4 * wid + i) * GB_BK;  // wave-uniform LDS base of this instruction
-      __builtin_amdgcn_global_load_lds((const void*)(ga[i] + k0), (lds_void_t*)(As + rb), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(ga[i] + k0), (lds_void_t*)(As + rb), 16, 0, GB_A_POL);
       __builtin_amdgcn_global_load_lds((const void*)(gw[i] + k0), (lds_void_t*)(Ws + rb), 16, 0, 0);
     }
   };
