@@ -228,6 +228,9 @@ extern "C" int tw_gemm_set_variant(int big) {
 #define GB_BM 256
 #define GB_BN 256
 #define GB_BK 64
+#ifndef GB_XKV_NT
+#define GB_XKV_NT 0  // 1: the cross-K/V epilogue stores non-temporally (experiment build)
+#endif
 #ifndef GB_A_POL
 #define GB_A_POL 0  // cache policy of k_gemm_big's activation-operand DMA (experiment builds: 2 = nt)
 #endif
@@ -319,6 +322,13 @@ __device__ inline void epi_store8(const EpiArgs& ea, int m, int n, int N, float4
         int h = hd >> 6, d = hd & 63;
         int b = m / S, s2 = m - b * S;
         idx = ((((size_t)(l * 2 + kv) * ea.kv_B + b) * ea.kv_H + h) * S + s2) * 64 + d;
+#if GB_XKV_NT
+        // the cross K/V cache is read back only by the decoder's non-temporal loads: write it past the caches too
+        typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+        const u32x4_nt wv = {w.x, w.y, w.z, w.w};
+        __builtin_nontemporal_store(wv, (u32x4_nt*)((bf16_t*)ea.out + idx));
+        return;
+#endif
       } else {
         idx = (size_t)m * ea.ldo + n;
       }
