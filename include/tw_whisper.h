@@ -166,8 +166,13 @@ int tw_attn_encoder_mx(const uint16_t* qkv, int B, int S, int H, uint8_t* out, u
  * k_attn_enc2 with 8 waves / 256 queries per workgroup, 4 = the same with 4 waves, 0 = the first kernel.
  * + 0x100: tw_attn_decode_cross in two passes (scores, softmax, P.V) instead of the one-pass online softmax.
  * + 0x200: the one-pass tw_attn_decode_cross with 512 threads (64 key groups) per (row, head) instead of 256.
- * + (s + 1) << 12: cross K/V of encoder slots >= s read non-temporally (0: every slot, the default; 0xff << 12: none). */
+ * + (s + 1) << 12: cross K/V of encoder slots >= s read non-temporally (0: every slot, the default; 0xff << 12: none).
+ * + p << 20: p x 16 KiB of extra LDS per encoder-attention workgroup (as tw_attn_set_lds_pad). */
 int tw_attn_set_variant(int variant);
+/* Process-wide: reserve units x 16 KiB (0..8) of extra LDS per tw_attn_encoder workgroup, capping its workgroups per CU
+ * so that decoder kernels launched beside it on another stream find free wave slots (the engine sets 4 for encoder
+ * chunks queued beside a decode, 0 otherwise). Returns 0, or TW_ERR_ARG. */
+int tw_attn_set_lds_pad(int units);
 /* Decoder residual+LayerNorm kernel (A/B): 0 = one wave per row when D == 1280 (default), 1 = the 4-wave block form. */
 int tw_ln_set_variant(int variant);
 

@@ -107,6 +107,42 @@ def test_damaged_and_truncated_streams_raise():
         audio.decode_flac(b"RIFF" + bytes(60))
 
 
+def _frames(pcm, bs, **kw):
+    """(header bytes, [frame bytes]) of a fixed-blocksize stream: frame k ends where the stream of the first k
+    blocks ends (the writer numbers and codes frames independently of what follows)."""
+    full = ao.flac_encode(pcm, 16000, 16, blocksizes=(bs,), **kw)
+    a0 = int(audio.flac_probe(full).audio_offset)
+    ends = [len(ao.flac_encode(pcm[: bs * k], 16000, 16, blocksizes=(bs,), **kw)) for k in range(1, len(pcm) // bs + 1)]
+    starts = [a0] + ends[:-1]
+    frames = [full[s:e] for s, e in zip(starts, ends)]
+    assert b"".join(frames) == full[a0:]
+    return full[:a0], frames
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_skipped_or_repeated_frames_raise(threads):
+    """frames [0, 2, 3, 3] still reach the STREAMINFO sample count; samples 1024..2047 would be left
+    unwritten. The decoder requires the frames to tile [0, total) and the output buffer starts zeroed."""
+    pcm = _pcm(4 * 1024, 1, 16, 15)
+    hdr, fr = _frames(pcm, 1024, subframe_kinds=("fixed2",))
+    assert np.array_equal(audio.decode_flac(hdr + b"".join(fr), threads=threads).pcm, pcm)
+    for order in ([0, 2, 3, 3], [0, 1, 1, 3], [1, 0, 2, 3]):
+        with pytest.raises(ValueError, match="contiguous|missing|repeated|decoded"):
+            audio.decode_flac(hdr + b"".join(fr[i] for i in order), threads=threads)
+
+
+def test_oversized_header_rejected_before_allocation():
+    """A STREAMINFO total of 2^36 - 1 samples on a few-kB stream is refused before anything is allocated."""
+    pcm = _pcm(2048, 1, 16, 16)
+    data = bytearray(ao.flac_encode(pcm, 16000, 16, blocksizes=(1024,), subframe_kinds=("fixed2",)))
+    # STREAMINFO: 4 (fLaC) + 4 (block header) + 13 bytes in: low 4 bits of byte 13 and bytes 14..17 = total samples
+    data[8 + 13] |= 0x0F
+    data[8 + 14: 8 + 18] = b"\xff\xff\xff\xff"
+    assert int(audio.flac_probe(bytes(data)).total_samples) == (1 << 36) - 1
+    with pytest.raises(ValueError, match="larger than"):
+        audio.decode_flac(bytes(data))
+
+
 @pytest.mark.parametrize("rates", [(192000, 16000), (44100, 16000), (48000, 16000), (8000, 16000),
                                    (22050, 16000), (16000, 16000)])
 def test_filter_bank_matches_oracle_design(rates):

@@ -52,6 +52,32 @@ def test_load_failure_returns_reference_error(tmp_path, monkeypatch):
     assert pipe.transcribe(_wav(tmp_path)) == {"error": "Failed to load transcription model"}
 
 
+def test_no_checkpoint_is_a_load_failure_not_gibberish(tmp_path, monkeypatch):
+    """the reference loads real weights or fails; without TW_CHECKPOINT the drop-in must not serve the
+    seeded synthetic preset under the reference's model name (opt-in: TW_ALLOW_SYNTHETIC=1)."""
+    monkeypatch.delenv("TW_CHECKPOINT", raising=False)
+    monkeypatch.delenv("TW_ALLOW_SYNTHETIC", raising=False)
+    built = []
+    monkeypatch.setattr(ap.TurboTranscriber, "from_pretrained", staticmethod(lambda *a, **k: built.append(a) or FakeASR()))
+    try:
+        ap.build_transcriber()
+        raise AssertionError("build_transcriber accepted no checkpoint")
+    except RuntimeError as e:
+        assert "TW_CHECKPOINT" in str(e)
+    ap._PIPELINE_CACHE["transcription_model"] = None
+    pipe = ap.AudioProcessingPipeline()
+    assert pipe.load_transcription_model() is False
+    assert pipe.transcribe(_wav(tmp_path)) == {"error": "Failed to load transcription model"}
+    assert built == []
+    # explicit opt-in, and a local checkpoint directory, both build
+    monkeypatch.setenv("TW_ALLOW_SYNTHETIC", "1")
+    ap.build_transcriber()
+    monkeypatch.delenv("TW_ALLOW_SYNTHETIC")
+    ap.build_transcriber(str(tmp_path))
+    assert len(built) == 2
+    ap._PIPELINE_CACHE["transcription_model"] = None
+
+
 def test_process_audio_schema_without_diarization(tmp_path):
     pipe = ap.AudioProcessingPipeline(transcriber=FakeASR())
     r = pipe.process_audio(_wav(tmp_path, 3.0))

@@ -156,6 +156,133 @@ def _serve_worker(rank, ws, port, q):
         dist.destroy_process_group()
 
 
+def long_windows(wav, windows):
+    """Windows whose 'generate' output ran several seek passes: more tokens than one pass can return (> 448)."""
+    return [[ST.timestamp_begin] + [300 + (w.start // 997 + i) % 20000 for i in range(600 + 37 * j)]
+            + [ST.timestamp_begin + 1400] for j, w in enumerate(windows)]
+
+
+def failing_on_rank1(wav, windows):
+    if twd.world()[0] == 1:
+        raise RuntimeError("engine fault on rank 1")
+    return fake_windows(wav, windows)
+
+
+def _edge_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        rng = np.random.default_rng(5)
+        wav = rng.standard_normal(16000 * 150).astype(np.float32)
+        windows = list(chunk_windows(len(wav), 30, 0, 16000))
+        res = {"long": twd.transcribe_sharded(long_windows, wav, windows)}
+        try:
+            twd.transcribe_sharded(failing_on_rank1, wav, windows)
+            res["fail"] = None
+        except twd.PeerError as e:
+            res["fail"] = ("peer", str(e))
+        except RuntimeError as e:
+            res["fail"] = ("own", str(e))
+        # the collectives still line up after a failed call
+        res["after"] = twd.transcribe_sharded(fake_windows, wav, windows)
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_long_windows_and_collective_failure():
+    """a window can return more than 448 tokens (several seek passes): the gather width is agreed over
+    the ranks instead of fixed; an engine failure on one rank raises on every rank instead of leaving the others
+    blocked in the all-gather, and the group stays usable."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_edge_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(5)
+    wav = rng.standard_normal(16000 * 150).astype(np.float32)
+    windows = list(chunk_windows(len(wav), 30, 0, 16000))
+    ref_long = []
+    for r in range(2):
+        lo, hi = twd.shard_range(len(windows), 2, r)
+        ref_long += long_windows(wav, windows[lo:hi])
+    assert max(len(s) for s in ref_long) > twd.MAX_TOKENS
+    for r in (0, 1):
+        assert res[r]["long"] == ref_long
+        assert res[r]["after"] == fake_windows(wav, windows)
+    assert res[1]["fail"] == ("own", "engine fault on rank 1")
+    assert res[0]["fail"][0] == "peer"
+
+
+class _LoadingASR(_RecordingASR):
+    """Decodes like TurboTranscriber.__call__: rank 0 loads the input (here: None is a broken upload) and tells the
+    other ranks through broadcast_waveform whether it failed."""
+
+    def __call__(self, inputs, **kw):
+        rank, ws = twd.world()
+        wav, err = None, None
+        if rank == 0:
+            try:
+                if inputs is None:
+                    raise ValueError("corrupt upload")
+                wav = np.asarray(inputs, np.float32)
+            except ValueError as e:
+                err = e
+        wav = twd.broadcast_waveform(wav, failed=err is not None)
+        if err is not None:
+            raise err
+        windows = list(chunk_windows(len(wav), kw["chunk_length_s"], kw.get("stride_length_s"), 16000))
+        seqs = twd.transcribe_sharded(fake_windows, wav, windows)
+        self.calls.append(kw)
+        return seqs
+
+
+def _serve_bad_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        fe = twd.RankZeroFrontend(_LoadingASR())
+        if rank == 0:
+            out = []
+            try:
+                fe(None, chunk_length_s=30, stride_length_s=0)
+            except ValueError as e:
+                out.append(str(e))
+            rng = np.random.default_rng(9)
+            out.append(fe(rng.standard_normal(16000 * 40).astype(np.float32), chunk_length_s=30, stride_length_s=0))
+            fe.close()
+            q.put((0, out))
+        else:
+            q.put((rank, fe.follow()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rank_zero_frontend_survives_bad_input():
+    """rank 0 failing to decode an upload must not leave the followers blocked in the waveform broadcast:
+    rank 0 raises (-> the reference's error dict upstream), followers skip the call and keep serving."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_serve_bad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res[0][0] == "corrupt upload"
+    assert res[1] == 1  # the good call was served, the failed one skipped
+    rng = np.random.default_rng(9)
+    wav = rng.standard_normal(16000 * 40).astype(np.float32)
+    assert res[0][1] == fake_windows(wav, list(chunk_windows(len(wav), 30, 0, 16000)))
+
+
 def test_rank_zero_frontend_serves_followers():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

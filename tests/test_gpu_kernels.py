@@ -186,6 +186,25 @@ def test_encoder_attention_vs_torch(B, L, H, variant):
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("pad", [4, 8])
+def test_encoder_attention_lds_pad_is_bit_identical(pad):
+    """tw_attn_set_lds_pad only reserves LDS (fewer workgroups per CU beside a decode): same bits as unpadded."""
+    B, L, H = 2, 1500, 5
+    D = H * 64
+    qkv = rand_bf16(B * L, 3 * D, seed=17)
+    qkv[:, :D] = bf(qkv[:, :D].float() * 0.375)
+    outs = []
+    for p in (0, pad):
+        _lib.call("tw_attn_set_lds_pad", p)
+        out = torch.empty(B * L, D, dtype=torch.bfloat16, device=DEV)
+        _lib.call("tw_attn_encoder", qkv.data_ptr(), B, L, H, out.data_ptr(), S())
+        outs.append(out)
+    _lib.call("tw_attn_set_lds_pad", 0)
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    with pytest.raises(_lib.TwError):
+        _lib.call("tw_attn_set_lds_pad", 9)
+
+
 def test_encoder_attention_online_softmax_rescale():
     """Force the running max to jump in a late key tile (rule 26: exercise the rescale branch)."""
     B, L, H = 1, 1500, 1

@@ -349,7 +349,19 @@ static int tw_dec_cross_1p = 1;
 // the encoder's operands): cross-attention 40.1 -> 35.2 us per launch, bench step 111.1 -> 109.0 ms.
 static int tw_dec_cross_nt = 0;
 static int tw_dec_cross_ng = 32;  // 8-lane key groups per one-pass block (64 measured 3% slower in the bench)
+// Extra (unused) LDS reserved per encoder-attention workgroup, in 16 KiB units: caps the attention's workgroups per CU
+// so that decoder waves queued beside it (run_batches' overlap) find free wave slots on every CU.
+// Measured (scripts/exp/interference.py, 24 windows): beside 4 x 16 KiB of padding (one workgroup per CU) a decoder
+// GEMV launch takes 5.6 instead of 21.9 us and the cross-attention 40.8 instead of 73.4 us, while the attention alone
+// slows 444 -> 543 us; the engine pads only the encoder chunks queued beside a decode (tw_attn_set_lds_pad).
+static int tw_attn_lds_pad = 0;
+extern "C" int tw_attn_set_lds_pad(int units) {
+  TW_REQUIRE(units >= 0 && units <= 8, "tw_attn_set_lds_pad: %d x 16 KiB (0..8)", units);
+  tw_attn_lds_pad = units;
+  return 0;
+}
 extern "C" int tw_attn_set_variant(int v) {
+  tw_attn_lds_pad = (v >> 20) & 0xf;  // bits 20-23
   tw_dec_cross_1p = (v & 0x100) ? 0 : 1;  // bit 8: the two-pass decoder cross-attention (A/B)
   // bits 12-19: 0 = every slot's cross K/V read non-temporally (default), else 1 + the first slot read so (0xff: none)
   tw_dec_cross_nt = (v >> 12) & 0xff ? ((v >> 12) & 0xff) - 1 : 0;
@@ -363,6 +375,7 @@ extern "C" int tw_attn_encoder(const bf16_t* qkv, int B, int S, int H, bf16_t* o
   TW_REQUIRE(qkv && out && B > 0 && S > 0 && H > 0, "tw_attn_encoder: bad args");
   const int D = H * 64;
   hipStream_t st = (hipStream_t)stream;
+  const size_t pad = (size_t)tw_attn_lds_pad * 16384;
   if (tw_attn_variant == 0) {
     hipLaunchKernelGGL(k_attn_encoder, dim3(tw_cdiv(S, 128), H, B), dim3(256), 0, st, qkv, S, H, D, out);
   } else if (tw_attn_variant == 4) {
@@ -370,10 +383,10 @@ extern "C" int tw_attn_encoder(const bf16_t* qkv, int B, int S, int H, bf16_t* o
     hipLaunchKernelGGL((k_attn_enc2<4, 2>), dim3(nwork), dim3(256), 0, st, qkv, S, H, D, nqb, nwork, out);
   } else if (tw_attn_variant == 9) {
     const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
-    hipLaunchKernelGGL((k_attn_enc2<8, 4>), dim3(nwork), dim3(512), 0, st, qkv, S, H, D, nqb, nwork, out);
+    hipLaunchKernelGGL((k_attn_enc2<8, 4>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
   } else {
     const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
-    hipLaunchKernelGGL((k_attn_enc2<8, 2>), dim3(nwork), dim3(512), 0, st, qkv, S, H, D, nqb, nwork, out);
+    hipLaunchKernelGGL((k_attn_enc2<8, 2>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
   }
   return tw_check_launch("tw_attn_encoder");
 }
@@ -566,17 +579,19 @@ __device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const 
   __syncthreads();
 }
 
+#ifndef TW_SELF_1P
+#define TW_SELF_1P 0  // 1: decoder self-attention in one pass. Measured in the bench: +6 ms per step (A/B builds)
+#endif
 // Self-attention step: qkv [B][3D] bf16 (q pre-scaled), appends k,v at position pos[b] into the cache
 // (layout [B][H][max_pos][64] for K and V of this layer) and attends over positions 0..pos[b].
 __global__ __launch_bounds__(256) void k_attn_decode_self(const bf16_t* __restrict__ qkv, int D, int max_pos,
                                                           const int* __restrict__ pos, bf16_t* __restrict__ kc,
                                                           bf16_t* __restrict__ vc, bf16_t* __restrict__ out) {
   TW_DEC_PRIO();
-  __shared__ float sc[DA_MAXK];
   __shared__ float part[32 * 64];
+  __shared__ float gml[64];
   __shared__ float qf[64];
   __shared__ float outv[64];
-  __shared__ float red[8];
   const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x;
   const int t = pos[b];
   const bf16_t* row = qkv + (size_t)b * 3 * D + h * 64;
@@ -589,7 +604,14 @@ __global__ __launch_bounds__(256) void k_attn_decode_self(const bf16_t* __restri
   }
   __threadfence_block();
   __syncthreads();
+#if TW_SELF_1P
+  // one pass (online softmax per 8-lane key group): K and V of <= 256 keys in flight together, one round trip
+  dec_attend_1p<32>(qf, K, V, t + 1, part, gml, outv);
+#else
+  __shared__ float sc[DA_MAXK];
+  __shared__ float red[8];
   dec_attend(qf, K, V, t + 1, sc, part, red, outv);
+#endif
   if (threadIdx.x < 64) out[(size_t)b * D + h * 64 + threadIdx.x] = f32_to_bf16(outv[threadIdx.x]);
 }
 

@@ -196,6 +196,9 @@ __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const f
   tw_row_ln_store<PACKED>(v, s, row, D, eps, g, bta, out, red);
 }
 
+#ifndef TW_LN_HOIST
+#define TW_LN_HOIST 0  // 1: gamma/beta loaded with the row. Measured in the bench: +2.5 ms per step (A/B builds)
+#endif
 // k_resid_ln for D = 256 * NV with ONE wave per row: every lane holds NV float4 chunks (c = lane + 64 i), both
 // LayerNorm reductions are wave shuffles, no LDS round trip or block barrier. A decode step runs 13 of these on 24
 // rows; the 4-wave form spends most of its ~6.8 us in its two barrier-separated reductions (tw_ln_set_variant(1)
@@ -209,6 +212,15 @@ __global__ __launch_bounds__(64) void k_resid_ln_w(float* __restrict__ x, const 
   const int row = blockIdx.x, lane = threadIdx.x;
   float* xr = x + (size_t)row * D;
   const float* pr = parts ? parts + (size_t)row * D : nullptr;
+  // gamma / beta first: their loads fly with the row's instead of after both reductions (one round trip less)
+  float4 gg[NV], bb[NV];
+  if (TW_LN_HOIST && g) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      gg[i] = ((const float4*)g)[lane + 64 * i];
+      bb[i] = ((const float4*)bta)[lane + 64 * i];
+    }
+  }
   float4 v[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) v[i] = ((const float4*)xr)[lane + 64 * i];
@@ -259,10 +271,13 @@ __global__ __launch_bounds__(64) void k_resid_ln_w(float* __restrict__ x, const 
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = lane + 64 * i;
-    const float4 gg = ((const float4*)g)[c], bb = ((const float4*)bta)[c];
+    if (!TW_LN_HOIST) {
+      gg[i] = ((const float4*)g)[c];
+      bb[i] = ((const float4*)bta)[c];
+    }
     uint2 w;
-    w.x = pack_bf16x2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
-    w.y = pack_bf16x2((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+    w.x = pack_bf16x2((v[i].x - mean) * rstd * gg[i].x + bb[i].x, (v[i].y - mean) * rstd * gg[i].y + bb[i].y);
+    w.y = pack_bf16x2((v[i].z - mean) * rstd * gg[i].z + bb[i].z, (v[i].w - mean) * rstd * gg[i].w + bb[i].w);
     if constexpr (PACKED) {
       *(uint2*)(out + tw_pack_act_idx(row, 4 * c)) = w;
     } else {

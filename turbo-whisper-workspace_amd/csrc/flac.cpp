@@ -370,6 +370,8 @@ size_t decode_frame(const uint8_t* d, size_t n, size_t pos, const TwFlacInfo& si
 struct Worker {
   size_t start = 0;     // byte offset of the first frame this worker owns (SIZE_MAX: none found)
   int64_t decoded = 0;  // max(first_sample + blocksize) over its frames
+  int64_t first = -1;   // first sample of its first frame
+  int64_t next = -1;    // first sample + blocksize of its last frame (frames must follow each other gap-free)
   bool ok = true;
   std::string err;
 };
@@ -483,6 +485,13 @@ extern "C" int tw_flac_decode(const uint8_t* data, int64_t size, int32_t* out, i
           w[t].err = msg;
           return;
         }
+        if (w[t].next >= 0 && fs != w[t].next) {  // a skipped or repeated sample range: not a valid stream
+          w[t].ok = false;
+          w[t].err = "frame sample numbers are not contiguous";
+          return;
+        }
+        if (w[t].first < 0) w[t].first = fs;
+        w[t].next = fs + bsz;
         w[t].decoded = std::max(w[t].decoded, fs + bsz);
         p += len;
       }
@@ -520,8 +529,17 @@ extern "C" int tw_flac_decode(const uint8_t* data, int64_t size, int32_t* out, i
       }
     return 1;
   }
+  // every output sample written exactly once: the workers' frame runs tile [0, total) in order
   int64_t got = 0;
-  for (auto& x : w) got = std::max(got, x.decoded);
+  for (auto& x : w) {
+    if (x.first < 0) continue;  // (a worker whose range held no frame start)
+    if (x.first != got) {
+      tw_set_error("tw_flac_decode: samples [%lld, %lld) missing or repeated", (long long)std::min(got, x.first),
+                   (long long)std::max(got, x.first));
+      return 1;
+    }
+    got = x.next;
+  }
   if (got != total) {
     tw_set_error("tw_flac_decode: decoded %lld of %lld samples", (long long)got, (long long)total);
     return 1;

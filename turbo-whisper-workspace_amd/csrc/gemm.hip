@@ -1330,6 +1330,8 @@ __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __r
     auto ldA1 = [&](int st) -> bf16x8 {
       return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024 + 512) : *(const bf16x8*)(ap1 + 32 * st);
     };
+    // Batches of U steps with every load in flight before the MFMAs, then the remainder step by step (measured,
+    // scripts/gemv_bench.py: a clamped last batch instead of the step loop is 0.5-1 us SLOWER per launch).
     int st = s0;
     for (; st + U <= s1; st += U) {
       bf16x8 bw[U], a0[U], a1[U];
@@ -1397,6 +1399,9 @@ static void launch_gemv_p3(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
 }
 
 
+#ifndef TW_PROJ_KW4
+#define TW_PROJ_KW4 0  // 1: proj_out with 4 K-slices per group: 25 vs 33 us alone, neutral in the bench (A/B)
+#endif
 template <int EPI, bool APACK>
 static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea, int splits,
                            hipStream_t s) {
@@ -1405,8 +1410,13 @@ static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
   const int steps = K / 32 / splits;
   int kw = 1;
   while (groups * kw < 1024 && kw < 8 && steps >= 8 * kw) kw *= 2;
+  // the vocabulary-wide proj_out (3242 column groups): 4 K-slices per group, 25.0 vs 32.8 us per launch with one
+  // (scripts/gemv_bench.py, B = 24): more waves in flight per CU for the one launch that streams 133 MB
+  const bool wide = N >= tw_gemv_nt_min_n;
+  if (TW_PROJ_KW4 && wide && steps >= 16) kw = 4;
   if (tw_tune_gemv_kw) kw = tw_tune_gemv_kw;
-  if (kw == 1 && N >= tw_gemv_nt_min_n) launch_gemv_p3<EPI, 1, 16, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
+  if (kw == 4 && wide) launch_gemv_p3<EPI, 4, 8, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
+  else if (kw == 1 && wide) launch_gemv_p3<EPI, 1, 16, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
   else if (kw == 1) launch_gemv_p3<EPI, 1, 16, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
   else if (kw == 2) launch_gemv_p3<EPI, 2, 8, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
   else if (kw == 4) launch_gemv_p3<EPI, 4, 8, APACK>(A, lda, Wp, M, N, K, ea, splits, s);

@@ -38,6 +38,7 @@ EXPORTED = (
     "tw_gemm_set_variant", "tw_attn_set_variant", "tw_ln_set_variant",
     "tw_dtw", "tw_attn_decode_cross_probs", "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_stream_create_masked", "tw_stream_destroy", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
     "tw_gemm_mx", "tw_quant_mx", "tw_layernorm_mx", "tw_attn_encoder_mx", "tw_gemm_mx_set_variant", "tw_logits_select_embed", "tw_gemm_set_group",
+    "tw_attn_set_lds_pad",
 )
 
 
@@ -106,6 +107,7 @@ _SIGS = {
     "tw_logits_select_embed": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), _P, _P, _I, _P, _P, _P, _P, _P, _I,
                                 _I, _P, _P, _P, _F, _P, _I, _P], _I),
     "tw_attn_set_variant": ([_I], _I),
+    "tw_attn_set_lds_pad": ([_I], _I),
     "tw_ln_set_variant": ([_I], _I),
     "tw_resid_layernorm": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
     "tw_dtw": ([_P, _I, _I, _P, _P, _P], _I),
@@ -129,14 +131,18 @@ _lib = None
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load (once) and type the library; raises if it is missing."""
+    """Load (once) and type the library; raises if it is missing. TW_LIB names another in-tree build of the same
+    C-ABI (A/B measurement of two builds in one session)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = os.environ.get("TW_LIB") or path
     if not os.path.exists(path):
         raise TwError(f"HIP library not built: {path} (run `make -C turbo-whisper-workspace_amd/csrc`)")
     lib = ctypes.CDLL(path)
     for name, (args, res) in _SIGS.items():
+        if os.environ.get("TW_LIB") and not hasattr(lib, name):
+            continue  # an older build under A/B: entry points it predates stay unbound
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res

@@ -16,6 +16,7 @@ from __future__ import annotations
 import ctypes
 import io
 import math
+import os
 import struct
 from typing import NamedTuple, Tuple, Union
 
@@ -50,7 +51,14 @@ def decode_flac(data: bytes, threads: int = 0) -> FlacStream:
     """FLAC bytes -> int32 PCM through the native decoder (frame CRCs checked; no concealment)."""
     _lib, lib = _flac_lib()
     info = flac_probe(data)
-    pcm = np.empty((int(info.total_samples), int(info.channels)), np.int32)
+    total, ch = int(info.total_samples), int(info.channels)
+    # bound the allocation before trusting the header: a frame codes at most 65535 samples per channel in no fewer
+    # than ~(6 + channels) bytes, and the decoded PCM is capped (TW_MAX_PCM_SAMPLES, default 2^31 frame-samples)
+    cap = int(os.environ.get("TW_MAX_PCM_SAMPLES", str(1 << 31)))
+    if total * ch > cap or total > (len(data) // (6 + ch) + 1) * 65535:
+        raise ValueError(f"FLAC header claims {total} samples x {ch} channels: larger than the stream can code "
+                         f"or than TW_MAX_PCM_SAMPLES={cap}")
+    pcm = np.zeros((total, ch), np.int32)  # never hand out uninitialised memory, whatever the decoder reports
     got = ctypes.c_int64()
     if lib.tw_flac_decode(ctypes.c_char_p(data), len(data), pcm.ctypes.data, pcm.shape[0], int(threads),
                           ctypes.byref(got)) != 0:

@@ -37,8 +37,17 @@ def _engine_options() -> Dict[str, Any]:
 
 
 def build_transcriber(model_name: str = DEFAULT_MODEL, **overrides) -> TurboTranscriber:
+    """The engine for `model_name` from a LOCAL checkpoint (TW_CHECKPOINT, or model_name naming a directory). The
+    reference either loads real weights or fails, so without a checkpoint this raises (load_transcription_model
+    turns that into its False / "Failed to load transcription model" convention) instead of serving gibberish from
+    seeded synthetic weights; TW_ALLOW_SYNTHETIC=1 opts into the synthetic preset (tests, benchmarks)."""
     opts = _engine_options()
     opts.update(overrides)
+    if opts.get("checkpoint") is None and not os.path.isdir(model_name) and \
+            os.environ.get("TW_ALLOW_SYNTHETIC", "0") != "1":
+        raise RuntimeError(f"no local checkpoint for {model_name!r}: set TW_CHECKPOINT to a Hugging Face Whisper "
+                           f"directory (config.json, *.safetensors, vocab.json), or TW_ALLOW_SYNTHETIC=1 for seeded "
+                           f"synthetic weights")
     return TurboTranscriber.from_pretrained(model_name, **opts)
 
 

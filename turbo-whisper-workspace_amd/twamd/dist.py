@@ -7,8 +7,14 @@ SURVEY.md §8e adds exactly one strategy for it. Windows are independent until `
   * `shard_range`      contiguous, order-preserving ranges: rank r takes windows [r*n/W, (r+1)*n/W)
   * each rank runs its windows through its own engine (weights replicated; no data-path collective)
   * `gather_tokens`    ONE all_gather_into_tensor of an int32 [n_local_max, 2 + T] array per rank
-                       (col 0 = number of tokens, col 1 = language id or -1, then the tokens, pad -1)
+                       (col 0 = number of tokens, col 1 = language id or -1, then the tokens, pad -1);
+                       T = the longest sequence over all ranks (one tiny MAX all-reduce agrees on it: a window
+                       that ran several seek passes can return more than max_target_positions tokens)
   * rank order = window order, so the gathered rows are already the global window list for stitching.
+
+Failures are collective: the same MAX all-reduce carries an error flag, so when one rank's engine raises, every
+rank raises (the failing rank its own exception, the others `PeerError`) instead of the healthy ranks blocking in
+the all-gather; a rank-0 input decode failure travels the same way through `broadcast_waveform`.
 
 With the nccl backend (= RCCL on ROCm) the gather runs over xGMI from device tensors; with gloo (CPU tests)
 from host tensors. Messages are tiny (1 h of audio = 120 windows x 450 x 4 B = 216 KB): latency-bound.
@@ -21,7 +27,11 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-MAX_TOKENS = 448  # max_target_positions: no window can return more tokens
+MAX_TOKENS = 448  # max_target_positions: the longest sequence ONE decode pass can return
+
+
+class PeerError(RuntimeError):
+    """Raised on the ranks whose own work succeeded when another rank failed the same collective call."""
 
 
 def world() -> Tuple[int, int]:
@@ -40,6 +50,22 @@ def shard_range(n: int, world_size: int, rank: int) -> Tuple[int, int]:
 
 def shard_sizes(n: int, world_size: int) -> List[int]:
     return [shard_range(n, world_size, r)[1] - shard_range(n, world_size, r)[0] for r in range(world_size)]
+
+
+def _coll_device(device: Optional[torch.device], group) -> torch.device:
+    """Where a collective's buffers live: cuda for nccl (= RCCL), cpu for gloo."""
+    if device is not None:
+        return device
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+        else torch.device("cpu")
+
+
+def agree(failed: bool, width: int, device: Optional[torch.device] = None, group=None) -> Tuple[bool, int]:
+    """One MAX all-reduce of (error flag, sequence width): (did any rank fail, the widest sequence anywhere)."""
+    t = torch.tensor([int(bool(failed)), int(width)], dtype=torch.int64, device=_coll_device(device, group))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    f, w = t.cpu().tolist()
+    return bool(f), int(w)
 
 
 def pack_tokens(seqs: Sequence[Sequence[int]], langs: Optional[Sequence[Optional[int]]], rows: int,
@@ -69,22 +95,28 @@ def unpack_tokens(arr: np.ndarray, n: int) -> Tuple[List[List[int]], List[Option
 
 def gather_tokens(local_seqs: Sequence[Sequence[int]], local_langs: Optional[Sequence[Optional[int]]], n_total: int,
                   device: Optional[torch.device] = None, group=None,
-                  width: int = MAX_TOKENS) -> Tuple[List[List[int]], List[Optional[int]]]:
+                  width: Optional[int] = None) -> Tuple[List[List[int]], List[Optional[int]]]:
     """All-gather every rank's window results; returns all n_total windows in global order (on every rank).
 
     `device`: where the collective's buffers live (a cuda device for RCCL, cpu for gloo; default: cuda when
-    the default backend is nccl)."""
+    the default backend is nccl). `width`: token columns per row, the SAME value on every rank; None = agree on
+    the longest local sequence with one MAX all-reduce (a shard-size mismatch is reported through it as well,
+    so no rank is left waiting in the gather)."""
     rank, ws = world()
     if ws == 1:
         return [list(s) for s in local_seqs], list(local_langs) if local_langs is not None else [None] * len(
             local_seqs)
     sizes = shard_sizes(n_total, ws)
-    if len(local_seqs) != sizes[rank]:
+    bad = len(local_seqs) != sizes[rank]
+    if width is None:
+        failed, width = agree(bad, max((len(s) for s in local_seqs), default=0), device, group)
+        if failed and not bad:
+            raise PeerError("another rank's window shard did not match its range")
+    if bad:
         raise ValueError(f"rank {rank} holds {len(local_seqs)} windows, its shard has {sizes[rank]}")
+    width = max(int(width), 1)
     rows = max(max(sizes), 1)
-    if device is None:
-        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
-            else torch.device("cpu")
+    device = _coll_device(device, group)
     loc = torch.from_numpy(pack_tokens(local_seqs, local_langs, rows, width)).to(device)
     allt = torch.empty(ws * rows, 2 + width, dtype=torch.int32, device=device)
     dist.all_gather_into_tensor(allt, loc, group=group)
@@ -99,16 +131,22 @@ def gather_tokens(local_seqs: Sequence[Sequence[int]], local_langs: Optional[Seq
 
 
 def broadcast_waveform(wav: Optional[np.ndarray], device: Optional[torch.device] = None, src: int = 0,
-                       group=None) -> np.ndarray:
-    """Rank `src` holds the decoded 16 kHz waveform; every rank returns a copy (length first, then samples)."""
+                       group=None, failed: bool = False) -> Optional[np.ndarray]:
+    """Rank `src` holds the decoded 16 kHz waveform; every rank returns a copy (length first, then samples).
+
+    `failed` (meaningful on `src`): decoding the input raised there. The length slot then carries -1: `src` gets
+    None back (and re-raises its own error), every other rank raises PeerError, so no rank waits for samples."""
     rank, ws = world()
     if ws == 1:
         return wav
-    if device is None:
-        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
-            else torch.device("cpu")
-    n = torch.tensor([0 if wav is None else len(wav)], dtype=torch.int64, device=device)
+    device = _coll_device(device, group)
+    n = torch.tensor([-1 if (rank == src and failed) else (0 if wav is None else len(wav))], dtype=torch.int64,
+                     device=device)
     dist.broadcast(n, src=src, group=group)
+    if int(n.item()) < 0:
+        if rank == src:
+            return None
+        raise PeerError(f"rank {src} failed to decode the input")
     buf = torch.empty(int(n.item()), dtype=torch.float32, device=device)
     if rank == src:
         buf.copy_(torch.from_numpy(np.ascontiguousarray(wav, np.float32)))
@@ -124,14 +162,25 @@ def transcribe_sharded(run_windows, wav: np.ndarray, windows: Sequence, device: 
     timestamps); the times are gathered too and the pairs are returned."""
     rank, ws = world()
     lo, hi = shard_range(len(windows), ws, rank)
-    local = run_windows(wav, list(windows[lo:hi])) if hi > lo else []
+    err: Optional[BaseException] = None
+    try:
+        local = run_windows(wav, list(windows[lo:hi])) if hi > lo else []
+        if len(local) != hi - lo:
+            raise ValueError(f"rank {rank}: {len(local)} results for {hi - lo} windows")
+    except Exception as e:  # made collective below: every rank learns of it before anyone enters the gather
+        err, local = e, []
+    toks = [t for t, _ in local] if timed else local
+    bits = [np.asarray(ts, dtype=np.float32).view(np.int32).tolist() for _, ts in local] if timed else []
+    failed, width = agree(err is not None, max((len(t) for t in list(toks) + bits), default=0), device, group)
+    if failed:
+        if err is not None:
+            raise err
+        raise PeerError("transcription failed on another rank")
+    seqs, _ = gather_tokens(toks, None, len(windows), device=device, group=group, width=width)
     if not timed:
-        seqs, _ = gather_tokens(local, None, len(windows), device=device, group=group)
         return seqs
     # word timestamps: (tokens, per-token float32 times); the times travel as their int32 bit patterns
-    seqs, _ = gather_tokens([t for t, _ in local], None, len(windows), device=device, group=group)
-    bits = [np.asarray(ts, dtype=np.float32).view(np.int32).tolist() for _, ts in local]
-    tsb, _ = gather_tokens(bits, None, len(windows), device=device, group=group)
+    tsb, _ = gather_tokens(bits, None, len(windows), device=device, group=group, width=width)
     return [(s, np.asarray(b, dtype=np.int32).view(np.float32).tolist()) for s, b in zip(seqs, tsb)]
 
 
@@ -153,12 +202,18 @@ class RankZeroFrontend:
         dist.broadcast_object_list([None], src=0, group=self.group)
 
     def follow(self) -> int:
-        """Loop of ranks != 0 until rank 0 calls close(); returns the number of calls served."""
+        """Loop of ranks != 0 until rank 0 calls close(); returns the number of calls served. A call that fails
+        (collectively: rank 0 could not decode its input, or some rank's engine raised) is skipped here; rank 0
+        raises it to its caller, which maps it to the reference's error convention."""
         n = 0
         while True:
             box = [None]
             dist.broadcast_object_list(box, src=0, group=self.group)
             if box[0] is None:
                 return n
-            self.transcriber(None, **box[0])
+            try:
+                self.transcriber(None, **box[0])
+            except Exception as e:  # every rank saw the same failure; keep serving
+                print(f"rank {dist.get_rank(self.group)}: call skipped: {e!r}")
+                continue
             n += 1

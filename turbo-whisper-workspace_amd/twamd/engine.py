@@ -154,6 +154,9 @@ class WhisperEngine:
             _lib.call("tw_ln_set_variant", int(os.environ["TW_LN_VARIANT"], 0))
         if os.environ.get("TW_ATTN_VARIANT"):
             _lib.call("tw_attn_set_variant", int(os.environ["TW_ATTN_VARIANT"], 0))
+        # encoder-attention LDS cap (16 KiB units) for chunks queued beside a decode; None: leave the library's setting
+        pad = os.environ.get("TW_ATTN_PAD", "4")
+        self._attn_pad_ctx = None if pad == "" or os.environ.get("TW_ATTN_VARIANT") else int(pad)
         d = weights.dims
         d.validate()
         self.d, self.w, self.gen = d, weights, gen
@@ -453,9 +456,14 @@ class WhisperEngine:
             pass
 
     def _set_gemm_context(self, alone: bool) -> None:
-        """Large-M GEMM kernel for the encoder chunk about to be queued (see __init__): 5 alone, 1 beside a decode."""
+        """Encoder kernels for the chunk about to be queued (see __init__): large-M GEMM 5 alone, 1 beside a decode;
+        the encoder attention capped at one workgroup per CU beside a decode (tw_attn_set_lds_pad: the decoder's
+        kernels then find free wave slots; measured decoder GEMV 21.9 -> 5.6 us per launch beside it, bench step
+        112.1 -> 108.5 ms), uncapped alone (the cap costs the attention itself 22 %)."""
         if not self._gemm_variant_fixed:
             _lib.call("tw_gemm_set_variant", 5 if alone else 1)
+        if self._attn_pad_ctx is not None:
+            _lib.call("tw_attn_set_lds_pad", 0 if alone else self._attn_pad_ctx)
 
     def _encode_steps(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True,
                       alone: bool = True):
@@ -561,7 +569,7 @@ class WhisperEngine:
         Residual stream xd stays f32; every d_model-wide projection (self/cross out_proj, fc2) is a split-K
         partial product whose sum, bias and residual add are folded into the next LayerNorm launch."""
         d, w = self.d, self.w
-        if v is None and self.packed_decoder and R > 32:  # the packed layout holds 32 rows: one pass per 32
+        if v is None and R > 32:  # the decoder GEMVs / skinny GEMMs take <= 32 rows: one pass per 32
             r_enc = R if r_enc is None else r_enc
             for r0 in range(0, R, 32):
                 self.decoder_step(min(32, R - r0), with_logits, self._view(r0, min(32, R - r0)), r_enc, pre_embedded)
@@ -949,10 +957,9 @@ class WhisperEngine:
         key = ("chains", R)
         if key not in self._chain_cache:
             k = max(1, min(self.n_chains, R // 4))
-            if self.packed_decoder:
-                k = max(k, (R + 31) // 32)
-                while len(self._chain_streams) < k:
-                    self._chain_streams.append(self._chain_streams[0])  # one stream: the chains run in turn
+            k = max(k, (R + 31) // 32)  # <= 32 rows per chain (packed GEMV and skinny GEMM limit)
+            while len(self._chain_streams) < k:
+                self._chain_streams.append(self._chain_streams[0])  # one stream: the chains run in turn
             views = []
             for i in range(k):
                 r0, r1 = i * R // k, (i + 1) * R // k

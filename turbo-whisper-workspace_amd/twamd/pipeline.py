@@ -88,9 +88,16 @@ class TurboTranscriber:
 
         rank, world = dist.world()
         dev = getattr(self.engine, "device", None)
-        wav = audio.load_input(inputs, self.sampling_rate, dev) if rank == 0 else None
+        wav, load_err = None, None
+        if rank == 0:
+            try:
+                wav = audio.load_input(inputs, self.sampling_rate, dev)
+            except Exception as e:  # raised below, after the other ranks have been told (no rank left waiting)
+                load_err = e
         if world > 1:  # SPMD: every rank calls with the same arguments; rank 0 decoded the input
-            wav = dist.broadcast_waveform(wav)
+            wav = dist.broadcast_waveform(wav, failed=load_err is not None)
+        if load_err is not None:
+            raise load_err
         if chunk_length_s:
             windows = list(chunk_windows(len(wav), chunk_length_s, stride_length_s, self.sampling_rate))
             with_stride = True
