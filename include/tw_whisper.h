@@ -166,6 +166,7 @@ int tw_attn_encoder_mx(const uint16_t* qkv, int B, int S, int H, uint8_t* out, u
  * k_attn_enc2 with 8 waves / 256 queries per workgroup, 4 = the same with 4 waves, 0 = the first kernel.
  * + 0x100: tw_attn_decode_cross in two passes (scores, softmax, P.V) instead of the one-pass online softmax.
  * + 0x200: the one-pass tw_attn_decode_cross with 512 threads (64 key groups) per (row, head) instead of 256.
+ * + 0x400: the one-pass tw_attn_decode_cross with its ~15 KiB LDS merge instead of the ~1.3 KiB shuffle merge.
  * + (s + 1) << 12: cross K/V of encoder slots >= s read non-temporally (0: every slot, the default; 0xff << 12: none).
  * + p << 20: p x 16 KiB of extra LDS per encoder-attention workgroup (as tw_attn_set_lds_pad). */
 int tw_attn_set_variant(int variant);

@@ -360,8 +360,10 @@ extern "C" int tw_attn_set_lds_pad(int units) {
   tw_attn_lds_pad = units;
   return 0;
 }
+static int tw_dec_cross_lean = 1;  // the one-pass cross-attention in its small-LDS form (0: the 15 KiB form; A/B)
 extern "C" int tw_attn_set_variant(int v) {
   tw_attn_lds_pad = (v >> 20) & 0xf;  // bits 20-23
+  tw_dec_cross_lean = (v & 0x400) ? 0 : 1;  // bit 10: the 15 KiB-LDS one-pass cross-attention (A/B)
   tw_dec_cross_1p = (v & 0x100) ? 0 : 1;  // bit 8: the two-pass decoder cross-attention (A/B)
   // bits 12-19: 0 = every slot's cross K/V read non-temporally (default), else 1 + the first slot read so (0xff: none)
   tw_dec_cross_nt = (v >> 12) & 0xff ? ((v >> 12) & 0xff) - 1 : 0;
@@ -579,6 +581,7 @@ __device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const 
   __syncthreads();
 }
 
+#define DA_SELF_MAXK 448  // decoder positions (max_target_positions of every Whisper checkpoint)
 #ifndef TW_SELF_1P
 #define TW_SELF_1P 0  // 1: decoder self-attention in one pass. Measured in the bench: +6 ms per step (A/B builds)
 #endif
@@ -608,7 +611,8 @@ __global__ __launch_bounds__(256) void k_attn_decode_self(const bf16_t* __restri
   // one pass (online softmax per 8-lane key group): K and V of <= 256 keys in flight together, one round trip
   dec_attend_1p<32>(qf, K, V, t + 1, part, gml, outv);
 #else
-  __shared__ float sc[DA_MAXK];
+  // scores of <= DA_SELF_MAXK positions (not DA_MAXK): ~10 KiB of LDS, two workgroups per CU beside an encoder GEMM
+  __shared__ float sc[DA_SELF_MAXK];
   __shared__ float red[8];
   dec_attend(qf, K, V, t + 1, sc, part, red, outv);
 #endif
@@ -620,7 +624,7 @@ __global__ __launch_bounds__(256) void k_attn_decode_self(const bf16_t* __restri
 extern "C" int tw_attn_decode_self(const bf16_t* qkv, int B, int H, int max_pos, const int* pos, bf16_t* k_cache,
                                    bf16_t* v_cache, bf16_t* out, void* stream) {
   TW_REQUIRE(qkv && pos && k_cache && v_cache && out && B > 0 && H > 0, "tw_attn_decode_self: bad args");
-  TW_REQUIRE(max_pos <= DA_MAXK, "tw_attn_decode_self: max_pos %d > %d", max_pos, DA_MAXK);
+  TW_REQUIRE(max_pos <= DA_SELF_MAXK, "tw_attn_decode_self: max_pos %d > %d", max_pos, DA_SELF_MAXK);
   hipLaunchKernelGGL(k_attn_decode_self, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos, pos,
                      k_cache, v_cache, out);
   return tw_check_launch("tw_attn_decode_self");
@@ -670,9 +674,126 @@ __global__ __launch_bounds__(NG * 8) void k_attn_decode_cross(const bf16_t* __re
   }
 }
 
+// k_attn_decode_cross_lean: the one-pass cross-attention with ~1.3 KiB of LDS instead of ~15 KiB. Beside an encoder
+// GEMM workgroup (136 KiB of the CU's 160 KiB) only one ~15 KiB workgroup fits per CU, so the 480 (row, head)
+// workgroups of a decode step took two rounds; these fit several per CU. q comes straight from global memory (each
+// lane its 8 dims), and the 8 key groups of a wave merge their online-softmax states with xor shuffles (lanes of one
+// dim slice: xor 8, 16, 32) before one LDS record per wave; one wave merges the NG/8 records.
+template <int NG, bool NT>
+__global__ __launch_bounds__(NG * 8) void k_attn_decode_cross_lean(const bf16_t* __restrict__ q, int D, int S, int Bt,
+                                                                const int* __restrict__ row_map,
+                                                                const bf16_t* __restrict__ ckv,
+                                                                bf16_t* __restrict__ out) {
+  TW_DEC_PRIO();
+  constexpr int NWV = NG / 8;
+  __shared__ float wpart[NWV][64];
+  __shared__ float wml[NWV][2];
+  const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = tid >> 3, gl = tid & 7;
+  const int slot = row_map ? row_map[b] : b;
+  float qv[8];
+  {
+    const uint4 qr = *(const uint4*)(q + (size_t)b * D + h * 64 + gl * 8);
+    const bf16_t* qe = (const bf16_t*)&qr;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qv[e] = bf16_to_f32(qe[e]);
+  }
+  const bf16_t* K = ckv + (((size_t)0 * Bt + slot) * H + h) * S * 64;
+  const bf16_t* V = ckv + (((size_t)1 * Bt + slot) * H + h) * S * 64;
+  float m = -INFINITY, l = 0.f;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int nit = (S + NG - 1) / NG;
+  for (int it0 = 0; it0 < nit; it0 += DA_UNR) {
+    uint4 kk[DA_UNR], vv[DA_UNR];
+#pragma unroll
+    for (int u = 0; u < DA_UNR; ++u) {
+      const int key = min((it0 + u) * NG + g, S - 1);
+      if constexpr (NT) {
+        typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+        const u32x4_nt a = __builtin_nontemporal_load((const u32x4_nt*)(K + (size_t)key * 64 + gl * 8));
+        const u32x4_nt c = __builtin_nontemporal_load((const u32x4_nt*)(V + (size_t)key * 64 + gl * 8));
+        kk[u] = make_uint4(a.x, a.y, a.z, a.w);
+        vv[u] = make_uint4(c.x, c.y, c.z, c.w);
+      } else {
+        kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
+        vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // all 2 x DA_UNR loads in flight before the first is consumed
+    float sv[DA_UNR];
+    float bm = m;
+#pragma unroll
+    for (int u = 0; u < DA_UNR; ++u) {
+      const bf16_t* ke = (const bf16_t*)&kk[u];
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      sv[u] = (it0 + u) * NG + g < S ? d : -INFINITY;
+      bm = fmaxf(bm, sv[u]);
+    }
+    if (bm == -INFINITY) continue;  // (no key of this group yet: short key ranges only)
+    const float sc = __expf(m - bm);  // 0 on the group's first keys (m = -inf)
+    l *= sc;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= sc;
+#pragma unroll
+    for (int u = 0; u < DA_UNR; ++u) {
+      const float p = __expf(sv[u] - bm);  // 0 for the masked keys
+      l += p;
+      const bf16_t* ve = (const bf16_t*)&vv[u];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += p * bf16_to_f32(ve[e]);
+    }
+    m = bm;
+  }
+  // the wave's 8 key groups -> one state per dim slice (lanes gl, gl + 8, ..., gl + 56)
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) {
+    const float m2 = __shfl_xor(m, o, 64), l2 = __shfl_xor(l, o, 64);
+    const float M = fmaxf(m, m2);
+    const float s1 = m == -INFINITY ? 0.f : __expf(m - M), s2 = m2 == -INFINITY ? 0.f : __expf(m2 - M);
+    l = l * s1 + l2 * s2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = acc[e] * s1 + __shfl_xor(acc[e], o, 64) * s2;
+    m = M;
+  }
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) wpart[wid][lane * 8 + e] = acc[e];
+    if (lane == 0) {
+      wml[wid][0] = m;
+      wml[wid][1] = l;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) M = fmaxf(M, wml[w][0]);
+    float v = 0.f, tot = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+      const float mg = wml[w][0];
+      const float wt = mg == -INFINITY ? 0.f : __expf(mg - M);
+      tot += wt * wml[w][1];
+      v += wt * wpart[w][tid];
+    }
+    out[(size_t)b * D + h * 64 + tid] = f32_to_bf16(v / tot);
+  }
+}
+
 extern "C" int tw_attn_decode_cross(const bf16_t* q, int B, int H, int S, int Bt, const int* row_map,
                                     const bf16_t* cross_kv, bf16_t* out, void* stream) {
   TW_REQUIRE(q && cross_kv && out && B > 0 && H > 0 && S > 0 && S <= DA_MAXK, "tw_attn_decode_cross: bad args");
+  if (tw_dec_cross_lean && tw_dec_cross_1p && tw_dec_cross_ng == 32 && tw_dec_cross_nt == 0) {
+    // (every slot non-temporal: the default; the per-slot nt split of the A/B knob stays on the 15 KiB kernel)
+    hipLaunchKernelGGL((k_attn_decode_cross_lean<32, true>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64,
+                       S, Bt, row_map, cross_kv, out);
+    return tw_check_launch("tw_attn_decode_cross");
+  }
   if (tw_dec_cross_ng == 64 && tw_dec_cross_1p)
     hipLaunchKernelGGL((k_attn_decode_cross<false, 64>), dim3(H, B), dim3(512), 0, (hipStream_t)stream, q, H * 64, S,
                        Bt, row_map, cross_kv, out, XProbs{}, 1, tw_dec_cross_nt);

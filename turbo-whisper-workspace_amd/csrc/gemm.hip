@@ -1306,7 +1306,8 @@ __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __r
                                                                EpiArgs ea) {
   TW_DEC_PRIO();
   constexpr int NW = KW > 4 ? KW : 4, GPB = NW / KW;
-  __shared__ float red[NW][32][17];
+  // (KW = 1: no cross-wave sum, no LDS — see the epilogue)
+  __shared__ float red[KW > 1 ? NW : 1][KW > 1 ? 32 : 1][17];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int gl = wid / KW, kw = wid - gl * KW;
   const int g = blockIdx.x * GPB + gl;
@@ -1360,6 +1361,30 @@ __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __r
     }
   }
   const int cc = lane & 15, rb = (lane >> 4) * 4;
+  auto store = [&](int m, int n, float v) {
+    if constexpr (EPI == TW_EPI_PARTIAL) {
+      ((float*)ea.out)[((size_t)blockIdx.y * M + m) * ea.ldo + n] = v;
+    } else if constexpr (EPI == TW_EPI_GELU_PACKED) {
+      if (ea.bias) v += ea.bias[n];
+      ((bf16_t*)ea.out)[tw_pack_act_idx(m, n)] = f32_to_bf16(gelu_erf(v));
+    } else {
+      epi_store<EPI>(ea, m, n, v);
+    }
+  };
+  if constexpr (KW == 1) {
+    // one wave per column group: its accumulators are the results. Stored straight from registers (16 lanes per
+    // row = 16 consecutive columns), so the kernel holds no LDS: the vocabulary-wide proj_out's 811 workgroups then
+    // co-reside with an encoder GEMM workgroup (136 KiB of the CU's 160 KiB LDS) several per CU, in one round.
+    const int n = g * 16 + cc;
+    if (g < ngroups && n < N) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (rb + r < M) store(rb + r, n, c0[r]);
+        if (TWO && 16 + rb + r < M) store(16 + rb + r, n, c1[r]);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     red[wid][rb + r][cc] = c0[r];
@@ -1375,14 +1400,7 @@ __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __r
       float v = 0.f;
 #pragma unroll
       for (int w = 0; w < KW; ++w) v += red[gg * KW + w][m][c];
-      if constexpr (EPI == TW_EPI_PARTIAL) {
-        ((float*)ea.out)[((size_t)blockIdx.y * M + m) * ea.ldo + n] = v;
-      } else if constexpr (EPI == TW_EPI_GELU_PACKED) {
-        if (ea.bias) v += ea.bias[n];
-        ((bf16_t*)ea.out)[tw_pack_act_idx(m, n)] = f32_to_bf16(gelu_erf(v));
-      } else {
-        epi_store<EPI>(ea, m, n, v);
-      }
+      store(m, n, v);
     }
   }
 }
