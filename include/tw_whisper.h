@@ -221,11 +221,18 @@ int tw_kv_reorder(uint16_t* k_cache, uint16_t* v_cache, uint16_t* k_scratch, uin
  * activation rows M..31 are never written (keep them finite, e.g. zeroed once).
  * tw_pack_weight: W bf16[N][ldw] -> Wp packed weight (setup time).
  * tw_gemv_packed: out = epi(A . W^T); A packed activation (a_packed = 1) or row-major [M][lda]; epi TW_EPI_BF16,
- *   TW_EPI_F32 (row-major [M][ldo]), TW_EPI_GELU_PACKED (packed activation, N % 32 == 0) or TW_EPI_PARTIAL_F32
- *   (splits > 1 allowed; bias ignored). */
+ *   TW_EPI_F32 (row-major [M][ldo]), TW_EPI_GELU_PACKED (packed activation, N % 32 == 0), TW_EPI_RESID_F32
+ *   (f32 [M][ldo] += A.W^T + bias: the decoder's residual update; splits = 1) or TW_EPI_PARTIAL_F32 (splits > 1
+ *   allowed; bias ignored).
+ * tw_gemv_packed_ln: the same with the A operand = LayerNorm(x) (nn.LayerNorm over K, eps; gamma/beta f32[K]) of the
+ *   f32 residual rows x[M][K], computed inside the kernel (the decoder's pre-LayerNorms fused into the projection
+ *   that consumes them, modeling_whisper.py:434,443,446); epi TW_EPI_BF16, TW_EPI_F32 or TW_EPI_GELU_PACKED;
+ *   K <= 2048. */
 int tw_pack_weight(const uint16_t* W, int N, int K, int ldw, uint16_t* Wp, void* stream);
 int tw_gemv_packed(const uint16_t* A, int a_packed, int lda, const uint16_t* Wp, int M, int N, int K, int epi,
                    void* out, int ldo, const float* bias, int splits, void* stream);
+int tw_gemv_packed_ln(const float* x, const float* gamma, const float* beta, float eps, const uint16_t* Wp, int M,
+                      int N, int K, int epi, void* out, int ldo, const float* bias, void* stream);
 /* tw_resid_layernorm with the normalised rows written as a packed activation (M <= 32, D % 32 == 0). */
 int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
                               const float* beta, int M, int D, float eps, uint16_t* out, void* stream);

@@ -84,6 +84,11 @@ def main():
         _lib.call("tw_gemm_set_variant", a.variant)
     _lib.call("tw_attn_set_variant", 8 | (a.attn_pad << 20))
 
+    nb = None
+    if a.variant in (103, 104):
+        import ctypes
+        nb = ctypes.CDLL(os.path.join(ROOT, "scripts", "exp", "libneighbors.so"))
+    nbout = torch.zeros(4096, device=dev)
     qkv_enc = rnd(M, 3 * D, sc=1.0)
     att_enc = torch.empty(M, D, dtype=bf, device=dev)
     xe = torch.randn(M, D, device=dev)
@@ -99,6 +104,11 @@ def main():
             elif a.variant == 102:  # encoder LayerNorm
                 _lib.call("tw_layernorm", xe.data_ptr(), g.data_ptr(), bb.data_ptr(), M, D, 1e-5, hln.data_ptr(),
                           sE.cuda_stream)
+            elif a.variant == 103:  # synthetic: MFMAs only, one 136 KiB workgroup per CU (scripts/exp/neighbors.hip)
+                nb.nb_mfma_spin(ctypes.c_void_p(nbout.data_ptr()), 2048, 20000, ctypes.c_void_p(sE.cuda_stream))
+            elif a.variant == 104:  # synthetic: LDS-DMA HBM streaming only, same occupancy
+                nb.nb_mem_stream(ctypes.c_void_p(A.data_ptr()), ctypes.c_size_t(A.numel() * 2),
+                                 ctypes.c_void_p(nbout.data_ptr()), 2048, 64, ctypes.c_void_p(sE.cuda_stream))
             else:
                 _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, K, K, a.epi, out.data_ptr(), N,
                           bias.data_ptr(), None, 0, None, sE.cuda_stream)

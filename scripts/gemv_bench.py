@@ -70,6 +70,27 @@ def main():
                 us = graph_time(fn, a.n)
                 print(f"serial_tail={serial} kw={kw} {name:28s} {us:8.2f} us  {byts / us / 1e3:8.1f} GB/s", flush=True)
     _lib.call("tw_gemm_set_variant", 1)
+    # the LayerNorm-fused consumers and the residual-epilogue producers (engine.ln_fused)
+    xf = rnd(B, F, dt=torch.float32, sc=1.0)
+    gF, bF = torch.ones(F, device=dev), torch.zeros(F, device=dev)
+
+    def gemv_ln(Wp, N, K, epi, out, ldo):
+        return lambda s: _lib.call("tw_gemv_packed_ln", x.data_ptr(), g.data_ptr(), bb.data_ptr(), 1e-5, Wp.data_ptr(),
+                                   B, N, K, epi, out.data_ptr(), ldo, bias.data_ptr(), s)
+
+    RES = _lib.TW_EPI_RESID_F32
+    fused = [
+        ("LN+qkv   N=3840 K=1280", gemv_ln(Wqkv, 3 * D, D, E_BF16, out_bf, 3 * D)),
+        ("LN+q_x   N=1280 K=1280", gemv_ln(Wd, D, D, E_BF16, out_bf, D)),
+        ("LN+fc1   N=5120 K=1280", gemv_ln(W1, F, D, E_GELUP, fp, F)),
+        ("o resid  N=1280 K=1280", gemv(att, 0, Wd, D, D, RES, xf, D, bias)),
+        ("fc2 resid N=1280 K=5120", gemv(fp, 1, W2, D, F, RES, xf, D, bias)),
+    ]
+    for kw in [int(k) for k in a.kws.split(",")]:
+        _lib.call("tw_gemm_set_variant", 1 | (kw << 16))
+        for name, fn in fused:
+            print(f"fused kw={kw} {name:28s} {graph_time(fn, a.n):8.2f} us", flush=True)
+    _lib.call("tw_gemm_set_variant", 1)
     for nparts in (0, 4):
         us = graph_time(lambda s: _lib.call("tw_resid_layernorm_packed", x.data_ptr(), parts.data_ptr(), nparts,
                                             bb.data_ptr(), g.data_ptr(), bb.data_ptr(), B, D, 1e-5, hp.data_ptr(), s),

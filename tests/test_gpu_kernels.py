@@ -410,6 +410,57 @@ def test_gemv_packed_vs_torch(M, N, K, epi, splits, a_packed):
     torch.testing.assert_close(out.float(), ref + bias, atol=tol, rtol=tol)
 
 
+@pytest.mark.parametrize("kw", [0, 1, 2, 4, 8])
+@pytest.mark.parametrize("M,N,K,epi", [(24, 3840, 1280, _lib.TW_EPI_BF16), (24, 1280, 1280, _lib.TW_EPI_BF16),
+                                       (24, 5120, 1280, _lib.TW_EPI_GELU_PACKED), (7, 51866, 1280, _lib.TW_EPI_F32),
+                                       (13, 1536, 384, _lib.TW_EPI_GELU_PACKED), (32, 640, 2048, _lib.TW_EPI_BF16)])
+def test_gemv_packed_ln_vs_torch(M, N, K, epi, kw):
+    """tw_gemv_packed_ln: epi(LayerNorm(x) . W^T + bias) with the LayerNorm computed inside the GEMV, vs torch fp32 LN
+    (rounded to bf16, as the separate LayerNorm launch hands it to the GEMV) then fp32 matmul. Every K-slice count."""
+    g = torch.Generator(device="cpu").manual_seed(N + K + M)
+    x = (torch.randn(M, K, generator=g) * 3 + torch.randn(1, K, generator=g) * 0.5).to(DEV)  # offset rows
+    gamma = (1 + 0.2 * torch.randn(K, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(K, generator=g)).to(DEV)
+    W = rand_bf16(N, K, scale=K ** -0.5, seed=43)
+    bias = torch.randn(N, device=DEV) * 0.1
+    Wp = pack_w(W)
+    h = bf(torch.nn.functional.layer_norm(x, (K,), gamma, beta, 1e-5))
+    ref = h.float() @ W.float().t() + bias
+    _lib.call("tw_gemm_set_variant", 1 | (kw << 16))
+    try:
+        if epi == _lib.TW_EPI_GELU_PACKED:
+            out = torch.zeros(N * 32, dtype=torch.bfloat16, device=DEV)
+            _lib.call("tw_gemv_packed_ln", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 1e-5, Wp.data_ptr(), M, N,
+                      K, epi, out.data_ptr(), 0, bias.data_ptr(), S())
+            got, want = unpack_act(out, M, N).float(), torch.nn.functional.gelu(ref)
+        else:
+            dt = torch.bfloat16 if epi == _lib.TW_EPI_BF16 else torch.float32
+            out = torch.full((M, N), float("nan"), dtype=dt, device=DEV)
+            _lib.call("tw_gemv_packed_ln", x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 1e-5, Wp.data_ptr(), M, N,
+                      K, epi, out.data_ptr(), N, bias.data_ptr(), S())
+            got, want = out.float(), ref
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("tw_gemm_set_variant", 1)
+    tol = 2e-3 if epi == _lib.TW_EPI_F32 else 2e-2
+    # bf16 rounding of the normalised operand may differ by one ulp from torch's on a few elements: sum of K terms
+    torch.testing.assert_close(got, want, atol=tol + 2e-2 * (epi == _lib.TW_EPI_F32), rtol=tol)
+
+
+@pytest.mark.parametrize("M,N,K,a_packed", [(24, 1280, 1280, 0), (24, 1280, 5120, 1), (5, 384, 1536, 1)])
+def test_gemv_packed_resid_epilogue(M, N, K, a_packed):
+    """TW_EPI_RESID_F32 on the packed GEMV: x += A.W^T + bias in place (the decoder's residual update)."""
+    A = rand_bf16(M, K, seed=51)
+    W = rand_bf16(N, K, scale=K ** -0.5, seed=52)
+    bias = torch.randn(N, device=DEV) * 0.1
+    x = torch.randn(M, N, device=DEV)
+    want = x + A.float() @ W.float().t() + bias
+    Ain = pack_act(A) if a_packed else A
+    _lib.call("tw_gemv_packed", Ain.data_ptr(), a_packed, K, pack_w(W).data_ptr(), M, N, K, _lib.TW_EPI_RESID_F32,
+              x.data_ptr(), N, bias.data_ptr(), 1, S())
+    torch.testing.assert_close(x, want, atol=2e-3, rtol=2e-3)
+
+
 @pytest.mark.parametrize("M,D,nparts", [(24, 1280, 4), (5, 384, 0), (17, 256, 2)])
 @pytest.mark.parametrize("lnv", [0, 1], ids=["wave", "block"])
 def test_resid_layernorm_packed_vs_torch(M, D, nparts, lnv):

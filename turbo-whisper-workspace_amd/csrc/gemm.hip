@@ -1298,16 +1298,30 @@ __global__ __launch_bounds__(256) void k_pack_weight(const bf16_t* __restrict__ 
   *(uint4*)(Wp + c * 8) = v;
 }
 
+// ALN (tw_gemv_packed_ln): the A operand is LayerNorm(x) of the f32 residual stream x [M][K] (row-major), computed
+// inside the GEMV instead of by a separate decoder LayerNorm launch: the prologue computes every row's mean and
+// 1/std (two-pass, as k_resid_ln_w, one wave per row in turn) into LDS, and each A fragment is normalised from x,
+// gamma and beta as it is loaded. The residual stream is then updated in place by the producing GEMVs' RESID
+// epilogue (x += A.W^T + bias, no split-K partials), so a decoder layer is 8 launches instead of 11.
+struct LnArgs {
+  const float* x;
+  const float* g;
+  const float* b;
+  float eps;
+};
+#define GEMV_LN_MAXV 8  // float4 chunks per lane of one row in the LN prologue: K <= 2048
+
 // NTW: weight fragments read with non-temporal loads (proj_out: 133 MB streamed once per step, kept out of the
 // caches so that the layer weights can stay in them).
-template <int EPI, int KW, int U, bool APACK, bool TWO, bool NTW = false>
+template <int EPI, int KW, int U, bool APACK, bool TWO, bool NTW = false, bool ALN = false>
 __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __restrict__ A, int lda,
                                                                const bf16_t* __restrict__ Wp, int M, int N, int K,
-                                                               EpiArgs ea) {
+                                                               EpiArgs ea, LnArgs la = LnArgs{}) {
   TW_DEC_PRIO();
   constexpr int NW = KW > 4 ? KW : 4, GPB = NW / KW;
   // (KW = 1: no cross-wave sum, no LDS — see the epilogue)
   __shared__ float red[KW > 1 ? NW : 1][KW > 1 ? 32 : 1][17];
+  __shared__ float lnst[ALN ? 32 : 1][2];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int gl = wid / KW, kw = wid - gl * KW;
   const int g = blockIdx.x * GPB + gl;
@@ -1315,6 +1329,36 @@ __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __r
   const int nsl = KW * gridDim.y, sl = blockIdx.y * KW + kw;
   const int s0 = (int)((long)sl * ns / nsl), s1 = (int)((long)(sl + 1) * ns / nsl);
   f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+  if constexpr (ALN) {
+    const int nc = K >> 2;
+    for (int r = wid; r < M; r += NW) {
+      const float4* xr = (const float4*)(la.x + (size_t)r * K);
+      float4 v[GEMV_LN_MAXV];
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < GEMV_LN_MAXV; ++i) {
+        if (64 * i < nc) {  // wave-uniform bound; the chunk index is clamped, not branched on
+          v[i] = xr[min(lane + 64 * i, nc - 1)];
+          if (lane + 64 * i < nc) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+        }
+      }
+      const float mean = wave_sum(s) / (float)K;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < GEMV_LN_MAXV; ++i) {
+        if (64 * i < nc && lane + 64 * i < nc) {
+          const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+          q += (a * a + b * b) + (c * c + d * d);
+        }
+      }
+      const float rstd = rsqrtf(wave_sum(q) / (float)K + la.eps);
+      if (lane == 0) {
+        lnst[r][0] = mean;
+        lnst[r][1] = rstd;
+      }
+    }
+    __syncthreads();
+  }
   if (g < ngroups) {
     const bf16_t* wp = Wp + (size_t)g * ns * 512 + lane * 8;
     const bf16_t* ap;
@@ -1325,10 +1369,32 @@ __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __r
       ap = A + (size_t)min(lane & 15, M - 1) * lda + 8 * (lane >> 4);
       ap1 = A + (size_t)min(16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4);
     }
+    // ALN: fragment (m-tile t, step st) of LayerNorm(x): lane = row 16t + (lane & 15), k = 32st + 8(lane >> 4) + j
+    auto ldA_ln = [&](int st, int t) -> bf16x8 {
+      const int m = min(16 * t + (lane & 15), M - 1);
+      const int k = 32 * st + 8 * (lane >> 4);
+      const float* xp = la.x + (size_t)m * K + k;
+      const float4 x0 = *(const float4*)xp, x1 = *(const float4*)(xp + 4);
+      const float4 g0 = *(const float4*)(la.g + k), g1 = *(const float4*)(la.g + k + 4);
+      const float4 b0 = *(const float4*)(la.b + k), b1 = *(const float4*)(la.b + k + 4);
+      const float mean = lnst[m][0], rstd = lnst[m][1];
+      bf16x8 r;
+      r[0] = (__bf16)((x0.x - mean) * rstd * g0.x + b0.x);
+      r[1] = (__bf16)((x0.y - mean) * rstd * g0.y + b0.y);
+      r[2] = (__bf16)((x0.z - mean) * rstd * g0.z + b0.z);
+      r[3] = (__bf16)((x0.w - mean) * rstd * g0.w + b0.w);
+      r[4] = (__bf16)((x1.x - mean) * rstd * g1.x + b1.x);
+      r[5] = (__bf16)((x1.y - mean) * rstd * g1.y + b1.y);
+      r[6] = (__bf16)((x1.z - mean) * rstd * g1.z + b1.z);
+      r[7] = (__bf16)((x1.w - mean) * rstd * g1.w + b1.w);
+      return r;
+    };
     auto ldA0 = [&](int st) -> bf16x8 {
+      if constexpr (ALN) return ldA_ln(st, 0);
       return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024) : *(const bf16x8*)(ap + 32 * st);
     };
     auto ldA1 = [&](int st) -> bf16x8 {
+      if constexpr (ALN) return ldA_ln(st, 1);
       return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024 + 512) : *(const bf16x8*)(ap1 + 32 * st);
     };
     // Batches of U steps with every load in flight before the MFMAs, then the remainder step by step (measured,
@@ -1411,9 +1477,38 @@ static void launch_gemv_p3(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
   constexpr int NW = KW > 4 ? KW : 4, GPB = NW / KW;
   dim3 grid(tw_cdiv(tw_cdiv(N, 16), GPB), splits);
   if (M > 16)
-    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, true, NTW>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea);
+    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, true, NTW>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea,
+                       LnArgs{});
   else
-    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, false, NTW>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea);
+    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, false, NTW>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea,
+                       LnArgs{});
+}
+
+// LayerNorm-fused GEMV (ALN): fewer steps per batch (U = 4: a step's A fragments are 4 x 16-byte x loads + gamma /
+// beta instead of one 16-byte packed load) and the launcher's K-slice heuristic
+template <int EPI, int KW>
+static void launch_gemv_ln3(const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea, const LnArgs& la, hipStream_t s) {
+  constexpr int NW = KW > 4 ? KW : 4, GPB = NW / KW;
+  dim3 grid(tw_cdiv(tw_cdiv(N, 16), GPB), 1);
+  if (M > 16)
+    hipLaunchKernelGGL((k_gemv_p<EPI, KW, 4, true, true, false, true>), grid, dim3(NW * 64), 0, s, nullptr, 0, Wp, M, N,
+                       K, ea, la);
+  else
+    hipLaunchKernelGGL((k_gemv_p<EPI, KW, 4, true, false, false, true>), grid, dim3(NW * 64), 0, s, nullptr, 0, Wp, M,
+                       N, K, ea, la);
+}
+
+template <int EPI>
+static void launch_gemv_ln(const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea, const LnArgs& la, hipStream_t s) {
+  const long groups = tw_cdiv(N, 16);
+  const int steps = K / 32;
+  int kw = 1;
+  while (groups * kw < 1024 && kw < 8 && steps >= 8 * kw) kw *= 2;
+  if (tw_tune_gemv_kw) kw = tw_tune_gemv_kw;
+  if (kw == 1) launch_gemv_ln3<EPI, 1>(Wp, M, N, K, ea, la, s);
+  else if (kw == 2) launch_gemv_ln3<EPI, 2>(Wp, M, N, K, ea, la, s);
+  else if (kw == 4) launch_gemv_ln3<EPI, 4>(Wp, M, N, K, ea, la, s);
+  else launch_gemv_ln3<EPI, 8>(Wp, M, N, K, ea, la, s);
 }
 
 
@@ -1555,9 +1650,33 @@ extern "C" int tw_gemv_packed(const bf16_t* A, int a_packed, int lda, const bf16
       ea.bias = nullptr;
       launch_gemv_p<TW_EPI_PARTIAL>(A, a_packed, lda, Wp, M, N, K, ea, splits, s);
       break;
+    case TW_EPI_RESID_F32:  // out[m][n] += A.W^T + bias: the decoder's residual update, one writer per element
+      TW_REQUIRE(ldo >= N, "tw_gemv_packed: ldo=%d < N", ldo);
+      launch_gemv_p<TW_EPI_RESID_F32>(A, a_packed, lda, Wp, M, N, K, ea, splits, s);
+      break;
     default: tw_set_error("tw_gemv_packed: unsupported epilogue %d", epi); return TW_ERR_ARG;
   }
   return tw_check_launch("tw_gemv_packed");
+}
+
+extern "C" int tw_gemv_packed_ln(const float* x, const float* gamma, const float* beta, float eps, const bf16_t* Wp,
+                                 int M, int N, int K, int epi, void* out, int ldo, const float* bias, void* stream) {
+  TW_REQUIRE(x && gamma && beta && Wp && out, "tw_gemv_packed_ln: null pointer");
+  TW_REQUIRE(M > 0 && M <= 32 && N > 0 && K > 0 && K % 32 == 0 && K <= 256 * GEMV_LN_MAXV,
+             "tw_gemv_packed_ln: M=%d N=%d K=%d (M <= 32, K %% 32, K <= %d)", M, N, K, 256 * GEMV_LN_MAXV);
+  EpiArgs ea{out, ldo, bias, nullptr, 0, 0, 0, 0, 0};
+  const LnArgs la{x, gamma, beta, eps};
+  hipStream_t s = (hipStream_t)stream;
+  switch (epi) {
+    case TW_EPI_BF16: launch_gemv_ln<TW_EPI_BF16>(Wp, M, N, K, ea, la, s); break;
+    case TW_EPI_F32: launch_gemv_ln<TW_EPI_F32>(Wp, M, N, K, ea, la, s); break;
+    case TW_EPI_GELU_PACKED:
+      TW_REQUIRE(N % 32 == 0, "tw_gemv_packed_ln: GELU_PACKED needs N %% 32 (it is the next GEMV's K)");
+      launch_gemv_ln<TW_EPI_GELU_PACKED>(Wp, M, N, K, ea, la, s);
+      break;
+    default: tw_set_error("tw_gemv_packed_ln: unsupported epilogue %d", epi); return TW_ERR_ARG;
+  }
+  return tw_check_launch("tw_gemv_packed_ln");
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -148,6 +148,19 @@ __device__ inline float f32_from_order_key(uint32_t k) {
     if (TW_DEC_PRIORITY) __builtin_amdgcn_s_setprio(TW_DEC_PRIORITY); \
   } while (0)
 
+// Register cap of the decoder kernels (VGPRs per wave; 0 = the compiler's choice). A decoder wave can only start on a
+// SIMD whose register file has room beside the encoder workgroup running there: k_gemm_big (184 VGPRs x 2 waves)
+// leaves 128 of 512, k_gemm_8p (211 x 2) 80, the encoder attention at one workgroup per CU 272. Decoder kernels
+// that need more wait for an encoder tile to retire (scripts/exp/interference.py: 2-9x slower launches).
+#ifndef TW_DEC_VGPR
+#define TW_DEC_VGPR 0
+#endif
+#if TW_DEC_VGPR
+#define TW_DEC_REGS __attribute__((amdgpu_num_vgpr(TW_DEC_VGPR)))
+#else
+#define TW_DEC_REGS
+#endif
+
 // Decoder fragment layouts (include/tw_whisper.h "packed" formats), M <= 32 activation rows:
 //   activation [K/32][2][64][8] bf16: element (m, k) at ((k/32 * 2 + m/16) * 64 + (m%16) + 16*((k/8)%4)) * 8 + k%8,
 //     i.e. step s = k/32, m-tile t = m/16 is the 16x32 A fragment of v_mfma_f32_16x16x32_bf16 (1 KiB contiguous)

@@ -274,6 +274,11 @@ class WhisperEngine:
         # wave-load of the per-token GEMVs is one contiguous 1 KiB fragment. TW_DEC_PACKED=0 keeps the row-major
         # skinny GEMM path (A/B measurement).
         self.packed_decoder = os.environ.get("TW_DEC_PACKED", "1") != "0"
+        # TW_DEC_LNFUSE=1: decoder pre-LayerNorms fused into the consuming GEMVs, residual adds into the producing ones
+        # (8 launches per layer instead of 11). Measured and NOT the default: every column group of the consuming GEMV
+        # re-normalises the whole operand (LN+q/k/v 12.5 us vs 3.3 + 4.3 us as two launches; bench step 120.4 vs
+        # 102.7 ms)
+        self.ln_fused = self.packed_decoder and os.environ.get("TW_DEC_LNFUSE", "0") == "1"
         self.dec_p: List[Dict[str, torch.Tensor]] = []
         self.emb_p: Optional[torch.Tensor] = None
         if self.packed_decoder:
@@ -315,8 +320,21 @@ class WhisperEngine:
                   ldo if ldo is not None else N, _lib.ptr(bias), splits, v.stream.cuda_stream)
         self._end_timer(rec, v.stream)
 
+    def _gemv_ln(self, g, b, Wp, M, N, K, epi, out, v: DecView, bias=None, ldo=None):
+        """out = epi(LayerNorm(xd) . W^T + bias): the pre-LayerNorm computed inside the GEMV (tw_gemv_packed_ln)."""
+        rec = self._begin_timer(("gemv_packed", epi), 2.0 * M * N * K, v.stream)
+        _lib.call("tw_gemv_packed_ln", v.xd.data_ptr(), g.data_ptr(), b.data_ptr(), LN_EPS, Wp.data_ptr(), M, N, K,
+                  epi, out.data_ptr(), ldo if ldo is not None else N, _lib.ptr(bias), v.stream.cuda_stream)
+        self._end_timer(rec, v.stream)
+
+    # timing-only ablations (scripts/exp: upper bounds of a fusion before building it; outputs are WRONG): a
+    # comma list of decoder stages whose launches are skipped, e.g. TW_ABLATE=ln. Never set in the product.
+    _ablate = frozenset(x for x in os.environ.get("TW_ABLATE", "").split(",") if x)
+
     def _resid_ln_p(self, R, nparts, bias, g, b, v: DecView):
         """xd += bias + sum(parts[:nparts]); hp = LayerNorm(xd) as a packed activation."""
+        if "ln" in self._ablate:
+            return
         _lib.call("tw_resid_layernorm_packed", v.xd.data_ptr(), v.parts.data_ptr() if nparts else None, nparts,
                   _lib.ptr(bias), _lib.ptr(g), _lib.ptr(b), R, self.d.d_model, LN_EPS, v.hp.data_ptr(),
                   v.stream.cuda_stream)
@@ -497,16 +515,23 @@ class WhisperEngine:
         yield
         if self.enc_fp8:
             yield from self._encode_layers_mx(R, st)
+        ab = self._ablate
         for L in ([] if self.enc_fp8 else w.enc):
-            self._ln(self.x, L.ln1_g, L.ln1_b, M15, self.hln, stream=st)
-            self._gemm(self.hln, L.wqkv, M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv, stream=st)
+            if "eln" not in ab:
+                self._ln(self.x, L.ln1_g, L.ln1_b, M15, self.hln, stream=st)
+            if "egemm" not in ab:
+                self._gemm(self.hln, L.wqkv, M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv, stream=st)
             rec = self._begin_timer(("attn_encoder", 0), 4.0 * S_ENC * S_ENC * 64 * H * R, st)
-            _lib.call("tw_attn_encoder", self.qkv.data_ptr(), R, S_ENC, H, self.att.data_ptr(), s)
+            if "eattn" not in ab:
+                _lib.call("tw_attn_encoder", self.qkv.data_ptr(), R, S_ENC, H, self.att.data_ptr(), s)
             self._end_timer(rec, st)
-            self._gemm(self.att, L.wo, M15, D, D, _lib.TW_EPI_RESID_F32, self.x, bias=L.bo, stream=st)
-            self._ln(self.x, L.ln2_g, L.ln2_b, M15, self.hln, stream=st)
-            self._gemm(self.hln, L.w1, M15, F, D, _lib.TW_EPI_GELU_BF16, self.ffn, bias=L.b1, stream=st)
-            self._gemm(self.ffn, L.w2, M15, D, F, _lib.TW_EPI_RESID_F32, self.x, bias=L.b2, stream=st)
+            if "egemm" not in ab:
+                self._gemm(self.att, L.wo, M15, D, D, _lib.TW_EPI_RESID_F32, self.x, bias=L.bo, stream=st)
+            if "eln" not in ab:
+                self._ln(self.x, L.ln2_g, L.ln2_b, M15, self.hln, stream=st)
+            if "egemm" not in ab:
+                self._gemm(self.hln, L.w1, M15, F, D, _lib.TW_EPI_GELU_BF16, self.ffn, bias=L.b1, stream=st)
+                self._gemm(self.ffn, L.w2, M15, D, F, _lib.TW_EPI_RESID_F32, self.x, bias=L.b2, stream=st)
             yield
         self._ln(self.x, w.enc_ln_g, w.enc_ln_b, M15, self.hln, stream=st)  # encoder last_hidden_state (bf16)
         geom = (ctypes.c_int * 4)(S_ENC, R, D, H)
@@ -620,6 +645,8 @@ class WhisperEngine:
             _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), v.ids.data_ptr(), v.pos.data_ptr(), R,
                       D, v.xd.data_ptr(), s)
         xkv_stride = 2 * r_enc * H * S_ENC * 64
+        if self.ln_fused:
+            return self._decoder_layers_lnfused(R, with_logits, v, r_enc, xkv_stride)
         nparts, pbias = 0, None
         PART, K4 = _lib.TW_EPI_PARTIAL_F32, DEC_SPLITS
         for li, L in enumerate(w.dec):
@@ -627,14 +654,16 @@ class WhisperEngine:
             if li or not pre_embedded:
                 self._resid_ln_p(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
             self._gemv(v.hp, True, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
-            _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
-                      self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
+            if "self" not in self._ablate:
+                _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
+                          self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
             self._gemv(v.attd, False, P["wo"], R, D, D, PART, v.parts, v, splits=K4)
             self._resid_ln_p(R, K4, L.bo, L.ln2_g, L.ln2_b, v)
             self._gemv(v.hp, True, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
             ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
             rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
-            self._cross_attend(li, R, r_enc, rmap, ckv, v)
+            if "cross" not in self._ablate:
+                self._cross_attend(li, R, r_enc, rmap, ckv, v)
             self._end_timer(rec, st)
             self._gemv(v.attd, False, P["wo_x"], R, D, D, PART, v.parts, v, splits=K4)
             self._resid_ln_p(R, K4, L.bo_x, L.ln3_g, L.ln3_b, v)
@@ -643,6 +672,36 @@ class WhisperEngine:
             nparts, pbias = K4, L.b2
         if with_logits:
             self._resid_ln_p(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
+            self._gemv(v.hp, True, self.emb_p, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, v)
+
+    def _decoder_layers_lnfused(self, R: int, with_logits: bool, v: DecView, r_enc: int, xkv_stride: int) -> None:
+        """The decoder layers with every pre-LayerNorm inside the projection that consumes it (tw_gemv_packed_ln:
+        self_attn_layer_norm -> q/k/v, encoder_attn_layer_norm -> cross q, final_layer_norm -> fc1) and every
+        residual add in the epilogue of the projection that produces it (out_proj, cross out_proj, fc2:
+        TW_EPI_RESID_F32 into xd, no split-K partials): 8 launches per layer instead of 11
+        (WhisperDecoderLayer.forward, $TF/models/whisper/modeling_whisper.py:468-505)."""
+        d, w = self.d, self.w
+        D, F, H, T = d.d_model, d.ffn, d.heads, d.max_target_positions
+        s = v.stream.cuda_stream
+        RES = _lib.TW_EPI_RESID_F32
+        for li, L in enumerate(w.dec):
+            P = self.dec_p[li]
+            self._gemv_ln(L.ln1_g, L.ln1_b, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
+            if "self" not in self._ablate:
+                _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
+                          self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
+            self._gemv(v.attd, False, P["wo"], R, D, D, RES, v.xd, v, bias=L.bo)
+            self._gemv_ln(L.ln2_g, L.ln2_b, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
+            ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
+            rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, v.stream)
+            if "cross" not in self._ablate:
+                self._cross_attend(li, R, r_enc, rmap, ckv, v)
+            self._end_timer(rec, v.stream)
+            self._gemv(v.attd, False, P["wo_x"], R, D, D, RES, v.xd, v, bias=L.bo_x)
+            self._gemv_ln(L.ln3_g, L.ln3_b, P["w1"], R, F, D, _lib.TW_EPI_GELU_PACKED, v.fp, v, bias=L.b1)
+            self._gemv(v.fp, True, P["w2"], R, D, F, RES, v.xd, v, bias=L.b2)
+        if with_logits:
+            self._resid_ln_p(R, 0, None, w.dec_ln_g, w.dec_ln_b, v)
             self._gemv(v.hp, True, self.emb_p, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, v)
 
     def _cross_attend(self, li: int, R: int, r_enc: int, rmap, ckv, v: DecView) -> None:
