@@ -145,6 +145,10 @@ int tw_gemm_mx_set_variant(int v);
  * the default: 8 for N >= 2560, else 1; 1 = row-major: one A row panel against every W column panel in turn).
  * Applies to tw_gemm_bf16 and tw_gemm_mx. */
 int tw_gemm_set_group(int group_m);
+/* Measurement knob (process-wide, returns 0): the largest K-slice count (waves per column group) the packed decoder
+ * GEMV picks, 1/2/4/8 (default 8; 4 keeps its workgroups at <= 256 threads, co-resident with an encoder GEMM
+ * workgroup). */
+int tw_gemv_set_max_kw(int kw);
 /* bf16 src[rows][ld] -> MX fp8 dst[rows][K] + scales (K % 128 == 0). Encoder weights once at load; the
  * attention output before out_proj (modeling_whisper.py:350-356). */
 int tw_quant_mx(const uint16_t* src, int rows, int K, int ld, uint8_t* dst, uint8_t* scales, int rows_pad,
@@ -233,6 +237,16 @@ int tw_gemv_packed(const uint16_t* A, int a_packed, int lda, const uint16_t* Wp,
                    void* out, int ldo, const float* bias, int splits, void* stream);
 int tw_gemv_packed_ln(const float* x, const float* gamma, const float* beta, float eps, const uint16_t* Wp, int M,
                       int N, int K, int epi, void* out, int ldo, const float* bias, void* stream);
+/* The decoder's LayerNorm across a kernel boundary (no launch of its own): tw_gemv_packed_stats is
+ *   tw_gemv_packed(.., TW_EPI_RESID_F32, splits = 1) into x[M][ldx] (N % 16 == 0) that also writes, for every
+ *   16-column group g of the updated rows, stats[(g*32 + m)*2 + {0, 1}] = (mean, sum of squared deviations from that
+ *   mean) of x[m][16g .. 16g+15]; tw_gemv_packed_lnst is tw_gemv_packed_ln whose row mean / variance come from those
+ *   K/16 group statistics (combined pairwise, Chan et al.) instead of a pass over x. stats: f32[N/16][32][2]. */
+int tw_gemv_packed_stats(const uint16_t* A, int a_packed, int lda, const uint16_t* Wp, int M, int N, int K, float* x,
+                         int ldx, const float* bias, float* stats, void* stream);
+int tw_gemv_packed_lnst(const float* x, const float* stats, const float* gamma, const float* beta, float eps,
+                        const uint16_t* Wp, int M, int N, int K, int epi, void* out, int ldo, const float* bias,
+                        void* stream);
 /* tw_resid_layernorm with the normalised rows written as a packed activation (M <= 32, D % 32 == 0). */
 int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
                               const float* beta, int M, int D, float eps, uint16_t* out, void* stream);

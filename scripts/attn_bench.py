@@ -17,10 +17,10 @@ qkv[:, :D] = (qkv[:, :D].float() * 0.125).to(torch.bfloat16)
 out = torch.empty(B * S, D, dtype=torch.bfloat16, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
 fl = 4.0 * S * S * 64 * H * B
-res = {v: [] for v in (0, 4, 8, 9)}
+res = {v: [] for v in (8, 10, 11)}
 outs = {}
 for r in range(5):
-    for v in (0, 4, 8, 9):
+    for v in (8, 10, 11):
         _lib.call("tw_attn_set_variant", v)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
@@ -32,6 +32,6 @@ for r in range(5):
         if r == 0:
             outs[v] = out.float().clone()
 for v, t in res.items():
-    print(f"variant {v}: min {min(t):.3f} ms = {fl / min(t) / 1e9:.0f} TF/s  max|diff vs v0| = "
-          f"{(outs[v] - outs[0]).abs().max().item():.3g}")
+    print(f"variant {v}: min {min(t):.3f} ms = {fl / min(t) / 1e9:.0f} TF/s  max|diff vs v8| = "
+          f"{(outs[v] - outs[8]).abs().max().item():.3g}")
 _lib.call("tw_attn_set_variant", 8)

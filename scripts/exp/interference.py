@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--n", type=int, default=40)
     ap.add_argument("--gemms", type=int, default=60)
     ap.add_argument("--attn-pad", type=int, default=0)  # encoder attention LDS padding, 16 KiB units
+    ap.add_argument("--kw", type=int, default=0)  # force the packed GEMV's K-slices per column group (0: heuristic)
     a = ap.parse_args()
     _lib.load()
     dev = "cuda"
@@ -80,8 +81,7 @@ def main():
     }
     sE = torch.cuda.Stream(priority=0)
     sD = torch.cuda.Stream(priority=-1)
-    if a.variant < 100:
-        _lib.call("tw_gemm_set_variant", a.variant)
+    _lib.call("tw_gemm_set_variant", (a.variant if a.variant < 100 else 1) | (a.kw << 16))
     _lib.call("tw_attn_set_variant", 8 | (a.attn_pad << 20))
 
     nb = None

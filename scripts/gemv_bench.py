@@ -79,7 +79,20 @@ def main():
                                    B, N, K, epi, out.data_ptr(), ldo, bias.data_ptr(), s)
 
     RES = _lib.TW_EPI_RESID_F32
+    lst = torch.zeros(D // 16 * 64, device=dev)
+
+    def gemv_lnst(Wp, N, K, epi, out, ldo):
+        return lambda s: _lib.call("tw_gemv_packed_lnst", x.data_ptr(), lst.data_ptr(), g.data_ptr(), bb.data_ptr(),
+                                   1e-5, Wp.data_ptr(), B, N, K, epi, out.data_ptr(), ldo, bias.data_ptr(), s)
+
+    def gemv_stats(A, apk, Wp, N, K):
+        return lambda s: _lib.call("tw_gemv_packed_stats", A.data_ptr(), apk, K, Wp.data_ptr(), B, N, K, x.data_ptr(),
+                                   N, bias.data_ptr(), lst.data_ptr(), s)
+
     fused = [
+        ("LNst+q_x N=1280 K=1280", gemv_lnst(Wd, D, D, E_BF16, out_bf, D)),
+        ("LNst+fc1 N=5120 K=1280", gemv_lnst(W1, F, D, E_GELUP, fp, F)),
+        ("o stats  N=1280 K=1280", gemv_stats(att, 0, Wd, D, D)),
         ("LN+qkv   N=3840 K=1280", gemv_ln(Wqkv, 3 * D, D, E_BF16, out_bf, 3 * D)),
         ("LN+q_x   N=1280 K=1280", gemv_ln(Wd, D, D, E_BF16, out_bf, D)),
         ("LN+fc1   N=5120 K=1280", gemv_ln(W1, F, D, E_GELUP, fp, F)),

@@ -64,7 +64,7 @@ def test_logmel_vs_oracle(n_mels):
 EPIS = [_lib.TW_EPI_BF16, _lib.TW_EPI_GELU_BF16, _lib.TW_EPI_RESID_F32, _lib.TW_EPI_F32]
 
 
-@pytest.mark.parametrize("variant", [1, 5, 6, 3, 4, 0])
+@pytest.mark.parametrize("variant", [1, 5, 6, 8, 3, 4, 0])
 @pytest.mark.parametrize("M,N,K", [(300, 384, 256), (1500, 1280, 1280), (24, 1280, 1280), (7, 51866, 384),
                                    (32, 5120, 1280), (129, 200, 64), (600, 512, 192), (257, 768, 3840)])
 @pytest.mark.parametrize("epi", EPIS)
@@ -132,7 +132,16 @@ def _test_resid_layernorm_vs_torch(M, D, nparts):
     torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=1e-2)
 
 
-def test_gemm_gelu_pos_and_crosskv():
+@pytest.mark.parametrize("variant", [1, 5, 8])
+def test_gemm_gelu_pos_and_crosskv(variant):
+    _lib.call("tw_gemm_set_variant", variant)
+    try:
+        _gemm_gelu_pos_and_crosskv()
+    finally:
+        _lib.call("tw_gemm_set_variant", 1)
+
+
+def _gemm_gelu_pos_and_crosskv():
     M, N, K = 3000, 256, 768
     A = rand_bf16(M, K, seed=3)
     W = rand_bf16(N, K, scale=K ** -0.5, seed=4)
@@ -171,8 +180,8 @@ def _ref_attn(q, k, v):  # [B,H,S,64] fp32, q already scaled
     return torch.softmax(q @ k.transpose(-1, -2), dim=-1) @ v
 
 
-@pytest.mark.parametrize("variant", [8, 9, 4, 0])
-@pytest.mark.parametrize("B,L,H", [(2, 1500, 4), (1, 100, 2), (1, 1500, 20), (3, 1500, 5)])
+@pytest.mark.parametrize("variant", [8, 10, 11, 9, 4, 0])
+@pytest.mark.parametrize("B,L,H", [(2, 1500, 4), (1, 100, 2), (1, 1500, 20), (3, 1500, 5), (1, 128, 3), (2, 40, 2)])
 def test_encoder_attention_vs_torch(B, L, H, variant):
     _lib.call("tw_attn_set_variant", variant)
     D = H * 64
@@ -205,8 +214,17 @@ def test_encoder_attention_lds_pad_is_bit_identical(pad):
         _lib.call("tw_attn_set_lds_pad", 9)
 
 
-def test_encoder_attention_online_softmax_rescale():
+@pytest.mark.parametrize("variant", [8, 10, 11])
+def test_encoder_attention_online_softmax_rescale(variant):
     """Force the running max to jump in a late key tile (rule 26: exercise the rescale branch)."""
+    _lib.call("tw_attn_set_variant", variant)
+    try:
+        _online_softmax_rescale()
+    finally:
+        _lib.call("tw_attn_set_variant", 8)
+
+
+def _online_softmax_rescale():
     B, L, H = 1, 1500, 1
     D = 64
     qkv = rand_bf16(B * L, 3 * D, scale=0.3, seed=8)
@@ -459,6 +477,80 @@ def test_gemv_packed_resid_epilogue(M, N, K, a_packed):
     _lib.call("tw_gemv_packed", Ain.data_ptr(), a_packed, K, pack_w(W).data_ptr(), M, N, K, _lib.TW_EPI_RESID_F32,
               x.data_ptr(), N, bias.data_ptr(), 1, S())
     torch.testing.assert_close(x, want, atol=2e-3, rtol=2e-3)
+
+
+@pytest.mark.parametrize("kw", [0, 1, 2, 8])
+@pytest.mark.parametrize("M,N,K", [(24, 1280, 1280), (24, 1280, 5120), (5, 384, 1536), (32, 640, 256), (16, 1280, 1280)])
+def test_gemv_packed_stats_vs_torch(M, N, K, kw):
+    """tw_gemv_packed_stats: x += A.W^T + bias (row-major A) and, per 16-column group of every updated row, the
+    group's mean and sum of squared deviations (f32 [N/16][32][2]), vs torch fp32; every K-slice count."""
+    A = rand_bf16(M, K, seed=61)
+    W = rand_bf16(N, K, scale=K ** -0.5, seed=62)
+    bias = torch.randn(N, device=DEV) * 0.1
+    x = torch.randn(M, N, device=DEV) * 2 + 0.5
+    want = x + A.float() @ W.float().t() + bias
+    stats = torch.full((N // 16, 32, 2), float("nan"), device=DEV)
+    _lib.call("tw_gemm_set_variant", 1 | (kw << 16))
+    try:
+        _lib.call("tw_gemv_packed_stats", A.data_ptr(), 0, K, pack_w(W).data_ptr(), M, N, K, x.data_ptr(), N,
+                  bias.data_ptr(), stats.data_ptr(), S())
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("tw_gemm_set_variant", 1)
+    torch.testing.assert_close(x, want, atol=2e-3, rtol=2e-3)
+    grp = x.view(M, N // 16, 16)  # the kernel's own updated rows: the statistics must describe exactly these
+    mean = grp.mean(-1)
+    m2 = ((grp - mean[..., None]) ** 2).sum(-1)
+    torch.testing.assert_close(stats[:, :M, 0], mean.t(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(stats[:, :M, 1], m2.t(), atol=1e-4, rtol=1e-4)
+    assert torch.isnan(stats[:, M:]).all()  # rows M..31 untouched
+
+
+@pytest.mark.parametrize("kw", [0, 1, 4])
+@pytest.mark.parametrize("M,N,K,epi", [(24, 1280, 1280, _lib.TW_EPI_BF16), (24, 5120, 1280, _lib.TW_EPI_GELU_PACKED),
+                                       (13, 1536, 384, _lib.TW_EPI_GELU_PACKED), (32, 640, 2048, _lib.TW_EPI_BF16),
+                                       (7, 3000, 1280, _lib.TW_EPI_F32)])
+def test_gemv_packed_lnst_chain_vs_torch(M, N, K, epi, kw):
+    """The decoder's cross-boundary LayerNorm: a residual-update GEMV writes x and its group statistics
+    (tw_gemv_packed_stats), the consuming GEMV normalises its operand from them (tw_gemv_packed_lnst). Against torch
+    fp32: x' = x + A.W1^T + b1; out = epi(bf16(LayerNorm(x')) . W2^T + b2). Rows with a large common offset check
+    the pairwise variance combine (mean^2 >> variance would break a one-pass E[x^2] - mean^2)."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    Kp = 256
+    A = rand_bf16(M, Kp, seed=71)
+    W1 = rand_bf16(K, Kp, scale=Kp ** -0.5, seed=72)
+    b1 = torch.randn(K, device=DEV) * 0.1
+    x = (torch.randn(M, K, generator=g) * 0.7 + 40.0 + torch.randn(M, 1, generator=g) * 5).to(DEV)
+    gamma = (1 + 0.2 * torch.randn(K, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(K, generator=g)).to(DEV)
+    W2 = rand_bf16(N, K, scale=K ** -0.5, seed=73)
+    b2 = torch.randn(N, device=DEV) * 0.1
+    xw = x + A.float() @ W1.float().t() + b1
+    h = bf(torch.nn.functional.layer_norm(xw, (K,), gamma, beta, 1e-5))
+    ref = h.float() @ W2.float().t() + b2
+    stats = torch.zeros(K // 16, 32, 2, device=DEV)
+    _lib.call("tw_gemm_set_variant", 1 | (kw << 16))
+    try:
+        _lib.call("tw_gemv_packed_stats", A.data_ptr(), 0, Kp, pack_w(W1).data_ptr(), M, K, Kp, x.data_ptr(), K,
+                  b1.data_ptr(), stats.data_ptr(), S())
+        if epi == _lib.TW_EPI_GELU_PACKED:
+            out = torch.zeros(N * 32, dtype=torch.bfloat16, device=DEV)
+            _lib.call("tw_gemv_packed_lnst", x.data_ptr(), stats.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 1e-5,
+                      pack_w(W2).data_ptr(), M, N, K, epi, out.data_ptr(), 0, b2.data_ptr(), S())
+            got, want = unpack_act(out, M, N).float(), torch.nn.functional.gelu(ref)
+        else:
+            dt = torch.bfloat16 if epi == _lib.TW_EPI_BF16 else torch.float32
+            out = torch.full((M, N), float("nan"), dtype=dt, device=DEV)
+            _lib.call("tw_gemv_packed_lnst", x.data_ptr(), stats.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 1e-5,
+                      pack_w(W2).data_ptr(), M, N, K, epi, out.data_ptr(), N, b2.data_ptr(), S())
+            got, want = out.float(), ref
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("tw_gemm_set_variant", 1)
+    torch.testing.assert_close(x, xw, atol=2e-3, rtol=1e-5)
+    tol = 2e-3 if epi == _lib.TW_EPI_F32 else 2e-2
+    # as test_gemv_packed_ln_vs_torch: one-ulp bf16 differences of the normalised operand on a few elements
+    torch.testing.assert_close(got, want, atol=tol + 2e-2 * (epi == _lib.TW_EPI_F32), rtol=tol)
 
 
 @pytest.mark.parametrize("M,D,nparts", [(24, 1280, 4), (5, 384, 0), (17, 256, 2)])

@@ -341,6 +341,178 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc2(const bf16_t* __rest
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_attn_enc3: k_attn_enc2's algorithm (same staging, swizzles, fragment maps, online softmax) with less VALU work
+// per key tile, the VALU being what bounds it (per 64-key tile a wave issues 16 MFMAs = 512 matrix cycles against
+// ~800 cycles of softmax VALU):
+//   * the softmax row sums come out of the matrix core: one extra 32x32x16 MFMA per P fragment whose A operand is
+//     a ones row (row 0 = 1, rows 1..31 = 0), so o2[0] accumulates sum_k P[q][k] for the lane's query (4 MFMAs
+//     instead of 32 adds + a cross-lane shuffle per tile; the rescale touches o2[0] only, the other rows stay 0);
+//   * tile maxima with v_max3_f32 (16 instead of 31 dependent maxes);
+//   * the ragged last tile (keys >= S masked) peeled out of the loop, so full tiles carry no masking code.
+// Same rounding of every product as k_attn_enc2 except the order in which the f32 row sum is accumulated.
+// ------------------------------------------------------------------------------------------------
+template <int NW, int WPS, bool ONES>
+__global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc3(const bf16_t* __restrict__ qkv, int S, int H, int D,
+                                                          int nqb, int nwork, bf16_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) bf16_t kbuf[2][EA_KT * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t vbuf[2][EA_KT * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int orig = blockIdx.x;
+  const int q8 = nwork / 8, r8 = nwork % 8, xcd = orig % 8;
+  const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int qb = work % nqb, bh = work / nqb;
+  const int h = bh % H, b = bh / H;
+  const int ld = 3 * D;
+  const bf16_t* base = qkv + (size_t)b * S * ld + h * 64;
+  const int q0 = qb * (NW * 32) + wid * 32;
+
+  bf16x8 qf[4];
+  {
+    const bf16_t* qp = base + (size_t)min(q0 + lr, S - 1) * ld + 8 * lh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+  }
+  constexpr int CPT = 512 / (NW * 64);
+  uint4 rk[CPT], rv[CPT];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + NW * 64 * i;
+      const int key = c >> 3, ch = c & 7;
+      const bf16_t* rp = base + (size_t)min(k0 + key, S - 1) * ld + ch * 8;
+      rk[i] = *(const uint4*)(rp + D);
+      rv[i] = *(const uint4*)(rp + 2 * D);
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + NW * 64 * i;
+      const int key = c >> 3, ch = c & 7;
+      *(uint4*)(&kbuf[buf][k2_off(key, ch)]) = rk[i];
+      *(uint4*)(&vbuf[buf][v2_off(key, ch)]) = rv[i];
+    }
+  };
+  bf16x8 ones;  // A operand of the row-sum MFMA (lane l holds A[row l & 31][k = 8 lh + j]): row 0 = 1, other rows 0
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)(lr == 0 ? 1.f : 0.f);
+
+  f32x16 o0 = {0}, o1 = {0}, o2 = {0};  // O^T (d 0..31, 32..63), row sums (row 0; ONES only)
+  float m_run = -INFINITY, l_sum = 0.f;  // (l_sum: the row sum by VALU adds when !ONES)
+  const int nfull = S / EA_KT, ntile = (S + EA_KT - 1) / EA_KT;
+  const int gq = (lane & 15) >> 2, gp = lane & 3, gd = ((lane >> 4) & 1) * 16;
+  auto tile = [&](int cur, int k0, auto MASKED) {
+    constexpr bool masked = decltype(MASKED)::value;
+    const bf16_t* ks = kbuf[cur];
+    const bf16_t* vs = vbuf[cur];
+    f32x16 s0 = {0}, s1 = {0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 ka = *(const bf16x8*)(ks + k2_off(lr, 2 * s + lh));
+      const bf16x8 kb = *(const bf16x8*)(ks + k2_off(32 + lr, 2 * s + lh));
+      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], s0, 0, 0, 0);
+      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[s], s1, 0, 0, 0);
+    }
+    if constexpr (masked) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (k0 + key >= S) s0[r] = -INFINITY;
+        if (k0 + 32 + key >= S) s1[r] = -INFINITY;
+      }
+    }
+    float tc[4];  // four independent v_max3 chains over 8 scores each
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float t = fmaxf(fmaxf(s0[4 * c], s0[4 * c + 1]), s0[4 * c + 2]);
+      t = fmaxf(fmaxf(t, s0[4 * c + 3]), s1[4 * c]);
+      t = fmaxf(fmaxf(t, s1[4 * c + 1]), s1[4 * c + 2]);
+      tc[c] = fmaxf(t, s1[4 * c + 3]);
+    }
+    float tmax = fmaxf(fmaxf(tc[0], tc[1]), fmaxf(tc[2], tc[3]));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    if (__any(tmax > m_run)) {
+      const float m_new = fmaxf(m_run, tmax);
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * EA_LOG2E);  // first tile: exp2(-inf) = 0
+      if constexpr (ONES) o2[0] *= alpha;
+      else l_sum *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      m_run = m_new;
+    }
+    const float mb = m_run * EA_LOG2E;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], EA_LOG2E, -mb));
+      s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], EA_LOG2E, -mb));
+    }
+    if constexpr (!ONES) {
+      float ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ps += s0[r] + s1[r];
+      l_sum += ps;  // (this lane's 32 keys; the lane pair is summed once after the loop)
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = (__bf16)(half ? s1[8 * s + j] : s0[8 * s + j]);
+        const int kb = half * 32 + 16 * s + 4 * lh + gq;
+        if constexpr (ONES) o2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pb, o2, 0, 0, 0);
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const int d = db * 32 + gd + 4 * gp;
+          const int ch = d >> 3, wi = d & 7;
+          const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4_t*)(vs + v2_off(kb, ch) + wi));
+          const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4_t*)(vs + v2_off(kb + 8, ch) + wi));
+          const short8_t v8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          const bf16x8 va = __builtin_bit_cast(bf16x8, v8);
+          if (db == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o0, 0, 0, 0);
+          else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o1, 0, 0, 0);
+        }
+      }
+    }
+  };
+  using BT = std::integral_constant<bool, true>;
+  using BF = std::integral_constant<bool, false>;
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int kt = 0; kt < nfull; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < ntile) gload((kt + 1) * EA_KT);
+    tile(cur, kt * EA_KT, BF{});
+    if (kt + 1 < ntile) swrite(cur ^ 1);
+    __syncthreads();
+  }
+  if (nfull < ntile) tile(nfull & 1, nfull * EA_KT, BT{});
+
+  // ONES: the row sum sits in o2[0] of lane (lr, lh = 0) (accumulator row 0); lane (lr, 1) holds row 4 = 0.
+  // Otherwise each lane of the pair (lr, lr + 32) summed its own 32 keys of every tile (same running max, so the
+  // two partial sums share one scale): add them once here.
+  const float l_run = ONES ? __shfl(o2[0], lr, 64) : l_sum + __shfl_xor(l_sum, 32, 64);
+  const int q = q0 + lr;
+  if (q < S) {
+    const float inv = 1.f / l_run;
+    bf16_t* op = out + ((size_t)b * S + q) * D + h * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * lh;
+      uint2 w0, w1;
+      w0.x = pack_bf16x2(o0[4 * g] * inv, o0[4 * g + 1] * inv);
+      w0.y = pack_bf16x2(o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
+      w1.x = pack_bf16x2(o1[4 * g] * inv, o1[4 * g + 1] * inv);
+      w1.y = pack_bf16x2(o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
+      *(uint2*)(op + d) = w0;
+      *(uint2*)(op + 32 + d) = w1;
+    }
+  }
+}
+
 static int tw_attn_variant = 8;  // 0 = k_attn_encoder, 4 / 8 = k_attn_enc2<NW>, 9 = <8> at 2 workgroups per CU
 // decoder cross-attention: 1 = one pass with an online softmax (default), 0 = two passes (scores, then P.V)
 static int tw_dec_cross_1p = 1;
@@ -369,7 +541,7 @@ extern "C" int tw_attn_set_variant(int v) {
   tw_dec_cross_nt = (v >> 12) & 0xff ? ((v >> 12) & 0xff) - 1 : 0;
   tw_dec_cross_ng = (v & 0x200) ? 64 : 32;  // bit 9: one-pass with 512 threads (64 key groups) instead of 256
   v &= 0xff;
-  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9) ? v : 8;
+  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9 || v == 10 || v == 11) ? v : 8;
   return 0;
 }
 
@@ -383,6 +555,12 @@ extern "C" int tw_attn_encoder(const bf16_t* qkv, int B, int S, int H, bf16_t* o
   } else if (tw_attn_variant == 4) {
     const int nqb = tw_cdiv(S, 128), nwork = nqb * H * B;
     hipLaunchKernelGGL((k_attn_enc2<4, 2>), dim3(nwork), dim3(256), 0, st, qkv, S, H, D, nqb, nwork, out);
+  } else if (tw_attn_variant == 10 || tw_attn_variant == 11) {
+    const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
+    if (tw_attn_variant == 10)
+      hipLaunchKernelGGL((k_attn_enc3<8, 4, false>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
+    else
+      hipLaunchKernelGGL((k_attn_enc3<8, 4, true>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
   } else if (tw_attn_variant == 9) {
     const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
     hipLaunchKernelGGL((k_attn_enc2<8, 4>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);

@@ -9,6 +9,7 @@
 // One wave per row, f32 in -> bf16 out (the GEMM A operand). The row is read once with 16-byte loads and
 // kept in registers (D <= 64 * 4 * LN_MAXC); mean and variance are two wave reductions over it.
 #define LN_MAXC 16
+template <int NC>  // float4 chunks per lane: ceil(D / 256) (registers sized to the row, not to LN_MAXC)
 __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, const float* __restrict__ g,
                                                    const float* __restrict__ bta, int M, int D, float eps,
                                                    bf16_t* __restrict__ out) {
@@ -17,20 +18,25 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, 
   if (row >= M) return;
   const int nc = D >> 2;
   const float4* xr = (const float4*)(x + (size_t)row * D);
-  float4 v[LN_MAXC];
+  float4 v[NC], gg[NC], bb[NC];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < LN_MAXC; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int c = lane + 64 * i;
     if (64 * i < nc) {  // wave-uniform trip bound; the lane index is clamped, not branched on
       v[i] = xr[min(c, nc - 1)];
-      if (c < nc) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+      // gamma / beta fly with the row instead of after both reductions (one dependent round trip less)
+      gg[i] = ((const float4*)g)[min(c, nc - 1)];
+      bb[i] = ((const float4*)bta)[min(c, nc - 1)];
     }
   }
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+    if (64 * i < nc && lane + 64 * i < nc) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
   const float mean = wave_sum(s) / (float)D;
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < LN_MAXC; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int c = lane + 64 * i;
     if (64 * i < nc && c < nc) {
       const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, d = v[i].w - mean;
@@ -40,13 +46,12 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, 
   const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
   uint2* orow = (uint2*)(out + (size_t)row * D);
 #pragma unroll
-  for (int i = 0; i < LN_MAXC; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int c = lane + 64 * i;
     if (64 * i < nc && c < nc) {
-      const float4 gg = ((const float4*)g)[c], bb = ((const float4*)bta)[c];
       uint2 w;
-      w.x = pack_bf16x2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
-      w.y = pack_bf16x2((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+      w.x = pack_bf16x2((v[i].x - mean) * rstd * gg[i].x + bb[i].x, (v[i].y - mean) * rstd * gg[i].y + bb[i].y);
+      w.y = pack_bf16x2((v[i].z - mean) * rstd * gg[i].z + bb[i].z, (v[i].w - mean) * rstd * gg[i].w + bb[i].w);
       orow[c] = w;
     }
   }
@@ -56,8 +61,18 @@ extern "C" int tw_layernorm(const float* x, const float* gamma, const float* bet
                             void* stream) {
   TW_REQUIRE(x && gamma && beta && out && M > 0, "tw_layernorm: bad args");
   TW_REQUIRE(D % 4 == 0 && D <= 256 * LN_MAXC, "tw_layernorm: D=%d must be a multiple of 4 and <= %d", D, 256 * LN_MAXC);
-  hipLaunchKernelGGL(k_layernorm, dim3(tw_cdiv(M, 4)), dim3(256), 0, (hipStream_t)stream, x, gamma, beta, M, D, eps,
-                     out);
+  const dim3 grid(tw_cdiv(M, 4)), blk(256);
+  hipStream_t st = (hipStream_t)stream;
+  switch (tw_cdiv(D, 256)) {
+    case 1: hipLaunchKernelGGL(k_layernorm<1>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
+    case 2: hipLaunchKernelGGL(k_layernorm<2>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
+    case 3: hipLaunchKernelGGL(k_layernorm<3>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
+    case 4: hipLaunchKernelGGL(k_layernorm<4>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
+    case 5: hipLaunchKernelGGL(k_layernorm<5>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
+    case 6: hipLaunchKernelGGL(k_layernorm<6>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
+    case 7: case 8: hipLaunchKernelGGL(k_layernorm<8>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
+    default: hipLaunchKernelGGL(k_layernorm<LN_MAXC>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
+  }
   return tw_check_launch("tw_layernorm");
 }
 

@@ -30,6 +30,7 @@ struct EpiArgs {
   uint8_t* sout;      // EPI_GELU_MX: e8m0 scales of the fp8 output, [N/128][s_rows][4]
   int s_rows;
   int group_m;        // large-M kernels: tile rows per group of the tile order (tw_tile_grouped); <= 1 row-major
+  float* stats;       // TW_EPI_RESID_STATS: per-16-column-group row statistics of the updated rows (tw_gemv_packed_stats)
 };
 
 // Tile (tm, tn) of tile id `wgid` (after the XCD remap, which hands each XCD a contiguous id range) in grouped
@@ -202,8 +203,17 @@ static inline int tw_group_for(int N) {
 static int tw_gemv_nt_min_n = 16384;
 static int tw_tune_skinny_nw = 0;  // 0 = heuristic; 4 / 8 / 16 force the skinny kernel's waves per block
 static int tw_tune_gemv_kw = 0;    // 0 = heuristic; 1 / 2 / 4 / 8 force the packed GEMV's K-slices per column group
+// Largest K-slice count the packed-GEMV heuristic picks (8: up to 512-thread workgroups). Capping it at 4 (256-thread
+// workgroups) makes the q/k/v GEMV co-reside with an encoder GEMM workgroup (scripts/exp/interference.py, beside
+// k_gemm_8p: 33.6 us per launch at KW = 8, 11.5 at KW = 4; alone 3.4 vs 3.7 us) but left the bench step unchanged
+// (104.7 vs 104.8 ms over three interleaved pairs), so the round-1 heuristic stays the default (A/B knob).
+static int tw_gemv_max_kw = 8;
+extern "C" int tw_gemv_set_max_kw(int kw) {
+  tw_gemv_max_kw = (kw == 1 || kw == 2 || kw == 4 || kw == 8) ? kw : 8;
+  return 0;
+}
 extern "C" int tw_gemm_set_variant(int big) {
-  tw_gemm_big_enabled = big & 7;
+  tw_gemm_big_enabled = big & 15;
   const int nw = (big >> 8) & 0xff;
   tw_tune_skinny_nw = (nw == 4 || nw == 8 || nw == 16) ? nw : 0;
   tw_gemv_nt_min_n = (big & 0x1000000) ? (1 << 30) : 16384;  // bit 24: proj_out weights through the caches (A/B)
@@ -1162,6 +1172,200 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8pp(const bf16_t* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_gemm_4w: 256 x 256 x 64 tiles on FOUR waves (256 threads, one wave per SIMD), each wave a 128 x 128 sub-tile =
+// 8 x 8 accumulators of v_mfma_f32_16x16x32_bf16 (256 accumulator registers; the unified register file holds them
+// beside the operand fragments at one wave per SIMD). Against the 8-wave kernels (128 x 64 per wave) a wave reads
+// 32 KiB of LDS per K-step for 2 MFLOP instead of 24 KiB for 1 MFLOP, and the CU issues half the LDS reads per FLOP;
+// it is the decomposition hipBLASLt picks on these shapes (MT256x256x64, MI16x16, 256 threads). Staging as
+// k_gemm_8p: buffer_load ... lds (LDS-DMA) through one wave-uniform descriptor per operand tile (rows past M / N
+// read as zeros), source-side chunk swizzle chunk ^ ((row >> 1) & 7) undone on the ds_read_b128 address; the
+// per-instruction row block rides in soffset, so the per-lane part is two 32-bit offsets per operand. K loop: DMA of
+// K-tile t+1 issued first, then the two 32-deep k-substeps of tile t (16 fragment reads + 64 MFMAs each), one
+// vmcnt(0) + barrier per K-tile. Epilogue: each wave stages 32-row slabs of its 128 x 128 f32 results in its own
+// LDS image (row stride 132 floats: conflict-free writes) and stores 8 consecutive columns per lane.
+// MEASURED SLOWER than k_gemm_8p and kept only as an A/B variant (tw_gemm_set_variant(8), scripts/gemm_bench.py,
+// MI355X): qkv 792 vs 1048, fc2 820 vs 1119 TF/s; with the K-loop DMA removed (timing only) fc2 reaches 1226, so
+// at one wave per SIMD this hipcc-scheduled loop (92 AGPR<->VGPR moves per K-tile, exposed fragment-read latency)
+// is the limit before the staging is; hipBLASLt's hand-scheduled kernel of this shape reaches 1318.
+// ------------------------------------------------------------------------------------------------
+#define G4_LD 132  // f32 row stride of a wave's epilogue image (128 + 4)
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void k_gemm_4w(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                    int M, int N, int K, int lda, int ldw, EpiArgs ea) {
+  // K loop: 2 buffers x (A | W) x 256 rows x 64 bf16 = 128 KiB; epilogue: 4 waves x 32 rows x 132 f32 = 66 KiB
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * 256 * 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform: soffset / LDS bases in SGPRs
+  const int ntm = (M + 255) / 256, ntn = (N + 255) / 256;
+  const int nwg = ntm * ntn;
+  const int orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  int tm, tn;
+  tw_tile_grouped(wgid, ntm, ntn, ea.group_m, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // DMA: wave w fills rows [64w, 64w + 64) of the A tile and of the W tile with 8 instructions each; instruction i
+  // moves rows 64w + 8i + (lane >> 3), 16-byte chunk (lane & 7) ^ swz(row). swz(row) depends on i only through its
+  // parity, so two voffsets per operand; the row block (64w + 8i) * ld goes into soffset with the K offset.
+  const int ra = M - m0, rw = N - n0;
+  const __amdgpu_buffer_rsrc_t rsA = tw_uniform_rsrc(A + (size_t)m0 * lda, max(0, min(256, ra)) * lda * 2);
+  const __amdgpu_buffer_rsrc_t rsW = tw_uniform_rsrc(W + (size_t)n0 * ldw, max(0, min(256, rw)) * ldw * 2);
+  unsigned va[2], vw[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int r = 8 * par + (lane >> 3);  // row within an aligned 16-row block: swz = (r >> 1) & 7
+    const int ch = (lane & 7) ^ ((r >> 1) & 7);
+    va[par] = (unsigned)((lane >> 3) * lda + ch * 8) * 2u;
+    vw[par] = (unsigned)((lane >> 3) * ldw + ch * 8) * 2u;
+  }
+  auto stage = [&](int buf, int k0) {
+    bf16_t* As = smem + buf * (2 * 256 * 64);
+    bf16_t* Ws = As + 256 * 64;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int rb = 64 * wid + 8 * i;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void_t*)(As + rb * 64), 16, va[i & 1],
+                                               (unsigned)(rb * lda + k0) * 2u, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (lds_void_t*)(Ws + rb * 64), 16, vw[i & 1],
+                                               (unsigned)(rb * ldw + k0) * 2u, 0, 0);
+    }
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // Software pipeline, one barrier per K-tile placed mid-tile (two LDS buffers; tile t lives in buffer t & 1):
+  //   phase A of tile t: 64 MFMAs on the k-substep-0 fragments F0(t) || ds_read of F1(t)
+  //   mid barrier:       vmcnt(0) (this wave's DMA of tile t+1 landed) + lgkmcnt(0) + s_barrier
+  //   phase B of tile t: 64 MFMAs on F1(t) || ds_read of F0(t+1) || DMA of tile t+2 into buffer t & 1
+  // RAW: F0(t+1) is read after the mid barrier of t, which follows every wave's wait for its DMA of tile t+1.
+  // WAR: the DMA of t+2 overwrites buffer t & 1 after the mid barrier of t, by which every wave's reads of F0(t)
+  // (phase B of t-1) and F1(t) (phase A of t, lgkmcnt(0) before the barrier) have completed.
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  auto rdfr = [&](int buf, int kk, bf16x8 (&af)[8], bf16x8 (&bw)[8]) {
+    const bf16_t* As = smem + buf * (2 * 256 * 64);
+    const bf16_t* Ws = As + 256 * 64;
+    const int kc = 4 * kk + fq;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = 128 * wc + 16 * j + fr;
+      bw[j] = *(const bf16x8*)(Ws + col * 64 + ((kc ^ gb_swz(col)) << 3));
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = 128 * wr + 16 * i + fr;
+      af[i] = *(const bf16x8*)(As + row * 64 + ((kc ^ gb_swz(row)) << 3));
+    }
+  };
+  auto mma = [&](const bf16x8 (&af)[8], const bf16x8 (&bw)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bw[j], acc[i][j], 0, 0, 0);
+  };
+  const int nk = K / GB_BK;
+  stage(0, 0);
+  if (nk > 1) stage(1, GB_BK);
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 (its 16 instructions were issued first)
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  rdfr(0, 0, fa0, fb0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    // phase A
+    rdfr(cur, 1, fa1, fb1);
+    mma(fa0, fb0);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 ds_read
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // phase B
+    if (kt + 1 < nk) rdfr(cur ^ 1, 0, fa0, fb0);
+    if (kt + 2 < nk) stage(cur, (kt + 2) * GB_BK);
+    mma(fa1, fb1);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 ds_read
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // 1 LDS-DMA (VMEM read)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // the epilogue reuses the staging LDS
+
+  // epilogue: four 32-row slabs per wave through its [32][G4_LD] f32 image; 16 lanes per row, 8 columns per lane
+  float* img = (float*)smem + wid * (32 * G4_LD);
+  const int rc = (lane & 15) * 8;  // this lane's 8 columns in the read-back
+  const int ncol = n0 + 128 * wc + rc;
+  float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+  if (ea.bias) {
+    b0.x = ea.bias[min(ncol, N - 1)];
+    b0.y = ea.bias[min(ncol + 1, N - 1)];
+    b0.z = ea.bias[min(ncol + 2, N - 1)];
+    b0.w = ea.bias[min(ncol + 3, N - 1)];
+    b1.x = ea.bias[min(ncol + 4, N - 1)];
+    b1.y = ea.bias[min(ncol + 5, N - 1)];
+    b1.z = ea.bias[min(ncol + 6, N - 1)];
+    b1.w = ea.bias[min(ncol + 7, N - 1)];
+  }
+  constexpr bool PRE = EPI == TW_EPI_RESID_F32 || EPI == TW_EPI_GELU_POS_F32;
+  const bool full = ncol + 7 < N;
+#pragma unroll
+  for (int sl = 0; sl < 4; ++sl) {  // slab sl = accumulator rows i = 2 sl, 2 sl + 1 (32 rows)
+    const int mrow0 = m0 + 128 * wr + 32 * sl;
+    float4 ad[8][2];
+    if constexpr (PRE) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int mq = min(mrow0 + q * 4 + (lane >> 4), M - 1);
+        ad[q][0] = epi_addend<EPI>(ea, mq, ncol, full);
+        ad[q][1] = epi_addend<EPI>(ea, mq, ncol + 4, full);
+      }
+    }
+    if (sl) __syncthreads();  // (first slab: the K loop ended on a barrier)
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) img[(16 * ii + 4 * fq + r) * G4_LD + 16 * j + fr] = acc[2 * sl + ii][j][r];
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      const int lr = rr * 4 + (lane >> 4);
+      const int m = mrow0 + lr;
+      float4 v0 = *(const float4*)(img + lr * G4_LD + rc);
+      float4 v1 = *(const float4*)(img + lr * G4_LD + rc + 4);
+      v0.x += b0.x; v0.y += b0.y; v0.z += b0.z; v0.w += b0.w;
+      v1.x += b1.x; v1.y += b1.y; v1.z += b1.z; v1.w += b1.w;
+      if constexpr (PRE) {
+        if (full) {
+          if (m < M) {
+            epi_store4_pre<EPI>(ea, m, ncol, v0, ad[rr][0]);
+            epi_store4_pre<EPI>(ea, m, ncol + 4, v1, ad[rr][1]);
+          }
+        } else if (m < M && ncol < N) {
+          epi_store8<EPI>(ea, m, ncol, N, v0, v1);
+        }
+      } else {
+        if (m < M && ncol < N) epi_store8<EPI>(ea, m, ncol, N, v0, v1);
+      }
+    }
+  }
+}
+
 static int tw_num_cus() {
   static int cus = 0;  // one device per process (the engine's)
   if (!cus) {
@@ -1185,6 +1389,12 @@ static int tw_num_cus() {
 // projections whose 80 column groups alone cannot fill 256 CUs): each block row writes its f32 partial
 // to part[y][M][ldo] and the consumer (tw_resid_layernorm) adds the partials, bias and residual.
 #define TW_EPI_PARTIAL 100
+// The decoder's residual update with LayerNorm statistics (tw_gemv_packed_stats): x[m][n] += acc + bias as
+// TW_EPI_RESID_F32, and for every 16-column group g the updated row slice's (mean, M2 = sum of squared deviations
+// from that mean) into stats[(g * 32 + m) * 2 ..]. The consuming GEMV (tw_gemv_packed_lnst) combines the K/16 groups
+// into the row's mean and variance (Chan, Golub & LeVeque's pairwise update, as exact as a two-pass LayerNorm),
+// so the LayerNorm between the two projections needs no launch of its own.
+#define TW_EPI_RESID_STATS 102
 
 template <int EPI, int NW, bool TWO>
 __global__ __launch_bounds__(NW * 64) void k_gemm_skinny(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
@@ -1308,6 +1518,7 @@ struct LnArgs {
   const float* g;
   const float* b;
   float eps;
+  const float* stats;  // non-null: the rows' statistics come from the producing GEMV (TW_EPI_RESID_STATS)
 };
 #define GEMV_LN_MAXV 8  // float4 chunks per lane of one row in the LN prologue: K <= 2048
 
@@ -1330,8 +1541,48 @@ __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __r
   const int s0 = (int)((long)sl * ns / nsl), s1 = (int)((long)(sl + 1) * ns / nsl);
   f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
   if constexpr (ALN) {
-    const int nc = K >> 2;
-    for (int r = wid; r < M; r += NW) {
+    if (la.stats) {
+      // statistics from the producer (TW_EPI_RESID_STATS): 8 lanes per row, each combining every 8th of the K/16
+      // groups' (mean, M2); one round of loads for all rows
+      const int G = K >> 4;
+      for (int r0 = 0; r0 < M; r0 += NW * 8) {
+        const int r = r0 + (tid >> 3), j0 = tid & 7;
+        float mg[GEMV_LN_MAXV * 2], s = 0.f, q = 0.f;
+#pragma unroll
+        for (int i = 0; i < GEMV_LN_MAXV * 2; ++i) {
+          const int j = j0 + 8 * i;
+          mg[i] = 0.f;
+          if (j < G && r < M) {
+            const float2 st = *(const float2*)(la.stats + ((size_t)j * 32 + r) * 2);
+            mg[i] = st.x;
+            s += st.x;
+            q += st.y;
+          }
+        }
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+          s += __shfl_xor(s, o, 64);
+          q += __shfl_xor(q, o, 64);
+        }
+        const float mean = s / (float)G;
+        float d2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < GEMV_LN_MAXV * 2; ++i)
+          if (j0 + 8 * i < G) {
+            const float d = mg[i] - mean;
+            d2 += d * d;
+          }
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) d2 += __shfl_xor(d2, o, 64);
+        if (j0 == 0 && r < M) {
+          lnst[r][0] = mean;
+          lnst[r][1] = rsqrtf((q + 16.f * d2) / (float)K + la.eps);
+        }
+      }
+      __syncthreads();
+    }
+    const int nc = la.stats ? 0 : K >> 2;  // (the row statistics computed here when no producer wrote them)
+    for (int r = wid; nc && r < M; r += NW) {
       const float4* xr = (const float4*)(la.x + (size_t)r * K);
       float4 v[GEMV_LN_MAXV];
       float s = 0.f;
@@ -1437,11 +1688,44 @@ __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __r
       epi_store<EPI>(ea, m, n, v);
     }
   };
+  // TW_EPI_RESID_STATS: the 16 lanes holding one row's 16 columns of group gs reduce the updated values to the
+  // group's (mean, M2); xn is this lane's updated element (0 for rows past M: the segment is then skipped whole)
+  auto group_stats = [&](int m, int gs, float xn, bool ok) {
+    float sm = xn;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) sm += __shfl_xor(sm, o, 64);
+    const float mg = sm * (1.f / 16.f);
+    const float d = ok ? xn - mg : 0.f;
+    float q = d * d;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) q += __shfl_xor(q, o, 64);
+    if (ok && (lane & 15) == 0) *(float2*)(ea.stats + ((size_t)gs * 32 + m) * 2) = make_float2(mg, q);
+  };
   if constexpr (KW == 1) {
     // one wave per column group: its accumulators are the results. Stored straight from registers (16 lanes per
     // row = 16 consecutive columns), so the kernel holds no LDS: the vocabulary-wide proj_out's 811 workgroups then
     // co-reside with an encoder GEMM workgroup (136 KiB of the CU's 160 KiB LDS) several per CU, in one round.
     const int n = g * 16 + cc;
+    if constexpr (EPI == TW_EPI_RESID_STATS) {  // (N % 16 == 0: a group's 16 columns are all valid or all not)
+      if (g < ngroups) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+          for (int t = 0; t < (TWO ? 2 : 1); ++t) {
+            const int m = 16 * t + rb + r;
+            const bool ok = m < M;
+            float xn = 0.f;
+            if (ok) {
+              float* o = (float*)ea.out + (size_t)m * ea.ldo + n;
+              xn = *o + ((t ? c1[r] : c0[r]) + (ea.bias ? ea.bias[n] : 0.f));
+              *o = xn;
+            }
+            group_stats(m, g, xn, ok);
+          }
+        }
+      }
+      return;
+    }
     if (g < ngroups && n < N) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1462,6 +1746,21 @@ __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __r
     const int gg = e / (ROWS * 16), rem = e - gg * ROWS * 16;
     const int m = rem >> 4, c = rem & 15;
     const int n = (blockIdx.x * GPB + gg) * 16 + c;
+    if constexpr (EPI == TW_EPI_RESID_STATS) {  // whole waves run each iteration: the 16-lane shuffles are safe
+      const int gs = blockIdx.x * GPB + gg;
+      const bool ok = m < M && gs < ngroups;
+      float xn = 0.f;
+      if (ok) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < KW; ++w) v += red[gg * KW + w][m][c];
+        float* o = (float*)ea.out + (size_t)m * ea.ldo + n;
+        xn = *o + (v + (ea.bias ? ea.bias[n] : 0.f));
+        *o = xn;
+      }
+      group_stats(m, gs, xn, ok);
+      continue;
+    }
     if (m < M && n < N) {
       float v = 0.f;
 #pragma unroll
@@ -1503,7 +1802,7 @@ static void launch_gemv_ln(const bf16_t* Wp, int M, int N, int K, const EpiArgs&
   const long groups = tw_cdiv(N, 16);
   const int steps = K / 32;
   int kw = 1;
-  while (groups * kw < 1024 && kw < 8 && steps >= 8 * kw) kw *= 2;
+  while (groups * kw < 1024 && kw < tw_gemv_max_kw && steps >= 8 * kw) kw *= 2;
   if (tw_tune_gemv_kw) kw = tw_tune_gemv_kw;
   if (kw == 1) launch_gemv_ln3<EPI, 1>(Wp, M, N, K, ea, la, s);
   else if (kw == 2) launch_gemv_ln3<EPI, 2>(Wp, M, N, K, ea, la, s);
@@ -1522,7 +1821,7 @@ static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
   const long groups = tw_cdiv(N, 16) * (long)splits;
   const int steps = K / 32 / splits;
   int kw = 1;
-  while (groups * kw < 1024 && kw < 8 && steps >= 8 * kw) kw *= 2;
+  while (groups * kw < 1024 && kw < tw_gemv_max_kw && steps >= 8 * kw) kw *= 2;
   // the vocabulary-wide proj_out (3242 column groups): 4 K-slices per group, 25.0 vs 32.8 us per launch with one
   // (scripts/gemv_bench.py, B = 24): more waves in flight per CU for the one launch that streams 133 MB
   const bool wide = N >= tw_gemv_nt_min_n;
@@ -1555,6 +1854,9 @@ static int launch_gemm(const bf16_t* A, const bf16_t* W, int M, int N, int K, in
     } else if (tw_gemm_big_enabled == 5) {
       unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
       hipLaunchKernelGGL(k_gemm_8p<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
+    } else if (tw_gemm_big_enabled == 8) {
+      unsigned nwg = tw_cdiv(M, 256) * tw_cdiv(N, 256);
+      hipLaunchKernelGGL(k_gemm_4w<EPI>, dim3(nwg), dim3(256), 0, s, A, W, M, N, K, lda, ldw, ea);
     } else if (tw_gemm_big_enabled == 6) {
       unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
       const unsigned grid = std::min<unsigned>(nwg, (unsigned)(tw_num_cus() & ~7));
@@ -1665,7 +1967,7 @@ extern "C" int tw_gemv_packed_ln(const float* x, const float* gamma, const float
   TW_REQUIRE(M > 0 && M <= 32 && N > 0 && K > 0 && K % 32 == 0 && K <= 256 * GEMV_LN_MAXV,
              "tw_gemv_packed_ln: M=%d N=%d K=%d (M <= 32, K %% 32, K <= %d)", M, N, K, 256 * GEMV_LN_MAXV);
   EpiArgs ea{out, ldo, bias, nullptr, 0, 0, 0, 0, 0};
-  const LnArgs la{x, gamma, beta, eps};
+  const LnArgs la{x, gamma, beta, eps, nullptr};
   hipStream_t s = (hipStream_t)stream;
   switch (epi) {
     case TW_EPI_BF16: launch_gemv_ln<TW_EPI_BF16>(Wp, M, N, K, ea, la, s); break;
@@ -1677,6 +1979,39 @@ extern "C" int tw_gemv_packed_ln(const float* x, const float* gamma, const float
     default: tw_set_error("tw_gemv_packed_ln: unsupported epilogue %d", epi); return TW_ERR_ARG;
   }
   return tw_check_launch("tw_gemv_packed_ln");
+}
+
+extern "C" int tw_gemv_packed_stats(const bf16_t* A, int a_packed, int lda, const bf16_t* Wp, int M, int N, int K,
+                                    float* x, int ldx, const float* bias, float* stats, void* stream) {
+  TW_REQUIRE(A && Wp && x && stats, "tw_gemv_packed_stats: null pointer");
+  TW_REQUIRE(M > 0 && M <= 32 && N > 0 && N % 16 == 0 && K > 0 && K % 32 == 0 && ldx >= N,
+             "tw_gemv_packed_stats: M=%d N=%d K=%d ldx=%d (M <= 32, N %% 16, K %% 32)", M, N, K, ldx);
+  TW_REQUIRE(a_packed || (lda >= K && lda % 8 == 0), "tw_gemv_packed_stats: lda=%d", lda);
+  EpiArgs ea{x, ldx, bias, nullptr, 0, 0, 0, 0, 0};
+  ea.stats = stats;
+  launch_gemv_p<TW_EPI_RESID_STATS>(A, a_packed, lda, Wp, M, N, K, ea, 1, (hipStream_t)stream);
+  return tw_check_launch("tw_gemv_packed_stats");
+}
+
+extern "C" int tw_gemv_packed_lnst(const float* x, const float* stats, const float* gamma, const float* beta, float eps,
+                                   const bf16_t* Wp, int M, int N, int K, int epi, void* out, int ldo,
+                                   const float* bias, void* stream) {
+  TW_REQUIRE(x && stats && gamma && beta && Wp && out, "tw_gemv_packed_lnst: null pointer");
+  TW_REQUIRE(M > 0 && M <= 32 && N > 0 && K > 0 && K % 32 == 0 && K <= 256 * GEMV_LN_MAXV,
+             "tw_gemv_packed_lnst: M=%d N=%d K=%d (M <= 32, K %% 32, K <= %d)", M, N, K, 256 * GEMV_LN_MAXV);
+  EpiArgs ea{out, ldo, bias, nullptr, 0, 0, 0, 0, 0};
+  const LnArgs la{x, gamma, beta, eps, stats};
+  hipStream_t s = (hipStream_t)stream;
+  switch (epi) {
+    case TW_EPI_BF16: launch_gemv_ln<TW_EPI_BF16>(Wp, M, N, K, ea, la, s); break;
+    case TW_EPI_F32: launch_gemv_ln<TW_EPI_F32>(Wp, M, N, K, ea, la, s); break;
+    case TW_EPI_GELU_PACKED:
+      TW_REQUIRE(N % 32 == 0, "tw_gemv_packed_lnst: GELU_PACKED needs N %% 32 (it is the next GEMV's K)");
+      launch_gemv_ln<TW_EPI_GELU_PACKED>(Wp, M, N, K, ea, la, s);
+      break;
+    default: tw_set_error("tw_gemv_packed_lnst: unsupported epilogue %d", epi); return TW_ERR_ARG;
+  }
+  return tw_check_launch("tw_gemv_packed_lnst");
 }
 
 // ------------------------------------------------------------------------------------------------

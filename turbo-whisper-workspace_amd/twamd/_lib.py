@@ -37,7 +37,7 @@ EXPORTED = (
     "tw_attn_decode_cross", "tw_embed_decoder", "tw_logits_select", "tw_gemm_bf16_partial", "tw_resid_layernorm",
     "tw_gemm_set_variant", "tw_attn_set_variant", "tw_ln_set_variant",
     "tw_dtw", "tw_attn_decode_cross_probs", "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_stream_create_masked", "tw_stream_destroy", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
-    "tw_gemm_mx", "tw_quant_mx", "tw_layernorm_mx", "tw_attn_encoder_mx", "tw_gemm_mx_set_variant", "tw_logits_select_embed", "tw_gemm_set_group",
+    "tw_gemm_mx", "tw_quant_mx", "tw_layernorm_mx", "tw_attn_encoder_mx", "tw_gemm_mx_set_variant", "tw_logits_select_embed", "tw_gemm_set_group", "tw_gemv_set_max_kw", "tw_gemv_packed_stats", "tw_gemv_packed_lnst",
     "tw_attn_set_lds_pad", "tw_gemv_packed_ln",
 )
 
@@ -104,6 +104,7 @@ _SIGS = {
     "tw_gemm_set_variant": ([_I], _I),
     "tw_gemm_mx_set_variant": ([_I], _I),
     "tw_gemm_set_group": ([_I], _I),
+    "tw_gemv_set_max_kw": ([_I], _I),
     "tw_logits_select_embed": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), _P, _P, _I, _P, _P, _P, _P, _P, _I,
                                 _I, _P, _P, _P, _F, _P, _I, _P], _I),
     "tw_attn_set_variant": ([_I], _I),
@@ -119,6 +120,8 @@ _SIGS = {
     "tw_pack_weight": ([_P, _I, _I, _I, _P, _P], _I),
     "tw_gemv_packed": ([_P, _I, _I, _P, _I, _I, _I, _I, _P, _I, _P, _I, _P], _I),
     "tw_gemv_packed_ln": ([_P, _P, _P, _F, _P, _I, _I, _I, _I, _P, _I, _P, _P], _I),
+    "tw_gemv_packed_stats": ([_P, _I, _I, _P, _I, _I, _I, _P, _I, _P, _P, _P], _I),
+    "tw_gemv_packed_lnst": ([_P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _P, _I, _P, _P], _I),
     "tw_resid_layernorm_packed": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
     "tw_stream_create_masked": ([_P, _I, ctypes.POINTER(ctypes.c_void_p)], _I),
     "tw_stream_destroy": ([_P], _I),

@@ -83,6 +83,7 @@ class DecView:
     pos: torch.Tensor
     hp: Optional[torch.Tensor] = None  # packed-activation LayerNorm output (tw_gemv_packed A operand), <= 32 rows
     fp: Optional[torch.Tensor] = None  # packed-activation fc1 output (fc2's A operand)
+    lst: Optional[torch.Tensor] = None  # f32 [d_model/16][32][2] row statistics of xd (tw_gemv_packed_stats)
 
 
 class _EncoderPump:
@@ -152,6 +153,8 @@ class WhisperEngine:
             _lib.call("tw_gemm_set_group", int(os.environ["TW_GEMM_GROUP"], 0))
         if os.environ.get("TW_LN_VARIANT"):
             _lib.call("tw_ln_set_variant", int(os.environ["TW_LN_VARIANT"], 0))
+        if os.environ.get("TW_GEMV_MAX_KW"):  # A/B: 4 = decoder GEMV workgroups of at most 256 threads
+            _lib.call("tw_gemv_set_max_kw", int(os.environ["TW_GEMV_MAX_KW"], 0))
         if os.environ.get("TW_ATTN_VARIANT"):
             _lib.call("tw_attn_set_variant", int(os.environ["TW_ATTN_VARIANT"], 0))
         # encoder-attention LDS cap (16 KiB units) for chunks queued beside a decode; None: leave the library's setting
@@ -279,6 +282,9 @@ class WhisperEngine:
         # re-normalises the whole operand (LN+q/k/v 12.5 us vs 3.3 + 4.3 us as two launches; bench step 120.4 vs
         # 102.7 ms)
         self.ln_fused = self.packed_decoder and os.environ.get("TW_DEC_LNFUSE", "0") == "1"
+        # TW_DEC_LNSTATS=1: the post-attention LayerNorms carried across the kernel boundary as row statistics
+        # (tw_gemv_packed_stats -> tw_gemv_packed_lnst): 9 launches per layer instead of 11
+        self.ln_stats = self.packed_decoder and not self.ln_fused and os.environ.get("TW_DEC_LNSTATS", "0") == "1"
         self.dec_p: List[Dict[str, torch.Tensor]] = []
         self.emb_p: Optional[torch.Tensor] = None
         if self.packed_decoder:
@@ -325,6 +331,20 @@ class WhisperEngine:
         rec = self._begin_timer(("gemv_packed", epi), 2.0 * M * N * K, v.stream)
         _lib.call("tw_gemv_packed_ln", v.xd.data_ptr(), g.data_ptr(), b.data_ptr(), LN_EPS, Wp.data_ptr(), M, N, K,
                   epi, out.data_ptr(), ldo if ldo is not None else N, _lib.ptr(bias), v.stream.cuda_stream)
+        self._end_timer(rec, v.stream)
+
+    def _gemv_stats(self, A, Wp, M, N, K, v: DecView, bias):
+        """xd += A . W^T + bias (A row-major [M][K]) and the updated rows' group statistics into v.lst."""
+        rec = self._begin_timer(("gemv_packed", _lib.TW_EPI_RESID_F32), 2.0 * M * N * K, v.stream)
+        _lib.call("tw_gemv_packed_stats", A.data_ptr(), 0, K, Wp.data_ptr(), M, N, K, v.xd.data_ptr(), N,
+                  _lib.ptr(bias), v.lst.data_ptr(), v.stream.cuda_stream)
+        self._end_timer(rec, v.stream)
+
+    def _gemv_lnst(self, g, b, Wp, M, N, K, epi, out, v: DecView, bias=None):
+        """out = epi(LayerNorm(xd) . W^T + bias) with xd's row statistics from the producing GEMV (v.lst)."""
+        rec = self._begin_timer(("gemv_packed", epi), 2.0 * M * N * K, v.stream)
+        _lib.call("tw_gemv_packed_lnst", v.xd.data_ptr(), v.lst.data_ptr(), g.data_ptr(), b.data_ptr(), LN_EPS,
+                  Wp.data_ptr(), M, N, K, epi, out.data_ptr(), N, _lib.ptr(bias), v.stream.cuda_stream)
         self._end_timer(rec, v.stream)
 
     # timing-only ablations (scripts/exp: upper bounds of a fusion before building it; outputs are WRONG): a
@@ -437,13 +457,15 @@ class WhisperEngine:
             return self._chain_cache[key]
         sl = slice(r0, r0 + n)
         hp = fp = None
+        lst = None
         if self.packed_decoder and n <= 32:  # per-view packed scratch (rows 0..n-1 of the view; pad rows zero)
             hp = torch.zeros(32 * self.d.d_model, dtype=torch.bfloat16, device=self.device)
             fp = torch.zeros(32 * self.d.ffn, dtype=torch.bfloat16, device=self.device)
+            lst = torch.zeros(self.d.d_model // 16 * 32 * 2, dtype=torch.float32, device=self.device)
         return DecView(r0, n, stream or self.stream, self.xd[sl], self.hd[sl], self.qkvd[sl], self.qd[sl],
                        self.attd[sl], self.ffnd[sl], self.logits[sl],
                        self.parts if parts is None else parts, self.sel_ws[sl], self.state[sl], self.tokens[sl],
-                       self.ids[sl], self.pos[sl], hp, fp)
+                       self.ids[sl], self.pos[sl], hp, fp, lst)
 
     def use_slot(self, slot: int) -> None:
         """Point the decoder at the cross-K/V (and feature) buffers of pipeline slot `slot`."""
@@ -647,6 +669,8 @@ class WhisperEngine:
         xkv_stride = 2 * r_enc * H * S_ENC * 64
         if self.ln_fused:
             return self._decoder_layers_lnfused(R, with_logits, v, r_enc, xkv_stride)
+        if self.ln_stats:
+            return self._decoder_layers_lnstats(R, with_logits, v, r_enc, xkv_stride, pre_embedded)
         nparts, pbias = 0, None
         PART, K4 = _lib.TW_EPI_PARTIAL_F32, DEC_SPLITS
         for li, L in enumerate(w.dec):
@@ -702,6 +726,42 @@ class WhisperEngine:
             self._gemv(v.fp, True, P["w2"], R, D, F, RES, v.xd, v, bias=L.b2)
         if with_logits:
             self._resid_ln_p(R, 0, None, w.dec_ln_g, w.dec_ln_b, v)
+            self._gemv(v.hp, True, self.emb_p, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, v)
+
+    def _decoder_layers_lnstats(self, R: int, with_logits: bool, v: DecView, r_enc: int, xkv_stride: int,
+                                pre_embedded: bool) -> None:
+        """The decoder layers with the two LayerNorms after the attention blocks carried across the kernel boundary:
+        self/cross out_proj update the residual stream and write its row statistics (tw_gemv_packed_stats), and the
+        consuming projections (cross q, fc1) normalise their operand from them (tw_gemv_packed_lnst). fc2 stays a
+        split-K partial product whose sum, bias and residual add fold into the next self_attn_layer_norm launch.
+        9 launches per layer instead of 11 (WhisperDecoderLayer.forward, $TF/models/whisper/modeling_whisper.py:
+        468-505)."""
+        d, w = self.d, self.w
+        D, F, H, T = d.d_model, d.ffn, d.heads, d.max_target_positions
+        s = v.stream.cuda_stream
+        PART, K4 = _lib.TW_EPI_PARTIAL_F32, DEC_SPLITS
+        nparts, pbias = 0, None
+        for li, L in enumerate(w.dec):
+            P = self.dec_p[li]
+            if li or not pre_embedded:
+                self._resid_ln_p(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
+            self._gemv(v.hp, True, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
+            if "self" not in self._ablate:
+                _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
+                          self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
+            self._gemv_stats(v.attd, P["wo"], R, D, D, v, L.bo)
+            self._gemv_lnst(L.ln2_g, L.ln2_b, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
+            ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
+            rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, v.stream)
+            if "cross" not in self._ablate:
+                self._cross_attend(li, R, r_enc, rmap, ckv, v)
+            self._end_timer(rec, v.stream)
+            self._gemv_stats(v.attd, P["wo_x"], R, D, D, v, L.bo_x)
+            self._gemv_lnst(L.ln3_g, L.ln3_b, P["w1"], R, F, D, _lib.TW_EPI_GELU_PACKED, v.fp, v, bias=L.b1)
+            self._gemv(v.fp, True, P["w2"], R, D, F, PART, v.parts, v, splits=K4)
+            nparts, pbias = K4, L.b2
+        if with_logits:
+            self._resid_ln_p(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
             self._gemv(v.hp, True, self.emb_p, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, v)
 
     def _cross_attend(self, li: int, R: int, r_enc: int, rmap, ckv, v: DecView) -> None:
