@@ -34,4 +34,4 @@ for r in range(5):
 for v, t in res.items():
     print(f"variant {v}: min {min(t):.3f} ms = {fl / min(t) / 1e9:.0f} TF/s  max|diff vs v8| = "
           f"{(outs[v] - outs[8]).abs().max().item():.3g}")
-_lib.call("tw_attn_set_variant", 8)
+_lib.call("tw_attn_set_variant", 10)

@@ -189,10 +189,26 @@ def test_encoder_attention_vs_torch(B, L, H, variant):
     qkv[:, :D] = bf(qkv[:, :D].float() * 0.125 * 3)  # scaled q with some dynamic range
     out = torch.empty(B * L, D, dtype=torch.bfloat16, device=DEV)
     _lib.call("tw_attn_encoder", qkv.data_ptr(), B, L, H, out.data_ptr(), S())
-    _lib.call("tw_attn_set_variant", 8)
+    _lib.call("tw_attn_set_variant", 10)
     t = qkv.float().view(B, L, 3, H, 64).permute(2, 0, 3, 1, 4)
     ref = _ref_attn(t[0], t[1], t[2]).permute(0, 2, 1, 3).reshape(B * L, D)
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("B,L,H", [(2, 1500, 4), (1, 100, 2), (1, 128, 3)])
+def test_encoder_attention_enc3_bit_identical_to_enc2(B, L, H):
+    """Variant 10 (k_attn_enc3: peeled ragged tile, v_max3 chains) keeps k_attn_enc2's arithmetic exactly."""
+    D = H * 64
+    qkv = rand_bf16(B * L, 3 * D, seed=27)
+    qkv[:, :D] = bf(qkv[:, :D].float() * 0.375)
+    outs = []
+    for v in (8, 10):
+        _lib.call("tw_attn_set_variant", v)
+        out = torch.empty(B * L, D, dtype=torch.bfloat16, device=DEV)
+        _lib.call("tw_attn_encoder", qkv.data_ptr(), B, L, H, out.data_ptr(), S())
+        outs.append(out)
+    _lib.call("tw_attn_set_variant", 10)
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
 
 
 @pytest.mark.parametrize("pad", [4, 8])
@@ -221,7 +237,7 @@ def test_encoder_attention_online_softmax_rescale(variant):
     try:
         _online_softmax_rescale()
     finally:
-        _lib.call("tw_attn_set_variant", 8)
+        _lib.call("tw_attn_set_variant", 10)
 
 
 def _online_softmax_rescale():
@@ -286,7 +302,7 @@ def test_attn_decode_cross_variants(Sx, mode):
                   S())
         torch.cuda.synchronize()
     finally:
-        _lib.call("tw_attn_set_variant", 8)
+        _lib.call("tw_attn_set_variant", 10)
     for b in range(B):
         s = int(rm[b])
         ref = _ref_attn(qx[b].float().view(H, 1, 64), ckv[0, s].float(), ckv[1, s].float())[:, 0].reshape(D)

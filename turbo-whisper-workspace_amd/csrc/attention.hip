@@ -350,7 +350,8 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc2(const bf16_t* __rest
 //     instead of 32 adds + a cross-lane shuffle per tile; the rescale touches o2[0] only, the other rows stay 0);
 //   * tile maxima with v_max3_f32 (16 instead of 31 dependent maxes);
 //   * the ragged last tile (keys >= S masked) peeled out of the loop, so full tiles carry no masking code.
-// Same rounding of every product as k_attn_enc2 except the order in which the f32 row sum is accumulated.
+// Without ONES (variant 10, the default) the outputs are bit-identical to k_attn_enc2's (max is exact, the sums keep
+// its order); with ONES (variant 11) only the order of the f32 row sum differs.
 // ------------------------------------------------------------------------------------------------
 template <int NW, int WPS, bool ONES>
 __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc3(const bf16_t* __restrict__ qkv, int S, int H, int D,
@@ -448,11 +449,12 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc3(const bf16_t* __rest
       s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], EA_LOG2E, -mb));
       s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], EA_LOG2E, -mb));
     }
-    if constexpr (!ONES) {
+    if constexpr (!ONES) {  // k_attn_enc2's summation order exactly (bit-identical outputs)
       float ps = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) ps += s0[r] + s1[r];
-      l_sum += ps;  // (this lane's 32 keys; the lane pair is summed once after the loop)
+      ps += __shfl_xor(ps, 32, 64);
+      l_sum += ps;
     }
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -492,9 +494,7 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc3(const bf16_t* __rest
   if (nfull < ntile) tile(nfull & 1, nfull * EA_KT, BT{});
 
   // ONES: the row sum sits in o2[0] of lane (lr, lh = 0) (accumulator row 0); lane (lr, 1) holds row 4 = 0.
-  // Otherwise each lane of the pair (lr, lr + 32) summed its own 32 keys of every tile (same running max, so the
-  // two partial sums share one scale): add them once here.
-  const float l_run = ONES ? __shfl(o2[0], lr, 64) : l_sum + __shfl_xor(l_sum, 32, 64);
+  const float l_run = ONES ? __shfl(o2[0], lr, 64) : l_sum;
   const int q = q0 + lr;
   if (q < S) {
     const float inv = 1.f / l_run;
@@ -513,7 +513,13 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc3(const bf16_t* __rest
   }
 }
 
-static int tw_attn_variant = 8;  // 0 = k_attn_encoder, 4 / 8 = k_attn_enc2<NW>, 9 = <8> at 2 workgroups per CU
+// 0 = k_attn_encoder, 4 / 8 = k_attn_enc2<NW>, 9 = <8> at 2 workgroups per CU, 10 / 11 = k_attn_enc3 (VALU row sums /
+// MFMA row sums). Measured alone (scripts/attn_bench.py, 24 windows, MI355X): 8: 653, 10: 699, 11: 629 TF/s (11 spills
+// 16 VGPRs at the 128-register cap of two workgroups per CU).
+#ifndef TW_ATTN_DEFAULT
+#define TW_ATTN_DEFAULT 10
+#endif
+static int tw_attn_variant = TW_ATTN_DEFAULT;
 // decoder cross-attention: 1 = one pass with an online softmax (default), 0 = two passes (scores, then P.V)
 static int tw_dec_cross_1p = 1;
 // Encoder slots >= this read their cross K/V with non-temporal loads. The 737 MB of cross K/V a decode step streams
@@ -541,7 +547,7 @@ extern "C" int tw_attn_set_variant(int v) {
   tw_dec_cross_nt = (v >> 12) & 0xff ? ((v >> 12) & 0xff) - 1 : 0;
   tw_dec_cross_ng = (v & 0x200) ? 64 : 32;  // bit 9: one-pass with 512 threads (64 key groups) instead of 256
   v &= 0xff;
-  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9 || v == 10 || v == 11) ? v : 8;
+  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9 || v == 10 || v == 11) ? v : TW_ATTN_DEFAULT;
   return 0;
 }
 
