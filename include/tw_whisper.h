@@ -146,8 +146,7 @@ int tw_gemm_mx_set_variant(int v);
  * Applies to tw_gemm_bf16 and tw_gemm_mx. */
 int tw_gemm_set_group(int group_m);
 /* Measurement knob (process-wide, returns 0): the largest K-slice count (waves per column group) the packed decoder
- * GEMV picks, 1/2/4/8 (default 8; 4 keeps its workgroups at <= 256 threads, co-resident with an encoder GEMM
- * workgroup). */
+ * GEMV picks, 1/2/4/8 (default 4: workgroups of <= 256 threads, co-resident with an encoder GEMM workgroup). */
 int tw_gemv_set_max_kw(int kw);
 /* bf16 src[rows][ld] -> MX fp8 dst[rows][K] + scales (K % 128 == 0). Encoder weights once at load; the
  * attention output before out_proj (modeling_whisper.py:350-356). */

@@ -16,6 +16,8 @@ from twamd import _lib  # noqa: E402
 SHAPES = [  # name, M, N, K, epi
     ("qkv", 36000, 3840, 1280, _lib.TW_EPI_BF16),
     ("o-proj", 36000, 1280, 1280, _lib.TW_EPI_RESID_F32),
+    ("o-bf16", 36000, 1280, 1280, _lib.TW_EPI_BF16),
+    ("fc1-bf16", 36000, 5120, 1280, _lib.TW_EPI_BF16),
     ("fc1", 36000, 5120, 1280, _lib.TW_EPI_GELU_BF16),
     ("fc2", 36000, 1280, 5120, _lib.TW_EPI_RESID_F32),
     ("conv2", 36000, 1280, 3840, _lib.TW_EPI_F32),

@@ -252,6 +252,40 @@ def _online_softmax_rescale():
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("mode", [0, 0x800], ids=["one_trip", "round1"])
+def test_decode_self_attention_positions(mode):
+    """tw_attn_decode_self at positions around the one-round-trip kernel's limits (t = 0, a group boundary, 255 = its
+    last key, 256 = the first two-pass history) vs fp32 attention over the cache rows 0..t with row t appended."""
+    B, H, T = 8, 4, 448
+    D = H * 64
+    kc = torch.full((B, H, T, 64), float("nan"), dtype=torch.bfloat16, device=DEV)  # rows past t never touched
+    vc = torch.full_like(kc, float("nan"))
+    pos = torch.tensor([0, 1, 31, 32, 100, 255, 256, 447], dtype=torch.int32, device=DEV)
+    for b in range(B):
+        p = int(pos[b])
+        kc[b, :, :p] = rand_bf16(H, p, 64, seed=90 + b) if p else kc[b, :, :0]
+        vc[b, :, :p] = rand_bf16(H, p, 64, seed=190 + b) if p else vc[b, :, :0]
+    qkv = rand_bf16(B, 3 * D, seed=11)
+    out = torch.empty(B, D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_attn_set_variant", 10 | mode)
+    try:
+        _lib.call("tw_attn_decode_self", qkv.data_ptr(), B, H, T, pos.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                  out.data_ptr(), S())
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("tw_attn_set_variant", 10)
+    q = qkv.float().view(B, 3, H, 64)
+    for b in range(B):
+        p = int(pos[b])
+        assert torch.equal(kc[b, :, p], qkv[b, D:2 * D].view(H, 64))
+        assert torch.equal(vc[b, :, p], qkv[b, 2 * D:].view(H, 64))
+        k = kc[b, :, : p + 1].float()
+        v = vc[b, :, : p + 1].float()
+        ref = _ref_attn(q[b, 0][:, None, :], k, v)[:, 0].reshape(D)
+        assert torch.isfinite(out[b].float()).all()
+        torch.testing.assert_close(out[b].float(), ref, atol=1e-2, rtol=1e-2)
+
+
 def test_decode_attention_self_and_cross():
     B, H, T = 3, 4, 448
     D = H * 64

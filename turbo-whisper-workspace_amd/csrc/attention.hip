@@ -538,10 +538,12 @@ extern "C" int tw_attn_set_lds_pad(int units) {
   tw_attn_lds_pad = units;
   return 0;
 }
+static int tw_dec_self2 = 1;  // decoder self-attention in one memory round trip (k_attn_decode_self2)
 static int tw_dec_cross_lean = 1;  // the one-pass cross-attention in its small-LDS form (0: the 15 KiB form; A/B)
 extern "C" int tw_attn_set_variant(int v) {
   tw_attn_lds_pad = (v >> 20) & 0xf;  // bits 20-23
   tw_dec_cross_lean = (v & 0x400) ? 0 : 1;  // bit 10: the 15 KiB-LDS one-pass cross-attention (A/B)
+  tw_dec_self2 = (v & 0x800) ? 0 : 1;       // bit 11: the round-1 three-round-trip self-attention (A/B)
   tw_dec_cross_1p = (v & 0x100) ? 0 : 1;  // bit 8: the two-pass decoder cross-attention (A/B)
   // bits 12-19: 0 = every slot's cross K/V read non-temporally (default), else 1 + the first slot read so (0xff: none)
   tw_dec_cross_nt = (v >> 12) & 0xff ? ((v >> 12) & 0xff) - 1 : 0;
@@ -803,13 +805,125 @@ __global__ __launch_bounds__(256) void k_attn_decode_self(const bf16_t* __restri
   if (threadIdx.x < 64) out[(size_t)b * D + h * 64 + threadIdx.x] = f32_to_bf16(outv[threadIdx.x]);
 }
 
+// k_attn_decode_self2: the decoder self-attention step in ONE memory round trip for up to DS2_KEYS keys. The cached
+// K and V rows of keys 0..t-1 do not depend on this step, so their loads fly together with the loads of this token's
+// q / k / v (the q/k/v GEMV output): the key t itself is taken from the loaded row instead of a read-back of the cache
+// write. 32 groups of 8 lanes; group g holds keys u*32 + g (u < DS2_U) of K and V in registers, the scores and the
+// softmax stay in registers (block max and sum through 8 floats of LDS), P.V is reduced over the 32 groups in LDS.
+// Longer histories (t >= DS2_KEYS: never in a 30-s window's first 255 tokens) take k_attn_decode_self's two-pass
+// path in the same launch. Same products and reductions as k_attn_decode_self up to the order of the f32 sums.
+#define DS2_U 8
+#define DS2_KEYS (DS2_U * 32)
+__global__ __launch_bounds__(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__ qkv, int D, int max_pos,
+                                                           const int* __restrict__ pos, bf16_t* __restrict__ kc,
+                                                           bf16_t* __restrict__ vc, bf16_t* __restrict__ out) {
+  TW_DEC_PRIO();
+  __shared__ float part[32 * 64];
+  __shared__ float red[16];
+  __shared__ float qf[64];
+  __shared__ float outv[64];
+  __shared__ float sc[DA_SELF_MAXK];
+  const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x;
+  const int tid = threadIdx.x, g = tid >> 3, gl = tid & 7, lane = tid & 63, wid = tid >> 6;
+  const int t = pos[b];
+  const bf16_t* row = qkv + (size_t)b * 3 * D + h * 64;
+  bf16_t* K = kc + ((size_t)b * H + h) * max_pos * 64;
+  bf16_t* V = vc + ((size_t)b * H + h) * max_pos * 64;
+  if (t >= DS2_KEYS) {  // long history: the two-pass form (cache write, then K / V re-read)
+    if (tid < 64) {
+      qf[tid] = bf16_to_f32(row[tid]);
+      K[(size_t)t * 64 + tid] = row[D + tid];
+      V[(size_t)t * 64 + tid] = row[2 * D + tid];
+    }
+    __threadfence_block();
+    __syncthreads();
+    dec_attend(qf, K, V, t + 1, sc, part, red, outv);
+    if (tid < 64) out[(size_t)b * D + h * 64 + tid] = f32_to_bf16(outv[tid]);
+    return;
+  }
+  // one round trip: this token's q / k / v chunks (every group: 8 lanes x 16 B) and the cached keys < t
+  const uint4 qr = *(const uint4*)(row + gl * 8);
+  const uint4 kr = *(const uint4*)(row + D + gl * 8);
+  const uint4 vr = *(const uint4*)(row + 2 * D + gl * 8);
+  uint4 kk[DS2_U], vv[DS2_U];
+  const int last = max(t - 1, 0);
+#pragma unroll
+  for (int u = 0; u < DS2_U; ++u) {
+    const int key = min(u * 32 + g, last);
+    kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
+    vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if (g == 0) {  // the cache append (read back by the following steps only)
+    *(uint4*)(K + (size_t)t * 64 + gl * 8) = kr;
+    *(uint4*)(V + (size_t)t * 64 + gl * 8) = vr;
+  }
+  float qv[8];
+  {
+    const bf16_t* qe = (const bf16_t*)&qr;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qv[e] = bf16_to_f32(qe[e]);
+  }
+  float p[DS2_U];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < DS2_U; ++u) {
+    const int key = u * 32 + g;
+    const uint4 kx = key == t ? kr : kk[u];
+    const bf16_t* ke = (const bf16_t*)&kx;
+    float d = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
+    d += __shfl_xor(d, 1, 64);
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 4, 64);
+    p[u] = key <= t ? d : -INFINITY;
+    mx = fmaxf(mx, p[u]);
+  }
+  mx = wave_max(mx);
+  if (lane == 0) red[wid] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float sum = 0.f;
+#pragma unroll
+  for (int u = 0; u < DS2_U; ++u) {
+    p[u] = __expf(p[u] - mx);  // 0 past key t
+    if (gl == 0) sum += p[u];
+  }
+  sum = wave_sum(sum);
+  if (lane == 0) red[4 + wid] = sum;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int u = 0; u < DS2_U; ++u) {
+    if (u * 32 + g > t) continue;  // (the clamped rows past t may hold anything on the first step: never 0 * them)
+    const uint4 vx = u * 32 + g == t ? vr : vv[u];
+    const bf16_t* ve = (const bf16_t*)&vx;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += p[u] * bf16_to_f32(ve[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[g * 64 + gl * 8 + e] = acc[e];
+  __syncthreads();
+  if (tid < 64) {
+    const float inv = 1.f / (red[4] + red[5] + red[6] + red[7]);
+    float v = 0.f;
+#pragma unroll 8
+    for (int gg = 0; gg < 32; ++gg) v += part[gg * 64 + tid];
+    out[(size_t)b * D + h * 64 + tid] = f32_to_bf16(v * inv);
+  }
+}
+
 // Cross-attention step: q [B][D] bf16 (pre-scaled); cross K/V layout [kv][Bt][H][S][64] for this layer,
 // batch row b reads block row_map[b] (the encoder batch slot holding that row's audio window).
 extern "C" int tw_attn_decode_self(const bf16_t* qkv, int B, int H, int max_pos, const int* pos, bf16_t* k_cache,
                                    bf16_t* v_cache, bf16_t* out, void* stream) {
   TW_REQUIRE(qkv && pos && k_cache && v_cache && out && B > 0 && H > 0, "tw_attn_decode_self: bad args");
   TW_REQUIRE(max_pos <= DA_SELF_MAXK, "tw_attn_decode_self: max_pos %d > %d", max_pos, DA_SELF_MAXK);
-  hipLaunchKernelGGL(k_attn_decode_self, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos, pos,
+  if (tw_dec_self2)
+    hipLaunchKernelGGL(k_attn_decode_self2, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos, pos,
+                       k_cache, v_cache, out);
+  else
+    hipLaunchKernelGGL(k_attn_decode_self, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos, pos,
                      k_cache, v_cache, out);
   return tw_check_launch("tw_attn_decode_self");
 }

@@ -218,8 +218,9 @@ __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const f
 // LayerNorm reductions are wave shuffles, no LDS round trip or block barrier. A decode step runs 13 of these on 24
 // rows; the 4-wave form spends most of its ~6.8 us in its two barrier-separated reductions (tw_ln_set_variant(1)
 // restores it for A/B).
+// (min 4 waves per SIMD: <= 128 VGPRs, so a wave fits beside an encoder GEMM workgroup's two ~190-VGPR waves)
 template <bool PACKED, int NV>
-__global__ __launch_bounds__(64) void k_resid_ln_w(float* __restrict__ x, const float* __restrict__ parts, int nparts,
+__global__ __launch_bounds__(64, 4) void k_resid_ln_w(float* __restrict__ x, const float* __restrict__ parts, int nparts,
                                                    long part_stride, const float* __restrict__ bias,
                                                    const float* __restrict__ g, const float* __restrict__ bta, int D,
                                                    float eps, bf16_t* __restrict__ out) {
@@ -236,22 +237,30 @@ __global__ __launch_bounds__(64) void k_resid_ln_w(float* __restrict__ x, const 
       bb[i] = ((const float4*)bta)[lane + 64 * i];
     }
   }
-  float4 v[NV];
+  // the row, the bias and up to four partials: every load in flight before the first add (one memory round trip;
+  // the sched_barrier keeps hipcc from interleaving them with the adds, which serialises them). Summation order as
+  // before: ((x + bias) + p0) + p1 + ...
+  float4 v[NV], bv[NV], q[4][NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) v[i] = ((const float4*)xr)[lane + 64 * i];
   if (bias) {
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const float4 bb = ((const float4*)bias)[lane + 64 * i];
-      v[i].x += bb.x; v[i].y += bb.y; v[i].z += bb.z; v[i].w += bb.w;
-    }
+    for (int i = 0; i < NV; ++i) bv[i] = ((const float4*)bias)[lane + 64 * i];
   }
   if (nparts > 0) {
-    float4 q[4][NV];  // all partial loads in flight together (clamped part index, unused ones discarded)
 #pragma unroll
     for (int p = 0; p < 4; ++p)
 #pragma unroll
       for (int i = 0; i < NV; ++i) q[p][i] = ((const float4*)(pr + min(p, nparts - 1) * part_stride))[lane + 64 * i];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if (bias) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      v[i].x += bv[i].x; v[i].y += bv[i].y; v[i].z += bv[i].z; v[i].w += bv[i].w;
+    }
+  }
+  if (nparts > 0) {
 #pragma unroll
     for (int p = 0; p < 4; ++p)
       if (p < nparts)
@@ -265,6 +274,14 @@ __global__ __launch_bounds__(64) void k_resid_ln_w(float* __restrict__ x, const 
         const float4 qq = ((const float4*)(pr + p * part_stride))[lane + 64 * i];
         v[i].x += qq.x; v[i].y += qq.y; v[i].z += qq.z; v[i].w += qq.w;
       }
+  }
+  // gamma / beta (not hoisted): issued before the two reductions, so their latency hides behind them
+  if (!TW_LN_HOIST && g) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      gg[i] = ((const float4*)g)[lane + 64 * i];
+      bb[i] = ((const float4*)bta)[lane + 64 * i];
+    }
   }
   if (nparts > 0 || bias) {
 #pragma unroll
@@ -286,10 +303,6 @@ __global__ __launch_bounds__(64) void k_resid_ln_w(float* __restrict__ x, const 
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = lane + 64 * i;
-    if (!TW_LN_HOIST) {
-      gg[i] = ((const float4*)g)[c];
-      bb[i] = ((const float4*)bta)[c];
-    }
     uint2 w;
     w.x = pack_bf16x2((v[i].x - mean) * rstd * gg[i].x + bb[i].x, (v[i].y - mean) * rstd * gg[i].y + bb[i].y);
     w.y = pack_bf16x2((v[i].z - mean) * rstd * gg[i].z + bb[i].z, (v[i].w - mean) * rstd * gg[i].w + bb[i].w);

@@ -203,13 +203,15 @@ static inline int tw_group_for(int N) {
 static int tw_gemv_nt_min_n = 16384;
 static int tw_tune_skinny_nw = 0;  // 0 = heuristic; 4 / 8 / 16 force the skinny kernel's waves per block
 static int tw_tune_gemv_kw = 0;    // 0 = heuristic; 1 / 2 / 4 / 8 force the packed GEMV's K-slices per column group
-// Largest K-slice count the packed-GEMV heuristic picks (8: up to 512-thread workgroups). Capping it at 4 (256-thread
-// workgroups) makes the q/k/v GEMV co-reside with an encoder GEMM workgroup (scripts/exp/interference.py, beside
-// k_gemm_8p: 33.6 us per launch at KW = 8, 11.5 at KW = 4; alone 3.4 vs 3.7 us) but left the bench step unchanged
-// (104.7 vs 104.8 ms over three interleaved pairs), so the round-1 heuristic stays the default (A/B knob).
-static int tw_gemv_max_kw = 8;
+// Largest K-slice count the packed-GEMV heuristic picks. 4 = at most 256-thread workgroups: one decoder wave per SIMD
+// then co-resides with an encoder GEMM workgroup (2 waves of ~190 VGPRs on every SIMD), where a 512-thread decoder
+// workgroup waits for GEMM workgroups to retire (scripts/exp/interference.py, q/k/v GEMV beside k_gemm_8p: 33.6 us per
+// launch at KW = 8, 11.5 at KW = 4; alone 3.3 vs 3.6 us). With the batched GEMV loads (k_gemv_p) the bench step went
+// 104.3 -> 99.9 ms (two interleaved pairs; scripts/exp/insitu_breakdown.py: the GEMVs of a decode step beside an encoder
+// GEMM +239 us at KW = 8, +128 us at KW = 4). 8 = the round-1 heuristic (A/B).
+static int tw_gemv_max_kw = 4;
 extern "C" int tw_gemv_set_max_kw(int kw) {
-  tw_gemv_max_kw = (kw == 1 || kw == 2 || kw == 4 || kw == 8) ? kw : 8;
+  tw_gemv_max_kw = (kw == 1 || kw == 2 || kw == 4 || kw == 8) ? kw : 4;
   return 0;
 }
 extern "C" int tw_gemm_set_variant(int big) {
@@ -1648,34 +1650,47 @@ __global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __r
       if constexpr (ALN) return ldA_ln(st, 1);
       return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024 + 512) : *(const bf16x8*)(ap1 + 32 * st);
     };
-    // Batches of U steps with every load in flight before the MFMAs, then the remainder step by step (measured,
-    // scripts/gemv_bench.py: a clamped last batch instead of the step loop is 0.5-1 us SLOWER per launch).
-    int st = s0;
-    for (; st + U <= s1; st += U) {
-      bf16x8 bw[U], a0[U], a1[U];
+    auto ldW = [&](int st) -> bf16x8 {
+      if constexpr (NTW) {
+        typedef short s16x8_nt __attribute__((ext_vector_type(8)));
+        const s16x8_nt t = __builtin_nontemporal_load((const s16x8_nt*)(wp + (size_t)st * 512));
+        return __builtin_bit_cast(bf16x8, t);
+      } else {
+        return *(const bf16x8*)(wp + (size_t)st * 512);
+      }
+    };
+    // One batch of NB steps: every load of the batch issued before the first MFMA (the sched_barrier keeps hipcc
+    // from interleaving the loads with the MFMAs, which it otherwise does to save registers: 2-3 loads in flight
+    // and a dependent memory round trip per step, the latency that dominates these launches, worse still beside an
+    // encoder GEMM). n <= NB valid steps: past s1 the loads are clamped to the last step and their MFMAs skipped.
+    auto batch = [&](auto NBc, int st0, int n) {
+      constexpr int NB = decltype(NBc)::value;
+      bf16x8 bw[NB], a0[NB], a1[NB];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if constexpr (NTW) {
-          typedef short s16x8_nt __attribute__((ext_vector_type(8)));
-          const s16x8_nt t = __builtin_nontemporal_load((const s16x8_nt*)(wp + (size_t)(st + u) * 512));
-          bw[u] = __builtin_bit_cast(bf16x8, t);
-        } else {
-          bw[u] = *(const bf16x8*)(wp + (size_t)(st + u) * 512);
+      for (int u = 0; u < NB; ++u) {
+        const int st = min(st0 + u, s1 - 1);
+        bw[u] = ldW(st);
+        a0[u] = ldA0(st);
+        if (TWO) a1[u] = ldA1(st);
+      }
+      // (not on the bandwidth-bound vocabulary-wide proj_out, NTW: its 3242 waves hide the latency, and 48 live
+      // fragments cost it occupancy: 26.2 -> 30.8 us per launch alone)
+      if constexpr (!ALN && !NTW) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        if (u < n) {
+          c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], bw[u], c0, 0, 0, 0);
+          if (TWO) c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], bw[u], c1, 0, 0, 0);
         }
-        a0[u] = ldA0(st + u);
-        if (TWO) a1[u] = ldA1(st + u);
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], bw[u], c0, 0, 0, 0);
-        if (TWO) c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], bw[u], c1, 0, 0, 0);
-      }
-    }
-    for (; st < s1; ++st) {
-      const bf16x8 bw = *(const bf16x8*)(wp + (size_t)st * 512);
-      c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ldA0(st), bw, c0, 0, 0, 0);
-      if (TWO) c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ldA1(st), bw, c1, 0, 0, 0);
-    }
+    };
+    using IU = std::integral_constant<int, U>;
+    int st = s0;
+    for (; st + U <= s1; st += U) batch(IU{}, st, U);
+    const int rem = s1 - st;  // 0 .. U-1: one predicated batch of the next size up (not a step-by-step loop)
+    if (rem > U / 2) batch(IU{}, st, rem);
+    else if (rem > U / 4) batch(std::integral_constant<int, (U / 2 > 0 ? U / 2 : 1)>{}, st, rem);
+    else if (rem > 0) batch(std::integral_constant<int, (U / 4 > 0 ? U / 4 : 1)>{}, st, rem);
   }
   const int cc = lane & 15, rb = (lane >> 4) * 4;
   auto store = [&](int m, int n, float v) {

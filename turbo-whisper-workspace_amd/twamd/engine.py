@@ -153,7 +153,7 @@ class WhisperEngine:
             _lib.call("tw_gemm_set_group", int(os.environ["TW_GEMM_GROUP"], 0))
         if os.environ.get("TW_LN_VARIANT"):
             _lib.call("tw_ln_set_variant", int(os.environ["TW_LN_VARIANT"], 0))
-        if os.environ.get("TW_GEMV_MAX_KW"):  # A/B: 4 = decoder GEMV workgroups of at most 256 threads
+        if os.environ.get("TW_GEMV_MAX_KW"):  # A/B: 8 = the round-1 decoder GEMVs of up to 512 threads
             _lib.call("tw_gemv_set_max_kw", int(os.environ["TW_GEMV_MAX_KW"], 0))
         if os.environ.get("TW_ATTN_VARIANT"):
             _lib.call("tw_attn_set_variant", int(os.environ["TW_ATTN_VARIANT"], 0))
