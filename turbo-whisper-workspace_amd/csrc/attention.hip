@@ -137,8 +137,8 @@ __global__ __launch_bounds__(256) void k_attn_encoder(const bf16_t* __restrict__
       w0.y = pack_bf16x2(o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
       w1.x = pack_bf16x2(o1[4 * g] * inv, o1[4 * g + 1] * inv);
       w1.y = pack_bf16x2(o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
-      *(uint2*)(op + d) = w0;
-      *(uint2*)(op + 32 + d) = w1;
+      tw_st_enc<TW_NT_ATTN>(op + d, w0);
+      tw_st_enc<TW_NT_ATTN>(op + 32 + d, w1);
     }
   }
 }
@@ -335,8 +335,8 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc2(const bf16_t* __rest
       w0.y = pack_bf16x2(o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
       w1.x = pack_bf16x2(o1[4 * g] * inv, o1[4 * g + 1] * inv);
       w1.y = pack_bf16x2(o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
-      *(uint2*)(op + d) = w0;
-      *(uint2*)(op + 32 + d) = w1;
+      tw_st_enc<TW_NT_ATTN>(op + d, w0);
+      tw_st_enc<TW_NT_ATTN>(op + 32 + d, w1);
     }
   }
 }
@@ -507,8 +507,8 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc3(const bf16_t* __rest
       w0.y = pack_bf16x2(o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
       w1.x = pack_bf16x2(o1[4 * g] * inv, o1[4 * g + 1] * inv);
       w1.y = pack_bf16x2(o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
-      *(uint2*)(op + d) = w0;
-      *(uint2*)(op + 32 + d) = w1;
+      tw_st_enc<TW_NT_ATTN>(op + d, w0);
+      tw_st_enc<TW_NT_ATTN>(op + 32 + d, w1);
     }
   }
 }
@@ -540,6 +540,7 @@ extern "C" int tw_attn_set_lds_pad(int units) {
 }
 static int tw_dec_self2 = 1;  // decoder self-attention in one memory round trip (k_attn_decode_self2)
 static int tw_dec_cross_lean = 1;  // the one-pass cross-attention in its small-LDS form (0: the 15 KiB form; A/B)
+static int tw_dec_cross_unr = 8;   // key rows in flight per 8-lane group of the lean form (tw_attn_set_variant bits 24-27)
 extern "C" int tw_attn_set_variant(int v) {
   tw_attn_lds_pad = (v >> 20) & 0xf;  // bits 20-23
   tw_dec_cross_lean = (v & 0x400) ? 0 : 1;  // bit 10: the 15 KiB-LDS one-pass cross-attention (A/B)
@@ -548,6 +549,11 @@ extern "C" int tw_attn_set_variant(int v) {
   // bits 12-19: 0 = every slot's cross K/V read non-temporally (default), else 1 + the first slot read so (0xff: none)
   tw_dec_cross_nt = (v >> 12) & 0xff ? ((v >> 12) & 0xff) - 1 : 0;
   tw_dec_cross_ng = (v & 0x200) ? 64 : 32;  // bit 9: one-pass with 512 threads (64 key groups) instead of 256
+  // bits 24-27: key rows of loads in flight per 8-lane group in the lean cross-attention (0: 8 = DA_UNR; 1: 12, 2: 4, 3: 6)
+  {
+    const int unr[4] = {8, 12, 4, 6};
+    tw_dec_cross_unr = unr[(v >> 24) & 3];
+  }
   v &= 0xff;
   tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9 || v == 10 || v == 11) ? v : TW_ATTN_DEFAULT;
   return 0;
@@ -814,7 +820,7 @@ __global__ __launch_bounds__(256) void k_attn_decode_self(const bf16_t* __restri
 // path in the same launch. Same products and reductions as k_attn_decode_self up to the order of the f32 sums.
 #define DS2_U 8
 #define DS2_KEYS (DS2_U * 32)
-__global__ __launch_bounds__(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__ qkv, int D, int max_pos,
+__global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__ qkv, int D, int max_pos,
                                                            const int* __restrict__ pos, bf16_t* __restrict__ kc,
                                                            bf16_t* __restrict__ vc, bf16_t* __restrict__ out) {
   TW_DEC_PRIO();
@@ -977,8 +983,8 @@ __global__ __launch_bounds__(NG * 8) void k_attn_decode_cross(const bf16_t* __re
 // workgroups of a decode step took two rounds; these fit several per CU. q comes straight from global memory (each
 // lane its 8 dims), and the 8 key groups of a wave merge their online-softmax states with xor shuffles (lanes of one
 // dim slice: xor 8, 16, 32) before one LDS record per wave; one wave merges the NG/8 records.
-template <int NG, bool NT>
-__global__ __launch_bounds__(NG * 8) void k_attn_decode_cross_lean(const bf16_t* __restrict__ q, int D, int S, int Bt,
+template <int NG, bool NT, int UNR = DA_UNR>
+__global__ TW_DEC_LB(NG * 8, UNR <= 4 ? 7 : 1) void k_attn_decode_cross_lean(const bf16_t* __restrict__ q, int D, int S, int Bt,
                                                                 const int* __restrict__ row_map,
                                                                 const bf16_t* __restrict__ ckv,
                                                                 bf16_t* __restrict__ out) {
@@ -1001,10 +1007,10 @@ __global__ __launch_bounds__(NG * 8) void k_attn_decode_cross_lean(const bf16_t*
   float m = -INFINITY, l = 0.f;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int nit = (S + NG - 1) / NG;
-  for (int it0 = 0; it0 < nit; it0 += DA_UNR) {
-    uint4 kk[DA_UNR], vv[DA_UNR];
+  for (int it0 = 0; it0 < nit; it0 += UNR) {
+    uint4 kk[UNR], vv[UNR];
 #pragma unroll
-    for (int u = 0; u < DA_UNR; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       const int key = min((it0 + u) * NG + g, S - 1);
       if constexpr (NT) {
         typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
@@ -1017,11 +1023,11 @@ __global__ __launch_bounds__(NG * 8) void k_attn_decode_cross_lean(const bf16_t*
         vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
       }
     }
-    __builtin_amdgcn_sched_barrier(0);  // all 2 x DA_UNR loads in flight before the first is consumed
-    float sv[DA_UNR];
+    __builtin_amdgcn_sched_barrier(0);  // all 2 x UNR loads in flight before the first is consumed
+    float sv[UNR];
     float bm = m;
 #pragma unroll
-    for (int u = 0; u < DA_UNR; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       const bf16_t* ke = (const bf16_t*)&kk[u];
       float d = 0.f;
 #pragma unroll
@@ -1038,7 +1044,7 @@ __global__ __launch_bounds__(NG * 8) void k_attn_decode_cross_lean(const bf16_t*
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] *= sc;
 #pragma unroll
-    for (int u = 0; u < DA_UNR; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       const float p = __expf(sv[u] - bm);  // 0 for the masked keys
       l += p;
       const bf16_t* ve = (const bf16_t*)&vv[u];
@@ -1088,8 +1094,18 @@ extern "C" int tw_attn_decode_cross(const bf16_t* q, int B, int H, int S, int Bt
   TW_REQUIRE(q && cross_kv && out && B > 0 && H > 0 && S > 0 && S <= DA_MAXK, "tw_attn_decode_cross: bad args");
   if (tw_dec_cross_lean && tw_dec_cross_1p && tw_dec_cross_ng == 32 && tw_dec_cross_nt == 0) {
     // (every slot non-temporal: the default; the per-slot nt split of the A/B knob stays on the 15 KiB kernel)
-    hipLaunchKernelGGL((k_attn_decode_cross_lean<32, true>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64,
-                       S, Bt, row_map, cross_kv, out);
+    if (tw_dec_cross_unr == 12)
+      hipLaunchKernelGGL((k_attn_decode_cross_lean<32, true, 12>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, q,
+                         H * 64, S, Bt, row_map, cross_kv, out);
+    else if (tw_dec_cross_unr == 4)
+      hipLaunchKernelGGL((k_attn_decode_cross_lean<32, true, 4>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, q,
+                         H * 64, S, Bt, row_map, cross_kv, out);
+    else if (tw_dec_cross_unr == 6)
+      hipLaunchKernelGGL((k_attn_decode_cross_lean<32, true, 6>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, q,
+                         H * 64, S, Bt, row_map, cross_kv, out);
+    else
+      hipLaunchKernelGGL((k_attn_decode_cross_lean<32, true>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64,
+                         S, Bt, row_map, cross_kv, out);
     return tw_check_launch("tw_attn_decode_cross");
   }
   if (tw_dec_cross_ng == 64 && tw_dec_cross_1p)

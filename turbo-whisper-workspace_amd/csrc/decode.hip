@@ -61,7 +61,7 @@ __device__ inline RowMask row_mask(const int* st, const TwSelectParams& p) {
 }
 
 // grid (B, TW_SELECT_CHUNKS): chunk c of row b scans vocab [c*V/NC, (c+1)*V/NC) with float4 loads where aligned.
-__global__ __launch_bounds__(256) void k_select_partial(const float* __restrict__ logits, int ld_logits,
+__global__ TW_DEC_LB(256, 1) void k_select_partial(const float* __restrict__ logits, int ld_logits,
                                                         const uint32_t* __restrict__ suppress_bits, TwSelectParams p,
                                                         const int* __restrict__ state, SelPart* __restrict__ ws) {
   TW_DEC_PRIO();
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(64) void k_select_final(const SelPart* __restrict__
 // partials). Replaces three launches per generated token with one; the results are those of the three.
 #define SFE_MAXV 4  // float4 chunks per thread: D <= 4096
 template <bool PACKED>
-__global__ __launch_bounds__(256) void k_select_final_embed(const SelPart* __restrict__ ws, int NC, TwSelectParams p,
+__global__ TW_DEC_LB(256, 1) void k_select_final_embed(const SelPart* __restrict__ ws, int NC, TwSelectParams p,
                                                             int* __restrict__ state, int* __restrict__ tokens_out,
                                                             int ld_tokens, int* __restrict__ next_ids,
                                                             int* __restrict__ pos, const bf16_t* __restrict__ tok_emb,

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, 
       uint2 w;
       w.x = pack_bf16x2((v[i].x - mean) * rstd * gg[i].x + bb[i].x, (v[i].y - mean) * rstd * gg[i].y + bb[i].y);
       w.y = pack_bf16x2((v[i].z - mean) * rstd * gg[i].z + bb[i].z, (v[i].w - mean) * rstd * gg[i].w + bb[i].w);
-      orow[c] = w;
+      tw_st_enc<TW_NT_LN>(orow + c, w);
     }
   }
 }
@@ -126,7 +126,7 @@ __global__ void k_im2col_conv2(const bf16_t* __restrict__ h1, int R, int D, bf16
     const int u = 2 * t + j - 1;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (u >= 0 && u < 3000) v = *(const uint4*)(h1 + ((size_t)r * 3000 + u) * D + c);
-    *(uint4*)(out + (size_t)m * 3 * D + k) = v;
+    tw_st_enc<TW_NT_IM2COL>(out + (size_t)m * 3 * D + k, v);
   }
 }
 
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const f
 // restores it for A/B).
 // (min 4 waves per SIMD: <= 128 VGPRs, so a wave fits beside an encoder GEMM workgroup's two ~190-VGPR waves)
 template <bool PACKED, int NV>
-__global__ __launch_bounds__(64, 4) void k_resid_ln_w(float* __restrict__ x, const float* __restrict__ parts, int nparts,
+__global__ TW_DEC_LB(64, 4) void k_resid_ln_w(float* __restrict__ x, const float* __restrict__ parts, int nparts,
                                                    long part_stride, const float* __restrict__ bias,
                                                    const float* __restrict__ g, const float* __restrict__ bta, int D,
                                                    float eps, bf16_t* __restrict__ out) {

@@ -246,6 +246,9 @@ extern "C" int tw_gemm_set_variant(int big) {
 #ifndef GB_A_POL
 #define GB_A_POL 0  // cache policy of k_gemm_big's activation-operand DMA (experiment builds: 2 = nt)
 #endif
+#ifndef GB_BIG_PADV
+#define GB_BIG_PADV 0
+#endif
 #define GB_EPI_LD 68  // f32 row stride of the epilogue staging image (64 + 4: conflict-free writes)
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -253,6 +256,12 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 __device__ inline int gb_swz(int r) { return (r >> 1) & 7; }
 
 // epilogue of 4 consecutive columns n..n+3 of row m (v already includes the bias)
+// TW_ENC_NT producer bit of a large-M GEMM epilogue
+constexpr int gb_nt_bit(int epi) {
+  return epi == TW_EPI_BF16 ? TW_NT_GEMM_BF16 : epi == TW_EPI_GELU_BF16 ? TW_NT_GEMM_GELU
+         : epi == TW_EPI_RESID_F32 ? TW_NT_GEMM_RESID : TW_NT_GEMM_OTHER;
+}
+
 template <int EPI>
 __device__ inline void epi_store4(const EpiArgs& ea, int m, int n, int N, float4 v) {
   if (n + 3 >= N) {  // ragged right edge (tests only: the model's N are multiples of 256)
@@ -268,19 +277,19 @@ __device__ inline void epi_store4(const EpiArgs& ea, int m, int n, int N, float4
     uint2 w;
     w.x = pack_bf16x2(v.x, v.y);
     w.y = pack_bf16x2(v.z, v.w);
-    *(uint2*)((bf16_t*)ea.out + (size_t)m * ea.ldo + n) = w;
+    tw_st_enc<gb_nt_bit(EPI)>((bf16_t*)ea.out + (size_t)m * ea.ldo + n, w);
   } else if constexpr (EPI == TW_EPI_RESID_F32) {
     float4* o = (float4*)((float*)ea.out + (size_t)m * ea.ldo + n);
     float4 x = *o;
     x.x += v.x; x.y += v.y; x.z += v.z; x.w += v.w;
-    *o = x;
+    tw_st_enc<gb_nt_bit(EPI)>(o, x);
   } else if constexpr (EPI == TW_EPI_GELU_POS_F32) {
     const float4 a = *(const float4*)(ea.aux + (size_t)(m % ea.aux_rows) * ea.ldo + n);
     float4 o = gelu_erf4(v);
     o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
-    *(float4*)((float*)ea.out + (size_t)m * ea.ldo + n) = o;
+    tw_st_enc<gb_nt_bit(EPI)>((float*)ea.out + (size_t)m * ea.ldo + n, o);
   } else if constexpr (EPI == TW_EPI_F32) {
-    *(float4*)((float*)ea.out + (size_t)m * ea.ldo + n) = v;
+    tw_st_enc<gb_nt_bit(EPI)>((float*)ea.out + (size_t)m * ea.ldo + n, v);
   } else if constexpr (EPI == TW_EPI_CROSSKV) {
     const int D = ea.kv_D, S = ea.kv_S;
     int l = n / (2 * D), rem = n - l * 2 * D;
@@ -291,7 +300,7 @@ __device__ inline void epi_store4(const EpiArgs& ea, int m, int n, int N, float4
     uint2 w;
     w.x = pack_bf16x2(v.x, v.y);
     w.y = pack_bf16x2(v.z, v.w);
-    *(uint2*)((bf16_t*)ea.out + idx) = w;
+    tw_st_enc<gb_nt_bit(EPI)>((bf16_t*)ea.out + idx, w);
   }
 }
 
@@ -308,7 +317,7 @@ template <int EPI>
 __device__ inline void epi_store4_pre(const EpiArgs& ea, int m, int n, float4 v, float4 a) {
   if constexpr (EPI == TW_EPI_GELU_POS_F32) v = gelu_erf4(v);
   v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
-  *(float4*)((float*)ea.out + (size_t)m * ea.ldo + n) = v;
+  tw_st_enc<gb_nt_bit(EPI)>((float*)ea.out + (size_t)m * ea.ldo + n, v);
 }
 
 // epilogue of 8 consecutive columns n..n+7 of row m (v already includes the bias): one 16-byte store for the bf16
@@ -344,7 +353,7 @@ __device__ inline void epi_store8(const EpiArgs& ea, int m, int n, int N, float4
       } else {
         idx = (size_t)m * ea.ldo + n;
       }
-      *(uint4*)((bf16_t*)ea.out + idx) = w;
+      tw_st_enc<gb_nt_bit(EPI)>((bf16_t*)ea.out + idx, w);
       return;
     }
   }
@@ -470,6 +479,14 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ 
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / GB_BK;
+#if GB_BIG_PADV
+  // diagnostic builds only: GB_BIG_PADV dummy registers live across the K loop (co-residency experiments)
+  float padv[GB_BIG_PADV];
+#pragma unroll
+  for (int i = 0; i < GB_BIG_PADV; ++i) padv[i] = (float)(lane * (i + 1));
+#pragma unroll
+  for (int i = 0; i < GB_BIG_PADV; ++i) asm volatile("" : "+v"(padv[i]));
+#endif
   stage(0, 0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
@@ -496,6 +513,10 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ 
     }
     __syncthreads();  // vmcnt(0) (tile kt+1 landed) + lgkmcnt(0) + barrier
   }
+#if GB_BIG_PADV
+#pragma unroll
+  for (int i = 0; i < GB_BIG_PADV; ++i) asm volatile("" : "+v"(padv[i]));
+#endif
 
   gemm_epi_128x64<EPI>(acc, (float*)smem + wid * (64 * GB_EPI_LD), lane, m0 + wr * 128, n0 + wc * 64, M, N, ea);
 }
@@ -1527,7 +1548,7 @@ struct LnArgs {
 // NTW: weight fragments read with non-temporal loads (proj_out: 133 MB streamed once per step, kept out of the
 // caches so that the layer weights can stay in them).
 template <int EPI, int KW, int U, bool APACK, bool TWO, bool NTW = false, bool ALN = false>
-__global__ __launch_bounds__(KW > 4 ? 512 : 256) void k_gemv_p(const bf16_t* __restrict__ A, int lda,
+__global__ TW_DEC_LB(KW > 4 ? 512 : 256, 1) void k_gemv_p(const bf16_t* __restrict__ A, int lda,
                                                                const bf16_t* __restrict__ Wp, int M, int N, int K,
                                                                EpiArgs ea, LnArgs la = LnArgs{}) {
   TW_DEC_PRIO();

@@ -140,6 +140,50 @@ __device__ inline float f32_from_order_key(uint32_t k) {
 
 // Decoder kernels raise their waves' issue priority so that, sharing CUs with the encoder GEMM of the next
 // window batch, their (latency-bound) instructions are picked first. Compile-time knob for A/B builds.
+// Encoder-side bulk outputs stored with the non-temporal hint, by producer (TW_ENC_NT bit mask): they are far larger
+// than the L2s, and streaming them keeps the L2s free of dirty lines, which every kernel boundary of the concurrently
+// running decoder step otherwise has to write back. Bits: 0 GEMM bf16 (q/k/v), 1 GEMM GELU (fc1), 2 GEMM residual
+// update (out_proj, fc2), 3 other GEMM epilogues (conv stem, cross K/V), 4 attention output, 5 LayerNorm output,
+// 6 conv2 im2col. Measured in the bench (10 steps, two interleaved rounds per build, MI355X): GEMM epilogues except
+// the residual update (0x0B) 92.9 ms vs 93.8 ms with none; all GEMM epilogues (0x0F) 93.1; adding the attention,
+// LayerNorm and im2col outputs (0x7F) 94.6 vs 93.4 (the next GEMM re-reads those as its A operand). In situ (scripts/
+// exp/insitu_breakdown.py) the decode step beside the fc1 GEMM went 849 -> 772 us with the GEMM bits set.
+// Write-through (device-scope sc1) stores instead were slower for every producer set tried (94.6-99.0 vs 93.0 ms).
+#define TW_NT_GEMM_BF16 1
+#define TW_NT_GEMM_GELU 2
+#define TW_NT_GEMM_RESID 4
+#define TW_NT_GEMM_OTHER 8
+#define TW_NT_ATTN 16
+#define TW_NT_LN 32
+#define TW_NT_IM2COL 64
+#ifndef TW_ENC_NT
+#define TW_ENC_NT (TW_NT_GEMM_BF16 | TW_NT_GEMM_GELU | TW_NT_GEMM_OTHER)
+#endif
+typedef unsigned int tw_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int tw_u32x4 __attribute__((ext_vector_type(4)));
+typedef float tw_f32x4 __attribute__((ext_vector_type(4)));
+template <int BIT>
+__device__ inline void tw_st_enc(void* p, uint2 w) {
+  if (TW_ENC_NT & BIT) __builtin_nontemporal_store((tw_u32x2){w.x, w.y}, (tw_u32x2*)p);
+  else *(uint2*)p = w;
+}
+template <int BIT>
+__device__ inline void tw_st_enc(void* p, uint4 w) {
+  if (TW_ENC_NT & BIT) __builtin_nontemporal_store((tw_u32x4){w.x, w.y, w.z, w.w}, (tw_u32x4*)p);
+  else *(uint4*)p = w;
+}
+template <int BIT>
+__device__ inline void tw_st_enc(void* p, float4 v) {
+  if (TW_ENC_NT & BIT) __builtin_nontemporal_store((tw_f32x4){v.x, v.y, v.z, v.w}, (tw_f32x4*)p);
+  else *(float4*)p = v;
+}
+
+// Minimum waves per SIMD the decoder-step kernels are compiled for (0: each kernel's own default). Experiment builds
+// (-DTW_DEC_WPE=6: <= 80 VGPRs) test decoder co-residency beside a fatter encoder GEMM (k_gemm_8p: 2 x 216 VGPRs).
+#ifndef TW_DEC_WPE
+#define TW_DEC_WPE 0
+#endif
+#define TW_DEC_LB(threads, wpe) __launch_bounds__(threads, TW_DEC_WPE ? TW_DEC_WPE : (wpe))
 #ifndef TW_DEC_PRIORITY
 #define TW_DEC_PRIORITY 3
 #endif

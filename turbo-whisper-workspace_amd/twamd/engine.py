@@ -159,7 +159,7 @@ class WhisperEngine:
             _lib.call("tw_attn_set_variant", int(os.environ["TW_ATTN_VARIANT"], 0))
         # encoder-attention LDS cap (16 KiB units) for chunks queued beside a decode; None: leave the library's setting
         pad = os.environ.get("TW_ATTN_PAD", "4")
-        self._attn_pad_ctx = None if pad == "" or os.environ.get("TW_ATTN_VARIANT") else int(pad)
+        self._attn_pad_ctx = None if pad == "" else int(pad)
         d = weights.dims
         d.validate()
         self.d, self.w, self.gen = d, weights, gen
