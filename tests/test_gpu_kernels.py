@@ -64,7 +64,7 @@ def test_logmel_vs_oracle(n_mels):
 EPIS = [_lib.TW_EPI_BF16, _lib.TW_EPI_GELU_BF16, _lib.TW_EPI_RESID_F32, _lib.TW_EPI_F32]
 
 
-@pytest.mark.parametrize("variant", [1, 5, 6, 8, 3, 4, 0])
+@pytest.mark.parametrize("variant", [1, 9, 5, 6, 8, 3, 4, 0])
 @pytest.mark.parametrize("M,N,K", [(300, 384, 256), (1500, 1280, 1280), (24, 1280, 1280), (7, 51866, 384),
                                    (32, 5120, 1280), (129, 200, 64), (600, 512, 192), (257, 768, 3840)])
 @pytest.mark.parametrize("epi", EPIS)
@@ -132,7 +132,33 @@ def _test_resid_layernorm_vs_torch(M, D, nparts):
     torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("variant", [1, 5, 8])
+@pytest.mark.parametrize("M,N,K", [(36000, 1280, 1280), (4000, 3840, 1280), (3000, 1280, 5120), (769, 512, 128)])
+@pytest.mark.parametrize("epi", [_lib.TW_EPI_BF16, _lib.TW_EPI_RESID_F32])
+def test_gemm_kh_bitexact_vs_big(M, N, K, epi):
+    """k_gemm_kh (variant 9: K-half LDS slots, 1.5 K-tiles of DMA in flight, counted vmcnt + raw barriers) makes
+    the same MFMA calls in the same order per accumulator as k_gemm_big: outputs bit-identical, on every repeat (a
+    slot read before its DMA landed, or refilled while still read, would show as a mismatch)."""
+    A = rand_bf16(M, K, seed=11)
+    W = rand_bf16(N, K, scale=K ** -0.5, seed=12)
+    bias = torch.randn(N, device=DEV) * 0.1
+    dt = torch.bfloat16 if epi == _lib.TW_EPI_BF16 else torch.float32
+    base = torch.randn(M, N, device=DEV).to(dt)
+    outs = {}
+    try:
+        for v in (1, 9, 9, 9):
+            _lib.call("tw_gemm_set_variant", v)
+            out = base.clone()
+            _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, K, K, epi, out.data_ptr(), N,
+                      bias.data_ptr(), None, 0, None, S())
+            torch.cuda.synchronize()
+            outs.setdefault(v, []).append(out)
+    finally:
+        _lib.call("tw_gemm_set_variant", 1)
+    for o in outs[9]:
+        assert torch.equal(o, outs[1][0])
+
+
+@pytest.mark.parametrize("variant", [1, 9, 5, 8])
 def test_gemm_gelu_pos_and_crosskv(variant):
     _lib.call("tw_gemm_set_variant", variant)
     try:

@@ -361,6 +361,22 @@ __device__ inline void epi_store8(const EpiArgs& ea, int m, int n, int N, float4
   if (n + 4 < N) epi_store4<EPI>(ea, m, n + 4, N, v1);
 }
 
+#ifndef GB_EPI_BLOCKSYNC
+#define GB_EPI_BLOCKSYNC 0  // 1: block barriers around the epilogue staging (the round-1 form; A/B builds)
+#endif
+// Ordering between a wave's own epilogue-image writes and reads: every wave stages through its own LDS region, and
+// LDS instructions of one wave execute in issue order, so a compiler fence (plus the LDS count) is enough; block
+// barriers here only made the 8 waves of a tile wait for each other (and, beside a running decode step, for the
+// wave the decoder's waves slow down most).
+__device__ inline void gb_epi_sync() {
+  if (GB_EPI_BLOCKSYNC) {
+    __syncthreads();
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // Epilogue of one wave's 128 x 64 sub-tile (rows mw0.., columns ncol0..) held as 8 x 4 16x16 MFMA accumulators,
 // through the wave's own [64][GB_EPI_LD] f32 LDS image `wimg` (shared by k_gemm_big and k_gemm_h; every wave of the
 // block calls it: it holds block barriers). The caller's K loop must have ended on a barrier.
@@ -395,14 +411,14 @@ __device__ inline void gemm_epi_128x64(const f32x4 (&acc)[8][4], float* wimg, in
 #pragma unroll
       for (int q = 0; q < 8; ++q) ad[q] = epi_addend<EPI>(ea, min(mrow0 + q * 4 + (lane >> 4), M - 1), ncol0 + rc, full);
     }
-    if (half) __syncthreads();  // (first pass: the K loop ended on a barrier)
+    if (half) gb_epi_sync();  // (first pass: the K loop ended on a barrier)
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) wimg[(ii * 16 + fq * 4 + r) * GB_EPI_LD + j * 16 + fr] = acc[ib + ii][j][r];
-    __syncthreads();
+    gb_epi_sync();
     if constexpr (PRE) {
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
@@ -517,6 +533,124 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ 
 #pragma unroll
   for (int i = 0; i < GB_BIG_PADV; ++i) asm volatile("" : "+v"(padv[i]));
 #endif
+
+  gemm_epi_128x64<EPI>(acc, (float*)smem + wid * (64 * GB_EPI_LD), lane, m0 + wr * 128, n0 + wc * 64, M, N, ea);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_gemm_kh: k_gemm_big's tile, waves, fragments and epilogue (so the same ~184 VGPRs: beside a running decode step
+// every SIMD keeps room for one decoder wave, DESIGN §4 "Round 2") with a deeper DMA pipeline. The LDS image is split
+// by K-half: slot (buffer, half) holds the A and W rows of one 32-deep half of a 64-deep K-tile as [256 rows][64 B]
+// (chunk swizzle c ^ ((row >> 2) & 3): a ds_read_b128 fragment's 16 rows hit 16 distinct bank groups). The loop runs
+// over half-steps u = 2t + h: wait for half u's DMA (counted vmcnt, 2 halves left in flight), one raw barrier, issue
+// the DMA of half u + 3 into the slot half u - 1 just released, then 32 MFMAs per wave on half u. A half is issued
+// 1.5 K-tiles before it is read (k_gemm_big: one K-tile), at two barriers per K-tile instead of one; no ordinary
+// global load sits in the loop, so hipcc's waits stay the counted ones.
+// ------------------------------------------------------------------------------------------------
+// Buffer descriptor from values the compiler can prove wave-uniform (readfirstlane'd base halves and size): the
+// descriptor then lives in SGPRs and every buffer op through it is one instruction, not a waterfall loop.
+__device__ inline __amdgpu_buffer_rsrc_t tw_uniform_rsrc(const void* p, int bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+__device__ inline int gk_swz(int r) { return (r >> 2) & 3; }
+
+template <int N>
+__device__ inline void gk_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm_kh(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                    int M, int N, int K, int lda, int ldw, EpiArgs ea) {
+  // 4 slots x [A | W][256 rows x 32 k] bf16 = 128 KiB for the K loop; 8 x [64][68] f32 = 136 KiB after it (one array)
+  __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 64 * GB_EPI_LD * 2];
+  constexpr int SLOT = 2 * GB_BM * 32;  // bf16 elements per slot (A rows, then W rows)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntm = (M + GB_BM - 1) / GB_BM, ntn = (N + GB_BN - 1) / GB_BN;
+  const int nwg = ntm * ntn;
+  const int orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  int tm, tn;
+  tw_tile_grouped(wgid, ntm, ntn, ea.group_m, tm, tn);
+  const int m0 = tm * GB_BM, n0 = tn * GB_BN;
+
+  // DMA: per half, wave w issues instructions i = 0, 1 for A and for W; instruction (w, i) fills rows
+  // 16 (2w + i) .. + 15 (16 rows x 64 B = 1 KiB). Lane l: row 16 (2w + i) + (l >> 2), LDS chunk slot l & 3 <- global
+  // chunk (l & 3) ^ gk_swz(row). Buffer descriptors (rows past M / N read as zeros; never stored) keep the per-lane
+  // part a 32-bit offset.
+  const __amdgpu_buffer_rsrc_t rsA = tw_uniform_rsrc(A + (size_t)m0 * lda, max(0, min(GB_BM, M - m0)) * lda * 2);
+  const __amdgpu_buffer_rsrc_t rsW = tw_uniform_rsrc(W + (size_t)n0 * ldw, max(0, min(GB_BN, N - n0)) * ldw * 2);
+  unsigned va[2], vw[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * (2 * wid + i) + (lane >> 2);
+    const int ch = (lane & 3) ^ gk_swz(row);
+    va[i] = (unsigned)(row * lda + ch * 8) * 2u;
+    vw[i] = (unsigned)(row * ldw + ch * 8) * 2u;
+  }
+  auto issue = [&](int u) {  // DMA of half-step u (K-tile u >> 1, half u & 1) into slot u & 3
+    bf16_t* As = smem + (u & 3) * SLOT;
+    bf16_t* Ws = As + GB_BM * 32;
+    const unsigned ko = (unsigned)(u * 32) * 2u;  // K offset (bytes) of this half
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rb = 16 * (2 * wid + i) * 32;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void_t*)(As + rb), 16, va[i], ko, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (lds_void_t*)(Ws + rb), 16, vw[i], ko, 0, 0);
+    }
+  };
+
+  const int wr = wid >> 2, wc = wid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int u) {
+    const bf16_t* As = smem + (u & 3) * SLOT;
+    const bf16_t* Ws = As + GB_BM * 32;
+    bf16x8 bfr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = wc * 64 + j * 16 + fr;
+      bfr[j] = *(const bf16x8*)(Ws + col * 32 + ((fq ^ gk_swz(col)) << 3));
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = wr * 128 + i * 16 + fr;
+      const bf16x8 af = *(const bf16x8*)(As + row * 32 + ((fq ^ gk_swz(row)) << 3));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  const int nh = 2 * (K / GB_BK);  // half-steps (the launcher guarantees nh >= 4)
+  issue(0);
+  issue(1);
+  issue(2);
+  // one half-step per iteration: half u landed (this wave's DMA by the count, every wave's by the barrier), then the
+  // slot of half u - 1 is free for half u + 3. One copy of the body (a peeled tail makes the register allocator copy
+  // the accumulators: 244 instead of ~184 VGPRs); the count drops to 4 / 0 on the last two halves (scalar branches).
+  for (int u = 0; u < nh; ++u) {
+    if (u < nh - 2) gk_vmcnt<8>();
+    else if (u == nh - 2) gk_vmcnt<4>();
+    else gk_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (u + 3 < nh) issue(u + 3);
+    compute(u);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __syncthreads();  // every wave done with the K-loop slots before the epilogue images reuse them
 
   gemm_epi_128x64<EPI>(acc, (float*)smem + wid * (64 * GB_EPI_LD), lane, m0 + wr * 128, n0 + wc * 64, M, N, ea);
 }
@@ -767,15 +901,6 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ns(const bf16_t* __restrict__ A
 //   RAW: a half-tile is waited for (vmcnt) before the first barrier of the phase before the one that reads it.
 //   WAR: a half-tile is restaged >= 2 phases after its last ds_read (A0 4, B0 2, B1 4, A1 4).
 // ------------------------------------------------------------------------------------------------
-// Buffer descriptor from values the compiler can prove wave-uniform (readfirstlane'd base halves and size): the
-// descriptor then lives in SGPRs and every buffer op through it is one instruction, not a waterfall loop.
-__device__ inline __amdgpu_buffer_rsrc_t tw_uniform_rsrc(const void* p, int bytes) {
-  const unsigned long long a = (unsigned long long)p;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0,
-                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
 template <int N>
 __device__ inline void p8_vmcnt() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -960,7 +1085,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
         ad[q][1] = epi_addend<EPI>(ea, mq, ncol + 4, full);
       }
     }
-    if (mh) __syncthreads();
+    if (mh) gb_epi_sync();
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -970,7 +1095,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             wimg[(i * 16 + fq * 4 + r) * GB_EPI_LD + nh * 32 + j * 16 + fr] = acc[mh][nh][i][j][r];
-    __syncthreads();
+    gb_epi_sync();
 #pragma unroll
     for (int rr = 0; rr < 8; ++rr) {
       const int lr = rr * 8 + (lane >> 3);
@@ -1890,6 +2015,9 @@ static int launch_gemm(const bf16_t* A, const bf16_t* W, int M, int N, int K, in
     } else if (tw_gemm_big_enabled == 5) {
       unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
       hipLaunchKernelGGL(k_gemm_8p<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
+    } else if (tw_gemm_big_enabled == 9 && K >= 2 * GB_BK) {
+      unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
+      hipLaunchKernelGGL(k_gemm_kh<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
     } else if (tw_gemm_big_enabled == 8) {
       unsigned nwg = tw_cdiv(M, 256) * tw_cdiv(N, 256);
       hipLaunchKernelGGL(k_gemm_4w<EPI>, dim3(nwg), dim3(256), 0, s, A, W, M, N, K, lda, ldw, ea);

@@ -145,6 +145,9 @@ class WhisperEngine:
         # beside a running decode it slows the latency-bound decoder kernels more than it gains (bench step 117.1 vs
         # 113.4 ms). An encoder that runs alone uses 5, one queued beside a decode (run_batches' overlap) uses 1.
         self._gemm_variant_fixed = bool(os.environ.get("TW_GEMM_VARIANT"))
+        # large-M GEMM kernel per context (tw_gemm_set_variant): alone = no decode beside the encoder chunk
+        self._gemm_alone = int(os.environ.get("TW_GEMM_ALONE", "5"), 0)
+        self._gemm_beside = int(os.environ.get("TW_GEMM_BESIDE", "1"), 0)
         if self._gemm_variant_fixed:
             _lib.call("tw_gemm_set_variant", int(os.environ["TW_GEMM_VARIANT"], 0))
         if os.environ.get("TW_GEMM_MX_VARIANT"):
@@ -501,7 +504,7 @@ class WhisperEngine:
         kernels then find free wave slots; measured decoder GEMV 21.9 -> 5.6 us per launch beside it, bench step
         112.1 -> 108.5 ms), uncapped alone (the cap costs the attention itself 22 %)."""
         if not self._gemm_variant_fixed:
-            _lib.call("tw_gemm_set_variant", 5 if alone else 1)
+            _lib.call("tw_gemm_set_variant", self._gemm_alone if alone else self._gemm_beside)
         if self._attn_pad_ctx is not None:
             _lib.call("tw_attn_set_lds_pad", 0 if alone else self._attn_pad_ctx)
 
