@@ -201,8 +201,12 @@ static inline int tw_group_for(int N) {
 }
 // packed GEMVs with N >= this (proj_out) read their weights non-temporally: bench step -1 ms (109.2 vs 110.3)
 static int tw_gemv_nt_min_n = 16384;
+#ifndef TW_PROJ_KW_DEFAULT
+#define TW_PROJ_KW_DEFAULT 1
+#endif
 static int tw_tune_skinny_nw = 0;  // 0 = heuristic; 4 / 8 / 16 force the skinny kernel's waves per block
 static int tw_tune_gemv_kw = 0;    // 0 = heuristic; 1 / 2 / 4 / 8 force the packed GEMV's K-slices per column group
+static int tw_proj_kw = TW_PROJ_KW_DEFAULT;  // K-slices per column group of the vocabulary-wide proj_out (1 / 2 / 4)
 // Largest K-slice count the packed-GEMV heuristic picks. 4 = at most 256-thread workgroups: one decoder wave per SIMD
 // then co-resides with an encoder GEMM workgroup (2 waves of ~190 VGPRs on every SIMD), where a 512-thread decoder
 // workgroup waits for GEMM workgroups to retire (scripts/exp/interference.py, q/k/v GEMV beside k_gemm_8p: 33.6 us per
@@ -219,6 +223,10 @@ extern "C" int tw_gemm_set_variant(int big) {
   const int nw = (big >> 8) & 0xff;
   tw_tune_skinny_nw = (nw == 4 || nw == 8 || nw == 16) ? nw : 0;
   tw_gemv_nt_min_n = (big & 0x1000000) ? (1 << 30) : 16384;  // bit 24: proj_out weights through the caches (A/B)
+  {  // bits 26-27: proj_out K-slices (0: the default, 1: 1, 2: 2, 3: 4)
+    const int pk = (big >> 26) & 3;
+    tw_proj_kw = pk == 0 ? TW_PROJ_KW_DEFAULT : (pk == 1 ? 1 : (pk == 2 ? 2 : 4));
+  }
   const int kw = (big >> 16) & 0xff;
   tw_tune_gemv_kw = (kw == 1 || kw == 2 || kw == 4 || kw == 8) ? kw : 0;
   return 0;
@@ -1987,8 +1995,10 @@ static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
   // (scripts/gemv_bench.py, B = 24): more waves in flight per CU for the one launch that streams 133 MB
   const bool wide = N >= tw_gemv_nt_min_n;
   if (TW_PROJ_KW4 && wide && steps >= 16) kw = 4;
+  if (wide && steps >= 8 * tw_proj_kw) kw = tw_proj_kw;
   if (tw_tune_gemv_kw) kw = tw_tune_gemv_kw;
   if (kw == 4 && wide) launch_gemv_p3<EPI, 4, 8, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
+  else if (kw == 2 && wide) launch_gemv_p3<EPI, 2, 8, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
   else if (kw == 1 && wide) launch_gemv_p3<EPI, 1, 16, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
   else if (kw == 1) launch_gemv_p3<EPI, 1, 16, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
   else if (kw == 2) launch_gemv_p3<EPI, 2, 8, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
