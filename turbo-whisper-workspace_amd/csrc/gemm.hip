@@ -376,6 +376,9 @@ __device__ inline void epi_store8(const EpiArgs& ea, int m, int n, int N, float4
 // LDS instructions of one wave execute in issue order, so a compiler fence (plus the LDS count) is enough; block
 // barriers here only made the 8 waves of a tile wait for each other (and, beside a running decode step, for the
 // wave the decoder's waves slow down most).
+#ifndef GB_EPI_WIDE
+#define GB_EPI_WIDE 1  // k_gemm_big's bf16 epilogues read back 8 columns per lane (16-byte stores); 0: 4 (A/B)
+#endif
 __device__ inline void gb_epi_sync() {
   if (GB_EPI_BLOCKSYNC) {
     __syncthreads();
@@ -410,6 +413,11 @@ __device__ inline void gemm_epi_128x64(const f32x4 (&acc)[8][4], float* wimg, in
   // to the same buffer), and the first eight loads fly while the accumulators are staged through LDS.
   constexpr bool PRE = EPI == TW_EPI_RESID_F32 || EPI == TW_EPI_GELU_POS_F32;
   const bool full = ncol0 + rc + 3 < N;
+  float b8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // (the 8-column read-back's bias)
+  if (GB_EPI_WIDE && !PRE && ea.bias) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) b8[q] = ea.bias[min(ncol0 + (lane & 7) * 8 + q, N - 1)];
+  }
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int ib = 4 * half;
@@ -440,6 +448,21 @@ __device__ inline void gemm_epi_128x64(const f32x4 (&acc)[8][4], float* wimg, in
           epi_store4<EPI>(ea, m, ncol0 + rc, N, v);
         }
         if (rr < 8) ad[rr] = epi_addend<EPI>(ea, min(m + 32, M - 1), ncol0 + rc, full);
+      }
+    } else if constexpr (GB_EPI_WIDE && (EPI == TW_EPI_BF16 || EPI == TW_EPI_GELU_BF16 || EPI == TW_EPI_CROSSKV)) {
+      // bf16 outputs: 8 consecutive columns per lane (8 lanes x 32 B per row, 8 rows per wave-instruction), one
+      // 16-byte store each: half the store instructions of the 4-column form, and whole 128-byte row segments per
+      // 8 lanes for the non-temporal stores (no partial-line write-backs)
+      const int rc8 = (lane & 7) * 8;
+#pragma unroll 4
+      for (int rr = 0; rr < 8; ++rr) {
+        const int lr = rr * 8 + (lane >> 3);
+        const int m = mrow0 + lr;
+        float4 v0 = *(const float4*)(wimg + lr * GB_EPI_LD + rc8);
+        float4 v1 = *(const float4*)(wimg + lr * GB_EPI_LD + rc8 + 4);
+        v0.x += b8[0]; v0.y += b8[1]; v0.z += b8[2]; v0.w += b8[3];
+        v1.x += b8[4]; v1.y += b8[5]; v1.z += b8[6]; v1.w += b8[7];
+        if (m < M && ncol0 + rc8 < N) epi_store8<EPI>(ea, m, ncol0 + rc8, N, v0, v1);
       }
     } else {
 #pragma unroll 4
