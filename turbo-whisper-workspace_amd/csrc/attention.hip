@@ -353,7 +353,12 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc2(const bf16_t* __rest
 // Without ONES (variant 10, the default) the outputs are bit-identical to k_attn_enc2's (max is exact, the sums keep
 // its order); with ONES (variant 11) only the order of the f32 row sum differs.
 // ------------------------------------------------------------------------------------------------
-template <int NW, int WPS, bool ONES>
+// PK (variant 12, VALU trimmed further; not bit-identical to k_attn_enc2): bit 0 = the exp arguments and the row sums
+// in packed f32 math (v_pk_fma_f32 / v_pk_add_f32: two results per issue), bit 1 = lazy rescaling (the running max
+// is raised only when a tile's max exceeds it by more than 2^8 in exp2 units: P entries then stay <= 256, exact in
+// bf16's exponent range, and the O / l rescale of most tiles is skipped; the final O / l is unchanged up to f32
+// rounding).
+template <int NW, int WPS, bool ONES, int PK = 0>
 __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc3(const bf16_t* __restrict__ qkv, int S, int H, int D,
                                                           int nqb, int nwork, bf16_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) bf16_t kbuf[2][EA_KT * 64];
@@ -434,7 +439,7 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc3(const bf16_t* __rest
     }
     float tmax = fmaxf(fmaxf(tc[0], tc[1]), fmaxf(tc[2], tc[3]));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    if (__any(tmax > m_run)) {
+    if (__any((PK & 2) ? tmax * EA_LOG2E > fmaf(m_run, EA_LOG2E, 8.f) : tmax > m_run)) {
       const float m_new = fmaxf(m_run, tmax);
       const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * EA_LOG2E);  // first tile: exp2(-inf) = 0
       if constexpr (ONES) o2[0] *= alpha;
@@ -444,12 +449,32 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc3(const bf16_t* __rest
       m_run = m_new;
     }
     const float mb = m_run * EA_LOG2E;
+    if constexpr (PK & 1) {
+      const f32x2 l2 = {EA_LOG2E, EA_LOG2E}, nm = {-mb, -mb};
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], EA_LOG2E, -mb));
-      s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], EA_LOG2E, -mb));
+      for (int r = 0; r < 16; r += 2) {
+        const f32x2 a = __builtin_elementwise_fma((f32x2){s0[r], s0[r + 1]}, l2, nm);
+        const f32x2 c = __builtin_elementwise_fma((f32x2){s1[r], s1[r + 1]}, l2, nm);
+        s0[r] = __builtin_amdgcn_exp2f(a.x);
+        s0[r + 1] = __builtin_amdgcn_exp2f(a.y);
+        s1[r] = __builtin_amdgcn_exp2f(c.x);
+        s1[r + 1] = __builtin_amdgcn_exp2f(c.y);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], EA_LOG2E, -mb));
+        s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], EA_LOG2E, -mb));
+      }
     }
-    if constexpr (!ONES) {  // k_attn_enc2's summation order exactly (bit-identical outputs)
+    if constexpr (!ONES && (PK & 1)) {  // packed partial sums: two interleaved chains
+      f32x2 p2 = {0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) p2 += (f32x2){s0[r], s0[r + 1]} + (f32x2){s1[r], s1[r + 1]};
+      float ps = p2.x + p2.y;
+      ps += __shfl_xor(ps, 32, 64);
+      l_sum += ps;
+    } else if constexpr (!ONES) {  // k_attn_enc2's summation order exactly (bit-identical outputs)
       float ps = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) ps += s0[r] + s1[r];
@@ -555,7 +580,7 @@ extern "C" int tw_attn_set_variant(int v) {
     tw_dec_cross_unr = unr[(v >> 24) & 3];
   }
   v &= 0xff;
-  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9 || v == 10 || v == 11) ? v : TW_ATTN_DEFAULT;
+  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9 || (v >= 10 && v <= 13)) ? v : TW_ATTN_DEFAULT;
   return 0;
 }
 
@@ -569,6 +594,12 @@ extern "C" int tw_attn_encoder(const bf16_t* qkv, int B, int S, int H, bf16_t* o
   } else if (tw_attn_variant == 4) {
     const int nqb = tw_cdiv(S, 128), nwork = nqb * H * B;
     hipLaunchKernelGGL((k_attn_enc2<4, 2>), dim3(nwork), dim3(256), 0, st, qkv, S, H, D, nqb, nwork, out);
+  } else if (tw_attn_variant == 12 || tw_attn_variant == 13) {
+    const int nqb = (S + 255) / 256, nwork = B * H * nqb;
+    if (tw_attn_variant == 12)
+      hipLaunchKernelGGL((k_attn_enc3<8, 4, false, 3>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
+    else
+      hipLaunchKernelGGL((k_attn_enc3<8, 4, false, 1>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
   } else if (tw_attn_variant == 10 || tw_attn_variant == 11) {
     const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
     if (tw_attn_variant == 10)

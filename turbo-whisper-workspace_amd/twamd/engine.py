@@ -274,6 +274,8 @@ class WhisperEngine:
         # greedy steps end with the fused select + next-step embedding + first LayerNorm (tw_logits_select_embed):
         # 47 launches per token instead of 49. TW_FUSED_SELECT=0: the separate kernels (A/B)
         self.fused_select = os.environ.get("TW_FUSED_SELECT", "1") != "0"
+        # the prompt phase of a decode pass replayed as one captured graph (TW_PROMPT_GRAPH=0: eager, A/B)
+        self.prompt_graph = os.environ.get("TW_PROMPT_GRAPH", "1") != "0"
         self.hostprof = ({"replay": 0.0, "pump": 0.0, "wait": 0.0, "steps": 0}
                          if os.environ.get("TW_HOSTPROF") == "1" else None)  # decode steps queued ahead while pumping
         # decoder projections in the packed fragment layout (tw_pack_weight; +~342 MB at large-v3-turbo): every
@@ -899,30 +901,47 @@ class WhisperEngine:
         st = self.gen.special
         dev = self.device
         self.stream.wait_event(self._enc_ev[self._slot])  # the cross-K/V of this slot is written
-        self.state[:R].zero_()
-        self.state[:R, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
-        self.pos[:R] = 0
-        self.ids[:R] = st.sot
-        detected = None
-        prompt_rest: List = []  # per-position token ids after SOT (int, or per-row list)
-        if st.is_multilingual:
-            prompt_rest.append(None if lang_ids is None else list(lang_ids))
-        prompt_rest.extend(int(t) for t in tail)
-        for k, tok in enumerate(prompt_rest):
-            if k == 0 and st.is_multilingual and lang_ids is None:
-                self.decoder_step(R)
-                self._select(R, self._select_params(1, max_new), tokens=False)  # ids <- lang, pos += 1
-                detected = self.state[:R, _lib.TW_ST_LANG].tolist()
-                continue
-            self.decoder_step(R, with_logits=False)
-            if isinstance(tok, list):
-                self.ids[:R] = torch.as_tensor(tok, dtype=torch.int32, device=dev)
-            else:
-                self.ids[:R] = tok
-            self.pos[:R] = k + 1
-        # last prompt token -> first generated token
+        detect = st.is_multilingual and lang_ids is None
         params = self._select_params(0, max_new, use_timestamps)
-        self._gen_step(R, params)
+
+        def prompt() -> None:
+            """State reset, the prompt steps [SOT, (lang), *tail] and the first generated token (one token per
+            step; the language detected from the SOT step's logits by the mode-1 selection when lang_ids is None)."""
+            self.state[:R].zero_()
+            self.state[:R, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
+            self.pos[:R] = 0
+            self.ids[:R] = st.sot
+            prompt_rest: List = []  # per-position token ids after SOT (int, or per-row list)
+            if st.is_multilingual:
+                prompt_rest.append(None if lang_ids is None else list(lang_ids))
+            prompt_rest.extend(int(t) for t in tail)
+            for k, tok in enumerate(prompt_rest):
+                if k == 0 and detect:
+                    self.decoder_step(R)
+                    self._select(R, self._select_params(1, max_new), tokens=False)  # ids <- lang, pos += 1
+                    continue
+                self.decoder_step(R, with_logits=False)
+                if isinstance(tok, list):
+                    self.ids[:R] = torch.as_tensor(tok, dtype=torch.int32, device=dev)
+                else:
+                    self.ids[:R] = tok
+                self.pos[:R] = k + 1
+            self._gen_step(R, params)  # last prompt token -> first generated token
+
+        # the prompt phase as one captured graph (its ~140 launches replayed instead of issued one by one from the
+        # host while the next batch's encoder keeps the GPU busy); per-row language ids given by the caller stay eager
+        # (their host-to-device copy is not capturable)
+        if self.use_graphs and self.prompt_graph and (detect or not st.is_multilingual):
+            key = ("prompt", R, tuple(int(t) for t in tail), max_new, use_timestamps, self._slot)
+            g = self._graphs.get(key)
+            if g is None:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=self.stream):  # records, does not execute
+                    prompt()
+                self._graphs[key] = g
+            g.replay()
+        else:
+            prompt()
         steps = 1
         # generation loop: the rows split into chains on their own high-priority streams, each replaying its
         # captured decode step; the chains' latency-bound kernels run concurrently
@@ -976,6 +995,7 @@ class WhisperEngine:
                 break
         ngen = self.state[:R, _lib.TW_ST_NGEN].tolist()
         toks = self.tokens[:R].tolist()
+        detected = self.state[:R, _lib.TW_ST_LANG].tolist() if detect else None  # (mode-1 selection only writes it)
         return PassResult([toks[r][: ngen[r]] for r in range(R)], detected if lang_ids is None else list(lang_ids))
 
     def _beam_buffers(self, R: int) -> dict:
