@@ -278,15 +278,16 @@ def _online_softmax_rescale():
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("mode", [0, 0x800], ids=["one_trip", "round1"])
+@pytest.mark.parametrize("mode", [0, 0x800, 0x4000000], ids=["one_trip", "round1", "two_wave"])
 def test_decode_self_attention_positions(mode):
-    """tw_attn_decode_self at positions around the one-round-trip kernel's limits (t = 0, a group boundary, 255 = its
-    last key, 256 = the first two-pass history) vs fp32 attention over the cache rows 0..t with row t appended."""
-    B, H, T = 8, 4, 448
+    """tw_attn_decode_self at positions around the one-round-trip kernels' limits (t = 0, group boundaries, 127 / 128
+    = the 2-wave kernel's last one-trip key / first looped history, 255 / 256 the same for the 4-wave kernel) vs fp32
+    attention over the cache rows 0..t with row t appended."""
+    B, H, T = 10, 4, 448
     D = H * 64
     kc = torch.full((B, H, T, 64), float("nan"), dtype=torch.bfloat16, device=DEV)  # rows past t never touched
     vc = torch.full_like(kc, float("nan"))
-    pos = torch.tensor([0, 1, 31, 32, 100, 255, 256, 447], dtype=torch.int32, device=DEV)
+    pos = torch.tensor([0, 1, 31, 32, 100, 127, 128, 255, 256, 447], dtype=torch.int32, device=DEV)
     for b in range(B):
         p = int(pos[b])
         kc[b, :, :p] = rand_bf16(H, p, 64, seed=90 + b) if p else kc[b, :, :0]

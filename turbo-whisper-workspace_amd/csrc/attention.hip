@@ -564,12 +564,14 @@ extern "C" int tw_attn_set_lds_pad(int units) {
   return 0;
 }
 static int tw_dec_self2 = 1;  // decoder self-attention in one memory round trip (k_attn_decode_self2)
+static int tw_dec_self3 = 0;  // ... in its 2-wave form (k_attn_decode_self3; tw_attn_set_variant bit 26)
 static int tw_dec_cross_lean = 1;  // the one-pass cross-attention in its small-LDS form (0: the 15 KiB form; A/B)
 static int tw_dec_cross_unr = 8;   // key rows in flight per 8-lane group of the lean form (tw_attn_set_variant bits 24-27)
 extern "C" int tw_attn_set_variant(int v) {
   tw_attn_lds_pad = (v >> 20) & 0xf;  // bits 20-23
   tw_dec_cross_lean = (v & 0x400) ? 0 : 1;  // bit 10: the 15 KiB-LDS one-pass cross-attention (A/B)
   tw_dec_self2 = (v & 0x800) ? 0 : 1;       // bit 11: the round-1 three-round-trip self-attention (A/B)
+  tw_dec_self3 = (v & 0x4000000) ? 1 : 0;   // bit 26: the 2-wave one-round-trip self-attention
   tw_dec_cross_1p = (v & 0x100) ? 0 : 1;  // bit 8: the two-pass decoder cross-attention (A/B)
   // bits 12-19: 0 = every slot's cross K/V read non-temporally (default), else 1 + the first slot read so (0xff: none)
   tw_dec_cross_nt = (v >> 12) & 0xff ? ((v >> 12) & 0xff) - 1 : 0;
@@ -723,7 +725,7 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
 // form streams all of K, then (after a block-wide softmax) all of V: two load ramps and three barriers between
 // them on an HBM-bound kernel. Same softmax up to f32 rounding (the rescaling order differs).
 // NG = 8-lane groups per block (32: 256 threads; 64: 512 threads, half the serial load round trips per group).
-template <int NG, bool NT = false>
+template <int NG, bool NT = false, int UNR = DA_UNR>
 __device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const bf16_t* K, const bf16_t* V, int nkeys,
                                      float* part /*[NG][64] LDS*/, float* gml /*[NG][2] LDS*/,
                                      float* outv /*[64] f32 LDS*/) {
@@ -734,10 +736,10 @@ __device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const 
   float m = -INFINITY, l = 0.f;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int nit = (nkeys + NG - 1) / NG;
-  for (int it0 = 0; it0 < nit; it0 += DA_UNR) {
-    uint4 kk[DA_UNR], vv[DA_UNR];
+  for (int it0 = 0; it0 < nit; it0 += UNR) {
+    uint4 kk[UNR], vv[UNR];
 #pragma unroll
-    for (int u = 0; u < DA_UNR; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       const int key = min((it0 + u) * NG + g, nkeys - 1);
       if constexpr (NT) {
         typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
@@ -750,11 +752,11 @@ __device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const 
         vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
       }
     }
-    __builtin_amdgcn_sched_barrier(0);  // all 2 x DA_UNR loads in flight before the first is consumed
-    float sv[DA_UNR];
+    __builtin_amdgcn_sched_barrier(0);  // all 2 x UNR loads in flight before the first is consumed
+    float sv[UNR];
     float bm = m;
 #pragma unroll
-    for (int u = 0; u < DA_UNR; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       const bf16_t* ke = (const bf16_t*)&kk[u];
       float d = 0.f;
 #pragma unroll
@@ -771,7 +773,7 @@ __device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const 
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] *= sc;
 #pragma unroll
-    for (int u = 0; u < DA_UNR; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       const float p = __expf(sv[u] - bm);  // 0 for the masked keys
       l += p;
       const bf16_t* ve = (const bf16_t*)&vv[u];
@@ -950,13 +952,129 @@ __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__
   }
 }
 
+// k_attn_decode_self3: k_attn_decode_self2 with half the workgroup (NGR = 16 key groups = 128 threads, U keys per
+// group in the one-round-trip path: t < NGR * U = 144 covers a 30-s window's 128 generated tokens + prompt). Beside
+// an encoder GEMM workgroup every SIMD keeps room for one decoder wave, so a 4-wave workgroup per CU took the step's
+// 480 (row, head) workgroups two rounds; 2-wave workgroups fit two per CU: one round. Longer histories take the
+// one-pass online-softmax loop (dec_attend_1p) over the cache after the append. Same products; the f32 sums differ
+// from k_attn_decode_self2 only in order.
+template <int NGR, int U>
+__global__ TW_DEC_LB(NGR * 8, 4) void k_attn_decode_self3(const bf16_t* __restrict__ qkv, int D, int max_pos,
+                                                           const int* __restrict__ pos, bf16_t* __restrict__ kc,
+                                                           bf16_t* __restrict__ vc, bf16_t* __restrict__ out) {
+  TW_DEC_PRIO();
+  constexpr int NWV = NGR / 8;  // waves
+  __shared__ float part[NGR * 64];
+  __shared__ float red[2 * NWV];
+  __shared__ float gml[NGR * 2];
+  __shared__ float qf[64];
+  __shared__ float outv[64];
+  const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x;
+  const int tid = threadIdx.x, g = tid >> 3, gl = tid & 7, lane = tid & 63, wid = tid >> 6;
+  const int t = pos[b];
+  const bf16_t* row = qkv + (size_t)b * 3 * D + h * 64;
+  bf16_t* K = kc + ((size_t)b * H + h) * max_pos * 64;
+  bf16_t* V = vc + ((size_t)b * H + h) * max_pos * 64;
+  if (t >= NGR * U) {  // long history: append, then one pass over the cache
+    if (tid < 64) {
+      qf[tid] = bf16_to_f32(row[tid]);
+      K[(size_t)t * 64 + tid] = row[D + tid];
+      V[(size_t)t * 64 + tid] = row[2 * D + tid];
+    }
+    __threadfence_block();
+    __syncthreads();
+    dec_attend_1p<NGR, false, 4>(qf, K, V, t + 1, part, gml, outv);
+    if (tid < 64) out[(size_t)b * D + h * 64 + tid] = f32_to_bf16(outv[tid]);
+    return;
+  }
+  const uint4 qr = *(const uint4*)(row + gl * 8);
+  const uint4 kr = *(const uint4*)(row + D + gl * 8);
+  const uint4 vr = *(const uint4*)(row + 2 * D + gl * 8);
+  uint4 kk[U], vv[U];
+  const int last = max(t - 1, 0);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int key = min(u * NGR + g, last);
+    kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
+    vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if (g == 0) {  // the cache append (read back by the following steps only)
+    *(uint4*)(K + (size_t)t * 64 + gl * 8) = kr;
+    *(uint4*)(V + (size_t)t * 64 + gl * 8) = vr;
+  }
+  float qv[8];
+  {
+    const bf16_t* qe = (const bf16_t*)&qr;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qv[e] = bf16_to_f32(qe[e]);
+  }
+  float p[U];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int key = u * NGR + g;
+    const uint4 kx = key == t ? kr : kk[u];
+    const bf16_t* ke = (const bf16_t*)&kx;
+    float d = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
+    d += __shfl_xor(d, 1, 64);
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 4, 64);
+    p[u] = key <= t ? d : -INFINITY;
+    mx = fmaxf(mx, p[u]);
+  }
+  mx = wave_max(mx);
+  if (lane == 0) red[wid] = mx;
+  __syncthreads();
+  {
+    float m2 = red[0];
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) m2 = fmaxf(m2, red[w]);
+    mx = m2;
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    p[u] = __expf(p[u] - mx);  // 0 past key t
+    if (gl == 0) sum += p[u];
+  }
+  sum = wave_sum(sum);
+  if (lane == 0) red[NWV + wid] = sum;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (u * NGR + g > t) continue;  // (the clamped rows past t may hold anything on the first step: never 0 * them)
+    const uint4 vx = u * NGR + g == t ? vr : vv[u];
+    const bf16_t* ve = (const bf16_t*)&vx;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += p[u] * bf16_to_f32(ve[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[g * 64 + gl * 8 + e] = acc[e];
+  __syncthreads();
+  if (tid < 64) {
+    float tot = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) tot += red[NWV + w];
+    float v = 0.f;
+#pragma unroll 8
+    for (int gg = 0; gg < NGR; ++gg) v += part[gg * 64 + tid];
+    out[(size_t)b * D + h * 64 + tid] = f32_to_bf16(v / tot);
+  }
+}
+
 // Cross-attention step: q [B][D] bf16 (pre-scaled); cross K/V layout [kv][Bt][H][S][64] for this layer,
 // batch row b reads block row_map[b] (the encoder batch slot holding that row's audio window).
 extern "C" int tw_attn_decode_self(const bf16_t* qkv, int B, int H, int max_pos, const int* pos, bf16_t* k_cache,
                                    bf16_t* v_cache, bf16_t* out, void* stream) {
   TW_REQUIRE(qkv && pos && k_cache && v_cache && out && B > 0 && H > 0, "tw_attn_decode_self: bad args");
   TW_REQUIRE(max_pos <= DA_SELF_MAXK, "tw_attn_decode_self: max_pos %d > %d", max_pos, DA_SELF_MAXK);
-  if (tw_dec_self2)
+  if (tw_dec_self2 && tw_dec_self3)
+    hipLaunchKernelGGL((k_attn_decode_self3<16, 8>), dim3(H, B), dim3(128), 0, (hipStream_t)stream, qkv, H * 64, max_pos,
+                       pos, k_cache, v_cache, out);
+  else if (tw_dec_self2)
     hipLaunchKernelGGL(k_attn_decode_self2, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos, pos,
                        k_cache, v_cache, out);
   else
