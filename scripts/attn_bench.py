@@ -17,10 +17,10 @@ qkv[:, :D] = (qkv[:, :D].float() * 0.125).to(torch.bfloat16)
 out = torch.empty(B * S, D, dtype=torch.bfloat16, device="cuda")
 s = torch.cuda.current_stream().cuda_stream
 fl = 4.0 * S * S * 64 * H * B
-res = {v: [] for v in (8, 10, 12, 13)}
+res = {v: [] for v in (8, 10, 12, 14)}
 outs = {}
 for r in range(5):
-    for v in (8, 10, 12, 13):
+    for v in (8, 10, 12, 14):
         _lib.call("tw_attn_set_variant", v)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()

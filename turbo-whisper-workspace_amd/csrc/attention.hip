@@ -380,12 +380,15 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc3(const bf16_t* __rest
 #pragma unroll
     for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
   }
-  constexpr int CPT = 512 / (NW * 64);
+  // 512 16-byte chunks of K and of V per 64-key tile; with NW = 12 (768 threads) the last 256 threads stage none
+  constexpr int CPT = (512 + NW * 64 - 1) / (NW * 64);
+  constexpr bool PART = 512 % (NW * 64) != 0;
   uint4 rk[CPT], rv[CPT];
   auto gload = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int c = tid + NW * 64 * i;
+      if (PART && c >= 512) continue;
       const int key = c >> 3, ch = c & 7;
       const bf16_t* rp = base + (size_t)min(k0 + key, S - 1) * ld + ch * 8;
       rk[i] = *(const uint4*)(rp + D);
@@ -396,6 +399,7 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc3(const bf16_t* __rest
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int c = tid + NW * 64 * i;
+      if (PART && c >= 512) continue;
       const int key = c >> 3, ch = c & 7;
       *(uint4*)(&kbuf[buf][k2_off(key, ch)]) = rk[i];
       *(uint4*)(&vbuf[buf][v2_off(key, ch)]) = rv[i];
@@ -582,7 +586,7 @@ extern "C" int tw_attn_set_variant(int v) {
     tw_dec_cross_unr = unr[(v >> 24) & 3];
   }
   v &= 0xff;
-  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9 || (v >= 10 && v <= 13)) ? v : TW_ATTN_DEFAULT;
+  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9 || (v >= 10 && v <= 14)) ? v : TW_ATTN_DEFAULT;
   return 0;
 }
 
@@ -596,6 +600,9 @@ extern "C" int tw_attn_encoder(const bf16_t* qkv, int B, int S, int H, bf16_t* o
   } else if (tw_attn_variant == 4) {
     const int nqb = tw_cdiv(S, 128), nwork = nqb * H * B;
     hipLaunchKernelGGL((k_attn_enc2<4, 2>), dim3(nwork), dim3(256), 0, st, qkv, S, H, D, nqb, nwork, out);
+  } else if (tw_attn_variant == 14) {  // 12 waves (384 queries) per workgroup: one per CU by registers, no LDS cap
+    const int nqb = (S + 383) / 384, nwork = B * H * nqb;
+    hipLaunchKernelGGL((k_attn_enc3<12, 4, false>), dim3(nwork), dim3(768), pad, st, qkv, S, H, D, nqb, nwork, out);
   } else if (tw_attn_variant == 12 || tw_attn_variant == 13) {
     const int nqb = (S + 255) / 256, nwork = B * H * nqb;
     if (tw_attn_variant == 12)

@@ -163,6 +163,8 @@ class WhisperEngine:
         # encoder-attention LDS cap (16 KiB units) for chunks queued beside a decode; None: leave the library's setting
         pad = os.environ.get("TW_ATTN_PAD", "4")
         self._attn_pad_ctx = None if pad == "" else int(pad)
+        # TW_ATTN_BESIDE=v: encoder-attention variant v (no LDS cap) for chunks queued beside a decode, 10 alone
+        self._attn_beside = int(os.environ["TW_ATTN_BESIDE"], 0) if os.environ.get("TW_ATTN_BESIDE") else None
         d = weights.dims
         d.validate()
         self.d, self.w, self.gen = d, weights, gen
@@ -507,7 +509,9 @@ class WhisperEngine:
         112.1 -> 108.5 ms), uncapped alone (the cap costs the attention itself 22 %)."""
         if not self._gemm_variant_fixed:
             _lib.call("tw_gemm_set_variant", self._gemm_alone if alone else self._gemm_beside)
-        if self._attn_pad_ctx is not None:
+        if self._attn_beside is not None:  # a different encoder-attention kernel beside a decode (A/B)
+            _lib.call("tw_attn_set_variant", 10 if alone else self._attn_beside)
+        elif self._attn_pad_ctx is not None:
             _lib.call("tw_attn_set_lds_pad", 0 if alone else self._attn_pad_ctx)
 
     def _encode_steps(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True,
