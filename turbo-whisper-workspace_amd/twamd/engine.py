@@ -936,7 +936,9 @@ class WhisperEngine:
         # host while the next batch's encoder keeps the GPU busy); per-row language ids given by the caller stay eager
         # (their host-to-device copy is not capturable)
         if self.use_graphs and self.prompt_graph and (detect or not st.is_multilingual):
-            key = ("prompt", R, tuple(int(t) for t in tail), max_new, use_timestamps, self._slot)
+            al = self._align  # (keyed like _graph_for: an alignment pass captures the probability-recording kernel)
+            key = ("prompt", R, tuple(int(t) for t in tail), max_new, use_timestamps, self._slot,
+                   None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()))
             g = self._graphs.get(key)
             if g is None:
                 g = torch.cuda.CUDAGraph()
