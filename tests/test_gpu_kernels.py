@@ -64,7 +64,7 @@ def test_logmel_vs_oracle(n_mels):
 EPIS = [_lib.TW_EPI_BF16, _lib.TW_EPI_GELU_BF16, _lib.TW_EPI_RESID_F32, _lib.TW_EPI_F32]
 
 
-@pytest.mark.parametrize("variant", [1, 9, 5, 6, 8, 3, 4, 0])
+@pytest.mark.parametrize("variant", [1, 10, 9, 5, 6, 8, 3, 4, 0])
 @pytest.mark.parametrize("M,N,K", [(300, 384, 256), (1500, 1280, 1280), (24, 1280, 1280), (7, 51866, 384),
                                    (32, 5120, 1280), (129, 200, 64), (600, 512, 192), (257, 768, 3840)])
 @pytest.mark.parametrize("epi", EPIS)
@@ -158,7 +158,7 @@ def test_gemm_kh_bitexact_vs_big(M, N, K, epi):
         assert torch.equal(o, outs[1][0])
 
 
-@pytest.mark.parametrize("variant", [1, 9, 5, 8])
+@pytest.mark.parametrize("variant", [1, 10, 9, 5, 8])
 def test_gemm_gelu_pos_and_crosskv(variant):
     _lib.call("tw_gemm_set_variant", variant)
     try:

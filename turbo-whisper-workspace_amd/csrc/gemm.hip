@@ -391,10 +391,10 @@ __device__ inline void gb_epi_sync() {
 // Epilogue of one wave's 128 x 64 sub-tile (rows mw0.., columns ncol0..) held as 8 x 4 16x16 MFMA accumulators,
 // through the wave's own [64][GB_EPI_LD] f32 LDS image `wimg` (shared by k_gemm_big and k_gemm_h; every wave of the
 // block calls it: it holds block barriers). The caller's K loop must have ended on a barrier.
-template <int EPI>
-__device__ inline void gemm_epi_128x64(const f32x4 (&acc)[8][4], float* wimg, int lane, int mw0, int ncol0, int M,
-                                       int N, const EpiArgs& ea) {
-  const int fr = lane & 15, fq = lane >> 4;
+// stage(half, wimg) writes rows 64 half .. 64 half + 63 of the wave's sub-tile into its [64][GB_EPI_LD] f32 image
+template <int EPI, class Stage>
+__device__ inline void gemm_epi_128x64_st(Stage stage, float* wimg, int lane, int mw0, int ncol0, int M, int N,
+                                          const EpiArgs& ea) {
   // ---- epilogue through LDS: each wave stages 64 of its 128 rows at a time in its own
   // [64][GB_EPI_LD] f32 image (k_gemm_big: 8 images = 136 KiB, the K loop's LDS plus 8 KiB), then reads
   // back 4 consecutive columns per lane (16 lanes x 16 B per row) for vectorised global I/O.
@@ -428,12 +428,7 @@ __device__ inline void gemm_epi_128x64(const f32x4 (&acc)[8][4], float* wimg, in
       for (int q = 0; q < 8; ++q) ad[q] = epi_addend<EPI>(ea, min(mrow0 + q * 4 + (lane >> 4), M - 1), ncol0 + rc, full);
     }
     if (half) gb_epi_sync();  // (first pass: the K loop ended on a barrier)
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) wimg[(ii * 16 + fq * 4 + r) * GB_EPI_LD + j * 16 + fr] = acc[ib + ii][j][r];
+    stage(half, wimg);
     gb_epi_sync();
     if constexpr (PRE) {
 #pragma unroll
@@ -475,6 +470,40 @@ __device__ inline void gemm_epi_128x64(const f32x4 (&acc)[8][4], float* wimg, in
       }
     }
   }
+}
+
+// the 16x16x32 MFMA layout (8 x 4 accumulators of 16 x 16: lane (fr, fq) holds rows 4 fq + r of column fr)
+template <int EPI>
+__device__ inline void gemm_epi_128x64(const f32x4 (&acc)[8][4], float* wimg, int lane, int mw0, int ncol0, int M,
+                                       int N, const EpiArgs& ea) {
+  const int fr = lane & 15, fq = lane >> 4;
+  auto stage = [&](int half, float* w) {
+    const int ib = 4 * half;
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[(ii * 16 + fq * 4 + r) * GB_EPI_LD + j * 16 + fr] = acc[ib + ii][j][r];
+  };
+  gemm_epi_128x64_st<EPI>(stage, wimg, lane, mw0, ncol0, M, N, ea);
+}
+// the 32x32x16 MFMA layout (4 x 2 accumulators of 32 x 32: lane l holds column l % 32, rows 8 (r / 4) + 4 (l / 32)
+// + r % 4 for its 16 registers r)
+template <int EPI>
+__device__ inline void gemm_epi_128x64_m32(const f32x16 (&acc)[4][2], float* wimg, int lane, int mw0, int ncol0,
+                                           int M, int N, const EpiArgs& ea) {
+  const int c = lane & 31, h4 = (lane >> 5) * 4;
+  auto stage = [&](int half, float* w) {
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          w[(i2 * 32 + (r >> 2) * 8 + h4 + (r & 3)) * GB_EPI_LD + j * 32 + c] = acc[2 * half + i2][j][r];
+  };
+  gemm_epi_128x64_st<EPI>(stage, wimg, lane, mw0, ncol0, M, N, ea);
 }
 
 template <int EPI>
@@ -566,6 +595,79 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ 
 #endif
 
   gemm_epi_128x64<EPI>(acc, (float*)smem + wid * (64 * GB_EPI_LD), lane, m0 + wr * 128, n0 + wc * 64, M, N, ea);
+}
+
+// k_gemm_big32: k_gemm_big with v_mfma_f32_32x32x16_bf16 (MI355X_MICROARCH / cdna_hip_programming §5.4 rule 28:
+// the chip can hold a different clock on the other bf16 MFMA shape; same wave tile, half the MFMA instructions).
+// Same LDS image, swizzle, DMA and one barrier per K-step; per 16-deep K substep a wave reads 4 A and 2 B fragments
+// (32 rows x 16 k: lane l row l % 32, k chunk 2 kk + l / 32) into 4 x 2 accumulators of 32 x 32.
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm_big32(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                       int M, int N, int K, int lda, int ldw, EpiArgs ea) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 64 * GB_EPI_LD * 2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntm = (M + GB_BM - 1) / GB_BM, ntn = (N + GB_BN - 1) / GB_BN;
+  const int nwg = ntm * ntn;
+  const int orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  int tm, tn;
+  tw_tile_grouped(wgid, ntm, ntn, ea.group_m, tm, tn);
+  const int m0 = tm * GB_BM, n0 = tn * GB_BN;
+  const bf16_t* ga[4];
+  const bf16_t* gw[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (4 * wid + i) + (lane >> 3);
+    const int ch = (lane & 7) ^ gb_swz(row);
+    ga[i] = A + (size_t)min(m0 + row, M - 1) * lda + ch * 8;
+    gw[i] = W + (size_t)min(n0 + row, N - 1) * ldw + ch * 8;
+  }
+  auto stage = [&](int buf, int k0) {
+    bf16_t* As = smem + buf * 2 * GB_BM * GB_BK;
+    bf16_t* Ws = As + GB_BM * GB_BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rb = 8 * (4 * wid + i) * GB_BK;
+      __builtin_amdgcn_global_load_lds((const void*)(ga[i] + k0), (lds_void_t*)(As + rb), 16, 0, GB_A_POL);
+      __builtin_amdgcn_global_load_lds((const void*)(gw[i] + k0), (lds_void_t*)(Ws + rb), 16, 0, 0);
+    }
+  };
+  const int wr = wid >> 2, wc = wid & 3;
+  const int lr = lane & 31, lh = lane >> 5;
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0.f};
+  const int nk = K / GB_BK;
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * GB_BK);
+    const bf16_t* As = smem + cur * 2 * GB_BM * GB_BK;
+    const bf16_t* Ws = As + GB_BM * GB_BK;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int kc = 2 * kk + lh;
+      bf16x8 bfr[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = wc * 64 + j * 32 + lr;
+        bfr[j] = *(const bf16x8*)(Ws + col * GB_BK + ((kc ^ gb_swz(col)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wr * 128 + i * 32 + lr;
+        const bf16x8 af = *(const bf16x8*)(As + row * GB_BK + ((kc ^ gb_swz(row)) << 3));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  gemm_epi_128x64_m32<EPI>(acc, (float*)smem + wid * (64 * GB_EPI_LD), lane, m0 + wr * 128, n0 + wc * 64, M, N, ea);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2048,6 +2150,9 @@ static int launch_gemm(const bf16_t* A, const bf16_t* W, int M, int N, int K, in
     } else if (tw_gemm_big_enabled == 5) {
       unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
       hipLaunchKernelGGL(k_gemm_8p<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
+    } else if (tw_gemm_big_enabled == 10) {
+      unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
+      hipLaunchKernelGGL(k_gemm_big32<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
     } else if (tw_gemm_big_enabled == 9 && K >= 2 * GB_BK) {
       unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
       hipLaunchKernelGGL(k_gemm_kh<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
