@@ -1,6 +1,6 @@
 #!/bin/bash
-# One GPU-box session: parity tests, the bench line, a rocprofv3 kernel-trace summary and the two
-# PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic. Every GPU step has its own time limit and the
+# One GPU-box session: parity tests, the bench line, a rocprofv3 kernel-trace summary, the two
+# PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic and one for MFMA utilisation. Every GPU step has its own time limit and the
 # chain stops at the first failure.  usage: [BENCH_ARGS="--config c5"] bash scripts/gpu_round.sh TAG [skip_tests]
 # (a config-5 TAG must contain "_c5": bench.py reads profiles/*_c5_traffic.json for it)
 set -u
@@ -24,6 +24,7 @@ fi
 step prof_kt 600 rocprofv3 --kernel-trace --stats -T -d $OUT/kt -o kt --output-format csv -- python bench.py $BA --profile-only --steps 2 --warmup 1
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/pmc_fetch -o pmc --output-format csv -- python bench.py $BA --profile-only --steps 1 --warmup 0
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/pmc_write -o pmc --output-format csv -- python bench.py $BA --profile-only --steps 1 --warmup 0
+step pmc_mfma 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_BF16 -T -d $OUT/pmc_mfma -o pmc --output-format csv -- python bench.py $BA --profile-only --steps 1 --warmup 0
 python scripts/summarize_prof.py $OUT > $OUT/summary.txt 2>&1
 cp $OUT/traffic.json profiles/${TAG}_traffic.json   # bench.py reads the newest profiles/*traffic.json
 step bench 900 python bench.py $BA --steps 5 --warmup 2

@@ -45,6 +45,32 @@ def pmc(root: str, sub: str, counter: str):
     return per
 
 
+SIMD_NUM = 256 * 4  # MI355X: 256 CUs x 4 SIMDs (rocprofv3's MfmaUtil: busy cycles / (GUI_ACTIVE x SIMD_NUM))
+
+
+def mfma_util(root: str):
+    """Per kernel (launch-averaged, from the pmc_mfma pass): MFMA busy % of all SIMD cycles while the GPU was active
+    (rocprofv3's MfmaUtil formula) and the bf16 MFMA rate from SQ_INSTS_VALU_MFMA_MOPS_BF16 x 512 FLOP over the
+    dispatch's own duration (rocprofv3 serialises dispatches under counter collection: each is measured alone)."""
+    rows = defaultdict(lambda: defaultdict(list))
+    dur = defaultdict(dict)
+    for f in _find(os.path.join(root, "pmc_mfma"), "*counter_collection.csv"):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                k, d = r["Kernel_Name"], r["Dispatch_Id"]
+                rows[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                dur[k][d] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    out = {}
+    for k, c in rows.items():
+        busy, gui, mops = (sum(c.get(n, [])) for n in ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE",
+                                                        "SQ_INSTS_VALU_MFMA_MOPS_BF16"))
+        ns = sum(dur[k].values())
+        if gui > 0 and mops > 0:
+            out[k] = {"launches": len(dur[k]), "mfma_util_pct": 100.0 * busy / (gui * SIMD_NUM),
+                      "bf16_tflops": mops * 512 / ns / 1e3 if ns > 0 else None}
+    return out
+
+
 def main(root: str) -> None:
     ks = kernel_stats(root)
     print(f"# rocprofv3 --kernel-trace --stats ({root})")
@@ -69,6 +95,16 @@ def main(root: str) -> None:
                   f"write={v['write_kib'] or 0:12.0f}KiB hbm={0 if hb is None else hb / 1e6:10.2f}MB")
     with open(os.path.join(root, "traffic.json"), "w") as fh:
         json.dump(traffic, fh, indent=1)
+    mu = mfma_util(root)
+    if mu:
+        print("\n# MFMA utilisation per launch (pmc_mfma pass: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 1024 SIMDs);"
+              " bf16 rate = SQ_INSTS_VALU_MFMA_MOPS_BF16 x 512 / dispatch time)")
+        for k, v in sorted(mu.items(), key=lambda kv: -kv[1]["mfma_util_pct"]):
+            tf = v["bf16_tflops"]
+            print(f"{k[:70]:70s} n={v['launches']:5d} mfma_busy={v['mfma_util_pct']:6.1f}% "
+                  f"bf16={0 if tf is None else tf:8.1f} TFLOP/s")
+        with open(os.path.join(root, "mfma.json"), "w") as fh:
+            json.dump(mu, fh, indent=1)
 
 
 if __name__ == "__main__":
