@@ -133,6 +133,7 @@ def main():
                 for k, v in fam.items()}
     # the bf16 family runs as k_gemm_big beside a decode and as k_gemm_8p alone (engine._set_gemm_context)
     traffic, traffic_src = measured_traffic(("k_" + dom,) if fp8 else ("k_gemm_big", "k_gemm_8p"), fp8)
+    mfma_busy, mfma_src = measured_mfma(("k_" + dom,) if fp8 else ("k_gemm_big", "k_gemm_8p"), fp8)
 
     # secondary (HBM-bound) kernel: decoder cross-attention, timed on one eager decode pass outside the timed
     # region (the timed decode steps replay a hipGraph, which has no room for events)
@@ -162,7 +163,8 @@ def main():
                                 "k_gemm_big / k_gemm_8p (all encoder/conv/cross-KV projections, bf16 MFMA)"),
                      "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
-                     "traffic_source": traffic_src, "launches_per_step": n_l // a.steps,
+                     "traffic_source": traffic_src, "mfma_busy_pct": mfma_busy, "mfma_source": mfma_src,
+                     "launches_per_step": n_l // a.steps,
                      "avg_launch_ms": round(avg_ms, 4), "flop_per_launch": work / n_l},
         "roofline_decode": dec,
         "kernel_families": families,
@@ -197,6 +199,27 @@ def measured_traffic(kernels, c5: bool = False):
         if hit:
             n = sum(h["launches"] for h in hit)
             return sum(h["hbm_bytes"] * h["launches"] for h in hit) / n, os.path.relpath(f, ROOT)
+    return None, None
+
+
+def measured_mfma(kernels, c5: bool = False):
+    """MFMA busy % of the dominant family's launches from the newest profiles/*mfma.json (scripts/summarize_prof.py:
+    rocprofv3 PMC pass, SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE per XCD x 1024 SIMDs; dispatches serialised by
+    the profiler, so this is the kernel's own utilisation, not the in-situ one), launch-weighted, or (None, None)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*mfma.json")), key=os.path.basename)
+    files = [f for f in files if ("_c5_" in os.path.basename(f)) == c5]
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        hit = [d[k] for k in kernels if k in d and d[k].get("launches")]
+        if hit:
+            n = sum(h["launches"] for h in hit)
+            return round(sum(h["mfma_util_pct"] * h["launches"] for h in hit) / n, 1), os.path.relpath(f, ROOT)
     return None, None
 
 

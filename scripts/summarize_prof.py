@@ -46,6 +46,8 @@ def pmc(root: str, sub: str, counter: str):
 
 
 SIMD_NUM = 256 * 4  # MI355X: 256 CUs x 4 SIMDs (rocprofv3's MfmaUtil: busy cycles / (GUI_ACTIVE x SIMD_NUM))
+N_XCD = 8  # rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs' GRBMs: one XCD's count is the GPU-active cycles
+# (checked: with the sum, k_gemm_8p read 5.3 % busy at 1014 TFLOP/s = 41 % of the MFMA peak; per XCD 42 %)
 
 
 def mfma_util(root: str):
@@ -66,7 +68,7 @@ def mfma_util(root: str):
                                                         "SQ_INSTS_VALU_MFMA_MOPS_BF16"))
         ns = sum(dur[k].values())
         if gui > 0 and mops > 0:
-            out[k] = {"launches": len(dur[k]), "mfma_util_pct": 100.0 * busy / (gui * SIMD_NUM),
+            out[k] = {"launches": len(dur[k]), "mfma_util_pct": 100.0 * busy / (gui / N_XCD * SIMD_NUM),
                       "bf16_tflops": mops * 512 / ns / 1e3 if ns > 0 else None}
     return out
 
@@ -97,7 +99,7 @@ def main(root: str) -> None:
         json.dump(traffic, fh, indent=1)
     mu = mfma_util(root)
     if mu:
-        print("\n# MFMA utilisation per launch (pmc_mfma pass: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 1024 SIMDs);"
+        print("\n# MFMA utilisation per launch (pmc_mfma pass: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs);"
               " bf16 rate = SQ_INSTS_VALU_MFMA_MOPS_BF16 x 512 / dispatch time)")
         for k, v in sorted(mu.items(), key=lambda kv: -kv[1]["mfma_util_pct"]):
             tf = v["bf16_tflops"]
