@@ -471,12 +471,24 @@ GEMV_CASES = [  # M, N, K, epi, splits
     (24, 5120, 1280, _lib.TW_EPI_GELU_PACKED, 1), (13, 1536, 384, _lib.TW_EPI_GELU_PACKED, 1),
     (24, 1280, 5120, _lib.TW_EPI_PARTIAL_F32, 4), (24, 1280, 1280, _lib.TW_EPI_PARTIAL_F32, 4),
     (1, 384, 1536, _lib.TW_EPI_PARTIAL_F32, 3), (24, 51866, 1280, _lib.TW_EPI_F32, 1), (5, 51864, 384, _lib.TW_EPI_F32, 1),
+    (24, 1296, 1280, _lib.TW_EPI_BF16, 1), (24, 1296, 1280, _lib.TW_EPI_PARTIAL_F32, 4),  # odd column-group count
 ]
 
 
+@pytest.mark.parametrize("pairs", [0, 1], ids=["gemv_p", "gemv_pc"])
 @pytest.mark.parametrize("a_packed", [1, 0])
 @pytest.mark.parametrize("M,N,K,epi,splits", GEMV_CASES)
-def test_gemv_packed_vs_torch(M, N, K, epi, splits, a_packed):
+def test_gemv_packed_vs_torch(M, N, K, epi, splits, a_packed, pairs):
+    """tw_gemv_packed vs torch fp32, two column groups per wave (k_gemv_pc, the default for the layer GEMVs) and one
+    (k_gemv_p, tw_gemm_set_variant bit 28; the vocabulary-wide proj_out always takes k_gemv_p)."""
+    _lib.call("tw_gemm_set_variant", 1 | ((1 - pairs) << 28))
+    try:
+        _gemv_packed_vs_torch(M, N, K, epi, splits, a_packed)
+    finally:
+        _lib.call("tw_gemm_set_variant", 1)
+
+
+def _gemv_packed_vs_torch(M, N, K, epi, splits, a_packed):
     A = rand_bf16(M, K, seed=41)
     W = rand_bf16(N, K, scale=K ** -0.5, seed=42)
     bias = torch.randn(N, device=DEV) * 0.1

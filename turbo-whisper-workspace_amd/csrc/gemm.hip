@@ -207,6 +207,10 @@ static int tw_gemv_nt_min_n = 16384;
 static int tw_tune_skinny_nw = 0;  // 0 = heuristic; 4 / 8 / 16 force the skinny kernel's waves per block
 static int tw_tune_gemv_kw = 0;    // 0 = heuristic; 1 / 2 / 4 / 8 force the packed GEMV's K-slices per column group
 static int tw_proj_kw = TW_PROJ_KW_DEFAULT;  // K-slices per column group of the vocabulary-wide proj_out (1 / 2 / 4)
+// the decoder's layer GEMVs as k_gemv_pc (two column groups per wave). Measured in the bench (three interleaved pairs,
+// 10 steps): 91.8 vs 92.4 ms, the encoder GEMM beside the decode 785 vs 781 TF/s (fewer decoder vector-memory
+// instructions in its CUs); per launch in situ equal (11.6 vs 11.3 us). tw_gemm_set_variant bit 28: k_gemv_p (A/B).
+static int tw_gemv_pairs = 1;
 // Largest K-slice count the packed-GEMV heuristic picks. 4 = at most 256-thread workgroups: one decoder wave per SIMD
 // then co-resides with an encoder GEMM workgroup (2 waves of ~190 VGPRs on every SIMD), where a 512-thread decoder
 // workgroup waits for GEMM workgroups to retire (scripts/exp/interference.py, q/k/v GEMV beside k_gemm_8p: 33.6 us per
@@ -223,6 +227,7 @@ extern "C" int tw_gemm_set_variant(int big) {
   const int nw = (big >> 8) & 0xff;
   tw_tune_skinny_nw = (nw == 4 || nw == 8 || nw == 16) ? nw : 0;
   tw_gemv_nt_min_n = (big & 0x1000000) ? (1 << 30) : 16384;  // bit 24: proj_out weights through the caches (A/B)
+  tw_gemv_pairs = ((big >> 28) & 1) ? 0 : 1;
   {  // bits 26-27: proj_out K-slices (0: the default, 1: 1, 2: 2, 3: 4)
     const int pk = (big >> 26) & 3;
     tw_proj_kw = pk == 0 ? TW_PROJ_KW_DEFAULT : (pk == 1 ? 1 : (pk == 2 ? 2 : 4));
@@ -2064,6 +2069,120 @@ __global__ TW_DEC_LB(KW > 4 ? 512 : 256, 1) void k_gemv_p(const bf16_t* __restri
   }
 }
 
+// k_gemv_pc: k_gemv_p with TWO column groups per wave (32 output columns) sharing each A fragment. At M = 17..32 rows
+// a step of k_gemv_p loads one W fragment and two A fragments (the activations, L2-resident and identical for every
+// column group); here a step loads two W fragments and the same two A fragments: a third fewer vector-memory
+// instructions and VGPRs per weight byte. Every decoder-step kernel shares its CU with an encoder GEMM workgroup
+// (run_batches' overlap), whose LDS-DMA keeps the same vector-memory path busy. KW >= 2 K-slices
+// per column-group pair, reduced through LDS; epilogues BF16, PARTIAL (split-K) and GELU_PACKED.
+template <int EPI, int KW, int U, bool APACK, bool TWO>
+__global__ TW_DEC_LB(256, 1) void k_gemv_pc(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ Wp,
+                                            int M, int N, int K, EpiArgs ea) {
+  TW_DEC_PRIO();
+  static_assert(KW == 2 || KW == 4, "k_gemv_pc: 2 or 4 K-slices");
+  constexpr int NW = 4, GPB = NW / KW;  // pairs per workgroup
+  __shared__ float red[NW][2][32][17];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int gl = wid / KW, kw = wid - gl * KW;
+  const int g0 = (blockIdx.x * GPB + gl) * 2;  // this wave's column groups g0, g0 + 1
+  const int ngroups = (N + 15) >> 4, ns = K >> 5;
+  const int nsl = KW * gridDim.y, sl = blockIdx.y * KW + kw;
+  const int s0 = (int)((long)sl * ns / nsl), s1 = (int)((long)(sl + 1) * ns / nsl);
+  f32x4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c10 = c00, c11 = c00;  // c<group><m-tile>
+  if (g0 < ngroups) {
+    const bool has1 = g0 + 1 < ngroups;
+    const bf16_t* wp0 = Wp + (size_t)g0 * ns * 512 + lane * 8;
+    const bf16_t* wp1 = has1 ? wp0 + (size_t)ns * 512 : wp0;  // (an odd last group: its twin re-reads group g0)
+    const bf16_t* ap;
+    const bf16_t* ap1 = nullptr;
+    if constexpr (APACK) {
+      ap = A + lane * 8;
+    } else {
+      ap = A + (size_t)min(lane & 15, M - 1) * lda + 8 * (lane >> 4);
+      ap1 = A + (size_t)min(16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4);
+    }
+    auto ldA0 = [&](int st) -> bf16x8 {
+      return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024) : *(const bf16x8*)(ap + 32 * st);
+    };
+    auto ldA1 = [&](int st) -> bf16x8 {
+      return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024 + 512) : *(const bf16x8*)(ap1 + 32 * st);
+    };
+    // one batch of NB steps, every load issued before the first MFMA (see k_gemv_p)
+    auto batch = [&](auto NBc, int st0, int n) {
+      constexpr int NB = decltype(NBc)::value;
+      bf16x8 b0[NB], b1[NB], a0[NB], a1[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int st = min(st0 + u, s1 - 1);
+        b0[u] = *(const bf16x8*)(wp0 + (size_t)st * 512);
+        b1[u] = *(const bf16x8*)(wp1 + (size_t)st * 512);
+        a0[u] = ldA0(st);
+        if (TWO) a1[u] = ldA1(st);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        if (u < n) {
+          c00 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], b0[u], c00, 0, 0, 0);
+          c10 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], b1[u], c10, 0, 0, 0);
+          if (TWO) {
+            c01 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], b0[u], c01, 0, 0, 0);
+            c11 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], b1[u], c11, 0, 0, 0);
+          }
+        }
+      }
+    };
+    using IU = std::integral_constant<int, U>;
+    int st = s0;
+    for (; st + U <= s1; st += U) batch(IU{}, st, U);
+    const int rem = s1 - st;
+    if (rem > U / 2) batch(IU{}, st, rem);
+    else if (rem > 0) batch(std::integral_constant<int, (U / 2 > 0 ? U / 2 : 1)>{}, st, rem);
+  }
+  const int cc = lane & 15, rb = (lane >> 4) * 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[wid][0][rb + r][cc] = c00[r];
+    red[wid][1][rb + r][cc] = c10[r];
+    if (TWO) {
+      red[wid][0][16 + rb + r][cc] = c01[r];
+      red[wid][1][16 + rb + r][cc] = c11[r];
+    }
+  }
+  __syncthreads();
+  constexpr int ROWS = TWO ? 32 : 16;
+  for (int e = tid; e < GPB * 2 * ROWS * 16; e += NW * 64) {
+    const int pg = e / (2 * ROWS * 16), rem = e - pg * 2 * ROWS * 16;  // pair in the block, then group, row, column
+    const int h = rem / (ROWS * 16), r2 = rem - h * ROWS * 16;
+    const int m = r2 >> 4, c = r2 & 15;
+    const int n = ((blockIdx.x * GPB + pg) * 2 + h) * 16 + c;
+    if (m < M && n < N) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < KW; ++w) v += red[pg * KW + w][h][m][c];
+      if constexpr (EPI == TW_EPI_PARTIAL) {
+        ((float*)ea.out)[((size_t)blockIdx.y * M + m) * ea.ldo + n] = v;
+      } else if constexpr (EPI == TW_EPI_GELU_PACKED) {
+        if (ea.bias) v += ea.bias[n];
+        ((bf16_t*)ea.out)[tw_pack_act_idx(m, n)] = f32_to_bf16(gelu_erf(v));
+      } else {
+        epi_store<EPI>(ea, m, n, v);
+      }
+    }
+  }
+}
+
+template <int EPI, int KW, bool APACK>
+static void launch_gemv_pc(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea,
+                           int splits, hipStream_t s) {
+  constexpr int GPB = 4 / KW;
+  dim3 grid(tw_cdiv(tw_cdiv(tw_cdiv(N, 16), 2), GPB), splits);
+  if (M > 16)
+    hipLaunchKernelGGL((k_gemv_pc<EPI, KW, 5, APACK, true>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
+  else
+    hipLaunchKernelGGL((k_gemv_pc<EPI, KW, 5, APACK, false>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
+}
+
 template <int EPI, int KW, int U, bool APACK, bool NTW = false>
 static void launch_gemv_p3(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea, int splits,
                            hipStream_t s) {
@@ -2122,6 +2241,16 @@ static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
   if (TW_PROJ_KW4 && wide && steps >= 16) kw = 4;
   if (wide && steps >= 8 * tw_proj_kw) kw = tw_proj_kw;
   if (tw_tune_gemv_kw) kw = tw_tune_gemv_kw;
+  if constexpr (EPI == TW_EPI_BF16 || EPI == TW_EPI_PARTIAL || EPI == TW_EPI_GELU_PACKED) {
+    if (tw_gemv_pairs && !wide && !tw_tune_gemv_kw) {  // column-group pairs (a forced K-slice count: k_gemv_p)
+      const long pairs = tw_cdiv(tw_cdiv(N, 16), 2) * (long)splits;
+      int kp = 2;
+      if (pairs * kp < 1024 && steps >= 8 * 4) kp = 4;
+      if (kp == 2) launch_gemv_pc<EPI, 2, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
+      else launch_gemv_pc<EPI, 4, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
+      return;
+    }
+  }
   if (kw == 4 && wide) launch_gemv_p3<EPI, 4, 8, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
   else if (kw == 2 && wide) launch_gemv_p3<EPI, 2, 8, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
   else if (kw == 1 && wide) launch_gemv_p3<EPI, 1, 16, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
