@@ -475,13 +475,14 @@ GEMV_CASES = [  # M, N, K, epi, splits
 ]
 
 
-@pytest.mark.parametrize("pairs", [0, 1], ids=["gemv_p", "gemv_pc"])
+@pytest.mark.parametrize("pairs", [0, 1, 2], ids=["gemv_p", "gemv_pc", "proj_pc"])
 @pytest.mark.parametrize("a_packed", [1, 0])
 @pytest.mark.parametrize("M,N,K,epi,splits", GEMV_CASES)
 def test_gemv_packed_vs_torch(M, N, K, epi, splits, a_packed, pairs):
     """tw_gemv_packed vs torch fp32, two column groups per wave (k_gemv_pc, the default for the layer GEMVs) and one
-    (k_gemv_p, tw_gemm_set_variant bit 28; the vocabulary-wide proj_out always takes k_gemv_p)."""
-    _lib.call("tw_gemm_set_variant", 1 | ((1 - pairs) << 28))
+    (k_gemv_p, tw_gemm_set_variant bit 28). The vocabulary-wide proj_out takes k_gemv_p by default and k_gemv_pc with
+    one K-slice under bit 29 ("proj_pc")."""
+    _lib.call("tw_gemm_set_variant", 1 | (int(pairs == 0) << 28) | (int(pairs == 2) << 29))
     try:
         _gemv_packed_vs_torch(M, N, K, epi, splits, a_packed)
     finally:

@@ -201,6 +201,9 @@ static inline int tw_group_for(int N) {
 }
 // packed GEMVs with N >= this (proj_out) read their weights non-temporally: bench step -1 ms (109.2 vs 110.3)
 static int tw_gemv_nt_min_n = 16384;
+#ifndef TW_PROJ_PAIRS_DEFAULT
+#define TW_PROJ_PAIRS_DEFAULT 0
+#endif
 #ifndef TW_PROJ_KW_DEFAULT
 #define TW_PROJ_KW_DEFAULT 1
 #endif
@@ -211,6 +214,7 @@ static int tw_proj_kw = TW_PROJ_KW_DEFAULT;  // K-slices per column group of the
 // 10 steps): 91.8 vs 92.4 ms, the encoder GEMM beside the decode 785 vs 781 TF/s (fewer decoder vector-memory
 // instructions in its CUs); per launch in situ equal (11.6 vs 11.3 us). tw_gemm_set_variant bit 28: k_gemv_p (A/B).
 static int tw_gemv_pairs = 1;
+static int tw_proj_pairs = TW_PROJ_PAIRS_DEFAULT;  // proj_out as k_gemv_pc with one K-slice (tw_gemm_set_variant bit 29)
 // Largest K-slice count the packed-GEMV heuristic picks. 4 = at most 256-thread workgroups: one decoder wave per SIMD
 // then co-resides with an encoder GEMM workgroup (2 waves of ~190 VGPRs on every SIMD), where a 512-thread decoder
 // workgroup waits for GEMM workgroups to retire (scripts/exp/interference.py, q/k/v GEMV beside k_gemm_8p: 33.6 us per
@@ -228,6 +232,7 @@ extern "C" int tw_gemm_set_variant(int big) {
   tw_tune_skinny_nw = (nw == 4 || nw == 8 || nw == 16) ? nw : 0;
   tw_gemv_nt_min_n = (big & 0x1000000) ? (1 << 30) : 16384;  // bit 24: proj_out weights through the caches (A/B)
   tw_gemv_pairs = ((big >> 28) & 1) ? 0 : 1;
+  tw_proj_pairs = ((big >> 29) & 1) ? !TW_PROJ_PAIRS_DEFAULT : TW_PROJ_PAIRS_DEFAULT;  // bit 29: the other proj_out form
   {  // bits 26-27: proj_out K-slices (0: the default, 1: 1, 2: 2, 3: 4)
     const int pk = (big >> 26) & 3;
     tw_proj_kw = pk == 0 ? TW_PROJ_KW_DEFAULT : (pk == 1 ? 1 : (pk == 2 ? 2 : 4));
@@ -2075,13 +2080,13 @@ __global__ TW_DEC_LB(KW > 4 ? 512 : 256, 1) void k_gemv_p(const bf16_t* __restri
 // instructions and VGPRs per weight byte. Every decoder-step kernel shares its CU with an encoder GEMM workgroup
 // (run_batches' overlap), whose LDS-DMA keeps the same vector-memory path busy. KW >= 2 K-slices
 // per column-group pair, reduced through LDS; epilogues BF16, PARTIAL (split-K) and GELU_PACKED.
-template <int EPI, int KW, int U, bool APACK, bool TWO>
+template <int EPI, int KW, int U, bool APACK, bool TWO, bool NTW = false>
 __global__ TW_DEC_LB(256, 1) void k_gemv_pc(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ Wp,
                                             int M, int N, int K, EpiArgs ea) {
   TW_DEC_PRIO();
-  static_assert(KW == 2 || KW == 4, "k_gemv_pc: 2 or 4 K-slices");
+  static_assert(KW == 1 || KW == 2 || KW == 4, "k_gemv_pc: 1, 2 or 4 K-slices");
   constexpr int NW = 4, GPB = NW / KW;  // pairs per workgroup
-  __shared__ float red[NW][2][32][17];
+  __shared__ float red[KW > 1 ? NW : 1][2][KW > 1 ? 32 : 1][17];  // (KW = 1: stored from registers, no LDS)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int gl = wid / KW, kw = wid - gl * KW;
   const int g0 = (blockIdx.x * GPB + gl) * 2;  // this wave's column groups g0, g0 + 1
@@ -2114,8 +2119,14 @@ __global__ TW_DEC_LB(256, 1) void k_gemv_pc(const bf16_t* __restrict__ A, int ld
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
         const int st = min(st0 + u, s1 - 1);
-        b0[u] = *(const bf16x8*)(wp0 + (size_t)st * 512);
-        b1[u] = *(const bf16x8*)(wp1 + (size_t)st * 512);
+        if constexpr (NTW) {  // (proj_out: 133 MB streamed once per step, kept out of the caches)
+          typedef short s16x8_nt __attribute__((ext_vector_type(8)));
+          b0[u] = __builtin_bit_cast(bf16x8, __builtin_nontemporal_load((const s16x8_nt*)(wp0 + (size_t)st * 512)));
+          b1[u] = __builtin_bit_cast(bf16x8, __builtin_nontemporal_load((const s16x8_nt*)(wp1 + (size_t)st * 512)));
+        } else {
+          b0[u] = *(const bf16x8*)(wp0 + (size_t)st * 512);
+          b1[u] = *(const bf16x8*)(wp1 + (size_t)st * 512);
+        }
         a0[u] = ldA0(st);
         if (TWO) a1[u] = ldA1(st);
       }
@@ -2140,6 +2151,24 @@ __global__ TW_DEC_LB(256, 1) void k_gemv_pc(const bf16_t* __restrict__ A, int ld
     else if (rem > 0) batch(std::integral_constant<int, (U / 2 > 0 ? U / 2 : 1)>{}, st, rem);
   }
   const int cc = lane & 15, rb = (lane >> 4) * 4;
+  if constexpr (KW == 1) {  // the accumulators are the results: 16 lanes per row store 16 consecutive columns
+    auto st1 = [&](int m, int n, float v) {
+      if constexpr (EPI == TW_EPI_PARTIAL) ((float*)ea.out)[((size_t)blockIdx.y * M + m) * ea.ldo + n] = v;
+      else if constexpr (EPI == TW_EPI_GELU_PACKED)
+        ((bf16_t*)ea.out)[tw_pack_act_idx(m, n)] = f32_to_bf16(gelu_erf(v + (ea.bias ? ea.bias[n] : 0.f)));
+      else epi_store<EPI>(ea, m, n, v);
+    };
+    const int n0 = g0 * 16 + cc, n1 = n0 + 16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = rb + r;
+      if (m < M && n0 < N) st1(m, n0, c00[r]);
+      if (m < M && n1 < N) st1(m, n1, c10[r]);
+      if (TWO && 16 + m < M && n0 < N) st1(16 + m, n0, c01[r]);
+      if (TWO && 16 + m < M && n1 < N) st1(16 + m, n1, c11[r]);
+    }
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     red[wid][0][rb + r][cc] = c00[r];
@@ -2172,15 +2201,15 @@ __global__ TW_DEC_LB(256, 1) void k_gemv_pc(const bf16_t* __restrict__ A, int ld
   }
 }
 
-template <int EPI, int KW, bool APACK>
+template <int EPI, int KW, bool APACK, int U = 5, bool NTW = false>
 static void launch_gemv_pc(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea,
                            int splits, hipStream_t s) {
   constexpr int GPB = 4 / KW;
   dim3 grid(tw_cdiv(tw_cdiv(tw_cdiv(N, 16), 2), GPB), splits);
   if (M > 16)
-    hipLaunchKernelGGL((k_gemv_pc<EPI, KW, 5, APACK, true>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
+    hipLaunchKernelGGL((k_gemv_pc<EPI, KW, U, APACK, true, NTW>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
   else
-    hipLaunchKernelGGL((k_gemv_pc<EPI, KW, 5, APACK, false>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
+    hipLaunchKernelGGL((k_gemv_pc<EPI, KW, U, APACK, false, NTW>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
 }
 
 template <int EPI, int KW, int U, bool APACK, bool NTW = false>
@@ -2248,6 +2277,12 @@ static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
       if (pairs * kp < 1024 && steps >= 8 * 4) kp = 4;
       if (kp == 2) launch_gemv_pc<EPI, 2, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
       else launch_gemv_pc<EPI, 4, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
+      return;
+    }
+  }
+  if constexpr (EPI == TW_EPI_F32) {
+    if (tw_proj_pairs && wide && kw == 1 && splits == 1) {  // proj_out in column-group pairs (variant bit 29: off)
+      launch_gemv_pc<EPI, 1, APACK, 6, true>(A, lda, Wp, M, N, K, ea, splits, s);
       return;
     }
   }
