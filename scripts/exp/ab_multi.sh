@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 for i in $(seq 1 $reps); do
   for e in "$@"; do
     if [ "$e" = "-" ]; then ev=""; else ev="$e"; fi
-    env $ev timeout -k 10 300 python bench.py --steps $steps --warmup 2 --no-cpu-baseline > gpurun_out/ab.log 2>&1 || { echo "$e FAILED"; tail -5 gpurun_out/ab.log; exit 1; }
+    env $ev timeout -k 10 300 python bench.py --steps $steps --warmup ${AB_WARMUP:-2} --no-cpu-baseline > gpurun_out/ab.log 2>&1 || { echo "$e FAILED"; tail -5 gpurun_out/ab.log; exit 1; }
     echo "$e $(tail -1 gpurun_out/ab.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['achieved'])")"
   done
 done

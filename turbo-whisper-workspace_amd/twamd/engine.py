@@ -150,6 +150,11 @@ class WhisperEngine:
         self._gemm_beside = int(os.environ.get("TW_GEMM_BESIDE", "1"), 0)
         if self._gemm_variant_fixed:
             _lib.call("tw_gemm_set_variant", int(os.environ["TW_GEMM_VARIANT"], 0))
+        # tw_gemm_set_variant bits OR-ed in for a decode pass with nothing of the encoder beside it (a single batch,
+        # the pipeline's last one): e.g. 0x0C000000 = proj_out with 4 K-slices (22.7 vs 33 us alone). 0: the in-situ
+        # forms everywhere
+        self._dec_alone_bits = int(os.environ.get("TW_DEC_ALONE_BITS", "0"), 0)
+        self._pass_alone = False
         if os.environ.get("TW_GEMM_MX_VARIANT"):
             _lib.call("tw_gemm_mx_set_variant", int(os.environ["TW_GEMM_MX_VARIANT"], 0))
         if os.environ.get("TW_GEMM_GROUP"):
@@ -904,6 +909,9 @@ class WhisperEngine:
                 self._align = None
         st = self.gen.special
         dev = self.device
+        self._pass_alone = bool(self._dec_alone_bits) and self._pump is None and not self._gemm_variant_fixed
+        if self._pass_alone:  # (the next encoder chunk queued re-selects its own kernels: _set_gemm_context)
+            _lib.call("tw_gemm_set_variant", self._gemm_alone | self._dec_alone_bits)
         self.stream.wait_event(self._enc_ev[self._slot])  # the cross-K/V of this slot is written
         detect = st.is_multilingual and lang_ids is None
         params = self._select_params(0, max_new, use_timestamps)
@@ -937,7 +945,7 @@ class WhisperEngine:
         # (their host-to-device copy is not capturable)
         if self.use_graphs and self.prompt_graph and (detect or not st.is_multilingual):
             al = self._align  # (keyed like _graph_for: an alignment pass captures the probability-recording kernel)
-            key = ("prompt", R, tuple(int(t) for t in tail), max_new, use_timestamps, self._slot,
+            key = ("prompt", R, tuple(int(t) for t in tail), max_new, use_timestamps, self._slot, self._pass_alone,
                    None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()))
             g = self._graphs.get(key)
             if g is None:
@@ -1118,7 +1126,7 @@ class WhisperEngine:
 
     def _graph_for(self, R: int, params, i: int, v: DecView, fused: bool = False) -> Optional[torch.cuda.CUDAGraph]:
         al = self._align
-        key = (R, params.max_new, params.use_timestamps, self._slot, i, fused,
+        key = (R, params.max_new, params.use_timestamps, self._slot, i, fused, self._pass_alone,
                None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()))
         g = self._graphs.get(key)
         if g is not None:
