@@ -346,9 +346,9 @@ def test_decode_attention_self_and_cross():
 
 
 @pytest.mark.parametrize("Sx", [1500, 33, 7])
-@pytest.mark.parametrize("mode", [0, 0x400, 0x200, 0x100, 0xFF000, 0x2000, 0x1000000, 0x2000000, 0x3000000],
-                         ids=["lean", "online256", "online512", "two_pass", "cached", "nt_from1", "lean_unr12",
-                              "lean_unr4", "lean_unr6"])
+@pytest.mark.parametrize("mode", [0, 0x400, 0x200, 0x100, 0xFF000, 0x2000, 0x1000000, 0x2000000, 0x3000000,
+                                  0x8000000], ids=["lean", "online256", "online512", "two_pass", "cached", "nt_from1",
+                                                   "lean_unr12", "lean_unr4", "lean_unr6", "lean_other_arith"])
 def test_attn_decode_cross_variants(Sx, mode):
     """tw_attn_decode_cross (one-pass online softmax over 32 key groups, the default; over 64 groups; and the two-pass
     form) vs fp32 attention, with key counts that leave 8-lane groups without keys (7) or with one partial chunk (33)."""

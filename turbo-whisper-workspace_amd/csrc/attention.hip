@@ -568,6 +568,10 @@ extern "C" int tw_attn_set_lds_pad(int units) {
   return 0;
 }
 static int tw_dec_self2 = 1;  // decoder self-attention in one memory round trip (k_attn_decode_self2)
+#ifndef TW_DEC_CROSS_PK
+#define TW_DEC_CROSS_PK 0
+#endif
+static int tw_dec_cross_pk = TW_DEC_CROSS_PK;  // lean cross-attention in packed arithmetic (tw_attn_set_variant bit 27)
 static int tw_dec_self3 = 0;  // ... in its 2-wave form (k_attn_decode_self3; tw_attn_set_variant bit 26)
 static int tw_dec_cross_lean = 1;  // the one-pass cross-attention in its small-LDS form (0: the 15 KiB form; A/B)
 static int tw_dec_cross_unr = 8;   // key rows in flight per 8-lane group of the lean form (tw_attn_set_variant bits 24-27)
@@ -576,6 +580,8 @@ extern "C" int tw_attn_set_variant(int v) {
   tw_dec_cross_lean = (v & 0x400) ? 0 : 1;  // bit 10: the 15 KiB-LDS one-pass cross-attention (A/B)
   tw_dec_self2 = (v & 0x800) ? 0 : 1;       // bit 11: the round-1 three-round-trip self-attention (A/B)
   tw_dec_self3 = (v & 0x4000000) ? 1 : 0;   // bit 26: the 2-wave one-round-trip self-attention
+  // bit 27: the lean cross-attention's other arithmetic form (packed: dot2 QK and packed-f32 PV; or scalar)
+  tw_dec_cross_pk = (v & 0x8000000) ? !TW_DEC_CROSS_PK : TW_DEC_CROSS_PK;
   tw_dec_cross_1p = (v & 0x100) ? 0 : 1;  // bit 8: the two-pass decoder cross-attention (A/B)
   // bits 12-19: 0 = every slot's cross K/V read non-temporally (default), else 1 + the first slot read so (0xff: none)
   tw_dec_cross_nt = (v >> 12) & 0xff ? ((v >> 12) & 0xff) - 1 : 0;
@@ -1139,7 +1145,7 @@ __global__ __launch_bounds__(NG * 8) void k_attn_decode_cross(const bf16_t* __re
 // workgroups of a decode step took two rounds; these fit several per CU. q comes straight from global memory (each
 // lane its 8 dims), and the 8 key groups of a wave merge their online-softmax states with xor shuffles (lanes of one
 // dim slice: xor 8, 16, 32) before one LDS record per wave; one wave merges the NG/8 records.
-template <int NG, bool NT, int UNR = DA_UNR>
+template <int NG, bool NT, int UNR = DA_UNR, bool PK = false>
 __global__ TW_DEC_LB(NG * 8, UNR <= 4 ? 7 : 1) void k_attn_decode_cross_lean(const bf16_t* __restrict__ q, int D, int S, int Bt,
                                                                 const int* __restrict__ row_map,
                                                                 const bf16_t* __restrict__ ckv,
@@ -1152,8 +1158,8 @@ __global__ TW_DEC_LB(NG * 8, UNR <= 4 ? 7 : 1) void k_attn_decode_cross_lean(con
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = tid >> 3, gl = tid & 7;
   const int slot = row_map ? row_map[b] : b;
   float qv[8];
+  const uint4 qr = *(const uint4*)(q + (size_t)b * D + h * 64 + gl * 8);
   {
-    const uint4 qr = *(const uint4*)(q + (size_t)b * D + h * 64 + gl * 8);
     const bf16_t* qe = (const bf16_t*)&qr;
 #pragma unroll
     for (int e = 0; e < 8; ++e) qv[e] = bf16_to_f32(qe[e]);
@@ -1184,10 +1190,20 @@ __global__ TW_DEC_LB(NG * 8, UNR <= 4 ? 7 : 1) void k_attn_decode_cross_lean(con
     float bm = m;
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const bf16_t* ke = (const bf16_t*)&kk[u];
       float d = 0.f;
+      if constexpr (PK) {  // v_dot2_f32_bf16: two exact bf16 products per issue, no bf16 -> f32 unpacking of K
+        typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+        const unsigned* qw = (const unsigned*)&qr;
+        const unsigned* kw = (const unsigned*)&kk[u];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
+        for (int j = 0; j < 4; ++j)
+          d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, qw[j]), __builtin_bit_cast(bf16x2v, kw[j]), d,
+                                              false);
+      } else {
+        const bf16_t* ke = (const bf16_t*)&kk[u];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
+      }
       d += __shfl_xor(d, 1, 64);
       d += __shfl_xor(d, 2, 64);
       d += __shfl_xor(d, 4, 64);
@@ -1197,15 +1213,38 @@ __global__ TW_DEC_LB(NG * 8, UNR <= 4 ? 7 : 1) void k_attn_decode_cross_lean(con
     if (bm == -INFINITY) continue;  // (no key of this group yet: short key ranges only)
     const float sc = __expf(m - bm);  // 0 on the group's first keys (m = -inf)
     l *= sc;
+    if constexpr (PK) {  // packed f32 (v_pk_mul_f32 / v_pk_fma_f32): the same roundings, half the issues
+      typedef float f32x2v __attribute__((ext_vector_type(2)));
+      f32x2v a2[4];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] *= sc;
+      for (int j = 0; j < 4; ++j) a2[j] = (f32x2v){acc[2 * j], acc[2 * j + 1]} * (f32x2v){sc, sc};
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const float p = __expf(sv[u] - bm);  // 0 for the masked keys
-      l += p;
-      const bf16_t* ve = (const bf16_t*)&vv[u];
+      for (int u = 0; u < UNR; ++u) {
+        const float p = __expf(sv[u] - bm);  // 0 for the masked keys
+        l += p;
+        const unsigned* vw = (const unsigned*)&vv[u];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += p * bf16_to_f32(ve[e]);
+        for (int j = 0; j < 4; ++j) {
+          const f32x2v v2 = {__uint_as_float(vw[j] << 16), __uint_as_float(vw[j] & 0xffff0000u)};
+          a2[j] = __builtin_elementwise_fma((f32x2v){p, p}, v2, a2[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] = a2[j].x;
+        acc[2 * j + 1] = a2[j].y;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] *= sc;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const float p = __expf(sv[u] - bm);  // 0 for the masked keys
+        l += p;
+        const bf16_t* ve = (const bf16_t*)&vv[u];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += p * bf16_to_f32(ve[e]);
+      }
     }
     m = bm;
   }
@@ -1250,6 +1289,11 @@ extern "C" int tw_attn_decode_cross(const bf16_t* q, int B, int H, int S, int Bt
   TW_REQUIRE(q && cross_kv && out && B > 0 && H > 0 && S > 0 && S <= DA_MAXK, "tw_attn_decode_cross: bad args");
   if (tw_dec_cross_lean && tw_dec_cross_1p && tw_dec_cross_ng == 32 && tw_dec_cross_nt == 0) {
     // (every slot non-temporal: the default; the per-slot nt split of the A/B knob stays on the 15 KiB kernel)
+    if (tw_dec_cross_pk && tw_dec_cross_unr == 8) {
+      hipLaunchKernelGGL((k_attn_decode_cross_lean<32, true, 8, true>), dim3(H, B), dim3(256), 0, (hipStream_t)stream,
+                         q, H * 64, S, Bt, row_map, cross_kv, out);
+      return tw_check_launch("tw_attn_decode_cross");
+    }
     if (tw_dec_cross_unr == 12)
       hipLaunchKernelGGL((k_attn_decode_cross_lean<32, true, 12>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, q,
                          H * 64, S, Bt, row_map, cross_kv, out);
