@@ -95,7 +95,9 @@ def main():
         dist.barrier()
     # HIP events around every launch of the dominant kernel (k_gemm_big) on the engine stream, inside the
     # timed region (the encoder is not graph-captured; ~0.3 us per event against 0.2-1 ms per launch)
-    eng.timers, eng.timer_families = ({}, {dom}) if os.environ.get("TW_BENCH_TIMERS", "1") != "0" else (None, None)
+    # (TW_BENCH_EXTRA_FAMILIES="attn_encoder,...": further families timed the same way and listed in kernel_families)
+    extra = {f for f in os.environ.get("TW_BENCH_EXTRA_FAMILIES", "").split(",") if f}
+    eng.timers, eng.timer_families = ({}, {dom} | extra) if os.environ.get("TW_BENCH_TIMERS", "1") != "0" else (None, None)
     if eng.hostprof is not None:
         eng.hostprof.update(replay=0.0, pump=0.0, wait=0.0, steps=0)
     t0 = time.perf_counter()
@@ -123,9 +125,10 @@ def main():
     n_tok = [len(s) for s in seqs]
 
     # dominant kernel: all k_gemm_big launches of the timed steps (every epilogue variant)
-    n_l = max(1, sum(v[0] for v in fam.values()))  # (0 with TW_BENCH_TIMERS=0: A/B runs without events)
-    work = sum(v[1] for v in fam.values())
-    tot_ms = sum(v[2] for v in fam.values())
+    dfam = [v for k, v in fam.items() if k[0] == dom]
+    n_l = max(1, sum(v[0] for v in dfam))  # (0 with TW_BENCH_TIMERS=0: A/B runs without events)
+    work = sum(v[1] for v in dfam)
+    tot_ms = sum(v[2] for v in dfam)
     avg_ms = max(tot_ms / n_l, 1e-9)
     achieved = (work / n_l) / (avg_ms * 1e-3) / 1e12
     families = {f"{k[0]}<{k[1]}>": {"launches": v[0], "tflop": round(v[1] / 1e12, 3), "ms": round(v[2], 3),
