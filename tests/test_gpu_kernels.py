@@ -206,7 +206,7 @@ def _ref_attn(q, k, v):  # [B,H,S,64] fp32, q already scaled
     return torch.softmax(q @ k.transpose(-1, -2), dim=-1) @ v
 
 
-@pytest.mark.parametrize("variant", [8, 10, 11, 12, 13, 14, 9, 4, 0])
+@pytest.mark.parametrize("variant", [8, 10, 11, 12, 13, 14, 15, 9, 4, 0])
 @pytest.mark.parametrize("B,L,H", [(2, 1500, 4), (1, 100, 2), (1, 1500, 20), (3, 1500, 5), (1, 128, 3), (2, 40, 2)])
 def test_encoder_attention_vs_torch(B, L, H, variant):
     _lib.call("tw_attn_set_variant", variant)
@@ -256,7 +256,7 @@ def test_encoder_attention_lds_pad_is_bit_identical(pad):
         _lib.call("tw_attn_set_lds_pad", 9)
 
 
-@pytest.mark.parametrize("variant", [8, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("variant", [8, 10, 11, 12, 13, 14, 15])
 def test_encoder_attention_online_softmax_rescale(variant):
     """Force the running max to jump in a late key tile (rule 26: exercise the rescale branch)."""
     _lib.call("tw_attn_set_variant", variant)

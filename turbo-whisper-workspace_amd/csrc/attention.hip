@@ -592,7 +592,7 @@ extern "C" int tw_attn_set_variant(int v) {
     tw_dec_cross_unr = unr[(v >> 24) & 3];
   }
   v &= 0xff;
-  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9 || (v >= 10 && v <= 14)) ? v : TW_ATTN_DEFAULT;
+  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9 || (v >= 10 && v <= 15)) ? v : TW_ATTN_DEFAULT;
   return 0;
 }
 
@@ -609,6 +609,9 @@ extern "C" int tw_attn_encoder(const bf16_t* qkv, int B, int S, int H, bf16_t* o
   } else if (tw_attn_variant == 14) {  // 12 waves (384 queries) per workgroup: one per CU by registers, no LDS cap
     const int nqb = (S + 383) / 384, nwork = B * H * nqb;
     hipLaunchKernelGGL((k_attn_enc3<12, 4, false>), dim3(nwork), dim3(768), pad, st, qkv, S, H, D, nqb, nwork, out);
+  } else if (tw_attn_variant == 15) {  // 4 waves (128 queries) per workgroup: two per CU under an LDS cap of 2
+    const int nqb = (S + 127) / 128, nwork = B * H * nqb;
+    hipLaunchKernelGGL((k_attn_enc3<4, 4, false>), dim3(nwork), dim3(256), pad, st, qkv, S, H, D, nqb, nwork, out);
   } else if (tw_attn_variant == 12 || tw_attn_variant == 13) {
     const int nqb = (S + 255) / 256, nwork = B * H * nqb;
     if (tw_attn_variant == 12)
