@@ -170,15 +170,38 @@ def main():
                      "launches_per_step": n_l // a.steps,
                      "avg_launch_ms": round(avg_ms, 4), "flop_per_launch": work / n_l},
         "roofline_decode": dec,
+        "parity": None,
         "kernel_families": families,
         "cpu_baseline": None,
     }
+    if rank == 0:
+        out["parity"], out["parity_detail"] = parity_vs_golden(eng, B, T, a.model, fp8)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(dims, gen, T, a.cpu_threads)
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def parity_vs_golden(eng, B, T, model, fp8):
+    """Rank 0's windows 0 (speech) and 23 (silent) of the last timed batch against transformers' fp32 decode of the
+    same seeded weights and audio (tests/golden/turbo.npz, tests/golden/turbo_parity.py): tokens equal, or diverging
+    first at a near-tie within TAU = 0.3 logits; language ids equal. Only the bf16 config-2 workload (24 windows, 128
+    tokens) has a golden; anything else reports None."""
+    if fp8 or B != 24 or T != 128 or model != "large-v3-turbo":
+        return None, {"skipped": "no fp32 golden for this workload"}
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+        import turbo_parity as tp
+
+        z = tp.load()
+        passes, langs = eng.batch_passes[-1], eng.batch_langs[-1]
+        det = {f"window{w}": tp.check_bench_window(z, w, passes[w][0], langs[w]) for w in tp.BENCH_WINDOWS}
+    except Exception as e:  # reported, never allowed to sink the GPU number
+        return False, {"error": repr(e)[:200]}
+    ok = all(r["lang_ok"] and r["status"] in ("exact", "within_tau") for r in det.values())
+    return ok, {"tau": tp.TAU, "reference": "transformers fp32 CPU, tests/golden/turbo.npz", **det}
 
 
 def measured_traffic(kernels, c5: bool = False):

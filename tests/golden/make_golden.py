@@ -301,6 +301,205 @@ def make_word(out):
                    "audio": "speech_like(40,5)+white_noise(35,11)", "cases": cases}, f)
 
 
+def make_defaults(out):
+    """The decode the ASR pipeline actually runs (num_beams / max_new_tokens reaching model.generate) for
+    checkpoint generation configs x call kwargs: Pipeline.__init__'s default-config resolution ($TF/pipelines/
+    base.py:887-908) and _forward's generate call (automatic_speech_recognition.py:483-529)."""
+    from transformers import AutomaticSpeechRecognitionPipeline, WhisperFeatureExtractor
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    tk = hf_tokenizer(gen.special)
+    ckpts = {"whisper_default": {}, "num_beams_1": {"num_beams": 1}, "num_beams_3": {"num_beams": 3},
+             "no_max_length": {"max_length": None}, "max_new_tokens_64": {"max_new_tokens": 64}}
+    calls = {"reference_call": {"task": "transcribe"}, "greedy": {"task": "transcribe", "num_beams": 1},
+             "mnt_40": {"task": "transcribe", "max_new_tokens": 40}}
+    cases = []
+    for cname, cfg in ckpts.items():
+        m = hf_model(d, sd, gen)
+        for k, v in cfg.items():
+            setattr(m.generation_config, k, v)
+        pipe = AutomaticSpeechRecognitionPipeline(model=m, feature_extractor=fe, tokenizer=tk, device=-1)
+        seen = {}
+
+        def spy(*a, _orig=m.generate, **kw):
+            gc = kw["generation_config"]
+            seen.update(num_beams=kw.get("num_beams", gc.num_beams),
+                        max_new_tokens=kw.get("max_new_tokens", gc.max_new_tokens),
+                        max_length=kw.get("max_length", gc.max_length))
+            raise StopIteration  # the resolved values are all that is wanted
+
+        m.generate = spy
+        for kname, kw in calls.items():
+            seen.clear()
+            try:
+                pipe(np.zeros(16000, np.float32), generate_kwargs=dict(kw), return_timestamps=True)
+            except (StopIteration, RuntimeError):
+                pass
+            cases.append({"checkpoint_generation_config": cfg, "generate_kwargs": kw, "resolved": dict(seen)})
+    with open(os.path.join(out, "defaults.json"), "w") as f:
+        json.dump({"transformers": __import__("transformers").__version__, "cases": cases}, f, indent=1)
+
+
+def make_ckpt(out):
+    """transformers' WhisperTokenizer loaded FROM a checkpoint directory written by tests/ckpt_util.py (byte-level
+    vocab.json with multi-byte UTF-8 tokens, merges.txt, added_tokens.json): decode() of seeded id lists, and the
+    special-token layout it reports."""
+    import tempfile
+
+    from transformers import WhisperTokenizer
+
+    sys.path.insert(0, os.path.dirname(HERE))
+    import ckpt_util as cu
+
+    st = GenerationSettings.default(DIMS).special
+    with tempfile.TemporaryDirectory() as d:
+        cu.write_tokenizer(d, st)
+        tk = WhisperTokenizer.from_pretrained(d)
+        cases = [{"ids": ids, "text": tk.decode(ids)} for ids in cu.decode_cases(st)]
+        layout = {k: tk.convert_tokens_to_ids(k) for k in ("<|endoftext|>", "<|startoftranscript|>", "<|en|>",
+                                                           "<|transcribe|>", "<|notimestamps|>", "<|0.00|>",
+                                                           "<|30.00|>")}
+        special = sorted(tk.all_special_ids)
+    with open(os.path.join(out, "ckpt_decode.json"), "w", encoding="utf-8") as f:
+        json.dump({"transformers": __import__("transformers").__version__, "vocab_size": len(tk), "layout": layout,
+                   "all_special_ids": special, "cases": cases}, f, ensure_ascii=False)
+
+
+TURBO_CLIPS = ("speech30", "noise12")
+TURBO_BENCH_WINDOWS = (0, 23)   # bench.py's rank-0 workload(24): window 0 speech_like(30, 1234), window 23 silent
+
+
+def _passes_from_segments(segs, prompt_len):
+    """Raw generated tokens (prompt stripped, trailing pads/EOS kept as generated) of every seek pass, from
+    generate(return_segments=True): consecutive segments of one pass share its `result` sequence."""
+    passes, last = [], None
+    for s in segs:
+        r = s["result"]
+        if last is not None and r is last:
+            continue
+        last = r
+        r = (r["sequences"] if isinstance(r, dict) else r).reshape(-1)
+        passes.append([int(t) for t in r[prompt_len:].tolist()])
+    return passes
+
+
+def _teacher_forced_pass_scores(m, feats, seek, prompt, toks, g, use_ts=True, k=16):
+    """transformers' logits along one seek pass (features sliced at `seek` and zero-padded, as _get_input_segment
+    does), run through the processor chain (oracle.process_logits, itself pinned to transformers' processors by
+    the test-mini goldens): per step the top-k processed scores and the timestamp-rule margin. These let a
+    device decode be checked within a stated tolerance at its first divergence from the fp32 sequence."""
+    seg = np.zeros_like(feats)
+    seg[:, : 3000 - seek] = feats[:, seek:]
+    ids = list(prompt) + [t for t in toks]
+    with torch.no_grad():
+        lg = m(input_features=torch.from_numpy(seg[None]), decoder_input_ids=torch.tensor([ids[:-1] if toks else ids])
+               ).logits[0].numpy()
+    lg = lg[len(prompt) - 1:]
+    top_i, top_v, margin = [], [], []
+    for t in range(len(toks)):
+        s = wo.process_logits(lg[t], toks[:t], g, use_ts)
+        order = np.argsort(-s, kind="stable")[:k]
+        top_i.append(order)
+        top_v.append(s[order])
+        margin.append(wo._ts_rule_margin(wo.process_logits_no_rule(lg[t], toks[:t], g), g.ts_begin) if use_ts else 0.0)
+    return (np.array(top_i, np.int32).reshape(-1, k), np.array(top_v, np.float32).reshape(-1, k),
+            np.array(margin, np.float32))
+
+
+def make_turbo(out):
+    """large-v3-turbo dims (d 1280, 32 + 4 layers, 20 heads, vocab 51866) with the seeded synthetic weights: the
+    encoder output, teacher-forced logits, generate() tokens + language, and bench.py's first-pass decode of two
+    of its windows (EOS suppressed, 128 new tokens), all from transformers on CPU fp32."""
+    from transformers import WhisperFeatureExtractor
+    from twamd.synth_audio import workload
+
+    d = PRESETS["large-v3-turbo"]
+    gen = GenerationSettings.default(d)
+    st = gen.special
+    g = wo.GenCfg(d.vocab, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate,
+                  st.notimestamps, gen.suppress_tokens, gen.begin_suppress_tokens)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    del sd
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    cl = clips()
+    feats = np.stack([fe(cl[k], sampling_rate=16000, return_tensors="np")["input_features"][0] for k in TURBO_CLIPS])
+    res = {}
+    with torch.no_grad():
+        enc = m.model.encoder(torch.from_numpy(feats)).last_hidden_state.numpy()
+    res["enc_rows_idx"] = np.array([0, 1, 2, 375, 750, 1124, 1498, 1499])
+    res["enc_rows"] = enc[:, res["enc_rows_idx"]].astype(np.float32)
+    res["enc_mean"] = enc.mean(axis=(1, 2))
+    res["enc_std"] = enc.std(axis=(1, 2))
+    res["enc_row_norm"] = np.linalg.norm(enc, axis=2).astype(np.float32)      # [2][1500]
+    res["enc_col_mean"] = enc.mean(axis=1).astype(np.float32)                 # [2][1280]
+    del enc
+    with torch.no_grad():
+        lang = m.detect_language(input_features=torch.from_numpy(feats)).numpy()
+    res["gen_lang"] = lang
+    with torch.no_grad():
+        o = m.generate(torch.from_numpy(feats), task="transcribe", return_timestamps=True, num_beams=1,
+                       max_new_tokens=40, return_segments=True)
+    res["gen_sequences"] = o["sequences"].numpy()
+    for i in range(len(TURBO_CLIPS)):
+        passes = _passes_from_segments(o["segments"][i], 3)
+        pr = [st.sot, int(lang[i]), st.transcribe]
+        seek, ti, tv, mg, kept = 0, [], [], [], []
+        offs = [0]
+        for p in passes:
+            toks = p[: p.index(st.eot) + 1] if st.eot in p else p
+            a, b, c = _teacher_forced_pass_scores(m, feats[i], seek, pr, toks, g)
+            ti.append(a); tv.append(b); mg.append(c)
+            seq = toks[:-1] if toks and toks[-1] == st.eot else toks
+            seg, off = wo.retrieve_segment(seq, 3000 - seek, g.ts_begin)
+            kept += seg
+            seek += off
+            offs.append(seek)
+        ref = [int(t) for t in res["gen_sequences"][i]]
+        while ref and ref[-1] == st.eot:
+            ref.pop()
+        assert kept == ref, ("pass reconstruction differs from generate()", i)
+        res[f"gen{i}_pass_len"] = np.array([len(x) for x in ti], np.int32)
+        res[f"gen{i}_pass_tokens"] = np.concatenate(
+            [np.array(p[: len(x)], np.int32) for p, x in zip(passes, ti)]) if passes else np.zeros(0, np.int32)
+        res[f"gen{i}_pass_seek"] = np.array(offs[:-1], np.int32)
+        res[f"gen{i}_top_idx"], res[f"gen{i}_top_val"] = np.concatenate(ti), np.concatenate(tv)
+        res[f"gen{i}_ts_margin"] = np.concatenate(mg)
+    # teacher-forced raw logits along clip 0's first pass (24 positions), as test-mini's model.npz
+    p0 = [st.sot, int(lang[0]), st.transcribe] + [int(t) for t in res["gen0_pass_tokens"][:21]]
+    res["tf_input_ids"] = np.array(p0[:24])
+    with torch.no_grad():
+        lg = m(input_features=torch.from_numpy(feats[:1]), decoder_input_ids=torch.tensor([p0[:24]])).logits[0].numpy()
+    top = np.argsort(-lg, axis=1, kind="stable")[:, :16]
+    res["tf_top_idx"] = top
+    res["tf_top_val"] = np.take_along_axis(lg, top, 1).astype(np.float32)
+    res["tf_lse"] = (np.log(np.exp(lg - lg.max(1, keepdims=True)).sum(1)) + lg.max(1)).astype(np.float64)
+    # bench.py's decode: EOS suppressed, 128 new tokens, first seek pass only (max_passes=1)
+    wl = workload(24, 30.0, seed=1234)
+    bfeats = np.stack([fe(wl[w], sampling_rate=16000, return_tensors="np")["input_features"][0]
+                       for w in TURBO_BENCH_WINDOWS])
+    gb = wo.GenCfg(d.vocab, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate,
+                   st.notimestamps, list(gen.suppress_tokens) + [st.eot], gen.begin_suppress_tokens)
+    with torch.no_grad():
+        blang = m.detect_language(input_features=torch.from_numpy(bfeats)).numpy()
+    m.generation_config.suppress_tokens = list(gen.suppress_tokens) + [st.eot]
+    for j, w in enumerate(TURBO_BENCH_WINDOWS):
+        # the seek loop's first pass (seek 0) is what bench.py decodes (max_passes=1); later passes are discarded
+        with torch.no_grad():
+            o = m.generate(torch.from_numpy(bfeats[j: j + 1]), task="transcribe", return_timestamps=True,
+                           num_beams=1, max_new_tokens=128, return_segments=True)
+        p = _passes_from_segments(o["segments"][0], 3)[0]
+        a, b, c = _teacher_forced_pass_scores(m, bfeats[j], 0, [st.sot, int(blang[j]), st.transcribe], p, gb)
+        res[f"bench_w{w}_lang"] = np.array([blang[j]], np.int32)
+        res[f"bench_w{w}_tokens"] = np.array(p, np.int32)
+        res[f"bench_w{w}_top_idx"], res[f"bench_w{w}_top_val"], res[f"bench_w{w}_ts_margin"] = a, b, c
+    m.generation_config.suppress_tokens = list(gen.suppress_tokens)
+    np.savez_compressed(os.path.join(out, "turbo.npz"), **res)
+
+
 def _jsonable(x):
     if isinstance(x, dict):
         return {k: _jsonable(v) for k, v in x.items()}

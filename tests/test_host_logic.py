@@ -127,10 +127,10 @@ class _OracleTranscriber(TurboTranscriber):
         self.engine = _E()
 
     def transcribe_windows(self, wav, windows, task, lang_id, return_timestamps, max_new_tokens=None, num_beams=1,
-                           word_timestamps=False, num_frames=None):
-        if word_timestamps:  # batches of `word_batch` windows, as the HF pipeline's batch_size groups them
+                           word_timestamps=False, num_frames=None, group=None):
+        if word_timestamps:  # batches of `group` windows: the product passes the pipeline's batch_size
             out, self.last_window_token_timestamps = [], []
-            B = getattr(self, "word_batch", 1)
+            B = group or 1
             heads = getattr(self, "alignment_heads", None) or self.gen.alignment_heads
             for b0 in range(0, len(windows), B):
                 feats = [wo.log_mel(wav[w.start: w.start + min(w.length, 480000)], self.n_mels)
@@ -172,7 +172,6 @@ def test_pipeline_word_timestamps_host_flow_matches_transformers():
     tr.alignment_heads = [tuple(h) for h in gold["alignment_heads"]]
     x = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)])
     for case in gold["cases"]:
-        tr.word_batch = case["kwargs"].get("batch_size", 1)
         r = tr(x[: case["n_samples"]], generate_kwargs={"task": "transcribe", "num_beams": 1, "max_new_tokens": 40},
                return_timestamps="word", **case["kwargs"])
         assert json.loads(json.dumps(r)) == case["output"], case["name"]

@@ -69,9 +69,16 @@ def load_transcription_model(self, model_name: str = DEFAULT_MODEL) -> bool:
         return False
 
 
-def install(reference_module) -> None:
+def install(reference_module, overlap_diarization: bool = False) -> None:
     """Patch the reference's AudioProcessingPipeline (module `vocalis.core.audio_pipeline` or the root
-    `audio_pipeline`) so its transcription callable is the MI355X engine. Its own _PIPELINE_CACHE is used."""
+    `audio_pipeline`) so its transcription callable is the MI355X engine. Its own _PIPELINE_CACHE is used.
+
+    overlap_diarization (BASELINE config 4): `process_audio` still runs the reference's own code, but the host-CPU
+    diarizer (sherpa-onnx, vocalis/core/model.py:451-470) is started in a worker thread when the call begins, so it
+    runs while the GPU transcribes instead of after it (the reference runs them back to back,
+    vocalis/core/audio_pipeline.py:589-624). The reference's later `load_diarizer` / `diarize` calls with the same
+    arguments then return the worker's results, so every result key is identical and only processing_times
+    change."""
     cls = reference_module.AudioProcessingPipeline
     cache = reference_module._PIPELINE_CACHE
 
@@ -81,6 +88,89 @@ def install(reference_module) -> None:
 
     _load.__doc__ = load_transcription_model.__doc__
     cls.load_transcription_model = _load
+    if overlap_diarization and not getattr(cls, "_tw_overlap", False):
+        _install_overlap(cls)
+
+
+def _install_overlap(cls) -> None:
+    import concurrent.futures
+    import inspect
+    import threading
+
+    orig_process, orig_load, orig_diarize = cls.process_audio, cls.load_diarizer, cls.diarize
+    defaults = {k: v.default for k, v in inspect.signature(orig_process).parameters.items()
+                if v.default is not inspect.Parameter.empty}
+
+    def process_audio(self, audio_path, *args, **kwargs):
+        bound = inspect.signature(orig_process).bind(self, audio_path, *args, **kwargs)
+        a = {**defaults, **bound.arguments}
+        load_key = (a["segmentation_model"], a["embedding_model"], a["num_speakers"], a["threshold"])
+        diar_key = (audio_path, a["num_speakers"])
+        pool = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="tw-diarize")
+        loaded = threading.Event()
+        state = {"load_key": load_key, "diar_key": diar_key, "loaded": loaded}
+
+        def work():
+            try:
+                need = self.diarizer is None or self.diarizer.segmentation_model != load_key[0] or \
+                    self.diarizer.embedding_model != load_key[1]
+                state["load_result"] = orig_load(self, *load_key) if need else True
+            finally:
+                loaded.set()
+            return orig_diarize(self, *diar_key)
+
+        state["future"] = pool.submit(work)
+        pool.shutdown(wait=False)
+        self._tw_prefetch = state
+        try:
+            return orig_process(self, audio_path, *args, **kwargs)
+        finally:
+            self._tw_prefetch = None
+
+    def load_diarizer(self, segmentation_model, embedding_model, num_speakers=2, threshold=0.5):
+        st = getattr(self, "_tw_prefetch", None)
+        if st is not None and st["load_key"] == (segmentation_model, embedding_model, num_speakers, threshold):
+            st["loaded"].wait()
+            if "load_result" in st:
+                return st["load_result"]
+        return orig_load(self, segmentation_model, embedding_model, num_speakers, threshold)
+
+    def diarize(self, audio_path, num_speakers=2):
+        st = getattr(self, "_tw_prefetch", None)
+        if st is not None and st.get("future") is not None and st["diar_key"] == (audio_path, num_speakers):
+            fut, st["future"] = st["future"], None
+            return fut.result()
+        return orig_diarize(self, audio_path, num_speakers)
+
+    process_audio.__doc__ = orig_process.__doc__
+    cls.process_audio, cls.load_diarizer, cls.diarize = process_audio, load_diarizer, diarize
+    cls._tw_overlap = True
+
+
+def create_transcript_with_speakers(transcript_segments, diarization_segments, layout: str = "vocalis"):
+    """SpeakerDiarizer.create_transcript_with_speakers: vocalis/core/diar.py:184-247 (dict or DiarizationSegment
+    diarization entries) and, for layout="root", diar.py:171-228 (attribute access only, so dict entries raise
+    AttributeError there, as in the reference). Transcript segments need 'text', 'start', 'end' (HF chunks lack
+    'start': KeyError, as in the reference)."""
+    result: List[Dict[str, Any]] = []
+    if not diarization_segments:
+        return [{"speaker": f"Speaker {i % 2}", "text": seg["text"], "start": seg["start"], "end": seg["end"]}
+                for i, seg in enumerate(transcript_segments)]
+    for seg in transcript_segments:
+        start_time, end_time, text = seg["start"], seg["end"], seg["text"]
+        speaker, max_overlap = "Unknown", 0
+        for d in diarization_segments:
+            if layout == "vocalis" and isinstance(d, dict):
+                ds, de, sp = d["start"], d["end"], d["speaker"]
+            else:
+                ds, de, sp = d.start_time, d.end_time, f"Speaker {d.speaker_id}"
+            overlap = max(0, min(end_time, de) - max(start_time, ds))
+            if overlap > max_overlap:
+                max_overlap, speaker = overlap, sp
+        if max_overlap == 0:
+            speaker = f"Speaker {len(result) % 2}"
+        result.append({"speaker": speaker, "text": text, "start": start_time, "end": end_time})
+    return result
 
 
 class AudioProcessingPipeline:
@@ -93,19 +183,23 @@ class AudioProcessingPipeline:
         # BASELINE config 4: run the host-CPU diarizer concurrently with the GPU transcription (the reference runs
         # them back to back, :589-624); results are identical, only processing_times change
         self.overlap_diarization = overlap_diarization
+        import torch
+
+        self.gpu_available = torch.cuda.is_available()  # the reference's _setup_gpu result (:49-114)
         if transcriber is not None and _PIPELINE_CACHE["transcription_model"] is None:
             _PIPELINE_CACHE["transcription_model"] = transcriber
 
     load_transcription_model = load_transcription_model
 
-    def transcribe(self, audio_path: str, task: str = "transcribe", return_timestamps: bool = True,
-                   batch_size: int = 512) -> Dict[str, Any]:
-        """:323-369 — the reference's exact call (chunk_length_s=60, stride_length_s=5) on the engine."""
+    def transcribe(self, audio_path: str, task: str = "transcribe", return_timestamps: bool = True) -> Dict[str, Any]:
+        """:323-369 — the reference's exact call (chunk_length_s=60, batch_size=512 on a GPU / 32 on CPU,
+        stride_length_s=5, generate_kwargs={"task": task}) on the engine."""
         if self.transcription_model is None:
             if not self.load_transcription_model():
                 return {"error": "Failed to load transcription model"}
         try:
-            return self.transcription_model(audio_path, chunk_length_s=60, batch_size=batch_size, stride_length_s=5,
+            return self.transcription_model(audio_path, chunk_length_s=60,
+                                            batch_size=512 if self.gpu_available else 32, stride_length_s=5,
                                             generate_kwargs={"task": task}, return_timestamps=return_timestamps)
         except Exception as e:
             print(f"Error during transcription: {e}")
@@ -125,8 +219,7 @@ class AudioProcessingPipeline:
                      "end": s.get("end", 0)} for i, s in enumerate(segs)]
         # the reference hands these to SpeakerDiarizer.create_transcript_with_speakers (vocalis/core/diar.py:
         # 184-247), which reads seg['start'] and so raises KeyError on HF chunks; reproduced as-is
-        return [{"speaker": _speaker_at(diarization_segments, s["start"], s["end"]), "text": s.get("text", ""),
-                 "start": s["start"], "end": s["end"]} for s in segs]
+        return create_transcript_with_speakers(segs, diarization_segments)
 
     def process_audio(self, audio_path: str, task: str = "transcribe",
                       segmentation_model: str = "pyannote/segmentation-3.0",
@@ -177,11 +270,63 @@ class AudioProcessingPipeline:
             return {"error": f"Processing error: {str(e)}"}
 
 
-def _speaker_at(diar, start, end) -> str:
-    best, ov = "Unknown", 0.0
-    for d in diar:
-        ds, de = (d["start"], d["end"]) if isinstance(d, dict) else (d.start, d.end)
-        o = min(end, de) - max(start, ds)
-        if o > ov:
-            ov, best = o, (d["speaker"] if isinstance(d, dict) else d.speaker)
-    return best
+class RootAudioProcessingPipeline(AudioProcessingPipeline):
+    """Mirror of the ROOT copy's result layout (/root/reference/audio_pipeline.py:610-799; used by app.py:66,
+    security_monitor.py:21 and the bar scripts): the result carries audio_path/task/num_speakers/threshold, the
+    transcript under "chunks", the diarization as "segments", and the merge converts each chunk's `timestamp` into
+    start/end (:779-789) before SpeakerDiarizer.create_transcript_with_speakers (diar.py:171-228, attribute access:
+    dict diarization entries raise AttributeError, and the root diarizer's DiarizationSegment objects are not
+    subscriptable at :676-682, so any non-empty diarization ends in the reference's "Processing error" result)."""
+
+    def _merge_transcription_with_diarization(self, transcription, diarization_segments):
+        chunks = transcription.get("chunks", [])
+        if not chunks:
+            return []
+        segs = [{"text": c["text"], "start": c["timestamp"][0], "end": c["timestamp"][1]} for c in chunks
+                if "timestamp" in c]
+        if not segs:
+            return []
+        return create_transcript_with_speakers(segs, diarization_segments, layout="root")
+
+    def process_audio(self, audio_path: str, task: str = "transcribe", segmentation_model: str = "",
+                      embedding_model: str = "", num_speakers: int = 2, threshold: float = 0.5) -> Dict[str, Any]:
+        result: Dict[str, Any] = {"audio_path": audio_path, "task": task, "num_speakers": num_speakers,
+                                  "threshold": threshold, "processing_times": {}}
+        try:
+            start_time = time.time()
+            result["duration"] = audio.duration_seconds(audio_path)
+            if self.transcription_model is None and not self.load_transcription_model():
+                return {"error": "Failed to load transcription model"}
+            diar_future = None
+            if self.overlap_diarization and self.diarize_fn:
+                import concurrent.futures
+
+                pool = concurrent.futures.ThreadPoolExecutor(max_workers=1)
+                t_d = time.time()
+                diar_future = pool.submit(self.diarize_fn, audio_path, num_speakers)
+                pool.shutdown(wait=False)
+            t0 = time.time()
+            transcription = self.transcribe(audio_path, task)
+            result["processing_times"]["transcription"] = time.time() - t0
+            if isinstance(transcription, dict) and "error" in transcription:
+                return transcription
+            result["text"] = transcription.get("text", "")
+            result["chunks"] = transcription.get("chunks", [])
+            if diar_future is not None:
+                diarization_segments = diar_future.result()
+                result["processing_times"]["diarization"] = time.time() - t_d
+            else:
+                t0 = time.time()
+                diarization_segments = self.diarize_fn(audio_path, num_speakers) if self.diarize_fn else []
+                result["processing_times"]["diarization"] = time.time() - t0
+            result["segments"] = [{"start": s["start"], "end": s["end"], "speaker": s["speaker"],
+                                   "text": s.get("text", "")} for s in diarization_segments]
+            t0 = time.time()
+            result["merged_segments"] = self._merge_transcription_with_diarization(transcription,
+                                                                                   diarization_segments)
+            result["processing_times"]["merge"] = time.time() - t0
+            result["processing_times"]["total"] = time.time() - start_time
+            return result
+        except Exception as e:
+            print(f"Error in audio processing pipeline: {e}")
+            return {"error": f"Processing error: {str(e)}"}

@@ -130,7 +130,12 @@ class GenerationSettings:
     max_initial_timestamp_index: Optional[int] = 50
     max_length: int = 448
     max_new_tokens: Optional[int] = None
+    # generation_config.json's num_beams: what model.generate() uses when the call does not pass one (the ASR
+    # pipeline callable overrides it with its own default 5, see pipeline.resolve_decode)
     num_beams: int = 1
+    # False when a checkpoint's generation_config.json leaves max_length unset (GenerationConfig's global default
+    # 20 then applies inside transformers, and the pipeline keeps its max_new_tokens=256)
+    max_length_set: bool = True
     # token-level timestamps (return_timestamps="word"): cross-attention heads used for DTW and the median filter
     # width (generation_config.alignment_heads, config.median_filter_width)
     alignment_heads: Optional[List[Tuple[int, int]]] = None
@@ -162,7 +167,9 @@ class GenerationSettings:
             if cfg.get("begin_suppress_tokens") is not None:
                 gs.begin_suppress_tokens = list(cfg["begin_suppress_tokens"])
             gs.max_initial_timestamp_index = cfg.get("max_initial_timestamp_index", gs.max_initial_timestamp_index)
-            gs.max_length = cfg.get("max_length", gs.max_length)
+            gs.max_length_set = cfg.get("max_length") is not None
+            gs.max_length = cfg.get("max_length") or gs.max_length
+            gs.num_beams = int(cfg.get("num_beams") or 1)
             if cfg.get("alignment_heads"):
                 gs.alignment_heads = [(int(a), int(b)) for a, b in cfg["alignment_heads"]]
         cfn = os.path.join(path, "config.json")

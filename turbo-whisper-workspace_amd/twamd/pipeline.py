@@ -29,6 +29,32 @@ from .weights import build_weights
 
 _NAME_TO_CODE = {v: k for k, v in LANGUAGE_NAMES.items()}
 
+# AutomaticSpeechRecognitionPipeline._default_generation_config ($TF/pipelines/automatic_speech_recognition.py:160-163)
+PIPELINE_DEFAULT_NUM_BEAMS = 5
+PIPELINE_DEFAULT_MAX_NEW_TOKENS = 256
+_GLOBAL_DEFAULT_MAX_LENGTH = 20  # GenerationConfig's own max_length default
+
+
+def resolve_decode(gen: GenerationSettings, gk: Dict[str, Any]) -> Dict[str, Any]:
+    """The decode the HF ASR pipeline runs when called the way the reference calls it.
+
+    Pipeline.__init__ ($TF/pipelines/base.py:887-908) prepares the pipeline's generation config from its class
+    default {max_new_tokens: 256, num_beams: 5} through `_prepare_generation_config` ($TF/generation/utils.py:
+    1771-1830): values the default sets are kept, only unset ones are filled from the checkpoint's
+    generation_config.json. So `num_beams` is 5 whatever the checkpoint says, unless the call passes it in
+    generate_kwargs (the reference passes only {"task": task}, vocalis/core/audio_pipeline.py:351-358). The pipeline's
+    max_new_tokens=256 is then dropped in favour of the checkpoint's max_length when that is set and differs from
+    GenerationConfig's global default 20 (Whisper checkpoints set 448). Pinned by tests/golden/defaults.json, made
+    by transformers itself (tests/golden/make_golden.py defaults).
+
+    Returns {"num_beams", "max_new_tokens"} (max_new_tokens None = bounded by max_length)."""
+    nb = gk.get("num_beams")
+    mnt = gk.get("max_new_tokens")
+    if mnt is None and "max_new_tokens" not in gk:
+        ml = gen.max_length if gen.max_length_set else _GLOBAL_DEFAULT_MAX_LENGTH
+        mnt = None if ml != _GLOBAL_DEFAULT_MAX_LENGTH else PIPELINE_DEFAULT_MAX_NEW_TOKENS
+    return {"num_beams": int(nb) if nb is not None else PIPELINE_DEFAULT_NUM_BEAMS, "max_new_tokens": mnt}
+
 
 class TurboTranscriber:
     """Callable with the HF ASR pipeline signature, backed by WhisperEngine (HIP)."""
@@ -43,10 +69,12 @@ class TurboTranscriber:
     @staticmethod
     def from_pretrained(model: str = "large-v3-turbo", checkpoint: Optional[str] = None, seed: int = 1234,
                         max_batch: int = 24, device: str = "cuda", use_graphs: bool = True,
-                        max_beams: int = 1, enc_fp8: Optional[bool] = None) -> "TurboTranscriber":
+                        max_beams: int = PIPELINE_DEFAULT_NUM_BEAMS, enc_fp8: Optional[bool] = None
+                        ) -> "TurboTranscriber":
         """`model`: a preset name (synthetic seeded weights) or, via `checkpoint`, a LOCAL Hugging Face
-        Whisper directory (config.json, *.safetensors, vocab.json, generation_config.json). enc_fp8: run the encoder
-        projections on MX fp8 (BASELINE config 5; default: env TW_ENC_FP8)."""
+        Whisper directory (config.json, *.safetensors, vocab.json, generation_config.json). max_beams: decoder rows
+        per window (the callable's default decode is beam-5, as the HF pipeline's; 1 = greedy-only engine). enc_fp8:
+        run the encoder projections on MX fp8 (BASELINE config 5; default: env TW_ENC_FP8)."""
         if checkpoint is None and model not in PRESETS and os.path.isdir(model):
             checkpoint = model
         if checkpoint is not None:
@@ -74,14 +102,18 @@ class TurboTranscriber:
             raise ValueError("Whisper cannot return `char` timestamps, only word level or segment level timestamps.")
         gk = dict(generate_kwargs or {})
         gk.update({k: kwargs.pop(k) for k in list(kwargs) if k in ("max_new_tokens", "language", "task", "num_beams")})
-        num_beams = int(gk.pop("num_beams", 1) or 1)
+        dec = resolve_decode(self.gen, gk)  # as shipped: beam-5, bounded by max_length (see resolve_decode)
+        gk.pop("num_beams", None)
+        gk.pop("max_new_tokens", None)
+        num_beams = dec["num_beams"]
         if num_beams < 1 or num_beams > 8:
             raise ValueError(f"num_beams={num_beams}: the engine supports 1 (greedy) to 8 beams")
         if word and num_beams > 1:
-            raise NotImplementedError("word-level timestamps with beam search are not implemented (greedy only)")
+            raise NotImplementedError("word-level timestamps with beam search are not implemented; pass "
+                                      "generate_kwargs={'num_beams': 1} (the pipeline's default decode is beam-5)")
         task = gk.pop("task", None)
         language = gk.pop("language", None)
-        max_new_tokens = gk.pop("max_new_tokens", None)
+        max_new_tokens = dec["max_new_tokens"]
         st = self.gen.special
         if not st.is_multilingual and (task is not None or language is not None):
             raise ValueError("Cannot specify `task` or `language` for an English-only model.")
@@ -123,7 +155,7 @@ class TurboTranscriber:
                       for x in ws]
                 toks = self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=True,
                                                max_new_tokens=max_new_tokens, num_beams=num_beams,
-                                               word_timestamps=True, num_frames=nf)
+                                               word_timestamps=True, num_frames=nf, group=batch_size)
                 return [(t, ts) for t, ts in zip(toks, self.last_window_token_timestamps)]
             return self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=bool(return_timestamps),
                                            max_new_tokens=max_new_tokens, num_beams=num_beams)
@@ -149,12 +181,17 @@ class TurboTranscriber:
     def transcribe_windows(self, wav: np.ndarray, windows: Sequence[Window], task: Optional[str],
                            lang_id: Optional[int], return_timestamps: bool,
                            max_new_tokens: Optional[int] = None, num_beams: int = 1, word_timestamps: bool = False,
-                           num_frames: Optional[Sequence[int]] = None) -> List[List[int]]:
+                           num_frames: Optional[Sequence[int]] = None, group: Optional[int] = None) -> List[List[int]]:
         """Log-mel + generate for every window; returns per-window token sequences (generate() output,
         right-padded with the pad token within each engine batch, as the HF batch output is). Batches of
-        max_batch windows go through WhisperEngine.run_batches: batch k+1 is encoded while batch k decodes."""
+        max_batch windows go through WhisperEngine.run_batches: batch k+1 is encoded while batch k decodes.
+
+        group: windows per engine batch when the batch's composition changes results. That is the case only for
+        word timestamps, whose per-pass standardisation runs over the padded batch, so the pipeline's
+        `batch_size` (its DataLoader batch, $TF/pipelines/base.py:1319-1339) is honoured there; segment-level
+        tokens are per-window results, so batching is then only a schedule and the engine fills max_batch."""
         eng = self.engine
-        B = eng.max_batch
+        B = eng.max_batch if not group else max(1, min(int(group), eng.max_batch))
         parts = [windows[b0: b0 + B] for b0 in range(0, len(windows), B)]
 
         def load(k):  # called on the engine's encoder stream
