@@ -18,11 +18,9 @@ import torch
 def _hf_state_dict(dims, seed: int) -> Dict[str, torch.Tensor]:
     from oracle import whisper_oracle as wo
 
-    sd = {}
-    for name, shape in wo.param_shapes(dims.d_model, dims.encoder_layers, dims.decoder_layers, dims.ffn,
-                                       dims.n_mels, dims.vocab):
-        tid, scale, off = wo.synth_spec(name, shape, dims.d_model)
-        sd[name] = torch.from_numpy(wo.synth_uniform(seed, tid, int(np.prod(shape)), scale, off).reshape(shape))
+    sd = {k: torch.from_numpy(v) for k, v in wo.synth_state_dict(dims.d_model, dims.encoder_layers,
+                                                                   dims.decoder_layers, dims.ffn, dims.n_mels,
+                                                                   dims.vocab, seed).items()}
     sd["proj_out.weight"] = sd["model.decoder.embed_tokens.weight"]
     return sd
 

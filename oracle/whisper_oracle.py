@@ -102,11 +102,19 @@ def synth_spec(name: str, shape: Tuple[int, ...], D: int) -> Tuple[int, float, f
 
 
 def synth_state_dict(D, L_enc, L_dec, F, n_mels, V, seed) -> Dict[str, np.ndarray]:
-    sd = {}
-    for name, shape in param_shapes(D, L_enc, L_dec, F, n_mels, V):
+    """Every parameter, generated tensor by tensor on a thread pool (numpy's integer ufuncs release the GIL)."""
+    import concurrent.futures
+    import os
+
+    shapes = param_shapes(D, L_enc, L_dec, F, n_mels, V)
+
+    def one(item):
+        name, shape = item
         tid, scale, off = synth_spec(name, shape, D)
-        sd[name] = synth_uniform(seed, tid, int(np.prod(shape)), scale, off).reshape(shape)
-    return sd
+        return name, synth_uniform(seed, tid, int(np.prod(shape)), scale, off).reshape(shape)
+
+    with concurrent.futures.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        return dict(ex.map(one, shapes))
 
 
 # ----------------------------------------------------------------------------- log-mel

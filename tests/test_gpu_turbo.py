@@ -3,13 +3,14 @@
 accumulation and residual stream) against transformers on CPU fp32 (tests/golden/turbo.npz, make_golden.py turbo;
 SURVEY §8c(ii)). The reference call being matched is vocalis/core/audio_pipeline.py:195-200 / :351-358.
 
-Tolerances (written here, measured margins in DESIGN.md §2):
+Tolerances (written here; about 3x the errors measured on MI355X, profiles/r03b_gputest.txt: encoder rows max 0.017,
+mean 0.0028, row norms 3e-4 relative, mean/std 3e-5; teacher-forced logits 0.025):
   encoder output   LayerNorm-scale outputs (std 1.0): |diff| <= ENC_MAX_ABS on the committed rows, mean |diff| <=
-                   ENC_MEAN_ABS, per-row L2 norms within ENC_NORM_REL relative, mean/std within 5e-3
+                   ENC_MEAN_ABS, per-row L2 norms within ENC_NORM_REL relative, mean/std within ENC_MOMENT
   decoder logits   teacher-forced over 24 positions: the 16 fp32-top logits within LOGIT_ABS, log-sum-exp within
                    LOGIT_ABS, same argmax wherever the fp32 top-2 margin exceeds TAU
   tokens           generate() and the bench decode equal to the fp32 sequences, or diverging first at a near-tie
-                   within TAU = 0.3 logits (tests/golden/turbo_parity.py); language ids equal
+                   within TAU = 0.15 logits (2 x LOGIT_ABS; tests/golden/turbo_parity.py); language ids equal
 """
 import os
 import sys
@@ -25,10 +26,11 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
 import turbo_parity as tp  # noqa: E402
 
 pytestmark = pytest.mark.gpu
-ENC_MAX_ABS = 0.25
-ENC_MEAN_ABS = 0.03
-ENC_NORM_REL = 0.01
-LOGIT_ABS = 0.3
+ENC_MAX_ABS = 0.05
+ENC_MEAN_ABS = 0.008
+ENC_NORM_REL = 1e-3
+ENC_MOMENT = 2e-4
+LOGIT_ABS = 0.08
 TAU = tp.TAU
 EOT = 50257
 
@@ -80,7 +82,7 @@ def test_turbo_encoder_vs_transformers(turbo, z):
               f"; col-mean max|d| {np.abs(enc[i].mean(0) - z['enc_col_mean'][i]).max():.4f}")
         assert d.max() <= ENC_MAX_ABS and d.mean() <= ENC_MEAN_ABS, (i, d.max(), d.mean())
         assert norm_rel.max() <= ENC_NORM_REL
-        assert abs(enc[i].mean() - z["enc_mean"][i]) < 5e-3 and abs(enc[i].std() - z["enc_std"][i]) < 5e-3
+        assert abs(enc[i].mean() - z["enc_mean"][i]) < ENC_MOMENT and abs(enc[i].std() - z["enc_std"][i]) < ENC_MOMENT
         assert np.all(np.isfinite(enc[i]))
 
 
