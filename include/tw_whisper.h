@@ -103,13 +103,10 @@ int tw_im2col_conv2(const uint16_t* h1, int R, int D, uint16_t* out, void* strea
  * cached by EncoderDecoderCache (:312-335). */
 int tw_gemm_bf16(const uint16_t* A, const uint16_t* W, int M, int N, int K, int lda, int ldw, int epi, void* out,
                  int ldo, const float* bias, const float* aux, int aux_rows, const int* kv_geom, void* stream);
-/* Measurement knob (process-wide, returns 0). Bits 0..2 select the large-M GEMM kernel of tw_gemm_bf16:
- * 1 = 256x256 2-stage BK=64 LDS-DMA (default; the engine switches to 5 for an encoder that runs without a decode
- * beside it), 0 = 128x128 register-staged, 3 = 256x256 counted-vmcnt + setprio, 4 = 256x128 3-stage ring,
- * 5 = 8-phase ping-pong, 6 = persistent 8-phase, 7 = 256x128 two blocks per CU. Bits 8..15: 4, 8 or 16 force the
- * skinny (M <= 32) kernel's waves per block; bits 16..23: 1/2/4/8 force the packed GEMV's K-slices; bit 24: the
- * packed GEMV of N >= 16384 (proj_out) reads its weights through the caches instead of non-temporally. */
-int tw_gemm_set_variant(int big);
+/* Process-wide kernel choice for the large-M path of tw_gemm_bf16 (returns 0): 1 = k_gemm_big (default: one
+ * barrier per K-tile, 184 VGPRs, the kernel the engine queues beside a running decode step), 5 = k_gemm_8p (8-phase
+ * ping-pong, faster when the encoder has the GPU to itself). Same results either way. */
+int tw_gemm_set_variant(int v);
 /* Split-K partial product for the decoder step (M <= 32 rows, K % 32 == 0): part f32[splits][M][ldp]
  * receives the `splits` partial sums of A . W^T over consecutive K ranges (no bias). Used for the
  * d_model-wide projections (self/cross out_proj, fc2) whose residual add is done by
@@ -138,16 +135,9 @@ int tw_layernorm(const float* x, const float* gamma, const float* beta, int M, i
 int tw_gemm_mx(const uint8_t* A, const uint8_t* Sa, const uint8_t* W, const uint8_t* Sw, int M, int N, int K, int lda,
                int ldw, int Mp, int Np, int epi, void* out, int ldo, const float* bias, uint8_t* sout, int sout_rows,
                void* stream);
-/* Measurement knob (process-wide, returns 0): tw_gemm_mx's kernel, 0 = chosen by shape (default),
- * 1 = k_gemm_mx (2-stage), 8 = k_gemm_8p_mx (8-phase ping-pong). */
+/* Process-wide (returns 0): tw_gemm_mx's kernel, 0 = chosen by shape (default), 1 = k_gemm_mx (2-stage),
+ * 8 = k_gemm_8p_mx (8-phase ping-pong); the forced forms exist so that tests cover both kernels on every shape. */
 int tw_gemm_mx_set_variant(int v);
-/* Measurement knob (process-wide, returns 0): tile rows per group of the large-M GEMM tile order (0 = by shape,
- * the default: 8 for N >= 2560, else 1; 1 = row-major: one A row panel against every W column panel in turn).
- * Applies to tw_gemm_bf16 and tw_gemm_mx. */
-int tw_gemm_set_group(int group_m);
-/* Measurement knob (process-wide, returns 0): the largest K-slice count (waves per column group) the packed decoder
- * GEMV picks, 1/2/4/8 (default 4: workgroups of <= 256 threads, co-resident with an encoder GEMM workgroup). */
-int tw_gemv_set_max_kw(int kw);
 /* bf16 src[rows][ld] -> MX fp8 dst[rows][K] + scales (K % 128 == 0). Encoder weights once at load; the
  * attention output before out_proj (modeling_whisper.py:350-356). */
 int tw_quant_mx(const uint16_t* src, int rows, int K, int ld, uint8_t* dst, uint8_t* scales, int rows_pad,
@@ -177,8 +167,6 @@ int tw_attn_set_variant(int variant);
  * so that decoder kernels launched beside it on another stream find free wave slots (the engine sets 4 for encoder
  * chunks queued beside a decode, 0 otherwise). Returns 0, or TW_ERR_ARG. */
 int tw_attn_set_lds_pad(int units);
-/* Decoder residual+LayerNorm kernel (A/B): 0 = one wave per row when D == 1280 (default), 1 = the 4-wave block form. */
-int tw_ln_set_variant(int variant);
 
 /* ---- beam search ------------------------------------------------------------------------------ */
 /* GenerationMixin._beam_search ($TF/generation/utils.py:3208-3512) with the Whisper processor chain, for W windows
@@ -226,39 +214,14 @@ int tw_kv_reorder(uint16_t* k_cache, uint16_t* v_cache, uint16_t* k_scratch, uin
  * tw_gemv_packed: out = epi(A . W^T); A packed activation (a_packed = 1) or row-major [M][lda]; epi TW_EPI_BF16,
  *   TW_EPI_F32 (row-major [M][ldo]), TW_EPI_GELU_PACKED (packed activation, N % 32 == 0), TW_EPI_RESID_F32
  *   (f32 [M][ldo] += A.W^T + bias: the decoder's residual update; splits = 1) or TW_EPI_PARTIAL_F32 (splits > 1
- *   allowed; bias ignored).
- * tw_gemv_packed_ln: the same with the A operand = LayerNorm(x) (nn.LayerNorm over K, eps; gamma/beta f32[K]) of the
- *   f32 residual rows x[M][K], computed inside the kernel (the decoder's pre-LayerNorms fused into the projection
- *   that consumes them, modeling_whisper.py:434,443,446); epi TW_EPI_BF16, TW_EPI_F32 or TW_EPI_GELU_PACKED;
- *   K <= 2048. */
+ *   allowed; bias ignored). */
 int tw_pack_weight(const uint16_t* W, int N, int K, int ldw, uint16_t* Wp, void* stream);
 int tw_gemv_packed(const uint16_t* A, int a_packed, int lda, const uint16_t* Wp, int M, int N, int K, int epi,
                    void* out, int ldo, const float* bias, int splits, void* stream);
-int tw_gemv_packed_ln(const float* x, const float* gamma, const float* beta, float eps, const uint16_t* Wp, int M,
-                      int N, int K, int epi, void* out, int ldo, const float* bias, void* stream);
-/* The decoder's LayerNorm across a kernel boundary (no launch of its own): tw_gemv_packed_stats is
- *   tw_gemv_packed(.., TW_EPI_RESID_F32, splits = 1) into x[M][ldx] (N % 16 == 0) that also writes, for every
- *   16-column group g of the updated rows, stats[(g*32 + m)*2 + {0, 1}] = (mean, sum of squared deviations from that
- *   mean) of x[m][16g .. 16g+15]; tw_gemv_packed_lnst is tw_gemv_packed_ln whose row mean / variance come from those
- *   K/16 group statistics (combined pairwise, Chan et al.) instead of a pass over x. stats: f32[N/16][32][2]. */
-int tw_gemv_packed_stats(const uint16_t* A, int a_packed, int lda, const uint16_t* Wp, int M, int N, int K, float* x,
-                         int ldx, const float* bias, float* stats, void* stream);
-int tw_gemv_packed_lnst(const float* x, const float* stats, const float* gamma, const float* beta, float eps,
-                        const uint16_t* Wp, int M, int N, int K, int epi, void* out, int ldo, const float* bias,
-                        void* stream);
 /* tw_resid_layernorm with the normalised rows written as a packed activation (M <= 32, D % 32 == 0). */
 int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
                               const float* beta, int M, int D, float eps, uint16_t* out, void* stream);
 
-/* ---- streams ---------------------------------------------------------------------------------------- */
-/* A HIP stream whose kernels run only on the CUs whose bits are set in mask = uint32[words] (hipExtStream-
- * CreateWithCUMask; the mask belongs to the stream's hardware queue, so hipGraph replays on it are confined too).
- * On MI355X bit i selects CU i/8 of XCD i%8 (measured with scripts/exp/cumask_probe.hip), and an XCD left with
- * no bit falls back to all of its CUs, so a balanced mask sets the same number of bits for every XCD. The engine
- * uses it to give the decoder of window batch k CUs of its own while batch k+1 is encoded (twamd/engine.py).
- * Setup-time calls: they allocate, are not capturable, and tw_stream_destroy synchronises the stream. */
-int tw_stream_create_masked(const uint32_t* mask, int32_t words, void** stream_out);
-int tw_stream_destroy(void* stream);
 /* Decoder self-attention for one new token per row: appends k,v of qkv bf16[B][3D] at pos[b] into
  * k_cache/v_cache bf16[B][H][max_pos][64] (this layer) and attends over 0..pos[b].
  * Replaces the causal self-attention + DynamicCache.update of modeling_whisper.py:312-335,448-505. */

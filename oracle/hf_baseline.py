@@ -68,11 +68,12 @@ def build_pipeline(dims, gen, seed: int = 1234, threads: Optional[int] = None):
 
 def time_reference(dims, gen, audio: np.ndarray, max_new_tokens: int, threads: int, seed: int = 1234,
                    num_beams: int = 1, one_pass: bool = False, chunk_length_s: float = 60,
-                   stride_length_s: float = 5) -> dict:
+                   stride_length_s: float = 5, pipe=None) -> dict:
     """Wall time of the ASR pipeline call on `audio` (default: the reference kwargs chunk 60 / stride 5 /
     batch 32, vocalis/core/audio_pipeline.py:351-358). one_pass: generation_config.force_unique_generate_call
-    (a single seek pass per window)."""
-    pipe = build_pipeline(dims, gen, seed, threads)
+    (a single seek pass per window). pipe: a pipeline from build_pipeline to reuse (weights are built once)."""
+    if pipe is None:
+        pipe = build_pipeline(dims, gen, seed, threads)
     if one_pass:
         pipe.generation_config.force_unique_generate_call = True
     t0 = time.perf_counter()

@@ -211,13 +211,10 @@ __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const f
   tw_row_ln_store<PACKED>(v, s, row, D, eps, g, bta, out, red);
 }
 
-#ifndef TW_LN_HOIST
-#define TW_LN_HOIST 0  // 1: gamma/beta loaded with the row. Measured in the bench: +2.5 ms per step (A/B builds)
-#endif
 // k_resid_ln for D = 256 * NV with ONE wave per row: every lane holds NV float4 chunks (c = lane + 64 i), both
 // LayerNorm reductions are wave shuffles, no LDS round trip or block barrier. A decode step runs 13 of these on 24
-// rows; the 4-wave form spends most of its ~6.8 us in its two barrier-separated reductions (tw_ln_set_variant(1)
-// restores it for A/B).
+// rows; the 4-wave form (k_resid_ln, the fallback for other D) spends most of its ~6.8 us in its two
+// barrier-separated reductions.
 // (min 4 waves per SIMD: <= 128 VGPRs, so a wave fits beside an encoder GEMM workgroup's two ~190-VGPR waves)
 template <bool PACKED, int NV>
 __global__ TW_DEC_LB(64, 4) void k_resid_ln_w(float* __restrict__ x, const float* __restrict__ parts, int nparts,
@@ -228,15 +225,7 @@ __global__ TW_DEC_LB(64, 4) void k_resid_ln_w(float* __restrict__ x, const float
   const int row = blockIdx.x, lane = threadIdx.x;
   float* xr = x + (size_t)row * D;
   const float* pr = parts ? parts + (size_t)row * D : nullptr;
-  // gamma / beta first: their loads fly with the row's instead of after both reductions (one round trip less)
   float4 gg[NV], bb[NV];
-  if (TW_LN_HOIST && g) {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      gg[i] = ((const float4*)g)[lane + 64 * i];
-      bb[i] = ((const float4*)bta)[lane + 64 * i];
-    }
-  }
   // the row, the bias and up to four partials: every load in flight before the first add (one memory round trip;
   // the sched_barrier keeps hipcc from interleaving them with the adds, which serialises them). Summation order as
   // before: ((x + bias) + p0) + p1 + ...
@@ -275,8 +264,9 @@ __global__ TW_DEC_LB(64, 4) void k_resid_ln_w(float* __restrict__ x, const float
         v[i].x += qq.x; v[i].y += qq.y; v[i].z += qq.z; v[i].w += qq.w;
       }
   }
-  // gamma / beta (not hoisted): issued before the two reductions, so their latency hides behind them
-  if (!TW_LN_HOIST && g) {
+  // gamma / beta issued before the two reductions, so their latency hides behind them (loading them with the row
+  // measured +2.5 ms per bench step)
+  if (g) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       gg[i] = ((const float4*)g)[lane + 64 * i];
@@ -314,19 +304,13 @@ __global__ TW_DEC_LB(64, 4) void k_resid_ln_w(float* __restrict__ x, const float
   }
 }
 
-static int tw_ln_variant = 0;  // 0: one wave per row when D == 1280, 1: always the 4-wave k_resid_ln
-extern "C" int tw_ln_set_variant(int v) {
-  tw_ln_variant = v == 1 ? 1 : 0;
-  return 0;
-}
-
 extern "C" int tw_resid_layernorm(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
                                   const float* beta, int M, int D, float eps, uint16_t* out, void* stream) {
   TW_REQUIRE(x && M > 0 && D > 0 && D % 4 == 0 && D <= 1024 * RLN_MAXV, "tw_resid_layernorm: bad args (D %% 4, D <= %d)",
              1024 * RLN_MAXV);
   TW_REQUIRE(nparts >= 0 && (nparts == 0 || parts), "tw_resid_layernorm: parts");
   TW_REQUIRE(!gamma || (beta && out), "tw_resid_layernorm: gamma without beta/out");
-  if (D == 1280 && tw_ln_variant == 0)
+  if (D == 1280)
     hipLaunchKernelGGL((k_resid_ln_w<false, 5>), dim3(M), dim3(64), 0, (hipStream_t)stream, x, parts, nparts,
                        (long)M * D, bias, gamma, beta, D, eps, out);
   else
@@ -341,7 +325,7 @@ extern "C" int tw_resid_layernorm_packed(float* x, const float* parts, int npart
   TW_REQUIRE(x && gamma && beta && out && M > 0 && M <= 32 && D > 0 && D % 32 == 0 && D <= 1024 * RLN_MAXV,
              "tw_resid_layernorm_packed: bad args (M <= 32, D %% 32, gamma/beta/out required)");
   TW_REQUIRE(nparts >= 0 && (nparts == 0 || parts), "tw_resid_layernorm_packed: parts");
-  if (D == 1280 && tw_ln_variant == 0)
+  if (D == 1280)
     hipLaunchKernelGGL((k_resid_ln_w<true, 5>), dim3(M), dim3(64), 0, (hipStream_t)stream, x, parts, nparts,
                        (long)M * D, bias, gamma, beta, D, eps, out);
   else

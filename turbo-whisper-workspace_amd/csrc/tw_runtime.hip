@@ -29,28 +29,6 @@ int tw_check_launch(const char* what) {
 extern "C" const char* tw_last_error(void) { return g_err; }
 extern "C" int tw_version(void) { return TW_ABI_VERSION; }
 
-extern "C" int tw_stream_create_masked(const uint32_t* mask, int32_t words, void** stream_out) {
-  TW_REQUIRE(mask && stream_out && words > 0, "tw_stream_create_masked: null mask/output or no words");
-  hipStream_t s = nullptr;
-  hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
-  if (e != hipSuccess) {
-    tw_set_error("tw_stream_create_masked: %s", hipGetErrorString(e));
-    return TW_ERR_LAUNCH;
-  }
-  *stream_out = (void*)s;
-  return TW_OK;
-}
-
-extern "C" int tw_stream_destroy(void* stream) {
-  TW_REQUIRE(stream, "tw_stream_destroy: null stream");
-  hipError_t e = hipStreamDestroy((hipStream_t)stream);
-  if (e != hipSuccess) {
-    tw_set_error("tw_stream_destroy: %s", hipGetErrorString(e));
-    return TW_ERR_LAUNCH;
-  }
-  return TW_OK;
-}
-
 // splitmix64-style counter hash -> 24-bit signed integer -> exact f32 in (-1, 1).
 __host__ __device__ inline float tw_synth_unit(uint64_t seed, uint32_t tensor_id, uint64_t idx) {
   uint64_t z = (seed * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)(tensor_id + 1u) * 0xD1B54A32D192ED03ull);

@@ -12,8 +12,7 @@ import os
 
 import torch  # noqa: F401  (load torch's HIP runtime before ours)
 
-# TW_LIB selects another in-tree build of the same sources (A/B builds with different compile-time options)
-LIB_PATH = os.environ.get("TW_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtwhip.so")
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtwhip.so")
 
 TW_EPI_BF16 = 0
 TW_EPI_GELU_BF16 = 1
@@ -35,10 +34,10 @@ EXPORTED = (
     "tw_version", "tw_last_error", "tw_fill_synth", "tw_f32_to_bf16", "tw_logmel", "tw_im2col_conv1",
     "tw_im2col_conv2", "tw_gemm_bf16", "tw_layernorm", "tw_attn_encoder", "tw_attn_decode_self",
     "tw_attn_decode_cross", "tw_embed_decoder", "tw_logits_select", "tw_gemm_bf16_partial", "tw_resid_layernorm",
-    "tw_gemm_set_variant", "tw_attn_set_variant", "tw_ln_set_variant",
-    "tw_dtw", "tw_attn_decode_cross_probs", "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_stream_create_masked", "tw_stream_destroy", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
-    "tw_gemm_mx", "tw_quant_mx", "tw_layernorm_mx", "tw_attn_encoder_mx", "tw_gemm_mx_set_variant", "tw_logits_select_embed", "tw_gemm_set_group", "tw_gemv_set_max_kw", "tw_gemv_packed_stats", "tw_gemv_packed_lnst",
-    "tw_attn_set_lds_pad", "tw_gemv_packed_ln",
+    "tw_gemm_set_variant", "tw_attn_set_variant",
+    "tw_dtw", "tw_attn_decode_cross_probs", "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
+    "tw_gemm_mx", "tw_quant_mx", "tw_layernorm_mx", "tw_attn_encoder_mx", "tw_gemm_mx_set_variant", "tw_logits_select_embed",
+    "tw_attn_set_lds_pad",
 )
 
 
@@ -103,13 +102,10 @@ _SIGS = {
     "tw_gemm_bf16_partial": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P], _I),
     "tw_gemm_set_variant": ([_I], _I),
     "tw_gemm_mx_set_variant": ([_I], _I),
-    "tw_gemm_set_group": ([_I], _I),
-    "tw_gemv_set_max_kw": ([_I], _I),
     "tw_logits_select_embed": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), _P, _P, _I, _P, _P, _P, _P, _P, _I,
                                 _I, _P, _P, _P, _F, _P, _I, _P], _I),
     "tw_attn_set_variant": ([_I], _I),
     "tw_attn_set_lds_pad": ([_I], _I),
-    "tw_ln_set_variant": ([_I], _I),
     "tw_resid_layernorm": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
     "tw_dtw": ([_P, _I, _I, _P, _P, _P], _I),
     "tw_attn_decode_cross_probs": ([_P, _I, _I, _I, _I, _P, _P, _P, _P, _U32, _I, _I, _P, _I, _I, _P], _I),
@@ -119,12 +115,7 @@ _SIGS = {
     "tw_kv_reorder": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P], _I),
     "tw_pack_weight": ([_P, _I, _I, _I, _P, _P], _I),
     "tw_gemv_packed": ([_P, _I, _I, _P, _I, _I, _I, _I, _P, _I, _P, _I, _P], _I),
-    "tw_gemv_packed_ln": ([_P, _P, _P, _F, _P, _I, _I, _I, _I, _P, _I, _P, _P], _I),
-    "tw_gemv_packed_stats": ([_P, _I, _I, _P, _I, _I, _I, _P, _I, _P, _P, _P], _I),
-    "tw_gemv_packed_lnst": ([_P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _P, _I, _P, _P], _I),
     "tw_resid_layernorm_packed": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
-    "tw_stream_create_masked": ([_P, _I, ctypes.POINTER(ctypes.c_void_p)], _I),
-    "tw_stream_destroy": ([_P], _I),
     "tw_flac_probe": ([_P, ctypes.c_int64, ctypes.POINTER(TwFlacInfo)], _I),
     "tw_flac_decode": ([_P, ctypes.c_int64, _P, ctypes.c_int64, _I, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_resample_pcm_i32": ([_P, ctypes.c_int64, _I, _F, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),
@@ -135,18 +126,14 @@ _lib = None
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load (once) and type the library; raises if it is missing. TW_LIB names another in-tree build of the same
-    C-ABI (A/B measurement of two builds in one session)."""
+    """Load (once) and type the library; raises if it is missing."""
     global _lib
     if _lib is not None:
         return _lib
-    path = os.environ.get("TW_LIB") or path
     if not os.path.exists(path):
         raise TwError(f"HIP library not built: {path} (run `make -C turbo-whisper-workspace_amd/csrc`)")
     lib = ctypes.CDLL(path)
     for name, (args, res) in _SIGS.items():
-        if os.environ.get("TW_LIB") and not hasattr(lib, name):
-            continue  # an older build under A/B: entry points it predates stay unbound
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res

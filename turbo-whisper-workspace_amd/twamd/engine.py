@@ -16,7 +16,6 @@ from __future__ import annotations
 import ctypes
 import dataclasses
 import os
-import time
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -69,11 +68,9 @@ class DecView:
     n: int
     stream: torch.cuda.Stream
     xd: torch.Tensor
-    hd: torch.Tensor
     qkvd: torch.Tensor
     qd: torch.Tensor
     attd: torch.Tensor
-    ffnd: torch.Tensor
     logits: torch.Tensor
     parts: torch.Tensor
     sel_ws: torch.Tensor
@@ -81,9 +78,8 @@ class DecView:
     tokens: torch.Tensor
     ids: torch.Tensor
     pos: torch.Tensor
-    hp: Optional[torch.Tensor] = None  # packed-activation LayerNorm output (tw_gemv_packed A operand), <= 32 rows
-    fp: Optional[torch.Tensor] = None  # packed-activation fc1 output (fc2's A operand)
-    lst: Optional[torch.Tensor] = None  # f32 [d_model/16][32][2] row statistics of xd (tw_gemv_packed_stats)
+    hp: torch.Tensor   # packed-activation LayerNorm output (tw_gemv_packed A operand), <= 32 rows
+    fp: torch.Tensor   # packed-activation fc1 output (fc2's A operand)
 
 
 class _EncoderPump:
@@ -136,40 +132,15 @@ class PassResult:
 
 class WhisperEngine:
     def __init__(self, weights: PackedWeights, gen: GenerationSettings, max_batch: int = 24,
-                 device: str = "cuda", use_graphs: bool = True, dec_cus: Optional[int] = None, max_beams: int = 1,
+                 device: str = "cuda", use_graphs: bool = True, max_beams: int = 1,
                  enc_fp8: Optional[bool] = None):
         _lib.load()
-        # kernel-variant overrides for A/B measurement (defaults are the measured-best kernels)
         # Large-M GEMM kernel per encoder context (tw_gemm_set_variant): the 8-phase ping-pong k_gemm_8p (5) is 6-19 %
         # faster than k_gemm_big (1) on every encoder shape when it has the GPU to itself (scripts/gemm_bench.py), but
         # beside a running decode it slows the latency-bound decoder kernels more than it gains (bench step 117.1 vs
-        # 113.4 ms). An encoder that runs alone uses 5, one queued beside a decode (run_batches' overlap) uses 1.
-        self._gemm_variant_fixed = bool(os.environ.get("TW_GEMM_VARIANT"))
-        # large-M GEMM kernel per context (tw_gemm_set_variant): alone = no decode beside the encoder chunk
-        self._gemm_alone = int(os.environ.get("TW_GEMM_ALONE", "5"), 0)
-        self._gemm_beside = int(os.environ.get("TW_GEMM_BESIDE", "1"), 0)
-        if self._gemm_variant_fixed:
-            _lib.call("tw_gemm_set_variant", int(os.environ["TW_GEMM_VARIANT"], 0))
-        # tw_gemm_set_variant bits OR-ed in for a decode pass with nothing of the encoder beside it (a single batch,
-        # the pipeline's last one): e.g. 0x0C000000 = proj_out with 4 K-slices (22.7 vs 33 us alone). 0: the in-situ
-        # forms everywhere
-        self._dec_alone_bits = int(os.environ.get("TW_DEC_ALONE_BITS", "0"), 0)
-        self._pass_alone = False
-        if os.environ.get("TW_GEMM_MX_VARIANT"):
-            _lib.call("tw_gemm_mx_set_variant", int(os.environ["TW_GEMM_MX_VARIANT"], 0))
-        if os.environ.get("TW_GEMM_GROUP"):
-            _lib.call("tw_gemm_set_group", int(os.environ["TW_GEMM_GROUP"], 0))
-        if os.environ.get("TW_LN_VARIANT"):
-            _lib.call("tw_ln_set_variant", int(os.environ["TW_LN_VARIANT"], 0))
-        if os.environ.get("TW_GEMV_MAX_KW"):  # A/B: 8 = the round-1 decoder GEMVs of up to 512 threads
-            _lib.call("tw_gemv_set_max_kw", int(os.environ["TW_GEMV_MAX_KW"], 0))
-        if os.environ.get("TW_ATTN_VARIANT"):
-            _lib.call("tw_attn_set_variant", int(os.environ["TW_ATTN_VARIANT"], 0))
-        # encoder-attention LDS cap (16 KiB units) for chunks queued beside a decode; None: leave the library's setting
-        pad = os.environ.get("TW_ATTN_PAD", "4")
-        self._attn_pad_ctx = None if pad == "" else int(pad)
-        # TW_ATTN_BESIDE=v: encoder-attention variant v (no LDS cap) for chunks queued beside a decode, 10 alone
-        self._attn_beside = int(os.environ["TW_ATTN_BESIDE"], 0) if os.environ.get("TW_ATTN_BESIDE") else None
+        # 113.4 ms). An encoder chunk that runs alone uses 5, one queued beside a decode (run_batches' overlap) uses 1.
+        # The encoder attention beside a decode reserves LDS for one workgroup per CU (tw_attn_set_lds_pad 4) so the
+        # decoder's kernels find free wave slots.
         d = weights.dims
         d.validate()
         self.d, self.w, self.gen = d, weights, gen
@@ -181,21 +152,9 @@ class WhisperEngine:
         self.use_graphs = use_graphs
         # a high-priority decoder stream and a default-priority stream for the front end + encoder: the
         # MFMA-bound encoder of the next window batch fills the CUs the latency-bound decode of this one leaves idle,
-        # and the dispatcher serves the decoder's small grids first
-        # dec_cus > 0 partitions the chip instead: the decoder streams own dec_cus CUs of every XCD, the encoder
-        # stream the rest (hipExtStreamCreateWithCUMask; see tw_stream_create_masked)
-        self.dec_cus = int(os.environ.get("TW_DEC_CUS", "0")) if dec_cus is None else int(dec_cus)
-        self._masked: List[int] = []
-        if self.dec_cus > 0:
-            self.stream = self._masked_stream(range(0, 8 * self.dec_cus))
-            self.enc_stream = self._masked_stream(range(8 * self.dec_cus, self._n_cus()))
-        else:
-            self.stream = torch.cuda.Stream(self.device, priority=-1)
-            self.enc_stream = torch.cuda.Stream(self.device, priority=0)
-            # TW_ENC_RESERVE=r keeps the encoder off r CUs of every XCD (the decoder stream stays unmasked)
-            reserve = int(os.environ.get("TW_ENC_RESERVE", "0"))
-            if reserve > 0:
-                self.enc_stream = self._masked_stream(range(8 * reserve, self._n_cus()))
+        # and the dispatcher serves the decoder's small grids first (CU-masked partitions measured slower: DESIGN §4)
+        self.stream = torch.cuda.Stream(self.device, priority=-1)
+        self.enc_stream = torch.cuda.Stream(self.device, priority=0)
         self._enc_ev = [torch.cuda.Event(), torch.cuda.Event()]
         D, F, H, V, B = d.d_model, d.ffn, d.heads, d.vocab, max_batch
         dev, bf, f32, i32 = self.device, torch.bfloat16, torch.float32, torch.int32
@@ -244,11 +203,9 @@ class WhisperEngine:
         self.kcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=bf, device=dev)
         self.vcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=bf, device=dev)
         self.xd = torch.empty(B, D, dtype=f32, device=dev)
-        self.hd = torch.empty(B, D, dtype=bf, device=dev)
         self.qkvd = torch.empty(B, 3 * D, dtype=bf, device=dev)
         self.qd = torch.empty(B, D, dtype=bf, device=dev)
         self.attd = torch.empty(B, D, dtype=bf, device=dev)
-        self.ffnd = torch.empty(B, F, dtype=bf, device=dev)
         self.logits = torch.empty(B, V, dtype=f32, device=dev)
         self.parts = torch.empty(DEC_SPLITS, B, D, dtype=f32, device=dev)   # split-K partials (decoder)
         self.sel_ws = torch.empty(B, _lib.TW_SELECT_WS_PER_ROW, dtype=f32, device=dev)
@@ -268,43 +225,32 @@ class WhisperEngine:
         # concurrent decode chains in the generation loop (measured: two 12-row chains on two streams run no faster
         # than one 24-row chain on MI355X, so one by default)
         self.n_chains = 1
-        self._chain_streams = [self._masked_stream(range(0, 8 * self.dec_cus)) if self.dec_cus > 0 else
-                               torch.cuda.Stream(self.device, priority=-1) for _ in range(self.n_chains)]
+        self._chain_streams = [torch.cuda.Stream(self.device, priority=-1) for _ in range(self.n_chains)]
         self._own_streams = {x.cuda_stream for x in [self.stream, self.enc_stream] + self._chain_streams}
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self._chain_cache: Dict[tuple, List[DecView]] = {}
         self._pump: Optional[_EncoderPump] = None  # paced next-batch encoder (run_batches)
-        # decode steps queued ahead of the host before it pumps encoder chunks or waits: 1 measured 0.8 ms/step
-        # better than 2 (3 interleaved A/B pairs, 108.6 vs 109.5 ms)
-        self.dec_ahead = int(os.environ.get("TW_DEC_AHEAD", "1"))
-        self.pump_ahead = int(os.environ.get("TW_PUMP_AHEAD", "2"))  # encoder chunks pending beside a decode
+        # decode steps queued ahead of the host before it pumps encoder chunks or waits, and encoder chunks pending
+        # beside a decode: 1 and 2 (queue depths 1-3 re-measured within +-0.5 %)
+        self.dec_ahead = 1
+        self.pump_ahead = 2
         # greedy steps end with the fused select + next-step embedding + first LayerNorm (tw_logits_select_embed):
-        # 47 launches per token instead of 49. TW_FUSED_SELECT=0: the separate kernels (A/B)
-        self.fused_select = os.environ.get("TW_FUSED_SELECT", "1") != "0"
-        # the prompt phase of a decode pass replayed as one captured graph (TW_PROMPT_GRAPH=0: eager, A/B)
-        self.prompt_graph = os.environ.get("TW_PROMPT_GRAPH", "1") != "0"
-        self.hostprof = ({"replay": 0.0, "pump": 0.0, "wait": 0.0, "steps": 0}
-                         if os.environ.get("TW_HOSTPROF") == "1" else None)  # decode steps queued ahead while pumping
+        # 47 launches per token instead of 49 (False: the separate launches; the tests check both decode alike)
+        self.fused_select = True
+        # the prompt phase of a decode pass replayed as one captured graph (False: eager)
+        self.prompt_graph = True
+        # run_batches encodes batch k+1 beside the decode of batch k (sequential 138.6 vs overlapped 114.5 ms per
+        # bench step, round 1); False: strictly in turn
+        self.overlap = True
         # decoder projections in the packed fragment layout (tw_pack_weight; +~342 MB at large-v3-turbo): every
-        # wave-load of the per-token GEMVs is one contiguous 1 KiB fragment. TW_DEC_PACKED=0 keeps the row-major
-        # skinny GEMM path (A/B measurement).
-        self.packed_decoder = os.environ.get("TW_DEC_PACKED", "1") != "0"
-        # TW_DEC_LNFUSE=1: decoder pre-LayerNorms fused into the consuming GEMVs, residual adds into the producing ones
-        # (8 launches per layer instead of 11). Measured and NOT the default: every column group of the consuming GEMV
-        # re-normalises the whole operand (LN+q/k/v 12.5 us vs 3.3 + 4.3 us as two launches; bench step 120.4 vs
-        # 102.7 ms)
-        self.ln_fused = self.packed_decoder and os.environ.get("TW_DEC_LNFUSE", "0") == "1"
-        # TW_DEC_LNSTATS=1: the post-attention LayerNorms carried across the kernel boundary as row statistics
-        # (tw_gemv_packed_stats -> tw_gemv_packed_lnst): 9 launches per layer instead of 11
-        self.ln_stats = self.packed_decoder and not self.ln_fused and os.environ.get("TW_DEC_LNSTATS", "0") == "1"
+        # wave-load of the per-token GEMVs is one contiguous 1 KiB fragment
         self.dec_p: List[Dict[str, torch.Tensor]] = []
         self.emb_p: Optional[torch.Tensor] = None
-        if self.packed_decoder:
-            with torch.cuda.device(self.device):
-                self.dec_p = [{k: self._pack(getattr(L, k)) for k in ("wqkv", "wo", "wq_x", "wo_x", "w1", "w2")}
-                              for L in weights.dec]
-                self.emb_p = self._pack(weights.emb)
-                torch.cuda.synchronize(self.device)
+        with torch.cuda.device(self.device):
+            self.dec_p = [{k: self._pack(getattr(L, k)) for k in ("wqkv", "wo", "wq_x", "wo_x", "w1", "w2")}
+                          for L in weights.dec]
+            self.emb_p = self._pack(weights.emb)
+            torch.cuda.synchronize(self.device)
 
     def _quant_weight(self, W: torch.Tensor) -> tuple:
         """bf16 [N][K] -> (fp8 [N][K], e8m0 scales [K/128][Np][4], Np) in the MX layout of tw_gemm_mx."""
@@ -338,53 +284,11 @@ class WhisperEngine:
                   ldo if ldo is not None else N, _lib.ptr(bias), splits, v.stream.cuda_stream)
         self._end_timer(rec, v.stream)
 
-    def _gemv_ln(self, g, b, Wp, M, N, K, epi, out, v: DecView, bias=None, ldo=None):
-        """out = epi(LayerNorm(xd) . W^T + bias): the pre-LayerNorm computed inside the GEMV (tw_gemv_packed_ln)."""
-        rec = self._begin_timer(("gemv_packed", epi), 2.0 * M * N * K, v.stream)
-        _lib.call("tw_gemv_packed_ln", v.xd.data_ptr(), g.data_ptr(), b.data_ptr(), LN_EPS, Wp.data_ptr(), M, N, K,
-                  epi, out.data_ptr(), ldo if ldo is not None else N, _lib.ptr(bias), v.stream.cuda_stream)
-        self._end_timer(rec, v.stream)
-
-    def _gemv_stats(self, A, Wp, M, N, K, v: DecView, bias):
-        """xd += A . W^T + bias (A row-major [M][K]) and the updated rows' group statistics into v.lst."""
-        rec = self._begin_timer(("gemv_packed", _lib.TW_EPI_RESID_F32), 2.0 * M * N * K, v.stream)
-        _lib.call("tw_gemv_packed_stats", A.data_ptr(), 0, K, Wp.data_ptr(), M, N, K, v.xd.data_ptr(), N,
-                  _lib.ptr(bias), v.lst.data_ptr(), v.stream.cuda_stream)
-        self._end_timer(rec, v.stream)
-
-    def _gemv_lnst(self, g, b, Wp, M, N, K, epi, out, v: DecView, bias=None):
-        """out = epi(LayerNorm(xd) . W^T + bias) with xd's row statistics from the producing GEMV (v.lst)."""
-        rec = self._begin_timer(("gemv_packed", epi), 2.0 * M * N * K, v.stream)
-        _lib.call("tw_gemv_packed_lnst", v.xd.data_ptr(), v.lst.data_ptr(), g.data_ptr(), b.data_ptr(), LN_EPS,
-                  Wp.data_ptr(), M, N, K, epi, out.data_ptr(), N, _lib.ptr(bias), v.stream.cuda_stream)
-        self._end_timer(rec, v.stream)
-
-    # timing-only ablations (scripts/exp: upper bounds of a fusion before building it; outputs are WRONG): a
-    # comma list of decoder stages whose launches are skipped, e.g. TW_ABLATE=ln. Never set in the product.
-    _ablate = frozenset(x for x in os.environ.get("TW_ABLATE", "").split(",") if x)
-
     def _resid_ln_p(self, R, nparts, bias, g, b, v: DecView):
         """xd += bias + sum(parts[:nparts]); hp = LayerNorm(xd) as a packed activation."""
-        if "ln" in self._ablate:
-            return
         _lib.call("tw_resid_layernorm_packed", v.xd.data_ptr(), v.parts.data_ptr() if nparts else None, nparts,
                   _lib.ptr(bias), _lib.ptr(g), _lib.ptr(b), R, self.d.d_model, LN_EPS, v.hp.data_ptr(),
                   v.stream.cuda_stream)
-
-    def _n_cus(self) -> int:
-        return torch.cuda.get_device_properties(self.device).multi_processor_count
-
-    def _masked_stream(self, bits) -> torch.cuda.ExternalStream:
-        """A stream confined to the CUs of `bits` (bit i = CU i//8 of XCD i%8 on MI355X)."""
-        n = self._n_cus()
-        mask = (ctypes.c_uint32 * ((n + 31) // 32))()
-        for b in bits:
-            mask[b // 32] |= 1 << (b % 32)
-        h = ctypes.c_void_p()
-        with torch.cuda.device(self.device):
-            _lib.call("tw_stream_create_masked", mask, len(mask), ctypes.byref(h))
-        self._masked.append(h.value)
-        return torch.cuda.ExternalStream(h.value, device=self.device)
 
     def set_suppress_tokens(self, tokens: Sequence[int]) -> None:
         """SuppressTokensLogitsProcessor's list as a device bitmask (in place: captured graphs stay valid)."""
@@ -468,16 +372,14 @@ class WhisperEngine:
                 self._chain_cache[key] = self._view(r0, n, self.stream, self.parts)
             return self._chain_cache[key]
         sl = slice(r0, r0 + n)
-        hp = fp = None
-        lst = None
-        if self.packed_decoder and n <= 32:  # per-view packed scratch (rows 0..n-1 of the view; pad rows zero)
-            hp = torch.zeros(32 * self.d.d_model, dtype=torch.bfloat16, device=self.device)
-            fp = torch.zeros(32 * self.d.ffn, dtype=torch.bfloat16, device=self.device)
-            lst = torch.zeros(self.d.d_model // 16 * 32 * 2, dtype=torch.float32, device=self.device)
-        return DecView(r0, n, stream or self.stream, self.xd[sl], self.hd[sl], self.qkvd[sl], self.qd[sl],
-                       self.attd[sl], self.ffnd[sl], self.logits[sl],
-                       self.parts if parts is None else parts, self.sel_ws[sl], self.state[sl], self.tokens[sl],
-                       self.ids[sl], self.pos[sl], hp, fp, lst)
+        if n > 32:
+            raise ValueError(f"decoder views hold <= 32 rows (packed GEMV), got {n}")
+        # per-view packed scratch (rows 0..n-1 of the view; pad rows zero)
+        hp = torch.zeros(32 * self.d.d_model, dtype=torch.bfloat16, device=self.device)
+        fp = torch.zeros(32 * self.d.ffn, dtype=torch.bfloat16, device=self.device)
+        return DecView(r0, n, stream or self.stream, self.xd[sl], self.qkvd[sl], self.qd[sl], self.attd[sl],
+                       self.logits[sl], self.parts if parts is None else parts, self.sel_ws[sl], self.state[sl],
+                       self.tokens[sl], self.ids[sl], self.pos[sl], hp, fp)
 
     def use_slot(self, slot: int) -> None:
         """Point the decoder at the cross-K/V (and feature) buffers of pipeline slot `slot`."""
@@ -512,12 +414,8 @@ class WhisperEngine:
         the encoder attention capped at one workgroup per CU beside a decode (tw_attn_set_lds_pad: the decoder's
         kernels then find free wave slots; measured decoder GEMV 21.9 -> 5.6 us per launch beside it, bench step
         112.1 -> 108.5 ms), uncapped alone (the cap costs the attention itself 22 %)."""
-        if not self._gemm_variant_fixed:
-            _lib.call("tw_gemm_set_variant", self._gemm_alone if alone else self._gemm_beside)
-        if self._attn_beside is not None:  # a different encoder-attention kernel beside a decode (A/B)
-            _lib.call("tw_attn_set_variant", 10 if alone else self._attn_beside)
-        elif self._attn_pad_ctx is not None:
-            _lib.call("tw_attn_set_lds_pad", 0 if alone else self._attn_pad_ctx)
+        _lib.call("tw_gemm_set_variant", 5 if alone else 1)
+        _lib.call("tw_attn_set_lds_pad", 0 if alone else 4)
 
     def _encode_steps(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True,
                       alone: bool = True):
@@ -551,23 +449,16 @@ class WhisperEngine:
         yield
         if self.enc_fp8:
             yield from self._encode_layers_mx(R, st)
-        ab = self._ablate
         for L in ([] if self.enc_fp8 else w.enc):
-            if "eln" not in ab:
-                self._ln(self.x, L.ln1_g, L.ln1_b, M15, self.hln, stream=st)
-            if "egemm" not in ab:
-                self._gemm(self.hln, L.wqkv, M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv, stream=st)
+            self._ln(self.x, L.ln1_g, L.ln1_b, M15, self.hln, stream=st)
+            self._gemm(self.hln, L.wqkv, M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv, stream=st)
             rec = self._begin_timer(("attn_encoder", 0), 4.0 * S_ENC * S_ENC * 64 * H * R, st)
-            if "eattn" not in ab:
-                _lib.call("tw_attn_encoder", self.qkv.data_ptr(), R, S_ENC, H, self.att.data_ptr(), s)
+            _lib.call("tw_attn_encoder", self.qkv.data_ptr(), R, S_ENC, H, self.att.data_ptr(), s)
             self._end_timer(rec, st)
-            if "egemm" not in ab:
-                self._gemm(self.att, L.wo, M15, D, D, _lib.TW_EPI_RESID_F32, self.x, bias=L.bo, stream=st)
-            if "eln" not in ab:
-                self._ln(self.x, L.ln2_g, L.ln2_b, M15, self.hln, stream=st)
-            if "egemm" not in ab:
-                self._gemm(self.hln, L.w1, M15, F, D, _lib.TW_EPI_GELU_BF16, self.ffn, bias=L.b1, stream=st)
-                self._gemm(self.ffn, L.w2, M15, D, F, _lib.TW_EPI_RESID_F32, self.x, bias=L.b2, stream=st)
+            self._gemm(self.att, L.wo, M15, D, D, _lib.TW_EPI_RESID_F32, self.x, bias=L.bo, stream=st)
+            self._ln(self.x, L.ln2_g, L.ln2_b, M15, self.hln, stream=st)
+            self._gemm(self.hln, L.w1, M15, F, D, _lib.TW_EPI_GELU_BF16, self.ffn, bias=L.b1, stream=st)
+            self._gemm(self.ffn, L.w2, M15, D, F, _lib.TW_EPI_RESID_F32, self.x, bias=L.b2, stream=st)
             yield
         self._ln(self.x, w.enc_ln_g, w.enc_ln_b, M15, self.hln, stream=st)  # encoder last_hidden_state (bf16)
         geom = (ctypes.c_int * 4)(S_ENC, R, D, H)
@@ -606,19 +497,6 @@ class WhisperEngine:
         return self.hln[: R * S_ENC].view(R, S_ENC, self.d.d_model)
 
     # ------------------------------------------------------------------ decoder
-    def _partial(self, A, W, M, N, K, v: DecView):
-        """v.parts[:DEC_SPLITS, :M] = split-K partial sums of A . W^T (decoder; residual add in _resid_ln)."""
-        rec = self._begin_timer(("gemm_skinny", "partial"), 2.0 * M * N * K, v.stream)
-        _lib.call("tw_gemm_bf16_partial", A.data_ptr(), W.data_ptr(), M, N, K, K, K, DEC_SPLITS, v.parts.data_ptr(),
-                  N, v.stream.cuda_stream)
-        self._end_timer(rec, v.stream)
-
-    def _resid_ln(self, R, nparts, bias, g, b, v: DecView):
-        """xd += bias + sum(parts[:nparts]); hd = LayerNorm(xd) (one fused launch)."""
-        _lib.call("tw_resid_layernorm", v.xd.data_ptr(), v.parts.data_ptr() if nparts else None, nparts,
-                  _lib.ptr(bias), _lib.ptr(g), _lib.ptr(b), R, self.d.d_model, LN_EPS, _lib.ptr(v.hd),
-                  v.stream.cuda_stream)
-
     @on_engine_streams
     def decoder_step(self, R: int, with_logits: bool = True, v: Optional[DecView] = None, r_enc: Optional[int] = None,
                      pre_embedded: bool = False) -> None:
@@ -627,52 +505,18 @@ class WhisperEngine:
         pre_embedded: the view's xd and first-layer LayerNorm output already hold this step's input (written by the
         previous step's fused select, _select(embed_next=True)); the step starts at layer 0's q/k/v projection.
 
-        Residual stream xd stays f32; every d_model-wide projection (self/cross out_proj, fc2) is a split-K
-        partial product whose sum, bias and residual add are folded into the next LayerNorm launch."""
-        d, w = self.d, self.w
-        if v is None and R > 32:  # the decoder GEMVs / skinny GEMMs take <= 32 rows: one pass per 32
+        WhisperDecoder.forward / WhisperDecoderLayer.forward ($TF/models/whisper/modeling_whisper.py:690-795, 448-505)
+        on the packed-GEMV path: the residual stream xd stays f32; LayerNorm outputs and fc1's GELU output are packed
+        activations (the GEMVs' A operand), attention outputs stay row-major; every d_model-wide projection (self /
+        cross out_proj, fc2) is a split-K partial product whose sum, bias and residual add are folded into the next
+        LayerNorm launch."""
+        if v is None and R > 32:  # the packed decoder GEMVs take <= 32 rows: one view per 32
             r_enc = R if r_enc is None else r_enc
             for r0 in range(0, R, 32):
                 self.decoder_step(min(32, R - r0), with_logits, self._view(r0, min(32, R - r0)), r_enc, pre_embedded)
             return
-        v = v or self._view()
+        v = v or self._view(0, R)
         r_enc = R if r_enc is None else r_enc
-        D, F, H, T = d.d_model, d.ffn, d.heads, d.max_target_positions
-        st = v.stream
-        s = st.cuda_stream
-        if v.hp is not None:
-            return self._decoder_step_packed(R, with_logits, v, r_enc, pre_embedded)
-        if not pre_embedded:
-            _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), v.ids.data_ptr(), v.pos.data_ptr(), R,
-                      D, v.xd.data_ptr(), s)
-        xkv_stride = 2 * r_enc * H * S_ENC * 64
-        nparts, pbias = 0, None
-        for li, L in enumerate(w.dec):
-            if li or not pre_embedded:
-                self._resid_ln(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
-            self._gemm(v.hd, L.wqkv, R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, bias=L.bqkv, stream=st)
-            _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
-                      self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
-            self._partial(v.attd, L.wo, R, D, D, v)
-            self._resid_ln(R, DEC_SPLITS, L.bo, L.ln2_g, L.ln2_b, v)
-            self._gemm(v.hd, L.wq_x, R, D, D, _lib.TW_EPI_BF16, v.qd, bias=L.bq_x, stream=st)
-            ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
-            rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
-            self._cross_attend(li, R, r_enc, rmap, ckv, v)
-            self._end_timer(rec, st)
-            self._partial(v.attd, L.wo_x, R, D, D, v)
-            self._resid_ln(R, DEC_SPLITS, L.bo_x, L.ln3_g, L.ln3_b, v)
-            self._gemm(v.hd, L.w1, R, F, D, _lib.TW_EPI_GELU_BF16, v.ffnd, bias=L.b1, stream=st)
-            self._partial(v.ffnd, L.w2, R, D, F, v)
-            nparts, pbias = DEC_SPLITS, L.b2
-        if with_logits:
-            self._resid_ln(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
-            self._gemm(v.hd, w.emb, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, stream=st)
-
-    def _decoder_step_packed(self, R: int, with_logits: bool, v: DecView, r_enc: int, pre_embedded: bool = False
-                             ) -> None:
-        """decoder_step on the packed-GEMV path: LayerNorm outputs and fc1's GELU output are packed activations,
-        attention outputs stay row-major, the d_model-wide projections are split-K partials (as decoder_step)."""
         d, w = self.d, self.w
         D, F, H, T = d.d_model, d.ffn, d.heads, d.max_target_positions
         st = v.stream
@@ -681,10 +525,6 @@ class WhisperEngine:
             _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), v.ids.data_ptr(), v.pos.data_ptr(), R,
                       D, v.xd.data_ptr(), s)
         xkv_stride = 2 * r_enc * H * S_ENC * 64
-        if self.ln_fused:
-            return self._decoder_layers_lnfused(R, with_logits, v, r_enc, xkv_stride)
-        if self.ln_stats:
-            return self._decoder_layers_lnstats(R, with_logits, v, r_enc, xkv_stride, pre_embedded)
         nparts, pbias = 0, None
         PART, K4 = _lib.TW_EPI_PARTIAL_F32, DEC_SPLITS
         for li, L in enumerate(w.dec):
@@ -692,86 +532,18 @@ class WhisperEngine:
             if li or not pre_embedded:
                 self._resid_ln_p(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
             self._gemv(v.hp, True, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
-            if "self" not in self._ablate:
-                _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
-                          self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
+            _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
+                      self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
             self._gemv(v.attd, False, P["wo"], R, D, D, PART, v.parts, v, splits=K4)
             self._resid_ln_p(R, K4, L.bo, L.ln2_g, L.ln2_b, v)
             self._gemv(v.hp, True, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
             ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
             rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
-            if "cross" not in self._ablate:
-                self._cross_attend(li, R, r_enc, rmap, ckv, v)
+            self._cross_attend(li, R, r_enc, rmap, ckv, v)
             self._end_timer(rec, st)
             self._gemv(v.attd, False, P["wo_x"], R, D, D, PART, v.parts, v, splits=K4)
             self._resid_ln_p(R, K4, L.bo_x, L.ln3_g, L.ln3_b, v)
             self._gemv(v.hp, True, P["w1"], R, F, D, _lib.TW_EPI_GELU_PACKED, v.fp, v, bias=L.b1)
-            self._gemv(v.fp, True, P["w2"], R, D, F, PART, v.parts, v, splits=K4)
-            nparts, pbias = K4, L.b2
-        if with_logits:
-            self._resid_ln_p(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
-            self._gemv(v.hp, True, self.emb_p, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, v)
-
-    def _decoder_layers_lnfused(self, R: int, with_logits: bool, v: DecView, r_enc: int, xkv_stride: int) -> None:
-        """The decoder layers with every pre-LayerNorm inside the projection that consumes it (tw_gemv_packed_ln:
-        self_attn_layer_norm -> q/k/v, encoder_attn_layer_norm -> cross q, final_layer_norm -> fc1) and every
-        residual add in the epilogue of the projection that produces it (out_proj, cross out_proj, fc2:
-        TW_EPI_RESID_F32 into xd, no split-K partials): 8 launches per layer instead of 11
-        (WhisperDecoderLayer.forward, $TF/models/whisper/modeling_whisper.py:468-505)."""
-        d, w = self.d, self.w
-        D, F, H, T = d.d_model, d.ffn, d.heads, d.max_target_positions
-        s = v.stream.cuda_stream
-        RES = _lib.TW_EPI_RESID_F32
-        for li, L in enumerate(w.dec):
-            P = self.dec_p[li]
-            self._gemv_ln(L.ln1_g, L.ln1_b, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
-            if "self" not in self._ablate:
-                _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
-                          self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
-            self._gemv(v.attd, False, P["wo"], R, D, D, RES, v.xd, v, bias=L.bo)
-            self._gemv_ln(L.ln2_g, L.ln2_b, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
-            ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
-            rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, v.stream)
-            if "cross" not in self._ablate:
-                self._cross_attend(li, R, r_enc, rmap, ckv, v)
-            self._end_timer(rec, v.stream)
-            self._gemv(v.attd, False, P["wo_x"], R, D, D, RES, v.xd, v, bias=L.bo_x)
-            self._gemv_ln(L.ln3_g, L.ln3_b, P["w1"], R, F, D, _lib.TW_EPI_GELU_PACKED, v.fp, v, bias=L.b1)
-            self._gemv(v.fp, True, P["w2"], R, D, F, RES, v.xd, v, bias=L.b2)
-        if with_logits:
-            self._resid_ln_p(R, 0, None, w.dec_ln_g, w.dec_ln_b, v)
-            self._gemv(v.hp, True, self.emb_p, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, v)
-
-    def _decoder_layers_lnstats(self, R: int, with_logits: bool, v: DecView, r_enc: int, xkv_stride: int,
-                                pre_embedded: bool) -> None:
-        """The decoder layers with the two LayerNorms after the attention blocks carried across the kernel boundary:
-        self/cross out_proj update the residual stream and write its row statistics (tw_gemv_packed_stats), and the
-        consuming projections (cross q, fc1) normalise their operand from them (tw_gemv_packed_lnst). fc2 stays a
-        split-K partial product whose sum, bias and residual add fold into the next self_attn_layer_norm launch.
-        9 launches per layer instead of 11 (WhisperDecoderLayer.forward, $TF/models/whisper/modeling_whisper.py:
-        468-505)."""
-        d, w = self.d, self.w
-        D, F, H, T = d.d_model, d.ffn, d.heads, d.max_target_positions
-        s = v.stream.cuda_stream
-        PART, K4 = _lib.TW_EPI_PARTIAL_F32, DEC_SPLITS
-        nparts, pbias = 0, None
-        for li, L in enumerate(w.dec):
-            P = self.dec_p[li]
-            if li or not pre_embedded:
-                self._resid_ln_p(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
-            self._gemv(v.hp, True, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
-            if "self" not in self._ablate:
-                _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
-                          self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
-            self._gemv_stats(v.attd, P["wo"], R, D, D, v, L.bo)
-            self._gemv_lnst(L.ln2_g, L.ln2_b, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
-            ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
-            rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, v.stream)
-            if "cross" not in self._ablate:
-                self._cross_attend(li, R, r_enc, rmap, ckv, v)
-            self._end_timer(rec, v.stream)
-            self._gemv_stats(v.attd, P["wo_x"], R, D, D, v, L.bo_x)
-            self._gemv_lnst(L.ln3_g, L.ln3_b, P["w1"], R, F, D, _lib.TW_EPI_GELU_PACKED, v.fp, v, bias=L.b1)
             self._gemv(v.fp, True, P["w2"], R, D, F, PART, v.parts, v, splits=K4)
             nparts, pbias = K4, L.b2
         if with_logits:
@@ -847,16 +619,15 @@ class WhisperEngine:
                 embed_next: bool = False) -> None:
         """Processors + greedy selection for the view's rows; embed_next: also the head of the next step (the chosen
         token's embedding into xd and layer 0's self_attn_layer_norm into the view's LN buffer, one fused launch)."""
-        v = v or self._view()
+        v = v or self._view(0, R)
         if embed_next:
             L0 = self.w.dec[0]
-            packed = v.hp is not None
             _lib.call("tw_logits_select_embed", v.logits.data_ptr(), R, self.d.vocab, self.suppress_bits.data_ptr(),
                       ctypes.byref(params), v.state.data_ptr(), v.tokens.data_ptr() if tokens else None,
                       v.tokens.shape[1], v.ids.data_ptr(), v.pos.data_ptr(), v.sel_ws.data_ptr(),
                       self.w.emb.data_ptr(), self.w.pos_dec.data_ptr(), self.d.d_model, self.d.max_target_positions,
                       v.xd.data_ptr(), L0.ln1_g.data_ptr(), L0.ln1_b.data_ptr(), LN_EPS,
-                      (v.hp if packed else v.hd).data_ptr(), int(packed), v.stream.cuda_stream)
+                      v.hp.data_ptr(), 1, v.stream.cuda_stream)
             return
         _lib.call("tw_logits_select", v.logits.data_ptr(), R, self.d.vocab, self.suppress_bits.data_ptr(),
                   ctypes.byref(params), v.state.data_ptr(), v.tokens.data_ptr() if tokens else None,
@@ -868,10 +639,7 @@ class WhisperEngine:
         L0 = self.w.dec[0]
         _lib.call("tw_embed_decoder", self.w.emb.data_ptr(), self.w.pos_dec.data_ptr(), v.ids.data_ptr(),
                   v.pos.data_ptr(), v.n, self.d.d_model, v.xd.data_ptr(), v.stream.cuda_stream)
-        if v.hp is not None:
-            self._resid_ln_p(v.n, 0, None, L0.ln1_g, L0.ln1_b, v)
-        else:
-            self._resid_ln(v.n, 0, None, L0.ln1_g, L0.ln1_b, v)
+        self._resid_ln_p(v.n, 0, None, L0.ln1_g, L0.ln1_b, v)
 
     def _gen_step(self, R: int, params, v: Optional[DecView] = None, r_enc: Optional[int] = None,
                   fused: bool = False) -> None:
@@ -909,9 +677,6 @@ class WhisperEngine:
                 self._align = None
         st = self.gen.special
         dev = self.device
-        self._pass_alone = bool(self._dec_alone_bits) and self._pump is None and not self._gemm_variant_fixed
-        if self._pass_alone:  # (the next encoder chunk queued re-selects its own kernels: _set_gemm_context)
-            _lib.call("tw_gemm_set_variant", self._gemm_alone | self._dec_alone_bits)
         self.stream.wait_event(self._enc_ev[self._slot])  # the cross-K/V of this slot is written
         detect = st.is_multilingual and lang_ids is None
         params = self._select_params(0, max_new, use_timestamps)
@@ -945,7 +710,7 @@ class WhisperEngine:
         # (their host-to-device copy is not capturable)
         if self.use_graphs and self.prompt_graph and (detect or not st.is_multilingual):
             al = self._align  # (keyed like _graph_for: an alignment pass captures the probability-recording kernel)
-            key = ("prompt", R, tuple(int(t) for t in tail), max_new, use_timestamps, self._slot, self._pass_alone,
+            key = ("prompt", R, tuple(int(t) for t in tail), max_new, use_timestamps, self._slot,
                    None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()))
             g = self._graphs.get(key)
             if g is None:
@@ -969,22 +734,15 @@ class WhisperEngine:
                 with torch.cuda.stream(c.stream):
                     self._embed_head(c)
         pump, inflight = self._pump, []
-        hp = self.hostprof  # optional host-time accounting (TW_HOSTPROF=1): replay / pump / wait seconds
-        clk = time.perf_counter
         while steps < max_new:
             n = min(check_every, max_new - steps)
             for _ in range(n):
-                t0 = clk() if hp is not None else 0.0
                 for i, c in enumerate(chains):
                     if graphs is not None:
                         with torch.cuda.stream(c.stream):
                             graphs[i].replay()
                     else:
                         self._gen_step(c.n, params, v=c, r_enc=R, fused=fused)
-                if hp is not None:
-                    t1 = clk()
-                    hp["replay"] += t1 - t0
-                    hp["steps"] += 1
                 if pump is not None:  # keep both queues shallow: <= dec_ahead steps, <= pump.ahead encoder chunks
                     ev = torch.cuda.Event()
                     ev.record(chains[-1].stream)
@@ -992,16 +750,8 @@ class WhisperEngine:
                     while len(inflight) > self.dec_ahead:
                         if inflight[0].query():
                             inflight.pop(0)
-                        else:
-                            tp = clk() if hp is not None else 0.0
-                            queued = pump()
-                            if hp is not None:
-                                hp["pump"] += clk() - tp
-                            if not queued:
-                                tw = clk() if hp is not None else 0.0
-                                inflight.pop(0).synchronize()
-                                if hp is not None:
-                                    hp["wait"] += clk() - tw
+                        elif not pump():
+                            inflight.pop(0).synchronize()
             steps += n
             for c in chains:
                 self.stream.wait_stream(c.stream)
@@ -1126,7 +876,7 @@ class WhisperEngine:
 
     def _graph_for(self, R: int, params, i: int, v: DecView, fused: bool = False) -> Optional[torch.cuda.CUDAGraph]:
         al = self._align
-        key = (R, params.max_new, params.use_timestamps, self._slot, i, fused, self._pass_alone,
+        key = (R, params.max_new, params.use_timestamps, self._slot, i, fused,
                None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()))
         g = self._graphs.get(key)
         if g is not None:
@@ -1276,20 +1026,16 @@ class WhisperEngine:
         self.batch_langs = []
         self.batch_passes = []
         self.batch_token_timestamps = []
-        overlap = os.environ.get("TW_OVERLAP", "1") != "0"  # 0: encoder and decoder strictly in turn (A/B)
-        paced = os.environ.get("TW_PACED", "1") != "0"  # 0: queue the next batch's encoder up front (A/B)
+        overlap = self.overlap  # False: encoder and decoder strictly in turn
         if sizes:
             prefetch(0)
         for k, n in enumerate(sizes):
             if not overlap and k > 0:
                 self.enc_stream.wait_stream(self.stream)
                 prefetch(k)
-            if overlap and k + 1 < len(sizes):
-                if paced:  # runs beside the decode of batch k, queued between its decode steps
-                    self._pump = _EncoderPump(self, prefetch_steps(k + 1), ahead=self.pump_ahead)
-                    self._pump()
-                else:
-                    prefetch(k + 1, alone=False)
+            if overlap and k + 1 < len(sizes):  # runs beside the decode of batch k, queued between its decode steps
+                self._pump = _EncoderPump(self, prefetch_steps(k + 1), ahead=self.pump_ahead)
+                self._pump()
             kw = dict(gen_kwargs, **(batch_kwargs[k] if batch_kwargs else {}))
             try:
                 out.append(self.generate(n, slot=k % 2, pre_encoded=True, **kw))
