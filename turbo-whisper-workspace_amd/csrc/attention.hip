@@ -157,6 +157,7 @@ __global__ __launch_bounds__(256) void k_attn_encoder(const bf16_t* __restrict__
 typedef __attribute__((ext_vector_type(4))) short short4_t;
 typedef __attribute__((ext_vector_type(8))) short short8_t;
 typedef __attribute__((address_space(3))) short4_t lds_short4_t;
+typedef __attribute__((address_space(3))) void lds_void_t;
 
 __device__ inline int k2_off(int key, int ch) { return key * 64 + ((ch ^ ((key >> 1) & 7)) << 3); }        // elements
 __device__ inline int v2_off(int key, int ch) { return key * 64 + ((ch ^ (((key >> 1) & 1) << 2)) << 3); } // elements
@@ -542,6 +543,190 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc3(const bf16_t* __rest
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_attn_enc4: k_attn_enc3's per-lane algorithm (swapped S^T = K.Q^T on v_mfma_f32_32x32x16_bf16, lane-local online
+// softmax, P^T straight from the accumulators into the PV MFMA, V^T by ds_read_b64_tr_b16) with 64 queries per wave:
+// every K fragment read from LDS feeds 4 MFMAs instead of 2 and every V^T fragment 4 instead of 2, halving the LDS
+// read traffic per MFMA (at 32 queries per wave a CU's K/V fragment reads equal its LDS bandwidth at full MFMA rate).
+// The wave's two 32-query blocks are independent chains, so one block's softmax (VALU) can issue beside the other's
+// MFMAs within the wave. K/V tiles (64 keys) are staged by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip):
+// the bank swizzles of enc2/enc3 are applied on the SOURCE chunk and undone on the read address (the LDS image stays
+// lane-linear), one barrier per tile, the DMA of tile t+1 in flight under tile t's MFMAs.
+// ------------------------------------------------------------------------------------------------
+template <int NW, int WPS>
+__global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc4(const bf16_t* __restrict__ qkv, int S, int H, int D,
+                                                          int nqb, int nwork, bf16_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) bf16_t kbuf[2][EA_KT * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t vbuf[2][EA_KT * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int orig = blockIdx.x;
+  const int q8 = nwork / 8, r8 = nwork % 8, xcd = orig % 8;
+  const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int qb = work % nqb, bh = work / nqb;
+  const int h = bh % H, b = bh / H;
+  const int ld = 3 * D;
+  const bf16_t* base = qkv + (size_t)b * S * ld + h * 64;
+  const int q0 = qb * (NW * 64) + wid * 64;
+
+  bf16x8 qf[2][4];  // query block t: lane holds Q[q0 + 32 t + lr][16 s + 8 lh + j]
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const bf16_t* qp = base + (size_t)min(q0 + 32 * t + lr, S - 1) * ld + 8 * lh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[t][s] = *(const bf16x8*)(qp + 16 * s);
+  }
+  // LDS-DMA staging: a tile is 64 keys x 8 16-byte chunks of K and of V; one wave-instruction fills 8 key rows
+  // (lane l: row 8 i + (l >> 3), LDS slot l & 7 <- global chunk (l & 7) ^ swz(row)). With NW waves each wave
+  // issues 8 / NW instructions for K and as many for V per tile.
+  constexpr int IPW = 8 / NW;
+  const bf16_t* gk[IPW];
+  const bf16_t* gv[IPW];
+  int krow[IPW];
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int row = 8 * (wid * IPW + i) + (lane >> 3);
+    const int sl = lane & 7;
+    krow[i] = row;
+    gk[i] = base + D + ((sl ^ ((row >> 1) & 7)) << 3);
+    gv[i] = base + 2 * D + ((sl ^ (((row >> 1) & 1) << 2)) << 3);
+  }
+  auto stage = [&](int buf, int k0) {
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const size_t roff = (size_t)min(k0 + krow[i], S - 1) * ld;
+      const int lb = 8 * (wid * IPW + i) * 64;  // wave-uniform LDS base (elements) of this instruction's 8 rows
+      __builtin_amdgcn_global_load_lds((const void*)(gk[i] + roff), (lds_void_t*)(kbuf[buf] + lb), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(gv[i] + roff), (lds_void_t*)(vbuf[buf] + lb), 16, 0, 0);
+    }
+  };
+
+  f32x16 o[2][2];  // O^T of query block t, d 0..31 / 32..63
+#pragma unroll
+  for (int t = 0; t < 2; ++t) o[t][0] = o[t][1] = (f32x16){0};
+  float m_run[2] = {-INFINITY, -INFINITY}, l_sum[2] = {0.f, 0.f};
+  const int nfull = S / EA_KT, ntile = (S + EA_KT - 1) / EA_KT;
+  const int gq = (lane & 15) >> 2, gp = lane & 3, gd = ((lane >> 4) & 1) * 16;
+  auto tile = [&](int cur, int k0, auto MASKED) {
+    constexpr bool masked = decltype(MASKED)::value;
+    const bf16_t* ks = kbuf[cur];
+    const bf16_t* vs = vbuf[cur];
+    f32x16 sc[2][2];  // [key half][query block]
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) sc[kh][t] = (f32x16){0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 ka = *(const bf16x8*)(ks + k2_off(lr, 2 * s + lh));
+      const bf16x8 kb = *(const bf16x8*)(ks + k2_off(32 + lr, 2 * s + lh));
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        sc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[t][s], sc[0][t], 0, 0, 0);
+        sc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[t][s], sc[1][t], 0, 0, 0);
+      }
+    }
+    if constexpr (masked) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = (r & 3) + 8 * (r >> 2) + 4 * lh;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          if (k0 + key >= S) sc[0][t][r] = -INFINITY;
+          if (k0 + 32 + key >= S) sc[1][t][r] = -INFINITY;
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float tc[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float x = fmaxf(fmaxf(sc[0][t][4 * c], sc[0][t][4 * c + 1]), sc[0][t][4 * c + 2]);
+        x = fmaxf(fmaxf(x, sc[0][t][4 * c + 3]), sc[1][t][4 * c]);
+        x = fmaxf(fmaxf(x, sc[1][t][4 * c + 1]), sc[1][t][4 * c + 2]);
+        tc[c] = fmaxf(x, sc[1][t][4 * c + 3]);
+      }
+      float tmax = fmaxf(fmaxf(tc[0], tc[1]), fmaxf(tc[2], tc[3]));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      if (__any(tmax > m_run[t])) {
+        const float m_new = fmaxf(m_run[t], tmax);
+        const float alpha = __builtin_amdgcn_exp2f((m_run[t] - m_new) * EA_LOG2E);  // first tile: 0
+        l_sum[t] *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          o[t][0][r] *= alpha;
+          o[t][1][r] *= alpha;
+        }
+        m_run[t] = m_new;
+      }
+      const float mb = m_run[t] * EA_LOG2E;
+      float ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sc[0][t][r] = __builtin_amdgcn_exp2f(fmaf(sc[0][t][r], EA_LOG2E, -mb));
+        sc[1][t][r] = __builtin_amdgcn_exp2f(fmaf(sc[1][t][r], EA_LOG2E, -mb));
+        ps += sc[0][t][r] + sc[1][t][r];
+      }
+      ps += __shfl_xor(ps, 32, 64);
+      l_sum[t] += ps;
+    }
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pb[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[t][j] = (__bf16)sc[kh][t][8 * s + j];
+        const int kb = kh * 32 + 16 * s + 4 * lh + gq;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const int d = db * 32 + gd + 4 * gp;
+          const int ch = d >> 3, wi = d & 7;
+          const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4_t*)(vs + v2_off(kb, ch) + wi));
+          const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4_t*)(vs + v2_off(kb + 8, ch) + wi));
+          const bf16x8 va = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int t = 0; t < 2; ++t) o[t][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb[t], o[t][db], 0, 0, 0);
+        }
+      }
+    }
+  };
+  using BT = std::integral_constant<bool, true>;
+  using BF = std::integral_constant<bool, false>;
+  stage(0, 0);
+  __syncthreads();  // vmcnt(0) + barrier: tile 0 landed
+  for (int kt = 0; kt < nfull; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < ntile) stage(cur ^ 1, (kt + 1) * EA_KT);  // (the buffer last read in tile kt-1: past the barrier)
+    tile(cur, kt * EA_KT, BF{});
+    __syncthreads();
+  }
+  if (nfull < ntile) tile(nfull & 1, nfull * EA_KT, BT{});
+
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int q = q0 + 32 * t + lr;
+    if (q < S) {
+      const float inv = 1.f / l_sum[t];
+      bf16_t* op = out + ((size_t)b * S + q) * D + h * 64;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 8 * g + 4 * lh;
+        uint2 w0, w1;
+        w0.x = pack_bf16x2(o[t][0][4 * g] * inv, o[t][0][4 * g + 1] * inv);
+        w0.y = pack_bf16x2(o[t][0][4 * g + 2] * inv, o[t][0][4 * g + 3] * inv);
+        w1.x = pack_bf16x2(o[t][1][4 * g] * inv, o[t][1][4 * g + 1] * inv);
+        w1.y = pack_bf16x2(o[t][1][4 * g + 2] * inv, o[t][1][4 * g + 3] * inv);
+        tw_st_enc<TW_NT_ATTN>(op + d, w0);
+        tw_st_enc<TW_NT_ATTN>(op + 32 + d, w1);
+      }
+    }
+  }
+}
+
 // 0 = k_attn_encoder, 4 / 8 = k_attn_enc2<NW>, 9 = <8> at 2 workgroups per CU, 10 / 11 = k_attn_enc3 (VALU row sums /
 // MFMA row sums). Measured alone (scripts/attn_bench.py, 24 windows, MI355X): 8: 653, 10: 699, 11: 629 TF/s (11 spills
 // 16 VGPRs at the 128-register cap of two workgroups per CU).
@@ -592,7 +777,7 @@ extern "C" int tw_attn_set_variant(int v) {
     tw_dec_cross_unr = unr[(v >> 24) & 3];
   }
   v &= 0xff;
-  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9 || (v >= 10 && v <= 15)) ? v : TW_ATTN_DEFAULT;
+  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9 || (v >= 10 && v <= 17)) ? v : TW_ATTN_DEFAULT;
   return 0;
 }
 
@@ -601,7 +786,15 @@ extern "C" int tw_attn_encoder(const bf16_t* qkv, int B, int S, int H, bf16_t* o
   const int D = H * 64;
   hipStream_t st = (hipStream_t)stream;
   const size_t pad = (size_t)tw_attn_lds_pad * 16384;
-  if (tw_attn_variant == 0) {
+  if (tw_attn_variant == 16 || tw_attn_variant == 17) {  // k_attn_enc4: 64 queries per wave, LDS-DMA K/V
+    if (tw_attn_variant == 16) {
+      const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
+      hipLaunchKernelGGL((k_attn_enc4<4, 2>), dim3(nwork), dim3(256), pad, st, qkv, S, H, D, nqb, nwork, out);
+    } else {
+      const int nqb = tw_cdiv(S, 512), nwork = nqb * H * B;
+      hipLaunchKernelGGL((k_attn_enc4<8, 1>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
+    }
+  } else if (tw_attn_variant == 0) {
     hipLaunchKernelGGL(k_attn_encoder, dim3(tw_cdiv(S, 128), H, B), dim3(256), 0, st, qkv, S, H, D, out);
   } else if (tw_attn_variant == 4) {
     const int nqb = tw_cdiv(S, 128), nwork = nqb * H * B;
