@@ -168,6 +168,13 @@ def failing_on_rank1(wav, windows):
     return fake_windows(wav, windows)
 
 
+def malformed_on_rank1(wav, windows):
+    """Rank 1 returns items that are not (tokens, times) pairs: a local failure that must still be collective."""
+    if twd.world()[0] == 1:
+        return [object() for _ in windows]
+    return fake_timed_windows(wav, windows)
+
+
 def _edge_worker(rank, ws, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
@@ -183,6 +190,28 @@ def _edge_worker(rank, ws, port, q):
             res["fail"] = ("peer", str(e))
         except RuntimeError as e:
             res["fail"] = ("own", str(e))
+        try:  # a malformed result on one rank (timed mode) is reported on every rank
+            twd.transcribe_sharded(malformed_on_rank1, wav, windows, timed=True)
+            res["malformed"] = None
+        except twd.PeerError:
+            res["malformed"] = "peer"
+        except (TypeError, ValueError):
+            res["malformed"] = "own"
+        # gather_tokens with an explicit width and a shard-size mismatch on one rank raises on every rank
+        lo, hi = twd.shard_range(len(windows), ws, rank)
+        mine = fake_windows(wav, windows[lo:hi])
+        if rank == 1:
+            mine = mine[:-1]
+        try:
+            twd.gather_tokens(mine, None, len(windows), width=8)
+            res["mismatch"] = None
+        except twd.PeerError:
+            res["mismatch"] = "peer"
+        except ValueError:
+            res["mismatch"] = "own"
+        # an explicit width narrower than the sequences is widened to the agreed maximum
+        full = fake_windows(wav, windows[lo:hi])
+        res["narrow"] = twd.gather_tokens(full, None, len(windows), width=1)[0]
         # the collectives still line up after a failed call
         res["after"] = twd.transcribe_sharded(fake_windows, wav, windows)
         q.put((rank, res))
@@ -217,6 +246,9 @@ def test_two_rank_long_windows_and_collective_failure():
         assert res[r]["after"] == fake_windows(wav, windows)
     assert res[1]["fail"] == ("own", "engine fault on rank 1")
     assert res[0]["fail"][0] == "peer"
+    assert (res[0]["malformed"], res[1]["malformed"]) == ("peer", "own")
+    assert (res[0]["mismatch"], res[1]["mismatch"]) == ("peer", "own")
+    assert res[0]["narrow"] == res[1]["narrow"] == fake_windows(wav, windows)
 
 
 class _LoadingASR(_RecordingASR):

@@ -99,22 +99,23 @@ def gather_tokens(local_seqs: Sequence[Sequence[int]], local_langs: Optional[Seq
     """All-gather every rank's window results; returns all n_total windows in global order (on every rank).
 
     `device`: where the collective's buffers live (a cuda device for RCCL, cpu for gloo; default: cuda when
-    the default backend is nccl). `width`: token columns per row, the SAME value on every rank; None = agree on
-    the longest local sequence with one MAX all-reduce (a shard-size mismatch is reported through it as well,
-    so no rank is left waiting in the gather)."""
+    the default backend is nccl). `width`: a minimum number of token columns per row; the columns used are the max
+    over ranks of it and of the longest local sequence, agreed with one MAX all-reduce that also reports a
+    shard-size mismatch, so no rank is left waiting in the gather."""
     rank, ws = world()
     if ws == 1:
         return [list(s) for s in local_seqs], list(local_langs) if local_langs is not None else [None] * len(
             local_seqs)
     sizes = shard_sizes(n_total, ws)
     bad = len(local_seqs) != sizes[rank]
-    if width is None:
-        failed, width = agree(bad, max((len(s) for s in local_seqs), default=0), device, group)
-        if failed and not bad:
-            raise PeerError("another rank's window shard did not match its range")
+    # always one collective agreement first (ADVICE r2): a shard-size mismatch on any rank is reported on every rank
+    # before the gather, also when the caller fixed the width; the width is the max over ranks and the caller's
+    failed, agreed = agree(bad, max([len(s) for s in local_seqs] + [int(width or 0)], default=0), device, group)
     if bad:
         raise ValueError(f"rank {rank} holds {len(local_seqs)} windows, its shard has {sizes[rank]}")
-    width = max(int(width), 1)
+    if failed:
+        raise PeerError("another rank's window shard did not match its range")
+    width = max(agreed, 1)
     rows = max(max(sizes), 1)
     device = _coll_device(device, group)
     loc = torch.from_numpy(pack_tokens(local_seqs, local_langs, rows, width)).to(device)
@@ -163,14 +164,17 @@ def transcribe_sharded(run_windows, wav: np.ndarray, windows: Sequence, device: 
     rank, ws = world()
     lo, hi = shard_range(len(windows), ws, rank)
     err: Optional[BaseException] = None
+    toks: List = []
+    bits: List = []
     try:
         local = run_windows(wav, list(windows[lo:hi])) if hi > lo else []
         if len(local) != hi - lo:
             raise ValueError(f"rank {rank}: {len(local)} results for {hi - lo} windows")
+        # (inside the try: a malformed result must reach agree() too)
+        toks = [list(t) for t, _ in local] if timed else [list(t) for t in local]
+        bits = [np.asarray(ts, dtype=np.float32).view(np.int32).tolist() for _, ts in local] if timed else []
     except Exception as e:  # made collective below: every rank learns of it before anyone enters the gather
-        err, local = e, []
-    toks = [t for t, _ in local] if timed else local
-    bits = [np.asarray(ts, dtype=np.float32).view(np.int32).tolist() for _, ts in local] if timed else []
+        err, toks, bits = e, [], []
     failed, width = agree(err is not None, max((len(t) for t in list(toks) + bits), default=0), device, group)
     if failed:
         if err is not None:
