@@ -37,9 +37,15 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", choices=("c2", "c3", "c5"), default="c2",
-                    help="c2: bf16, 24 windows/GPU (BASELINE configs[1], weak scaling); c3: 1 h of audio = 120 "
-                         "windows split over the ranks (configs[2], strong scaling); c5: MX fp8 encoder + bf16 "
-                         "decoder, 64 windows/GPU (configs[4], weak scaling)")
+                    help="c2: bf16, 24 windows/GPU (BASELINE configs[1], weak scaling); c3: one full "
+                         "TurboTranscriber call on 1 h of audio (120 x 30 s windows) sharded over the ranks "
+                         "(configs[2], strong scaling); c5: MX fp8 encoder + bf16 decoder, 64 windows/GPU "
+                         "(configs[4], weak scaling)")
+    ap.add_argument("--c3-share", type=int, default=1,
+                    help="c3 at one GPU: transcribe 1/R of the hour (the share one rank of R gets) instead of all "
+                         "of it (a per-rank measurement; value is then that share's audio seconds / time)")
+    ap.add_argument("--sub-batch-min", type=int, default=0,
+                    help="c3: TurboTranscriber.sub_batch_min (split a one-batch share into two; 0 = the default)")
     ap.add_argument("--batch", type=int, default=0, help="windows per GPU (default 24 for c2, 64 for c5)")
     ap.add_argument("--decode-tokens", type=int, default=128)
     ap.add_argument("--model", default="large-v3-turbo")
@@ -67,21 +73,39 @@ def main():
     gen = GenerationSettings.default(dims)
     fp8 = a.config == "c5"
     strong = a.config == "c3"
-    if strong:  # one hour = 120 windows, contiguous shares (twamd.dist.shard_range), padded to the largest share
-        B = a.batch or -(-120 // world)
+    if strong:  # engine batches of <= 24 windows; a rank's share of the 120 windows is cut by pipeline.batch_sizes
+        B = a.batch or 24
     else:
         B = a.batch or (64 if fp8 else 24)
     T = a.decode_tokens
-    w = build_weights(dims, seed=1234)
-    eng = WhisperEngine(w, gen, max_batch=B, device=f"cuda:{local}", enc_fp8=fp8)
+    if strong:  # the product call path: TurboTranscriber (ASR-pipeline signature) over the engine
+        from twamd.pipeline import TurboTranscriber
+        tr = TurboTranscriber.from_pretrained(a.model, seed=1234, max_batch=B, device=f"cuda:{local}", max_beams=1)
+        if a.sub_batch_min:
+            tr.sub_batch_min = a.sub_batch_min
+        eng = tr.engine
+    else:
+        w = build_weights(dims, seed=1234)
+        eng = WhisperEngine(w, gen, max_batch=B, device=f"cuda:{local}", enc_fp8=fp8)
     dom = "gemm_mx" if fp8 else "gemm_big"
     peak = FP8_DENSE_PEAK_TFLOPS if fp8 else BF16_DENSE_PEAK_TFLOPS
     eng.set_suppress_tokens(list(gen.suppress_tokens) + [gen.special.eot])  # fixed decode length
-    audio = workload(B, 30.0, seed=1234 + 1000 * rank)
-    eng.wave[:B].copy_(torch.from_numpy(audio))
     from twamd import dist as twd
+    if strong:
+        # 1 h of synthetic speech-like audio (120 seeded 30-s windows back to back), on the host as a caller's array
+        hour = workload(120 // max(1, a.c3_share), 30.0, seed=1234).reshape(-1)
+        call_kw = dict(chunk_length_s=30, stride_length_s=0, batch_size=B, return_timestamps=True,
+                       generate_kwargs={"task": "transcribe", "num_beams": 1, "max_new_tokens": T, "max_passes": 1})
+    else:
+        audio = workload(B, 30.0, seed=1234 + 1000 * rank)
+        eng.wave[:B].copy_(torch.from_numpy(audio))
 
     def run(n_steps):
+        if strong:  # one step = one full call: host waveform -> broadcast -> shard -> batches -> gather -> text
+            out = None
+            for _ in range(n_steps):
+                out = tr(hour, **call_kw)
+            return [p for w in tr.last_window_passes for p in w[:1]] if out is not None else []
         """n_steps batches of B windows through the engine's two-slot pipeline (the encoder of batch k+1 runs on
         a second HIP stream beside the decode of batch k); every rank then all-gathers each batch's tokens."""
         res = eng.run_batches([B] * n_steps, task="transcribe", max_new_tokens=T, max_passes=1)
@@ -115,7 +139,7 @@ def main():
             print(json.dumps({"profile_only": True, "ms_per_step": 1000 * dt / a.steps}))
         return
     ms = 1000.0 * dt / a.steps
-    audio_s = (120 * 30.0) if strong and not a.batch else world * B * 30.0
+    audio_s = (120 // max(1, a.c3_share)) * 30.0 if strong else world * B * 30.0
     rtf = audio_s / (dt / a.steps)
     n_tok = [len(s) for s in seqs]
 
@@ -151,9 +175,14 @@ def main():
         "dtype": "fp8-e4m3 (MX) encoder projections + bf16" if fp8 else "bf16",
         "data": "synthetic (seeded speech-like 16 kHz audio, 10% silent windows; seeded synthetic weights)",
         "config": {"workload": f"whisper-{a.model} {'MX-fp8 encoder + bf16 decoder' if fp8 else 'bf16'}, "
-                               + ("1 h of audio (120 x 30s windows) split over the GPUs, " if strong else "")
-                               + f"batch={B} x 30s windows per GPU, greedy, "
-                               f"{T} new tokens/window (EOS suppressed), timestamps on, language detected",
+                               + (f"one TurboTranscriber call on {audio_s / 3600:g} h of host audio "
+                                  f"({int(audio_s // 30)} x 30s windows, chunk_length_s=30, stride 0) sharded over "
+                                  f"the GPUs, engine batches of <= {B} (sub-batches: "
+                                  f"{tr.sub_batch_min or 'off'}), " if strong else
+                                  f"batch={B} x 30s windows per GPU, ")
+                               + f"greedy, {T} new tokens/window (EOS suppressed, one seek pass), timestamps on, "
+                               "language detected",
+                   "c3_share": a.c3_share if strong else None,
                    "global_batch": int(audio_s // 30), "seq_len": 3000, "parallelism": f"chunk-dp{world}",
                    "decode_tokens_per_window": T, "mean_tokens_out": float(np.mean(n_tok))},
         "roofline": {"bound": "mfma",
@@ -170,7 +199,9 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0:
-        out["parity"], out["parity_detail"] = parity_vs_golden(eng, B, T, a.model, fp8)
+        out["parity"], out["parity_detail"] = (parity_vs_golden(eng, B, T, a.model, fp8) if not strong else
+                                               (None, {"skipped": "c3 windows differ from the golden's; the same "
+                                                                  "engine's parity is the c2 line's"}))
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(dims, gen, T, a.cpu_threads)
     if rank == 0:

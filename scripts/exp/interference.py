@@ -82,7 +82,7 @@ def main():
     sE = torch.cuda.Stream(priority=0)
     sD = torch.cuda.Stream(priority=-1)
     _lib.call("tw_gemm_set_variant", (a.variant if a.variant < 100 else 1) | (a.kw << 16))
-    _lib.call("tw_attn_set_variant", 8 | (a.attn_pad << 20))
+    _lib.call("tw_attn_set_variant", 16); _lib.call("tw_attn_set_lds_pad", a.attn_pad)
 
     nb = None
     if a.variant in (103, 104):

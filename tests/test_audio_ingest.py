@@ -166,3 +166,29 @@ def test_flac_needs_gpu_to_resample_on_cpu():
     data = ao.flac_encode(_pcm(4000, 1, 16, 15), 44100, 16, blocksizes=(1024,))
     with pytest.raises(RuntimeError, match="GPU"):
         audio.load_input(data)
+
+
+def test_constant_subframe_stream_over_duration_cap(monkeypatch):
+    """constant subframes code 4096 samples in a few bytes, so a small valid stream can claim hours; the
+    claimed length is checked against TW_MAX_AUDIO_S x sample_rate (from STREAMINFO) before anything is allocated."""
+    pcm = np.full((4096 * 64, 1), 7, np.int32)
+    data = ao.flac_encode(pcm, 16000, 16, blocksizes=(4096,), subframe_kinds=("constant",))
+    assert len(data) < 4096  # ~16 s of audio in a few hundred bytes
+    assert np.array_equal(audio.decode_flac(data).pcm, pcm)
+    monkeypatch.setenv("TW_MAX_AUDIO_S", "10")
+    with pytest.raises(ValueError, match="TW_MAX_AUDIO_S=10"):
+        audio.decode_flac(data)
+
+
+def test_undecoded_containers_named_and_garbage_reported_as_reference():
+    """MP3 / Ogg / WebM / M4A uploads are refused by name; bytes no container matches get the reference's own
+    decode-failure message (transformers' ffmpeg_read), which its transcribe() returns as {"error": ...}."""
+    cases = {b"ID3\x04\x00" + bytes(64): "MP3", b"\xff\xfb\x90\x00" + bytes(64): "MP3", b"OggS\x00\x02" + bytes(64): "Ogg",
+             b"\x1aE\xdf\xa3" + bytes(64): "Matroska/WebM", b"\x00\x00\x00\x20ftypM4A " + bytes(64): "MP4/M4A"}
+    for data, name in cases.items():
+        assert audio.container_name(data) == name
+        with pytest.raises(ValueError, match=f"^{name} audio is not decoded"):
+            audio.load_input(data)
+    with pytest.raises(ValueError) as e:
+        audio.load_input(b"hello, not audio" * 8)
+    assert str(e.value) == audio.MALFORMED and str(e.value).startswith("Soundfile is either not in the correct format")

@@ -331,3 +331,91 @@ def test_rank_zero_frontend_serves_followers():
     for s, out in zip((95, 40), res[0]):
         wav = rng.standard_normal(16000 * s).astype(np.float32)
         assert out == fake_windows(wav, list(chunk_windows(len(wav), 30, 0, 16000)))
+
+
+# ---------------------------------------------------------------- the product call path, sharded (bench --config c3)
+class _FakeEngine:
+    """WhisperEngine's surface as TurboTranscriber.transcribe_windows drives it (max_batch, wave, run_batches with
+    load(k) filling wave[:n]); each window's tokens are fake_windows' function of the samples that load() put in
+    wave, so the test sees exactly what the sharded upload delivered."""
+
+    def __init__(self, max_batch):
+        self.max_batch = max_batch
+        self.wave = torch.zeros(max_batch, 480000)
+        self.gen = GenerationSettings.default(PRESETS["large-v3-turbo"])
+        self.device = torch.device("cpu")
+        self.sizes = []
+
+        class d:
+            max_source_positions = 1500
+        self.d = d
+
+    def run_batches(self, sizes, load=None, batch_kwargs=None, **kw):
+        from twamd.frontend import Window
+        out, self.batch_langs, self.batch_passes, self.batch_token_timestamps = [], [], [], []
+        for k, n in enumerate(sizes):
+            load(k)
+            rows = self.wave[:n].numpy()
+            toks = fake_windows(rows.reshape(-1), [Window(j * 480000, 480000, 0, 0, False) for j in range(n)])
+            out.append(toks)
+            self.batch_langs.append([None] * n)
+            self.batch_passes.append([[t] for t in toks])
+        self.sizes.append(list(sizes))
+        return out
+
+
+def _call_kwargs():
+    return dict(chunk_length_s=30, stride_length_s=0, batch_size=24, return_timestamps=True,
+                generate_kwargs={"task": "transcribe", "num_beams": 1, "max_new_tokens": 128, "max_passes": 1})
+
+
+def _call_worker(rank, ws, port, n_samples, max_batch, q):
+    from twamd.pipeline import TurboTranscriber
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        eng = _FakeEngine(max_batch)
+        tr = TurboTranscriber(eng, WhisperVocab.synthetic(ST))
+        wav = np.random.default_rng(5).standard_normal(n_samples).astype(np.float32) if rank == 0 else None
+        q.put((rank, tr(wav, **_call_kwargs()), eng.sizes))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_transcriber_call_equals_single_process():
+    """TurboTranscriber.__call__ at world size 2 (gloo), the path `bench.py --config c3` times: rank 0 decodes the
+    input, the waveform is broadcast (kept as the collective's tensor), each rank uploads its windows from it into
+    engine batches, the token arrays are all-gathered and stitched. Rank 0's transcript equals the single-process
+    call's, and each rank ran its own half of the 24 windows."""
+    from twamd.pipeline import TurboTranscriber
+    n_samples = 24 * 480000 - 16000 * 7  # 24 windows, the last one ragged
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_call_worker, args=(r, 2, port, n_samples, 8, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    eng = _FakeEngine(8)
+    tr = TurboTranscriber(eng, WhisperVocab.synthetic(ST))
+    ref = tr(np.random.default_rng(5).standard_normal(n_samples).astype(np.float32), **_call_kwargs())
+    assert eng.sizes == [[8, 8, 8]]
+    assert res[0][1] == ref and res[1][1] == ref  # every rank returns the stitched result
+    assert res[0][2] == [[6, 6]] and res[1][2] == [[6, 6]]  # 12 windows per rank: two near-equal batches
+
+
+def test_batch_sizes_policy():
+    from twamd.pipeline import batch_sizes
+    assert batch_sizes(0, 24) == []
+    assert batch_sizes(120, 24) == [24] * 5
+    assert batch_sizes(30, 24) == [15, 15]
+    assert batch_sizes(49, 24) == [17, 16, 16]
+    assert batch_sizes(15, 24) == [15]
+    assert batch_sizes(15, 24, sub_batch_min=4) == [8, 7]
+    assert batch_sizes(7, 24, sub_batch_min=4) == [7]
+    for n in range(1, 100):
+        s = batch_sizes(n, 24, 6)
+        assert sum(s) == n and max(s) <= 24 and max(s) - min(s) <= 1

@@ -127,7 +127,7 @@ class _OracleTranscriber(TurboTranscriber):
         self.engine = _E()
 
     def transcribe_windows(self, wav, windows, task, lang_id, return_timestamps, max_new_tokens=None, num_beams=1,
-                           word_timestamps=False, num_frames=None, group=None):
+                           word_timestamps=False, num_frames=None, group=None, max_passes=None):
         if word_timestamps:  # batches of `group` windows: the product passes the pipeline's batch_size
             out, self.last_window_token_timestamps = [], []
             B = group or 1

@@ -202,3 +202,17 @@ def test_install_overlap_runs_diarizer_beside_transcription():
     assert [k for k, _ in p.log].count("load") == 1 and [k for k, _ in p.log].count("diarize") == 1
     # a later diarize() with other arguments is the reference's own call, not the prefetched result
     assert p.diarize("/b.wav", 2) == r["d"] and p.log[-1][0] == "diarize"
+
+
+@pytest.mark.parametrize("layout", ["vocalis", "root"])
+def test_undecodable_upload_reaches_reference_error_convention(layout, tmp_path):
+    """An upload the engine cannot decode (here an MP3) surfaces as the reference's transcribe() error result,
+    {"error": "Transcription error: <message>"} (the "raises" fixture above), not as an exception."""
+    cls = ap.AudioProcessingPipeline if layout == "vocalis" else ap.RootAudioProcessingPipeline
+    p = cls()
+    p.transcription_model = lambda inputs, **kw: tw_audio.load_input(inputs)
+    f = tmp_path / "upload.mp3"
+    f.write_bytes(b"ID3\x04\x00\x00" + bytes(256))
+    got = p.transcribe(str(f), "transcribe")
+    assert got == {"error": "Transcription error: MP3 audio is not decoded by this engine (decoded containers: FLAC, "
+                            "WAV); convert the upload to FLAC or WAV"}

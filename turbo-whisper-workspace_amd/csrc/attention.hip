@@ -2,13 +2,14 @@
 //
 // (1) Encoder self-attention (non-causal, S = 1500, 64-wide heads): replaces WhisperAttention +
 //     eager/SDPA attention ($TF/models/whisper/modeling_whisper.py:215-238, 241-356) for the encoder.
-//     Flash-style: one wave = 32 queries, a workgroup = 4 waves = 128 queries of one (batch, head).
+//     Flash-style (k_attn_enc4, the default: 64 queries per wave, 4 waves per workgroup; k_attn_enc2: 32 per wave,
+//     its register-staged predecessor, kept as the bit-identical cross-check and for the MX-fp8 output of config 5).
 //     The score tile is computed SWAPPED, S^T = K.Q^T with v_mfma_f32_32x32x16_bf16, so each lane holds
 //     16 keys of ONE query: the online-softmax max/sum is lane-local plus one xor-32 shuffle. The f32
 //     accumulator is then converted pairwise to bf16 and used in place as the B operand of O^T = V^T.P^T
-//     (no LDS round trip for P). K tiles are staged row-major with an XOR chunk swizzle; V tiles are
-//     staged transposed ([d][key], row stride 68) so the A operand of the PV product is two
-//     conflict-free ds_read_b64 per fragment. Keys past S are masked to -inf in the last tile.
+//     (no LDS round trip for P). K and V tiles are staged row-major with XOR chunk swizzles; the V^T
+//     A operand of the PV product is read with ds_read_b64_tr_b16 (hardware transpose), bank-conflict
+//     free. Keys past S are masked to -inf in the last tile.
 //     q is already multiplied by head_dim^-0.5 (folded into the q projection, exact: 0.125 = 2^-3).
 //
 // (2) Decoder single-token attention over the self KV cache (causal by construction: keys 0..t)
@@ -18,133 +19,10 @@
 #include "../../include/tw_whisper.h"
 
 #define EA_KT 64           // keys per tile
-#define EA_VS 68           // transposed-V LDS row stride (bf16): conflict-free ds_read_b64
 #define EA_LOG2E 1.4426950408889634f
 
-__device__ inline int ka_off(int key, int chunk) { return key * 64 + ((chunk ^ (key & 7)) << 3); }
-
-__global__ __launch_bounds__(256) void k_attn_encoder(const bf16_t* __restrict__ qkv, int S, int H, int D,
-                                                      bf16_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) bf16_t ks[EA_KT * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t vts[64 * EA_VS];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int lr = lane & 31, lh = lane >> 5;
-  const int h = blockIdx.y, b = blockIdx.z;
-  const int ld = 3 * D;
-  const bf16_t* base = qkv + (size_t)b * S * ld;
-  const int q0 = blockIdx.x * 128 + wid * 32;
-
-  // Q^T fragments (B operand): lane holds Q[q = lr][d = 16 s + 8 lh + j]
-  bf16x8 qf[4];
-  {
-    int qi = min(q0 + lr, S - 1);
-    const bf16_t* qp = base + (size_t)qi * ld + h * 64 + 8 * lh;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
-  }
-  f32x16 o0 = {0}, o1 = {0};   // O^T for d in [0,32) and [32,64): row = d, col = query
-  float m_run = -INFINITY, l_run = 0.f;
-
-  const int ntile = (S + EA_KT - 1) / EA_KT;
-  for (int kt = 0; kt < ntile; ++kt) {
-    const int k0 = kt * EA_KT;
-    __syncthreads();  // previous tile fully consumed
-    // stage K (row-major, swizzled) and V^T: 64 keys x 8 chunks = 512 chunks, 2 per thread
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int c = tid + 256 * i;
-      int key = c >> 3, ch = c & 7;
-      int kk = min(k0 + key, S - 1);
-      const bf16_t* rowp = base + (size_t)kk * ld + h * 64 + ch * 8;
-      uint4 kv = *(const uint4*)(rowp + D);
-      uint4 vv = *(const uint4*)(rowp + 2 * D);
-      *(uint4*)(ks + ka_off(key, ch)) = kv;
-      const bf16_t* ve = (const bf16_t*)&vv;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) vts[(ch * 8 + e) * EA_VS + key] = ve[e];
-    }
-    __syncthreads();
-
-    // S^T = K . Q^T for key halves 0..31 and 32..63
-    f32x16 s0 = {0}, s1 = {0};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bf16x8 ka = *(const bf16x8*)(ks + ka_off(lr, 2 * s + lh));
-      bf16x8 kb = *(const bf16x8*)(ks + ka_off(32 + lr, 2 * s + lh));
-      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], s0, 0, 0, 0);
-      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[s], s1, 0, 0, 0);
-    }
-    // mask keys >= S; scale into log2 domain
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      int key = (r & 3) + 8 * (r >> 2) + 4 * lh;
-      float a = (k0 + key < S) ? s0[r] * EA_LOG2E : -INFINITY;
-      float c = (k0 + 32 + key < S) ? s1[r] * EA_LOG2E : -INFINITY;
-      s0[r] = a; s1[r] = c;
-      tmax = fmaxf(tmax, fmaxf(a, c));
-    }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
-    const float alpha = (m_run == -INFINITY) ? 0.f : exp2f(m_run - m_new);
-    float psum = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s0[r] = exp2f(s0[r] - m_new);
-      s1[r] = exp2f(s1[r] - m_new);
-      psum += s0[r] + s1[r];
-    }
-    psum += __shfl_xor(psum, 32, 64);
-    l_run = l_run * alpha + psum;
-    m_run = m_new;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
-
-    // O^T += V^T . P^T ; B operand = P^T registers 8s..8s+7 (keys 16s + 8(j>>2) + 4lh + (j&3))
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 pb;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float pv = half ? s1[8 * s + j] : s0[8 * s + j];
-          pb[j] = (__bf16)pv;
-        }
-        const int kbase = half * 32 + 16 * s + 4 * lh;
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          const bf16_t* vp = vts + (db * 32 + lr) * EA_VS + kbase;
-          bf16x4 lo = *(const bf16x4*)(vp);
-          bf16x4 hi = *(const bf16x4*)(vp + 8);
-          bf16x8 va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          if (db == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o0, 0, 0, 0);
-          else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o1, 0, 0, 0);
-        }
-      }
-    }
-  }
-
-  const int q = q0 + lr;
-  if (q < S) {
-    const float inv = 1.f / l_run;
-    bf16_t* op = out + ((size_t)b * S + q) * D + h * 64;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 8 * g + 4 * lh;
-      uint2 w0, w1;
-      w0.x = pack_bf16x2(o0[4 * g] * inv, o0[4 * g + 1] * inv);
-      w0.y = pack_bf16x2(o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
-      w1.x = pack_bf16x2(o1[4 * g] * inv, o1[4 * g + 1] * inv);
-      w1.y = pack_bf16x2(o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
-      tw_st_enc<TW_NT_ATTN>(op + d, w0);
-      tw_st_enc<TW_NT_ATTN>(op + 32 + d, w1);
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
-// k_attn_enc2: the same algorithm restructured for CDNA4 throughput
+// k_attn_enc2: 32 queries per wave, register-staged K/V tiles
 //   * NW waves x 32 queries per workgroup (NW = 8: 256 queries share every staged K/V tile);
 //   * K/V tiles double-buffered in LDS, register-staged one tile ahead (loads for tile t+1 are issued before
 //     tile t's MFMAs and written after them), ONE barrier per 64-key tile;
@@ -343,221 +221,21 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc2(const bf16_t* __rest
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_attn_enc3: k_attn_enc2's algorithm (same staging, swizzles, fragment maps, online softmax) with less VALU work
-// per key tile, the VALU being what bounds it (per 64-key tile a wave issues 16 MFMAs = 512 matrix cycles against
-// ~800 cycles of softmax VALU):
-//   * the softmax row sums come out of the matrix core: one extra 32x32x16 MFMA per P fragment whose A operand is
-//     a ones row (row 0 = 1, rows 1..31 = 0), so o2[0] accumulates sum_k P[q][k] for the lane's query (4 MFMAs
-//     instead of 32 adds + a cross-lane shuffle per tile; the rescale touches o2[0] only, the other rows stay 0);
-//   * tile maxima with v_max3_f32 (16 instead of 31 dependent maxes);
-//   * the ragged last tile (keys >= S masked) peeled out of the loop, so full tiles carry no masking code.
-// Without ONES (variant 10, the default) the outputs are bit-identical to k_attn_enc2's (max is exact, the sums keep
-// its order); with ONES (variant 11) only the order of the f32 row sum differs.
-// ------------------------------------------------------------------------------------------------
-// PK (variant 12, VALU trimmed further; not bit-identical to k_attn_enc2): bit 0 = the exp arguments and the row sums
-// in packed f32 math (v_pk_fma_f32 / v_pk_add_f32: two results per issue), bit 1 = lazy rescaling (the running max
-// is raised only when a tile's max exceeds it by more than 2^8 in exp2 units: P entries then stay <= 256, exact in
-// bf16's exponent range, and the O / l rescale of most tiles is skipped; the final O / l is unchanged up to f32
-// rounding).
-template <int NW, int WPS, bool ONES, int PK = 0>
-__global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc3(const bf16_t* __restrict__ qkv, int S, int H, int D,
-                                                          int nqb, int nwork, bf16_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) bf16_t kbuf[2][EA_KT * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t vbuf[2][EA_KT * 64];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int lr = lane & 31, lh = lane >> 5;
-  const int orig = blockIdx.x;
-  const int q8 = nwork / 8, r8 = nwork % 8, xcd = orig % 8;
-  const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int qb = work % nqb, bh = work / nqb;
-  const int h = bh % H, b = bh / H;
-  const int ld = 3 * D;
-  const bf16_t* base = qkv + (size_t)b * S * ld + h * 64;
-  const int q0 = qb * (NW * 32) + wid * 32;
-
-  bf16x8 qf[4];
-  {
-    const bf16_t* qp = base + (size_t)min(q0 + lr, S - 1) * ld + 8 * lh;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
-  }
-  // 512 16-byte chunks of K and of V per 64-key tile; with NW = 12 (768 threads) the last 256 threads stage none
-  constexpr int CPT = (512 + NW * 64 - 1) / (NW * 64);
-  constexpr bool PART = 512 % (NW * 64) != 0;
-  uint4 rk[CPT], rv[CPT];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = tid + NW * 64 * i;
-      if (PART && c >= 512) continue;
-      const int key = c >> 3, ch = c & 7;
-      const bf16_t* rp = base + (size_t)min(k0 + key, S - 1) * ld + ch * 8;
-      rk[i] = *(const uint4*)(rp + D);
-      rv[i] = *(const uint4*)(rp + 2 * D);
-    }
-  };
-  auto swrite = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = tid + NW * 64 * i;
-      if (PART && c >= 512) continue;
-      const int key = c >> 3, ch = c & 7;
-      *(uint4*)(&kbuf[buf][k2_off(key, ch)]) = rk[i];
-      *(uint4*)(&vbuf[buf][v2_off(key, ch)]) = rv[i];
-    }
-  };
-  bf16x8 ones;  // A operand of the row-sum MFMA (lane l holds A[row l & 31][k = 8 lh + j]): row 0 = 1, other rows 0
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)(lr == 0 ? 1.f : 0.f);
-
-  f32x16 o0 = {0}, o1 = {0}, o2 = {0};  // O^T (d 0..31, 32..63), row sums (row 0; ONES only)
-  float m_run = -INFINITY, l_sum = 0.f;  // (l_sum: the row sum by VALU adds when !ONES)
-  const int nfull = S / EA_KT, ntile = (S + EA_KT - 1) / EA_KT;
-  const int gq = (lane & 15) >> 2, gp = lane & 3, gd = ((lane >> 4) & 1) * 16;
-  auto tile = [&](int cur, int k0, auto MASKED) {
-    constexpr bool masked = decltype(MASKED)::value;
-    const bf16_t* ks = kbuf[cur];
-    const bf16_t* vs = vbuf[cur];
-    f32x16 s0 = {0}, s1 = {0};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8 ka = *(const bf16x8*)(ks + k2_off(lr, 2 * s + lh));
-      const bf16x8 kb = *(const bf16x8*)(ks + k2_off(32 + lr, 2 * s + lh));
-      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], s0, 0, 0, 0);
-      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[s], s1, 0, 0, 0);
-    }
-    if constexpr (masked) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (k0 + key >= S) s0[r] = -INFINITY;
-        if (k0 + 32 + key >= S) s1[r] = -INFINITY;
-      }
-    }
-    float tc[4];  // four independent v_max3 chains over 8 scores each
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      float t = fmaxf(fmaxf(s0[4 * c], s0[4 * c + 1]), s0[4 * c + 2]);
-      t = fmaxf(fmaxf(t, s0[4 * c + 3]), s1[4 * c]);
-      t = fmaxf(fmaxf(t, s1[4 * c + 1]), s1[4 * c + 2]);
-      tc[c] = fmaxf(t, s1[4 * c + 3]);
-    }
-    float tmax = fmaxf(fmaxf(tc[0], tc[1]), fmaxf(tc[2], tc[3]));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    if (__any((PK & 2) ? tmax * EA_LOG2E > fmaf(m_run, EA_LOG2E, 8.f) : tmax > m_run)) {
-      const float m_new = fmaxf(m_run, tmax);
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * EA_LOG2E);  // first tile: exp2(-inf) = 0
-      if constexpr (ONES) o2[0] *= alpha;
-      else l_sum *= alpha;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
-      m_run = m_new;
-    }
-    const float mb = m_run * EA_LOG2E;
-    if constexpr (PK & 1) {
-      const f32x2 l2 = {EA_LOG2E, EA_LOG2E}, nm = {-mb, -mb};
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const f32x2 a = __builtin_elementwise_fma((f32x2){s0[r], s0[r + 1]}, l2, nm);
-        const f32x2 c = __builtin_elementwise_fma((f32x2){s1[r], s1[r + 1]}, l2, nm);
-        s0[r] = __builtin_amdgcn_exp2f(a.x);
-        s0[r + 1] = __builtin_amdgcn_exp2f(a.y);
-        s1[r] = __builtin_amdgcn_exp2f(c.x);
-        s1[r + 1] = __builtin_amdgcn_exp2f(c.y);
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], EA_LOG2E, -mb));
-        s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], EA_LOG2E, -mb));
-      }
-    }
-    if constexpr (!ONES && (PK & 1)) {  // packed partial sums: two interleaved chains
-      f32x2 p2 = {0.f, 0.f};
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) p2 += (f32x2){s0[r], s0[r + 1]} + (f32x2){s1[r], s1[r + 1]};
-      float ps = p2.x + p2.y;
-      ps += __shfl_xor(ps, 32, 64);
-      l_sum += ps;
-    } else if constexpr (!ONES) {  // k_attn_enc2's summation order exactly (bit-identical outputs)
-      float ps = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) ps += s0[r] + s1[r];
-      ps += __shfl_xor(ps, 32, 64);
-      l_sum += ps;
-    }
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 pb;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pb[j] = (__bf16)(half ? s1[8 * s + j] : s0[8 * s + j]);
-        const int kb = half * 32 + 16 * s + 4 * lh + gq;
-        if constexpr (ONES) o2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pb, o2, 0, 0, 0);
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          const int d = db * 32 + gd + 4 * gp;
-          const int ch = d >> 3, wi = d & 7;
-          const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4_t*)(vs + v2_off(kb, ch) + wi));
-          const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4_t*)(vs + v2_off(kb + 8, ch) + wi));
-          const short8_t v8 = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-          const bf16x8 va = __builtin_bit_cast(bf16x8, v8);
-          if (db == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o0, 0, 0, 0);
-          else o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o1, 0, 0, 0);
-        }
-      }
-    }
-  };
-  using BT = std::integral_constant<bool, true>;
-  using BF = std::integral_constant<bool, false>;
-  gload(0);
-  swrite(0);
-  __syncthreads();
-  for (int kt = 0; kt < nfull; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < ntile) gload((kt + 1) * EA_KT);
-    tile(cur, kt * EA_KT, BF{});
-    if (kt + 1 < ntile) swrite(cur ^ 1);
-    __syncthreads();
-  }
-  if (nfull < ntile) tile(nfull & 1, nfull * EA_KT, BT{});
-
-  // ONES: the row sum sits in o2[0] of lane (lr, lh = 0) (accumulator row 0); lane (lr, 1) holds row 4 = 0.
-  const float l_run = ONES ? __shfl(o2[0], lr, 64) : l_sum;
-  const int q = q0 + lr;
-  if (q < S) {
-    const float inv = 1.f / l_run;
-    bf16_t* op = out + ((size_t)b * S + q) * D + h * 64;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 8 * g + 4 * lh;
-      uint2 w0, w1;
-      w0.x = pack_bf16x2(o0[4 * g] * inv, o0[4 * g + 1] * inv);
-      w0.y = pack_bf16x2(o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
-      w1.x = pack_bf16x2(o1[4 * g] * inv, o1[4 * g + 1] * inv);
-      w1.y = pack_bf16x2(o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
-      tw_st_enc<TW_NT_ATTN>(op + d, w0);
-      tw_st_enc<TW_NT_ATTN>(op + 32 + d, w1);
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// k_attn_enc4: k_attn_enc3's per-lane algorithm (swapped S^T = K.Q^T on v_mfma_f32_32x32x16_bf16, lane-local online
+// k_attn_enc4: k_attn_enc2's per-lane algorithm (swapped S^T = K.Q^T on v_mfma_f32_32x32x16_bf16, lane-local online
 // softmax, P^T straight from the accumulators into the PV MFMA, V^T by ds_read_b64_tr_b16) with 64 queries per wave:
 // every K fragment read from LDS feeds 4 MFMAs instead of 2 and every V^T fragment 4 instead of 2, halving the LDS
 // read traffic per MFMA (at 32 queries per wave a CU's K/V fragment reads equal its LDS bandwidth at full MFMA rate).
 // The wave's two 32-query blocks are independent chains, so one block's softmax (VALU) can issue beside the other's
 // MFMAs within the wave. K/V tiles (64 keys) are staged by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip):
-// the bank swizzles of enc2/enc3 are applied on the SOURCE chunk and undone on the read address (the LDS image stays
+// the bank swizzles of enc2 are applied on the SOURCE chunk and undone on the read address (the LDS image stays
 // lane-linear), one barrier per tile, the DMA of tile t+1 in flight under tile t's MFMAs.
 // ------------------------------------------------------------------------------------------------
 template <int NW, int WPS>
 __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc4(const bf16_t* __restrict__ qkv, int S, int H, int D,
                                                           int nqb, int nwork, bf16_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) bf16_t kbuf[2][EA_KT * 64];
-  __shared__ __attribute__((aligned(16))) bf16_t vbuf[2][EA_KT * 64];
+  // ONE __shared__ array for both K/V double buffers: with two LDS objects hipcc cannot tell the LDS-DMA target
+  // from the tile being read and drains vmcnt(0) before every ds_read, serialising tile t+1's DMA with tile t
+  __shared__ __attribute__((aligned(16))) bf16_t kvbuf[4 * EA_KT * 64];  // [K0 | K1 | V0 | V1]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 31, lh = lane >> 5;
   const int orig = blockIdx.x;
@@ -596,8 +274,8 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc4(const bf16_t* __rest
     for (int i = 0; i < IPW; ++i) {
       const size_t roff = (size_t)min(k0 + krow[i], S - 1) * ld;
       const int lb = 8 * (wid * IPW + i) * 64;  // wave-uniform LDS base (elements) of this instruction's 8 rows
-      __builtin_amdgcn_global_load_lds((const void*)(gk[i] + roff), (lds_void_t*)(kbuf[buf] + lb), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(gv[i] + roff), (lds_void_t*)(vbuf[buf] + lb), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(gk[i] + roff), (lds_void_t*)(kvbuf + buf * EA_KT * 64 + lb), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(gv[i] + roff), (lds_void_t*)(kvbuf + (2 + buf) * EA_KT * 64 + lb), 16, 0, 0);
     }
   };
 
@@ -609,21 +287,22 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc4(const bf16_t* __rest
   const int gq = (lane & 15) >> 2, gp = lane & 3, gd = ((lane >> 4) & 1) * 16;
   auto tile = [&](int cur, int k0, auto MASKED) {
     constexpr bool masked = decltype(MASKED)::value;
-    const bf16_t* ks = kbuf[cur];
-    const bf16_t* vs = vbuf[cur];
+    const bf16_t* ks = kvbuf + cur * EA_KT * 64;
+    const bf16_t* vs = kvbuf + (2 + cur) * EA_KT * 64;
     f32x16 sc[2][2];  // [key half][query block]
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) sc[kh][t] = (f32x16){0};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const bf16x8 ka = *(const bf16x8*)(ks + k2_off(lr, 2 * s + lh));
       const bf16x8 kb = *(const bf16x8*)(ks + k2_off(32 + lr, 2 * s + lh));
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        sc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[t][s], sc[0][t], 0, 0, 0);
-        sc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[t][s], sc[1][t], 0, 0, 0);
+        if (s == 0) {  // first K-step straight from a zero accumulator (an inline constant, no register zeroing)
+          sc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[t][s], (f32x16){}, 0, 0, 0);
+          sc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[t][s], (f32x16){}, 0, 0, 0);
+        } else {
+          sc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[t][s], sc[0][t], 0, 0, 0);
+          sc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[t][s], sc[1][t], 0, 0, 0);
+        }
       }
     }
     if constexpr (masked) {
@@ -649,7 +328,9 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc4(const bf16_t* __rest
       }
       float tmax = fmaxf(fmaxf(tc[0], tc[1]), fmaxf(tc[2], tc[3]));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      if (__any(tmax > m_run[t])) {
+      // a wave-uniform scalar branch (ballot), so the O rescale is skipped, not predicated, on tiles where no
+      // query's max grew
+      if (__builtin_amdgcn_readfirstlane(__ballot(tmax > m_run[t]) != 0ull ? 1 : 0)) {
         const float m_new = fmaxf(m_run[t], tmax);
         const float alpha = __builtin_amdgcn_exp2f((m_run[t] - m_new) * EA_LOG2E);  // first tile: 0
         l_sum[t] *= alpha;
@@ -661,13 +342,14 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc4(const bf16_t* __rest
         m_run[t] = m_new;
       }
       const float mb = m_run[t] * EA_LOG2E;
-      float ps = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         sc[0][t][r] = __builtin_amdgcn_exp2f(fmaf(sc[0][t][r], EA_LOG2E, -mb));
         sc[1][t][r] = __builtin_amdgcn_exp2f(fmaf(sc[1][t][r], EA_LOG2E, -mb));
-        ps += sc[0][t][r] + sc[1][t][r];
       }
+      float ps = 0.f;  // k_attn_enc2's summation order exactly (bit-identical outputs)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ps += sc[0][t][r] + sc[1][t][r];
       ps += __shfl_xor(ps, 32, 64);
       l_sum[t] += ps;
     }
@@ -726,21 +408,12 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc4(const bf16_t* __rest
     }
   }
 }
-
-// 0 = k_attn_encoder, 4 / 8 = k_attn_enc2<NW>, 9 = <8> at 2 workgroups per CU, 10 / 11 = k_attn_enc3 (VALU row sums /
-// MFMA row sums). Measured alone (scripts/attn_bench.py, 24 windows, MI355X): 8: 653, 10: 699, 11: 629 TF/s (11 spills
-// 16 VGPRs at the 128-register cap of two workgroups per CU).
-#ifndef TW_ATTN_DEFAULT
-#define TW_ATTN_DEFAULT 10
-#endif
-static int tw_attn_variant = TW_ATTN_DEFAULT;
-// decoder cross-attention: 1 = one pass with an online softmax (default), 0 = two passes (scores, then P.V)
-static int tw_dec_cross_1p = 1;
-// Encoder slots >= this read their cross K/V with non-temporal loads. The 737 MB of cross K/V a decode step streams
-// (B = 24) cannot stay in the 256 MB Infinity Cache anyway; read nt it stops evicting what can (the decoder weights,
-// the encoder's operands): cross-attention 40.1 -> 35.2 us per launch, bench step 111.1 -> 109.0 ms.
-static int tw_dec_cross_nt = 0;
-static int tw_dec_cross_ng = 32;  // 8-lane key groups per one-pass block (64 measured 3% slower in the bench)
+// Encoder attention kernel: 16 = k_attn_enc4<4 waves, 2 workgroups per CU> (the default), 8 = k_attn_enc2<8, 2> (the
+// bit-identical cross-check). Measured alone (scripts/attn_bench.py, 24 windows x 20 heads, MI355X r03): 16: 778,
+// 8: ~650 TF/s; beside a decode with 4 x 16 KiB of LDS padding 16: ~590 TF/s. Round-2/3 alternatives (k_attn_enc3's
+// MFMA row sums and packed exp, 12-wave workgroups, k_attn_enc4 at 8 waves) measured slower in situ and are archived
+// under scripts/exp/archive.
+static int tw_attn_variant = 16;
 // Extra (unused) LDS reserved per encoder-attention workgroup, in 16 KiB units: caps the attention's workgroups per CU
 // so that decoder waves queued beside it (run_batches' overlap) find free wave slots on every CU.
 // Measured (scripts/exp/interference.py, 24 windows): beside 4 x 16 KiB of padding (one workgroup per CU) a decoder
@@ -752,32 +425,9 @@ extern "C" int tw_attn_set_lds_pad(int units) {
   tw_attn_lds_pad = units;
   return 0;
 }
-static int tw_dec_self2 = 1;  // decoder self-attention in one memory round trip (k_attn_decode_self2)
-#ifndef TW_DEC_CROSS_PK
-#define TW_DEC_CROSS_PK 0
-#endif
-static int tw_dec_cross_pk = TW_DEC_CROSS_PK;  // lean cross-attention in packed arithmetic (tw_attn_set_variant bit 27)
-static int tw_dec_self3 = 0;  // ... in its 2-wave form (k_attn_decode_self3; tw_attn_set_variant bit 26)
-static int tw_dec_cross_lean = 1;  // the one-pass cross-attention in its small-LDS form (0: the 15 KiB form; A/B)
-static int tw_dec_cross_unr = 8;   // key rows in flight per 8-lane group of the lean form (tw_attn_set_variant bits 24-27)
 extern "C" int tw_attn_set_variant(int v) {
-  tw_attn_lds_pad = (v >> 20) & 0xf;  // bits 20-23
-  tw_dec_cross_lean = (v & 0x400) ? 0 : 1;  // bit 10: the 15 KiB-LDS one-pass cross-attention (A/B)
-  tw_dec_self2 = (v & 0x800) ? 0 : 1;       // bit 11: the round-1 three-round-trip self-attention (A/B)
-  tw_dec_self3 = (v & 0x4000000) ? 1 : 0;   // bit 26: the 2-wave one-round-trip self-attention
-  // bit 27: the lean cross-attention's other arithmetic form (packed: dot2 QK and packed-f32 PV; or scalar)
-  tw_dec_cross_pk = (v & 0x8000000) ? !TW_DEC_CROSS_PK : TW_DEC_CROSS_PK;
-  tw_dec_cross_1p = (v & 0x100) ? 0 : 1;  // bit 8: the two-pass decoder cross-attention (A/B)
-  // bits 12-19: 0 = every slot's cross K/V read non-temporally (default), else 1 + the first slot read so (0xff: none)
-  tw_dec_cross_nt = (v >> 12) & 0xff ? ((v >> 12) & 0xff) - 1 : 0;
-  tw_dec_cross_ng = (v & 0x200) ? 64 : 32;  // bit 9: one-pass with 512 threads (64 key groups) instead of 256
-  // bits 24-27: key rows of loads in flight per 8-lane group in the lean cross-attention (0: 8 = DA_UNR; 1: 12, 2: 4, 3: 6)
-  {
-    const int unr[4] = {8, 12, 4, 6};
-    tw_dec_cross_unr = unr[(v >> 24) & 3];
-  }
-  v &= 0xff;
-  tw_attn_variant = (v == 0 || v == 4 || v == 8 || v == 9 || (v >= 10 && v <= 17)) ? v : TW_ATTN_DEFAULT;
+  TW_REQUIRE(v == 8 || v == 16, "tw_attn_set_variant: %d (8 = k_attn_enc2, 16 = k_attn_enc4)", v);
+  tw_attn_variant = v;
   return 0;
 }
 
@@ -786,47 +436,13 @@ extern "C" int tw_attn_encoder(const bf16_t* qkv, int B, int S, int H, bf16_t* o
   const int D = H * 64;
   hipStream_t st = (hipStream_t)stream;
   const size_t pad = (size_t)tw_attn_lds_pad * 16384;
-  if (tw_attn_variant == 16 || tw_attn_variant == 17) {  // k_attn_enc4: 64 queries per wave, LDS-DMA K/V
-    if (tw_attn_variant == 16) {
-      const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
-      hipLaunchKernelGGL((k_attn_enc4<4, 2>), dim3(nwork), dim3(256), pad, st, qkv, S, H, D, nqb, nwork, out);
-    } else {
-      const int nqb = tw_cdiv(S, 512), nwork = nqb * H * B;
-      hipLaunchKernelGGL((k_attn_enc4<8, 1>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
-    }
-  } else if (tw_attn_variant == 0) {
-    hipLaunchKernelGGL(k_attn_encoder, dim3(tw_cdiv(S, 128), H, B), dim3(256), 0, st, qkv, S, H, D, out);
-  } else if (tw_attn_variant == 4) {
-    const int nqb = tw_cdiv(S, 128), nwork = nqb * H * B;
-    hipLaunchKernelGGL((k_attn_enc2<4, 2>), dim3(nwork), dim3(256), 0, st, qkv, S, H, D, nqb, nwork, out);
-  } else if (tw_attn_variant == 14) {  // 12 waves (384 queries) per workgroup: one per CU by registers, no LDS cap
-    const int nqb = (S + 383) / 384, nwork = B * H * nqb;
-    hipLaunchKernelGGL((k_attn_enc3<12, 4, false>), dim3(nwork), dim3(768), pad, st, qkv, S, H, D, nqb, nwork, out);
-  } else if (tw_attn_variant == 15) {  // 4 waves (128 queries) per workgroup: two per CU under an LDS cap of 2
-    const int nqb = (S + 127) / 128, nwork = B * H * nqb;
-    hipLaunchKernelGGL((k_attn_enc3<4, 4, false>), dim3(nwork), dim3(256), pad, st, qkv, S, H, D, nqb, nwork, out);
-  } else if (tw_attn_variant == 12 || tw_attn_variant == 13) {
-    const int nqb = (S + 255) / 256, nwork = B * H * nqb;
-    if (tw_attn_variant == 12)
-      hipLaunchKernelGGL((k_attn_enc3<8, 4, false, 3>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
-    else
-      hipLaunchKernelGGL((k_attn_enc3<8, 4, false, 1>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
-  } else if (tw_attn_variant == 10 || tw_attn_variant == 11) {
-    const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
-    if (tw_attn_variant == 10)
-      hipLaunchKernelGGL((k_attn_enc3<8, 4, false>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
-    else
-      hipLaunchKernelGGL((k_attn_enc3<8, 4, true>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
-  } else if (tw_attn_variant == 9) {
-    const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
-    hipLaunchKernelGGL((k_attn_enc2<8, 4>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
-  } else {
-    const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
+  const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;  // both: 256 queries per workgroup
+  if (tw_attn_variant == 16)
+    hipLaunchKernelGGL((k_attn_enc4<4, 2>), dim3(nwork), dim3(256), pad, st, qkv, S, H, D, nqb, nwork, out);
+  else
     hipLaunchKernelGGL((k_attn_enc2<8, 2>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
-  }
   return tw_check_launch("tw_attn_encoder");
 }
-
 extern "C" int tw_attn_encoder_mx(const bf16_t* qkv, int B, int S, int H, uint8_t* out, uint8_t* scales, int rows_pad,
                                   void* stream) {
   TW_REQUIRE(qkv && out && scales && B > 0 && S > 0 && H > 0, "tw_attn_encoder_mx: bad args");
@@ -928,138 +544,15 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
   __syncthreads();
 }
 
-// dec_attend in ONE pass over the keys (flash-decoding's online softmax per 8-lane group): each group loads the K
-// and the V row of its keys together (DA_UNR keys = 16 x 16-byte loads in flight per lane), rescales its running
-// (max, sum, P.V) once per DA_UNR keys, and the 32 groups' states are merged through LDS at the end. The two-pass
-// form streams all of K, then (after a block-wide softmax) all of V: two load ramps and three barriers between
-// them on an HBM-bound kernel. Same softmax up to f32 rounding (the rescaling order differs).
-// NG = 8-lane groups per block (32: 256 threads; 64: 512 threads, half the serial load round trips per group).
-template <int NG, bool NT = false, int UNR = DA_UNR>
-__device__ inline void dec_attend_1p(const float* qf /*[64] f32 in LDS*/, const bf16_t* K, const bf16_t* V, int nkeys,
-                                     float* part /*[NG][64] LDS*/, float* gml /*[NG][2] LDS*/,
-                                     float* outv /*[64] f32 LDS*/) {
-  const int tid = threadIdx.x, g = tid >> 3, gl = tid & 7;
-  float qv[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) qv[e] = qf[gl * 8 + e];
-  float m = -INFINITY, l = 0.f;
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int nit = (nkeys + NG - 1) / NG;
-  for (int it0 = 0; it0 < nit; it0 += UNR) {
-    uint4 kk[UNR], vv[UNR];
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int key = min((it0 + u) * NG + g, nkeys - 1);
-      if constexpr (NT) {
-        typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
-        const u32x4_nt a = __builtin_nontemporal_load((const u32x4_nt*)(K + (size_t)key * 64 + gl * 8));
-        const u32x4_nt c = __builtin_nontemporal_load((const u32x4_nt*)(V + (size_t)key * 64 + gl * 8));
-        kk[u] = make_uint4(a.x, a.y, a.z, a.w);
-        vv[u] = make_uint4(c.x, c.y, c.z, c.w);
-      } else {
-        kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
-        vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);  // all 2 x UNR loads in flight before the first is consumed
-    float sv[UNR];
-    float bm = m;
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const bf16_t* ke = (const bf16_t*)&kk[u];
-      float d = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
-      d += __shfl_xor(d, 1, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 4, 64);
-      sv[u] = (it0 + u) * NG + g < nkeys ? d : -INFINITY;
-      bm = fmaxf(bm, sv[u]);
-    }
-    if (bm == -INFINITY) continue;  // (no key of this group yet: short self-attention rows only)
-    const float sc = __expf(m - bm);  // 0 on the group's first keys (m = -inf)
-    l *= sc;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] *= sc;
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const float p = __expf(sv[u] - bm);  // 0 for the masked keys
-      l += p;
-      const bf16_t* ve = (const bf16_t*)&vv[u];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += p * bf16_to_f32(ve[e]);
-    }
-    m = bm;
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) part[g * 64 + gl * 8 + e] = acc[e];
-  if (gl == 0) {
-    gml[2 * g] = m;
-    gml[2 * g + 1] = l;
-  }
-  __syncthreads();
-  if (tid < 64) {
-    float M = -INFINITY;
-#pragma unroll 8
-    for (int gg = 0; gg < NG; ++gg) M = fmaxf(M, gml[2 * gg]);
-    float v = 0.f, tot = 0.f;
-#pragma unroll 8
-    for (int gg = 0; gg < NG; ++gg) {
-      const float mg = gml[2 * gg];
-      const float w = mg == -INFINITY ? 0.f : __expf(mg - M);
-      tot += w * gml[2 * gg + 1];
-      v += w * part[gg * 64 + tid];
-    }
-    outv[tid] = v / tot;
-  }
-  __syncthreads();
-}
-
 #define DA_SELF_MAXK 448  // decoder positions (max_target_positions of every Whisper checkpoint)
-#ifndef TW_SELF_1P
-#define TW_SELF_1P 0  // 1: decoder self-attention in one pass. Measured in the bench: +6 ms per step (A/B builds)
-#endif
-// Self-attention step: qkv [B][3D] bf16 (q pre-scaled), appends k,v at position pos[b] into the cache
-// (layout [B][H][max_pos][64] for K and V of this layer) and attends over positions 0..pos[b].
-__global__ __launch_bounds__(256) void k_attn_decode_self(const bf16_t* __restrict__ qkv, int D, int max_pos,
-                                                          const int* __restrict__ pos, bf16_t* __restrict__ kc,
-                                                          bf16_t* __restrict__ vc, bf16_t* __restrict__ out) {
-  TW_DEC_PRIO();
-  __shared__ float part[32 * 64];
-  __shared__ float gml[64];
-  __shared__ float qf[64];
-  __shared__ float outv[64];
-  const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x;
-  const int t = pos[b];
-  const bf16_t* row = qkv + (size_t)b * 3 * D + h * 64;
-  bf16_t* K = kc + ((size_t)b * H + h) * max_pos * 64;
-  bf16_t* V = vc + ((size_t)b * H + h) * max_pos * 64;
-  if (threadIdx.x < 64) {
-    qf[threadIdx.x] = bf16_to_f32(row[threadIdx.x]);
-    K[(size_t)t * 64 + threadIdx.x] = row[D + threadIdx.x];
-    V[(size_t)t * 64 + threadIdx.x] = row[2 * D + threadIdx.x];
-  }
-  __threadfence_block();
-  __syncthreads();
-#if TW_SELF_1P
-  // one pass (online softmax per 8-lane key group): K and V of <= 256 keys in flight together, one round trip
-  dec_attend_1p<32>(qf, K, V, t + 1, part, gml, outv);
-#else
-  // scores of <= DA_SELF_MAXK positions (not DA_MAXK): ~10 KiB of LDS, two workgroups per CU beside an encoder GEMM
-  __shared__ float sc[DA_SELF_MAXK];
-  __shared__ float red[8];
-  dec_attend(qf, K, V, t + 1, sc, part, red, outv);
-#endif
-  if (threadIdx.x < 64) out[(size_t)b * D + h * 64 + threadIdx.x] = f32_to_bf16(outv[threadIdx.x]);
-}
 
 // k_attn_decode_self2: the decoder self-attention step in ONE memory round trip for up to DS2_KEYS keys. The cached
 // K and V rows of keys 0..t-1 do not depend on this step, so their loads fly together with the loads of this token's
 // q / k / v (the q/k/v GEMV output): the key t itself is taken from the loaded row instead of a read-back of the cache
 // write. 32 groups of 8 lanes; group g holds keys u*32 + g (u < DS2_U) of K and V in registers, the scores and the
 // softmax stay in registers (block max and sum through 8 floats of LDS), P.V is reduced over the 32 groups in LDS.
-// Longer histories (t >= DS2_KEYS: never in a 30-s window's first 255 tokens) take k_attn_decode_self's two-pass
-// path in the same launch. Same products and reductions as k_attn_decode_self up to the order of the f32 sums.
+// Longer histories (t >= DS2_KEYS: never in a 30-s window's first 255 tokens) take dec_attend's two-pass path (cache
+// append, then K / V re-read) in the same launch; the two agree up to the order of the f32 sums.
 #define DS2_U 8
 #define DS2_KEYS (DS2_U * 32)
 __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__ qkv, int D, int max_pos,
@@ -1161,133 +654,13 @@ __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__
   }
 }
 
-// k_attn_decode_self3: k_attn_decode_self2 with half the workgroup (NGR = 16 key groups = 128 threads, U keys per
-// group in the one-round-trip path: t < NGR * U = 144 covers a 30-s window's 128 generated tokens + prompt). Beside
-// an encoder GEMM workgroup every SIMD keeps room for one decoder wave, so a 4-wave workgroup per CU took the step's
-// 480 (row, head) workgroups two rounds; 2-wave workgroups fit two per CU: one round. Longer histories take the
-// one-pass online-softmax loop (dec_attend_1p) over the cache after the append. Same products; the f32 sums differ
-// from k_attn_decode_self2 only in order.
-template <int NGR, int U>
-__global__ TW_DEC_LB(NGR * 8, 4) void k_attn_decode_self3(const bf16_t* __restrict__ qkv, int D, int max_pos,
-                                                           const int* __restrict__ pos, bf16_t* __restrict__ kc,
-                                                           bf16_t* __restrict__ vc, bf16_t* __restrict__ out) {
-  TW_DEC_PRIO();
-  constexpr int NWV = NGR / 8;  // waves
-  __shared__ float part[NGR * 64];
-  __shared__ float red[2 * NWV];
-  __shared__ float gml[NGR * 2];
-  __shared__ float qf[64];
-  __shared__ float outv[64];
-  const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x;
-  const int tid = threadIdx.x, g = tid >> 3, gl = tid & 7, lane = tid & 63, wid = tid >> 6;
-  const int t = pos[b];
-  const bf16_t* row = qkv + (size_t)b * 3 * D + h * 64;
-  bf16_t* K = kc + ((size_t)b * H + h) * max_pos * 64;
-  bf16_t* V = vc + ((size_t)b * H + h) * max_pos * 64;
-  if (t >= NGR * U) {  // long history: append, then one pass over the cache
-    if (tid < 64) {
-      qf[tid] = bf16_to_f32(row[tid]);
-      K[(size_t)t * 64 + tid] = row[D + tid];
-      V[(size_t)t * 64 + tid] = row[2 * D + tid];
-    }
-    __threadfence_block();
-    __syncthreads();
-    dec_attend_1p<NGR, false, 4>(qf, K, V, t + 1, part, gml, outv);
-    if (tid < 64) out[(size_t)b * D + h * 64 + tid] = f32_to_bf16(outv[tid]);
-    return;
-  }
-  const uint4 qr = *(const uint4*)(row + gl * 8);
-  const uint4 kr = *(const uint4*)(row + D + gl * 8);
-  const uint4 vr = *(const uint4*)(row + 2 * D + gl * 8);
-  uint4 kk[U], vv[U];
-  const int last = max(t - 1, 0);
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int key = min(u * NGR + g, last);
-    kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
-    vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  if (g == 0) {  // the cache append (read back by the following steps only)
-    *(uint4*)(K + (size_t)t * 64 + gl * 8) = kr;
-    *(uint4*)(V + (size_t)t * 64 + gl * 8) = vr;
-  }
-  float qv[8];
-  {
-    const bf16_t* qe = (const bf16_t*)&qr;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) qv[e] = bf16_to_f32(qe[e]);
-  }
-  float p[U];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int key = u * NGR + g;
-    const uint4 kx = key == t ? kr : kk[u];
-    const bf16_t* ke = (const bf16_t*)&kx;
-    float d = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
-    d += __shfl_xor(d, 1, 64);
-    d += __shfl_xor(d, 2, 64);
-    d += __shfl_xor(d, 4, 64);
-    p[u] = key <= t ? d : -INFINITY;
-    mx = fmaxf(mx, p[u]);
-  }
-  mx = wave_max(mx);
-  if (lane == 0) red[wid] = mx;
-  __syncthreads();
-  {
-    float m2 = red[0];
-#pragma unroll
-    for (int w = 1; w < NWV; ++w) m2 = fmaxf(m2, red[w]);
-    mx = m2;
-  }
-  float sum = 0.f;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    p[u] = __expf(p[u] - mx);  // 0 past key t
-    if (gl == 0) sum += p[u];
-  }
-  sum = wave_sum(sum);
-  if (lane == 0) red[NWV + wid] = sum;
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    if (u * NGR + g > t) continue;  // (the clamped rows past t may hold anything on the first step: never 0 * them)
-    const uint4 vx = u * NGR + g == t ? vr : vv[u];
-    const bf16_t* ve = (const bf16_t*)&vx;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] += p[u] * bf16_to_f32(ve[e]);
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) part[g * 64 + gl * 8 + e] = acc[e];
-  __syncthreads();
-  if (tid < 64) {
-    float tot = 0.f;
-#pragma unroll
-    for (int w = 0; w < NWV; ++w) tot += red[NWV + w];
-    float v = 0.f;
-#pragma unroll 8
-    for (int gg = 0; gg < NGR; ++gg) v += part[gg * 64 + tid];
-    out[(size_t)b * D + h * 64 + tid] = f32_to_bf16(v / tot);
-  }
-}
-
-// Cross-attention step: q [B][D] bf16 (pre-scaled); cross K/V layout [kv][Bt][H][S][64] for this layer,
-// batch row b reads block row_map[b] (the encoder batch slot holding that row's audio window).
+// Self-attention step: qkv [B][3D] bf16 (q pre-scaled), appends k,v at position pos[b] into the cache
+// (layout [B][H][max_pos][64] for K and V of this layer) and attends over positions 0..pos[b].
 extern "C" int tw_attn_decode_self(const bf16_t* qkv, int B, int H, int max_pos, const int* pos, bf16_t* k_cache,
                                    bf16_t* v_cache, bf16_t* out, void* stream) {
   TW_REQUIRE(qkv && pos && k_cache && v_cache && out && B > 0 && H > 0, "tw_attn_decode_self: bad args");
   TW_REQUIRE(max_pos <= DA_SELF_MAXK, "tw_attn_decode_self: max_pos %d > %d", max_pos, DA_SELF_MAXK);
-  if (tw_dec_self2 && tw_dec_self3)
-    hipLaunchKernelGGL((k_attn_decode_self3<16, 8>), dim3(H, B), dim3(128), 0, (hipStream_t)stream, qkv, H * 64, max_pos,
-                       pos, k_cache, v_cache, out);
-  else if (tw_dec_self2)
-    hipLaunchKernelGGL(k_attn_decode_self2, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos, pos,
-                       k_cache, v_cache, out);
-  else
-    hipLaunchKernelGGL(k_attn_decode_self, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos, pos,
+  hipLaunchKernelGGL(k_attn_decode_self2, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos, pos,
                      k_cache, v_cache, out);
   return tw_check_launch("tw_attn_decode_self");
 }
@@ -1302,14 +675,15 @@ struct XProbs {
   int slot0, n_slots, pos0, n_steps;
 };
 
-template <bool PROBS, int NG = 32>
-__global__ __launch_bounds__(NG * 8) void k_attn_decode_cross(const bf16_t* __restrict__ q, int D, int S, int Bt,
-                                                           const int* __restrict__ row_map,
-                                                           const bf16_t* __restrict__ ckv, bf16_t* __restrict__ out,
-                                                           XProbs xp, int one_pass, int tw_nt_from = 1 << 30) {
+// The cross-attention step with the alignment heads' probabilities (two passes: the normalised scores of every key
+// are in LDS after dec_attend's softmax, copied out for the heads in xp.head_mask).
+__global__ __launch_bounds__(256) void k_attn_decode_cross_probs(const bf16_t* __restrict__ q, int D, int S, int Bt,
+                                                                 const int* __restrict__ row_map,
+                                                                 const bf16_t* __restrict__ ckv,
+                                                                 bf16_t* __restrict__ out, XProbs xp) {
   TW_DEC_PRIO();
   __shared__ float sc[DA_MAXK];
-  __shared__ float part[NG * 64];
+  __shared__ float part[32 * 64];
   __shared__ float qf[64];
   __shared__ float outv[64];
   __shared__ float red[8];
@@ -1319,19 +693,15 @@ __global__ __launch_bounds__(NG * 8) void k_attn_decode_cross(const bf16_t* __re
   __syncthreads();
   const bf16_t* K = ckv + (((size_t)0 * Bt + slot) * H + h) * S * 64;
   const bf16_t* V = ckv + (((size_t)1 * Bt + slot) * H + h) * S * 64;
-  if (!PROBS && one_pass && slot >= tw_nt_from) dec_attend_1p<NG, true>(qf, K, V, S, part, sc, outv);
-  else if (!PROBS && one_pass) dec_attend_1p<NG>(qf, K, V, S, part, sc, outv);  // (probabilities: two passes)
-  else if constexpr (NG == 32) dec_attend(qf, K, V, S, sc, part, red, outv);
+  dec_attend(qf, K, V, S, sc, part, red, outv);
   if (threadIdx.x < 64) out[(size_t)b * D + h * 64 + threadIdx.x] = f32_to_bf16(outv[threadIdx.x]);
-  if constexpr (PROBS) {
-    if ((xp.head_mask >> h) & 1u) {
-      const int k = xp.pos[b] - xp.pos0;
-      if (k >= 0 && k < xp.n_steps) {
-        const int sl = xp.slot0 + __popc(xp.head_mask & ((1u << h) - 1u));
-        const float inv = 1.f / (red[4] + red[5] + red[6] + red[7]);  // dec_attend's softmax denominator
-        float* dst = xp.probs + (((size_t)b * xp.n_steps + k) * xp.n_slots + sl) * S;
-        for (int i = threadIdx.x; i < S; i += 256) dst[i] = sc[i] * inv;
-      }
+  if ((xp.head_mask >> h) & 1u) {
+    const int k = xp.pos[b] - xp.pos0;
+    if (k >= 0 && k < xp.n_steps) {
+      const int sl = xp.slot0 + __popc(xp.head_mask & ((1u << h) - 1u));
+      const float inv = 1.f / (red[4] + red[5] + red[6] + red[7]);  // dec_attend's softmax denominator
+      float* dst = xp.probs + (((size_t)b * xp.n_steps + k) * xp.n_slots + sl) * S;
+      for (int i = threadIdx.x; i < S; i += 256) dst[i] = sc[i] * inv;
     }
   }
 }
@@ -1341,8 +711,11 @@ __global__ __launch_bounds__(NG * 8) void k_attn_decode_cross(const bf16_t* __re
 // workgroups of a decode step took two rounds; these fit several per CU. q comes straight from global memory (each
 // lane its 8 dims), and the 8 key groups of a wave merge their online-softmax states with xor shuffles (lanes of one
 // dim slice: xor 8, 16, 32) before one LDS record per wave; one wave merges the NG/8 records.
-template <int NG, bool NT, int UNR = DA_UNR, bool PK = false>
-__global__ TW_DEC_LB(NG * 8, UNR <= 4 ? 7 : 1) void k_attn_decode_cross_lean(const bf16_t* __restrict__ q, int D, int S, int Bt,
+// The 737 MB of cross K/V a decode step streams (B = 24) cannot stay in the 256 MB Infinity Cache, so it is read
+// non-temporally: it stops evicting what can stay (the decoder weights, the encoder's operands): 40.1 -> 35.2 us per
+// launch, bench step -2 ms (r02 A/B).
+template <int NG, int UNR = DA_UNR>
+__global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_lean(const bf16_t* __restrict__ q, int D, int S, int Bt,
                                                                 const int* __restrict__ row_map,
                                                                 const bf16_t* __restrict__ ckv,
                                                                 bf16_t* __restrict__ out) {
@@ -1370,16 +743,11 @@ __global__ TW_DEC_LB(NG * 8, UNR <= 4 ? 7 : 1) void k_attn_decode_cross_lean(con
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int key = min((it0 + u) * NG + g, S - 1);
-      if constexpr (NT) {
-        typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
-        const u32x4_nt a = __builtin_nontemporal_load((const u32x4_nt*)(K + (size_t)key * 64 + gl * 8));
-        const u32x4_nt c = __builtin_nontemporal_load((const u32x4_nt*)(V + (size_t)key * 64 + gl * 8));
-        kk[u] = make_uint4(a.x, a.y, a.z, a.w);
-        vv[u] = make_uint4(c.x, c.y, c.z, c.w);
-      } else {
-        kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
-        vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
-      }
+      typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+      const u32x4_nt a = __builtin_nontemporal_load((const u32x4_nt*)(K + (size_t)key * 64 + gl * 8));
+      const u32x4_nt c = __builtin_nontemporal_load((const u32x4_nt*)(V + (size_t)key * 64 + gl * 8));
+      kk[u] = make_uint4(a.x, a.y, a.z, a.w);
+      vv[u] = make_uint4(c.x, c.y, c.z, c.w);
     }
     __builtin_amdgcn_sched_barrier(0);  // all 2 x UNR loads in flight before the first is consumed
     float sv[UNR];
@@ -1387,19 +755,9 @@ __global__ TW_DEC_LB(NG * 8, UNR <= 4 ? 7 : 1) void k_attn_decode_cross_lean(con
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       float d = 0.f;
-      if constexpr (PK) {  // v_dot2_f32_bf16: two exact bf16 products per issue, no bf16 -> f32 unpacking of K
-        typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-        const unsigned* qw = (const unsigned*)&qr;
-        const unsigned* kw = (const unsigned*)&kk[u];
+      const bf16_t* ke = (const bf16_t*)&kk[u];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, qw[j]), __builtin_bit_cast(bf16x2v, kw[j]), d,
-                                              false);
-      } else {
-        const bf16_t* ke = (const bf16_t*)&kk[u];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
-      }
+      for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
       d += __shfl_xor(d, 1, 64);
       d += __shfl_xor(d, 2, 64);
       d += __shfl_xor(d, 4, 64);
@@ -1409,38 +767,15 @@ __global__ TW_DEC_LB(NG * 8, UNR <= 4 ? 7 : 1) void k_attn_decode_cross_lean(con
     if (bm == -INFINITY) continue;  // (no key of this group yet: short key ranges only)
     const float sc = __expf(m - bm);  // 0 on the group's first keys (m = -inf)
     l *= sc;
-    if constexpr (PK) {  // packed f32 (v_pk_mul_f32 / v_pk_fma_f32): the same roundings, half the issues
-      typedef float f32x2v __attribute__((ext_vector_type(2)));
-      f32x2v a2[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) a2[j] = (f32x2v){acc[2 * j], acc[2 * j + 1]} * (f32x2v){sc, sc};
+    for (int e = 0; e < 8; ++e) acc[e] *= sc;
 #pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        const float p = __expf(sv[u] - bm);  // 0 for the masked keys
-        l += p;
-        const unsigned* vw = (const unsigned*)&vv[u];
+    for (int u = 0; u < UNR; ++u) {
+      const float p = __expf(sv[u] - bm);  // 0 for the masked keys
+      l += p;
+      const bf16_t* ve = (const bf16_t*)&vv[u];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f32x2v v2 = {__uint_as_float(vw[j] << 16), __uint_as_float(vw[j] & 0xffff0000u)};
-          a2[j] = __builtin_elementwise_fma((f32x2v){p, p}, v2, a2[j]);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[2 * j] = a2[j].x;
-        acc[2 * j + 1] = a2[j].y;
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] *= sc;
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        const float p = __expf(sv[u] - bm);  // 0 for the masked keys
-        l += p;
-        const bf16_t* ve = (const bf16_t*)&vv[u];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += p * bf16_to_f32(ve[e]);
-      }
+      for (int e = 0; e < 8; ++e) acc[e] += p * bf16_to_f32(ve[e]);
     }
     m = bm;
   }
@@ -1480,36 +815,13 @@ __global__ TW_DEC_LB(NG * 8, UNR <= 4 ? 7 : 1) void k_attn_decode_cross_lean(con
   }
 }
 
+// Cross-attention step: q [B][D] bf16 (pre-scaled); cross K/V layout [kv][Bt][H][S][64] for this layer,
+// batch row b reads block row_map[b] (the encoder batch slot holding that row's audio window).
 extern "C" int tw_attn_decode_cross(const bf16_t* q, int B, int H, int S, int Bt, const int* row_map,
                                     const bf16_t* cross_kv, bf16_t* out, void* stream) {
   TW_REQUIRE(q && cross_kv && out && B > 0 && H > 0 && S > 0 && S <= DA_MAXK, "tw_attn_decode_cross: bad args");
-  if (tw_dec_cross_lean && tw_dec_cross_1p && tw_dec_cross_ng == 32 && tw_dec_cross_nt == 0) {
-    // (every slot non-temporal: the default; the per-slot nt split of the A/B knob stays on the 15 KiB kernel)
-    if (tw_dec_cross_pk && tw_dec_cross_unr == 8) {
-      hipLaunchKernelGGL((k_attn_decode_cross_lean<32, true, 8, true>), dim3(H, B), dim3(256), 0, (hipStream_t)stream,
-                         q, H * 64, S, Bt, row_map, cross_kv, out);
-      return tw_check_launch("tw_attn_decode_cross");
-    }
-    if (tw_dec_cross_unr == 12)
-      hipLaunchKernelGGL((k_attn_decode_cross_lean<32, true, 12>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, q,
-                         H * 64, S, Bt, row_map, cross_kv, out);
-    else if (tw_dec_cross_unr == 4)
-      hipLaunchKernelGGL((k_attn_decode_cross_lean<32, true, 4>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, q,
-                         H * 64, S, Bt, row_map, cross_kv, out);
-    else if (tw_dec_cross_unr == 6)
-      hipLaunchKernelGGL((k_attn_decode_cross_lean<32, true, 6>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, q,
-                         H * 64, S, Bt, row_map, cross_kv, out);
-    else
-      hipLaunchKernelGGL((k_attn_decode_cross_lean<32, true>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64,
-                         S, Bt, row_map, cross_kv, out);
-    return tw_check_launch("tw_attn_decode_cross");
-  }
-  if (tw_dec_cross_ng == 64 && tw_dec_cross_1p)
-    hipLaunchKernelGGL((k_attn_decode_cross<false, 64>), dim3(H, B), dim3(512), 0, (hipStream_t)stream, q, H * 64, S,
-                       Bt, row_map, cross_kv, out, XProbs{}, 1, tw_dec_cross_nt);
-  else
-    hipLaunchKernelGGL(k_attn_decode_cross<false>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt,
-                       row_map, cross_kv, out, XProbs{}, tw_dec_cross_1p, tw_dec_cross_nt);
+  hipLaunchKernelGGL((k_attn_decode_cross_lean<32>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt,
+                     row_map, cross_kv, out);
   return tw_check_launch("tw_attn_decode_cross");
 }
 
@@ -1521,7 +833,7 @@ extern "C" int tw_attn_decode_cross_probs(const bf16_t* q, int B, int H, int S, 
              "tw_attn_decode_cross_probs: bad args");
   TW_REQUIRE(slot0 >= 0 && slot0 + __builtin_popcount(head_mask) <= n_slots && n_steps > 0,
              "tw_attn_decode_cross_probs: slots");
-  hipLaunchKernelGGL(k_attn_decode_cross<true>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt,
-                     row_map, cross_kv, out, XProbs{probs, pos, head_mask, slot0, n_slots, pos0, n_steps}, 0, 1 << 30);
+  hipLaunchKernelGGL(k_attn_decode_cross_probs, dim3(H, B), dim3(256), 0, (hipStream_t)stream, q, H * 64, S, Bt,
+                     row_map, cross_kv, out, XProbs{probs, pos, head_mask, slot0, n_slots, pos0, n_steps});
   return tw_check_launch("tw_attn_decode_cross_probs");
 }

@@ -18,7 +18,7 @@ import io
 import math
 import os
 import struct
-from typing import NamedTuple, Tuple, Union
+from typing import NamedTuple, Optional, Tuple, Union
 
 import numpy as np
 
@@ -53,11 +53,12 @@ def decode_flac(data: bytes, threads: int = 0) -> FlacStream:
     info = flac_probe(data)
     total, ch = int(info.total_samples), int(info.channels)
     # bound the allocation before trusting the header: a frame codes at most 65535 samples per channel in no fewer
-    # than ~(6 + channels) bytes, and the decoded PCM is capped (TW_MAX_PCM_SAMPLES, default 2^31 frame-samples)
-    cap = int(os.environ.get("TW_MAX_PCM_SAMPLES", str(1 << 31)))
-    if total * ch > cap or total > (len(data) // (6 + ch) + 1) * 65535:
-        raise ValueError(f"FLAC header claims {total} samples x {ch} channels: larger than the stream can code "
-                         f"or than TW_MAX_PCM_SAMPLES={cap}")
+    # than ~(6 + channels) bytes, and the stream may last at most max_audio_seconds() (constant-subframe frames code
+    # 65535 samples in a few bytes, so the byte bound alone admits ~0.2 Gsamples per MB)
+    max_s = max_audio_seconds()
+    if total > (len(data) // (6 + ch) + 1) * 65535 or total > max_s * int(info.sample_rate):
+        raise ValueError(f"FLAC header claims {total} samples x {ch} channels at {int(info.sample_rate)} Hz: larger "
+                         f"than the stream can code or longer than TW_MAX_AUDIO_S={max_s:g} s")
     pcm = np.zeros((total, ch), np.int32)  # never hand out uninitialised memory, whatever the decoder reports
     got = ctypes.c_int64()
     if lib.tw_flac_decode(ctypes.c_char_p(data), len(data), pcm.ctypes.data, pcm.shape[0], int(threads),
@@ -181,6 +182,36 @@ def resample(x: np.ndarray, sr_in: int, sr_out: int = TARGET_SR, device=None) ->
     return resample_device(np.asarray(x, np.float32), sr_in, sr_out, device=device).cpu().numpy()
 
 
+def max_audio_seconds() -> float:
+    """Longest input decoded (env TW_MAX_AUDIO_S, default 4 h): caps a container's claimed length before any
+    allocation."""
+    return float(os.environ.get("TW_MAX_AUDIO_S", "14400"))
+
+
+# Containers the engine recognises but does not decode (no MP3 / AAC / Vorbis / Opus decoder is built in): reported
+# by name, as a ValueError like the reference's own decode failure (ffmpeg_read, which its transcribe() turns into
+# its {"error": ...} result).
+_UNDECODED = ((b"ID3", "MP3"), (b"\xff\xfb", "MP3"), (b"\xff\xf3", "MP3"), (b"\xff\xf2", "MP3"), (b"OggS", "Ogg"),
+              (b"\x1aE\xdf\xa3", "Matroska/WebM"), (b"\xff\xf1", "AAC (ADTS)"), (b"\xff\xf9", "AAC (ADTS)"))
+# transformers' ffmpeg_read message for a payload ffmpeg cannot decode (pipelines/audio_utils.py)
+MALFORMED = ("Soundfile is either not in the correct format or is malformed. Ensure that the soundfile has a valid "
+             "audio file extension (e.g. wav, flac or mp3) and is not corrupted. If reading from a remote URL, ensure "
+             "that the URL is the full address to **download** the audio file.")
+
+
+def container_name(data: bytes) -> Optional[str]:
+    if data[:4] == b"RIFF":
+        return "WAV"
+    if data[:4] == b"fLaC":
+        return "FLAC"
+    if data[4:8] == b"ftyp":
+        return "MP4/M4A"
+    for magic, name in _UNDECODED:
+        if data.startswith(magic):
+            return name
+    return None
+
+
 def decode_bytes(data: bytes, sr_out: int = TARGET_SR, device=None) -> np.ndarray:
     if data[:4] == b"RIFF":
         x, sr = decode_wav(data)
@@ -189,7 +220,11 @@ def decode_bytes(data: bytes, sr_out: int = TARGET_SR, device=None) -> np.ndarra
         fl = decode_flac(data)
         scale = 2.0 ** -(fl.bits_per_sample - 1)  # ffmpeg's s16/s32 -> flt conversion of the coded samples
         return resample_device(fl.pcm, fl.sample_rate, sr_out, scale=scale, device=device).cpu().numpy()
-    raise ValueError("unrecognised audio container (supported: FLAC, RIFF/WAVE)")
+    name = container_name(data)
+    if name is None:
+        raise ValueError(MALFORMED)
+    raise ValueError(f"{name} audio is not decoded by this engine (decoded containers: FLAC, WAV); convert the "
+                     "upload to FLAC or WAV")
 
 
 def load_input(inputs: Union[str, bytes, np.ndarray, dict], sr_out: int = TARGET_SR, device=None) -> np.ndarray:

@@ -132,8 +132,9 @@ def gather_tokens(local_seqs: Sequence[Sequence[int]], local_langs: Optional[Seq
 
 
 def broadcast_waveform(wav: Optional[np.ndarray], device: Optional[torch.device] = None, src: int = 0,
-                       group=None, failed: bool = False) -> Optional[np.ndarray]:
-    """Rank `src` holds the decoded 16 kHz waveform; every rank returns a copy (length first, then samples).
+                       group=None, failed: bool = False, as_tensor: bool = False):
+    """Rank `src` holds the decoded 16 kHz waveform; every rank returns a copy (length first, then samples):
+    a host array, or with as_tensor the collective's own buffer (device memory under RCCL: no host round trip).
 
     `failed` (meaningful on `src`): decoding the input raised there. The length slot then carries -1: `src` gets
     None back (and re-raises its own error), every other rank raises PeerError, so no rank waits for samples."""
@@ -152,7 +153,7 @@ def broadcast_waveform(wav: Optional[np.ndarray], device: Optional[torch.device]
     if rank == src:
         buf.copy_(torch.from_numpy(np.ascontiguousarray(wav, np.float32)))
     dist.broadcast(buf, src=src, group=group)
-    return buf.cpu().numpy()
+    return buf if as_tensor else buf.cpu().numpy()
 
 
 def transcribe_sharded(run_windows, wav: np.ndarray, windows: Sequence, device: Optional[torch.device] = None,

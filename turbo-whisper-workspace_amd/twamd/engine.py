@@ -239,6 +239,10 @@ class WhisperEngine:
         self.fused_select = True
         # the prompt phase of a decode pass replayed as one captured graph (False: eager)
         self.prompt_graph = True
+        # encoder attention kernel (tw_attn_set_variant) and its LDS cap in 16 KiB units (tw_attn_set_lds_pad) for an
+        # encoder chunk alone / beside a running decode
+        self.attn_kernel = (16, 16)
+        self.attn_pad = (0, 4)
         # run_batches encodes batch k+1 beside the decode of batch k (sequential 138.6 vs overlapped 114.5 ms per
         # bench step, round 1); False: strictly in turn
         self.overlap = True
@@ -319,8 +323,11 @@ class WhisperEngine:
     timer_families: Optional[set] = None
 
     def _begin_timer(self, key, work, stream=None):
-        """HIP events on the stream the kernel is launched on."""
+        """HIP events on the stream the kernel is launched on (none inside a graph capture: a captured launch's
+        events would time the capture, not the replay)."""
         if self.timers is None or (self.timer_families is not None and key[0] not in self.timer_families):
+            return None
+        if torch.cuda.is_current_stream_capturing():
             return None
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
@@ -415,7 +422,8 @@ class WhisperEngine:
         kernels then find free wave slots; measured decoder GEMV 21.9 -> 5.6 us per launch beside it, bench step
         112.1 -> 108.5 ms), uncapped alone (the cap costs the attention itself 22 %)."""
         _lib.call("tw_gemm_set_variant", 5 if alone else 1)
-        _lib.call("tw_attn_set_lds_pad", 0 if alone else 4)
+        _lib.call("tw_attn_set_variant", self.attn_kernel[0 if alone else 1])
+        _lib.call("tw_attn_set_lds_pad", self.attn_pad[0 if alone else 1])
 
     def _encode_steps(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True,
                       alone: bool = True):

@@ -64,6 +64,12 @@ class TurboTranscriber:
         self.vocab = vocab
         self.sampling_rate = sampling_rate
         self.gen = engine.gen
+        # A share of n <= max_batch windows is split into two sub-batches when n >= 2 * sub_batch_min, so that
+        # run_batches' two-slot pipeline encodes the second beside the first one's decode (a single 1-h request on
+        # 8 GPUs gives each rank 15 windows: one batch, no overlap). None: never split (see DESIGN.md §C3 for the
+        # measured trade: the decode step is latency-bound, so two decodes of 8 cost about two of 15).
+        self.sub_batch_min: Optional[int] = None
+        self._staging = None  # two pinned host buffers for the per-batch waveform upload (host-array inputs)
 
     # -------------------------------------------------------------- construction
     @staticmethod
@@ -114,6 +120,8 @@ class TurboTranscriber:
         task = gk.pop("task", None)
         language = gk.pop("language", None)
         max_new_tokens = dec["max_new_tokens"]
+        # extension (not a transformers generate kwarg): bound the seek loop to this many passes per window
+        max_passes = gk.pop("max_passes", None)
         st = self.gen.special
         if not st.is_multilingual and (task is not None or language is not None):
             raise ValueError("Cannot specify `task` or `language` for an English-only model.")
@@ -127,7 +135,8 @@ class TurboTranscriber:
             except Exception as e:  # raised below, after the other ranks have been told (no rank left waiting)
                 load_err = e
         if world > 1:  # SPMD: every rank calls with the same arguments; rank 0 decoded the input
-            wav = dist.broadcast_waveform(wav, failed=load_err is not None)
+            # (the waveform stays in device memory: each rank copies its windows out of it on the GPU)
+            wav = dist.broadcast_waveform(wav, failed=load_err is not None, as_tensor=True)
         if load_err is not None:
             raise load_err
         if chunk_length_s:
@@ -155,10 +164,11 @@ class TurboTranscriber:
                       for x in ws]
                 toks = self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=True,
                                                max_new_tokens=max_new_tokens, num_beams=num_beams,
-                                               word_timestamps=True, num_frames=nf, group=batch_size)
+                                               word_timestamps=True, num_frames=nf, group=batch_size,
+                                               max_passes=max_passes)
                 return [(t, ts) for t, ts in zip(toks, self.last_window_token_timestamps)]
             return self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=bool(return_timestamps),
-                                           max_new_tokens=max_new_tokens, num_beams=num_beams)
+                                           max_new_tokens=max_new_tokens, num_beams=num_beams, max_passes=max_passes)
 
         # one window shard per rank + one all-gather of the token arrays (twamd.dist); plain call on 1 GPU
         outputs = dist.transcribe_sharded(run, wav, windows, timed=word) if world > 1 else run(wav, windows)
@@ -181,7 +191,8 @@ class TurboTranscriber:
     def transcribe_windows(self, wav: np.ndarray, windows: Sequence[Window], task: Optional[str],
                            lang_id: Optional[int], return_timestamps: bool,
                            max_new_tokens: Optional[int] = None, num_beams: int = 1, word_timestamps: bool = False,
-                           num_frames: Optional[Sequence[int]] = None, group: Optional[int] = None) -> List[List[int]]:
+                           num_frames: Optional[Sequence[int]] = None, group: Optional[int] = None,
+                           max_passes: Optional[int] = None) -> List[List[int]]:
         """Log-mel + generate for every window; returns per-window token sequences (generate() output,
         right-padded with the pad token within each engine batch, as the HF batch output is). Batches of
         max_batch windows go through WhisperEngine.run_batches: batch k+1 is encoded while batch k decodes.
@@ -189,26 +200,46 @@ class TurboTranscriber:
         group: windows per engine batch when the batch's composition changes results. That is the case only for
         word timestamps, whose per-pass standardisation runs over the padded batch, so the pipeline's
         `batch_size` (its DataLoader batch, $TF/pipelines/base.py:1319-1339) is honoured there; segment-level
-        tokens are per-window results, so batching is then only a schedule and the engine fills max_batch."""
+        tokens are per-window results, so batching is then only a schedule: the windows are cut into near-equal
+        batches of at most max_batch (and into two when sub_batch_min says so).
+
+        wav: a host array, or a torch tensor (a rank's copy of the broadcast waveform, in device memory)."""
         eng = self.engine
-        B = eng.max_batch if not group else max(1, min(int(group), eng.max_batch))
-        parts = [windows[b0: b0 + B] for b0 in range(0, len(windows), B)]
+        if group:
+            B = max(1, min(int(group), eng.max_batch))
+            sizes = [min(B, len(windows) - b0) for b0 in range(0, len(windows), B)]
+        else:
+            sizes = batch_sizes(len(windows), eng.max_batch, self.sub_batch_min)
+        offs = np.cumsum([0] + sizes).tolist()
+        parts = [windows[offs[k]: offs[k + 1]] for k in range(len(sizes))]
+        on_device = torch.is_tensor(wav)
 
         def load(k):  # called on the engine's encoder stream
             part = parts[k]
-            host = np.zeros((len(part), CHUNK_SAMPLES), np.float32)
+            if on_device:  # device-to-device slices of the rank's waveform copy
+                dst = eng.wave[: len(part)]
+                for j, w in enumerate(part):
+                    n = min(w.length, CHUNK_SAMPLES)  # feature extractor truncation
+                    dst[j, :n].copy_(wav[w.start: w.start + n], non_blocking=True)
+                    dst[j, n:].zero_()
+                return
+            host = self._host_staging(k % 2, len(part))
             for j, w in enumerate(part):
                 seg = wav[w.start: w.start + min(w.length, CHUNK_SAMPLES)]  # feature extractor truncation
-                host[j, : len(seg)] = seg
-            eng.wave[: len(part)].copy_(torch.from_numpy(host))
+                host[j, : len(seg)] = torch.from_numpy(np.ascontiguousarray(seg, np.float32))
+                host[j, len(seg):] = 0
+            eng.wave[: len(part)].copy_(host, non_blocking=host.is_pinned())
+            if self._staging is not None:
+                self._staging[1][k % 2].record(torch.cuda.current_stream(eng.wave.device))
 
         bkw = None
         if word_timestamps:
-            bkw = [{"word_timestamps": True, "num_frames": list(num_frames[b0: b0 + B])}
-                   for b0 in range(0, len(windows), B)]
-        res = eng.run_batches([len(p) for p in parts], load=load, batch_kwargs=bkw, task=task,
-                              lang_ids=None if lang_id is None else [lang_id] * B, max_new_tokens=max_new_tokens,
-                              return_timestamps=return_timestamps, num_beams=num_beams)
+            bkw = [{"word_timestamps": True, "num_frames": list(num_frames[offs[k]: offs[k + 1]])}
+                   for k in range(len(sizes))]
+        res = eng.run_batches(sizes, load=load, batch_kwargs=bkw, task=task,
+                              lang_ids=None if lang_id is None else [lang_id] * max(sizes, default=1),
+                              max_new_tokens=max_new_tokens, return_timestamps=return_timestamps, num_beams=num_beams,
+                              max_passes=max_passes)
         out: List[List[int]] = []
         for seqs in res:
             out.extend(pad_right(seqs, self.gen.special.eot))
@@ -218,6 +249,31 @@ class TurboTranscriber:
         if word_timestamps:  # per window the concatenated segments' token times (not padded, as the pipeline's)
             self.last_window_token_timestamps = [t for bt in eng.batch_token_timestamps for t in bt]
         return out
+
+    def _host_staging(self, i: int, rows: int) -> torch.Tensor:
+        """Pinned host buffer i (of two, alternating per batch) for a batch's waveforms: the upload is then an async
+        copy on the encoder stream; a buffer is refilled only after its previous copy has completed."""
+        wave = self.engine.wave
+        if not (torch.is_tensor(wave) and wave.is_cuda):
+            return torch.zeros(rows, CHUNK_SAMPLES, dtype=torch.float32)
+        if self._staging is None:
+            bufs = [torch.empty(wave.shape[0], CHUNK_SAMPLES, dtype=torch.float32, pin_memory=True) for _ in range(2)]
+            self._staging = (bufs, [torch.cuda.Event() for _ in range(2)])
+        self._staging[1][i].synchronize()
+        return self._staging[0][i][:rows]
+
+
+def batch_sizes(n: int, max_batch: int, sub_batch_min: Optional[int] = None) -> List[int]:
+    """Engine batch sizes for n windows: ceil(n / max_batch) near-equal batches (e.g. 30 windows at 24 -> 15 + 15,
+    so that the encoder of the second overlaps the decode of the first with the same work on each side), and two
+    when a single batch would hold >= 2 * sub_batch_min windows."""
+    if n <= 0:
+        return []
+    k = -(-n // max_batch)
+    if k == 1 and sub_batch_min is not None and n >= 2 * sub_batch_min:
+        k = 2
+    base, rem = divmod(n, k)
+    return [base + 1] * rem + [base] * (k - rem)
 
 
 def _dims_from_checkpoint(path: str) -> WhisperDims:
