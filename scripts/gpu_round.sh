@@ -19,7 +19,8 @@ step() {  # step NAME TIMEOUT CMD...
   if [ $rc -ne 0 ] && [ $rc -ne 5 ]; then echo "STOP after $name"; exit $rc; fi
 }
 if [ "$SKIP_TESTS" != "1" ]; then
-  step tests 900 python -m pytest tests -q -m gpu -x -p no:cacheprovider
+  step tests 900 python -u -m pytest tests -q -m gpu -x -p no:cacheprovider --timeout 300 --timeout-method thread
+  cp $OUT/tests.log profiles/${TAG}_gputest.txt
 fi
 step prof_kt 600 rocprofv3 --kernel-trace --stats -T -d $OUT/kt -o kt --output-format csv -- python bench.py $BA --profile-only --steps 2 --warmup 1
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/pmc_fetch -o pmc --output-format csv -- python bench.py $BA --profile-only --steps 1 --warmup 0
@@ -27,6 +28,8 @@ step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/pmc_write -o pmc --outp
 step pmc_mfma 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_BF16 -T -d $OUT/pmc_mfma -o pmc --output-format csv -- python bench.py $BA --profile-only --steps 1 --warmup 0
 python scripts/summarize_prof.py $OUT > $OUT/summary.txt 2>&1
 cp $OUT/traffic.json profiles/${TAG}_traffic.json   # bench.py reads the newest profiles/*traffic.json
+[ -f $OUT/mfma.json ] && cp $OUT/mfma.json profiles/${TAG}_mfma.json
 step bench 900 python bench.py $BA --steps 5 --warmup 2
 grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
+cp $OUT/bench.json profiles/${TAG}_bench.json; cp $OUT/summary.txt profiles/${TAG}_rocprof_summary.txt
 echo done
