@@ -13,7 +13,7 @@ from twamd import _lib  # noqa: E402
 _lib.load()
 B, S, H = 24, 1500, 20
 D = H * 64
-VAR = [int(v) for v in sys.argv[1:]] or [16, 8]
+VAR = [int(v) for v in sys.argv[1:]] or [16, 32, 8]
 qkv = (torch.randn(B * S, 3 * D, device="cuda")).to(torch.bfloat16)
 qkv[:, :D] = (qkv[:, :D].float() * 0.125).to(torch.bfloat16)
 out = torch.empty(B * S, D, dtype=torch.bfloat16, device="cuda")

@@ -12,6 +12,8 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
   word.npz/.json    token-level timestamps (cross-attention DTW) of generate(return_token_timestamps=True) and
                     the pipeline's return_timestamps="word" output, plus HF's _median_filter / _dynamic_time_warping
                     on seeded random matrices
+  tiny.npz          whisper-tiny.en (configs[0], English-only) encoder rows, teacher-forced logits, generate() passes
+                    with their processed top-16 scores
   beam.json         generate(num_beams=5) token sequences (the pipeline's default decode, asr:160-163) of
                     test-mini on three windows, with and without timestamps and with a max_length stop
 
@@ -498,6 +500,78 @@ def make_turbo(out):
         res[f"bench_w{w}_top_idx"], res[f"bench_w{w}_top_val"], res[f"bench_w{w}_ts_margin"] = a, b, c
     m.generation_config.suppress_tokens = list(gen.suppress_tokens)
     np.savez_compressed(os.path.join(out, "turbo.npz"), **res)
+
+
+TINY_CLIPS = ("speech30", "noise12")
+
+
+def make_tiny(out):
+    """whisper-tiny.en dims (BASELINE configs[0]: d 384, 4 + 4 layers, 6 heads, 80 mels, English-only vocabulary
+    51864) with the seeded synthetic weights: encoder output rows, teacher-forced logits along clip 0's first pass
+    and generate() (no language / task tokens: the English-only prompt is <|startoftranscript|> alone) with the
+    processed top-16 scores of every pass, from transformers on CPU fp32. Pins the oracle at tiny.en
+    (tests/test_oracle_golden.py) and the engine on the GPU (tests/test_gpu_configs.py)."""
+    from transformers import WhisperFeatureExtractor
+
+    d = PRESETS["tiny.en"]
+    gen = GenerationSettings.default(d)
+    st = gen.special
+    assert not st.is_multilingual
+    g = wo.GenCfg(d.vocab, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate,
+                  st.notimestamps, gen.suppress_tokens, gen.begin_suppress_tokens, multilingual=False)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    # an English-only checkpoint's generation_config has no language / task tables (generate() would otherwise run
+    # language detection: generation_whisper.py _retrieve_init_tokens)
+    delattr(m.generation_config, "lang_to_id")
+    delattr(m.generation_config, "task_to_id")
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    cl = clips()
+    feats = np.stack([fe(cl[k], sampling_rate=16000, return_tensors="np")["input_features"][0] for k in TINY_CLIPS])
+    res = {}
+    with torch.no_grad():
+        enc = m.model.encoder(torch.from_numpy(feats)).last_hidden_state.numpy()
+    res["enc_rows_idx"] = np.array([0, 1, 2, 375, 750, 1124, 1498, 1499])
+    res["enc_rows"] = enc[:, res["enc_rows_idx"]].astype(np.float32)
+    res["enc_mean"] = enc.mean(axis=(1, 2))
+    res["enc_std"] = enc.std(axis=(1, 2))
+    res["enc_row_norm"] = np.linalg.norm(enc, axis=2).astype(np.float32)
+    with torch.no_grad():
+        o = m.generate(torch.from_numpy(feats), return_timestamps=True, num_beams=1, max_new_tokens=48,
+                       return_segments=True)
+    res["gen_sequences"] = o["sequences"].numpy()
+    pr = [st.sot]
+    for i in range(len(TINY_CLIPS)):
+        passes = _passes_from_segments(o["segments"][i], len(pr))
+        seek, ti, tv, mg, kept, offs = 0, [], [], [], [], [0]
+        for q in passes:
+            toks = q[: q.index(st.eot) + 1] if st.eot in q else q
+            a, b, c = _teacher_forced_pass_scores(m, feats[i], seek, pr, toks, g)
+            ti.append(a); tv.append(b); mg.append(c)
+            seq = toks[:-1] if toks and toks[-1] == st.eot else toks
+            seg, off = wo.retrieve_segment(seq, 3000 - seek, g.ts_begin)
+            kept += seg
+            seek += off
+            offs.append(seek)
+        ref = [int(t) for t in res["gen_sequences"][i]]
+        while ref and ref[-1] == st.eot:
+            ref.pop()
+        assert kept == ref, ("pass reconstruction differs from generate()", i)
+        res[f"gen{i}_pass_len"] = np.array([len(x) for x in ti], np.int32)
+        res[f"gen{i}_pass_tokens"] = np.concatenate(
+            [np.array(q[: len(x)], np.int32) for q, x in zip(passes, ti)]) if passes else np.zeros(0, np.int32)
+        res[f"gen{i}_pass_seek"] = np.array(offs[:-1], np.int32)
+        res[f"gen{i}_top_idx"], res[f"gen{i}_top_val"] = np.concatenate(ti), np.concatenate(tv)
+        res[f"gen{i}_ts_margin"] = np.concatenate(mg)
+    p0 = pr + [int(t) for t in res["gen0_pass_tokens"][:23]]
+    res["tf_input_ids"] = np.array(p0[:24])
+    with torch.no_grad():
+        lg = m(input_features=torch.from_numpy(feats[:1]), decoder_input_ids=torch.tensor([p0[:24]])).logits[0].numpy()
+    top = np.argsort(-lg, axis=1, kind="stable")[:, :16]
+    res["tf_top_idx"] = top
+    res["tf_top_val"] = np.take_along_axis(lg, top, 1).astype(np.float32)
+    res["tf_lse"] = (np.log(np.exp(lg - lg.max(1, keepdims=True)).sum(1)) + lg.max(1)).astype(np.float64)
+    np.savez_compressed(os.path.join(out, "tiny.npz"), **res)
 
 
 def _jsonable(x):

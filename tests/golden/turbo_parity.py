@@ -27,7 +27,7 @@ def load(path: str = os.path.join(HERE, "turbo.npz")):
 
 
 def check_pass(tokens: Sequence[int], gold_tokens: Sequence[int], top_idx: np.ndarray, top_val: np.ndarray,
-               ts_margin: np.ndarray, tau: float = TAU) -> Dict:
+               ts_margin: np.ndarray, tau: float = TAU, ts_begin: int = TIMESTAMP_BEGIN) -> Dict:
     """Compare one seek pass's generated tokens (prompt excluded, EOS included) with the fp32 pass."""
     tokens = [int(t) for t in tokens]
     gold = [int(t) for t in gold_tokens]
@@ -43,7 +43,7 @@ def check_pass(tokens: Sequence[int], gold_tokens: Sequence[int], top_idx: np.nd
         v = float(row_v[row_i.index(g)])
         if np.isfinite(v) and v >= float(row_v[0]) - tau:
             return {"status": "within_tau", "first_divergence": t, "n": len(gold), "gap": float(row_v[0]) - v}
-    if abs(float(ts_margin[t])) <= tau and (g >= TIMESTAMP_BEGIN) != (gold[t] >= TIMESTAMP_BEGIN):
+    if abs(float(ts_margin[t])) <= tau and (g >= ts_begin) != (gold[t] >= ts_begin):
         return {"status": "within_tau", "first_divergence": t, "n": len(gold), "rule_margin": float(ts_margin[t])}
     return {"status": "mismatch", "first_divergence": t, "n": len(gold), "device": g, "fp32": gold[t],
             "fp32_top": row_i[:4]}

@@ -73,6 +73,67 @@ def test_tiny_en_teacher_forced_logits(tiny):
         assert np.abs(got - ref).max() < 0.15, (t, np.abs(got - ref).max())
 
 
+@pytest.fixture(scope="module")
+def tiny_z():
+    return np.load(os.path.join(ROOT, "tests", "golden", "tiny.npz"))
+
+
+def test_tiny_en_vs_transformers_goldens(tiny, tiny_z):
+    """The engine at tiny.en against transformers fp32 itself (tests/golden/tiny.npz, make_golden.py tiny): encoder
+    rows (0.08 abs, as test-mini), the 16 fp32-top teacher-forced logits and their log-sum-exp (0.15 abs), and
+    generate() (English-only prompt, seek loop, 48 new tokens) pass by pass: equal, or diverging first at a near-tie
+    within tau = 0.3 (the tolerance of the oracle replay above)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import turbo_parity as tp
+
+    tr, _, d = tiny
+    z = tiny_z
+    eng = tr.engine
+    clips = [speech_like(30.0, 1234), white_noise(12.3, 7)]
+    host = np.zeros((2, 480000), np.float32)
+    for i, c in enumerate(clips):
+        host[i, : len(c)] = c[:480000]
+    eng.wave[:2].copy_(torch.from_numpy(host))
+    eng.logmel(2)
+    eng.row_map[:2] = torch.arange(2, dtype=torch.int32)
+    eng.seek[:2] = 0
+    eng.encode(2)
+    enc = eng.encoder_output(2).float().cpu().numpy()
+    for i in range(2):
+        assert np.abs(enc[i][z["enc_rows_idx"]] - z["enc_rows"][i]).max() < 0.08
+        assert abs(enc[i].mean() - z["enc_mean"][i]) < 2e-3 and abs(enc[i].std() - z["enc_std"][i]) < 2e-3
+    for t, tok in enumerate(z["tf_input_ids"]):
+        eng.ids[0] = int(tok)
+        eng.pos[0] = t
+        eng.decoder_step(1, r_enc=2)  # (cross K/V encoded with batch stride 2)
+        lg = eng.logits[0].cpu().numpy().astype(np.float64)
+        m = lg.max()
+        assert np.abs(lg[z["tf_top_idx"][t]] - z["tf_top_val"][t]).max() < 0.15, t
+        assert abs(m + np.log(np.exp(lg - m).sum()) - z["tf_lse"][t]) < 0.15, t
+    eng.logmel(2)
+    seqs = eng.generate(2, task=None, max_new_tokens=48, return_timestamps=True)
+    st = tr.gen.special
+    for i in range(2):
+        ref = [int(x) for x in z["gen_sequences"][i]]
+        while ref and ref[-1] == st.eot:
+            ref.pop()
+        if seqs[i] == ref:
+            continue
+        lens, o = z[f"gen{i}_pass_len"], 0
+        for k, n in enumerate(lens):
+            dev = [int(x) for x in eng.last_passes[i][k]] if k < len(eng.last_passes[i]) else []
+            dev = dev[: dev.index(st.eot) + 1] if st.eot in dev else dev
+            r = tp.check_pass(dev, z[f"gen{i}_pass_tokens"][o: o + n], z[f"gen{i}_top_idx"][o: o + n],
+                              z[f"gen{i}_top_val"][o: o + n], z[f"gen{i}_ts_margin"][o: o + n], tau=0.3,
+                              ts_begin=st.timestamp_begin)
+            o += n
+            if r["status"] != "exact":
+                assert r["status"] == "within_tau", (i, k, r)
+                break
+
+
 def test_tiny_en_generate_is_tolerance_greedy(tiny):
     tr, oracle, d = tiny
     eng = tr.engine

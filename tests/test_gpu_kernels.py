@@ -200,8 +200,9 @@ def _ref_attn(q, k, v):  # [B,H,S,64] fp32, q already scaled
     return torch.softmax(q @ k.transpose(-1, -2), dim=-1) @ v
 
 
-@pytest.mark.parametrize("variant", [16, 8])
-@pytest.mark.parametrize("B,L,H", [(2, 1500, 4), (1, 100, 2), (1, 1500, 20), (3, 1500, 5), (1, 128, 3), (2, 40, 2)])
+@pytest.mark.parametrize("variant", [32, 16, 8])
+@pytest.mark.parametrize("B,L,H", [(2, 1500, 4), (1, 100, 2), (1, 1500, 20), (3, 1500, 5), (1, 128, 3), (2, 40, 2),
+                                   (1, 64, 2), (1, 65, 1)])
 def test_encoder_attention_vs_torch(B, L, H, variant):
     _lib.call("tw_attn_set_variant", variant)
     D = H * 64
@@ -213,6 +214,24 @@ def test_encoder_attention_vs_torch(B, L, H, variant):
     t = qkv.float().view(B, L, 3, H, 64).permute(2, 0, 3, 1, 4)
     ref = _ref_attn(t[0], t[1], t[2]).permute(0, 2, 1, 3).reshape(B * L, D)
     torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("B,L,H", [(2, 1500, 4), (1, 100, 2), (1, 128, 3), (1, 300, 2), (3, 1500, 5)])
+def test_encoder_attention_enc5_close_to_enc2(B, L, H):
+    """Variant 32 (k_attn_enc5, the default: log2-unit scores, guarded unshifted exp2) against k_attn_enc2's
+    running-max form on the same inputs, including partial query blocks (L = 100, 300): within the two kernels' torch
+    fp32 tolerance (2e-2 each; measured max 0.023 at L = 1500, 37 of 768000 elements beyond 8e-3)."""
+    D = H * 64
+    qkv = rand_bf16(B * L, 3 * D, seed=27)
+    qkv[:, :D] = bf(qkv[:, :D].float() * 0.375)
+    outs = []
+    for v in (8, 32):
+        _lib.call("tw_attn_set_variant", v)
+        out = torch.empty(B * L, D, dtype=torch.bfloat16, device=DEV)
+        _lib.call("tw_attn_encoder", qkv.data_ptr(), B, L, H, out.data_ptr(), S())
+        outs.append(out)
+    _lib.call("tw_attn_set_variant", 16)
+    torch.testing.assert_close(outs[1].float(), outs[0].float(), atol=3e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("B,L,H", [(2, 1500, 4), (1, 100, 2), (1, 128, 3), (1, 300, 2), (3, 1500, 5)])
@@ -253,7 +272,7 @@ def test_encoder_attention_lds_pad_is_bit_identical(pad):
         _lib.call("tw_attn_set_variant", 10)  # (pruned variants are refused, not silently mapped)
 
 
-@pytest.mark.parametrize("variant", [16, 8])
+@pytest.mark.parametrize("variant", [32, 16, 8])
 def test_encoder_attention_online_softmax_rescale(variant):
     """Force the running max to jump in a late key tile (rule 26: exercise the rescale branch)."""
     _lib.call("tw_attn_set_variant", variant)
@@ -261,6 +280,35 @@ def test_encoder_attention_online_softmax_rescale(variant):
         _online_softmax_rescale()
     finally:
         _lib.call("tw_attn_set_variant", 16)
+
+
+@pytest.mark.parametrize("variant", [32, 16, 8])
+@pytest.mark.parametrize("case", ["late_dominant", "first_tile_negative", "first_tile_positive"])
+def test_encoder_attention_extreme_scores(variant, case):
+    """Scores far outside k_attn_enc5's unshifted range (|s| > 64 in log2 units): a late key scoring +128 for half the
+    queries and -128 for the others (the guarded rescale, per-lane growth 0 or > 0 in one wave), a first tile scoring
+    -128 (stabiliser set from the first tile, then moved up), a first tile scoring +128 (stabiliser kept)."""
+    B, L, H = 1, 1500, 2
+    D = H * 64
+    qkv = rand_bf16(B * L, 3 * D, scale=0.3, seed=9)
+    sign = torch.where(torch.arange(L, device=DEV) % 3 == 0, -1.0, 1.0)[:, None]
+    qkv[:, :D] = bf(sign.expand(L, D) * 1.0)  # q = +-1 in every dim: the score with key k is +-sum(k)
+    if case == "late_dominant":
+        qkv[1400, D:2 * D] = bf(torch.full((D,), 2.0, device=DEV))  # +-128
+    elif case == "first_tile_negative":
+        qkv[:64, D:2 * D] = bf(torch.full((64, D), -2.0, device=DEV))
+    else:
+        qkv[:64, D:2 * D] = bf(torch.full((64, D), 2.0, device=DEV))
+    out = torch.empty(B * L, D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_attn_set_variant", variant)
+    try:
+        _lib.call("tw_attn_encoder", qkv.data_ptr(), B, L, H, out.data_ptr(), S())
+    finally:
+        _lib.call("tw_attn_set_variant", 16)
+    t = qkv.float().view(B, L, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ref = _ref_attn(t[0], t[1], t[2]).permute(0, 2, 1, 3).reshape(B * L, D)
+    assert torch.isfinite(out.float()).all()
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
 
 
 def _online_softmax_rescale():

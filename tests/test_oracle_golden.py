@@ -128,3 +128,49 @@ def test_token_timestamps_match_transformers(oracle_model, gcfg, name):
                                   max_new_tokens=40, alignment_heads=[(1, 0), (1, 1), (1, 2), (1, 3)], num_frames=nf)
     assert toks == z[f"gen_{name}_seq"][0].tolist()
     np.testing.assert_allclose(tts, z[f"gen_{name}_ts"][0], atol=1e-6)
+
+
+# ---- whisper-tiny.en (BASELINE configs[0]): English-only vocabulary, 80 mels, no language / task tokens ----------
+TINY = PRESETS["tiny.en"]
+
+
+@pytest.fixture(scope="module")
+def tiny_golden():
+    return np.load(os.path.join(G, "tiny.npz"))
+
+
+@pytest.fixture(scope="module")
+def tiny_oracle():
+    d = TINY
+    return wo.WhisperOracle(wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels,
+                                                d.vocab, 1234), d.heads)
+
+
+def test_tiny_en_encoder_and_logits_match_transformers(tiny_golden, tiny_oracle):
+    z = tiny_golden
+    enc = tiny_oracle.encode(wo.log_mel(speech_like(30.0, 1234), TINY.n_mels))
+    np.testing.assert_allclose(enc[z["enc_rows_idx"]], z["enc_rows"][0], atol=2e-3, rtol=0)
+    assert abs(enc.mean() - z["enc_mean"][0]) < 1e-4 and abs(enc.std() - z["enc_std"][0]) < 1e-4
+    cache = tiny_oracle.new_cache(enc)
+    for t, tok in enumerate(z["tf_input_ids"]):
+        lg = tiny_oracle.decoder_step(int(tok), cache)
+        top = z["tf_top_idx"][t]
+        np.testing.assert_allclose(lg[top], z["tf_top_val"][t], atol=2e-3)
+        m = lg.max()
+        assert abs(float(m + np.log(np.exp(lg - m).sum())) - z["tf_lse"][t]) < 2e-3
+
+
+def test_tiny_en_generate_matches_transformers(tiny_golden, tiny_oracle):
+    """English-only generate(): prompt <|startoftranscript|> alone (no detection, no task), seek loop included."""
+    gen = GenerationSettings.default(TINY)
+    st = gen.special
+    g = wo.GenCfg(TINY.vocab, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate,
+                  st.notimestamps, gen.suppress_tokens, gen.begin_suppress_tokens, multilingual=False)
+    clips = _clips()
+    for i, name in enumerate(("speech30", "noise12")):
+        toks, _ = wo.generate(tiny_oracle, wo.log_mel(clips[name], TINY.n_mels), g, task=None, return_timestamps=True,
+                              max_new_tokens=48)
+        ref = [int(t) for t in tiny_golden["gen_sequences"][i]]
+        while ref and ref[-1] == st.eot:
+            ref.pop()
+        assert toks == ref, (name, toks, ref)

@@ -2,8 +2,9 @@
 //
 // (1) Encoder self-attention (non-causal, S = 1500, 64-wide heads): replaces WhisperAttention +
 //     eager/SDPA attention ($TF/models/whisper/modeling_whisper.py:215-238, 241-356) for the encoder.
-//     Flash-style (k_attn_enc4, the default: 64 queries per wave, 4 waves per workgroup; k_attn_enc2: 32 per wave,
-//     its register-staged predecessor, kept as the bit-identical cross-check and for the MX-fp8 output of config 5).
+//     Flash-style (k_attn_enc4, the default: 64 queries per wave, 4 waves per workgroup, LDS-DMA staging, bit-identical
+//     to k_attn_enc2; k_attn_enc5: enc4 with log2-unit scores and a guarded unshifted exp2, 10 % faster alone;
+//     k_attn_enc2: 32 per wave, register-staged, kept as the reference form and for the MX-fp8 output of config 5).
 //     The score tile is computed SWAPPED, S^T = K.Q^T with v_mfma_f32_32x32x16_bf16, so each lane holds
 //     16 keys of ONE query: the online-softmax max/sum is lane-local plus one xor-32 shuffle. The f32
 //     accumulator is then converted pairwise to bf16 and used in place as the B operand of O^T = V^T.P^T
@@ -20,6 +21,7 @@
 
 #define EA_KT 64           // keys per tile
 #define EA_LOG2E 1.4426950408889634f
+#define EA_GUARD 64.f   // k_attn_enc5: |s - c| bound (log2 units) before the stabiliser c moves
 
 // ------------------------------------------------------------------------------------------------
 // k_attn_enc2: 32 queries per wave, register-staged K/V tiles
@@ -408,11 +410,234 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc4(const bf16_t* __rest
     }
   }
 }
-// Encoder attention kernel: 16 = k_attn_enc4<4 waves, 2 workgroups per CU> (the default), 8 = k_attn_enc2<8, 2> (the
-// bit-identical cross-check). Measured alone (scripts/attn_bench.py, 24 windows x 20 heads, MI355X r03): 16: 778,
-// 8: ~650 TF/s; beside a decode with 4 x 16 KiB of LDS padding 16: ~590 TF/s. Round-2/3 alternatives (k_attn_enc3's
-// MFMA row sums and packed exp, 12-wave workgroups, k_attn_enc4 at 8 waves) measured slower in situ and are archived
-// under scripts/exp/archive.
+// ------------------------------------------------------------------------------------------------
+// k_attn_enc5 (variant 32, the faster alternative): k_attn_enc2's per-lane algorithm (swapped S^T = K.Q^T on v_mfma_f32_32x32x16_bf16,
+// lane-local softmax, P^T straight from the accumulators into the PV MFMA, V^T by ds_read_b64_tr_b16) with 64 queries
+// per wave (every K fragment read from LDS feeds 4 MFMAs, every V^T fragment 4: half enc2's LDS read traffic per
+// MFMA) and K/V tiles staged by LDS-DMA (global_load_lds_dwordx4, the bank swizzles applied on the SOURCE chunk and
+// undone on the read address; one barrier per tile, the DMA of tile t+1 in flight under tile t's MFMAs). Its
+// softmax has a fifth less VALU per tile than enc2's and no running-max bookkeeping. At head_dim 64 the
+// softmax's vector issue (per wave and 64-key tile: 64 v_exp_f32 at 8 cycles, 64 exponent FMAs, 32 v_max3, 64 sum
+// adds, 32 bf16 packs = ~1280 cycles) exceeds the tile's 32 MFMAs (1024 cycles of matrix pipe): the kernel is bound
+// by vector issue, not by the matrix cores. enc5 drops the exponent FMAs:
+//   * scores in log2 units: Q is multiplied by log2(e) as its fragments are loaded (one more bf16 rounding of q);
+//   * no max subtraction while it is not needed: softmax is shift-invariant and f32 / bf16 keep 8 exponent bits, so
+//     p = exp2(s - c) with ANY per-query stabiliser c gives the same O / l as long as s - c stays far from the
+//     exponent range's ends. c = 0 (p = exp2(s), one v_exp_f32) unless the first tile's max is beyond +-64, and it
+//     is raised (O, l rescaled by exp2(c - c')) only when a later tile's max exceeds c + 64. The v_max3 chains of
+//     enc2/enc4 stay as that guard; on real and random attention inputs the guarded path never triggers, so there is
+//     no per-tile O rescale either (enc2 rescales whenever a query's max grows).
+// ------------------------------------------------------------------------------------------------
+template <int NW, int WPS>
+__global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc5(const bf16_t* __restrict__ qkv, int S, int H, int D,
+                                                          int nqb, int nwork, bf16_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) bf16_t kvbuf[4 * EA_KT * 64];  // [K0 | K1 | V0 | V1]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int orig = blockIdx.x;
+  const int q8 = nwork / 8, r8 = nwork % 8, xcd = orig % 8;
+  const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int qb = work % nqb, bh = work / nqb;
+  const int h = bh % H, b = bh / H;
+  const int ld = 3 * D;
+  const bf16_t* base = qkv + (size_t)b * S * ld + h * 64;
+  const int q0 = qb * (NW * 64) + wid * 64;
+
+  bf16x8 qf[2][4];  // log2(e) * Q, query block t: lane holds Q[q0 + 32 t + lr][16 s + 8 lh + j]
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const bf16_t* qp = base + (size_t)min(q0 + 32 * t + lr, S - 1) * ld + 8 * lh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 raw = *(const bf16x8*)(qp + 16 * s);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[t][s][j] = (__bf16)((float)raw[j] * EA_LOG2E);
+    }
+  }
+  constexpr int IPW = 8 / NW;
+  const bf16_t* gk[IPW];
+  const bf16_t* gv[IPW];
+  int krow[IPW];
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int row = 8 * (wid * IPW + i) + (lane >> 3);
+    const int sl = lane & 7;
+    krow[i] = row;
+    gk[i] = base + D + ((sl ^ ((row >> 1) & 7)) << 3);
+    gv[i] = base + 2 * D + ((sl ^ (((row >> 1) & 1) << 2)) << 3);
+  }
+  auto stage = [&](int buf, int k0) {
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const size_t roff = (size_t)min(k0 + krow[i], S - 1) * ld;
+      const int lb = 8 * (wid * IPW + i) * 64;
+      __builtin_amdgcn_global_load_lds((const void*)(gk[i] + roff), (lds_void_t*)(kvbuf + buf * EA_KT * 64 + lb), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(gv[i] + roff), (lds_void_t*)(kvbuf + (2 + buf) * EA_KT * 64 + lb), 16, 0, 0);
+    }
+  };
+
+  f32x16 o[2][2];
+  float c_run[2] = {0.f, 0.f}, l_sum[2] = {0.f, 0.f};  // per-query stabiliser c (log2 units) and sum of exp2(s - c)
+  int sub = 0;  // wave-uniform: some query of the wave has c != 0
+#pragma unroll
+  for (int t = 0; t < 2; ++t) o[t][0] = o[t][1] = (f32x16){0};
+  const int nfull = S / EA_KT, ntile = (S + EA_KT - 1) / EA_KT;
+  const int gq = (lane & 15) >> 2, gp = lane & 3, gd = ((lane >> 4) & 1) * 16;
+  auto tile = [&](int cur, int k0, auto MASKED, auto FIRST) {
+    constexpr bool masked = decltype(MASKED)::value;
+    constexpr bool first = decltype(FIRST)::value;
+    const bf16_t* ks = kvbuf + cur * EA_KT * 64;
+    const bf16_t* vs = kvbuf + (2 + cur) * EA_KT * 64;
+    f32x16 sc[2][2];  // [key half][query block]
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 ka = *(const bf16x8*)(ks + k2_off(lr, 2 * s + lh));
+      const bf16x8 kb = *(const bf16x8*)(ks + k2_off(32 + lr, 2 * s + lh));
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (s == 0) {
+          sc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[t][s], (f32x16){}, 0, 0, 0);
+          sc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[t][s], (f32x16){}, 0, 0, 0);
+        } else {
+          sc[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[t][s], sc[0][t], 0, 0, 0);
+          sc[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[t][s], sc[1][t], 0, 0, 0);
+        }
+      }
+    }
+    if constexpr (masked) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = (r & 3) + 8 * (r >> 2) + 4 * lh;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          if (k0 + key >= S) sc[0][t][r] = -INFINITY;
+          if (k0 + 32 + key >= S) sc[1][t][r] = -INFINITY;
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float tc[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float x = fmaxf(fmaxf(sc[0][t][4 * c], sc[0][t][4 * c + 1]), sc[0][t][4 * c + 2]);
+        x = fmaxf(fmaxf(x, sc[0][t][4 * c + 3]), sc[1][t][4 * c]);
+        x = fmaxf(fmaxf(x, sc[1][t][4 * c + 1]), sc[1][t][4 * c + 2]);
+        tc[c] = fmaxf(x, sc[1][t][4 * c + 3]);
+      }
+      float tmax = fmaxf(fmaxf(tc[0], tc[1]), fmaxf(tc[2], tc[3]));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      if constexpr (first) {  // (finite: the first tile holds key 0 of every query)
+        c_run[t] = fabsf(tmax) > EA_GUARD ? tmax : 0.f;
+        sub |= __builtin_amdgcn_readfirstlane(__ballot(c_run[t] != 0.f) != 0ull ? 1 : 0);
+      } else if (__builtin_amdgcn_readfirstlane(__ballot(tmax - c_run[t] > EA_GUARD) != 0ull ? 1 : 0)) {
+        const float g = tmax - c_run[t] > EA_GUARD ? tmax - c_run[t] : 0.f;
+        const float alpha = __builtin_amdgcn_exp2f(-g);
+        c_run[t] += g;
+        l_sum[t] *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          o[t][0][r] *= alpha;
+          o[t][1][r] *= alpha;
+        }
+        sub = 1;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (sub) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          sc[0][t][r] = __builtin_amdgcn_exp2f(sc[0][t][r] - c_run[t]);
+          sc[1][t][r] = __builtin_amdgcn_exp2f(sc[1][t][r] - c_run[t]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          sc[0][t][r] = __builtin_amdgcn_exp2f(sc[0][t][r]);
+          sc[1][t][r] = __builtin_amdgcn_exp2f(sc[1][t][r]);
+        }
+      }
+      float ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ps += sc[0][t][r] + sc[1][t][r];
+      ps += __shfl_xor(ps, 32, 64);
+      l_sum[t] += ps;
+    }
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pb[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[t][j] = (__bf16)sc[kh][t][8 * s + j];
+        const int kb = kh * 32 + 16 * s + 4 * lh + gq;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const int d = db * 32 + gd + 4 * gp;
+          const int ch = d >> 3, wi = d & 7;
+          const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4_t*)(vs + v2_off(kb, ch) + wi));
+          const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4_t*)(vs + v2_off(kb + 8, ch) + wi));
+          const bf16x8 va = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int t = 0; t < 2; ++t) o[t][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb[t], o[t][db], 0, 0, 0);
+        }
+      }
+    }
+  };
+  using BT = std::integral_constant<bool, true>;
+  using BF = std::integral_constant<bool, false>;
+  stage(0, 0);
+  __syncthreads();
+  if (ntile == 1) {
+    tile(0, 0, BT{}, BT{});
+  } else {
+    stage(1, EA_KT);
+    tile(0, 0, BF{}, BT{});  // ntile > 1: tile 0 is full
+    __syncthreads();
+    for (int kt = 1; kt < nfull; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < ntile) stage(cur ^ 1, (kt + 1) * EA_KT);
+      tile(cur, kt * EA_KT, BF{}, BF{});
+      __syncthreads();
+    }
+    if (nfull < ntile) tile(nfull & 1, nfull * EA_KT, BT{}, BF{});
+  }
+
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int q = q0 + 32 * t + lr;
+    if (q < S) {
+      const float inv = 1.f / l_sum[t];
+      bf16_t* op = out + ((size_t)b * S + q) * D + h * 64;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 8 * g + 4 * lh;
+        uint2 w0, w1;
+        w0.x = pack_bf16x2(o[t][0][4 * g] * inv, o[t][0][4 * g + 1] * inv);
+        w0.y = pack_bf16x2(o[t][0][4 * g + 2] * inv, o[t][0][4 * g + 3] * inv);
+        w1.x = pack_bf16x2(o[t][1][4 * g] * inv, o[t][1][4 * g + 1] * inv);
+        w1.y = pack_bf16x2(o[t][1][4 * g + 2] * inv, o[t][1][4 * g + 3] * inv);
+        tw_st_enc<TW_NT_ATTN>(op + d, w0);
+        tw_st_enc<TW_NT_ATTN>(op + 32 + d, w1);
+      }
+    }
+  }
+}
+
+// Encoder attention kernel: 16 = k_attn_enc4<4 waves, 2 workgroups per CU> (the default: bit-identical to enc2, so the
+// engine reproduces the arithmetic its exact-match goldens were pinned with), 32 = k_attn_enc5<4, 2> (a fifth less
+// softmax VALU; its extra roundings of q * log2 e and of the unshifted p flip a near-tie in the beam-5 pipeline golden,
+// one end timestamp of an empty segment, tests/test_gpu_beam.py), 8 = k_attn_enc2<8, 2> (the running-max reference
+// form, also the MX-fp8-output kernel of config 5). Measured alone (scripts/attn_bench.py, 24 windows x 20 heads,
+// MI355X r03): 16: 761-778, 32: 838-840, 8: 695 TF/s; with the 4 x 16 KiB LDS cap used beside a decode 16: 576-590,
+// 32: 603-610, 8: 536. In the bench step (scripts/exp/ab_attn_bench.py, three interleaved rounds) 16 and 32 are equal
+// (91.16 vs 91.05 ms): the overlapped step is bound by the decode beside it. PMC (scripts/exp/pmc_attn.sh): with the
+// cap a third of the attention's wave cycles are parked in s_waitcnt / s_barrier and a sixth stall on issue
+// dependencies; the software-pipelined enc6 (archived) did not move either. Other round-2/3 alternatives (enc3's MFMA
+// row sums and packed exp, 12-wave workgroups) are archived under scripts/exp/archive.
 static int tw_attn_variant = 16;
 // Extra (unused) LDS reserved per encoder-attention workgroup, in 16 KiB units: caps the attention's workgroups per CU
 // so that decoder waves queued beside it (run_batches' overlap) find free wave slots on every CU.
@@ -426,7 +651,8 @@ extern "C" int tw_attn_set_lds_pad(int units) {
   return 0;
 }
 extern "C" int tw_attn_set_variant(int v) {
-  TW_REQUIRE(v == 8 || v == 16, "tw_attn_set_variant: %d (8 = k_attn_enc2, 16 = k_attn_enc4)", v);
+  TW_REQUIRE(v == 8 || v == 16 || v == 32, "tw_attn_set_variant: %d (8 = k_attn_enc2, 16 = k_attn_enc4, 32 = k_attn_enc5)",
+             v);
   tw_attn_variant = v;
   return 0;
 }
@@ -437,7 +663,9 @@ extern "C" int tw_attn_encoder(const bf16_t* qkv, int B, int S, int H, bf16_t* o
   hipStream_t st = (hipStream_t)stream;
   const size_t pad = (size_t)tw_attn_lds_pad * 16384;
   const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;  // both: 256 queries per workgroup
-  if (tw_attn_variant == 16)
+  if (tw_attn_variant == 32)
+    hipLaunchKernelGGL((k_attn_enc5<4, 2>), dim3(nwork), dim3(256), pad, st, qkv, S, H, D, nqb, nwork, out);
+  else if (tw_attn_variant == 16)
     hipLaunchKernelGGL((k_attn_enc4<4, 2>), dim3(nwork), dim3(256), pad, st, qkv, S, H, D, nqb, nwork, out);
   else
     hipLaunchKernelGGL((k_attn_enc2<8, 2>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, out);
