@@ -44,6 +44,8 @@ extern "C" {
 #define TW_ST_LASTTS 3   /* last generated timestamp token id, -1 if none                       */
 #define TW_ST_FINISHED 4 /* 1 once EOS was produced or max length reached                       */
 #define TW_ST_LANG 5     /* language id chosen by mode-1 selection                              */
+#define TW_ST_SUMLP 6    /* f32 bits: sum of the chosen tokens' log-probabilities (tw_logits_sample) */
+#define TW_ST_NOSPEECH 7 /* f32 bits: no-speech probability (tw_token_prob)                      */
 
 /* tw_logits_select workspace: f32[B][TW_SELECT_WS_PER_ROW] (TW_SELECT_CHUNKS vocab chunks per row). */
 #define TW_SELECT_CHUNKS 16
@@ -271,6 +273,21 @@ int tw_logits_select_embed(const float* logits, int B, int ld_logits, const uint
                            int* pos, float* workspace, const uint16_t* tok_emb, const uint16_t* pos_emb, int D,
                            int max_pos, float* x, const float* gamma, const float* beta, float eps, uint16_t* out,
                            int packed, void* stream);
+
+/* Temperature-fallback decode step (WhisperGenerationMixin.generate_with_fallback,
+ * $TF/models/whisper/generation_whisper.py:970-1116), one workgroup per row, same arguments as tw_logits_select minus
+ * the workspace. temperature == 0: the greedy token, bit-identical to tw_logits_select. temperature > 0 (do_sample):
+ * TemperatureLogitsWarper + TopKLogitsWarper(top_k; <= 0 = off; ties at the k-th value kept) and a draw from the
+ * softmax of the kept scores by the Gumbel-max trick with a counter-based hash of (seed, row_key[b] (NULL: b), token
+ * index in the pass, vocabulary id): the distribution of _sample's torch.multinomial, not its random stream.
+ * Every row unfinished before the step adds log_softmax(scores)[token] (the scores generate() returns with
+ * output_scores, at temperature 1: _retrieve_avg_logprobs, :1958-1975) to state[TW_ST_SUMLP] (f32 bits). */
+int tw_logits_sample(const float* logits, int B, int ld_logits, const uint32_t* suppress_bits,
+                     const TwSelectParams* params, float temperature, int top_k, uint64_t seed, const int* row_key,
+                     int* state, int* tokens_out, int ld_tokens, int* next_ids, int* pos, void* stream);
+/* state[b][TW_ST_NOSPEECH] (f32 bits) = softmax(logits[b][0:V])[token]: WhisperNoSpeechDetection's no_speech_prob
+ * ($TF/generation/logits_process.py:2050-2112) from the logits at the <|startoftranscript|> position. */
+int tw_token_prob(const float* logits, int B, int ld_logits, int V, int token, int* state, void* stream);
 
 #ifdef __cplusplus
 }

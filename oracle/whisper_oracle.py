@@ -689,6 +689,38 @@ def generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, task: Optional[
     return out, lang
 
 
+def pass_criteria(model: WhisperOracle, feats: np.ndarray, g: GenCfg, prompt: Sequence[int], toks: Sequence[int],
+                  seek: int = 0, use_ts: bool = True):
+    """The temperature-fallback criteria of one greedy seek pass (generation_whisper.py:1243-1287) in fp32:
+    (compression ratio of toks — _retrieve_compression_ratio, :1949-1956 —, average of log_softmax(processed
+    scores)[token] over toks — _retrieve_avg_logprobs, :1958-1975 —, and WhisperNoSpeechDetection's softmax of the raw
+    logits at the <|startoftranscript|> position at no_timestamps - 1 — logits_process.py:2091-2112). toks: the
+    pass's generated tokens, EOS included, pads not (generate_with_fallback's cut, :1058-1066)."""
+    import math
+    import zlib
+
+    length = int(math.log2(g.V) / 8) + 1
+    raw = b"".join(int(t).to_bytes(length, "little") for t in toks)
+    cr = len(raw) / len(zlib.compress(raw))
+    feats = np.asarray(feats, np.float32)
+    seg = np.zeros_like(feats)
+    seg[:, : 3000 - seek] = feats[:, seek:]
+    cache = model.new_cache(model.encode(seg))
+    ids = list(prompt) + list(toks)
+    lp, nsp = 0.0, None
+    for t in range(len(ids) - 1):
+        lg = model.decoder_step(int(ids[t]), cache)
+        if t == 0:
+            nsp = float(_softmax(lg.astype(np.float32))[g.notimestamps - 1])
+        k = t - (len(prompt) - 1)
+        if k >= 0:
+            sc = process_logits(lg, list(toks[:k]), g, use_ts)
+            fin = sc[np.isfinite(sc)]
+            m = float(fin.max())
+            lp += float(sc[int(toks[k])]) - (m + float(np.log(np.exp(fin - m).sum())))
+    return cr, lp / max(1, len(toks)), nsp
+
+
 def generate_batch_word(model: WhisperOracle, feats_list: Sequence[np.ndarray], g: GenCfg, alignment_heads,
                         num_frames: Sequence[int], task: Optional[str] = "transcribe", language: Optional[int] = None,
                         max_new_tokens: Optional[int] = None, median_width: int = 7, forced=None):

@@ -12,6 +12,8 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
   word.npz/.json    token-level timestamps (cross-attention DTW) of generate(return_token_timestamps=True) and
                     the pipeline's return_timestamps="word" output, plus HF's _median_filter / _dynamic_time_warping
                     on seeded random matrices
+  fallback.json     the temperature-fallback criteria (compression ratio, avg logprob, no-speech probability) of
+                    every seek pass and a deterministic no-speech skip, spied from transformers' generate()
   tiny.npz          whisper-tiny.en (configs[0], English-only) encoder rows, teacher-forced logits, generate() passes
                     with their processed top-16 scores
   beam.json         generate(num_beams=5) token sequences (the pipeline's default decode, asr:160-163) of
@@ -572,6 +574,61 @@ def make_tiny(out):
     res["tf_top_val"] = np.take_along_axis(lg, top, 1).astype(np.float32)
     res["tf_lse"] = (np.log(np.exp(lg - lg.max(1, keepdims=True)).sum(1)) + lg.max(1)).astype(np.float64)
     np.savez_compressed(os.path.join(out, "tiny.npz"), **res)
+
+
+FALLBACK_CLIPS = ("speech30", "noise12", "zeros30")
+FALLBACK_SKIP = {"temperature": [0.0], "compression_ratio_threshold": None, "logprob_threshold": -3.0,
+                 "no_speech_threshold": 3e-5}
+
+
+def make_fallback(out):
+    """generate()'s temperature-fallback criteria on test-mini (generation_whisper.py:970-1116, 1243-1287): every
+    _need_fallback call is spied on (its seek_sequence, transformers' own _retrieve_compression_ratio and
+    _retrieve_avg_logprobs on it, WhisperNoSpeechDetection's no_speech_prob, and the returned decision) in
+      "metrics": inert thresholds (nothing fires; every pass's criteria are recorded), temperature (0.0,);
+      "skip":    FALLBACK_SKIP (the silent window's first pass has avg logprob < -3 and no_speech_prob > 3e-5: it is
+                 skipped; the others keep their greedy tokens), temperature (0.0,) — a deterministic outcome,
+    with the final generate() sequences of both. Sampled retries (temperature > 0) draw from torch's random stream and
+    are not fixtures."""
+    from transformers import WhisperFeatureExtractor
+    from transformers.generation.logits_process import WhisperNoSpeechDetection
+    from transformers.models.whisper.generation_whisper import _get_attr_from_logit_processors
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    cl = clips()
+    feats = torch.from_numpy(np.stack([fe(cl[k], sampling_rate=16000, return_tensors="np")["input_features"][0]
+                                       for k in FALLBACK_CLIPS]))
+    res = {"seed": SEED, "dims": "test-mini", "clips": list(FALLBACK_CLIPS), "max_new_tokens": 40}
+    for name, kw in (("metrics", {"temperature": [0.0], "compression_ratio_threshold": 1e9, "logprob_threshold": -1e9,
+                                  "no_speech_threshold": 2.0}),
+                     ("skip", FALLBACK_SKIP)):
+        m = hf_model(d, sd, gen)
+        rec = []
+        orig = m._need_fallback
+
+        def spy(seek_sequence, seek_outputs, index, logits_processor, generation_config, vocab_size, temperature,
+                _m=m, _orig=orig, _rec=rec):
+            cr = _m._retrieve_compression_ratio(seek_sequence, vocab_size)
+            lp = _m._retrieve_avg_logprobs(seek_outputs[index]["scores"], seek_sequence, temperature)
+            nsp = _get_attr_from_logit_processors(logits_processor, WhisperNoSpeechDetection, "no_speech_prob")
+            o = _orig(seek_sequence, seek_outputs, index, logits_processor, generation_config, vocab_size, temperature)
+            _rec.append({"index": int(index), "tokens": [int(t) for t in seek_sequence.tolist()],
+                         "compression_ratio": float(cr), "avg_logprob": float(lp),
+                         "no_speech_prob": None if nsp is None else float(nsp[index]),
+                         "needs_fallback": bool(o[0]), "should_skip": bool(o[1])})
+            return o
+
+        m._need_fallback = spy
+        with torch.no_grad():
+            o = m.generate(feats, task="transcribe", return_timestamps=True, max_new_tokens=40, return_segments=True,
+                           temperature=tuple(kw["temperature"]),
+                           **{k: v for k, v in kw.items() if k != "temperature" and v is not None})
+        res[name] = {"kwargs": kw, "calls": rec, "sequences": o["sequences"].tolist()}
+    with open(os.path.join(out, "fallback.json"), "w") as f:
+        json.dump(res, f)
 
 
 def _jsonable(x):

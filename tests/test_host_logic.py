@@ -175,3 +175,36 @@ def test_pipeline_word_timestamps_host_flow_matches_transformers():
         r = tr(x[: case["n_samples"]], generate_kwargs={"task": "transcribe", "num_beams": 1, "max_new_tokens": 40},
                return_timestamps="word", **case["kwargs"])
         assert json.loads(json.dumps(r)) == case["output"], case["name"]
+
+
+# ---- temperature fallback criteria (generation_whisper.py:1243-1287) vs transformers' own values --------------------
+def _fallback_golden():
+    import json
+
+    return json.load(open(os.path.join(os.path.dirname(__file__), "golden", "fallback.json")))
+
+
+def test_fallback_compression_ratio_and_decisions_match_transformers():
+    """twamd.segments: _retrieve_compression_ratio exactly, and _need_fallback's decisions (incl. the no-speech skip)
+    from transformers' own criteria values, for every seek pass of the spied generate() runs."""
+    from twamd.segments import FallbackConfig, compression_ratio, need_fallback
+
+    z = _fallback_golden()
+    for name in ("metrics", "skip"):
+        kw = z[name]["kwargs"]
+        cfg = FallbackConfig(temperatures=tuple(kw["temperature"]),
+                             compression_ratio_threshold=kw["compression_ratio_threshold"],
+                             logprob_threshold=kw["logprob_threshold"], no_speech_threshold=kw["no_speech_threshold"])
+        for c in z[name]["calls"]:
+            assert compression_ratio(c["tokens"], 51866) == c["compression_ratio"]
+            got = need_fallback(c["tokens"], c["avg_logprob"] * len(c["tokens"]), c["no_speech_prob"], 51866, cfg)
+            assert got == (c["needs_fallback"], c["should_skip"]), (name, c["index"])
+
+
+def test_fallback_sequence_cut():
+    from twamd.segments import fallback_sequence
+
+    assert fallback_sequence([5, 6, 50257, 50257, 50257], 50257, 50257) == [5, 6, 50257]
+    assert fallback_sequence([5, 6, 7], 50257, 50257) == [5, 6, 7]
+    assert fallback_sequence([5, 6, 50257], 50257, 50257) == [5, 6, 50257]
+    assert fallback_sequence([5, 0, 0], 0, 50257) == [5]

@@ -174,3 +174,23 @@ def test_tiny_en_generate_matches_transformers(tiny_golden, tiny_oracle):
         while ref and ref[-1] == st.eot:
             ref.pop()
         assert toks == ref, (name, toks, ref)
+
+
+def test_fallback_criteria_match_transformers(oracle_model, gcfg):
+    """oracle.pass_criteria (compression ratio, avg logprob of the processed scores, no-speech probability) against
+    the values transformers' own _need_fallback saw on the first seek pass of every window (tests/golden/
+    fallback.json, make_golden.py fallback)."""
+    import json
+
+    z = json.load(open(os.path.join(G, "fallback.json")))
+    clips = _clips()
+    calls = z["metrics"]["calls"][:3]  # the first pass: all three windows, seek 0, batch index = window
+    for i, name in enumerate(z["clips"]):
+        c = calls[i]
+        assert c["index"] == i
+        feats = wo.log_mel(clips[name], 128)
+        lang = wo.detect_language(oracle_model, oracle_model.encode(feats), gcfg)
+        cr, lp, nsp = wo.pass_criteria(oracle_model, feats, gcfg, [gcfg.sot, lang, gcfg.transcribe], c["tokens"])
+        assert cr == c["compression_ratio"]
+        assert abs(lp - c["avg_logprob"]) < 1e-3, (name, lp, c["avg_logprob"])
+        assert abs(nsp - c["no_speech_prob"]) < 1e-3 * c["no_speech_prob"] + 1e-9, (name, nsp, c["no_speech_prob"])

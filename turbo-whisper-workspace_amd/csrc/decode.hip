@@ -60,18 +60,16 @@ __device__ inline RowMask row_mask(const int* st, const TwSelectParams& p) {
   return r;
 }
 
-// grid (B, TW_SELECT_CHUNKS): chunk c of row b scans vocab [c*V/NC, (c+1)*V/NC) with float4 loads where aligned.
-__global__ TW_DEC_LB(256, 1) void k_select_partial(const float* __restrict__ logits, int ld_logits,
-                                                        const uint32_t* __restrict__ suppress_bits, TwSelectParams p,
-                                                        const int* __restrict__ state, SelPart* __restrict__ ws) {
-  TW_DEC_PRIO();
-  __shared__ SelPart sp[4];
-  const int b = blockIdx.x, c = blockIdx.y, NC = gridDim.y;
+// One vocab chunk [v0, v1) of one row with a 256-thread block (4 waves): the processed (masked) logits' best text and
+// best timestamp candidates and the timestamp logsumexp state, reduced to one record in `out` (valid in thread 0).
+// TX: also accumulate (per thread, unreduced) the logsumexp state of the unmasked TEXT logits into m_tx / s_tx
+// (k_select_full's log_softmax denominator); off, the arithmetic is k_select_partial's exactly.
+template <bool TX>
+__device__ inline void sel_chunk(const float* __restrict__ row, const uint32_t* __restrict__ suppress_bits,
+                                 const TwSelectParams& p, const RowMask& rm, int v0, int v1, SelPart* sp,
+                                 SelPart& out, float& m_tx, float& s_tx) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const RowMask rm = row_mask(state + b * TW_STATE_STRIDE, p);
-  const float* row = logits + (size_t)b * ld_logits;
-  const int V = p.V, tsb = p.ts_begin;
-  const int v0 = (int)((long)c * V / NC), v1 = (int)((long)(c + 1) * V / NC);
+  const int tsb = p.ts_begin;
   Best bt{-INFINITY, 0x7fffffff}, bs{-INFINITY, 0x7fffffff};
   float m_ts = -INFINITY, s_ts = 0.f;
   // 4 loads in flight per thread; indices clamped into the chunk (duplicates are dropped by `ok`)
@@ -110,6 +108,7 @@ __global__ TW_DEC_LB(256, 1) void k_select_partial(const float* __restrict__ log
       if (!ok) continue;
       if (v < tsb || !p.use_timestamps || p.mode == 1) {
         bt = best_of(bt, Best{x, v});
+        if (TX && x != -INFINITY) lse_merge(m_tx, s_tx, x, 1.f);
       } else {
         bs = best_of(bs, Best{x, v});
         if (x != -INFINITY) lse_merge(m_ts, s_ts, x, 1.f);
@@ -133,19 +132,34 @@ __global__ TW_DEC_LB(256, 1) void k_select_partial(const float* __restrict__ log
       bs = best_of(bs, Best{sp[w].bs_v, sp[w].bs_i});
       lse_merge(m_ts, s_ts, sp[w].m_ts, sp[w].s_ts);
     }
-    ws[b * NC + c] = SelPart{bt.v, bt.i, bs.v, bs.i, m_ts, s_ts, 0.f, 0.f};
+    out = SelPart{bt.v, bt.i, bs.v, bs.i, m_ts, s_ts, 0.f, 0.f};
   }
 }
 
-// One wave per row: merge the row's chunk records (in chunk order: ties keep the first index), then the
-// selection rule of the timestamp processor, the pad-after-EOS / stopping rule of _sample, and the processor
-// state update. Lane 0 returns the token fed to the next step (tok) and the row's next position (npos).
-__device__ inline void select_final_row(const SelPart* __restrict__ ws, int NC, const TwSelectParams& p,
-                                        int* __restrict__ state, int* __restrict__ tokens_out, int ld_tokens,
-                                        int* __restrict__ next_ids, int* __restrict__ pos, int b, int lane,
-                                        int& tok_out, int& npos) {
-  Best bt{-INFINITY, 0x7fffffff}, bs{-INFINITY, 0x7fffffff};
-  float m_ts = -INFINITY, s_ts = 0.f;
+// grid (B, TW_SELECT_CHUNKS): chunk c of row b scans vocab [c*V/NC, (c+1)*V/NC) with float4 loads where aligned.
+__global__ TW_DEC_LB(256, 1) void k_select_partial(const float* __restrict__ logits, int ld_logits,
+                                                        const uint32_t* __restrict__ suppress_bits, TwSelectParams p,
+                                                        const int* __restrict__ state, SelPart* __restrict__ ws) {
+  TW_DEC_PRIO();
+  __shared__ SelPart sp[4];
+  const int b = blockIdx.x, c = blockIdx.y, NC = gridDim.y;
+  const RowMask rm = row_mask(state + b * TW_STATE_STRIDE, p);
+  const int V = p.V;
+  const int v0 = (int)((long)c * V / NC), v1 = (int)((long)(c + 1) * V / NC);
+  SelPart out;
+  float m_tx = -INFINITY, s_tx = 0.f;
+  sel_chunk<false>(logits + (size_t)b * ld_logits, suppress_bits, p, rm, v0, v1, sp, out, m_tx, s_tx);
+  if (threadIdx.x == 0) ws[b * NC + c] = out;
+}
+
+// Merge of a row's chunk records (in chunk order: ties keep the first index): every lane ends with the row's best
+// text / best timestamp candidates and its timestamp logsumexp state.
+__device__ inline void sel_merge(const SelPart* __restrict__ ws, int NC, int b, int lane, Best& bt, Best& bs,
+                                 float& m_ts, float& s_ts) {
+  bt = Best{-INFINITY, 0x7fffffff};
+  bs = Best{-INFINITY, 0x7fffffff};
+  m_ts = -INFINITY;
+  s_ts = 0.f;
   for (int c = lane; c < NC; c += 64) {
     const SelPart r = ws[b * NC + c];
     bt = best_of(bt, Best{r.bt_v, r.bt_i});
@@ -161,27 +175,23 @@ __device__ inline void select_final_row(const SelPart* __restrict__ ws, int NC, 
     float m2 = __shfl_xor(m_ts, o, 64), s2 = __shfl_xor(s_ts, o, 64);
     lse_merge(m_ts, s_ts, m2, s2);
   }
-  if (lane != 0) return;
-  int* st = state + b * TW_STATE_STRIDE;
+}
+// The timestamp processor's rule ("if sum of probability over timestamps is above any other token, sample timestamp":
+// the text logits are masked when the timestamps' logsumexp beats the best text logit) and the greedy choice.
+__device__ inline bool sel_rule_fires(const TwSelectParams& p, Best bt, float m_ts, float s_ts) {
+  if (!p.use_timestamps) return false;
+  const float lse_ts = (m_ts == -INFINITY) ? -INFINITY : m_ts + __logf(s_ts);
+  return lse_ts > bt.v;
+}
+__device__ inline int sel_greedy(const TwSelectParams& p, Best bt, Best bs, float m_ts, float s_ts) {
+  if (!p.use_timestamps) return bt.i;
+  return sel_rule_fires(p, bt, m_ts, s_ts) ? bs.i : best_of(bt, bs).i;
+}
+// _sample's pad-after-EOS / stopping rule and the processor state update for the chosen `sel`; returns the token fed
+// to the next step.
+__device__ inline int sel_commit(const TwSelectParams& p, int* __restrict__ st, int sel, int* __restrict__ tokens_out,
+                                 int ld_tokens, int* __restrict__ next_ids, int b) {
   const int n_gen = st[TW_ST_NGEN], last = st[TW_ST_LAST];
-  npos = 0;
-  if (pos) npos = pos[b] += 1;  // the next decoder step writes its K/V one position later
-  int sel;
-  if (p.mode == 1) {
-    sel = bt.i;
-    st[TW_ST_LANG] = sel;
-    if (next_ids) next_ids[b] = sel;
-    tok_out = sel;
-    return;
-  }
-  if (p.use_timestamps) {
-    // "if sum of probability over timestamps is above any other token, sample timestamp"
-    const float lse_ts = (m_ts == -INFINITY) ? -INFINITY : m_ts + __logf(s_ts);
-    if (lse_ts > bt.v) sel = bs.i;
-    else sel = best_of(bt, bs).i;
-  } else {
-    sel = bt.i;
-  }
   const int finished = st[TW_ST_FINISHED];
   const int tok = finished ? p.pad : sel;
   if (tokens_out) tokens_out[(size_t)b * ld_tokens + n_gen] = tok;
@@ -191,7 +201,31 @@ __device__ inline void select_final_row(const SelPart* __restrict__ ws, int NC, 
   if (tok >= p.ts_begin && p.use_timestamps) st[TW_ST_LASTTS] = tok;
   st[TW_ST_NGEN] = n_gen + 1;
   if (!finished && (tok == p.eos || n_gen + 1 >= p.max_new)) st[TW_ST_FINISHED] = 1;
-  tok_out = tok;
+  return tok;
+}
+
+// One wave per row: merge the row's chunk records, then the selection rule of the timestamp processor, the
+// pad-after-EOS / stopping rule of _sample, and the processor state update. Lane 0 returns the token fed to the next
+// step (tok) and the row's next position (npos).
+__device__ inline void select_final_row(const SelPart* __restrict__ ws, int NC, const TwSelectParams& p,
+                                        int* __restrict__ state, int* __restrict__ tokens_out, int ld_tokens,
+                                        int* __restrict__ next_ids, int* __restrict__ pos, int b, int lane,
+                                        int& tok_out, int& npos) {
+  Best bt, bs;
+  float m_ts, s_ts;
+  sel_merge(ws, NC, b, lane, bt, bs, m_ts, s_ts);
+  if (lane != 0) return;
+  int* st = state + b * TW_STATE_STRIDE;
+  npos = 0;
+  if (pos) npos = pos[b] += 1;  // the next decoder step writes its K/V one position later
+  if (p.mode == 1) {
+    const int sel = bt.i;
+    st[TW_ST_LANG] = sel;
+    if (next_ids) next_ids[b] = sel;
+    tok_out = sel;
+    return;
+  }
+  tok_out = sel_commit(p, st, sel_greedy(p, bt, bs, m_ts, s_ts), tokens_out, ld_tokens, next_ids, b);
 }
 
 // grid B, one wave per row
@@ -294,6 +328,215 @@ extern "C" int tw_logits_select_embed(const float* logits, int B, int ld_logits,
     hipLaunchKernelGGL(k_select_final_embed<false>, dim3(B), dim3(256), 0, s, ws, TW_SELECT_CHUNKS, *params, state,
                        tokens_out, ld_tokens, next_ids, pos, tok_emb, pos_emb, D, max_pos, x, gamma, beta, eps, out);
   return tw_check_launch("tw_logits_select_embed");
+}
+
+// =================================================================================================
+// Temperature fallback (WhisperGenerationMixin.generate_with_fallback, $TF/models/whisper/generation_whisper.py:
+// 970-1116): one workgroup per row does the whole selection of a decode step, because the fallback criteria need the
+// step's log-probability and sampling needs the row's top-k.
+//   * the processors and the chosen greedy token are tw_logits_select's, bit for bit: the row is scanned as the same
+//     TW_SELECT_CHUNKS chunks with the same per-thread mapping (sel_chunk) and merged in the same order (sel_merge);
+//   * temperature > 0 (do_sample): TemperatureLogitsWarper then TopKLogitsWarper (GenerationConfig's default top_k 50,
+//     ties at the k-th value kept: logits_process.py TopKLogitsWarper) and a draw from the softmax of what is left
+//     ($TF/generation/utils.py _sample: multinomial) by the Gumbel-max trick — argmax of s/T + G, G = -log(-log U) with
+//     U from a counter-based hash of (seed, row key, token index in the pass, vocabulary id): the same distribution as
+//     torch.multinomial, not its random stream (sampled tokens are therefore not comparable token for token);
+//   * the log-probability of the chosen token under the step's scores as generate() returns them (output_scores: the
+//     processed scores, after the warpers when sampling) at temperature 1 — _retrieve_avg_logprobs
+//     (generation_whisper.py:1958-1975) — is added to the row's state slot TW_ST_SUMLP (f32 bits) while the row is
+//     unfinished (EOS included, pads not).
+// =================================================================================================
+__device__ inline uint64_t tw_mix64(uint64_t z) {  // splitmix64 finaliser
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__device__ inline float tw_gumbel(uint64_t seed, uint32_t key, uint32_t step, uint32_t v) {
+  const uint64_t h = tw_mix64(seed ^ tw_mix64(((uint64_t)key << 32) ^ ((uint64_t)step << 20) ^ (uint64_t)v));
+  const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1), 24 bits
+  return -logf(-logf(u));
+}
+// the processed value of vocabulary entry v (the masks of sel_chunk, mode 0)
+__device__ inline float sel_processed(const float* __restrict__ row, const uint32_t* __restrict__ suppress_bits,
+                                      const TwSelectParams& p, const RowMask& rm, int v) {
+  const int tsb = p.ts_begin;
+  bool masked = suppress_bits ? (suppress_bits[v >> 5] >> (v & 31)) & 1u : false;
+  if (rm.init_step)
+    for (int i = 0; i < p.n_begin_suppress; ++i) masked |= (v == p.begin_suppress[i]);
+  if (p.use_timestamps) {
+    masked |= (v == p.no_timestamps);
+    if (v >= tsb) {
+      masked |= rm.mask_ts_all || (v < rm.ts_hi_block);
+      if (rm.init_step && p.max_initial_ts >= 0) masked |= (v > tsb + p.max_initial_ts);
+    } else {
+      masked |= (rm.mask_text_lt_eos && v < p.eos) || rm.init_step;
+    }
+  }
+  return masked ? -INFINITY : row[v];
+}
+__device__ inline float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+__device__ inline void block_lse256(float& m, float& s, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lse_merge(m, s, __shfl_xor(m, o, 64), __shfl_xor(s, o, 64));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    red[2 * (threadIdx.x >> 6)] = m;
+    red[2 * (threadIdx.x >> 6) + 1] = s;
+  }
+  __syncthreads();
+  m = red[0];
+  s = red[1];
+  for (int w = 1; w < 4; ++w) lse_merge(m, s, red[2 * w], red[2 * w + 1]);
+}
+
+// grid B, 256 threads (mode 0)
+__global__ __launch_bounds__(256) void k_select_full(const float* __restrict__ logits, int ld_logits,
+                                                     const uint32_t* __restrict__ suppress_bits, TwSelectParams p,
+                                                     float temperature, int top_k, uint64_t seed,
+                                                     const int* __restrict__ row_key, int* __restrict__ state,
+                                                     int* __restrict__ tokens_out, int ld_tokens,
+                                                     int* __restrict__ next_ids, int* __restrict__ pos) {
+  __shared__ SelPart sp[4];
+  __shared__ SelPart parts[TW_SELECT_CHUNKS];
+  __shared__ float red[8];
+  __shared__ uint32_t hist[256];
+  __shared__ int bcast[4];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  int* st = state + b * TW_STATE_STRIDE;
+  const RowMask rm = row_mask(st, p);
+  const float* row = logits + (size_t)b * ld_logits;
+  const int V = p.V, NC = TW_SELECT_CHUNKS, tsb = p.ts_begin;
+  float m_tx = -INFINITY, s_tx = 0.f;
+  for (int c = 0; c < NC; ++c) {
+    SelPart out;
+    sel_chunk<true>(row, suppress_bits, p, rm, (int)((long)c * V / NC), (int)((long)(c + 1) * V / NC), sp, out, m_tx,
+                    s_tx);
+    if (tid == 0) parts[c] = out;
+    __syncthreads();
+  }
+  block_lse256(m_tx, s_tx, red);  // every thread: the unmasked text logits' logsumexp state
+  Best bt, bs;
+  float m_ts, s_ts;
+  sel_merge(parts, NC, 0, lane, bt, bs, m_ts, s_ts);  // (every wave merges the same records: identical results)
+  const bool fire = sel_rule_fires(p, bt, m_ts, s_ts);
+  int sel;
+  float lse;  // log_softmax denominator of the scores generate() reports for this step
+  if (temperature <= 0.f) {
+    sel = sel_greedy(p, bt, bs, m_ts, s_ts);
+    float m = fire ? -INFINITY : m_tx, sm = fire ? 0.f : s_tx;
+    if (p.use_timestamps) lse_merge(m, sm, m_ts, s_ts);
+    lse = m + __logf(sm);
+  } else {
+    // eligible: unmasked after the processors (the rule masks every text logit when it fires)
+    const float invT = 1.f / temperature;
+    auto elig = [&](int v, float x) { return x != -INFINITY && !(fire && v < tsb); };
+    // k-th largest eligible key (f32_order_key of the value: order-preserving), MSB-first radix select
+    uint32_t prefix = 0u, mask = 0u;
+    int n_el = 0;
+    for (int v = tid; v < V; v += 256) n_el += elig(v, sel_processed(row, suppress_bits, p, rm, v)) ? 1 : 0;
+    n_el = (int)block_sum256((float)n_el, red);
+    const bool restrict_k = top_k > 0 && n_el > top_k;
+    if (restrict_k) {
+      int k_rem = top_k;
+      for (int shift = 24; shift >= 0; shift -= 8) {
+        hist[tid] = 0u;
+        __syncthreads();
+        for (int v = tid; v < V; v += 256) {
+          const float x = sel_processed(row, suppress_bits, p, rm, v);
+          if (!elig(v, x)) continue;
+          const uint32_t key = f32_order_key(x);
+          if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (tid == 0) {
+          int cum = 0, d = 255;
+          for (; d > 0; --d) {
+            if (cum + (int)hist[d] >= k_rem) break;
+            cum += (int)hist[d];
+          }
+          bcast[0] = d;
+          bcast[1] = k_rem - cum;
+        }
+        __syncthreads();
+        prefix |= (uint32_t)bcast[0] << shift;
+        mask |= 255u << shift;
+        k_rem = bcast[1];
+        __syncthreads();
+      }
+    }
+    // Gumbel-max over the kept set (key >= the k-th largest), and the kept set's logsumexp (scores * T = x)
+    const uint32_t rkey = row_key ? (uint32_t)row_key[b] : (uint32_t)b;
+    const uint32_t step = (uint32_t)st[TW_ST_NGEN];
+    Best g{-INFINITY, 0x7fffffff};
+    float m = -INFINITY, sm = 0.f;
+    for (int v = tid; v < V; v += 256) {
+      const float x = sel_processed(row, suppress_bits, p, rm, v);
+      if (!elig(v, x) || (restrict_k && f32_order_key(x) < prefix)) continue;
+      lse_merge(m, sm, x, 1.f);
+      g = best_of(g, Best{x * invT + tw_gumbel(seed, rkey, step, (uint32_t)v), v});
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) g = best_of(g, Best{__shfl_xor(g.v, o, 64), __shfl_xor(g.i, o, 64)});
+    __syncthreads();
+    if (lane == 0) {
+      red[tid >> 6] = g.v;
+      bcast[tid >> 6] = g.i;
+    }
+    __syncthreads();
+    g = Best{red[0], bcast[0]};
+    for (int w = 1; w < 4; ++w) g = best_of(g, Best{red[w], bcast[w]});
+    sel = g.i;
+    block_lse256(m, sm, red);
+    lse = m + __logf(sm);
+  }
+  if (tid != 0) return;
+  if (pos) pos[b] += 1;
+  const int was_finished = st[TW_ST_FINISHED];
+  const int tok = sel_commit(p, st, sel, tokens_out, ld_tokens, next_ids, b);
+  if (!was_finished) {
+    const float lp = row[tok] - lse;
+    st[TW_ST_SUMLP] = __float_as_int(__int_as_float(st[TW_ST_SUMLP]) + lp);
+  }
+}
+
+// grid B, 256 threads: softmax(raw logits)[token] into the state slot TW_ST_NOSPEECH (f32 bits)
+__global__ __launch_bounds__(256) void k_token_prob(const float* __restrict__ logits, int ld_logits, int V, int token,
+                                                    int* __restrict__ state) {
+  __shared__ float red[8];
+  const float* row = logits + (size_t)blockIdx.x * ld_logits;
+  float m = -INFINITY, s = 0.f;
+  for (int v = threadIdx.x; v < V; v += 256) lse_merge(m, s, row[v], 1.f);
+  block_lse256(m, s, red);
+  if (threadIdx.x == 0)
+    state[blockIdx.x * TW_STATE_STRIDE + TW_ST_NOSPEECH] = __float_as_int(__expf(row[token] - (m + __logf(s))));
+}
+
+extern "C" int tw_logits_sample(const float* logits, int B, int ld_logits, const uint32_t* suppress_bits,
+                                const TwSelectParams* params, float temperature, int top_k, uint64_t seed,
+                                const int* row_key, int* state, int* tokens_out, int ld_tokens, int* next_ids,
+                                int* pos, void* stream) {
+  TW_REQUIRE(logits && params && state && B > 0, "tw_logits_sample: bad args");
+  TW_REQUIRE(params->mode == 0, "tw_logits_sample: generation steps (mode 0) only");
+  TW_REQUIRE(params->V > 0 && params->V <= ld_logits, "tw_logits_sample: V=%d ld=%d", params->V, ld_logits);
+  TW_REQUIRE(params->n_begin_suppress >= 0 && params->n_begin_suppress <= 8, "tw_logits_sample: begin_suppress");
+  TW_REQUIRE(temperature >= 0.f && temperature == temperature, "tw_logits_sample: temperature %f", temperature);
+  hipLaunchKernelGGL(k_select_full, dim3(B), dim3(256), 0, (hipStream_t)stream, logits, ld_logits, suppress_bits,
+                     *params, temperature, top_k, seed, row_key, state, tokens_out, ld_tokens, next_ids, pos);
+  return tw_check_launch("tw_logits_sample");
+}
+
+extern "C" int tw_token_prob(const float* logits, int B, int ld_logits, int V, int token, int* state, void* stream) {
+  TW_REQUIRE(logits && state && B > 0 && V > 0 && V <= ld_logits && token >= 0 && token < V,
+             "tw_token_prob: B=%d V=%d token=%d", B, V, token);
+  hipLaunchKernelGGL(k_token_prob, dim3(B), dim3(256), 0, (hipStream_t)stream, logits, ld_logits, V, token, state);
+  return tw_check_launch("tw_token_prob");
 }
 
 // =================================================================================================

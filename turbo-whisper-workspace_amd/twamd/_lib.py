@@ -28,6 +28,7 @@ TW_SELECT_CHUNKS = 16
 TW_SELECT_WS_PER_ROW = 128
 TW_STATE_STRIDE = 8
 TW_ST_NGEN, TW_ST_LAST, TW_ST_PENULT, TW_ST_LASTTS, TW_ST_FINISHED, TW_ST_LANG = 0, 1, 2, 3, 4, 5
+TW_ST_SUMLP, TW_ST_NOSPEECH = 6, 7  # f32 bits (tw_logits_sample / tw_token_prob)
 
 # every symbol include/tw_whisper.h + include/tw_audio.h declare (tests check the .so exports all of them)
 EXPORTED = (
@@ -37,7 +38,7 @@ EXPORTED = (
     "tw_gemm_set_variant", "tw_attn_set_variant",
     "tw_dtw", "tw_attn_decode_cross_probs", "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
     "tw_gemm_mx", "tw_quant_mx", "tw_layernorm_mx", "tw_attn_encoder_mx", "tw_gemm_mx_set_variant", "tw_logits_select_embed",
-    "tw_attn_set_lds_pad",
+    "tw_attn_set_lds_pad", "tw_logits_sample", "tw_token_prob",
 )
 
 
@@ -99,6 +100,9 @@ _SIGS = {
     "tw_attn_decode_cross": ([_P, _I, _I, _I, _I, _P, _P, _P, _P], _I),
     "tw_embed_decoder": ([_P, _P, _P, _P, _I, _I, _P, _P], _I),
     "tw_logits_select": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), _P, _P, _I, _P, _P, _P, _P], _I),
+    "tw_logits_sample": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), ctypes.c_float, _I, ctypes.c_uint64, _P, _P,
+                          _P, _I, _P, _P, _P], _I),
+    "tw_token_prob": ([_P, _I, _I, _I, _I, _P, _P], _I),
     "tw_gemm_bf16_partial": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P], _I),
     "tw_gemm_set_variant": ([_I], _I),
     "tw_gemm_mx_set_variant": ([_I], _I),

@@ -140,6 +140,11 @@ class GenerationSettings:
     # width (generation_config.alignment_heads, config.median_filter_width)
     alignment_heads: Optional[List[Tuple[int, int]]] = None
     median_filter_width: int = 7
+    # segment criteria of the temperature fallback when the call does not pass them (_set_thresholds_and_condition,
+    # generation_whisper.py:1702-1730: the call's value, else generation_config's)
+    compression_ratio_threshold: Optional[float] = None
+    logprob_threshold: Optional[float] = None
+    no_speech_threshold: Optional[float] = None
 
     @staticmethod
     def default(dims: WhisperDims) -> "GenerationSettings":
@@ -172,6 +177,9 @@ class GenerationSettings:
             gs.num_beams = int(cfg.get("num_beams") or 1)
             if cfg.get("alignment_heads"):
                 gs.alignment_heads = [(int(a), int(b)) for a, b in cfg["alignment_heads"]]
+            for k in ("compression_ratio_threshold", "logprob_threshold", "no_speech_threshold"):
+                if cfg.get(k) is not None:
+                    setattr(gs, k, float(cfg[k]))
         cfn = os.path.join(path, "config.json")
         if os.path.exists(cfn):
             with open(cfn) as f:

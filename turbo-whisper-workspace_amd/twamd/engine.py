@@ -24,7 +24,7 @@ import torch
 from . import _lib, alignment
 from .config import GenerationSettings, WhisperDims
 from .frontend import CHUNK_SAMPLES, N_FRAMES, dft_basis, mel_table
-from .segments import retrieve_segment, strip_generated
+from .segments import FallbackConfig, fallback_sequence, need_fallback, retrieve_segment, strip_generated
 from .weights import PackedWeights
 
 import functools
@@ -128,6 +128,8 @@ class PassResult:
     tokens: List[List[int]]      # generated tokens per row (as _sample returns them, before stripping)
     lang_ids: Optional[List[int]]
     token_ts: Optional[List[np.ndarray]] = None  # per row, token-level times (prompt zeros first; word timestamps)
+    sum_logprob: Optional[List[float]] = None  # per row, sum of the chosen tokens' log-probs (sample_pass)
+    no_speech_prob: Optional[List[float]] = None  # per row, softmax at the SOT position of <|nospeech|> (sample_pass)
 
 
 class WhisperEngine:
@@ -770,6 +772,81 @@ class WhisperEngine:
         detected = self.state[:R, _lib.TW_ST_LANG].tolist() if detect else None  # (mode-1 selection only writes it)
         return PassResult([toks[r][: ngen[r]] for r in range(R)], detected if lang_ids is None else list(lang_ids))
 
+    @on_engine_streams
+    def sample_pass(self, R: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
+                    temperature: float = 0.0, top_k: int = 50, seed: int = 0, row_keys: Optional[Sequence[int]] = None,
+                    use_timestamps: bool = True, enc_rows: Optional[Sequence[int]] = None, r_enc: Optional[int] = None,
+                    no_speech_token: Optional[int] = None, check_every: int = 8) -> PassResult:
+        """One decode pass of the temperature-fallback loop (WhisperGenerationMixin.generate_with_fallback,
+        generation_whisper.py:970-1116), eager, one tw_logits_sample per token: greedy when temperature == 0
+        (the tokens of decode_pass), else a draw from softmax(processed / T) over the top_k scores. Per row it also
+        returns the sum of the chosen tokens' log-probabilities (the avg_logprob criterion's numerator) and, with
+        no_speech_token, WhisperNoSpeechDetection's probability of it at the SOT position. enc_rows: the encoder
+        rows (of the r_enc-row encoded batch in this slot) the R decoder rows read (default 0..R-1)."""
+        st = self.gen.special
+        dev = self.device
+        r_enc = R if r_enc is None else r_enc
+        self.stream.wait_event(self._enc_ev[self._slot])
+        detect = st.is_multilingual and lang_ids is None
+        params = self._select_params(0, max_new, use_timestamps)
+        keys = torch.as_tensor(list(row_keys) if row_keys is not None else list(range(R)), dtype=torch.int32,
+                               device=dev)
+        V = self.d.vocab
+        s = self.stream.cuda_stream
+        if enc_rows is not None:
+            self.dec_row_map[:R] = torch.as_tensor(list(enc_rows), dtype=torch.int32, device=dev)
+            self._use_dec_row_map = True
+        try:
+            self.state[:R].zero_()
+            self.state[:R, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
+            self.pos[:R] = 0
+            self.ids[:R] = st.sot
+            prompt_rest: List = []
+            if st.is_multilingual:
+                prompt_rest.append(None if lang_ids is None else list(lang_ids))
+            prompt_rest.extend(int(t) for t in tail)
+
+            def no_speech() -> None:  # the logits of the step that fed <|startoftranscript|>
+                if no_speech_token is not None:
+                    _lib.call("tw_token_prob", self.logits.data_ptr(), R, V, V, int(no_speech_token),
+                              self.state.data_ptr(), s)
+
+            for k, tok in enumerate(prompt_rest):
+                want = k == 0 and (detect or no_speech_token is not None)
+                self.decoder_step(R, with_logits=want, r_enc=r_enc)
+                if k == 0:
+                    no_speech()
+                if k == 0 and detect:
+                    self._select(R, self._select_params(1, max_new), tokens=False)  # ids <- lang, pos += 1
+                    continue
+                if isinstance(tok, list):
+                    self.ids[:R] = torch.as_tensor(tok, dtype=torch.int32, device=dev)
+                else:
+                    self.ids[:R] = tok
+                self.pos[:R] = k + 1
+            steps = 0
+            while steps < max_new:
+                self.decoder_step(R, r_enc=r_enc)
+                if steps == 0 and not prompt_rest:
+                    no_speech()
+                _lib.call("tw_logits_sample", self.logits.data_ptr(), R, V, self.suppress_bits.data_ptr(),
+                          ctypes.byref(params), float(temperature), int(top_k), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                          keys.data_ptr(), self.state.data_ptr(), self.tokens.data_ptr(), self.tokens.shape[1],
+                          self.ids.data_ptr(), self.pos.data_ptr(), s)
+                steps += 1
+                if steps % check_every == 0 and bool(self.state[:R, _lib.TW_ST_FINISHED].all().item()):
+                    break
+            stt = self.state[:R].cpu()
+        finally:
+            self._use_dec_row_map = False
+        ngen = stt[:, _lib.TW_ST_NGEN].tolist()
+        toks = self.tokens[:R].tolist()
+        f32 = stt.view(torch.float32)
+        return PassResult([toks[r][: ngen[r]] for r in range(R)],
+                          stt[:, _lib.TW_ST_LANG].tolist() if detect else list(lang_ids) if lang_ids is not None else None,
+                          sum_logprob=f32[:, _lib.TW_ST_SUMLP].tolist(),
+                          no_speech_prob=f32[:, _lib.TW_ST_NOSPEECH].tolist() if no_speech_token is not None else None)
+
     def _beam_buffers(self, R: int) -> dict:
         if self._beam is None or self._beam["rows"] < R:
             dev, d = self.device, self.d
@@ -931,13 +1008,16 @@ class WhisperEngine:
                  max_new_tokens: Optional[int] = None, return_timestamps: bool = True,
                  max_passes: Optional[int] = None, slot: Optional[int] = None,
                  pre_encoded: bool = False, num_beams: int = 1, word_timestamps: bool = False,
-                 num_frames: Optional[Sequence[int]] = None) -> List[List[int]]:
+                 num_frames: Optional[Sequence[int]] = None, fallback: Optional[FallbackConfig] = None
+                 ) -> List[List[int]]:
         """Whisper short-form generate() over feats[slot][:n_chunks] (each 3000 frames): language
         detection, the seek loop and segment extraction, returning for every chunk the concatenated
         segment tokens (what generate() returns before padding).
 
         pre_encoded: the first seek pass (all chunks, seek 0, n_chunks <= max_batch) was already encoded into
-        this slot by encode(n_chunks, row_map=False, seek=False, slot=slot, sync=False) (pipelined prefetch)."""
+        this slot by encode(n_chunks, row_map=False, seek=False, slot=slot, sync=False) (pipelined prefetch).
+        fallback: generate()'s temperature / compression_ratio_threshold / logprob_threshold / no_speech_threshold;
+        when it asks for more than greedy decoding every pass runs generate_with_fallback's loop (sample_pass)."""
         if slot is not None:
             self.use_slot(slot)
         if pre_encoded and n_chunks > self.max_batch:
@@ -954,6 +1034,10 @@ class WhisperEngine:
         langs: List[Optional[int]] = list(lang_ids)[:n_chunks] if lang_ids is not None else [None] * n_chunks
         if word_timestamps and num_beams > 1:
             raise NotImplementedError("word-level timestamps with beam search are not implemented (greedy only)")
+        fb = fallback if fallback is not None and fallback.active else None
+        if fb is not None and (num_beams > 1 or word_timestamps):
+            raise NotImplementedError("temperature fallback / segment criteria with beam search or word-level "
+                                      "timestamps are not implemented (greedy passes only)")
         # word timestamps: per chunk the segments' token times (segment token_timestamps of generate(), i.e. the
         # pass's DTW times of the kept tokens + seek * 0.01 s); num_frames: the chunks' valid feature frames
         tts: List[List[float]] = [[] for _ in range(n_chunks)]
@@ -974,6 +1058,23 @@ class WhisperEngine:
                 known = all(lg is not None for lg in part_langs) or not st.is_multilingual
                 given = part_langs if (known and st.is_multilingual) else None
                 nf_part = None if num_frames is None else [int(num_frames[i]) - seek[i] for i in part]
+                if fb is not None:
+                    pre = pre_encoded and passes == 0
+                    toks_f, skip_f, lang_f = self._fallback_pass(
+                        R, tail, given, max_new, return_timestamps, fb, [part[j] for j in range(R)], passes,
+                        enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R)
+                    for j, i in enumerate(part):
+                        if not known:
+                            langs[i] = lang_f[j]
+                        passes_raw[i].append(list(toks_f[j]))
+                        if skip_f[j]:  # generate(): seek += seek_num_frames, nothing kept
+                            seek[i] = N_FRAMES
+                            continue
+                        seg_tokens, offset = retrieve_segment(toks_f[j], seek[i], N_FRAMES - seek[i],
+                                                              st.timestamp_begin)
+                        segs[i].extend(seg_tokens)
+                        seek[i] += offset
+                    continue
                 if num_beams > 1:  # pre-encoded first pass: this part's windows sit at encoder rows b0..
                     pre = pre_encoded and passes == 0
                     res = self.beam_pass(R, num_beams, tail, given, max_new, use_timestamps=return_timestamps,
@@ -1002,6 +1103,46 @@ class WhisperEngine:
         self.last_passes = passes_raw
         self.last_token_timestamps = tts if word_timestamps else None
         return segs
+
+    def _fallback_pass(self, R: int, tail, given, max_new: int, return_timestamps: bool, fb: FallbackConfig,
+                       windows: Sequence[int], pass_no: int, enc_row0: int = 0, r_enc: Optional[int] = None):
+        """generate_with_fallback (generation_whisper.py:970-1116) for one seek pass of R encoded rows: decode at
+        the first temperature, re-decode the rows whose criteria fail at the next one, until none does or the
+        temperatures run out. Returns per row the kept sequence (EOS removed), should_skip, and the language ids.
+        Bug-compatible with transformers: needs_fallback / should_skip are written at the row's position in the
+        CURRENT (shrinking) subset, and the main loop reads should_skip by batch position (:1074-1088, :879)."""
+        st = self.gen.special
+        V = self.d.vocab
+        idx = list(range(R))
+        seqs: List[Optional[List[int]]] = [None] * R
+        skip = [False] * R
+        langs = list(given) if given is not None else None
+        ns_tok = st.notimestamps - 1 if fb.no_speech_threshold is not None else None  # no_timestamps_token_id - 1
+        temps = list(fb.temperatures) or [None]
+        for fi, t in enumerate(temps):
+            do_sample = t is not None and t > 0.0
+            res = self.sample_pass(len(idx), tail, None if langs is None else [langs[i] for i in idx], max_new,
+                                   temperature=float(t) if do_sample else 0.0, top_k=fb.top_k, seed=fb.seed,
+                                   row_keys=[(int(windows[i]) * 1024 + pass_no) * 16 + fi for i in idx],
+                                   use_timestamps=return_timestamps, enc_rows=[enc_row0 + i for i in idx],
+                                   r_enc=r_enc, no_speech_token=ns_tok)
+            if langs is None and res.lang_ids is not None:  # detected on the first round (all rows)
+                langs = list(res.lang_ids)
+            new_idx = []
+            for j, toks in enumerate(res.tokens):
+                seq = fallback_sequence(toks, st.eot, st.eot)
+                needs, sk = need_fallback(seq, res.sum_logprob[j],
+                                          None if res.no_speech_prob is None else res.no_speech_prob[j], V, fb)
+                skip[j] = sk
+                if seq and seq[-1] == st.eot:
+                    seq = seq[:-1]
+                seqs[idx[j]] = seq
+                if needs:
+                    new_idx.append(idx[j])
+            idx = new_idx
+            if not idx or fi == len(temps) - 1:
+                break
+        return seqs, skip, langs if langs is not None else [None] * R
 
     @on_engine_streams
     def run_batches(self, sizes: Sequence[int], load=None, batch_kwargs: Optional[Sequence[dict]] = None,

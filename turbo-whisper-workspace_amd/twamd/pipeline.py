@@ -23,7 +23,7 @@ from . import audio, dist
 from .config import PRESETS, GenerationSettings, WhisperDims
 from .engine import WhisperEngine
 from .frontend import CHUNK_SAMPLES, SAMPLE_RATE, Window, chunk_windows, time_precision
-from .segments import pad_right
+from .segments import FallbackConfig, pad_right
 from .tokenizer import LANGUAGE_NAMES, WhisperVocab, decode_asr
 from .weights import build_weights
 
@@ -69,6 +69,7 @@ class TurboTranscriber:
         # 8 GPUs gives each rank 15 windows: one batch, no overlap). None: never split (see DESIGN.md §C3 for the
         # measured trade: the decode step is latency-bound, so two decodes of 8 cost about two of 15).
         self.sub_batch_min: Optional[int] = None
+        self.sample_seed = 0  # key of the fallback sampler (generate_kwargs "seed" overrides it per call)
         self._staging = None  # two pinned host buffers for the per-batch waveform upload (host-array inputs)
 
     # -------------------------------------------------------------- construction
@@ -122,6 +123,13 @@ class TurboTranscriber:
         max_new_tokens = dec["max_new_tokens"]
         # extension (not a transformers generate kwarg): bound the seek loop to this many passes per window
         max_passes = gk.pop("max_passes", None)
+        fallback = self._fallback_config(gk)
+        if fallback.active and (num_beams > 1 or word):
+            raise NotImplementedError("temperature fallback / segment criteria run with greedy passes only: pass "
+                                      "generate_kwargs={'num_beams': 1} (the pipeline's default decode is beam-5) "
+                                      "and segment-level timestamps")
+        if gk:
+            raise ValueError(f"generate_kwargs not supported by this engine: {sorted(gk)}")
         st = self.gen.special
         if not st.is_multilingual and (task is not None or language is not None):
             raise ValueError("Cannot specify `task` or `language` for an English-only model.")
@@ -168,7 +176,8 @@ class TurboTranscriber:
                                                max_passes=max_passes)
                 return [(t, ts) for t, ts in zip(toks, self.last_window_token_timestamps)]
             return self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=bool(return_timestamps),
-                                           max_new_tokens=max_new_tokens, num_beams=num_beams, max_passes=max_passes)
+                                           max_new_tokens=max_new_tokens, num_beams=num_beams, max_passes=max_passes,
+                                           **({"fallback": fallback} if fallback.active else {}))
 
         # one window shard per rank + one all-gather of the token arrays (twamd.dist); plain call on 1 GPU
         outputs = dist.transcribe_sharded(run, wav, windows, timed=word) if world > 1 else run(wav, windows)
@@ -192,7 +201,8 @@ class TurboTranscriber:
                            lang_id: Optional[int], return_timestamps: bool,
                            max_new_tokens: Optional[int] = None, num_beams: int = 1, word_timestamps: bool = False,
                            num_frames: Optional[Sequence[int]] = None, group: Optional[int] = None,
-                           max_passes: Optional[int] = None) -> List[List[int]]:
+                           max_passes: Optional[int] = None, fallback: Optional[FallbackConfig] = None
+                           ) -> List[List[int]]:
         """Log-mel + generate for every window; returns per-window token sequences (generate() output,
         right-padded with the pad token within each engine batch, as the HF batch output is). Batches of
         max_batch windows go through WhisperEngine.run_batches: batch k+1 is encoded while batch k decodes.
@@ -239,7 +249,7 @@ class TurboTranscriber:
         res = eng.run_batches(sizes, load=load, batch_kwargs=bkw, task=task,
                               lang_ids=None if lang_id is None else [lang_id] * max(sizes, default=1),
                               max_new_tokens=max_new_tokens, return_timestamps=return_timestamps, num_beams=num_beams,
-                              max_passes=max_passes)
+                              max_passes=max_passes, **({"fallback": fallback} if fallback is not None else {}))
         out: List[List[int]] = []
         for seqs in res:
             out.extend(pad_right(seqs, self.gen.special.eot))
@@ -249,6 +259,23 @@ class TurboTranscriber:
         if word_timestamps:  # per window the concatenated segments' token times (not padded, as the pipeline's)
             self.last_window_token_timestamps = [t for bt in eng.batch_token_timestamps for t in bt]
         return out
+
+    def _fallback_config(self, gk: Dict[str, Any]) -> FallbackConfig:
+        """Pops generate()'s temperature-fallback kwargs (generation_whisper.py:398-401): `temperature` (a float or
+        a list / tuple of temperatures tried in turn), the three segment criteria (else the checkpoint's
+        generation_config values), `top_k` (sampling; GenerationConfig's default 50), `do_sample` (ignored: the
+        temperature decides, as generate_with_fallback does), and the extension `seed` (the sampler's key).
+        condition_on_prev_tokens=True (prompting a pass with the previous segment) is not implemented."""
+        g = self.gen
+        t = gk.pop("temperature", None)
+        temps = tuple(t) if isinstance(t, (list, tuple)) else (t,)
+        gk.pop("do_sample", None)
+        if gk.pop("condition_on_prev_tokens", None):
+            raise NotImplementedError("condition_on_prev_tokens=True is not implemented")
+        pick = lambda k: gk.pop(k) if gk.get(k) is not None else (gk.pop(k, None), getattr(g, k))[1]  # noqa: E731
+        return FallbackConfig(temperatures=temps, compression_ratio_threshold=pick("compression_ratio_threshold"),
+                              logprob_threshold=pick("logprob_threshold"), no_speech_threshold=pick("no_speech_threshold"),
+                              top_k=int(gk.pop("top_k", 50) or 0), seed=int(gk.pop("seed", getattr(self, "sample_seed", 0))))
 
     def _host_staging(self, i: int, rows: int) -> torch.Tensor:
         """Pinned host buffer i (of two, alternating per batch) for a batch's waveforms: the upload is then an async

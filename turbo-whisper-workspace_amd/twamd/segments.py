@@ -6,11 +6,17 @@ Restates, on plain int lists:
   * _retrieve_segment (:1977-2074) reduced to what the pipeline consumes: the tokens the pass
     contributes to the final sequence (segment slices are contiguous from 0, so their
     concatenation is a prefix of the sequence) and the seek advance in mel frames,
-  * the final right padding of _pad_to_max_length (:125-232).
+  * the final right padding of _pad_to_max_length (:125-232),
+  * the temperature-fallback criteria of _need_fallback (:1243-1287): compression ratio
+    (_retrieve_compression_ratio, :1949-1956), average log-probability (_retrieve_avg_logprobs, :1958-1975, from
+    the device's per-row sum) and the no-speech skip.
 """
 from __future__ import annotations
 
-from typing import List, Sequence, Tuple
+import math
+import zlib
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
 
 INPUT_STRIDE = 2  # conv1.stride * conv2.stride: mel frames per encoder position
 
@@ -45,3 +51,59 @@ def retrieve_segment(seq: Sequence[int], seek: int, seek_num_frames: int, timest
 def pad_right(seqs: Sequence[Sequence[int]], pad: int) -> List[List[int]]:
     n = max((len(s) for s in seqs), default=0)
     return [list(s) + [pad] * (n - len(s)) for s in seqs]
+
+
+def fallback_sequence(seq: Sequence[int], pad: int, eos: int) -> List[int]:
+    """generate_with_fallback's per-row cut (:1058-1066): every pad token removed from a sequence that ends on one,
+    except one when pad == eos (the EOS counts in the average log-probability)."""
+    seq = list(seq)
+    if seq and seq[-1] == pad:
+        n = sum(1 for t in seq if t == pad) - (1 if pad == eos else 0)
+        if n:
+            seq = seq[:-n]
+    return seq
+
+
+def compression_ratio(tokens: Sequence[int], vocab_size: int) -> float:
+    """_retrieve_compression_ratio: raw little-endian token bytes over their zlib-compressed length."""
+    length = int(math.log2(vocab_size) / 8) + 1
+    raw = b"".join(int(t).to_bytes(length, "little") for t in tokens)
+    return len(raw) / len(zlib.compress(raw))
+
+
+@dataclass
+class FallbackConfig:
+    """The generate() kwargs of the temperature fallback (generation_whisper.py:398-401, 483-512)."""
+    temperatures: Tuple[Optional[float], ...] = (None,)
+    compression_ratio_threshold: Optional[float] = None
+    logprob_threshold: Optional[float] = None
+    no_speech_threshold: Optional[float] = None
+    top_k: int = 50          # GenerationConfig's default, applied when sampling (TopKLogitsWarper)
+    seed: int = 0
+
+    @property
+    def active(self) -> bool:
+        """Anything beyond plain greedy decoding: sampling, or a criterion (which may skip a segment)."""
+        return (any(t is not None and t > 0.0 for t in self.temperatures) or self.compression_ratio_threshold is not None
+                or self.logprob_threshold is not None or self.no_speech_threshold is not None)
+
+
+def need_fallback(seq: Sequence[int], sum_logprob: float, no_speech_prob: Optional[float], vocab_size: int,
+                  cfg: FallbackConfig) -> Tuple[bool, bool]:
+    """_need_fallback for one row: (needs_fallback, should_skip). seq is fallback_sequence's cut (EOS kept);
+    sum_logprob the device's sum of log_softmax(scores)[token] over it."""
+    needs, skip = False, False
+    if cfg.compression_ratio_threshold is not None:
+        if compression_ratio(seq, vocab_size) > cfg.compression_ratio_threshold:
+            needs = True
+    logprob = None
+    if cfg.logprob_threshold is not None:
+        logprob = sum_logprob / len(seq) if seq else float("-inf")
+        if logprob < cfg.logprob_threshold:
+            needs = True
+    if cfg.no_speech_threshold is not None:
+        if logprob is None:  # transformers reads an unset local here (UnboundLocalError)
+            raise ValueError("no_speech_threshold needs logprob_threshold (generation_whisper.py:1275-1283)")
+        if logprob < cfg.logprob_threshold and no_speech_prob > cfg.no_speech_threshold:
+            needs, skip = False, True
+    return needs, skip
