@@ -162,3 +162,66 @@ def test_turbo_bench_decode_vs_transformers(turbo, z):
             assert r["lang_ok"] and r["status"] in ("exact", "within_tau"), (w, r)
     finally:
         eng.set_suppress_tokens(list(gen.suppress_tokens))
+
+
+# ---- config 5's MX-fp8 encoder at the benchmarked depth ------------------------------------------------------------
+# What fp8 costs at 32 encoder layers against transformers fp32 (the oracle's own MX restatement is pinned at
+# test-mini by tests/test_gpu_fp8_encoder.py). Measured on MI355X (profiles/r03m_fp8_gputest.txt): encoder rows
+# mean |d| 0.083 / 0.071, min row cosine 0.994; teacher-forced top-16 logits mean |d| 0.16, worst 0.52; generate()
+# diverging first at near-ties of 0.04 / 0.07. Bounds about 1.5-3x those; the token check's tau is the measured worst
+# logit error (not below the bf16 TAU).
+FP8_ENC_MEAN_ABS = 0.12
+FP8_ENC_COS_MIN = 0.99
+FP8_LOGIT_MEAN_ABS = 0.5
+
+
+@pytest.fixture(scope="module")
+def turbo8():
+    tr = TurboTranscriber.from_pretrained("large-v3-turbo", seed=1234, max_batch=2, max_beams=1, enc_fp8=True)
+    yield tr
+    del tr
+    torch.cuda.empty_cache()
+
+
+def test_turbo_fp8_encoder_and_logits_vs_transformers(turbo8, z):
+    """The MX-fp8 encoder (q/k/v/o, fc1/fc2 on v_mfma_scale_f32_16x16x128_f8f6f4) + bf16 decoder at large-v3-turbo
+    depth: encoder rows and teacher-forced logits against transformers fp32 (tests/golden/turbo.npz), the language
+    detected, and the greedy generate() within the fp8 logit error of the fp32 choice at its first divergence."""
+    eng = turbo8.engine
+    assert eng.enc_fp8
+    _load(turbo8, _clips())
+    eng.row_map[:2] = torch.arange(2, dtype=torch.int32)
+    eng.seek[:2] = 0
+    eng.encode(2)
+    enc = eng.encoder_output(2).float().cpu().numpy()
+    for i in range(2):
+        rows = enc[i][z["enc_rows_idx"]]
+        d = np.abs(rows - z["enc_rows"][i])
+        cos = (rows * z["enc_rows"][i]).sum(1) / (np.linalg.norm(rows, axis=1) * np.linalg.norm(z["enc_rows"][i], axis=1))
+        print(f"turbo fp8 encoder clip {i}: rows max|d| {d.max():.4f} mean|d| {d.mean():.4f} min cos {cos.min():.5f}; "
+              f"mean {enc[i].mean() - z['enc_mean'][i]:+.2e} std {enc[i].std() - z['enc_std'][i]:+.2e}")
+        assert np.all(np.isfinite(enc[i]))
+        assert d.mean() <= FP8_ENC_MEAN_ABS and cos.min() >= FP8_ENC_COS_MIN, (i, d.mean(), cos.min())
+    worst, mean_d = 0.0, []
+    for t, tok in enumerate(z["tf_input_ids"]):
+        eng.ids[0] = int(tok)
+        eng.pos[0] = t
+        eng.decoder_step(1, r_enc=2)
+        lg = eng.logits[0].cpu().numpy().astype(np.float64)
+        d = np.abs(lg[z["tf_top_idx"][t]] - z["tf_top_val"][t])
+        worst = max(worst, d.max())
+        mean_d.append(d.mean())
+    print(f"turbo fp8 teacher-forced: top-16 logits worst |d| {worst:.4f}, mean {np.mean(mean_d):.4f}")
+    assert np.mean(mean_d) <= FP8_LOGIT_MEAN_ABS
+    _load(turbo8, _clips())
+    seqs = eng.generate(2, task="transcribe", max_new_tokens=40, return_timestamps=True)
+    assert eng.last_langs == [int(x) for x in z["gen_lang"]]
+    tau = max(worst, tp.TAU)
+    for i in range(2):
+        for k, (seek, gt, ti, tv, mg) in enumerate(tp.gen_passes(z, i)):
+            dev = eng.last_passes[i]
+            r = tp.check_pass(_cut(dev[k]) if k < len(dev) else [], gt, ti, tv, mg, tau=tau)
+            print(f"turbo fp8 generate clip {i} pass {k}: {r}")
+            if r["status"] != "exact":
+                assert r["status"] == "within_tau", (i, k, r)
+                break
