@@ -9,6 +9,8 @@
  *
  *   tw_flac_probe / tw_flac_decode   FLAC container + frame decode on HOST memory (multi-threaded over frames),
  *                                    bit-exact PCM (checked against the stream's own STREAMINFO MD5)
+ *   tw_g711_decode                   G.711 mu-law / A-law expansion (WAV, AU, AIFF-C telephony codecs)
+ *   tw_ima_adpcm_wav_decode          IMA ADPCM in WAV blocks
  *   tw_resample_pcm_i32 / _f32       downmix + polyphase resample on the GPU (DEVICE memory, `stream`), the
  *                                    libswresample default filter restated (Kaiser-windowed sinc, see
  *                                    twamd/audio.py: swr_filter_bank)
@@ -55,6 +57,17 @@ int tw_resample_pcm_i32(const int32_t* pcm, int64_t n_in, int32_t channels, floa
                         const float* taps, int32_t ntaps, float* y, int64_t n_out, void* stream);
 int tw_resample_pcm_f32(const float* x, int64_t n_in, int32_t channels, int32_t up, int32_t down, const float* taps,
                         int32_t ntaps, float* y, int64_t n_out, void* stream);
+
+/* G.711 expansion of n codes to s16 (HOST memory): mu-law (alaw == 0) or A-law, the classic ITU-T G.711 tables
+ * (WAV format tags 7 / 6, AU encodings 1 / 27, AIFF-C 'ulaw' / 'alaw'; what ffmpeg_read's pcm_mulaw / pcm_alaw give). */
+int tw_g711_decode(const uint8_t* in, int64_t n, int32_t alaw, int16_t* out);
+
+/* IMA ADPCM in Microsoft's WAV block layout (format tag 0x11, 4 bits per sample; ffmpeg's adpcm_ima_wav): blocks of
+ * block_align bytes (the last may be shorter), each channel's 4-byte header {s16 first sample, u8 step index, u8 0},
+ * then 4-byte words of 8 samples per channel, interleaved, low nibble first. out = int16[out_frames][channels]
+ * interleaved (HOST); *frames_decoded receives the frames written (1 + 8 * whole words per channel per block). */
+int tw_ima_adpcm_wav_decode(const uint8_t* data, int64_t size, int32_t channels, int32_t block_align, int16_t* out,
+                            int64_t out_frames, int64_t* frames_decoded);
 
 #ifdef __cplusplus
 }

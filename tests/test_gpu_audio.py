@@ -89,3 +89,54 @@ def test_flac_file_through_process_audio(tmp_path):
     wav = ao.swr_resample(pcm / 32768.0, 192000, 16000).astype(np.float32)
     ref = tr(wav, chunk_length_s=60, stride_length_s=5, generate_kwargs={"max_new_tokens": 32}, return_timestamps=True)
     assert res["text"] == ref["text"]
+
+
+@pytest.mark.parametrize("kind", ["wav_ulaw", "wav_ima", "au_alaw", "aifc_ulaw"])
+def test_telephony_files_through_load_input(kind):
+    """8 kHz call recordings (G.711 / IMA ADPCM) through the product path: native host decode, then the GPU resampler
+    to 16 kHz, against the oracle resampler applied to the stdlib (audioop) decode of the same bytes."""
+    import audioop
+    import struct
+
+    x = np.clip(_sig(8000, 2.1, 1, 11)[:, 0] * 0.8, -1, 1)
+    lin = np.round(x * 32767).astype("<i2").tobytes()
+    if kind == "wav_ima":
+        # a Microsoft IMA encoder: per 505-sample block, the header carries the first sample and the running step
+        # index; audioop codes the other 504 (high nibble first, swapped to WAV's low-nibble-first order)
+        s16 = np.frombuffer(lin, "<i2")
+        payload, index = bytearray(), 0
+        for i in range(0, len(s16) - 504, 505):
+            codes, (_, nxt) = audioop.lin2adpcm(s16[i + 1: i + 505].tobytes(), 2, (int(s16[i]), index))
+            payload += struct.pack("<hBB", int(s16[i]), index, 0) + bytes(((b & 0x0F) << 4) | (b >> 4) for b in codes)
+            index = nxt
+        fmt = struct.pack("<HHIIHHHH", 0x11, 1, 8000, 4055, 256, 4, 2, 505)
+        data = b"RIFF" + struct.pack("<I", 4 + 8 + len(fmt) + 8 + len(payload)) + b"WAVEfmt " + \
+            struct.pack("<I", len(fmt)) + fmt + b"data" + struct.pack("<I", len(payload)) + bytes(payload)
+        ref_lin = audio.decode_wav(data)[0][:, 0].astype(np.float64)  # checked against audioop in test_audio_codecs
+    else:
+        alaw = kind == "au_alaw"
+        codes = audioop.lin2alaw(lin, 2) if alaw else audioop.lin2ulaw(lin, 2)
+        ref_lin = np.frombuffer(audioop.alaw2lin(codes, 2) if alaw else audioop.ulaw2lin(codes, 2), "=i2") / 32768.0
+        if kind == "wav_ulaw":
+            fmt = struct.pack("<HHIIHH", 7, 1, 8000, 8000, 1, 8)
+            data = b"RIFF" + struct.pack("<I", 4 + 8 + len(fmt) + 8 + len(codes)) + b"WAVEfmt " + \
+                struct.pack("<I", len(fmt)) + fmt + b"data" + struct.pack("<I", len(codes)) + codes
+        elif kind == "au_alaw":
+            data = b".snd" + struct.pack(">IIIII", 24, len(codes), 27, 8000, 1) + codes
+        else:
+            import aifc
+            import io
+
+            buf = io.BytesIO()
+            w = aifc.open(buf, "wb")
+            w.setnchannels(1), w.setsampwidth(2), w.setframerate(8000), w.setcomptype(b"ulaw", b"")
+            w.writeframes(lin)
+            w._patchheader()
+            data = buf.getvalue()
+            w._file = None
+    got = audio.load_input(data)
+    ref = ao.swr_resample(ref_lin, 8000, 16000)
+    assert got.shape == ref.shape == (2 * len(ref_lin),)
+    assert np.abs(got - ref).max() < TOL
+    clean = ao.swr_resample(x[: len(ref_lin)], 8000, 16000)
+    assert np.abs(ref - clean)[100:-100].mean() < 0.03  # codec noise, not garbage

@@ -7,7 +7,9 @@ which this image does not have), dicts carry {"raw"|"array", "sampling_rate"} an
 differs, multi-channel arrays are averaged to mono.
 
 Containers: FLAC (native multi-threaded decoder in libtwhip.so, include/tw_audio.h; bit-exact, verifiable
-against the stream's STREAMINFO MD5) and RIFF/WAVE (PCM 8/16/24/32-bit, IEEE float 32/64).
+against the stream's STREAMINFO MD5), RIFF/WAVE (PCM 8/16/24/32-bit, IEEE float 32/64, G.711 A-law / mu-law, IMA
+ADPCM), Sun AU and AIFF / AIFF-C (PCM, float, G.711) — the telephony codecs through native decoders
+(tw_g711_decode, tw_ima_adpcm_wav_decode), pinned to CPython's audioop / aifc / sunau / wave.
 Resampling runs on the GPU (tw_resample_pcm_*) with libswresample's default filter restated in
 swr_filter_bank. There is no CPU resampler in the product: resampling without a GPU raises.
 """
@@ -133,8 +135,64 @@ def resample_device(x: np.ndarray, sr_in: int, sr_out: int = TARGET_SR, scale: f
     return y
 
 
+def g711_decode(codes: bytes, alaw: bool) -> np.ndarray:
+    """G.711 mu-law / A-law bytes -> int16 (native tw_g711_decode: the ITU-T tables ffmpeg's pcm_mulaw / pcm_alaw
+    use)."""
+    _lib, lib = _flac_lib()
+    src = np.frombuffer(codes, np.uint8)
+    out = np.empty(len(src), np.int16)
+    if lib.tw_g711_decode(src.ctypes.data, len(src), int(alaw), out.ctypes.data) != 0:
+        raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    return out
+
+
+def ima_adpcm_wav_decode(data: bytes, channels: int, block_align: int) -> np.ndarray:
+    """Microsoft IMA ADPCM blocks (WAV format tag 0x11) -> int16 [frames, channels] (native
+    tw_ima_adpcm_wav_decode; ffmpeg's adpcm_ima_wav)."""
+    _lib, lib = _flac_lib()
+    if block_align < 4 * channels:
+        raise ValueError(f"IMA ADPCM block_align {block_align} < 4 x {channels} channels")
+    per = 1 + ((block_align - 4 * channels) // (4 * channels)) * 8
+    cap = (len(data) // block_align + 1) * per
+    if cap > max_audio_seconds() * 192000:
+        raise ValueError("IMA ADPCM stream longer than TW_MAX_AUDIO_S")
+    out = np.zeros((cap, channels), np.int16)
+    got = ctypes.c_int64()
+    src = np.frombuffer(data, np.uint8)
+    if lib.tw_ima_adpcm_wav_decode(src.ctypes.data, len(src), channels, block_align, out.ctypes.data, cap,
+                                   ctypes.byref(got)) != 0:
+        raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    return out[: got.value]
+
+
+def _pcm_to_float(raw: bytes, bits: int, big_endian: bool = False, unsigned8: bool = True) -> np.ndarray:
+    """Integer PCM -> float32 in [-1, 1) the way ffmpeg's s8/s16/s24/s32 -> flt conversion scales (2^-(bits-1))."""
+    e = ">" if big_endian else "<"
+    if bits == 8:
+        v = np.frombuffer(raw, np.uint8 if unsigned8 else np.int8).astype(np.float32)
+        return (v - 128.0) / 128.0 if unsigned8 else v / 128.0
+    if bits == 16:
+        return np.frombuffer(raw[: len(raw) // 2 * 2], e + "i2").astype(np.float32) / 32768.0
+    if bits == 24:
+        b = np.frombuffer(raw[: len(raw) // 3 * 3], np.uint8).reshape(-1, 3).astype(np.int32)
+        if big_endian:
+            b = b[:, ::-1]
+        v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
+        v = np.where(v >= 1 << 23, v - (1 << 24), v)
+        return v.astype(np.float32) / float(1 << 23)
+    if bits == 32:
+        return np.frombuffer(raw[: len(raw) // 4 * 4], e + "i4").astype(np.float32) / 2147483648.0
+    raise ValueError(f"unsupported PCM width {bits}")
+
+
+def _frames(x: np.ndarray, ch: int) -> np.ndarray:
+    n = len(x) // ch
+    return x[: n * ch].reshape(n, ch)
+
+
 def decode_wav(data: bytes) -> Tuple[np.ndarray, int]:
-    """RIFF/WAVE bytes -> (float32 [frames, channels] in [-1, 1], sample_rate)."""
+    """RIFF/WAVE bytes -> (float32 [frames, channels] in [-1, 1], sample_rate). Format tags: 1 PCM 8/16/24/32,
+    3 IEEE float 32/64, 6 A-law, 7 mu-law, 0x11 IMA ADPCM, and WAVE_FORMAT_EXTENSIBLE carrying any of them."""
     if len(data) < 12 or data[:4] != b"RIFF" or data[8:12] != b"WAVE":
         raise ValueError("not a RIFF/WAVE stream")
     pos, fmt, pcm = 12, None, None
@@ -142,36 +200,104 @@ def decode_wav(data: bytes) -> Tuple[np.ndarray, int]:
         cid, size = data[pos: pos + 4], struct.unpack("<I", data[pos + 4: pos + 8])[0]
         body = data[pos + 8: pos + 8 + size]
         if cid == b"fmt ":
-            tag, ch, sr, _, _, bits = struct.unpack("<HHIIHH", body[:16])
+            tag, ch, sr, _, align, bits = struct.unpack("<HHIIHH", body[:16])
             if tag == 0xFFFE and len(body) >= 26:  # WAVE_FORMAT_EXTENSIBLE: subformat GUID's first 2 bytes
                 tag = struct.unpack("<H", body[24:26])[0]
-            fmt = (tag, ch, sr, bits)
+            fmt = (tag, ch, sr, bits, align)
         elif cid == b"data":
             pcm = body
         pos += 8 + size + (size & 1)
     if fmt is None or pcm is None:
         raise ValueError("WAVE stream without fmt/data chunks")
-    tag, ch, sr, bits = fmt
+    tag, ch, sr, bits, align = fmt
+    if ch < 1:
+        raise ValueError("WAVE stream with no channels")
     if tag == 1:
-        if bits == 8:
-            x = (np.frombuffer(pcm, np.uint8).astype(np.float32) - 128.0) / 128.0
-        elif bits == 16:
-            x = np.frombuffer(pcm[: len(pcm) // 2 * 2], "<i2").astype(np.float32) / 32768.0
-        elif bits == 24:
-            b = np.frombuffer(pcm[: len(pcm) // 3 * 3], np.uint8).reshape(-1, 3).astype(np.int32)
-            v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
-            v = np.where(v >= 1 << 23, v - (1 << 24), v)
-            x = v.astype(np.float32) / float(1 << 23)
-        elif bits == 32:
-            x = np.frombuffer(pcm[: len(pcm) // 4 * 4], "<i4").astype(np.float32) / 2147483648.0
-        else:
-            raise ValueError(f"unsupported PCM width {bits}")
+        x = _pcm_to_float(pcm, bits)
     elif tag == 3:
-        x = np.frombuffer(pcm, "<f4" if bits == 32 else "<f8").astype(np.float32)
+        x = np.frombuffer(pcm[: len(pcm) // (bits // 8) * (bits // 8)], "<f4" if bits == 32 else "<f8").astype(np.float32)
+    elif tag in (6, 7):
+        x = g711_decode(pcm, alaw=tag == 6).astype(np.float32) / 32768.0
+    elif tag == 0x11:
+        if bits != 4:
+            raise ValueError(f"IMA ADPCM with {bits} bits per sample (4 supported)")
+        return ima_adpcm_wav_decode(pcm, ch, align).astype(np.float32) / 32768.0, sr
     else:
         raise ValueError(f"unsupported WAVE format tag {tag}")
-    n = len(x) // ch
-    return x[: n * ch].reshape(n, ch), sr
+    return _frames(x, ch), sr
+
+
+# Sun/NeXT .au encodings (ffmpeg's au demuxer): 1 mu-law, 2/3/4/5 big-endian signed PCM 8/16/24/32, 6/7 float 32/64,
+# 27 A-law
+def decode_au(data: bytes) -> Tuple[np.ndarray, int]:
+    """Sun .au / .snd bytes -> (float32 [frames, channels], sample_rate)."""
+    if len(data) < 24 or data[:4] != b".snd":
+        raise ValueError("not a Sun .au stream")
+    off, size, enc, sr, ch = struct.unpack(">IIIII", data[4:24])
+    if ch < 1 or off < 24:
+        raise ValueError("bad .au header")
+    body = data[off:] if size == 0xFFFFFFFF else data[off: off + size]
+    if enc == 1 or enc == 27:
+        x = g711_decode(body, alaw=enc == 27).astype(np.float32) / 32768.0
+    elif enc in (2, 3, 4, 5):
+        x = _pcm_to_float(body, 8 * (enc - 1), big_endian=True, unsigned8=False)
+    elif enc in (6, 7):
+        w = 4 if enc == 6 else 8
+        x = np.frombuffer(body[: len(body) // w * w], ">f4" if enc == 6 else ">f8").astype(np.float32)
+    else:
+        raise ValueError(f"unsupported .au encoding {enc}")
+    return _frames(x, ch), sr
+
+
+def _ieee_extended(b: bytes) -> float:
+    """80-bit IEEE 754 extended (AIFF COMM sampleRate)."""
+    exp = struct.unpack(">H", b[:2])[0]
+    mant = struct.unpack(">Q", b[2:10])[0]
+    sign = -1.0 if exp & 0x8000 else 1.0
+    exp &= 0x7FFF
+    if exp == 0 and mant == 0:
+        return 0.0
+    return sign * mant * 2.0 ** (exp - 16383 - 63)
+
+
+def decode_aiff(data: bytes) -> Tuple[np.ndarray, int]:
+    """AIFF / AIFF-C bytes -> (float32 [frames, channels], sample_rate). Compression types: NONE / twos (big-endian
+    PCM), sowt (little-endian PCM), fl32 / fl64, ulaw, alaw (ffmpeg's aiff demuxer)."""
+    if len(data) < 12 or data[:4] != b"FORM" or data[8:12] not in (b"AIFF", b"AIFC"):
+        raise ValueError("not an AIFF stream")
+    aifc = data[8:12] == b"AIFC"
+    pos, comm, ssnd = 12, None, None
+    while pos + 8 <= len(data):
+        cid, size = data[pos: pos + 4], struct.unpack(">I", data[pos + 4: pos + 8])[0]
+        body = data[pos + 8: pos + 8 + size]
+        if cid == b"COMM":
+            ch, nframes, bits = struct.unpack(">hIh", body[:8])
+            sr = _ieee_extended(body[8:18])
+            ctype = body[18:22] if aifc and len(body) >= 22 else b"NONE"
+            comm = (ch, nframes, bits, sr, ctype)
+        elif cid == b"SSND":
+            offset = struct.unpack(">I", body[:4])[0]
+            ssnd = body[8 + offset:]
+        pos += 8 + size + (size & 1)
+    if comm is None or ssnd is None:
+        raise ValueError("AIFF stream without COMM/SSND chunks")
+    ch, nframes, bits, sr, ctype = comm
+    if ch < 1:
+        raise ValueError("AIFF stream with no channels")
+    if ctype in (b"NONE", b"twos"):
+        x = _pcm_to_float(ssnd, (bits + 7) // 8 * 8, big_endian=True, unsigned8=False)
+    elif ctype == b"sowt":
+        x = _pcm_to_float(ssnd, (bits + 7) // 8 * 8, big_endian=False, unsigned8=False)
+    elif ctype in (b"fl32", b"FL32"):
+        x = np.frombuffer(ssnd[: len(ssnd) // 4 * 4], ">f4").astype(np.float32)
+    elif ctype in (b"fl64", b"FL64"):
+        x = np.frombuffer(ssnd[: len(ssnd) // 8 * 8], ">f8").astype(np.float32)
+    elif ctype in (b"ulaw", b"ULAW", b"alaw", b"ALAW"):
+        x = g711_decode(ssnd, alaw=ctype.lower() == b"alaw").astype(np.float32) / 32768.0
+    else:
+        raise ValueError(f"unsupported AIFF-C compression {ctype!r}")
+    fr = _frames(x, ch)
+    return fr[:nframes], int(round(sr))
 
 
 def resample(x: np.ndarray, sr_in: int, sr_out: int = TARGET_SR, device=None) -> np.ndarray:
@@ -204,6 +330,10 @@ def container_name(data: bytes) -> Optional[str]:
         return "WAV"
     if data[:4] == b"fLaC":
         return "FLAC"
+    if data[:4] == b".snd":
+        return "AU"
+    if data[:4] == b"FORM" and data[8:12] in (b"AIFF", b"AIFC"):
+        return "AIFF"
     if data[4:8] == b"ftyp":
         return "MP4/M4A"
     for magic, name in _UNDECODED:
@@ -212,19 +342,23 @@ def container_name(data: bytes) -> Optional[str]:
     return None
 
 
+_DECODERS = {"WAV": decode_wav, "AU": decode_au, "AIFF": decode_aiff}
+DECODED = "FLAC, WAV (PCM, float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C"
+
+
 def decode_bytes(data: bytes, sr_out: int = TARGET_SR, device=None) -> np.ndarray:
-    if data[:4] == b"RIFF":
-        x, sr = decode_wav(data)
+    name = container_name(data)
+    if name in _DECODERS:
+        x, sr = _DECODERS[name](data)
         return resample(x.mean(axis=1) if x.shape[1] > 1 else x[:, 0], sr, sr_out, device)
-    if data[:4] == b"fLaC":
+    if name == "FLAC":
         fl = decode_flac(data)
         scale = 2.0 ** -(fl.bits_per_sample - 1)  # ffmpeg's s16/s32 -> flt conversion of the coded samples
         return resample_device(fl.pcm, fl.sample_rate, sr_out, scale=scale, device=device).cpu().numpy()
-    name = container_name(data)
     if name is None:
         raise ValueError(MALFORMED)
-    raise ValueError(f"{name} audio is not decoded by this engine (decoded containers: FLAC, WAV); convert the "
-                     "upload to FLAC or WAV")
+    raise ValueError(f"{name} audio is not decoded by this engine (decoded containers: {DECODED}); convert the "
+                     "upload to one of them")
 
 
 def load_input(inputs: Union[str, bytes, np.ndarray, dict], sr_out: int = TARGET_SR, device=None) -> np.ndarray:
@@ -262,10 +396,11 @@ def duration_seconds(path: str) -> float:
     librosa; here from the decoded stream)."""
     with open(path, "rb") as f:
         data = f.read()
-    if data[:4] == b"RIFF":
-        x, sr = decode_wav(data)
+    name = container_name(data)
+    if name in _DECODERS:
+        x, sr = _DECODERS[name](data)
         return x.shape[0] / float(sr)
-    if data[:4] == b"fLaC":
+    if name == "FLAC":
         info = flac_probe(data)
         return int(info.total_samples) / float(info.sample_rate)
     raise ValueError("duration: unsupported container")
