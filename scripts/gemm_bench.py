@@ -44,7 +44,7 @@ def main():
         else:
             out = torch.zeros(M, N, device="cuda")
         res = {1: [], 5: [], "blas": [], "mx1": [], "mx8": []}
-        mx = name not in ("conv2", "xkv")  # the MX fp8 encoder GEMM (config 5) on the layer shapes
+        mx = name not in ("conv2", "xkv") and not os.environ.get("GEMM_BENCH_NO_MX")  # MX fp8 (config 5) layer shapes
         if mx:
             Mp, Np = (M + 255) // 256 * 256, (N + 255) // 256 * 256
             Aq = torch.empty(M, K, dtype=torch.uint8, device="cuda")
