@@ -18,6 +18,9 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
                     with their processed top-16 scores
   beam.json         generate(num_beams=5) token sequences (the pipeline's default decode, asr:160-163) of
                     test-mini on three windows, with and without timestamps and with a max_length stop
+  turbo_beam.npz    generate(num_beams=5) at large-v3-turbo dims, with and without timestamps: the 5 finished
+                    hypotheses and their beam scores (oracle beam search on the fp32 model's logits, checked to
+                    return generate()'s best hypothesis)
 
 Usage: python tests/golden/make_golden.py   (≈1-2 min on 8 CPU cores)
 """
@@ -502,6 +505,75 @@ def make_turbo(out):
         res[f"bench_w{w}_top_idx"], res[f"bench_w{w}_top_val"], res[f"bench_w{w}_ts_margin"] = a, b, c
     m.generation_config.suppress_tokens = list(gen.suppress_tokens)
     np.savez_compressed(os.path.join(out, "turbo.npz"), **res)
+
+
+def make_turbo_beam(out):
+    """large-v3-turbo, seeded synthetic weights: generate(num_beams=5) — the ASR pipeline's default decode
+    (asr:160-163), i.e. what the reference's transcribe() runs — on TURBO_CLIPS, with timestamps (40 new tokens) and
+    without (24). transformers' generate() gives the best hypothesis; the oracle's restatement of _beam_search
+    (beam_search_core, pinned token-for-token to generate() at test-mini by test_oracle_golden.py), driven by the
+    same fp32 model's logits, must return the same best hypothesis here too, and supplies all 5 finished hypotheses
+    with their beam scores (sum of processed log-probs / generated length). A bf16 device decode may rank a near-tie
+    the other way; the test accepts its hypothesis when it is one of these five and within a stated score tolerance
+    of the best."""
+    from transformers import WhisperFeatureExtractor
+    from transformers.modeling_outputs import BaseModelOutput
+
+    d = PRESETS["large-v3-turbo"]
+    gen = GenerationSettings.default(d)
+    st = gen.special
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    del sd
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    cl = clips()
+    feats = np.stack([fe(cl[k], sampling_rate=16000, return_tensors="np")["input_features"][0] for k in TURBO_CLIPS])
+    with torch.no_grad():
+        lang = m.detect_language(input_features=torch.from_numpy(feats)).numpy()
+        enc = m.model.encoder(torch.from_numpy(feats)).last_hidden_state
+    res = {"lang": lang.astype(np.int32)}
+    for ts, mnt in ((True, 40), (False, 24)):
+        g = wo.GenCfg(d.vocab, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate,
+                      st.notimestamps, gen.suppress_tokens, gen.begin_suppress_tokens)
+        with torch.no_grad():
+            hf = m.generate(torch.from_numpy(feats), task="transcribe", return_timestamps=ts, num_beams=5,
+                            max_new_tokens=mnt, return_segments=True)
+        tag = f"ts{int(ts)}"
+        seqs, scores = [], []
+        for i in range(len(TURBO_CLIPS)):
+            prompt = [st.sot, int(lang[i]), st.transcribe] + ([] if ts else [st.notimestamps])
+            e = BaseModelOutput(last_hidden_state=enc[i: i + 1])
+            hist = {"h": [[] for _ in range(5)]}
+
+            def logits_of(rows):
+                ids = torch.tensor([prompt + r for r in rows])
+                with torch.no_grad():
+                    lg = m(encoder_outputs=BaseModelOutput(last_hidden_state=enc[i: i + 1].expand(len(rows), -1, -1)),
+                           decoder_input_ids=ids).logits[:, -1].numpy()
+                return [x.astype(np.float32) for x in lg]
+
+            def step(srcs, toks):
+                hist["h"] = [hist["h"][s_] + [t] for s_, t in zip(srcs, toks)]
+                return logits_of(hist["h"])
+
+            del e
+            first = logits_of([[]])[0]
+            best, tr = wo.beam_search_core(first, step, len(prompt), mnt, g, ts, 5)
+            # generate()'s first seek pass (the whole window: the beams searched over features from seek 0)
+            p0 = _passes_from_segments(hf["segments"][i], len(prompt))[0]
+            ref = p0[: p0.index(st.eot) + 1] if st.eot in p0 else p0
+            assert list(best) == ref, ("oracle beam search differs from generate()'s first pass", tag, i, best, ref)
+            seqs.append([list(map(int, x)) for x in tr["fin_seq"]])
+            scores.append(np.asarray(tr["fin_score"], np.float32))
+        L = max(len(x) for c in seqs for x in c)
+        arr = np.full((len(TURBO_CLIPS), 5, L), -1, np.int32)
+        for i, c in enumerate(seqs):
+            for k, x in enumerate(c):
+                arr[i, k, : len(x)] = x
+        res[f"{tag}_fin_seq"] = arr          # [clip][5][L], -1 padded, generated tokens incl. EOS
+        res[f"{tag}_fin_score"] = np.stack(scores)
+        res[f"{tag}_max_new_tokens"] = np.array([mnt], np.int32)
+    np.savez_compressed(os.path.join(out, "turbo_beam.npz"), **res)
 
 
 TINY_CLIPS = ("speech30", "noise12")

@@ -225,3 +225,78 @@ def test_turbo_fp8_encoder_and_logits_vs_transformers(turbo8, z):
             if r["status"] != "exact":
                 assert r["status"] == "within_tau", (i, k, r)
                 break
+
+
+BEAM_TAU = 0.1  # beam-score units (processed log-prob per generated token); see test docstring
+BEAM_SCORE_ABS = 0.03
+
+
+def _tf_beam_scores(eng, langs, seqs, use_ts):
+    """Beam scores (sum over generated tokens of the processed log-probs, as _beam_search accumulates them, / the
+    generated length) of one token sequence per clip, teacher-forced through the device decoder (row i reads clip
+    i's encoder output) with the Whisper processors applied on the host by the oracle's restatement."""
+    from oracle import whisper_oracle as wo
+    from twamd.config import PRESETS, GenerationSettings
+
+    d = PRESETS["large-v3-turbo"]
+    gen = GenerationSettings.default(d)
+    st = gen.special
+    g = wo.GenCfg(d.vocab, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate,
+                  st.notimestamps, gen.suppress_tokens, gen.begin_suppress_tokens)
+    prompts = [[st.sot, int(lg), st.transcribe] + ([] if use_ts else [st.notimestamps]) for lg in langs]
+    full = [p + list(s) for p, s in zip(prompts, seqs)]
+    R = len(full)
+    scores = [0.0] * R
+    eng.row_map[:R] = torch.arange(R, dtype=torch.int32)
+    eng.seek[:R] = 0
+    eng.encode(R)
+    for t in range(max(len(f) for f in full) - 1):
+        for r in range(R):
+            eng.ids[r] = full[r][min(t, len(full[r]) - 1)]
+            eng.pos[r] = t
+        eng.decoder_step(R, r_enc=R)
+        lg = eng.logits[:R].cpu().numpy()
+        for r in range(R):
+            P = len(prompts[r])
+            j = t + 1 - P  # generated token predicted at this position
+            if 0 <= j < len(seqs[r]):
+                lp = wo.process_logits(wo._log_softmax32(lg[r]), list(seqs[r][:j]), g, use_ts)
+                scores[r] += float(lp[seqs[r][j]])
+    return [sc / len(s) for sc, s in zip(scores, seqs)]
+
+
+def test_turbo_beam5_first_pass_vs_transformers(turbo):
+    """generate(num_beams=5) — the ASR pipeline's default decode, what the reference's transcribe() runs — at turbo
+    depth, first seek pass, with timestamps (40 new tokens) and without (24), against transformers fp32
+    (tests/golden/turbo_beam.npz: the 5 finished hypotheses and their beam scores; make_golden.py turbo_beam).
+
+    With the seeded random weights the five fp32 hypotheses lie within 0.02-0.07 of each other, so a bf16 search
+    can leave the fp32 path at any near-tie. Tolerances, in beam-score units (processed log-prob per generated
+    token):
+      numerics  the device teacher-forced score of the fp32 best hypothesis is within BEAM_SCORE_ABS of its fp32
+                score, and the device search's own score of its best hypothesis within 2e-3 of that hypothesis'
+                device teacher-forced score;
+      search    the device's best hypothesis equals the fp32 best, or scores (device numerics) at least the fp32
+                best's device score - BEAM_TAU: the search found a hypothesis as good as the fp32 one up to a
+                near-tie."""
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "turbo_beam.npz"))
+    eng = turbo.engine
+    for ts in (True, False):
+        tag = f"ts{int(ts)}"
+        mnt = int(z[f"{tag}_max_new_tokens"][0])
+        _load(turbo, _clips())
+        eng.generate(2, task="transcribe", max_new_tokens=mnt, return_timestamps=ts, num_beams=5, max_passes=1)
+        assert eng.last_langs == [int(x) for x in z["lang"]]
+        fs = eng._beam_buffers(10)["fin_score"][:10].view(2, 5).cpu().numpy()
+        best = [[int(t) for t in eng.last_passes[i][0]] for i in range(2)]
+        gold = [[int(t) for t in z[f"{tag}_fin_seq"][i, 0] if t >= 0] for i in range(2)]
+        gsc = z[f"{tag}_fin_score"][:, 0]
+        s_gold = _tf_beam_scores(eng, z["lang"], gold, ts)
+        s_best = _tf_beam_scores(eng, z["lang"], best, ts)
+        for i in range(2):
+            print(f"turbo beam {tag} clip {i}: {'exact' if best[i] == gold[i] else 'diverged'}; fp32 best "
+                  f"{gsc[i]:.4f}, its device score {s_gold[i]:.4f}; device best {s_best[i]:.4f} (search {fs[i, 0]:.4f})")
+            assert abs(s_gold[i] - float(gsc[i])) <= BEAM_SCORE_ABS, (tag, i, s_gold[i], gsc[i])
+            assert abs(s_best[i] - float(fs[i, 0])) <= 2e-3, (tag, i, s_best[i], fs[i, 0])
+            if best[i] != gold[i]:
+                assert s_best[i] >= s_gold[i] - BEAM_TAU, (tag, i, s_best[i], s_gold[i])
