@@ -18,6 +18,7 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
                     with their processed top-16 scores
   beam.json         generate(num_beams=5) token sequences (the pipeline's default decode, asr:160-163) of
                     test-mini on three windows, with and without timestamps and with a max_length stop
+  turbo_word.npz    generate(return_token_timestamps=True) at large-v3-turbo dims with the default alignment heads
   turbo_beam.npz    generate(num_beams=5) at large-v3-turbo dims, with and without timestamps: the 5 finished
                     hypotheses and their beam scores (oracle beam search on the fp32 model's logits, checked to
                     return generate()'s best hypothesis)
@@ -574,6 +575,33 @@ def make_turbo_beam(out):
         res[f"{tag}_fin_score"] = np.stack(scores)
         res[f"{tag}_max_new_tokens"] = np.array([mnt], np.int32)
     np.savez_compressed(os.path.join(out, "turbo_beam.npz"), **res)
+
+
+def make_turbo_word(out):
+    """large-v3-turbo, seeded synthetic weights, the engine's default alignment heads (every head of the upper half
+    of the decoder, GenerationSettings.default): generate(return_timestamps=True, return_token_timestamps=True,
+    max_new_tokens=40) on TURBO_CLIPS — token-level timestamps from cross-attention DTW at the benchmarked depth."""
+    from transformers import WhisperFeatureExtractor
+
+    d = PRESETS["large-v3-turbo"]
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    del sd
+    m.generation_config.alignment_heads = [list(h) for h in gen.alignment_heads]
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    cl = clips()
+    res = {}
+    for i, name in enumerate(TURBO_CLIPS):
+        f = fe(cl[name], sampling_rate=16000, return_tensors="pt", return_attention_mask=True)
+        with torch.no_grad():
+            o = m.generate(f["input_features"], attention_mask=f["attention_mask"], task="transcribe",
+                           return_timestamps=True, return_token_timestamps=True, max_new_tokens=40)
+        res[f"seq{i}"] = o["sequences"].numpy().astype(np.int32)
+        res[f"ts{i}"] = o["token_timestamps"].numpy().astype(np.float32)
+        res[f"nframes{i}"] = np.array([int(f["attention_mask"].sum())], np.int32)
+    res["alignment_heads"] = np.array(gen.alignment_heads, np.int32)
+    np.savez_compressed(os.path.join(out, "turbo_word.npz"), **res)
 
 
 TINY_CLIPS = ("speech30", "noise12")

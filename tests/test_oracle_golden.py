@@ -194,3 +194,18 @@ def test_fallback_criteria_match_transformers(oracle_model, gcfg):
         assert cr == c["compression_ratio"]
         assert abs(lp - c["avg_logprob"]) < 1e-3, (name, lp, c["avg_logprob"])
         assert abs(nsp - c["no_speech_prob"]) < 1e-3 * c["no_speech_prob"] + 1e-9, (name, nsp, c["no_speech_prob"])
+
+
+def test_turbo_beam_and_word_goldens_consistent():
+    """Shape / ordering invariants of the large-v3-turbo beam and token-timestamp fixtures (made by
+    make_golden.py turbo_beam / turbo_word from transformers; checked against the engine by tests/test_gpu_turbo.py)."""
+    zb = np.load(os.path.join(G, "turbo_beam.npz"))
+    for tag in ("ts1", "ts0"):
+        sc, seq = zb[f"{tag}_fin_score"], zb[f"{tag}_fin_seq"]
+        assert sc.shape == (2, 5) and seq.shape[:2] == (2, 5)
+        assert np.all(np.diff(sc, axis=1) <= 0)  # finished hypotheses best first
+        assert seq.shape[2] <= int(zb[f"{tag}_max_new_tokens"][0])
+    zw = np.load(os.path.join(G, "turbo_word.npz"))
+    for i in range(2):
+        assert zw[f"seq{i}"].shape == zw[f"ts{i}"].shape
+        assert np.all(np.isfinite(zw[f"ts{i}"])) and np.all(zw[f"ts{i}"] >= 0)
