@@ -225,7 +225,9 @@ class WhisperEngine:
         self.suppress_bits = torch.zeros((V + 31) // 32, dtype=torch.int32, device=dev)
         self.set_suppress_tokens(gen.suppress_tokens)
         # concurrent decode chains in the generation loop (measured: two 12-row chains on two streams run no faster
-        # than one 24-row chain on MI355X, so one by default)
+        # than one 24-row chain on MI355X, so one by default; re-measured in round 3 for a pass with no encoder
+        # beside it, scripts/exp/chains_ab.py: 15 rows 48.3 ms with one chain vs 52.7-194 ms with two, 24 rows 57.4 vs
+        # 50.7-56.2 ms: no dependable gain)
         self.n_chains = 1
         self._chain_streams = [torch.cuda.Stream(self.device, priority=-1) for _ in range(self.n_chains)]
         self._own_streams = {x.cuda_stream for x in [self.stream, self.enc_stream] + self._chain_streams}
