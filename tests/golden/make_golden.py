@@ -18,6 +18,8 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
                     with their processed top-16 scores
   beam.json         generate(num_beams=5) token sequences (the pipeline's default decode, asr:160-163) of
                     test-mini on three windows, with and without timestamps and with a max_length stop
+  large_v3.npz      whisper-large-v3 dims (the reference's default model: 32-layer decoder): encoder rows,
+                    teacher-forced logits, generate() passes with processed top-16 scores
   turbo_word.npz    generate(return_token_timestamps=True) at large-v3-turbo dims with the default alignment heads
   turbo_beam.npz    generate(num_beams=5) at large-v3-turbo dims, with and without timestamps: the 5 finished
                     hypotheses and their beam scores (oracle beam search on the fp32 model's logits, checked to
@@ -602,6 +604,58 @@ def make_turbo_word(out):
         res[f"nframes{i}"] = np.array([int(f["attention_mask"].sum())], np.int32)
     res["alignment_heads"] = np.array(gen.alignment_heads, np.int32)
     np.savez_compressed(os.path.join(out, "turbo_word.npz"), **res)
+
+
+def make_large_v3(out):
+    """openai/whisper-large-v3 dims — the reference's default model (vocalis/core/audio_pipeline.py:171): the turbo
+    encoder with a 32-layer decoder — with the seeded synthetic weights, on clip speech30: encoder rows, teacher-forced
+    raw logits over 24 positions, and generate(num_beams=1, return_timestamps=True, max_new_tokens=40) passes with
+    their processed top-16 scores (transformers on CPU fp32)."""
+    from transformers import WhisperFeatureExtractor
+
+    d = PRESETS["large-v3"]
+    gen = GenerationSettings.default(d)
+    st = gen.special
+    g = wo.GenCfg(d.vocab, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate,
+                  st.notimestamps, gen.suppress_tokens, gen.begin_suppress_tokens)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    del sd
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    feats = fe(clips()["speech30"], sampling_rate=16000, return_tensors="np")["input_features"]
+    res = {}
+    with torch.no_grad():
+        enc = m.model.encoder(torch.from_numpy(feats)).last_hidden_state.numpy()
+        lang = m.detect_language(input_features=torch.from_numpy(feats)).numpy()
+        o = m.generate(torch.from_numpy(feats), task="transcribe", return_timestamps=True, num_beams=1,
+                       max_new_tokens=40, return_segments=True)
+    res["enc_rows_idx"] = np.array([0, 1, 750, 1499])
+    res["enc_rows"] = enc[0, res["enc_rows_idx"]].astype(np.float32)
+    res["lang"] = lang.astype(np.int32)
+    res["gen_sequence"] = o["sequences"].numpy()[0].astype(np.int32)
+    pr = [st.sot, int(lang[0]), st.transcribe]
+    seek, ti, tv, mg, toks_all, seeks = 0, [], [], [], [], []
+    for p in _passes_from_segments(o["segments"][0], 3):
+        toks = p[: p.index(st.eot) + 1] if st.eot in p else p
+        a, b, c = _teacher_forced_pass_scores(m, feats[0], seek, pr, toks, g)
+        ti.append(a); tv.append(b); mg.append(c); toks_all.append(np.array(toks, np.int32)); seeks.append(seek)
+        seq = toks[:-1] if toks and toks[-1] == st.eot else toks
+        _, off = wo.retrieve_segment(seq, 3000 - seek, g.ts_begin)
+        seek += off
+    res["pass_len"] = np.array([len(x) for x in toks_all], np.int32)
+    res["pass_seek"] = np.array(seeks, np.int32)
+    res["pass_tokens"] = np.concatenate(toks_all)
+    res["top_idx"], res["top_val"], res["ts_margin"] = np.concatenate(ti), np.concatenate(tv), np.concatenate(mg)
+    p0 = pr + [int(t) for t in toks_all[0][:21]]
+    res["tf_input_ids"] = np.array(p0[:24])
+    with torch.no_grad():
+        lg = m(input_features=torch.from_numpy(feats), decoder_input_ids=torch.tensor([p0[:24]])).logits[0].numpy()
+    top = np.argsort(-lg, axis=1, kind="stable")[:, :16]
+    res["tf_top_idx"] = top
+    res["tf_top_val"] = np.take_along_axis(lg, top, 1).astype(np.float32)
+    res["tf_lse"] = (np.log(np.exp(lg - lg.max(1, keepdims=True)).sum(1)) + lg.max(1)).astype(np.float64)
+    res["sot_lang_logits"] = lg[0, st.lang_begin: st.lang_end].astype(np.float32)  # detect_language's candidates
+    np.savez_compressed(os.path.join(out, "large_v3.npz"), **res)
 
 
 TINY_CLIPS = ("speech30", "noise12")
