@@ -60,9 +60,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU over RCCL; TW_DIST_BACKEND=gloo is a rehearsal of the multi-rank control path on fewer GPUs
+    # than ranks (ranks share the cards round-robin; the numbers are then not a scaling measurement)
+    backend = os.environ.get("TW_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from twamd.config import PRESETS, GenerationSettings
     from twamd.engine import WhisperEngine
@@ -131,7 +139,7 @@ def main():
     fam = eng.timer_summary()
     eng.timers, eng.timer_families = None, None
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=eng.device)
+        t = torch.tensor([dt], dtype=torch.float64, device=eng.device if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     if a.profile_only:
