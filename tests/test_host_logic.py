@@ -208,3 +208,32 @@ def test_fallback_sequence_cut():
     assert fallback_sequence([5, 6, 7], 50257, 50257) == [5, 6, 7]
     assert fallback_sequence([5, 6, 50257], 50257, 50257) == [5, 6, 50257]
     assert fallback_sequence([5, 0, 0], 0, 50257) == [5]
+
+
+def test_lcs_vectorised_scan_equals_sequential_scan():
+    """find_longest_common_sequence's diagonal-sum form (no token timestamps) picks the same overlap as the
+    sequential scan of tokenization_whisper.py:1153-1270 (restated here) on random and planted-overlap runs."""
+    from twamd.tokenizer import find_longest_common_sequence
+
+    def scan(sequences):
+        left, total = sequences[0], []
+        for right in sequences[1:]:
+            L, R = len(left), len(right)
+            best, idx = 0.0, (L, L, 0, 0)
+            for i in range(1, L + R):
+                ls, le, rs, re_ = max(0, L - i), min(L, L + R - i), max(0, i - L), min(R, i)
+                m = sum(1 for k in range(le - ls) if left[ls + k] == right[rs + k])
+                if m > 1 and m / i + i / 10000.0 > best:
+                    best, idx = m / i + i / 10000.0, (ls, le, rs, re_)
+            ls, le, rs, re_ = idx
+            total.extend(left[:(le + ls) // 2])
+            left = right[(re_ + rs) // 2:]
+        return total + list(left)
+
+    rng = np.random.default_rng(11)
+    for _ in range(1500):
+        V = int(rng.choice([2, 4, 16, 50000]))
+        seqs = [[int(x) for x in rng.integers(0, V, rng.integers(0, 40))] for _ in range(int(rng.integers(2, 5)))]
+        if len(seqs[0]) > 4 and rng.random() < 0.5:
+            seqs[1] = seqs[0][-int(rng.integers(1, len(seqs[0]))):] + seqs[1]
+        assert find_longest_common_sequence(seqs) == scan(seqs), seqs

@@ -93,6 +93,10 @@ class WhisperVocab:
         self.special = special
         self.byte_decoder = {v: k for k, v in bytes_to_unicode().items()}
         self.all_special_ids = set(special.special_ids())
+        # per token: its bytes when every character is in the byte-level table (None otherwise), so decode() of
+        # byte-level runs is one join + one UTF-8 decode (rank 0 stitches every window of a sharded hour on the host)
+        bd = self.byte_decoder
+        self._token_bytes = [bytes(bd[c] for c in t) if all(c in bd for c in t) else None for t in self.id_to_token]
 
     @staticmethod
     def synthetic(special: SpecialTokens) -> "WhisperVocab":
@@ -119,6 +123,11 @@ class WhisperVocab:
 
     def decode(self, ids: Sequence[int]) -> str:
         """tokenizer.decode(ids) for text tokens (specials render as their strings)."""
+        tb = self._token_bytes
+        try:
+            return b"".join(tb[i] for i in ids).decode("utf-8", errors="replace")
+        except TypeError:  # a token with characters outside the byte table: the general path below
+            pass
         text = "".join(self.id_to_token[i] for i in ids)
         data = bytearray()
         out = []
@@ -152,22 +161,33 @@ def find_longest_common_sequence(sequences: List[List[int]], token_timestamp_seq
         best = 0.0
         best_idx = (left_len, left_len, 0, 0)
         right_len = len(right)
-        la = np.asarray(left)
-        ra = np.asarray(right)
-        for i in range(1, left_len + right_len):
-            eps = i / 10000.0
-            ls, le = max(0, left_len - i), min(left_len, left_len + right_len - i)
-            rs, re_ = max(0, i - left_len), min(right_len, i)
-            if with_ts:
+        if with_ts:
+            for i in range(1, left_len + right_len):
+                eps = i / 10000.0
+                ls, le = max(0, left_len - i), min(left_len, left_len + right_len - i)
+                rs, re_ = max(0, i - left_len), min(right_len, i)
                 rts = token_timestamp_sequences[seq_idx + 1]
                 matches = sum(1 for k in range(le - ls)
                               if left[ls + k] == right[rs + k] and tuple(left_ts[ls + k]) <= tuple(rts[rs + k]))
-            else:
-                matches = int(np.sum(la[ls:le] == ra[rs:re_])) if le > ls else 0
-            matching = matches / i + eps
-            if matches > 1 and matching > best:
-                best = matching
-                best_idx = (ls, le, rs, re_)
+                matching = matches / i + eps
+                if matches > 1 and matching > best:
+                    best = matching
+                    best_idx = (ls, le, rs, re_)
+        elif left_len and right_len:
+            # the same scan, vectorised: offset i aligns left[a] with right[b] where b - a = i - left_len, so the
+            # matches at every offset are the diagonal sums of the equality matrix; the first offset with the
+            # largest matches / i + i / 10000 (matches > 1) wins, as the strict '>' of the sequential scan picks it
+            a, b = np.nonzero(np.asarray(left)[:, None] == np.asarray(right)[None, :])
+            n = left_len + right_len
+            matches = np.bincount(b - a + left_len, minlength=n)[1:n]
+            i = np.arange(1, n)
+            matching = matches / i + i / 10000.0
+            ok = matches > 1
+            if ok.any():
+                k = int(np.argmax(np.where(ok, matching, -np.inf)))
+                i_best = k + 1
+                best_idx = (max(0, left_len - i_best), min(left_len, left_len + right_len - i_best),
+                            max(0, i_best - left_len), min(right_len, i_best))
         ls, le, rs, re_ = best_idx
         lmid = (le + ls) // 2
         rmid = (re_ + rs) // 2
