@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--profile-only", action="store_true", help="warmup + steps only (for rocprofv3)")
+    ap.add_argument("--eos", action="store_true",
+                    help="free-running decode (SURVEY §8d, reported separately): EOS not suppressed, each window stops "
+                         "at its EOS or after --decode-tokens; the roofline accounting's fixed length is the default")
     return ap.parse_args()
 
 
@@ -97,7 +100,8 @@ def main():
         eng = WhisperEngine(w, gen, max_batch=B, device=f"cuda:{local}", enc_fp8=fp8)
     dom = "gemm_mx" if fp8 else "gemm_big"
     peak = FP8_DENSE_PEAK_TFLOPS if fp8 else BF16_DENSE_PEAK_TFLOPS
-    eng.set_suppress_tokens(list(gen.suppress_tokens) + [gen.special.eot])  # fixed decode length
+    if not a.eos:
+        eng.set_suppress_tokens(list(gen.suppress_tokens) + [gen.special.eot])  # fixed decode length
     from twamd import dist as twd
     if strong:
         # 1 h of synthetic speech-like audio (120 seeded 30-s windows back to back), on the host as a caller's array
@@ -188,8 +192,10 @@ def main():
                                   f"the GPUs, engine batches of <= {B} (sub-batches: "
                                   f"{tr.sub_batch_min or 'off'}), " if strong else
                                   f"batch={B} x 30s windows per GPU, ")
-                               + f"greedy, {T} new tokens/window (EOS suppressed, one seek pass), timestamps on, "
-                               "language detected",
+                               + (f"greedy, free-running (EOS allowed, at most {T} new tokens/window), one seek "
+                                  "pass, timestamps on, language detected" if a.eos else
+                                  f"greedy, {T} new tokens/window (EOS suppressed, one seek pass), timestamps on, "
+                                  "language detected"),
                    "c3_share": a.c3_share if strong else None,
                    "global_batch": int(audio_s // 30), "seq_len": 3000, "parallelism": f"chunk-dp{world}",
                    "decode_tokens_per_window": T, "mean_tokens_out": float(np.mean(n_tok))},
@@ -207,7 +213,9 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0:
-        out["parity"], out["parity_detail"] = (parity_vs_golden(eng, B, T, a.model, fp8) if not strong else
+        out["parity"], out["parity_detail"] = (parity_vs_golden(eng, B, T, a.model, fp8) if not strong and not a.eos else
+                                               (None, {"skipped": "free-running decode: the golden is the EOS-suppressed "
+                                                                  "decode"}) if a.eos else
                                                (None, {"skipped": "c3 windows differ from the golden's; the same "
                                                                   "engine's parity is the c2 line's"}))
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
