@@ -18,6 +18,7 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
                     with their processed top-16 scores
   beam.json         generate(num_beams=5) token sequences (the pipeline's default decode, asr:160-163) of
                     test-mini on three windows, with and without timestamps and with a max_length stop
+  edge.json         the ASR pipeline on empty and sub-frame inputs (outputs or the exception transcribe() wraps)
   large_v3.npz      whisper-large-v3 dims (the reference's default model: 32-layer decoder): encoder rows,
                     teacher-forced logits, generate() passes with processed top-16 scores
   turbo_word.npz    generate(return_token_timestamps=True) at large-v3-turbo dims with the default alignment heads
@@ -656,6 +657,34 @@ def make_large_v3(out):
     res["tf_lse"] = (np.log(np.exp(lg - lg.max(1, keepdims=True)).sum(1)) + lg.max(1)).astype(np.float64)
     res["sot_lang_logits"] = lg[0, st.lang_begin: st.lang_end].astype(np.float32)  # detect_language's candidates
     np.savez_compressed(os.path.join(out, "large_v3.npz"), **res)
+
+
+def make_edge(out):
+    """The ASR pipeline (test-mini, greedy, 8 new tokens, timestamps) on empty and sub-frame inputs, with the
+    reference's chunking (60 / 5) and without: the output, or the exception type and message the reference's
+    transcribe() would wrap as {"error": "Transcription error: <message>"}."""
+    from transformers import AutomaticSpeechRecognitionPipeline, WhisperFeatureExtractor
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    pipe = AutomaticSpeechRecognitionPipeline(model=m, feature_extractor=fe, tokenizer=hf_tokenizer(gen.special),
+                                              device=-1)
+    cases = []
+    for n in (0, 1, 160, 1600):
+        for name, kw in (("ref_60_5", dict(chunk_length_s=60, stride_length_s=5, batch_size=32)), ("plain", {})):
+            c = {"n_samples": n, "name": name, "kwargs": kw}
+            try:
+                c["output"] = _jsonable(pipe(np.zeros(n, np.float32), return_timestamps=True,
+                                             generate_kwargs={"task": "transcribe", "num_beams": 1,
+                                                              "max_new_tokens": 8}, **kw))
+            except Exception as e:  # noqa: BLE001 - the reference's transcribe() catches everything
+                c["error"] = {"type": type(e).__name__, "message": str(e)}
+            cases.append(c)
+    with open(os.path.join(out, "edge.json"), "w") as f:
+        json.dump({"dims": "test-mini", "cases": cases}, f, indent=1)
 
 
 TINY_CLIPS = ("speech30", "noise12")

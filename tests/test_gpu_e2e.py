@@ -206,3 +206,24 @@ def test_pipelined_batches_equal_sequential(tr):
 
     got = eng.run_batches([2, 2, 2], load=load, task="transcribe", max_new_tokens=30)
     assert got == seq_ref
+
+
+def test_pipeline_edge_inputs_match_transformers(tr):
+    """Empty and sub-frame inputs with the reference's chunking and without (tests/golden/edge.json): the same
+    output as the transformers pipeline, or the same exception type and message (an empty chunked input raises
+    StopIteration, which the reference's transcribe() turns into {"error": "Transcription error: "})."""
+    gold = json.load(open(os.path.join(G, "edge.json")))
+    for c in gold["cases"]:
+        kw = dict(c["kwargs"])
+        call = lambda: tr(np.zeros(c["n_samples"], np.float32), return_timestamps=True,  # noqa: E731
+                          generate_kwargs={"task": "transcribe", "num_beams": 1, "max_new_tokens": 8}, **kw)
+        if "error" in c:
+            with pytest.raises(Exception) as ei:
+                call()
+            assert (type(ei.value).__name__, str(ei.value)) == (c["error"]["type"], c["error"]["message"]), c
+            continue
+        r = call()
+        ref = c["output"]
+        assert r["text"] == ref["text"], (c["n_samples"], c["name"])
+        assert [(list(x["timestamp"]), x["text"]) for x in r["chunks"]] == \
+            [(list(x["timestamp"]), x["text"]) for x in ref["chunks"]], (c["n_samples"], c["name"])

@@ -149,6 +149,9 @@ class TurboTranscriber:
             raise load_err
         if chunk_length_s:
             windows = list(chunk_windows(len(wav), chunk_length_s, stride_length_s, self.sampling_rate))
+            if not windows:  # an empty input: the pipeline's chunk iterator yields nothing and its first next()
+                # raises StopIteration (tests/golden/edge.json), which transcribe() reports as "Transcription error: "
+                raise StopIteration
             with_stride = True
         else:
             if len(wav) > CHUNK_SAMPLES:
