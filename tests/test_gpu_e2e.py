@@ -227,3 +227,28 @@ def test_pipeline_edge_inputs_match_transformers(tr):
         assert r["text"] == ref["text"], (c["n_samples"], c["name"])
         assert [(list(x["timestamp"]), x["text"]) for x in r["chunks"]] == \
             [(list(x["timestamp"]), x["text"]) for x in ref["chunks"]], (c["n_samples"], c["name"])
+
+
+def test_more_than_32_decoder_rows_equal_small_batches():
+    """Engine batches whose decoder rows exceed one 32-row packed view — config 5's 64 windows, beam-5 over more
+    than 6 windows (the drop-in's default decode) — give every window the same tokens as small batches (greedy and
+    beam rows are independent; the per-view kernels see the same rows)."""
+    from twamd.synth_audio import workload
+
+    big = TurboTranscriber.from_pretrained("test-mini", seed=1234, max_batch=40, max_beams=5)
+    eng = big.engine
+    wav = workload(40, 30.0, seed=77)
+    eng.wave[:40].copy_(torch.from_numpy(wav))
+    eng.logmel(40)
+    greedy = eng.generate(40, task="transcribe", max_new_tokens=16)
+    for b0 in range(0, 40, 8):
+        eng.wave[:8].copy_(torch.from_numpy(wav[b0: b0 + 8]))
+        eng.logmel(8)
+        assert eng.generate(8, task="transcribe", max_new_tokens=16) == greedy[b0: b0 + 8], b0
+    eng.wave[:8].copy_(torch.from_numpy(wav[:8]))
+    eng.logmel(8)
+    beams = eng.generate(8, task="transcribe", max_new_tokens=12, num_beams=5)  # 40 decoder rows
+    for b0 in range(0, 8, 2):
+        eng.wave[:2].copy_(torch.from_numpy(wav[b0: b0 + 2]))
+        eng.logmel(2)
+        assert eng.generate(2, task="transcribe", max_new_tokens=12, num_beams=5) == beams[b0: b0 + 2], b0

@@ -631,6 +631,10 @@ class WhisperEngine:
                 embed_next: bool = False) -> None:
         """Processors + greedy selection for the view's rows; embed_next: also the head of the next step (the chosen
         token's embedding into xd and layer 0's self_attn_layer_norm into the view's LN buffer, one fused launch)."""
+        if v is None and R > 32:  # per-row selection over the <= 32-row views decoder_step(R) ran (beam / config-5 rows)
+            for r0 in range(0, R, 32):
+                self._select(min(32, R - r0), params, tokens, self._view(r0, min(32, R - r0)), embed_next)
+            return
         v = v or self._view(0, R)
         if embed_next:
             L0 = self.w.dec[0]
