@@ -18,6 +18,7 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
                     with their processed top-16 scores
   beam.json         generate(num_beams=5) token sequences (the pipeline's default decode, asr:160-163) of
                     test-mini on three windows, with and without timestamps and with a max_length stop
+  beam_long.json    the reference's call (default beam-5) on 8 minutes of audio at test-mini (50 beam rows per batch)
   edge.json         the ASR pipeline on empty and sub-frame inputs (outputs or the exception transcribe() wraps)
   large_v3.npz      whisper-large-v3 dims (the reference's default model: 32-layer decoder): encoder rows,
                     teacher-forced logits, generate() passes with processed top-16 scores
@@ -685,6 +686,26 @@ def make_edge(out):
             cases.append(c)
     with open(os.path.join(out, "edge.json"), "w") as f:
         json.dump({"dims": "test-mini", "cases": cases}, f, indent=1)
+
+
+def make_beam_long(out):
+    """The reference's call (chunk_length_s=60, stride_length_s=5, batch_size=32, task only: the pipeline's default
+    beam-5) on 8 minutes of audio at test-mini: 10 windows, so the drop-in's engine batch carries 50 beam rows."""
+    from transformers import AutomaticSpeechRecognitionPipeline, WhisperFeatureExtractor
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    pipe = AutomaticSpeechRecognitionPipeline(model=m, feature_extractor=fe, tokenizer=hf_tokenizer(gen.special),
+                                              device=-1)
+    audio = np.concatenate([speech_like(200.0, 21), white_noise(80.0, 22), speech_like(200.0, 23)])  # 480 s
+    kw = dict(chunk_length_s=60, stride_length_s=5, batch_size=32)
+    r = pipe(audio.copy(), generate_kwargs={"task": "transcribe", "max_new_tokens": 24}, return_timestamps=True, **kw)
+    with open(os.path.join(out, "beam_long.json"), "w") as f:
+        json.dump({"dims": "test-mini", "audio": "speech_like(200,21)+white_noise(80,22)+speech_like(200,23)",
+                   "kwargs": kw, "max_new_tokens": 24, "output": _jsonable(r)}, f)
 
 
 TINY_CLIPS = ("speech30", "noise12")

@@ -164,3 +164,21 @@ def test_pipeline_beam5_matches_transformers_pipeline(mini, name):
     assert r["text"] == ref["text"]
     assert [(tuple(c["timestamp"]), c["text"]) for c in r["chunks"]] == \
         [(tuple(c["timestamp"]), c["text"]) for c in ref["chunks"]]
+
+
+def test_default_callable_long_audio_matches_transformers_pipeline():
+    """The drop-in as from_pretrained builds it by default (engine batches of 24 windows, beam-5 rows) with the
+    reference's call on 8 minutes of audio (10 windows: 50 decoder rows in one batch) reproduces the transformers
+    pipeline (tests/golden/beam_long.json)."""
+    from twamd.pipeline import TurboTranscriber
+    from twamd.synth_audio import speech_like, white_noise
+
+    gold = json.load(open(os.path.join(G, "beam_long.json")))
+    tr = TurboTranscriber.from_pretrained("test-mini", seed=1234)
+    audio = np.concatenate([speech_like(200.0, 21), white_noise(80.0, 22), speech_like(200.0, 23)])
+    r = tr(audio, generate_kwargs={"task": "transcribe", "max_new_tokens": gold["max_new_tokens"]},
+           return_timestamps=True, **gold["kwargs"])
+    ref = gold["output"]
+    assert r["text"] == ref["text"]
+    assert [(tuple(c["timestamp"]), c["text"]) for c in r["chunks"]] == \
+        [(tuple(c["timestamp"]), c["text"]) for c in ref["chunks"]]
