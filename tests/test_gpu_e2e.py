@@ -245,6 +245,22 @@ def test_more_than_32_decoder_rows_equal_small_batches():
         eng.wave[:8].copy_(torch.from_numpy(wav[b0: b0 + 8]))
         eng.logmel(8)
         assert eng.generate(8, task="transcribe", max_new_tokens=16) == greedy[b0: b0 + 8], b0
+    # segment criteria without resampling (temperature 0 only: greedy passes, per-window criteria, no-speech skip)
+    from twamd.segments import FallbackConfig
+
+    fb = FallbackConfig(temperatures=(0.0,), logprob_threshold=-3.0, no_speech_threshold=0.5)
+    eng.wave[:40].copy_(torch.from_numpy(wav))
+    eng.logmel(40)
+    crit = eng.generate(40, task="transcribe", max_new_tokens=16, fallback=fb)
+    for b0 in range(0, 40, 8):
+        eng.wave[:8].copy_(torch.from_numpy(wav[b0: b0 + 8]))
+        eng.logmel(8)
+        assert eng.generate(8, task="transcribe", max_new_tokens=16, fallback=fb) == crit[b0: b0 + 8], b0
+    # and a sampled fallback over 40 rows runs (its sampler keys depend on the window's place in the call)
+    eng.wave[:40].copy_(torch.from_numpy(wav))
+    eng.logmel(40)
+    eng.generate(40, task="transcribe", max_new_tokens=16,
+                 fallback=FallbackConfig(temperatures=(0.0, 0.5), logprob_threshold=-0.5))
     eng.wave[:8].copy_(torch.from_numpy(wav[:8]))
     eng.logmel(8)
     beams = eng.generate(8, task="transcribe", max_new_tokens=12, num_beams=5)  # 40 decoder rows
