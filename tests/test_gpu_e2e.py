@@ -261,6 +261,9 @@ def test_more_than_32_decoder_rows_equal_small_batches():
     eng.logmel(40)
     eng.generate(40, task="transcribe", max_new_tokens=16,
                  fallback=FallbackConfig(temperatures=(0.0, 0.5), logprob_threshold=-0.5))
+    # token-level timestamps over 40 rows run (their per-pass standardisation spans the batch, so no comparison)
+    eng.generate(40, task="transcribe", max_new_tokens=16, word_timestamps=True, num_frames=[3000] * 40)
+    assert len(eng.last_token_timestamps) == 40
     eng.wave[:8].copy_(torch.from_numpy(wav[:8]))
     eng.logmel(8)
     beams = eng.generate(8, task="transcribe", max_new_tokens=12, num_beams=5)  # 40 decoder rows
