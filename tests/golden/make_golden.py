@@ -19,6 +19,7 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
   beam.json         generate(num_beams=5) token sequences (the pipeline's default decode, asr:160-163) of
                     test-mini on three windows, with and without timestamps and with a max_length stop
   beam_long.json    the reference's call (default beam-5) on 8 minutes of audio at test-mini (50 beam rows per batch)
+  options.json      the ASR pipeline with translate (reference call), no timestamps, a forced language, return_language
   edge.json         the ASR pipeline on empty and sub-frame inputs (outputs or the exception transcribe() wraps)
   large_v3.npz      whisper-large-v3 dims (the reference's default model: 32-layer decoder): encoder rows,
                     teacher-forced logits, generate() passes with processed top-16 scores
@@ -706,6 +707,42 @@ def make_beam_long(out):
     with open(os.path.join(out, "beam_long.json"), "w") as f:
         json.dump({"dims": "test-mini", "audio": "speech_like(200,21)+white_noise(80,22)+speech_like(200,23)",
                    "kwargs": kw, "max_new_tokens": 24, "output": _jsonable(r)}, f)
+
+
+def make_options(out):
+    """The ASR pipeline at test-mini on 75 s of audio with the call options a user of the reference's transcribe()
+    can reach: task="translate" with the reference's call (default beam-5), return_timestamps=False, a forced
+    language, return_language=True (greedy where not the reference's call)."""
+    from transformers import AutomaticSpeechRecognitionPipeline, WhisperFeatureExtractor
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    pipe = AutomaticSpeechRecognitionPipeline(model=m, feature_extractor=fe, tokenizer=hf_tokenizer(gen.special),
+                                              device=-1)
+    audio = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)])
+    ref = dict(chunk_length_s=60, stride_length_s=5, batch_size=32)
+    cases = [
+        ("translate_ref_call", ref, {"task": "translate", "max_new_tokens": 24}, True, {}),
+        ("translate_greedy", ref, {"task": "translate", "num_beams": 1, "max_new_tokens": 24}, True, {}),
+        ("no_timestamps", dict(chunk_length_s=30, stride_length_s=0, batch_size=2),
+         {"task": "transcribe", "num_beams": 1, "max_new_tokens": 24}, False, {}),
+        ("language_fr", ref, {"task": "transcribe", "language": "fr", "num_beams": 1, "max_new_tokens": 24}, True, {}),
+        ("return_language", ref, {"task": "transcribe", "num_beams": 1, "max_new_tokens": 24}, True,
+         {"return_language": True}),
+    ]
+    res = []
+    for name, kw, gk, ts, extra in cases:
+        c = {"name": name, "kwargs": kw, "generate_kwargs": gk, "return_timestamps": ts, "extra": extra}
+        try:
+            c["output"] = _jsonable(pipe(audio.copy(), generate_kwargs=dict(gk), return_timestamps=ts, **kw, **extra))
+        except Exception as e:  # noqa: BLE001 - recorded as the reference would surface it
+            c["error"] = {"type": type(e).__name__, "message": str(e)}
+        res.append(c)
+    with open(os.path.join(out, "options.json"), "w") as f:
+        json.dump({"dims": "test-mini", "audio": "speech_like(40,5)+white_noise(35,11)", "cases": res}, f, indent=1)
 
 
 TINY_CLIPS = ("speech30", "noise12")

@@ -271,3 +271,82 @@ def test_more_than_32_decoder_rows_equal_small_batches():
         eng.wave[:2].copy_(torch.from_numpy(wav[b0: b0 + 2]))
         eng.logmel(2)
         assert eng.generate(2, task="transcribe", max_new_tokens=12, num_beams=5) == beams[b0: b0 + 2], b0
+
+
+BEAM_TAU = 0.1  # beam-score units (processed log-prob per generated token), as tests/test_gpu_turbo.py
+
+
+def _beam_score(orc, enc, prompt, toks, g, use_ts):
+    """fp32 beam score of one hypothesis (sum of the processed log-probs / its length), teacher-forced through the
+    oracle decoder."""
+    cache = orc.new_cache(enc)
+    for t in prompt[:-1]:
+        orc.decoder_step(t, cache)
+    logits = orc.decoder_step(prompt[-1], cache)
+    sc, hist = 0.0, []
+    for t in toks:
+        sc += float(wo.process_logits(wo._log_softmax32(logits), hist, g, use_ts)[t])
+        hist.append(t)
+        logits = orc.decoder_step(t, cache)
+    return sc / len(toks)
+
+
+def _beam_passes_within_tau(t, oracle, audio, kw, task, max_new):
+    """Replay every window's beam-5 seek passes on the fp32 oracle (its beam search is pinned to transformers):
+    passes equal until the first that differs, whose device hypothesis must score within BEAM_TAU of the oracle's
+    best (a near-tie of the random-weight model ranked the other way by bf16 logits)."""
+    from twamd.frontend import chunk_windows
+
+    g = _gcfg()
+    diverged = 0
+    for k, w in enumerate(chunk_windows(len(audio), kw["chunk_length_s"], kw["stride_length_s"], 16000)):
+        feats = wo.log_mel(audio[w.start: w.start + min(w.length, 480000)], D.n_mels)
+        prompt = [g.sot, int(t.last_window_langs[k]), g.translate if task == "translate" else g.transcribe]
+        seek = 0
+        for raw in t.last_window_passes[k]:
+            seg = np.zeros_like(feats)
+            seg[:, : 3000 - seek] = feats[:, seek:]
+            enc = oracle.encode(seg)
+            ora = wo.beam_pass(oracle, enc, prompt, max_new, g, True, 5)
+            dev = [int(x) for x in raw]
+            dev = dev[: dev.index(g.eot) + 1] if g.eot in dev else dev
+            if ora != dev:
+                gap = _beam_score(oracle, enc, prompt, ora, g, True) - _beam_score(oracle, enc, prompt, dev, g, True)
+                print(f"window {k}: device pass leaves the fp32 beam search, fp32 score gap {gap:.4f}")
+                assert gap <= BEAM_TAU, (k, gap)
+                diverged += 1
+                break
+            seq = dev[:-1] if dev and dev[-1] == g.eot else dev
+            _, off = wo.retrieve_segment(seq, 3000 - seek, g.ts_begin)
+            seek += off
+    return diverged
+
+
+@pytest.mark.parametrize("name", ["translate_ref_call", "translate_greedy", "no_timestamps", "language_fr"])
+def test_pipeline_call_options_match_transformers(tr, oracle, name):
+    """Call options a user of the reference's transcribe() reaches (tests/golden/options.json): task="translate"
+    with the reference's call (the pipeline's default beam-5) and greedy, return_timestamps=False, a forced language:
+    the transformers pipeline's output exactly, or for beam-5, where the text differs, every seek pass equal to the
+    fp32 oracle's beam search up to one whose hypothesis scores within BEAM_TAU of the oracle's best. (The
+    golden's return_language=True case raises IndexError inside transformers 5.15's pipeline batching; the reference
+    never passes it, so it is recorded, not compared.)"""
+    from twamd.synth_audio import speech_like, white_noise
+
+    gold = json.load(open(os.path.join(G, "options.json")))
+    c = next(x for x in gold["cases"] if x["name"] == name)
+    audio = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)])
+    t = TurboTranscriber.from_pretrained("test-mini", seed=1234, max_batch=4, max_beams=5)
+    r = t(audio, generate_kwargs=dict(c["generate_kwargs"]), return_timestamps=c["return_timestamps"], **c["kwargs"],
+          **c["extra"])
+    ref = c["output"]
+    if r["text"] != ref["text"] and c["generate_kwargs"].get("num_beams", 5) > 1:
+        # beam-5 at a near-tie: every device pass checked against the fp32 beam search instead
+        assert _beam_passes_within_tau(t, oracle, audio, c["kwargs"], c["generate_kwargs"]["task"],
+                                       c["generate_kwargs"]["max_new_tokens"]) > 0
+        return
+    assert r["text"] == ref["text"]
+    if "chunks" in ref:
+        assert [(tuple(x["timestamp"]), x["text"]) for x in r["chunks"]] == \
+            [(tuple(x["timestamp"]), x["text"]) for x in ref["chunks"]]
+    else:
+        assert "chunks" not in r
