@@ -20,6 +20,7 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
                     test-mini on three windows, with and without timestamps and with a max_length stop
   beam_long.json    the reference's call (default beam-5) on 8 minutes of audio at test-mini (50 beam rows per batch)
   options.json      the ASR pipeline with translate (reference call), no timestamps, a forced language, return_language
+  sweep.json        the ASR pipeline over chunk / stride / batch / beam / timestamp / task / language variations
   edge.json         the ASR pipeline on empty and sub-frame inputs (outputs or the exception transcribe() wraps)
   large_v3.npz      whisper-large-v3 dims (the reference's default model: 32-layer decoder): encoder rows,
                     teacher-forced logits, generate() passes with processed top-16 scores
@@ -743,6 +744,53 @@ def make_options(out):
         res.append(c)
     with open(os.path.join(out, "options.json"), "w") as f:
         json.dump({"dims": "test-mini", "audio": "speech_like(40,5)+white_noise(35,11)", "cases": res}, f, indent=1)
+
+
+SWEEP_CASES = [  # name, audio [(kind, seconds, seed)], pipeline kwargs, generate_kwargs, return_timestamps
+    ("c20_s4_greedy", [("speech", 50.0, 31), ("noise", 20.0, 32)], dict(chunk_length_s=20, stride_length_s=4, batch_size=3),
+     {"task": "transcribe", "num_beams": 1, "max_new_tokens": 32}, True),
+    ("c45_asym_beam3", [("speech", 70.0, 33)], dict(chunk_length_s=45, stride_length_s=(6, 3), batch_size=4),
+     {"task": "transcribe", "num_beams": 3, "max_new_tokens": 20}, True),
+    ("c30_greedy_nots", [("noise", 30.0, 34), ("speech", 40.0, 35)], dict(chunk_length_s=30, stride_length_s=0, batch_size=5),
+     {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40}, False),
+    ("nochunk_beam5", [("speech", 25.0, 36)], {}, {"task": "transcribe", "num_beams": 5, "max_new_tokens": 24}, True),
+    ("c15_translate_greedy", [("speech", 60.0, 37), ("silence", 10.0, 0)],
+     dict(chunk_length_s=15, stride_length_s=3, batch_size=8), {"task": "translate", "num_beams": 1, "max_new_tokens": 24},
+     True),
+    ("c10_greedy", [("speech", 100.0, 38)], dict(chunk_length_s=10, stride_length_s=2, batch_size=16),
+     {"task": "transcribe", "num_beams": 1, "max_new_tokens": 16}, True),
+    ("ref_de_beam5", [("speech", 180.0, 39)], dict(chunk_length_s=60, stride_length_s=5, batch_size=32),
+     {"task": "transcribe", "language": "de", "max_new_tokens": 24}, True),
+]
+
+
+def sweep_audio(spec):
+    parts = []
+    for kind, sec, seed in spec:
+        parts.append(speech_like(sec, seed) if kind == "speech" else white_noise(sec, seed) if kind == "noise"
+                     else silence(sec))
+    return np.concatenate(parts).astype(np.float32)
+
+
+def make_sweep(out):
+    """The ASR pipeline at test-mini over a sweep of chunk / stride / batch sizes, greedy and beam, timestamps on and
+    off, translate and a forced language (SWEEP_CASES): outputs for the engine's end-to-end comparison."""
+    from transformers import AutomaticSpeechRecognitionPipeline, WhisperFeatureExtractor
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    pipe = AutomaticSpeechRecognitionPipeline(model=m, feature_extractor=fe, tokenizer=hf_tokenizer(gen.special),
+                                              device=-1)
+    res = []
+    for name, spec, kw, gk, ts in SWEEP_CASES:
+        r = pipe(sweep_audio(spec), generate_kwargs=dict(gk), return_timestamps=ts, **kw)
+        res.append({"name": name, "audio": spec, "kwargs": kw, "generate_kwargs": gk, "return_timestamps": ts,
+                    "output": _jsonable(r)})
+    with open(os.path.join(out, "sweep.json"), "w") as f:
+        json.dump({"dims": "test-mini", "cases": res}, f, indent=1)
 
 
 TINY_CLIPS = ("speech30", "noise12")
