@@ -930,8 +930,8 @@ class WhisperEngine:
                                    bb["src_rows"].data_ptr())
             s = self.stream.cuda_stream
             L, H = self.d.decoder_layers, self.d.heads
-            steps = 0
-            while steps < max_new:
+
+            def step() -> None:
                 self.decoder_step(R, r_enc=r_enc)
                 _lib.call("tw_beam_step", self.logits.data_ptr(), W, self.d.vocab, self.suppress_bits.data_ptr(),
                           ctypes.byref(sel), ctypes.byref(bp), ctypes.byref(bst), self.state.data_ptr(),
@@ -939,6 +939,25 @@ class WhisperEngine:
                 _lib.call("tw_kv_reorder", self.kcache.data_ptr(), self.vcache.data_ptr(), bb["kscr"].data_ptr(),
                           bb["vscr"].data_ptr(), L, self.max_rows, H, T, R, bb["src_rows"].data_ptr(),
                           self.pos.data_ptr(), s)
+
+            # one beam step (decoder step over every row, tw_beam_step, the K/V reorder) as one captured graph: the
+            # step reads its position, scores and histories from device memory, so the same graph serves every step
+            # (eager, each of its ~100 launches would be issued from the host every token)
+            g = None
+            if self.use_graphs:
+                key = ("beam", R, nb, max_new, bool(use_timestamps), float(length_penalty), self._slot, r_enc)
+                g = self._graphs.get(key)
+                if g is None:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=self.stream):  # records, does not execute
+                        step()
+                    self._graphs[key] = g
+            steps = 0
+            while steps < max_new:
+                if g is not None:
+                    g.replay()
+                else:
+                    step()
                 steps += 1
                 if steps % check_every == 0 or steps >= max_new:
                     if bool(bb["win"][:W, 1].all().item()):
