@@ -200,8 +200,8 @@ size_t tw_beam_workspace_bytes(int rows);
 int tw_beam_step(const float* logits, int W, int ld_logits, const uint32_t* suppress_bits,
                  const TwSelectParams* params, const TwBeamParams* beam, const TwBeamState* bstate, int* state,
                  int* tokens, int* ids, int* pos, void* workspace, void* stream);
-/* caches bf16[layers][rows_cap][H][T][64]: rows 0..R-1 take positions [0, pos[r]) of row src_rows[r]; scratch has
- * the caches' shape. */
+/* caches bf16[layers][rows_cap][H][T][64]: rows 0..R-1 take positions [0, pos[r]) of row src_rows[r] (any
+ * permutation, R <= 512), in place. k_scratch / v_scratch are unused (may be NULL; kept for ABI stability). */
 int tw_kv_reorder(uint16_t* k_cache, uint16_t* v_cache, uint16_t* k_scratch, uint16_t* v_scratch, int layers,
                   int rows_cap, int H, int T, int R, const int* src_rows, const int* pos, void* stream);
 
@@ -233,6 +233,15 @@ int tw_attn_decode_self(const uint16_t* qkv, int B, int H, int max_pos, const in
  * cross_kv bf16[2][Bt][H][S][64]; row b reads slot row_map[b] (NULL = b). */
 int tw_attn_decode_cross(const uint16_t* q, int B, int H, int S, int Bt, const int* row_map, const uint16_t* cross_kv,
                          uint16_t* out, void* stream);
+/* The same for rows that share an encoder slot in groups (the beams of one window, rows w * num_beams + j): the first
+ * `first` rows (0 <= first < group, the tail of a group that began before this view) form one group, then every
+ * `group` rows (2..8) one group; all rows of a group must hold the same row_map entry (required, not checked). Each
+ * K/V row is read once per group; the keys are split in slices whose states ws (device memory of
+ * tw_attn_decode_cross_grouped_ws_bytes(B, H) bytes) holds until a second launch combines them. Agrees with
+ * tw_attn_decode_cross to bf16 rounding (another softmax merge order). */
+size_t tw_attn_decode_cross_grouped_ws_bytes(int B, int H);
+int tw_attn_decode_cross_grouped(const uint16_t* q, int B, int H, int S, int Bt, const int* row_map, int group,
+                                 int first, const uint16_t* cross_kv, float* ws, uint16_t* out, void* stream);
 /* The same plus the attention probabilities of selected heads (token-level timestamps, the cross_attentions of
  * WhisperGenerationMixin._extract_token_timestamps, $TF/models/whisper/generation_whisper.py:241-380):
  * probs f32[B][n_steps][n_slots][S] receives, for every head h with bit h of head_mask set (H <= 32), row b's

@@ -118,6 +118,65 @@ def test_kv_reorder_matches_gather():
     assert torch.equal(k[:, R:], k0[:, R:])
 
 
+def test_kv_reorder_large_window_permutations():
+    """Beam-shaped reorder at the turbo decoder's scale (60 rows = 12 windows x 5 beams, 20 heads, 448 positions):
+    sources inside each window, rows at different positions, the LDS-tile path of the in-place kernel."""
+    L, cap, H, T, R, nb = 2, 64, 20, 448, 60, 5
+    g = torch.Generator(device="cpu").manual_seed(7)
+    k = torch.randn(L, cap, H, T, 64, generator=g).to(torch.bfloat16).to(DEV)
+    v = torch.randn(L, cap, H, T, 64, generator=g).to(torch.bfloat16).to(DEV)
+    k0, v0 = k.clone(), v.clone()
+    src = torch.tensor([w * nb + int(j) for w in range(R // nb) for j in torch.randint(0, nb, (nb,), generator=g)],
+                       dtype=torch.int32)
+    pos = torch.tensor([int(p) for p in torch.randint(1, T + 1, (R // nb,), generator=g) for _ in range(nb)],
+                       dtype=torch.int32)
+    assert int(src.min()) >= 0 and int(src.max()) < R and int(pos.max()) <= T  # the kernel trusts them
+    src_d, pos_d = src.to(DEV), pos.to(DEV)  # held: a temporary's memory could be reused before the launch
+    _lib.call("tw_kv_reorder", k.data_ptr(), v.data_ptr(), None, None, L, cap, H, T, R, src_d.data_ptr(),
+              pos_d.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for r in range(R):
+        p, s = int(pos[r]), int(src[r])
+        assert torch.equal(k[:, r, :, :p], k0[:, s, :, :p]) and torch.equal(v[:, r, :, :p], v0[:, s, :, :p]), r
+        assert torch.equal(k[:, r, :, p:], k0[:, r, :, p:]) and torch.equal(v[:, r, :, p:], v0[:, r, :, p:]), r
+    assert torch.equal(k[:, R:], k0[:, R:])
+
+
+@pytest.mark.parametrize("group,first,B", [(5, 0, 30), (5, 3, 32), (5, 2, 28), (2, 1, 7), (8, 0, 32), (3, 2, 2)])
+def test_cross_grouped_matches_lean(group, first, B):
+    """tw_attn_decode_cross_grouped (one K/V read per beam group) against tw_attn_decode_cross row for row on a beam
+    row map (rows of a group share their window's encoder slot), including a leading partial group; the
+    keys split in slices merged by a second launch (another softmax merge order), so equal to within 4 bf16 ulps (of max(|x|, 0.02))
+    (tolerance written here; measured on MI355X in profiles/r03q_beam_kernels.txt)."""
+    H, S, Bt = 20, 1500, 12
+    gen = torch.Generator(device="cpu").manual_seed(group * 100 + first)
+    q = (torch.randn(B, H * 64, generator=gen) * 0.125).to(torch.bfloat16).to(DEV)
+    ckv = torch.randn(2, Bt, H, S, 64, generator=gen).to(torch.bfloat16).to(DEV)
+    rows = [0] * first + [1 + (r // group) for r in range(B - first)]
+    rmap = torch.tensor([x % Bt for x in rows], dtype=torch.int32, device=DEV)
+    a = torch.empty(B, H * 64, dtype=torch.bfloat16, device=DEV)
+    b = torch.empty_like(a)
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.call("tw_attn_decode_cross", q.data_ptr(), B, H, S, Bt, rmap.data_ptr(), ckv.data_ptr(), a.data_ptr(), s)
+    ws = torch.empty(int(_lib.load().tw_attn_decode_cross_grouped_ws_bytes(B, H)) // 4, device=DEV)
+    _lib.call("tw_attn_decode_cross_grouped", q.data_ptr(), B, H, S, Bt, rmap.data_ptr(), group, first, ckv.data_ptr(),
+              ws.data_ptr(), b.data_ptr(), s)
+    torch.cuda.synchronize()
+    d = (a.float() - b.float()).abs()
+    # bf16 ulp of the larger magnitude, floored at that of 0.02 (outputs here are ~0.05: near-zero entries would
+    # otherwise count a rounding step of their neighbours' scale as many ulps)
+    ulp = torch.maximum(a.float().abs(), b.float().abs()).clamp_min(0.02) * 2.0 ** -7
+    print(f"grouped vs lean: {int((d > 0).sum())} of {d.numel()} differ, max {d.max().item():.2e}, "
+          f"max in ulps {(d / ulp).max().item():.2f}")
+    assert bool((d <= 4 * ulp).all())
+    # and against an fp32 reference of softmax(q K^T) V
+    kf, vf = ckv[0].float(), ckv[1].float()
+    for r in (0, B - 1):
+        sc = torch.einsum("hd,hsd->hs", q[r].float().view(H, 64), kf[rmap[r]])
+        ref = torch.einsum("hs,hsd->hd", sc.softmax(-1), vf[rmap[r]]).reshape(-1)
+        assert (b[r].float() - ref).abs().max().item() < 2e-2
+
+
 @pytest.fixture(scope="module")
 def mini():
     from twamd.pipeline import TurboTranscriber

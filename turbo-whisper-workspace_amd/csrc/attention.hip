@@ -1043,6 +1043,187 @@ __global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_lean(const bf16_t* __re
   }
 }
 
+// k_attn_decode_cross_grp: the lean kernel for G rows that read the SAME encoder slot (the beams of one window): each
+// key/value row is loaded once for all G queries (num_beams x less cross K/V traffic: the beam-5 step's largest
+// kernel streamed 60 x 20 x 384 KB per layer for 12 distinct windows). One group per block would leave most CUs idle
+// (20 heads x 7 groups per 32-row view; measured slower than the lean kernel), so the keys are also split NSPLIT
+// ways (flash-decoding): grid (H, nblk, NSPLIT), each block writes its rows' unnormalised state (max, sum, 64 sums)
+// to ws and k_attn_cross_merge combines the NSPLIT states. Per row and key slice the arithmetic is the lean
+// kernel's (NG key groups, UNR blocks, the same merges).
+// Block y takes rows [r_lo, r_hi): the first `first` rows of the view (the tail of a window that began in the
+// previous view), then groups of G.
+#define DA_XSPLIT 3
+template <int G, int NG = 32, int UNR = DA_UNR>
+__global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_grp(const bf16_t* __restrict__ q, int D, int S, int Bt, int R,
+                                                               int first, const int* __restrict__ row_map,
+                                                               const bf16_t* __restrict__ ckv,
+                                                               float* __restrict__ ws) {
+  TW_DEC_PRIO();
+  constexpr int NWV = NG / 8;
+  __shared__ float wpart[NWV][G][64];
+  __shared__ float wml[NWV][G][2];
+  const int h = blockIdx.x, y = blockIdx.y, z = blockIdx.z, H = gridDim.x, NS = gridDim.z;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = tid >> 3, gl = tid & 7;
+  const int r_lo = first > 0 ? (y == 0 ? 0 : first + (y - 1) * G) : y * G;
+  const int r_hi = min(R, first > 0 && y == 0 ? first : r_lo + G);
+  const int n = r_hi - r_lo;
+  const int k0 = (int)((long)z * S / NS), k1 = (int)((long)(z + 1) * S / NS);
+  const int slot = row_map[r_lo];
+  float qv[G][8];
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const uint4 qr = *(const uint4*)(q + (size_t)(r_lo + min(j, n - 1)) * D + h * 64 + gl * 8);
+    const bf16_t* qe = (const bf16_t*)&qr;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qv[j][e] = bf16_to_f32(qe[e]);
+  }
+  const bf16_t* K = ckv + (((size_t)0 * Bt + slot) * H + h) * S * 64;
+  const bf16_t* V = ckv + (((size_t)1 * Bt + slot) * H + h) * S * 64;
+  float m[G], l[G], acc[G][8];
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    m[j] = -INFINITY;
+    l[j] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
+  }
+  const int nit = (k1 - k0 + NG - 1) / NG;
+  for (int it0 = 0; it0 < nit; it0 += UNR) {
+    uint4 kk[UNR], vv[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int key = min(k0 + (it0 + u) * NG + g, k1 - 1);
+      typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+      const u32x4_nt a = __builtin_nontemporal_load((const u32x4_nt*)(K + (size_t)key * 64 + gl * 8));
+      const u32x4_nt c = __builtin_nontemporal_load((const u32x4_nt*)(V + (size_t)key * 64 + gl * 8));
+      kk[u] = make_uint4(a.x, a.y, a.z, a.w);
+      vv[u] = make_uint4(c.x, c.y, c.z, c.w);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      float sv[UNR];
+      float bm = m[j];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        float d = 0.f;
+        const bf16_t* ke = (const bf16_t*)&kk[u];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += qv[j][e] * bf16_to_f32(ke[e]);
+        d += __shfl_xor(d, 1, 64);
+        d += __shfl_xor(d, 2, 64);
+        d += __shfl_xor(d, 4, 64);
+        sv[u] = k0 + (it0 + u) * NG + g < k1 ? d : -INFINITY;
+        bm = fmaxf(bm, sv[u]);
+      }
+      if (bm == -INFINITY) continue;
+      const float sc = __expf(m[j] - bm);
+      l[j] *= sc;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[j][e] *= sc;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const float p = __expf(sv[u] - bm);
+        l[j] += p;
+        const bf16_t* ve = (const bf16_t*)&vv[u];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[j][e] += p * bf16_to_f32(ve[e]);
+      }
+      m[j] = bm;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+      const float m2 = __shfl_xor(m[j], o, 64), l2 = __shfl_xor(l[j], o, 64);
+      const float M = fmaxf(m[j], m2);
+      const float s1 = m[j] == -INFINITY ? 0.f : __expf(m[j] - M), s2 = m2 == -INFINITY ? 0.f : __expf(m2 - M);
+      l[j] = l[j] * s1 + l2 * s2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[j][e] = acc[j][e] * s1 + __shfl_xor(acc[j][e], o, 64) * s2;
+      m[j] = M;
+    }
+    if (lane < 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) wpart[wid][j][lane * 8 + e] = acc[j][e];
+      if (lane == 0) {
+        wml[wid][j][0] = m[j];
+        wml[wid][j][1] = l[j];
+      }
+    }
+  }
+  __syncthreads();
+  // this key slice's state per row: ws[((row * H + h) * NS + z) * 66 + {0: max, 1: sum, 2..65: unnormalised P.V}]
+  for (int idx = tid; idx < n * 64; idx += NG * 8) {
+    const int j = idx >> 6, c = idx & 63;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) M = fmaxf(M, wml[w][j][0]);
+    float v = 0.f, tot = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+      const float mg = wml[w][j][0];
+      const float wt = mg == -INFINITY ? 0.f : __expf(mg - M);
+      tot += wt * wml[w][j][1];
+      v += wt * wpart[w][j][c];
+    }
+    float* rec = ws + (((size_t)(r_lo + j) * H + h) * NS + z) * 66;
+    rec[2 + c] = v;
+    if (c == 0) {
+      rec[0] = M;
+      rec[1] = tot;
+    }
+  }
+}
+
+// grid (H, B), 64 threads: out[b][h*64 + c] = the NS key slices' states combined.
+__global__ __launch_bounds__(64) void k_attn_cross_merge(const float* __restrict__ ws, int NS, int D,
+                                                         bf16_t* __restrict__ out) {
+  TW_DEC_PRIO();
+  const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x, c = threadIdx.x;
+  const float* rec = ws + ((size_t)b * H + h) * NS * 66;
+  float M = -INFINITY;
+  for (int z = 0; z < NS; ++z) M = fmaxf(M, rec[z * 66]);
+  float v = 0.f, tot = 0.f;
+  for (int z = 0; z < NS; ++z) {
+    const float mz = rec[z * 66];
+    const float wt = mz == -INFINITY ? 0.f : __expf(mz - M);
+    tot += wt * rec[z * 66 + 1];
+    v += wt * rec[z * 66 + 2 + c];
+  }
+  out[(size_t)b * D + h * 64 + c] = f32_to_bf16(v / tot);
+}
+
+extern "C" size_t tw_attn_decode_cross_grouped_ws_bytes(int B, int H) {
+  return (size_t)B * H * DA_XSPLIT * 66 * sizeof(float);
+}
+
+extern "C" int tw_attn_decode_cross_grouped(const bf16_t* q, int B, int H, int S, int Bt, const int* row_map,
+                                            int group, int first, const bf16_t* cross_kv, float* ws, bf16_t* out,
+                                            void* stream) {
+  TW_REQUIRE(q && cross_kv && out && row_map && ws && B > 0 && H > 0 && S >= DA_XSPLIT && S <= DA_MAXK,
+             "tw_attn_decode_cross_grouped: bad args");
+  TW_REQUIRE(group >= 2 && group <= 8 && first >= 0 && first < group,
+             "tw_attn_decode_cross_grouped: group=%d first=%d (2 <= group <= 8, 0 <= first < group)", group, first);
+  const int f = min(first, B);
+  const int nblk = (f > 0 ? 1 : 0) + (B - f + group - 1) / group;
+  const dim3 grid(H, nblk, DA_XSPLIT), blk(256);
+  hipStream_t s = (hipStream_t)stream;
+  const int D = H * 64;
+  switch (group) {
+    case 2: hipLaunchKernelGGL((k_attn_decode_cross_grp<2>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
+    case 3: hipLaunchKernelGGL((k_attn_decode_cross_grp<3>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
+    case 4: hipLaunchKernelGGL((k_attn_decode_cross_grp<4>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
+    case 5: hipLaunchKernelGGL((k_attn_decode_cross_grp<5>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
+    case 6: hipLaunchKernelGGL((k_attn_decode_cross_grp<6>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
+    case 7: hipLaunchKernelGGL((k_attn_decode_cross_grp<7>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
+    default: hipLaunchKernelGGL((k_attn_decode_cross_grp<8>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
+  }
+  hipLaunchKernelGGL(k_attn_cross_merge, dim3(H, B), dim3(64), 0, s, ws, DA_XSPLIT, D, out);
+  return tw_check_launch("tw_attn_decode_cross_grouped");
+}
+
 // Cross-attention step: q [B][D] bf16 (pre-scaled); cross K/V layout [kv][Bt][H][S][64] for this layer,
 // batch row b reads block row_map[b] (the encoder batch slot holding that row's audio window).
 extern "C" int tw_attn_decode_cross(const bf16_t* q, int B, int H, int S, int Bt, const int* row_map,

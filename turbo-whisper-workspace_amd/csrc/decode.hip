@@ -557,19 +557,19 @@ struct Cand {
 };
 __device__ inline bool cand_better(float v, int i, const Cand& c) { return v > c.v || (v == c.v && i < c.i); }
 
+// Sorted insert as a compare-swap chain: every index is static, so the list stays in VGPRs (the shifting form with
+// an early return was lowered to scratch: 80-272 B/lane, k_beam_partial 139 us per step at 60 rows).
 template <int K>
 __device__ inline void cand_insert(Cand (&L)[K], float v, int i) {
   if (!cand_better(v, i, L[K - 1])) return;
+  Cand c{v, i};
 #pragma unroll
-  for (int j = K - 1; j > 0; --j) {
-    if (cand_better(v, i, L[j - 1])) {
-      L[j] = L[j - 1];
-    } else {
-      L[j] = Cand{v, i};
-      return;
-    }
+  for (int j = 0; j < K; ++j) {
+    const bool better = cand_better(c.v, c.i, L[j]);
+    const Cand o = L[j];
+    L[j] = better ? c : o;
+    c = better ? o : c;
   }
-  L[0] = Cand{v, i};
 }
 
 // K rounds of wave argmax over the lanes' sorted lists: out (LDS, K entries) = the wave's top-K, descending.
@@ -589,11 +589,10 @@ __device__ inline void wave_topk(Cand (&L)[K], Cand* out, int lane) {
       }
     }
     if (lane == 0) out[r] = Cand{bv, bi};
-    if (lane == bl) {  // pop the head
+    const bool pop = lane == bl;  // pop the head (selects, not a branch around register moves)
 #pragma unroll
-      for (int j = 0; j < K - 1; ++j) L[j] = L[j + 1];
-      L[K - 1] = Cand{-INFINITY, 0x7fffffff};
-    }
+    for (int j = 0; j < K - 1; ++j) L[j] = pop ? L[j + 1] : L[j];
+    L[K - 1] = pop ? Cand{-INFINITY, 0x7fffffff} : L[K - 1];
   }
 }
 
@@ -716,6 +715,11 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
   __shared__ int s_src[TW_BEAM_MAXNB], s_tok[TW_BEAM_MAXNB], f_from[TW_BEAM_MAXNB], f_flag[TW_BEAM_MAXNB];
   __shared__ float s_score[TW_BEAM_MAXNB], f_score[TW_BEAM_MAXNB];
   __shared__ int c_beam[2 * K], c_tok[2 * K];
+  // per-row sorted lists and the one-thread bookkeeping arrays live in LDS: as per-thread arrays with runtime
+  // indices they were lowered to scratch (224-768 B/lane) and the serial section ran at scratch latency
+  __shared__ Cand tops[TW_BEAM_MAXNB][2][K];
+  __shared__ float csc[2 * K], rsc[2 * K], merged[TW_BEAM_MAXNB + 2 * K];
+  __shared__ bool taken[TW_BEAM_MAXNB][K], hits[2 * K], rsel[2 * K], msel[TW_BEAM_MAXNB + 2 * K];
   const int w = blockIdx.x, nb = bp.num_beams, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int ldt = bp.ld_tokens;
   int* win = bs.win + 4 * w;
@@ -740,7 +744,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
       lse_merge(m_ts, s_ts, m2, s2);
     }
     // top-K of the text list and of the timestamp list over the NC chunk lists (<= 4 entries per lane)
-    Cand top[2][K];
+    Cand(*top)[K] = tops[wid];
     for (int l = 0; l < 2; ++l) {
       Cand mine[4];
       bool used[4];
@@ -771,11 +775,12 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
             bl = ol;
           }
         }
-        if (lane == bl && bq >= 0) used[bq] = true;
-        top[l][r] = Cand{bv, bi};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) used[q] = used[q] || (lane == bl && bq == q);
+        if (lane == 0) top[l][r] = Cand{bv, bi};
       }
     }
-    if (lane == 0) {
+    if (lane == 0) {  // lane 0 wrote top
       const float lse_all = m_all + __logf(s_all);
       const float lse_ts = (m_ts == -INFINITY) ? -INFINITY : m_ts + __logf(s_ts);
       // WhisperTimeStampLogitsProcessor: timestamp mass above every text token -> text tokens -inf
@@ -809,9 +814,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
   // 2. the window's beam bookkeeping (one thread: nb * K <= 128 candidates)
   if (tid == 0) {
     const int V = p.V;
-    float csc[2 * K];
     // top-K over all beams' candidates by accumulated log-prob; ties -> lower flat index beam * V + token
-    bool taken[TW_BEAM_MAXNB][K];
     for (int j = 0; j < nb; ++j)
       for (int k = 0; k < K; ++k) taken[j][k] = false;
     for (int c = 0; c < K; ++c) {
@@ -836,15 +839,12 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
       c_tok[c] = rc[bj][bk].i;
       csc[c] = bv;
     }
-    bool hits[2 * K];
     bool all_hit = true;
     for (int c = 0; c < K; ++c) {
       hits[c] = c_tok[c] == p.eos || t + 1 >= bp.max_new;
       all_hit = all_hit && hits[c];
     }
     // e. running beams for the next step: best nb of the non-finished continuations
-    float rsc[2 * K];
-    bool rsel[2 * K];
     for (int c = 0; c < K; ++c) {
       rsc[c] = csc[c] + (hits[c] ? NEG : 0.f);
       rsel[c] = false;
@@ -861,7 +861,6 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
     // f. finished beams: previous best nb merged with the just-finished top-nb continuations
     const int unsat_prev = win[0];
     const float lp_div = __powf((float)(t + 1), bp.length_penalty);
-    float merged[TW_BEAM_MAXNB + 2 * K];
     for (int q = 0; q < nb; ++q) merged[q] = bs.fin_score[w * nb + q];
     for (int c = 0; c < K; ++c) {
       float v = csc[c] / lp_div;
@@ -870,7 +869,6 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
       if (!just) v += NEG;
       merged[nb + c] = v;
     }
-    bool msel[TW_BEAM_MAXNB + 2 * K];
     for (int e = 0; e < nb + K; ++e) msel[e] = false;
     float min_fin = INFINITY;
     bool all_fin = true;
@@ -974,31 +972,58 @@ extern "C" int tw_beam_step(const float* logits, int W, int ld_logits, const uin
 }
 
 // Self-attention K/V reorder after a beam step: row r continues row src_rows[r]; positions [0, pos[r]) move.
-// Two passes through scratch (same layout as the caches) so a permutation never reads a row it already overwrote.
-__global__ __launch_bounds__(256) void k_kv_reorder(bf16_t* __restrict__ cache, bf16_t* __restrict__ scratch,
+// In place, one launch for K and V: block (layer*head, position tile, K|V) stages the tile of every moved row's
+// source in LDS, then writes the destinations. Tiles are disjoint across blocks and a block reads all its sources
+// before it writes, so any permutation is safe; HBM traffic is one read + one write per moved (row, position)
+// (the earlier two-phase copy through a cache-sized scratch moved every byte twice, in four launches).
+#define TW_KVR_LDS 57344
+__global__ __launch_bounds__(256) void k_kv_reorder(bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
                                                     const int* __restrict__ src_rows, const int* __restrict__ pos,
-                                                    int rows_cap, int H, int T, int phase) {
-  const int r = blockIdx.x, lh = blockIdx.y, l = lh / H, h = lh - l * H;
-  const int s = src_rows[r];
-  if (s == r) return;
-  const int n = pos[r] * 64 / 8;  // uint4 chunks of the valid positions
-  const size_t dst_off = (((size_t)l * rows_cap + r) * H + h) * (size_t)T * 64;
-  const size_t src_off = (((size_t)l * rows_cap + s) * H + h) * (size_t)T * 64;
-  const uint4* from = (const uint4*)(phase == 0 ? cache + src_off : scratch + dst_off);
-  uint4* to = (uint4*)(phase == 0 ? scratch + dst_off : cache + dst_off);
-  for (int e = threadIdx.x; e < n; e += 256) to[e] = from[e];
+                                                    int rows_cap, int H, int T, int R, int TT) {
+  extern __shared__ uint4 kvr_tile[];  // [R][TT * 8] uint4 (a position of one head = 64 bf16 = 8 uint4)
+  __shared__ int s_src[512], s_n[512];
+  __shared__ int s_any;
+  const int lh = blockIdx.x, l = lh / H, h = lh - l * H, t0 = blockIdx.y * TT;
+  bf16_t* cache = blockIdx.z == 0 ? k_cache : v_cache;
+  if (threadIdx.x == 0) s_any = 0;
+  __syncthreads();
+  for (int r = threadIdx.x; r < R; r += 256) {
+    const int s = src_rows[r];
+    // positions of this tile row r takes from s (an out-of-range source or position moves nothing: never a fault)
+    const bool ok = s != r && s >= 0 && s < rows_cap;
+    const int n = ok ? min(max(min(pos[r], T) - t0, 0), TT) : 0;
+    s_src[r] = s;
+    s_n[r] = n;
+    if (n > 0) s_any = 1;
+  }
+  __syncthreads();
+  if (!s_any) return;
+  const int per_row = TT * 8;
+  const size_t head = (size_t)T * 8;  // uint4 per (layer, row, head)
+  const uint4* c4 = (const uint4*)cache;
+  for (int e = threadIdx.x; e < R * per_row; e += 256) {
+    const int r = e / per_row, q = e - r * per_row;
+    if (q < s_n[r] * 8)
+      kvr_tile[e] = c4[(((size_t)l * rows_cap + s_src[r]) * H + h) * head + (size_t)t0 * 8 + q];
+  }
+  __syncthreads();
+  uint4* w4 = (uint4*)cache;
+  for (int e = threadIdx.x; e < R * per_row; e += 256) {
+    const int r = e / per_row, q = e - r * per_row;
+    if (q < s_n[r] * 8) w4[(((size_t)l * rows_cap + r) * H + h) * head + (size_t)t0 * 8 + q] = kvr_tile[e];
+  }
 }
 
 extern "C" int tw_kv_reorder(uint16_t* k_cache, uint16_t* v_cache, uint16_t* k_scratch, uint16_t* v_scratch, int layers,
                              int rows_cap, int H, int T, int R, const int* src_rows, const int* pos, void* stream) {
-  TW_REQUIRE(k_cache && v_cache && k_scratch && v_scratch && src_rows && pos && R > 0 && R <= rows_cap,
-             "tw_kv_reorder: bad args");
-  hipStream_t s = (hipStream_t)stream;
-  for (int phase = 0; phase < 2; ++phase) {
-    hipLaunchKernelGGL(k_kv_reorder, dim3(R, layers * H), dim3(256), 0, s, (bf16_t*)k_cache, (bf16_t*)k_scratch,
-                       src_rows, pos, rows_cap, H, T, phase);
-    hipLaunchKernelGGL(k_kv_reorder, dim3(R, layers * H), dim3(256), 0, s, (bf16_t*)v_cache, (bf16_t*)v_scratch,
-                       src_rows, pos, rows_cap, H, T, phase);
-  }
+  (void)k_scratch;
+  (void)v_scratch;
+  TW_REQUIRE(k_cache && v_cache && src_rows && pos && R > 0 && R <= rows_cap && R <= 512 && T > 0,
+             "tw_kv_reorder: bad args (R=%d rows_cap=%d T=%d)", R, rows_cap, T);
+  int TT = 16;  // positions per tile: R * TT * 128 B of LDS
+  while (TT > 1 && (size_t)R * TT * 128 > TW_KVR_LDS) TT >>= 1;
+  const dim3 grid(layers * H, (T + TT - 1) / TT, 2);
+  hipLaunchKernelGGL(k_kv_reorder, grid, dim3(256), (size_t)R * TT * 128, (hipStream_t)stream, (bf16_t*)k_cache,
+                     (bf16_t*)v_cache, src_rows, pos, rows_cap, H, T, R, TT);
   return tw_check_launch("tw_kv_reorder");
 }

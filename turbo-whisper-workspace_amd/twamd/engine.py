@@ -219,6 +219,8 @@ class WhisperEngine:
         self.seek = torch.zeros(max_batch, dtype=i32, device=dev)
         self.dec_row_map = torch.zeros(B, dtype=i32, device=dev)  # decoder row -> cross-K/V row (beam search)
         self._use_dec_row_map = False
+        self._row_group = 1
+        self._xws: Optional[torch.Tensor] = None
         self._beam: Optional[dict] = None  # beam-search buffers, allocated on first use
         self._align: Optional[dict] = None  # token-level timestamps: alignment-head attention recording
         self._align_buf: Optional[torch.Tensor] = None
@@ -573,6 +575,14 @@ class WhisperEngine:
             _lib.call("tw_attn_decode_cross_probs", v.qd.data_ptr(), R, H, S_ENC, r_enc, rmap, ckv, v.attd.data_ptr(),
                       al["buf"].data_ptr() + v.r0 * row_stride, mask, slot0, al["n_slots"], v.pos.data_ptr(),
                       al["pos0"], al["n_steps"], s)
+        elif self._row_group > 1 and rmap is not None:  # beam rows: one K/V read per window's beams
+            g = self._row_group
+            if self._xws is None:  # per-row key-slice states, rows at their global index (views never overlap)
+                nbytes = int(_lib.load().tw_attn_decode_cross_grouped_ws_bytes(self.max_rows, H))
+                self._xws = torch.empty(nbytes // 4, dtype=torch.float32, device=self.device)
+            row_bytes = self._xws.numel() * 4 // self.max_rows
+            _lib.call("tw_attn_decode_cross_grouped", v.qd.data_ptr(), R, H, S_ENC, r_enc, rmap, g, (g - v.r0 % g) % g,
+                      ckv, self._xws.data_ptr() + v.r0 * row_bytes, v.attd.data_ptr(), s)
         else:
             _lib.call("tw_attn_decode_cross", v.qd.data_ptr(), R, H, S_ENC, r_enc, rmap, ckv, v.attd.data_ptr(), s)
 
@@ -802,6 +812,7 @@ class WhisperEngine:
         if enc_rows is not None:
             self.dec_row_map[:R] = torch.as_tensor(list(enc_rows), dtype=torch.int32, device=dev)
             self._use_dec_row_map = True
+            self._row_group = 1
         try:
             self.state[:R].zero_()
             self.state[:R, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
@@ -845,6 +856,7 @@ class WhisperEngine:
             stt = self.state[:R].cpu()
         finally:
             self._use_dec_row_map = False
+            self._row_group = 1
         ngen = stt[:, _lib.TW_ST_NGEN].tolist()
         toks = self.tokens[:R].tolist()
         f32 = stt.view(torch.float32)
@@ -868,8 +880,6 @@ class WhisperEngine:
                 "win": torch.zeros(self.max_batch, 4, dtype=torch.int32, device=dev),
                 "src_rows": torch.zeros(self.max_rows, dtype=torch.int32, device=dev),
                 "ws": torch.empty(ws_bytes, dtype=torch.uint8, device=dev),
-                "kscr": torch.empty_like(self.kcache),
-                "vscr": torch.empty_like(self.vcache),
             }
         return self._beam
 
@@ -894,6 +904,7 @@ class WhisperEngine:
         self.stream.wait_event(self._enc_ev[self._slot])
         self.dec_row_map[:R] = enc_row0 + torch.arange(R, dtype=torch.int32, device=dev) // nb
         self._use_dec_row_map = True
+        self._row_group = nb  # rows w * nb + j share window w's cross K/V
         try:
             self.state[:R].zero_()
             self.state[:R, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
@@ -936,8 +947,8 @@ class WhisperEngine:
                 _lib.call("tw_beam_step", self.logits.data_ptr(), W, self.d.vocab, self.suppress_bits.data_ptr(),
                           ctypes.byref(sel), ctypes.byref(bp), ctypes.byref(bst), self.state.data_ptr(),
                           self.tokens.data_ptr(), self.ids.data_ptr(), self.pos.data_ptr(), bb["ws"].data_ptr(), s)
-                _lib.call("tw_kv_reorder", self.kcache.data_ptr(), self.vcache.data_ptr(), bb["kscr"].data_ptr(),
-                          bb["vscr"].data_ptr(), L, self.max_rows, H, T, R, bb["src_rows"].data_ptr(),
+                _lib.call("tw_kv_reorder", self.kcache.data_ptr(), self.vcache.data_ptr(), None, None, L,
+                          self.max_rows, H, T, R, bb["src_rows"].data_ptr(),
                           self.pos.data_ptr(), s)
 
             # one beam step (decoder step over every row, tw_beam_step, the K/V reorder) as one captured graph: the
@@ -966,6 +977,7 @@ class WhisperEngine:
             ftok = bb["fin_tokens"][:R:nb].tolist()
         finally:
             self._use_dec_row_map = False
+            self._row_group = 1
         return PassResult([ftok[w][: flen[w]] for w in range(W)], detected if lang_ids is None else list(lang_ids))
 
     def _chains(self, R: int) -> List[DecView]:
