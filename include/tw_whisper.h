@@ -194,6 +194,10 @@ typedef struct TwBeamState {
   int32_t* fin_tokens;   /* i32[R][ld_tokens]                                             */
   int32_t* win;          /* i32[W][4]                                                     */
   int32_t* src_rows;     /* i32[R]   out                                                  */
+  int32_t* kv_tab;       /* i32[R][ld_tokens] or NULL: the self-attention K/V position table
+                          * (tw_attn_decode_self_tab): row r's positions [0, pos[r]) take row src_rows[r]'s
+                          * entries, in place of a tw_kv_reorder copy. Initialise kv_tab[r][*] = r; its row
+                          * stride ld_tokens must equal the caches' max_pos.                                 */
 } TwBeamState;
 /* workspace: tw_beam_workspace_bytes(R) bytes of device memory. */
 size_t tw_beam_workspace_bytes(int rows);
@@ -229,6 +233,13 @@ int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const fl
  * Replaces the causal self-attention + DynamicCache.update of modeling_whisper.py:312-335,448-505. */
 int tw_attn_decode_self(const uint16_t* qkv, int B, int H, int max_pos, const int* pos, uint16_t* k_cache,
                         uint16_t* v_cache, uint16_t* out, void* stream);
+/* The same with beam search's copy-free K/V history: position q < pos[b] of row b is read from cache row
+ * kv_tab[(row0 + b) * max_pos + q] (a global row: k_cache / v_cache point at row row0 of the layer's caches, which
+ * hold rows_cap rows); the step's own K/V is written to row b at pos[b], and kv_tab[(row0 + b) * max_pos + pos[b]]
+ * must equal row0 + b (tw_beam_step keeps it so). Each physical (row, position) is written once per pass, so no
+ * history is ever overwritten while another beam still reads it. */
+int tw_attn_decode_self_tab(const uint16_t* qkv, int B, int H, int max_pos, const int* pos, uint16_t* k_cache,
+                            uint16_t* v_cache, const int* kv_tab, int row0, uint16_t* out, void* stream);
 /* Decoder cross-attention for one query per row over the cached encoder K/V of this layer,
  * cross_kv bf16[2][Bt][H][S][64]; row b reads slot row_map[b] (NULL = b). */
 int tw_attn_decode_cross(const uint16_t* q, int B, int H, int S, int Bt, const int* row_map, const uint16_t* cross_kv,

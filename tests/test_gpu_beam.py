@@ -142,7 +142,41 @@ def test_kv_reorder_large_window_permutations():
     assert torch.equal(k[:, R:], k0[:, R:])
 
 
-@pytest.mark.parametrize("group,first,B", [(5, 0, 30), (5, 3, 32), (5, 2, 28), (2, 1, 7), (8, 0, 32), (3, 2, 2)])
+@pytest.mark.parametrize("t_max", [40, 300])  # the one-round-trip path (< 256 keys) and the two-pass path
+def test_self_attention_position_table_equals_gathered_history(t_max):
+    """tw_attn_decode_self_tab (beam search's copy-free K/V history) against tw_attn_decode_self on caches where each
+    row's history has been gathered through the table: same outputs bit for bit (only the addresses differ), the
+    step's own K/V written to its own row. A view offset (row0) and sources in other views are included."""
+    H, T, cap, R, row0 = 4, 448, 24, 10, 6
+    gen = torch.Generator(device="cpu").manual_seed(t_max)
+    k = torch.randn(cap, H, T, 64, generator=gen).to(torch.bfloat16).to(DEV)
+    v = torch.randn(cap, H, T, 64, generator=gen).to(torch.bfloat16).to(DEV)
+    qkv = (torch.randn(R, 3 * H * 64, generator=gen) * 0.125).to(torch.bfloat16).to(DEV)
+    pos = torch.randint(t_max // 2, t_max, (R,), generator=gen, dtype=torch.int32)
+    tab = torch.arange(cap, dtype=torch.int32)[:, None].repeat(1, T)
+    for r in range(R):  # positions < pos of view row r come from random global rows; pos itself stays own
+        tab[row0 + r, : int(pos[r])] = torch.randint(0, cap, (int(pos[r]),), generator=gen, dtype=torch.int32)
+    kg, vg = k.clone(), v.clone()  # gathered: row0 + r holds its logical history contiguously
+    for r in range(R):
+        for q in range(int(pos[r])):
+            kg[row0 + r, :, q] = k[int(tab[row0 + r, q]), :, q]
+            vg[row0 + r, :, q] = v[int(tab[row0 + r, q]), :, q]
+    tab_d, pos_d = tab.to(DEV), pos.to(DEV)
+    a = torch.empty(R, H * 64, dtype=torch.bfloat16, device=DEV)
+    b = torch.empty_like(a)
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.call("tw_attn_decode_self", qkv.data_ptr(), R, H, T, pos_d.data_ptr(), kg[row0].data_ptr(), vg[row0].data_ptr(),
+              a.data_ptr(), s)
+    _lib.call("tw_attn_decode_self_tab", qkv.data_ptr(), R, H, T, pos_d.data_ptr(), k[row0].data_ptr(),
+              v[row0].data_ptr(), tab_d.data_ptr(), row0, b.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    for r in range(R):  # the step's K/V appended to the row's own cache at pos
+        p = int(pos[r])
+        assert torch.equal(k[row0 + r, :, p], kg[row0 + r, :, p]) and torch.equal(v[row0 + r, :, p], vg[row0 + r, :, p])
+
+
+@pytest.mark.parametrize("group,first,B",[(5, 0, 30), (5, 3, 32), (5, 2, 28), (2, 1, 7), (8, 0, 32), (3, 2, 2)])
 def test_cross_grouped_matches_lean(group, first, B):
     """tw_attn_decode_cross_grouped (one K/V read per beam group) against tw_attn_decode_cross row for row on a beam
     row map (rows of a group share their window's encoder slot), including a leading partial group; the

@@ -692,9 +692,15 @@ extern "C" int tw_attn_encoder_mx(const bf16_t* qkv, int B, int S, int H, uint8_
 #define DA_MAXK 1536
 #define DA_UNR 8  // key rows of loads in flight per 8-lane group
 
-__device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf16_t* K, const bf16_t* V, int nkeys,
-                                  float* sc /*[DA_MAXK] LDS*/, float* part /*[32][64] LDS*/, float* red /*[8]*/,
-                                  float* outv /*[64] f32 LDS*/) {
+// off(key): element offset of key row `key` from K (and V): key * 64 for a contiguous history; beam search's
+// position table maps a key to another row's cache (dec_attend_self_tab).
+struct KeyRows {
+  __device__ long operator()(int key) const { return (long)key * 64; }
+};
+template <typename Off>
+__device__ inline void dec_attend_off(const float* qf /*[64] f32 in LDS*/, const bf16_t* K, const bf16_t* V,
+                                      int nkeys, float* sc /*[DA_MAXK] LDS*/, float* part /*[32][64] LDS*/,
+                                      float* red /*[8]*/, float* outv /*[64] f32 LDS*/, Off off) {
   const int tid = threadIdx.x, g = tid >> 3, gl = tid & 7;
   float qv[8];
 #pragma unroll
@@ -707,7 +713,7 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
 #pragma unroll
     for (int u = 0; u < DA_UNR; ++u) {
       const int key = min((it0 + u) * 32 + g, nkeys - 1);
-      kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
+      kk[u] = *(const uint4*)(K + off(key) + gl * 8);
     }
     __builtin_amdgcn_sched_barrier(0);  // all DA_UNR loads in flight before the first is consumed
 #pragma unroll
@@ -748,7 +754,7 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
 #pragma unroll
     for (int u = 0; u < DA_UNR; ++u) {
       const int key = min((it0 + u) * 32 + g, nkeys - 1);
-      vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
+      vv[u] = *(const uint4*)(V + off(key) + gl * 8);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -772,6 +778,11 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
   __syncthreads();
 }
 
+__device__ inline void dec_attend(const float* qf, const bf16_t* K, const bf16_t* V, int nkeys, float* sc, float* part,
+                                  float* red, float* outv) {
+  dec_attend_off(qf, K, V, nkeys, sc, part, red, outv, KeyRows{});
+}
+
 #define DA_SELF_MAXK 448  // decoder positions (max_target_positions of every Whisper checkpoint)
 
 // k_attn_decode_self2: the decoder self-attention step in ONE memory round trip for up to DS2_KEYS keys. The cached
@@ -783,9 +794,23 @@ __device__ inline void dec_attend(const float* qf /*[64] f32 in LDS*/, const bf1
 // append, then K / V re-read) in the same launch; the two agree up to the order of the f32 sums.
 #define DS2_U 8
 #define DS2_KEYS (DS2_U * 32)
+// TAB (beam search): key q < t of row b lives in cache row kv_tab[(row0 + b) * max_pos + q] (a global row; kc / vc
+// point at row row0), so a beam continuing another reads that beam's history in place instead of a copy of it.
+// The row offsets are one more load in front of the K / V loads (two round trips instead of one).
+struct TabRows {
+  const int* tr;  // this row's table
+  long row_stride;  // elements between consecutive cache rows of one head: H * max_pos * 64
+  int self;         // this row's global index
+  __device__ long operator()(int key) const {
+    return (long)(tr[key] - self) * row_stride + (long)key * 64;
+  }
+};
+
+template <bool TAB>
 __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__ qkv, int D, int max_pos,
                                                            const int* __restrict__ pos, bf16_t* __restrict__ kc,
-                                                           bf16_t* __restrict__ vc, bf16_t* __restrict__ out) {
+                                                           bf16_t* __restrict__ vc, const int* __restrict__ kv_tab,
+                                                           int row0, bf16_t* __restrict__ out) {
   TW_DEC_PRIO();
   __shared__ float part[32 * 64];
   __shared__ float red[16];
@@ -806,7 +831,12 @@ __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__
     }
     __threadfence_block();
     __syncthreads();
-    dec_attend(qf, K, V, t + 1, sc, part, red, outv);
+    if constexpr (TAB) {
+      dec_attend_off(qf, K, V, t + 1, sc, part, red, outv,
+                     TabRows{kv_tab + (size_t)(row0 + b) * max_pos, (long)H * max_pos * 64, row0 + b});
+    } else {
+      dec_attend(qf, K, V, t + 1, sc, part, red, outv);
+    }
     if (tid < 64) out[(size_t)b * D + h * 64 + tid] = f32_to_bf16(outv[tid]);
     return;
   }
@@ -819,8 +849,10 @@ __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__
 #pragma unroll
   for (int u = 0; u < DS2_U; ++u) {
     const int key = min(u * 32 + g, last);
-    kk[u] = *(const uint4*)(K + (size_t)key * 64 + gl * 8);
-    vv[u] = *(const uint4*)(V + (size_t)key * 64 + gl * 8);
+    long o = (long)key * 64;
+    if constexpr (TAB) o = TabRows{kv_tab + (size_t)(row0 + b) * max_pos, (long)H * max_pos * 64, row0 + b}(key);
+    kk[u] = *(const uint4*)(K + o + gl * 8);
+    vv[u] = *(const uint4*)(V + o + gl * 8);
   }
   __builtin_amdgcn_sched_barrier(0);
   if (g == 0) {  // the cache append (read back by the following steps only)
@@ -888,9 +920,19 @@ extern "C" int tw_attn_decode_self(const bf16_t* qkv, int B, int H, int max_pos,
                                    bf16_t* v_cache, bf16_t* out, void* stream) {
   TW_REQUIRE(qkv && pos && k_cache && v_cache && out && B > 0 && H > 0, "tw_attn_decode_self: bad args");
   TW_REQUIRE(max_pos <= DA_SELF_MAXK, "tw_attn_decode_self: max_pos %d > %d", max_pos, DA_SELF_MAXK);
-  hipLaunchKernelGGL(k_attn_decode_self2, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos, pos,
-                     k_cache, v_cache, out);
+  hipLaunchKernelGGL(k_attn_decode_self2<false>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos,
+                     pos, k_cache, v_cache, nullptr, 0, out);
   return tw_check_launch("tw_attn_decode_self");
+}
+
+extern "C" int tw_attn_decode_self_tab(const bf16_t* qkv, int B, int H, int max_pos, const int* pos, bf16_t* k_cache,
+                                       bf16_t* v_cache, const int* kv_tab, int row0, bf16_t* out, void* stream) {
+  TW_REQUIRE(qkv && pos && k_cache && v_cache && kv_tab && out && B > 0 && H > 0 && row0 >= 0,
+             "tw_attn_decode_self_tab: bad args");
+  TW_REQUIRE(max_pos <= DA_SELF_MAXK, "tw_attn_decode_self_tab: max_pos %d > %d", max_pos, DA_SELF_MAXK);
+  hipLaunchKernelGGL(k_attn_decode_self2<true>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos,
+                     pos, k_cache, v_cache, kv_tab, row0, out);
+  return tw_check_launch("tw_attn_decode_self_tab");
 }
 
 // Optional output for token-level timestamps (return_timestamps="word"): the attention probabilities of the

@@ -620,10 +620,9 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
 #pragma unroll
   for (int j = 0; j < K; ++j) T[j] = S[j] = Cand{-INFINITY, 0x7fffffff};
   float m_all = -INFINITY, s_all = 0.f, m_ts = -INFINITY, s_ts = 0.f;
-  for (int v = v0 + tid; v < v1; v += 256) {
-    const float x = row[v];
+  auto visit = [&](int v, float x, uint32_t sbw) {
     lse_merge(m_all, s_all, x, 1.f);
-    bool masked = (suppress_bits ? (suppress_bits[v >> 5] >> (v & 31)) & 1u : 0u);
+    bool masked = (sbw >> (v & 31)) & 1u;
     if (rm.init_step)
       for (int i = 0; i < p.n_begin_suppress; ++i) masked |= (v == p.begin_suppress[i]);
     if (p.use_timestamps) {
@@ -635,14 +634,31 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
         masked |= (rm.mask_text_lt_eos && v < p.eos) || rm.init_step;
       }
     }
-    if (masked) continue;
+    if (masked) return;
     if (v < tsb || !p.use_timestamps) {
       cand_insert<K>(T, x, v);
     } else {
       cand_insert<K>(S, x, v);
       lse_merge(m_ts, s_ts, x, 1.f);
     }
+  };
+  // every logit (and suppress word) of this thread's share in flight at once: one load per loop trip serialised ~13
+  // memory round trips (57 us per launch at 60 rows); a share past BP_MAXE per thread (V > 65536) takes the tail loop
+  constexpr int BP_MAXE = 16;
+  float xs[BP_MAXE];
+  uint32_t sb[BP_MAXE];
+#pragma unroll
+  for (int u = 0; u < BP_MAXE; ++u) {
+    const int v = min(v0 + tid + 256 * u, v1 - 1);
+    xs[u] = row[v];
+    sb[u] = suppress_bits ? suppress_bits[v >> 5] : 0u;
   }
+#pragma unroll
+  for (int u = 0; u < BP_MAXE; ++u) {
+    const int v = v0 + tid + 256 * u;
+    if (v < v1) visit(v, xs[u], sb[u]);
+  }
+  for (int v = v0 + tid + 256 * BP_MAXE; v < v1; v += 256) visit(v, row[v], suppress_bits ? suppress_bits[v >> 5] : 0u);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     float m2 = __shfl_xor(m_all, o, 64), s2 = __shfl_xor(s_all, o, 64);
@@ -651,8 +667,14 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
     s2 = __shfl_xor(s_ts, o, 64);
     lse_merge(m_ts, s_ts, m2, s2);
   }
+#if TW_BP_PROBE == 1  // timing probe only (scripts/exp/beam_kernels_bench.py): no list reductions
+  if (lane == 0) {
+    for (int j = 0; j < K; ++j) { wl[0][wid][j] = T[j]; wl[1][wid][j] = S[j]; }
+  }
+#else
   wave_topk<K>(T, wl[0][wid], lane);
   wave_topk<K>(S, wl[1][wid], lane);
+#endif
   if (lane == 0) {
     wst[wid][0] = m_all;
     wst[wid][1] = s_all;
@@ -711,6 +733,8 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
   __shared__ int old_tok[TW_BEAM_MAXNB][TW_BEAM_MAXT];
   __shared__ int old_fin[TW_BEAM_MAXNB][TW_BEAM_MAXT];
   __shared__ int old_st[TW_BEAM_MAXNB][TW_STATE_STRIDE];
+  __shared__ int old_tab[TW_BEAM_MAXNB][TW_BEAM_MAXT];  // the K/V position table rows (bs.kv_tab)
+  __shared__ int old_pos[TW_BEAM_MAXNB];
   __shared__ int old_flen[TW_BEAM_MAXNB];
   __shared__ int s_src[TW_BEAM_MAXNB], s_tok[TW_BEAM_MAXNB], f_from[TW_BEAM_MAXNB], f_flag[TW_BEAM_MAXNB];
   __shared__ float s_score[TW_BEAM_MAXNB], f_score[TW_BEAM_MAXNB];
@@ -725,6 +749,24 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
   int* win = bs.win + 4 * w;
   const int t = win[2];
   const float NEG = -1.0e9f;
+  // the window's running and finished histories and processor states, loaded now so their latency hides behind
+  // step 1 (as a load-then-LDS-store loop after it, each trip waited for its own loads); positions past a history's
+  // length are staged too (any value: they are never read back)
+  constexpr int STG = (TW_BEAM_MAXNB * TW_BEAM_MAXT + 511) / 512;
+  int rt[STG], rf[STG], rk[STG];
+  const bool tab = bs.kv_tab != nullptr;
+#pragma unroll
+  for (int u = 0; u < STG; ++u) {
+    const int e = tid + 512 * u, j = e / TW_BEAM_MAXT, q = e % TW_BEAM_MAXT;
+    const bool ok = j < nb && q < ldt;
+    const size_t off = (size_t)(w * nb + (ok ? j : 0)) * ldt + (ok ? q : 0);
+    rt[u] = ok ? tokens[off] : 0;
+    rf[u] = ok ? bs.fin_tokens[off] : 0;
+    rk[u] = ok && tab ? bs.kv_tab[off] : 0;
+  }
+  const int st_v = tid < nb * TW_STATE_STRIDE ? state[(w * nb) * TW_STATE_STRIDE + tid] : 0;
+  const int fl_v = tid < nb ? bs.fin_len[w * nb + tid] : 0;
+  const int ps_v = tid < nb ? pos[w * nb + tid] : 0;
 
   // 1. per row (one wave each): merge the chunk records, apply the timestamp rule, score the candidates
   if (wid < nb) {
@@ -801,14 +843,20 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
     }
   }
   // stage the old running histories, finished histories and processor states of the window
-  for (int e = tid; e < nb * TW_BEAM_MAXT; e += blockDim.x) {
-    const int j = e / TW_BEAM_MAXT, q = e % TW_BEAM_MAXT;
-    const int row = w * nb + j;
-    old_tok[j][q] = q < t ? tokens[(size_t)row * ldt + q] : 0;
-    old_fin[j][q] = q < bs.fin_len[row] ? bs.fin_tokens[(size_t)row * ldt + q] : 0;
+#pragma unroll
+  for (int u = 0; u < STG; ++u) {
+    const int e = tid + 512 * u, j = e / TW_BEAM_MAXT, q = e % TW_BEAM_MAXT;
+    if (j < nb) {
+      old_tok[j][q] = rt[u];
+      old_fin[j][q] = rf[u];
+      old_tab[j][q] = rk[u];
+    }
   }
-  if (tid < nb * TW_STATE_STRIDE) old_st[tid / TW_STATE_STRIDE][tid % TW_STATE_STRIDE] = state[(w * nb) * TW_STATE_STRIDE + tid];
-  if (tid < nb) old_flen[tid] = bs.fin_len[w * nb + tid];
+  if (tid < nb * TW_STATE_STRIDE) old_st[tid / TW_STATE_STRIDE][tid % TW_STATE_STRIDE] = st_v;
+  if (tid < nb) {
+    old_flen[tid] = fl_v;
+    old_pos[tid] = ps_v;
+  }
   __syncthreads();
 
   // 2. the window's beam bookkeeping (one thread: nb * K <= 128 candidates)
@@ -898,6 +946,14 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
   for (int e = tid; e < nb * (t + 1); e += blockDim.x) {
     const int j = e / (t + 1), q = e % (t + 1);
     tokens[(size_t)(w * nb + j) * ldt + q] = q < t ? old_tok[s_src[j]][q] : s_tok[j];
+  }
+  // K/V position table: the new beam j reads its source's history, positions [0, pos + 1) (this step's position
+  // included: the source wrote it); later positions keep j's own row (kv_tab[r][*] = r from the pass start)
+  if (tab) {
+    for (int e = tid; e < nb * TW_BEAM_MAXT; e += blockDim.x) {
+      const int j = e / TW_BEAM_MAXT, q = e % TW_BEAM_MAXT;
+      if (q <= old_pos[j] && q < ldt && s_src[j] != j) bs.kv_tab[(size_t)(w * nb + j) * ldt + q] = old_tab[s_src[j]][q];
+    }
   }
   for (int e = tid; e < nb * TW_BEAM_MAXT; e += blockDim.x) {
     const int qs = e / TW_BEAM_MAXT, q = e % TW_BEAM_MAXT;

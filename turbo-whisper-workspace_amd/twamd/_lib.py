@@ -36,7 +36,7 @@ EXPORTED = (
     "tw_im2col_conv2", "tw_gemm_bf16", "tw_layernorm", "tw_attn_encoder", "tw_attn_decode_self",
     "tw_attn_decode_cross", "tw_embed_decoder", "tw_logits_select", "tw_gemm_bf16_partial", "tw_resid_layernorm",
     "tw_gemm_set_variant", "tw_attn_set_variant",
-    "tw_dtw", "tw_attn_decode_cross_probs", "tw_attn_decode_cross_grouped", "tw_attn_decode_cross_grouped_ws_bytes", "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
+    "tw_dtw", "tw_attn_decode_cross_probs", "tw_attn_decode_cross_grouped", "tw_attn_decode_cross_grouped_ws_bytes", "tw_attn_decode_self_tab", "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
     "tw_gemm_mx", "tw_quant_mx", "tw_layernorm_mx", "tw_attn_encoder_mx", "tw_gemm_mx_set_variant", "tw_logits_select_embed",
     "tw_attn_set_lds_pad", "tw_logits_sample", "tw_token_prob", "tw_g711_decode", "tw_ima_adpcm_wav_decode",
 )
@@ -59,7 +59,7 @@ class TwBeamParams(ctypes.Structure):
 class TwBeamState(ctypes.Structure):
     _fields_ = [("run_score", ctypes.c_void_p), ("fin_score", ctypes.c_void_p), ("fin_flag", ctypes.c_void_p),
                 ("fin_len", ctypes.c_void_p), ("fin_tokens", ctypes.c_void_p), ("win", ctypes.c_void_p),
-                ("src_rows", ctypes.c_void_p)]
+                ("src_rows", ctypes.c_void_p), ("kv_tab", ctypes.c_void_p)]
 
 
 class TwFlacInfo(ctypes.Structure):
@@ -116,6 +116,7 @@ _SIGS = {
     "tw_attn_decode_cross_probs": ([_P, _I, _I, _I, _I, _P, _P, _P, _P, _U32, _I, _I, _P, _I, _I, _P], _I),
     "tw_beam_workspace_bytes": ([_I], ctypes.c_size_t),
     "tw_attn_decode_cross_grouped_ws_bytes": ([_I, _I], ctypes.c_size_t),
+    "tw_attn_decode_self_tab": ([_P, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P], _I),
     "tw_beam_step": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), ctypes.POINTER(TwBeamParams),
                       ctypes.POINTER(TwBeamState), _P, _P, _P, _P, _P, _P], _I),
     "tw_kv_reorder": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P], _I),

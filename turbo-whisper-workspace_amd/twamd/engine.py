@@ -221,6 +221,7 @@ class WhisperEngine:
         self._use_dec_row_map = False
         self._row_group = 1
         self._xws: Optional[torch.Tensor] = None
+        self._kv_tab: Optional[torch.Tensor] = None  # beam pass: the self-attention K/V position table
         self._beam: Optional[dict] = None  # beam-search buffers, allocated on first use
         self._align: Optional[dict] = None  # token-level timestamps: alignment-head attention recording
         self._align_buf: Optional[torch.Tensor] = None
@@ -546,8 +547,13 @@ class WhisperEngine:
             if li or not pre_embedded:
                 self._resid_ln_p(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
             self._gemv(v.hp, True, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
-            _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
-                      self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
+            if self._kv_tab is not None:  # beam pass: histories through the position table
+                _lib.call("tw_attn_decode_self_tab", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
+                          self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), self._kv_tab.data_ptr(),
+                          v.r0, v.attd.data_ptr(), s)
+            else:
+                _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
+                          self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
             self._gemv(v.attd, False, P["wo"], R, D, D, PART, v.parts, v, splits=K4)
             self._resid_ln_p(R, K4, L.bo, L.ln2_g, L.ln2_b, v)
             self._gemv(v.hp, True, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
@@ -880,6 +886,7 @@ class WhisperEngine:
                 "win": torch.zeros(self.max_batch, 4, dtype=torch.int32, device=dev),
                 "src_rows": torch.zeros(self.max_rows, dtype=torch.int32, device=dev),
                 "ws": torch.empty(ws_bytes, dtype=torch.uint8, device=dev),
+                "kv_tab": torch.empty(self.max_rows, T, dtype=torch.int32, device=dev),
             }
         return self._beam
 
@@ -890,7 +897,7 @@ class WhisperEngine:
         """Beam-search decode (GenerationMixin._beam_search, $TF/generation/utils.py:3208-3512) of W windows with
         num_beams rows each (row = w * num_beams + j, all reading window w's cross-K/V): the prompt as
         decode_pass (language detected from the SOT step when lang_ids is None), then per token one decoder step
-        over all rows, tw_beam_step and the self-attention K/V reorder. Returns the best finished hypothesis of
+        over all rows and tw_beam_step (which also repoints the self-attention K/V position table). Returns the best finished hypothesis of
         every window (with its EOS when it ended on one). enc_row0 / r_enc: the windows' first row and the batch
         the cross-K/V slot was encoded with (default 0 / W)."""
         nb, R = num_beams, W * num_beams
@@ -905,6 +912,10 @@ class WhisperEngine:
         self.dec_row_map[:R] = enc_row0 + torch.arange(R, dtype=torch.int32, device=dev) // nb
         self._use_dec_row_map = True
         self._row_group = nb  # rows w * nb + j share window w's cross K/V
+        # self-attention K/V position table: every row starts on its own history; tw_beam_step points a continuing
+        # beam at its source's rows (no K/V copy: the reorder moved ~550 MB per step at 60 rows)
+        bb["kv_tab"][:R] = torch.arange(R, dtype=torch.int32, device=dev)[:, None]
+        self._kv_tab = bb["kv_tab"]
         try:
             self.state[:R].zero_()
             self.state[:R, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
@@ -938,20 +949,16 @@ class WhisperEngine:
             bp = _lib.TwBeamParams(nb, max_new, float(length_penalty), T)
             bst = _lib.TwBeamState(bb["run_score"].data_ptr(), bb["fin_score"].data_ptr(), bb["fin_flag"].data_ptr(),
                                    bb["fin_len"].data_ptr(), bb["fin_tokens"].data_ptr(), bb["win"].data_ptr(),
-                                   bb["src_rows"].data_ptr())
+                                   bb["src_rows"].data_ptr(), bb["kv_tab"].data_ptr())
             s = self.stream.cuda_stream
-            L, H = self.d.decoder_layers, self.d.heads
 
             def step() -> None:
                 self.decoder_step(R, r_enc=r_enc)
                 _lib.call("tw_beam_step", self.logits.data_ptr(), W, self.d.vocab, self.suppress_bits.data_ptr(),
                           ctypes.byref(sel), ctypes.byref(bp), ctypes.byref(bst), self.state.data_ptr(),
                           self.tokens.data_ptr(), self.ids.data_ptr(), self.pos.data_ptr(), bb["ws"].data_ptr(), s)
-                _lib.call("tw_kv_reorder", self.kcache.data_ptr(), self.vcache.data_ptr(), None, None, L,
-                          self.max_rows, H, T, R, bb["src_rows"].data_ptr(),
-                          self.pos.data_ptr(), s)
 
-            # one beam step (decoder step over every row, tw_beam_step, the K/V reorder) as one captured graph: the
+            # one beam step (decoder step over every row, tw_beam_step with its K/V table update) as one captured graph: the
             # step reads its position, scores and histories from device memory, so the same graph serves every step
             # (eager, each of its ~100 launches would be issued from the host every token)
             g = None
@@ -978,6 +985,7 @@ class WhisperEngine:
         finally:
             self._use_dec_row_map = False
             self._row_group = 1
+            self._kv_tab = None
         return PassResult([ftok[w][: flen[w]] for w in range(W)], detected if lang_ids is None else list(lang_ids))
 
     def _chains(self, R: int) -> List[DecView]:
