@@ -1094,7 +1094,9 @@ __global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_lean(const bf16_t* __re
 // kernel's (NG key groups, UNR blocks, the same merges).
 // Block y takes rows [r_lo, r_hi): the first `first` rows of the view (the tail of a window that began in the
 // previous view), then groups of G.
+#ifndef DA_XSPLIT
 #define DA_XSPLIT 3
+#endif
 template <int G, int NG = 32, int UNR = DA_UNR>
 __global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_grp(const bf16_t* __restrict__ q, int D, int S, int Bt, int R,
                                                                int first, const int* __restrict__ row_map,
