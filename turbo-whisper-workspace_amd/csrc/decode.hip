@@ -615,7 +615,11 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
   const RowMask rm = row_mask(state + b * TW_STATE_STRIDE, p);
   const float* row = logits + (size_t)b * ld_logits;
   const int V = p.V, tsb = p.ts_begin;
-  const int v0 = (int)((long)c * V / NC), v1 = (int)((long)(c + 1) * V / NC);
+  // with timestamps the last chunk is exactly the timestamp tokens and the others split the text tokens, so no block
+  // holds both kinds: each reduces one candidate list (the block holding both set the launch's duration)
+  const bool split_ts = p.use_timestamps && tsb > 0 && tsb < V && NC > 1;
+  const int v0 = split_ts ? (c == NC - 1 ? tsb : (int)((long)c * tsb / (NC - 1))) : (int)((long)c * V / NC);
+  const int v1 = split_ts ? (c == NC - 1 ? V : (int)((long)(c + 1) * tsb / (NC - 1))) : (int)((long)(c + 1) * V / NC);
   Cand T[K], S[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) T[j] = S[j] = Cand{-INFINITY, 0x7fffffff};
@@ -667,14 +671,12 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
     s2 = __shfl_xor(s_ts, o, 64);
     lse_merge(m_ts, s_ts, m2, s2);
   }
-#if TW_BP_PROBE == 1  // timing probe only (scripts/exp/beam_kernels_bench.py): no list reductions
-  if (lane == 0) {
-    for (int j = 0; j < K; ++j) { wl[0][wid][j] = T[j]; wl[1][wid][j] = S[j]; }
-  }
-#else
-  wave_topk<K>(T, wl[0][wid], lane);
-  wave_topk<K>(S, wl[1][wid], lane);
-#endif
+  // a chunk wholly below the timestamps has no timestamp candidate (14 of the 16 chunks at large-v3 sizes), one
+  // wholly inside them no text candidate: that list's K dependent argmax rounds (here and in the merge below) are
+  // skipped, uniformly per block (each round is a 6-level shuffle chain: the reductions were ~20 us of 55)
+  const bool any_ts = p.use_timestamps && v1 > tsb, any_tx = !p.use_timestamps || v0 < tsb;
+  if (any_tx) wave_topk<K>(T, wl[0][wid], lane);
+  if (any_ts) wave_topk<K>(S, wl[1][wid], lane);
   if (lane == 0) {
     wst[wid][0] = m_all;
     wst[wid][1] = s_all;
@@ -685,6 +687,13 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
   if (wid != 0) return;
   BeamPart<K>* out = ws + (size_t)b * NC + c;
   for (int l = 0; l < 2; ++l) {  // merge the 4 wave lists: lane q holds entry q (4K <= 64), K rounds of argmax
+    if (!(l == 0 ? any_tx : any_ts)) {  // an empty list
+      if (lane < K) {
+        if (l == 0) out->t[lane] = Cand{-INFINITY, 0x7fffffff};
+        else out->s[lane] = Cand{-INFINITY, 0x7fffffff};
+      }
+      continue;
+    }
     Cand mine = lane < 4 * K ? wl[l][lane / K][lane % K] : Cand{-INFINITY, 0x7fffffff};
     bool used = false;
     for (int r = 0; r < K; ++r) {
