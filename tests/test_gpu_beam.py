@@ -156,6 +156,11 @@ def test_self_attention_position_table_equals_gathered_history(t_max):
     tab = torch.arange(cap, dtype=torch.int32)[:, None].repeat(1, T)
     for r in range(R):  # positions < pos of view row r come from random global rows; pos itself stays own
         tab[row0 + r, : int(pos[r])] = torch.randint(0, cap, (int(pos[r]),), generator=gen, dtype=torch.int32)
+    for r in range(R):  # (row0 + r2, pos[r2]) is written by this very launch: no history entry may read it. Beam
+        for r2 in range(R):  # search never builds such a table (a window's beams share one position), the random
+            p2 = int(pos[r2])  # per-row positions here could, and the read would race the write
+            if p2 < int(pos[r]) and int(tab[row0 + r, p2]) == row0 + r2:
+                tab[row0 + r, p2] = row0 + r
     kg, vg = k.clone(), v.clone()  # gathered: row0 + r holds its logical history contiguously
     for r in range(R):
         for q in range(int(pos[r])):
