@@ -237,7 +237,9 @@ int tw_attn_decode_self(const uint16_t* qkv, int B, int H, int max_pos, const in
  * kv_tab[(row0 + b) * max_pos + q] (a global row: k_cache / v_cache point at row row0 of the layer's caches, which
  * hold rows_cap rows); the step's own K/V is written to row b at pos[b], and kv_tab[(row0 + b) * max_pos + pos[b]]
  * must equal row0 + b (tw_beam_step keeps it so). Each physical (row, position) is written once per pass, so no
- * history is ever overwritten while another beam still reads it. */
+ * history is ever overwritten while another beam still reads it. Caller contract: no history entry q < pos[b] may
+ * name a row b2 of this launch with q == pos[b2] (that cell is written by the same launch; the read would race).
+ * Beam tables keep it: a window's beams share one position. */
 int tw_attn_decode_self_tab(const uint16_t* qkv, int B, int H, int max_pos, const int* pos, uint16_t* k_cache,
                             uint16_t* v_cache, const int* kv_tab, int row0, uint16_t* out, void* stream);
 /* Decoder cross-attention for one query per row over the cached encoder K/V of this layer,
