@@ -58,8 +58,40 @@ def parse():
     return ap.parse_args()
 
 
+def launch_plan(gpus: int, env) -> str:
+    """How this process runs `--gpus gpus`: "run" (it is one of the ranks, or the only one), "spawn" (no launcher
+    started it and gpus > 1: start one worker per GPU through torch.distributed.run before anything touches the GPU,
+    then exit with their code), or "mismatch" (a launcher started WORLD_SIZE ranks that differ from --gpus)."""
+    if gpus < 1:
+        return "mismatch"
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "spawn" if gpus > 1 else "run"
+    return "run" if int(ws) == gpus else "mismatch"
+
+
+def spawn_workers(gpus: int, argv) -> int:
+    """One worker process per GPU (torchrun, rendezvous on 127.0.0.1); returns their exit code. The parent never
+    initialises the GPU (no HIP call happens before this), and it starts the launcher as a child, never exec()s."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     a = parse()
+    plan = launch_plan(a.gpus, os.environ)
+    if plan == "mismatch":
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')}", file=sys.stderr)
+        sys.exit(2)
+    if plan == "spawn":
+        sys.exit(spawn_workers(a.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -205,7 +205,7 @@ int tw_beam_step(const float* logits, int W, int ld_logits, const uint32_t* supp
                  const TwSelectParams* params, const TwBeamParams* beam, const TwBeamState* bstate, int* state,
                  int* tokens, int* ids, int* pos, void* workspace, void* stream);
 /* caches bf16[layers][rows_cap][H][T][64]: rows 0..R-1 take positions [0, pos[r]) of row src_rows[r] (any
- * permutation, R <= 512), in place. k_scratch / v_scratch are unused (may be NULL; kept for ABI stability). */
+ * permutation, R <= 448 = the 56 KiB LDS tile at one position), in place. k_scratch / v_scratch are unused (may be NULL; kept for ABI stability). */
 int tw_kv_reorder(uint16_t* k_cache, uint16_t* v_cache, uint16_t* k_scratch, uint16_t* v_scratch, int layers,
                   int rows_cap, int H, int T, int R, const int* src_rows, const int* pos, void* stream);
 
@@ -239,9 +239,17 @@ int tw_attn_decode_self(const uint16_t* qkv, int B, int H, int max_pos, const in
  * must equal row0 + b (tw_beam_step keeps it so). Each physical (row, position) is written once per pass, so no
  * history is ever overwritten while another beam still reads it. Caller contract: no history entry q < pos[b] may
  * name a row b2 of this launch with q == pos[b2] (that cell is written by the same launch; the read would race).
- * Beam tables keep it: a window's beams share one position. */
+ * Beam tables keep it: a window's beams share one position. A library built with -DTW_DEBUG=1 (`make debug`,
+ * libtwhip_dbg.so) checks the contract with tw_kv_tab_check before every launch outside a graph capture and returns
+ * TW_ERR_ARG naming the row instead of racing. */
 int tw_attn_decode_self_tab(const uint16_t* qkv, int B, int H, int max_pos, const int* pos, uint16_t* k_cache,
                             uint16_t* v_cache, const int* kv_tab, int row0, uint16_t* out, void* stream);
+/* The contract of tw_attn_decode_self_tab as a check: bad int32[B] (device) receives, per row b of a launch with the
+ * same (kv_tab, pos, row0, B, max_pos), the number of history entries that name a (row, position) that launch
+ * writes (0 everywhere = the launch is race-free). Asynchronous on `stream`. */
+int tw_kv_tab_check(const int* kv_tab, const int* pos, int row0, int B, int max_pos, int* bad, void* stream);
+/* 1 if the library was built with -DTW_DEBUG=1 (the guarded tw_attn_decode_self_tab), else 0. */
+int tw_debug_build(void);
 /* Decoder cross-attention for one query per row over the cached encoder K/V of this layer,
  * cross_kv bf16[2][Bt][H][S][64]; row b reads slot row_map[b] (NULL = b). */
 int tw_attn_decode_cross(const uint16_t* q, int B, int H, int S, int Bt, const int* row_map, const uint16_t* cross_kv,

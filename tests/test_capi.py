@@ -59,3 +59,28 @@ def test_errors_are_reported_not_raised_in_c(lib_path):
         _lib.call("tw_gemm_bf16", 1, 1, 16, 16, 48, 48, 48, 0, 1, 16, None, None, 0, None, None)
     with pytest.raises(_lib.TwError, match="null"):
         _lib.call("tw_logmel", None, 1, None, None, None, 80, None, None, None)
+
+
+def test_debug_library_exports_the_same_abi_and_says_so():
+    """libtwhip_dbg.so (make debug: -DTW_DEBUG=1, the C-ABI contract checks) exports the same symbols and reports
+    itself as the debug build; the product library does not."""
+    dbg = os.path.join(ROOT, "turbo-whisper-workspace_amd", "twamd", "libtwhip_dbg.so")
+    if not os.path.exists(dbg):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "turbo-whisper-workspace_amd", "csrc"), "-j8", "debug"],
+                       check=True, capture_output=True)
+    out = subprocess.run(["nm", "-D", "--defined-only", dbg], check=True, capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (tw_\w+)", out))
+    assert not [n for n in _declared() if n not in exported]
+    import torch  # noqa: F401
+    assert ctypes.CDLL(dbg).tw_debug_build() == 1
+    assert ctypes.CDLL(LIB).tw_debug_build() == 0
+
+
+def test_tw_lib_override_is_refused(monkeypatch):
+    """The old A/B scripts' TW_LIB variable is refused, not silently ignored."""
+    import torch  # noqa: F401
+    from twamd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setenv("TW_LIB", "/tmp/other.so")
+    with pytest.raises(_lib.TwError, match="TW_LIB"):
+        _lib.load()

@@ -419,3 +419,48 @@ def test_batch_sizes_policy():
     for n in range(1, 100):
         s = batch_sizes(n, 24, 6)
         assert sum(s) == n and max(s) <= 24 and max(s) - min(s) <= 1
+
+
+def test_fallback_keys_are_global_window_indices():
+    """the fallback sampler's row keys come from global window indices (batch offset + rank shard
+    base), so window j of batch 0 and window j of batch 1 draw different noise."""
+    from twamd.engine import fallback_row_key
+    from twamd.pipeline import TurboTranscriber
+    from twamd.segments import FallbackConfig
+    keys = {fallback_row_key(w, p, f) for w in range(200) for p in range(3) for f in range(6)}
+    assert len(keys) == 200 * 3 * 6
+    with pytest.raises(ValueError):
+        fallback_row_key(2 ** 21, 0, 0)
+
+    seen = []
+
+    class Eng(_FakeEngine):
+        def run_batches(self, sizes, load=None, batch_kwargs=None, **kw):
+            seen.append((list(sizes), kw.get("window_offset")))
+            return super().run_batches(sizes, load, batch_kwargs)
+
+    eng = Eng(8)
+    tr = TurboTranscriber(eng, WhisperVocab.synthetic(ST))
+    fb = FallbackConfig(temperatures=(0.0, 0.2), compression_ratio_threshold=2.4, logprob_threshold=-1.0,
+                        no_speech_threshold=None, top_k=50, seed=0)
+    wav = np.random.default_rng(5).standard_normal(20 * 480000).astype(np.float32)
+    from twamd.frontend import chunk_windows
+    ws = list(chunk_windows(len(wav), 30, 0, 16000))
+    tr.transcribe_windows(wav, ws[10:], task="transcribe", lang_id=None, return_timestamps=True, fallback=fb,
+                          window_base=10)
+    assert seen == [([5, 5], 10)]  # run_batches adds each batch's offset: keys of windows 10..19
+
+
+def test_checkpoint_thresholds_with_default_beams_say_why():
+    """a checkpoint whose generation_config sets a fallback threshold turns the fallback on for every
+    call; with the pipeline's default beam-5 the call raises and names the checkpoint field."""
+    from twamd.pipeline import TurboTranscriber
+    eng = _FakeEngine(8)
+    eng.gen.logprob_threshold = -1.0
+    tr = TurboTranscriber(eng, WhisperVocab.synthetic(ST))
+    wav = np.zeros(16000, np.float32)
+    with pytest.raises(NotImplementedError, match="logprob_threshold"):
+        tr(wav, chunk_length_s=30, generate_kwargs={"task": "transcribe"}, return_timestamps=True)
+    out = tr(wav, chunk_length_s=30, generate_kwargs={"task": "transcribe", "num_beams": 1, "max_passes": 1},
+             return_timestamps=True)
+    assert "text" in out

@@ -280,3 +280,94 @@ def test_default_callable_long_audio_matches_transformers_pipeline():
     assert r["text"] == ref["text"]
     assert [(tuple(c["timestamp"]), c["text"]) for c in r["chunks"]] == \
         [(tuple(c["timestamp"]), c["text"]) for c in ref["chunks"]]
+
+
+def _racy_table(R, cap, T, row0, seed):
+    """Random per-row positions and history sources, WITHOUT removing the entries that name a (row, position) the
+    same launch writes (the contract tw_attn_decode_self_tab states), plus the host count of such entries per row."""
+    gen = torch.Generator(device="cpu").manual_seed(seed)
+    pos = torch.randint(20, 60, (R,), generator=gen, dtype=torch.int32)
+    tab = torch.arange(cap, dtype=torch.int32)[:, None].repeat(1, T)
+    for r in range(R):
+        tab[row0 + r, : int(pos[r])] = torch.randint(row0, row0 + R, (int(pos[r]),), generator=gen, dtype=torch.int32)
+    bad = [sum(1 for q in range(int(pos[r])) if 0 <= int(tab[row0 + r, q]) - row0 < R
+               and int(pos[int(tab[row0 + r, q]) - row0]) == q) for r in range(R)]
+    return tab, pos, bad
+
+
+def test_kv_tab_check_counts_contract_violations():
+    """tw_kv_tab_check against a host count of the entries that would race, on a racy table and on the same table
+    with those entries pointed back at the row itself (0 everywhere)."""
+    R, cap, T, row0 = 12, 20, 448, 5
+    tab, pos, bad = _racy_table(R, cap, T, row0, 11)
+    assert sum(bad) > 0
+    out = torch.full((R,), -1, dtype=torch.int32, device=DEV)
+    tab_d, pos_d = tab.to(DEV), pos.to(DEV)
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.call("tw_kv_tab_check", tab_d.data_ptr(), pos_d.data_ptr(), row0, R, T, out.data_ptr(), s)
+    assert out.cpu().tolist() == bad
+    for r in range(R):
+        for q in range(int(pos[r])):
+            r2 = int(tab[row0 + r, q]) - row0
+            if 0 <= r2 < R and int(pos[r2]) == q:
+                tab[row0 + r, q] = row0 + r
+    tab_d = tab.to(DEV)
+    _lib.call("tw_kv_tab_check", tab_d.data_ptr(), pos_d.data_ptr(), row0, R, T, out.data_ptr(), s)
+    assert out.cpu().tolist() == [0] * R
+
+
+def test_debug_build_refuses_racy_position_table():
+    """the -DTW_DEBUG=1 library (libtwhip_dbg.so) checks the position-table contract before the
+    launch and fails loudly (TW_ERR_ARG naming the row) instead of racing; a valid table runs and gives the product
+    library's output bit for bit."""
+    dbg = _lib.load_debug()
+    R, cap, T, row0, H = 12, 20, 448, 5, 4
+    tab, pos, bad = _racy_table(R, cap, T, row0, 12)
+    assert sum(bad) > 0
+    gen = torch.Generator(device="cpu").manual_seed(3)
+    k = torch.randn(cap, H, T, 64, generator=gen).to(torch.bfloat16).to(DEV)
+    v = torch.randn(cap, H, T, 64, generator=gen).to(torch.bfloat16).to(DEV)
+    qkv = (torch.randn(R, 3 * H * 64, generator=gen) * 0.125).to(torch.bfloat16).to(DEV)
+    out = torch.empty(R, H * 64, dtype=torch.bfloat16, device=DEV)
+    s = torch.cuda.current_stream().cuda_stream
+    tab_d, pos_d = tab.to(DEV), pos.to(DEV)
+    k1, v1 = k.clone(), v.clone()
+    rc = dbg.tw_attn_decode_self_tab(qkv.data_ptr(), R, H, T, pos_d.data_ptr(), k1[row0].data_ptr(),
+                                     v1[row0].data_ptr(), tab_d.data_ptr(), row0, out.data_ptr(), s)
+    assert rc == 1, rc
+    first = next(r for r in range(R) if bad[r])
+    msg = dbg.tw_last_error().decode()
+    assert "precondition violated" in msg and f"row {row0 + first}" in msg, msg
+    assert torch.equal(k1, k) and torch.equal(v1, v)  # refused before the launch: nothing written
+    for r in range(R):  # repaired table: runs, same output as the product library
+        for q in range(int(pos[r])):
+            r2 = int(tab[row0 + r, q]) - row0
+            if 0 <= r2 < R and int(pos[r2]) == q:
+                tab[row0 + r, q] = row0 + r
+    tab_d = tab.to(DEV)
+    k2, v2 = k.clone(), v.clone()
+    out2 = torch.empty_like(out)
+    assert dbg.tw_attn_decode_self_tab(qkv.data_ptr(), R, H, T, pos_d.data_ptr(), k1[row0].data_ptr(),
+                                       v1[row0].data_ptr(), tab_d.data_ptr(), row0, out.data_ptr(), s) == 0
+    _lib.call("tw_attn_decode_self_tab", qkv.data_ptr(), R, H, T, pos_d.data_ptr(), k2[row0].data_ptr(),
+              v2[row0].data_ptr(), tab_d.data_ptr(), row0, out2.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2) and torch.equal(k1, k2) and torch.equal(v1, v2)
+
+
+def test_kv_reorder_row_limit():
+    """tw_kv_reorder stages one position of every moved row in LDS (R * 128 B <= 56 KiB): R = 448 runs,
+    R = 449 is refused up front instead of asking for more LDS than the launch may use."""
+    L, H, T = 1, 1, 4
+    for R, ok in ((448, True), (449, False)):
+        k = torch.randn(L, R, H, T, 64, device=DEV).to(torch.bfloat16)
+        v = torch.randn(L, R, H, T, 64, device=DEV).to(torch.bfloat16)
+        k0 = k.clone()
+        src = torch.arange(R, dtype=torch.int32, device=DEV).flip(0)
+        pos = torch.full((R,), 3, dtype=torch.int32, device=DEV)
+        rc = _lib.load().tw_kv_reorder(k.data_ptr(), v.data_ptr(), None, None, L, R, H, T, R, src.data_ptr(),
+                                       pos.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert (rc == 0) == ok, (R, rc)
+        if ok:
+            assert torch.equal(k[:, :, :, :3], k0[:, src.long(), :, :3])

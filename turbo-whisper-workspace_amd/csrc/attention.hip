@@ -925,15 +925,85 @@ extern "C" int tw_attn_decode_self(const bf16_t* qkv, int B, int H, int max_pos,
   return tw_check_launch("tw_attn_decode_self");
 }
 
+// The position table's precondition (tw_whisper.h, tw_attn_decode_self_tab): no history entry of a row of the launch
+// (key q < pos[b]) may name a (cache row, position) that the same launch writes, i.e. kv_tab[row0 + b][q] == row0 + b2
+// with q == pos[b2] for some row b2 of the launch. One block per row; bad[b] = the number of such entries of row b
+// (plain per-row stores, no atomics).
+__global__ __launch_bounds__(256) void k_kv_tab_check(const int* __restrict__ kv_tab, const int* __restrict__ pos,
+                                                      int row0, int B, int max_pos, int* __restrict__ bad) {
+  __shared__ int cnt[4];
+  const int b = blockIdx.x, t = min(pos[b], max_pos);
+  const int* tr = kv_tab + (size_t)(row0 + b) * max_pos;
+  int n = 0;
+  for (int q = threadIdx.x; q < t; q += blockDim.x) {
+    const int r2 = tr[q] - row0;
+    n += (r2 >= 0 && r2 < B && pos[r2] == q) ? 1 : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+  if ((threadIdx.x & 63) == 0) cnt[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) bad[b] = cnt[0] + cnt[1] + cnt[2] + cnt[3];
+}
+
+extern "C" int tw_kv_tab_check(const int* kv_tab, const int* pos, int row0, int B, int max_pos, int* bad,
+                               void* stream) {
+  TW_REQUIRE(kv_tab && pos && bad && B > 0 && row0 >= 0 && max_pos > 0, "tw_kv_tab_check: bad args");
+  hipLaunchKernelGGL(k_kv_tab_check, dim3(B), dim3(256), 0, (hipStream_t)stream, kv_tab, pos, row0, B, max_pos, bad);
+  return tw_check_launch("tw_kv_tab_check");
+}
+
+#if TW_DEBUG
+// Debug builds (-DTW_DEBUG=1, `make debug`): every tw_attn_decode_self_tab outside a graph capture validates the
+// table first and fails with TW_ERR_ARG instead of racing (the check synchronises the stream).
+static int tw_debug_tab_guard(const int* kv_tab, const int* pos, int row0, int B, int max_pos, hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return TW_OK;
+  static int* d_bad = nullptr;
+  static int cap = 0;
+  if (cap < B) {
+    if (d_bad) hipFree(d_bad);
+    cap = 0;
+    if (hipMalloc(&d_bad, sizeof(int) * B) != hipSuccess) {
+      d_bad = nullptr;
+      tw_set_error("tw_attn_decode_self_tab (debug): hipMalloc failed");
+      return TW_ERR_LAUNCH;
+    }
+    cap = B;
+  }
+  if (tw_kv_tab_check(kv_tab, pos, row0, B, max_pos, d_bad, st) != TW_OK) return TW_ERR_LAUNCH;
+  int* h = (int*)alloca(sizeof(int) * B);
+  if (hipMemcpyAsync(h, d_bad, sizeof(int) * B, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    tw_set_error("tw_attn_decode_self_tab (debug): table check failed to run");
+    return TW_ERR_LAUNCH;
+  }
+  for (int b = 0; b < B; ++b)
+    if (h[b]) {
+      tw_set_error("tw_attn_decode_self_tab: precondition violated: %d history entries of row %d name a (row, "
+                   "position) this launch writes",
+                   h[b], row0 + b);
+      return TW_ERR_ARG;
+    }
+  return TW_OK;
+}
+#endif
+
 extern "C" int tw_attn_decode_self_tab(const bf16_t* qkv, int B, int H, int max_pos, const int* pos, bf16_t* k_cache,
                                        bf16_t* v_cache, const int* kv_tab, int row0, bf16_t* out, void* stream) {
   TW_REQUIRE(qkv && pos && k_cache && v_cache && kv_tab && out && B > 0 && H > 0 && row0 >= 0,
              "tw_attn_decode_self_tab: bad args");
   TW_REQUIRE(max_pos <= DA_SELF_MAXK, "tw_attn_decode_self_tab: max_pos %d > %d", max_pos, DA_SELF_MAXK);
+#if TW_DEBUG
+  if (int rc = tw_debug_tab_guard(kv_tab, pos, row0, B, max_pos, (hipStream_t)stream)) return rc;
+#endif
   hipLaunchKernelGGL(k_attn_decode_self2<true>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos,
                      pos, k_cache, v_cache, kv_tab, row0, out);
   return tw_check_launch("tw_attn_decode_self_tab");
 }
+
+// 1 in a library built with -DTW_DEBUG=1 (the position-table guard above is compiled in), else 0.
+extern "C" int tw_debug_build(void) { return TW_DEBUG ? 1 : 0; }
 
 // Optional output for token-level timestamps (return_timestamps="word"): the attention probabilities of the
 // alignment heads, probs[b][pos[b] - pos0][slot][S] f32 for the heads whose bit is set in head_mask (slot = slot0 +

@@ -1084,8 +1084,9 @@ extern "C" int tw_kv_reorder(uint16_t* k_cache, uint16_t* v_cache, uint16_t* k_s
                              int rows_cap, int H, int T, int R, const int* src_rows, const int* pos, void* stream) {
   (void)k_scratch;
   (void)v_scratch;
-  TW_REQUIRE(k_cache && v_cache && src_rows && pos && R > 0 && R <= rows_cap && R <= 512 && T > 0,
-             "tw_kv_reorder: bad args (R=%d rows_cap=%d T=%d)", R, rows_cap, T);
+  // one position per tile at least: R * 128 B of dynamic LDS within TW_KVR_LDS (R <= 448)
+  TW_REQUIRE(k_cache && v_cache && src_rows && pos && R > 0 && R <= rows_cap && R <= TW_KVR_LDS / 128 && T > 0,
+             "tw_kv_reorder: bad args (R=%d rows_cap=%d T=%d; R <= %d)", R, rows_cap, T, TW_KVR_LDS / 128);
   int TT = 16;  // positions per tile: R * TT * 128 B of LDS
   while (TT > 1 && (size_t)R * TT * 128 > TW_KVR_LDS) TT >>= 1;
   const dim3 grid(layers * H, (T + TT - 1) / TT, 2);

@@ -15,6 +15,10 @@ typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 
 #define TW_WAVE 64
 
+#ifndef TW_DEBUG
+#define TW_DEBUG 0  // -DTW_DEBUG=1 (make debug): contract checks on the C-ABI (tw_attn_decode_self_tab's table)
+#endif
+
 // ---- bf16 <-> f32 (round-to-nearest-even; NaN kept NaN) --------------------------------------
 __host__ __device__ inline float bf16_to_f32(bf16_t h) {
   union { uint32_t u; float f; } v; v.u = ((uint32_t)h) << 16; return v.f;

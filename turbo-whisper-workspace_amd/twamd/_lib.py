@@ -13,6 +13,8 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime before ours)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtwhip.so")
+# the same library built with -DTW_DEBUG=1 (`make -C turbo-whisper-workspace_amd/csrc debug`): C-ABI contract checks
+DEBUG_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtwhip_dbg.so")
 
 TW_EPI_BF16 = 0
 TW_EPI_GELU_BF16 = 1
@@ -39,6 +41,7 @@ EXPORTED = (
     "tw_dtw", "tw_attn_decode_cross_probs", "tw_attn_decode_cross_grouped", "tw_attn_decode_cross_grouped_ws_bytes", "tw_attn_decode_self_tab", "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
     "tw_gemm_mx", "tw_quant_mx", "tw_layernorm_mx", "tw_attn_encoder_mx", "tw_gemm_mx_set_variant", "tw_logits_select_embed",
     "tw_attn_set_lds_pad", "tw_logits_sample", "tw_token_prob", "tw_g711_decode", "tw_ima_adpcm_wav_decode",
+    "tw_kv_tab_check", "tw_debug_build",
 )
 
 
@@ -117,6 +120,8 @@ _SIGS = {
     "tw_beam_workspace_bytes": ([_I], ctypes.c_size_t),
     "tw_attn_decode_cross_grouped_ws_bytes": ([_I, _I], ctypes.c_size_t),
     "tw_attn_decode_self_tab": ([_P, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P], _I),
+    "tw_kv_tab_check": ([_P, _P, _I, _I, _I, _P, _P], _I),
+    "tw_debug_build": ([], _I),
     "tw_beam_step": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), ctypes.POINTER(TwBeamParams),
                       ctypes.POINTER(TwBeamState), _P, _P, _P, _P, _P, _P], _I),
     "tw_kv_reorder": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P], _I),
@@ -132,13 +137,10 @@ _SIGS = {
 }
 
 _lib = None
+_dbg = None
 
 
-def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load (once) and type the library; raises if it is missing."""
-    global _lib
-    if _lib is not None:
-        return _lib
+def _open(path: str) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise TwError(f"HIP library not built: {path} (run `make -C turbo-whisper-workspace_amd/csrc`)")
     lib = ctypes.CDLL(path)
@@ -146,8 +148,30 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
-    _lib = lib
     return lib
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) and type the library; raises if it is missing. The library is always the in-tree build:
+    an environment override (the TW_LIB of old A/B scripts) is refused rather than silently ignored."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if os.environ.get("TW_LIB"):
+        raise TwError("TW_LIB is no longer read: A/B builds load their library explicitly (_lib.load_debug or a "
+                      "separate process over another in-tree build)")
+    _lib = _open(path)
+    return _lib
+
+
+def load_debug() -> ctypes.CDLL:
+    """The -DTW_DEBUG=1 build (its own ctypes handle beside the product library; contract checks compiled in)."""
+    global _dbg
+    if _dbg is None:
+        _dbg = _open(DEBUG_LIB_PATH)
+        if _dbg.tw_debug_build() != 1:
+            raise TwError(f"{DEBUG_LIB_PATH} is not a TW_DEBUG build")
+    return _dbg
 
 
 def call(name: str, *args) -> None:

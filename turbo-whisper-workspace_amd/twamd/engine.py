@@ -123,6 +123,15 @@ class _EncoderPump:
         self.pending.clear()
 
 
+def fallback_row_key(window: int, pass_no: int, fi: int) -> int:
+    """The fallback sampler's row key (int32): one counter-based noise stream per (global window, seek pass,
+    temperature index)."""
+    key = (int(window) * 1024 + int(pass_no)) * 16 + int(fi)
+    if not 0 <= key < 2 ** 31:
+        raise ValueError(f"sampler key out of range: window {window}, pass {pass_no}")
+    return key
+
+
 @dataclasses.dataclass
 class PassResult:
     tokens: List[List[int]]      # generated tokens per row (as _sample returns them, before stripping)
@@ -1053,8 +1062,8 @@ class WhisperEngine:
                  max_new_tokens: Optional[int] = None, return_timestamps: bool = True,
                  max_passes: Optional[int] = None, slot: Optional[int] = None,
                  pre_encoded: bool = False, num_beams: int = 1, word_timestamps: bool = False,
-                 num_frames: Optional[Sequence[int]] = None, fallback: Optional[FallbackConfig] = None
-                 ) -> List[List[int]]:
+                 num_frames: Optional[Sequence[int]] = None, fallback: Optional[FallbackConfig] = None,
+                 window_offset: int = 0) -> List[List[int]]:
         """Whisper short-form generate() over feats[slot][:n_chunks] (each 3000 frames): language
         detection, the seek loop and segment extraction, returning for every chunk the concatenated
         segment tokens (what generate() returns before padding).
@@ -1062,7 +1071,9 @@ class WhisperEngine:
         pre_encoded: the first seek pass (all chunks, seek 0, n_chunks <= max_batch) was already encoded into
         this slot by encode(n_chunks, row_map=False, seek=False, slot=slot, sync=False) (pipelined prefetch).
         fallback: generate()'s temperature / compression_ratio_threshold / logprob_threshold / no_speech_threshold;
-        when it asks for more than greedy decoding every pass runs generate_with_fallback's loop (sample_pass)."""
+        when it asks for more than greedy decoding every pass runs generate_with_fallback's loop (sample_pass).
+        window_offset: the global index of chunk 0 (run_batches' batch offset): the sampler's per-row keys are built
+        from global window indices, so windows of different batches draw independent noise."""
         if slot is not None:
             self.use_slot(slot)
         if pre_encoded and n_chunks > self.max_batch:
@@ -1106,7 +1117,7 @@ class WhisperEngine:
                 if fb is not None:
                     pre = pre_encoded and passes == 0
                     toks_f, skip_f, lang_f = self._fallback_pass(
-                        R, tail, given, max_new, return_timestamps, fb, [part[j] for j in range(R)], passes,
+                        R, tail, given, max_new, return_timestamps, fb, [window_offset + i for i in part], passes,
                         enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R)
                     for j, i in enumerate(part):
                         if not known:
@@ -1168,7 +1179,7 @@ class WhisperEngine:
             do_sample = t is not None and t > 0.0
             res = self.sample_pass(len(idx), tail, None if langs is None else [langs[i] for i in idx], max_new,
                                    temperature=float(t) if do_sample else 0.0, top_k=fb.top_k, seed=fb.seed,
-                                   row_keys=[(int(windows[i]) * 1024 + pass_no) * 16 + fi for i in idx],
+                                   row_keys=[fallback_row_key(windows[i], pass_no, fi) for i in idx],
                                    use_timestamps=return_timestamps, enc_rows=[enc_row0 + i for i in idx],
                                    r_enc=r_enc, no_speech_token=ns_tok)
             if langs is None and res.lang_ids is not None:  # detected on the first round (all rows)
@@ -1231,6 +1242,7 @@ class WhisperEngine:
                 self._pump = _EncoderPump(self, prefetch_steps(k + 1), ahead=self.pump_ahead)
                 self._pump()
             kw = dict(gen_kwargs, **(batch_kwargs[k] if batch_kwargs else {}))
+            kw["window_offset"] = kw.get("window_offset", 0) + sum(sizes[:k])
             try:
                 out.append(self.generate(n, slot=k % 2, pre_encoded=True, **kw))
             finally:

@@ -125,9 +125,13 @@ class TurboTranscriber:
         max_passes = gk.pop("max_passes", None)
         fallback = self._fallback_config(gk)
         if fallback.active and (num_beams > 1 or word):
-            raise NotImplementedError("temperature fallback / segment criteria run with greedy passes only: pass "
-                                      "generate_kwargs={'num_beams': 1} (the pipeline's default decode is beam-5) "
-                                      "and segment-level timestamps")
+            from_ckpt = [k for k in ("compression_ratio_threshold", "logprob_threshold", "no_speech_threshold")
+                         if k not in (generate_kwargs or {}) and getattr(self.gen, k, None) is not None]
+            raise NotImplementedError(
+                "temperature fallback / segment criteria run with greedy passes only: pass "
+                "generate_kwargs={'num_beams': 1} (the pipeline's default decode is beam-5) and segment-level timestamps"
+                + (f"; the checkpoint's generation_config.json sets {from_ckpt}, which turns the fallback on for every "
+                   "call, so such a checkpoint needs num_beams=1" if from_ckpt else ""))
         if gk:
             raise ValueError(f"generate_kwargs not supported by this engine: {sorted(gk)}")
         st = self.gen.special
@@ -170,6 +174,7 @@ class TurboTranscriber:
             lang_id = lt[tok]
 
         def run(w, ws):
+            base = windows.index(ws[0]) if ws else 0  # this shard's first global window (the sampler's row keys)
             if word:  # token times ride along as floats after the tokens (one all-gather carries both)
                 nf = [min(x.length, CHUNK_SAMPLES) // 160 + (1 if min(x.length, CHUNK_SAMPLES) % 160 else 0)
                       for x in ws]
@@ -180,7 +185,7 @@ class TurboTranscriber:
                 return [(t, ts) for t, ts in zip(toks, self.last_window_token_timestamps)]
             return self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=bool(return_timestamps),
                                            max_new_tokens=max_new_tokens, num_beams=num_beams, max_passes=max_passes,
-                                           **({"fallback": fallback} if fallback.active else {}))
+                                           **({"fallback": fallback, "window_base": base} if fallback.active else {}))
 
         # one window shard per rank + one all-gather of the token arrays (twamd.dist); plain call on 1 GPU
         outputs = dist.transcribe_sharded(run, wav, windows, timed=word) if world > 1 else run(wav, windows)
@@ -204,8 +209,8 @@ class TurboTranscriber:
                            lang_id: Optional[int], return_timestamps: bool,
                            max_new_tokens: Optional[int] = None, num_beams: int = 1, word_timestamps: bool = False,
                            num_frames: Optional[Sequence[int]] = None, group: Optional[int] = None,
-                           max_passes: Optional[int] = None, fallback: Optional[FallbackConfig] = None
-                           ) -> List[List[int]]:
+                           max_passes: Optional[int] = None, fallback: Optional[FallbackConfig] = None,
+                           window_base: int = 0) -> List[List[int]]:
         """Log-mel + generate for every window; returns per-window token sequences (generate() output,
         right-padded with the pad token within each engine batch, as the HF batch output is). Batches of
         max_batch windows go through WhisperEngine.run_batches: batch k+1 is encoded while batch k decodes.
@@ -252,7 +257,8 @@ class TurboTranscriber:
         res = eng.run_batches(sizes, load=load, batch_kwargs=bkw, task=task,
                               lang_ids=None if lang_id is None else [lang_id] * max(sizes, default=1),
                               max_new_tokens=max_new_tokens, return_timestamps=return_timestamps, num_beams=num_beams,
-                              max_passes=max_passes, **({"fallback": fallback} if fallback is not None else {}))
+                              max_passes=max_passes,
+                              **({"fallback": fallback, "window_offset": window_base} if fallback is not None else {}))
         out: List[List[int]] = []
         for seqs in res:
             out.extend(pad_right(seqs, self.gen.special.eot))
