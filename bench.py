@@ -259,10 +259,13 @@ def main():
 
 
 def parity_vs_golden(eng, B, T, model, fp8):
-    """Rank 0's windows 0 (speech) and 23 (silent) of the last timed batch against transformers' fp32 decode of the
-    same seeded weights and audio (tests/golden/turbo.npz, tests/golden/turbo_parity.py): tokens equal, or diverging
-    first at a near-tie within TAU = 0.15 logits; language ids equal. Only the bf16 config-2 workload (24 windows, 128
-    tokens) has a golden; anything else reports None."""
+    """Rank 0's last timed batch against transformers' fp32 decode of the same seeded weights and audio:
+    free_decode — windows 0 (speech) and 23 (silent) as decoded in the timed region (tests/golden/turbo.npz): tokens
+    equal, or diverging first at a near-tie within TAU = 0.15 logits; language ids equal. teacher_forced — 6 windows
+    (turbo_bench.npz) at all 128 positions: each fp32 sequence fed through the same captured B = 24 decode after the
+    timed region, top-16 logits within LOGIT_ABS, argmax and timestamp-rule margin within TAU at every position
+    (turbo_parity.forced_decode). Only the bf16 config-2 workload (24 windows, 128 tokens) has a golden; anything
+    else reports None."""
     if fp8 or B != 24 or T != 128 or model != "large-v3-turbo":
         return None, {"skipped": "no fp32 golden for this workload"}
     try:
@@ -272,10 +275,15 @@ def parity_vs_golden(eng, B, T, model, fp8):
         z = tp.load()
         passes, langs = eng.batch_passes[-1], eng.batch_langs[-1]
         det = {f"window{w}": tp.check_bench_window(z, w, passes[w][0], langs[w]) for w in tp.BENCH_WINDOWS}
+        # every position: the fp32 sequences of 6 windows teacher-forced through the same captured B = 24 decode
+        # (after the timed region, on the same engine and resident waveforms)
+        forced = tp.forced_decode(eng, tp.load_bench(), B, T)
     except Exception as e:  # reported, never allowed to sink the GPU number
         return False, {"error": repr(e)[:200]}
-    ok = all(r["lang_ok"] and r["status"] in ("exact", "within_tau") for r in det.values())
-    return ok, {"tau": tp.TAU, "reference": "transformers fp32 CPU, tests/golden/turbo.npz", **det}
+    ok = all(r["lang_ok"] and r["status"] in ("exact", "within_tau") for r in det.values()) and forced["ok"]
+    return ok, {"tau": tp.TAU, "reference": "transformers fp32 CPU, tests/golden/turbo.npz + turbo_bench.npz",
+                "free_decode": det, "teacher_forced": forced, "positions_checked": forced["positions_checked"],
+                "worst_d_logit": forced["worst_d_logit"]}
 
 
 def measured_traffic(kernels, c5: bool = False):

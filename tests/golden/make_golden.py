@@ -514,6 +514,88 @@ def make_turbo(out):
     np.savez_compressed(os.path.join(out, "turbo.npz"), **res)
 
 
+TURBO_BENCH_ALL = (0, 5, 11, 17, 22, 23)  # bench windows with an all-position golden (22, 23: the silent ones)
+
+
+def _mask_intervals(mask: np.ndarray) -> np.ndarray:
+    """[lo, hi) runs of True in a boolean row."""
+    d = np.diff(np.concatenate([[0], mask.astype(np.int8), [0]]))
+    return np.stack([np.flatnonzero(d == 1), np.flatnonzero(d == -1)], 1).astype(np.int32)
+
+
+def make_turbo_bench(out):
+    """bench.py's headline workload at every position: for TURBO_BENCH_ALL windows of workload(24, seed 1234), the
+    fp32 first-pass decode (EOS suppressed, 128 new tokens, language detected), and along that sequence (teacher-
+    forced) at each of the 128 positions: the raw logits' top-16 (indices, values, log-sum-exp), the processed top-16
+    and the timestamp-rule margin, and the processors' -inf mask before the rule as [lo, hi) intervals. The mask plus
+    the rule (tests/golden/turbo_parity.process_row) reproduces the oracle's process_logits exactly — asserted here on
+    every fp32 row — so a device's raw logits can be processed on the host with the fp32 history (turbo_bench.npz)."""
+    from transformers import WhisperFeatureExtractor
+    from twamd.synth_audio import workload
+    sys.path.insert(0, HERE)
+    import turbo_parity as tp
+
+    d = PRESETS["large-v3-turbo"]
+    gen = GenerationSettings.default(d)
+    st = gen.special
+    sup = list(gen.suppress_tokens) + [st.eot]
+    g = wo.GenCfg(d.vocab, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate,
+                  st.notimestamps, sup, gen.begin_suppress_tokens)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    del sd
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    wl = workload(24, 30.0, seed=1234)
+    res = {"windows": np.array(TURBO_BENCH_ALL, np.int32)}
+    m.generation_config.suppress_tokens = sup
+    for w in TURBO_BENCH_ALL:
+        feats = fe(wl[w], sampling_rate=16000, return_tensors="np")["input_features"][0]
+        with torch.no_grad():
+            lang = int(m.detect_language(input_features=torch.from_numpy(feats[None])).numpy()[0])
+            o = m.generate(torch.from_numpy(feats[None]), task="transcribe", return_timestamps=True, num_beams=1,
+                           max_new_tokens=128, return_segments=True)
+        p = _passes_from_segments(o["segments"][0], 3)[0]
+        assert len(p) == 128, len(p)
+        prompt = [st.sot, lang, st.transcribe]
+        ids = prompt + p[:-1]
+        with torch.no_grad():
+            lg = m(input_features=torch.from_numpy(feats[None]), decoder_input_ids=torch.tensor([ids])).logits[0].numpy()
+        lg = lg[len(prompt) - 1:].astype(np.float32)
+        assert lg.shape[0] == 128
+        raw_i, raw_v, lse, pi, pv, mg, ivs, offs = [], [], [], [], [], [], [], [0]
+        for t in range(128):
+            row = lg[t]
+            o16 = np.argsort(-row, kind="stable")[:16]
+            raw_i.append(o16)
+            raw_v.append(row[o16])
+            mx = float(row.max())
+            lse.append(mx + np.log(np.exp(row.astype(np.float64) - mx).sum()))
+            ref = wo.process_logits(row, p[:t], g, True)
+            iv = _mask_intervals(np.isneginf(wo.process_logits_no_rule(np.zeros_like(row), p[:t], g)))
+            s, margin = tp.process_row(row, iv, st.timestamp_begin)
+            assert np.array_equal(s, ref), (w, t)  # the host restatement of the chain is exact on the fp32 row
+            assert int(np.argmax(ref)) == p[t], (w, t)  # generate() chose the processed argmax
+            o16p = np.argsort(-ref, kind="stable")[:16]
+            pi.append(o16p)
+            pv.append(ref[o16p])
+            mg.append(wo._ts_rule_margin(wo.process_logits_no_rule(row, p[:t], g), g.ts_begin))
+            assert mg[-1] == margin or abs(mg[-1] - margin) < 1e-5, (w, t, mg[-1], margin)
+            ivs.append(iv)
+            offs.append(offs[-1] + len(iv))
+        k = f"w{w}_"
+        res[k + "lang"] = np.array([lang], np.int32)
+        res[k + "tokens"] = np.array(p, np.int32)
+        res[k + "raw_idx"], res[k + "raw_val"] = np.array(raw_i, np.int32), np.array(raw_v, np.float32)
+        res[k + "lse"] = np.array(lse, np.float64)
+        res[k + "top_idx"], res[k + "top_val"] = np.array(pi, np.int32), np.array(pv, np.float32)
+        res[k + "ts_margin"] = np.array(mg, np.float32)
+        res[k + "mask_iv"], res[k + "mask_off"] = np.concatenate(ivs), np.array(offs, np.int32)
+        print(f"turbo_bench window {w}: lang {lang}, {len(p)} tokens, {sum(t >= st.timestamp_begin for t in p)} "
+              f"timestamps", flush=True)
+    m.generation_config.suppress_tokens = list(gen.suppress_tokens)
+    np.savez_compressed(os.path.join(out, "turbo_bench.npz"), **res)
+
+
 def make_turbo_beam(out):
     """large-v3-turbo, seeded synthetic weights: generate(num_beams=5) — the ASR pipeline's default decode
     (asr:160-163), i.e. what the reference's transcribe() runs — on TURBO_CLIPS, with timestamps (40 new tokens) and

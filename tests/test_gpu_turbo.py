@@ -341,3 +341,25 @@ def test_turbo_token_timestamps_vs_transformers(turbo):
         assert d.max() <= 0.2 + 1e-4 and (d < 1e-4).mean() >= 0.9, (i, d)
         compared += 1
     assert compared >= 1
+
+
+def test_turbo_bench_every_position_teacher_forced(turbo):
+    """bench.py's headline workload (B = 24 windows, EOS suppressed, 128 new tokens) checked at
+    all 128 positions of 6 windows (tests/golden/turbo_bench.npz: windows 0, 5, 11, 17 speech, 22, 23 silent; fp32
+    transformers). Each window's fp32 sequence is teacher-forced through the same captured B = 24 decode the bench
+    replays (run_batches -> decode_pass, step_hook); at every position the fp32 top-16 raw logits and log-sum-exp are
+    within LOGIT_ABS, the device's processed argmax is the fp32 token or within TAU of it, and the timestamp-rule
+    margin within TAU (turbo_parity.check_forced_position)."""
+    zb = tp.load_bench()
+    eng = turbo.engine
+    B, T = 24, 128
+    gen = turbo.gen
+    eng.set_suppress_tokens(list(gen.suppress_tokens) + [gen.special.eot])
+    try:
+        eng.wave[:B].copy_(torch.from_numpy(workload(B, 30.0, seed=1234)))
+        out = tp.forced_decode(eng, zb, B, T)
+    finally:
+        eng.set_suppress_tokens(list(gen.suppress_tokens))
+    print("turbo bench teacher-forced:", {k: v for k, v in out.items() if k != "first_bad"})
+    assert out["positions_checked"] == len(zb["windows"]) * T
+    assert out["ok"], out["first_bad"]

@@ -209,3 +209,41 @@ def test_turbo_beam_and_word_goldens_consistent():
     for i in range(2):
         assert zw[f"seq{i}"].shape == zw[f"ts{i}"].shape
         assert np.all(np.isfinite(zw[f"ts{i}"])) and np.all(zw[f"ts{i}"] >= 0)
+
+
+def test_turbo_bench_golden_and_host_processing():
+    """tests/golden/turbo_bench.npz (all 128 positions of 6 bench windows, transformers fp32): consistent with
+    turbo.npz where both hold a window, the stored masks reproduce the oracle's processor chain (itself pinned to
+    transformers) for histories of every kind, the fp32 token is the processed argmax of its stored top-16, and
+    turbo_parity.check_forced_position accepts the fp32 row itself."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import turbo_parity as tp
+    zb, z = tp.load_bench(), tp.load()
+    d = PRESETS["large-v3-turbo"]
+    gen = GenerationSettings.default(d)
+    st = gen.special
+    g = wo.GenCfg(d.vocab, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate,
+                  st.notimestamps, list(gen.suppress_tokens) + [st.eot], gen.begin_suppress_tokens)
+    assert [int(w) for w in zb["windows"]] == [0, 5, 11, 17, 22, 23]
+    for w in (0, 23):
+        assert np.array_equal(zb[f"w{w}_tokens"], z[f"bench_w{w}_tokens"])
+        assert np.array_equal(zb[f"w{w}_top_val"], z[f"bench_w{w}_top_val"])
+    rng = np.random.default_rng(0)
+    for w in (int(x) for x in zb["windows"]):
+        k = f"w{w}_"
+        toks = [int(t) for t in zb[k + "tokens"]]
+        off = zb[k + "mask_off"]
+        assert len(toks) == 128 and len(off) == 129
+        for t in list(range(6)) + list(rng.choice(np.arange(6, 128), 10, replace=False)):
+            iv = zb[k + "mask_iv"][off[t]: off[t + 1]]
+            raw = rng.standard_normal(d.vocab).astype(np.float32) * 3
+            raw[st.timestamp_begin:] -= rng.uniform(0, 6)  # both sides of the timestamp rule
+            s, margin = tp.process_row(raw, iv, st.timestamp_begin)
+            assert np.array_equal(s, wo.process_logits(raw, toks[:t], g, True)), (w, t)
+            assert int(zb[k + "top_idx"][t][0]) == toks[t]
+            # the fp32 row's own stored top-16, scattered into a row: accepted at distance 0
+            row = np.full(d.vocab, -30.0, np.float32)
+            row[zb[k + "raw_idx"][t]] = zb[k + "raw_val"][t]
+            r = tp.check_forced_position(zb, w, t, row)
+            assert r["d_top"] == 0.0

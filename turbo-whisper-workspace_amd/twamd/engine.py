@@ -674,6 +674,22 @@ class WhisperEngine:
                   ctypes.byref(params), v.state.data_ptr(), v.tokens.data_ptr() if tokens else None,
                   v.tokens.shape[1], v.ids.data_ptr(), v.pos.data_ptr(), v.sel_ws.data_ptr(), v.stream.cuda_stream)
 
+    # Teacher-forcing hook of decode_pass (parity harness, tests/test_gpu_turbo.py and bench.py's parity leg):
+    # hook(k, view) runs on the host after the step that produced generated position k (view None: the prompt's last
+    # step, all rows), with that step's logits in place and the stream idle; it may overwrite `ids` of the view's rows
+    # and re-run the head of the next step (embed_head) so the next replay of the captured step consumes the forced
+    # token instead of the one the selection chose. None in normal decoding.
+    step_hook = None
+
+    def embed_head(self, v: Optional[DecView] = None, R: Optional[int] = None) -> None:
+        """The next step's head (embedding of ids at pos + layer 0's LayerNorm) for view v, or for rows [0, R) when
+        v is None, as the fused selection would have written it."""
+        if v is not None:
+            self._embed_head(v)
+            return
+        for r0 in range(0, R, 32):
+            self._embed_head(self._view(r0, min(32, R - r0)))
+
     def _embed_head(self, v: DecView) -> None:
         """The head of a decoder step alone (embedding + layer 0's self_attn_layer_norm) for view v: primes a chain
         whose captured steps run pre_embedded."""
@@ -769,6 +785,11 @@ class WhisperEngine:
         fused = self.fused_select
         graphs = ([self._graph_for(R, params, i, c, fused) for i, c in enumerate(chains)] if self.use_graphs
                   else None)
+        hook = self.step_hook
+        if hook is not None:  # teacher forcing (parity harness): logits of generated position 0 are in place
+            self.stream.synchronize()
+            with torch.cuda.stream(self.stream):
+                hook(0, None)
         for c in chains:
             c.stream.wait_stream(self.stream)
             if fused and max_new > 1:
@@ -776,7 +797,7 @@ class WhisperEngine:
                     self._embed_head(c)
         pump, inflight = self._pump, []
         while steps < max_new:
-            n = min(check_every, max_new - steps)
+            n = min(check_every if hook is None else 1, max_new - steps)
             for _ in range(n):
                 for i, c in enumerate(chains):
                     if graphs is not None:
@@ -784,6 +805,11 @@ class WhisperEngine:
                             graphs[i].replay()
                     else:
                         self._gen_step(c.n, params, v=c, r_enc=R, fused=fused)
+                if hook is not None:
+                    for i, c in enumerate(chains):
+                        c.stream.synchronize()
+                        with torch.cuda.stream(c.stream):
+                            hook(steps, c)
                 if pump is not None:  # keep both queues shallow: <= dec_ahead steps, <= pump.ahead encoder chunks
                     ev = torch.cuda.Event()
                     ev.record(chains[-1].stream)
