@@ -136,10 +136,10 @@ def check_forced_position(zb, w: int, t: int, raw: np.ndarray, tb: int = TIMESTA
         d_margin = float("inf")
     # a flip of the rule's decision at a near-tie is a class change the token check sees through the margin
     rule_flip_ok = abs(fm) <= TAU and (dev_tok >= tb) != (gold >= tb)
-    ok = (d_top <= LOGIT_ABS and d_lse <= LOGIT_ABS and d_margin <= TAU
-          and (gap <= TAU or rule_flip_ok))
-    return {"ok": bool(ok), "d_top": d_top, "d_lse": d_lse, "gap": gap, "d_margin": d_margin,
-            "argmax_equal": dev_tok == gold}
+    flip = dev_tok != gold and gap > TAU and rule_flip_ok
+    ok = d_top <= LOGIT_ABS and d_lse <= LOGIT_ABS and d_margin <= TAU and (gap <= TAU or flip)
+    return {"ok": bool(ok), "d_top": d_top, "d_lse": d_lse, "gap": None if flip else gap, "d_margin": d_margin,
+            "argmax_equal": dev_tok == gold, "rule_flip": bool(flip)}
 
 
 def summarize_forced(results: Dict[int, list]) -> Dict:
@@ -152,7 +152,8 @@ def summarize_forced(results: Dict[int, list]) -> Dict:
             "worst_d_logit": round(max((r["d_top"] for r in allr), default=0.0), 4),
             "worst_d_lse": round(max((r["d_lse"] for r in allr), default=0.0), 4),
             "worst_d_margin": round(max((r["d_margin"] for r in allr), default=0.0), 4),
-            "worst_gap": round(max((r["gap"] for r in allr), default=0.0), 4),
+            "worst_gap": round(max((r["gap"] for r in allr if r["gap"] is not None), default=0.0), 4),
+            "rule_flips": sum(r["rule_flip"] for r in allr),
             "logit_abs": LOGIT_ABS, "tau": TAU}
 
 
