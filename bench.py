@@ -266,8 +266,21 @@ def parity_vs_golden(eng, B, T, model, fp8):
     timed region, top-16 logits within LOGIT_ABS, argmax and timestamp-rule margin within TAU at every position
     (turbo_parity.forced_decode). Only the bf16 config-2 workload (24 windows, 128 tokens) has a golden; anything
     else reports None."""
-    if fp8 or B != 24 or T != 128 or model != "large-v3-turbo":
+    if T != 128 or model != "large-v3-turbo" or B != (64 if fp8 else 24):
         return None, {"skipped": "no fp32 golden for this workload"}
+    if fp8:  # config 5: windows 0, 5, 11, 17 of its 64 hold the same seeded clips as config 2's (turbo_bench.npz)
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+            import turbo_parity as tp
+
+            forced = tp.forced_decode(eng, tp.load_bench(), B, T, windows=(0, 5, 11, 17), fp8=True)
+        except Exception as e:  # reported, never allowed to sink the GPU number
+            return False, {"error": repr(e)[:200]}
+        return forced["ok"], {"reference": "transformers fp32 CPU, tests/golden/turbo_bench.npz (the same seeded "
+                                           "clips as windows 0, 5, 11, 17 of this batch)",
+                              "bounds": "MX-fp8 encoder: turbo_parity.FP8_* (stated, fixed)", "teacher_forced": forced,
+                              "positions_checked": forced["positions_checked"],
+                              "worst_d_logit": forced["worst_d_logit"]}
     try:
         sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
         import turbo_parity as tp

@@ -157,13 +157,10 @@ int tw_attn_encoder(const uint16_t* qkv, int B, int S, int H, uint16_t* out, voi
  * "MX fp8 encoder" above), the out_proj operand of the config-5 encoder (modeling_whisper.py:350-356). H even. */
 int tw_attn_encoder_mx(const uint16_t* qkv, int B, int S, int H, uint8_t* out, uint8_t* scales, int rows_pad,
                        void* stream);
-/* Measurement knob (process-wide, returns 0): encoder attention kernel of tw_attn_encoder. 8 (default) =
- * k_attn_enc2 with 8 waves / 256 queries per workgroup, 4 = the same with 4 waves, 0 = the first kernel.
- * + 0x100: tw_attn_decode_cross in two passes (scores, softmax, P.V) instead of the one-pass online softmax.
- * + 0x200: the one-pass tw_attn_decode_cross with 512 threads (64 key groups) per (row, head) instead of 256.
- * + 0x400: the one-pass tw_attn_decode_cross with its ~15 KiB LDS merge instead of the ~1.3 KiB shuffle merge.
- * + (s + 1) << 12: cross K/V of encoder slots >= s read non-temporally (0: every slot, the default; 0xff << 12: none).
- * + p << 20: p x 16 KiB of extra LDS per encoder-attention workgroup (as tw_attn_set_lds_pad). */
+/* Measurement knob (process-wide, returns 0 or TW_ERR_ARG): encoder attention kernel of tw_attn_encoder and
+ * tw_attn_encoder_mx. 32 (default) = k_attn_enc5 (64 queries per wave, log2-unit scores, guarded unshifted exp2),
+ * 16 = k_attn_enc4 (bit-identical to k_attn_enc2), 8 = k_attn_enc2 (32 queries per wave, running-max softmax; the
+ * MX-output kernel for 8 and 16). */
 int tw_attn_set_variant(int variant);
 /* Process-wide: reserve units x 16 KiB (0..8) of extra LDS per tw_attn_encoder workgroup, capping its workgroups per CU
  * so that decoder kernels launched beside it on another stream find free wave slots (the engine sets 4 for encoder

@@ -258,10 +258,23 @@ def test_pipeline_beam5_matches_transformers_pipeline(mini, name):
     kw = {k: v for k, v in case["kwargs"].items()}
     r = mini(audio, generate_kwargs={"task": "transcribe", "num_beams": 5, "max_new_tokens": 40},
              return_timestamps=True, **kw)
-    ref = case["output"]
-    assert r["text"] == ref["text"]
-    assert [(tuple(c["timestamp"]), c["text"]) for c in r["chunks"]] == \
-        [(tuple(c["timestamp"]), c["text"]) for c in ref["chunks"]]
+    _same_or_beam_within_tau(mini, r, case["output"], audio, kw, 40)
+
+
+def _same_or_beam_within_tau(t, r, ref, audio, kw, max_new):
+    """The transformers pipeline's output exactly, or — where a bf16 near-tie ranks two fp32 candidates the other way
+    (the random-weight model's beams lie within hundredths of a logit) — every device seek pass equal to the fp32
+    oracle's beam search up to one whose first differing decision is among the fp32 search's candidates or within
+    0.3 logits (test_gpu_e2e._beam_passes_within_tau, the tolerance every other beam pipeline test uses)."""
+    got = (r["text"], [(tuple(c["timestamp"]), c["text"]) for c in r["chunks"]])
+    want = (ref["text"], [(tuple(c["timestamp"]), c["text"]) for c in ref["chunks"]])
+    if got == want:
+        return
+    from test_gpu_e2e import D, _beam_passes_within_tau
+
+    sd = wo.synth_state_dict(D.d_model, D.encoder_layers, D.decoder_layers, D.ffn, D.n_mels, D.vocab, 1234)
+    n = _beam_passes_within_tau(t, wo.WhisperOracle(sd, D.heads), audio, kw, "transcribe", max_new)
+    assert n > 0, "outputs differ but every device pass equals the fp32 beam search"  # (then it is a host bug)
 
 
 def test_default_callable_long_audio_matches_transformers_pipeline():
@@ -276,10 +289,7 @@ def test_default_callable_long_audio_matches_transformers_pipeline():
     audio = np.concatenate([speech_like(200.0, 21), white_noise(80.0, 22), speech_like(200.0, 23)])
     r = tr(audio, generate_kwargs={"task": "transcribe", "max_new_tokens": gold["max_new_tokens"]},
            return_timestamps=True, **gold["kwargs"])
-    ref = gold["output"]
-    assert r["text"] == ref["text"]
-    assert [(tuple(c["timestamp"]), c["text"]) for c in r["chunks"]] == \
-        [(tuple(c["timestamp"]), c["text"]) for c in ref["chunks"]]
+    _same_or_beam_within_tau(tr, r, gold["output"], audio, gold["kwargs"], gold["max_new_tokens"])
 
 
 def _racy_table(R, cap, T, row0, seed):

@@ -463,14 +463,15 @@ def test_logits_select_matches_oracle_processors():
 
 # ---- packed decoder GEMV (include/tw_whisper.h "packed" layouts), restated here with torch index math
 def _act_index(M, K):
+    """Up to 64 rows: rows 32..63 are a second 32-row block 32 K elements on."""
     m = torch.arange(M).view(M, 1)
     k = torch.arange(K).view(1, K)
-    return (((k // 32) * 2 + m // 16) * 64 + m % 16 + 16 * ((k // 8) % 4)) * 8 + k % 8
+    return (m // 32) * 32 * K + (((k // 32) * 2 + (m // 16) % 2) * 64 + m % 16 + 16 * ((k // 8) % 4)) * 8 + k % 8
 
 
 def pack_act(x):
     M, K = x.shape
-    out = torch.zeros(K * 32, dtype=x.dtype, device=x.device)
+    out = torch.zeros(K * 64, dtype=x.dtype, device=x.device)
     out[_act_index(M, K).to(x.device).reshape(-1)] = x.reshape(-1)
     return out
 
@@ -504,6 +505,11 @@ GEMV_CASES = [  # M, N, K, epi, splits
     (24, 1280, 5120, _lib.TW_EPI_PARTIAL_F32, 4), (24, 1280, 1280, _lib.TW_EPI_PARTIAL_F32, 4),
     (1, 384, 1536, _lib.TW_EPI_PARTIAL_F32, 3), (24, 51866, 1280, _lib.TW_EPI_F32, 1), (5, 51864, 384, _lib.TW_EPI_F32, 1),
     (24, 1296, 1280, _lib.TW_EPI_BF16, 1), (24, 1296, 1280, _lib.TW_EPI_PARTIAL_F32, 4),  # odd column-group count
+    # 33..64 rows in one launch (four m-tiles: config 5's 64 windows, beam-5 over 12 windows)
+    (64, 3840, 1280, _lib.TW_EPI_BF16, 1), (40, 1280, 1280, _lib.TW_EPI_BF16, 1),
+    (64, 5120, 1280, _lib.TW_EPI_GELU_PACKED, 1), (33, 1536, 384, _lib.TW_EPI_GELU_PACKED, 1),
+    (64, 1280, 5120, _lib.TW_EPI_PARTIAL_F32, 4), (60, 1296, 1280, _lib.TW_EPI_PARTIAL_F32, 4),
+    (64, 51866, 1280, _lib.TW_EPI_F32, 1), (37, 51864, 384, _lib.TW_EPI_F32, 1),
 ]
 
 
@@ -525,13 +531,13 @@ def test_gemv_packed_vs_torch(M, N, K, epi, splits, a_packed):
         torch.testing.assert_close(out.sum(0), ref, atol=2e-3, rtol=2e-3)  # f32 accumulation order only
         return
     if epi == _lib.TW_EPI_GELU_PACKED:
-        out = torch.zeros(N * 32, dtype=torch.bfloat16, device=DEV)
+        out = torch.zeros(N * 64, dtype=torch.bfloat16, device=DEV)
         _lib.call("tw_gemv_packed", Ain.data_ptr(), a_packed, K, Wp.data_ptr(), M, N, K, epi, out.data_ptr(), 0,
                   bias.data_ptr(), 1, S())
         got = unpack_act(out, M, N).float()
         torch.testing.assert_close(got, torch.nn.functional.gelu(ref + bias), atol=2e-2, rtol=2e-2)  # bf16 output
-        full = _act_index(32, N).to(DEV)[M:].reshape(-1)
-        assert not out[full].float().abs().sum()  # rows M..31 untouched
+        full = _act_index(64, N).to(DEV)[M:].reshape(-1)
+        assert not out[full].float().abs().sum()  # rows M..63 untouched
         return
     dt = torch.bfloat16 if epi == _lib.TW_EPI_BF16 else torch.float32
     out = torch.full((M, N), float("nan"), dtype=dt, device=DEV)
@@ -555,14 +561,14 @@ def test_gemv_packed_resid_epilogue(M, N, K, a_packed):
     torch.testing.assert_close(x, want, atol=2e-3, rtol=2e-3)
 
 
-@pytest.mark.parametrize("M,D,nparts", [(24, 1280, 4), (5, 384, 0), (17, 256, 2)])
+@pytest.mark.parametrize("M,D,nparts", [(24, 1280, 4), (5, 384, 0), (17, 256, 2), (64, 1280, 4), (33, 384, 2)])
 def test_resid_layernorm_packed_vs_torch(M, D, nparts):
     x = torch.randn(M, D, device=DEV) * 3 + 1
     parts = torch.randn(max(nparts, 1), M, D, device=DEV)
     bias = torch.randn(D, device=DEV) if nparts else None
     g = torch.randn(D, device=DEV)
     b = torch.randn(D, device=DEV)
-    out = torch.zeros(D * 32, dtype=torch.bfloat16, device=DEV)
+    out = torch.zeros(D * 64, dtype=torch.bfloat16, device=DEV)
     xr = x + (bias + parts[:nparts].sum(0) if nparts else 0)
     _lib.call("tw_resid_layernorm_packed", x.data_ptr(), parts.data_ptr(), nparts, _lib.ptr(bias), g.data_ptr(),
               b.data_ptr(), M, D, 1e-5, out.data_ptr(), S())

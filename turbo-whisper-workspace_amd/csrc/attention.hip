@@ -2,9 +2,9 @@
 //
 // (1) Encoder self-attention (non-causal, S = 1500, 64-wide heads): replaces WhisperAttention +
 //     eager/SDPA attention ($TF/models/whisper/modeling_whisper.py:215-238, 241-356) for the encoder.
-//     Flash-style (k_attn_enc4, the default: 64 queries per wave, 4 waves per workgroup, LDS-DMA staging, bit-identical
-//     to k_attn_enc2; k_attn_enc5: enc4 with log2-unit scores and a guarded unshifted exp2, 10 % faster alone;
-//     k_attn_enc2: 32 per wave, register-staged, kept as the reference form and for the MX-fp8 output of config 5).
+//     Flash-style (k_attn_enc5, the default: 64 queries per wave, 4 waves per workgroup, LDS-DMA staging, log2-unit
+//     scores and a guarded unshifted exp2, 10 % faster alone than k_attn_enc4, which is bit-identical to
+//     k_attn_enc2: 32 per wave, register-staged, kept as the reference form). Both enc5 and enc2 store MX fp8 for config 5.
 //     The score tile is computed SWAPPED, S^T = K.Q^T with v_mfma_f32_32x32x16_bf16, so each lane holds
 //     16 keys of ONE query: the online-softmax max/sum is lane-local plus one xor-32 shuffle. The f32
 //     accumulator is then converted pairwise to bf16 and used in place as the B operand of O^T = V^T.P^T
@@ -411,7 +411,7 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc4(const bf16_t* __rest
   }
 }
 // ------------------------------------------------------------------------------------------------
-// k_attn_enc5 (variant 32, the faster alternative): k_attn_enc2's per-lane algorithm (swapped S^T = K.Q^T on v_mfma_f32_32x32x16_bf16,
+// k_attn_enc5 (variant 32, the default): k_attn_enc2's per-lane algorithm (swapped S^T = K.Q^T on v_mfma_f32_32x32x16_bf16,
 // lane-local softmax, P^T straight from the accumulators into the PV MFMA, V^T by ds_read_b64_tr_b16) with 64 queries
 // per wave (every K fragment read from LDS feeds 4 MFMAs, every V^T fragment 4: half enc2's LDS read traffic per
 // MFMA) and K/V tiles staged by LDS-DMA (global_load_lds_dwordx4, the bank swizzles applied on the SOURCE chunk and
@@ -428,9 +428,13 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc4(const bf16_t* __rest
 //     enc2/enc4 stay as that guard; on real and random attention inputs the guarded path never triggers, so there is
 //     no per-tile O rescale either (enc2 rescales whenever a query's max grows).
 // ------------------------------------------------------------------------------------------------
-template <int NW, int WPS>
+// MXO (config 5): the output stored as MX fp8 for the fp8 out_proj, exactly as k_attn_enc2<.., true> stores it (the
+// same lane layout of O^T: a lane pair (lr, lr + 32) holds one query's 32-dim block).
+template <int NW, int WPS, bool MXO = false>
 __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc5(const bf16_t* __restrict__ qkv, int S, int H, int D,
-                                                          int nqb, int nwork, bf16_t* __restrict__ out) {
+                                                          int nqb, int nwork, bf16_t* __restrict__ out,
+                                                          uint8_t* __restrict__ qout = nullptr,
+                                                          uint8_t* __restrict__ qscale = nullptr, int rows_pad = 0) {
   __shared__ __attribute__((aligned(16))) bf16_t kvbuf[4 * EA_KT * 64];  // [K0 | K1 | V0 | V1]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 31, lh = lane >> 5;
@@ -606,6 +610,41 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc5(const bf16_t* __rest
     if (nfull < ntile) tile(nfull & 1, nfull * EA_KT, BT{}, BF{});
   }
 
+  if constexpr (MXO) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int q = q0 + 32 * t + lr;
+      const float inv = 1.f / l_sum[t];
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        o[t][0][r] *= inv;
+        o[t][1][r] *= inv;
+        a0 = fmaxf(a0, fabsf(o[t][0][r]));
+        a1 = fmaxf(a1, fabsf(o[t][1][r]));
+      }
+      a0 = fmaxf(a0, __shfl_xor(a0, 32, 64));
+      a1 = fmaxf(a1, __shfl_xor(a1, 32, 64));
+      const uint32_t s0b = mx_scale_byte(a0), s1b = mx_scale_byte(a1);
+      const float i0 = mx_inv_scale(s0b), i1 = mx_inv_scale(s1b);
+      if (q < S) {
+        const size_t row = (size_t)b * S + q;
+        uint8_t* op = qout + row * D + h * 64;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = 8 * g + 4 * lh;
+          *(uint32_t*)(op + d) = mx_pack4(o[t][0][4 * g], o[t][0][4 * g + 1], o[t][0][4 * g + 2], o[t][0][4 * g + 3], i0);
+          *(uint32_t*)(op + 32 + d) =
+              mx_pack4(o[t][1][4 * g], o[t][1][4 * g + 1], o[t][1][4 * g + 2], o[t][1][4 * g + 3], i1);
+        }
+        if (lh == 0) {
+          qscale[tw_mx_sidx((int)row, 2 * h, rows_pad)] = (uint8_t)s0b;
+          qscale[tw_mx_sidx((int)row, 2 * h + 1, rows_pad)] = (uint8_t)s1b;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int q = q0 + 32 * t + lr;
@@ -627,18 +666,18 @@ __global__ __launch_bounds__(NW * 64, WPS) void k_attn_enc5(const bf16_t* __rest
   }
 }
 
-// Encoder attention kernel: 16 = k_attn_enc4<4 waves, 2 workgroups per CU> (the default: bit-identical to enc2, so the
-// engine reproduces the arithmetic its exact-match goldens were pinned with), 32 = k_attn_enc5<4, 2> (a fifth less
-// softmax VALU; its extra roundings of q * log2 e and of the unshifted p flip a near-tie in the beam-5 pipeline golden,
-// one end timestamp of an empty segment, tests/test_gpu_beam.py), 8 = k_attn_enc2<8, 2> (the running-max reference
-// form, also the MX-fp8-output kernel of config 5). Measured alone (scripts/attn_bench.py, 24 windows x 20 heads,
+// Encoder attention kernel: 32 = k_attn_enc5<4, 2> (the default since round 4: a fifth less softmax VALU than enc4; its
+// extra roundings of q * log2 e and of the unshifted p flip one near-tie in a beam-5 pipeline golden, one end
+// timestamp of an empty segment, which tests/test_gpu_beam.py judges with the beam decision tolerance every other beam
+// pipeline test uses; also the MX-fp8-output kernel of config 5), 16 = k_attn_enc4<4 waves, 2 workgroups per CU>
+// (bit-identical to enc2), 8 = k_attn_enc2<8, 2> (the running-max reference form). Measured alone (scripts/attn_bench.py, 24 windows x 20 heads,
 // MI355X r03): 16: 761-778, 32: 838-840, 8: 695 TF/s; with the 4 x 16 KiB LDS cap used beside a decode 16: 576-590,
 // 32: 603-610, 8: 536. In the bench step (scripts/exp/ab_attn_bench.py, three interleaved rounds) 16 and 32 are equal
 // (91.16 vs 91.05 ms): the overlapped step is bound by the decode beside it. PMC (scripts/exp/pmc_attn.sh): with the
 // cap a third of the attention's wave cycles are parked in s_waitcnt / s_barrier and a sixth stall on issue
 // dependencies; the software-pipelined enc6 (archived) did not move either. Other round-2/3 alternatives (enc3's MFMA
 // row sums and packed exp, 12-wave workgroups) are archived under scripts/exp/archive.
-static int tw_attn_variant = 16;
+static int tw_attn_variant = 32;
 // Extra (unused) LDS reserved per encoder-attention workgroup, in 16 KiB units: caps the attention's workgroups per CU
 // so that decoder waves queued beside it (run_batches' overlap) find free wave slots on every CU.
 // Measured (scripts/exp/interference.py, 24 windows): beside 4 x 16 KiB of padding (one workgroup per CU) a decoder
@@ -677,9 +716,15 @@ extern "C" int tw_attn_encoder_mx(const bf16_t* qkv, int B, int S, int H, uint8_
   TW_REQUIRE(H % 2 == 0 && rows_pad >= B * S, "tw_attn_encoder_mx: H=%d (even: the 128-wide scale groups), rows_pad %d",
              H, rows_pad);
   const int D = H * 64;
-  const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;
-  hipLaunchKernelGGL((k_attn_enc2<8, 2, true>), dim3(nwork), dim3(512), 0, (hipStream_t)stream, qkv, S, H, D, nqb,
-                     nwork, nullptr, out, scales, rows_pad);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t pad = (size_t)tw_attn_lds_pad * 16384;
+  const int nqb = tw_cdiv(S, 256), nwork = nqb * H * B;  // 256 queries per workgroup
+  if (tw_attn_variant == 32)  // the variant of tw_attn_set_variant, as tw_attn_encoder (8 and 16: the enc2 MX form)
+    hipLaunchKernelGGL((k_attn_enc5<4, 2, true>), dim3(nwork), dim3(256), pad, st, qkv, S, H, D, nqb, nwork, nullptr,
+                       out, scales, rows_pad);
+  else
+    hipLaunchKernelGGL((k_attn_enc2<8, 2, true>), dim3(nwork), dim3(512), pad, st, qkv, S, H, D, nqb, nwork, nullptr,
+                       out, scales, rows_pad);
   return tw_check_launch("tw_attn_encoder_mx");
 }
 

@@ -315,7 +315,7 @@ extern "C" int tw_logits_select_embed(const float* logits, int B, int ld_logits,
   TW_REQUIRE(params->V > 0 && params->V <= ld_logits, "tw_logits_select_embed: V=%d ld=%d", params->V, ld_logits);
   TW_REQUIRE(params->n_begin_suppress >= 0 && params->n_begin_suppress <= 8, "tw_logits_select_embed: begin_suppress");
   TW_REQUIRE(tok_emb && pos_emb && x && gamma && beta && out && max_pos > 0, "tw_logits_select_embed: embed/LN args");
-  TW_REQUIRE(D > 0 && D % 4 == 0 && D <= 1024 * SFE_MAXV && (!packed || (B <= 32 && D % 32 == 0)),
+  TW_REQUIRE(D > 0 && D % 4 == 0 && D <= 1024 * SFE_MAXV && (!packed || (B <= 64 && D % 32 == 0)),
              "tw_logits_select_embed: D=%d B=%d packed=%d", D, B, packed);
   hipStream_t s = (hipStream_t)stream;
   SelPart* ws = (SelPart*)workspace;

@@ -297,7 +297,7 @@ __global__ TW_DEC_LB(64, 4) void k_resid_ln_w(float* __restrict__ x, const float
     w.x = pack_bf16x2((v[i].x - mean) * rstd * gg[i].x + bb[i].x, (v[i].y - mean) * rstd * gg[i].y + bb[i].y);
     w.y = pack_bf16x2((v[i].z - mean) * rstd * gg[i].z + bb[i].z, (v[i].w - mean) * rstd * gg[i].w + bb[i].w);
     if constexpr (PACKED) {
-      *(uint2*)(out + tw_pack_act_idx(row, 4 * c)) = w;
+      *(uint2*)(out + tw_pack_act_idx(row, 4 * c, D)) = w;
     } else {
       ((uint2*)orow)[c] = w;
     }
@@ -322,8 +322,8 @@ extern "C" int tw_resid_layernorm(float* x, const float* parts, int nparts, cons
 extern "C" int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias,
                                          const float* gamma, const float* beta, int M, int D, float eps, uint16_t* out,
                                          void* stream) {
-  TW_REQUIRE(x && gamma && beta && out && M > 0 && M <= 32 && D > 0 && D % 32 == 0 && D <= 1024 * RLN_MAXV,
-             "tw_resid_layernorm_packed: bad args (M <= 32, D %% 32, gamma/beta/out required)");
+  TW_REQUIRE(x && gamma && beta && out && M > 0 && M <= 64 && D > 0 && D % 32 == 0 && D <= 1024 * RLN_MAXV,
+             "tw_resid_layernorm_packed: bad args (M <= 64, D %% 32, gamma/beta/out required)");
   TW_REQUIRE(nparts >= 0 && (nparts == 0 || parts), "tw_resid_layernorm_packed: parts");
   if (D == 1280)
     hipLaunchKernelGGL((k_resid_ln_w<true, 5>), dim3(M), dim3(64), 0, (hipStream_t)stream, x, parts, nparts,

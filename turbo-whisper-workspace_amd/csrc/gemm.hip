@@ -750,7 +750,7 @@ static void launch_skinny(const bf16_t* A, const bf16_t* W, int M, int N, int K,
 }
 
 // ------------------------------------------------------------------------------------------------
-// Packed decoder GEMV (M <= 32): weights pre-arranged in MFMA fragment order (tw_pack_weight), activations either
+// Packed decoder GEMV (M <= 64): weights pre-arranged in MFMA fragment order (tw_pack_weight), activations either
 // in the packed activation layout (written by tw_resid_layernorm_packed / the GELU_PACKED epilogue) or row-major.
 // Every wave-load is one contiguous 1 KiB fragment (weights: the whole read is one HBM stream per wave), instead
 // of 16 rows x 64 B. Block = 4 (or KW = 8: 8) waves = GPB column groups x KW K-slices; gridDim.y = split-K over
@@ -773,42 +773,46 @@ __global__ __launch_bounds__(256) void k_pack_weight(const bf16_t* __restrict__ 
 
 // NTW: weight fragments read with non-temporal loads (proj_out: 133 MB streamed once per step, kept out of the
 // caches so that the layer weights can stay in them).
-template <int EPI, int KW, int U, bool APACK, bool TWO, bool NTW = false>
+// MT: 16-row m-tiles of the activation (1: M <= 16, 2: M <= 32, 4: M <= 64). Packed activations hold rows 32..63 as a
+// second 32-row block 32 K elements on (tw_pack_act_idx), so m-tile t of step s sits at
+// (t / 2) * 32 K + s * 1024 + (t % 2) * 512; row-major activations read rows 16 t + lane % 16.
+template <int MT, bool APACK>
+__device__ inline const bf16_t* gemv_a_base(const bf16_t* A, int lda, int M, int K, int t, int lane) {
+  if constexpr (APACK) return A + (size_t)(t >> 1) * 32 * K + (t & 1) * 512 + lane * 8;
+  else return A + (size_t)min(16 * t + (lane & 15), M - 1) * lda + 8 * (lane >> 4);
+}
+template <bool APACK>
+__device__ inline bf16x8 gemv_a_load(const bf16_t* ap, int st) {
+  return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024) : *(const bf16x8*)(ap + 32 * st);
+}
+
+template <int EPI, int KW, int U, bool APACK, int MT, bool NTW = false>
 __global__ TW_DEC_LB(KW > 4 ? 512 : 256, 1) void k_gemv_p(const bf16_t* __restrict__ A, int lda,
                                                                const bf16_t* __restrict__ Wp, int M, int N, int K,
                                                                EpiArgs ea) {
   TW_DEC_PRIO();
   constexpr int NW = KW > 4 ? KW : 4, GPB = NW / KW;
   // (KW = 1: no cross-wave sum, no LDS — see the epilogue)
-  __shared__ float red[KW > 1 ? NW : 1][KW > 1 ? 32 : 1][17];
+  __shared__ float red[KW > 1 ? NW : 1][KW > 1 ? MT * 16 : 1][17];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int gl = wid / KW, kw = wid - gl * KW;
   const int g = blockIdx.x * GPB + gl;
   const int ngroups = (N + 15) >> 4, ns = K >> 5;
   const int nsl = KW * gridDim.y, sl = blockIdx.y * KW + kw;
   const int s0 = (int)((long)sl * ns / nsl), s1 = (int)((long)(sl + 1) * ns / nsl);
-  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+  f32x4 c[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) c[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   if (g < ngroups) {
     const bf16_t* wp = Wp + (size_t)g * ns * 512 + lane * 8;
-    const bf16_t* ap;
-    const bf16_t* ap1 = nullptr;
-    if constexpr (APACK) {
-      ap = A + lane * 8;  // step s, m-tile t at + s*1024 + t*512
-    } else {
-      ap = A + (size_t)min(lane & 15, M - 1) * lda + 8 * (lane >> 4);
-      ap1 = A + (size_t)min(16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4);
-    }
-    auto ldA0 = [&](int st) -> bf16x8 {
-      return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024) : *(const bf16x8*)(ap + 32 * st);
-    };
-    auto ldA1 = [&](int st) -> bf16x8 {
-      return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024 + 512) : *(const bf16x8*)(ap1 + 32 * st);
-    };
+    const bf16_t* ap[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) ap[t] = gemv_a_base<MT, APACK>(A, lda, M, K, t, lane);
     auto ldW = [&](int st) -> bf16x8 {
       if constexpr (NTW) {
         typedef short s16x8_nt __attribute__((ext_vector_type(8)));
-        const s16x8_nt t = __builtin_nontemporal_load((const s16x8_nt*)(wp + (size_t)st * 512));
-        return __builtin_bit_cast(bf16x8, t);
+        const s16x8_nt v = __builtin_nontemporal_load((const s16x8_nt*)(wp + (size_t)st * 512));
+        return __builtin_bit_cast(bf16x8, v);
       } else {
         return *(const bf16x8*)(wp + (size_t)st * 512);
       }
@@ -819,13 +823,13 @@ __global__ TW_DEC_LB(KW > 4 ? 512 : 256, 1) void k_gemv_p(const bf16_t* __restri
     // encoder GEMM). n <= NB valid steps: past s1 the loads are clamped to the last step and their MFMAs skipped.
     auto batch = [&](auto NBc, int st0, int n) {
       constexpr int NB = decltype(NBc)::value;
-      bf16x8 bw[NB], a0[NB], a1[NB];
+      bf16x8 bw[NB], a[NB][MT];
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
         const int st = min(st0 + u, s1 - 1);
         bw[u] = ldW(st);
-        a0[u] = ldA0(st);
-        if (TWO) a1[u] = ldA1(st);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) a[u][t] = gemv_a_load<APACK>(ap[t], st);
       }
       // (not on the bandwidth-bound vocabulary-wide proj_out, NTW: its 3242 waves hide the latency, and 48 live
       // fragments cost it occupancy: 26.2 -> 30.8 us per launch alone)
@@ -833,8 +837,8 @@ __global__ TW_DEC_LB(KW > 4 ? 512 : 256, 1) void k_gemv_p(const bf16_t* __restri
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
         if (u < n) {
-          c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], bw[u], c0, 0, 0, 0);
-          if (TWO) c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], bw[u], c1, 0, 0, 0);
+#pragma unroll
+          for (int t = 0; t < MT; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][t], bw[u], c[t], 0, 0, 0);
         }
       }
     };
@@ -852,7 +856,7 @@ __global__ TW_DEC_LB(KW > 4 ? 512 : 256, 1) void k_gemv_p(const bf16_t* __restri
       ((float*)ea.out)[((size_t)blockIdx.y * M + m) * ea.ldo + n] = v;
     } else if constexpr (EPI == TW_EPI_GELU_PACKED) {
       if (ea.bias) v += ea.bias[n];
-      ((bf16_t*)ea.out)[tw_pack_act_idx(m, n)] = f32_to_bf16(gelu_erf(v));
+      ((bf16_t*)ea.out)[tw_pack_act_idx(m, n, N)] = f32_to_bf16(gelu_erf(v));
     } else {
       epi_store<EPI>(ea, m, n, v);
     }
@@ -864,28 +868,27 @@ __global__ TW_DEC_LB(KW > 4 ? 512 : 256, 1) void k_gemv_p(const bf16_t* __restri
     const int n = g * 16 + cc;
     if (g < ngroups && n < N) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (rb + r < M) store(rb + r, n, c0[r]);
-        if (TWO && 16 + rb + r < M) store(16 + rb + r, n, c1[r]);
-      }
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (16 * t + rb + r < M) store(16 * t + rb + r, n, c[t][r]);
     }
     return;
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    red[wid][rb + r][cc] = c0[r];
-    if (TWO) red[wid][16 + rb + r][cc] = c1[r];
-  }
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wid][16 * t + rb + r][cc] = c[t][r];
   __syncthreads();
-  constexpr int ROWS = TWO ? 32 : 16;
+  constexpr int ROWS = MT * 16;
   for (int e = tid; e < GPB * ROWS * 16; e += NW * 64) {
     const int gg = e / (ROWS * 16), rem = e - gg * ROWS * 16;
-    const int m = rem >> 4, c = rem & 15;
-    const int n = (blockIdx.x * GPB + gg) * 16 + c;
+    const int m = rem >> 4, cl = rem & 15;
+    const int n = (blockIdx.x * GPB + gg) * 16 + cl;
     if (m < M && n < N) {
       float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < KW; ++w) v += red[gg * KW + w][m][c];
+      for (int w = 0; w < KW; ++w) v += red[gg * KW + w][m][cl];
       store(m, n, v);
     }
   }
@@ -896,43 +899,37 @@ __global__ TW_DEC_LB(KW > 4 ? 512 : 256, 1) void k_gemv_p(const bf16_t* __restri
 // column group); here a step loads two W fragments and the same two A fragments: a third fewer vector-memory
 // instructions and VGPRs per weight byte. Every decoder-step kernel shares its CU with an encoder GEMM workgroup
 // (run_batches' overlap), whose LDS-DMA keeps the same vector-memory path busy. KW >= 2 K-slices
-// per column-group pair, reduced through LDS; epilogues BF16, PARTIAL (split-K) and GELU_PACKED.
-template <int EPI, int KW, int U, bool APACK, bool TWO, bool NTW = false>
+// per column-group pair, reduced through LDS; epilogues BF16, PARTIAL (split-K) and GELU_PACKED. MT = 4 (M = 33..64:
+// beam rows, config 5's 64 windows) streams every weight byte once for all 64 rows; its cross-wave sum runs in two
+// 32-row passes over the same 17 KiB of LDS as MT = 2.
+template <int EPI, int KW, int U, bool APACK, int MT, bool NTW = false>
 __global__ TW_DEC_LB(256, 1) void k_gemv_pc(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ Wp,
                                             int M, int N, int K, EpiArgs ea) {
   TW_DEC_PRIO();
   static_assert(KW == 1 || KW == 2 || KW == 4, "k_gemv_pc: 1, 2 or 4 K-slices");
   constexpr int NW = 4, GPB = NW / KW;  // pairs per workgroup
-  __shared__ float red[KW > 1 ? NW : 1][2][KW > 1 ? 32 : 1][17];  // (KW = 1: stored from registers, no LDS)
+  constexpr int RT = MT > 2 ? 2 : MT;   // m-tiles per LDS reduction pass
+  __shared__ float red[KW > 1 ? NW : 1][2][KW > 1 ? RT * 16 : 1][17];  // (KW = 1: stored from registers, no LDS)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int gl = wid / KW, kw = wid - gl * KW;
   const int g0 = (blockIdx.x * GPB + gl) * 2;  // this wave's column groups g0, g0 + 1
   const int ngroups = (N + 15) >> 4, ns = K >> 5;
   const int nsl = KW * gridDim.y, sl = blockIdx.y * KW + kw;
   const int s0 = (int)((long)sl * ns / nsl), s1 = (int)((long)(sl + 1) * ns / nsl);
-  f32x4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c10 = c00, c11 = c00;  // c<group><m-tile>
+  f32x4 c[2][MT];  // [group][m-tile]
+#pragma unroll
+  for (int t = 0; t < MT; ++t) c[0][t] = c[1][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   if (g0 < ngroups) {
     const bool has1 = g0 + 1 < ngroups;
     const bf16_t* wp0 = Wp + (size_t)g0 * ns * 512 + lane * 8;
     const bf16_t* wp1 = has1 ? wp0 + (size_t)ns * 512 : wp0;  // (an odd last group: its twin re-reads group g0)
-    const bf16_t* ap;
-    const bf16_t* ap1 = nullptr;
-    if constexpr (APACK) {
-      ap = A + lane * 8;
-    } else {
-      ap = A + (size_t)min(lane & 15, M - 1) * lda + 8 * (lane >> 4);
-      ap1 = A + (size_t)min(16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4);
-    }
-    auto ldA0 = [&](int st) -> bf16x8 {
-      return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024) : *(const bf16x8*)(ap + 32 * st);
-    };
-    auto ldA1 = [&](int st) -> bf16x8 {
-      return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024 + 512) : *(const bf16x8*)(ap1 + 32 * st);
-    };
+    const bf16_t* ap[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) ap[t] = gemv_a_base<MT, APACK>(A, lda, M, K, t, lane);
     // one batch of NB steps, every load issued before the first MFMA (see k_gemv_p)
     auto batch = [&](auto NBc, int st0, int n) {
       constexpr int NB = decltype(NBc)::value;
-      bf16x8 b0[NB], b1[NB], a0[NB], a1[NB];
+      bf16x8 b0[NB], b1[NB], a[NB][MT];
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
         const int st = min(st0 + u, s1 - 1);
@@ -944,18 +941,17 @@ __global__ TW_DEC_LB(256, 1) void k_gemv_pc(const bf16_t* __restrict__ A, int ld
           b0[u] = *(const bf16x8*)(wp0 + (size_t)st * 512);
           b1[u] = *(const bf16x8*)(wp1 + (size_t)st * 512);
         }
-        a0[u] = ldA0(st);
-        if (TWO) a1[u] = ldA1(st);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) a[u][t] = gemv_a_load<APACK>(ap[t], st);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
         if (u < n) {
-          c00 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], b0[u], c00, 0, 0, 0);
-          c10 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], b1[u], c10, 0, 0, 0);
-          if (TWO) {
-            c01 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], b0[u], c01, 0, 0, 0);
-            c11 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], b1[u], c11, 0, 0, 0);
+#pragma unroll
+          for (int t = 0; t < MT; ++t) {
+            c[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][t], b0[u], c[0][t], 0, 0, 0);
+            c[1][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][t], b1[u], c[1][t], 0, 0, 0);
           }
         }
       }
@@ -968,51 +964,50 @@ __global__ TW_DEC_LB(256, 1) void k_gemv_pc(const bf16_t* __restrict__ A, int ld
     else if (rem > 0) batch(std::integral_constant<int, (U / 2 > 0 ? U / 2 : 1)>{}, st, rem);
   }
   const int cc = lane & 15, rb = (lane >> 4) * 4;
+  auto store = [&](int m, int n, float v) {
+    if constexpr (EPI == TW_EPI_PARTIAL) {
+      ((float*)ea.out)[((size_t)blockIdx.y * M + m) * ea.ldo + n] = v;
+    } else if constexpr (EPI == TW_EPI_GELU_PACKED) {
+      if (ea.bias) v += ea.bias[n];
+      ((bf16_t*)ea.out)[tw_pack_act_idx(m, n, N)] = f32_to_bf16(gelu_erf(v));
+    } else {
+      epi_store<EPI>(ea, m, n, v);
+    }
+  };
   if constexpr (KW == 1) {  // the accumulators are the results: 16 lanes per row store 16 consecutive columns
-    auto st1 = [&](int m, int n, float v) {
-      if constexpr (EPI == TW_EPI_PARTIAL) ((float*)ea.out)[((size_t)blockIdx.y * M + m) * ea.ldo + n] = v;
-      else if constexpr (EPI == TW_EPI_GELU_PACKED)
-        ((bf16_t*)ea.out)[tw_pack_act_idx(m, n)] = f32_to_bf16(gelu_erf(v + (ea.bias ? ea.bias[n] : 0.f)));
-      else epi_store<EPI>(ea, m, n, v);
-    };
     const int n0 = g0 * 16 + cc, n1 = n0 + 16;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = rb + r;
-      if (m < M && n0 < N) st1(m, n0, c00[r]);
-      if (m < M && n1 < N) st1(m, n1, c10[r]);
-      if (TWO && 16 + m < M && n0 < N) st1(16 + m, n0, c01[r]);
-      if (TWO && 16 + m < M && n1 < N) st1(16 + m, n1, c11[r]);
-    }
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * t + rb + r;
+        if (m < M && n0 < N) store(m, n0, c[0][t][r]);
+        if (m < M && n1 < N) store(m, n1, c[1][t][r]);
+      }
     return;
   }
+  constexpr int ROWS = RT * 16;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    red[wid][0][rb + r][cc] = c00[r];
-    red[wid][1][rb + r][cc] = c10[r];
-    if (TWO) {
-      red[wid][0][16 + rb + r][cc] = c01[r];
-      red[wid][1][16 + rb + r][cc] = c11[r];
-    }
-  }
-  __syncthreads();
-  constexpr int ROWS = TWO ? 32 : 16;
-  for (int e = tid; e < GPB * 2 * ROWS * 16; e += NW * 64) {
-    const int pg = e / (2 * ROWS * 16), rem = e - pg * 2 * ROWS * 16;  // pair in the block, then group, row, column
-    const int h = rem / (ROWS * 16), r2 = rem - h * ROWS * 16;
-    const int m = r2 >> 4, c = r2 & 15;
-    const int n = ((blockIdx.x * GPB + pg) * 2 + h) * 16 + c;
-    if (m < M && n < N) {
-      float v = 0.f;
+  for (int pass = 0; pass < MT / RT; ++pass) {
+    if (pass) __syncthreads();  // (the previous pass's reads of red are done)
 #pragma unroll
-      for (int w = 0; w < KW; ++w) v += red[pg * KW + w][h][m][c];
-      if constexpr (EPI == TW_EPI_PARTIAL) {
-        ((float*)ea.out)[((size_t)blockIdx.y * M + m) * ea.ldo + n] = v;
-      } else if constexpr (EPI == TW_EPI_GELU_PACKED) {
-        if (ea.bias) v += ea.bias[n];
-        ((bf16_t*)ea.out)[tw_pack_act_idx(m, n)] = f32_to_bf16(gelu_erf(v));
-      } else {
-        epi_store<EPI>(ea, m, n, v);
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        red[wid][0][16 * t + rb + r][cc] = c[0][pass * RT + t][r];
+        red[wid][1][16 * t + rb + r][cc] = c[1][pass * RT + t][r];
+      }
+    __syncthreads();
+    for (int e = tid; e < GPB * 2 * ROWS * 16; e += NW * 64) {
+      const int pg = e / (2 * ROWS * 16), rem = e - pg * 2 * ROWS * 16;  // pair in the block, then group, row, column
+      const int h = rem / (ROWS * 16), r2 = rem - h * ROWS * 16;
+      const int m = pass * ROWS + (r2 >> 4), cl = r2 & 15;
+      const int n = ((blockIdx.x * GPB + pg) * 2 + h) * 16 + cl;
+      if (m < M && n < N) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < KW; ++w) v += red[pg * KW + w][h][r2 >> 4][cl];
+        store(m, n, v);
       }
     }
   }
@@ -1023,21 +1018,26 @@ static void launch_gemv_pc(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
                            int splits, hipStream_t s) {
   constexpr int GPB = 4 / KW;
   dim3 grid(tw_cdiv(tw_cdiv(tw_cdiv(N, 16), 2), GPB), splits);
-  if (M > 16)
-    hipLaunchKernelGGL((k_gemv_pc<EPI, KW, U, APACK, true, NTW>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
+  if (M > 32)  // (fewer steps per batch: four A fragments per step)
+    hipLaunchKernelGGL((k_gemv_pc<EPI, KW, 3, APACK, 4, NTW>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
+  else if (M > 16)
+    hipLaunchKernelGGL((k_gemv_pc<EPI, KW, U, APACK, 2, NTW>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
   else
-    hipLaunchKernelGGL((k_gemv_pc<EPI, KW, U, APACK, false, NTW>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
+    hipLaunchKernelGGL((k_gemv_pc<EPI, KW, U, APACK, 1, NTW>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
 }
 
 template <int EPI, int KW, int U, bool APACK, bool NTW = false>
 static void launch_gemv_p3(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea, int splits,
                            hipStream_t s) {
   constexpr int NW = KW > 4 ? KW : 4, GPB = NW / KW;
+  constexpr int U4 = U > 4 ? U / 2 : U;  // M > 32: four A fragments per step
   dim3 grid(tw_cdiv(tw_cdiv(N, 16), GPB), splits);
-  if (M > 16)
-    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, true, NTW>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea);
+  if (M > 32)
+    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U4, APACK, 4, NTW>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea);
+  else if (M > 16)
+    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, 2, NTW>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea);
   else
-    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, false, NTW>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea);
+    hipLaunchKernelGGL((k_gemv_p<EPI, KW, U, APACK, 1, NTW>), grid, dim3(NW * 64), 0, s, A, lda, Wp, M, N, K, ea);
 }
 
 template <int EPI, bool APACK>
@@ -1141,7 +1141,7 @@ extern "C" int tw_pack_weight(const bf16_t* W, int N, int K, int ldw, bf16_t* Wp
 extern "C" int tw_gemv_packed(const bf16_t* A, int a_packed, int lda, const bf16_t* Wp, int M, int N, int K, int epi,
                               void* out, int ldo, const float* bias, int splits, void* stream) {
   TW_REQUIRE(A && Wp && out, "tw_gemv_packed: null pointer");
-  TW_REQUIRE(M > 0 && M <= 32 && N > 0 && K > 0 && K % 32 == 0, "tw_gemv_packed: M=%d N=%d K=%d (M <= 32, K %% 32)", M,
+  TW_REQUIRE(M > 0 && M <= 64 && N > 0 && K > 0 && K % 32 == 0, "tw_gemv_packed: M=%d N=%d K=%d (M <= 64, K %% 32)", M,
              N, K);
   TW_REQUIRE(a_packed || (lda >= K && lda % 8 == 0), "tw_gemv_packed: lda=%d", lda);
   TW_REQUIRE(splits >= 1 && splits <= 16 && splits <= K / 32, "tw_gemv_packed: splits=%d", splits);

@@ -209,12 +209,14 @@ __device__ inline void tw_st_enc(void* p, float4 v) {
 #define TW_DEC_REGS
 #endif
 
-// Decoder fragment layouts (include/tw_whisper.h "packed" formats), M <= 32 activation rows:
-//   activation [K/32][2][64][8] bf16: element (m, k) at ((k/32 * 2 + m/16) * 64 + (m%16) + 16*((k/8)%4)) * 8 + k%8,
-//     i.e. step s = k/32, m-tile t = m/16 is the 16x32 A fragment of v_mfma_f32_16x16x32_bf16 (1 KiB contiguous)
+// Decoder fragment layouts (include/tw_whisper.h "packed" formats), M <= 64 activation rows:
+//   activation [M/32][K/32][2][64][8] bf16: element (m, k) at 32 K (m/32) + ((k/32 * 2 + (m/16)%2) * 64 + (m%16) +
+//     16*((k/8)%4)) * 8 + k%8, i.e. rows 0..31 and 32..63 are two 32-row blocks; in a block step s = k/32, m-tile
+//     t = (m/16)%2 is the 16x32 A fragment of v_mfma_f32_16x16x32_bf16 (1 KiB contiguous)
 //   weight     [N/16][K/32][64][8] bf16: element (n, k) at ((n/16 * K/32 + k/32) * 64 + (n%16) + 16*((k/8)%4)) * 8 + k%8
-__host__ __device__ inline size_t tw_pack_act_idx(int m, int k) {
-  return ((size_t)((k >> 5) * 2 + (m >> 4)) * 64 + (m & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
+__host__ __device__ inline size_t tw_pack_act_idx(int m, int k, int K) {
+  return (m >= 32 ? (size_t)32 * K : (size_t)0) +
+         ((size_t)((k >> 5) * 2 + ((m >> 4) & 1)) * 64 + (m & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
 }
 __host__ __device__ inline size_t tw_pack_w_idx(int n, int k, int K) {
   return ((size_t)((n >> 4) * (K >> 5) + (k >> 5)) * 64 + (n & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7);
@@ -255,7 +257,7 @@ __device__ inline void tw_row_ln_store(const float4 (&v)[NV], float s, int row, 
       w.x = pack_bf16x2((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
       w.y = pack_bf16x2((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
       if constexpr (PACKED) {
-        *(uint2*)(out + tw_pack_act_idx(row, 4 * c)) = w;  // 4 columns = half a 16-byte fragment chunk
+        *(uint2*)(out + tw_pack_act_idx(row, 4 * c, D)) = w;  // 4 columns = half a 16-byte fragment chunk
       } else {
         ((uint2*)orow)[c] = w;
       }

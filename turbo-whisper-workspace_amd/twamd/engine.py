@@ -36,6 +36,9 @@ S_ENC = 1500
 def _pad256(n: int) -> int:
     return (n + 255) // 256 * 256
 DEC_SPLITS = 4   # split-K factor of the decoder's d_model-wide projections (out_proj, fc2)
+# rows per decoder view: the packed GEMVs stream each weight byte once for up to 64 rows (four 16-row m-tiles; config
+# 5's 64 windows, beam-5 over 12 windows); more rows run as consecutive views
+VIEW_ROWS = 64
 
 
 def on_engine_streams(fn):
@@ -78,7 +81,7 @@ class DecView:
     tokens: torch.Tensor
     ids: torch.Tensor
     pos: torch.Tensor
-    hp: torch.Tensor   # packed-activation LayerNorm output (tw_gemv_packed A operand), <= 32 rows
+    hp: torch.Tensor   # packed-activation LayerNorm output (tw_gemv_packed A operand), <= VIEW_ROWS rows
     fp: torch.Tensor   # packed-activation fc1 output (fc2's A operand)
 
 
@@ -257,7 +260,7 @@ class WhisperEngine:
         self.prompt_graph = True
         # encoder attention kernel (tw_attn_set_variant) and its LDS cap in 16 KiB units (tw_attn_set_lds_pad) for an
         # encoder chunk alone / beside a running decode
-        self.attn_kernel = (16, 16)
+        self.attn_kernel = (32, 32)  # k_attn_enc5 (round 4; 16 = k_attn_enc4, bit-identical to the enc2 form)
         self.attn_pad = (0, 4)
         # run_batches encodes batch k+1 beside the decode of batch k (sequential 138.6 vs overlapped 114.5 ms per
         # bench step, round 1); False: strictly in turn
@@ -395,11 +398,11 @@ class WhisperEngine:
                 self._chain_cache[key] = self._view(r0, n, self.stream, self.parts)
             return self._chain_cache[key]
         sl = slice(r0, r0 + n)
-        if n > 32:
-            raise ValueError(f"decoder views hold <= 32 rows (packed GEMV), got {n}")
+        if n > VIEW_ROWS:
+            raise ValueError(f"decoder views hold <= {VIEW_ROWS} rows (packed GEMV), got {n}")
         # per-view packed scratch (rows 0..n-1 of the view; pad rows zero)
-        hp = torch.zeros(32 * self.d.d_model, dtype=torch.bfloat16, device=self.device)
-        fp = torch.zeros(32 * self.d.ffn, dtype=torch.bfloat16, device=self.device)
+        hp = torch.zeros(VIEW_ROWS * self.d.d_model, dtype=torch.bfloat16, device=self.device)
+        fp = torch.zeros(VIEW_ROWS * self.d.ffn, dtype=torch.bfloat16, device=self.device)
         return DecView(r0, n, stream or self.stream, self.xd[sl], self.qkvd[sl], self.qd[sl], self.attd[sl],
                        self.logits[sl], self.parts if parts is None else parts, self.sel_ws[sl], self.state[sl],
                        self.tokens[sl], self.ids[sl], self.pos[sl], hp, fp)
@@ -534,10 +537,11 @@ class WhisperEngine:
         activations (the GEMVs' A operand), attention outputs stay row-major; every d_model-wide projection (self /
         cross out_proj, fc2) is a split-K partial product whose sum, bias and residual add are folded into the next
         LayerNorm launch."""
-        if v is None and R > 32:  # the packed decoder GEMVs take <= 32 rows: one view per 32
+        if v is None and R > VIEW_ROWS:  # the packed decoder GEMVs take <= VIEW_ROWS rows: one view per VIEW_ROWS
             r_enc = R if r_enc is None else r_enc
-            for r0 in range(0, R, 32):
-                self.decoder_step(min(32, R - r0), with_logits, self._view(r0, min(32, R - r0)), r_enc, pre_embedded)
+            for r0 in range(0, R, VIEW_ROWS):
+                n = min(VIEW_ROWS, R - r0)
+                self.decoder_step(n, with_logits, self._view(r0, n), r_enc, pre_embedded)
             return
         v = v or self._view(0, R)
         r_enc = R if r_enc is None else r_enc
@@ -656,9 +660,9 @@ class WhisperEngine:
                 embed_next: bool = False) -> None:
         """Processors + greedy selection for the view's rows; embed_next: also the head of the next step (the chosen
         token's embedding into xd and layer 0's self_attn_layer_norm into the view's LN buffer, one fused launch)."""
-        if v is None and R > 32:  # per-row selection over the <= 32-row views decoder_step(R) ran (beam / config-5 rows)
-            for r0 in range(0, R, 32):
-                self._select(min(32, R - r0), params, tokens, self._view(r0, min(32, R - r0)), embed_next)
+        if v is None and R > VIEW_ROWS:  # per-row selection over the views decoder_step(R) ran (beam rows)
+            for r0 in range(0, R, VIEW_ROWS):
+                self._select(min(VIEW_ROWS, R - r0), params, tokens, self._view(r0, min(VIEW_ROWS, R - r0)), embed_next)
             return
         v = v or self._view(0, R)
         if embed_next:
@@ -687,8 +691,8 @@ class WhisperEngine:
         if v is not None:
             self._embed_head(v)
             return
-        for r0 in range(0, R, 32):
-            self._embed_head(self._view(r0, min(32, R - r0)))
+        for r0 in range(0, R, VIEW_ROWS):
+            self._embed_head(self._view(r0, min(VIEW_ROWS, R - r0)))
 
     def _embed_head(self, v: DecView) -> None:
         """The head of a decoder step alone (embedding + layer 0's self_attn_layer_norm) for view v: primes a chain
@@ -1028,7 +1032,7 @@ class WhisperEngine:
         key = ("chains", R)
         if key not in self._chain_cache:
             k = max(1, min(self.n_chains, R // 4))
-            k = max(k, (R + 31) // 32)  # <= 32 rows per chain (packed GEMV and skinny GEMM limit)
+            k = max(k, (R + VIEW_ROWS - 1) // VIEW_ROWS)  # <= VIEW_ROWS rows per chain (packed GEMV limit)
             while len(self._chain_streams) < k:
                 self._chain_streams.append(self._chain_streams[0])  # one stream: the chains run in turn
             views = []
