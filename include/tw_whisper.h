@@ -221,9 +221,14 @@ int tw_kv_reorder(uint16_t* k_cache, uint16_t* v_cache, uint16_t* k_scratch, uin
 int tw_pack_weight(const uint16_t* W, int N, int K, int ldw, uint16_t* Wp, void* stream);
 int tw_gemv_packed(const uint16_t* A, int a_packed, int lda, const uint16_t* Wp, int M, int N, int K, int epi,
                    void* out, int ldo, const float* bias, int splits, void* stream);
-/* tw_resid_layernorm with the normalised rows written as a packed activation (M <= 32, D % 32 == 0). */
+/* tw_resid_layernorm with the normalised rows written as a packed activation (M <= 64, D % 32 == 0). */
 int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
                               const float* beta, int M, int D, float eps, uint16_t* out, void* stream);
+/* The same with the updated residual rows written to x_out instead of in place (x is only read; x_out may equal x):
+ * the step after tw_attn_decode_cross_q, whose residual went to a second buffer. */
+int tw_resid_layernorm_packed_to(const float* x, float* x_out, const float* parts, int nparts, const float* bias,
+                                 const float* gamma, const float* beta, int M, int D, float eps, uint16_t* out,
+                                 void* stream);
 
 /* Decoder self-attention for one new token per row: appends k,v of qkv bf16[B][3D] at pos[b] into
  * k_cache/v_cache bf16[B][H][max_pos][64] (this layer) and attends over 0..pos[b].
@@ -251,6 +256,17 @@ int tw_debug_build(void);
  * cross_kv bf16[2][Bt][H][S][64]; row b reads slot row_map[b] (NULL = b). */
 int tw_attn_decode_cross(const uint16_t* q, int B, int H, int S, int Bt, const int* row_map, const uint16_t* cross_kv,
                          uint16_t* out, void* stream);
+/* tw_attn_decode_cross with the two steps before it folded in (one launch instead of three): row b's residual
+ * update and encoder_attn_layer_norm, x_out[b] = x[b] + bias + sum_{p < nparts} parts[p][b] (parts f32[nparts][B][D],
+ * D = 64 H <= 1280) and LN = bf16(LayerNorm(x_out[b]) * gamma + beta), then the head's query
+ * q = bf16(LN . wq[64 h .. 64 h + 63][:]^T + bq) (wq bf16 [D][D] row-major = nn.Linear, q already scaled by 64^-0.5
+ * as the decoder's q_proj weights are), then the attention of tw_attn_decode_cross. x_out must not alias x.
+ * Replaces the residual add + LayerNorm + q_proj of WhisperDecoderLayer.forward's cross-attention block
+ * ($TF/models/whisper/modeling_whisper.py:486-496, 279-282). */
+int tw_attn_decode_cross_q(const float* x, const float* parts, int nparts, const float* bias, const float* gamma,
+                           const float* beta, float eps, const uint16_t* wq, const float* bq, float* x_out, int B,
+                           int H, int S, int Bt, const int* row_map, const uint16_t* cross_kv, uint16_t* out,
+                           void* stream);
 /* The same for rows that share an encoder slot in groups (the beams of one window, rows w * num_beams + j): the first
  * `first` rows (0 <= first < group, the tail of a group that began before this view) form one group, then every
  * `group` rows (2..8) one group; all rows of a group must hold the same row_map entry (required, not checked). Each

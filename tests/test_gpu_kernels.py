@@ -584,3 +584,72 @@ def test_resid_layernorm_packed_vs_torch(M, D, nparts):
     _lib.call("tw_resid_layernorm_packed", x3.data_ptr(), parts.data_ptr(), nparts, _lib.ptr(bias), g.data_ptr(),
               b.data_ptr(), M, D, 1e-5, out.data_ptr(), S())
     assert torch.equal(unpack_act(out, M, D).view(torch.int16), rm.view(torch.int16))
+
+
+@pytest.mark.parametrize("B,H,nparts,Sx", [(24, 20, 4, 1500), (5, 6, 2, 1500), (64, 20, 4, 1500), (3, 20, 0, 33)])
+def test_attn_decode_cross_q_vs_separate_launches(B, H, nparts, Sx):
+    """tw_attn_decode_cross_q (residual + LayerNorm + the head's q projection + cross-attention in one launch) against
+    the three launches it replaces (tw_resid_layernorm_packed, the q GEMV, tw_attn_decode_cross) and against fp32:
+    the residual rows bit-identical (same per-element summation order), the attention output within 2 bf16 ulps of
+    the separate launches (the LayerNorm's reductions run in another order) and within 2e-2 of fp32."""
+    D = H * 64
+    g = torch.Generator(device="cpu").manual_seed(B * 100 + H)
+    x = (torch.randn(B, D, generator=g) * 2 + 0.5).to(DEV)
+    parts = torch.randn(max(nparts, 1), B, D, generator=g).to(DEV)
+    bias = torch.randn(D, generator=g).to(DEV) * 0.1
+    gam = (torch.rand(D, generator=g) + 0.5).to(DEV)
+    bet = (torch.randn(D, generator=g) * 0.1).to(DEV)
+    wq = rand_bf16(D, D, scale=D ** -0.5 * 0.125 * 4, seed=B + 7)
+    bq = torch.randn(D, generator=g).to(DEV) * 0.05
+    Bt = B
+    ckv = rand_bf16(2, Bt, H, Sx, 64, seed=H + Sx)
+    rm = torch.arange(B, dtype=torch.int32, device=DEV).flip(0).contiguous()
+    # fused
+    x_out = torch.full_like(x, float("nan"))
+    out = torch.empty(B, D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_attn_decode_cross_q", x.data_ptr(), parts.data_ptr(), nparts, bias.data_ptr(), gam.data_ptr(),
+              bet.data_ptr(), 1e-5, wq.data_ptr(), bq.data_ptr(), x_out.data_ptr(), B, H, Sx, Bt, rm.data_ptr(),
+              ckv.data_ptr(), out.data_ptr(), S())
+    # separate launches (views of <= 64 rows)
+    x2 = x.clone()
+    hp = torch.zeros(D * 64, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_resid_layernorm_packed", x2.data_ptr(), parts.data_ptr(), nparts, bias.data_ptr(), gam.data_ptr(),
+              bet.data_ptr(), B, D, 1e-5, hp.data_ptr(), S())
+    q = torch.empty(B, D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_gemv_packed", hp.data_ptr(), 1, D, pack_w(wq).data_ptr(), B, D, D, _lib.TW_EPI_BF16, q.data_ptr(), D,
+              bq.data_ptr(), 1, S())
+    out2 = torch.empty_like(out)
+    _lib.call("tw_attn_decode_cross", q.data_ptr(), B, H, Sx, Bt, rm.data_ptr(), ckv.data_ptr(), out2.data_ptr(), S())
+    torch.cuda.synchronize()
+    assert torch.equal(x_out, x2)
+    ulp = torch.maximum(out.float().abs(), out2.float().abs()).clamp_min(0.02) * 2.0 ** -7
+    d = (out.float() - out2.float()).abs()
+    print(f"cross_q vs separate: max |d| {d.max().item():.2e}, {(d / ulp).max().item():.2f} ulps")
+    assert bool((d <= 2 * ulp).all())
+    # fp32 reference of the whole block
+    xr = x + (bias + parts[:nparts].sum(0) if nparts else bias)
+    ln = torch.nn.functional.layer_norm(xr, (D,), gam, bet, 1e-5)
+    qf = ln @ wq.float().t() + bq
+    for b in range(B):
+        s = int(rm[b])
+        ref = _ref_attn(qf[b].view(H, 1, 64), ckv[0, s].float(), ckv[1, s].float())[:, 0].reshape(D)
+        torch.testing.assert_close(out[b].float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_resid_layernorm_packed_to_writes_the_other_buffer():
+    """tw_resid_layernorm_packed_to: the in-place kernel's arithmetic, the updated rows in x_out, x untouched."""
+    M, D = 24, 1280
+    x = torch.randn(M, D, device=DEV)
+    parts = torch.randn(4, M, D, device=DEV)
+    bias, g, b = torch.randn(D, device=DEV), torch.randn(D, device=DEV), torch.randn(D, device=DEV)
+    x0 = x.clone()
+    xo = torch.full_like(x, float("nan"))
+    out1 = torch.zeros(D * 64, dtype=torch.bfloat16, device=DEV)
+    out2 = torch.zeros_like(out1)
+    _lib.call("tw_resid_layernorm_packed_to", x.data_ptr(), xo.data_ptr(), parts.data_ptr(), 4, bias.data_ptr(),
+              g.data_ptr(), b.data_ptr(), M, D, 1e-5, out1.data_ptr(), S())
+    x2 = x0.clone()
+    _lib.call("tw_resid_layernorm_packed", x2.data_ptr(), parts.data_ptr(), 4, bias.data_ptr(), g.data_ptr(),
+              b.data_ptr(), M, D, 1e-5, out2.data_ptr(), S())
+    torch.cuda.synchronize()
+    assert torch.equal(x, x0) and torch.equal(xo, x2) and torch.equal(out1, out2)

@@ -1200,6 +1200,236 @@ __global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_lean(const bf16_t* __re
   }
 }
 
+// k_attn_decode_cross_q: the lean cross-attention with the two launches before it folded into its prologue — the
+// residual + encoder_attn_layer_norm of row b (what tw_resid_layernorm_packed did: x + bias + the out_proj's split-K
+// partials, then LayerNorm) and this head's 64 columns of the q projection (what the cross-q GEMV did:
+// bf16(LN(x)) . Wq[h*64 .. h*64+63][:]^T + bq, rounded to bf16 like the GEMV's output). Every (row, head) block
+// recomputes its row's LayerNorm (40 KB of L2 reads) and reads its head's 160 KB slice of Wq (L2 / Infinity-Cache
+// resident: 3.3 MB per layer for all blocks), in two rounds of 20 16-byte loads per lane, the first issued before the
+// LayerNorm's loads so that both latencies overlap; the K/V stream then runs exactly as in the lean kernel. The
+// updated residual row is written once, by head 0's block, to x_out (a second buffer: the other heads' blocks still
+// read x). Saves two launches per decoder layer (a decode step: 47 -> 39).
+#define XQ_MAXC 2  // float4 chunks of the row per thread: D <= 2048
+template <int NG, int UNR = DA_UNR>
+__global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_q(const float* __restrict__ x, const float* __restrict__ parts,
+                                                             int nparts, long part_stride, const float* __restrict__ bias,
+                                                             const float* __restrict__ gam, const float* __restrict__ bet,
+                                                             float eps, const bf16_t* __restrict__ wq,
+                                                             const float* __restrict__ bq, float* __restrict__ x_out,
+                                                             int S, int Bt, const int* __restrict__ row_map,
+                                                             const bf16_t* __restrict__ ckv, bf16_t* __restrict__ out) {
+  TW_DEC_PRIO();
+  static_assert(NG == 32, "k_attn_decode_cross_q: 256 threads");
+  constexpr int NWV = NG / 8;
+  __shared__ float wpart[NWV][64];
+  __shared__ float wml[NWV][2];
+  __shared__ float ys[2048];  // bf16-rounded LayerNorm output of the row (D <= 2048)
+  __shared__ float qs[64];
+  __shared__ float red[8];
+  const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x, D = H * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = tid >> 3, gl = tid & 7;
+  const int nc = D >> 2, nch = D >> 3;  // float4 chunks of the row; 16-byte bf16 chunks of a Wq row
+  // ---- q projection, round 1 (issued first: it depends on nothing): wave wid owns Wq rows 16 wid .. 16 wid + 15 of
+  // this head, taken as row pairs (two consecutive rows = 2 D / 8 contiguous 16-byte chunks); lane l reads chunks
+  // l + 64 i (i < 5 for D = 1280: every load instruction 1 KiB contiguous, no idle lanes)
+  constexpr int PPR = 4;                           // row pairs per round
+  constexpr int CPL = 5;                           // chunks per lane per pair (2 D / 8 / 64 at D = 1280; <= 6)
+  const bf16_t* wrow0 = wq + (size_t)(h * 64 + wid * 16) * D;
+  uint4 wr[PPR][CPL];
+  auto wload = [&](int pr0) {
+#pragma unroll
+    for (int p = 0; p < PPR; ++p)
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        const int c = min(lane + 64 * i, 2 * nch - 1);
+        wr[p][i] = *(const uint4*)(wrow0 + (size_t)(2 * (pr0 + p)) * D + c * 8);
+      }
+  };
+  wload(0);
+  // ---- residual + LayerNorm of row b (summation order as k_resid_ln_w: ((x + bias) + p0) + p1 + ...)
+  const float* xr = x + (size_t)b * D;
+  const float* pr = parts ? parts + (size_t)b * D : nullptr;
+  float4 v[XQ_MAXC];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < XQ_MAXC; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nc) {
+      float4 a = ((const float4*)xr)[c];
+      if (bias) {
+        const float4 bb = ((const float4*)bias)[c];
+        a.x += bb.x; a.y += bb.y; a.z += bb.z; a.w += bb.w;
+      }
+      for (int p = 0; p < nparts; ++p) {
+        const float4 q = ((const float4*)(pr + p * part_stride))[c];
+        a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
+      }
+      v[i] = a;
+      s += (a.x + a.y) + (a.z + a.w);
+      if (h == 0) ((float4*)(x_out + (size_t)b * D))[c] = a;
+    }
+  }
+  s = wave_sum(s);
+  if (lane == 0) red[wid] = s;
+  __syncthreads();
+  const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)D;
+  float q2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < XQ_MAXC; ++i) {
+    if (tid + 256 * i < nc) {
+      const float a = v[i].x - mean, bb = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+      q2 += (a * a + bb * bb) + (c * c + d * d);
+    }
+  }
+  q2 = wave_sum(q2);
+  if (lane == 0) red[4 + wid] = q2;
+  __syncthreads();
+  const float rstd = rsqrtf((red[4] + red[5] + red[6] + red[7]) / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < XQ_MAXC; ++i) {
+    const int c = tid + 256 * i;
+    if (c < nc) {
+      const float4 gg = ((const float4*)gam)[c], bb = ((const float4*)bet)[c];
+      ys[4 * c + 0] = bf16_to_f32(f32_to_bf16((v[i].x - mean) * rstd * gg.x + bb.x));
+      ys[4 * c + 1] = bf16_to_f32(f32_to_bf16((v[i].y - mean) * rstd * gg.y + bb.y));
+      ys[4 * c + 2] = bf16_to_f32(f32_to_bf16((v[i].z - mean) * rstd * gg.z + bb.z));
+      ys[4 * c + 3] = bf16_to_f32(f32_to_bf16((v[i].w - mean) * rstd * gg.w + bb.w));
+    }
+  }
+  __syncthreads();
+  // ---- the two rounds of dot products (chunk c of a pair: row c / nch of the pair, columns 8 (c % nch) ..)
+  auto wdot = [&](int pr0) {
+#pragma unroll
+    for (int p = 0; p < PPR; ++p) {
+      float d0 = 0.f, d1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        const int c = lane + 64 * i;
+        if (c < 2 * nch) {
+          const int kc = c < nch ? c : c - nch;
+          const float4 y0 = *(const float4*)(ys + kc * 8), y1 = *(const float4*)(ys + kc * 8 + 4);
+          const bf16_t* we = (const bf16_t*)&wr[p][i];
+          const float d = ((y0.x * bf16_to_f32(we[0]) + y0.y * bf16_to_f32(we[1])) +
+                           (y0.z * bf16_to_f32(we[2]) + y0.w * bf16_to_f32(we[3]))) +
+                          ((y1.x * bf16_to_f32(we[4]) + y1.y * bf16_to_f32(we[5])) +
+                           (y1.z * bf16_to_f32(we[6]) + y1.w * bf16_to_f32(we[7])));
+          if (c < nch) d0 += d; else d1 += d;
+        }
+      }
+      d0 = wave_sum(d0);
+      d1 = wave_sum(d1);
+      if (lane == 0) {
+        const int j = wid * 16 + 2 * (pr0 + p);
+        qs[j] = bf16_to_f32(f32_to_bf16(d0 + bq[h * 64 + j]));
+        qs[j + 1] = bf16_to_f32(f32_to_bf16(d1 + bq[h * 64 + j + 1]));
+      }
+    }
+  };
+  wdot(0);
+  wload(PPR);
+  wdot(PPR);
+  __syncthreads();
+  float qv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) qv[e] = qs[gl * 8 + e];
+  // ---- the lean kernel's attention over the row's cross K/V
+  const int slot = row_map ? row_map[b] : b;
+  const bf16_t* K = ckv + (((size_t)0 * Bt + slot) * H + h) * S * 64;
+  const bf16_t* V = ckv + (((size_t)1 * Bt + slot) * H + h) * S * 64;
+  float m = -INFINITY, l = 0.f;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int nit = (S + NG - 1) / NG;
+  for (int it0 = 0; it0 < nit; it0 += UNR) {
+    uint4 kk[UNR], vv[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int key = min((it0 + u) * NG + g, S - 1);
+      typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+      const u32x4_nt a = __builtin_nontemporal_load((const u32x4_nt*)(K + (size_t)key * 64 + gl * 8));
+      const u32x4_nt c = __builtin_nontemporal_load((const u32x4_nt*)(V + (size_t)key * 64 + gl * 8));
+      kk[u] = make_uint4(a.x, a.y, a.z, a.w);
+      vv[u] = make_uint4(c.x, c.y, c.z, c.w);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    float sv[UNR];
+    float bm = m;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      float d = 0.f;
+      const bf16_t* ke = (const bf16_t*)&kk[u];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      sv[u] = (it0 + u) * NG + g < S ? d : -INFINITY;
+      bm = fmaxf(bm, sv[u]);
+    }
+    if (bm == -INFINITY) continue;
+    const float sc = __expf(m - bm);
+    l *= sc;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= sc;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const float p = __expf(sv[u] - bm);
+      l += p;
+      const bf16_t* ve = (const bf16_t*)&vv[u];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += p * bf16_to_f32(ve[e]);
+    }
+    m = bm;
+  }
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) {
+    const float m2 = __shfl_xor(m, o, 64), l2 = __shfl_xor(l, o, 64);
+    const float M = fmaxf(m, m2);
+    const float s1 = m == -INFINITY ? 0.f : __expf(m - M), s2 = m2 == -INFINITY ? 0.f : __expf(m2 - M);
+    l = l * s1 + l2 * s2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = acc[e] * s1 + __shfl_xor(acc[e], o, 64) * s2;
+    m = M;
+  }
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) wpart[wid][lane * 8 + e] = acc[e];
+    if (lane == 0) {
+      wml[wid][0] = m;
+      wml[wid][1] = l;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) M = fmaxf(M, wml[w][0]);
+    float vsum = 0.f, tot = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+      const float mg = wml[w][0];
+      const float wt = mg == -INFINITY ? 0.f : __expf(mg - M);
+      tot += wt * wml[w][1];
+      vsum += wt * wpart[w][tid];
+    }
+    out[(size_t)b * D + h * 64 + tid] = f32_to_bf16(vsum / tot);
+  }
+}
+
+extern "C" int tw_attn_decode_cross_q(const float* x, const float* parts, int nparts, const float* bias,
+                                      const float* gamma, const float* beta, float eps, const uint16_t* wq,
+                                      const float* bq, float* x_out, int B, int H, int S, int Bt, const int* row_map,
+                                      const uint16_t* cross_kv, uint16_t* out, void* stream) {
+  TW_REQUIRE(x && gamma && beta && wq && bq && x_out && cross_kv && out && x_out != x && B > 0 && H > 0 && S > 0 &&
+                 S <= DA_MAXK,
+             "tw_attn_decode_cross_q: bad args");
+  TW_REQUIRE(H * 64 <= 2048 && 2 * (H * 64 / 8) <= 64 * 5 && nparts >= 0 && nparts <= 8 && (nparts == 0 || parts),
+             "tw_attn_decode_cross_q: H=%d (H * 64 <= 1280), nparts=%d", H, nparts);
+  hipLaunchKernelGGL((k_attn_decode_cross_q<32>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, x, parts, nparts,
+                     (long)B * H * 64, bias, gamma, beta, eps, (const bf16_t*)wq, bq, x_out, S, Bt, row_map,
+                     (const bf16_t*)cross_kv, (bf16_t*)out);
+  return tw_check_launch("tw_attn_decode_cross_q");
+}
+
 // k_attn_decode_cross_grp: the lean kernel for G rows that read the SAME encoder slot (the beams of one window): each
 // key/value row is loaded once for all G queries (num_beams x less cross K/V traffic: the beam-5 step's largest
 // kernel streamed 60 x 20 x 384 KB per layer for 12 distinct windows). One group per block would leave most CUs idle

@@ -166,16 +166,18 @@ extern "C" int tw_embed_decoder(const bf16_t* tok_emb, const bf16_t* pos_emb, co
 #define RLN_MAXV 4  // float4 chunks per thread: D <= 4096
 // All loads are unconditional (index clamped into the row, result discarded): a guarded load per
 // element makes hipcc wait vmcnt(0) per element, a chain of L2 round trips.
+// (x_out: where the updated row goes; x itself for the in-place form)
 template <bool PACKED>
-__global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const float* __restrict__ parts, int nparts,
+__global__ __launch_bounds__(256) void k_resid_ln(const float* x, const float* __restrict__ parts, int nparts,
                                                   long part_stride, const float* __restrict__ bias,
                                                   const float* __restrict__ g, const float* __restrict__ bta, int D,
-                                                  float eps, bf16_t* __restrict__ out) {
+                                                  float eps, bf16_t* __restrict__ out, float* x_out) {
   TW_DEC_PRIO();
   __shared__ float red[8];
   const int row = blockIdx.x, tid = threadIdx.x;
   const int nc = D >> 2;
-  float* xr = x + (size_t)row * D;
+  const float* xr = x + (size_t)row * D;
+  float* xo = x_out + (size_t)row * D;
   const float* pr = parts ? parts + (size_t)row * D : nullptr;
   float4 v[RLN_MAXV];
   float s = 0.f;
@@ -202,10 +204,10 @@ __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const f
     v[i] = a;
     if (tid + 256 * i < nc) s += (a.x + a.y) + (a.z + a.w);
   }
-  if (nparts > 0 || bias) {
+  if (nparts > 0 || bias || x_out != x) {
 #pragma unroll
     for (int i = 0; i < RLN_MAXV; ++i)
-      if (tid + 256 * i < nc) ((float4*)xr)[tid + 256 * i] = v[i];
+      if (tid + 256 * i < nc) ((float4*)xo)[tid + 256 * i] = v[i];
   }
   if (!g) return;
   tw_row_ln_store<PACKED>(v, s, row, D, eps, g, bta, out, red);
@@ -217,13 +219,14 @@ __global__ __launch_bounds__(256) void k_resid_ln(float* __restrict__ x, const f
 // barrier-separated reductions.
 // (min 4 waves per SIMD: <= 128 VGPRs, so a wave fits beside an encoder GEMM workgroup's two ~190-VGPR waves)
 template <bool PACKED, int NV>
-__global__ TW_DEC_LB(64, 4) void k_resid_ln_w(float* __restrict__ x, const float* __restrict__ parts, int nparts,
+__global__ TW_DEC_LB(64, 4) void k_resid_ln_w(const float* x, const float* __restrict__ parts, int nparts,
                                                    long part_stride, const float* __restrict__ bias,
                                                    const float* __restrict__ g, const float* __restrict__ bta, int D,
-                                                   float eps, bf16_t* __restrict__ out) {
+                                                   float eps, bf16_t* __restrict__ out, float* x_out) {
   TW_DEC_PRIO();
   const int row = blockIdx.x, lane = threadIdx.x;
-  float* xr = x + (size_t)row * D;
+  const float* xr = x + (size_t)row * D;
+  float* xo = x_out + (size_t)row * D;
   const float* pr = parts ? parts + (size_t)row * D : nullptr;
   float4 gg[NV], bb[NV];
   // the row, the bias and up to four partials: every load in flight before the first add (one memory round trip;
@@ -273,9 +276,9 @@ __global__ TW_DEC_LB(64, 4) void k_resid_ln_w(float* __restrict__ x, const float
       bb[i] = ((const float4*)bta)[lane + 64 * i];
     }
   }
-  if (nparts > 0 || bias) {
+  if (nparts > 0 || bias || x_out != x) {
 #pragma unroll
-    for (int i = 0; i < NV; ++i) ((float4*)xr)[lane + 64 * i] = v[i];
+    for (int i = 0; i < NV; ++i) ((float4*)xo)[lane + 64 * i] = v[i];
   }
   if (!g) return;
   float s = 0.f;
@@ -312,24 +315,36 @@ extern "C" int tw_resid_layernorm(float* x, const float* parts, int nparts, cons
   TW_REQUIRE(!gamma || (beta && out), "tw_resid_layernorm: gamma without beta/out");
   if (D == 1280)
     hipLaunchKernelGGL((k_resid_ln_w<false, 5>), dim3(M), dim3(64), 0, (hipStream_t)stream, x, parts, nparts,
-                       (long)M * D, bias, gamma, beta, D, eps, out);
+                       (long)M * D, bias, gamma, beta, D, eps, out, x);
   else
     hipLaunchKernelGGL(k_resid_ln<false>, dim3(M), dim3(256), 0, (hipStream_t)stream, x, parts, nparts, (long)M * D,
-                       bias, gamma, beta, D, eps, out);
+                       bias, gamma, beta, D, eps, out, x);
   return tw_check_launch("tw_resid_layernorm");
+}
+
+static int resid_ln_packed(const float* x, float* x_out, const float* parts, int nparts, const float* bias,
+                           const float* gamma, const float* beta, int M, int D, float eps, uint16_t* out,
+                           void* stream) {
+  TW_REQUIRE(x && x_out && gamma && beta && out && M > 0 && M <= 64 && D > 0 && D % 32 == 0 && D <= 1024 * RLN_MAXV,
+             "tw_resid_layernorm_packed: bad args (M <= 64, D %% 32, gamma/beta/out required)");
+  TW_REQUIRE(nparts >= 0 && (nparts == 0 || parts), "tw_resid_layernorm_packed: parts");
+  if (D == 1280)
+    hipLaunchKernelGGL((k_resid_ln_w<true, 5>), dim3(M), dim3(64), 0, (hipStream_t)stream, x, parts, nparts,
+                       (long)M * D, bias, gamma, beta, D, eps, out, x_out);
+  else
+    hipLaunchKernelGGL(k_resid_ln<true>, dim3(M), dim3(256), 0, (hipStream_t)stream, x, parts, nparts, (long)M * D,
+                       bias, gamma, beta, D, eps, out, x_out);
+  return tw_check_launch("tw_resid_layernorm_packed");
 }
 
 extern "C" int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias,
                                          const float* gamma, const float* beta, int M, int D, float eps, uint16_t* out,
                                          void* stream) {
-  TW_REQUIRE(x && gamma && beta && out && M > 0 && M <= 64 && D > 0 && D % 32 == 0 && D <= 1024 * RLN_MAXV,
-             "tw_resid_layernorm_packed: bad args (M <= 64, D %% 32, gamma/beta/out required)");
-  TW_REQUIRE(nparts >= 0 && (nparts == 0 || parts), "tw_resid_layernorm_packed: parts");
-  if (D == 1280)
-    hipLaunchKernelGGL((k_resid_ln_w<true, 5>), dim3(M), dim3(64), 0, (hipStream_t)stream, x, parts, nparts,
-                       (long)M * D, bias, gamma, beta, D, eps, out);
-  else
-    hipLaunchKernelGGL(k_resid_ln<true>, dim3(M), dim3(256), 0, (hipStream_t)stream, x, parts, nparts, (long)M * D,
-                       bias, gamma, beta, D, eps, out);
-  return tw_check_launch("tw_resid_layernorm_packed");
+  return resid_ln_packed(x, x, parts, nparts, bias, gamma, beta, M, D, eps, out, stream);
+}
+
+extern "C" int tw_resid_layernorm_packed_to(const float* x, float* x_out, const float* parts, int nparts,
+                                            const float* bias, const float* gamma, const float* beta, int M, int D,
+                                            float eps, uint16_t* out, void* stream) {
+  return resid_ln_packed(x, x_out, parts, nparts, bias, gamma, beta, M, D, eps, out, stream);
 }

@@ -71,6 +71,7 @@ class DecView:
     n: int
     stream: torch.cuda.Stream
     xd: torch.Tensor
+    xd2: torch.Tensor  # the residual rows between the fused cross-attention and the next LayerNorm (cross_q)
     qkvd: torch.Tensor
     qd: torch.Tensor
     attd: torch.Tensor
@@ -217,6 +218,7 @@ class WhisperEngine:
         self.kcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=bf, device=dev)
         self.vcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=bf, device=dev)
         self.xd = torch.empty(B, D, dtype=f32, device=dev)
+        self.xd2 = torch.empty(B, D, dtype=f32, device=dev)
         self.qkvd = torch.empty(B, 3 * D, dtype=bf, device=dev)
         self.qd = torch.empty(B, D, dtype=bf, device=dev)
         self.attd = torch.empty(B, D, dtype=bf, device=dev)
@@ -258,6 +260,10 @@ class WhisperEngine:
         self.fused_select = True
         # the prompt phase of a decode pass replayed as one captured graph (False: eager)
         self.prompt_graph = True
+        # the cross-attention block's residual add + LayerNorm + q projection folded into the cross-attention launch
+        # (tw_attn_decode_cross_q: 39 launches per token instead of 47); not with word timestamps (the probability-
+        # recording kernel) or grouped beam rows, which keep the separate launches. False: the separate launches
+        self.fuse_cross_q = True
         # encoder attention kernel (tw_attn_set_variant) and its LDS cap in 16 KiB units (tw_attn_set_lds_pad) for an
         # encoder chunk alone / beside a running decode
         self.attn_kernel = (32, 32)  # k_attn_enc5 (round 4; 16 = k_attn_enc4, bit-identical to the enc2 form)
@@ -403,7 +409,7 @@ class WhisperEngine:
         # per-view packed scratch (rows 0..n-1 of the view; pad rows zero)
         hp = torch.zeros(VIEW_ROWS * self.d.d_model, dtype=torch.bfloat16, device=self.device)
         fp = torch.zeros(VIEW_ROWS * self.d.ffn, dtype=torch.bfloat16, device=self.device)
-        return DecView(r0, n, stream or self.stream, self.xd[sl], self.qkvd[sl], self.qd[sl], self.attd[sl],
+        return DecView(r0, n, stream or self.stream, self.xd[sl], self.xd2[sl], self.qkvd[sl], self.qd[sl], self.attd[sl],
                        self.logits[sl], self.parts if parts is None else parts, self.sel_ws[sl], self.state[sl],
                        self.tokens[sl], self.ids[sl], self.pos[sl], hp, fp)
 
@@ -554,6 +560,7 @@ class WhisperEngine:
                       D, v.xd.data_ptr(), s)
         xkv_stride = 2 * r_enc * H * S_ENC * 64
         nparts, pbias = 0, None
+        fuse = self.fuse_cross_q and self._align is None and not (self._row_group > 1 and self._use_dec_row_map)
         PART, K4 = _lib.TW_EPI_PARTIAL_F32, DEC_SPLITS
         for li, L in enumerate(w.dec):
             P = self.dec_p[li]
@@ -568,14 +575,24 @@ class WhisperEngine:
                 _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
                           self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
             self._gemv(v.attd, False, P["wo"], R, D, D, PART, v.parts, v, splits=K4)
-            self._resid_ln_p(R, K4, L.bo, L.ln2_g, L.ln2_b, v)
-            self._gemv(v.hp, True, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
             ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
-            rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
-            self._cross_attend(li, R, r_enc, rmap, ckv, v)
-            self._end_timer(rec, st)
-            self._gemv(v.attd, False, P["wo_x"], R, D, D, PART, v.parts, v, splits=K4)
-            self._resid_ln_p(R, K4, L.bo_x, L.ln3_g, L.ln3_b, v)
+            if fuse:  # residual + encoder_attn_layer_norm + q_proj + attention in one launch; residual -> xd2
+                rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)
+                _lib.call("tw_attn_decode_cross_q", v.xd.data_ptr(), v.parts.data_ptr(), K4, L.bo.data_ptr(),
+                          L.ln2_g.data_ptr(), L.ln2_b.data_ptr(), LN_EPS, L.wq_x.data_ptr(), L.bq_x.data_ptr(),
+                          v.xd2.data_ptr(), R, H, S_ENC, r_enc, rmap, ckv, v.attd.data_ptr(), s)
+                self._end_timer(rec, st)
+                self._gemv(v.attd, False, P["wo_x"], R, D, D, PART, v.parts, v, splits=K4)
+                _lib.call("tw_resid_layernorm_packed_to", v.xd2.data_ptr(), v.xd.data_ptr(), v.parts.data_ptr(), K4,
+                          L.bo_x.data_ptr(), L.ln3_g.data_ptr(), L.ln3_b.data_ptr(), R, D, LN_EPS, v.hp.data_ptr(), s)
+            else:
+                self._resid_ln_p(R, K4, L.bo, L.ln2_g, L.ln2_b, v)
+                self._gemv(v.hp, True, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
+                rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
+                self._cross_attend(li, R, r_enc, rmap, ckv, v)
+                self._end_timer(rec, st)
+                self._gemv(v.attd, False, P["wo_x"], R, D, D, PART, v.parts, v, splits=K4)
+                self._resid_ln_p(R, K4, L.bo_x, L.ln3_g, L.ln3_b, v)
             self._gemv(v.hp, True, P["w1"], R, F, D, _lib.TW_EPI_GELU_PACKED, v.fp, v, bias=L.b1)
             self._gemv(v.fp, True, P["w2"], R, D, F, PART, v.parts, v, splits=K4)
             nparts, pbias = K4, L.b2
