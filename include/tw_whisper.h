@@ -235,6 +235,17 @@ int tw_resid_layernorm_packed_to(const float* x, float* x_out, const float* part
  * Replaces the causal self-attention + DynamicCache.update of modeling_whisper.py:312-335,448-505. */
 int tw_attn_decode_self(const uint16_t* qkv, int B, int H, int max_pos, const int* pos, uint16_t* k_cache,
                         uint16_t* v_cache, uint16_t* out, void* stream);
+/* tw_attn_decode_self with the two steps before it folded in (one launch instead of three): row b's residual update
+ * and self_attn_layer_norm, x_out[b] = x[b] + bias + sum_{p < nparts} parts[p][b] (bias may be NULL, nparts 0: the
+ * embedding itself) and LN = bf16(LayerNorm(x_out[b]) * gamma + beta), then the head's q / k / v rows
+ * bf16(LN . wqkv[s D + 64 h + i][:]^T + bqkv[..]) (wqkv bf16 [3 D][D] row-major, q rows pre-scaled by 64^-0.5), then
+ * the cache append at pos[b] and the attention of tw_attn_decode_self. D = 64 H <= 1280; x_out must not alias x.
+ * Replaces the residual add + LayerNorm + q/k/v projections of WhisperDecoderLayer.forward's self-attention block
+ * ($TF/models/whisper/modeling_whisper.py:468-482, 279-282). */
+int tw_attn_decode_self_q(const float* x, const float* parts, int nparts, const float* bias, const float* gamma,
+                          const float* beta, float eps, const uint16_t* wqkv, const float* bqkv, float* x_out, int B,
+                          int H, int max_pos, const int* pos, uint16_t* k_cache, uint16_t* v_cache, uint16_t* out,
+                          void* stream);
 /* The same with beam search's copy-free K/V history: position q < pos[b] of row b is read from cache row
  * kv_tab[(row0 + b) * max_pos + q] (a global row: k_cache / v_cache point at row row0 of the layer's caches, which
  * hold rows_cap rows); the step's own K/V is written to row b at pos[b], and kv_tab[(row0 + b) * max_pos + pos[b]]

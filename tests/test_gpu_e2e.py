@@ -400,11 +400,11 @@ def test_pipeline_sweep_matches_transformers(oracle):
     print("sweep:", summary)
 
 
-def test_fused_cross_q_decoder_step_vs_separate_launches(tr):
-    """The decoder step with the cross-attention block's residual + LayerNorm + q projection folded into the
-    attention launch (WhisperEngine.fuse_cross_q, tw_attn_decode_cross_q: 39 launches per token) against the separate
-    launches (47): teacher-forced logits within 0.02 (the LayerNorm's reductions and the q dot products run in another
-    order; bf16 rounding of q otherwise the same) and the same greedy decode of three clips up to a near-tie."""
+def test_fused_prologues_decoder_step_vs_separate_launches(tr):
+    """The decoder step with both attention blocks' residual + LayerNorm + projections folded into the attention
+    launches (WhisperEngine.fuse_self_q / fuse_cross_q: tw_attn_decode_self_q, tw_attn_decode_cross_q; 31 launches
+    per token) against the separate launches (47): teacher-forced logits within 0.02 (the LayerNorms' reductions and
+    the projections' dot products run in another order; the bf16 roundings otherwise the same)."""
     eng = tr.engine
     _load(tr, [speech_like(30.0, 21), white_noise(30.0, 5), speech_like(17.0, 8)])
     eng.row_map[:3] = torch.arange(3, dtype=torch.int32)
@@ -413,7 +413,7 @@ def test_fused_cross_q_decoder_step_vs_separate_launches(tr):
     ids = [50258, 50259, 50360, 50365, 400, 1200, 50390, 50391, 77, 9000]
     lg = {}
     for fuse in (True, False):
-        eng.fuse_cross_q = fuse
+        eng.fuse_cross_q = eng.fuse_self_q = fuse
         rows = []
         for t, tok in enumerate(ids):
             eng.ids[:3] = tok
@@ -421,7 +421,7 @@ def test_fused_cross_q_decoder_step_vs_separate_launches(tr):
             eng.decoder_step(3)
             rows.append(eng.logits[:3].float().cpu())
         lg[fuse] = torch.stack(rows)
-    eng.fuse_cross_q = True
+    eng.fuse_cross_q = eng.fuse_self_q = True
     d = (lg[True] - lg[False]).abs().max().item()
-    print(f"fused cross-q vs separate launches: teacher-forced logits max |d| {d:.2e}")
+    print(f"fused self/cross prologues vs separate launches: teacher-forced logits max |d| {d:.2e}")
     assert d <= 0.02

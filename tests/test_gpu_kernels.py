@@ -661,3 +661,67 @@ def test_resid_layernorm_packed_to_writes_the_other_buffer():
               b.data_ptr(), M, D, 1e-5, out2.data_ptr(), S())
     torch.cuda.synchronize()
     assert torch.equal(x, x0) and torch.equal(xo, x2) and torch.equal(out1, out2)
+
+
+@pytest.mark.parametrize("B,H,nparts,t_max", [(24, 20, 4, 200), (5, 6, 0, 40), (64, 20, 4, 300), (3, 20, 4, 1)])
+def test_attn_decode_self_q_vs_separate_launches(B, H, nparts, t_max):
+    """tw_attn_decode_self_q (residual + LayerNorm + the head's q/k/v projection + the self-attention step in one
+    launch) against the three launches it replaces (tw_resid_layernorm_packed, the q/k/v GEMV, tw_attn_decode_self):
+    the residual rows bit-identical, the appended K/V within one bf16 ulp of the GEMV's (the dot products run in
+    another order), the attention output no further from fp32 than the separate launches' (within 2e-2 or 1.5x theirs).
+    Histories of 1 to 300 positions: both the one-round-trip and the two-pass paths."""
+    D, T = H * 64, 448
+    g = torch.Generator(device="cpu").manual_seed(B * 10 + H + t_max)
+    x = (torch.randn(B, D, generator=g) * 2 + 0.3).to(DEV)
+    parts = torch.randn(max(nparts, 1), B, D, generator=g).to(DEV)
+    bias = (torch.randn(D, generator=g) * 0.1).to(DEV) if nparts else None
+    gam = (torch.rand(D, generator=g) + 0.5).to(DEV)
+    bet = (torch.randn(D, generator=g) * 0.1).to(DEV)
+    wqkv = rand_bf16(3 * D, D, scale=D ** -0.5, seed=B + H)
+    bqkv = (torch.randn(3 * D, generator=g) * 0.05).to(DEV)
+    pos = torch.randint(max(0, t_max - 20), t_max, (B,), generator=g, dtype=torch.int32).to(DEV)
+    kc = rand_bf16(B, H, T, 64, seed=H + 5)
+    vc = rand_bf16(B, H, T, 64, seed=H + 6)
+    kc2, vc2 = kc.clone(), vc.clone()
+    x_out = torch.full_like(x, float("nan"))
+    out = torch.empty(B, D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_attn_decode_self_q", x.data_ptr(), parts.data_ptr() if nparts else None, nparts, _lib.ptr(bias),
+              gam.data_ptr(), bet.data_ptr(), 1e-5, wqkv.data_ptr(), bqkv.data_ptr(), x_out.data_ptr(), B, H, T,
+              pos.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(), S())
+    x2 = x.clone()
+    hp = torch.zeros(D * 64, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_resid_layernorm_packed", x2.data_ptr(), parts.data_ptr(), nparts, _lib.ptr(bias), gam.data_ptr(),
+              bet.data_ptr(), B, D, 1e-5, hp.data_ptr(), S())
+    qkv = torch.empty(B, 3 * D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_gemv_packed", hp.data_ptr(), 1, D, pack_w(wqkv).data_ptr(), B, 3 * D, D, _lib.TW_EPI_BF16,
+              qkv.data_ptr(), 3 * D, bqkv.data_ptr(), 1, S())
+    out2 = torch.empty_like(out)
+    _lib.call("tw_attn_decode_self", qkv.data_ptr(), B, H, T, pos.data_ptr(), kc2.data_ptr(), vc2.data_ptr(),
+              out2.data_ptr(), S())
+    torch.cuda.synchronize()
+    assert torch.equal(x_out, x2)
+    rows = torch.arange(B, device=DEV)
+    pl = pos.long()
+    for cache, cache2, off in ((kc, kc2, D), (vc, vc2, 2 * D)):
+        a = cache[rows, :, pl].float()
+        b2 = cache2[rows, :, pl].float()
+        ulp = torch.maximum(a.abs(), b2.abs()).clamp_min(1e-3) * 2.0 ** -7
+        assert bool(((a - b2).abs() <= ulp).all())  # one bf16 ulp at most
+        keep = torch.ones(T, dtype=torch.bool, device=DEV)
+        for r in range(B):  # positions other than pos untouched by both
+            keep[:] = True
+            keep[pl[r]] = False
+            assert torch.equal(cache[r][:, keep], cache2[r][:, keep])
+    # fp32 reference over the appended caches (the fused kernel's own k/v)
+    ef = es = 0.0
+    xr = x + ((bias + parts[:nparts].sum(0)) if nparts else 0)
+    ln = torch.nn.functional.layer_norm(xr, (D,), gam, bet, 1e-5)
+    q = (ln @ wqkv.float().t() + bqkv)[:, :D]
+    for r in range(B):
+        n = int(pos[r]) + 1
+        ref = _ref_attn(q[r].view(H, 1, 64), kc[r, :, :n].float(), vc[r, :, :n].float())[:, 0].reshape(D)
+        ef = max(ef, (out[r].float() - ref).abs().max().item())
+        ref2 = _ref_attn(q[r].view(H, 1, 64), kc2[r, :, :n].float(), vc2[r, :, :n].float())[:, 0].reshape(D)
+        es = max(es, (out2[r].float() - ref2).abs().max().item())
+    print(f"self_q vs fp32: fused {ef:.3e}, separate launches {es:.3e}")
+    assert ef <= max(2e-2, 1.5 * es)

@@ -261,9 +261,13 @@ class WhisperEngine:
         # the prompt phase of a decode pass replayed as one captured graph (False: eager)
         self.prompt_graph = True
         # the cross-attention block's residual add + LayerNorm + q projection folded into the cross-attention launch
-        # (tw_attn_decode_cross_q: 39 launches per token instead of 47); not with word timestamps (the probability-
-        # recording kernel) or grouped beam rows, which keep the separate launches. False: the separate launches
+        # (tw_attn_decode_cross_q); not with word timestamps (the probability-recording kernel) or grouped beam rows,
+        # which keep the separate launches. False: the separate launches
         self.fuse_cross_q = True
+        # the self-attention block's residual add + LayerNorm + q/k/v projection folded into the self-attention launch
+        # (tw_attn_decode_self_q); not for beam rows (histories through the position table). With both: 31 launches per
+        # token instead of 47
+        self.fuse_self_q = True
         # encoder attention kernel (tw_attn_set_variant) and its LDS cap in 16 KiB units (tw_attn_set_lds_pad) for an
         # encoder chunk alone / beside a running decode
         self.attn_kernel = (32, 32)  # k_attn_enc5 (round 4; 16 = k_attn_enc4, bit-identical to the enc2 form)
@@ -312,6 +316,12 @@ class WhisperEngine:
         _lib.call("tw_gemv_packed", A.data_ptr(), int(a_packed), K, Wp.data_ptr(), M, N, K, epi, out.data_ptr(),
                   ldo if ldo is not None else N, _lib.ptr(bias), splits, v.stream.cuda_stream)
         self._end_timer(rec, v.stream)
+
+    def _resid_ln_to(self, x, x_out, nparts, bias, g, b, v: DecView):
+        """x_out = x + bias + sum(parts[:nparts]) (x_out may be x); hp = LayerNorm(x_out) as a packed activation."""
+        _lib.call("tw_resid_layernorm_packed_to", x.data_ptr(), x_out.data_ptr(), v.parts.data_ptr() if nparts else None,
+                  nparts, _lib.ptr(bias), _lib.ptr(g), _lib.ptr(b), v.n, self.d.d_model, LN_EPS, v.hp.data_ptr(),
+                  v.stream.cuda_stream)
 
     def _resid_ln_p(self, R, nparts, bias, g, b, v: DecView):
         """xd += bias + sum(parts[:nparts]); hp = LayerNorm(xd) as a packed activation."""
@@ -561,43 +571,51 @@ class WhisperEngine:
         xkv_stride = 2 * r_enc * H * S_ENC * 64
         nparts, pbias = 0, None
         fuse = self.fuse_cross_q and self._align is None and not (self._row_group > 1 and self._use_dec_row_map)
+        fuse_self = self.fuse_self_q and self._kv_tab is None
         PART, K4 = _lib.TW_EPI_PARTIAL_F32, DEC_SPLITS
+        # the residual rows: xd holds them at the step's start (the embedding); a fused launch reads them from one
+        # buffer and writes the updated rows to the other (its other blocks still read them), so they alternate
+        x, xo = v.xd, v.xd2
         for li, L in enumerate(w.dec):
             P = self.dec_p[li]
-            if li or not pre_embedded:
-                self._resid_ln_p(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
-            self._gemv(v.hp, True, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
-            if self._kv_tab is not None:  # beam pass: histories through the position table
-                _lib.call("tw_attn_decode_self_tab", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
-                          self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), self._kv_tab.data_ptr(),
-                          v.r0, v.attd.data_ptr(), s)
+            kc, vc = self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr()
+            if fuse_self:  # residual + self_attn_layer_norm + q/k/v projection + attention in one launch
+                _lib.call("tw_attn_decode_self_q", x.data_ptr(), v.parts.data_ptr() if nparts else None, nparts,
+                          _lib.ptr(pbias), L.ln1_g.data_ptr(), L.ln1_b.data_ptr(), LN_EPS, L.wqkv.data_ptr(),
+                          L.bqkv.data_ptr(), xo.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc, v.attd.data_ptr(), s)
+                x, xo = xo, x
             else:
-                _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(),
-                          self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr(), v.attd.data_ptr(), s)
+                if li or not pre_embedded:
+                    self._resid_ln_to(x, x, nparts, pbias, L.ln1_g, L.ln1_b, v)
+                self._gemv(v.hp, True, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
+                if self._kv_tab is not None:  # beam pass: histories through the position table
+                    _lib.call("tw_attn_decode_self_tab", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc,
+                              self._kv_tab.data_ptr(), v.r0, v.attd.data_ptr(), s)
+                else:
+                    _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc,
+                              v.attd.data_ptr(), s)
             self._gemv(v.attd, False, P["wo"], R, D, D, PART, v.parts, v, splits=K4)
             ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
-            if fuse:  # residual + encoder_attn_layer_norm + q_proj + attention in one launch; residual -> xd2
+            if fuse:  # residual + encoder_attn_layer_norm + q_proj + attention in one launch
                 rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)
-                _lib.call("tw_attn_decode_cross_q", v.xd.data_ptr(), v.parts.data_ptr(), K4, L.bo.data_ptr(),
+                _lib.call("tw_attn_decode_cross_q", x.data_ptr(), v.parts.data_ptr(), K4, L.bo.data_ptr(),
                           L.ln2_g.data_ptr(), L.ln2_b.data_ptr(), LN_EPS, L.wq_x.data_ptr(), L.bq_x.data_ptr(),
-                          v.xd2.data_ptr(), R, H, S_ENC, r_enc, rmap, ckv, v.attd.data_ptr(), s)
+                          xo.data_ptr(), R, H, S_ENC, r_enc, rmap, ckv, v.attd.data_ptr(), s)
                 self._end_timer(rec, st)
-                self._gemv(v.attd, False, P["wo_x"], R, D, D, PART, v.parts, v, splits=K4)
-                _lib.call("tw_resid_layernorm_packed_to", v.xd2.data_ptr(), v.xd.data_ptr(), v.parts.data_ptr(), K4,
-                          L.bo_x.data_ptr(), L.ln3_g.data_ptr(), L.ln3_b.data_ptr(), R, D, LN_EPS, v.hp.data_ptr(), s)
+                x, xo = xo, x
             else:
-                self._resid_ln_p(R, K4, L.bo, L.ln2_g, L.ln2_b, v)
+                self._resid_ln_to(x, x, K4, L.bo, L.ln2_g, L.ln2_b, v)
                 self._gemv(v.hp, True, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
                 rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
                 self._cross_attend(li, R, r_enc, rmap, ckv, v)
                 self._end_timer(rec, st)
-                self._gemv(v.attd, False, P["wo_x"], R, D, D, PART, v.parts, v, splits=K4)
-                self._resid_ln_p(R, K4, L.bo_x, L.ln3_g, L.ln3_b, v)
+            self._gemv(v.attd, False, P["wo_x"], R, D, D, PART, v.parts, v, splits=K4)
+            self._resid_ln_to(x, x, K4, L.bo_x, L.ln3_g, L.ln3_b, v)
             self._gemv(v.hp, True, P["w1"], R, F, D, _lib.TW_EPI_GELU_PACKED, v.fp, v, bias=L.b1)
             self._gemv(v.fp, True, P["w2"], R, D, F, PART, v.parts, v, splits=K4)
             nparts, pbias = K4, L.b2
         if with_logits:
-            self._resid_ln_p(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
+            self._resid_ln_to(x, x, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
             self._gemv(v.hp, True, self.emb_p, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, v)
 
     def _cross_attend(self, li: int, R: int, r_enc: int, rmap, ckv, v: DecView) -> None:
