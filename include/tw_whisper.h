@@ -246,6 +246,12 @@ int tw_attn_decode_self_q(const float* x, const float* parts, int nparts, const 
                           const float* beta, float eps, const uint16_t* wqkv, const float* bqkv, float* x_out, int B,
                           int H, int max_pos, const int* pos, uint16_t* k_cache, uint16_t* v_cache, uint16_t* out,
                           void* stream);
+/* The same for beam rows: histories through the position table kv_tab with view offset row0, under
+ * tw_attn_decode_self_tab's contract (checked in a TW_DEBUG build). */
+int tw_attn_decode_self_q_tab(const float* x, const float* parts, int nparts, const float* bias, const float* gamma,
+                              const float* beta, float eps, const uint16_t* wqkv, const float* bqkv, float* x_out,
+                              int B, int H, int max_pos, const int* pos, uint16_t* k_cache, uint16_t* v_cache,
+                              const int* kv_tab, int row0, uint16_t* out, void* stream);
 /* The same with beam search's copy-free K/V history: position q < pos[b] of row b is read from cache row
  * kv_tab[(row0 + b) * max_pos + q] (a global row: k_cache / v_cache point at row row0 of the layer's caches, which
  * hold rows_cap rows); the step's own K/V is written to row b at pos[b], and kv_tab[(row0 + b) * max_pos + pos[b]]

@@ -1113,15 +1113,17 @@ __device__ __attribute__((always_inline)) inline void dec_ln_proj(const bf16_t* 
 // k_attn_decode_cross_q does for the cross-attention): row b's residual update + self_attn_layer_norm (dec_row_ln;
 // the updated row written to x_out by head 0's block) and this head's 192 rows of the q/k/v projection
 // (dec_ln_proj<3>: 480 KB of wqkv per block from L2 / Infinity Cache, twelve double-buffered rounds), rounded to bf16
-// as the q/k/v GEMV stores them; then self2_step on that LDS row (the cache append and the attention). Greedy rows
-// only (no position table). Saves two launches per decoder layer.
+// as the q/k/v GEMV stores them; then self2_step on that LDS row (the cache append and the attention; TAB: beam rows,
+// histories through the position table as tw_attn_decode_self_tab). Saves two launches per decoder layer.
+template <bool TAB>
 __global__ TW_DEC_LB(256, 4) void k_attn_decode_self_q(const float* __restrict__ x, const float* __restrict__ parts,
                                                        int nparts, long part_stride, const float* __restrict__ bias,
                                                        const float* __restrict__ gam, const float* __restrict__ bet,
                                                        float eps, const bf16_t* __restrict__ wqkv,
                                                        const float* __restrict__ bqkv, float* __restrict__ x_out,
                                                        int max_pos, const int* __restrict__ pos, bf16_t* __restrict__ kc,
-                                                       bf16_t* __restrict__ vc, bf16_t* __restrict__ out) {
+                                                       bf16_t* __restrict__ vc, const int* __restrict__ kv_tab, int row0,
+                                                       bf16_t* __restrict__ out) {
   TW_DEC_PRIO();
   __shared__ __attribute__((aligned(16))) float big[2048];  // the LayerNorm row
   __shared__ float outs[192];
@@ -1133,22 +1135,54 @@ __global__ TW_DEC_LB(256, 4) void k_attn_decode_self_q(const float* __restrict__
   });
   if (tid < 192) qkv_b[tid] = f32_to_bf16(outs[tid]);  // (exact: outs are bf16 values)
   __syncthreads();
-  self2_step<false>(qkv_b, 64, D, max_pos, pos, kc, vc, nullptr, 0, out);
+  self2_step<TAB>(qkv_b, 64, D, max_pos, pos, kc, vc, kv_tab, row0, out);
+}
+
+#if TW_DEBUG
+static int tw_debug_tab_guard(const int* kv_tab, const int* pos, int row0, int B, int max_pos, hipStream_t st);
+#endif
+static int self_q_launch(const float* x, const float* parts, int nparts, const float* bias, const float* gamma,
+                         const float* beta, float eps, const uint16_t* wqkv, const float* bqkv, float* x_out, int B,
+                         int H, int max_pos, const int* pos, uint16_t* k_cache, uint16_t* v_cache, const int* kv_tab,
+                         int row0, uint16_t* out, void* stream) {
+  TW_REQUIRE(x && gamma && beta && wqkv && bqkv && x_out && pos && k_cache && v_cache && out && x_out != x && B > 0 &&
+                 H > 0 && row0 >= 0,
+             "tw_attn_decode_self_q: bad args");
+  TW_REQUIRE(H * 64 <= 1280 && nparts >= 0 && nparts <= 8 && (nparts == 0 || parts) && max_pos <= DA_SELF_MAXK,
+             "tw_attn_decode_self_q: H=%d (H * 64 <= 1280), nparts=%d, max_pos=%d", H, nparts, max_pos);
+  const dim3 grid(H, B), blk(256);
+  hipStream_t st = (hipStream_t)stream;
+  if (kv_tab) {
+#if TW_DEBUG
+    if (int rc = tw_debug_tab_guard(kv_tab, pos, row0, B, max_pos, st)) return rc;
+#endif
+    hipLaunchKernelGGL(k_attn_decode_self_q<true>, grid, blk, 0, st, x, parts, nparts, (long)B * H * 64, bias, gamma,
+                       beta, eps, (const bf16_t*)wqkv, bqkv, x_out, max_pos, pos, (bf16_t*)k_cache, (bf16_t*)v_cache,
+                       kv_tab, row0, (bf16_t*)out);
+  } else {
+    hipLaunchKernelGGL(k_attn_decode_self_q<false>, grid, blk, 0, st, x, parts, nparts, (long)B * H * 64, bias, gamma,
+                       beta, eps, (const bf16_t*)wqkv, bqkv, x_out, max_pos, pos, (bf16_t*)k_cache, (bf16_t*)v_cache,
+                       nullptr, 0, (bf16_t*)out);
+  }
+  return tw_check_launch("tw_attn_decode_self_q");
 }
 
 extern "C" int tw_attn_decode_self_q(const float* x, const float* parts, int nparts, const float* bias,
                                      const float* gamma, const float* beta, float eps, const uint16_t* wqkv,
                                      const float* bqkv, float* x_out, int B, int H, int max_pos, const int* pos,
                                      uint16_t* k_cache, uint16_t* v_cache, uint16_t* out, void* stream) {
-  TW_REQUIRE(x && gamma && beta && wqkv && bqkv && x_out && pos && k_cache && v_cache && out && x_out != x && B > 0 &&
-                 H > 0,
-             "tw_attn_decode_self_q: bad args");
-  TW_REQUIRE(H * 64 <= 1280 && nparts >= 0 && nparts <= 8 && (nparts == 0 || parts) && max_pos <= DA_SELF_MAXK,
-             "tw_attn_decode_self_q: H=%d (H * 64 <= 1280), nparts=%d, max_pos=%d", H, nparts, max_pos);
-  hipLaunchKernelGGL(k_attn_decode_self_q, dim3(H, B), dim3(256), 0, (hipStream_t)stream, x, parts, nparts,
-                     (long)B * H * 64, bias, gamma, beta, eps, (const bf16_t*)wqkv, bqkv, x_out, max_pos, pos,
-                     (bf16_t*)k_cache, (bf16_t*)v_cache, (bf16_t*)out);
-  return tw_check_launch("tw_attn_decode_self_q");
+  return self_q_launch(x, parts, nparts, bias, gamma, beta, eps, wqkv, bqkv, x_out, B, H, max_pos, pos, k_cache,
+                       v_cache, nullptr, 0, out, stream);
+}
+
+extern "C" int tw_attn_decode_self_q_tab(const float* x, const float* parts, int nparts, const float* bias,
+                                         const float* gamma, const float* beta, float eps, const uint16_t* wqkv,
+                                         const float* bqkv, float* x_out, int B, int H, int max_pos, const int* pos,
+                                         uint16_t* k_cache, uint16_t* v_cache, const int* kv_tab, int row0,
+                                         uint16_t* out, void* stream) {
+  TW_REQUIRE(kv_tab, "tw_attn_decode_self_q_tab: kv_tab");
+  return self_q_launch(x, parts, nparts, bias, gamma, beta, eps, wqkv, bqkv, x_out, B, H, max_pos, pos, k_cache,
+                       v_cache, kv_tab, row0, out, stream);
 }
 
 // Self-attention step: qkv [B][3D] bf16 (q pre-scaled), appends k,v at position pos[b] into the cache

@@ -265,8 +265,8 @@ class WhisperEngine:
         # which keep the separate launches. False: the separate launches
         self.fuse_cross_q = True
         # the self-attention block's residual add + LayerNorm + q/k/v projection folded into the self-attention launch
-        # (tw_attn_decode_self_q); not for beam rows (histories through the position table). With both: 31 launches per
-        # token instead of 47
+        # (tw_attn_decode_self_q, tw_attn_decode_self_q_tab for beam rows). With both: 31 launches per token instead
+        # of 47 (beam rows keep the grouped cross-attention and its separate LayerNorm / q launches: 39)
         self.fuse_self_q = True
         # encoder attention kernel (tw_attn_set_variant) and its LDS cap in 16 KiB units (tw_attn_set_lds_pad) for an
         # encoder chunk alone / beside a running decode
@@ -571,7 +571,7 @@ class WhisperEngine:
         xkv_stride = 2 * r_enc * H * S_ENC * 64
         nparts, pbias = 0, None
         fuse = self.fuse_cross_q and self._align is None and not (self._row_group > 1 and self._use_dec_row_map)
-        fuse_self = self.fuse_self_q and self._kv_tab is None
+        fuse_self = self.fuse_self_q
         PART, K4 = _lib.TW_EPI_PARTIAL_F32, DEC_SPLITS
         # the residual rows: xd holds them at the step's start (the embedding); a fused launch reads them from one
         # buffer and writes the updated rows to the other (its other blocks still read them), so they alternate
@@ -580,9 +580,13 @@ class WhisperEngine:
             P = self.dec_p[li]
             kc, vc = self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr()
             if fuse_self:  # residual + self_attn_layer_norm + q/k/v projection + attention in one launch
-                _lib.call("tw_attn_decode_self_q", x.data_ptr(), v.parts.data_ptr() if nparts else None, nparts,
-                          _lib.ptr(pbias), L.ln1_g.data_ptr(), L.ln1_b.data_ptr(), LN_EPS, L.wqkv.data_ptr(),
-                          L.bqkv.data_ptr(), xo.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc, v.attd.data_ptr(), s)
+                args = (x.data_ptr(), v.parts.data_ptr() if nparts else None, nparts, _lib.ptr(pbias),
+                        L.ln1_g.data_ptr(), L.ln1_b.data_ptr(), LN_EPS, L.wqkv.data_ptr(), L.bqkv.data_ptr(),
+                        xo.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc)
+                if self._kv_tab is not None:  # beam pass: histories through the position table
+                    _lib.call("tw_attn_decode_self_q_tab", *args, self._kv_tab.data_ptr(), v.r0, v.attd.data_ptr(), s)
+                else:
+                    _lib.call("tw_attn_decode_self_q", *args, v.attd.data_ptr(), s)
                 x, xo = xo, x
             else:
                 if li or not pre_embedded:
