@@ -40,8 +40,10 @@ def main():
         eng.seek[:R] = 0
         eng.encode(R)
         torch.cuda.synchronize()
-        for mode in ("fused", "separate"):
-            eng.fuse_self_q = eng.fuse_cross_q = mode == "fused"
+        for mode in ("fused", "cross_only", "self_only", "separate"):
+            eng.fuse_self_q = mode in ("fused", "self_only")
+            eng.fuse_cross_q = mode in ("fused", "cross_only")
+            eng._graphs.clear()  # (captured steps are keyed by shape, not by these switches)
             eng.decode_pass(R, tail, None, 128)  # warm-up: graph captures
             torch.cuda.synchronize()
             best = 1e9
@@ -53,7 +55,7 @@ def main():
             assert all(len(t) == 128 for t in res.tokens)
             print(json.dumps({"rows": R, "mode": mode, "pass_ms": round(best * 1e3, 2),
                               "step_us": round(best * 1e6 / 130, 1),
-                              "launches_per_token": 31 if mode == "fused" else 47}), flush=True)
+                              "launches_per_token": {"fused": 31, "cross_only": 39, "self_only": 39, "separate": 47}[mode]}), flush=True)
         eng.fuse_self_q = eng.fuse_cross_q = True
 
 

@@ -268,9 +268,14 @@ class WhisperEngine:
         # (tw_attn_decode_self_q, tw_attn_decode_self_q_tab for beam rows). With both: 31 launches per token instead
         # of 47 (beam rows keep the grouped cross-attention and its separate LayerNorm / q launches: 39)
         self.fuse_self_q = True
+        # (A/B overrides for measurement runs: TW_FUSE_SELF / TW_FUSE_CROSS = 0 or 1, TW_ENC_ATTN = 16 or 32)
+        self.fuse_self_q = os.environ.get("TW_FUSE_SELF", "1" if self.fuse_self_q else "0") == "1"
+        self.fuse_cross_q = os.environ.get("TW_FUSE_CROSS", "1" if self.fuse_cross_q else "0") == "1"
         # encoder attention kernel (tw_attn_set_variant) and its LDS cap in 16 KiB units (tw_attn_set_lds_pad) for an
         # encoder chunk alone / beside a running decode
         self.attn_kernel = (32, 32)  # k_attn_enc5 (round 4; 16 = k_attn_enc4, bit-identical to the enc2 form)
+        if os.environ.get("TW_ENC_ATTN"):
+            self.attn_kernel = (int(os.environ["TW_ENC_ATTN"]),) * 2
         self.attn_pad = (0, 4)
         # run_batches encodes batch k+1 beside the decode of batch k (sequential 138.6 vs overlapped 114.5 ms per
         # bench step, round 1); False: strictly in turn
