@@ -224,8 +224,7 @@ int tw_gemv_packed(const uint16_t* A, int a_packed, int lda, const uint16_t* Wp,
 /* tw_resid_layernorm with the normalised rows written as a packed activation (M <= 64, D % 32 == 0). */
 int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
                               const float* beta, int M, int D, float eps, uint16_t* out, void* stream);
-/* The same with the updated residual rows written to x_out instead of in place (x is only read; x_out may equal x):
- * the step after tw_attn_decode_cross_q, whose residual went to a second buffer. */
+/* The same with the updated residual rows written to x_out instead of in place (x is only read; x_out may equal x). */
 int tw_resid_layernorm_packed_to(const float* x, float* x_out, const float* parts, int nparts, const float* bias,
                                  const float* gamma, const float* beta, int M, int D, float eps, uint16_t* out,
                                  void* stream);
@@ -235,23 +234,6 @@ int tw_resid_layernorm_packed_to(const float* x, float* x_out, const float* part
  * Replaces the causal self-attention + DynamicCache.update of modeling_whisper.py:312-335,448-505. */
 int tw_attn_decode_self(const uint16_t* qkv, int B, int H, int max_pos, const int* pos, uint16_t* k_cache,
                         uint16_t* v_cache, uint16_t* out, void* stream);
-/* tw_attn_decode_self with the two steps before it folded in (one launch instead of three): row b's residual update
- * and self_attn_layer_norm, x_out[b] = x[b] + bias + sum_{p < nparts} parts[p][b] (bias may be NULL, nparts 0: the
- * embedding itself) and LN = bf16(LayerNorm(x_out[b]) * gamma + beta), then the head's q / k / v rows
- * bf16(LN . wqkv[s D + 64 h + i][:]^T + bqkv[..]) (wqkv bf16 [3 D][D] row-major, q rows pre-scaled by 64^-0.5), then
- * the cache append at pos[b] and the attention of tw_attn_decode_self. D = 64 H <= 1280; x_out must not alias x.
- * Replaces the residual add + LayerNorm + q/k/v projections of WhisperDecoderLayer.forward's self-attention block
- * ($TF/models/whisper/modeling_whisper.py:468-482, 279-282). */
-int tw_attn_decode_self_q(const float* x, const float* parts, int nparts, const float* bias, const float* gamma,
-                          const float* beta, float eps, const uint16_t* wqkv, const float* bqkv, float* x_out, int B,
-                          int H, int max_pos, const int* pos, uint16_t* k_cache, uint16_t* v_cache, uint16_t* out,
-                          void* stream);
-/* The same for beam rows: histories through the position table kv_tab with view offset row0, under
- * tw_attn_decode_self_tab's contract (checked in a TW_DEBUG build). */
-int tw_attn_decode_self_q_tab(const float* x, const float* parts, int nparts, const float* bias, const float* gamma,
-                              const float* beta, float eps, const uint16_t* wqkv, const float* bqkv, float* x_out,
-                              int B, int H, int max_pos, const int* pos, uint16_t* k_cache, uint16_t* v_cache,
-                              const int* kv_tab, int row0, uint16_t* out, void* stream);
 /* The same with beam search's copy-free K/V history: position q < pos[b] of row b is read from cache row
  * kv_tab[(row0 + b) * max_pos + q] (a global row: k_cache / v_cache point at row row0 of the layer's caches, which
  * hold rows_cap rows); the step's own K/V is written to row b at pos[b], and kv_tab[(row0 + b) * max_pos + pos[b]]
@@ -273,17 +255,6 @@ int tw_debug_build(void);
  * cross_kv bf16[2][Bt][H][S][64]; row b reads slot row_map[b] (NULL = b). */
 int tw_attn_decode_cross(const uint16_t* q, int B, int H, int S, int Bt, const int* row_map, const uint16_t* cross_kv,
                          uint16_t* out, void* stream);
-/* tw_attn_decode_cross with the two steps before it folded in (one launch instead of three): row b's residual
- * update and encoder_attn_layer_norm, x_out[b] = x[b] + bias + sum_{p < nparts} parts[p][b] (parts f32[nparts][B][D],
- * D = 64 H <= 1280) and LN = bf16(LayerNorm(x_out[b]) * gamma + beta), then the head's query
- * q = bf16(LN . wq[64 h .. 64 h + 63][:]^T + bq) (wq bf16 [D][D] row-major = nn.Linear, q already scaled by 64^-0.5
- * as the decoder's q_proj weights are), then the attention of tw_attn_decode_cross. x_out must not alias x.
- * Replaces the residual add + LayerNorm + q_proj of WhisperDecoderLayer.forward's cross-attention block
- * ($TF/models/whisper/modeling_whisper.py:486-496, 279-282). */
-int tw_attn_decode_cross_q(const float* x, const float* parts, int nparts, const float* bias, const float* gamma,
-                           const float* beta, float eps, const uint16_t* wq, const float* bq, float* x_out, int B,
-                           int H, int S, int Bt, const int* row_map, const uint16_t* cross_kv, uint16_t* out,
-                           void* stream);
 /* The same for rows that share an encoder slot in groups (the beams of one window, rows w * num_beams + j): the first
  * `first` rows (0 <= first < group, the tail of a group that began before this view) form one group, then every
  * `group` rows (2..8) one group; all rows of a group must hold the same row_map entry (required, not checked). Each

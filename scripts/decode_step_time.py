@@ -1,6 +1,5 @@
 """Measurement (not a bench line): the greedy decode pass alone (no encoder beside it) at large-v3-turbo dims, per
-decoder step, with the fused attention prologues (tw_attn_decode_self_q / tw_attn_decode_cross_q: 31 launches per
-token) and with the separate launches (47), for several row counts. One pass = the prompt graph (SOT, language
+decoder step (47 launches per token), for several row counts. One pass = the prompt graph (SOT, language
 detection, task token) + 128 generated tokens with EOS suppressed, i.e. 130 decoder steps; the encoder runs once
 before, untimed. Prints one JSON line per (rows, mode).
 
@@ -40,10 +39,8 @@ def main():
         eng.seek[:R] = 0
         eng.encode(R)
         torch.cuda.synchronize()
-        for mode in ("fused", "cross_only", "self_only", "separate"):
-            eng.fuse_self_q = mode in ("fused", "self_only")
-            eng.fuse_cross_q = mode in ("fused", "cross_only")
-            eng._graphs.clear()  # (captured steps are keyed by shape, not by these switches)
+        for mode in ("separate",):
+            eng._graphs.clear()
             eng.decode_pass(R, tail, None, 128)  # warm-up: graph captures
             torch.cuda.synchronize()
             best = 1e9
@@ -54,9 +51,7 @@ def main():
                 best = min(best, time.perf_counter() - t0)
             assert all(len(t) == 128 for t in res.tokens)
             print(json.dumps({"rows": R, "mode": mode, "pass_ms": round(best * 1e3, 2),
-                              "step_us": round(best * 1e6 / 130, 1),
-                              "launches_per_token": {"fused": 31, "cross_only": 39, "self_only": 39, "separate": 47}[mode]}), flush=True)
-        eng.fuse_self_q = eng.fuse_cross_q = True
+                              "step_us": round(best * 1e6 / 130, 1)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -381,59 +381,3 @@ def test_kv_reorder_row_limit():
         assert (rc == 0) == ok, (R, rc)
         if ok:
             assert torch.equal(k[:, :, :, :3], k0[:, src.long(), :, :3])
-
-
-def test_fused_self_q_tab_vs_separate_launches():
-    """tw_attn_decode_self_q_tab (beam rows: residual + LayerNorm + q/k/v projection + the table-addressed
-    self-attention in one launch) against tw_resid_layernorm_packed + the q/k/v GEMV + tw_attn_decode_self_tab on a
-    beam-shaped table (12 windows x 5 beams at a shared position per window, sources among the window's beams, a view
-    offset): residual rows bit-identical, appended K/V within one bf16 ulp, outputs within 4e-2 of each other (q/k/v
-    may round one bf16 ulp apart; tests/test_gpu_kernels.py bounds the same kernel against fp32)."""
-    from test_gpu_kernels import pack_w
-
-    H, T, nb, W = 20, 448, 5, 12
-    R, row0 = nb * W, 4
-    cap, D = R + row0, H * 64
-    g = torch.Generator(device="cpu").manual_seed(5)
-    x = (torch.randn(R, D, generator=g) + 0.2).to(DEV)
-    parts = torch.randn(4, R, D, generator=g).to(DEV)
-    bias = (torch.randn(D, generator=g) * 0.1).to(DEV)
-    gam, bet = (torch.rand(D, generator=g) + 0.5).to(DEV), (torch.randn(D, generator=g) * 0.1).to(DEV)
-    wqkv = (torch.randn(3 * D, D, generator=g) * D ** -0.5).to(torch.bfloat16).to(DEV)
-    bqkv = (torch.randn(3 * D, generator=g) * 0.05).to(DEV)
-    wpos = torch.randint(5, 120, (W,), generator=g, dtype=torch.int32)
-    pos = wpos.repeat_interleave(nb)
-    tab = torch.arange(cap, dtype=torch.int32)[:, None].repeat(1, T)
-    for r in range(R):
-        w = r // nb
-        tab[row0 + r, : int(pos[r])] = row0 + w * nb + torch.randint(0, nb, (int(pos[r]),), generator=g,
-                                                                      dtype=torch.int32)
-    kc = (torch.randn(cap, H, T, 64, generator=g)).to(torch.bfloat16).to(DEV)
-    vc = (torch.randn(cap, H, T, 64, generator=g)).to(torch.bfloat16).to(DEV)
-    kc2, vc2 = kc.clone(), vc.clone()
-    tab_d, pos_d = tab.to(DEV), pos.to(DEV)
-    s = torch.cuda.current_stream().cuda_stream
-    xo = torch.full_like(x, float("nan"))
-    out = torch.empty(R, D, dtype=torch.bfloat16, device=DEV)
-    _lib.call("tw_attn_decode_self_q_tab", x.data_ptr(), parts.data_ptr(), 4, bias.data_ptr(), gam.data_ptr(),
-              bet.data_ptr(), 1e-5, wqkv.data_ptr(), bqkv.data_ptr(), xo.data_ptr(), R, H, T, pos_d.data_ptr(),
-              kc[row0].data_ptr(), vc[row0].data_ptr(), tab_d.data_ptr(), row0, out.data_ptr(), s)
-    x2 = x.clone()
-    hp = torch.zeros(D * 64, dtype=torch.bfloat16, device=DEV)
-    _lib.call("tw_resid_layernorm_packed", x2.data_ptr(), parts.data_ptr(), 4, bias.data_ptr(), gam.data_ptr(),
-              bet.data_ptr(), R, D, 1e-5, hp.data_ptr(), s)
-    qkv = torch.empty(R, 3 * D, dtype=torch.bfloat16, device=DEV)
-    _lib.call("tw_gemv_packed", hp.data_ptr(), 1, D, pack_w(wqkv).data_ptr(), R, 3 * D, D, _lib.TW_EPI_BF16,
-              qkv.data_ptr(), 3 * D, bqkv.data_ptr(), 1, s)
-    out2 = torch.empty_like(out)
-    _lib.call("tw_attn_decode_self_tab", qkv.data_ptr(), R, H, T, pos_d.data_ptr(), kc2[row0].data_ptr(),
-              vc2[row0].data_ptr(), tab_d.data_ptr(), row0, out2.data_ptr(), s)
-    torch.cuda.synchronize()
-    assert torch.equal(xo, x2)
-    rows = torch.arange(row0, row0 + R, device=DEV)
-    for c1, c2 in ((kc, kc2), (vc, vc2)):
-        a, b = c1[rows, :, pos_d.long()].float(), c2[rows, :, pos_d.long()].float()
-        assert bool(((a - b).abs() <= torch.maximum(a.abs(), b.abs()).clamp_min(1e-3) * 2.0 ** -7).all())
-    d = (out.float() - out2.float()).abs().max().item()
-    print(f"self_q_tab vs separate launches: max |d| {d:.3e}")
-    assert d <= 4e-2

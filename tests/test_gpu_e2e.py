@@ -398,30 +398,3 @@ def test_pipeline_sweep_matches_transformers(oracle):
                 assert st["ok"], (c["name"], k, st)
         summary.append((c["name"], "within tolerance"))
     print("sweep:", summary)
-
-
-def test_fused_prologues_decoder_step_vs_separate_launches(tr):
-    """The decoder step with both attention blocks' residual + LayerNorm + projections folded into the attention
-    launches (WhisperEngine.fuse_self_q / fuse_cross_q: tw_attn_decode_self_q, tw_attn_decode_cross_q; 31 launches
-    per token) against the separate launches (47): teacher-forced logits within 0.02 (the LayerNorms' reductions and
-    the projections' dot products run in another order; the bf16 roundings otherwise the same)."""
-    eng = tr.engine
-    _load(tr, [speech_like(30.0, 21), white_noise(30.0, 5), speech_like(17.0, 8)])
-    eng.row_map[:3] = torch.arange(3, dtype=torch.int32)
-    eng.seek[:3] = 0
-    eng.encode(3)
-    ids = [50258, 50259, 50360, 50365, 400, 1200, 50390, 50391, 77, 9000]
-    lg = {}
-    for fuse in (True, False):
-        eng.fuse_cross_q = eng.fuse_self_q = fuse
-        rows = []
-        for t, tok in enumerate(ids):
-            eng.ids[:3] = tok
-            eng.pos[:3] = t
-            eng.decoder_step(3)
-            rows.append(eng.logits[:3].float().cpu())
-        lg[fuse] = torch.stack(rows)
-    eng.fuse_cross_q = eng.fuse_self_q = True
-    d = (lg[True] - lg[False]).abs().max().item()
-    print(f"fused self/cross prologues vs separate launches: teacher-forced logits max |d| {d:.2e}")
-    assert d <= 0.02

@@ -586,64 +586,6 @@ def test_resid_layernorm_packed_vs_torch(M, D, nparts):
     assert torch.equal(unpack_act(out, M, D).view(torch.int16), rm.view(torch.int16))
 
 
-@pytest.mark.parametrize("B,H,nparts,Sx", [(24, 20, 4, 1500), (5, 6, 2, 1500), (64, 20, 4, 1500), (3, 20, 0, 33)])
-def test_attn_decode_cross_q_vs_separate_launches(B, H, nparts, Sx):
-    """tw_attn_decode_cross_q (residual + LayerNorm + the head's q projection + cross-attention in one launch) against
-    the three launches it replaces (tw_resid_layernorm_packed, the q GEMV, tw_attn_decode_cross) and against fp32:
-    the residual rows bit-identical (same per-element summation order), the attention output close to
-    the separate launches up to q's bf16 rounding (the LayerNorm's reductions and the q dot products run in another
-    order, so an element of q can round one bf16 ulp the other way; through the 4x-peaked softmax that moves outputs
-    by up to ~8 output ulps: measured 2.0 at 24 rows, 6.6 at 64) and no further from fp32 than the separate launches
-    (within 2e-2, or 1.5x their own distance on this peaked softmax)."""
-    D = H * 64
-    g = torch.Generator(device="cpu").manual_seed(B * 100 + H)
-    x = (torch.randn(B, D, generator=g) * 2 + 0.5).to(DEV)
-    parts = torch.randn(max(nparts, 1), B, D, generator=g).to(DEV)
-    bias = torch.randn(D, generator=g).to(DEV) * 0.1
-    gam = (torch.rand(D, generator=g) + 0.5).to(DEV)
-    bet = (torch.randn(D, generator=g) * 0.1).to(DEV)
-    wq = rand_bf16(D, D, scale=D ** -0.5 * 0.125 * 4, seed=B + 7)
-    bq = torch.randn(D, generator=g).to(DEV) * 0.05
-    Bt = B
-    ckv = rand_bf16(2, Bt, H, Sx, 64, seed=H + Sx)
-    rm = torch.arange(B, dtype=torch.int32, device=DEV).flip(0).contiguous()
-    # fused
-    x_out = torch.full_like(x, float("nan"))
-    out = torch.empty(B, D, dtype=torch.bfloat16, device=DEV)
-    _lib.call("tw_attn_decode_cross_q", x.data_ptr(), parts.data_ptr(), nparts, bias.data_ptr(), gam.data_ptr(),
-              bet.data_ptr(), 1e-5, wq.data_ptr(), bq.data_ptr(), x_out.data_ptr(), B, H, Sx, Bt, rm.data_ptr(),
-              ckv.data_ptr(), out.data_ptr(), S())
-    # separate launches (views of <= 64 rows)
-    x2 = x.clone()
-    hp = torch.zeros(D * 64, dtype=torch.bfloat16, device=DEV)
-    _lib.call("tw_resid_layernorm_packed", x2.data_ptr(), parts.data_ptr(), nparts, bias.data_ptr(), gam.data_ptr(),
-              bet.data_ptr(), B, D, 1e-5, hp.data_ptr(), S())
-    q = torch.empty(B, D, dtype=torch.bfloat16, device=DEV)
-    _lib.call("tw_gemv_packed", hp.data_ptr(), 1, D, pack_w(wq).data_ptr(), B, D, D, _lib.TW_EPI_BF16, q.data_ptr(), D,
-              bq.data_ptr(), 1, S())
-    out2 = torch.empty_like(out)
-    _lib.call("tw_attn_decode_cross", q.data_ptr(), B, H, Sx, Bt, rm.data_ptr(), ckv.data_ptr(), out2.data_ptr(), S())
-    torch.cuda.synchronize()
-    assert torch.equal(x_out, x2)
-    ulp = torch.maximum(out.float().abs(), out2.float().abs()).clamp_min(0.02) * 2.0 ** -7
-    d = (out.float() - out2.float()).abs()
-    print(f"cross_q vs separate: max |d| {d.max().item():.2e}, {(d / ulp).max().item():.2f} ulps")
-    assert bool((d <= 10 * ulp).all())
-    # fp32 reference of the whole block
-    xr = x + (bias + parts[:nparts].sum(0) if nparts else bias)
-    ln = torch.nn.functional.layer_norm(xr, (D,), gam, bet, 1e-5)
-    qf = ln @ wq.float().t() + bq
-    ef = es = 0.0
-    for b in range(B):
-        s = int(rm[b])
-        ref = _ref_attn(qf[b].view(H, 1, 64), ckv[0, s].float(), ckv[1, s].float())[:, 0].reshape(D)
-        ef = max(ef, (out[b].float() - ref).abs().max().item())
-        es = max(es, (out2[b].float() - ref).abs().max().item())
-    print(f"vs fp32: fused max |d| {ef:.3e}, separate launches {es:.3e}")
-    # (this softmax is peaked: q's bf16 rounding alone moves outputs by ~1e-2 on either path)
-    assert ef <= max(2e-2, 1.5 * es)
-
-
 def test_resid_layernorm_packed_to_writes_the_other_buffer():
     """tw_resid_layernorm_packed_to: the in-place kernel's arithmetic, the updated rows in x_out, x untouched."""
     M, D = 24, 1280
@@ -661,67 +603,3 @@ def test_resid_layernorm_packed_to_writes_the_other_buffer():
               b.data_ptr(), M, D, 1e-5, out2.data_ptr(), S())
     torch.cuda.synchronize()
     assert torch.equal(x, x0) and torch.equal(xo, x2) and torch.equal(out1, out2)
-
-
-@pytest.mark.parametrize("B,H,nparts,t_max", [(24, 20, 4, 200), (5, 6, 0, 40), (64, 20, 4, 300), (3, 20, 4, 1)])
-def test_attn_decode_self_q_vs_separate_launches(B, H, nparts, t_max):
-    """tw_attn_decode_self_q (residual + LayerNorm + the head's q/k/v projection + the self-attention step in one
-    launch) against the three launches it replaces (tw_resid_layernorm_packed, the q/k/v GEMV, tw_attn_decode_self):
-    the residual rows bit-identical, the appended K/V within one bf16 ulp of the GEMV's (the dot products run in
-    another order), the attention output no further from fp32 than the separate launches' (within 2e-2 or 1.5x theirs).
-    Histories of 1 to 300 positions: both the one-round-trip and the two-pass paths."""
-    D, T = H * 64, 448
-    g = torch.Generator(device="cpu").manual_seed(B * 10 + H + t_max)
-    x = (torch.randn(B, D, generator=g) * 2 + 0.3).to(DEV)
-    parts = torch.randn(max(nparts, 1), B, D, generator=g).to(DEV)
-    bias = (torch.randn(D, generator=g) * 0.1).to(DEV) if nparts else None
-    gam = (torch.rand(D, generator=g) + 0.5).to(DEV)
-    bet = (torch.randn(D, generator=g) * 0.1).to(DEV)
-    wqkv = rand_bf16(3 * D, D, scale=D ** -0.5, seed=B + H)
-    bqkv = (torch.randn(3 * D, generator=g) * 0.05).to(DEV)
-    pos = torch.randint(max(0, t_max - 20), t_max, (B,), generator=g, dtype=torch.int32).to(DEV)
-    kc = rand_bf16(B, H, T, 64, seed=H + 5)
-    vc = rand_bf16(B, H, T, 64, seed=H + 6)
-    kc2, vc2 = kc.clone(), vc.clone()
-    x_out = torch.full_like(x, float("nan"))
-    out = torch.empty(B, D, dtype=torch.bfloat16, device=DEV)
-    _lib.call("tw_attn_decode_self_q", x.data_ptr(), parts.data_ptr() if nparts else None, nparts, _lib.ptr(bias),
-              gam.data_ptr(), bet.data_ptr(), 1e-5, wqkv.data_ptr(), bqkv.data_ptr(), x_out.data_ptr(), B, H, T,
-              pos.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(), S())
-    x2 = x.clone()
-    hp = torch.zeros(D * 64, dtype=torch.bfloat16, device=DEV)
-    _lib.call("tw_resid_layernorm_packed", x2.data_ptr(), parts.data_ptr(), nparts, _lib.ptr(bias), gam.data_ptr(),
-              bet.data_ptr(), B, D, 1e-5, hp.data_ptr(), S())
-    qkv = torch.empty(B, 3 * D, dtype=torch.bfloat16, device=DEV)
-    _lib.call("tw_gemv_packed", hp.data_ptr(), 1, D, pack_w(wqkv).data_ptr(), B, 3 * D, D, _lib.TW_EPI_BF16,
-              qkv.data_ptr(), 3 * D, bqkv.data_ptr(), 1, S())
-    out2 = torch.empty_like(out)
-    _lib.call("tw_attn_decode_self", qkv.data_ptr(), B, H, T, pos.data_ptr(), kc2.data_ptr(), vc2.data_ptr(),
-              out2.data_ptr(), S())
-    torch.cuda.synchronize()
-    assert torch.equal(x_out, x2)
-    rows = torch.arange(B, device=DEV)
-    pl = pos.long()
-    for cache, cache2, off in ((kc, kc2, D), (vc, vc2, 2 * D)):
-        a = cache[rows, :, pl].float()
-        b2 = cache2[rows, :, pl].float()
-        ulp = torch.maximum(a.abs(), b2.abs()).clamp_min(1e-3) * 2.0 ** -7
-        assert bool(((a - b2).abs() <= ulp).all())  # one bf16 ulp at most
-        keep = torch.ones(T, dtype=torch.bool, device=DEV)
-        for r in range(B):  # positions other than pos untouched by both
-            keep[:] = True
-            keep[pl[r]] = False
-            assert torch.equal(cache[r][:, keep], cache2[r][:, keep])
-    # fp32 reference over the appended caches (the fused kernel's own k/v)
-    ef = es = 0.0
-    xr = x + ((bias + parts[:nparts].sum(0)) if nparts else 0)
-    ln = torch.nn.functional.layer_norm(xr, (D,), gam, bet, 1e-5)
-    q = (ln @ wqkv.float().t() + bqkv)[:, :D]
-    for r in range(B):
-        n = int(pos[r]) + 1
-        ref = _ref_attn(q[r].view(H, 1, 64), kc[r, :, :n].float(), vc[r, :, :n].float())[:, 0].reshape(D)
-        ef = max(ef, (out[r].float() - ref).abs().max().item())
-        ref2 = _ref_attn(q[r].view(H, 1, 64), kc2[r, :, :n].float(), vc2[r, :, :n].float())[:, 0].reshape(D)
-        es = max(es, (out2[r].float() - ref2).abs().max().item())
-    print(f"self_q vs fp32: fused {ef:.3e}, separate launches {es:.3e}")
-    assert ef <= max(2e-2, 1.5 * es)

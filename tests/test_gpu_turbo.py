@@ -341,10 +341,7 @@ def test_turbo_token_timestamps_vs_transformers(turbo):
     standardise -> median filter -> DTW) at turbo depth, one window per batch as the golden was made
     (tests/golden/turbo_word.npz, make_golden.py turbo_word; default alignment heads: every head of decoder layers
     2-3). Compared where the device tokens equal the fp32 tokens (a bf16 near-tie elsewhere changes the text and with
-    it the DTW path); tolerance: per token |d| <= 0.2 s (10 frames) and >= 80 % of the tokens equal (measured on
-    MI355X: 100 % equal with the separate decoder launches, 20 of 23 equal and the others 1-3 frames off with the fused
-    attention prologues, whose LayerNorm / projection sums run in another order: the DTW path over random-weight
-    attention moves at near-ties)."""
+    it the DTW path); tolerance as tests/test_gpu_word.py: per token |d| <= 0.2 s and >= 90 % of the tokens equal."""
     z = np.load(os.path.join(os.path.dirname(__file__), "golden", "turbo_word.npz"))
     eng = turbo.engine
     assert [tuple(h) for h in z["alignment_heads"].tolist()] == [tuple(h) for h in eng.gen.alignment_heads]
@@ -373,7 +370,7 @@ def test_turbo_token_timestamps_vs_transformers(turbo):
         d = np.abs(got - ref)
         print(f"turbo token timestamps clip {i}: {len(ref_t)} tokens, max |d| {d.max():.3f} s, "
               f"{(d < 1e-4).mean():.0%} equal")  # (times are multiples of 0.02 s; the offset is added in f32)
-        assert d.max() <= 0.2 + 1e-4 and (d < 1e-4).mean() >= 0.8, (i, d)
+        assert d.max() <= 0.2 + 1e-4 and (d < 1e-4).mean() >= 0.9, (i, d)
         compared += 1
     assert compared >= 1
 

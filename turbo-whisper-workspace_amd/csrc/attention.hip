@@ -851,13 +851,12 @@ struct TabRows {
   }
 };
 
-// The body of a self-attention step for block (h, b): this token's q / k / v at row[0..63], row[rs..rs+63],
-// row[2 rs..2 rs+63] (global memory: the q/k/v GEMV output, rs = D; or LDS: k_attn_decode_self_q's own projection,
-// rs = 64), the cache append and the attention over positions 0..pos[b]. part / red / qf / outv / sc: LDS scratch.
 template <bool TAB>
-__device__ __attribute__((always_inline)) inline void self2_step(const bf16_t* __restrict__ row, int rs, int D, int max_pos, const int* __restrict__ pos,
-                                  bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, const int* __restrict__ kv_tab,
-                                  int row0, bf16_t* __restrict__ out) {
+__global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__ qkv, int D, int max_pos,
+                                                           const int* __restrict__ pos, bf16_t* __restrict__ kc,
+                                                           bf16_t* __restrict__ vc, const int* __restrict__ kv_tab,
+                                                           int row0, bf16_t* __restrict__ out) {
+  TW_DEC_PRIO();
   __shared__ float part[32 * 64];
   __shared__ float red[16];
   __shared__ float qf[64];
@@ -866,13 +865,14 @@ __device__ __attribute__((always_inline)) inline void self2_step(const bf16_t* _
   const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x;
   const int tid = threadIdx.x, g = tid >> 3, gl = tid & 7, lane = tid & 63, wid = tid >> 6;
   const int t = pos[b];
+  const bf16_t* row = qkv + (size_t)b * 3 * D + h * 64;
   bf16_t* K = kc + ((size_t)b * H + h) * max_pos * 64;
   bf16_t* V = vc + ((size_t)b * H + h) * max_pos * 64;
   if (t >= DS2_KEYS) {  // long history: the two-pass form (cache write, then K / V re-read)
     if (tid < 64) {
       qf[tid] = bf16_to_f32(row[tid]);
-      K[(size_t)t * 64 + tid] = row[rs + tid];
-      V[(size_t)t * 64 + tid] = row[2 * rs + tid];
+      K[(size_t)t * 64 + tid] = row[D + tid];
+      V[(size_t)t * 64 + tid] = row[2 * D + tid];
     }
     __threadfence_block();
     __syncthreads();
@@ -887,8 +887,8 @@ __device__ __attribute__((always_inline)) inline void self2_step(const bf16_t* _
   }
   // one round trip: this token's q / k / v chunks (every group: 8 lanes x 16 B) and the cached keys < t
   const uint4 qr = *(const uint4*)(row + gl * 8);
-  const uint4 kr = *(const uint4*)(row + rs + gl * 8);
-  const uint4 vr = *(const uint4*)(row + 2 * rs + gl * 8);
+  const uint4 kr = *(const uint4*)(row + D + gl * 8);
+  const uint4 vr = *(const uint4*)(row + 2 * D + gl * 8);
   uint4 kk[DS2_U], vv[DS2_U];
   const int last = max(t - 1, 0);
 #pragma unroll
@@ -957,232 +957,6 @@ __device__ __attribute__((always_inline)) inline void self2_step(const bf16_t* _
     for (int gg = 0; gg < 32; ++gg) v += part[gg * 64 + tid];
     out[(size_t)b * D + h * 64 + tid] = f32_to_bf16(v * inv);
   }
-}
-
-
-template <bool TAB>
-__global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__ qkv, int D, int max_pos,
-                                                           const int* __restrict__ pos, bf16_t* __restrict__ kc,
-                                                           bf16_t* __restrict__ vc, const int* __restrict__ kv_tab,
-                                                           int row0, bf16_t* __restrict__ out) {
-  TW_DEC_PRIO();
-  self2_step<TAB>(qkv + (size_t)blockIdx.y * 3 * D + blockIdx.x * 64, D, D, max_pos, pos, kc, vc, kv_tab, row0, out);
-}
-
-// ---- decoder fused prologues (k_attn_decode_cross_q, k_attn_decode_self_q) --------------------------------------
-// dec_row_ln: the residual update and LayerNorm of row b by the whole 256-thread block: x_row + bias + sum of the
-// split-K partials (summation order as k_resid_ln_w: ((x + bias) + p0) + p1 + ...), the updated row stored to x_out
-// when write_x (one block per row does it), and bf16(LayerNorm * gamma + beta) as floats in ys[D] (LDS). Ends with
-// a block barrier (ys complete).
-#define XQ_MAXC 2  // float4 chunks of the row per thread: D <= 2048
-__device__ __attribute__((always_inline)) inline void dec_row_ln(const float* x, const float* parts, int nparts, long part_stride,
-                                  const float* __restrict__ bias, const float* __restrict__ gam,
-                                  const float* __restrict__ bet, float eps, float* x_out, bool write_x, int D, int b,
-                                  float* ys, float* red) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nc = D >> 2;
-  const float* xr = x + (size_t)b * D;
-  const float* pr = parts ? parts + (size_t)b * D : nullptr;
-  float4 v[XQ_MAXC];
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < XQ_MAXC; ++i) {
-    const int c = tid + 256 * i;
-    if (c < nc) {
-      float4 a = ((const float4*)xr)[c];
-      if (bias) {
-        const float4 bb = ((const float4*)bias)[c];
-        a.x += bb.x; a.y += bb.y; a.z += bb.z; a.w += bb.w;
-      }
-      for (int p = 0; p < nparts; ++p) {
-        const float4 q = ((const float4*)(pr + p * part_stride))[c];
-        a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
-      }
-      v[i] = a;
-      s += (a.x + a.y) + (a.z + a.w);
-      if (write_x) ((float4*)(x_out + (size_t)b * D))[c] = a;
-    }
-  }
-  s = wave_sum(s);
-  if (lane == 0) red[wid] = s;
-  __syncthreads();
-  const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)D;
-  float q2 = 0.f;
-#pragma unroll
-  for (int i = 0; i < XQ_MAXC; ++i) {
-    if (tid + 256 * i < nc) {
-      const float a = v[i].x - mean, bb = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
-      q2 += (a * a + bb * bb) + (c * c + d * d);
-    }
-  }
-  q2 = wave_sum(q2);
-  if (lane == 0) red[4 + wid] = q2;
-  __syncthreads();
-  const float rstd = rsqrtf((red[4] + red[5] + red[6] + red[7]) / (float)D + eps);
-#pragma unroll
-  for (int i = 0; i < XQ_MAXC; ++i) {
-    const int c = tid + 256 * i;
-    if (c < nc) {
-      const float4 gg = ((const float4*)gam)[c], bb = ((const float4*)bet)[c];
-      ys[4 * c + 0] = bf16_to_f32(f32_to_bf16((v[i].x - mean) * rstd * gg.x + bb.x));
-      ys[4 * c + 1] = bf16_to_f32(f32_to_bf16((v[i].y - mean) * rstd * gg.y + bb.y));
-      ys[4 * c + 2] = bf16_to_f32(f32_to_bf16((v[i].z - mean) * rstd * gg.z + bb.z));
-      ys[4 * c + 3] = bf16_to_f32(f32_to_bf16((v[i].w - mean) * rstd * gg.w + bb.w));
-    }
-  }
-  __syncthreads();
-}
-
-// dec_ln_proj<NSEC>: ln() (dec_row_ln) plus this head's projection of the normalised row: NSEC sections of 64 output
-// rows (1: cross q; 3: self q, k, v), output row i = W row (i / 64) * D + 64 h + i % 64 of w (bf16 [NSEC D][D]
-// row-major, nn.Linear), outs[i] = bf16(ys . W[row] + bias[row]) as floats (the projection GEMV's bf16 epilogue).
-// Wave wid owns output rows [16 NSEC wid, 16 NSEC (wid + 1)) as row pairs (two consecutive W rows = 2 D / 8 contiguous
-// 16-byte chunks; lane l reads chunks l + 64 i, i < XP_CPL: every load instruction 1 KiB contiguous), XP_PPR pairs
-// (20 loads per lane) per round; round 0 is issued before ln() so that its latency overlaps the LayerNorm's.
-#define XP_PPR 2
-#define XP_CPL 5  // chunks per lane per pair: 2 D / 8 / 64 at D = 1280 (D <= 1280)
-template <int NSEC, typename LnFn>
-__device__ __attribute__((always_inline)) inline void dec_ln_proj(const bf16_t* __restrict__ w, int D, int h, const float* __restrict__ bias,
-                                   const float* ys, float* outs, LnFn ln) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  constexpr int ROUNDS = 8 * NSEC / XP_PPR;  // 16 NSEC rows per wave = 8 NSEC pairs
-  const int nch = D >> 3;
-  typedef uint4 Buf[XP_PPR][XP_CPL];
-  Buf wa, wb;  // double buffer: round r + 1's loads in flight while round r's dot products run
-  auto wrow = [&](int i) { return (size_t)((i >> 6) * D + h * 64 + (i & 63)); };  // output row -> W row
-  auto wload = [&](Buf& wr, int rd) {
-#pragma unroll
-    for (int p = 0; p < XP_PPR; ++p) {
-      const int i0 = wid * 16 * NSEC + 2 * (rd * XP_PPR + p);
-      const bf16_t* src = w + wrow(i0) * D;
-#pragma unroll
-      for (int i = 0; i < XP_CPL; ++i) {
-        const int c = min(lane + 64 * i, 2 * nch - 1);
-        wr[p][i] = *(const uint4*)(src + c * 8);
-      }
-    }
-  };
-  auto wdot = [&](const Buf& wr, int rd) {
-#pragma unroll
-    for (int p = 0; p < XP_PPR; ++p) {
-      float d0 = 0.f, d1 = 0.f;
-#pragma unroll
-      for (int i = 0; i < XP_CPL; ++i) {
-        const int c = lane + 64 * i;
-        if (c < 2 * nch) {
-          const int kc = c < nch ? c : c - nch;
-          const float4 y0 = *(const float4*)(ys + kc * 8), y1 = *(const float4*)(ys + kc * 8 + 4);
-          const bf16_t* we = (const bf16_t*)&wr[p][i];
-          const float d = ((y0.x * bf16_to_f32(we[0]) + y0.y * bf16_to_f32(we[1])) +
-                           (y0.z * bf16_to_f32(we[2]) + y0.w * bf16_to_f32(we[3]))) +
-                          ((y1.x * bf16_to_f32(we[4]) + y1.y * bf16_to_f32(we[5])) +
-                           (y1.z * bf16_to_f32(we[6]) + y1.w * bf16_to_f32(we[7])));
-          if (c < nch) d0 += d; else d1 += d;
-        }
-      }
-      d0 = wave_sum(d0);
-      d1 = wave_sum(d1);
-      if (lane == 0) {
-        const int i0 = wid * 16 * NSEC + 2 * (rd * XP_PPR + p);
-        outs[i0] = bf16_to_f32(f32_to_bf16(d0 + bias[wrow(i0)]));
-        outs[i0 + 1] = bf16_to_f32(f32_to_bf16(d1 + bias[wrow(i0 + 1)]));
-      }
-    }
-  };
-  wload(wa, 0);
-  if (ROUNDS > 1) wload(wb, 1);
-  ln();
-  auto step = [&](int rd) {
-    wdot(wa, rd);
-    if (rd + 2 < ROUNDS) wload(wa, rd + 2);
-    if (rd + 1 < ROUNDS) {
-      wdot(wb, rd + 1);
-      if (rd + 3 < ROUNDS) wload(wb, rd + 3);
-    }
-  };
-  if constexpr (ROUNDS <= 4) {
-#pragma unroll
-    for (int rd = 0; rd < ROUNDS; rd += 2) step(rd);
-  } else {  // (unrolled, hipcc hoists later rounds' loads: 245 VGPRs, or scratch under a 128 cap)
-#pragma unroll 1
-    for (int rd = 0; rd < ROUNDS; rd += 2) step(rd);
-  }
-  __syncthreads();  // outs complete
-}
-
-// k_attn_decode_self_q: the self-attention step with the two launches before it folded into its prologue (as
-// k_attn_decode_cross_q does for the cross-attention): row b's residual update + self_attn_layer_norm (dec_row_ln;
-// the updated row written to x_out by head 0's block) and this head's 192 rows of the q/k/v projection
-// (dec_ln_proj<3>: 480 KB of wqkv per block from L2 / Infinity Cache, twelve double-buffered rounds), rounded to bf16
-// as the q/k/v GEMV stores them; then self2_step on that LDS row (the cache append and the attention; TAB: beam rows,
-// histories through the position table as tw_attn_decode_self_tab). Saves two launches per decoder layer.
-template <bool TAB>
-__global__ TW_DEC_LB(256, 4) void k_attn_decode_self_q(const float* __restrict__ x, const float* __restrict__ parts,
-                                                       int nparts, long part_stride, const float* __restrict__ bias,
-                                                       const float* __restrict__ gam, const float* __restrict__ bet,
-                                                       float eps, const bf16_t* __restrict__ wqkv,
-                                                       const float* __restrict__ bqkv, float* __restrict__ x_out,
-                                                       int max_pos, const int* __restrict__ pos, bf16_t* __restrict__ kc,
-                                                       bf16_t* __restrict__ vc, const int* __restrict__ kv_tab, int row0,
-                                                       bf16_t* __restrict__ out) {
-  TW_DEC_PRIO();
-  __shared__ __attribute__((aligned(16))) float big[2048];  // the LayerNorm row
-  __shared__ float outs[192];
-  __shared__ __attribute__((aligned(16))) bf16_t qkv_b[192];
-  __shared__ float red[8];
-  const int h = blockIdx.x, b = blockIdx.y, D = gridDim.x * 64, tid = threadIdx.x;
-  dec_ln_proj<3>(wqkv, D, h, bqkv, big, outs, [&] {
-    dec_row_ln(x, parts, nparts, part_stride, bias, gam, bet, eps, x_out, h == 0, D, b, big, red);
-  });
-  if (tid < 192) qkv_b[tid] = f32_to_bf16(outs[tid]);  // (exact: outs are bf16 values)
-  __syncthreads();
-  self2_step<TAB>(qkv_b, 64, D, max_pos, pos, kc, vc, kv_tab, row0, out);
-}
-
-#if TW_DEBUG
-static int tw_debug_tab_guard(const int* kv_tab, const int* pos, int row0, int B, int max_pos, hipStream_t st);
-#endif
-static int self_q_launch(const float* x, const float* parts, int nparts, const float* bias, const float* gamma,
-                         const float* beta, float eps, const uint16_t* wqkv, const float* bqkv, float* x_out, int B,
-                         int H, int max_pos, const int* pos, uint16_t* k_cache, uint16_t* v_cache, const int* kv_tab,
-                         int row0, uint16_t* out, void* stream) {
-  TW_REQUIRE(x && gamma && beta && wqkv && bqkv && x_out && pos && k_cache && v_cache && out && x_out != x && B > 0 &&
-                 H > 0 && row0 >= 0,
-             "tw_attn_decode_self_q: bad args");
-  TW_REQUIRE(H * 64 <= 1280 && nparts >= 0 && nparts <= 8 && (nparts == 0 || parts) && max_pos <= DA_SELF_MAXK,
-             "tw_attn_decode_self_q: H=%d (H * 64 <= 1280), nparts=%d, max_pos=%d", H, nparts, max_pos);
-  const dim3 grid(H, B), blk(256);
-  hipStream_t st = (hipStream_t)stream;
-  if (kv_tab) {
-#if TW_DEBUG
-    if (int rc = tw_debug_tab_guard(kv_tab, pos, row0, B, max_pos, st)) return rc;
-#endif
-    hipLaunchKernelGGL(k_attn_decode_self_q<true>, grid, blk, 0, st, x, parts, nparts, (long)B * H * 64, bias, gamma,
-                       beta, eps, (const bf16_t*)wqkv, bqkv, x_out, max_pos, pos, (bf16_t*)k_cache, (bf16_t*)v_cache,
-                       kv_tab, row0, (bf16_t*)out);
-  } else {
-    hipLaunchKernelGGL(k_attn_decode_self_q<false>, grid, blk, 0, st, x, parts, nparts, (long)B * H * 64, bias, gamma,
-                       beta, eps, (const bf16_t*)wqkv, bqkv, x_out, max_pos, pos, (bf16_t*)k_cache, (bf16_t*)v_cache,
-                       nullptr, 0, (bf16_t*)out);
-  }
-  return tw_check_launch("tw_attn_decode_self_q");
-}
-
-extern "C" int tw_attn_decode_self_q(const float* x, const float* parts, int nparts, const float* bias,
-                                     const float* gamma, const float* beta, float eps, const uint16_t* wqkv,
-                                     const float* bqkv, float* x_out, int B, int H, int max_pos, const int* pos,
-                                     uint16_t* k_cache, uint16_t* v_cache, uint16_t* out, void* stream) {
-  return self_q_launch(x, parts, nparts, bias, gamma, beta, eps, wqkv, bqkv, x_out, B, H, max_pos, pos, k_cache,
-                       v_cache, nullptr, 0, out, stream);
-}
-
-extern "C" int tw_attn_decode_self_q_tab(const float* x, const float* parts, int nparts, const float* bias,
-                                         const float* gamma, const float* beta, float eps, const uint16_t* wqkv,
-                                         const float* bqkv, float* x_out, int B, int H, int max_pos, const int* pos,
-                                         uint16_t* k_cache, uint16_t* v_cache, const int* kv_tab, int row0,
-                                         uint16_t* out, void* stream) {
-  TW_REQUIRE(kv_tab, "tw_attn_decode_self_q_tab: kv_tab");
-  return self_q_launch(x, parts, nparts, bias, gamma, beta, eps, wqkv, bqkv, x_out, B, H, max_pos, pos, k_cache,
-                       v_cache, kv_tab, row0, out, stream);
 }
 
 // Self-attention step: qkv [B][3D] bf16 (q pre-scaled), appends k,v at position pos[b] into the cache
@@ -1424,137 +1198,6 @@ __global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_lean(const bf16_t* __re
     }
     out[(size_t)b * D + h * 64 + tid] = f32_to_bf16(v / tot);
   }
-}
-
-// k_attn_decode_cross_q: the lean cross-attention with the two launches before it folded into its prologue — the
-// residual + encoder_attn_layer_norm of row b (what tw_resid_layernorm_packed did: x + bias + the out_proj's split-K
-// partials, then LayerNorm) and this head's 64 columns of the q projection (what the cross-q GEMV did:
-// bf16(LN(x)) . Wq[h*64 .. h*64+63][:]^T + bq, rounded to bf16 like the GEMV's output). Every (row, head) block
-// recomputes its row's LayerNorm (40 KB of L2 reads) and reads its head's 160 KB slice of Wq (L2 / Infinity-Cache
-// resident: 3.3 MB per layer for all blocks), in two rounds of 20 16-byte loads per lane, the first issued before the
-// LayerNorm's loads so that both latencies overlap; the K/V stream then runs exactly as in the lean kernel. The
-// updated residual row is written once, by head 0's block, to x_out (a second buffer: the other heads' blocks still
-// read x). Saves two launches per decoder layer.
-template <int NG, int UNR = DA_UNR>
-__global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_q(const float* __restrict__ x, const float* __restrict__ parts,
-                                                             int nparts, long part_stride, const float* __restrict__ bias,
-                                                             const float* __restrict__ gam, const float* __restrict__ bet,
-                                                             float eps, const bf16_t* __restrict__ wq,
-                                                             const float* __restrict__ bq, float* __restrict__ x_out,
-                                                             int S, int Bt, const int* __restrict__ row_map,
-                                                             const bf16_t* __restrict__ ckv, bf16_t* __restrict__ out) {
-  TW_DEC_PRIO();
-  static_assert(NG == 32, "k_attn_decode_cross_q: 256 threads");
-  constexpr int NWV = NG / 8;
-  __shared__ float wpart[NWV][64];
-  __shared__ float wml[NWV][2];
-  __shared__ __attribute__((aligned(16))) float ys[2048];  // bf16-rounded LayerNorm output of the row (D <= 2048)
-  __shared__ float qs[64];
-  __shared__ float red[8];
-  const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x, D = H * 64;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = tid >> 3, gl = tid & 7;
-  dec_ln_proj<1>(wq, D, h, bq, ys, qs, [&] {
-    dec_row_ln(x, parts, nparts, part_stride, bias, gam, bet, eps, x_out, h == 0, D, b, ys, red);
-  });
-  float qv[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) qv[e] = qs[gl * 8 + e];
-  // ---- the lean kernel's attention over the row's cross K/V
-  const int slot = row_map ? row_map[b] : b;
-  const bf16_t* K = ckv + (((size_t)0 * Bt + slot) * H + h) * S * 64;
-  const bf16_t* V = ckv + (((size_t)1 * Bt + slot) * H + h) * S * 64;
-  float m = -INFINITY, l = 0.f;
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int nit = (S + NG - 1) / NG;
-  for (int it0 = 0; it0 < nit; it0 += UNR) {
-    uint4 kk[UNR], vv[UNR];
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int key = min((it0 + u) * NG + g, S - 1);
-      typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
-      const u32x4_nt a = __builtin_nontemporal_load((const u32x4_nt*)(K + (size_t)key * 64 + gl * 8));
-      const u32x4_nt c = __builtin_nontemporal_load((const u32x4_nt*)(V + (size_t)key * 64 + gl * 8));
-      kk[u] = make_uint4(a.x, a.y, a.z, a.w);
-      vv[u] = make_uint4(c.x, c.y, c.z, c.w);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    float sv[UNR];
-    float bm = m;
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      float d = 0.f;
-      const bf16_t* ke = (const bf16_t*)&kk[u];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
-      d += __shfl_xor(d, 1, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 4, 64);
-      sv[u] = (it0 + u) * NG + g < S ? d : -INFINITY;
-      bm = fmaxf(bm, sv[u]);
-    }
-    if (bm == -INFINITY) continue;
-    const float sc = __expf(m - bm);
-    l *= sc;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] *= sc;
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const float p = __expf(sv[u] - bm);
-      l += p;
-      const bf16_t* ve = (const bf16_t*)&vv[u];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += p * bf16_to_f32(ve[e]);
-    }
-    m = bm;
-  }
-#pragma unroll
-  for (int o = 8; o < 64; o <<= 1) {
-    const float m2 = __shfl_xor(m, o, 64), l2 = __shfl_xor(l, o, 64);
-    const float M = fmaxf(m, m2);
-    const float s1 = m == -INFINITY ? 0.f : __expf(m - M), s2 = m2 == -INFINITY ? 0.f : __expf(m2 - M);
-    l = l * s1 + l2 * s2;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = acc[e] * s1 + __shfl_xor(acc[e], o, 64) * s2;
-    m = M;
-  }
-  if (lane < 8) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) wpart[wid][lane * 8 + e] = acc[e];
-    if (lane == 0) {
-      wml[wid][0] = m;
-      wml[wid][1] = l;
-    }
-  }
-  __syncthreads();
-  if (tid < 64) {
-    float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < NWV; ++w) M = fmaxf(M, wml[w][0]);
-    float vsum = 0.f, tot = 0.f;
-#pragma unroll
-    for (int w = 0; w < NWV; ++w) {
-      const float mg = wml[w][0];
-      const float wt = mg == -INFINITY ? 0.f : __expf(mg - M);
-      tot += wt * wml[w][1];
-      vsum += wt * wpart[w][tid];
-    }
-    out[(size_t)b * D + h * 64 + tid] = f32_to_bf16(vsum / tot);
-  }
-}
-
-extern "C" int tw_attn_decode_cross_q(const float* x, const float* parts, int nparts, const float* bias,
-                                      const float* gamma, const float* beta, float eps, const uint16_t* wq,
-                                      const float* bq, float* x_out, int B, int H, int S, int Bt, const int* row_map,
-                                      const uint16_t* cross_kv, uint16_t* out, void* stream) {
-  TW_REQUIRE(x && gamma && beta && wq && bq && x_out && cross_kv && out && x_out != x && B > 0 && H > 0 && S > 0 &&
-                 S <= DA_MAXK,
-             "tw_attn_decode_cross_q: bad args");
-  TW_REQUIRE(H * 64 <= 1280 && nparts >= 0 && nparts <= 8 && (nparts == 0 || parts),
-             "tw_attn_decode_cross_q: H=%d (H * 64 <= 1280), nparts=%d", H, nparts);
-  hipLaunchKernelGGL((k_attn_decode_cross_q<32>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, x, parts, nparts,
-                     (long)B * H * 64, bias, gamma, beta, eps, (const bf16_t*)wq, bq, x_out, S, Bt, row_map,
-                     (const bf16_t*)cross_kv, (bf16_t*)out);
-  return tw_check_launch("tw_attn_decode_cross_q");
 }
 
 // k_attn_decode_cross_grp: the lean kernel for G rows that read the SAME encoder slot (the beams of one window): each

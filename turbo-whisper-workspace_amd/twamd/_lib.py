@@ -41,8 +41,7 @@ EXPORTED = (
     "tw_dtw", "tw_attn_decode_cross_probs", "tw_attn_decode_cross_grouped", "tw_attn_decode_cross_grouped_ws_bytes", "tw_attn_decode_self_tab", "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
     "tw_gemm_mx", "tw_quant_mx", "tw_layernorm_mx", "tw_attn_encoder_mx", "tw_gemm_mx_set_variant", "tw_logits_select_embed",
     "tw_attn_set_lds_pad", "tw_logits_sample", "tw_token_prob", "tw_g711_decode", "tw_ima_adpcm_wav_decode",
-    "tw_kv_tab_check", "tw_debug_build", "tw_attn_decode_cross_q", "tw_resid_layernorm_packed_to",
-    "tw_attn_decode_self_q", "tw_attn_decode_self_q_tab",
+    "tw_kv_tab_check", "tw_debug_build", "tw_resid_layernorm_packed_to",
 )
 
 
@@ -130,10 +129,6 @@ _SIGS = {
     "tw_gemv_packed": ([_P, _I, _I, _P, _I, _I, _I, _I, _P, _I, _P, _I, _P], _I),
     "tw_resid_layernorm_packed": ([_P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
     "tw_resid_layernorm_packed_to": ([_P, _P, _P, _I, _P, _P, _P, _I, _I, _F, _P, _P], _I),
-    "tw_attn_decode_cross_q": ([_P, _P, _I, _P, _P, _P, _F, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P], _I),
-    "tw_attn_decode_self_q": ([_P, _P, _I, _P, _P, _P, _F, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P], _I),
-    "tw_attn_decode_self_q_tab": ([_P, _P, _I, _P, _P, _P, _F, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P],
-                                  _I),
     "tw_flac_probe": ([_P, ctypes.c_int64, ctypes.POINTER(TwFlacInfo)], _I),
     "tw_flac_decode": ([_P, ctypes.c_int64, _P, ctypes.c_int64, _I, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_g711_decode": ([_P, ctypes.c_int64, _I, _P], _I),

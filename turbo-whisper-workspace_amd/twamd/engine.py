@@ -71,7 +71,6 @@ class DecView:
     n: int
     stream: torch.cuda.Stream
     xd: torch.Tensor
-    xd2: torch.Tensor  # the residual rows between the fused cross-attention and the next LayerNorm (cross_q)
     qkvd: torch.Tensor
     qd: torch.Tensor
     attd: torch.Tensor
@@ -218,7 +217,6 @@ class WhisperEngine:
         self.kcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=bf, device=dev)
         self.vcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=bf, device=dev)
         self.xd = torch.empty(B, D, dtype=f32, device=dev)
-        self.xd2 = torch.empty(B, D, dtype=f32, device=dev)
         self.qkvd = torch.empty(B, 3 * D, dtype=bf, device=dev)
         self.qd = torch.empty(B, D, dtype=bf, device=dev)
         self.attd = torch.empty(B, D, dtype=bf, device=dev)
@@ -260,17 +258,6 @@ class WhisperEngine:
         self.fused_select = True
         # the prompt phase of a decode pass replayed as one captured graph (False: eager)
         self.prompt_graph = True
-        # the cross-attention block's residual add + LayerNorm + q projection folded into the cross-attention launch
-        # (tw_attn_decode_cross_q); not with word timestamps (the probability-recording kernel) or grouped beam rows,
-        # which keep the separate launches. False: the separate launches
-        self.fuse_cross_q = True
-        # the self-attention block's residual add + LayerNorm + q/k/v projection folded into the self-attention launch
-        # (tw_attn_decode_self_q, tw_attn_decode_self_q_tab for beam rows). With both: 31 launches per token instead
-        # of 47 (beam rows keep the grouped cross-attention and its separate LayerNorm / q launches: 39)
-        self.fuse_self_q = True
-        # (A/B overrides for measurement runs: TW_FUSE_SELF / TW_FUSE_CROSS = 0 or 1, TW_ENC_ATTN = 16 or 32)
-        self.fuse_self_q = os.environ.get("TW_FUSE_SELF", "1" if self.fuse_self_q else "0") == "1"
-        self.fuse_cross_q = os.environ.get("TW_FUSE_CROSS", "1" if self.fuse_cross_q else "0") == "1"
         # encoder attention kernel (tw_attn_set_variant) and its LDS cap in 16 KiB units (tw_attn_set_lds_pad) for an
         # encoder chunk alone / beside a running decode
         self.attn_kernel = (32, 32)  # k_attn_enc5 (round 4; 16 = k_attn_enc4, bit-identical to the enc2 form)
@@ -321,12 +308,6 @@ class WhisperEngine:
         _lib.call("tw_gemv_packed", A.data_ptr(), int(a_packed), K, Wp.data_ptr(), M, N, K, epi, out.data_ptr(),
                   ldo if ldo is not None else N, _lib.ptr(bias), splits, v.stream.cuda_stream)
         self._end_timer(rec, v.stream)
-
-    def _resid_ln_to(self, x, x_out, nparts, bias, g, b, v: DecView):
-        """x_out = x + bias + sum(parts[:nparts]) (x_out may be x); hp = LayerNorm(x_out) as a packed activation."""
-        _lib.call("tw_resid_layernorm_packed_to", x.data_ptr(), x_out.data_ptr(), v.parts.data_ptr() if nparts else None,
-                  nparts, _lib.ptr(bias), _lib.ptr(g), _lib.ptr(b), v.n, self.d.d_model, LN_EPS, v.hp.data_ptr(),
-                  v.stream.cuda_stream)
 
     def _resid_ln_p(self, R, nparts, bias, g, b, v: DecView):
         """xd += bias + sum(parts[:nparts]); hp = LayerNorm(xd) as a packed activation."""
@@ -424,7 +405,7 @@ class WhisperEngine:
         # per-view packed scratch (rows 0..n-1 of the view; pad rows zero)
         hp = torch.zeros(VIEW_ROWS * self.d.d_model, dtype=torch.bfloat16, device=self.device)
         fp = torch.zeros(VIEW_ROWS * self.d.ffn, dtype=torch.bfloat16, device=self.device)
-        return DecView(r0, n, stream or self.stream, self.xd[sl], self.xd2[sl], self.qkvd[sl], self.qd[sl], self.attd[sl],
+        return DecView(r0, n, stream or self.stream, self.xd[sl], self.qkvd[sl], self.qd[sl], self.attd[sl],
                        self.logits[sl], self.parts if parts is None else parts, self.sel_ws[sl], self.state[sl],
                        self.tokens[sl], self.ids[sl], self.pos[sl], hp, fp)
 
@@ -575,56 +556,35 @@ class WhisperEngine:
                       D, v.xd.data_ptr(), s)
         xkv_stride = 2 * r_enc * H * S_ENC * 64
         nparts, pbias = 0, None
-        fuse = self.fuse_cross_q and self._align is None and not (self._row_group > 1 and self._use_dec_row_map)
-        fuse_self = self.fuse_self_q
         PART, K4 = _lib.TW_EPI_PARTIAL_F32, DEC_SPLITS
-        # the residual rows: xd holds them at the step's start (the embedding); a fused launch reads them from one
-        # buffer and writes the updated rows to the other (its other blocks still read them), so they alternate
-        x, xo = v.xd, v.xd2
+        # (the attention blocks with their LayerNorm / projection launches folded in, tw_attn_decode_self_q /
+        # tw_attn_decode_cross_q, 31 launches per token, measured slower and archived: DESIGN §4, round 4)
         for li, L in enumerate(w.dec):
             P = self.dec_p[li]
             kc, vc = self.kcache[li, v.r0:].data_ptr(), self.vcache[li, v.r0:].data_ptr()
-            if fuse_self:  # residual + self_attn_layer_norm + q/k/v projection + attention in one launch
-                args = (x.data_ptr(), v.parts.data_ptr() if nparts else None, nparts, _lib.ptr(pbias),
-                        L.ln1_g.data_ptr(), L.ln1_b.data_ptr(), LN_EPS, L.wqkv.data_ptr(), L.bqkv.data_ptr(),
-                        xo.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc)
-                if self._kv_tab is not None:  # beam pass: histories through the position table
-                    _lib.call("tw_attn_decode_self_q_tab", *args, self._kv_tab.data_ptr(), v.r0, v.attd.data_ptr(), s)
-                else:
-                    _lib.call("tw_attn_decode_self_q", *args, v.attd.data_ptr(), s)
-                x, xo = xo, x
+            if li or not pre_embedded:
+                self._resid_ln_p(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
+            self._gemv(v.hp, True, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
+            if self._kv_tab is not None:  # beam pass: histories through the position table
+                _lib.call("tw_attn_decode_self_tab", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc,
+                          self._kv_tab.data_ptr(), v.r0, v.attd.data_ptr(), s)
             else:
-                if li or not pre_embedded:
-                    self._resid_ln_to(x, x, nparts, pbias, L.ln1_g, L.ln1_b, v)
-                self._gemv(v.hp, True, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
-                if self._kv_tab is not None:  # beam pass: histories through the position table
-                    _lib.call("tw_attn_decode_self_tab", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc,
-                              self._kv_tab.data_ptr(), v.r0, v.attd.data_ptr(), s)
-                else:
-                    _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc,
-                              v.attd.data_ptr(), s)
+                _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc,
+                          v.attd.data_ptr(), s)
             self._gemv(v.attd, False, P["wo"], R, D, D, PART, v.parts, v, splits=K4)
+            self._resid_ln_p(R, K4, L.bo, L.ln2_g, L.ln2_b, v)
+            self._gemv(v.hp, True, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
             ckv, rmap = self._cross_ptrs(li, xkv_stride, v)
-            if fuse:  # residual + encoder_attn_layer_norm + q_proj + attention in one launch
-                rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)
-                _lib.call("tw_attn_decode_cross_q", x.data_ptr(), v.parts.data_ptr(), K4, L.bo.data_ptr(),
-                          L.ln2_g.data_ptr(), L.ln2_b.data_ptr(), LN_EPS, L.wq_x.data_ptr(), L.bq_x.data_ptr(),
-                          xo.data_ptr(), R, H, S_ENC, r_enc, rmap, ckv, v.attd.data_ptr(), s)
-                self._end_timer(rec, st)
-                x, xo = xo, x
-            else:
-                self._resid_ln_to(x, x, K4, L.bo, L.ln2_g, L.ln2_b, v)
-                self._gemv(v.hp, True, P["wq_x"], R, D, D, _lib.TW_EPI_BF16, v.qd, v, bias=L.bq_x)
-                rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
-                self._cross_attend(li, R, r_enc, rmap, ckv, v)
-                self._end_timer(rec, st)
+            rec = self._begin_timer(("attn_decode_cross", 0), 2.0 * R * H * S_ENC * 64 * 2, st)  # K+V bytes read
+            self._cross_attend(li, R, r_enc, rmap, ckv, v)
+            self._end_timer(rec, st)
             self._gemv(v.attd, False, P["wo_x"], R, D, D, PART, v.parts, v, splits=K4)
-            self._resid_ln_to(x, x, K4, L.bo_x, L.ln3_g, L.ln3_b, v)
+            self._resid_ln_p(R, K4, L.bo_x, L.ln3_g, L.ln3_b, v)
             self._gemv(v.hp, True, P["w1"], R, F, D, _lib.TW_EPI_GELU_PACKED, v.fp, v, bias=L.b1)
             self._gemv(v.fp, True, P["w2"], R, D, F, PART, v.parts, v, splits=K4)
             nparts, pbias = K4, L.b2
         if with_logits:
-            self._resid_ln_to(x, x, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
+            self._resid_ln_p(R, nparts, pbias, w.dec_ln_g, w.dec_ln_b, v)
             self._gemv(v.hp, True, self.emb_p, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, v)
 
     def _cross_attend(self, li: int, R: int, r_enc: int, rmap, ckv, v: DecView) -> None:
