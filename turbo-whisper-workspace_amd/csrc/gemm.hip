@@ -927,9 +927,14 @@ __global__ TW_DEC_LB(256, 1) void k_gemv_pc(const bf16_t* __restrict__ A, int ld
 #pragma unroll
     for (int t = 0; t < MT; ++t) ap[t] = gemv_a_base<MT, APACK>(A, lda, M, K, t, lane);
     // one batch of NB steps, every load issued before the first MFMA (see k_gemv_p)
+    // MT = 4 runs the batch in two halves of two m-tiles over the same weight registers: the second half's
+    // activation fragments (L2-resident) load after the first half's MFMAs into the same VGPRs, so a batch keeps
+    // U = 5 steps of weights in flight within the 128-VGPR budget (four m-tiles at once allowed only U = 3: twice the
+    // HBM round trips per weight byte)
+    constexpr int TH = MT > 2 ? 2 : MT;
     auto batch = [&](auto NBc, int st0, int n) {
       constexpr int NB = decltype(NBc)::value;
-      bf16x8 b0[NB], b1[NB], a[NB][MT];
+      bf16x8 b0[NB], b1[NB], a[NB][TH];
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
         const int st = min(st0 + u, s1 - 1);
@@ -942,18 +947,30 @@ __global__ TW_DEC_LB(256, 1) void k_gemv_pc(const bf16_t* __restrict__ A, int ld
           b1[u] = *(const bf16x8*)(wp1 + (size_t)st * 512);
         }
 #pragma unroll
-        for (int t = 0; t < MT; ++t) a[u][t] = gemv_a_load<APACK>(ap[t], st);
+        for (int t = 0; t < TH; ++t) a[u][t] = gemv_a_load<APACK>(ap[t], st);
       }
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int u = 0; u < NB; ++u) {
-        if (u < n) {
+      for (int h = 0; h < MT / TH; ++h) {
+        if (h) {
 #pragma unroll
-          for (int t = 0; t < MT; ++t) {
-            c[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][t], b0[u], c[0][t], 0, 0, 0);
-            c[1][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][t], b1[u], c[1][t], 0, 0, 0);
+          for (int u = 0; u < NB; ++u) {
+            const int st = min(st0 + u, s1 - 1);
+#pragma unroll
+            for (int t = 0; t < TH; ++t) a[u][t] = gemv_a_load<APACK>(ap[h * TH + t], st);
           }
         }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          if (u < n) {
+#pragma unroll
+            for (int t = 0; t < TH; ++t) {
+              c[0][h * TH + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][t], b0[u], c[0][h * TH + t], 0, 0, 0);
+              c[1][h * TH + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][t], b1[u], c[1][h * TH + t], 0, 0, 0);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
     };
     using IU = std::integral_constant<int, U>;
@@ -1018,8 +1035,8 @@ static void launch_gemv_pc(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
                            int splits, hipStream_t s) {
   constexpr int GPB = 4 / KW;
   dim3 grid(tw_cdiv(tw_cdiv(tw_cdiv(N, 16), 2), GPB), splits);
-  if (M > 32)  // (fewer steps per batch: four A fragments per step)
-    hipLaunchKernelGGL((k_gemv_pc<EPI, KW, 3, APACK, 4, NTW>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
+  if (M > 32)  // (four m-tiles per step, run as two halves: see k_gemv_pc)
+    hipLaunchKernelGGL((k_gemv_pc<EPI, KW, U, APACK, 4, NTW>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
   else if (M > 16)
     hipLaunchKernelGGL((k_gemv_pc<EPI, KW, U, APACK, 2, NTW>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
   else
