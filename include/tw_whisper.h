@@ -80,12 +80,21 @@ int tw_f32_to_bf16(const float* in, uint16_t* out, long n, float scale, void* st
 
 /* ---- front end ------------------------------------------------------------------------------ */
 /* Log-mel of n_chunks 30-s windows: wave f32[n_chunks][480000] -> feats f32[n_chunks][n_mels][3000].
- * basis_cos/basis_sin: f32[400][224] periodic-Hann-windowed DFT basis (cols >= 201 zero);
- * mel_fb: f32[224][ceil32(n_mels)] slaney filterbank (rows >= 201, cols >= n_mels zero);
+ * basis_cos/basis_sin: the [400][224] periodic-Hann-windowed DFT basis (cols >= 201 zero) and
+ * mel_fb: the [224][ceil32(n_mels)] slaney filterbank (rows >= 201, cols >= n_mels zero), both f32 in "k8" order:
+ * element [k][c] of a [K][C] table at ((k/8 * C + c) * 2 + k%2) * 4 + (k%8)/2 (twamd.frontend.pack_k8);
  * maxkeys: u32[n_chunks] workspace. Replaces WhisperFeatureExtractor._torch_extract_fbank_features
  * ($TF/models/whisper/feature_extraction_whisper.py:135-168), run on the host CPU by the reference. */
 int tw_logmel(const float* wave, int n_chunks, const float* basis_cos, const float* basis_sin, const float* mel_fb,
               int n_mels, float* feats, uint32_t* maxkeys, void* stream);
+
+/* Log-mel of ONE input of any length > 200 samples (long-form generate(), > 30 s without chunking; the ASR pipeline's
+ * feature extractor with truncation=False, padding="longest"): wave f32[n_samples] -> feats f32[n_mels][feats_ld],
+ * frames 0 .. n_samples/160 - 1 written (reflect padding at the input's two ends only), the clamp at max - 8 over
+ * the whole input; columns >= n_samples/160 are left untouched (the caller zeroes them: _get_input_segment's pad).
+ * maxkey: u32[1] workspace. Basis / filterbank as tw_logmel. */
+int tw_logmel_long(const float* wave, long n_samples, const float* basis_cos, const float* basis_sin,
+                   const float* mel_fb, int n_mels, float* feats, long feats_ld, uint32_t* maxkey, void* stream);
 
 /* conv1 im2col with the seek-window slice: out bf16[R*3000][kpad], k = j*n_mels + c, value
  * feats[row_map[r]][c][seek[r] + t + j - 1] inside [0, 3000 - seek[r]), else 0. row_map/seek may
@@ -93,9 +102,20 @@ int tw_logmel(const float* wave, int n_chunks, const float* basis_cos, const flo
  * 1831-1850) + the Conv1d(k3,p1) input of WhisperEncoder.forward ($TF/.../modeling_whisper.py:618). */
 int tw_im2col_conv1(const float* feats, int n_mels, const int* row_map, const int* seek, int R, int kpad,
                     uint16_t* out, void* stream);
+/* tw_im2col_conv1 over feature rows of ld >= 3000 frames (long-form inputs): row r reads feature row row_map[r]
+ * (NULL: r) from frame seek[r], valid frames u < min(3000, max_frames[row] - seek[r]) (generate()'s seek_num_frames;
+ * max_frames[row] <= ld), zero beyond. */
+int tw_im2col_conv1_long(const float* feats, int n_mels, long ld, const int* max_frames, const int* row_map,
+                         const int* seek, int R, int kpad, uint16_t* out, void* stream);
 /* conv2 im2col (k3, stride 2, pad 1): h1 bf16[R*3000][D] -> out bf16[R*1500][3D], k = j*D + c.
  * Replaces the Conv1d(k3,s2,p1) input of modeling_whisper.py:619. */
 int tw_im2col_conv2(const uint16_t* h1, int R, int D, uint16_t* out, void* stream);
+/* conv2 + GELU + positional add without the im2col copy (the engine's path): out f32[R*1500][D] =
+ * gelu(Conv1d(k3,s2,p1)(h1)[r][t] + bias) + pos[t], h1 bf16[R][3000][D] read in place as an operand of row stride
+ * 2D. D % 32 == 0. The D elements in front of h1 must be readable memory (the caller allocates one row before the
+ * first frame; its contents do not matter). Replaces modeling_whisper.py:566-568 (conv2, GELU, embed_positions). */
+int tw_conv2_gemm(const uint16_t* h1, int R, int D, const uint16_t* W, const float* bias, const float* pos, float* out,
+                  void* stream);
 
 /* ---- dense ops ------------------------------------------------------------------------------ */
 /* C = A[M][K] . W[N][K]^T (bf16, f32 accumulate) with epilogue `epi` (TW_EPI_*). K % 64 == 0.
@@ -245,6 +265,14 @@ int tw_attn_decode_self(const uint16_t* qkv, int B, int H, int max_pos, const in
  * TW_ERR_ARG naming the row instead of racing. */
 int tw_attn_decode_self_tab(const uint16_t* qkv, int B, int H, int max_pos, const int* pos, uint16_t* k_cache,
                             uint16_t* v_cache, const int* kv_tab, int row0, uint16_t* out, void* stream);
+/* tw_attn_decode_self / _tab with left-padded prompts (condition_on_prev_tokens over a batch: generate()'s
+ * decoder_attention_mask, generation_whisper.py:1893-1908): kv_start int32[B] (device) = row b's pad count; a query at
+ * pos[b] >= kv_start[b] attends keys kv_start[b] .. pos[b] only (the pad positions still take their positions). */
+int tw_attn_decode_self_masked(const uint16_t* qkv, int B, int H, int max_pos, const int* pos, uint16_t* k_cache,
+                               uint16_t* v_cache, const int* kv_start, uint16_t* out, void* stream);
+int tw_attn_decode_self_tab_masked(const uint16_t* qkv, int B, int H, int max_pos, const int* pos, uint16_t* k_cache,
+                                   uint16_t* v_cache, const int* kv_tab, int row0, const int* kv_start, uint16_t* out,
+                                   void* stream);
 /* The contract of tw_attn_decode_self_tab as a check: bad int32[B] (device) receives, per row b of a launch with the
  * same (kv_tab, pos, row0, B, max_pos), the number of history entries that name a (row, position) that launch
  * writes (0 everywhere = the launch is race-free). Asynchronous on `stream`. */

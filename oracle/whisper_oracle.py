@@ -137,17 +137,23 @@ def mel_filters(n_mels: int) -> np.ndarray:
     return fb * (2.0 / (pts[2: n_mels + 2] - pts[:n_mels]))[None, :]
 
 
-def log_mel(wave: np.ndarray, n_mels: int) -> np.ndarray:
-    """One 30-s window (padded/truncated to 480000) -> f32 [n_mels][3000]."""
-    x = np.zeros(480000, np.float64)
-    w = np.asarray(wave, np.float32)[:480000]
-    x[: len(w)] = w
+def log_mel(wave: np.ndarray, n_mels: int, long: bool = False) -> np.ndarray:
+    """One 30-s window (padded/truncated to 480000) -> f32 [n_mels][3000]. long: the whole input as it is (the
+    feature extractor with truncation=False, padding="longest" on one sequence, asr:450-457) -> [n_mels][n // 160],
+    the max - 8 clamp over all of it (feature_extraction_whisper.py:135-168)."""
+    if long:
+        x = np.asarray(wave, np.float32).astype(np.float64)
+    else:
+        x = np.zeros(480000, np.float64)
+        w = np.asarray(wave, np.float32)[:480000]
+        x[: len(w)] = w
+    nfr = len(x) // 160
     xp = np.pad(x, (200, 200), mode="reflect")
-    idx = np.arange(3001)[:, None] * 160 + np.arange(400)[None, :]
+    idx = np.arange(nfr + 1)[:, None] * 160 + np.arange(400)[None, :]
     n = np.arange(400)
     win = 0.5 - 0.5 * np.cos(2 * np.pi * n / 400)
     spec = np.fft.rfft(xp[idx] * win[None, :], axis=1)          # [3001][201]
-    mag = (np.abs(spec[:-1]) ** 2).T                               # [201][3000]
+    mag = (np.abs(spec[:-1]) ** 2).T                               # [201][frames]
     mel = mel_filters(n_mels).T.astype(np.float32).astype(np.float64) @ mag
     ls = np.log10(np.maximum(mel, 1e-10))
     ls = np.maximum(ls, ls.max() - 8.0)
@@ -322,13 +328,16 @@ class WhisperOracle:
             x = (x + self._lin_mx(mx_round(_gelu(self._lin_mx(h, f"{p}.fc1"))), f"{p}.fc2")).astype(np.float32)
         return _ln(x, sd["model.encoder.layer_norm.weight"], sd["model.encoder.layer_norm.bias"]).astype(np.float32)
 
-    def new_cache(self, enc: np.ndarray) -> dict:
+    def new_cache(self, enc: np.ndarray, pos0: int = 0) -> dict:
+        """pos0: the position of the first token fed — a row left padded by pos0 tokens that its queries never attend
+        (generate()'s decoder_attention_mask over a conditioned batch) computes exactly this: pads take positions,
+        nothing else."""
         cross = []
         for i in range(self.L_dec):
             p = f"model.decoder.layers.{i}.encoder_attn"
             cross.append((self._lin(enc, f"{p}.k_proj", bias=False), self._lin(enc, f"{p}.v_proj")))
         return {"self": [(np.zeros((0, self.D), np.float32), np.zeros((0, self.D), np.float32))
-                         for _ in range(self.L_dec)], "cross": cross, "len": 0}
+                         for _ in range(self.L_dec)], "cross": cross, "len": pos0}
 
     def decoder_step(self, token: int, cache: dict) -> np.ndarray:
         """One token at position cache['len'] -> f32 logits [V] (updates cache)."""
@@ -616,6 +625,15 @@ def detect_language(model: WhisperOracle, enc: np.ndarray, g: GenCfg) -> int:
     return int(np.argmax(m))
 
 
+def segment_input(feats: np.ndarray, seek: int, max_frames: int = 3000) -> np.ndarray:
+    """_get_input_segment (generation_whisper.py:1831-1850): feats[:, seek : seek + seek_num_frames], seek_num_frames =
+    min(max_frames - seek, 3000), zero padded to 3000 frames."""
+    snf = min(max_frames - seek, 3000)
+    seg = np.zeros((feats.shape[0], 3000), np.float32)
+    seg[:, :snf] = feats[:, seek: seek + snf]
+    return seg
+
+
 def retrieve_segment(seq, seek_num_frames, tb):
     ts = [t >= tb for t in seq]
     single = ts[-2:] == [False, True]
@@ -631,7 +649,7 @@ def retrieve_segment(seq, seek_num_frames, tb):
 def generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, task: Optional[str] = "transcribe",
              language: Optional[int] = None, return_timestamps: bool = True, max_new_tokens: Optional[int] = None,
              encoder_cache: Optional[dict] = None, num_beams: int = 1, alignment_heads=None,
-             num_frames: Optional[int] = None, median_width: int = 7):
+             num_frames: Optional[int] = None, median_width: int = 7, max_frames: int = 3000):
     """Short-form WhisperGenerationMixin.generate for ONE 3000-frame window (greedy, or beam search with
     num_beams > 1). Returns (final token sequence, language id); with alignment_heads (greedy only) also the
     token-level timestamps of return_token_timestamps=True (the top-level "token_timestamps": every pass's DTW
@@ -639,8 +657,7 @@ def generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, task: Optional[
     feats = np.asarray(feats, np.float32)
 
     def enc_at(seek):
-        seg = np.zeros_like(feats)
-        seg[:, : 3000 - seek] = feats[:, seek:]
+        seg = segment_input(feats, seek, max_frames)
         if encoder_cache is not None and seek in encoder_cache:
             return encoder_cache[seek]
         e = model.encode(seg)
@@ -664,7 +681,7 @@ def generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, task: Optional[
     seek, out = 0, []
     tts: List[float] = []
     pass_seeks: List[int] = []
-    while seek < 3000:
+    while seek < max_frames:
         xattn = {} if alignment_heads is not None else None
         if num_beams > 1:
             seq = beam_pass(model, enc_at(seek), prompt, max_new, g, return_timestamps, num_beams)
@@ -678,7 +695,7 @@ def generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, task: Optional[
             raw_ts = token_timestamps(w, P, nf, median_width)
         if seq and seq[-1] == g.eot:
             seq = seq[:-1]
-        toks, off = retrieve_segment(seq, 3000 - seek, g.ts_begin)
+        toks, off = retrieve_segment(seq, min(max_frames - seek, 3000), g.ts_begin)
         out += toks
         if raw_ts is not None:
             tts += [float(x) for x in raw_ts[P: P + len(toks)]]
@@ -844,16 +861,18 @@ def process_logits_no_rule(scores: np.ndarray, sampled: Sequence[int], g: GenCfg
 
 def replay_generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, passes: Sequence[Sequence[int]],
                     lang: Optional[int], task: Optional[str] = "transcribe", return_timestamps: bool = True,
-                    max_new_tokens: Optional[int] = None, tau: float = 0.3, mx: bool = False) -> dict:
+                    max_new_tokens: Optional[int] = None, tau: float = 0.3, mx: bool = False,
+                    max_frames: int = 3000, prefixes: Optional[Sequence] = None) -> dict:
     """Follow a device decode of ONE window (its raw per-seek-pass token lists and detected language) through the
     f32 reference, checking every decision with decision_ok. Returns {"ok", "decisions", "exact", "first_bad"}.
-    mx: the reference encoder is encode_mx (config 5's MX fp8 projections)."""
+    mx: the reference encoder is encode_mx (config 5's MX fp8 projections). max_frames: the input's feature frames
+    (long-form). prefixes: per pass None or (tokens, pads) — the condition_on_prev_tokens prompt the device fed ahead of
+    the init tokens (its pad tokens left out: new_cache(pos0=pads))."""
     feats = np.asarray(feats, np.float32)
     stats = {"ok": True, "decisions": 0, "exact": 0, "first_bad": None}
 
     def enc_at(seek):
-        seg = np.zeros_like(feats)
-        seg[:, : 3000 - seek] = feats[:, seek:]
+        seg = segment_input(feats, seek, max_frames)
         return model.encode_mx(seg) if mx else model.encode(seg)
 
     def check(scores, sampled, tok, use_ts):
@@ -886,24 +905,29 @@ def replay_generate(model: WhisperOracle, feats: np.ndarray, g: GenCfg, passes: 
     P = len(prompt)
     max_new = max_new_tokens if max_new_tokens is not None else min(g.max_length + P, 448) - P
     seek = 0
-    for seq_raw in passes:
-        if seek >= 3000:
+    for k, seq_raw in enumerate(passes):
+        if seek >= max_frames:
             stats["ok"], stats["first_bad"] = False, ("extra pass", seek, None)
             break
-        cache = model.new_cache(enc_at(seek))
-        for t in prompt[:-1]:
+        pf = prefixes[k] if prefixes is not None else None
+        toks_p, pads = (list(pf[0][pf[1]:]), int(pf[1])) if pf is not None else ([], 0)
+        cache = model.new_cache(enc_at(seek), pos0=pads)
+        for t in toks_p + prompt[:-1]:
             model.decoder_step(t, cache)
         logits = model.decoder_step(prompt[-1], cache)
+        mn = max_new
+        if pf is not None and max_new_tokens is None:
+            mn = min(g.max_length + P + len(pf[0]), 448) - P - len(pf[0])
         out: List[int] = []
         for tok in seq_raw:
             check(logits, out, int(tok), return_timestamps)
             out.append(int(tok))
-            if tok == g.eot or len(out) >= max_new:
+            if tok == g.eot or len(out) >= mn:
                 break
             logits = model.decoder_step(int(tok), cache)
         seq = out[:-1] if out and out[-1] == g.eot else out
-        _, off = retrieve_segment(seq, 3000 - seek, g.ts_begin)
+        _, off = retrieve_segment(seq, min(max_frames - seek, 3000), g.ts_begin)
         seek += off
-    if seek < 3000:
+    if seek < max_frames:
         stats["ok"], stats["first_bad"] = False, ("missing pass", seek, None)
     return stats

@@ -12,6 +12,8 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
   word.npz/.json    token-level timestamps (cross-attention DTW) of generate(return_token_timestamps=True) and
                     the pipeline's return_timestamps="word" output, plus HF's _median_filter / _dynamic_time_warping
                     on seeded random matrices
+  longform.json     long-form (unchunked > 30 s) pipeline outputs and condition_on_prev_tokens, with every seek
+                    pass's decoder prompt and raw output (spied from generate_with_fallback)
   fallback.json     the temperature-fallback criteria (compression ratio, avg logprob, no-speech probability) of
                     every seek pass and a deterministic no-speech skip, spied from transformers' generate()
   tiny.npz          whisper-tiny.en (configs[0], English-only) encoder rows, teacher-forced logits, generate() passes
@@ -873,6 +875,64 @@ def make_sweep(out):
                     "output": _jsonable(r)})
     with open(os.path.join(out, "sweep.json"), "w") as f:
         json.dump({"dims": "test-mini", "cases": res}, f, indent=1)
+
+
+LONGFORM_CASES = [  # name, pipeline kwargs, generate_kwargs, return_timestamps
+    ("long_greedy", {}, {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40}, True),
+    ("long_beam3", {}, {"task": "transcribe", "num_beams": 3, "max_new_tokens": 24}, True),
+    ("long_cond", {}, {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40, "condition_on_prev_tokens": True},
+     True),
+    ("long_no_ts", {}, {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40}, False),
+    ("chunk30_cond_b3", dict(chunk_length_s=30, stride_length_s=0, batch_size=3),
+     {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40, "condition_on_prev_tokens": True}, True),
+]
+
+
+def make_longform(out):
+    """Long-form input (75 s, no chunk_length_s: generate()'s sequential seek loop over the features of the whole
+    input, asr:450-457) and condition_on_prev_tokens at test-mini: the pipeline outputs (or the error it raises), the
+    long-form features of the feature extractor (truncation=False, padding="longest"), and per case every seek pass's
+    decoder prompt and raw output as generate_with_fallback saw them (a spy: conditioning prompts are built from the
+    previous passes' segments, generation_whisper.py:1853-1918)."""
+    from transformers import AutomaticSpeechRecognitionPipeline, WhisperFeatureExtractor
+    from transformers.models.whisper import generation_whisper as gw
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    pipe = AutomaticSpeechRecognitionPipeline(model=m, feature_extractor=fe, tokenizer=hf_tokenizer(gen.special),
+                                              device=-1)
+    audio = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)]).astype(np.float32)
+    f = fe(audio, sampling_rate=16000, truncation=False, padding="longest", return_tensors="np")["input_features"][0]
+    feats = {"shape": list(f.shape), "sub": f[:, ::97].tolist(), "colsum": f.sum(axis=0)[::7].tolist()}
+    orig = gw.WhisperGenerationMixin.generate_with_fallback
+    log = []
+
+    def spy(self, *a, **kw):
+        r = orig(self, *a, **kw)
+        log.append({"prompts": kw["decoder_input_ids"].tolist(), "rows": [int(i) for i in kw["batch_idx_map"]],
+                    "seek": kw["seek"].tolist(), "sequences": [x.tolist() for x in r[0]]})
+        return r
+
+    res = []
+    gw.WhisperGenerationMixin.generate_with_fallback = spy
+    try:
+        for name, kw, gk, ts in LONGFORM_CASES:
+            log.clear()
+            c = {"name": name, "kwargs": kw, "generate_kwargs": gk, "return_timestamps": ts}
+            try:
+                c["output"] = _jsonable(pipe(audio.copy(), generate_kwargs=dict(gk), return_timestamps=ts, **kw))
+            except Exception as e:  # noqa: BLE001 - recorded as the reference would surface it
+                c["error"] = {"type": type(e).__name__, "message": str(e)}
+            c["passes"] = list(log)
+            res.append(c)
+    finally:
+        gw.WhisperGenerationMixin.generate_with_fallback = orig
+    with open(os.path.join(out, "longform.json"), "w") as fo:
+        json.dump({"dims": "test-mini", "audio": "speech_like(40,5)+white_noise(35,11)", "n_samples": len(audio),
+                   "features": feats, "cases": res}, fo)
 
 
 TINY_CLIPS = ("speech30", "noise12")

@@ -353,6 +353,7 @@ class _FakeEngine:
     def run_batches(self, sizes, load=None, batch_kwargs=None, **kw):
         from twamd.frontend import Window
         out, self.batch_langs, self.batch_passes, self.batch_token_timestamps = [], [], [], []
+        self.batch_prefixes = []
         for k, n in enumerate(sizes):
             load(k)
             rows = self.wave[:n].numpy()
@@ -360,6 +361,7 @@ class _FakeEngine:
             out.append(toks)
             self.batch_langs.append([None] * n)
             self.batch_passes.append([[t] for t in toks])
+            self.batch_prefixes.append([[None] for _ in toks])
         self.sizes.append(list(sizes))
         return out
 

@@ -11,7 +11,7 @@ import torch
 
 from oracle import whisper_oracle as wo
 from twamd import _lib
-from twamd.frontend import dft_basis, mel_table
+from twamd.frontend import dft_basis, mel_table, pack_k8
 from twamd.synth_audio import silence, speech_like, white_noise
 
 pytestmark = pytest.mark.gpu
@@ -51,7 +51,7 @@ def test_logmel_vs_oracle(n_mels):
     w = torch.from_numpy(wave).to(DEV)
     feats = torch.empty(B, n_mels, 3000, device=DEV)
     mk = torch.empty(B, dtype=torch.int32, device=DEV)
-    bc, bs, fb = (torch.from_numpy(a).to(DEV) for a in (c, s, mel_table(n_mels)))
+    bc, bs, fb = (torch.from_numpy(pack_k8(a)).to(DEV) for a in (c, s, mel_table(n_mels)))
     _lib.call("tw_logmel", w.data_ptr(), B, bc.data_ptr(), bs.data_ptr(), fb.data_ptr(), n_mels, feats.data_ptr(),
               mk.data_ptr(), S())
     got = feats.cpu().numpy()
@@ -88,6 +88,38 @@ def test_gemm_vs_torch(M, N, K, epi, variant):
         ref = base + ref
     tol = 2e-2 if out.dtype == torch.bfloat16 else 2e-3  # bf16 output rounding / f32 accumulation order
     torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("variant", [1, 5], ids=["big", "8p"])
+@pytest.mark.parametrize("R,D", [(3, 1280), (1, 384), (40, 64)])
+def test_conv2_implicit_gemm_vs_torch_conv1d(R, D, variant):
+    """tw_conv2_gemm (h1 read in place at row stride 2 D, t = 0 rows recomputed from taps 1-2) against torch's fp32
+    Conv1d(k3, s2, p1) + GELU + positional rows, and against the im2col + GEMM path it replaces. R = 40 puts the
+    t = 0 recompute on the large-M kernel (> 32 rows)."""
+    _lib.call("tw_gemm_set_variant", variant)
+    h1_rows = rand_bf16(R * 3000 + 1, D, seed=31)  # (the row in front: arbitrary, must not reach the output)
+    h1 = h1_rows[1:]
+    W = rand_bf16(D, 3 * D, scale=(3 * D) ** -0.5, seed=32)  # [out][j * D + c]
+    bias = torch.randn(D, device=DEV) * 0.1
+    pos = torch.randn(1500, D, device=DEV) * 0.5
+    out = torch.full((R * 1500, D), float("nan"), device=DEV)
+    _lib.call("tw_conv2_gemm", h1.data_ptr(), R, D, W.data_ptr(), bias.data_ptr(), pos.data_ptr(), out.data_ptr(), S())
+    a2 = torch.empty(R * 1500, 3 * D, dtype=torch.bfloat16, device=DEV)
+    _lib.call("tw_im2col_conv2", h1.data_ptr(), R, D, a2.data_ptr(), S())
+    old = torch.empty(R * 1500, D, device=DEV)
+    _lib.call("tw_gemm_bf16", a2.data_ptr(), W.data_ptr(), R * 1500, D, 3 * D, 3 * D, 3 * D, _lib.TW_EPI_GELU_POS_F32,
+              old.data_ptr(), D, bias.data_ptr(), pos.data_ptr(), 1500, None, S())
+    _lib.call("tw_gemm_set_variant", 1)
+    wconv = W.float().view(D, 3, D).permute(0, 2, 1)  # [out][in][tap]
+    x = h1.float().view(R, 3000, D).transpose(1, 2)
+    ref = torch.nn.functional.conv1d(x, wconv, bias, stride=2, padding=1)  # [R][D][1500]
+    ref = (torch.nn.functional.gelu(ref).transpose(1, 2) + pos).reshape(R * 1500, D)
+    assert torch.isfinite(out).all()
+    torch.testing.assert_close(out, ref, atol=2e-3, rtol=2e-3)  # f32 accumulation order only
+    torch.testing.assert_close(out, old, atol=2e-3, rtol=2e-3)
+    # rows t >= 1 run the same kernel over the same products in the same order as the im2col path: bit-identical
+    o3, d3 = out.view(R, 1500, D), old.view(R, 1500, D)
+    assert torch.equal(o3[:, 1:], d3[:, 1:])
 
 
 @pytest.mark.parametrize("M,N,K,splits", [(24, 1280, 1280, 4), (24, 1280, 5120, 4), (1, 384, 1536, 3),

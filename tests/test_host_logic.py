@@ -11,7 +11,7 @@ from hypothesis import strategies as hs
 from oracle import whisper_oracle as wo
 from twamd import audio
 from twamd.config import PRESETS, GenerationSettings, SpecialTokens
-from twamd.frontend import chunk_windows, dft_basis, mel_filterbank, mel_table
+from twamd.frontend import chunk_windows, dft_basis, mel_filterbank, mel_table, pack_k8
 from twamd.pipeline import TurboTranscriber
 from twamd.segments import retrieve_segment, strip_generated
 from twamd.synth_audio import speech_like, white_noise
@@ -91,6 +91,15 @@ def test_frontend_tables():
     assert c.shape == (400, 224) and not c[:, 201:].any() and not s[:, 201:].any()
     t = mel_table(80)
     assert t.shape == (224, 96) and not t[201:].any() and not t[:, 80:].any()
+
+
+def test_pack_k8_index_formula():
+    """tw_logmel's "k8" operand order (include/tw_whisper.h): [k][c] at ((k/8 * C + c) * 2 + k%2) * 4 + (k%8)/2."""
+    a = np.arange(400 * 224, dtype=np.float32).reshape(400, 224)
+    p = pack_k8(a).ravel()
+    k, c = np.meshgrid(np.arange(400), np.arange(224), indexing="ij")
+    idx = ((k // 8 * 224 + c) * 2 + k % 2) * 4 + (k % 8) // 2
+    assert np.array_equal(p[idx], a)
 
 
 def test_wav_roundtrip(tmp_path):

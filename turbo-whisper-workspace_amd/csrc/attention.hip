@@ -851,11 +851,15 @@ struct TabRows {
   }
 };
 
+// kv_start (NULL: none): per row the first position its queries attend once they are past it — the left padding of a
+// prompt conditioned on previous segments (generate()'s decoder_attention_mask, generation_whisper.py:1893-1908): pad
+// positions are fed (they take positions, as transformers' cache positions do) but masked out of every later query.
 template <bool TAB>
 __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__ qkv, int D, int max_pos,
                                                            const int* __restrict__ pos, bf16_t* __restrict__ kc,
                                                            bf16_t* __restrict__ vc, const int* __restrict__ kv_tab,
-                                                           int row0, bf16_t* __restrict__ out) {
+                                                           int row0, bf16_t* __restrict__ out,
+                                                           const int* __restrict__ kv_start) {
   TW_DEC_PRIO();
   __shared__ float part[32 * 64];
   __shared__ float red[16];
@@ -865,6 +869,8 @@ __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__
   const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x;
   const int tid = threadIdx.x, g = tid >> 3, gl = tid & 7, lane = tid & 63, wid = tid >> 6;
   const int t = pos[b];
+  int ks = kv_start ? kv_start[b] : 0;  // first attended key (0 while the query itself is a pad position)
+  ks = t >= ks ? ks : 0;
   const bf16_t* row = qkv + (size_t)b * 3 * D + h * 64;
   bf16_t* K = kc + ((size_t)b * H + h) * max_pos * 64;
   bf16_t* V = vc + ((size_t)b * H + h) * max_pos * 64;
@@ -876,11 +882,12 @@ __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__
     }
     __threadfence_block();
     __syncthreads();
+    // keys ks .. t: the cache viewed from position ks
     if constexpr (TAB) {
-      dec_attend_off(qf, K, V, t + 1, sc, part, red, outv,
-                     TabRows{kv_tab + (size_t)(row0 + b) * max_pos, (long)H * max_pos * 64, row0 + b});
+      dec_attend_off(qf, K + (size_t)ks * 64, V + (size_t)ks * 64, t + 1 - ks, sc, part, red, outv,
+                     TabRows{kv_tab + (size_t)(row0 + b) * max_pos + ks, (long)H * max_pos * 64, row0 + b});
     } else {
-      dec_attend(qf, K, V, t + 1, sc, part, red, outv);
+      dec_attend(qf, K + (size_t)ks * 64, V + (size_t)ks * 64, t + 1 - ks, sc, part, red, outv);
     }
     if (tid < 64) out[(size_t)b * D + h * 64 + tid] = f32_to_bf16(outv[tid]);
     return;
@@ -923,7 +930,7 @@ __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__
     d += __shfl_xor(d, 1, 64);
     d += __shfl_xor(d, 2, 64);
     d += __shfl_xor(d, 4, 64);
-    p[u] = key <= t ? d : -INFINITY;
+    p[u] = key <= t && key >= ks ? d : -INFINITY;
     mx = fmaxf(mx, p[u]);
   }
   mx = wave_max(mx);
@@ -941,7 +948,8 @@ __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int u = 0; u < DS2_U; ++u) {
-    if (u * 32 + g > t) continue;  // (the clamped rows past t may hold anything on the first step: never 0 * them)
+    // (the clamped rows past t may hold anything on the first step, masked pad rows anything at all: never 0 * them)
+    if (u * 32 + g > t || u * 32 + g < ks) continue;
     const uint4 vx = u * 32 + g == t ? vr : vv[u];
     const bf16_t* ve = (const bf16_t*)&vx;
 #pragma unroll
@@ -966,8 +974,19 @@ extern "C" int tw_attn_decode_self(const bf16_t* qkv, int B, int H, int max_pos,
   TW_REQUIRE(qkv && pos && k_cache && v_cache && out && B > 0 && H > 0, "tw_attn_decode_self: bad args");
   TW_REQUIRE(max_pos <= DA_SELF_MAXK, "tw_attn_decode_self: max_pos %d > %d", max_pos, DA_SELF_MAXK);
   hipLaunchKernelGGL(k_attn_decode_self2<false>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos,
-                     pos, k_cache, v_cache, nullptr, 0, out);
+                     pos, k_cache, v_cache, nullptr, 0, out, (const int*)nullptr);
   return tw_check_launch("tw_attn_decode_self");
+}
+
+extern "C" int tw_attn_decode_self_masked(const bf16_t* qkv, int B, int H, int max_pos, const int* pos,
+                                          bf16_t* k_cache, bf16_t* v_cache, const int* kv_start, bf16_t* out,
+                                          void* stream) {
+  TW_REQUIRE(qkv && pos && k_cache && v_cache && kv_start && out && B > 0 && H > 0,
+             "tw_attn_decode_self_masked: bad args");
+  TW_REQUIRE(max_pos <= DA_SELF_MAXK, "tw_attn_decode_self_masked: max_pos %d > %d", max_pos, DA_SELF_MAXK);
+  hipLaunchKernelGGL(k_attn_decode_self2<false>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos,
+                     pos, k_cache, v_cache, nullptr, 0, out, kv_start);
+  return tw_check_launch("tw_attn_decode_self_masked");
 }
 
 // The position table's precondition (tw_whisper.h, tw_attn_decode_self_tab): no history entry of a row of the launch
@@ -1034,8 +1053,8 @@ static int tw_debug_tab_guard(const int* kv_tab, const int* pos, int row0, int B
 }
 #endif
 
-extern "C" int tw_attn_decode_self_tab(const bf16_t* qkv, int B, int H, int max_pos, const int* pos, bf16_t* k_cache,
-                                       bf16_t* v_cache, const int* kv_tab, int row0, bf16_t* out, void* stream) {
+static int attn_self_tab(const bf16_t* qkv, int B, int H, int max_pos, const int* pos, bf16_t* k_cache,
+                         bf16_t* v_cache, const int* kv_tab, int row0, const int* kv_start, bf16_t* out, void* stream) {
   TW_REQUIRE(qkv && pos && k_cache && v_cache && kv_tab && out && B > 0 && H > 0 && row0 >= 0,
              "tw_attn_decode_self_tab: bad args");
   TW_REQUIRE(max_pos <= DA_SELF_MAXK, "tw_attn_decode_self_tab: max_pos %d > %d", max_pos, DA_SELF_MAXK);
@@ -1043,8 +1062,20 @@ extern "C" int tw_attn_decode_self_tab(const bf16_t* qkv, int B, int H, int max_
   if (int rc = tw_debug_tab_guard(kv_tab, pos, row0, B, max_pos, (hipStream_t)stream)) return rc;
 #endif
   hipLaunchKernelGGL(k_attn_decode_self2<true>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos,
-                     pos, k_cache, v_cache, kv_tab, row0, out);
+                     pos, k_cache, v_cache, kv_tab, row0, out, kv_start);
   return tw_check_launch("tw_attn_decode_self_tab");
+}
+
+extern "C" int tw_attn_decode_self_tab(const bf16_t* qkv, int B, int H, int max_pos, const int* pos, bf16_t* k_cache,
+                                       bf16_t* v_cache, const int* kv_tab, int row0, bf16_t* out, void* stream) {
+  return attn_self_tab(qkv, B, H, max_pos, pos, k_cache, v_cache, kv_tab, row0, nullptr, out, stream);
+}
+
+extern "C" int tw_attn_decode_self_tab_masked(const bf16_t* qkv, int B, int H, int max_pos, const int* pos,
+                                              bf16_t* k_cache, bf16_t* v_cache, const int* kv_tab, int row0,
+                                              const int* kv_start, bf16_t* out, void* stream) {
+  TW_REQUIRE(kv_start, "tw_attn_decode_self_tab_masked: kv_start is NULL");
+  return attn_self_tab(qkv, B, H, max_pos, pos, k_cache, v_cache, kv_tab, row0, kv_start, out, stream);
 }
 
 // 1 in a library built with -DTW_DEBUG=1 (the position-table guard above is compiled in), else 0.

@@ -78,8 +78,11 @@ extern "C" int tw_layernorm(const float* x, const float* gamma, const float* bet
 
 // conv1 im2col: A[r*3000 + t][k], k = j*n_mels + c (kw-major, weights reordered to match),
 // value = seg[c][t + j - 1] where seg = feats[row_map[r]][:, seek[r]:] zero-padded to 3000 frames.
+// (feats rows of ld frames; maxf: per-row feature length — the seek window is feats[seek : min(seek + 3000, maxf)],
+// _get_input_segment's seek_num_frames; NULL = 3000, the 30-s windows)
 __global__ void k_im2col_conv1(const float* __restrict__ feats, int n_mels, const int* __restrict__ row_map,
-                               const int* __restrict__ seek, int R, int kpad, bf16_t* __restrict__ out) {
+                               const int* __restrict__ seek, int R, int kpad, bf16_t* __restrict__ out, long ld,
+                               const int* __restrict__ maxf) {
   const long total = (long)R * 3000 * kpad;
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long stride = (long)gridDim.x * blockDim.x;
@@ -92,10 +95,8 @@ __global__ void k_im2col_conv1(const float* __restrict__ feats, int n_mels, cons
       const int j = k / n_mels, c = k - j * n_mels;
       const int sk = seek ? seek[r] : 0;
       const int u = t + j - 1;
-      if (u >= 0 && u < 3000 - sk) {
-        const int chunk = row_map ? row_map[r] : r;
-        v = feats[((size_t)chunk * n_mels + c) * 3000 + sk + u];
-      }
+      const int chunk = row_map ? row_map[r] : r;
+      if (u >= 0 && u < min(3000, (maxf ? maxf[chunk] : 3000) - sk)) v = feats[((size_t)chunk * n_mels + c) * ld + sk + u];
     }
     out[i] = f32_to_bf16(v);
   }
@@ -108,8 +109,20 @@ extern "C" int tw_im2col_conv1(const float* feats, int n_mels, const int* row_ma
   unsigned grid = tw_cdiv(total, 256);
   if (grid > 16384) grid = 16384;
   hipLaunchKernelGGL(k_im2col_conv1, dim3(grid), dim3(256), 0, (hipStream_t)stream, feats, n_mels, row_map, seek, R,
-                     kpad, out);
+                     kpad, out, 3000L, (const int*)nullptr);
   return tw_check_launch("tw_im2col_conv1");
+}
+
+extern "C" int tw_im2col_conv1_long(const float* feats, int n_mels, long ld, const int* max_frames, const int* row_map,
+                                    const int* seek, int R, int kpad, bf16_t* out, void* stream) {
+  TW_REQUIRE(feats && max_frames && seek && out && R > 0 && kpad >= 3 * n_mels && kpad % 64 == 0 && ld >= 3000,
+             "tw_im2col_conv1_long: bad args");
+  long total = (long)R * 3000 * kpad;
+  unsigned grid = tw_cdiv(total, 256);
+  if (grid > 16384) grid = 16384;
+  hipLaunchKernelGGL(k_im2col_conv1, dim3(grid), dim3(256), 0, (hipStream_t)stream, feats, n_mels, row_map, seek, R,
+                     kpad, out, ld, max_frames);
+  return tw_check_launch("tw_im2col_conv1_long");
 }
 
 // conv2 im2col (stride 2): A[r*1500 + t][j*D + c] = h1[r*3000 + 2t + j - 1][c], zero outside [0, 3000).

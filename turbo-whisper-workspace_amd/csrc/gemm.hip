@@ -459,7 +459,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
   for (int h = 0; h < 4; ++h) {
     const int r0 = (h < 2 ? m0 : n0) + 128 * (h & 1), lim = h < 2 ? M : N, ld = h < 2 ? lda : ldw;
     const int rows = max(0, min(128, lim - r0));
-    rs[h] = tw_uniform_rsrc((h < 2 ? A : W) + (size_t)r0 * ld, rows * ld * 2);
+    // (the last row's K elements: an operand whose rows overlap, ld < K, tw_conv2_gemm's implicit im2col)
+    rs[h] = tw_uniform_rsrc((h < 2 ? A : W) + (size_t)r0 * ld, rows ? ((rows - 1) * ld + K) * 2 : 0);
   }
   unsigned voff[2][2];
 #pragma unroll
@@ -1131,6 +1132,26 @@ extern "C" int tw_gemm_bf16(const bf16_t* A, const bf16_t* W, int M, int N, int 
       return launch_gemm<TW_EPI_CROSSKV>(A, W, M, N, K, lda, ldw, ea, s);
     default: tw_set_error("tw_gemm_bf16: unknown epilogue %d", epi); return TW_ERR_ARG;
   }
+}
+
+// Encoder conv2 + GELU + positional add as an implicit GEMM (modeling_whisper.py:566-568: Conv1d(D, D, 3, stride 2,
+// padding 1)). Output frame t of window r reads input frames 2t-1, 2t, 2t+1; in the time-major h1 [R][3000][D]
+// those are 3 D contiguous elements starting at frame 2t-1, so the A operand is h1 itself read at a row stride of
+// 2 D (rows overlapping by D) — no im2col copy. Frame -1 is the zero padding, which that view does not see: the
+// t = 0 row of window r takes its first tap from window r-1's last frame (window 0: from the row in front of h1), so
+// those R rows are recomputed afterwards from taps 1-2 alone (K = 2 D, A rows one window apart).
+extern "C" int tw_conv2_gemm(const bf16_t* h1, int R, int D, const bf16_t* W, const float* bias, const float* pos,
+                             float* out, void* stream) {
+  TW_REQUIRE(h1 && W && bias && pos && out, "tw_conv2_gemm: null pointer");
+  TW_REQUIRE(R > 0 && D > 0 && D % 32 == 0, "tw_conv2_gemm: R=%d D=%d (D %% 32 required)", R, D);
+  hipStream_t s = (hipStream_t)stream;
+  EpiArgs ea{out, D, bias, pos, 1500, 0, 0, 0, 0};
+  ea.group_m = tw_group_for(D);
+  int rc = launch_gemm<TW_EPI_GELU_POS_F32>(h1 - D, W, R * 1500, D, 3 * D, 2 * D, 3 * D, ea, s);
+  if (rc) return rc;
+  EpiArgs e0{out, 1500 * D, bias, pos, 1, 0, 0, 0, 0};  // row r -> output row 1500 r; positional row 0
+  e0.group_m = 1;
+  return launch_gemm<TW_EPI_GELU_POS_F32>(h1, W + D, R, D, 2 * D, 3000 * D, 3 * D, e0, s);
 }
 
 extern "C" int tw_gemm_bf16_partial(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int ldw,

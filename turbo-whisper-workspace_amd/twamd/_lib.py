@@ -41,7 +41,8 @@ EXPORTED = (
     "tw_dtw", "tw_attn_decode_cross_probs", "tw_attn_decode_cross_grouped", "tw_attn_decode_cross_grouped_ws_bytes", "tw_attn_decode_self_tab", "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
     "tw_gemm_mx", "tw_quant_mx", "tw_layernorm_mx", "tw_attn_encoder_mx", "tw_gemm_mx_set_variant", "tw_logits_select_embed",
     "tw_attn_set_lds_pad", "tw_logits_sample", "tw_token_prob", "tw_g711_decode", "tw_ima_adpcm_wav_decode",
-    "tw_kv_tab_check", "tw_debug_build", "tw_resid_layernorm_packed_to",
+    "tw_kv_tab_check", "tw_debug_build", "tw_resid_layernorm_packed_to", "tw_conv2_gemm",
+    "tw_logmel_long", "tw_im2col_conv1_long", "tw_attn_decode_self_masked", "tw_attn_decode_self_tab_masked",
 )
 
 
@@ -91,7 +92,10 @@ _SIGS = {
     "tw_f32_to_bf16": ([_P, _P, _L, _F, _P], _I),
     "tw_logmel": ([_P, _I, _P, _P, _P, _I, _P, _P, _P], _I),
     "tw_im2col_conv1": ([_P, _I, _P, _P, _I, _I, _P, _P], _I),
+    "tw_im2col_conv1_long": ([_P, _I, _L, _P, _P, _P, _I, _I, _P, _P], _I),
+    "tw_logmel_long": ([_P, _L, _P, _P, _P, _I, _P, _L, _P, _P], _I),
     "tw_im2col_conv2": ([_P, _I, _I, _P, _P], _I),
+    "tw_conv2_gemm": ([_P, _I, _I, _P, _P, _P, _P, _P], _I),
     "tw_gemm_bf16": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _P], _I),
     "tw_layernorm": ([_P, _P, _P, _I, _I, _F, _P, _P], _I),
     "tw_gemm_mx": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P], _I),
@@ -100,6 +104,7 @@ _SIGS = {
     "tw_layernorm_mx": ([_P, _P, _P, _I, _I, _F, _P, _P, _I, _P], _I),
     "tw_attn_encoder": ([_P, _I, _I, _I, _P, _P], _I),
     "tw_attn_decode_self": ([_P, _I, _I, _I, _P, _P, _P, _P, _P], _I),
+    "tw_attn_decode_self_masked": ([_P, _I, _I, _I, _P, _P, _P, _P, _P, _P], _I),
     "tw_attn_decode_cross": ([_P, _I, _I, _I, _I, _P, _P, _P, _P], _I),
     "tw_attn_decode_cross_grouped": ([_P, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P, _P], _I),
     "tw_embed_decoder": ([_P, _P, _P, _P, _I, _I, _P, _P], _I),
@@ -120,6 +125,7 @@ _SIGS = {
     "tw_beam_workspace_bytes": ([_I], ctypes.c_size_t),
     "tw_attn_decode_cross_grouped_ws_bytes": ([_I, _I], ctypes.c_size_t),
     "tw_attn_decode_self_tab": ([_P, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P], _I),
+    "tw_attn_decode_self_tab_masked": ([_P, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P], _I),
     "tw_kv_tab_check": ([_P, _P, _I, _I, _I, _P, _P], _I),
     "tw_debug_build": ([], _I),
     "tw_beam_step": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), ctypes.POINTER(TwBeamParams),

@@ -145,6 +145,9 @@ class GenerationSettings:
     compression_ratio_threshold: Optional[float] = None
     logprob_threshold: Optional[float] = None
     no_speech_threshold: Optional[float] = None
+    # <|startofprev|> of condition_on_prev_tokens prompts (generation_config.prev_sot_token_id; None: transformers
+    # falls back to suppress_tokens[-2], generation_whisper.py:1876-1881)
+    prev_sot_token_id: Optional[int] = None
 
     @staticmethod
     def default(dims: WhisperDims) -> "GenerationSettings":
@@ -177,6 +180,8 @@ class GenerationSettings:
             gs.num_beams = int(cfg.get("num_beams") or 1)
             if cfg.get("alignment_heads"):
                 gs.alignment_heads = [(int(a), int(b)) for a, b in cfg["alignment_heads"]]
+            if cfg.get("prev_sot_token_id") is not None:
+                gs.prev_sot_token_id = int(cfg["prev_sot_token_id"])
             for k in ("compression_ratio_threshold", "logprob_threshold", "no_speech_threshold"):
                 if cfg.get(k) is not None:
                     setattr(gs, k, float(cfg[k]))

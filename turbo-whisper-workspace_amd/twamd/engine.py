@@ -23,8 +23,9 @@ import torch
 
 from . import _lib, alignment
 from .config import GenerationSettings, WhisperDims
-from .frontend import CHUNK_SAMPLES, N_FRAMES, dft_basis, mel_table
-from .segments import FallbackConfig, fallback_sequence, need_fallback, retrieve_segment, strip_generated
+from .frontend import CHUNK_SAMPLES, N_FRAMES, dft_basis, mel_table, pack_k8
+from .segments import (FallbackConfig, condition_prefixes, fallback_sequence, need_fallback, retrieve_segment,
+                       segment_slices, strip_generated)
 from .weights import PackedWeights
 
 import functools
@@ -173,9 +174,9 @@ class WhisperEngine:
         D, F, H, V, B = d.d_model, d.ffn, d.heads, d.vocab, max_batch
         dev, bf, f32, i32 = self.device, torch.bfloat16, torch.float32, torch.int32
         c, s = dft_basis()
-        self.basis_cos = torch.from_numpy(c).to(dev)
-        self.basis_sin = torch.from_numpy(s).to(dev)
-        self.mel_fb = torch.from_numpy(mel_table(d.n_mels)).to(dev)
+        self.basis_cos = torch.from_numpy(pack_k8(c)).to(dev)
+        self.basis_sin = torch.from_numpy(pack_k8(s)).to(dev)
+        self.mel_fb = torch.from_numpy(pack_k8(mel_table(d.n_mels))).to(dev)
         # front end
         self.wave = torch.zeros(B, CHUNK_SAMPLES, dtype=f32, device=dev)
         self.feats_buf = torch.zeros(2, B, d.n_mels, N_FRAMES, dtype=f32, device=dev)  # [slot]
@@ -184,8 +185,13 @@ class WhisperEngine:
         # encoder activations
         M3, M15 = B * N_FRAMES, B * S_ENC
         self.a1 = torch.empty(M3, weights.kpad1, dtype=bf, device=dev)
-        self.h1 = torch.empty(M3, D, dtype=bf, device=dev)
-        self.a2 = torch.empty(M15, 3 * D, dtype=bf, device=dev)
+        # conv1's output with one row in front: tw_conv2_gemm reads it in place as an operand of row stride 2 D
+        # starting one row early (the t = 0 rows it then recomputes; the row in front only has to be readable)
+        self._h1_rows = torch.zeros(M3 + 1, D, dtype=bf, device=dev)
+        self.h1 = self._h1_rows[1:]
+        # (A/B: TW_CONV2_IM2COL=1 materialises conv2's im2col operand, 276 MB at B = 24, as before round 4)
+        self._conv2_im2col = os.environ.get("TW_CONV2_IM2COL", "0") == "1"
+        self.a2 = torch.empty(M15, 3 * D, dtype=bf, device=dev) if self._conv2_im2col else None
         self.x = torch.empty(M15, D, dtype=f32, device=dev)
         self.hln = torch.empty(M15, D, dtype=bf, device=dev)
         self.qkv = torch.empty(M15, 3 * D, dtype=bf, device=dev)
@@ -234,6 +240,11 @@ class WhisperEngine:
         self._row_group = 1
         self._xws: Optional[torch.Tensor] = None
         self._kv_tab: Optional[torch.Tensor] = None  # beam pass: the self-attention K/V position table
+        self._long: Optional[dict] = None  # long-form input features (set_long_input)
+        # prompts conditioned on previous segments (condition_on_prev_tokens): per row the left-pad count of the pass's
+        # prefix; while _masked, the self-attention masks those positions (tw_attn_decode_self_masked)
+        self._kv_start = torch.zeros(self.max_rows, dtype=torch.int32, device=dev)
+        self._masked = False
         self._beam: Optional[dict] = None  # beam-search buffers, allocated on first use
         self._align: Optional[dict] = None  # token-level timestamps: alignment-head attention recording
         self._align_buf: Optional[torch.Tensor] = None
@@ -409,6 +420,30 @@ class WhisperEngine:
                        self.logits[sl], self.parts if parts is None else parts, self.sel_ws[sl], self.state[sl],
                        self.tokens[sl], self.ids[sl], self.pos[sl], hp, fp)
 
+    @on_engine_streams
+    def set_long_input(self, wave: Optional[torch.Tensor]) -> int:
+        """Long-form source (generate() over one input longer than 30 s, the ASR pipeline without chunk_length_s):
+        the log-mel of the whole input (tw_logmel_long: one STFT, the max - 8 clamp over the whole input, as the
+        feature extractor with truncation=False / padding="longest") becomes the encoder's feature row 0 until
+        set_long_input(None). Returns its frame count T (generate()'s total_input_frames = max_frames)."""
+        if wave is None:
+            self._long = None
+            return 0
+        wave = wave.to(self.device, torch.float32).contiguous()
+        n = int(wave.numel())
+        T = n // 160
+        ld = max(T, N_FRAMES)
+        feats = torch.zeros(self.d.n_mels, ld, dtype=torch.float32, device=self.device)
+        key = torch.zeros(1, dtype=torch.int32, device=self.device)
+        _lib.call("tw_logmel_long", wave.data_ptr(), n, self.basis_cos.data_ptr(), self.basis_sin.data_ptr(),
+                  self.mel_fb.data_ptr(), self.d.n_mels, feats.data_ptr(), ld, key.data_ptr(),
+                  torch.cuda.current_stream(self.device).cuda_stream)
+        mf = torch.tensor([T], dtype=torch.int32, device=self.device)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        self.enc_stream.wait_stream(torch.cuda.current_stream(self.device))
+        self._long = {"feats": feats, "ld": ld, "max_frames": mf, "T": T, "wave": wave}
+        return T
+
     def use_slot(self, slot: int) -> None:
         """Point the decoder at the cross-K/V (and feature) buffers of pipeline slot `slot`."""
         self._slot = slot
@@ -468,13 +503,25 @@ class WhisperEngine:
         M3, M15 = R * N_FRAMES, R * S_ENC
         st = self._enc_begin(sync)
         s = st.cuda_stream
-        _lib.call("tw_im2col_conv1", self.feats_buf[slot].data_ptr(), d.n_mels,
-                  self.row_map.data_ptr() if row_map else None, self.seek.data_ptr() if seek else None, R, w.kpad1,
-                  self.a1.data_ptr(), s)
+        if self._long is not None:  # a long-form input's features (set_long_input): one row of T frames
+            lf = self._long
+            _lib.call("tw_im2col_conv1_long", lf["feats"].data_ptr(), d.n_mels, lf["ld"], lf["max_frames"].data_ptr(),
+                      self.row_map.data_ptr() if row_map else None, self.seek.data_ptr(), R, w.kpad1,
+                      self.a1.data_ptr(), s)
+        else:
+            _lib.call("tw_im2col_conv1", self.feats_buf[slot].data_ptr(), d.n_mels,
+                      self.row_map.data_ptr() if row_map else None, self.seek.data_ptr() if seek else None, R, w.kpad1,
+                      self.a1.data_ptr(), s)
         self._gemm(self.a1, w.conv1_w, M3, D, w.kpad1, _lib.TW_EPI_GELU_BF16, self.h1, bias=w.conv1_b, stream=st)
-        _lib.call("tw_im2col_conv2", self.h1.data_ptr(), R, D, self.a2.data_ptr(), s)
-        self._gemm(self.a2, w.conv2_w, M15, D, 3 * D, _lib.TW_EPI_GELU_POS_F32, self.x, bias=w.conv2_b,
-                   aux=w.pos_enc, aux_rows=S_ENC, stream=st)
+        if self._conv2_im2col:
+            _lib.call("tw_im2col_conv2", self.h1.data_ptr(), R, D, self.a2.data_ptr(), s)
+            self._gemm(self.a2, w.conv2_w, M15, D, 3 * D, _lib.TW_EPI_GELU_POS_F32, self.x, bias=w.conv2_b,
+                       aux=w.pos_enc, aux_rows=S_ENC, stream=st)
+        else:
+            rec = self._begin_timer(("gemm_big", _lib.TW_EPI_GELU_POS_F32), 2.0 * M15 * D * 3 * D, st)
+            _lib.call("tw_conv2_gemm", self.h1.data_ptr(), R, D, w.conv2_w.data_ptr(), w.conv2_b.data_ptr(),
+                      w.pos_enc.data_ptr(), self.x.data_ptr(), s)
+            self._end_timer(rec, st)
         yield
         if self.enc_fp8:
             yield from self._encode_layers_mx(R, st)
@@ -565,9 +612,17 @@ class WhisperEngine:
             if li or not pre_embedded:
                 self._resid_ln_p(R, nparts, pbias, L.ln1_g, L.ln1_b, v)
             self._gemv(v.hp, True, P["wqkv"], R, 3 * D, D, _lib.TW_EPI_BF16, v.qkvd, v, bias=L.bqkv)
+            ks = self._kv_start[v.r0:].data_ptr() if self._masked else None  # left-padded prompts (prefill)
             if self._kv_tab is not None:  # beam pass: histories through the position table
-                _lib.call("tw_attn_decode_self_tab", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc,
-                          self._kv_tab.data_ptr(), v.r0, v.attd.data_ptr(), s)
+                if ks is not None:
+                    _lib.call("tw_attn_decode_self_tab_masked", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc,
+                              self._kv_tab.data_ptr(), v.r0, ks, v.attd.data_ptr(), s)
+                else:
+                    _lib.call("tw_attn_decode_self_tab", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc,
+                              self._kv_tab.data_ptr(), v.r0, v.attd.data_ptr(), s)
+            elif ks is not None:
+                _lib.call("tw_attn_decode_self_masked", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc, ks,
+                          v.attd.data_ptr(), s)
             else:
                 _lib.call("tw_attn_decode_self", v.qkvd.data_ptr(), R, H, T, v.pos.data_ptr(), kc, vc,
                           v.attd.data_ptr(), s)
@@ -713,10 +768,34 @@ class WhisperEngine:
         self.decoder_step(R, v=v, r_enc=r_enc, pre_embedded=fused)
         self._select(R, params, v=v, embed_next=fused)
 
+    def _prefill(self, R: int, prefix, r_enc: Optional[int] = None) -> int:
+        """condition_on_prev_tokens: feed a pass's left-padded prefix (per row [<|startofprev|>] + the previous
+        segments' tokens, generation_whisper.py:1853-1918) at positions 0 .. L-1 ahead of the init tokens; returns L.
+        prefix = (rows [R][L], pads [R]). The pad positions are fed too (transformers' cache positions count them) and
+        masked out of every later query (kv_start, tw_attn_decode_self_masked); the caller ends the pass with
+        _masked = False."""
+        if prefix is None:
+            return 0
+        rows, pads = prefix
+        L = len(rows[0]) if rows else 0
+        if L == 0:
+            return 0
+        if len(rows) != R or any(len(r) != L for r in rows):
+            raise ValueError("prefix: one left-padded row of equal length per decoder row")
+        dev = self.device
+        cols = torch.as_tensor(rows, dtype=torch.int32, device=dev)
+        self._kv_start[:R] = torch.as_tensor(list(pads), dtype=torch.int32, device=dev)
+        self._masked = True
+        for k in range(L):
+            self.ids[:R] = cols[:, k]
+            self.pos[:R] = k
+            self.decoder_step(R, with_logits=False, r_enc=r_enc)
+        return L
+
     @on_engine_streams
     def decode_pass(self, R: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
                     check_every: int = 8, use_timestamps: bool = True, align: bool = False,
-                    num_frames: Optional[Sequence[int]] = None) -> PassResult:
+                    num_frames: Optional[Sequence[int]] = None, prefix=None) -> PassResult:
         """Greedy decode of R rows from the prompt [SOT, (lang), *tail] (the init tokens of
         _retrieve_init_tokens; the language is detected from the SOT step when lang_ids is None on a
         multilingual model). Returns the generated tokens of every row; with align, also every row's token-level
@@ -745,13 +824,14 @@ class WhisperEngine:
         self.stream.wait_event(self._enc_ev[self._slot])  # the cross-K/V of this slot is written
         detect = st.is_multilingual and lang_ids is None
         params = self._select_params(0, max_new, use_timestamps)
+        base = self._prefill(R, prefix)  # (condition_on_prev_tokens: the init tokens start at position base)
 
         def prompt() -> None:
             """State reset, the prompt steps [SOT, (lang), *tail] and the first generated token (one token per
             step; the language detected from the SOT step's logits by the mode-1 selection when lang_ids is None)."""
             self.state[:R].zero_()
             self.state[:R, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
-            self.pos[:R] = 0
+            self.pos[:R] = base
             self.ids[:R] = st.sot
             prompt_rest: List = []  # per-position token ids after SOT (int, or per-row list)
             if st.is_multilingual:
@@ -767,13 +847,13 @@ class WhisperEngine:
                     self.ids[:R] = torch.as_tensor(tok, dtype=torch.int32, device=dev)
                 else:
                     self.ids[:R] = tok
-                self.pos[:R] = k + 1
+                self.pos[:R] = base + k + 1
             self._gen_step(R, params)  # last prompt token -> first generated token
 
         # the prompt phase as one captured graph (its ~140 launches replayed instead of issued one by one from the
         # host while the next batch's encoder keeps the GPU busy); per-row language ids given by the caller stay eager
         # (their host-to-device copy is not capturable)
-        if self.use_graphs and self.prompt_graph and (detect or not st.is_multilingual):
+        if self.use_graphs and self.prompt_graph and (detect or not st.is_multilingual) and not base:
             al = self._align  # (keyed like _graph_for: an alignment pass captures the probability-recording kernel)
             key = ("prompt", R, tuple(int(t) for t in tail), max_new, use_timestamps, self._slot,
                    None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()))
@@ -841,7 +921,7 @@ class WhisperEngine:
     def sample_pass(self, R: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
                     temperature: float = 0.0, top_k: int = 50, seed: int = 0, row_keys: Optional[Sequence[int]] = None,
                     use_timestamps: bool = True, enc_rows: Optional[Sequence[int]] = None, r_enc: Optional[int] = None,
-                    no_speech_token: Optional[int] = None, check_every: int = 8) -> PassResult:
+                    no_speech_token: Optional[int] = None, check_every: int = 8, prefix=None) -> PassResult:
         """One decode pass of the temperature-fallback loop (WhisperGenerationMixin.generate_with_fallback,
         generation_whisper.py:970-1116), eager, one tw_logits_sample per token: greedy when temperature == 0
         (the tokens of decode_pass), else a draw from softmax(processed / T) over the top_k scores. Per row it also
@@ -863,9 +943,10 @@ class WhisperEngine:
             self._use_dec_row_map = True
             self._row_group = 1
         try:
+            base = self._prefill(R, prefix, r_enc)
             self.state[:R].zero_()
             self.state[:R, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
-            self.pos[:R] = 0
+            self.pos[:R] = base
             self.ids[:R] = st.sot
             prompt_rest: List = []
             if st.is_multilingual:
@@ -889,7 +970,7 @@ class WhisperEngine:
                     self.ids[:R] = torch.as_tensor(tok, dtype=torch.int32, device=dev)
                 else:
                     self.ids[:R] = tok
-                self.pos[:R] = k + 1
+                self.pos[:R] = base + k + 1
             steps = 0
             while steps < max_new:
                 self.decoder_step(R, r_enc=r_enc)
@@ -936,7 +1017,7 @@ class WhisperEngine:
     @on_engine_streams
     def beam_pass(self, W: int, num_beams: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
                   use_timestamps: bool = True, check_every: int = 8, length_penalty: float = 1.0,
-                  enc_row0: int = 0, r_enc: Optional[int] = None) -> PassResult:
+                  enc_row0: int = 0, r_enc: Optional[int] = None, prefix=None) -> PassResult:
         """Beam-search decode (GenerationMixin._beam_search, $TF/generation/utils.py:3208-3512) of W windows with
         num_beams rows each (row = w * num_beams + j, all reading window w's cross-K/V): the prompt as
         decode_pass (language detected from the SOT step when lang_ids is None), then per token one decoder step
@@ -960,9 +1041,13 @@ class WhisperEngine:
         bb["kv_tab"][:R] = torch.arange(R, dtype=torch.int32, device=dev)[:, None]
         self._kv_tab = bb["kv_tab"]
         try:
+            # (a window's prefix on each of its beam rows)
+            base = self._prefill(R, None if prefix is None else
+                                 ([prefix[0][w] for w in range(W) for _ in range(nb)],
+                                  [prefix[1][w] for w in range(W) for _ in range(nb)]), r_enc)
             self.state[:R].zero_()
             self.state[:R, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
-            self.pos[:R] = 0
+            self.pos[:R] = base
             self.ids[:R] = st.sot
             detected = None
             prompt_rest: List = []
@@ -980,7 +1065,7 @@ class WhisperEngine:
                     self.ids[:R] = torch.as_tensor(tok, dtype=torch.int32, device=dev)
                 else:
                     self.ids[:R] = tok
-                self.pos[:R] = k + 1
+                self.pos[:R] = base + k + 1
             bb["run_score"][:R].view(W, nb).fill_(-1e9)
             bb["run_score"][:R].view(W, nb)[:, 0] = 0.0
             bb["fin_score"][:R] = -1e9
@@ -1006,7 +1091,8 @@ class WhisperEngine:
             # (eager, each of its ~100 launches would be issued from the host every token)
             g = None
             if self.use_graphs:
-                key = ("beam", R, nb, max_new, bool(use_timestamps), float(length_penalty), self._slot, r_enc)
+                key = ("beam", R, nb, max_new, bool(use_timestamps), float(length_penalty), self._slot, r_enc,
+                       self._masked)
                 g = self._graphs.get(key)
                 if g is None:
                     g = torch.cuda.CUDAGraph()
@@ -1050,7 +1136,7 @@ class WhisperEngine:
     def _graph_for(self, R: int, params, i: int, v: DecView, fused: bool = False) -> Optional[torch.cuda.CUDAGraph]:
         al = self._align
         key = (R, params.max_new, params.use_timestamps, self._slot, i, fused,
-               None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()))
+               None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()), self._masked)
         g = self._graphs.get(key)
         if g is not None:
             return g
@@ -1097,7 +1183,7 @@ class WhisperEngine:
                  max_passes: Optional[int] = None, slot: Optional[int] = None,
                  pre_encoded: bool = False, num_beams: int = 1, word_timestamps: bool = False,
                  num_frames: Optional[Sequence[int]] = None, fallback: Optional[FallbackConfig] = None,
-                 window_offset: int = 0) -> List[List[int]]:
+                 window_offset: int = 0, condition_on_prev_tokens: bool = False) -> List[List[int]]:
         """Whisper short-form generate() over feats[slot][:n_chunks] (each 3000 frames): language
         detection, the seek loop and segment extraction, returning for every chunk the concatenated
         segment tokens (what generate() returns before padding).
@@ -1107,7 +1193,9 @@ class WhisperEngine:
         fallback: generate()'s temperature / compression_ratio_threshold / logprob_threshold / no_speech_threshold;
         when it asks for more than greedy decoding every pass runs generate_with_fallback's loop (sample_pass).
         window_offset: the global index of chunk 0 (run_batches' batch offset): the sampler's per-row keys are built
-        from global window indices, so windows of different batches draw independent noise."""
+        from global window indices, so windows of different batches draw independent noise.
+        condition_on_prev_tokens: every pass after a chunk's first is prompted with <|startofprev|> + the chunk's
+        previous segments (_prepare_decoder_input_ids, generation_whisper.py:1853-1918), left padded over the batch."""
         if slot is not None:
             self.use_slot(slot)
         if pre_encoded and n_chunks > self.max_batch:
@@ -1131,15 +1219,57 @@ class WhisperEngine:
         # word timestamps: per chunk the segments' token times (segment token_timestamps of generate(), i.e. the
         # pass's DTW times of the kept tokens + seek * 0.01 s); num_frames: the chunks' valid feature frames
         tts: List[List[float]] = [[] for _ in range(n_chunks)]
+        # condition_on_prev_tokens: every chunk's segments so far (current_segments' "tokens") and the per-position
+        # flags of generate_with_fallback (written at the row's position in the pass's batch, read by chunk index:
+        # transformers' indexing, :1089-1093 / :1885)
+        if condition_on_prev_tokens and word_timestamps:
+            raise NotImplementedError("condition_on_prev_tokens with word-level timestamps is not implemented")
+        seg_lists: List[List[List[int]]] = [[] for _ in range(n_chunks)]
+        do_cond = [bool(condition_on_prev_tokens)] * n_chunks
+        prev_sot = self.gen.prev_sot_token_id
+        if prev_sot is None and len(self.gen.suppress_tokens) >= 2:
+            prev_sot = self.gen.suppress_tokens[-2]  # (:1876-1881)
+        # max_frames (_retrieve_max_frames_and_seek): 3000 per 30-s window; a long-form input's total frames
+        if self._long is not None:
+            if n_chunks != 1 or pre_encoded:
+                raise ValueError("a long-form input is one chunk (set_long_input), encoded per seek pass")
+            maxf = [self._long["T"]]
+        else:
+            maxf = [N_FRAMES] * n_chunks
         passes = 0
-        while any(s < N_FRAMES for s in seek):
-            rows = [i for i in range(n_chunks) if seek[i] < N_FRAMES]
+        self.last_pass_prefixes: List[list] = [[] for _ in range(n_chunks)]
+        try:
+            return self._seek_loop(n_chunks, tail, prompt_len, max_new_tokens, max_new, seek, segs, passes_raw, langs,
+                                   tts, maxf, seg_lists, do_cond, prev_sot, condition_on_prev_tokens, max_passes,
+                                   pre_encoded, num_beams, word_timestamps, num_frames, fb, return_timestamps,
+                                   window_offset)
+        finally:
+            self._masked = False
+
+    def _seek_loop(self, n_chunks, tail, prompt_len, max_new_tokens, max_new, seek, segs, passes_raw, langs, tts, maxf,
+                   seg_lists, do_cond, prev_sot, condition, max_passes, pre_encoded, num_beams, word_timestamps,
+                   num_frames, fb, return_timestamps, window_offset):
+        st = self.gen.special
+        passes = 0
+        while any(seek[i] < maxf[i] for i in range(n_chunks)):
+            rows = [i for i in range(n_chunks) if seek[i] < maxf[i]]
             per = self.max_batch if num_beams == 1 else min(self.max_batch, self.max_rows // num_beams)
             if per < 1:
                 raise ValueError(f"num_beams={num_beams} > the engine's {self.max_rows} decoder rows")
+            prefix = None
+            if condition and any(do_cond) and len(seg_lists[0]) > 0:
+                if len(rows) > per:
+                    raise NotImplementedError(f"condition_on_prev_tokens over more than {per} rows in one pass")
+                prefix = condition_prefixes([seg_lists[i] if do_cond[i] else None for i in rows], prev_sot, st.eot,
+                                            st.timestamp_begin, self.d.max_target_positions // 2 - 1)
+            L = len(prefix[0][0]) if prefix is not None and prefix[0] else 0
+            mnew = self.max_new_for(prompt_len + L, max_new_tokens) if L else max_new
             for b0 in range(0, len(rows), per):
                 part = rows[b0: b0 + per]
                 R = len(part)
+                pfx = None if prefix is None else (prefix[0][b0: b0 + per], prefix[1][b0: b0 + per])
+                for j, i in enumerate(part):  # (diagnostics: the prompt prefix each pass was fed)
+                    self.last_pass_prefixes[i].append(None if pfx is None else (pfx[0][j], pfx[1][j]))
                 if not (pre_encoded and passes == 0):
                     self.row_map[:R] = torch.as_tensor(part, dtype=torch.int32, device=self.device)
                     self.seek[:R] = torch.as_tensor([seek[i] for i in part], dtype=torch.int32, device=self.device)
@@ -1150,35 +1280,43 @@ class WhisperEngine:
                 nf_part = None if num_frames is None else [int(num_frames[i]) - seek[i] for i in part]
                 if fb is not None:
                     pre = pre_encoded and passes == 0
-                    toks_f, skip_f, lang_f = self._fallback_pass(
-                        R, tail, given, max_new, return_timestamps, fb, [window_offset + i for i in part], passes,
-                        enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R)
+                    toks_f, skip_f, lang_f, temp_f = self._fallback_pass(
+                        R, tail, given, mnew, return_timestamps, fb, [window_offset + i for i in part], passes,
+                        enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R, prefix=pfx)
+                    for j in range(R):  # (by position in the pass's batch, as transformers writes it)
+                        do_cond[j] = bool(condition) and (temp_f[j] is None or temp_f[j] < 0.5)
                     for j, i in enumerate(part):
                         if not known:
                             langs[i] = lang_f[j]
                         passes_raw[i].append(list(toks_f[j]))
+                        snf = min(maxf[i] - seek[i], N_FRAMES)  # seek_num_frames
                         if skip_f[j]:  # generate(): seek += seek_num_frames, nothing kept
-                            seek[i] = N_FRAMES
+                            seek[i] += snf
                             continue
-                        seg_tokens, offset = retrieve_segment(toks_f[j], seek[i], N_FRAMES - seek[i],
-                                                              st.timestamp_begin)
+                        seg_tokens, offset = retrieve_segment(toks_f[j], seek[i], snf, st.timestamp_begin)
                         segs[i].extend(seg_tokens)
+                        seg_lists[i].extend(segment_slices(toks_f[j], st.timestamp_begin))
                         seek[i] += offset
                     continue
                 if num_beams > 1:  # pre-encoded first pass: this part's windows sit at encoder rows b0..
                     pre = pre_encoded and passes == 0
-                    res = self.beam_pass(R, num_beams, tail, given, max_new, use_timestamps=return_timestamps,
-                                         enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R)
+                    res = self.beam_pass(R, num_beams, tail, given, mnew, use_timestamps=return_timestamps,
+                                         enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R, prefix=pfx)
                 else:
-                    res = self.decode_pass(R, tail, given, max_new, use_timestamps=return_timestamps,
-                                           align=word_timestamps, num_frames=nf_part)
+                    res = self.decode_pass(R, tail, given, mnew, use_timestamps=return_timestamps,
+                                           align=word_timestamps, num_frames=nf_part, prefix=pfx)
+                self._masked = False
+                for j in range(R):
+                    do_cond[j] = bool(condition)
                 for j, i in enumerate(part):
                     if not known:
                         langs[i] = res.lang_ids[j]
                     passes_raw[i].append(list(res.tokens[j]))
                     seq = strip_generated(res.tokens[j], st.eot)
-                    seg_tokens, offset = retrieve_segment(seq, seek[i], N_FRAMES - seek[i], st.timestamp_begin)
+                    seg_tokens, offset = retrieve_segment(seq, seek[i], min(maxf[i] - seek[i], N_FRAMES),
+                                                          st.timestamp_begin)
                     segs[i].extend(seg_tokens)
+                    seg_lists[i].extend(segment_slices(seq, st.timestamp_begin))
                     if word_timestamps:
                         raw = res.token_ts[j][prompt_len: prompt_len + len(seg_tokens)]
                         off = np.float32(seek[i] * 0.02 / 2)  # time_offset = seek * time_precision / input_stride
@@ -1195,7 +1333,8 @@ class WhisperEngine:
         return segs
 
     def _fallback_pass(self, R: int, tail, given, max_new: int, return_timestamps: bool, fb: FallbackConfig,
-                       windows: Sequence[int], pass_no: int, enc_row0: int = 0, r_enc: Optional[int] = None):
+                       windows: Sequence[int], pass_no: int, enc_row0: int = 0, r_enc: Optional[int] = None,
+                       prefix=None):
         """generate_with_fallback (generation_whisper.py:970-1116) for one seek pass of R encoded rows: decode at
         the first temperature, re-decode the rows whose criteria fail at the next one, until none does or the
         temperatures run out. Returns per row the kept sequence (EOS removed), should_skip, and the language ids.
@@ -1209,13 +1348,19 @@ class WhisperEngine:
         langs = list(given) if given is not None else None
         ns_tok = st.notimestamps - 1 if fb.no_speech_threshold is not None else None  # no_timestamps_token_id - 1
         temps = list(fb.temperatures) or [None]
+        final_t: List[Optional[float]] = [None] * R  # the temperature of each row's last round
         for fi, t in enumerate(temps):
             do_sample = t is not None and t > 0.0
             res = self.sample_pass(len(idx), tail, None if langs is None else [langs[i] for i in idx], max_new,
                                    temperature=float(t) if do_sample else 0.0, top_k=fb.top_k, seed=fb.seed,
                                    row_keys=[fallback_row_key(windows[i], pass_no, fi) for i in idx],
                                    use_timestamps=return_timestamps, enc_rows=[enc_row0 + i for i in idx],
-                                   r_enc=r_enc, no_speech_token=ns_tok)
+                                   r_enc=r_enc, no_speech_token=ns_tok,
+                                   prefix=None if prefix is None else ([prefix[0][i] for i in idx],
+                                                                       [prefix[1][i] for i in idx]))
+            self._masked = False
+            for i in idx:
+                final_t[i] = t
             if langs is None and res.lang_ids is not None:  # detected on the first round (all rows)
                 langs = list(res.lang_ids)
             new_idx = []
@@ -1232,7 +1377,7 @@ class WhisperEngine:
             idx = new_idx
             if not idx or fi == len(temps) - 1:
                 break
-        return seqs, skip, langs if langs is not None else [None] * R
+        return seqs, skip, langs if langs is not None else [None] * R, final_t
 
     @on_engine_streams
     def run_batches(self, sizes: Sequence[int], load=None, batch_kwargs: Optional[Sequence[dict]] = None,
@@ -1265,6 +1410,7 @@ class WhisperEngine:
         self.batch_langs = []
         self.batch_passes = []
         self.batch_token_timestamps = []
+        self.batch_prefixes = []
         overlap = self.overlap  # False: encoder and decoder strictly in turn
         if sizes:
             prefetch(0)
@@ -1285,5 +1431,6 @@ class WhisperEngine:
             self.batch_langs.append(self.last_langs)
             self.batch_passes.append(self.last_passes)
             self.batch_token_timestamps.append(self.last_token_timestamps)
+            self.batch_prefixes.append(self.last_pass_prefixes)
         self.use_slot(0)
         return out

@@ -74,6 +74,14 @@ def mel_table(n_mels: int) -> np.ndarray:
     return t
 
 
+def pack_k8(a: np.ndarray) -> np.ndarray:
+    """A [K][C] table (K % 8 == 0) in tw_logmel's "k8" order [K/8][C][2][4]: element [k][c] at
+    ((k/8 * C + c) * 2 + k%2) * 4 + (k%8)/2, so one 16-byte load holds a column's values for 4 MFMA steps."""
+    K, C = a.shape
+    assert K % 8 == 0
+    return np.ascontiguousarray(a.reshape(K // 8, 4, 2, C).transpose(0, 3, 2, 1))
+
+
 class Window(NamedTuple):
     start: int       # first sample of the chunk in the input
     length: int      # samples actually present (<= chunk_len)

@@ -123,6 +123,11 @@ class TurboTranscriber:
         max_new_tokens = dec["max_new_tokens"]
         # extension (not a transformers generate kwarg): bound the seek loop to this many passes per window
         max_passes = gk.pop("max_passes", None)
+        # prompt every seek pass after a window's first with its previous segments (generate()'s
+        # condition_on_prev_tokens; the batch then shapes results through the left padding, so batch_size is kept)
+        cond = bool(gk.pop("condition_on_prev_tokens", None) or False)
+        if cond and word:
+            raise NotImplementedError("condition_on_prev_tokens with word-level timestamps is not implemented")
         fallback = self._fallback_config(gk)
         if fallback.active and (num_beams > 1 or word):
             from_ckpt = [k for k in ("compression_ratio_threshold", "logprob_threshold", "no_speech_threshold")
@@ -157,21 +162,14 @@ class TurboTranscriber:
                 # raises StopIteration (tests/golden/edge.json), which transcribe() reports as "Transcription error: "
                 raise StopIteration
             with_stride = True
+        elif len(wav) > CHUNK_SAMPLES:  # long-form: one sequential generate() over the whole input (asr:450-457)
+            return self._long_form(wav, task=task, language=language, return_timestamps=return_timestamps,
+                                   return_language=return_language, max_new_tokens=max_new_tokens,
+                                   num_beams=num_beams, max_passes=max_passes, fallback=fallback, condition=cond)
         else:
-            if len(wav) > CHUNK_SAMPLES:
-                raise NotImplementedError("long-form (> 30 s without chunk_length_s) sequential decoding is not "
-                                          "implemented; pass chunk_length_s")
             windows = [Window(0, len(wav), 0, 0, True)]
             with_stride = False
-        lang_id = None
-        if language is not None:
-            code = language.lower()
-            code = _NAME_TO_CODE.get(code, code)
-            tok = f"<|{code}|>"
-            lt = st.lang_to_id()
-            if tok not in lt:
-                raise ValueError(f"Unsupported language: {language}.")
-            lang_id = lt[tok]
+        lang_id = self._lang_id(language)
 
         def run(w, ws):
             base = windows.index(ws[0]) if ws else 0  # this shard's first global window (the sampler's row keys)
@@ -185,7 +183,8 @@ class TurboTranscriber:
                 return [(t, ts) for t, ts in zip(toks, self.last_window_token_timestamps)]
             return self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=bool(return_timestamps),
                                            max_new_tokens=max_new_tokens, num_beams=num_beams, max_passes=max_passes,
-                                           **({"fallback": fallback, "window_base": base} if fallback.active else {}))
+                                           **({"fallback": fallback, "window_base": base} if fallback.active else {}),
+                                           **({"condition_on_prev_tokens": True, "group": batch_size} if cond else {}))
 
         # one window shard per rank + one all-gather of the token arrays (twamd.dist); plain call on 1 GPU
         outputs = dist.transcribe_sharded(run, wav, windows, timed=word) if world > 1 else run(wav, windows)
@@ -205,18 +204,61 @@ class TurboTranscriber:
                                     time_precision=time_precision(self.engine.d.max_source_positions))
         return {"text": text, **optional}
 
+    def _lang_id(self, language: Optional[str]) -> Optional[int]:
+        if language is None:
+            return None
+        code = language.lower()
+        code = _NAME_TO_CODE.get(code, code)
+        tok = f"<|{code}|>"
+        lt = self.gen.special.lang_to_id()
+        if tok not in lt:
+            raise ValueError(f"Unsupported language: {language}.")
+        return lt[tok]
+
+    def _long_form(self, wav, *, task, language, return_timestamps, return_language, max_new_tokens, num_beams,
+                   max_passes, fallback, condition=False) -> dict:
+        """An input longer than 30 s without chunk_length_s: the pipeline hands generate() the features of the whole
+        input (feature extractor with truncation=False, padding="longest", $TF/pipelines/automatic_speech_recognition
+        .py:450-457) and generate() runs its seek loop over all of them (generation_whisper.py:647-968: is_shortform
+        False, max_frames = the input's frames, every pass the 30-s segment at seek, zero padded). One chunk, no
+        stride; every rank computes it (nothing to shard: each pass depends on the previous one's seek)."""
+        # (the pipeline never passes return_timestamps=False on to generate(), asr:506-508, so generate() switches
+        # timestamps on for a long-form input instead of raising; the text is then decoded without them)
+        if return_timestamps == "word":
+            raise NotImplementedError("word-level timestamps on a long-form input (> 30 s without chunk_length_s) "
+                                      "are not implemented; pass chunk_length_s")
+        eng = self.engine
+        lang_id = self._lang_id(language)
+        x = wav if torch.is_tensor(wav) else torch.from_numpy(np.ascontiguousarray(wav, np.float32))
+        eng.set_long_input(x)
+        try:
+            kw = {"fallback": fallback} if fallback.active else {}
+            toks = eng.generate(1, task=task, lang_ids=None if lang_id is None else [lang_id],
+                                max_new_tokens=max_new_tokens, return_timestamps=True, num_beams=num_beams,
+                                max_passes=max_passes, condition_on_prev_tokens=condition, **kw)[0]
+        finally:
+            eng.set_long_input(None)
+        self.last_window_langs = list(eng.last_langs)
+        self.last_window_passes = list(eng.last_passes)
+        self.last_window_prefixes = list(eng.last_pass_prefixes)
+        text, optional = decode_asr(self.vocab, [{"tokens": toks}], return_timestamps=bool(return_timestamps),
+                                    return_language=return_language,
+                                    time_precision=time_precision(self.engine.d.max_source_positions))
+        return {"text": text, **optional}
+
     def transcribe_windows(self, wav: np.ndarray, windows: Sequence[Window], task: Optional[str],
                            lang_id: Optional[int], return_timestamps: bool,
                            max_new_tokens: Optional[int] = None, num_beams: int = 1, word_timestamps: bool = False,
                            num_frames: Optional[Sequence[int]] = None, group: Optional[int] = None,
                            max_passes: Optional[int] = None, fallback: Optional[FallbackConfig] = None,
-                           window_base: int = 0) -> List[List[int]]:
+                           window_base: int = 0, condition_on_prev_tokens: bool = False) -> List[List[int]]:
         """Log-mel + generate for every window; returns per-window token sequences (generate() output,
         right-padded with the pad token within each engine batch, as the HF batch output is). Batches of
         max_batch windows go through WhisperEngine.run_batches: batch k+1 is encoded while batch k decodes.
 
-        group: windows per engine batch when the batch's composition changes results. That is the case only for
-        word timestamps, whose per-pass standardisation runs over the padded batch, so the pipeline's
+        group: windows per engine batch when the batch's composition changes results. That is the case for
+        word timestamps, whose per-pass standardisation runs over the padded batch, and for
+        condition_on_prev_tokens, whose prompts are left padded to the batch's longest, so the pipeline's
         `batch_size` (its DataLoader batch, $TF/pipelines/base.py:1319-1339) is honoured there; segment-level
         tokens are per-window results, so batching is then only a schedule: the windows are cut into near-equal
         batches of at most max_batch (and into two when sub_batch_min says so).
@@ -258,13 +300,15 @@ class TurboTranscriber:
                               lang_ids=None if lang_id is None else [lang_id] * max(sizes, default=1),
                               max_new_tokens=max_new_tokens, return_timestamps=return_timestamps, num_beams=num_beams,
                               max_passes=max_passes,
-                              **({"fallback": fallback, "window_offset": window_base} if fallback is not None else {}))
+                              **({"fallback": fallback, "window_offset": window_base} if fallback is not None else {}),
+                              **({"condition_on_prev_tokens": True} if condition_on_prev_tokens else {}))
         out: List[List[int]] = []
         for seqs in res:
             out.extend(pad_right(seqs, self.gen.special.eot))
         # per-window record of the last call (languages, raw tokens of every seek pass) for diagnostics/tests
         self.last_window_langs = [lg for bl in eng.batch_langs for lg in bl]
         self.last_window_passes = [p for bp in eng.batch_passes for p in bp]
+        self.last_window_prefixes = [p for bp in eng.batch_prefixes for p in bp]
         if word_timestamps:  # per window the concatenated segments' token times (not padded, as the pipeline's)
             self.last_window_token_timestamps = [t for bt in eng.batch_token_timestamps for t in bt]
         return out
@@ -274,13 +318,11 @@ class TurboTranscriber:
         a list / tuple of temperatures tried in turn), the three segment criteria (else the checkpoint's
         generation_config values), `top_k` (sampling; GenerationConfig's default 50), `do_sample` (ignored: the
         temperature decides, as generate_with_fallback does), and the extension `seed` (the sampler's key).
-        condition_on_prev_tokens=True (prompting a pass with the previous segment) is not implemented."""
+        (condition_on_prev_tokens is popped by the caller.)"""
         g = self.gen
         t = gk.pop("temperature", None)
         temps = tuple(t) if isinstance(t, (list, tuple)) else (t,)
         gk.pop("do_sample", None)
-        if gk.pop("condition_on_prev_tokens", None):
-            raise NotImplementedError("condition_on_prev_tokens=True is not implemented")
         pick = lambda k: gk.pop(k) if gk.get(k) is not None else (gk.pop(k, None), getattr(g, k))[1]  # noqa: E731
         return FallbackConfig(temperatures=temps, compression_ratio_threshold=pick("compression_ratio_threshold"),
                               logprob_threshold=pick("logprob_threshold"), no_speech_threshold=pick("no_speech_threshold"),

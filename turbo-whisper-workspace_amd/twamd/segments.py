@@ -48,6 +48,47 @@ def retrieve_segment(seq: Sequence[int], seek: int, seek_num_frames: int, timest
     return list(seq), seek_num_frames
 
 
+def segment_slices(seq: Sequence[int], timestamp_begin: int) -> List[List[int]]:
+    """The "tokens" of the segments _retrieve_segment (:1991-2072) cuts one pass into: at every pair of consecutive
+    timestamps, the last slice ending after the closing timestamp (or at the end on a single timestamp ending);
+    no pair: one segment of the whole sequence. Their concatenation is retrieve_segment's tokens."""
+    seq = list(seq)
+    ts = [t >= timestamp_begin for t in seq]
+    pair_idx = [i + 1 for i in range(len(seq) - 1) if ts[i] and ts[i + 1]]
+    if not pair_idx:
+        return [seq]
+    cuts = list(pair_idx)
+    if ts[-2:] == [False, True]:
+        cuts.append(len(seq))
+    else:
+        cuts[-1] += 1
+    out, last = [], 0
+    for c in cuts:
+        out.append(seq[last:c])
+        last = c
+    return out
+
+
+def condition_prefixes(segments: Sequence[Optional[Sequence[Sequence[int]]]], prev_sot: Optional[int], pad: int,
+                       timestamp_begin: int, cut_off_length: int) -> Tuple[List[List[int]], List[int]]:
+    """_prepare_decoder_input_ids' previous-token prompts (generation_whisper.py:1883-1906 via _pad_to_max_length with
+    padding_side="left", skip_ending_double_timestamps=True, :126-232): per active row its segments' tokens (a segment
+    ending in two timestamps loses the last one; None = the row is not conditioned), the last cut_off_length of them
+    behind <|startofprev|>, left padded with `pad` to the longest. Returns (rows, pad counts)."""
+    seqs = []
+    for segs in segments:
+        if segs is not None and len(segs) > 0:
+            toks: List[int] = []
+            for d in segs:
+                toks.extend(d[:-1] if len(d) > 2 and d[-2] >= timestamp_begin else d)
+            toks = toks[-cut_off_length:] if cut_off_length else toks
+            seqs.append(([prev_sot] if prev_sot is not None else []) + toks)
+        else:
+            seqs.append([prev_sot] if prev_sot is not None else [])
+    L = max((len(x) for x in seqs), default=0)
+    return [[pad] * (L - len(x)) + x for x in seqs], [L - len(x) for x in seqs]
+
+
 def pad_right(seqs: Sequence[Sequence[int]], pad: int) -> List[List[int]]:
     n = max((len(s) for s in seqs), default=0)
     return [list(s) + [pad] * (n - len(s)) for s in seqs]
