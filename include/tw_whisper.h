@@ -215,6 +215,10 @@ typedef struct TwBeamState {
                           * (tw_attn_decode_self_tab): row r's positions [0, pos[r]) take row src_rows[r]'s
                           * entries, in place of a tw_kv_reorder copy. Initialise kv_tab[r][*] = r; its row
                           * stride ld_tokens must equal the caches' max_pos.                                 */
+  int32_t* fin_tab;      /* i32[R][ld_tokens] or NULL (needs kv_tab): finished slot s of window w gets the row
+                          * that fed each position of its history (kv_tab of its source at the step it finished,
+                          * positions 0 .. its last fed one) — the beam_indices of token-level timestamps
+                          * (generation_whisper.py:265-300): position p's cross-attention is that row's.       */
 } TwBeamState;
 /* workspace: tw_beam_workspace_bytes(R) bytes of device memory. */
 size_t tw_beam_workspace_bytes(int rows);

@@ -12,6 +12,8 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
   word.npz/.json    token-level timestamps (cross-attention DTW) of generate(return_token_timestamps=True) and
                     the pipeline's return_timestamps="word" output, plus HF's _median_filter / _dynamic_time_warping
                     on seeded random matrices
+  beam_word.json    token-level timestamps with beam search (generate() token times, pipeline word chunks)
+  fallback_beam.json  the temperature-fallback criteria and outcomes with beam search (num_beams=3)
   longform.json     long-form (unchunked > 30 s) pipeline outputs and condition_on_prev_tokens, with every seek
                     pass's decoder prompt and raw output (spied from generate_with_fallback)
   fallback.json     the temperature-fallback criteria (compression ratio, avg logprob, no-speech probability) of
@@ -315,6 +317,40 @@ def make_word(out):
     with open(os.path.join(out, "word.json"), "w") as f:
         json.dump({"seed": SEED, "dims": "test-mini", "alignment_heads": ALIGN_HEADS_MINI,
                    "audio": "speech_like(40,5)+white_noise(35,11)", "cases": cases}, f)
+
+
+def make_beam_word(out):
+    """Token-level timestamps with beam search (return_timestamps="word" / return_token_timestamps with num_beams=3,
+    the alignment-head cross-attentions gathered along each hypothesis' beam_indices, generation_whisper.py:265-300):
+    generate() sequences + token times of two clips, and the ASR pipeline's word chunks (single window, 30-s mode)."""
+    from transformers import AutomaticSpeechRecognitionPipeline, WhisperFeatureExtractor
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    m.generation_config.alignment_heads = ALIGN_HEADS_MINI
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    cl = clips()
+    gens = []
+    for name in ("speech30", "noise12"):
+        f = fe(cl[name], sampling_rate=16000, return_tensors="pt", return_attention_mask=True)
+        with torch.no_grad():
+            o = m.generate(f["input_features"], attention_mask=f["attention_mask"], task="transcribe", num_beams=3,
+                           return_timestamps=True, return_token_timestamps=True, max_new_tokens=24)
+        gens.append({"clip": name, "sequences": o["sequences"].tolist(), "token_timestamps": o["token_timestamps"].tolist()})
+    pipe = AutomaticSpeechRecognitionPipeline(model=m, feature_extractor=fe, tokenizer=hf_tokenizer(gen.special),
+                                              device=-1)
+    audio = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)])
+    cases = []
+    for name, x, kw in (("single_20s_beam3", audio[: 20 * 16000], {}),
+                        ("mode_30_0_beam3", audio, dict(chunk_length_s=30, stride_length_s=0, batch_size=3))):
+        r = pipe(x.copy(), generate_kwargs={"task": "transcribe", "num_beams": 3, "max_new_tokens": 24},
+                 return_timestamps="word", **kw)
+        cases.append({"name": name, "kwargs": kw, "n_samples": int(len(x)), "output": _jsonable(r)})
+    with open(os.path.join(out, "beam_word.json"), "w") as f:
+        json.dump({"seed": SEED, "dims": "test-mini", "alignment_heads": ALIGN_HEADS_MINI, "num_beams": 3,
+                   "generate": gens, "cases": cases}, f)
 
 
 def make_defaults(out):
@@ -1059,6 +1095,58 @@ def make_fallback(out):
                            **{k: v for k, v in kw.items() if k != "temperature" and v is not None})
         res[name] = {"kwargs": kw, "calls": rec, "sequences": o["sequences"].tolist()}
     with open(os.path.join(out, "fallback.json"), "w") as f:
+        json.dump(res, f)
+
+
+def make_fallback_beam(out):
+    """The temperature fallback with beam search (num_beams=3; generate_with_fallback, generation_whisper.py:970-1116):
+    spied like make_fallback. The beam pass's average log-probability is _retrieve_avg_logprobs over the processed
+    beam scores gathered along the hypothesis' beam_indices (log_softmax renormalises them over the allowed tokens);
+    "metrics": inert thresholds, every pass's criteria; "skip": FALLBACK_SKIP with beams; "resample": temperature
+    (0.0, 0.4) with logprob_threshold -2.5: the calls record the decoding mode (a sampling round sets
+    generation_config.num_beams = 1 for the rest of the generate() call) and the first round's decisions."""
+    from transformers import WhisperFeatureExtractor
+    from transformers.generation.logits_process import WhisperNoSpeechDetection
+    from transformers.models.whisper.generation_whisper import _get_attr_from_logit_processors
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    cl = clips()
+    feats = torch.from_numpy(np.stack([fe(cl[k], sampling_rate=16000, return_tensors="np")["input_features"][0]
+                                       for k in FALLBACK_CLIPS]))
+    res = {"seed": SEED, "dims": "test-mini", "clips": list(FALLBACK_CLIPS), "max_new_tokens": 24, "num_beams": 3}
+    for name, kw in (("metrics", {"temperature": [0.0], "compression_ratio_threshold": 1e9, "logprob_threshold": -1e9,
+                                  "no_speech_threshold": 2.0}),
+                     ("skip", FALLBACK_SKIP),
+                     ("resample", {"temperature": [0.0, 0.4], "compression_ratio_threshold": None,
+                                   "logprob_threshold": -2.5, "no_speech_threshold": None})):
+        m = hf_model(d, sd, gen)
+        rec = []
+        orig = m._need_fallback
+
+        def spy(seek_sequence, seek_outputs, index, logits_processor, generation_config, vocab_size, temperature,
+                _m=m, _orig=orig, _rec=rec):
+            cr = _m._retrieve_compression_ratio(seek_sequence, vocab_size)
+            lp = _m._retrieve_avg_logprobs(seek_outputs[index]["scores"], seek_sequence, temperature)
+            nsp = _get_attr_from_logit_processors(logits_processor, WhisperNoSpeechDetection, "no_speech_prob")
+            o = _orig(seek_sequence, seek_outputs, index, logits_processor, generation_config, vocab_size, temperature)
+            _rec.append({"index": int(index), "tokens": [int(t) for t in seek_sequence.tolist()],
+                         "temperature": temperature, "num_beams": int(generation_config.num_beams),
+                         "compression_ratio": float(cr), "avg_logprob": float(lp),
+                         "no_speech_prob": None if nsp is None else float(nsp[index]),
+                         "needs_fallback": bool(o[0]), "should_skip": bool(o[1])})
+            return o
+
+        m._need_fallback = spy
+        torch.manual_seed(0)
+        with torch.no_grad():
+            o = m.generate(feats, task="transcribe", return_timestamps=True, max_new_tokens=24, return_segments=True,
+                           num_beams=3, temperature=tuple(kw["temperature"]),
+                           **{k: v for k, v in kw.items() if k != "temperature" and v is not None})
+        res[name] = {"kwargs": kw, "calls": rec, "sequences": o["sequences"].tolist()}
+    with open(os.path.join(out, "fallback_beam.json"), "w") as f:
         json.dump(res, f)
 
 

@@ -601,15 +601,17 @@ struct BeamPart {
   Cand t[K];  // top-K masked text candidates (logit value)
   Cand s[K];  // top-K masked timestamp candidates
   float m_all, s_all, m_ts, s_ts;
+  float m_tx, s_tx;  // (renorm) log-sum-exp of the allowed text tokens
 };
 
 template <int K>
 __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ logits, int ld_logits,
                                                       const uint32_t* __restrict__ suppress_bits, TwSelectParams p,
-                                                      const int* __restrict__ state, BeamPart<K>* __restrict__ ws) {
+                                                      const int* __restrict__ state, BeamPart<K>* __restrict__ ws,
+                                                      int renorm) {
   TW_DEC_PRIO();
   __shared__ Cand wl[2][4][K];
-  __shared__ float wst[4][4];
+  __shared__ float wst[4][6];
   const int b = blockIdx.x, c = blockIdx.y, NC = gridDim.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const RowMask rm = row_mask(state + b * TW_STATE_STRIDE, p);
@@ -623,7 +625,7 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
   Cand T[K], S[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) T[j] = S[j] = Cand{-INFINITY, 0x7fffffff};
-  float m_all = -INFINITY, s_all = 0.f, m_ts = -INFINITY, s_ts = 0.f;
+  float m_all = -INFINITY, s_all = 0.f, m_ts = -INFINITY, s_ts = 0.f, m_tx = -INFINITY, s_tx = 0.f;
   auto visit = [&](int v, float x, uint32_t sbw) {
     lse_merge(m_all, s_all, x, 1.f);
     bool masked = (sbw >> (v & 31)) & 1u;
@@ -641,6 +643,7 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
     if (masked) return;
     if (v < tsb || !p.use_timestamps) {
       cand_insert<K>(T, x, v);
+      if (renorm) lse_merge(m_tx, s_tx, x, 1.f);
     } else {
       cand_insert<K>(S, x, v);
       lse_merge(m_ts, s_ts, x, 1.f);
@@ -670,6 +673,11 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
     m2 = __shfl_xor(m_ts, o, 64);
     s2 = __shfl_xor(s_ts, o, 64);
     lse_merge(m_ts, s_ts, m2, s2);
+    if (renorm) {
+      m2 = __shfl_xor(m_tx, o, 64);
+      s2 = __shfl_xor(s_tx, o, 64);
+      lse_merge(m_tx, s_tx, m2, s2);
+    }
   }
   // a chunk wholly below the timestamps has no timestamp candidate (14 of the 16 chunks at large-v3 sizes), one
   // wholly inside them no text candidate: that list's K dependent argmax rounds (here and in the merge below) are
@@ -682,6 +690,8 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
     wst[wid][1] = s_all;
     wst[wid][2] = m_ts;
     wst[wid][3] = s_ts;
+    wst[wid][4] = m_tx;
+    wst[wid][5] = s_tx;
   }
   __syncthreads();
   if (wid != 0) return;
@@ -717,15 +727,18 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
     }
   }
   if (lane == 0) {
-    float ma = wst[0][0], sa = wst[0][1], mt = wst[0][2], st2 = wst[0][3];
+    float ma = wst[0][0], sa = wst[0][1], mt = wst[0][2], st2 = wst[0][3], mx = wst[0][4], sx = wst[0][5];
     for (int w = 1; w < 4; ++w) {
       lse_merge(ma, sa, wst[w][0], wst[w][1]);
       lse_merge(mt, st2, wst[w][2], wst[w][3]);
+      lse_merge(mx, sx, wst[w][4], wst[w][5]);
     }
     out->m_all = ma;
     out->s_all = sa;
     out->m_ts = mt;
     out->s_ts = st2;
+    out->m_tx = mx;
+    out->s_tx = sx;
   }
 }
 
@@ -743,10 +756,14 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
   __shared__ int old_fin[TW_BEAM_MAXNB][TW_BEAM_MAXT];
   __shared__ int old_st[TW_BEAM_MAXNB][TW_STATE_STRIDE];
   __shared__ int old_tab[TW_BEAM_MAXNB][TW_BEAM_MAXT];  // the K/V position table rows (bs.kv_tab)
+  __shared__ int old_ftab[TW_BEAM_MAXNB][TW_BEAM_MAXT];  // the finished hypotheses' tables (bs.fin_tab)
   __shared__ int old_pos[TW_BEAM_MAXNB];
   __shared__ int old_flen[TW_BEAM_MAXNB];
   __shared__ int s_src[TW_BEAM_MAXNB], s_tok[TW_BEAM_MAXNB], f_from[TW_BEAM_MAXNB], f_flag[TW_BEAM_MAXNB];
   __shared__ float s_score[TW_BEAM_MAXNB], f_score[TW_BEAM_MAXNB];
+  // (bs.run_lp: every candidate's running sum of log-probabilities renormalised over the allowed tokens — what
+  // _retrieve_avg_logprobs takes from the processed beam scores — carried beside the beam scores)
+  __shared__ float rc_lp[TW_BEAM_MAXNB][K], c_lp[2 * K], s_lp[TW_BEAM_MAXNB], f_lp[TW_BEAM_MAXNB];
   __shared__ int c_beam[2 * K], c_tok[2 * K];
   // per-row sorted lists and the one-thread bookkeeping arrays live in LDS: as per-thread arrays with runtime
   // indices they were lowered to scratch (224-768 B/lane) and the serial section ran at scratch latency
@@ -755,6 +772,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
   __shared__ bool hits[2 * K];
   const int w = blockIdx.x, nb = bp.num_beams, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int ldt = bp.ld_tokens;
+  const bool lpt = bs.run_lp != nullptr && bs.fin_lp != nullptr;
   int* win = bs.win + 4 * w;
   const int t = win[2];
   const float NEG = -1.0e9f;
@@ -762,8 +780,9 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
   // step 1 (as a load-then-LDS-store loop after it, each trip waited for its own loads); positions past a history's
   // length are staged too (any value: they are never read back)
   constexpr int STG = (TW_BEAM_MAXNB * TW_BEAM_MAXT + 511) / 512;
-  int rt[STG], rf[STG], rk[STG];
+  int rt[STG], rf[STG], rk[STG], rft[STG];
   const bool tab = bs.kv_tab != nullptr;
+  const bool ftab = tab && bs.fin_tab != nullptr;
 #pragma unroll
   for (int u = 0; u < STG; ++u) {
     const int e = tid + 512 * u, j = e / TW_BEAM_MAXT, q = e % TW_BEAM_MAXT;
@@ -772,6 +791,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
     rt[u] = ok ? tokens[off] : 0;
     rf[u] = ok ? bs.fin_tokens[off] : 0;
     rk[u] = ok && tab ? bs.kv_tab[off] : 0;
+    rft[u] = ok && ftab ? bs.fin_tab[off] : 0;
   }
   const int st_v = tid < nb * TW_STATE_STRIDE ? state[(w * nb) * TW_STATE_STRIDE + tid] : 0;
   const int fl_v = tid < nb ? bs.fin_len[w * nb + tid] : 0;
@@ -781,10 +801,11 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
   if (wid < nb) {
     const int row = w * nb + wid;
     const BeamPart<K>* parts = ws + (size_t)row * NC;
-    float m_all = -INFINITY, s_all = 0.f, m_ts = -INFINITY, s_ts = 0.f;
+    float m_all = -INFINITY, s_all = 0.f, m_ts = -INFINITY, s_ts = 0.f, m_tx = -INFINITY, s_tx = 0.f;
     for (int c = lane; c < NC; c += 64) {
       lse_merge(m_all, s_all, parts[c].m_all, parts[c].s_all);
       lse_merge(m_ts, s_ts, parts[c].m_ts, parts[c].s_ts);
+      if (lpt) lse_merge(m_tx, s_tx, parts[c].m_tx, parts[c].s_tx);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -793,6 +814,11 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
       m2 = __shfl_xor(m_ts, o, 64);
       s2 = __shfl_xor(s_ts, o, 64);
       lse_merge(m_ts, s_ts, m2, s2);
+      if (lpt) {
+        m2 = __shfl_xor(m_tx, o, 64);
+        s2 = __shfl_xor(s_tx, o, 64);
+        lse_merge(m_tx, s_tx, m2, s2);
+      }
     }
     // top-K of the text list and of the timestamp list over the NC chunk lists (<= 4 entries per lane)
     Cand(*top)[K] = tops[wid];
@@ -837,6 +863,14 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
       // WhisperTimeStampLogitsProcessor: timestamp mass above every text token -> text tokens -inf
       const bool fires = p.use_timestamps && lse_ts > top[0][0].v;
       const float run = bs.run_score[row];
+      // the allowed set log_softmax renormalises over: the allowed timestamps alone when the rule fires
+      float lse_ok = 0.f, run_lp = 0.f;
+      if (lpt) {
+        const float lse_tx = (m_tx == -INFINITY) ? -INFINITY : m_tx + __logf(s_tx);
+        lse_ok = fires ? lse_ts : (lse_tx == -INFINITY ? lse_ts : lse_ts == -INFINITY ? lse_tx
+                                   : fmaxf(lse_tx, lse_ts) + log1pf(__expf(-fabsf(lse_tx - lse_ts))));
+        run_lp = bs.run_lp[row];
+      }
       int a = 0, bb = 0;
       for (int k = 0; k < K; ++k) {
         Cand pick;
@@ -848,6 +882,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
           pick = top[1][bb++];
         }
         rc[wid][k] = Cand{pick.v == -INFINITY ? -INFINITY : run + (pick.v - lse_all), pick.i};
+        if (lpt) rc_lp[wid][k] = pick.v == -INFINITY ? -INFINITY : run_lp + (pick.v - lse_ok);
       }
     }
   }
@@ -859,6 +894,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
       old_tok[j][q] = rt[u];
       old_fin[j][q] = rf[u];
       old_tab[j][q] = rk[u];
+      old_ftab[j][q] = rft[u];
     }
   }
   if (tid < nb * TW_STATE_STRIDE) old_st[tid / TW_STATE_STRIDE][tid % TW_STATE_STRIDE] = st_v;
@@ -888,6 +924,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
       c_beam[rank] = j;
       c_tok[rank] = rc[j][k].i;
       csc[rank] = v;
+      if (lpt) c_lp[rank] = rc_lp[j][k];
     }
   }
   __syncthreads();
@@ -922,6 +959,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
       s_src[rank] = c_beam[c];
       s_tok[rank] = c_tok[c];
       s_score[rank] = rsc[c];
+      if (lpt) s_lp[rank] = c_lp[c];
     }
   }
   // f. finished beams: best nb of the nb + K merged scores (ties -> lower e)
@@ -933,6 +971,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
       f_from[rank] = e;
       f_score[rank] = merged[e];
       f_flag[rank] = e < nb ? bs.fin_flag[w * nb + e] : (hits[e - nb] && e - nb < nb);
+      if (lpt) f_lp[rank] = e < nb ? bs.fin_lp[w * nb + e] : c_lp[e - nb];
     }
   }
   __syncthreads();
@@ -978,6 +1017,18 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
       v = q < t ? old_tok[c_beam[c]][q] : c_tok[c];
     }
     if (q < len) bs.fin_tokens[(size_t)(w * nb + qs) * ldt + q] = v;
+    // the rows that fed the history's positions: a kept slot's own table, or (just finished) its source beam's
+    // table up to the position the source fed this step
+    if (ftab && q < ldt) {
+      int r;
+      if (from < nb) {
+        r = old_ftab[from][q];
+      } else {
+        const int src = c_beam[from - nb];
+        r = q <= old_pos[src] ? old_tab[src][q] : 0;
+      }
+      bs.fin_tab[(size_t)(w * nb + qs) * ldt + q] = r;
+    }
   }
   if (tid < nb) {
     const int j = tid, row = w * nb + j, src = s_src[j], tok = s_tok[j];
@@ -995,6 +1046,10 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
     bs.fin_score[row] = f_score[j];
     bs.fin_flag[row] = f_flag[j];
     bs.fin_len[row] = from < nb ? old_flen[from] : t + 1;
+    if (lpt) {
+      bs.run_lp[row] = s_lp[j];
+      bs.fin_lp[row] = f_lp[j];
+    }
   }
 }
 
@@ -1005,7 +1060,7 @@ static int launch_beam(const float* logits, int W, int ld_logits, const uint32_t
   const int R = W * bp->num_beams;
   BeamPart<K>* ws = (BeamPart<K>*)workspace;
   hipLaunchKernelGGL(k_beam_partial<K>, dim3(R, TW_SELECT_CHUNKS), dim3(256), 0, s, logits, ld_logits, suppress_bits,
-                     *p, state, ws);
+                     *p, state, ws, (int)(bs.run_lp != nullptr && bs.fin_lp != nullptr));
   hipLaunchKernelGGL(k_beam_step<K>, dim3(W), dim3(512), 0, s, ws, TW_SELECT_CHUNKS, *p, *bp, bs, state, tokens, ids,
                      pos);
   return tw_check_launch("tw_beam_step");

@@ -1011,19 +1011,50 @@ class WhisperEngine:
                 "src_rows": torch.zeros(self.max_rows, dtype=torch.int32, device=dev),
                 "ws": torch.empty(ws_bytes, dtype=torch.uint8, device=dev),
                 "kv_tab": torch.empty(self.max_rows, T, dtype=torch.int32, device=dev),
+                "fin_tab": torch.zeros(self.max_rows, T, dtype=torch.int32, device=dev),
             }
         return self._beam
 
     @on_engine_streams
     def beam_pass(self, W: int, num_beams: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
                   use_timestamps: bool = True, check_every: int = 8, length_penalty: float = 1.0,
-                  enc_row0: int = 0, r_enc: Optional[int] = None, prefix=None) -> PassResult:
+                  enc_row0: int = 0, r_enc: Optional[int] = None, prefix=None, align: bool = False,
+                  num_frames: Optional[Sequence[int]] = None) -> PassResult:
         """Beam-search decode (GenerationMixin._beam_search, $TF/generation/utils.py:3208-3512) of W windows with
         num_beams rows each (row = w * num_beams + j, all reading window w's cross-K/V): the prompt as
         decode_pass (language detected from the SOT step when lang_ids is None), then per token one decoder step
         over all rows and tw_beam_step (which also repoints the self-attention K/V position table). Returns the best finished hypothesis of
         every window (with its EOS when it ended on one). enc_row0 / r_enc: the windows' first row and the batch
-        the cross-K/V slot was encoded with (default 0 / W)."""
+        the cross-K/V slot was encoded with (default 0 / W). align: also every window's token-level timestamps, from
+        the alignment heads' cross-attention of the rows that fed its best hypothesis (the kernel's fin_tab: generate's
+        beam_indices, generation_whisper.py:265-300; past a hypothesis' end, row 0's, as index -1 -> 0 there)."""
+        if align:
+            P = 1 + (1 if self.gen.special.is_multilingual else 0) + len(tail)
+            self._align_setup(W * num_beams, P, max_new)
+            try:
+                res = self.beam_pass(W, num_beams, tail, lang_ids, max_new, use_timestamps, check_every, length_penalty,
+                                     enc_row0, r_enc, prefix)
+                bb = self._beam
+                nb, st = num_beams, self.gen.special
+                lens = [len(t) for t in res.tokens]  # generated tokens, EOS included (beam_indices' entries)
+                rows = max(lens) - 1 if lens else 0
+                res.token_ts = []
+                if rows > 0:
+                    al = self._align
+                    b = al["buf"][: W * nb * al["n_steps"] * al["n_slots"] * S_ENC].view(
+                        W * nb, al["n_steps"], al["n_slots"], S_ENC)
+                    ftab = bb["fin_tab"][: W * nb: nb, P: P + rows].long()  # rows that fed positions P .. P+rows-1
+                    i = torch.arange(rows, device=self.device)
+                    ftab = torch.where(i[None, :] + 1 < torch.tensor(lens, device=self.device)[:, None], ftab, 0)
+                    w = b[ftab, i[None, :]].permute(0, 2, 1, 3)[:, al["perm"]].float().cpu().numpy()
+                for k in range(W):
+                    nf = None if num_frames is None else int(num_frames[k])
+                    ts = (alignment.token_timestamps(w[k], 0, nf, self.gen.median_filter_width) if rows > 0
+                          else np.zeros(1, np.float32))
+                    res.token_ts.append(np.concatenate([np.zeros(P, np.float32), ts]))
+                return res
+            finally:
+                self._align = None
         nb, R = num_beams, W * num_beams
         r_enc = W if r_enc is None else r_enc
         if R > self.max_rows:
@@ -1077,7 +1108,8 @@ class WhisperEngine:
             bp = _lib.TwBeamParams(nb, max_new, float(length_penalty), T)
             bst = _lib.TwBeamState(bb["run_score"].data_ptr(), bb["fin_score"].data_ptr(), bb["fin_flag"].data_ptr(),
                                    bb["fin_len"].data_ptr(), bb["fin_tokens"].data_ptr(), bb["win"].data_ptr(),
-                                   bb["src_rows"].data_ptr(), bb["kv_tab"].data_ptr())
+                                   bb["src_rows"].data_ptr(), bb["kv_tab"].data_ptr(),
+                                   bb["fin_tab"].data_ptr() if self._align is not None else None)
             s = self.stream.cuda_stream
 
             def step() -> None:
@@ -1091,8 +1123,9 @@ class WhisperEngine:
             # (eager, each of its ~100 launches would be issued from the host every token)
             g = None
             if self.use_graphs:
+                al = self._align
                 key = ("beam", R, nb, max_new, bool(use_timestamps), float(length_penalty), self._slot, r_enc,
-                       self._masked)
+                       self._masked, None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()))
                 g = self._graphs.get(key)
                 if g is None:
                     g = torch.cuda.CUDAGraph()
@@ -1210,8 +1243,6 @@ class WhisperEngine:
         # language: given, or detected on the first pass (seek == 0, the whole 30-s window) as
         # _retrieve_init_tokens -> detect_language does before the seek loop
         langs: List[Optional[int]] = list(lang_ids)[:n_chunks] if lang_ids is not None else [None] * n_chunks
-        if word_timestamps and num_beams > 1:
-            raise NotImplementedError("word-level timestamps with beam search are not implemented (greedy only)")
         fb = fallback if fallback is not None and fallback.active else None
         if fb is not None and (num_beams > 1 or word_timestamps):
             raise NotImplementedError("temperature fallback / segment criteria with beam search or word-level "
@@ -1301,7 +1332,8 @@ class WhisperEngine:
                 if num_beams > 1:  # pre-encoded first pass: this part's windows sit at encoder rows b0..
                     pre = pre_encoded and passes == 0
                     res = self.beam_pass(R, num_beams, tail, given, mnew, use_timestamps=return_timestamps,
-                                         enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R, prefix=pfx)
+                                         enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R, prefix=pfx,
+                                         align=word_timestamps, num_frames=nf_part)
                 else:
                     res = self.decode_pass(R, tail, given, mnew, use_timestamps=return_timestamps,
                                            align=word_timestamps, num_frames=nf_part, prefix=pfx)

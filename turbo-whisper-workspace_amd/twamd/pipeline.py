@@ -115,9 +115,6 @@ class TurboTranscriber:
         num_beams = dec["num_beams"]
         if num_beams < 1 or num_beams > 8:
             raise ValueError(f"num_beams={num_beams}: the engine supports 1 (greedy) to 8 beams")
-        if word and num_beams > 1:
-            raise NotImplementedError("word-level timestamps with beam search are not implemented; pass "
-                                      "generate_kwargs={'num_beams': 1} (the pipeline's default decode is beam-5)")
         task = gk.pop("task", None)
         language = gk.pop("language", None)
         max_new_tokens = dec["max_new_tokens"]
