@@ -219,6 +219,10 @@ typedef struct TwBeamState {
                           * that fed each position of its history (kv_tab of its source at the step it finished,
                           * positions 0 .. its last fed one) — the beam_indices of token-level timestamps
                           * (generation_whisper.py:265-300): position p's cross-attention is that row's.       */
+  float* run_lp;         /* f32[R] or NULL (with fin_lp): per running beam the sum of its tokens' log-probabilities
+                          * renormalised over the allowed tokens (log_softmax of the processed beam scores:
+                          * _retrieve_avg_logprobs, generation_whisper.py:1958-1975); initialise 0                  */
+  float* fin_lp;         /* f32[R] or NULL: the same sum of each finished slot's hypothesis                       */
 } TwBeamState;
 /* workspace: tw_beam_workspace_bytes(R) bytes of device memory. */
 size_t tw_beam_workspace_bytes(int rows);

@@ -453,16 +453,18 @@ def test_fallback_keys_are_global_window_indices():
     assert seen == [([5, 5], 10)]  # run_batches adds each batch's offset: keys of windows 10..19
 
 
-def test_checkpoint_thresholds_with_default_beams_say_why():
+def test_checkpoint_thresholds_turn_the_fallback_on_and_say_why():
     """a checkpoint whose generation_config sets a fallback threshold turns the fallback on for every
-    call; with the pipeline's default beam-5 the call raises and names the checkpoint field."""
+    call. With the pipeline's default beam-5 the call runs (beam rounds inside the fallback); with word-level
+    timestamps, which the fallback does not take, it raises and names the checkpoint field."""
     from twamd.pipeline import TurboTranscriber
     eng = _FakeEngine(8)
     eng.gen.logprob_threshold = -1.0
     tr = TurboTranscriber(eng, WhisperVocab.synthetic(ST))
     wav = np.zeros(16000, np.float32)
     with pytest.raises(NotImplementedError, match="logprob_threshold"):
-        tr(wav, chunk_length_s=30, generate_kwargs={"task": "transcribe"}, return_timestamps=True)
-    out = tr(wav, chunk_length_s=30, generate_kwargs={"task": "transcribe", "num_beams": 1, "max_passes": 1},
-             return_timestamps=True)
-    assert "text" in out
+        tr(wav, chunk_length_s=30, generate_kwargs={"task": "transcribe", "num_beams": 1}, return_timestamps="word")
+    for nb in (None, 1):
+        gk = {"task": "transcribe", "max_passes": 1, **({"num_beams": nb} if nb else {})}
+        out = tr(wav, chunk_length_s=30, generate_kwargs=gk, return_timestamps=True)
+        assert "text" in out

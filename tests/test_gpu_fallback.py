@@ -259,5 +259,83 @@ def test_temperature_fallback_resamples_failing_windows(mini):
     assert "text" in r and "chunks" in r
     with pytest.raises(ValueError, match="not supported"):
         mini(audio, chunk_length_s=30, generate_kwargs={"num_beams": 1, "bogus_kwarg": 1})
-    with pytest.raises(NotImplementedError):
-        mini(audio, chunk_length_s=30, generate_kwargs={"temperature": (0.0, 0.2), "logprob_threshold": -1.0})
+    r = mini(audio, chunk_length_s=30, generate_kwargs={"temperature": (0.0, 0.2), "logprob_threshold": -1.0,
+                                                         "max_new_tokens": 24})  # (the default decode: beam-5)
+    assert "text" in r
+
+
+# ---- the fallback with beam search (num_beams = 3) vs transformers (tests/golden/fallback_beam.json) ----------------
+@pytest.fixture(scope="module")
+def fbz():
+    return json.load(open(os.path.join(G, "fallback_beam.json")))
+
+
+def test_beam_first_pass_criteria_vs_transformers(mini, fbz):
+    """beam_pass(criteria=True) over the three windows: the best hypotheses, their average log-probability from the
+    scores renormalised over the allowed tokens (what _retrieve_avg_logprobs takes from the processed beam scores) and
+    the no-speech probability at <|startoftranscript|>, against the values transformers' _need_fallback saw on the
+    first seek pass with num_beams=3."""
+    eng = mini.engine
+    _load3(mini)
+    eng.row_map[:3] = torch.arange(3, dtype=torch.int32)
+    eng.seek[:3] = 0
+    eng.encode(3)
+    st = mini.gen.special
+    tail = eng.prompt_tail("transcribe", True)
+    res = eng.beam_pass(3, 3, tail, None, 24, criteria=True, no_speech_token=st.notimestamps - 1)
+    compared = 0
+    for i, c in enumerate(fbz["metrics"]["calls"][:3]):
+        toks = [int(t) for t in res.tokens[i]]
+        ref = c["tokens"]
+        avg = res.sum_logprob[i] / len(toks)
+        print(f"window {i}: tokens equal {toks == ref}, avg logprob {avg:.4f} vs {c['avg_logprob']:.4f}, "
+              f"no-speech {res.no_speech_prob[i]:.3e} vs {c['no_speech_prob']:.3e}")
+        if toks == ref:
+            assert abs(avg - c["avg_logprob"]) < 0.03
+            compared += 1
+        assert abs(res.no_speech_prob[i] - c["no_speech_prob"]) <= 0.1 * c["no_speech_prob"]
+    assert compared >= 2
+
+
+def test_beam_fallback_outcome_matches_transformers(mini, fbz):
+    """FALLBACK_SKIP with num_beams=3 (one temperature: the criteria are evaluated, nothing re-decodes): generate()'s
+    sequences."""
+    eng = mini.engine
+    _load3(mini)
+    kw = fbz["skip"]["kwargs"]
+    fb = FallbackConfig(temperatures=tuple(kw["temperature"]), logprob_threshold=kw["logprob_threshold"],
+                        no_speech_threshold=kw["no_speech_threshold"])
+    seqs = eng.generate(3, task="transcribe", max_new_tokens=24, return_timestamps=True, fallback=fb, num_beams=3)
+    eot = mini.gen.special.eot
+    for i, ref in enumerate(fbz["skip"]["sequences"]):
+        ref = list(ref)
+        while ref and ref[-1] == eot:
+            ref.pop()
+        assert seqs[i] == ref, (i, seqs[i][:8], ref[:8])
+
+
+def test_beam_fallback_sampling_round_turns_the_call_greedy(mini, fbz):
+    """temperature (0.0, 0.4), logprob_threshold -2.5, num_beams=3: the first pass's beam round fails every window
+    (as transformers' decisions in fallback_beam.json "resample"), the retry samples, and from then on the call decodes
+    without beams (transformers leaves generation_config.num_beams = 1): exactly one beam search in the call."""
+    eng = mini.engine
+    _load3(mini)
+    calls = fbz["resample"]["calls"]
+    assert [c["num_beams"] for c in calls][:3] == [3, 3, 3] and all(c["num_beams"] == 1 for c in calls[3:])
+    kw = fbz["resample"]["kwargs"]
+    fb = FallbackConfig(temperatures=tuple(kw["temperature"]), logprob_threshold=kw["logprob_threshold"], seed=3)
+    n_beam = []
+    orig = eng.beam_pass
+
+    def counting(*a, **k):
+        n_beam.append(a[0])
+        return orig(*a, **k)
+
+    eng.beam_pass = counting
+    try:
+        seqs = eng.generate(3, task="transcribe", max_new_tokens=24, return_timestamps=True, fallback=fb, num_beams=3,
+                            max_passes=3)
+    finally:
+        del eng.beam_pass
+    assert n_beam == [3], n_beam
+    assert all(isinstance(s, list) for s in seqs)

@@ -63,7 +63,8 @@ class TwBeamParams(ctypes.Structure):
 class TwBeamState(ctypes.Structure):
     _fields_ = [("run_score", ctypes.c_void_p), ("fin_score", ctypes.c_void_p), ("fin_flag", ctypes.c_void_p),
                 ("fin_len", ctypes.c_void_p), ("fin_tokens", ctypes.c_void_p), ("win", ctypes.c_void_p),
-                ("src_rows", ctypes.c_void_p), ("kv_tab", ctypes.c_void_p), ("fin_tab", ctypes.c_void_p)]
+                ("src_rows", ctypes.c_void_p), ("kv_tab", ctypes.c_void_p), ("fin_tab", ctypes.c_void_p),
+                ("run_lp", ctypes.c_void_p), ("fin_lp", ctypes.c_void_p)]
 
 
 class TwFlacInfo(ctypes.Structure):

@@ -1012,6 +1012,8 @@ class WhisperEngine:
                 "ws": torch.empty(ws_bytes, dtype=torch.uint8, device=dev),
                 "kv_tab": torch.empty(self.max_rows, T, dtype=torch.int32, device=dev),
                 "fin_tab": torch.zeros(self.max_rows, T, dtype=torch.int32, device=dev),
+                "run_lp": torch.zeros(self.max_rows, dtype=torch.float32, device=dev),
+                "fin_lp": torch.zeros(self.max_rows, dtype=torch.float32, device=dev),
             }
         return self._beam
 
@@ -1019,7 +1021,8 @@ class WhisperEngine:
     def beam_pass(self, W: int, num_beams: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
                   use_timestamps: bool = True, check_every: int = 8, length_penalty: float = 1.0,
                   enc_row0: int = 0, r_enc: Optional[int] = None, prefix=None, align: bool = False,
-                  num_frames: Optional[Sequence[int]] = None) -> PassResult:
+                  num_frames: Optional[Sequence[int]] = None, enc_rows: Optional[Sequence[int]] = None,
+                  criteria: bool = False, no_speech_token: Optional[int] = None) -> PassResult:
         """Beam-search decode (GenerationMixin._beam_search, $TF/generation/utils.py:3208-3512) of W windows with
         num_beams rows each (row = w * num_beams + j, all reading window w's cross-K/V): the prompt as
         decode_pass (language detected from the SOT step when lang_ids is None), then per token one decoder step
@@ -1027,7 +1030,11 @@ class WhisperEngine:
         every window (with its EOS when it ended on one). enc_row0 / r_enc: the windows' first row and the batch
         the cross-K/V slot was encoded with (default 0 / W). align: also every window's token-level timestamps, from
         the alignment heads' cross-attention of the rows that fed its best hypothesis (the kernel's fin_tab: generate's
-        beam_indices, generation_whisper.py:265-300; past a hypothesis' end, row 0's, as index -1 -> 0 there)."""
+        beam_indices, generation_whisper.py:265-300; past a hypothesis' end, row 0's, as index -1 -> 0 there).
+        enc_rows: each window's encoder row (instead of enc_row0 + w: a fallback round's subset). criteria: also each
+        best hypothesis' sum of log-probabilities renormalised over the allowed tokens (the fallback's average
+        log-probability numerator, tw_beam_step's fin_lp) and, with no_speech_token, WhisperNoSpeechDetection's
+        probability at the <|startoftranscript|> step (PassResult.sum_logprob / no_speech_prob)."""
         if align:
             P = 1 + (1 if self.gen.special.is_multilingual else 0) + len(tail)
             self._align_setup(W * num_beams, P, max_new)
@@ -1064,7 +1071,11 @@ class WhisperEngine:
         T = self.d.max_target_positions
         bb = self._beam_buffers(R)
         self.stream.wait_event(self._enc_ev[self._slot])
-        self.dec_row_map[:R] = enc_row0 + torch.arange(R, dtype=torch.int32, device=dev) // nb
+        if enc_rows is not None:
+            self.dec_row_map[:R] = torch.as_tensor([int(enc_rows[w]) for w in range(W) for _ in range(nb)],
+                                                   dtype=torch.int32, device=dev)
+        else:
+            self.dec_row_map[:R] = enc_row0 + torch.arange(R, dtype=torch.int32, device=dev) // nb
         self._use_dec_row_map = True
         self._row_group = nb  # rows w * nb + j share window w's cross K/V
         # self-attention K/V position table: every row starts on its own history; tw_beam_step points a continuing
@@ -1085,13 +1096,23 @@ class WhisperEngine:
             if st.is_multilingual:
                 prompt_rest.append(None if lang_ids is None else [int(x) for x in lang_ids for _ in range(nb)])
             prompt_rest.extend(int(t) for t in tail)
+            V = self.d.vocab
+
+            def no_speech() -> None:  # the logits of the step that fed <|startoftranscript|>
+                if no_speech_token is not None:
+                    _lib.call("tw_token_prob", self.logits.data_ptr(), R, V, V, int(no_speech_token),
+                              self.state.data_ptr(), self.stream.cuda_stream)
+
             for k, tok in enumerate(prompt_rest):
                 if k == 0 and st.is_multilingual and lang_ids is None:
                     self.decoder_step(R, r_enc=r_enc)
+                    no_speech()
                     self._select(R, self._select_params(1, max_new), tokens=False)  # ids <- lang, pos += 1
                     detected = self.state[:R:nb, _lib.TW_ST_LANG].tolist()
                     continue
-                self.decoder_step(R, with_logits=False, r_enc=r_enc)
+                self.decoder_step(R, with_logits=k == 0 and no_speech_token is not None, r_enc=r_enc)
+                if k == 0:
+                    no_speech()
                 if isinstance(tok, list):
                     self.ids[:R] = torch.as_tensor(tok, dtype=torch.int32, device=dev)
                 else:
@@ -1102,6 +1123,9 @@ class WhisperEngine:
             bb["fin_score"][:R] = -1e9
             bb["fin_flag"][:R] = 0
             bb["fin_len"][:R] = 0
+            if criteria:
+                bb["run_lp"][:R] = 0.0
+                bb["fin_lp"][:R] = 0.0
             bb["win"][:W] = torch.tensor([1, 0, 0, 0], dtype=torch.int32, device=dev)
             self.state[:R, _lib.TW_ST_NGEN] = 0
             sel = self._select_params(0, max_new, use_timestamps)
@@ -1109,7 +1133,9 @@ class WhisperEngine:
             bst = _lib.TwBeamState(bb["run_score"].data_ptr(), bb["fin_score"].data_ptr(), bb["fin_flag"].data_ptr(),
                                    bb["fin_len"].data_ptr(), bb["fin_tokens"].data_ptr(), bb["win"].data_ptr(),
                                    bb["src_rows"].data_ptr(), bb["kv_tab"].data_ptr(),
-                                   bb["fin_tab"].data_ptr() if self._align is not None else None)
+                                   bb["fin_tab"].data_ptr() if self._align is not None else None,
+                                   bb["run_lp"].data_ptr() if criteria else None,
+                                   bb["fin_lp"].data_ptr() if criteria else None)
             s = self.stream.cuda_stream
 
             def step() -> None:
@@ -1125,7 +1151,8 @@ class WhisperEngine:
             if self.use_graphs:
                 al = self._align
                 key = ("beam", R, nb, max_new, bool(use_timestamps), float(length_penalty), self._slot, r_enc,
-                       self._masked, None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()))
+                       self._masked, None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()),
+                       bool(criteria))
                 g = self._graphs.get(key)
                 if g is None:
                     g = torch.cuda.CUDAGraph()
@@ -1134,7 +1161,14 @@ class WhisperEngine:
                     self._graphs[key] = g
             steps = 0
             while steps < max_new:
-                if g is not None:
+                if steps == 0 and not prompt_rest and no_speech_token is not None:
+                    # (a bare <|startoftranscript|> prompt: its step is the first beam step, eager with the probability)
+                    self.decoder_step(R, r_enc=r_enc)
+                    no_speech()
+                    _lib.call("tw_beam_step", self.logits.data_ptr(), W, V, self.suppress_bits.data_ptr(),
+                              ctypes.byref(sel), ctypes.byref(bp), ctypes.byref(bst), self.state.data_ptr(),
+                              self.tokens.data_ptr(), self.ids.data_ptr(), self.pos.data_ptr(), bb["ws"].data_ptr(), s)
+                elif g is not None:
                     g.replay()
                 else:
                     step()
@@ -1144,11 +1178,15 @@ class WhisperEngine:
                         break
             flen = bb["fin_len"][:R:nb].tolist()
             ftok = bb["fin_tokens"][:R:nb].tolist()
+            sum_lp = bb["fin_lp"][:R:nb].tolist() if criteria else None
+            nsp = (self.state[:R:nb, _lib.TW_ST_NOSPEECH].contiguous().view(torch.float32).tolist()
+                   if no_speech_token is not None else None)
         finally:
             self._use_dec_row_map = False
             self._row_group = 1
             self._kv_tab = None
-        return PassResult([ftok[w][: flen[w]] for w in range(W)], detected if lang_ids is None else list(lang_ids))
+        return PassResult([ftok[w][: flen[w]] for w in range(W)], detected if lang_ids is None else list(lang_ids),
+                          sum_logprob=sum_lp, no_speech_prob=nsp)
 
     def _chains(self, R: int) -> List[DecView]:
         """Contiguous row ranges of [0, R), one per decode chain (each with its own partial-sum buffer)."""
@@ -1244,9 +1282,9 @@ class WhisperEngine:
         # _retrieve_init_tokens -> detect_language does before the seek loop
         langs: List[Optional[int]] = list(lang_ids)[:n_chunks] if lang_ids is not None else [None] * n_chunks
         fb = fallback if fallback is not None and fallback.active else None
-        if fb is not None and (num_beams > 1 or word_timestamps):
-            raise NotImplementedError("temperature fallback / segment criteria with beam search or word-level "
-                                      "timestamps are not implemented (greedy passes only)")
+        if fb is not None and word_timestamps:
+            raise NotImplementedError("temperature fallback / segment criteria with word-level timestamps are not "
+                                      "implemented")
         # word timestamps: per chunk the segments' token times (segment token_timestamps of generate(), i.e. the
         # pass's DTW times of the kept tokens + seek * 0.01 s); num_frames: the chunks' valid feature frames
         tts: List[List[float]] = [[] for _ in range(n_chunks)]
@@ -1311,9 +1349,10 @@ class WhisperEngine:
                 nf_part = None if num_frames is None else [int(num_frames[i]) - seek[i] for i in part]
                 if fb is not None:
                     pre = pre_encoded and passes == 0
-                    toks_f, skip_f, lang_f, temp_f = self._fallback_pass(
+                    toks_f, skip_f, lang_f, temp_f, nb_left = self._fallback_pass(
                         R, tail, given, mnew, return_timestamps, fb, [window_offset + i for i in part], passes,
-                        enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R, prefix=pfx)
+                        enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R, prefix=pfx, num_beams=num_beams)
+                    num_beams = nb_left  # (a sampling round left generation_config.num_beams = 1)
                     for j in range(R):  # (by position in the pass's batch, as transformers writes it)
                         do_cond[j] = bool(condition) and (temp_f[j] is None or temp_f[j] < 0.5)
                     for j, i in enumerate(part):
@@ -1366,12 +1405,18 @@ class WhisperEngine:
 
     def _fallback_pass(self, R: int, tail, given, max_new: int, return_timestamps: bool, fb: FallbackConfig,
                        windows: Sequence[int], pass_no: int, enc_row0: int = 0, r_enc: Optional[int] = None,
-                       prefix=None):
+                       prefix=None, num_beams: int = 1):
         """generate_with_fallback (generation_whisper.py:970-1116) for one seek pass of R encoded rows: decode at
         the first temperature, re-decode the rows whose criteria fail at the next one, until none does or the
-        temperatures run out. Returns per row the kept sequence (EOS removed), should_skip, and the language ids.
+        temperatures run out. Returns per row the kept sequence (EOS removed), should_skip, the language ids, each
+        row's last temperature, and the beam count left for the rest of the generate() call.
         Bug-compatible with transformers: needs_fallback / should_skip are written at the row's position in the
-        CURRENT (shrinking) subset, and the main loop reads should_skip by batch position (:1074-1088, :879)."""
+        CURRENT (shrinking) subset, and the main loop reads should_skip by batch position (:1074-1088, :879); the
+        no-speech probability of a retry round is read by subset position from the whole pass's (the processor's
+        inputs are the pass's full batch, :999-1000, logits_process.py WhisperNoSpeechDetection); with num_beams > 1 a
+        round at temperature <= 0 is a beam search (its average log-probability from the hypothesis' renormalised
+        scores, beam_pass(criteria=True)), and a sampling round sets num_beams = 1 for the rest of the call
+        (generation_config.num_beams, :1004-1005, never restored)."""
         st = self.gen.special
         V = self.d.vocab
         idx = list(range(R))
@@ -1381,16 +1426,27 @@ class WhisperEngine:
         ns_tok = st.notimestamps - 1 if fb.no_speech_threshold is not None else None  # no_timestamps_token_id - 1
         temps = list(fb.temperatures) or [None]
         final_t: List[Optional[float]] = [None] * R  # the temperature of each row's last round
+        nb = num_beams
+        ns_pass: Optional[List[float]] = None  # the first round's no-speech probabilities (the whole pass's rows)
         for fi, t in enumerate(temps):
             do_sample = t is not None and t > 0.0
-            res = self.sample_pass(len(idx), tail, None if langs is None else [langs[i] for i in idx], max_new,
-                                   temperature=float(t) if do_sample else 0.0, top_k=fb.top_k, seed=fb.seed,
-                                   row_keys=[fallback_row_key(windows[i], pass_no, fi) for i in idx],
-                                   use_timestamps=return_timestamps, enc_rows=[enc_row0 + i for i in idx],
-                                   r_enc=r_enc, no_speech_token=ns_tok,
-                                   prefix=None if prefix is None else ([prefix[0][i] for i in idx],
-                                                                       [prefix[1][i] for i in idx]))
+            if do_sample:
+                nb = 1
+            sub_lang = None if langs is None else [langs[i] for i in idx]
+            sub_pfx = None if prefix is None else ([prefix[0][i] for i in idx], [prefix[1][i] for i in idx])
+            if nb > 1:
+                res = self.beam_pass(len(idx), nb, tail, sub_lang, max_new, use_timestamps=return_timestamps,
+                                     enc_rows=[enc_row0 + i for i in idx], r_enc=r_enc, prefix=sub_pfx,
+                                     criteria=True, no_speech_token=ns_tok)
+            else:
+                res = self.sample_pass(len(idx), tail, sub_lang, max_new,
+                                       temperature=float(t) if do_sample else 0.0, top_k=fb.top_k, seed=fb.seed,
+                                       row_keys=[fallback_row_key(windows[i], pass_no, fi) for i in idx],
+                                       use_timestamps=return_timestamps, enc_rows=[enc_row0 + i for i in idx],
+                                       r_enc=r_enc, no_speech_token=ns_tok, prefix=sub_pfx)
             self._masked = False
+            if ns_pass is None and res.no_speech_prob is not None:
+                ns_pass = list(res.no_speech_prob)
             for i in idx:
                 final_t[i] = t
             if langs is None and res.lang_ids is not None:  # detected on the first round (all rows)
@@ -1398,8 +1454,7 @@ class WhisperEngine:
             new_idx = []
             for j, toks in enumerate(res.tokens):
                 seq = fallback_sequence(toks, st.eot, st.eot)
-                needs, sk = need_fallback(seq, res.sum_logprob[j],
-                                          None if res.no_speech_prob is None else res.no_speech_prob[j], V, fb)
+                needs, sk = need_fallback(seq, res.sum_logprob[j], None if ns_pass is None else ns_pass[j], V, fb)
                 skip[j] = sk
                 if seq and seq[-1] == st.eot:
                     seq = seq[:-1]
@@ -1409,7 +1464,7 @@ class WhisperEngine:
             idx = new_idx
             if not idx or fi == len(temps) - 1:
                 break
-        return seqs, skip, langs if langs is not None else [None] * R, final_t
+        return seqs, skip, langs if langs is not None else [None] * R, final_t, nb
 
     @on_engine_streams
     def run_batches(self, sizes: Sequence[int], load=None, batch_kwargs: Optional[Sequence[dict]] = None,

@@ -126,14 +126,14 @@ class TurboTranscriber:
         if cond and word:
             raise NotImplementedError("condition_on_prev_tokens with word-level timestamps is not implemented")
         fallback = self._fallback_config(gk)
-        if fallback.active and (num_beams > 1 or word):
+        if fallback.active and word:
             from_ckpt = [k for k in ("compression_ratio_threshold", "logprob_threshold", "no_speech_threshold")
                          if k not in (generate_kwargs or {}) and getattr(self.gen, k, None) is not None]
             raise NotImplementedError(
-                "temperature fallback / segment criteria run with greedy passes only: pass "
-                "generate_kwargs={'num_beams': 1} (the pipeline's default decode is beam-5) and segment-level timestamps"
+                "temperature fallback / segment criteria with word-level timestamps are not implemented: pass "
+                "segment-level timestamps"
                 + (f"; the checkpoint's generation_config.json sets {from_ckpt}, which turns the fallback on for every "
-                   "call, so such a checkpoint needs num_beams=1" if from_ckpt else ""))
+                   "call" if from_ckpt else ""))
         if gk:
             raise ValueError(f"generate_kwargs not supported by this engine: {sorted(gk)}")
         st = self.gen.special
@@ -178,10 +178,14 @@ class TurboTranscriber:
                                                word_timestamps=True, num_frames=nf, group=batch_size,
                                                max_passes=max_passes)
                 return [(t, ts) for t, ts in zip(toks, self.last_window_token_timestamps)]
+            # (batch composition shapes results with conditioned prompts — their left padding — and with beams under
+            # the fallback — a sampling round turns the rest of that generate() call greedy —, so batch_size is kept)
+            grouped = cond or (fallback.active and num_beams > 1)
             return self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=bool(return_timestamps),
                                            max_new_tokens=max_new_tokens, num_beams=num_beams, max_passes=max_passes,
                                            **({"fallback": fallback, "window_base": base} if fallback.active else {}),
-                                           **({"condition_on_prev_tokens": True, "group": batch_size} if cond else {}))
+                                           **({"condition_on_prev_tokens": True} if cond else {}),
+                                           **({"group": batch_size} if grouped else {}))
 
         # one window shard per rank + one all-gather of the token arrays (twamd.dist); plain call on 1 GPU
         outputs = dist.transcribe_sharded(run, wav, windows, timed=word) if world > 1 else run(wav, windows)
