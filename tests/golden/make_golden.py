@@ -14,6 +14,8 @@ in-memory tokenizer built from twamd.tokenizer.synthetic_vocab, then stores smal
                     on seeded random matrices
   beam_word.json    token-level timestamps with beam search (generate() token times, pipeline word chunks)
   fallback_beam.json  the temperature-fallback criteria and outcomes with beam search (num_beams=3)
+  word_combos.json  word timestamps with long-form input / condition_on_prev_tokens / the fallback criteria, and
+                    the fallback with beam search (pipeline outputs)
   longform.json     long-form (unchunked > 30 s) pipeline outputs and condition_on_prev_tokens, with every seek
                     pass's decoder prompt and raw output (spied from generate_with_fallback)
   fallback.json     the temperature-fallback criteria (compression ratio, avg logprob, no-speech probability) of
@@ -351,6 +353,49 @@ def make_beam_word(out):
     with open(os.path.join(out, "beam_word.json"), "w") as f:
         json.dump({"seed": SEED, "dims": "test-mini", "alignment_heads": ALIGN_HEADS_MINI, "num_beams": 3,
                    "generate": gens, "cases": cases}, f)
+
+
+WORD_COMBO_CASES = [  # name, pipeline kwargs, generate_kwargs, return_timestamps
+    ("long_word", {}, {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40}, "word"),
+    ("cond_word", dict(chunk_length_s=30, stride_length_s=0, batch_size=3),
+     {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40, "condition_on_prev_tokens": True}, "word"),
+    ("fallback_word", dict(chunk_length_s=30, stride_length_s=0, batch_size=3),
+     {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40, "temperature": (0.0,), "logprob_threshold": -3.0,
+      "no_speech_threshold": 3e-5}, "word"),
+    ("fallback_beam3", dict(chunk_length_s=30, stride_length_s=0, batch_size=3),
+     {"task": "transcribe", "num_beams": 3, "max_new_tokens": 24, "temperature": (0.0,), "logprob_threshold": -3.0,
+      "no_speech_threshold": 3e-5}, True),
+    ("long_cond_word", {}, {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40,
+                            "condition_on_prev_tokens": True}, "word"),
+]
+
+
+def make_word_combos(out):
+    """The ASR pipeline at test-mini (alignment heads ALIGN_HEADS_MINI) on 75 s of audio with the call options
+    combined: word timestamps on a long-form input, with condition_on_prev_tokens, with the fallback criteria (one
+    temperature: deterministic), and the fallback with beam search."""
+    from transformers import AutomaticSpeechRecognitionPipeline, WhisperFeatureExtractor
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    m.generation_config.alignment_heads = ALIGN_HEADS_MINI
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    pipe = AutomaticSpeechRecognitionPipeline(model=m, feature_extractor=fe, tokenizer=hf_tokenizer(gen.special),
+                                              device=-1)
+    audio = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)]).astype(np.float32)
+    res = []
+    for name, kw, gk, ts in WORD_COMBO_CASES:
+        c = {"name": name, "kwargs": kw, "generate_kwargs": gk, "return_timestamps": ts}
+        try:
+            c["output"] = _jsonable(pipe(audio.copy(), generate_kwargs=dict(gk), return_timestamps=ts, **kw))
+        except Exception as e:  # noqa: BLE001 - recorded as the reference would surface it
+            c["error"] = {"type": type(e).__name__, "message": str(e)}
+        res.append(c)
+    with open(os.path.join(out, "word_combos.json"), "w") as f:
+        json.dump({"dims": "test-mini", "alignment_heads": ALIGN_HEADS_MINI,
+                   "audio": "speech_like(40,5)+white_noise(35,11)", "cases": res}, f)
 
 
 def make_defaults(out):

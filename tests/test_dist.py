@@ -453,18 +453,25 @@ def test_fallback_keys_are_global_window_indices():
     assert seen == [([5, 5], 10)]  # run_batches adds each batch's offset: keys of windows 10..19
 
 
-def test_checkpoint_thresholds_turn_the_fallback_on_and_say_why():
+def test_checkpoint_thresholds_turn_the_fallback_on():
     """a checkpoint whose generation_config sets a fallback threshold turns the fallback on for every
-    call. With the pipeline's default beam-5 the call runs (beam rounds inside the fallback); with word-level
-    timestamps, which the fallback does not take, it raises and names the checkpoint field."""
+    call; with the pipeline's default beam-5 the call runs (beam rounds inside the fallback) as with greedy passes,
+    and the engine receives the checkpoint's criteria."""
     from twamd.pipeline import TurboTranscriber
     eng = _FakeEngine(8)
     eng.gen.logprob_threshold = -1.0
+    seen = []
+    orig = eng.run_batches
+
+    def rb(sizes, load=None, batch_kwargs=None, **kw):
+        seen.append((kw.get("num_beams"), kw.get("fallback")))
+        return orig(sizes, load, batch_kwargs, **kw)
+
+    eng.run_batches = rb
     tr = TurboTranscriber(eng, WhisperVocab.synthetic(ST))
     wav = np.zeros(16000, np.float32)
-    with pytest.raises(NotImplementedError, match="logprob_threshold"):
-        tr(wav, chunk_length_s=30, generate_kwargs={"task": "transcribe", "num_beams": 1}, return_timestamps="word")
     for nb in (None, 1):
         gk = {"task": "transcribe", "max_passes": 1, **({"num_beams": nb} if nb else {})}
         out = tr(wav, chunk_length_s=30, generate_kwargs=gk, return_timestamps=True)
         assert "text" in out
+    assert [nb for nb, _ in seen] == [5, 1] and all(f.logprob_threshold == -1.0 for _, f in seen)

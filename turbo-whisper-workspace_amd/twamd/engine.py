@@ -768,6 +768,26 @@ class WhisperEngine:
         self.decoder_step(R, v=v, r_enc=r_enc, pre_embedded=fused)
         self._select(R, params, v=v, embed_next=fused)
 
+    def _prompt_len(self, tail: Sequence[int], prefix=None) -> int:
+        """decoder_input_ids' length: [prefix] + SOT (+ language) + tail (num_input_ids of the token timestamps)."""
+        L = len(prefix[0][0]) if prefix is not None and prefix[0] else 0
+        return L + 1 + (1 if self.gen.special.is_multilingual else 0) + len(tail)
+
+    def _token_ts(self, R: int, P: int, res: PassResult, num_frames: Optional[Sequence[int]]) -> None:
+        """res.token_ts from the alignment heads' probabilities of a greedy / sampled pass (self._align): the pass's
+        rows standardised over its padded length (max generated - 1 fed tokens), as _extract_token_timestamps does
+        over the batch (generation_whisper.py:241-381); prompt positions 0."""
+        st = self.gen.special
+        real = [(t.index(st.eot) + 1) if st.eot in t else len(t) for t in res.tokens]
+        rows = max(real) - 1 if real else 0
+        w = self._align_weights(R, rows) if rows > 0 else None
+        res.token_ts = []
+        for r in range(R):
+            nf = None if num_frames is None else int(num_frames[r])
+            ts = (alignment.token_timestamps(w[r], 0, nf, self.gen.median_filter_width) if w is not None
+                  else np.zeros(1, np.float32))
+            res.token_ts.append(np.concatenate([np.zeros(P, np.float32), ts]))
+
     def _prefill(self, R: int, prefix, r_enc: Optional[int] = None) -> int:
         """condition_on_prev_tokens: feed a pass's left-padded prefix (per row [<|startofprev|>] + the previous
         segments' tokens, generation_whisper.py:1853-1918) at positions 0 .. L-1 ahead of the init tokens; returns L.
@@ -802,20 +822,11 @@ class WhisperEngine:
         timestamps (alignment-head cross-attention of the fed tokens -> DTW; num_frames: the rows' valid frames
         minus their seek, as generate() passes them)."""
         if align:
-            P = 1 + (1 if self.gen.special.is_multilingual else 0) + len(tail)
+            P = self._prompt_len(tail, prefix)
             self._align_setup(R, P, max_new)
             try:
-                res = self.decode_pass(R, tail, lang_ids, max_new, check_every, use_timestamps)
-                st = self.gen.special
-                real = [(t.index(st.eot) + 1) if st.eot in t else len(t) for t in res.tokens]
-                rows = max(real) - 1 if real else 0
-                w = self._align_weights(R, rows) if rows > 0 else None
-                res.token_ts = []
-                for r in range(R):
-                    nf = None if num_frames is None else int(num_frames[r])
-                    ts = (alignment.token_timestamps(w[r], 0, nf, self.gen.median_filter_width) if w is not None
-                          else np.zeros(1, np.float32))
-                    res.token_ts.append(np.concatenate([np.zeros(P, np.float32), ts]))
+                res = self.decode_pass(R, tail, lang_ids, max_new, check_every, use_timestamps, prefix=prefix)
+                self._token_ts(R, P, res, num_frames)
                 return res
             finally:
                 self._align = None
@@ -921,13 +932,25 @@ class WhisperEngine:
     def sample_pass(self, R: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
                     temperature: float = 0.0, top_k: int = 50, seed: int = 0, row_keys: Optional[Sequence[int]] = None,
                     use_timestamps: bool = True, enc_rows: Optional[Sequence[int]] = None, r_enc: Optional[int] = None,
-                    no_speech_token: Optional[int] = None, check_every: int = 8, prefix=None) -> PassResult:
+                    no_speech_token: Optional[int] = None, check_every: int = 8, prefix=None, align: bool = False,
+                    num_frames: Optional[Sequence[int]] = None) -> PassResult:
         """One decode pass of the temperature-fallback loop (WhisperGenerationMixin.generate_with_fallback,
         generation_whisper.py:970-1116), eager, one tw_logits_sample per token: greedy when temperature == 0
         (the tokens of decode_pass), else a draw from softmax(processed / T) over the top_k scores. Per row it also
         returns the sum of the chosen tokens' log-probabilities (the avg_logprob criterion's numerator) and, with
         no_speech_token, WhisperNoSpeechDetection's probability of it at the SOT position. enc_rows: the encoder
-        rows (of the r_enc-row encoded batch in this slot) the R decoder rows read (default 0..R-1)."""
+        rows (of the r_enc-row encoded batch in this slot) the R decoder rows read (default 0..R-1). align: also the
+        rows' token-level timestamps (as decode_pass)."""
+        if align:
+            P = self._prompt_len(tail, prefix)
+            self._align_setup(R, P, max_new)
+            try:
+                res = self.sample_pass(R, tail, lang_ids, max_new, temperature, top_k, seed, row_keys, use_timestamps,
+                                       enc_rows, r_enc, no_speech_token, check_every, prefix)
+                self._token_ts(R, P, res, num_frames)
+                return res
+            finally:
+                self._align = None
         st = self.gen.special
         dev = self.device
         r_enc = R if r_enc is None else r_enc
@@ -1036,11 +1059,12 @@ class WhisperEngine:
         log-probability numerator, tw_beam_step's fin_lp) and, with no_speech_token, WhisperNoSpeechDetection's
         probability at the <|startoftranscript|> step (PassResult.sum_logprob / no_speech_prob)."""
         if align:
-            P = 1 + (1 if self.gen.special.is_multilingual else 0) + len(tail)
+            P = self._prompt_len(tail, prefix)
             self._align_setup(W * num_beams, P, max_new)
             try:
                 res = self.beam_pass(W, num_beams, tail, lang_ids, max_new, use_timestamps, check_every, length_penalty,
-                                     enc_row0, r_enc, prefix)
+                                     enc_row0, r_enc, prefix, enc_rows=enc_rows, criteria=criteria,
+                                     no_speech_token=no_speech_token)
                 bb = self._beam
                 nb, st = num_beams, self.gen.special
                 lens = [len(t) for t in res.tokens]  # generated tokens, EOS included (beam_indices' entries)
@@ -1282,17 +1306,12 @@ class WhisperEngine:
         # _retrieve_init_tokens -> detect_language does before the seek loop
         langs: List[Optional[int]] = list(lang_ids)[:n_chunks] if lang_ids is not None else [None] * n_chunks
         fb = fallback if fallback is not None and fallback.active else None
-        if fb is not None and word_timestamps:
-            raise NotImplementedError("temperature fallback / segment criteria with word-level timestamps are not "
-                                      "implemented")
         # word timestamps: per chunk the segments' token times (segment token_timestamps of generate(), i.e. the
         # pass's DTW times of the kept tokens + seek * 0.01 s); num_frames: the chunks' valid feature frames
         tts: List[List[float]] = [[] for _ in range(n_chunks)]
         # condition_on_prev_tokens: every chunk's segments so far (current_segments' "tokens") and the per-position
         # flags of generate_with_fallback (written at the row's position in the pass's batch, read by chunk index:
         # transformers' indexing, :1089-1093 / :1885)
-        if condition_on_prev_tokens and word_timestamps:
-            raise NotImplementedError("condition_on_prev_tokens with word-level timestamps is not implemented")
         seg_lists: List[List[List[int]]] = [[] for _ in range(n_chunks)]
         do_cond = [bool(condition_on_prev_tokens)] * n_chunks
         prev_sot = self.gen.prev_sot_token_id
@@ -1349,9 +1368,10 @@ class WhisperEngine:
                 nf_part = None if num_frames is None else [int(num_frames[i]) - seek[i] for i in part]
                 if fb is not None:
                     pre = pre_encoded and passes == 0
-                    toks_f, skip_f, lang_f, temp_f, nb_left = self._fallback_pass(
+                    toks_f, skip_f, lang_f, temp_f, nb_left, ts_f = self._fallback_pass(
                         R, tail, given, mnew, return_timestamps, fb, [window_offset + i for i in part], passes,
-                        enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R, prefix=pfx, num_beams=num_beams)
+                        enc_row0=b0 if pre else 0, r_enc=n_chunks if pre else R, prefix=pfx, num_beams=num_beams,
+                        align=word_timestamps, num_frames=nf_part)
                     num_beams = nb_left  # (a sampling round left generation_config.num_beams = 1)
                     for j in range(R):  # (by position in the pass's batch, as transformers writes it)
                         do_cond[j] = bool(condition) and (temp_f[j] is None or temp_f[j] < 0.5)
@@ -1366,6 +1386,8 @@ class WhisperEngine:
                         seg_tokens, offset = retrieve_segment(toks_f[j], seek[i], snf, st.timestamp_begin)
                         segs[i].extend(seg_tokens)
                         seg_lists[i].extend(segment_slices(toks_f[j], st.timestamp_begin))
+                        if word_timestamps:
+                            self._add_times(tts[i], ts_f[j], prompt_len + L, len(seg_tokens), seek[i])
                         seek[i] += offset
                     continue
                 if num_beams > 1:  # pre-encoded first pass: this part's windows sit at encoder rows b0..
@@ -1389,9 +1411,7 @@ class WhisperEngine:
                     segs[i].extend(seg_tokens)
                     seg_lists[i].extend(segment_slices(seq, st.timestamp_begin))
                     if word_timestamps:
-                        raw = res.token_ts[j][prompt_len: prompt_len + len(seg_tokens)]
-                        off = np.float32(seek[i] * 0.02 / 2)  # time_offset = seek * time_precision / input_stride
-                        tts[i].extend(float(np.float32(x) + off) for x in raw)
+                        self._add_times(tts[i], res.token_ts[j], prompt_len + L, len(seg_tokens), seek[i])
                     seek[i] += offset
             passes += 1
             if max_passes is not None and passes >= max_passes:
@@ -1403,13 +1423,22 @@ class WhisperEngine:
         self.last_token_timestamps = tts if word_timestamps else None
         return segs
 
+    @staticmethod
+    def _add_times(out: List[float], token_ts: np.ndarray, P: int, n: int, seek: int) -> None:
+        """A segment's token_timestamps (_retrieve_segment, :2034-2037): the pass's times of its n kept tokens (after the
+        P prompt positions) + time_offset = seek * time_precision / input_stride."""
+        off = np.float32(seek * 0.02 / 2)
+        out.extend(float(np.float32(x) + off) for x in token_ts[P: P + n])
+
     def _fallback_pass(self, R: int, tail, given, max_new: int, return_timestamps: bool, fb: FallbackConfig,
                        windows: Sequence[int], pass_no: int, enc_row0: int = 0, r_enc: Optional[int] = None,
-                       prefix=None, num_beams: int = 1):
+                       prefix=None, num_beams: int = 1, align: bool = False,
+                       num_frames: Optional[Sequence[int]] = None):
         """generate_with_fallback (generation_whisper.py:970-1116) for one seek pass of R encoded rows: decode at
         the first temperature, re-decode the rows whose criteria fail at the next one, until none does or the
         temperatures run out. Returns per row the kept sequence (EOS removed), should_skip, the language ids, each
-        row's last temperature, and the beam count left for the rest of the generate() call.
+        row's last temperature, the beam count left for the rest of the generate() call and (align) each row's token
+        times from the round that decided it (its round's batch: _postprocess_outputs per round, :1051).
         Bug-compatible with transformers: needs_fallback / should_skip are written at the row's position in the
         CURRENT (shrinking) subset, and the main loop reads should_skip by batch position (:1074-1088, :879); the
         no-speech probability of a retry round is read by subset position from the whole pass's (the processor's
@@ -1428,23 +1457,29 @@ class WhisperEngine:
         final_t: List[Optional[float]] = [None] * R  # the temperature of each row's last round
         nb = num_beams
         ns_pass: Optional[List[float]] = None  # the first round's no-speech probabilities (the whole pass's rows)
+        row_ts: List[Optional[np.ndarray]] = [None] * R
         for fi, t in enumerate(temps):
             do_sample = t is not None and t > 0.0
             if do_sample:
                 nb = 1
             sub_lang = None if langs is None else [langs[i] for i in idx]
             sub_pfx = None if prefix is None else ([prefix[0][i] for i in idx], [prefix[1][i] for i in idx])
+            sub_nf = None if num_frames is None else [num_frames[i] for i in idx]
             if nb > 1:
                 res = self.beam_pass(len(idx), nb, tail, sub_lang, max_new, use_timestamps=return_timestamps,
                                      enc_rows=[enc_row0 + i for i in idx], r_enc=r_enc, prefix=sub_pfx,
-                                     criteria=True, no_speech_token=ns_tok)
+                                     criteria=True, no_speech_token=ns_tok, align=align, num_frames=sub_nf)
             else:
                 res = self.sample_pass(len(idx), tail, sub_lang, max_new,
                                        temperature=float(t) if do_sample else 0.0, top_k=fb.top_k, seed=fb.seed,
                                        row_keys=[fallback_row_key(windows[i], pass_no, fi) for i in idx],
                                        use_timestamps=return_timestamps, enc_rows=[enc_row0 + i for i in idx],
-                                       r_enc=r_enc, no_speech_token=ns_tok, prefix=sub_pfx)
+                                       r_enc=r_enc, no_speech_token=ns_tok, prefix=sub_pfx, align=align,
+                                       num_frames=sub_nf)
             self._masked = False
+            if align:
+                for j, i in enumerate(idx):
+                    row_ts[i] = res.token_ts[j]
             if ns_pass is None and res.no_speech_prob is not None:
                 ns_pass = list(res.no_speech_prob)
             for i in idx:
@@ -1464,7 +1499,7 @@ class WhisperEngine:
             idx = new_idx
             if not idx or fi == len(temps) - 1:
                 break
-        return seqs, skip, langs if langs is not None else [None] * R, final_t, nb
+        return seqs, skip, langs if langs is not None else [None] * R, final_t, nb, (row_ts if align else None)
 
     @on_engine_streams
     def run_batches(self, sizes: Sequence[int], load=None, batch_kwargs: Optional[Sequence[dict]] = None,

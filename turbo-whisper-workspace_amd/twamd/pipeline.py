@@ -123,17 +123,7 @@ class TurboTranscriber:
         # prompt every seek pass after a window's first with its previous segments (generate()'s
         # condition_on_prev_tokens; the batch then shapes results through the left padding, so batch_size is kept)
         cond = bool(gk.pop("condition_on_prev_tokens", None) or False)
-        if cond and word:
-            raise NotImplementedError("condition_on_prev_tokens with word-level timestamps is not implemented")
         fallback = self._fallback_config(gk)
-        if fallback.active and word:
-            from_ckpt = [k for k in ("compression_ratio_threshold", "logprob_threshold", "no_speech_threshold")
-                         if k not in (generate_kwargs or {}) and getattr(self.gen, k, None) is not None]
-            raise NotImplementedError(
-                "temperature fallback / segment criteria with word-level timestamps are not implemented: pass "
-                "segment-level timestamps"
-                + (f"; the checkpoint's generation_config.json sets {from_ckpt}, which turns the fallback on for every "
-                   "call" if from_ckpt else ""))
         if gk:
             raise ValueError(f"generate_kwargs not supported by this engine: {sorted(gk)}")
         st = self.gen.special
@@ -170,22 +160,20 @@ class TurboTranscriber:
 
         def run(w, ws):
             base = windows.index(ws[0]) if ws else 0  # this shard's first global window (the sampler's row keys)
+            # (batch composition shapes results with word timestamps — standardised over the padded batch —, with
+            # conditioned prompts — their left padding — and with beams under the fallback — a sampling round turns the
+            # rest of that generate() call greedy —, so batch_size is kept there)
+            grouped = word or cond or (fallback.active and num_beams > 1)
+            kw = dict(task=task, lang_id=lang_id, return_timestamps=bool(return_timestamps) or word,
+                      max_new_tokens=max_new_tokens, num_beams=num_beams, max_passes=max_passes,
+                      **({"fallback": fallback, "window_base": base} if fallback.active else {}),
+                      **({"condition_on_prev_tokens": True} if cond else {}),
+                      **({"group": batch_size} if grouped else {}))
             if word:  # token times ride along as floats after the tokens (one all-gather carries both)
-                nf = [min(x.length, CHUNK_SAMPLES) // 160 + (1 if min(x.length, CHUNK_SAMPLES) % 160 else 0)
-                      for x in ws]
-                toks = self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=True,
-                                               max_new_tokens=max_new_tokens, num_beams=num_beams,
-                                               word_timestamps=True, num_frames=nf, group=batch_size,
-                                               max_passes=max_passes)
+                nf = [-(-min(x.length, CHUNK_SAMPLES) // 160) for x in ws]
+                toks = self.transcribe_windows(w, ws, word_timestamps=True, num_frames=nf, **kw)
                 return [(t, ts) for t, ts in zip(toks, self.last_window_token_timestamps)]
-            # (batch composition shapes results with conditioned prompts — their left padding — and with beams under
-            # the fallback — a sampling round turns the rest of that generate() call greedy —, so batch_size is kept)
-            grouped = cond or (fallback.active and num_beams > 1)
-            return self.transcribe_windows(w, ws, task=task, lang_id=lang_id, return_timestamps=bool(return_timestamps),
-                                           max_new_tokens=max_new_tokens, num_beams=num_beams, max_passes=max_passes,
-                                           **({"fallback": fallback, "window_base": base} if fallback.active else {}),
-                                           **({"condition_on_prev_tokens": True} if cond else {}),
-                                           **({"group": batch_size} if grouped else {}))
+            return self.transcribe_windows(w, ws, **kw)
 
         # one window shard per rank + one all-gather of the token arrays (twamd.dist); plain call on 1 GPU
         outputs = dist.transcribe_sharded(run, wav, windows, timed=word) if world > 1 else run(wav, windows)
@@ -225,15 +213,15 @@ class TurboTranscriber:
         stride; every rank computes it (nothing to shard: each pass depends on the previous one's seek)."""
         # (the pipeline never passes return_timestamps=False on to generate(), asr:506-508, so generate() switches
         # timestamps on for a long-form input instead of raising; the text is then decoded without them)
-        if return_timestamps == "word":
-            raise NotImplementedError("word-level timestamps on a long-form input (> 30 s without chunk_length_s) "
-                                      "are not implemented; pass chunk_length_s")
+        word = return_timestamps == "word"
         eng = self.engine
         lang_id = self._lang_id(language)
         x = wav if torch.is_tensor(wav) else torch.from_numpy(np.ascontiguousarray(wav, np.float32))
         eng.set_long_input(x)
         try:
             kw = {"fallback": fallback} if fallback.active else {}
+            if word:  # num_frames: the feature extractor's attention mask, one per hop (_set_num_frames)
+                kw.update(word_timestamps=True, num_frames=[-(-int(x.shape[0]) // 160)])
             toks = eng.generate(1, task=task, lang_ids=None if lang_id is None else [lang_id],
                                 max_new_tokens=max_new_tokens, return_timestamps=True, num_beams=num_beams,
                                 max_passes=max_passes, condition_on_prev_tokens=condition, **kw)[0]
@@ -242,7 +230,11 @@ class TurboTranscriber:
         self.last_window_langs = list(eng.last_langs)
         self.last_window_passes = list(eng.last_passes)
         self.last_window_prefixes = list(eng.last_pass_prefixes)
-        text, optional = decode_asr(self.vocab, [{"tokens": toks}], return_timestamps=bool(return_timestamps),
+        out = {"tokens": toks}
+        if word:
+            self.last_window_token_timestamps = list(eng.last_token_timestamps)
+            out["token_timestamps"] = eng.last_token_timestamps[0]
+        text, optional = decode_asr(self.vocab, [out], return_timestamps="word" if word else bool(return_timestamps),
                                     return_language=return_language,
                                     time_precision=time_precision(self.engine.d.max_source_positions))
         return {"text": text, **optional}
