@@ -249,6 +249,10 @@ int tw_kv_reorder(uint16_t* k_cache, uint16_t* v_cache, uint16_t* k_scratch, uin
 int tw_pack_weight(const uint16_t* W, int N, int K, int ldw, uint16_t* Wp, void* stream);
 int tw_gemv_packed(const uint16_t* A, int a_packed, int lda, const uint16_t* Wp, int M, int N, int K, int epi,
                    void* out, int ldo, const float* bias, int splits, void* stream);
+/* Process-wide K-slice count (1, 2 or 4; default 1) of tw_gemv_packed's vocabulary-wide case (N >= 16384: proj_out):
+ * 1 beside a running encoder GEMM, 4 when the decode has the GPU to itself. Same results up to the f32 order of the
+ * K-slice sum. Returns 0. */
+int tw_gemv_set_wide_slices(int kw);
 /* tw_resid_layernorm with the normalised rows written as a packed activation (M <= 64, D % 32 == 0). */
 int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
                               const float* beta, int M, int D, float eps, uint16_t* out, void* stream);

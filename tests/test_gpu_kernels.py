@@ -545,6 +545,31 @@ GEMV_CASES = [  # M, N, K, epi, splits
 ]
 
 
+@pytest.mark.parametrize("kw", [2, 4])
+@pytest.mark.parametrize("M,K", [(24, 1280), (60, 1280), (5, 384), (33, 64)])
+def test_gemv_wide_k_slices_vs_torch(M, K, kw):
+    """The vocabulary-wide proj_out with 2 / 4 K-slices per column group (tw_gemv_set_wide_slices: decode passes with no
+    encoder beside them) against torch fp32 and against the one-slice launch (same products, f32 order only); K too
+    short for the slices falls back to fewer."""
+    N = 51866
+    A = rand_bf16(M, K, seed=43)
+    W = rand_bf16(N, K, scale=K ** -0.5, seed=44)
+    Wp, Ain = pack_w(W), pack_act(A)
+    outs = []
+    for k in (1, kw):
+        _lib.call("tw_gemv_set_wide_slices", k)
+        out = torch.full((M, N), float("nan"), device=DEV)
+        _lib.call("tw_gemv_packed", Ain.data_ptr(), 1, K, Wp.data_ptr(), M, N, K, _lib.TW_EPI_F32, out.data_ptr(), N,
+                  None, 1, S())
+        outs.append(out)
+    _lib.call("tw_gemv_set_wide_slices", 1)
+    ref = A.float() @ W.float().t()
+    torch.testing.assert_close(outs[1], ref, atol=2e-3, rtol=2e-3)
+    torch.testing.assert_close(outs[1], outs[0], atol=1e-4, rtol=1e-4)
+    with pytest.raises(_lib.TwError):
+        _lib.call("tw_gemv_set_wide_slices", 3)
+
+
 @pytest.mark.parametrize("a_packed", [1, 0])
 @pytest.mark.parametrize("M,N,K,epi,splits", GEMV_CASES)
 def test_gemv_packed_vs_torch(M, N, K, epi, splits, a_packed):

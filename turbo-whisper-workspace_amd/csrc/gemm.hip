@@ -81,6 +81,15 @@ static int tw_gemm_kernel = 1;
 static inline int tw_group_for(int N) { return (N + 255) / 256 >= 10 ? 8 : 1; }
 // packed GEMVs with N >= this (proj_out) read their weights non-temporally: bench step -1 ms (109.2 vs 110.3)
 static constexpr int tw_gemv_nt_min_n = 16384;
+// K-slices per column group of the vocabulary-wide proj_out (tw_gemv_set_wide_slices): 1 beside an encoder GEMM (its
+// MALL residency is what the other decoder weights lose: bench 93.1 vs 92.5 ms with 2 / 4), 4 for a decode pass with the
+// GPU to itself (22.7 vs 33 us per launch alone at 24 rows)
+static int tw_gemv_wide_kw = 1;
+extern "C" int tw_gemv_set_wide_slices(int kw) {
+  TW_REQUIRE(kw == 1 || kw == 2 || kw == 4, "tw_gemv_set_wide_slices: kw=%d (1, 2 or 4)", kw);
+  tw_gemv_wide_kw = kw;
+  return 0;
+}
 // Largest K-slice count the packed-GEMV heuristic picks: 4 = at most 256-thread workgroups, so one decoder wave per
 // SIMD co-resides with an encoder GEMM workgroup (2 waves of ~190 VGPRs on every SIMD), where a 512-thread decoder
 // workgroup waits for GEMM workgroups to retire (q/k/v GEMV beside k_gemm_8p: 33.6 us per launch at 8, 11.5 at 4).
@@ -1070,7 +1079,9 @@ static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
   // non-temporal weight loads (its MALL residency is what the decoder's layer weights would lose)
   const bool wide = N >= tw_gemv_nt_min_n;
   if (wide) {
-    launch_gemv_p3<EPI, 1, 16, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
+    if (tw_gemv_wide_kw == 4 && steps >= 8 * 4) launch_gemv_p3<EPI, 4, 8, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
+    else if (tw_gemv_wide_kw >= 2 && steps >= 8 * 2) launch_gemv_p3<EPI, 2, 8, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
+    else launch_gemv_p3<EPI, 1, 16, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
     return;
   }
   if constexpr (EPI == TW_EPI_BF16 || EPI == TW_EPI_PARTIAL || EPI == TW_EPI_GELU_PACKED) {

@@ -43,6 +43,7 @@ EXPORTED = (
     "tw_attn_set_lds_pad", "tw_logits_sample", "tw_token_prob", "tw_g711_decode", "tw_ima_adpcm_wav_decode",
     "tw_kv_tab_check", "tw_debug_build", "tw_resid_layernorm_packed_to", "tw_conv2_gemm",
     "tw_logmel_long", "tw_im2col_conv1_long", "tw_attn_decode_self_masked", "tw_attn_decode_self_tab_masked",
+    "tw_gemv_set_wide_slices",
 )
 
 
@@ -114,6 +115,7 @@ _SIGS = {
                           _P, _I, _P, _P, _P], _I),
     "tw_token_prob": ([_P, _I, _I, _I, _I, _P, _P], _I),
     "tw_gemm_bf16_partial": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P], _I),
+    "tw_gemv_set_wide_slices": ([_I], _I),
     "tw_gemm_set_variant": ([_I], _I),
     "tw_gemm_mx_set_variant": ([_I], _I),
     "tw_logits_select_embed": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), _P, _P, _I, _P, _P, _P, _P, _P, _I,

@@ -245,6 +245,7 @@ class WhisperEngine:
         # prefix; while _masked, the self-attention masks those positions (tw_attn_decode_self_masked)
         self._kv_start = torch.zeros(self.max_rows, dtype=torch.int32, device=dev)
         self._masked = False
+        self._wide_kw = 1  # the library's tw_gemv_set_wide_slices state (its default)
         self._beam: Optional[dict] = None  # beam-search buffers, allocated on first use
         self._align: Optional[dict] = None  # token-level timestamps: alignment-head attention recording
         self._align_buf: Optional[torch.Tensor] = None
@@ -768,6 +769,20 @@ class WhisperEngine:
         self.decoder_step(R, v=v, r_enc=r_enc, pre_embedded=fused)
         self._select(R, params, v=v, embed_next=fused)
 
+    # K-slices of the vocabulary-wide proj_out for a decode pass with no encoder beside it (the pipeline's last batch, a
+    # single-batch call, beam passes of the as-shipped call, long-form): 4 (22.7 vs 33 us per launch alone); beside an
+    # encoder chunk 1. TW_DEC_ALONE_WIDE_KW overrides (1 / 2 / 4).
+    dec_alone_wide_kw = int(os.environ.get("TW_DEC_ALONE_WIDE_KW", "4"))
+
+    def _dec_context(self) -> int:
+        """Set the proj_out K-slice count for a pass starting now: alone unless run_batches' encoder pump is queued
+        beside it. Graph keys carry the returned value (a captured step bakes the launch it recorded)."""
+        kw = 1 if self._pump is not None else self.dec_alone_wide_kw
+        if kw != self._wide_kw:
+            _lib.call("tw_gemv_set_wide_slices", kw)
+            self._wide_kw = kw
+        return kw
+
     def _prompt_len(self, tail: Sequence[int], prefix=None) -> int:
         """decoder_input_ids' length: [prefix] + SOT (+ language) + tail (num_input_ids of the token timestamps)."""
         L = len(prefix[0][0]) if prefix is not None and prefix[0] else 0
@@ -832,6 +847,7 @@ class WhisperEngine:
                 self._align = None
         st = self.gen.special
         dev = self.device
+        self._dec_context()
         self.stream.wait_event(self._enc_ev[self._slot])  # the cross-K/V of this slot is written
         detect = st.is_multilingual and lang_ids is None
         params = self._select_params(0, max_new, use_timestamps)
@@ -867,7 +883,7 @@ class WhisperEngine:
         if self.use_graphs and self.prompt_graph and (detect or not st.is_multilingual) and not base:
             al = self._align  # (keyed like _graph_for: an alignment pass captures the probability-recording kernel)
             key = ("prompt", R, tuple(int(t) for t in tail), max_new, use_timestamps, self._slot,
-                   None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()))
+                   None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()), self._wide_kw)
             g = self._graphs.get(key)
             if g is None:
                 g = torch.cuda.CUDAGraph()
@@ -954,6 +970,7 @@ class WhisperEngine:
         st = self.gen.special
         dev = self.device
         r_enc = R if r_enc is None else r_enc
+        self._dec_context()
         self.stream.wait_event(self._enc_ev[self._slot])
         detect = st.is_multilingual and lang_ids is None
         params = self._select_params(0, max_new, use_timestamps)
@@ -1094,6 +1111,7 @@ class WhisperEngine:
         dev = self.device
         T = self.d.max_target_positions
         bb = self._beam_buffers(R)
+        self._dec_context()
         self.stream.wait_event(self._enc_ev[self._slot])
         if enc_rows is not None:
             self.dec_row_map[:R] = torch.as_tensor([int(enc_rows[w]) for w in range(W) for _ in range(nb)],
@@ -1176,7 +1194,7 @@ class WhisperEngine:
                 al = self._align
                 key = ("beam", R, nb, max_new, bool(use_timestamps), float(length_penalty), self._slot, r_enc,
                        self._masked, None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()),
-                       bool(criteria))
+                       bool(criteria), self._wide_kw)
                 g = self._graphs.get(key)
                 if g is None:
                     g = torch.cuda.CUDAGraph()
@@ -1231,7 +1249,7 @@ class WhisperEngine:
     def _graph_for(self, R: int, params, i: int, v: DecView, fused: bool = False) -> Optional[torch.cuda.CUDAGraph]:
         al = self._align
         key = (R, params.max_new, params.use_timestamps, self._slot, i, fused,
-               None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()), self._masked)
+               None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()), self._masked, self._wide_kw)
         g = self._graphs.get(key)
         if g is not None:
             return g
