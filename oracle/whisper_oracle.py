@@ -740,7 +740,8 @@ def pass_criteria(model: WhisperOracle, feats: np.ndarray, g: GenCfg, prompt: Se
 
 def generate_batch_word(model: WhisperOracle, feats_list: Sequence[np.ndarray], g: GenCfg, alignment_heads,
                         num_frames: Sequence[int], task: Optional[str] = "transcribe", language: Optional[int] = None,
-                        max_new_tokens: Optional[int] = None, median_width: int = 7, forced=None):
+                        max_new_tokens: Optional[int] = None, median_width: int = 7, forced=None,
+                        max_frames: Optional[Sequence[int]] = None):
     """generate(return_timestamps=True, return_token_timestamps=True) over a BATCH of windows (greedy), as the
     ASR pipeline's batched forward runs it: every seek pass decodes the batch's active rows together, and
     _extract_token_timestamps runs over the pass's padded batch -- rows that hit EOS keep being fed the pad
@@ -750,14 +751,14 @@ def generate_batch_word(model: WhisperOracle, feats_list: Sequence[np.ndarray], 
 
     forced: optional per window (language id, [raw tokens of every seek pass]) of a device decode; the passes are
     then teacher-forced instead of decoded greedily (token-level timestamps of the device's own tokens, for inputs
-    where bf16 took the other side of a greedy near-tie)."""
+    where bf16 took the other side of a greedy near-tie). max_frames: per window its feature frames (a long-form
+    input's; default 3000)."""
     n = len(feats_list)
     feats_list = [np.asarray(f, np.float32) for f in feats_list]
+    maxf = list(max_frames) if max_frames is not None else [3000] * n
 
     def enc_at(i, seek):
-        seg = np.zeros_like(feats_list[i])
-        seg[:, : 3000 - seek] = feats_list[i][:, seek:]
-        return model.encode(seg)
+        return model.encode(segment_input(feats_list[i], seek, maxf[i]))
 
     langs: List[Optional[int]] = [None] * n
     prompts = []
@@ -777,8 +778,8 @@ def generate_batch_word(model: WhisperOracle, feats_list: Sequence[np.ndarray], 
     outs: List[List[int]] = [[] for _ in range(n)]
     tts: List[List[float]] = [[] for _ in range(n)]
     npass = [0] * n
-    while any(s < 3000 for s in seek):
-        act = [i for i in range(n) if seek[i] < 3000]
+    while any(seek[i] < maxf[i] for i in range(n)):
+        act = [i for i in range(n) if seek[i] < maxf[i]]
         seqs, xs, caches = {}, {}, {}
         for i in act:
             xs[i], co = {}, []
@@ -803,7 +804,7 @@ def generate_batch_word(model: WhisperOracle, feats_list: Sequence[np.ndarray], 
             w = np.stack([np.stack([xs[i][t][l][h] for t in range(rows)]) for l, h in alignment_heads])
             raw_ts = token_timestamps(w, P, num_frames[i] - seek[i], median_width)
             seq = seqs[i][:-1] if seqs[i][-1] == g.eot else seqs[i]
-            toks, off = retrieve_segment(seq, 3000 - seek[i], g.ts_begin)
+            toks, off = retrieve_segment(seq, min(maxf[i] - seek[i], 3000), g.ts_begin)
             outs[i] += toks
             o = np.float32(seek[i] * 0.02 / 2)
             tts[i] += [float(np.float32(x) + o) for x in raw_ts[P: P + len(toks)]]

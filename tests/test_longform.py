@@ -108,3 +108,29 @@ def test_long_form_seek_positions(gold):
             _, off = retrieve_segment(p["sequences"][0], seek, min(T - seek, 3000), st.timestamp_begin)
             seek += off
         assert seek >= T
+
+
+def test_oracle_long_form_word_timestamps_match_transformers():
+    """The oracle's generate_batch_word over a long-form input (max_frames = the input's frames, num_frames = the
+    feature extractor's attention mask length ceil(n / 160)) through the host's decode_asr equals the transformers
+    pipeline's return_timestamps="word" output on 75 s without chunking (word_combos.json "long_word") exactly: the
+    semantics the engine's long-form word path follows."""
+    from twamd.frontend import time_precision
+    from twamd.tokenizer import WhisperVocab, decode_asr
+
+    gold = json.load(open(os.path.join(G, "word_combos.json")))
+    case = next(c for c in gold["cases"] if c["name"] == "long_word")
+    gen = GenerationSettings.default(D)
+    st = gen.special
+    g = wo.GenCfg(D.vocab, st.eot, st.sot, st.lang_begin, st.n_languages, st.transcribe, st.translate,
+                  st.notimestamps, gen.suppress_tokens, gen.begin_suppress_tokens)
+    m = wo.WhisperOracle(wo.synth_state_dict(D.d_model, D.encoder_layers, D.decoder_layers, D.ffn, D.n_mels, D.vocab,
+                                             1234), D.heads)
+    x = _audio()
+    f = wo.log_mel(x, D.n_mels, long=True)
+    heads = [tuple(h) for h in gold["alignment_heads"]]
+    (toks, _, tts), = wo.generate_batch_word(m, [f], g, heads, [-(-len(x) // 160)], max_new_tokens=40,
+                                             max_frames=[f.shape[1]])
+    text, opt = decode_asr(WhisperVocab.synthetic(st), [{"tokens": toks, "token_timestamps": tts}],
+                           return_timestamps="word", return_language=False, time_precision=time_precision(1500))
+    assert json.loads(json.dumps({"text": text, **opt})) == case["output"]
