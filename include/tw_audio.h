@@ -11,6 +11,7 @@
  *                                    bit-exact PCM (checked against the stream's own STREAMINFO MD5)
  *   tw_g711_decode                   G.711 mu-law / A-law expansion (WAV, AU, AIFF-C telephony codecs)
  *   tw_ima_adpcm_wav_decode          IMA ADPCM in WAV blocks
+ *   tw_vorbis_probe / tw_vorbis_decode  Ogg Vorbis I (floor 1, residues 0/1/2, coupling, IMDCT, overlap-add)
  *   tw_resample_pcm_i32 / _f32       downmix + polyphase resample on the GPU (DEVICE memory, `stream`), the
  *                                    libswresample default filter restated (Kaiser-windowed sinc, see
  *                                    twamd/audio.py: swr_filter_bank)
@@ -68,6 +69,27 @@ int tw_g711_decode(const uint8_t* in, int64_t n, int32_t alaw, int16_t* out);
  * interleaved (HOST); *frames_decoded receives the frames written (1 + 8 * whole words per channel per block). */
 int tw_ima_adpcm_wav_decode(const uint8_t* data, int64_t size, int32_t channels, int32_t block_align, int16_t* out,
                             int64_t out_frames, int64_t* frames_decoded);
+
+typedef struct TwVorbisInfo {
+  int32_t sample_rate;   /* Hz (identification header)                                            */
+  int32_t channels;      /* 1..16                                                                 */
+  int32_t blocksize0;    /* short / long MDCT block sizes                                         */
+  int32_t blocksize1;
+  int64_t total_samples; /* per channel: the granule position of the stream's last audio page      */
+} TwVorbisInfo;
+
+/* Ogg Vorbis I (HOST memory; the first logical stream of the file): check the Ogg pages (CRC-32) and parse the
+ * identification, comment and setup headers. Floor type 0 streams are refused with an error. */
+int tw_vorbis_probe(const uint8_t* data, int64_t size, TwVorbisInfo* info);
+
+/* Decode every audio packet into out = f32[out_frames][channels] (interleaved, HOST; the codec's own scale,
+ * nominally [-1, 1]). out_frames must be >= info.total_samples. The first packet primes the overlap (no output);
+ * the end is trimmed to the last page's granule position. *frames_decoded receives the frames written. */
+int tw_vorbis_decode(const uint8_t* data, int64_t size, float* out, int64_t out_frames, int64_t* frames_decoded);
+
+/* The Vorbis inverse MDCT alone (for tests): y[i] = sum_{k < n/2} X[k] cos(2 pi / n (i + 1/2 + n/4)(k + 1/2)),
+ * i < n, n a power of two >= 4. HOST memory. */
+int tw_vorbis_imdct(const float* X, int32_t n, float* y);
 
 #ifdef __cplusplus
 }

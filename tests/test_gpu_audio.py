@@ -60,6 +60,24 @@ def test_flac_bytes_through_load_input():
     assert np.abs(got - ref).max() < TOL
 
 
+def test_ogg_vorbis_bytes_through_load_input():
+    """Native Vorbis decode (host) -> GPU downmix + resample, against the oracle's decoder + float64 resampler:
+    the image's real libVorbis file when present, and a random-syntax stream from the oracle's writer."""
+    import os
+
+    from oracle import vorbis_oracle as vo
+
+    real = "/usr/local/lib/python3.10/dist-packages/kaleido/executable/etc/mathjax/extensions/a11y/invalid_keypress.ogg"
+    streams = [open(real, "rb").read()] if os.path.exists(real) else []
+    streams.append(vo.write_stream(np.random.default_rng(7), channels=2, bs_exp=(7, 9), n_packets=14, rate=44100))
+    for data in streams:
+        x, sr = vo.decode(data)
+        got = audio.load_input(data)
+        ref = ao.swr_resample(x.astype(np.float64).mean(axis=1), sr, 16000)
+        scale = max(1.0, float(np.abs(ref).max()))
+        assert got.shape == ref.shape and np.abs(got - ref).max() < TOL * scale
+
+
 def test_flac_file_through_process_audio(tmp_path):
     """BASELINE config 1 shape: a single FLAC file at 192 kHz through AudioProcessingPipeline.process_audio on the
     tiny.en engine; the transcript equals the one of the same audio handed over as a decoded 16 kHz array."""

@@ -43,7 +43,7 @@ EXPORTED = (
     "tw_attn_set_lds_pad", "tw_logits_sample", "tw_token_prob", "tw_g711_decode", "tw_ima_adpcm_wav_decode",
     "tw_kv_tab_check", "tw_debug_build", "tw_resid_layernorm_packed_to", "tw_conv2_gemm",
     "tw_logmel_long", "tw_im2col_conv1_long", "tw_attn_decode_self_masked", "tw_attn_decode_self_tab_masked",
-    "tw_gemv_set_wide_slices",
+    "tw_gemv_set_wide_slices", "tw_vorbis_probe", "tw_vorbis_decode", "tw_vorbis_imdct",
 )
 
 
@@ -73,6 +73,13 @@ class TwFlacInfo(ctypes.Structure):
         ("sample_rate", ctypes.c_int32), ("channels", ctypes.c_int32), ("bits_per_sample", ctypes.c_int32),
         ("min_blocksize", ctypes.c_int32), ("max_blocksize", ctypes.c_int32), ("reserved", ctypes.c_int32),
         ("total_samples", ctypes.c_int64), ("audio_offset", ctypes.c_int64), ("md5", ctypes.c_uint8 * 16),
+    ]
+
+
+class TwVorbisInfo(ctypes.Structure):
+    _fields_ = [
+        ("sample_rate", ctypes.c_int32), ("channels", ctypes.c_int32), ("blocksize0", ctypes.c_int32),
+        ("blocksize1", ctypes.c_int32), ("total_samples", ctypes.c_int64),
     ]
 
 
@@ -141,6 +148,9 @@ _SIGS = {
     "tw_flac_probe": ([_P, ctypes.c_int64, ctypes.POINTER(TwFlacInfo)], _I),
     "tw_flac_decode": ([_P, ctypes.c_int64, _P, ctypes.c_int64, _I, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_g711_decode": ([_P, ctypes.c_int64, _I, _P], _I),
+    "tw_vorbis_probe": ([_P, ctypes.c_int64, ctypes.POINTER(TwVorbisInfo)], _I),
+    "tw_vorbis_decode": ([_P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)], _I),
+    "tw_vorbis_imdct": ([_P, _I, _P], _I),
     "tw_ima_adpcm_wav_decode": ([_P, ctypes.c_int64, _I, _I, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_resample_pcm_i32": ([_P, ctypes.c_int64, _I, _F, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),
     "tw_resample_pcm_f32": ([_P, ctypes.c_int64, _I, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),

@@ -7,7 +7,7 @@ which this image does not have), dicts carry {"raw"|"array", "sampling_rate"} an
 differs, multi-channel arrays are averaged to mono.
 
 Containers: FLAC (native multi-threaded decoder in libtwhip.so, include/tw_audio.h; bit-exact, verifiable
-against the stream's STREAMINFO MD5), RIFF/WAVE (PCM 8/16/24/32-bit, IEEE float 32/64, G.711 A-law / mu-law, IMA
+against the stream's STREAMINFO MD5), Ogg Vorbis (native decoder, csrc/vorbis.cpp), RIFF/WAVE (PCM 8/16/24/32-bit, IEEE float 32/64, G.711 A-law / mu-law, IMA
 ADPCM), Sun AU and AIFF / AIFF-C (PCM, float, G.711) — the telephony codecs through native decoders
 (tw_g711_decode, tw_ima_adpcm_wav_decode), pinned to CPython's audioop / aifc / sunau / wave.
 Resampling runs on the GPU (tw_resample_pcm_*) with libswresample's default filter restated in
@@ -133,6 +133,31 @@ def resample_device(x: np.ndarray, sr_in: int, sr_out: int = TARGET_SR, scale: f
             _lib.call("tw_resample_pcm_f32", xd.data_ptr(), n_in, ch, up, down, td.data_ptr(), taps.shape[1],
                       y.data_ptr(), n_out, st)
     return y
+
+
+def vorbis_probe(data: bytes):
+    _lib, lib = _flac_lib()
+    info = _lib.TwVorbisInfo()
+    if lib.tw_vorbis_probe(ctypes.c_char_p(data), len(data), ctypes.byref(info)) != 0:
+        raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    return info
+
+
+def decode_vorbis(data: bytes) -> Tuple[np.ndarray, int]:
+    """Ogg Vorbis bytes -> f32 [frames, channels] through the native decoder (csrc/vorbis.cpp; Ogg page CRCs
+    checked, the end trimmed to the last page's granule position)."""
+    _lib, lib = _flac_lib()
+    info = vorbis_probe(data)
+    total, ch, sr = int(info.total_samples), int(info.channels), int(info.sample_rate)
+    # bound the allocation before trusting the granule: a packet of >= 1 byte codes at most blocksize1 / 2 frames
+    if total < 0 or total > (len(data) + 1) * int(info.blocksize1) // 2 or total > max_audio_seconds() * sr:
+        raise ValueError(f"Ogg Vorbis stream claims {total} frames x {ch} channels at {sr} Hz: larger than the "
+                         f"stream can code or longer than TW_MAX_AUDIO_S={max_audio_seconds():g} s")
+    out = np.zeros((total, ch), np.float32)
+    got = ctypes.c_int64()
+    if lib.tw_vorbis_decode(ctypes.c_char_p(data), len(data), out.ctypes.data, total, ctypes.byref(got)) != 0:
+        raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    return out[: got.value], sr
 
 
 def g711_decode(codes: bytes, alaw: bool) -> np.ndarray:
@@ -314,7 +339,7 @@ def max_audio_seconds() -> float:
     return float(os.environ.get("TW_MAX_AUDIO_S", "14400"))
 
 
-# Containers the engine recognises but does not decode (no MP3 / AAC / Vorbis / Opus decoder is built in): reported
+# Containers the engine recognises but does not decode (no MP3 / AAC / Opus decoder is built in): reported
 # by name, as a ValueError like the reference's own decode failure (ffmpeg_read, which its transcribe() turns into
 # its {"error": ...} result).
 _UNDECODED = ((b"ID3", "MP3"), (b"\xff\xfb", "MP3"), (b"\xff\xf3", "MP3"), (b"\xff\xf2", "MP3"), (b"OggS", "Ogg"),
@@ -336,14 +361,19 @@ def container_name(data: bytes) -> Optional[str]:
         return "AIFF"
     if data[4:8] == b"ftyp":
         return "MP4/M4A"
+    if data[:4] == b"OggS":
+        head = data[28: 28 + 8]  # the first packet of a one-segment first page (every Ogg codec's header packet)
+        if head[:7] == b"\x01vorbis":
+            return "Ogg Vorbis"
+        return "Ogg Opus" if head == b"OpusHead" else "Ogg"
     for magic, name in _UNDECODED:
         if data.startswith(magic):
             return name
     return None
 
 
-_DECODERS = {"WAV": decode_wav, "AU": decode_au, "AIFF": decode_aiff}
-DECODED = "FLAC, WAV (PCM, float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C"
+_DECODERS = {"WAV": decode_wav, "AU": decode_au, "AIFF": decode_aiff, "Ogg Vorbis": decode_vorbis}
+DECODED = "FLAC, Ogg Vorbis, WAV (PCM, float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C"
 
 
 def decode_bytes(data: bytes, sr_out: int = TARGET_SR, device=None) -> np.ndarray:
@@ -397,6 +427,9 @@ def duration_seconds(path: str) -> float:
     with open(path, "rb") as f:
         data = f.read()
     name = container_name(data)
+    if name == "Ogg Vorbis":
+        info = vorbis_probe(data)
+        return int(info.total_samples) / float(info.sample_rate)
     if name in _DECODERS:
         x, sr = _DECODERS[name](data)
         return x.shape[0] / float(sr)
