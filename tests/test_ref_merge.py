@@ -215,5 +215,5 @@ def test_undecodable_upload_reaches_reference_error_convention(layout, tmp_path)
     f.write_bytes(b"ID3\x04\x00\x00" + bytes(256))
     got = p.transcribe(str(f), "transcribe")
     assert got == {"error": "Transcription error: MP3 audio is not decoded by this engine (decoded containers: FLAC, "
-                            "WAV (PCM, float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C); convert the upload to "
+                            "Ogg Vorbis, WAV (PCM, float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C); convert the upload to "
                             "one of them"}

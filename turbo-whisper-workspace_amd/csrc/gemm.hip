@@ -1160,9 +1160,15 @@ extern "C" int tw_conv2_gemm(const bf16_t* h1, int R, int D, const bf16_t* W, co
   ea.group_m = tw_group_for(D);
   int rc = launch_gemm<TW_EPI_GELU_POS_F32>(h1 - D, W, R * 1500, D, 3 * D, 2 * D, 3 * D, ea, s);
   if (rc) return rc;
-  EpiArgs e0{out, 1500 * D, bias, pos, 1, 0, 0, 0, 0};  // row r -> output row 1500 r; positional row 0
-  e0.group_m = 1;
-  return launch_gemm<TW_EPI_GELU_POS_F32>(h1, W + D, R, D, 2 * D, 3000 * D, 3 * D, e0, s);
+  // fixup rows in chunks of <= 32 windows: always the skinny kernel, whose per-row sums do not depend on the row
+  // count, so a window's encoder output is the same in a batch of 8 as in a batch of 64
+  for (int r0 = 0; r0 < R && !rc; r0 += 32) {
+    EpiArgs e0{out + (size_t)r0 * 1500 * D, 1500 * D, bias, pos, 1, 0, 0, 0, 0};  // row r -> output row 1500 r
+    e0.group_m = 1;
+    rc = launch_gemm<TW_EPI_GELU_POS_F32>(h1 + (size_t)r0 * 3000 * D, W + D, std::min(32, R - r0), D, 2 * D,
+                                          3000 * D, 3 * D, e0, s);
+  }
+  return rc;
 }
 
 extern "C" int tw_gemm_bf16_partial(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int ldw,
