@@ -84,8 +84,11 @@ int tw_vorbis_probe(const uint8_t* data, int64_t size, TwVorbisInfo* info);
 
 /* Decode every audio packet into out = f32[out_frames][channels] (interleaved, HOST; the codec's own scale,
  * nominally [-1, 1]). out_frames must be >= info.total_samples. The first packet primes the overlap (no output);
- * the end is trimmed to the last page's granule position. *frames_decoded receives the frames written. */
-int tw_vorbis_decode(const uint8_t* data, int64_t size, float* out, int64_t out_frames, int64_t* frames_decoded);
+ * the end is trimmed to the last page's granule position. Packets decode on n_threads threads (<= 0: hardware
+ * concurrency; the output does not depend on it), the overlap-add runs in order. *frames_decoded receives the
+ * frames written. */
+int tw_vorbis_decode(const uint8_t* data, int64_t size, float* out, int64_t out_frames, int32_t n_threads,
+                     int64_t* frames_decoded);
 
 /* The Vorbis inverse MDCT alone (for tests): y[i] = sum_{k < n/2} X[k] cos(2 pi / n (i + 1/2 + n/4)(k + 1/2)),
  * i < n, n a power of two >= 4. HOST memory. */

@@ -763,8 +763,8 @@ def write_stream(rng, channels: int = 2, bs_exp=(7, 9), n_packets: int = 12, rat
         if f:
             bw.write(flags[k - 1] if k > 0 else 1, 1)
             bw.write(flags[k + 1] if k + 1 < n_packets else 1, 1)
-        for _ in range(int(rng.integers(*packet_bytes)) * 8):
-            bw.write(int(rng.integers(2)), 1)
+        payload = np.frombuffer(rng.bytes(int(rng.integers(*packet_bytes))), np.uint8)
+        bw.bits.extend(np.unpackbits(payload, bitorder="little").tolist())
         audio.append(bw.bytes())
     ns = [bs[f] for f in flags]
     total = sum(a // 4 + b // 4 for a, b in zip(ns, ns[1:]))

@@ -9,5 +9,7 @@ timeout -k 10 600 python -u bench.py --config c3 --c3-share 8 --steps 5 --warmup
 grep '^{' $O/c3_share8.log | tail -1 > $O/c3_share8.json
 timeout -k 10 600 python -u scripts/exp/as_shipped_rtf.py > $O/as_shipped.log 2>&1 || exit $?
 tail -1 $O/as_shipped.log > $O/as_shipped_beam5.json
+timeout -k 10 300 python -u scripts/vorbis_speed.py > $O/vorbis_speed.log 2>&1 || exit $?
+cat $O/vorbis_speed.log
 BENCH_ARGS="--config c5" bash scripts/gpu_round.sh r04o_c5 1 || exit $?
 echo final-c3-c5-done

@@ -106,3 +106,13 @@ def test_native_entry_points_declared():
     info = _lib.TwVorbisInfo()
     assert lib.tw_vorbis_probe(ctypes.c_char_p(b"nope"), 4, ctypes.byref(info)) != 0
     assert b"Ogg" in lib.tw_last_error()
+
+
+def test_threads_do_not_change_the_output():
+    """Packets decode in parallel rounds of 1024 (the overlap-add after each round, in order): a stream longer than
+    one round gives the same samples on 1 and 3 threads, and the oracle's."""
+    data = vo.write_stream(np.random.default_rng(11), channels=2, bs_exp=(6, 8), n_packets=1100, packet_bytes=(4, 40))
+    x1, _ = audio.decode_vorbis(data, threads=1)
+    x3, _ = audio.decode_vorbis(data, threads=3)
+    assert np.array_equal(x1, x3) and len(x1) > 50000
+    _close(x1, vo.decode(data)[0])

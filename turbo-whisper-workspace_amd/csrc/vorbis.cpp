@@ -6,7 +6,7 @@
 // the Ogg framing specification (RFC 3533) and the Vorbis I specification: Ogg pages (CRC-32 checked) and packet
 // lacing; the identification / setup headers (Huffman codebooks with VQ lookup types 1 and 2, floor type 1,
 // residue types 0 / 1 / 2, mappings with channel coupling, modes); audio packets: floor-1 curve synthesis, residue
-// decode, inverse coupling, the floor x residue product, the inverse MDCT (an N-point complex FFT), the power-sine
+// decode, inverse coupling, the floor x residue product, the inverse MDCT (an N/4-point complex FFT), the power-sine
 // windows with short / long transitions, overlap-add, and the end trim to the last page's granule position.
 // Floor type 0 (LSP) is refused: no encoder in use emits it (libvorbis has written floor 1 since 2002).
 //
@@ -16,7 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
-#include <complex>
+#include <thread>
 #include <vector>
 
 #include "../../include/tw_audio.h"
@@ -121,19 +121,35 @@ struct BitReader {
   const uint8_t* d;
   size_t n;
   size_t bit = 0;
-  bool eop = false;  // read past the end of the packet
+  bool eop = false;  // read past the end of the packet (sticky; every later read returns 0)
   BitReader(const uint8_t* d_, size_t n_) : d(d_), n(n_) {}
-  uint32_t get(int k) {  // k <= 32
-    uint32_t v = 0;
-    for (int i = 0; i < k; i++) {
-      const size_t b = bit >> 3;
-      if (b >= n) {
-        eop = true;
-        return 0;
-      }
-      v |= (uint32_t)((d[b] >> (bit & 7)) & 1) << i;
-      bit++;
+  size_t left() const { return eop ? 0 : n * 8 - bit; }
+  uint32_t peek24() const {  // the next 24 bits, zero-padded past the end
+    const size_t b = bit >> 3;
+    uint32_t w = 0;
+    if (b + 4 <= n) {
+      memcpy(&w, d + b, 4);
+    } else {
+      for (size_t i = 0; b + i < n && i < 4; i++) w |= (uint32_t)d[b + i] << (8 * i);
     }
+    return (w >> (bit & 7)) & 0xffffffu;
+  }
+  uint32_t get(int k) {  // k <= 32; a read that runs past the end returns 0
+    if (eop || bit + k > n * 8) {
+      eop = true;
+      bit = n * 8;
+      return 0;
+    }
+    uint32_t v;
+    if (k <= 24) {
+      v = peek24() & ((1u << k) - 1);
+    } else {
+      const uint32_t lo = peek24();
+      bit += 24;
+      v = lo | ((peek24() & ((1u << (k - 24)) - 1)) << 24);
+      bit -= 24;
+    }
+    bit += k;
     return v;
   }
   uint32_t get1() { return get(1); }
@@ -219,8 +235,51 @@ struct Codebook {
     return true;
   }
 
+  // codewords of up to FB bits by one table lookup on the next FB bits (first bit read = lowest index bit):
+  // fast[idx] = entry | length << 24, -1 for no codeword, -2 for the prefix of a longer codeword (tree walk)
+  static constexpr int FB = 10;
+  std::vector<int32_t> fast;
+
+  void build_fast() {
+    fast.assign(1 << FB, -1);
+    std::vector<std::pair<int, int>> stack{{0, 0}};  // (node, depth) ; path bits kept alongside
+    std::vector<uint32_t> path{0};
+    while (!stack.empty()) {
+      const auto [node, depth] = stack.back();
+      const uint32_t bits = path.back();
+      stack.pop_back();
+      path.pop_back();
+      for (int b = 0; b < 2; b++) {
+        const int32_t c = tree[2 * node + b];
+        const uint32_t nb = bits | ((uint32_t)b << depth);
+        if (c < 0) {
+          for (uint32_t f = 0; f < (1u << (FB - depth - 1)); f++)
+            fast[nb | (f << (depth + 1))] = (-c - 1) | ((depth + 1) << 24);
+        } else if (c > 0) {
+          if (depth + 1 < FB) {
+            stack.push_back({c, depth + 1});
+            path.push_back(nb);
+          } else {
+            fast[nb] = -2;
+          }
+        }
+      }
+    }
+  }
+
   int decode(BitReader& br) const {  // entry number, -1 at the end of the packet
     if (used == 0) return -1;
+    const int32_t t = fast[br.peek24() & ((1u << FB) - 1)];
+    if (t >= 0) {
+      const int L = t >> 24;
+      if ((size_t)L > br.left()) {
+        br.get(L);  // (runs past the end: sets eop)
+        return -1;
+      }
+      br.bit += L;
+      return t & 0xffffff;
+    }
+    if (t == -1) return -1;
     int node = 0;
     for (int depth = 0; depth < 33; depth++) {
       const int b = (int)br.get1();
@@ -316,7 +375,9 @@ bool read_codebook(BitReader& br, Codebook& cb, const char** err) {
     *err = "Vorbis: truncated setup header";
     return false;
   }
-  return cb.build(err);
+  if (!cb.build(err)) return false;
+  if (cb.used > 0) cb.build_fast();
+  return true;
 }
 
 // ---- floor 1 ---------------------------------------------------------------------------------------------------------
@@ -384,44 +445,84 @@ struct Mode {
 };
 
 // ---- inverse MDCT ------------------------------------------------------------------------------------------------------
-// y[i] = sum_{k < N/2} X[k] cos(2 pi / N (i + 1/2 + N/4)(k + 1/2)), i < N: with Z[k] = X[k] e^{i 2 pi n0 k / N}
-// (n0 = 1/2 + N/4, zero for k >= N/2), y[i] = Re(e^{i pi (i + n0) / N} sum_k Z[k] e^{i 2 pi i k / N}), an N-point
-// complex FFT.
+// y[i] = sum_{k < M} X[k] cos(pi / M (i + 1/2 + M/2)(k + 1/2)), i < N = 2M. With u = DCT-IV(X),
+// u[j] = sum_k X[k] cos(pi / M (j + 1/2)(k + 1/2)), the output unfolds as y[i] = u[i + M/2] (i < M/2),
+// -u[3M/2 - 1 - i] (i < 3M/2), -u[i - 3M/2] (i < 2M); u comes from one M/2-point complex FFT:
+// v[j] = (X[2j] + i X[M-1-2j]) e^{-i pi (j + 1/4) / M}, V = FFT(v), V[j] *= e^{-i pi j / M}, u[2j] = Re V[j],
+// u[M-1-2j] = -Im V[j].
 struct Imdct {
-  int N = 0;
-  std::vector<std::complex<double>> tw, pre, post;
+  int N = 0, M = 0, H = 0;
+  std::vector<float> twr, twi;                  // per stage len: twiddles e^{-2 pi i j / len}, j < len/2, at [len/2 + j]
+  std::vector<float> prer, prei, postr, posti;  // e^{-i pi (j + 1/4) / M}, e^{-i pi j / M}
   std::vector<int> rev;
   void init(int n) {
     N = n;
+    M = n / 2;
+    H = M / 2;
     int lg = 0;
-    while ((1 << lg) < n) lg++;
-    rev.resize(n);
-    for (int i = 0; i < n; i++) {
+    while ((1 << lg) < H) lg++;
+    rev.resize(H);
+    for (int i = 0; i < H; i++) {
       int r = 0;
       for (int b = 0; b < lg; b++) r |= ((i >> b) & 1) << (lg - 1 - b);
       rev[i] = r;
     }
-    tw.resize(n / 2);
-    for (int i = 0; i < n / 2; i++) tw[i] = std::polar(1.0, 2.0 * M_PI * i / n);
-    const double n0 = 0.5 + n / 4.0;
-    pre.resize(n / 2);
-    for (int k = 0; k < n / 2; k++) pre[k] = std::polar(1.0, 2.0 * M_PI * n0 * k / n);
-    post.resize(n);
-    for (int i = 0; i < n; i++) post[i] = std::polar(1.0, M_PI * (i + n0) / n);
-  }
-  void run(const float* X, float* y, std::vector<std::complex<double>>& a) const {
-    a.assign(N, 0.0);
-    for (int k = 0; k < N / 2; k++) a[rev[k]] = (double)X[k] * pre[k];
-    for (int len = 2; len <= N; len <<= 1) {
-      const int half = len >> 1, step = N / len;
-      for (int s = 0; s < N; s += len)
-        for (int j = 0; j < half; j++) {
-          const std::complex<double> u = a[s + j], v = a[s + j + half] * tw[j * step];
-          a[s + j] = u + v;
-          a[s + j + half] = u - v;
-        }
+    twr.assign(std::max(H, 2), 0.f);
+    twi.assign(std::max(H, 2), 0.f);
+    for (int len = 2; len <= H; len <<= 1)
+      for (int j = 0; j < len / 2; j++) {
+        twr[len / 2 + j] = (float)cos(-2.0 * M_PI * j / len);
+        twi[len / 2 + j] = (float)sin(-2.0 * M_PI * j / len);
+      }
+    prer.resize(H);
+    prei.resize(H);
+    postr.resize(H);
+    posti.resize(H);
+    for (int j = 0; j < H; j++) {
+      prer[j] = (float)cos(-M_PI * (j + 0.25) / M);
+      prei[j] = (float)sin(-M_PI * (j + 0.25) / M);
+      postr[j] = (float)cos(-M_PI * j / M);
+      posti[j] = (float)sin(-M_PI * j / M);
     }
-    for (int i = 0; i < N; i++) y[i] = (float)(post[i] * a[i]).real();
+  }
+  // y[0 .. N) from X[0 .. M) in float (as libvorbis and ffmpeg's decoder compute it); re / im: scratch
+  void run(const float* X, float* y, std::vector<float>& re, std::vector<float>& im) const {
+    re.resize(H);
+    im.resize(H);
+    float* ar = re.data();
+    float* ai = im.data();
+    for (int j = 0; j < H; j++) {
+      const float xr = X[2 * j], xi = X[M - 1 - 2 * j];
+      ar[rev[j]] = xr * prer[j] - xi * prei[j];
+      ai[rev[j]] = xr * prei[j] + xi * prer[j];
+    }
+    for (int len = 2; len <= H; len <<= 1) {
+      const int half = len >> 1;
+      const float* wr = twr.data() + half;
+      const float* wi = twi.data() + half;
+      for (int s0 = 0; s0 < H; s0 += len) {
+        float* pr = ar + s0;
+        float* pi = ai + s0;
+        float* qr = pr + half;
+        float* qi = pi + half;
+        for (int j = 0; j < half; j++) {
+          const float tr = qr[j] * wr[j] - qi[j] * wi[j], ti = qr[j] * wi[j] + qi[j] * wr[j];
+          qr[j] = pr[j] - tr;
+          qi[j] = pi[j] - ti;
+          pr[j] += tr;
+          pi[j] += ti;
+        }
+      }
+    }
+    // u[2j] = Re(V[j] post[j]), u[M-1-2j] = -Im(V[j] post[j]); y unfolds u (see above), written directly
+    const int q = M / 2;
+    auto u = [&](int k) -> float {
+      const int j = (k & 1) ? (M - 1 - k) >> 1 : k >> 1;
+      return (k & 1) ? -(ar[j] * posti[j] + ai[j] * postr[j]) : ar[j] * postr[j] - ai[j] * posti[j];
+    };
+    for (int i = 0; i < q; i++) y[i] = u(i + q);
+    for (int i = q; i < 3 * q; i++) y[i] = -u(3 * q - 1 - i);
+    for (int i = 3 * q; i < N; i++) y[i] = -u(i - 3 * q);
   }
 };
 
@@ -434,6 +535,7 @@ struct Decoder {
   std::vector<Mode> modes;
   Imdct mdct[2];
   std::vector<float> win_slope[2];  // rising half-window of length bs[b] / 2
+  std::vector<float> windows[5];    // [0]: short block; [1 + 2 prev + next]: long block with its neighbours' sizes
 
   bool ident(const std::vector<uint8_t>& p, const char** err) {
     if (p.size() < 30 || p[0] != 1 || memcmp(p.data() + 1, "vorbis", 6) != 0) {
@@ -465,6 +567,9 @@ struct Decoder {
         win_slope[b][i] = (float)sin(M_PI / 2 * s * s);
       }
     }
+    window(0, 0, 0, windows[0]);
+    for (int pf = 0; pf < 2; pf++)
+      for (int nf = 0; nf < 2; nf++) window(1, pf, nf, windows[1 + 2 * pf + nf]);
     return true;
   }
 
@@ -652,7 +757,7 @@ struct Decoder {
   }
 
   // floor 1 of one channel: false = unused; else fl[0 .. n/2) = the curve
-  bool floor1(const Floor1& f, BitReader& br, int n2, std::vector<float>& fl) const {
+  bool floor1(const Floor1& f, BitReader& br, int n2, std::vector<float>& fl, std::vector<int>& v) const {
     if (!br.get1()) return false;
     static const int ranges[4] = {256, 128, 86, 64};
     const int range = ranges[f.mult - 1], rb = ilog((uint32_t)(range - 1));
@@ -704,7 +809,7 @@ struct Decoder {
       }
     }
     // curve synthesis (step 2): lines between the used posts in x order, then the dB table
-    std::vector<int> v(n2, 0);
+    v.assign(n2, 0);
     int lx = 0, ly = fy[f.order[0]] * f.mult, hx = 0, hy = ly;
     for (int k = 1; k < nx; k++) {
       const int i = f.order[k];
@@ -790,6 +895,93 @@ struct Decoder {
     }
   }
 
+  struct Scratch {
+    std::vector<std::vector<float>> resid, flo;
+    std::vector<int> curve;
+    std::vector<float> re, im;
+  };
+
+  // One audio packet -> its windowed block, channel-major [channels][n] in `block`. Returns n, 0 for a packet that
+  // is skipped (not an audio packet, or it ends before its window flags), -1 for a bad mode number.
+  int packet(const std::vector<uint8_t>& pk, Scratch& sc, std::vector<float>& block) const {
+    if (pk.empty()) return 0;
+    BitReader br(pk.data(), pk.size());
+    if (br.get1() != 0) return 0;
+    const int mode = (int)br.get(ilog((uint32_t)(modes.size() - 1)));
+    if (mode >= (int)modes.size()) return -1;
+    const int flag = modes[mode].blockflag, n = bs[flag], n2 = n / 2;
+    int prevflag = 0, nextflag = 0;
+    if (flag) {
+      prevflag = (int)br.get1();
+      nextflag = (int)br.get1();
+    }
+    if (br.eop) return 0;
+    const int C = channels;
+    sc.resid.resize(C);
+    sc.flo.resize(C);
+    const Mapping& m = maps[modes[mode].mapping];
+    bool unused[16], noresid[16];
+    for (int c = 0; c < C; c++) {
+      unused[c] = !floor1(floors[m.floor_of[m.mux[c]]], br, n2, sc.flo[c], sc.curve);
+      noresid[c] = unused[c];
+      sc.resid[c].assign(n2, 0.f);
+    }
+    for (size_t k = 0; k < m.mag.size(); k++)
+      if (!noresid[m.mag[k]] || !noresid[m.ang[k]]) noresid[m.mag[k]] = noresid[m.ang[k]] = false;
+    for (int sm = 0; sm < m.submaps; sm++) {
+      std::vector<std::vector<float>*> vecs;
+      std::vector<bool> skip;
+      for (int c = 0; c < C; c++)
+        if (m.mux[c] == sm) {
+          vecs.push_back(&sc.resid[c]);
+          skip.push_back(noresid[c]);
+        }
+      if (!vecs.empty()) residue(residues[m.residue_of[sm]], br, n2, vecs, skip);
+    }
+    for (int k = (int)m.mag.size() - 1; k >= 0; k--) {  // inverse coupling (§9.3.5)
+      float* M = sc.resid[m.mag[k]].data();
+      float* A = sc.resid[m.ang[k]].data();
+      for (int j = 0; j < n2; j++) {
+        const float mv = M[j], av = A[j];
+        float nm, na;
+        if (mv > 0) {
+          if (av > 0) {
+            nm = mv;
+            na = mv - av;
+          } else {
+            na = mv;
+            nm = mv + av;
+          }
+        } else {
+          if (av > 0) {
+            nm = mv;
+            na = mv + av;
+          } else {
+            na = mv;
+            nm = mv - av;
+          }
+        }
+        M[j] = nm;
+        A[j] = na;
+      }
+    }
+    const float* w = windows[flag ? 1 + 2 * prevflag + nextflag : 0].data();
+    block.resize((size_t)C * n);
+    for (int c = 0; c < C; c++) {
+      float* y = block.data() + (size_t)c * n;
+      if (unused[c]) {
+        std::fill(y, y + n, 0.f);
+        continue;
+      }
+      float* r = sc.resid[c].data();
+      const float* f = sc.flo[c].data();
+      for (int j = 0; j < n2; j++) r[j] *= f[j];
+      mdct[flag].run(r, y, sc.re, sc.im);
+      for (int i = 0; i < n; i++) y[i] *= w[i];
+    }
+    return n;
+  }
+
   // window value i of an n-sample block with left / right halves from the neighbouring block sizes
   void window(int flag, int prevflag, int nextflag, std::vector<float>& w) const {
     const int n = bs[flag];
@@ -844,116 +1036,71 @@ extern "C" int tw_vorbis_probe(const uint8_t* data, int64_t size, TwVorbisInfo* 
   return 0;
 }
 
-extern "C" int tw_vorbis_decode(const uint8_t* data, int64_t size, float* out, int64_t out_frames,
+extern "C" int tw_vorbis_decode(const uint8_t* data, int64_t size, float* out, int64_t out_frames, int32_t n_threads,
                                 int64_t* frames_decoded) {
   TwVorbisStream s;
   if (vorbis_open(data, size, s)) return 1;
-  if (!out || !frames_decoded) {
+  if (!out || !frames_decoded || out_frames < 0) {
     tw_set_error("tw_vorbis_decode: null output");
     return 1;
   }
-  Decoder& d = s.dec;
+  const Decoder& d = s.dec;
   const int C = d.channels;
-  int64_t total = 0;   // frames written
   int64_t end_granule = -1;
   for (size_t i = 3; i < s.packets.size(); i++)
     if (s.packets[i].granule >= 0) end_granule = s.packets[i].granule;
-  std::vector<std::vector<float>> prev(C), cur(C), resid(C), flo(C);
-  std::vector<float> w, tmp;
-  std::vector<std::complex<double>> scratch;
+  // Packets decode independently (floor, residue, IMDCT, window); only the overlap-add chains them. Rounds of RP
+  // packets: the round's blocks in parallel (packet p on thread p mod T), then the overlap-add in order.
+  int T = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+  T = std::max(1, std::min(T, 64));
+  constexpr size_t RP = 1024;
+  std::vector<std::vector<float>> blocks(RP);
+  std::vector<int> bn(RP);
+  std::vector<Decoder::Scratch> scr(T);
+  std::vector<float> prev;
   int prev_n = 0;
-  const int mode_bits = ilog((uint32_t)(d.modes.size() - 1));
-  for (size_t pi = 3; pi < s.packets.size(); pi++) {
-    const std::vector<uint8_t>& pk = s.packets[pi].data;
-    if (pk.empty()) continue;
-    BitReader br(pk.data(), pk.size());
-    if (br.get1() != 0) continue;  // (not an audio packet: skipped, as decoders do)
-    const int mode = (int)br.get(mode_bits);
-    if (mode >= (int)d.modes.size()) {
-      tw_set_error("tw_vorbis_decode: bad mode number in packet %zu", pi);
-      return 1;
+  int64_t total = 0;
+  for (size_t r0 = 3; r0 < s.packets.size(); r0 += RP) {
+    const size_t r1 = std::min(s.packets.size(), r0 + RP), cnt = r1 - r0;
+    auto work = [&](int t, int nt) {
+      for (size_t p = r0 + t; p < r1; p += nt) bn[p - r0] = d.packet(s.packets[p].data, scr[t], blocks[p - r0]);
+    };
+    const int nt = (int)std::min<size_t>(T, (cnt + 7) / 8);
+    if (nt <= 1) {
+      work(0, 1);
+    } else {
+      std::vector<std::thread> th;
+      for (int t = 1; t < nt; t++) th.emplace_back(work, t, nt);
+      work(0, nt);
+      for (auto& x : th) x.join();
     }
-    const int flag = d.modes[mode].blockflag, n = d.bs[flag], n2 = n / 2;
-    int prevflag = 0, nextflag = 0;
-    if (flag) {
-      prevflag = (int)br.get1();
-      nextflag = (int)br.get1();
-    }
-    if (br.eop) continue;
-    const Mapping& m = d.maps[d.modes[mode].mapping];
-    std::vector<bool> unused(C);
-    for (int c = 0; c < C; c++) {
-      const int sm = m.mux[c];
-      unused[c] = !d.floor1(d.floors[m.floor_of[sm]], br, n2, flo[c]);
-      resid[c].assign(n2, 0.f);
-    }
-    std::vector<bool> noresid = unused;
-    for (size_t k = 0; k < m.mag.size(); k++)
-      if (!noresid[m.mag[k]] || !noresid[m.ang[k]]) noresid[m.mag[k]] = noresid[m.ang[k]] = false;
-    for (int sm = 0; sm < m.submaps; sm++) {
-      std::vector<std::vector<float>*> vecs;
-      std::vector<bool> skip;
-      for (int c = 0; c < C; c++)
-        if (m.mux[c] == sm) {
-          vecs.push_back(&resid[c]);
-          skip.push_back(noresid[c]);
-        }
-      if (!vecs.empty()) d.residue(d.residues[m.residue_of[sm]], br, n2, vecs, skip);
-    }
-    for (int k = (int)m.mag.size() - 1; k >= 0; k--) {  // inverse coupling (§9.3.5)
-      float* M = resid[m.mag[k]].data();
-      float* A = resid[m.ang[k]].data();
-      for (int j = 0; j < n2; j++) {
-        const float mv = M[j], av = A[j];
-        float nm, na;
-        if (mv > 0) {
-          if (av > 0) {
-            nm = mv;
-            na = mv - av;
-          } else {
-            na = mv;
-            nm = mv + av;
-          }
-        } else {
-          if (av > 0) {
-            nm = mv;
-            na = mv + av;
-          } else {
-            na = mv;
-            nm = mv - av;
-          }
-        }
-        M[j] = nm;
-        A[j] = na;
+    for (size_t k = 0; k < cnt; k++) {
+      const int n = bn[k];
+      if (n < 0) {
+        tw_set_error("tw_vorbis_decode: bad mode number in packet %zu", r0 + k);
+        return 1;
       }
-    }
-    d.window(flag, prevflag, nextflag, w);
-    for (int c = 0; c < C; c++) {
-      cur[c].assign(n, 0.f);
-      if (!unused[c]) {
-        for (int j = 0; j < n2; j++) resid[c][j] *= flo[c][j];
-        d.mdct[flag].run(resid[c].data(), cur[c].data(), scratch);
-        for (int i = 0; i < n; i++) cur[c][i] *= w[i];
-      }
-    }
-    if (prev_n) {  // overlap-add: from the previous block's centre to this block's centre
-      const int cnt = prev_n / 4 + n / 4;
-      const int shift = n / 4 - prev_n / 4;  // this block's index of output sample i is i + shift
-      for (int i = 0; i < cnt; i++) {
-        if (total >= out_frames) break;
+      if (n == 0) continue;
+      const std::vector<float>& cur = blocks[k];
+      if (prev_n) {  // overlap-add: from the previous block's centre to this block's centre
+        // output i = prev[prev_n / 2 + i] (i < prev_n / 2) + cur[i + shift] (i + shift >= 0): prev alone on [0, a),
+        // both on [a, b), cur alone on [b, cnt)
+        const int shift = n / 4 - prev_n / 4;
+        const int cnt = (int)std::min<int64_t>(prev_n / 4 + n / 4, out_frames - total);
+        const int a = std::min(cnt, std::max(0, -shift)), b = std::max(a, std::min(cnt, prev_n / 2));
         for (int c = 0; c < C; c++) {
-          float v = 0.f;
-          const int pi2 = prev_n / 2 + i;
-          if (pi2 < prev_n) v += prev[c][pi2];
-          const int ci = i + shift;
-          if (ci >= 0 && ci < n) v += cur[c][ci];
-          out[total * C + c] = v;
+          const float* P = prev.data() + (size_t)c * prev_n + prev_n / 2;
+          const float* Q = cur.data() + (size_t)c * n + shift;
+          float* o = out + total * C + c;
+          for (int i = 0; i < a; i++) o[(size_t)i * C] = P[i];
+          for (int i = a; i < b; i++) o[(size_t)i * C] = P[i] + Q[i];
+          for (int i = b; i < cnt; i++) o[(size_t)i * C] = Q[i];
         }
-        total++;
+        total += std::max(cnt, 0);
       }
+      prev.swap(blocks[k]);
+      prev_n = n;
     }
-    std::swap(prev, cur);
-    prev_n = n;
   }
   if (end_granule >= 0 && total > end_granule) total = end_granule;  // the last page's granule ends the stream
   *frames_decoded = total;
@@ -967,7 +1114,7 @@ extern "C" int tw_vorbis_imdct(const float* X, int32_t n, float* y) {
   }
   Imdct t;
   t.init(n);
-  std::vector<std::complex<double>> a;
-  t.run(X, y, a);
+  std::vector<float> re, im;
+  t.run(X, y, re, im);
   return 0;
 }

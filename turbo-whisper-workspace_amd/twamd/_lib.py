@@ -149,7 +149,7 @@ _SIGS = {
     "tw_flac_decode": ([_P, ctypes.c_int64, _P, ctypes.c_int64, _I, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_g711_decode": ([_P, ctypes.c_int64, _I, _P], _I),
     "tw_vorbis_probe": ([_P, ctypes.c_int64, ctypes.POINTER(TwVorbisInfo)], _I),
-    "tw_vorbis_decode": ([_P, ctypes.c_int64, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)], _I),
+    "tw_vorbis_decode": ([_P, ctypes.c_int64, _P, ctypes.c_int64, _I, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_vorbis_imdct": ([_P, _I, _P], _I),
     "tw_ima_adpcm_wav_decode": ([_P, ctypes.c_int64, _I, _I, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_resample_pcm_i32": ([_P, ctypes.c_int64, _I, _F, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),

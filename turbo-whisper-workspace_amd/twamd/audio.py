@@ -143,7 +143,7 @@ def vorbis_probe(data: bytes):
     return info
 
 
-def decode_vorbis(data: bytes) -> Tuple[np.ndarray, int]:
+def decode_vorbis(data: bytes, threads: int = 0) -> Tuple[np.ndarray, int]:
     """Ogg Vorbis bytes -> f32 [frames, channels] through the native decoder (csrc/vorbis.cpp; Ogg page CRCs
     checked, the end trimmed to the last page's granule position)."""
     _lib, lib = _flac_lib()
@@ -155,7 +155,8 @@ def decode_vorbis(data: bytes) -> Tuple[np.ndarray, int]:
                          f"stream can code or longer than TW_MAX_AUDIO_S={max_audio_seconds():g} s")
     out = np.zeros((total, ch), np.float32)
     got = ctypes.c_int64()
-    if lib.tw_vorbis_decode(ctypes.c_char_p(data), len(data), out.ctypes.data, total, ctypes.byref(got)) != 0:
+    if lib.tw_vorbis_decode(ctypes.c_char_p(data), len(data), out.ctypes.data, total, int(threads),
+                            ctypes.byref(got)) != 0:
         raise ValueError(lib.tw_last_error().decode(errors="replace"))
     return out[: got.value], sr
 
