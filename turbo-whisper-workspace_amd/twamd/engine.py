@@ -770,9 +770,10 @@ class WhisperEngine:
         self._select(R, params, v=v, embed_next=fused)
 
     # K-slices of the vocabulary-wide proj_out for a decode pass with no encoder beside it (the pipeline's last batch, a
-    # single-batch call, beam passes of the as-shipped call, long-form): 4 (22.7 vs 33 us per launch alone); beside an
-    # encoder chunk 1. TW_DEC_ALONE_WIDE_KW overrides (1 / 2 / 4).
-    dec_alone_wide_kw = int(os.environ.get("TW_DEC_ALONE_WIDE_KW", "4"))
+    # single-batch call, beam passes of the as-shipped call, long-form). 1 by default: 4 slices make the launch itself
+    # faster alone (22.7 vs 33 us) but the captured step slower (444.4 vs 439.6 us at 24 rows, bench 99.6 vs 98.9 ms,
+    # profiles/r04n_ab.txt). TW_DEC_ALONE_WIDE_KW overrides (1 / 2 / 4).
+    dec_alone_wide_kw = int(os.environ.get("TW_DEC_ALONE_WIDE_KW", "1"))
 
     def _dec_context(self) -> int:
         """Set the proj_out K-slice count for a pass starting now: alone unless run_batches' encoder pump is queued
