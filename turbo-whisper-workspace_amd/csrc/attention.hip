@@ -854,7 +854,7 @@ struct TabRows {
 // kv_start (NULL: none): per row the first position its queries attend once they are past it — the left padding of a
 // prompt conditioned on previous segments (generate()'s decoder_attention_mask, generation_whisper.py:1893-1908): pad
 // positions are fed (they take positions, as transformers' cache positions do) but masked out of every later query.
-template <bool TAB>
+template <bool TAB, bool MASK>
 __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__ qkv, int D, int max_pos,
                                                            const int* __restrict__ pos, bf16_t* __restrict__ kc,
                                                            bf16_t* __restrict__ vc, const int* __restrict__ kv_tab,
@@ -869,8 +869,13 @@ __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__
   const int h = blockIdx.x, b = blockIdx.y, H = gridDim.x;
   const int tid = threadIdx.x, g = tid >> 3, gl = tid & 7, lane = tid & 63, wid = tid >> 6;
   const int t = pos[b];
-  int ks = kv_start ? kv_start[b] : 0;  // first attended key (0 while the query itself is a pad position)
-  ks = t >= ks ? ks : 0;
+  // first attended key (0 while the query itself is a pad position); MASK = false: the unmasked code, ks = 0 folded
+  // away (a live ks costs the fast path registers it has none to spare for: 32 B of scratch instead of 16)
+  int ks = 0;
+  if constexpr (MASK) {
+    ks = kv_start[b];
+    ks = t >= ks ? ks : 0;
+  }
   const bf16_t* row = qkv + (size_t)b * 3 * D + h * 64;
   bf16_t* K = kc + ((size_t)b * H + h) * max_pos * 64;
   bf16_t* V = vc + ((size_t)b * H + h) * max_pos * 64;
@@ -973,8 +978,8 @@ extern "C" int tw_attn_decode_self(const bf16_t* qkv, int B, int H, int max_pos,
                                    bf16_t* v_cache, bf16_t* out, void* stream) {
   TW_REQUIRE(qkv && pos && k_cache && v_cache && out && B > 0 && H > 0, "tw_attn_decode_self: bad args");
   TW_REQUIRE(max_pos <= DA_SELF_MAXK, "tw_attn_decode_self: max_pos %d > %d", max_pos, DA_SELF_MAXK);
-  hipLaunchKernelGGL(k_attn_decode_self2<false>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos,
-                     pos, k_cache, v_cache, nullptr, 0, out, (const int*)nullptr);
+  hipLaunchKernelGGL((k_attn_decode_self2<false, false>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64,
+                     max_pos, pos, k_cache, v_cache, nullptr, 0, out, (const int*)nullptr);
   return tw_check_launch("tw_attn_decode_self");
 }
 
@@ -984,8 +989,8 @@ extern "C" int tw_attn_decode_self_masked(const bf16_t* qkv, int B, int H, int m
   TW_REQUIRE(qkv && pos && k_cache && v_cache && kv_start && out && B > 0 && H > 0,
              "tw_attn_decode_self_masked: bad args");
   TW_REQUIRE(max_pos <= DA_SELF_MAXK, "tw_attn_decode_self_masked: max_pos %d > %d", max_pos, DA_SELF_MAXK);
-  hipLaunchKernelGGL(k_attn_decode_self2<false>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos,
-                     pos, k_cache, v_cache, nullptr, 0, out, kv_start);
+  hipLaunchKernelGGL((k_attn_decode_self2<false, true>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64,
+                     max_pos, pos, k_cache, v_cache, nullptr, 0, out, kv_start);
   return tw_check_launch("tw_attn_decode_self_masked");
 }
 
@@ -1061,8 +1066,12 @@ static int attn_self_tab(const bf16_t* qkv, int B, int H, int max_pos, const int
 #if TW_DEBUG
   if (int rc = tw_debug_tab_guard(kv_tab, pos, row0, B, max_pos, (hipStream_t)stream)) return rc;
 #endif
-  hipLaunchKernelGGL(k_attn_decode_self2<true>, dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64, max_pos,
-                     pos, k_cache, v_cache, kv_tab, row0, out, kv_start);
+  if (kv_start)
+    hipLaunchKernelGGL((k_attn_decode_self2<true, true>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64,
+                       max_pos, pos, k_cache, v_cache, kv_tab, row0, out, kv_start);
+  else
+    hipLaunchKernelGGL((k_attn_decode_self2<true, false>), dim3(H, B), dim3(256), 0, (hipStream_t)stream, qkv, H * 64,
+                       max_pos, pos, k_cache, v_cache, kv_tab, row0, out, kv_start);
   return tw_check_launch("tw_attn_decode_self_tab");
 }
 

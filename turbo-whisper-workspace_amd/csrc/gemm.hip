@@ -980,7 +980,9 @@ __global__ TW_DEC_LB(256, 1) void k_gemv_pc(const bf16_t* __restrict__ A, int ld
             }
           }
         }
-        __builtin_amdgcn_sched_barrier(0);
+        // (between the halves only: at MT <= 2 a barrier here makes hipcc keep 8 more registers live into the next
+        // batch, 134 instead of 128, and the step beside an encoder GEMM slower, profiles/r04q_*)
+        if constexpr (MT > TH) __builtin_amdgcn_sched_barrier(0);
       }
     };
     using IU = std::integral_constant<int, U>;
