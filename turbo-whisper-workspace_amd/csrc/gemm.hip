@@ -796,8 +796,10 @@ __device__ inline bf16x8 gemv_a_load(const bf16_t* ap, int st) {
   return APACK ? *(const bf16x8*)(ap + (size_t)st * 1024) : *(const bf16x8*)(ap + 32 * st);
 }
 
+// (NTW, the vocabulary-wide proj_out: at most 128 registers, like every other kernel of the decoder step, so that
+// its waves fit beside an encoder GEMM workgroup's two waves on a SIMD; uncapped it took 134 at MT = 2)
 template <int EPI, int KW, int U, bool APACK, int MT, bool NTW = false>
-__global__ TW_DEC_LB(KW > 4 ? 512 : 256, 1) void k_gemv_p(const bf16_t* __restrict__ A, int lda,
+__global__ TW_DEC_LB(KW > 4 ? 512 : 256, NTW ? 4 : 1) void k_gemv_p(const bf16_t* __restrict__ A, int lda,
                                                                const bf16_t* __restrict__ Wp, int M, int N, int K,
                                                                EpiArgs ea) {
   TW_DEC_PRIO();
