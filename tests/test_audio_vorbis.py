@@ -116,3 +116,19 @@ def test_threads_do_not_change_the_output():
     x3, _ = audio.decode_vorbis(data, threads=3)
     assert np.array_equal(x1, x3) and len(x1) > 50000
     _close(x1, vo.decode(data)[0])
+
+
+def test_hostile_codebook_sizes_are_refused():
+    """A setup header claiming a 2^24 - 1-entry, 1000-dimension codebook is an error, not a multi-gigabyte
+    allocation."""
+    packets, gran = vo.ogg_packets(vo.write_stream(np.random.default_rng(2), channels=1, n_packets=3))
+    bw = vo.BitWriter()
+    bw.write(0, 8)  # one codebook
+    bw.write(0x564342, 24)
+    bw.write(1000, 16)
+    bw.write((1 << 24) - 1, 24)
+    bw.write(0, 1)  # unordered
+    bw.write(0, 1)  # dense
+    packets[2] = b"\x05vorbis" + bw.bytes() + bytes(64)
+    with pytest.raises(ValueError, match="too large"):
+        audio.decode_vorbis(vo.ogg_write(packets, gran))

@@ -322,6 +322,12 @@ bool read_codebook(BitReader& br, Codebook& cb, const char** err) {
     *err = "Vorbis: empty codebook";
     return false;
   }
+  // (bounds no encoder comes near — libvorbis's largest books hold a few thousand entries of <= 8 dimensions — that
+  // keep a damaged or hostile header from allocating gigabytes for its tree or VQ table)
+  if (cb.entries > (1 << 20) || (long)cb.entries * cb.dims > (1L << 24)) {
+    *err = "Vorbis: codebook too large";
+    return false;
+  }
   cb.len.assign(cb.entries, 0);
   const bool ordered = br.get1();
   if (!ordered) {
