@@ -67,9 +67,9 @@ def mfma_util(root: str):
         busy, gui, mops = (sum(c.get(n, [])) for n in ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE",
                                                         "SQ_INSTS_VALU_MFMA_MOPS_BF16"))
         ns = sum(dur[k].values())
-        if gui > 0 and mops > 0:
+        if gui > 0 and busy > 0:  # (MX-fp8 kernels count no bf16 MOPS: their busy % is kept, bf16_tflops None)
             out[k] = {"launches": len(dur[k]), "mfma_util_pct": 100.0 * busy / (gui / N_XCD * SIMD_NUM),
-                      "bf16_tflops": mops * 512 / ns / 1e3 if ns > 0 else None}
+                      "bf16_tflops": mops * 512 / ns / 1e3 if ns > 0 and mops > 0 else None}
     return out
 
 
