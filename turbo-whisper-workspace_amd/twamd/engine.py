@@ -263,8 +263,8 @@ class WhisperEngine:
         self._pump: Optional[_EncoderPump] = None  # paced next-batch encoder (run_batches)
         # decode steps queued ahead of the host before it pumps encoder chunks or waits, and encoder chunks pending
         # beside a decode: 1 and 2 (queue depths 1-3 re-measured within +-0.5 %)
-        self.dec_ahead = 1
-        self.pump_ahead = 2
+        self.dec_ahead = int(os.environ.get("TW_DEC_AHEAD", "1"))
+        self.pump_ahead = int(os.environ.get("TW_PUMP_AHEAD", "2"))
         # greedy steps end with the fused select + next-step embedding + first LayerNorm (tw_logits_select_embed):
         # 47 launches per token instead of 49 (False: the separate launches; the tests check both decode alike)
         self.fused_select = True
@@ -275,7 +275,7 @@ class WhisperEngine:
         self.attn_kernel = (32, 32)  # k_attn_enc5 (round 4; 16 = k_attn_enc4, bit-identical to the enc2 form)
         if os.environ.get("TW_ENC_ATTN"):
             self.attn_kernel = (int(os.environ["TW_ENC_ATTN"]),) * 2
-        self.attn_pad = (0, 4)
+        self.attn_pad = (0, int(os.environ.get("TW_ATTN_PAD_BESIDE", "4")))  # (A/B: TW_ATTN_PAD_BESIDE)
         # run_batches encodes batch k+1 beside the decode of batch k (sequential 138.6 vs overlapped 114.5 ms per
         # bench step, round 1); False: strictly in turn
         self.overlap = True
