@@ -144,6 +144,9 @@ int tw_resid_layernorm(float* x, const float* parts, int nparts, const float* bi
  * :371,377,434,443,446,573,682). */
 int tw_layernorm(const float* x, const float* gamma, const float* beta, int M, int D, float eps, uint16_t* out,
                  void* stream);
+/* Dynamic LDS (KiB, 0..64) requested by every later tw_layernorm workgroup: a cap on its workgroups per CU, set by the
+ * caller beside a decode so that each SIMD keeps room for a decoder wave (as tw_attn_set_lds_pad); 0 (default) alone. */
+int tw_layernorm_set_lds_pad(int kib);
 
 /* ---- MX fp8 encoder (BASELINE config 5: fp8 MFMA encoder + bf16 decoder) --------------------- */
 /* MX block format: e4m3fn elements [rows][K] (row-major bytes), e8m0 scales [K/128][rows_pad][4] bytes (byte

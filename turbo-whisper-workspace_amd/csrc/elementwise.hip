@@ -57,21 +57,32 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, 
   }
 }
 
+// Dynamic LDS requested per LayerNorm workgroup (KiB; tw_layernorm_set_lds_pad): none alone; beside a decode it caps
+// the LayerNorm's workgroups per CU so that their waves leave registers and LDS for a decoder wave on every SIMD
+// (uncapped, ~6 LayerNorm waves of 78 registers fill a SIMD) — the encoder attention's cap (tw_attn_set_lds_pad), here.
+static int tw_ln_lds_pad_kib = 0;
+extern "C" int tw_layernorm_set_lds_pad(int kib) {
+  TW_REQUIRE(kib >= 0 && kib <= 64, "tw_layernorm_set_lds_pad: %d KiB (0..64)", kib);
+  tw_ln_lds_pad_kib = kib;
+  return 0;
+}
+
 extern "C" int tw_layernorm(const float* x, const float* gamma, const float* beta, int M, int D, float eps, bf16_t* out,
                             void* stream) {
   TW_REQUIRE(x && gamma && beta && out && M > 0, "tw_layernorm: bad args");
   TW_REQUIRE(D % 4 == 0 && D <= 256 * LN_MAXC, "tw_layernorm: D=%d must be a multiple of 4 and <= %d", D, 256 * LN_MAXC);
   const dim3 grid(tw_cdiv(M, 4)), blk(256);
   hipStream_t st = (hipStream_t)stream;
+  const size_t lds = (size_t)tw_ln_lds_pad_kib * 1024;
   switch (tw_cdiv(D, 256)) {
-    case 1: hipLaunchKernelGGL(k_layernorm<1>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
-    case 2: hipLaunchKernelGGL(k_layernorm<2>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
-    case 3: hipLaunchKernelGGL(k_layernorm<3>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
-    case 4: hipLaunchKernelGGL(k_layernorm<4>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
-    case 5: hipLaunchKernelGGL(k_layernorm<5>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
-    case 6: hipLaunchKernelGGL(k_layernorm<6>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
-    case 7: case 8: hipLaunchKernelGGL(k_layernorm<8>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
-    default: hipLaunchKernelGGL(k_layernorm<LN_MAXC>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out); break;
+    case 1: hipLaunchKernelGGL(k_layernorm<1>, grid, blk, lds, st, x, gamma, beta, M, D, eps, out); break;
+    case 2: hipLaunchKernelGGL(k_layernorm<2>, grid, blk, lds, st, x, gamma, beta, M, D, eps, out); break;
+    case 3: hipLaunchKernelGGL(k_layernorm<3>, grid, blk, lds, st, x, gamma, beta, M, D, eps, out); break;
+    case 4: hipLaunchKernelGGL(k_layernorm<4>, grid, blk, lds, st, x, gamma, beta, M, D, eps, out); break;
+    case 5: hipLaunchKernelGGL(k_layernorm<5>, grid, blk, lds, st, x, gamma, beta, M, D, eps, out); break;
+    case 6: hipLaunchKernelGGL(k_layernorm<6>, grid, blk, lds, st, x, gamma, beta, M, D, eps, out); break;
+    case 7: case 8: hipLaunchKernelGGL(k_layernorm<8>, grid, blk, lds, st, x, gamma, beta, M, D, eps, out); break;
+    default: hipLaunchKernelGGL(k_layernorm<LN_MAXC>, grid, blk, lds, st, x, gamma, beta, M, D, eps, out); break;
   }
   return tw_check_launch("tw_layernorm");
 }

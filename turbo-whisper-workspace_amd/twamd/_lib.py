@@ -44,6 +44,7 @@ EXPORTED = (
     "tw_kv_tab_check", "tw_debug_build", "tw_resid_layernorm_packed_to", "tw_conv2_gemm",
     "tw_logmel_long", "tw_im2col_conv1_long", "tw_attn_decode_self_masked", "tw_attn_decode_self_tab_masked",
     "tw_gemv_set_wide_slices", "tw_vorbis_probe", "tw_vorbis_decode", "tw_vorbis_imdct",
+    "tw_layernorm_set_lds_pad",
 )
 
 
@@ -151,6 +152,7 @@ _SIGS = {
     "tw_vorbis_probe": ([_P, ctypes.c_int64, ctypes.POINTER(TwVorbisInfo)], _I),
     "tw_vorbis_decode": ([_P, ctypes.c_int64, _P, ctypes.c_int64, _I, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_vorbis_imdct": ([_P, _I, _P], _I),
+    "tw_layernorm_set_lds_pad": ([_I], _I),
     "tw_ima_adpcm_wav_decode": ([_P, ctypes.c_int64, _I, _I, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_resample_pcm_i32": ([_P, ctypes.c_int64, _I, _F, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),
     "tw_resample_pcm_f32": ([_P, ctypes.c_int64, _I, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),

@@ -276,6 +276,8 @@ class WhisperEngine:
         if os.environ.get("TW_ENC_ATTN"):
             self.attn_kernel = (int(os.environ["TW_ENC_ATTN"]),) * 2
         self.attn_pad = (0, int(os.environ.get("TW_ATTN_PAD_BESIDE", "4")))  # (A/B: TW_ATTN_PAD_BESIDE)
+        # the encoder LayerNorm's LDS request in KiB (tw_layernorm_set_lds_pad), alone / beside a decode
+        self.ln_pad = (0, int(os.environ.get("TW_LN_PAD_BESIDE", "0")))
         # run_batches encodes batch k+1 beside the decode of batch k (sequential 138.6 vs overlapped 114.5 ms per
         # bench step, round 1); False: strictly in turn
         self.overlap = True
@@ -481,6 +483,7 @@ class WhisperEngine:
         _lib.call("tw_gemm_set_variant", 5 if alone else 1)
         _lib.call("tw_attn_set_variant", self.attn_kernel[0 if alone else 1])
         _lib.call("tw_attn_set_lds_pad", self.attn_pad[0 if alone else 1])
+        _lib.call("tw_layernorm_set_lds_pad", self.ln_pad[0 if alone else 1])
 
     def _encode_steps(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True,
                       alone: bool = True):
