@@ -777,11 +777,13 @@ class WhisperEngine:
     # faster alone (22.7 vs 33 us) but the captured step slower (444.4 vs 439.6 us at 24 rows, bench 99.6 vs 98.9 ms,
     # profiles/r04n_ab.txt). TW_DEC_ALONE_WIDE_KW overrides (1 / 2 / 4).
     dec_alone_wide_kw = int(os.environ.get("TW_DEC_ALONE_WIDE_KW", "1"))
+    # (the same beside an encoder chunk: 1; TW_DEC_BESIDE_WIDE_KW for A/B)
+    dec_beside_wide_kw = int(os.environ.get("TW_DEC_BESIDE_WIDE_KW", "1"))
 
     def _dec_context(self) -> int:
         """Set the proj_out K-slice count for a pass starting now: alone unless run_batches' encoder pump is queued
         beside it. Graph keys carry the returned value (a captured step bakes the launch it recorded)."""
-        kw = 1 if self._pump is not None else self.dec_alone_wide_kw
+        kw = self.dec_beside_wide_kw if self._pump is not None else self.dec_alone_wide_kw
         if kw != self._wide_kw:
             _lib.call("tw_gemv_set_wide_slices", kw)
             self._wide_kw = kw
