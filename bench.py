@@ -29,6 +29,7 @@ import torch.distributed as dist  # noqa: E402
 BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense bf16
 FP8_DENSE_PEAK_TFLOPS = 5000.0    # MI355X_MICROARCH.md: ~5 PF dense fp8 (MX-scaled e4m3)
 HBM_PEAK_GBS = 8000.0
+HBM_COPY_GBS = 6290.0  # measured float4-copy rate on MI355X (MI355X_MICROARCH.md), for context beside the spec peak
 
 
 def parse():
@@ -357,7 +358,9 @@ def decode_cross_roofline(eng, B, traffic_lookup):
     gbs = (work / n_l) / (tot_ms / n_l * 1e-3) / 1e9
     return {"bound": "hbm", "kernel": "k_attn_decode_cross", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic_lookup[0],
-            "bytes_per_launch": work / n_l, "avg_launch_ms": round(tot_ms / n_l, 4)}
+            "bytes_per_launch": work / n_l, "avg_launch_ms": round(tot_ms / n_l, 4),
+            # the chip's measured streaming ceiling (MI355X_MICROARCH.md: a float4 copy reaches 6.29 TB/s)
+            "copy_peak": HBM_COPY_GBS, "frac_of_copy": round(gbs / HBM_COPY_GBS, 4)}
 
 
 def cpu_baseline(dims, gen, T, threads):
