@@ -109,6 +109,40 @@ def test_flac_file_through_process_audio(tmp_path):
     assert res["text"] == ref["text"]
 
 
+def test_ogg_file_through_process_audio(tmp_path):
+    """An Ogg Vorbis upload (the image's real libVorbis file when present, else a random-syntax stream) through
+    AudioProcessingPipeline.process_audio on the tiny.en engine: the duration is the stream's granule length and the
+    transcript equals the one of the oracle-decoded, oracle-resampled array."""
+    import os
+
+    from oracle import vorbis_oracle as vo
+    from twamd.audio_pipeline import AudioProcessingPipeline
+    from twamd.pipeline import TurboTranscriber
+
+    real = "/usr/local/lib/python3.10/dist-packages/kaleido/executable/etc/mathjax/extensions/a11y/invalid_keypress.ogg"
+    data = open(real, "rb").read() if os.path.exists(real) else vo.write_stream(np.random.default_rng(9), channels=2)
+    path = str(tmp_path / "upload.ogg")
+    with open(path, "wb") as f:
+        f.write(data)
+    tr = TurboTranscriber.from_pretrained("tiny.en", seed=1234, max_batch=4)
+    pipe = AudioProcessingPipeline(transcriber=tr)
+    orig = pipe.transcribe
+
+    def _tr(audio_path, task="transcribe", **kw):  # tiny.en is English-only: the reference's task kwarg raises
+        return tr(audio_path, chunk_length_s=60, stride_length_s=5, generate_kwargs={"max_new_tokens": 32},
+                  return_timestamps=True)
+
+    pipe.transcribe = _tr
+    res = pipe.process_audio(path)
+    pipe.transcribe = orig
+    assert "error" not in res, res
+    x, sr = vo.decode(data)
+    assert abs(res["duration"] - len(x) / sr) < 1e-6
+    wav = ao.swr_resample(x.astype(np.float64).mean(axis=1), sr, 16000).astype(np.float32)
+    ref = tr(wav, chunk_length_s=60, stride_length_s=5, generate_kwargs={"max_new_tokens": 32}, return_timestamps=True)
+    assert res["text"] == ref["text"]
+
+
 @pytest.mark.parametrize("kind", ["wav_ulaw", "wav_ima", "au_alaw", "aifc_ulaw"])
 def test_telephony_files_through_load_input(kind):
     """8 kHz call recordings (G.711 / IMA ADPCM) through the product path: native host decode, then the GPU resampler
