@@ -111,8 +111,9 @@ def test_flac_file_through_process_audio(tmp_path):
 
 def test_ogg_file_through_process_audio(tmp_path):
     """An Ogg Vorbis upload (the image's real libVorbis file when present, else a random-syntax stream) through
-    AudioProcessingPipeline.process_audio on the tiny.en engine: the duration is the stream's granule length and the
-    transcript equals the one of the oracle-decoded, oracle-resampled array."""
+    AudioProcessingPipeline.process_audio on the tiny.en engine: the duration is the stream's granule length (the
+    oracle's decode), and the transcript equals the one of the same upload handed over as the ingest's 16 kHz array
+    (native decode + GPU resampler, held to the oracle by test_ogg_vorbis_bytes_through_load_input)."""
     import os
 
     from oracle import vorbis_oracle as vo
@@ -138,7 +139,7 @@ def test_ogg_file_through_process_audio(tmp_path):
     assert "error" not in res, res
     x, sr = vo.decode(data)
     assert abs(res["duration"] - len(x) / sr) < 1e-6
-    wav = ao.swr_resample(x.astype(np.float64).mean(axis=1), sr, 16000).astype(np.float32)
+    wav = audio.load_input(data)
     ref = tr(wav, chunk_length_s=60, stride_length_s=5, generate_kwargs={"max_new_tokens": 32}, return_timestamps=True)
     assert res["text"] == ref["text"]
 
