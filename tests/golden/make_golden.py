@@ -1016,6 +1016,69 @@ def make_longform(out):
                    "features": feats, "cases": res}, fo)
 
 
+PROMPT_TOKENS = [1000, 2000, 3000, 4000, 5000, 6000]  # the prompt's text tokens (prompt_ids = [<|startofprev|>] + these)
+PROMPT_CASES = [  # name, pipeline kwargs, generate_kwargs (prompt_ids added by the maker), return_timestamps
+    ("chunk30_prompt_b3", dict(chunk_length_s=30, stride_length_s=0, batch_size=3),
+     {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40}, True),
+    ("long_prompt", {}, {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40}, True),
+    ("long_prompt_cond", {}, {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40,
+                              "condition_on_prev_tokens": True}, True),
+    ("long_prompt_all", {}, {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40,
+                             "condition_on_prev_tokens": True, "prompt_condition_type": "all-segments"}, True),
+    ("chunk30_prompt_no_ts", dict(chunk_length_s=30, stride_length_s=0, batch_size=3),
+     {"task": "transcribe", "num_beams": 1, "max_new_tokens": 40}, False),
+]
+
+
+def make_prompt(out):
+    """prompt_ids (generate()'s initial prompt, generation_whisper.py:1119-1124, 1885-1912) at test-mini on the 75-s
+    audio of make_longform: chunked 30-s windows and long-form, with and without condition_on_prev_tokens, both
+    prompt_condition_type values; the pipeline outputs and every seek pass's decoder prompt and raw output (the same
+    spy as make_longform)."""
+    from transformers import AutomaticSpeechRecognitionPipeline, WhisperFeatureExtractor
+    from transformers.models.whisper import generation_whisper as gw
+
+    d = DIMS
+    gen = GenerationSettings.default(d)
+    sd = wo.synth_state_dict(d.d_model, d.encoder_layers, d.decoder_layers, d.ffn, d.n_mels, d.vocab, SEED)
+    m = hf_model(d, sd, gen)
+    fe = WhisperFeatureExtractor(feature_size=d.n_mels)
+    pipe = AutomaticSpeechRecognitionPipeline(model=m, feature_extractor=fe, tokenizer=hf_tokenizer(gen.special),
+                                              device=-1)
+    audio = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)]).astype(np.float32)
+    # <|startofprev|>: a real checkpoint's generation_config names it (prev_sot_token_id); this synthetic one gets the
+    # token transformers falls back to without it (suppress_tokens[-2], generation_whisper.py:1876-1881)
+    m.generation_config.prev_sot_token_id = int(m.generation_config.suppress_tokens[-2])
+    prompt = [int(m.generation_config.prev_sot_token_id)] + PROMPT_TOKENS
+    orig = gw.WhisperGenerationMixin.generate_with_fallback
+    log = []
+
+    def spy(self, *a, **kw):
+        r = orig(self, *a, **kw)
+        log.append({"prompts": kw["decoder_input_ids"].tolist(), "rows": [int(i) for i in kw["batch_idx_map"]],
+                    "seek": kw["seek"].tolist(), "sequences": [x.tolist() for x in r[0]]})
+        return r
+
+    res = []
+    gw.WhisperGenerationMixin.generate_with_fallback = spy
+    try:
+        for name, kw, gk, ts in PROMPT_CASES:
+            log.clear()
+            c = {"name": name, "kwargs": kw, "generate_kwargs": gk, "return_timestamps": ts}
+            try:
+                c["output"] = _jsonable(pipe(audio.copy(), generate_kwargs=dict(gk, prompt_ids=torch.tensor(prompt)),
+                                             return_timestamps=ts, **kw))
+            except Exception as e:  # noqa: BLE001 - recorded as the reference would surface it
+                c["error"] = {"type": type(e).__name__, "message": str(e)}
+            c["passes"] = list(log)
+            res.append(c)
+    finally:
+        gw.WhisperGenerationMixin.generate_with_fallback = orig
+    with open(os.path.join(out, "prompt.json"), "w") as fo:
+        json.dump({"dims": "test-mini", "audio": "speech_like(40,5)+white_noise(35,11)", "prompt_ids": prompt,
+                   "cases": res}, fo)
+
+
 TINY_CLIPS = ("speech30", "noise12")
 
 

@@ -834,6 +834,23 @@ class WhisperEngine:
         return L
 
     @on_engine_streams
+    def _detect_languages(self, R: int) -> List[int]:
+        """detect_language (generation_whisper.py:1455-1520) for the R rows encoded into the current slot: one decoder
+        step on [SOT] at position 0 and the language argmax (the mode-1 selection), with no prompt in front — what
+        generate() does before its seek loop. Positions it writes are rewritten by the pass that follows."""
+        st = self.gen.special
+        self._dec_context()
+        self.stream.wait_event(self._enc_ev[self._slot])
+        with torch.cuda.stream(self.stream):
+            self.state[:R].zero_()
+            self.state[:R, _lib.TW_ST_LAST:_lib.TW_ST_LASTTS + 1] = -1
+            self.pos[:R] = 0
+            self.ids[:R] = st.sot
+            self.decoder_step(R)
+            self._select(R, self._select_params(1, 1), tokens=False)  # ids <- lang
+            out = self.ids[:R].tolist()
+        return [int(x) for x in out]
+
     def decode_pass(self, R: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
                     check_every: int = 8, use_timestamps: bool = True, align: bool = False,
                     num_frames: Optional[Sequence[int]] = None, prefix=None) -> PassResult:
@@ -1302,7 +1319,9 @@ class WhisperEngine:
                  max_passes: Optional[int] = None, slot: Optional[int] = None,
                  pre_encoded: bool = False, num_beams: int = 1, word_timestamps: bool = False,
                  num_frames: Optional[Sequence[int]] = None, fallback: Optional[FallbackConfig] = None,
-                 window_offset: int = 0, condition_on_prev_tokens: bool = False) -> List[List[int]]:
+                 window_offset: int = 0, condition_on_prev_tokens: bool = False,
+                 prompt_ids: Optional[Sequence[int]] = None,
+                 prompt_condition_type: Optional[str] = None) -> List[List[int]]:
         """Whisper short-form generate() over feats[slot][:n_chunks] (each 3000 frames): language
         detection, the seek loop and segment extraction, returning for every chunk the concatenated
         segment tokens (what generate() returns before padding).
@@ -1314,7 +1333,12 @@ class WhisperEngine:
         window_offset: the global index of chunk 0 (run_batches' batch offset): the sampler's per-row keys are built
         from global window indices, so windows of different batches draw independent noise.
         condition_on_prev_tokens: every pass after a chunk's first is prompted with <|startofprev|> + the chunk's
-        previous segments (_prepare_decoder_input_ids, generation_whisper.py:1853-1918), left padded over the batch."""
+        previous segments (_prepare_decoder_input_ids, generation_whisper.py:1853-1918), left padded over the batch.
+        prompt_ids / prompt_condition_type: generate()'s initial prompt (<|startofprev|> + text tokens). Unconditioned,
+        every pass is prompted with it (:1909-1912); conditioned, "first-segment" makes it the chunks' first segment
+        (:1119-1124: behind <|startofprev|>, cut with the rest to the last 223 tokens) and "all-segments" puts it in
+        front of the previous segments of every pass after the first (:1887-1888). The language is detected from the
+        SOT step alone, before any prompt (detect_language); the prompt is not part of the returned tokens."""
         if slot is not None:
             self.use_slot(slot)
         if pre_encoded and n_chunks > self.max_batch:
@@ -1341,6 +1365,20 @@ class WhisperEngine:
         prev_sot = self.gen.prev_sot_token_id
         if prev_sot is None and len(self.gen.suppress_tokens) >= 2:
             prev_sot = self.gen.suppress_tokens[-2]  # (:1876-1881)
+        prompt = None
+        if prompt_ids is not None:
+            prompt = [int(t) for t in prompt_ids]
+            ptype = prompt_condition_type or "first-segment"  # (_set_prompt_condition_type, :1732-1748)
+            if ptype not in ("first-segment", "all-segments"):
+                raise ValueError(f"`prompt_condition_type={ptype} does not exist. Make sure to set "
+                                 "`prompt_condition_type` to one of first-segment, all-segments")
+            if ptype == "all-segments" and not condition_on_prev_tokens:
+                raise ValueError("Make sure to set `condition_on_prev_tokens=True` when setting "
+                                 "`prompt_condition_type='all-segments'`.")
+            if ptype == "first-segment":  # the prompt is every chunk's first segment (_prepare_segments, :1119-1124)
+                first = prompt[1:] if prompt and prompt[0] == self.gen.prev_sot_token_id else prompt
+                seg_lists = [[list(first)] for _ in range(n_chunks)]
+            prompt = {"ids": prompt, "all": ptype == "all-segments"}
         # max_frames (_retrieve_max_frames_and_seek): 3000 per 30-s window; a long-form input's total frames
         if self._long is not None:
             if n_chunks != 1 or pre_encoded:
@@ -1354,13 +1392,13 @@ class WhisperEngine:
             return self._seek_loop(n_chunks, tail, prompt_len, max_new_tokens, max_new, seek, segs, passes_raw, langs,
                                    tts, maxf, seg_lists, do_cond, prev_sot, condition_on_prev_tokens, max_passes,
                                    pre_encoded, num_beams, word_timestamps, num_frames, fb, return_timestamps,
-                                   window_offset)
+                                   window_offset, prompt)
         finally:
             self._masked = False
 
     def _seek_loop(self, n_chunks, tail, prompt_len, max_new_tokens, max_new, seek, segs, passes_raw, langs, tts, maxf,
                    seg_lists, do_cond, prev_sot, condition, max_passes, pre_encoded, num_beams, word_timestamps,
-                   num_frames, fb, return_timestamps, window_offset):
+                   num_frames, fb, return_timestamps, window_offset, prompt=None):
         st = self.gen.special
         passes = 0
         while any(seek[i] < maxf[i] for i in range(n_chunks)):
@@ -1372,8 +1410,11 @@ class WhisperEngine:
             if condition and any(do_cond) and len(seg_lists[0]) > 0:
                 if len(rows) > per:
                     raise NotImplementedError(f"condition_on_prev_tokens over more than {per} rows in one pass")
-                prefix = condition_prefixes([seg_lists[i] if do_cond[i] else None for i in rows], prev_sot, st.eot,
+                bos = prompt["ids"] if prompt is not None and prompt["all"] else prev_sot
+                prefix = condition_prefixes([seg_lists[i] if do_cond[i] else None for i in rows], bos, st.eot,
                                             st.timestamp_begin, self.d.max_target_positions // 2 - 1)
+            elif prompt is not None:  # every pass prompted, no padding (:1909-1912)
+                prefix = ([list(prompt["ids"]) for _ in rows], [0] * len(rows))
             L = len(prefix[0][0]) if prefix is not None and prefix[0] else 0
             mnew = self.max_new_for(prompt_len + L, max_new_tokens) if L else max_new
             for b0 in range(0, len(rows), per):
@@ -1388,6 +1429,10 @@ class WhisperEngine:
                     self.encode(R)
                 part_langs = [langs[i] for i in part]
                 known = all(lg is not None for lg in part_langs) or not st.is_multilingual
+                if not known and pfx is not None:  # detect_language sees [SOT] alone, never the prompt
+                    det = self._detect_languages(R)
+                    part_langs = [lg if lg is not None else d for lg, d in zip(part_langs, det)]
+                    known = True
                 given = part_langs if (known and st.is_multilingual) else None
                 nf_part = None if num_frames is None else [int(num_frames[i]) - seek[i] for i in part]
                 if fb is not None:

@@ -123,6 +123,17 @@ class TurboTranscriber:
         # prompt every seek pass after a window's first with its previous segments (generate()'s
         # condition_on_prev_tokens; the batch then shapes results through the left padding, so batch_size is kept)
         cond = bool(gk.pop("condition_on_prev_tokens", None) or False)
+        # generate()'s initial prompt (<|startofprev|> + text tokens, WhisperProcessor.get_prompt_ids) and where it
+        # conditions (first-segment / all-segments)
+        prompt = {}
+        if gk.get("prompt_ids") is not None:
+            pid = gk.pop("prompt_ids")
+            pid = pid.tolist() if hasattr(pid, "tolist") else list(pid)
+            prompt = {"prompt_ids": [int(t) for t in np.asarray(pid).reshape(-1)],
+                      "prompt_condition_type": gk.pop("prompt_condition_type", None)}
+        gk.pop("prompt_ids", None)
+        if "prompt_condition_type" in gk:
+            prompt.setdefault("prompt_condition_type", gk.pop("prompt_condition_type"))
         fallback = self._fallback_config(gk)
         if gk:
             raise ValueError(f"generate_kwargs not supported by this engine: {sorted(gk)}")
@@ -152,7 +163,8 @@ class TurboTranscriber:
         elif len(wav) > CHUNK_SAMPLES:  # long-form: one sequential generate() over the whole input (asr:450-457)
             return self._long_form(wav, task=task, language=language, return_timestamps=return_timestamps,
                                    return_language=return_language, max_new_tokens=max_new_tokens,
-                                   num_beams=num_beams, max_passes=max_passes, fallback=fallback, condition=cond)
+                                   num_beams=num_beams, max_passes=max_passes, fallback=fallback, condition=cond,
+                                   prompt=prompt)
         else:
             windows = [Window(0, len(wav), 0, 0, True)]
             with_stride = False
@@ -168,6 +180,7 @@ class TurboTranscriber:
                       max_new_tokens=max_new_tokens, num_beams=num_beams, max_passes=max_passes,
                       **({"fallback": fallback, "window_base": base} if fallback.active else {}),
                       **({"condition_on_prev_tokens": True} if cond else {}),
+                      **({"prompt": prompt} if prompt else {}),
                       **({"group": batch_size} if grouped else {}))
             if word:  # token times ride along as floats after the tokens (one all-gather carries both)
                 nf = [-(-min(x.length, CHUNK_SAMPLES) // 160) for x in ws]
@@ -205,7 +218,7 @@ class TurboTranscriber:
         return lt[tok]
 
     def _long_form(self, wav, *, task, language, return_timestamps, return_language, max_new_tokens, num_beams,
-                   max_passes, fallback, condition=False) -> dict:
+                   max_passes, fallback, condition=False, prompt=None) -> dict:
         """An input longer than 30 s without chunk_length_s: the pipeline hands generate() the features of the whole
         input (feature extractor with truncation=False, padding="longest", $TF/pipelines/automatic_speech_recognition
         .py:450-457) and generate() runs its seek loop over all of them (generation_whisper.py:647-968: is_shortform
@@ -220,6 +233,7 @@ class TurboTranscriber:
         eng.set_long_input(x)
         try:
             kw = {"fallback": fallback} if fallback.active else {}
+            kw.update(prompt or {})
             if word:  # num_frames: the feature extractor's attention mask, one per hop (_set_num_frames)
                 kw.update(word_timestamps=True, num_frames=[-(-int(x.shape[0]) // 160)])
             toks = eng.generate(1, task=task, lang_ids=None if lang_id is None else [lang_id],
@@ -244,7 +258,8 @@ class TurboTranscriber:
                            max_new_tokens: Optional[int] = None, num_beams: int = 1, word_timestamps: bool = False,
                            num_frames: Optional[Sequence[int]] = None, group: Optional[int] = None,
                            max_passes: Optional[int] = None, fallback: Optional[FallbackConfig] = None,
-                           window_base: int = 0, condition_on_prev_tokens: bool = False) -> List[List[int]]:
+                           window_base: int = 0, condition_on_prev_tokens: bool = False,
+                           prompt: Optional[dict] = None) -> List[List[int]]:
         """Log-mel + generate for every window; returns per-window token sequences (generate() output,
         right-padded with the pad token within each engine batch, as the HF batch output is). Batches of
         max_batch windows go through WhisperEngine.run_batches: batch k+1 is encoded while batch k decodes.
@@ -294,7 +309,8 @@ class TurboTranscriber:
                               max_new_tokens=max_new_tokens, return_timestamps=return_timestamps, num_beams=num_beams,
                               max_passes=max_passes,
                               **({"fallback": fallback, "window_offset": window_base} if fallback is not None else {}),
-                              **({"condition_on_prev_tokens": True} if condition_on_prev_tokens else {}))
+                              **({"condition_on_prev_tokens": True} if condition_on_prev_tokens else {}),
+                              **(prompt or {}))
         out: List[List[int]] = []
         for seqs in res:
             out.extend(pad_right(seqs, self.gen.special.eot))

@@ -69,12 +69,15 @@ def segment_slices(seq: Sequence[int], timestamp_begin: int) -> List[List[int]]:
     return out
 
 
-def condition_prefixes(segments: Sequence[Optional[Sequence[Sequence[int]]]], prev_sot: Optional[int], pad: int,
+def condition_prefixes(segments: Sequence[Optional[Sequence[Sequence[int]]]], prev_sot, pad: int,
                        timestamp_begin: int, cut_off_length: int) -> Tuple[List[List[int]], List[int]]:
     """_prepare_decoder_input_ids' previous-token prompts (generation_whisper.py:1883-1906 via _pad_to_max_length with
     padding_side="left", skip_ending_double_timestamps=True, :126-232): per active row its segments' tokens (a segment
     ending in two timestamps loses the last one; None = the row is not conditioned), the last cut_off_length of them
-    behind <|startofprev|>, left padded with `pad` to the longest. Returns (rows, pad counts)."""
+    behind <|startofprev|>, left padded with `pad` to the longest. Returns (rows, pad counts).
+    prev_sot: the token in front (an int), or a token list (prompt_condition_type="all-segments": the prompt_ids,
+    generate()'s bos_token_tensor = prompt_ids, :1887-1888), or None."""
+    bos = [] if prev_sot is None else [int(t) for t in prev_sot] if isinstance(prev_sot, (list, tuple)) else [prev_sot]
     seqs = []
     for segs in segments:
         if segs is not None and len(segs) > 0:
@@ -82,9 +85,9 @@ def condition_prefixes(segments: Sequence[Optional[Sequence[Sequence[int]]]], pr
             for d in segs:
                 toks.extend(d[:-1] if len(d) > 2 and d[-2] >= timestamp_begin else d)
             toks = toks[-cut_off_length:] if cut_off_length else toks
-            seqs.append(([prev_sot] if prev_sot is not None else []) + toks)
+            seqs.append(bos + toks)
         else:
-            seqs.append([prev_sot] if prev_sot is not None else [])
+            seqs.append(list(bos))
     L = max((len(x) for x in seqs), default=0)
     return [[pad] * (L - len(x)) + x for x in seqs], [L - len(x) for x in seqs]
 
