@@ -1417,6 +1417,12 @@ class WhisperEngine:
                 prefix = ([list(prompt["ids"]) for _ in rows], [0] * len(rows))
             L = len(prefix[0][0]) if prefix is not None and prefix[0] else 0
             mnew = self.max_new_for(prompt_len + L, max_new_tokens) if L else max_new
+            if (prefix is not None and pre_encoded and passes == 0 and st.is_multilingual
+                    and any(langs[i] is None for i in rows)):
+                # (a pre-encoded first pass holds every chunk in the slot: detect them all before it is split)
+                det = self._detect_languages(len(rows))
+                for j, i in enumerate(rows):
+                    langs[i] = det[j] if langs[i] is None else langs[i]
             for b0 in range(0, len(rows), per):
                 part = rows[b0: b0 + per]
                 R = len(part)
