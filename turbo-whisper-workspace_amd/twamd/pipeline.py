@@ -134,6 +134,16 @@ class TurboTranscriber:
         gk.pop("prompt_ids", None)
         if "prompt_condition_type" in gk:
             prompt.setdefault("prompt_condition_type", gk.pop("prompt_condition_type"))
+        # (_set_prompt_condition_type's checks, generation_whisper.py:1732-1748, before any work is queued)
+        pct = prompt.get("prompt_condition_type") or "first-segment"
+        if pct not in ("first-segment", "all-segments"):
+            raise ValueError(f"`prompt_condition_type={pct} does not exist. Make sure to set `prompt_condition_type` "
+                             "to one of first-segment, all-segments")
+        if pct == "all-segments" and not cond:
+            raise ValueError("Make sure to set `condition_on_prev_tokens=True` when setting "
+                             "`prompt_condition_type='all-segments'`.")
+        if "prompt_ids" not in prompt:
+            prompt = {}
         fallback = self._fallback_config(gk)
         if gk:
             raise ValueError(f"generate_kwargs not supported by this engine: {sorted(gk)}")
