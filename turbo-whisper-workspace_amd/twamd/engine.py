@@ -1438,6 +1438,8 @@ class WhisperEngine:
                 if not known and pfx is not None:  # detect_language sees [SOT] alone, never the prompt
                     det = self._detect_languages(R)
                     part_langs = [lg if lg is not None else d for lg, d in zip(part_langs, det)]
+                    for j, i in enumerate(part):  # (kept for the later passes and last_langs)
+                        langs[i] = part_langs[j]
                     known = True
                 given = part_langs if (known and st.is_multilingual) else None
                 nf_part = None if num_frames is None else [int(num_frames[i]) - seek[i] for i in part]
