@@ -13,8 +13,10 @@ stream, and (optionally) hipGraph capture of the per-token decoder step.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import dataclasses
+import gc
 import os
 from typing import Dict, List, Optional, Sequence
 
@@ -32,6 +34,22 @@ import functools
 
 LN_EPS = 1e-5
 S_ENC = 1500
+
+
+@contextlib.contextmanager
+def _capture(g: "torch.cuda.CUDAGraph", stream):
+    """torch.cuda.graph with Python's cyclic GC held off while the graph records: a collection inside the capture runs
+    finalizers of earlier engines' graphs / events / buffers (HIP frees and destroys, illegal while a stream captures),
+    which aborted a full GPU suite run (r04ae)."""
+    was = gc.isenabled()
+    gc.collect()
+    gc.disable()
+    try:
+        with torch.cuda.graph(g, stream=stream):
+            yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def _pad256(n: int) -> int:
@@ -910,7 +928,7 @@ class WhisperEngine:
             g = self._graphs.get(key)
             if g is None:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=self.stream):  # records, does not execute
+                with _capture(g, self.stream):  # records, does not execute
                     prompt()
                 self._graphs[key] = g
             g.replay()
@@ -1221,7 +1239,7 @@ class WhisperEngine:
                 g = self._graphs.get(key)
                 if g is None:
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, stream=self.stream):  # records, does not execute
+                    with _capture(g, self.stream):  # records, does not execute
                         step()
                     self._graphs[key] = g
             steps = 0
@@ -1279,7 +1297,7 @@ class WhisperEngine:
         g = torch.cuda.CUDAGraph()
         v.stream.wait_stream(self.stream)
         with torch.cuda.stream(v.stream):
-            with torch.cuda.graph(g, stream=v.stream):  # records, does not execute
+            with _capture(g, v.stream):  # records, does not execute
                 self._gen_step(v.n, params, v=v, r_enc=R, fused=fused)
         self.stream.wait_stream(v.stream)
         self._graphs[key] = g
