@@ -300,6 +300,17 @@ def parity_vs_golden(eng, B, T, model, fp8):
                 "worst_d_logit": forced["worst_d_logit"]}
 
 
+def profile_order(path: str):
+    """Sort key of a profiles/ file by its round tag: (round, tag length, tag) — r05b < r05z < r05ab < r06a. A plain
+    basename sort put r04t after r04ae (and would put r05b after r05ab)."""
+    import re
+
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    if not m:
+        return (-1, 0, os.path.basename(path))
+    return (int(m.group(1)), len(m.group(2)), m.group(2))
+
+
 def measured_traffic(kernels, c5: bool = False):
     """HBM bytes per launch of the `kernels` (names of one family, launch-weighted together) from the newest
     rocprofv3 PMC summary under profiles/ that has any of them (scripts/summarize_prof.py: 2*FETCH_SIZE + WRITE_SIZE
@@ -307,9 +318,8 @@ def measured_traffic(kernels, c5: bool = False):
     own."""
     import glob
 
-    # newest = the latest round tag (profiles/rNN<x>_..., names sort by round); file mtimes do not survive the copy
-    # to the GPU box reliably
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json")), key=os.path.basename)
+    # newest = the latest round tag (profile_order); file mtimes do not survive the copy to the GPU box reliably
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json")), key=profile_order)
     files = [f for f in files if ("_c5_" in os.path.basename(f)) == c5]
     for f in reversed(files):
         try:
@@ -330,7 +340,7 @@ def measured_mfma(kernels, c5: bool = False):
     the profiler, so this is the kernel's own utilisation, not the in-situ one), launch-weighted, or (None, None)."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*mfma.json")), key=os.path.basename)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*mfma.json")), key=profile_order)
     files = [f for f in files if ("_c5_" in os.path.basename(f)) == c5]
     for f in reversed(files):
         try:

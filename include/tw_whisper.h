@@ -256,6 +256,10 @@ int tw_gemv_packed(const uint16_t* A, int a_packed, int lda, const uint16_t* Wp,
  * 1 beside a running encoder GEMM, 4 when the decode has the GPU to itself. Same results up to the f32 order of the
  * K-slice sum. Returns 0. */
 int tw_gemv_set_wide_slices(int kw);
+/* Process-wide kernel of tw_gemv_packed's decoder-layer shapes (N < 16384, epilogues BF16 / GELU_PACKED / PARTIAL):
+ * 0 = two column groups per wave in batches of 5 K-steps, 1 = one column group per wave with its whole K-slice of
+ * weight fragments in flight (<= 10 steps). Same results up to the f32 order of the K-slice sum. Returns 0. */
+int tw_gemv_set_variant(int v);
 /* tw_resid_layernorm with the normalised rows written as a packed activation (M <= 64, D % 32 == 0). */
 int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
                               const float* beta, int M, int D, float eps, uint16_t* out, void* stream);

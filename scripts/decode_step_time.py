@@ -25,6 +25,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, nargs="+", default=[15, 24, 64])
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--check-every", type=int, nargs="+", default=[8])
+    ap.add_argument("--graph-steps", type=int, nargs="+", default=[1])
+    ap.add_argument("--slope", type=int, default=0, help="also time 64-token passes: per-step slope without the "
+                    "pass's fixed costs")
     a = ap.parse_args()
     dims = PRESETS["large-v3-turbo"]
     gen = GenerationSettings.default(dims)
@@ -39,19 +43,42 @@ def main():
         eng.seek[:R] = 0
         eng.encode(R)
         torch.cuda.synchronize()
-        for mode in ("separate",):
-            eng._graphs.clear()
-            eng.decode_pass(R, tail, None, 128)  # warm-up: graph captures
-            torch.cuda.synchronize()
-            best = 1e9
-            for _ in range(a.reps):
-                t0 = time.perf_counter()
-                res = eng.decode_pass(R, tail, None, 128)
+        ref = None
+        for ce in a.check_every:
+            for gs in a.graph_steps:
+                eng.graph_steps_alone = gs
+                eng._graphs.clear()
+                eng.decode_pass(R, tail, None, 128, check_every=ce)  # warm-up: graph captures
                 torch.cuda.synchronize()
-                best = min(best, time.perf_counter() - t0)
-            assert all(len(t) == 128 for t in res.tokens)
-            print(json.dumps({"rows": R, "mode": mode, "pass_ms": round(best * 1e3, 2),
-                              "step_us": round(best * 1e6 / 130, 1)}), flush=True)
+                best = 1e9
+                eng.pass_events = []
+                for _ in range(a.reps):
+                    t0 = time.perf_counter()
+                    res = eng.decode_pass(R, tail, None, 128, check_every=ce)
+                    torch.cuda.synchronize()
+                    best = min(best, time.perf_counter() - t0)
+                loop_us = min(e0.elapsed_time(e1) * 1e3 / n for e0, e1, n, _ in eng.pass_events)
+                eng.pass_events = None
+                print(json.dumps({"rows": R, "check_every": ce, "graph_steps": gs, "loop_us_per_step": round(loop_us, 1)}),
+                      flush=True)
+                assert all(len(t) == 128 for t in res.tokens)
+                ref = res.tokens if ref is None else ref
+                if a.slope:
+                    eng.decode_pass(R, tail, None, 64, check_every=ce)
+                    torch.cuda.synchronize()
+                    b64 = 1e9
+                    for _ in range(a.reps):
+                        t0 = time.perf_counter()
+                        eng.decode_pass(R, tail, None, 64, check_every=ce)
+                        torch.cuda.synchronize()
+                        b64 = min(b64, time.perf_counter() - t0)
+                    print(json.dumps({"rows": R, "check_every": ce, "graph_steps": gs,
+                                      "pass64_ms": round(b64 * 1e3, 2),
+                                      "slope_us_per_step": round((best - b64) * 1e6 / 64, 1),
+                                      "fixed_ms": round((b64 - 66 * (best - b64) / 64) * 1e3, 2)}), flush=True)
+                print(json.dumps({"rows": R, "check_every": ce, "graph_steps": gs, "pass_ms": round(best * 1e3, 2),
+                                  "step_us": round(best * 1e6 / 130, 1), "tokens_equal": res.tokens == ref}),
+                      flush=True)
 
 
 if __name__ == "__main__":

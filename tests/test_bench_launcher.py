@@ -52,3 +52,12 @@ def test_mismatch_exits_nonzero_before_any_gpu_call():
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 2
     assert "WORLD_SIZE=3" in p.stderr
+
+
+def test_profile_order_is_by_round_then_tag_length():
+    """profiles/ summaries are picked newest-first by round tag, not by basename (r04t sorted after r04ae)."""
+    names = ["r05ab_traffic.json", "r05b_traffic.json", "r04ae_traffic.json", "r04t_traffic.json", "r06a_traffic.json",
+             "r05z_c5_traffic.json"]
+    got = [os.path.basename(p) for p in sorted(names, key=bench.profile_order)]
+    assert got == ["r04t_traffic.json", "r04ae_traffic.json", "r05b_traffic.json", "r05z_c5_traffic.json",
+                   "r05ab_traffic.json", "r06a_traffic.json"]

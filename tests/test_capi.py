@@ -65,9 +65,9 @@ def test_debug_library_exports_the_same_abi_and_says_so():
     """libtwhip_dbg.so (make debug: -DTW_DEBUG=1, the C-ABI contract checks) exports the same symbols and reports
     itself as the debug build; the product library does not."""
     dbg = os.path.join(ROOT, "turbo-whisper-workspace_amd", "twamd", "libtwhip_dbg.so")
-    if not os.path.exists(dbg):
-        subprocess.run(["make", "-C", os.path.join(ROOT, "turbo-whisper-workspace_amd", "csrc"), "-j8", "debug"],
-                       check=True, capture_output=True)
+    # (incremental: rebuilds only what changed since the last debug build)
+    subprocess.run(["make", "-C", os.path.join(ROOT, "turbo-whisper-workspace_amd", "csrc"), "-j8", "debug"],
+                   check=True, capture_output=True)
     out = subprocess.run(["nm", "-D", "--defined-only", dbg], check=True, capture_output=True, text=True).stdout
     exported = set(re.findall(r"\bT (tw_\w+)", out))
     assert not [n for n in _declared() if n not in exported]

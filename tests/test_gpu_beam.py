@@ -330,6 +330,8 @@ def test_debug_build_refuses_racy_position_table():
     """the -DTW_DEBUG=1 library (libtwhip_dbg.so) checks the position-table contract before the
     launch and fails loudly (TW_ERR_ARG naming the row) instead of racing; a valid table runs and gives the product
     library's output bit for bit."""
+    if not os.path.exists(_lib.DEBUG_LIB_PATH):
+        pytest.skip("libtwhip_dbg.so not built (make -C turbo-whisper-workspace_amd/csrc debug)")
     dbg = _lib.load_debug()
     R, cap, T, row0, H = 12, 20, 448, 5, 4
     tab, pos, bad = _racy_table(R, cap, T, row0, 12)

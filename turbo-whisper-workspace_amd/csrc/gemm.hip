@@ -94,6 +94,14 @@ extern "C" int tw_gemv_set_wide_slices(int kw) {
 // SIMD co-resides with an encoder GEMM workgroup (2 waves of ~190 VGPRs on every SIMD), where a 512-thread decoder
 // workgroup waits for GEMM workgroups to retire (q/k/v GEMV beside k_gemm_8p: 33.6 us per launch at 8, 11.5 at 4).
 static constexpr int tw_gemv_max_kw = 4;
+// The decoder layer GEMVs' kernel (tw_gemv_set_variant): 0 = k_gemv_pc (two column groups per wave, batches of 5
+// steps), 1 = k_gemv_q (one column group per wave, its whole K-slice in flight)
+static int tw_gemv_kernel = 0;
+extern "C" int tw_gemv_set_variant(int v) {
+  TW_REQUIRE(v == 0 || v == 1, "tw_gemv_set_variant: v=%d (0 or 1)", v);
+  tw_gemv_kernel = v;
+  return 0;
+}
 extern "C" int tw_gemm_set_variant(int v) {
   tw_gemm_kernel = (v & 15) == 5 ? 5 : 1;
   return 0;
@@ -1057,6 +1065,130 @@ static void launch_gemv_pc(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
     hipLaunchKernelGGL((k_gemv_pc<EPI, KW, U, APACK, 1, NTW>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
 }
 
+// k_gemv_q: ONE column group per wave and every weight fragment of the wave's K-slice in flight at once (n <= U
+// steps, one HBM round trip per wave), spread over >= 256 workgroups where the shape allows; the activation fragments
+// (L2-resident, shared by every column group) stream two steps behind through a double buffer, so they cost no
+// long-lived registers. k_gemv_pc's waves instead hold two column groups and run their K-slice in batches of 5 steps
+// (two dependent HBM round trips per wave for the 40-step slices of q/k/v, cross-q, fc1, fc2) on 40-160 workgroups.
+// Block = 4 waves = GPB column groups x KW K-slices (reduced through LDS); gridDim.y = split-K slices over blocks
+// (PARTIAL only). n = this wave's step count, wave-uniform (the guards are scalar branches, not clamped re-loads).
+template <int EPI, int KW, int U, bool APACK, int MT>
+__global__ TW_DEC_LB(256, 1) void k_gemv_q(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ Wp,
+                                           int M, int N, int K, EpiArgs ea) {
+  TW_DEC_PRIO();
+  static_assert(KW == 1 || KW == 2 || KW == 4, "k_gemv_q: 1, 2 or 4 K-slices");
+  constexpr int NW = 4, GPB = NW / KW;
+  __shared__ float red[KW > 1 ? NW : 1][KW > 1 ? MT * 16 : 1][17];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int gl = wid / KW, kw = wid - gl * KW;
+  const int g = blockIdx.x * GPB + gl;
+  const int ngroups = (N + 15) >> 4, ns = K >> 5;
+  const int nsl = KW * gridDim.y, sl = blockIdx.y * KW + kw;
+  const int s0 = (int)((long)sl * ns / nsl), s1 = (int)((long)(sl + 1) * ns / nsl);
+  const int n = s1 - s0;
+  f32x4 c[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) c[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (g < ngroups) {
+    const bf16_t* wp = Wp + ((size_t)g * ns + s0) * 512 + lane * 8;
+    const bf16_t* ap[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) ap[t] = gemv_a_base<MT, APACK>(A, lda, M, K, t, lane);
+    bf16x8 w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (u < n) w[u] = *(const bf16x8*)(wp + (size_t)u * 512);
+    bf16x8 a[2][MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) a[0][t] = gemv_a_load<APACK>(ap[t], s0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < n) {
+        if (u + 1 < n) {
+#pragma unroll
+          for (int t = 0; t < MT; ++t) a[(u + 1) & 1][t] = gemv_a_load<APACK>(ap[t], s0 + u + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) c[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u & 1][t], w[u], c[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  const int cc = lane & 15, rb = (lane >> 4) * 4;
+  auto store = [&](int m, int col, float v) {
+    if constexpr (EPI == TW_EPI_PARTIAL) {
+      ((float*)ea.out)[((size_t)blockIdx.y * M + m) * ea.ldo + col] = v;
+    } else if constexpr (EPI == TW_EPI_GELU_PACKED) {
+      if (ea.bias) v += ea.bias[col];
+      ((bf16_t*)ea.out)[tw_pack_act_idx(m, col, N)] = f32_to_bf16(gelu_erf(v));
+    } else {
+      epi_store<EPI>(ea, m, col, v);
+    }
+  };
+  if constexpr (KW == 1) {
+    const int col = g * 16 + cc;
+    if (g < ngroups && col < N) {
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (16 * t + rb + r < M) store(16 * t + rb + r, col, c[t][r]);
+    }
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wid][16 * t + rb + r][cc] = c[t][r];
+  __syncthreads();
+  constexpr int ROWS = MT * 16;
+  for (int e = tid; e < GPB * ROWS * 16; e += NW * 64) {
+    const int gg = e / (ROWS * 16), rem = e - gg * ROWS * 16;
+    const int m = rem >> 4, cl = rem & 15;
+    const int col = (blockIdx.x * GPB + gg) * 16 + cl;
+    if (m < M && col < N) {
+      float v = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < KW; ++w2) v += red[gg * KW + w2][m][cl];
+      store(m, col, v);
+    }
+  }
+}
+
+// k_gemv_q's geometry: the fewest K-slices per block that bring every wave to <= 10 steps. Returns false when the
+// shape needs more (the caller falls back to k_gemv_pc).
+template <int EPI, bool APACK, int KW, int MT>
+static void launch_gemv_q_mt(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea,
+                             int splits, hipStream_t s) {
+  dim3 grid(tw_cdiv(tw_cdiv(N, 16), 4 / KW), splits);
+  hipLaunchKernelGGL((k_gemv_q<EPI, KW, 10, APACK, MT>), grid, dim3(256), 0, s, A, lda, Wp, M, N, K, ea);
+}
+template <int EPI, bool APACK, int KW>
+static void launch_gemv_q_kw(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea,
+                             int splits, hipStream_t s) {
+  if (M > 32) launch_gemv_q_mt<EPI, APACK, KW, 4>(A, lda, Wp, M, N, K, ea, splits, s);
+  else if (M > 16) launch_gemv_q_mt<EPI, APACK, KW, 2>(A, lda, Wp, M, N, K, ea, splits, s);
+  else launch_gemv_q_mt<EPI, APACK, KW, 1>(A, lda, Wp, M, N, K, ea, splits, s);
+}
+template <int EPI, bool APACK>
+static bool launch_gemv_q(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea,
+                          int splits, hipStream_t s) {
+  const int per = K / 32 / splits;  // steps per split-K slice
+  const int ngroups = tw_cdiv(N, 16);
+  // K-slices per block: the fewest that bring a wave to <= 10 steps; one more halving while the grid stays below
+  // 256 workgroups and the waves keep >= 5 steps (o_proj: 80 groups x 4 splits of 10 steps -> KW = 2, 160 blocks)
+  int kw = 1;
+  while (kw < 4 && (per + kw - 1) / kw > 10) kw *= 2;
+  if ((per + kw - 1) / kw > 10) return false;
+  while (kw < 4 && (long)tw_cdiv(ngroups, 4 / kw) * splits < 256 && (per + 2 * kw - 1) / (2 * kw) >= 5) kw *= 2;
+  if (kw == 1) launch_gemv_q_kw<EPI, APACK, 1>(A, lda, Wp, M, N, K, ea, splits, s);
+  else if (kw == 2) launch_gemv_q_kw<EPI, APACK, 2>(A, lda, Wp, M, N, K, ea, splits, s);
+  else launch_gemv_q_kw<EPI, APACK, 4>(A, lda, Wp, M, N, K, ea, splits, s);
+  return true;
+}
+
 template <int EPI, int KW, int U, bool APACK, bool NTW = false>
 static void launch_gemv_p3(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea, int splits,
                            hipStream_t s) {
@@ -1090,6 +1222,7 @@ static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
   }
   if constexpr (EPI == TW_EPI_BF16 || EPI == TW_EPI_PARTIAL || EPI == TW_EPI_GELU_PACKED) {
     // the layer GEMVs as column-group pairs (k_gemv_pc): a third fewer vector-memory instructions per weight byte
+    if (tw_gemv_kernel == 1 && launch_gemv_q<EPI, APACK>(A, lda, Wp, M, N, K, ea, splits, s)) return;
     const long pairs = tw_cdiv(tw_cdiv(N, 16), 2) * (long)splits;
     if (pairs * 2 < 1024 && steps >= 8 * 4) launch_gemv_pc<EPI, 4, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
     else launch_gemv_pc<EPI, 2, APACK>(A, lda, Wp, M, N, K, ea, splits, s);

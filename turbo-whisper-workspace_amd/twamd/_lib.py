@@ -44,7 +44,7 @@ EXPORTED = (
     "tw_kv_tab_check", "tw_debug_build", "tw_resid_layernorm_packed_to", "tw_conv2_gemm",
     "tw_logmel_long", "tw_im2col_conv1_long", "tw_attn_decode_self_masked", "tw_attn_decode_self_tab_masked",
     "tw_gemv_set_wide_slices", "tw_vorbis_probe", "tw_vorbis_decode", "tw_vorbis_imdct",
-    "tw_layernorm_set_lds_pad",
+    "tw_layernorm_set_lds_pad", "tw_gemv_set_variant",
 )
 
 
@@ -124,6 +124,7 @@ _SIGS = {
     "tw_token_prob": ([_P, _I, _I, _I, _I, _P, _P], _I),
     "tw_gemm_bf16_partial": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P], _I),
     "tw_gemv_set_wide_slices": ([_I], _I),
+    "tw_gemv_set_variant": ([_I], _I),
     "tw_gemm_set_variant": ([_I], _I),
     "tw_gemm_mx_set_variant": ([_I], _I),
     "tw_logits_select_embed": ([_P, _I, _I, _P, ctypes.POINTER(TwSelectParams), _P, _P, _I, _P, _P, _P, _P, _P, _I,

@@ -18,6 +18,7 @@ import ctypes
 import dataclasses
 import gc
 import os
+import time
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -286,6 +287,10 @@ class WhisperEngine:
         # greedy steps end with the fused select + next-step embedding + first LayerNorm (tw_logits_select_embed):
         # 47 launches per token instead of 49 (False: the separate launches; the tests check both decode alike)
         self.fused_select = True
+        # decoder steps per graph replay in the generation loop: alone (no encoder chunks pumped between steps) and
+        # beside run_batches' encoder pump (TW_GRAPH_STEPS_ALONE / _BESIDE for A/B)
+        self.graph_steps_alone = int(os.environ.get("TW_GRAPH_STEPS_ALONE", "1"))
+        self.graph_steps_beside = int(os.environ.get("TW_GRAPH_STEPS_BESIDE", "1"))
         # the prompt phase of a decode pass replayed as one captured graph (False: eager)
         self.prompt_graph = True
         # encoder attention kernel (tw_attn_set_variant) and its LDS cap in 16 KiB units (tw_attn_set_lds_pad) for an
@@ -765,6 +770,9 @@ class WhisperEngine:
     # and re-run the head of the next step (embed_head) so the next replay of the captured step consumes the forced
     # token instead of the one the selection chose. None in normal decoding.
     step_hook = None
+    # measurement: a list to which decode_pass appends (start event, end event, steps) of its generation loop
+    pass_events: Optional[list] = None
+    replay_host: list = []
 
     def embed_head(self, v: Optional[DecView] = None, R: Optional[int] = None) -> None:
         """The next step's head (embedding of ids at pos + layer 0's LayerNorm) for view v, or for rows [0, R) when
@@ -869,6 +877,7 @@ class WhisperEngine:
             out = self.ids[:R].tolist()
         return [int(x) for x in out]
 
+    @on_engine_streams
     def decode_pass(self, R: int, tail: Sequence[int], lang_ids: Optional[Sequence[int]], max_new: int,
                     check_every: int = 8, use_timestamps: bool = True, align: bool = False,
                     num_frames: Optional[Sequence[int]] = None, prefix=None) -> PassResult:
@@ -952,13 +961,33 @@ class WhisperEngine:
                 with torch.cuda.stream(c.stream):
                     self._embed_head(c)
         pump, inflight = self._pump, []
+        # steps per graph replay: several captured back to back when no encoder chunk is pumped between steps and no
+        # teacher-forcing hook runs after each (one host replay per graph_steps tokens)
+        gs = 1 if (hook is not None or graphs is None) else (
+            self.graph_steps_beside if pump is not None else self.graph_steps_alone)
+        if gs > 1 and max_new - steps >= gs:  # (captured before the loop, like the one-step graphs)
+            for i, c in enumerate(chains):
+                self._graph_for(R, params, i, c, fused, gs)
+        ev0 = None
+        if self.pass_events is not None:  # (measurement: HIP events around the generation loop)
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record(chains[0].stream)
+            th0 = time.perf_counter()
         while steps < max_new:
             n = min(check_every if hook is None else 1, max_new - steps)
-            for _ in range(n):
+            done = 0
+            while done < n:
+                k = gs if n - done >= gs else 1
+                done += k
                 for i, c in enumerate(chains):
                     if graphs is not None:
+                        g = graphs[i] if k == 1 else self._graph_for(R, params, i, c, fused, k)
+                        if ev0 is not None:
+                            tr = time.perf_counter()
                         with torch.cuda.stream(c.stream):
-                            graphs[i].replay()
+                            g.replay()
+                        if ev0 is not None:
+                            self.replay_host.append(time.perf_counter() - tr)
                     else:
                         self._gen_step(c.n, params, v=c, r_enc=R, fused=fused)
                 if hook is not None:
@@ -980,6 +1009,10 @@ class WhisperEngine:
                 self.stream.wait_stream(c.stream)
             if bool(self.state[:R, _lib.TW_ST_FINISHED].all().item()):
                 break
+        if ev0 is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record(self.stream)
+            self.pass_events.append((ev0, ev1, steps - 1, time.perf_counter() - th0))
         ngen = self.state[:R, _lib.TW_ST_NGEN].tolist()
         toks = self.tokens[:R].tolist()
         detected = self.state[:R, _lib.TW_ST_LANG].tolist() if detect else None  # (mode-1 selection only writes it)
@@ -1287,10 +1320,13 @@ class WhisperEngine:
             self._chain_cache[key] = views
         return self._chain_cache[key]
 
-    def _graph_for(self, R: int, params, i: int, v: DecView, fused: bool = False) -> Optional[torch.cuda.CUDAGraph]:
+    def _graph_for(self, R: int, params, i: int, v: DecView, fused: bool = False,
+                   n_steps: int = 1) -> Optional[torch.cuda.CUDAGraph]:
+        """The captured decode step of chain i (n_steps > 1: that many steps back to back in one graph)."""
         al = self._align
         key = (R, params.max_new, params.use_timestamps, self._slot, i, fused,
-               None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()), self._masked, self._wide_kw)
+               None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()), self._masked, self._wide_kw,
+               n_steps)
         g = self._graphs.get(key)
         if g is not None:
             return g
@@ -1298,7 +1334,8 @@ class WhisperEngine:
         v.stream.wait_stream(self.stream)
         with torch.cuda.stream(v.stream):
             with _capture(g, v.stream):  # records, does not execute
-                self._gen_step(v.n, params, v=v, r_enc=R, fused=fused)
+                for _ in range(n_steps):
+                    self._gen_step(v.n, params, v=v, r_enc=R, fused=fused)
         self.stream.wait_stream(v.stream)
         self._graphs[key] = g
         return g
