@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--decode-tokens", type=int, default=128)
     ap.add_argument("--model", default="large-v3-turbo")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="N = 1: run the RCCL path anyway (an nccl group of one; the per-batch token all-gather, c3's "
+                         "waveform broadcast and sharded call)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--profile-only", action="store_true", help="warmup + steps only (for rocprofv3)")
     ap.add_argument("--eos", action="store_true",
@@ -107,6 +110,14 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    forced = world == 1 and a.force_collective
+    if forced:  # an RCCL group of one: the per-batch all-gather runs on device tensors exactly as at N > 1
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", local))
 
     from twamd.config import PRESETS, GenerationSettings
     from twamd.engine import WhisperEngine
@@ -136,6 +147,8 @@ def main():
     if not a.eos:
         eng.set_suppress_tokens(list(gen.suppress_tokens) + [gen.special.eot])  # fixed decode length
     from twamd import dist as twd
+    if forced:
+        twd.FORCE_COLLECTIVE = True
     if strong:
         # 1 h of synthetic speech-like audio (120 seeded 30-s windows back to back), on the host as a caller's array
         hour = workload(120 // max(1, a.c3_share), 30.0, seed=1234).reshape(-1)
@@ -154,7 +167,7 @@ def main():
         """n_steps batches of B windows through the engine's two-slot pipeline (the encoder of batch k+1 runs on
         a second HIP stream beside the decode of batch k); every rank then all-gathers each batch's tokens."""
         res = eng.run_batches([B] * n_steps, task="transcribe", max_new_tokens=T, max_passes=1)
-        if world > 1:  # rank r holds windows [rB, (r+1)B) of each batch: one RCCL all-gather per batch
+        if world > 1 or forced:  # rank r holds windows [rB, (r+1)B) of each batch: one RCCL all-gather per batch
             res = [twd.gather_tokens(seqs, lg, world * B)[0] for seqs, lg in zip(res, eng.batch_langs)]
         return res[-1] if res else []
 
@@ -230,6 +243,8 @@ def main():
                                   f"greedy, {T} new tokens/window (EOS suppressed, one seek pass), timestamps on, "
                                   "language detected"),
                    "c3_share": a.c3_share if strong else None,
+                   "collectives": ("rccl" if backend == "nccl" else backend) if world > 1 else
+                                  ("rccl (group of one, forced)" if forced else "none"),
                    "global_batch": int(audio_s // 30), "seq_len": 3000, "parallelism": f"chunk-dp{world}",
                    "decode_tokens_per_window": T, "mean_tokens_out": float(np.mean(n_tok))},
         "roofline": {"bound": "mfma",
@@ -255,7 +270,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(dims, gen, T, a.cpu_threads)
     if rank == 0:
         print(json.dumps(out))
-    if world > 1:
+    if world > 1 or forced:
         dist.destroy_process_group()
 
 

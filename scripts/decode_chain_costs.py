@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--variants", type=int, nargs="+", default=[0], help="tw_gemv_set_variant values to compare")
     ap.add_argument("--families", type=int, default=1, help="0: the full step only")
     ap.add_argument("--passlike", type=int, default=0)
+    ap.add_argument("--wide-kw", type=int, nargs="+", default=[1], help="proj_out K-slices (tw_gemv_set_wide_slices)")
     a = ap.parse_args()
     dims = PRESETS["large-v3-turbo"]
     gen = GenerationSettings.default(dims)
@@ -97,8 +98,9 @@ def main():
             return us
 
         ref_logits = None
-        for var in a.variants:
+        for var, wkw in [(v_, w_) for w_ in a.wide_kw for v_ in a.variants]:
             _real_call("tw_gemv_set_variant", var)
+            _real_call("tw_gemv_set_wide_slices", wkw)
             with torch.cuda.stream(eng.stream):
                 eng.ids[:R] = 50300
                 eng.pos[:R] = a.pos
@@ -110,7 +112,7 @@ def main():
                 ref_logits = lg
             diff = float((lg - ref_logits).abs().max())
             base = timed(step, "full")
-            print(json.dumps({"rows": R, "gemv_variant": var, "case": "full step", "us": round(base, 1),
+            print(json.dumps({"rows": R, "gemv_variant": var, "wide_kw": wkw, "case": "full step", "us": round(base, 1),
                               "logits_maxdiff_vs_first": diff}), flush=True)
         if a.passlike:
             # the step graph replayed as a pass replays it: positions advancing from 3, state carried (pass-like),
@@ -219,29 +221,38 @@ def main():
                       flush=True)
 
             plain("plain again")
-            for label, with_prompt, sync_after_prompt in (("A prompt+loop", True, False), ("B loop only", False, False),
-                                                          ("C prompt, sync, loop", True, True)):
-                plain("plain before " + label)
+
+            def variant(label, wait, head, sync, e1_on_eng):
                 torch.cuda.synchronize()
                 with torch.cuda.stream(eng.stream):
-                    if with_prompt:
-                        eng._graphs[pk[0]].replay()
-                    else:
-                        eng.pos[:R] = 3
-                    if sync_after_prompt:
+                    eng.pos[:R] = 3
+                    if wait:
+                        c.stream.wait_stream(eng.stream)
+                    if head:
+                        with torch.cuda.stream(c.stream):
+                            eng._embed_head(c)
+                    if sync:
                         torch.cuda.synchronize()
-                    c.stream.wait_stream(eng.stream)
-                    with torch.cuda.stream(c.stream):
-                        eng._embed_head(c)
                     e0.record(c.stream)
                     for _ in range(127):
                         with torch.cuda.stream(c.stream):
                             g.replay()
-                    eng.stream.wait_stream(c.stream)
-                    e1.record(eng.stream)
+                    if e1_on_eng:
+                        eng.stream.wait_stream(c.stream)
+                        e1.record(eng.stream)
+                    else:
+                        e1.record(c.stream)
                 torch.cuda.synchronize()
                 print(json.dumps({"rows": R, "case": label, "us": round(e0.elapsed_time(e1) * 1e3 / 127, 1)}),
                       flush=True)
+
+            variant("B  wait+head, no sync, e1 on eng", True, True, False, True)
+            variant("B1 wait, no head, no sync, e1 on eng", True, False, False, True)
+            variant("B2 wait+head, sync", True, True, True, True)
+            variant("B3 head, no wait, no sync", False, True, False, True)
+            variant("B4 wait, sync, no head", True, False, True, True)
+            variant("B5 wait+head, no sync, e1 on chain", True, True, False, False)
+            variant("B6 nothing, no sync, e1 on chain", False, False, False, False)
             plain("plain after")
             with torch.cuda.stream(eng.stream):
                 eng.state[:R].zero_()

@@ -570,11 +570,19 @@ def test_gemv_wide_k_slices_vs_torch(M, K, kw):
         _lib.call("tw_gemv_set_wide_slices", 3)
 
 
+@pytest.fixture(params=[0, 1], ids=["gemv_pc", "gemv_q"])
+def gemv_variant(request):
+    """tw_gemv_set_variant for the test (0: k_gemv_pc, 1: k_gemv_q from 17 rows), restored to 0 afterwards."""
+    _lib.call("tw_gemv_set_variant", request.param)
+    yield request.param
+    _lib.call("tw_gemv_set_variant", 0)
+
+
 @pytest.mark.parametrize("a_packed", [1, 0])
 @pytest.mark.parametrize("M,N,K,epi,splits", GEMV_CASES)
-def test_gemv_packed_vs_torch(M, N, K, epi, splits, a_packed):
-    """tw_gemv_packed vs torch fp32: the layer GEMVs as column-group pairs (k_gemv_pc), the vocabulary-wide proj_out
-    and the F32 / RESID epilogues as k_gemv_p."""
+def test_gemv_packed_vs_torch(M, N, K, epi, splits, a_packed, gemv_variant):
+    """tw_gemv_packed vs torch fp32: the layer GEMVs as column-group pairs (k_gemv_pc) or one column group per wave
+    (k_gemv_q), the vocabulary-wide proj_out and the F32 / RESID epilogues as k_gemv_p."""
     A = rand_bf16(M, K, seed=41)
     W = rand_bf16(N, K, scale=K ** -0.5, seed=42)
     bias = torch.randn(N, device=DEV) * 0.1

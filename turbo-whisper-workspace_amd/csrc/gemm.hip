@@ -1222,7 +1222,8 @@ static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
   }
   if constexpr (EPI == TW_EPI_BF16 || EPI == TW_EPI_PARTIAL || EPI == TW_EPI_GELU_PACKED) {
     // the layer GEMVs as column-group pairs (k_gemv_pc): a third fewer vector-memory instructions per weight byte
-    if (tw_gemv_kernel == 1 && launch_gemv_q<EPI, APACK>(A, lda, Wp, M, N, K, ea, splits, s)) return;
+    // (k_gemv_q from 17 rows: at <= 16 one m-tile leaves its waves too little work, step 328 vs 323 us at 15 rows)
+    if (tw_gemv_kernel == 1 && M > 16 && launch_gemv_q<EPI, APACK>(A, lda, Wp, M, N, K, ea, splits, s)) return;
     const long pairs = tw_cdiv(tw_cdiv(N, 16), 2) * (long)splits;
     if (pairs * 2 < 1024 && steps >= 8 * 4) launch_gemv_pc<EPI, 4, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
     else launch_gemv_pc<EPI, 2, APACK>(A, lda, Wp, M, N, K, ea, splits, s);

@@ -21,6 +21,7 @@ from host tensors. Messages are tiny (1 h of audio = 120 windows x 450 x 4 B = 2
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -39,6 +40,20 @@ def world() -> Tuple[int, int]:
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     return 0, 1
+
+
+# force_collective: run the collectives even in a world of one (an nccl = RCCL group of size 1 exercises the device-
+# tensor all-gather / broadcast on a one-GPU box; the results must equal the host path's). TW_FORCE_COLLECTIVE=1 sets
+# the default for every call.
+FORCE_COLLECTIVE = os.environ.get("TW_FORCE_COLLECTIVE", "0") == "1"
+
+
+def collective_path(force_collective: Optional[bool] = None) -> bool:
+    """Whether the sharded path (broadcast, shard, all-gather) runs: more than one rank, or forced in an initialised
+    world of one."""
+    _, ws = world()
+    forced = FORCE_COLLECTIVE if force_collective is None else bool(force_collective)
+    return ws > 1 or (forced and dist.is_available() and dist.is_initialized())
 
 
 def shard_range(n: int, world_size: int, rank: int) -> Tuple[int, int]:
@@ -94,16 +109,16 @@ def unpack_tokens(arr: np.ndarray, n: int) -> Tuple[List[List[int]], List[Option
 
 
 def gather_tokens(local_seqs: Sequence[Sequence[int]], local_langs: Optional[Sequence[Optional[int]]], n_total: int,
-                  device: Optional[torch.device] = None, group=None,
-                  width: Optional[int] = None) -> Tuple[List[List[int]], List[Optional[int]]]:
+                  device: Optional[torch.device] = None, group=None, width: Optional[int] = None,
+                  force_collective: Optional[bool] = None) -> Tuple[List[List[int]], List[Optional[int]]]:
     """All-gather every rank's window results; returns all n_total windows in global order (on every rank).
 
     `device`: where the collective's buffers live (a cuda device for RCCL, cpu for gloo; default: cuda when
     the default backend is nccl). `width`: a minimum number of token columns per row; the columns used are the max
     over ranks of it and of the longest local sequence, agreed with one MAX all-reduce that also reports a
-    shard-size mismatch, so no rank is left waiting in the gather."""
+    shard-size mismatch, so no rank is left waiting in the gather. force_collective: see FORCE_COLLECTIVE."""
     rank, ws = world()
-    if ws == 1:
+    if not collective_path(force_collective):
         return [list(s) for s in local_seqs], list(local_langs) if local_langs is not None else [None] * len(
             local_seqs)
     sizes = shard_sizes(n_total, ws)
@@ -132,14 +147,15 @@ def gather_tokens(local_seqs: Sequence[Sequence[int]], local_langs: Optional[Seq
 
 
 def broadcast_waveform(wav: Optional[np.ndarray], device: Optional[torch.device] = None, src: int = 0,
-                       group=None, failed: bool = False, as_tensor: bool = False):
+                       group=None, failed: bool = False, as_tensor: bool = False,
+                       force_collective: Optional[bool] = None):
     """Rank `src` holds the decoded 16 kHz waveform; every rank returns a copy (length first, then samples):
     a host array, or with as_tensor the collective's own buffer (device memory under RCCL: no host round trip).
 
     `failed` (meaningful on `src`): decoding the input raised there. The length slot then carries -1: `src` gets
     None back (and re-raises its own error), every other rank raises PeerError, so no rank waits for samples."""
     rank, ws = world()
-    if ws == 1:
+    if not collective_path(force_collective):
         return wav
     device = _coll_device(device, group)
     n = torch.tensor([-1 if (rank == src and failed) else (0 if wav is None else len(wav))], dtype=torch.int64,
@@ -157,7 +173,7 @@ def broadcast_waveform(wav: Optional[np.ndarray], device: Optional[torch.device]
 
 
 def transcribe_sharded(run_windows, wav: np.ndarray, windows: Sequence, device: Optional[torch.device] = None,
-                       group=None, timed: bool = False) -> List:
+                       group=None, timed: bool = False, force_collective: Optional[bool] = None) -> List:
     """Every rank calls this with the same `windows` (chunk_iter windows over `wav`); each rank runs
     `run_windows(wav, windows[lo:hi]) -> List[List[int]]` on its own shard, then the results are all-gathered
     into the global window order. `timed`: run_windows returns (tokens, per-token times) pairs (word
@@ -181,11 +197,13 @@ def transcribe_sharded(run_windows, wav: np.ndarray, windows: Sequence, device: 
         if err is not None:
             raise err
         raise PeerError("transcription failed on another rank")
-    seqs, _ = gather_tokens(toks, None, len(windows), device=device, group=group, width=width)
+    seqs, _ = gather_tokens(toks, None, len(windows), device=device, group=group, width=width,
+                            force_collective=force_collective)
     if not timed:
         return seqs
     # word timestamps: (tokens, per-token float32 times); the times travel as their int32 bit patterns
-    tsb, _ = gather_tokens(bits, None, len(windows), device=device, group=group, width=width)
+    tsb, _ = gather_tokens(bits, None, len(windows), device=device, group=group, width=width,
+                           force_collective=force_collective)
     return [(s, np.asarray(b, dtype=np.int32).view(np.float32).tolist()) for s, b in zip(seqs, tsb)]
 
 

@@ -264,7 +264,7 @@ class WhisperEngine:
         # prefix; while _masked, the self-attention masks those positions (tw_attn_decode_self_masked)
         self._kv_start = torch.zeros(self.max_rows, dtype=torch.int32, device=dev)
         self._masked = False
-        self._wide_kw = 1  # the library's tw_gemv_set_wide_slices state (its default)
+        self._dec_ctx = (1, 0)  # the library's (tw_gemv_set_wide_slices, tw_gemv_set_variant) state (its defaults)
         self._beam: Optional[dict] = None  # beam-search buffers, allocated on first use
         self._align: Optional[dict] = None  # token-level timestamps: alignment-head attention recording
         self._align_buf: Optional[torch.Tensor] = None
@@ -806,14 +806,29 @@ class WhisperEngine:
     # (the same beside an encoder chunk: 1; TW_DEC_BESIDE_WIDE_KW for A/B)
     dec_beside_wide_kw = int(os.environ.get("TW_DEC_BESIDE_WIDE_KW", "1"))
 
-    def _dec_context(self) -> int:
-        """Set the proj_out K-slice count for a pass starting now: alone unless run_batches' encoder pump is queued
-        beside it. Graph keys carry the returned value (a captured step bakes the launch it recorded)."""
-        kw = self.dec_beside_wide_kw if self._pump is not None else self.dec_alone_wide_kw
-        if kw != self._wide_kw:
-            _lib.call("tw_gemv_set_wide_slices", kw)
-            self._wide_kw = kw
-        return kw
+    # The layer GEMVs' kernel (tw_gemv_set_variant) for a decode pass alone: k_gemv_q (1: one column group per wave, the
+    # whole K-slice in flight; the library keeps k_gemv_pc at <= 16 rows) — captured step 393.5 -> 384.8 us at 24 rows,
+    # 682.6 -> 651.1 at 64 (profiles/r05i_decode_chain.txt); beside an encoder chunk k_gemv_pc (0): 87.86 vs 88.45 ms
+    # per bench step (two interleaved pairs, profiles/r05i_gemv_ab.txt). TW_DEC_ALONE_GEMV / _BESIDE_GEMV for A/B.
+    dec_alone_gemv = int(os.environ.get("TW_DEC_ALONE_GEMV", "1"))
+    dec_beside_gemv = int(os.environ.get("TW_DEC_BESIDE_GEMV", "0"))
+
+    @property
+    def _wide_kw(self) -> int:
+        return self._dec_ctx[0]
+
+    def _dec_context(self) -> tuple:
+        """Set the decoder-step kernel choices for a pass starting now (the proj_out K-slice count and the layer GEMV
+        kernel): alone unless run_batches' encoder pump is queued beside it. Graph keys carry the returned value (a
+        captured step bakes the launches it recorded)."""
+        beside = self._pump is not None
+        ctx = ((self.dec_beside_wide_kw, self.dec_beside_gemv) if beside
+               else (self.dec_alone_wide_kw, self.dec_alone_gemv))
+        if ctx != self._dec_ctx:
+            _lib.call("tw_gemv_set_wide_slices", ctx[0])
+            _lib.call("tw_gemv_set_variant", ctx[1])
+            self._dec_ctx = ctx
+        return ctx
 
     def _prompt_len(self, tail: Sequence[int], prefix=None) -> int:
         """decoder_input_ids' length: [prefix] + SOT (+ language) + tail (num_input_ids of the token timestamps)."""
@@ -933,7 +948,7 @@ class WhisperEngine:
         if self.use_graphs and self.prompt_graph and (detect or not st.is_multilingual) and not base:
             al = self._align  # (keyed like _graph_for: an alignment pass captures the probability-recording kernel)
             key = ("prompt", R, tuple(int(t) for t in tail), max_new, use_timestamps, self._slot,
-                   None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()), self._wide_kw)
+                   None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()), self._dec_ctx)
             g = self._graphs.get(key)
             if g is None:
                 g = torch.cuda.CUDAGraph()
@@ -1005,10 +1020,19 @@ class WhisperEngine:
                         elif not pump():
                             inflight.pop(0).synchronize()
             steps += n
-            for c in chains:
-                self.stream.wait_stream(c.stream)
-            if bool(self.state[:R, _lib.TW_ST_FINISHED].all().item()):
+            # the finished check on the chains' own stream: a wait of the engine stream on the chain stream here, with
+            # the steps still queued, slowed every queued step by ~50 us (438 vs 389 us at 24 rows,
+            # scripts/decode_chain_costs.py --passlike); the engine stream joins once the host has synchronised
+            cs = chains[0].stream
+            for c in chains[1:]:
+                if c.stream is not cs:
+                    cs.wait_stream(c.stream)
+            with torch.cuda.stream(cs):
+                done_all = bool(self.state[:R, _lib.TW_ST_FINISHED].all().item())
+            if done_all:
                 break
+        for c in chains:
+            self.stream.wait_stream(c.stream)
         if ev0 is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record(self.stream)
@@ -1268,7 +1292,7 @@ class WhisperEngine:
                 al = self._align
                 key = ("beam", R, nb, max_new, bool(use_timestamps), float(length_penalty), self._slot, r_enc,
                        self._masked, None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()),
-                       bool(criteria), self._wide_kw)
+                       bool(criteria), self._dec_ctx)
                 g = self._graphs.get(key)
                 if g is None:
                     g = torch.cuda.CUDAGraph()
@@ -1325,7 +1349,7 @@ class WhisperEngine:
         """The captured decode step of chain i (n_steps > 1: that many steps back to back in one graph)."""
         al = self._align
         key = (R, params.max_new, params.use_timestamps, self._slot, i, fused,
-               None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()), self._masked, self._wide_kw,
+               None if al is None else (al["pos0"], al["n_steps"], al["buf"].data_ptr()), self._masked, self._dec_ctx,
                n_steps)
         g = self._graphs.get(key)
         if g is not None:

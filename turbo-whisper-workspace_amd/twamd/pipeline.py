@@ -152,6 +152,7 @@ class TurboTranscriber:
             raise ValueError("Cannot specify `task` or `language` for an English-only model.")
 
         rank, world = dist.world()
+        sharded = dist.collective_path()  # (world > 1, or a forced collective in a world of one)
         dev = getattr(self.engine, "device", None)
         wav, load_err = None, None
         if rank == 0:
@@ -159,7 +160,7 @@ class TurboTranscriber:
                 wav = audio.load_input(inputs, self.sampling_rate, dev)
             except Exception as e:  # raised below, after the other ranks have been told (no rank left waiting)
                 load_err = e
-        if world > 1:  # SPMD: every rank calls with the same arguments; rank 0 decoded the input
+        if sharded:  # SPMD: every rank calls with the same arguments; rank 0 decoded the input
             # (the waveform stays in device memory: each rank copies its windows out of it on the GPU)
             wav = dist.broadcast_waveform(wav, failed=load_err is not None, as_tensor=True)
         if load_err is not None:
@@ -199,7 +200,7 @@ class TurboTranscriber:
             return self.transcribe_windows(w, ws, **kw)
 
         # one window shard per rank + one all-gather of the token arrays (twamd.dist); plain call on 1 GPU
-        outputs = dist.transcribe_sharded(run, wav, windows, timed=word) if world > 1 else run(wav, windows)
+        outputs = dist.transcribe_sharded(run, wav, windows, timed=word) if sharded else run(wav, windows)
         model_outputs = []
         for w, toks in zip(windows, outputs):
             if word:

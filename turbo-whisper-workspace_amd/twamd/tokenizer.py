@@ -287,27 +287,49 @@ def collate_word_timestamps(vocab: "WhisperVocab", tokens: List[int], token_time
             for w, ix in zip(words, idx)]
 
 
-def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps, return_language: bool = False,
-               time_precision: float = 0.02, segment_size: int = 1500) -> Tuple[str, dict]:
-    """outputs: [{"tokens": [ids...], "stride": (chunk_len_s, left_s, right_s) optional,
-    "token_timestamps": [s...] (return_timestamps="word")}, ...] in chunk order."""
-    word = return_timestamps == "word"
-    st = vocab.special
-    last_language = None
+class AsrStitcher:
+    """`_decode_asr` as a resumable state machine: feed() the pipeline's model outputs in window order, finish() for
+    (text, optional). Everything carried from one window to the next is `state()` — the open chunk, the token runs
+    still waiting for their closing timestamp (and their word times), the skip flag, the last language and the time
+    offset — so a shard of windows can be stitched from a given incoming state and its closed chunks concatenated
+    with the other shards' (twamd.dist.stitch_sharded)."""
 
-    def new_chunk():
-        return {"language": last_language, "timestamp": [None, None], "text": ""}
+    def __init__(self, vocab: WhisperVocab, return_timestamps, return_language: bool = False,
+                 time_precision: float = 0.02, segment_size: int = 1500, state: Optional[dict] = None):
+        self.vocab, self.return_timestamps, self.return_language = vocab, return_timestamps, return_language
+        self.time_precision, self.segment_size = time_precision, segment_size
+        self.word = return_timestamps == "word"
+        self.chunks: List[dict] = []  # closed chunks, in order
+        st = state or self.initial_state()
+        self.chunk = {"language": st["chunk"]["language"], "timestamp": list(st["chunk"]["timestamp"]),
+                      "text": st["chunk"]["text"]}
+        self.previous_tokens = [list(t) for t in st["previous_tokens"]]
+        self.previous_token_timestamps = [list(t) for t in st["previous_token_timestamps"]]
+        self.skip, self.last_language, self.time_offset = st["skip"], st["last_language"], st["time_offset"]
 
-    chunks = []
-    chunk = new_chunk()
-    time_offset = 0.0
-    timestamp_begin = st.timestamp_begin
-    previous_tokens: List[List[int]] = []
-    previous_token_timestamps: list = []
-    skip = False
-    right_stride_start = None
-    special_ids = vocab.all_special_ids
-    for output in outputs:
+    @staticmethod
+    def initial_state(last_language: Optional[str] = None, time_offset: float = 0.0) -> dict:
+        """A clean state: no open chunk, nothing pending (what decode_asr starts from, and what holds after every
+        window whose last segment closed)."""
+        return {"chunk": {"language": last_language, "timestamp": [None, None], "text": ""}, "previous_tokens": [],
+                "previous_token_timestamps": [], "skip": False, "last_language": last_language,
+                "time_offset": time_offset}
+
+    def state(self) -> dict:
+        return {"chunk": {"language": self.chunk["language"], "timestamp": list(self.chunk["timestamp"]),
+                          "text": self.chunk["text"]},
+                "previous_tokens": [list(t) for t in self.previous_tokens],
+                "previous_token_timestamps": [[tuple(x) for x in t] for t in self.previous_token_timestamps],
+                "skip": self.skip, "last_language": self.last_language, "time_offset": self.time_offset}
+
+    def _new_chunk(self) -> dict:
+        return {"language": self.last_language, "timestamp": [None, None], "text": ""}
+
+    def feed(self, output: dict) -> None:
+        vocab, st, word = self.vocab, self.vocab.special, self.word
+        time_precision, segment_size = self.time_precision, self.segment_size
+        timestamp_begin = st.timestamp_begin
+        special_ids = vocab.all_special_ids
         token_ids = list(output["tokens"])
         # _strip_prompt: a leading <|startofprev|> prompt is cut up to <|startoftranscript|>
         if token_ids and token_ids[0] == st.startofprev:
@@ -320,7 +342,7 @@ def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps, 
         penultimate_timestamp = 0.0
         if "stride" in output:
             chunk_len, stride_left, stride_right = output["stride"]
-            time_offset -= stride_left
+            self.time_offset -= stride_left
             right_stride_start = chunk_len - stride_right
             if stride_left:
                 first_timestamp = stride_left / time_precision + timestamp_begin
@@ -332,21 +354,22 @@ def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps, 
                         last_timestamp = token
         current_tokens: List[int] = []
         current_token_timestamps: list = []
+        chunk = self.chunk
         for i, token in enumerate(token_ids):
             if token in special_ids:
                 text = vocab.id_to_token[token][2:-2]
                 language = LANGUAGE_NAMES.get(text)
                 if language is not None:
-                    if last_language and language != last_language and not return_timestamps:
-                        previous_tokens.append(current_tokens)
-                        resolved = find_longest_common_sequence(previous_tokens)
+                    if self.last_language and language != self.last_language and not self.return_timestamps:
+                        self.previous_tokens.append(current_tokens)
+                        resolved = find_longest_common_sequence(self.previous_tokens)
                         chunk["text"] = vocab.decode(resolved)
-                        chunks.append(chunk)
-                        previous_tokens = []
+                        self.chunks.append(chunk)
+                        self.previous_tokens = []
                         current_tokens = []
-                        chunk = new_chunk()
+                        chunk = self._new_chunk()
                     chunk["language"] = language
-                    last_language = language
+                    self.last_language = language
             elif token >= timestamp_begin:
                 timestamp = float((token - timestamp_begin) * time_precision)
                 if timestamp < cur_max_timestamp:
@@ -359,12 +382,12 @@ def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps, 
                         prev_segments_len += penultimate_timestamp
                 penultimate_timestamp = cur_max_timestamp
                 cur_max_timestamp = timestamp
-                time = (token - timestamp_begin) * time_precision + time_offset + prev_segments_len
+                time = (token - timestamp_begin) * time_precision + self.time_offset + prev_segments_len
                 time = round(time, 2)
                 if last_timestamp and token >= last_timestamp:
-                    skip = True
-                elif skip or (previous_tokens and token < first_timestamp):
-                    skip = False
+                    self.skip = True
+                elif self.skip or (self.previous_tokens and token < first_timestamp):
+                    self.skip = False
                 elif chunk["timestamp"][0] is None:
                     chunk["timestamp"][0] = time
                 else:
@@ -372,43 +395,55 @@ def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps, 
                         pass
                     else:
                         chunk["timestamp"][1] = time
-                        previous_tokens.append(current_tokens)
+                        self.previous_tokens.append(current_tokens)
                         if word:
-                            previous_token_timestamps.append(current_token_timestamps)
-                        resolved, resolved_ts = find_longest_common_sequence(previous_tokens, previous_token_timestamps)
+                            self.previous_token_timestamps.append(current_token_timestamps)
+                        resolved, resolved_ts = find_longest_common_sequence(self.previous_tokens,
+                                                                             self.previous_token_timestamps)
                         chunk["text"] = vocab.decode(resolved)
                         if word:
-                            chunk["words"] = collate_word_timestamps(vocab, resolved, resolved_ts, last_language,
-                                                                     return_language)
-                        chunks.append(chunk)
-                        previous_tokens = []
+                            chunk["words"] = collate_word_timestamps(vocab, resolved, resolved_ts, self.last_language,
+                                                                     self.return_language)
+                        self.chunks.append(chunk)
+                        self.previous_tokens = []
                         current_tokens = []
-                        previous_token_timestamps = []
+                        self.previous_token_timestamps = []
                         current_token_timestamps = []
-                        chunk = new_chunk()
+                        chunk = self._new_chunk()
             else:
                 current_tokens.append(token)
                 if word:
-                    start = round(0.0 + time_offset, 2) if i == 0 else round(token_timestamps[i - 1] + time_offset, 2)
-                    current_token_timestamps.append((start, round(token_timestamps[i] + time_offset, 2)))
+                    start = (round(0.0 + self.time_offset, 2) if i == 0
+                             else round(token_timestamps[i - 1] + self.time_offset, 2))
+                    current_token_timestamps.append((start, round(token_timestamps[i] + self.time_offset, 2)))
         if "stride" in output:
-            time_offset += chunk_len - stride_right
+            self.time_offset += chunk_len - stride_right
         if current_tokens:
-            previous_tokens.append(current_tokens)
+            self.previous_tokens.append(current_tokens)
             if word:
-                previous_token_timestamps.append(current_token_timestamps)
-        elif not any(p for p in previous_tokens):
-            chunk = new_chunk()
-            previous_tokens = []
-            current_tokens = []
-            previous_token_timestamps = []
-            current_token_timestamps = []
-    if previous_tokens:
-        resolved, resolved_ts = find_longest_common_sequence(previous_tokens, previous_token_timestamps)
-        chunk["text"] = vocab.decode(resolved)
-        if word:
-            chunk["words"] = collate_word_timestamps(vocab, resolved, resolved_ts, last_language, return_language)
-        chunks.append(chunk)
+                self.previous_token_timestamps.append(current_token_timestamps)
+        elif not any(p for p in self.previous_tokens):
+            chunk = self._new_chunk()
+            self.previous_tokens = []
+            self.previous_token_timestamps = []
+        self.chunk = chunk
+
+    def finish(self) -> Tuple[str, dict]:
+        chunks = list(self.chunks)
+        if self.previous_tokens:
+            chunk = self.chunk
+            resolved, resolved_ts = find_longest_common_sequence(self.previous_tokens, self.previous_token_timestamps)
+            chunk["text"] = self.vocab.decode(resolved)
+            if self.word:
+                chunk["words"] = collate_word_timestamps(self.vocab, resolved, resolved_ts, self.last_language,
+                                                         self.return_language)
+            chunks.append(chunk)
+        return assemble_asr(chunks, self.return_timestamps, self.return_language)
+
+
+def assemble_asr(chunks: List[dict], return_timestamps, return_language: bool) -> Tuple[str, dict]:
+    """The tail of _decode_asr: the full text and the optional chunk / word list from the closed chunks."""
+    word = return_timestamps == "word"
     full_text = "".join(c["text"] for c in chunks)
     if return_timestamps or return_language:
         for c in chunks:
@@ -425,3 +460,13 @@ def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps, 
     else:
         optional = {}
     return full_text, optional
+
+
+def decode_asr(vocab: WhisperVocab, outputs: Sequence[dict], return_timestamps, return_language: bool = False,
+               time_precision: float = 0.02, segment_size: int = 1500) -> Tuple[str, dict]:
+    """outputs: [{"tokens": [ids...], "stride": (chunk_len_s, left_s, right_s) optional,
+    "token_timestamps": [s...] (return_timestamps="word")}, ...] in chunk order."""
+    stitcher = AsrStitcher(vocab, return_timestamps, return_language, time_precision, segment_size)
+    for output in outputs:
+        stitcher.feed(output)
+    return stitcher.finish()
