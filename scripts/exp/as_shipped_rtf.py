@@ -18,8 +18,10 @@ from twamd.synth_audio import speech_like  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--minutes", type=float, default=10.0)
+ap.add_argument("--model", default="large-v3-turbo", help="large-v3: the reference's own default model "
+                "(vocalis/core/audio_pipeline.py:171), the turbo encoder with a 32-layer decoder")
 a = ap.parse_args()
-tr = TurboTranscriber.from_pretrained("large-v3-turbo", seed=1234)
+tr = TurboTranscriber.from_pretrained(a.model, seed=1234)
 audio = np.concatenate([speech_like(60.0, 500 + i) for i in range(int(a.minutes))]).astype(np.float32)
 kw = dict(chunk_length_s=60, stride_length_s=5, batch_size=32, return_timestamps=True)
 out = {}
@@ -32,4 +34,4 @@ for name, gk in (("as_shipped_beam5", {"task": "transcribe"}), ("greedy", {"task
     dt = time.perf_counter() - t0
     out[name] = {"wall_s": round(dt, 3), "rtf": round(len(audio) / 16000 / dt, 1), "chunks": len(r["chunks"])}
     print(name, out[name], flush=True)
-print(json.dumps({"audio_s": len(audio) / 16000, "windows_60_5": len(tr.last_window_passes), **out}))
+print(json.dumps({"model": a.model, "audio_s": len(audio) / 16000, "windows_60_5": len(tr.last_window_passes), **out}))

@@ -246,3 +246,60 @@ def test_lcs_vectorised_scan_equals_sequential_scan():
         if len(seqs[0]) > 4 and rng.random() < 0.5:
             seqs[1] = seqs[0][-int(rng.integers(1, len(seqs[0]))):] + seqs[1]
         assert find_longest_common_sequence(seqs) == scan(seqs), seqs
+
+
+def _sharded_stitch(vocab, outs, n_shards, **kw):
+    """twamd.dist.stitch_sharded without a process group: every shard's piece computed here, then the merge."""
+    from twamd import dist as twd
+    bounds = [twd.shard_range(len(outs), n_shards, r) for r in range(n_shards)]
+    pieces = [twd.shard_piece(vocab, outs, lo, hi, **kw) for lo, hi in bounds]
+    return twd.merge_pieces(vocab, outs, pieces, bounds, **kw)
+
+
+def test_sharded_stitching_equals_decode_asr_on_transformers_cases():
+    """_decode_asr split over ranks (each stitches its window shard from the state it expects, the
+    pieces merged) equals the serial stitching — and so transformers — on every decode_asr.json case, every shard
+    count."""
+    cases = json.load(open(os.path.join(G, "decode_asr.json")))
+    vocab = WhisperVocab.synthetic(SpecialTokens.for_vocab(51866))
+    for c in cases:
+        outs = [{"tokens": o["tokens"], "stride": tuple(o["stride"])} for o in c["outputs"]]
+        kw = dict(return_timestamps=c["return_timestamps"], return_language=c["return_language"])
+        for n in range(1, len(outs) + 2):
+            text, opt = _sharded_stitch(vocab, outs, n, **kw)
+            assert text == c["text"]
+            assert json.loads(json.dumps(opt)) == c["optional"]
+
+
+@given(data=hs.data())
+@settings(max_examples=300, deadline=None)
+def test_sharded_stitching_equals_serial_random_windows(data):
+    """Random window token streams (text, timestamps in and out of order, open segments across windows, language
+    switches, strides) and random shard counts: the merged pieces equal the serial decode_asr."""
+    st = SpecialTokens.for_vocab(51866)
+    vocab = WhisperVocab.synthetic(st)
+    langs = [st.lang_begin, st.lang_begin + 1, st.lang_begin + 7]
+    n_win = data.draw(hs.integers(1, 9))
+    stride = data.draw(hs.sampled_from([(30.0, 0.0, 0.0), (30.0, 5.0, 5.0), (20.0, 2.5, 0.0)]))
+    outs = []
+    for w in range(n_win):
+        toks = []
+        if data.draw(hs.booleans()):
+            toks += [st.sot, data.draw(hs.sampled_from(langs)), st.transcribe]
+        for _ in range(data.draw(hs.integers(0, 10))):
+            kind = data.draw(hs.integers(0, 2))
+            if kind == 0:
+                toks.append(data.draw(hs.integers(200, 240)))  # text (repeats: LCS overlaps)
+            elif kind == 1:
+                toks.append(st.timestamp_begin + data.draw(hs.integers(0, 1500)))
+            else:
+                toks.append(data.draw(hs.sampled_from(langs)))
+        left = 0.0 if w == 0 else stride[1]
+        right = 0.0 if w == n_win - 1 else stride[2]
+        tts = sorted(data.draw(hs.lists(hs.floats(0, 30, allow_nan=False), min_size=len(toks), max_size=len(toks))))
+        outs.append({"tokens": toks, "stride": (stride[0], left, right), "token_timestamps": tts})
+    rt = data.draw(hs.sampled_from([True, False, "word"]))
+    rl = data.draw(hs.booleans())
+    want = decode_asr(vocab, outs, return_timestamps=rt, return_language=rl)
+    for n in range(1, n_win + 1):
+        assert _sharded_stitch(vocab, outs, n, return_timestamps=rt, return_language=rl) == want

@@ -207,6 +207,102 @@ def transcribe_sharded(run_windows, wav: np.ndarray, windows: Sequence, device: 
     return [(s, np.asarray(b, dtype=np.int32).view(np.float32).tolist()) for s, b in zip(seqs, tsb)]
 
 
+# ---- sharded _decode_asr -------------------------------------------------------------------------------------------
+# $TF/models/whisper/tokenization_whisper.py:901-1150 walks the windows in order and carries a state from one window
+# to the next (twamd.tokenizer.AsrStitcher.state). Each rank stitches its own shard of windows from the state it
+# expects to come in — clean (every segment closed), with the exact last language and time offset of the windows
+# before it, both computable from those windows' tokens and strides alone — and the closed chunks of all shards are
+# gathered. The merge walks the shards in order: where a shard's assumed incoming state is the previous shard's
+# final state, its chunks are taken as they are; otherwise (a segment left open across the shard boundary) that
+# shard is stitched again from the true state. The result equals the serial _decode_asr by construction.
+
+def _language_of(vocab, tokens) -> Optional[str]:
+    """The last language token's name in one window's tokens (as AsrStitcher.feed reads them), or None."""
+    from .tokenizer import LANGUAGE_NAMES
+    st = vocab.special
+    ids = list(tokens)
+    if ids and ids[0] == st.startofprev:
+        ids = ids[ids.index(st.sot):] if st.sot in ids else []
+    special = vocab.all_special_ids
+    for t in reversed(ids):
+        if t in special:
+            lang = LANGUAGE_NAMES.get(vocab.id_to_token[t][2:-2])
+            if lang is not None:
+                return lang
+    return None
+
+
+def assumed_state(vocab, outputs: Sequence[dict], lo: int) -> dict:
+    """The incoming state a shard starting at window `lo` assumes: clean, last language and time offset exact."""
+    from .tokenizer import AsrStitcher
+    lang = None
+    for o in reversed(outputs[:lo]):
+        lang = _language_of(vocab, o["tokens"])
+        if lang is not None:
+            break
+    t = 0.0
+    for o in outputs[:lo]:  # the same float operations, in the same order, as AsrStitcher.feed
+        if "stride" in o:
+            chunk_len, stride_left, stride_right = o["stride"]
+            t -= stride_left
+            t += chunk_len - stride_right
+    return AsrStitcher.initial_state(lang, t)
+
+
+def shard_piece(vocab, outputs: Sequence[dict], lo: int, hi: int, **kw) -> tuple:
+    """One shard's stitching: (assumed incoming state, its closed chunks, its final state)."""
+    from .tokenizer import AsrStitcher
+    st0 = assumed_state(vocab, outputs, lo)
+    sti = AsrStitcher(vocab, state=st0, **kw)
+    for o in outputs[lo:hi]:
+        sti.feed(o)
+    return st0, sti.chunks, sti.state()
+
+
+def merge_pieces(vocab, outputs: Sequence[dict], pieces: Sequence[tuple], bounds: Sequence[Tuple[int, int]],
+                 **kw) -> Tuple[str, dict]:
+    """The serial _decode_asr result from the shards' pieces (see above); returns (text, optional)."""
+    from .tokenizer import AsrStitcher
+    chunks: List[dict] = []
+    true = AsrStitcher.initial_state()
+    restitched = 0
+    for (assumed, ch, final), (lo, hi) in zip(pieces, bounds):
+        if assumed == true:
+            chunks.extend(ch)
+            true = final
+        else:  # a segment open across the boundary (or a skip in flight): this shard again, from the true state
+            sti = AsrStitcher(vocab, state=true, **kw)
+            for o in outputs[lo:hi]:
+                sti.feed(o)
+            chunks.extend(sti.chunks)
+            true = sti.state()
+            restitched += 1
+    end = AsrStitcher(vocab, state=true, **kw)
+    end.chunks = chunks
+    merge_pieces.last_restitched = restitched
+    return end.finish()
+
+
+merge_pieces.last_restitched = 0
+
+
+def stitch_sharded(vocab, outputs: Sequence[dict], group=None, force_collective: Optional[bool] = None,
+                   **kw) -> Tuple[str, dict]:
+    """decode_asr over every window (`outputs` in global order, identical on every rank), with the work split over
+    the ranks: each stitches its own window shard, one all_gather_object brings the pieces to every rank, and every
+    rank merges them (merge_pieces). kw: decode_asr's return_timestamps, return_language, time_precision,
+    segment_size."""
+    from .tokenizer import decode_asr
+    rank, ws = world()
+    if not collective_path(force_collective):
+        return decode_asr(vocab, outputs, **kw)
+    bounds = [shard_range(len(outputs), ws, r) for r in range(ws)]
+    piece = shard_piece(vocab, outputs, *bounds[rank], **kw)
+    pieces: List = [None] * ws
+    dist.all_gather_object(pieces, piece, group=group)
+    return merge_pieces(vocab, outputs, pieces, bounds, **kw)
+
+
 class RankZeroFrontend:
     """Serving on N GPUs: rank 0 owns the request surface (AudioProcessingPipeline / POST /api/transcribe) and
     calls this like the single-GPU callable; the other ranks sit in `follow()`. Each call broadcasts the call's

@@ -37,20 +37,43 @@ LN_EPS = 1e-5
 S_ENC = 1500
 
 
+# Python's cyclic GC held off while a graph records (defence in depth): a collection inside a capture that finds an
+# unreachable engine in a reference cycle runs its graphs' / events' finalizers (HIP destroys, illegal while a stream
+# captures), which aborted a full GPU suite run in r04ae. The cause is gone — engines hold no reference cycles (the
+# encoder pump is dropped in run_batches' finally, step hooks are reset by their setters) and WhisperEngine.close()
+# releases graphs, events and buffers in order — and tests/test_gpu_capture.py captures with the guard off
+# (CAPTURE_GC_GUARD = False) after dropping an engine, with a collection forced inside the capture.
+CAPTURE_GC_GUARD = True
+
+
 @contextlib.contextmanager
 def _capture(g: "torch.cuda.CUDAGraph", stream):
-    """torch.cuda.graph with Python's cyclic GC held off while the graph records: a collection inside the capture runs
-    finalizers of earlier engines' graphs / events / buffers (HIP frees and destroys, illegal while a stream captures),
-    which aborted a full GPU suite run (r04ae)."""
+    """torch.cuda.graph, with the cyclic GC held off while the graph records when CAPTURE_GC_GUARD is set."""
+    guard = CAPTURE_GC_GUARD
     was = gc.isenabled()
-    gc.collect()
-    gc.disable()
+    if guard:
+        gc.collect()
+        gc.disable()
     try:
         with torch.cuda.graph(g, stream=stream):
             yield
     finally:
-        if was:
+        if guard and was:
             gc.enable()
+
+
+# how the decode loop waits for a queued step: polling the event (default) or a blocking event synchronize, whose
+# wake-up latency depends on the runtime's scheduling mode (a process that has an RCCL communicator up paid ~10 ms per
+# bench step with the blocking wait: profiles/r05l_*). TW_WAIT=sync for A/B.
+_WAIT_POLL = os.environ.get("TW_WAIT", "poll") != "sync"
+
+
+def _wait(ev: "torch.cuda.Event") -> None:
+    if not _WAIT_POLL:
+        ev.synchronize()
+        return
+    while not ev.query():
+        time.sleep(0)  # (releases the GIL: the C4 diarizer thread keeps running)
 
 
 def _pad256(n: int) -> int:
@@ -68,6 +91,8 @@ def on_engine_streams(fn):
 
     @functools.wraps(fn)
     def wrapper(self, *args, **kwargs):
+        if self.closed:
+            raise RuntimeError("WhisperEngine is closed")
         cur = torch.cuda.current_stream(self.device)
         if cur.cuda_stream in self._own_streams:
             return fn(self, *args, **kwargs)
@@ -313,6 +338,40 @@ class WhisperEngine:
                           for L in weights.dec]
             self.emb_p = self._pack(weights.emb)
             torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------ lifetime
+    closed = False
+
+    def close(self) -> None:
+        """Release the engine's GPU state in order, deterministically (no finalizer left for the cyclic GC): wait for
+        its streams, destroy every captured graph (newest first), drop timers / events, the decode views and the
+        encoder pump, then the buffers and weights (back to torch's caching allocator). The engine is unusable
+        afterwards; a second close() is a no-op. Also the context-manager exit."""
+        if self.closed:
+            return
+        for st in [self.stream, self.enc_stream] + list(getattr(self, "_chain_streams", [])):
+            st.synchronize()
+        for key in reversed(list(self._graphs)):
+            self._graphs.pop(key).reset()
+        self._graphs.clear()
+        self._pump = None
+        self.step_hook = None
+        self.pass_events = None
+        self.timers = None
+        self._enc_ev = []
+        self._chain_cache.clear()
+        keep = {"d", "gen", "max_batch", "max_beams", "max_rows", "device", "closed", "_own_streams"}
+        for name in list(vars(self)):
+            if name not in keep and isinstance(getattr(self, name), (torch.Tensor, list, dict, tuple)):
+                setattr(self, name, None)
+        self.w = None
+        self.closed = True
+
+    def __enter__(self) -> "WhisperEngine":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
 
     def _quant_weight(self, W: torch.Tensor) -> tuple:
         """bf16 [N][K] -> (fp8 [N][K], e8m0 scales [K/128][Np][4], Np) in the MX layout of tw_gemm_mx."""
@@ -1018,7 +1077,7 @@ class WhisperEngine:
                         if inflight[0].query():
                             inflight.pop(0)
                         elif not pump():
-                            inflight.pop(0).synchronize()
+                            _wait(inflight.pop(0))
             steps += n
             # the finished check on the chains' own stream: a wait of the engine stream on the chain stream here, with
             # the steps still queued, slowed every queued step by ~50 us (438 vs 389 us at 24 rows,

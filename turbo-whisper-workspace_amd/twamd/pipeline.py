@@ -101,6 +101,18 @@ class TurboTranscriber:
         return TurboTranscriber(eng, vocab)
 
     # -------------------------------------------------------------- call
+    def close(self) -> None:
+        """Release the engine (WhisperEngine.close) and the pinned staging buffers; the callable is unusable after."""
+        self._staging = None
+        if self.engine is not None:
+            self.engine.close()
+
+    def __enter__(self) -> "TurboTranscriber":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
     def __call__(self, inputs: Union[str, bytes, np.ndarray, dict], *, chunk_length_s: float = 0,
                  stride_length_s=None, batch_size: int = 1, generate_kwargs: Optional[Dict[str, Any]] = None,
                  return_timestamps: Union[bool, str] = False, return_language: bool = False, **kwargs) -> dict:
@@ -212,9 +224,12 @@ class TurboTranscriber:
                 sr = self.sampling_rate
                 o["stride"] = (w.length / sr, w.stride_left / sr, w.stride_right / sr)
             model_outputs.append(o)
-        text, optional = decode_asr(self.vocab, model_outputs, return_timestamps="word" if word else bool(return_timestamps),
-                                    return_language=return_language,
-                                    time_precision=time_precision(self.engine.d.max_source_positions))
+        kw = dict(return_timestamps="word" if word else bool(return_timestamps), return_language=return_language,
+                  time_precision=time_precision(self.engine.d.max_source_positions))
+        # sharded: every rank stitches its own windows and the pieces are merged (dist.stitch_sharded: the serial
+        # _decode_asr result, without rank 0 walking every window of the call)
+        text, optional = (dist.stitch_sharded(self.vocab, model_outputs, **kw) if sharded else
+                          decode_asr(self.vocab, model_outputs, **kw))
         return {"text": text, **optional}
 
     def _lang_id(self, language: Optional[str]) -> Optional[int]:
