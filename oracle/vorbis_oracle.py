@@ -396,6 +396,9 @@ def floor1(f, books, br: Bits, n2: int):
         else:
             used.append(False)
             fy.append(pred)
+        # ffmpeg's vorbis decoder (the decoder ffmpeg_read runs, $TF/pipelines/audio_utils.py:9-45) clips every final
+        # post to 16 bits (av_clip_uint16); the specification leaves out-of-range posts of a malformed stream open
+        fy[i] = min(max(fy[i], 0), 65535)
     v = np.zeros(n2, np.int64)
     order = sorted(range(n), key=lambda i: X[i])
     lx, ly = 0, fy[order[0]] * f["mult"]

@@ -433,6 +433,10 @@ def test_fallback_keys_are_global_window_indices():
     assert len(keys) == 200 * 3 * 6
     with pytest.raises(ValueError):
         fallback_row_key(2 ** 21, 0, 0)
+    with pytest.raises(ValueError):  # a field past its width would alias another row's stream
+        fallback_row_key(0, 1024, 0)
+    with pytest.raises(ValueError):
+        fallback_row_key(0, 0, 16)
 
     seen = []
 

@@ -224,15 +224,36 @@ bool residual(Bits& b, int bs, int order, int32_t* out) {
   return true;
 }
 
+// Sample arithmetic wraps modulo 2^32 (unsigned), never signed-overflows: a valid stream's samples and predictions
+// fit their 32 bits, so the wrapped results are the exact ones, while a damaged upload (residuals far outside the
+// frame's bit depth) decodes to garbage that its CRC-16 then rejects — not to undefined behaviour (found by the
+// -fsanitize=undefined fuzz build, tests/test_codec_sanitize.py).
+static inline int32_t wrap_add(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+
+template <typename Acc>
+struct LpcAcc;
+template <>
+struct LpcAcc<int32_t> {  // the narrow path: exact for valid streams (see subframe()), modular otherwise
+  static inline uint32_t mul(int32_t c, int32_t x) { return (uint32_t)c * (uint32_t)x; }
+  static inline int32_t shifted(uint32_t acc, int shift) { return (int32_t)acc >> shift; }
+  using T = uint32_t;
+};
+template <>
+struct LpcAcc<int64_t> {  // |coef| < 2^15, |x| < 2^31: 32 terms stay far inside 64 bits
+  static inline int64_t mul(int32_t c, int32_t x) { return (int64_t)c * (int64_t)x; }
+  static inline int32_t shifted(int64_t acc, int shift) { return (int32_t)(acc >> shift); }
+  using T = int64_t;
+};
+
 template <int ORDER, typename Acc>
 void lpc_fixed_order(int32_t* out, int bs, const int32_t* coef, int shift) {
   int32_t c[ORDER];
   for (int j = 0; j < ORDER; j++) c[j] = coef[j];
   for (int i = ORDER; i < bs; i++) {
-    Acc acc = 0;
+    typename LpcAcc<Acc>::T acc = 0;
 #pragma GCC unroll 16
-    for (int j = 0; j < ORDER; j++) acc += (Acc)c[j] * (Acc)out[i - 1 - j];
-    out[i] += (int32_t)(acc >> shift);
+    for (int j = 0; j < ORDER; j++) acc += LpcAcc<Acc>::mul(c[j], out[i - 1 - j]);
+    out[i] = wrap_add(out[i], LpcAcc<Acc>::shifted(acc, shift));
   }
 }
 
@@ -251,7 +272,7 @@ bool lpc_dispatch(int32_t* out, int bs, const int32_t* coef, int order, int shif
       for (int i = order; i < bs; i++) {
         int64_t acc = 0;
         for (int j = 0; j < order; j++) acc += (int64_t)coef[j] * out[i - 1 - j];
-        out[i] += (int32_t)(acc >> shift);
+        out[i] = wrap_add(out[i], (int32_t)(acc >> shift));
       }
       return true;
   }
@@ -281,18 +302,19 @@ bool subframe(Bits& b, int bs, int bps, int32_t* out) {
     if (order > bs) return false;
     for (int i = 0; i < order; i++) out[i] = b.s(bps);
     if (!residual(b, bs, order, out)) return false;
-    switch (order) {  // fixed polynomial predictors
+    uint32_t* u = (uint32_t*)out;  // fixed polynomial predictors, modulo 2^32 (see wrap_add)
+    switch (order) {
       case 1:
-        for (int i = 1; i < bs; i++) out[i] += out[i - 1];
+        for (int i = 1; i < bs; i++) u[i] += u[i - 1];
         break;
       case 2:
-        for (int i = 2; i < bs; i++) out[i] += 2 * out[i - 1] - out[i - 2];
+        for (int i = 2; i < bs; i++) u[i] += 2u * u[i - 1] - u[i - 2];
         break;
       case 3:
-        for (int i = 3; i < bs; i++) out[i] += 3 * out[i - 1] - 3 * out[i - 2] + out[i - 3];
+        for (int i = 3; i < bs; i++) u[i] += 3u * u[i - 1] - 3u * u[i - 2] + u[i - 3];
         break;
       case 4:
-        for (int i = 4; i < bs; i++) out[i] += 4 * out[i - 1] - 6 * out[i - 2] + 4 * out[i - 3] - out[i - 4];
+        for (int i = 4; i < bs; i++) u[i] += 4u * u[i - 1] - 6u * u[i - 2] + 4u * u[i - 3] - u[i - 4];
         break;
       default:
         break;
@@ -348,16 +370,16 @@ size_t decode_frame(const uint8_t* d, size_t n, size_t pos, const TwFlacInfo& si
   } else if (h.chan_assign == 8) {  // left, side
     for (int i = 0; i < bs; i++) {
       o[2 * i] = s0[i];
-      o[2 * i + 1] = s0[i] - s1[i];
+      o[2 * i + 1] = (int32_t)((uint32_t)s0[i] - (uint32_t)s1[i]);
     }
   } else if (h.chan_assign == 9) {  // side, right
     for (int i = 0; i < bs; i++) {
-      o[2 * i] = s0[i] + s1[i];
+      o[2 * i] = wrap_add(s0[i], s1[i]);
       o[2 * i + 1] = s1[i];
     }
   } else {  // mid, side
     for (int i = 0; i < bs; i++) {
-      int64_t mid = ((int64_t)s0[i] << 1) | (s1[i] & 1);
+      int64_t mid = (int64_t)s0[i] * 2 + (s1[i] & 1);  // (s0 << 1 | side's low bit; no shift of a negative)
       o[2 * i] = (int32_t)((mid + s1[i]) >> 1);
       o[2 * i + 1] = (int32_t)((mid - s1[i]) >> 1);
     }

@@ -428,8 +428,8 @@ void render_line(int x0, int y0, int x1, int y1, int n, std::vector<int>& v) {
 
 int render_point(int x0, int y0, int x1, int y1, int X) {
   const int dy = y1 - y0, adx = x1 - x0, ady = abs(dy);
-  const int err = ady * (X - x0);
-  const int off = err / adx;
+  const long long err = (long long)ady * (X - x0);  // (64-bit: no overflow for any post values)
+  const int off = (int)(err / adx);
   return dy < 0 ? y0 - off : y0 + off;
 }
 
@@ -797,7 +797,7 @@ struct Decoder {
     // amplitude value synthesis (§7.2.4 step 1)
     int fy[65];
     bool step2[65];
-    fy[0] = Y[0];
+    fy[0] = Y[0];  // (read with ilog(range - 1) bits: < 2^16)
     fy[1] = Y[1];
     step2[0] = step2[1] = true;
     for (int i = 2; i < nx; i++) {
@@ -813,6 +813,10 @@ struct Decoder {
         step2[i] = false;
         fy[i] = pred;
       }
+      // a hostile codebook entry (up to 2^20) can put a post far outside [0, range): clipped to [0, 65535] as ffmpeg's
+      // decoder (the one ffmpeg_read runs) clips floor1_Y_final with av_clip_uint16, so neither the predictions
+      // (render_point, 64-bit) nor the curve arithmetic can overflow; a valid stream's posts are unchanged
+      fy[i] = std::min(std::max(fy[i], 0), 65535);
     }
     // curve synthesis (step 2): lines between the used posts in x order, then the dB table
     v.assign(n2, 0);

@@ -174,6 +174,8 @@ class _EncoderPump:
 def fallback_row_key(window: int, pass_no: int, fi: int) -> int:
     """The fallback sampler's row key (int32): one counter-based noise stream per (global window, seek pass,
     temperature index)."""
+    if not (0 <= int(pass_no) < 1024 and 0 <= int(fi) < 16):  # (fields would alias another row's noise stream)
+        raise ValueError(f"sampler key fields out of range: pass {pass_no} (< 1024), temperature index {fi} (< 16)")
     key = (int(window) * 1024 + int(pass_no)) * 16 + int(fi)
     if not 0 <= key < 2 ** 31:
         raise ValueError(f"sampler key out of range: window {window}, pass {pass_no}")
