@@ -24,7 +24,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 import torch
 
-from . import _lib, alignment
+from . import _lib, _ops, alignment
 from .config import GenerationSettings, WhisperDims
 from .frontend import CHUNK_SAMPLES, N_FRAMES, dft_basis, mel_table, pack_k8
 from .segments import (FallbackConfig, condition_prefixes, fallback_sequence, need_fallback, retrieve_segment,
@@ -196,6 +196,9 @@ class WhisperEngine:
                  device: str = "cuda", use_graphs: bool = True, max_beams: int = 1,
                  enc_fp8: Optional[bool] = None):
         _lib.load()
+        self.ops = _ops.load()  # torch.ops.tw (the encoder path's launches)
+        # (A/B: TW_ENC_OPS=0 issues the same encoder kernels through the C-ABI directly, without the dispatcher)
+        self.enc_via_ops = os.environ.get("TW_ENC_OPS", "1") != "0"
         # Large-M GEMM kernel per encoder context (tw_gemm_set_variant): the 8-phase ping-pong k_gemm_8p (5) is 6-19 %
         # faster than k_gemm_big (1) on every encoder shape when it has the GPU to itself (scripts/gemm_bench.py), but
         # beside a running decode it slows the latency-bound decoder kernels more than it gains (bench step 117.1 vs
@@ -428,12 +431,26 @@ class WhisperEngine:
     def _s(self) -> int:
         return self.stream.cuda_stream
 
-    def _gemm(self, A, W, M, N, K, epi, out, bias=None, aux=None, aux_rows=0, kv_geom=None, lda=None, ldw=None,
-              ldo=None, stream=None):
+    def _on(self, st):
+        """The context a torch.ops.tw call needs to launch on stream st (the ops use the current stream)."""
+        if torch.cuda.current_stream(self.device).cuda_stream == st.cuda_stream:
+            return contextlib.nullcontext()
+        return torch.cuda.stream(st)
+
+    def _gemm(self, A, W, M, N, K, epi, out, bias=None, aux=None, aux_rows=0, kv_geom=None, stream=None):
+        """torch.ops.tw.gemm_bf16_out on A[:M] (K columns) x W^T (N rows) into out[:M] (CROSSKV: the head-major
+        cross-K/V block, kv_geom = (S, B, D, H))."""
         st = stream or self.stream
         rec = self._begin_timer(("gemm_skinny" if M <= 32 else "gemm_big", epi), 2.0 * M * N * K, st)
-        _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, lda or K, ldw or K, epi, out.data_ptr(),
-                  ldo or N, _lib.ptr(bias), _lib.ptr(aux), aux_rows, kv_geom, st.cuda_stream)
+        assert A.shape[1] == K and W.shape[0] == N and W.shape[1] == K
+        if self.enc_via_ops:
+            with self._on(st):
+                self.ops.gemm_bf16_out(A[:M], W, epi, out if epi == _lib.TW_EPI_CROSSKV else out[:M], bias, aux,
+                                       aux_rows, list(kv_geom) if kv_geom is not None else None)
+        else:
+            _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, K, K, epi, out.data_ptr(), N,
+                      _lib.ptr(bias), _lib.ptr(aux), aux_rows,
+                      None if kv_geom is None else (ctypes.c_int * 4)(*kv_geom), st.cuda_stream)
         self._end_timer(rec, st)
 
     # per-launch HIP-event timing of kernel families (bench roofline; off by default). timer_families: the
@@ -469,8 +486,12 @@ class WhisperEngine:
         return out
 
     def _ln(self, x, g, b, M, out, stream=None):
-        _lib.call("tw_layernorm", x.data_ptr(), g.data_ptr(), b.data_ptr(), M, self.d.d_model, LN_EPS,
-                  out.data_ptr(), (stream or self.stream).cuda_stream)
+        if not self.enc_via_ops:
+            _lib.call("tw_layernorm", x.data_ptr(), g.data_ptr(), b.data_ptr(), M, self.d.d_model, LN_EPS,
+                      out.data_ptr(), (stream or self.stream).cuda_stream)
+            return
+        with self._on(stream or self.stream):
+            self.ops.layernorm_out(x[:M], g, b, LN_EPS, out[:M])
 
     # ------------------------------------------------------------------ streams / slots
     def _pump_drain(self) -> None:
@@ -543,9 +564,9 @@ class WhisperEngine:
         """feats[slot][:n] = log-mel of wave[:n] (each row one 30-s window, zero padded)."""
         slot = self._slot if slot is None else slot
         st = self._enc_begin(sync)
-        _lib.call("tw_logmel", self.wave.data_ptr(), n, self.basis_cos.data_ptr(), self.basis_sin.data_ptr(),
-                  self.mel_fb.data_ptr(), self.d.n_mels, self.feats_buf[slot].data_ptr(), self.maxkeys.data_ptr(),
-                  st.cuda_stream)
+        with self._on(st):
+            self.ops.logmel_out(self.wave[:n], self.basis_cos, self.basis_sin, self.mel_fb, self.d.n_mels,
+                                self.feats_buf[slot][:n], self.maxkeys)
         self._enc_end(sync, slot)
 
     # ------------------------------------------------------------------ encoder
@@ -617,7 +638,11 @@ class WhisperEngine:
             self._ln(self.x, L.ln1_g, L.ln1_b, M15, self.hln, stream=st)
             self._gemm(self.hln, L.wqkv, M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv, stream=st)
             rec = self._begin_timer(("attn_encoder", 0), 4.0 * S_ENC * S_ENC * 64 * H * R, st)
-            _lib.call("tw_attn_encoder", self.qkv.data_ptr(), R, S_ENC, H, self.att.data_ptr(), s)
+            if self.enc_via_ops:
+                with self._on(st):
+                    self.ops.attn_encoder_out(self.qkv[:M15], R, H, self.att[:M15])
+            else:
+                _lib.call("tw_attn_encoder", self.qkv.data_ptr(), R, S_ENC, H, self.att.data_ptr(), s)
             self._end_timer(rec, st)
             self._gemm(self.att, L.wo, M15, D, D, _lib.TW_EPI_RESID_F32, self.x, bias=L.bo, stream=st)
             self._ln(self.x, L.ln2_g, L.ln2_b, M15, self.hln, stream=st)
@@ -625,7 +650,7 @@ class WhisperEngine:
             self._gemm(self.ffn, L.w2, M15, D, F, _lib.TW_EPI_RESID_F32, self.x, bias=L.b2, stream=st)
             yield
         self._ln(self.x, w.enc_ln_g, w.enc_ln_b, M15, self.hln, stream=st)  # encoder last_hidden_state (bf16)
-        geom = (ctypes.c_int * 4)(S_ENC, R, D, H)
+        geom = (S_ENC, R, D, H)
         self._gemm(self.hln, w.wkv_x, M15, d.decoder_layers * 2 * D, D, _lib.TW_EPI_CROSSKV, self.cross_kv_buf[slot],
                    bias=w.bkv_x, kv_geom=geom, stream=st)
         self._enc_end(sync, slot)
