@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--n", type=int, default=32)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--pos", type=int, default=64)
+    ap.add_argument("--flush", type=int, default=0)
     a = ap.parse_args()
     dims = PRESETS["large-v3-turbo"]
     gen = GenerationSettings.default(dims)
@@ -108,6 +109,27 @@ def main():
         return e0.elapsed_time(e1) * 1e3 / a.reps / n
 
     t_triv = timed(trivial, a.n)
+    if a.flush:
+        # where a cold GEMV's weights come from: X behind a copy that evicts the L2s only (2 x 20 MB moved) or the
+        # Infinity Cache too (2 x 300 MB), against X behind a trivial kernel (everything warm)
+        for mb in (20, 300):
+            src = torch.empty(mb << 18, device="cuda")  # mb MiB of f32
+            dst = torch.empty_like(src)
+
+            def flush(src=src, dst=dst):
+                dst.copy_(src)
+            t_f = timed(flush, a.n // 2)
+            for name, fn in cases:
+                if name not in ("qkv", "fc1", "q_x", "o_proj", "resid_ln4"):
+                    continue
+
+                def pair(fn=fn, flush=flush):
+                    fn()
+                    flush()
+                tp = timed(pair, a.n // 2) - t_f
+                print(json.dumps({"rows": R, "kernel": name, "behind_copy_MiB": mb, "us": round(tp, 2),
+                                  "copy_alone_us": round(t_f, 2)}), flush=True)
+        return
     for var in (0, 1):
         _lib.call("tw_gemv_set_variant", var)
         for name, fn in cases:

@@ -96,7 +96,12 @@ def test_op_attn_encoder_and_layernorm_vs_torch():
     tw = _ops.load()
     B, S, H = 2, 1500, 4
     qkv = _rand_bf16(B * S, 3 * H * 64, seed=5)
+    D = H * 64
+    qkv[:, :D] = (qkv[:, :D].float() * 0.125 * 3).to(torch.bfloat16)  # scaled q (as the C-ABI kernel test)
     out = tw.attn_encoder(qkv, B, H)
+    capi = torch.empty_like(out)
+    _lib.call("tw_attn_encoder", qkv.data_ptr(), B, S, H, capi.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert torch.equal(out.view(torch.int16), capi.view(torch.int16))  # the same kernel
     q, k, v = qkv.float().view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
     ref = torch.softmax(q @ k.transpose(-1, -2), -1) @ v  # (q carries the 1/8 scale, as the packed weights do)
     torch.testing.assert_close(out.float().view(B, S, H, 64).permute(0, 2, 1, 3), ref, atol=2e-2, rtol=2e-2)

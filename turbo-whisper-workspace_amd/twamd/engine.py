@@ -431,11 +431,28 @@ class WhisperEngine:
     def _s(self) -> int:
         return self.stream.cuda_stream
 
+    _enc_cur = None  # the stream handle an encoder chunk's launches are issued under (_enc_chunk_ctx)
+
     def _on(self, st):
-        """The context a torch.ops.tw call needs to launch on stream st (the ops use the current stream)."""
-        if torch.cuda.current_stream(self.device).cuda_stream == st.cuda_stream:
+        """The context a torch.ops.tw call needs to launch on stream st (the ops use the current stream): nothing
+        inside an encoder chunk already entered on st."""
+        if self._enc_cur == st.cuda_stream or torch.cuda.current_stream(self.device).cuda_stream == st.cuda_stream:
             return contextlib.nullcontext()
         return torch.cuda.stream(st)
+
+    @contextlib.contextmanager
+    def _enc_chunk_ctx(self, st):
+        """One encoder chunk's launches (between two yields of _encode_chunks) under one stream context."""
+        with torch.cuda.stream(st):
+            self._enc_cur = st.cuda_stream
+            try:
+                yield
+            finally:
+                self._enc_cur = None
+
+    @staticmethod
+    def _rows(t, M):
+        return t if t.shape[0] == M else t[:M]
 
     def _gemm(self, A, W, M, N, K, epi, out, bias=None, aux=None, aux_rows=0, kv_geom=None, stream=None):
         """torch.ops.tw.gemm_bf16_out on A[:M] (K columns) x W^T (N rows) into out[:M] (CROSSKV: the head-major
@@ -445,8 +462,9 @@ class WhisperEngine:
         assert A.shape[1] == K and W.shape[0] == N and W.shape[1] == K
         if self.enc_via_ops:
             with self._on(st):
-                self.ops.gemm_bf16_out(A[:M], W, epi, out if epi == _lib.TW_EPI_CROSSKV else out[:M], bias, aux,
-                                       aux_rows, list(kv_geom) if kv_geom is not None else None)
+                self.ops.gemm_bf16_out(self._rows(A, M), W, epi, out if epi == _lib.TW_EPI_CROSSKV else
+                                       self._rows(out, M), bias, aux, aux_rows,
+                                       list(kv_geom) if kv_geom is not None else None)
         else:
             _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, K, K, epi, out.data_ptr(), N,
                       _lib.ptr(bias), _lib.ptr(aux), aux_rows,
@@ -491,7 +509,7 @@ class WhisperEngine:
                       out.data_ptr(), (stream or self.stream).cuda_stream)
             return
         with self._on(stream or self.stream):
-            self.ops.layernorm_out(x[:M], g, b, LN_EPS, out[:M])
+            self.ops.layernorm_out(self._rows(x, M), g, b, LN_EPS, self._rows(out, M))
 
     # ------------------------------------------------------------------ streams / slots
     def _pump_drain(self) -> None:
@@ -612,47 +630,51 @@ class WhisperEngine:
         M3, M15 = R * N_FRAMES, R * S_ENC
         st = self._enc_begin(sync)
         s = st.cuda_stream
-        if self._long is not None:  # a long-form input's features (set_long_input): one row of T frames
-            lf = self._long
-            _lib.call("tw_im2col_conv1_long", lf["feats"].data_ptr(), d.n_mels, lf["ld"], lf["max_frames"].data_ptr(),
-                      self.row_map.data_ptr() if row_map else None, self.seek.data_ptr(), R, w.kpad1,
-                      self.a1.data_ptr(), s)
-        else:
-            _lib.call("tw_im2col_conv1", self.feats_buf[slot].data_ptr(), d.n_mels,
-                      self.row_map.data_ptr() if row_map else None, self.seek.data_ptr() if seek else None, R, w.kpad1,
-                      self.a1.data_ptr(), s)
-        self._gemm(self.a1, w.conv1_w, M3, D, w.kpad1, _lib.TW_EPI_GELU_BF16, self.h1, bias=w.conv1_b, stream=st)
-        if self._conv2_im2col:
-            _lib.call("tw_im2col_conv2", self.h1.data_ptr(), R, D, self.a2.data_ptr(), s)
-            self._gemm(self.a2, w.conv2_w, M15, D, 3 * D, _lib.TW_EPI_GELU_POS_F32, self.x, bias=w.conv2_b,
-                       aux=w.pos_enc, aux_rows=S_ENC, stream=st)
-        else:
-            rec = self._begin_timer(("gemm_big", _lib.TW_EPI_GELU_POS_F32), 2.0 * M15 * D * 3 * D, st)
-            _lib.call("tw_conv2_gemm", self.h1.data_ptr(), R, D, w.conv2_w.data_ptr(), w.conv2_b.data_ptr(),
-                      w.pos_enc.data_ptr(), self.x.data_ptr(), s)
-            self._end_timer(rec, st)
+        # (one stream context per chunk, never across a yield: the caller runs there)
+        with self._enc_chunk_ctx(st):
+            if self._long is not None:  # a long-form input's features (set_long_input): one row of T frames
+                lf = self._long
+                _lib.call("tw_im2col_conv1_long", lf["feats"].data_ptr(), d.n_mels, lf["ld"],
+                          lf["max_frames"].data_ptr(), self.row_map.data_ptr() if row_map else None,
+                          self.seek.data_ptr(), R, w.kpad1, self.a1.data_ptr(), s)
+            else:
+                _lib.call("tw_im2col_conv1", self.feats_buf[slot].data_ptr(), d.n_mels,
+                          self.row_map.data_ptr() if row_map else None, self.seek.data_ptr() if seek else None, R,
+                          w.kpad1, self.a1.data_ptr(), s)
+            self._gemm(self.a1, w.conv1_w, M3, D, w.kpad1, _lib.TW_EPI_GELU_BF16, self.h1, bias=w.conv1_b, stream=st)
+            if self._conv2_im2col:
+                _lib.call("tw_im2col_conv2", self.h1.data_ptr(), R, D, self.a2.data_ptr(), s)
+                self._gemm(self.a2, w.conv2_w, M15, D, 3 * D, _lib.TW_EPI_GELU_POS_F32, self.x, bias=w.conv2_b,
+                           aux=w.pos_enc, aux_rows=S_ENC, stream=st)
+            else:
+                rec = self._begin_timer(("gemm_big", _lib.TW_EPI_GELU_POS_F32), 2.0 * M15 * D * 3 * D, st)
+                _lib.call("tw_conv2_gemm", self.h1.data_ptr(), R, D, w.conv2_w.data_ptr(), w.conv2_b.data_ptr(),
+                          w.pos_enc.data_ptr(), self.x.data_ptr(), s)
+                self._end_timer(rec, st)
         yield
         if self.enc_fp8:
             yield from self._encode_layers_mx(R, st)
         for L in ([] if self.enc_fp8 else w.enc):
-            self._ln(self.x, L.ln1_g, L.ln1_b, M15, self.hln, stream=st)
-            self._gemm(self.hln, L.wqkv, M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv, stream=st)
-            rec = self._begin_timer(("attn_encoder", 0), 4.0 * S_ENC * S_ENC * 64 * H * R, st)
-            if self.enc_via_ops:
-                with self._on(st):
-                    self.ops.attn_encoder_out(self.qkv[:M15], R, H, self.att[:M15])
-            else:
-                _lib.call("tw_attn_encoder", self.qkv.data_ptr(), R, S_ENC, H, self.att.data_ptr(), s)
-            self._end_timer(rec, st)
-            self._gemm(self.att, L.wo, M15, D, D, _lib.TW_EPI_RESID_F32, self.x, bias=L.bo, stream=st)
-            self._ln(self.x, L.ln2_g, L.ln2_b, M15, self.hln, stream=st)
-            self._gemm(self.hln, L.w1, M15, F, D, _lib.TW_EPI_GELU_BF16, self.ffn, bias=L.b1, stream=st)
-            self._gemm(self.ffn, L.w2, M15, D, F, _lib.TW_EPI_RESID_F32, self.x, bias=L.b2, stream=st)
+            with self._enc_chunk_ctx(st):
+                self._ln(self.x, L.ln1_g, L.ln1_b, M15, self.hln, stream=st)
+                self._gemm(self.hln, L.wqkv, M15, 3 * D, D, _lib.TW_EPI_BF16, self.qkv, bias=L.bqkv, stream=st)
+                rec = self._begin_timer(("attn_encoder", 0), 4.0 * S_ENC * S_ENC * 64 * H * R, st)
+                if self.enc_via_ops:
+                    with self._on(st):
+                        self.ops.attn_encoder_out(self._rows(self.qkv, M15), R, H, self._rows(self.att, M15))
+                else:
+                    _lib.call("tw_attn_encoder", self.qkv.data_ptr(), R, S_ENC, H, self.att.data_ptr(), s)
+                self._end_timer(rec, st)
+                self._gemm(self.att, L.wo, M15, D, D, _lib.TW_EPI_RESID_F32, self.x, bias=L.bo, stream=st)
+                self._ln(self.x, L.ln2_g, L.ln2_b, M15, self.hln, stream=st)
+                self._gemm(self.hln, L.w1, M15, F, D, _lib.TW_EPI_GELU_BF16, self.ffn, bias=L.b1, stream=st)
+                self._gemm(self.ffn, L.w2, M15, D, F, _lib.TW_EPI_RESID_F32, self.x, bias=L.b2, stream=st)
             yield
-        self._ln(self.x, w.enc_ln_g, w.enc_ln_b, M15, self.hln, stream=st)  # encoder last_hidden_state (bf16)
-        geom = (S_ENC, R, D, H)
-        self._gemm(self.hln, w.wkv_x, M15, d.decoder_layers * 2 * D, D, _lib.TW_EPI_CROSSKV, self.cross_kv_buf[slot],
-                   bias=w.bkv_x, kv_geom=geom, stream=st)
+        with self._enc_chunk_ctx(st):
+            self._ln(self.x, w.enc_ln_g, w.enc_ln_b, M15, self.hln, stream=st)  # encoder last_hidden_state (bf16)
+            geom = (S_ENC, R, D, H)
+            self._gemm(self.hln, w.wkv_x, M15, d.decoder_layers * 2 * D, D, _lib.TW_EPI_CROSSKV,
+                       self.cross_kv_buf[slot], bias=w.bkv_x, kv_geom=geom, stream=st)
         self._enc_end(sync, slot)
 
     def _encode_layers_mx(self, R: int, st):
