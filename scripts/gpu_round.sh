@@ -29,7 +29,7 @@ step pmc_mfma 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_IN
 python scripts/summarize_prof.py $OUT > $OUT/summary.txt 2>&1
 cp $OUT/traffic.json profiles/${TAG}_traffic.json   # bench.py reads the newest profiles/*traffic.json
 [ -f $OUT/mfma.json ] && cp $OUT/mfma.json profiles/${TAG}_mfma.json
-step bench 900 python bench.py $BA --steps 5 --warmup 2
+step bench 900 python bench.py $BA --steps 20 --warmup 5
 grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
 cp $OUT/bench.json profiles/${TAG}_bench.json; cp $OUT/summary.txt profiles/${TAG}_rocprof_summary.txt
 echo done

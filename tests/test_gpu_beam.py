@@ -261,6 +261,31 @@ def test_pipeline_beam5_matches_transformers_pipeline(mini, name):
     _same_or_beam_within_tau(mini, r, case["output"], audio, kw, 40)
 
 
+@pytest.mark.parametrize("name", ["ref_60_5", "mode_30_0"])
+def test_pipeline_beam5_exact_with_enc4_attention(mini, name):
+    """one exact-match run of the beam-5 pipeline goldens. With the encoder attention at k_attn_enc4
+    (tw_attn_set_variant 16, bit-identical to the enc2 form these goldens were first matched with) the drop-in's
+    output equals the transformers pipeline's exactly — no tolerance — so a host-side beam or segment regression
+    cannot hide behind the near-tie allowance the default (enc5) runs need."""
+    from twamd.synth_audio import speech_like, white_noise
+
+    gold = json.load(open(os.path.join(G, "beam.json")))
+    case = next(c for c in gold["pipeline"] if c["name"] == name)
+    audio = np.concatenate([speech_like(40.0, 5), white_noise(35.0, 11)])
+    eng = mini.engine
+    saved = eng.attn_kernel
+    eng.attn_kernel = (16, 16)
+    try:
+        r = mini(audio, generate_kwargs={"task": "transcribe", "num_beams": 5, "max_new_tokens": 40},
+                 return_timestamps=True, **case["kwargs"])
+    finally:
+        eng.attn_kernel = saved
+    ref = case["output"]
+    assert r["text"] == ref["text"]
+    assert [(tuple(c["timestamp"]), c["text"]) for c in r["chunks"]] == \
+        [(tuple(c["timestamp"]), c["text"]) for c in ref["chunks"]]
+
+
 def _same_or_beam_within_tau(t, r, ref, audio, kw, max_new):
     """The transformers pipeline's output exactly, or — where a bf16 near-tie ranks two fp32 candidates the other way
     (the random-weight model's beams lie within hundredths of a logit) — every device seek pass equal to the fp32
