@@ -255,8 +255,8 @@ def test_c4_process_audio_with_overlapped_diarization(tmp_path, monkeypatch):
     """configs[3]: install(module, overlap_diarization=True) on the stand-in class with the real turbo engine as the
     reference loads it (load_transcription_model -> the as-shipped beam-5 call through the drop-in) and a host
     diarizer doing GIL-releasing numpy work sized to ~60 % of the transcription. The overlapped process_audio returns
-    the serial run's result dict (processing_times aside) and its wall time is below serial - 80 % of the diarizer's
-    time."""
+    the serial run's result dict (processing_times aside) and its wall time is below serial - 80 % of the shorter of
+    the diarizer's and the transcription's time (the part one can hide behind the other)."""
     from twamd import audio_pipeline as tw_ap
 
     monkeypatch.setenv("TW_ALLOW_SYNTHETIC", "1")
@@ -268,8 +268,9 @@ def test_c4_process_audio_with_overlapped_diarization(tmp_path, monkeypatch):
     p0 = probe.AudioProcessingPipeline()
     assert p0.load_transcription_model("openai/whisper-large-v3-turbo")  # configs[3]'s model (synthetic weights)
     assert p0.transcription_model.engine.d.decoder_layers == 4
+    ref_asr = p0.transcribe(str(path))  # (the first call captures the engine's graphs)
     t = time.perf_counter()
-    ref_asr = p0.transcribe(str(path))
+    ref_asr = p0.transcribe(str(path))  # warm: the time process_audio's transcription takes
     t_asr = time.perf_counter() - t
     assert "error" not in ref_asr, ref_asr
     _StandInDiarizer.work(4)  # (BLAS threads started)
@@ -297,4 +298,5 @@ def test_c4_process_audio_with_overlapped_diarization(tmp_path, monkeypatch):
     assert strip(over) == strip(serial)
     assert strip(serial)["text"] == ref_asr["text"] and serial["segments"] == ref_asr["chunks"]
     assert d >= 0.3 * t_asr, (d, t_asr)  # the diarizer is a real share of the call
-    assert t_over < t_serial - 0.8 * d, (t_over, t_serial, d)
+    # the hideable share is the shorter of the two (the diarizer behind the GPU work, or the reverse)
+    assert t_over < t_serial - 0.8 * min(d, t_serial - d), (t_over, t_serial, d)
