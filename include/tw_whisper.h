@@ -34,6 +34,7 @@ extern "C" {
 #define TW_EPI_CROSSKV 5      /* out bf16 scattered to [layer][k|v][b][head][s][64]             */
 #define TW_EPI_GELU_PACKED 6  /* tw_gemv_packed: out = packed activation (below) of gelu(acc+bias) (fc1 -> fc2) */
 #define TW_EPI_GELU_MX 7      /* tw_gemm_mx: out fp8 e4m3[M][ldo] + e8m0 scales of gelu(acc+bias) (fc1 -> fc2) */
+#define TW_EPI_GELU_F32 8     /* tw_gemm_f32: out f32 = gelu_erf(acc + bias)         (fc1, conv1 of the f32 path) */
 #define TW_EPI_PARTIAL_F32 100 /* tw_gemv_packed: out f32[splits][M][ldo] split-K partials (no bias)          */
 
 /* Decoder per-row state (tw_logits_select), int32[TW_STATE_STRIDE] per batch row. */
@@ -322,6 +323,39 @@ int tw_attn_decode_cross_probs(const uint16_t* q, int B, int H, int S, int Bt, c
  * _dynamic_time_warping (generation_whisper.py:64-114); text_idx / time_idx int32[n + m] receive the path,
  * *path_len its length. */
 int tw_dtw(const double* matrix, int n, int m, int* text_idx, int* time_idx, int* path_len);
+
+/* ---- fp32 path (BASELINE configs[0]: whisper-tiny.en fp32) --------------------------------------------------
+ * The same modules as the bf16 entries above at f32 operand / activation / cache precision, for the reference's
+ * fp32 load (/root/reference/vocalis/core/audio_pipeline.py:195-200, torch_dtype=torch.float32; csrc/f32path.hip).
+ * tw_gemm_f32: C = A[M][K] . W[N][K]^T on v_mfma_f32_16x16x4_f32, K % 16 == 0, lda / ldw multiples of 4, epi
+ *   TW_EPI_F32, TW_EPI_GELU_F32, TW_EPI_RESID_F32, TW_EPI_GELU_POS_F32 or TW_EPI_CROSSKV (f32 out, kv_geom as
+ *   tw_gemm_bf16). Replaces nn.Linear / Conv1d-as-GEMM (modeling_whisper.py:279-282,375-376,566-567,970). */
+int tw_gemm_f32(const float* A, const float* W, int M, int N, int K, int lda, int ldw, int epi, float* out, int ldo,
+                const float* bias, const float* aux, int aux_rows, const int* kv_geom, void* stream);
+/* out f32[M][D] = LayerNorm(x f32[M][D]) (out != x). */
+int tw_layernorm_f32(const float* x, const float* gamma, const float* beta, int M, int D, float eps, float* out,
+                     void* stream);
+/* tw_im2col_conv1 / tw_im2col_conv1_long with f32 output: feature rows of ld frames (3000: the 30-s windows, then
+ * max_frames and seek may be NULL; ld > 3000: long-form rows, both required). */
+int tw_im2col_conv1_f32(const float* feats, int n_mels, long ld, const int* max_frames, const int* row_map,
+                        const int* seek, int R, int kpad, float* out, void* stream);
+/* tw_im2col_conv2 with f32 operands (D % 4 == 0). */
+int tw_im2col_conv2_f32(const float* h1, int R, int D, float* out, void* stream);
+/* x f32[B][D] = tok_emb f32[ids[b]] + pos_emb f32[pos[b]]. */
+int tw_embed_decoder_f32(const float* tok_emb, const float* pos_emb, const int* ids, const int* pos, int B, int D,
+                         float* x, void* stream);
+/* Encoder self-attention over qkv f32[B*S][3*H*64] (q pre-scaled) -> out f32[B*S][H*64]. */
+int tw_attn_encoder_f32(const float* qkv, int B, int S, int H, float* out, void* stream);
+/* tw_attn_decode_self[_tab][_masked] in one entry, f32 caches [B][H][max_pos][64]: kv_tab (NULL: none) with row0 as
+ * tw_attn_decode_self_tab, kv_start (NULL: none) as tw_attn_decode_self_masked. max_pos <= 2048. */
+int tw_attn_decode_self_f32(const float* qkv, int B, int H, int max_pos, const int* pos, float* k_cache,
+                            float* v_cache, const int* kv_tab, int row0, const int* kv_start, float* out,
+                            void* stream);
+/* tw_attn_decode_cross[_probs] in one entry, cross_kv f32[2][Bt][H][S][64] (S <= 2048); probs NULL: no alignment
+ * heads, else as tw_attn_decode_cross_probs. */
+int tw_attn_decode_cross_f32(const float* q, int B, int H, int S, int Bt, const int* row_map, const float* cross_kv,
+                             float* out, float* probs, unsigned head_mask, int slot0, int n_slots, const int* pos,
+                             int pos0, int n_steps, void* stream);
 
 /* ---- decoder glue --------------------------------------------------------------------------- */
 /* x f32[B][D] = embed_tokens[ids[b]] + embed_positions[pos[b]] (modeling_whisper.py:737,753-762). */

@@ -438,6 +438,44 @@ __device__ inline __amdgpu_buffer_rsrc_t tw_uniform_rsrc(const void* p, int byte
 //   RAW: a half-tile is waited for (vmcnt) before the first barrier of the phase before the one that reads it.
 //   WAR: a half-tile is restaged >= 2 phases after its last ds_read (A0 4, B0 2, B1 4, A1 4).
 // ------------------------------------------------------------------------------------------------
+#ifdef TW_GEMM_PROBE
+// Measurement build only (make probe -> scripts/exp/libtwhip_probe.so, scripts/exp/gemm_probe.py; never shipped):
+// per-workgroup timestamps of the large-M kernels' phases. Slots: 0 start, 1 first K-tile landed, 2 K loop done,
+// 3 epilogue stores retired (100 MHz s_memrealtime); 4, 5 core-clock s_memtime at start / K loop done; 6 HW_ID, 7 XCC_ID.
+__device__ unsigned long long tw_probe_ts[32768 * 8];
+#define TW_PROBE(slot)                                                                                     \
+  do {                                                                                                     \
+    if (threadIdx.x == 0) tw_probe_ts[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime();         \
+  } while (0)
+#define TW_PROBE_CLK(slot)                                                                                 \
+  do {                                                                                                     \
+    if (threadIdx.x == 0) tw_probe_ts[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memtime();            \
+  } while (0)
+__device__ inline void tw_probe_ids() {
+  if (threadIdx.x == 0) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    tw_probe_ts[blockIdx.x * 8 + 6] = hw;
+    tw_probe_ts[blockIdx.x * 8 + 7] = xcc;
+  }
+}
+extern "C" int tw_gemm_probe_read(unsigned long long* host, int nwg) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tw_probe_ts), (size_t)nwg * 8 * 8, 0, hipMemcpyDeviceToHost);
+}
+#define TW_PROBE_END()                                \
+  do {                                                \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+    __syncthreads();                                  \
+    TW_PROBE(3);                                      \
+  } while (0)
+#else
+#define TW_PROBE(slot) do {} while (0)
+#define TW_PROBE_CLK(slot) do {} while (0)
+#define TW_PROBE_END() do {} while (0)
+__device__ inline void tw_probe_ids() {}
+#endif
+
 template <int N>
 __device__ inline void p8_vmcnt() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -454,6 +492,9 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
   // second __shared__ object makes hipcc drain vmcnt before every ds_read)
   __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 64 * GB_EPI_LD * 2];
   constexpr int HT = 128 * GB_BK;
+  TW_PROBE(0);
+  TW_PROBE_CLK(4);
+  tw_probe_ids();
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int ntm = (M + GB_BM - 1) / GB_BM, ntn = (N + GB_BN - 1) / GB_BN;
   const int nwg = ntm * ntn;
@@ -548,6 +589,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
   for (int h = 0; h < 4; ++h) stage(0, h, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  TW_PROBE(1);
   if (wr == 1) __builtin_amdgcn_s_barrier();  // ping-pong: group 1 one barrier behind
   // one K-tile = 4 phases; NXT: stage K-tile t+1 (compile-time, so the steady-state loop has no branches)
   auto ktile = [&](int t, auto NXT) {
@@ -591,6 +633,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
   ktile(nk - 1, BF{});
   if (wr == 0) __builtin_amdgcn_s_barrier();  // realign the groups
   __syncthreads();
+  TW_PROBE(2);
+  TW_PROBE_CLK(5);
 
   // epilogue through LDS: per wave two 64-row halves (mh) of [64][64] f32 (cols = its two 32-col chunks), read
   // back 8 consecutive columns per lane (8 lanes per row) for 16-byte global stores
@@ -661,6 +705,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
       }
     }
   }
+  TW_PROBE_END();
 }
 
 // ------------------------------------------------------------------------------------------------

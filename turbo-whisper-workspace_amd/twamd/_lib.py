@@ -24,6 +24,7 @@ TW_EPI_F32 = 4
 TW_EPI_CROSSKV = 5
 TW_EPI_GELU_PACKED = 6
 TW_EPI_GELU_MX = 7
+TW_EPI_GELU_F32 = 8
 TW_EPI_PARTIAL_F32 = 100
 
 TW_SELECT_CHUNKS = 16
@@ -45,6 +46,8 @@ EXPORTED = (
     "tw_logmel_long", "tw_im2col_conv1_long", "tw_attn_decode_self_masked", "tw_attn_decode_self_tab_masked",
     "tw_gemv_set_wide_slices", "tw_vorbis_probe", "tw_vorbis_decode", "tw_vorbis_imdct",
     "tw_layernorm_set_lds_pad", "tw_gemv_set_variant",
+    "tw_gemm_f32", "tw_layernorm_f32", "tw_im2col_conv1_f32", "tw_im2col_conv2_f32", "tw_embed_decoder_f32",
+    "tw_attn_encoder_f32", "tw_attn_decode_self_f32", "tw_attn_decode_cross_f32",
 )
 
 
@@ -108,6 +111,14 @@ _SIGS = {
     "tw_conv2_gemm": ([_P, _I, _I, _P, _P, _P, _P, _P], _I),
     "tw_gemm_bf16": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _P], _I),
     "tw_layernorm": ([_P, _P, _P, _I, _I, _F, _P, _P], _I),
+    "tw_gemm_f32": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _P], _I),
+    "tw_layernorm_f32": ([_P, _P, _P, _I, _I, _F, _P, _P], _I),
+    "tw_im2col_conv1_f32": ([_P, _I, _L, _P, _P, _P, _I, _I, _P, _P], _I),
+    "tw_im2col_conv2_f32": ([_P, _I, _I, _P, _P], _I),
+    "tw_embed_decoder_f32": ([_P, _P, _P, _P, _I, _I, _P, _P], _I),
+    "tw_attn_encoder_f32": ([_P, _I, _I, _I, _P, _P], _I),
+    "tw_attn_decode_self_f32": ([_P, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P], _I),
+    "tw_attn_decode_cross_f32": ([_P, _I, _I, _I, _I, _P, _P, _P, _P, _U32, _I, _I, _P, _I, _I, _P], _I),
     "tw_gemm_mx": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P], _I),
     "tw_quant_mx": ([_P, _I, _I, _I, _P, _P, _I, _P], _I),
     "tw_attn_encoder_mx": ([_P, _I, _I, _I, _P, _P, _I, _P], _I),

@@ -29,11 +29,14 @@ DEFAULT_MODEL = "openai/whisper-large-v3"  # the reference's default name (:171)
 
 def _engine_options() -> Dict[str, Any]:
     """Engine construction from the environment (the reference reads LLM_MODEL etc. the same way):
-    TW_CHECKPOINT = local HF Whisper directory (no hub access offline), TW_MAX_BATCH, TW_SEED, TW_DEVICE."""
+    TW_CHECKPOINT = local HF Whisper directory (no hub access offline), TW_MAX_BATCH, TW_SEED, TW_DEVICE, and
+    TW_PRECISION = bf16 (default) or fp32 (BASELINE configs[0]: the reference's torch_dtype=torch.float32 load,
+    /root/reference/vocalis/core/audio_pipeline.py:199)."""
     return {"checkpoint": os.environ.get("TW_CHECKPOINT") or None,
             "max_batch": int(os.environ.get("TW_MAX_BATCH", "24")),
             "seed": int(os.environ.get("TW_SEED", "1234")),
-            "device": os.environ.get("TW_DEVICE", "cuda")}
+            "device": os.environ.get("TW_DEVICE", "cuda"),
+            "precision": os.environ.get("TW_PRECISION", "bf16")}
 
 
 def build_transcriber(model_name: str = DEFAULT_MODEL, **overrides) -> TurboTranscriber:

@@ -207,6 +207,9 @@ class WhisperEngine:
         # decoder's kernels find free wave slots.
         d = weights.dims
         d.validate()
+        if self.F32 != (weights.conv1_w.dtype == torch.float32):
+            raise ValueError(f"{type(self).__name__} needs {'f32' if self.F32 else 'bf16'} weights "
+                             "(build_weights(..., dtype=...))")
         self.d, self.w, self.gen = d, weights, gen
         self.max_batch = max_batch
         # decoder rows: windows x beams (beam search decodes num_beams rows per window against one cross-K/V)
@@ -222,6 +225,7 @@ class WhisperEngine:
         self._enc_ev = [torch.cuda.Event(), torch.cuda.Event()]
         D, F, H, V, B = d.d_model, d.ffn, d.heads, d.vocab, max_batch
         dev, bf, f32, i32 = self.device, torch.bfloat16, torch.float32, torch.int32
+        act = f32 if self.F32 else bf  # activation / cache dtype of the encoder and decoder
         c, s = dft_basis()
         self.basis_cos = torch.from_numpy(pack_k8(c)).to(dev)
         self.basis_sin = torch.from_numpy(pack_k8(s)).to(dev)
@@ -233,22 +237,24 @@ class WhisperEngine:
         self.maxkeys = torch.zeros(B, dtype=torch.int32, device=dev)
         # encoder activations
         M3, M15 = B * N_FRAMES, B * S_ENC
-        self.a1 = torch.empty(M3, weights.kpad1, dtype=bf, device=dev)
+        self.a1 = torch.empty(M3, weights.kpad1, dtype=act, device=dev)
         # conv1's output with one row in front: tw_conv2_gemm reads it in place as an operand of row stride 2 D
         # starting one row early (the t = 0 rows it then recomputes; the row in front only has to be readable)
-        self._h1_rows = torch.zeros(M3 + 1, D, dtype=bf, device=dev)
+        self._h1_rows = torch.zeros(M3 + 1, D, dtype=act, device=dev)
         self.h1 = self._h1_rows[1:]
         # (A/B: TW_CONV2_IM2COL=1 materialises conv2's im2col operand, 276 MB at B = 24, as before round 4)
         self._conv2_im2col = os.environ.get("TW_CONV2_IM2COL", "0") == "1"
-        self.a2 = torch.empty(M15, 3 * D, dtype=bf, device=dev) if self._conv2_im2col else None
+        self.a2 = torch.empty(M15, 3 * D, dtype=act, device=dev) if self._conv2_im2col or self.F32 else None
         self.x = torch.empty(M15, D, dtype=f32, device=dev)
-        self.hln = torch.empty(M15, D, dtype=bf, device=dev)
-        self.qkv = torch.empty(M15, 3 * D, dtype=bf, device=dev)
-        self.att = torch.empty(M15, D, dtype=bf, device=dev)
-        self.ffn = torch.empty(M15, F, dtype=bf, device=dev)
+        self.hln = torch.empty(M15, D, dtype=act, device=dev)
+        self.qkv = torch.empty(M15, 3 * D, dtype=act, device=dev)
+        self.att = torch.empty(M15, D, dtype=act, device=dev)
+        self.ffn = torch.empty(M15, F, dtype=act, device=dev)
         # cross-attention K/V of the encoded windows, one buffer per pipeline slot
         # BASELINE config 5: the encoder projections on MX fp8 operands (tw_gemm_mx); TW_ENC_FP8=1 turns it on
         self.enc_fp8 = (os.environ.get("TW_ENC_FP8", "0") == "1") if enc_fp8 is None else bool(enc_fp8)
+        if self.F32 and self.enc_fp8:
+            raise ValueError("the fp32 path has no MX fp8 encoder")
         self.enc_mx: List[Dict[str, tuple]] = []
         if self.enc_fp8:
             u8 = torch.uint8
@@ -263,18 +269,18 @@ class WhisperEngine:
                 self.enc_mx = [{k: self._quant_weight(getattr(L, k)) for k in ("wqkv", "wo", "w1", "w2")}
                                for L in weights.enc]
                 torch.cuda.synchronize(self.device)
-        self.cross_kv_buf = torch.empty(2, d.decoder_layers, 2, B, H, S_ENC, 64, dtype=bf, device=dev)
+        self.cross_kv_buf = torch.empty(2, d.decoder_layers, 2, B, H, S_ENC, 64, dtype=act, device=dev)
         self.cross_kv = self.cross_kv_buf[0]
         self._slot = 0  # slot the decoder reads
         # decoder state (max_rows = max_batch * max_beams rows)
         T = d.max_target_positions
         B = self.max_rows
-        self.kcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=bf, device=dev)
-        self.vcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=bf, device=dev)
+        self.kcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=act, device=dev)
+        self.vcache = torch.zeros(d.decoder_layers, B, H, T, 64, dtype=act, device=dev)
         self.xd = torch.empty(B, D, dtype=f32, device=dev)
-        self.qkvd = torch.empty(B, 3 * D, dtype=bf, device=dev)
-        self.qd = torch.empty(B, D, dtype=bf, device=dev)
-        self.attd = torch.empty(B, D, dtype=bf, device=dev)
+        self.qkvd = torch.empty(B, 3 * D, dtype=act, device=dev)
+        self.qd = torch.empty(B, D, dtype=act, device=dev)
+        self.attd = torch.empty(B, D, dtype=act, device=dev)
         self.logits = torch.empty(B, V, dtype=f32, device=dev)
         self.parts = torch.empty(DEC_SPLITS, B, D, dtype=f32, device=dev)   # split-K partials (decoder)
         self.sel_ws = torch.empty(B, _lib.TW_SELECT_WS_PER_ROW, dtype=f32, device=dev)
@@ -316,7 +322,7 @@ class WhisperEngine:
         self.pump_ahead = int(os.environ.get("TW_PUMP_AHEAD", "2"))
         # greedy steps end with the fused select + next-step embedding + first LayerNorm (tw_logits_select_embed):
         # 47 launches per token instead of 49 (False: the separate launches; the tests check both decode alike)
-        self.fused_select = True
+        self.fused_select = not self.F32
         # decoder steps per graph replay in the generation loop: alone (no encoder chunks pumped between steps) and
         # beside run_batches' encoder pump (TW_GRAPH_STEPS_ALONE / _BESIDE for A/B)
         self.graph_steps_alone = int(os.environ.get("TW_GRAPH_STEPS_ALONE", "1"))
@@ -338,14 +344,16 @@ class WhisperEngine:
         # wave-load of the per-token GEMVs is one contiguous 1 KiB fragment
         self.dec_p: List[Dict[str, torch.Tensor]] = []
         self.emb_p: Optional[torch.Tensor] = None
-        with torch.cuda.device(self.device):
-            self.dec_p = [{k: self._pack(getattr(L, k)) for k in ("wqkv", "wo", "wq_x", "wo_x", "w1", "w2")}
-                          for L in weights.dec]
-            self.emb_p = self._pack(weights.emb)
-            torch.cuda.synchronize(self.device)
+        if not self.F32:  # (the fp32 path's decoder runs tw_gemm_f32 on the row-major weights)
+            with torch.cuda.device(self.device):
+                self.dec_p = [{k: self._pack(getattr(L, k)) for k in ("wqkv", "wo", "wq_x", "wo_x", "w1", "w2")}
+                              for L in weights.dec]
+                self.emb_p = self._pack(weights.emb)
+                torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ lifetime
     closed = False
+    F32 = False  # the fp32 arithmetic path (twamd/engine_f32.py WhisperEngineF32)
 
     def close(self) -> None:
         """Release the engine's GPU state in order, deterministically (no finalizer left for the cyclic GC): wait for
@@ -540,8 +548,10 @@ class WhisperEngine:
         if n > VIEW_ROWS:
             raise ValueError(f"decoder views hold <= {VIEW_ROWS} rows (packed GEMV), got {n}")
         # per-view packed scratch (rows 0..n-1 of the view; pad rows zero)
-        hp = torch.zeros(VIEW_ROWS * self.d.d_model, dtype=torch.bfloat16, device=self.device)
-        fp = torch.zeros(VIEW_ROWS * self.d.ffn, dtype=torch.bfloat16, device=self.device)
+        # (fp32 path: the row-major f32 LayerNorm / fc1 outputs)
+        adt = torch.float32 if self.F32 else torch.bfloat16
+        hp = torch.zeros(VIEW_ROWS * self.d.d_model, dtype=adt, device=self.device)
+        fp = torch.zeros(VIEW_ROWS * self.d.ffn, dtype=adt, device=self.device)
         return DecView(r0, n, stream or self.stream, self.xd[sl], self.qkvd[sl], self.qd[sl], self.attd[sl],
                        self.logits[sl], self.parts if parts is None else parts, self.sel_ws[sl], self.state[sl],
                        self.tokens[sl], self.ids[sl], self.pos[sl], hp, fp)
@@ -829,11 +839,11 @@ class WhisperEngine:
     def _cross_ptrs(self, li: int, xkv_stride: int, v: DecView):
         """This layer's [k|v][r_enc][H][S][64] block and the row map for the view's rows: identity rows start at
         the view's first row; with beam search every row reads its window's slot through dec_row_map."""
-        H = self.d.heads
-        base = self.cross_kv.data_ptr() + li * xkv_stride * 2
+        H, esz = self.d.heads, self.cross_kv.element_size()
+        base = self.cross_kv.data_ptr() + li * xkv_stride * esz
         if self._use_dec_row_map:
             return base, self.dec_row_map.data_ptr() + 4 * v.r0
-        return base + v.r0 * H * S_ENC * 64 * 2, None
+        return base + v.r0 * H * S_ENC * 64 * esz, None
 
     def _select_params(self, mode: int, max_new: int, use_timestamps: bool = True) -> _lib.TwSelectParams:
         st, g = self.gen.special, self.gen

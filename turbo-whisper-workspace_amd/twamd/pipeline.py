@@ -22,6 +22,7 @@ import torch
 from . import audio, dist
 from .config import PRESETS, GenerationSettings, WhisperDims
 from .engine import WhisperEngine
+from .engine_f32 import WhisperEngineF32
 from .frontend import CHUNK_SAMPLES, SAMPLE_RATE, Window, chunk_windows, time_precision
 from .segments import FallbackConfig, pad_right
 from .tokenizer import LANGUAGE_NAMES, WhisperVocab, decode_asr
@@ -76,12 +77,16 @@ class TurboTranscriber:
     @staticmethod
     def from_pretrained(model: str = "large-v3-turbo", checkpoint: Optional[str] = None, seed: int = 1234,
                         max_batch: int = 24, device: str = "cuda", use_graphs: bool = True,
-                        max_beams: int = PIPELINE_DEFAULT_NUM_BEAMS, enc_fp8: Optional[bool] = None
-                        ) -> "TurboTranscriber":
+                        max_beams: int = PIPELINE_DEFAULT_NUM_BEAMS, enc_fp8: Optional[bool] = None,
+                        precision: str = "bf16") -> "TurboTranscriber":
         """`model`: a preset name (synthetic seeded weights) or, via `checkpoint`, a LOCAL Hugging Face
         Whisper directory (config.json, *.safetensors, vocab.json, generation_config.json). max_beams: decoder rows
         per window (the callable's default decode is beam-5, as the HF pipeline's; 1 = greedy-only engine). enc_fp8:
-        run the encoder projections on MX fp8 (BASELINE config 5; default: env TW_ENC_FP8)."""
+        run the encoder projections on MX fp8 (BASELINE config 5; default: env TW_ENC_FP8). precision: "bf16" (the
+        engine's default arithmetic) or "fp32" (every operand, activation and cache f32: BASELINE configs[0], the
+        reference's torch_dtype=torch.float32 load; WhisperEngineF32)."""
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(f"precision {precision!r}: 'bf16' or 'fp32'")
         if checkpoint is None and model not in PRESETS and os.path.isdir(model):
             checkpoint = model
         if checkpoint is not None:
@@ -95,9 +100,11 @@ class TurboTranscriber:
             dims = PRESETS[key]
             gen = GenerationSettings.default(dims)
             vocab = WhisperVocab.synthetic(gen.special)
-        weights = build_weights(dims, seed=seed, checkpoint=checkpoint)
-        eng = WhisperEngine(weights, gen, max_batch=max_batch, device=device, use_graphs=use_graphs, max_beams=max_beams,
-                            enc_fp8=enc_fp8)
+        f32 = precision == "fp32"
+        weights = build_weights(dims, seed=seed, checkpoint=checkpoint, dtype=torch.float32 if f32 else torch.bfloat16)
+        cls = WhisperEngineF32 if f32 else WhisperEngine
+        eng = cls(weights, gen, max_batch=max_batch, device=device, use_graphs=use_graphs, max_beams=max_beams,
+                  enc_fp8=enc_fp8)
         return TurboTranscriber(eng, vocab)
 
     # -------------------------------------------------------------- call

@@ -182,8 +182,10 @@ def synth_state_dict(d: WhisperDims, seed: int, device: str = "cuda") -> Dict[st
     return sd
 
 
-def load_checkpoint_state_dict(path: str, d: WhisperDims, device: str = "cuda") -> Dict[str, torch.Tensor]:
-    """Read a local Hugging Face Whisper checkpoint directory (*.safetensors; no network)."""
+def load_checkpoint_state_dict(path: str, d: WhisperDims, device: str = "cuda",
+                               dtype: torch.dtype = torch.bfloat16) -> Dict[str, torch.Tensor]:
+    """Read a local Hugging Face Whisper checkpoint directory (*.safetensors; no network): matrices as `dtype`,
+    vectors f32."""
     from safetensors.torch import load_file
 
     files = sorted(f for f in os.listdir(path) if f.endswith(".safetensors"))
@@ -202,17 +204,18 @@ def load_checkpoint_state_dict(path: str, d: WhisperDims, device: str = "cuda") 
         v = sd[name]
         if tuple(v.shape) != tuple(shape):
             raise ValueError(f"{name}: shape {tuple(v.shape)} != {shape}")
-        out[name] = v.to(device=device, dtype=torch.float32 if len(shape) == 1 else torch.bfloat16)
+        out[name] = v.to(device=device, dtype=torch.float32 if len(shape) == 1 else dtype)
     return out
 
 
-def pack(sd: Dict[str, torch.Tensor], d: WhisperDims) -> PackedWeights:
-    """Repack a state dict (bf16 matrices / f32 vectors on the device) into the engine layout.
+def pack(sd: Dict[str, torch.Tensor], d: WhisperDims, dtype: torch.dtype = torch.bfloat16) -> PackedWeights:
+    """Repack a state dict (matrices / f32 vectors on the device) into the engine layout, matrices as `dtype` (bf16:
+    the bf16 engine; f32: the fp32 path, WhisperEngineF32). The q scale 0.125 is a power of two: exact in both.
 
     Runs once at model load (torch ops used as device-memory plumbing, not on the hot path)."""
     D, F, M = d.d_model, d.ffn, d.n_mels
     dev = sd["model.encoder.conv1.bias"].device
-    bf, f32 = torch.bfloat16, torch.float32
+    bf, f32 = dtype, torch.float32
 
     def mat(n):
         return sd[n].to(bf).contiguous()
@@ -268,8 +271,11 @@ def pack(sd: Dict[str, torch.Tensor], d: WhisperDims) -> PackedWeights:
         wkv_x=torch.cat(kv_w, 0).contiguous(), bkv_x=torch.cat(kv_b).contiguous())
 
 
-def build_weights(d: WhisperDims, seed: Optional[int] = 1234, checkpoint: Optional[str] = None) -> PackedWeights:
-    sd = load_checkpoint_state_dict(checkpoint, d) if checkpoint else synth_state_dict(d, seed)
-    pw = pack(sd, d)
+def build_weights(d: WhisperDims, seed: Optional[int] = 1234, checkpoint: Optional[str] = None,
+                  dtype: torch.dtype = torch.bfloat16) -> PackedWeights:
+    """dtype: the matrices' type (bf16, or f32 for the fp32 path; the synthetic matrices are bf16-valued either way,
+    the values transformers' fp32 goldens were made with)."""
+    sd = load_checkpoint_state_dict(checkpoint, d, dtype=dtype) if checkpoint else synth_state_dict(d, seed)
+    pw = pack(sd, d, dtype)
     del sd
     return pw
