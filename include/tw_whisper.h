@@ -261,6 +261,10 @@ int tw_gemv_set_wide_slices(int kw);
  * 0 = two column groups per wave in batches of 5 K-steps, 1 = one column group per wave with its whole K-slice of
  * weight fragments in flight (<= 10 steps). Same results up to the f32 order of the K-slice sum. Returns 0. */
 int tw_gemv_set_variant(int v);
+/* Epilogue form of tw_gemm_bf16's large-M kernels: 0 (default) = the f32 LDS image of row-major accumulators, 1 =
+ * transposed accumulators (the MFMA as W . A^T: bias / GELU in registers, bf16 outputs staged as packed bf16, f32
+ * outputs stored from registers). The same sums either way (A/B switch; results agree to the output rounding). */
+int tw_gemm_set_epilogue(int tr);
 /* tw_resid_layernorm with the normalised rows written as a packed activation (M <= 64, D % 32 == 0). */
 int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
                               const float* beta, int M, int D, float eps, uint16_t* out, void* stream);

@@ -21,9 +21,16 @@ EPI = {"bf16": 0, "gelu_bf16": 1, "resid_f32": 2}  # TW_EPI_* of include/tw_whis
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", default=os.path.join(ROOT, "scripts", "exp", "libtwhip_probe.so"))
+    ap.add_argument("--epilogue", type=int, default=0, help="tw_gemm_set_epilogue (1 = transposed accumulators)")
+    ap.add_argument("--small", action="store_true", help="only the few-workgroup cases")
+    args = ap.parse_args()
     from twamd import _lib
     assert (_lib.TW_EPI_BF16, _lib.TW_EPI_GELU_BF16, _lib.TW_EPI_RESID_F32) == tuple(EPI.values())
-    lib = ctypes.CDLL(os.path.join(ROOT, "scripts", "exp", "libtwhip_probe.so"))
+    lib = ctypes.CDLL(args.lib)
+    lib.tw_gemm_set_epilogue(args.epilogue)
     vp, i = ctypes.c_void_p, ctypes.c_int
     lib.tw_gemm_bf16.argtypes = [vp, vp, i, i, i, i, i, i, vp, i, vp, vp, i, vp, vp]
     lib.tw_gemm_probe_read.argtypes = [vp, i]
@@ -36,6 +43,8 @@ def main():
              ("qkv_2K", 36000, 3840, 2560, "bf16")]
     cases += [("qkv_m%d" % m, m, 3840, 1280, "bf16") for m in (256, 2048, 4352, 8704)]
     cases += [("o_proj_m%d" % m, m, 1280, 1280, "resid_f32") for m in (256, 2048, 13056)]
+    if args.small:
+        cases = [c for c in cases if c[1] < 36000]
     for name, M, N, K, epi in cases:
         A = (torch.randn(M, K, device="cuda") * 0.5).to(torch.bfloat16)
         W = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
@@ -57,9 +66,9 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ev_us = e0.elapsed_time(e1) * 1e3
-        buf = np.zeros(nwg * 8, np.uint64)
+        buf = np.zeros(nwg * 16, np.uint64)
         assert lib.tw_gemm_probe_read(buf.ctypes.data, nwg) == 0
-        p = buf.reshape(nwg, 8).astype(np.int64)
+        p = buf.reshape(nwg, 16).astype(np.int64)
         t0, t1, t2, t3 = (p[:, k] - p[:, 0].min() for k in range(4))
         us = 0.01  # s_memrealtime ticks at 100 MHz
         span = t3.max() * us
@@ -79,7 +88,7 @@ def main():
         clk = (p[:, 5] - p[:, 4]) / np.maximum(p[:, 2] - p[:, 0], 1) * 100.0  # MHz
         flop = 2.0 * M * N * K
         print(json.dumps({
-            "shape": name, "M": M, "N": N, "K": K, "epi": epi, "workgroups": nwg, "cus": int(ncu),
+            "lib": os.path.basename(args.lib), "epilogue": args.epilogue, "shape": name, "M": M, "N": N, "K": K, "epi": epi, "workgroups": nwg, "cus": int(ncu),
             "event_us": round(ev_us, 1), "span_us": round(span, 1), "tflops": round(flop / ev_us / 1e6, 1),
             "prologue_us_med": round(float(np.median(t1 - t0)) * us, 2),
             "kloop_us_med": round(float(np.median(t2 - t1)) * us, 2),
@@ -90,6 +99,10 @@ def main():
             "all_cus_busy_us": round(float(full), 1), "tail_us": round(float(span - full), 1),
             "kloop_tflops_per_cu_med": round(2.0 * 256 * 256 * K / float(np.median(t2 - t1) * us) / 1e6, 2),
             "clock_mhz_med": round(float(np.median(clk)), 0),
+            # epilogue sub-phases of wave 0 (each after a vmcnt(0)): bias in, half 0 staged, half 0 stored, half 1
+            # staged, half 1 stored, then the block's stores retired
+            "epi_phases_us_med": [round(float(np.median(p[:, b] - p[:, a])) * us, 2)
+                                  for a, b in ((2, 8), (8, 9), (9, 10), (10, 11), (11, 12), (12, 3))],
         }), flush=True)
         del A, W, out
 

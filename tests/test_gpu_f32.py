@@ -1,8 +1,9 @@
 """The fp32 arithmetic path (BASELINE configs[0], whisper-tiny.en fp32; csrc/f32path.hip, twamd/engine_f32.py).
 
 Kernels against float64 restatements on the host (tolerances in each test, f32 accumulation over K terms); the engine
-at tiny.en fp32 against transformers fp32 itself (tests/golden/tiny.npz, make_golden.py tiny) at bounds 50x tighter
-than the bf16 engine's, and its generate() token-for-token equal to transformers' greedy sequences."""
+at tiny.en fp32 against transformers fp32 itself (tests/golden/tiny.npz, make_golden.py tiny) at 1e-4 (encoder) and
+2e-4 (logits) — the bf16 engine's bounds are 0.08 / 0.15 — and its generate() token-for-token equal to transformers'
+greedy sequences (measured: encoder 5.7e-6, logits 1.0e-5, profiles/r05s_f32_gputest.txt)."""
 import ctypes
 import os
 
@@ -196,7 +197,7 @@ def tiny32():
 
 def test_tiny_en_fp32_vs_transformers_goldens(tiny32):
     """Encoder rows, 24 teacher-forced positions (16 fp32-top logits and the log-sum-exp) and generate() (English-only
-    prompt, seek loop, 48 new tokens, timestamps) against transformers fp32: bounds 50x tighter than the bf16 engine's
+    prompt, seek loop, 48 new tokens, timestamps) against transformers fp32: bounds 800x tighter than the bf16 engine's
     (0.08 / 0.15), and the greedy sequences token-for-token equal."""
     import sys
 
@@ -218,9 +219,9 @@ def test_tiny_en_fp32_vs_transformers_goldens(tiny32):
     eng.encode(2)
     enc = eng.encoder_output(2).cpu().numpy()
     enc_err = max(float(np.abs(enc[i][z["enc_rows_idx"]] - z["enc_rows"][i]).max()) for i in range(2))
-    assert enc_err < 2e-3, enc_err
+    assert enc_err < 1e-4, enc_err  # (measured 5.7e-6)
     for i in range(2):
-        assert abs(enc[i].mean() - z["enc_mean"][i]) < 1e-4 and abs(enc[i].std() - z["enc_std"][i]) < 1e-4
+        assert abs(enc[i].mean() - z["enc_mean"][i]) < 2e-5 and abs(enc[i].std() - z["enc_std"][i]) < 2e-5
     worst = 0.0
     for t, tok in enumerate(z["tf_input_ids"]):
         eng.ids[0] = int(tok)
@@ -230,7 +231,7 @@ def test_tiny_en_fp32_vs_transformers_goldens(tiny32):
         m = lg.max()
         worst = max(worst, float(np.abs(lg[z["tf_top_idx"][t]] - z["tf_top_val"][t]).max()),
                     abs(m + np.log(np.exp(lg - m).sum()) - float(z["tf_lse"][t])))
-    assert worst < 3e-3, worst
+    assert worst < 2e-4, worst  # (measured 1.0e-5)
     eng.logmel(2)
     seqs = eng.generate(2, task=None, max_new_tokens=48, return_timestamps=True)
     st = tiny32.gen.special

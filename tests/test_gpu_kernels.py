@@ -64,11 +64,19 @@ def test_logmel_vs_oracle(n_mels):
 EPIS = [_lib.TW_EPI_BF16, _lib.TW_EPI_GELU_BF16, _lib.TW_EPI_RESID_F32, _lib.TW_EPI_F32]
 
 
-@pytest.mark.parametrize("variant", [1, 5], ids=["big", "8p"])
+@pytest.fixture(params=[0, 1], ids=["f32img", "tr"])
+def gemm_epilogue(request):
+    """The large-M kernels' epilogue form (tw_gemm_set_epilogue): f32 LDS image (default) / transposed accumulators."""
+    _lib.call("tw_gemm_set_epilogue", request.param)
+    yield request.param
+    _lib.call("tw_gemm_set_epilogue", 0)
+
+
+@pytest.mark.parametrize("variant", [1, 5, 6], ids=["big", "8p", "8pp"])
 @pytest.mark.parametrize("M,N,K", [(300, 384, 256), (1500, 1280, 1280), (24, 1280, 1280), (7, 51866, 384),
                                    (32, 5120, 1280), (129, 200, 64), (600, 512, 192), (257, 768, 3840)])
 @pytest.mark.parametrize("epi", EPIS)
-def test_gemm_vs_torch(M, N, K, epi, variant):
+def test_gemm_vs_torch(M, N, K, epi, variant, gemm_epilogue):
     _lib.call("tw_gemm_set_variant", variant)
     A = rand_bf16(M, K, seed=1)
     W = rand_bf16(N, K, scale=K ** -0.5, seed=2)
@@ -90,9 +98,9 @@ def test_gemm_vs_torch(M, N, K, epi, variant):
     torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
 
 
-@pytest.mark.parametrize("variant", [1, 5], ids=["big", "8p"])
+@pytest.mark.parametrize("variant", [1, 5, 6], ids=["big", "8p", "8pp"])
 @pytest.mark.parametrize("R,D", [(3, 1280), (1, 384), (40, 64)])
-def test_conv2_implicit_gemm_vs_torch_conv1d(R, D, variant):
+def test_conv2_implicit_gemm_vs_torch_conv1d(R, D, variant, gemm_epilogue):
     """tw_conv2_gemm (h1 read in place at row stride 2 D, t = 0 rows recomputed from taps 1-2) against torch's fp32
     Conv1d(k3, s2, p1) + GELU + positional rows, and against the im2col + GEMM path it replaces. R = 40 puts the
     t = 0 recompute on the large-M kernel (> 32 rows)."""
@@ -158,10 +166,11 @@ def test_resid_layernorm_vs_torch(M, D, nparts):
 
 @pytest.mark.parametrize("M,N,K", [(36000, 1280, 1280), (4000, 3840, 1280), (3000, 1280, 5120), (769, 512, 128)])
 @pytest.mark.parametrize("epi", [_lib.TW_EPI_BF16, _lib.TW_EPI_RESID_F32])
-def test_gemm_repeatable_and_kernels_agree(M, N, K, epi):
+def test_gemm_repeatable_and_kernels_agree(M, N, K, epi, gemm_epilogue):
     """k_gemm_8p (counted vmcnt, raw barriers, ping-pong wave groups) gives the same bits on every repeat (a half-tile
     read before its DMA landed, or restaged while still read, would show as a mismatch), and agrees with k_gemm_big
-    to f32 accumulation order."""
+    to f32 accumulation order; the persistent k_gemm_8pp (the next tile's DMA in flight under the epilogue, vmcnt(16)
+    over the stores) gives k_gemm_8p's bits exactly (the same products in the same order per tile)."""
     A = rand_bf16(M, K, seed=11)
     W = rand_bf16(N, K, scale=K ** -0.5, seed=12)
     bias = torch.randn(N, device=DEV) * 0.1
@@ -169,7 +178,7 @@ def test_gemm_repeatable_and_kernels_agree(M, N, K, epi):
     base = torch.randn(M, N, device=DEV).to(dt)
     outs = {}
     try:
-        for v in (1, 5, 5, 5):
+        for v in (1, 5, 5, 5, 6, 6, 6):
             _lib.call("tw_gemm_set_variant", v)
             out = base.clone()
             _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, K, K, epi, out.data_ptr(), N,
@@ -178,14 +187,50 @@ def test_gemm_repeatable_and_kernels_agree(M, N, K, epi):
             outs.setdefault(v, []).append(out)
     finally:
         _lib.call("tw_gemm_set_variant", 1)
-    for o in outs[5][1:]:
+    for o in outs[5][1:] + (outs[6] if gemm_epilogue == 0 else []):  # (k_gemm_8pp has the f32-image epilogue only)
         assert torch.equal(o, outs[5][0])
+    for o in outs[6][1:]:
+        assert torch.equal(o, outs[6][0])
     tol = 2e-2 if dt == torch.bfloat16 else 2e-3
     torch.testing.assert_close(outs[5][0].float(), outs[1][0].float(), atol=tol, rtol=tol)
 
 
 @pytest.mark.parametrize("variant", [1, 5], ids=["big", "8p"])
-def test_gemm_gelu_pos_and_crosskv(variant):
+@pytest.mark.parametrize("M,N,K", [(4000, 3840, 1280), (300, 200, 64)])
+@pytest.mark.parametrize("epi", [_lib.TW_EPI_BF16, _lib.TW_EPI_GELU_BF16, _lib.TW_EPI_RESID_F32, _lib.TW_EPI_F32,
+                                 _lib.TW_EPI_GELU_POS_F32])
+def test_gemm_epilogue_forms_agree(M, N, K, epi, variant):
+    """The transposed-accumulator epilogue against the f32-image one: the same products (the MFMA with its operands
+    swapped), so bf16 outputs agree to one bf16 rounding step and f32 outputs to f32 summation order."""
+    A = rand_bf16(M, K, seed=41)
+    W = rand_bf16(N, K, scale=K ** -0.5, seed=42)
+    bias = torch.randn(N, device=DEV) * 0.1
+    pos = torch.randn(1500, N, device=DEV)
+    dt = torch.bfloat16 if epi in (_lib.TW_EPI_BF16, _lib.TW_EPI_GELU_BF16) else torch.float32
+    base = torch.randn(M, N, device=DEV).to(dt)
+    outs = []
+    try:
+        _lib.call("tw_gemm_set_variant", variant)
+        for tr in (0, 1, 1):
+            _lib.call("tw_gemm_set_epilogue", tr)
+            out = base.clone()
+            _lib.call("tw_gemm_bf16", A.data_ptr(), W.data_ptr(), M, N, K, K, K, epi, out.data_ptr(), N,
+                      bias.data_ptr(), pos.data_ptr() if epi == _lib.TW_EPI_GELU_POS_F32 else None,
+                      1500 if epi == _lib.TW_EPI_GELU_POS_F32 else 0, None, S())
+            torch.cuda.synchronize()
+            outs.append(out.float())
+    finally:
+        _lib.call("tw_gemm_set_variant", 1)
+        _lib.call("tw_gemm_set_epilogue", 0)
+    assert torch.equal(outs[1], outs[2])  # repeatable
+    if dt == torch.bfloat16:
+        torch.testing.assert_close(outs[1], outs[0], atol=1e-2, rtol=2 ** -7)
+    else:
+        torch.testing.assert_close(outs[1], outs[0], atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("variant", [1, 5, 6], ids=["big", "8p", "8pp"])
+def test_gemm_gelu_pos_and_crosskv(variant, gemm_epilogue):
     _lib.call("tw_gemm_set_variant", variant)
     try:
         _gemm_gelu_pos_and_crosskv()

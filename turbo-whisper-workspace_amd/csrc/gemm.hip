@@ -76,6 +76,16 @@ __device__ inline void epi_store(const EpiArgs& ea, int m, int n, float v) {
 
 // Large-M kernel per context (tw_gemm_set_variant): 5 = k_gemm_8p (alone), 1 = k_gemm_big (beside a decode).
 static int tw_gemm_kernel = 1;
+// Epilogue form of the large-M kernels (tw_gemm_set_epilogue): 0 = the f32 LDS image of the row-major accumulators
+// (gemm_epi_128x64 / k_gemm_8p's own), 1 = transposed accumulators (gemm_epi_tr). 0: the transposed form measured
+// 0.94-0.99x on the encoder shapes (1.06x on cross-K/V only; profiles/r05s_gemm_epi_ab.txt) — the epilogue's time is
+// neither its LDS staging nor its instruction count (scripts/exp/gemm_probe.py)
+static int tw_gemm_tr = 0;
+extern "C" int tw_gemm_set_epilogue(int tr) {
+  TW_REQUIRE(tr == 0 || tr == 1, "tw_gemm_set_epilogue: %d (0 or 1)", tr);
+  tw_gemm_tr = tr;
+  return 0;
+}
 // tw_tile_grouped rows per group: 8 for the wide-N shapes (>= 10 column tiles: q/k/v, fc1, cross-K/V; 2-7 % measured),
 // row-major for the 5-column-tile ones (o_proj, fc2, conv2), scripts/gemm_bench.py, M = 36000
 static inline int tw_group_for(int N) { return (N + 255) / 256 >= 10 ? 8 : 1; }
@@ -103,8 +113,20 @@ extern "C" int tw_gemv_set_variant(int v) {
   return 0;
 }
 extern "C" int tw_gemm_set_variant(int v) {
-  tw_gemm_kernel = (v & 15) == 5 ? 5 : 1;
+  tw_gemm_kernel = (v & 15) == 5 ? 5 : (v & 15) == 6 ? 6 : 1;
   return 0;
+}
+// persistent grid of k_gemm_8pp: the device's CUs, a multiple of the 8 XCDs (blocks b, b + 8, ... share one XCD)
+static int tw_persistent_grid() {
+  static int g = 0;
+  if (!g) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 8)
+      cus = 256;
+    g = cus / 8 * 8;
+  }
+  return g;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -243,7 +265,7 @@ __device__ inline void gb_epi_sync() {
 // stage(half, wimg) writes rows 64 half .. 64 half + 63 of the wave's sub-tile into its [64][GB_EPI_LD] f32 image
 template <int EPI, class Stage>
 __device__ inline void gemm_epi_128x64_st(Stage stage, float* wimg, int lane, int mw0, int ncol0, int M, int N,
-                                          const EpiArgs& ea) {
+                                          const EpiArgs& ea, bool interior = false) {
   // ---- epilogue through LDS: each wave stages 64 of its 128 rows at a time in its own
   // [64][GB_EPI_LD] f32 image (k_gemm_big: 8 images = 136 KiB, the K loop's LDS plus 8 KiB), then reads
   // back 4 consecutive columns per lane (16 lanes x 16 B per row) for vectorised global I/O.
@@ -280,6 +302,20 @@ __device__ inline void gemm_epi_128x64_st(Stage stage, float* wimg, int lane, in
     stage(half, wimg);
     gb_epi_sync();
     if constexpr (PRE) {
+      if (interior) {
+        // every row and column of the tile in range: straight-line code, so hipcc counts the addend waits instead
+        // of draining vmcnt to 0 at each use (which retired every row's stores before the next row's math)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int lr = rr * 4 + (lane >> 4);
+          const int m = mrow0 + lr;
+          float4 v = *(const float4*)(wimg + lr * GB_EPI_LD + rc);
+          v.x += bias4.x; v.y += bias4.y; v.z += bias4.z; v.w += bias4.w;
+          epi_store4_pre<EPI>(ea, m, ncol0 + rc, v, ad[rr & 7]);
+          if (rr < 8) ad[rr] = epi_addend<EPI>(ea, m + 32, ncol0 + rc, true);
+        }
+        continue;
+      }
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
         const int lr = rr * 4 + (lane >> 4);  // 4 rows per wave-instruction
@@ -324,7 +360,7 @@ __device__ inline void gemm_epi_128x64_st(Stage stage, float* wimg, int lane, in
 // the 16x16x32 MFMA layout (8 x 4 accumulators of 16 x 16: lane (fr, fq) holds rows 4 fq + r of column fr)
 template <int EPI>
 __device__ inline void gemm_epi_128x64(const f32x4 (&acc)[8][4], float* wimg, int lane, int mw0, int ncol0, int M,
-                                       int N, const EpiArgs& ea) {
+                                       int N, const EpiArgs& ea, bool interior = false) {
   const int fr = lane & 15, fq = lane >> 4;
   auto stage = [&](int half, float* w) {
     const int ib = 4 * half;
@@ -335,9 +371,125 @@ __device__ inline void gemm_epi_128x64(const f32x4 (&acc)[8][4], float* wimg, in
 #pragma unroll
         for (int r = 0; r < 4; ++r) w[(ii * 16 + fq * 4 + r) * GB_EPI_LD + j * 16 + fr] = acc[ib + ii][j][r];
   };
-  gemm_epi_128x64_st<EPI>(stage, wimg, lane, mw0, ncol0, M, N, ea);
+  gemm_epi_128x64_st<EPI>(stage, wimg, lane, mw0, ncol0, M, N, ea, interior);
 }
-template <int EPI>
+// ------------------------------------------------------------------------------------------------
+// Transposed-accumulator epilogue (TR). The K loop runs the MFMA as W . A^T (operands swapped: the fragment reads
+// are unchanged), so lane (fr, fq) of accumulator block (i, j) holds sub-tile row 16 i + fr, columns 16 j + 4 fq ..
+// + 3 — four consecutive output columns in registers. The fused bias (+ GELU) then applies before any staging, bf16
+// outputs pack to 8-byte bf16x4 units, and f32 outputs leave straight from registers:
+//   bf16 (BF16 / GELU_BF16 / CROSSKV): units staged in the wave's own [128][64] bf16 LDS image (16 KiB; unit
+//     index XOR row & 15: conflict-free ds_write_b64 and ds_read_b128, scripts/exp/tr_swizzle_check.py), read
+//     back as 8 consecutive columns per lane (one 16-byte store, 8 lanes per 128-byte row): per wave 32 ds_write_b64
+//     + 16 ds_read_b128 instead of 128 ds_write_b32 + 16 ds_read_b128 of the f32 image, and half the LDS bytes.
+//   f32 (RESID / GELU_POS / F32): 16-byte accesses of 4 columns, 4 lanes per 64-byte row run; the residual / table
+//     operand of block row i + 1 is loaded while block row i is stored.
+// The tile's bias sits in LDS (bias_s, tile-local columns, staged with the first K-tile).
+// acc(i, j): the accumulator of block (i, j) of the wave's 128 x 64 sub-tile; rowmap(lr) its global row for sub-tile
+// row lr (0..127); tcol(lc) the tile-local column of sub-tile column lc (0..63; runs of 8 stay contiguous).
+// ------------------------------------------------------------------------------------------------
+template <int EPI, class Acc, class RowMap, class TCol>
+__device__ inline void gemm_epi_tr(Acc acc, bf16_t* img, const float* bias_s, int lane, RowMap rowmap, TCol tcol, int n0,
+                                   int M, int N, const EpiArgs& ea) {
+  const int fr = lane & 15, fq = lane >> 4;
+  float4 b4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    b4[j] = ea.bias ? *(const float4*)(bias_s + tcol(16 * j + 4 * fq)) : make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (EPI == TW_EPI_BF16 || EPI == TW_EPI_GELU_BF16 || EPI == TW_EPI_CROSSKV) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = 16 * i + fr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 a = acc(i, j);
+        float4 v = make_float4(a[0] + b4[j].x, a[1] + b4[j].y, a[2] + b4[j].z, a[3] + b4[j].w);
+        if constexpr (EPI == TW_EPI_GELU_BF16) v = gelu_erf4(v);
+        uint2 w;
+        w.x = pack_bf16x2(v.x, v.y);
+        w.y = pack_bf16x2(v.z, v.w);
+        *(uint2*)(img + row * 64 + (((4 * j + fq) ^ (row & 15)) << 2)) = w;
+      }
+    }
+    gb_epi_sync();
+#pragma unroll 4
+    for (int rr = 0; rr < 16; ++rr) {
+      const int row = rr * 8 + (lane >> 3), p = lane & 7, g = row & 15;
+      uint4 d = *(const uint4*)(img + row * 64 + ((p ^ (g >> 1)) << 3));
+      if (g & 1) d = make_uint4(d.z, d.w, d.x, d.y);  // (the XOR swapped the two 8-byte units)
+      const int m = rowmap(row), n = n0 + tcol(8 * p);
+      if (m >= M || n >= N) continue;
+      if (n + 7 < N) {
+        size_t idx;
+        if constexpr (EPI == TW_EPI_CROSSKV) {  // 8 | 64: the group stays inside one head's 64 contiguous dims
+          const int D = ea.kv_D, S = ea.kv_S;
+          const int l = n / (2 * D), rem = n - l * 2 * D;
+          const int kv = rem / D, hd = rem - kv * D;
+          const int b = m / S, s2 = m - b * S;
+          idx = ((((size_t)(l * 2 + kv) * ea.kv_B + b) * ea.kv_H + (hd >> 6)) * S + s2) * 64 + (hd & 63);
+        } else {
+          idx = (size_t)m * ea.ldo + n;
+        }
+        tw_st_enc<gb_nt_bit(EPI)>((bf16_t*)ea.out + idx, d);
+      } else {  // ragged right edge (tests only)
+        const uint32_t u[4] = {d.x, d.y, d.z, d.w};
+        EpiArgs e2 = ea;
+        e2.bias = nullptr;
+        for (int e = 0; e < 8 && n + e < N; ++e) {
+          const bf16_t h = (bf16_t)((u[e >> 1] >> (16 * (e & 1))) & 0xffffu);
+          if constexpr (EPI == TW_EPI_CROSSKV) {
+            epi_store<EPI>(e2, m, n + e, bf16_to_f32(h));
+          } else {
+            ((bf16_t*)ea.out)[(size_t)m * ea.ldo + n + e] = h;
+          }
+        }
+      }
+    }
+  } else {
+    constexpr bool PRE = EPI == TW_EPI_RESID_F32 || EPI == TW_EPI_GELU_POS_F32;
+    float4 ad[2][4];
+    auto load_ad = [&](int i, float4 (&dst)[4]) {
+      const int m = min(rowmap(16 * i + fr), M - 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + tcol(16 * j + 4 * fq);
+        dst[j] = epi_addend<EPI>(ea, m, n, n + 3 < N);
+      }
+    };
+    if constexpr (PRE) load_ad(0, ad[0]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr (PRE) {
+        if (i + 1 < 8) load_ad(i + 1, ad[(i + 1) & 1]);
+      }
+      const int m = rowmap(16 * i + fr);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 a = acc(i, j);
+        const float4 v = make_float4(a[0] + b4[j].x, a[1] + b4[j].y, a[2] + b4[j].z, a[3] + b4[j].w);
+        const int n = n0 + tcol(16 * j + 4 * fq);
+        if (m >= M || n >= N) continue;
+        if (n + 3 < N) {
+          if constexpr (PRE) epi_store4_pre<EPI>(ea, m, n, v, ad[i & 1][j]);
+          else epi_store4<EPI>(ea, m, n, N, v);
+        } else {
+          epi_store4<EPI>(ea, m, n, N, v);
+        }
+      }
+    }
+  }
+}
+
+// The tile's bias into LDS (tile-local columns 0..255, clamped at N - 1): wave 0 issues the loads beside the first
+// K-tile's DMA, writes them after that wait, and the barrier that publishes the K-tile publishes them too.
+__device__ inline void gemm_bias_load(const EpiArgs& ea, int n0, int N, float4& b) {
+  const int c = n0 + 4 * (threadIdx.x & 63);
+  if (ea.bias)
+    b = make_float4(ea.bias[min(c, N - 1)], ea.bias[min(c + 1, N - 1)], ea.bias[min(c + 2, N - 1)],
+                    ea.bias[min(c + 3, N - 1)]);
+}
+
+template <int EPI, bool TR>
 __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                      int M, int N, int K, int lda, int ldw, EpiArgs ea) {
   // [buf][A | W][256 rows x 64 k] bf16 = 128 KiB for the K loop; 8 x [64][68] f32 = 136 KiB after it
@@ -386,7 +538,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ 
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / GB_BK;
+  // (TR: the tile's bias in the LDS spare beyond the K loop's 128 KiB, staged with the first K-tile)
+  float* bias_s = (float*)(smem + 4 * GB_BM * GB_BK);
+  float4 bl = make_float4(0.f, 0.f, 0.f, 0.f);
   stage(0, 0);
+  if (TR && wid == 0) gemm_bias_load(ea, n0, N, bl);
+  if (TR && wid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *(float4*)(bias_s + 4 * lane) = bl;
+  }
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
@@ -407,13 +567,22 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const bf16_t* __restrict__ 
         const int row = wr * 128 + i * 16 + fr;
         const bf16x8 af = *(const bf16x8*)(As + row * GB_BK + ((kc ^ gb_swz(row)) << 3));
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) {
+          if constexpr (TR) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af, acc[i][j], 0, 0, 0);
+          else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+        }
       }
     }
     __syncthreads();  // vmcnt(0) (tile kt+1 landed) + lgkmcnt(0) + barrier
   }
 
-  gemm_epi_128x64<EPI>(acc, (float*)smem + wid * (64 * GB_EPI_LD), lane, m0 + wr * 128, n0 + wc * 64, M, N, ea);
+  if constexpr (TR) {
+    gemm_epi_tr<EPI>([&](int i, int j) { return acc[i][j]; }, smem + wid * (128 * 64), bias_s, lane,
+                     [&](int lr) { return m0 + wr * 128 + lr; }, [&](int lc) { return wc * 64 + lc; }, n0, M, N, ea);
+  } else {
+    gemm_epi_128x64<EPI>(acc, (float*)smem + wid * (64 * GB_EPI_LD), lane, m0 + wr * 128, n0 + wc * 64, M, N, ea,
+                         m0 + GB_BM <= M && n0 + GB_BN <= N);
+  }
 }
 
 // Buffer descriptor from values the compiler can prove wave-uniform (readfirstlane'd base halves and size): the
@@ -441,28 +610,36 @@ __device__ inline __amdgpu_buffer_rsrc_t tw_uniform_rsrc(const void* p, int byte
 #ifdef TW_GEMM_PROBE
 // Measurement build only (make probe -> scripts/exp/libtwhip_probe.so, scripts/exp/gemm_probe.py; never shipped):
 // per-workgroup timestamps of the large-M kernels' phases. Slots: 0 start, 1 first K-tile landed, 2 K loop done,
-// 3 epilogue stores retired (100 MHz s_memrealtime); 4, 5 core-clock s_memtime at start / K loop done; 6 HW_ID, 7 XCC_ID.
-__device__ unsigned long long tw_probe_ts[32768 * 8];
+// 3 epilogue stores retired (100 MHz s_memrealtime); 4, 5 core-clock s_memtime at start / K loop done; 6 HW_ID, 7 XCC_ID;
+// 8.. epilogue sub-phases of wave 0 (TW_PROBE_W: a vmcnt(0) first, so each names the data it waited for).
+#define TW_PROBE_SLOTS 16
+__device__ unsigned long long tw_probe_ts[32768 * TW_PROBE_SLOTS];
 #define TW_PROBE(slot)                                                                                     \
   do {                                                                                                     \
-    if (threadIdx.x == 0) tw_probe_ts[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime();         \
+    if (threadIdx.x == 0) tw_probe_ts[blockIdx.x * TW_PROBE_SLOTS + (slot)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #define TW_PROBE_CLK(slot)                                                                                 \
   do {                                                                                                     \
-    if (threadIdx.x == 0) tw_probe_ts[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memtime();            \
+    if (threadIdx.x == 0) tw_probe_ts[blockIdx.x * TW_PROBE_SLOTS + (slot)] = __builtin_amdgcn_s_memtime();  \
   } while (0)
 __device__ inline void tw_probe_ids() {
   if (threadIdx.x == 0) {
     unsigned hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    tw_probe_ts[blockIdx.x * 8 + 6] = hw;
-    tw_probe_ts[blockIdx.x * 8 + 7] = xcc;
+    tw_probe_ts[blockIdx.x * TW_PROBE_SLOTS + 6] = hw;
+    tw_probe_ts[blockIdx.x * TW_PROBE_SLOTS + 7] = xcc;
   }
 }
 extern "C" int tw_gemm_probe_read(unsigned long long* host, int nwg) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tw_probe_ts), (size_t)nwg * 8 * 8, 0, hipMemcpyDeviceToHost);
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tw_probe_ts), (size_t)nwg * TW_PROBE_SLOTS * 8, 0,
+                                  hipMemcpyDeviceToHost);
 }
+#define TW_PROBE_W(slot)                              \
+  do {                                                \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+    TW_PROBE(slot);                                   \
+  } while (0)
 #define TW_PROBE_END()                                \
   do {                                                \
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
@@ -473,6 +650,7 @@ extern "C" int tw_gemm_probe_read(unsigned long long* host, int nwg) {
 #define TW_PROBE(slot) do {} while (0)
 #define TW_PROBE_CLK(slot) do {} while (0)
 #define TW_PROBE_END() do {} while (0)
+#define TW_PROBE_W(slot) do {} while (0)
 __device__ inline void tw_probe_ids() {}
 #endif
 
@@ -485,7 +663,7 @@ __device__ inline void p8_vmcnt() {
   else static_assert(N == 0, "unsupported vmcnt");
 }
 
-template <int EPI>
+template <int EPI, bool TR>
 __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                     int M, int N, int K, int lda, int ldw, EpiArgs ea) {
   // K loop: 2 buffers x 4 half-tiles x 16 KiB = 128 KiB; epilogue: 8 x [64][68] f32 = 136 KiB (one array: a
@@ -577,7 +755,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[mh][nh][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bfr[j][kk], acc[mh][nh][i][j], 0, 0, 0);
+          acc[mh][nh][i][j] = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[mh][nh][i][j], 0, 0, 0)
+                                 : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bfr[j][kk], acc[mh][nh][i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   };
@@ -585,9 +764,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
   using I1 = std::integral_constant<int, 1>;
 
   const int nk = K / GB_BK;
+  // (TR: the tile's bias in the LDS spare beyond the K loop's 128 KiB, loaded beside the first K-tile's DMA)
+  float* bias_s = (float*)(smem + 8 * HT);
+  float4 bl = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int h = 0; h < 4; ++h) stage(0, h, 0);
+  if (TR && wid == 0) gemm_bias_load(ea, n0, N, bl);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (TR && wid == 0) *(float4*)(bias_s + 4 * lane) = bl;
+  if (TR) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   TW_PROBE(1);
   if (wr == 1) __builtin_amdgcn_s_barrier();  // ping-pong: group 1 one barrier behind
@@ -635,6 +820,14 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
   __syncthreads();
   TW_PROBE(2);
   TW_PROBE_CLK(5);
+  if constexpr (TR) {
+    TW_PROBE_W(8);
+    gemm_epi_tr<EPI>([&](int i, int j) { return acc[i >> 2][j >> 1][i & 3][j & 1]; }, smem + wid * (128 * 64), bias_s,
+                     lane, [&](int lr) { return m0 + 128 * (lr >> 6) + 64 * wr + (lr & 63); },
+                     [&](int lc) { return 128 * (lc >> 5) + 32 * wc + (lc & 31); }, n0, M, N, ea);
+    TW_PROBE_END();
+    return;
+  }
 
   // epilogue through LDS: per wave two 64-row halves (mh) of [64][64] f32 (cols = its two 32-col chunks), read
   // back 8 consecutive columns per lane (8 lanes per row) for 16-byte global stores
@@ -652,6 +845,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
     b1.w = ea.bias[min(ncol + 7, N - 1)];
   }
   float* wimg = (float*)smem + wid * (64 * GB_EPI_LD);
+  TW_PROBE_W(8);
   // RESID / GELU_POS: second operand loaded ahead, rows rr and rr + 4 sharing a slot (see k_gemm_big)
   constexpr bool PRE = EPI == TW_EPI_RESID_F32 || EPI == TW_EPI_GELU_POS_F32;
   const bool full = ncol + 7 < N;
@@ -678,6 +872,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
           for (int r = 0; r < 4; ++r)
             wimg[(i * 16 + fq * 4 + r) * GB_EPI_LD + nh * 32 + j * 16 + fr] = acc[mh][nh][i][j][r];
     gb_epi_sync();
+    TW_PROBE_W(9 + 2 * mh);
 #pragma unroll
     for (int rr = 0; rr < 8; ++rr) {
       const int lr = rr * 8 + (lane >> 3);
@@ -704,8 +899,312 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(const bf16_t* __restrict__ A
         if (m < M && ncol < N) epi_store8<EPI>(ea, m, ncol, N, v0, v1);
       }
     }
+    TW_PROBE_W(10 + 2 * mh);
   }
   TW_PROBE_END();
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_gemm_8pp: k_gemm_8p made persistent — one workgroup per CU walks tiles slot, slot + S, ... of its XCD's contiguous
+// range (the same XCD split and grouped order as k_gemm_8p's remap). The epilogue of a 256 x 256 tile costs ~7 us of a
+// ~40-us tile with no MFMA beside it (scripts/exp/gemm_probe.py, profiles/r05t_*): bias loads 0.8, LDS staging 0.6,
+// store issue and write-ack ~2.6 per half, with a fresh workgroup's first K-tile DMA (1.5) after it. Here, per tile:
+//   * the NEXT tile's first K-tile (and its bias) is DMA'd into buffer 0 before this tile's epilogue stores issue;
+//   * the epilogue stages through buffer 1 + the spare, in 32-row quarters (8 x [32][68] f32 = 68 KiB);
+//   * an interior bf16 tile (16 stores per wave) then waits vmcnt(16) only: vector memory operations retire in issue
+//     order, so the DMA ahead of the stores has landed while the stores may still drain — into the next tile's first
+//     K-tile, whose phases 1-3 need no wait (its four halves are in) and whose phase 4 waits for K-tile 1.
+// LDS: [0, 64K) buffer 0 | [64K, 128K) buffer 1 | staging [64K, 132K) between K loops | bias slots 2 x 1 KiB at 132K.
+// ------------------------------------------------------------------------------------------------
+// The read-back of 4 rows x 8 columns of an epilogue image as one asm block (8 ds_read_b128, then lgkmcnt(0)): while
+// the next tile's LDS DMA is in flight, hipcc would otherwise put a vmcnt(0) before every ds_read of the same
+// __shared__ array (it cannot tell the image from the DMA's buffer), draining the epilogue's own stores each time.
+__device__ inline void gb_read_rows4(const float* img, float4 (&v)[4][2]) {
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)img;
+  asm volatile(
+      "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:16\n\t"
+      "ds_read_b128 %2, %8 offset:%9\n\tds_read_b128 %3, %8 offset:%10\n\t"
+      "ds_read_b128 %4, %8 offset:%11\n\tds_read_b128 %5, %8 offset:%12\n\t"
+      "ds_read_b128 %6, %8 offset:%13\n\tds_read_b128 %7, %8 offset:%14\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=v"(v[0][0]), "=v"(v[0][1]), "=v"(v[1][0]), "=v"(v[1][1]), "=v"(v[2][0]), "=v"(v[2][1]), "=v"(v[3][0]),
+        "=v"(v[3][1])
+      : "v"(a), "i"(8 * GB_EPI_LD * 4), "i"(8 * GB_EPI_LD * 4 + 16), "i"(16 * GB_EPI_LD * 4),
+        "i"(16 * GB_EPI_LD * 4 + 16), "i"(24 * GB_EPI_LD * 4), "i"(24 * GB_EPI_LD * 4 + 16)
+      : "memory");
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_gemm_8pp(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                     int M, int N, int K, int lda, int ldw, EpiArgs ea) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[8 * 64 * GB_EPI_LD * 2];
+  constexpr int HT = 128 * GB_BK;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntm = (M + GB_BM - 1) / GB_BM, ntn = (N + GB_BN - 1) / GB_BN;
+  const int nwg = ntm * ntn;
+  const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8, S = gridDim.x / 8;
+  const int q8 = nwg / 8, r8 = nwg % 8;
+  const int cnt = q8 + (xcd < r8 ? 1 : 0);
+  const int base = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  if (slot >= cnt) return;  // (workgroup-uniform, before any barrier)
+  const int wr = wid >> 2, wc = wid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  float* const bias_sl = (float*)(smem + 4 * HT) + 8 * 32 * GB_EPI_LD;  // 2 x 256 f32
+
+  __amdgpu_buffer_rsrc_t rs[4];
+  auto set_tile = [&](int tile, int& m0, int& n0) {
+    int tm, tn;
+    tw_tile_grouped(tile, ntm, ntn, ea.group_m, tm, tn);
+    m0 = tm * GB_BM;
+    n0 = tn * GB_BN;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int r0 = (h < 2 ? m0 : n0) + 128 * (h & 1), lim = h < 2 ? M : N, ld = h < 2 ? lda : ldw;
+      const int rows = max(0, min(128, lim - r0));
+      rs[h] = tw_uniform_rsrc((h < 2 ? A : W) + (size_t)r0 * ld, rows ? ((rows - 1) * ld + K) * 2 : 0);
+    }
+  };
+  unsigned voff[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 8 * (2 * wid + i) + (lane >> 3);
+    const int ch = (lane & 7) ^ gb_swz(row);
+    voff[0][i] = (unsigned)(row * lda + ch * 8) * 2u;
+    voff[1][i] = (unsigned)(row * ldw + ch * 8) * 2u;
+  }
+  auto stage = [&](int buf, int h, int k0) {
+    bf16_t* dst = smem + (buf * 4 + h) * HT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs[h], (lds_void_t*)(dst + 8 * (2 * wid + i) * GB_BK), 16,
+                                               voff[h >> 1][i], (unsigned)k0 * 2u, 0, 0);
+  };
+  // the tile's 256 bias values (columns clamped into [0, N - 4]; host: N % 4 == 0, bias 16-byte aligned) by wave 0
+  auto stage_bias = [&](int sl, int n0) {
+    if (ea.bias && wid == 0)
+      __builtin_amdgcn_global_load_lds((const void*)(ea.bias + min(n0 + 4 * lane, N - 4)),
+                                       (lds_void_t*)(bias_sl + 256 * sl), 16, 0, 0);
+  };
+
+  bf16x8 af[4][2], bfr[2][2];
+  auto readA = [&](int buf, int mh) {
+    const bf16_t* As = smem + (buf * 4 + mh) * HT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int row = 64 * wr + 16 * i + fr, kc = 4 * kk + fq;
+        af[i][kk] = *(const bf16x8*)(As + row * GB_BK + ((kc ^ gb_swz(row)) << 3));
+      }
+  };
+  auto readB = [&](int buf, int nh) {
+    const bf16_t* Bs = smem + (buf * 4 + 2 + nh) * HT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int row = 32 * wc + 16 * j + fr, kc = 4 * kk + fq;
+        bfr[j][kk] = *(const bf16x8*)(Bs + row * GB_BK + ((kc ^ gb_swz(row)) << 3));
+      }
+  };
+  f32x4 acc[2][2][4][2];
+  auto mfma_q = [&](auto MH, auto NH) {
+    constexpr int mh = decltype(MH)::value, nh = decltype(NH)::value;
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mh][nh][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bfr[j][kk], acc[mh][nh][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  // one K-tile = 4 phases (k_gemm_8p's); NXT: stage K-tile t+1; FIRST: K-tile 0, all four halves already waited for
+  // (no phase 1 / 2 waits: they would also drain the previous tile's epilogue stores)
+  auto ktile = [&](int t, auto NXT, auto FIRST) {
+    constexpr bool nxt = decltype(NXT)::value, first = decltype(FIRST)::value;
+    const int buf = t & 1, nb = buf ^ 1, kn = (t + 1) * GB_BK;
+    readB(buf, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    readA(buf, 0);
+    if constexpr (nxt) {
+      stage(nb, 0, kn);
+      if constexpr (!first) p8_vmcnt<4>();
+    } else if constexpr (!first) {
+      p8_vmcnt<2>();
+    }
+    mfma_q(I0{}, I0{});
+    readB(buf, 1);
+    if constexpr (nxt) {
+      stage(nb, 2, kn);
+      if constexpr (!first) p8_vmcnt<4>();
+    } else if constexpr (!first) {
+      p8_vmcnt<0>();
+    }
+    mfma_q(I0{}, I1{});
+    readA(buf, 1);
+    if constexpr (nxt) stage(nb, 3, kn);
+    mfma_q(I1{}, I1{});
+    readB(buf, 0);
+    if constexpr (nxt) {
+      stage(nb, 1, kn);
+      p8_vmcnt<4>();  // A0, B0 of K-tile t+1 (and, for K-tile 0, the previous tile's stores ahead of them)
+    }
+    mfma_q(I1{}, I0{});
+  };
+  using BT = std::integral_constant<bool, true>;
+  using BF = std::integral_constant<bool, false>;
+
+  constexpr bool PRE = EPI == TW_EPI_RESID_F32 || EPI == TW_EPI_GELU_POS_F32;
+  constexpr bool BF16OUT = EPI == TW_EPI_BF16 || EPI == TW_EPI_GELU_BF16 || EPI == TW_EPI_CROSSKV;
+  // epilogue through LDS in 32-row quarters (mh, ih) of the wave's 128 x 64 piece, 8 consecutive columns per lane in
+  // the read-back (8 lanes per row) for 16-byte global stores; bias from the tile's LDS slot
+  auto epilogue = [&](int m0, int n0, const float* bias_s) {
+    const int rc = (lane & 7) * 8;
+    const int lcol = rc < 32 ? 32 * wc + rc : 128 + 32 * wc + rc - 32;
+    const int ncol = n0 + lcol;
+    float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+    if (ea.bias) {
+      b0 = *(const float4*)(bias_s + lcol);
+      b1 = *(const float4*)(bias_s + lcol + 4);
+    }
+    float* wimg = (float*)(smem + 4 * HT) + wid * (32 * GB_EPI_LD);
+    const bool full = ncol + 7 < N;
+    auto stage_q = [&](int q, float4 (&vv)[4][2]) {  // quarter q of the wave's piece -> rows (lane >> 3) + 8 rr
+      const int mh = q >> 1, ih = q & 1;
+      if (q) gb_epi_sync();
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              wimg[(ii * 16 + fq * 4 + r) * GB_EPI_LD + nh * 32 + j * 16 + fr] = acc[mh][nh][2 * ih + ii][j][r];
+      gb_epi_sync();
+      gb_read_rows4(wimg + (lane >> 3) * GB_EPI_LD + rc, vv);
+    };
+    if constexpr (PRE) {
+      if (m0 + GB_BM <= M && n0 + GB_BN <= N) {
+        // interior tile: straight-line code (no lane conditions), so hipcc counts its waits instead of draining vmcnt
+        // to 0 before every addend use — which made each row group's stores retire before the next group's math
+        // (one drain per quarter remains: the quarter's addend loads are issued after the previous quarter's stores)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int mr = m0 + 128 * (q >> 1) + 64 * wr + 32 * (q & 1) + (lane >> 3);
+          float4 ad[4][2];
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            ad[rr][0] = epi_addend<EPI>(ea, mr + rr * 8, ncol, true);
+            ad[rr][1] = epi_addend<EPI>(ea, mr + rr * 8, ncol + 4, true);
+          }
+          float4 vv[4][2];
+          stage_q(q, vv);
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            float4 v0 = vv[rr][0], v1 = vv[rr][1];
+            v0.x += b0.x; v0.y += b0.y; v0.z += b0.z; v0.w += b0.w;
+            v1.x += b1.x; v1.y += b1.y; v1.z += b1.z; v1.w += b1.w;
+            epi_store4_pre<EPI>(ea, mr + rr * 8, ncol, v0, ad[rr][0]);
+            epi_store4_pre<EPI>(ea, mr + rr * 8, ncol + 4, v1, ad[rr][1]);
+          }
+        }
+        return;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int mh = q >> 1, ih = q & 1;
+      const int mrow0 = m0 + 128 * mh + 64 * wr + 32 * ih;
+      float4 ad[4][2];
+      if constexpr (PRE) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int mq = min(mrow0 + rr * 8 + (lane >> 3), M - 1);
+          ad[rr][0] = epi_addend<EPI>(ea, mq, ncol, full);
+          ad[rr][1] = epi_addend<EPI>(ea, mq, ncol + 4, full);
+        }
+      }
+      float4 vv[4][2];  // rows rr * 8 + (lane >> 3), rr = 0..3 (8 rows = 8 * GB_EPI_LD floats apart)
+      stage_q(q, vv);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int lr = rr * 8 + (lane >> 3);
+        const int m = mrow0 + lr;
+        float4 v0 = vv[rr][0], v1 = vv[rr][1];
+        v0.x += b0.x; v0.y += b0.y; v0.z += b0.z; v0.w += b0.w;
+        v1.x += b1.x; v1.y += b1.y; v1.z += b1.z; v1.w += b1.w;
+        if constexpr (PRE) {
+          if (full) {
+            if (m < M) {
+              epi_store4_pre<EPI>(ea, m, ncol, v0, ad[rr][0]);
+              epi_store4_pre<EPI>(ea, m, ncol + 4, v1, ad[rr][1]);
+            }
+          } else if (m < M && ncol < N) {
+            epi_store8<EPI>(ea, m, ncol, N, v0, v1);
+          }
+        } else {
+          if (m < M && ncol < N) epi_store8<EPI>(ea, m, ncol, N, v0, v1);
+        }
+      }
+    }
+  };
+
+  const int nk = K / GB_BK;
+  int local = slot, m0, n0;
+  set_tile(base + local, m0, n0);
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage(0, h, 0);
+  stage_bias(0, n0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // ping-pong: group 1 one barrier behind
+  for (int it = 0;; ++it) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (nk == 1) {
+      ktile(0, BF{}, BT{});
+    } else {
+      ktile(0, BT{}, BT{});
+      for (int t = 1; t + 1 < nk; ++t) ktile(t, BT{}, BF{});
+      ktile(nk - 1, BF{}, BF{});
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();  // realign the groups
+    __syncthreads();
+    const int nlocal = local + S;
+    const bool has_next = nlocal < cnt;
+    const int cm0 = m0, cn0 = n0;
+    if (has_next) {  // the next tile's first K-tile + bias, ahead of this tile's stores
+      set_tile(base + nlocal, m0, n0);
+#pragma unroll
+      for (int h = 0; h < 4; ++h) stage(0, h, 0);
+      stage_bias((it + 1) & 1, n0);
+    }
+    epilogue(cm0, cn0, bias_sl + 256 * (it & 1));
+    if (!has_next) break;
+    if (BF16OUT && cm0 + GB_BM <= M && cn0 + GB_BN <= N)
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // exactly 16 stores per wave follow the DMA
+    else if (PRE && cm0 + GB_BM <= M && cn0 + GB_BN <= N)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // the last quarter's 8 stores end the interior epilogue
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();
+    local = nlocal;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1293,10 +1792,18 @@ static int launch_gemm(const bf16_t* A, const bf16_t* W, int M, int N, int K, in
     launch_skinny<EPI>(A, W, M, N, K, lda, ldw, ea, 1, s);
   } else {
     const unsigned nwg = tw_cdiv(M, GB_BM) * tw_cdiv(N, GB_BN);
-    if (tw_gemm_kernel == 5)
-      hipLaunchKernelGGL(k_gemm_8p<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
+    // k_gemm_8pp stages the bias by 16-byte DMA: N % 4 == 0 and a 16-byte aligned bias (else k_gemm_8p)
+    if (tw_gemm_kernel == 6 && N % 4 == 0 && N >= 4 && ((uintptr_t)ea.bias & 15) == 0)
+      hipLaunchKernelGGL(k_gemm_8pp<EPI>, dim3(std::min<unsigned>(tw_persistent_grid(), (nwg + 7) / 8 * 8)), dim3(512),
+                         0, s, A, W, M, N, K, lda, ldw, ea);
+    else if (tw_gemm_kernel >= 5 && tw_gemm_tr)
+      hipLaunchKernelGGL((k_gemm_8p<EPI, true>), dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
+    else if (tw_gemm_kernel >= 5)
+      hipLaunchKernelGGL((k_gemm_8p<EPI, false>), dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
+    else if (tw_gemm_tr)
+      hipLaunchKernelGGL((k_gemm_big<EPI, true>), dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
     else
-      hipLaunchKernelGGL(k_gemm_big<EPI>, dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
+      hipLaunchKernelGGL((k_gemm_big<EPI, false>), dim3(nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, ea);
   }
   return tw_check_launch("tw_gemm_bf16");
 }

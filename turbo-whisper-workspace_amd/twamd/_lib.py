@@ -47,7 +47,7 @@ EXPORTED = (
     "tw_gemv_set_wide_slices", "tw_vorbis_probe", "tw_vorbis_decode", "tw_vorbis_imdct",
     "tw_layernorm_set_lds_pad", "tw_gemv_set_variant",
     "tw_gemm_f32", "tw_layernorm_f32", "tw_im2col_conv1_f32", "tw_im2col_conv2_f32", "tw_embed_decoder_f32",
-    "tw_attn_encoder_f32", "tw_attn_decode_self_f32", "tw_attn_decode_cross_f32",
+    "tw_attn_encoder_f32", "tw_attn_decode_self_f32", "tw_attn_decode_cross_f32", "tw_gemm_set_epilogue",
 )
 
 
@@ -111,6 +111,7 @@ _SIGS = {
     "tw_conv2_gemm": ([_P, _I, _I, _P, _P, _P, _P, _P], _I),
     "tw_gemm_bf16": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _P], _I),
     "tw_layernorm": ([_P, _P, _P, _I, _I, _F, _P, _P], _I),
+    "tw_gemm_set_epilogue": ([_I], _I),
     "tw_gemm_f32": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _P], _I),
     "tw_layernorm_f32": ([_P, _P, _P, _I, _I, _F, _P, _P], _I),
     "tw_im2col_conv1_f32": ([_P, _I, _L, _P, _P, _P, _I, _I, _P, _P], _I),

@@ -14,7 +14,7 @@ import torch
 
 from . import _lib
 from .frontend import N_FRAMES
-from .engine import LN_EPS, S_ENC, VIEW_ROWS, DecView, WhisperEngine
+from .engine import LN_EPS, S_ENC, VIEW_ROWS, DecView, WhisperEngine, on_engine_streams
 
 __all__ = ["WhisperEngineF32"]
 
@@ -84,6 +84,7 @@ class WhisperEngineF32(WhisperEngine):
         self._enc_end(sync, slot)
 
     # ------------------------------------------------------------------ decoder
+    @on_engine_streams
     def decoder_step(self, R: int, with_logits: bool = True, v: Optional[DecView] = None, r_enc: Optional[int] = None,
                      pre_embedded: bool = False) -> None:
         """WhisperDecoder.forward for one token per row at f32 (as WhisperEngine.decoder_step: ids[b] at pos[b] ->
