@@ -105,7 +105,9 @@ extern "C" int tw_gemv_set_wide_slices(int kw) {
 // workgroup waits for GEMM workgroups to retire (q/k/v GEMV beside k_gemm_8p: 33.6 us per launch at 8, 11.5 at 4).
 static constexpr int tw_gemv_max_kw = 4;
 // The decoder layer GEMVs' kernel (tw_gemv_set_variant): 0 = k_gemv_pc (two column groups per wave, batches of 5
-// steps), 1 = k_gemv_q (one column group per wave, its whole K-slice in flight)
+// steps), 1 = k_gemv_q (one column group per wave, its whole K-slice in flight) for 17..32 rows; k_gemv_pc at <= 16
+// rows and at 64 (config 5's decode passes alone: 198.8-198.9 vs 201.7-202.5 ms per step with k_gemv_q, three
+// interleaved pairs, profiles/r05aa_c5_gemv_ab.txt)
 static int tw_gemv_kernel = 0;
 extern "C" int tw_gemv_set_variant(int v) {
   TW_REQUIRE(v == 0 || v == 1, "tw_gemv_set_variant: v=%d (0 or 1)", v);
@@ -1767,7 +1769,7 @@ static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
   if constexpr (EPI == TW_EPI_BF16 || EPI == TW_EPI_PARTIAL || EPI == TW_EPI_GELU_PACKED) {
     // the layer GEMVs as column-group pairs (k_gemv_pc): a third fewer vector-memory instructions per weight byte
     // (k_gemv_q from 17 rows: at <= 16 one m-tile leaves its waves too little work, step 328 vs 323 us at 15 rows)
-    if (tw_gemv_kernel == 1 && M > 16 && launch_gemv_q<EPI, APACK>(A, lda, Wp, M, N, K, ea, splits, s)) return;
+    if (tw_gemv_kernel == 1 && M > 16 && M <= 32 && launch_gemv_q<EPI, APACK>(A, lda, Wp, M, N, K, ea, splits, s)) return;
     const long pairs = tw_cdiv(tw_cdiv(N, 16), 2) * (long)splits;
     if (pairs * 2 < 1024 && steps >= 8 * 4) launch_gemv_pc<EPI, 4, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
     else launch_gemv_pc<EPI, 2, APACK>(A, lda, Wp, M, N, K, ea, splits, s);
@@ -2096,26 +2098,32 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
   const int wr = wid >> 2, wc = wid & 3;
   const int fr = lane & 15, fq = lane >> 4;
 
-  const uint8_t* gsrc[4][2];
+  // operands through one buffer descriptor per half-tile (as k_gemm_8p: 32-bit per-lane offsets instead of eight 64-bit
+  // pointers — the registers this kernel's spill margin needs; rows past M / N read as zeros, never stored)
+  __amdgpu_buffer_rsrc_t rs[4];
 #pragma unroll
-  for (int h = 0; h < 4; ++h)
+  for (int h = 0; h < 4; ++h) {
+    const int r0 = (h < 2 ? m0 : n0) + 128 * (h & 1), lim = h < 2 ? M : N, ld = h < 2 ? lda : ldw;
+    const int rows = max(0, min(128, lim - r0));
+    rs[h] = tw_uniform_rsrc((h < 2 ? A : W) + (size_t)r0 * ld, rows ? (rows - 1) * ld + K : 0);
+  }
+  unsigned voff[2][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = 8 * (2 * wid + i) + (lane >> 3);
-      const int ch = (lane & 7) ^ gb_swz(row);
-      gsrc[h][i] = h < 2 ? A + (size_t)min(m0 + 128 * h + row, M - 1) * lda + ch * 16
-                         : W + (size_t)min(n0 + 128 * (h - 2) + row, N - 1) * ldw + ch * 16;
-    }
+  for (int i = 0; i < 2; ++i) {
+    const int row = 8 * (2 * wid + i) + (lane >> 3);
+    const int ch = (lane & 7) ^ gb_swz(row);
+    voff[0][i] = (unsigned)(row * lda + ch * 16);
+    voff[1][i] = (unsigned)(row * ldw + ch * 16);
+  }
   // scale DMA: wave w < 4 -> A scale dwords of rows 64w + lane, w >= 4 -> W rows 64(w-4) + lane
   const uint8_t* gsc = wid < 4 ? Sa + (size_t)(m0 + 64 * wid + lane) * 4 : Sw + (size_t)(n0 + 64 * (wid - 4) + lane) * 4;
   const size_t gsc_step = (size_t)(wid < 4 ? Mp : Np) * 4;
   auto stage = [&](int buf, int h, int kt) {
     uint8_t* dst = smem + (buf * 4 + h) * HT;
-    const int k0 = kt * MX_BK;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(gsrc[h][i] + k0), (lds_void_t*)(dst + 8 * (2 * wid + i) * MX_BK),
-                                       16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs[h], (lds_void_t*)(dst + 8 * (2 * wid + i) * MX_BK), 16,
+                                               voff[h >> 1][i], (unsigned)(kt * MX_BK), 0, 0);
   };
   auto stage_sc = [&](int buf, int kt) {
     __builtin_amdgcn_global_load_lds((const void*)(gsc + kt * gsc_step),
@@ -2123,7 +2131,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
   };
 
   i32x8 af[4], bfr[2];
-  int sa[2][4], sb[2][2];
+  int sap[2], sbp;
   auto frag = [&](const uint8_t* base, int row) {
     const uint8_t* p = base + row * MX_BK;
     const int4 lo = *(const int4*)(p + ((fq ^ gb_swz(row)) << 4));
@@ -2140,16 +2148,22 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
 #pragma unroll
     for (int j = 0; j < 2; ++j) bfr[j] = frag(Bs, 32 * wc + 16 * j + fr);
   };
-  auto readS = [&](int buf) {  // this lane's scale bytes: (tile row, K block fq) of every fragment of the K-tile
+  auto readS = [&](int buf) {  // this lane's scale bytes: (tile row, K block fq) of every fragment of the K-tile,
+    // packed four to a register (the MFMA's op_sel picks the byte): 3 VGPRs instead of 12, the kernel's spill margin
     const uint8_t* S = smem + MX8_SC + buf * 2048;
 #pragma unroll
-    for (int mh = 0; mh < 2; ++mh)
+    for (int mh = 0; mh < 2; ++mh) {
+      uint32_t p = 0;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sa[mh][i] = S[(128 * mh + 64 * wr + 16 * i + fr) * 4 + fq];
+      for (int i = 0; i < 4; ++i) p |= (uint32_t)S[(128 * mh + 64 * wr + 16 * i + fr) * 4 + fq] << (8 * i);
+      sap[mh] = (int)p;
+    }
+    uint32_t q = 0;
 #pragma unroll
     for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) sb[nh][j] = S[1024 + (128 * nh + 32 * wc + 16 * j + fr) * 4 + fq];
+      for (int j = 0; j < 2; ++j) q |= (uint32_t)S[1024 + (128 * nh + 32 * wc + 16 * j + fr) * 4 + fq] << (8 * (2 * nh + j));
+    sbp = (int)q;
   };
   f32x4 acc[2][2][4][2];
 #pragma unroll
@@ -2165,12 +2179,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
     __builtin_amdgcn_s_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[mh][nh][i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[mh][nh][i][j], 0, 0, 0,
-                                                                             sa[mh][i], 0, sb[nh][j]);
+#define TW_MXS(i, j)                                                                                          \
+  acc[mh][nh][i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[mh][nh][i][j], 0, 0, i, \
+                                                                       sap[mh], 2 * nh + j, sbp)
+    TW_MXS(0, 0); TW_MXS(0, 1); TW_MXS(1, 0); TW_MXS(1, 1); TW_MXS(2, 0); TW_MXS(2, 1); TW_MXS(3, 0); TW_MXS(3, 1);
+#undef TW_MXS
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   };
@@ -2288,18 +2301,19 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
   }
 }
 
-// tw_gemm_mx kernel choice: 0 = by shape (default), 1 = k_gemm_mx, 8 = k_gemm_8p_mx (tw_gemm_mx_set_variant, A/B).
-// Measured (scripts/gemm_bench.py, B = 24 and 64 windows): the 8-phase kernel wins on the long-K / wide-N FFN
-// shapes (fc1 +10-14 %, fc2 +14-18 %) and on o_proj at M = 96000 (+11 %); the 2-stage kernel on qkv (+3-5 %) and
-// on o_proj at M = 36000 (+2 %).
+// tw_gemm_mx kernel choice: 0 = default (k_gemm_8p_mx), 1 = k_gemm_mx, 8 = k_gemm_8p_mx (tw_gemm_mx_set_variant, A/B).
+// Round 4 picked by shape (k_gemm_mx on q/k/v and on o_proj at M = 36000). Since k_gemm_8p_mx packs its scale bytes
+// four to a register (op_sel) and streams through buffer descriptors, its spills went 136 -> 84 bytes (GELU_MX: 36 ->
+// 0) and it wins every encoder shape: q/k/v +3-4 %, o_proj +7-17 %, fc1 +19 %, fc2 +18 % at M = 96000 and 36000
+// (scripts/gemm_mx_ab.py, profiles/r05y_gemm_mx_ab.txt).
 static int tw_gemm_mx_variant = 0;
 extern "C" int tw_gemm_mx_set_variant(int v) {
   tw_gemm_mx_variant = (v == 1 || v == 8) ? v : 0;
   return 0;
 }
 static inline bool mx_use_8p(int M, int N, int K) {
-  if (tw_gemm_mx_variant) return tw_gemm_mx_variant == 8;
-  return N >= 4096 || K >= 4096 || (N <= 1280 && M >= 65536);
+  (void)M; (void)N; (void)K;
+  return tw_gemm_mx_variant != 1;
 }
 
 template <int EPI>

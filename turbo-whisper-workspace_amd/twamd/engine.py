@@ -930,9 +930,10 @@ class WhisperEngine:
     dec_beside_wide_kw = int(os.environ.get("TW_DEC_BESIDE_WIDE_KW", "1"))
 
     # The layer GEMVs' kernel (tw_gemv_set_variant) for a decode pass alone: k_gemv_q (1: one column group per wave, the
-    # whole K-slice in flight; the library keeps k_gemv_pc at <= 16 rows) — captured step 393.5 -> 384.8 us at 24 rows,
-    # 682.6 -> 651.1 at 64 (profiles/r05i_decode_chain.txt); beside an encoder chunk k_gemv_pc (0): 87.86 vs 88.45 ms
-    # per bench step (two interleaved pairs, profiles/r05i_gemv_ab.txt). TW_DEC_ALONE_GEMV / _BESIDE_GEMV for A/B.
+    # whole K-slice in flight; the library keeps k_gemv_pc at <= 16 rows and above 32) — captured step 393.5 -> 384.8
+    # us at 24 rows (profiles/r05i_decode_chain.txt; at 64 rows 682.6 -> 651.1 in the captured step, but config 5's
+    # bench 201.7-202.5 vs 198.8-198.9 ms with k_gemv_pc, profiles/r05aa_c5_gemv_ab.txt); beside an encoder chunk
+    # k_gemv_pc (0): 87.86 vs 88.45 ms per bench step (profiles/r05i_gemv_ab.txt). TW_DEC_ALONE_GEMV / _BESIDE_GEMV.
     dec_alone_gemv = int(os.environ.get("TW_DEC_ALONE_GEMV", "1"))
     dec_beside_gemv = int(os.environ.get("TW_DEC_BESIDE_GEMV", "0"))
 
