@@ -212,8 +212,10 @@ def main():
                                     "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 1) if v[2] > 0 else None}
                 for k, v in fam.items()}
     # the bf16 family runs as k_gemm_big beside a decode and as k_gemm_8p alone (engine._set_gemm_context)
-    traffic, traffic_src = measured_traffic(("k_" + dom,) if fp8 else ("k_gemm_big", "k_gemm_8p"), fp8)
-    mfma_busy, mfma_src = measured_mfma(("k_" + dom,) if fp8 else ("k_gemm_big", "k_gemm_8p"), fp8)
+    # (the MX family: k_gemm_8p_mx on every encoder shape since round 5, k_gemm_mx before and on request)
+    fam_k = ("k_gemm_mx", "k_gemm_8p_mx") if fp8 else ("k_gemm_big", "k_gemm_8p", "k_gemm_8pp")
+    traffic, traffic_src = measured_traffic(fam_k, fp8)
+    mfma_busy, mfma_src = measured_mfma(fam_k, fp8)
 
     # secondary (HBM-bound) kernel: decoder cross-attention, timed on one eager decode pass outside the timed
     # region (the timed decode steps replay a hipGraph, which has no room for events)
@@ -248,8 +250,8 @@ def main():
                    "global_batch": int(audio_s // 30), "seq_len": 3000, "parallelism": f"chunk-dp{world}",
                    "decode_tokens_per_window": T, "mean_tokens_out": float(np.mean(n_tok))},
         "roofline": {"bound": "mfma",
-                     "kernel": ("k_gemm_mx (encoder q/k/v/o + fc1/fc2, MX fp8 MFMA)" if fp8 else
-                                "k_gemm_big / k_gemm_8p (all encoder/conv/cross-KV projections, bf16 MFMA)"),
+                     "kernel": ("k_gemm_8p_mx / k_gemm_mx (encoder q/k/v/o + fc1/fc2, MX fp8 MFMA)" if fp8 else
+                                "k_gemm_big / k_gemm_8p / k_gemm_8pp (all encoder/conv/cross-KV projections, bf16 MFMA)"),
                      "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "traffic_source": traffic_src, "mfma_busy_pct": mfma_busy, "mfma_source": mfma_src,
