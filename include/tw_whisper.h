@@ -265,6 +265,9 @@ int tw_gemv_set_variant(int v);
  * transposed accumulators (the MFMA as W . A^T: bias / GELU in registers, bf16 outputs staged as packed bf16, f32
  * outputs stored from registers). The same sums either way (A/B switch; results agree to the output rounding). */
 int tw_gemm_set_epilogue(int tr);
+/* Workgroups of the persistent large-M GEMM (tw_gemm_set_variant(6)): 0 = one per CU, else n (a multiple of 8, one per
+ * CU on n / 8 CUs of every XCD) — the rest of the CUs stay free for other queues' kernels. */
+int tw_gemm_set_persistent_grid(int n);
 /* tw_resid_layernorm with the normalised rows written as a packed activation (M <= 64, D % 32 == 0). */
 int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
                               const float* beta, int M, int D, float eps, uint16_t* out, void* stream);

@@ -118,9 +118,17 @@ extern "C" int tw_gemm_set_variant(int v) {
   tw_gemm_kernel = (v & 15) == 5 ? 5 : (v & 15) == 6 ? 6 : 1;
   return 0;
 }
-// persistent grid of k_gemm_8pp: the device's CUs, a multiple of the 8 XCDs (blocks b, b + 8, ... share one XCD)
+// persistent grid of k_gemm_8pp: the device's CUs, a multiple of the 8 XCDs (blocks b, b + 8, ... share one XCD), or
+// fewer (tw_gemm_set_persistent_grid: a GEMM queued beside a decode that leaves CUs to the decoder's kernels)
+static int tw_pgrid_override = 0;
+extern "C" int tw_gemm_set_persistent_grid(int n) {
+  TW_REQUIRE(n == 0 || (n >= 8 && n % 8 == 0), "tw_gemm_set_persistent_grid: %d (0 = all CUs, else a multiple of 8)", n);
+  tw_pgrid_override = n;
+  return 0;
+}
 static int tw_persistent_grid() {
   static int g = 0;
+  if (tw_pgrid_override) return tw_pgrid_override;
   if (!g) {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||

@@ -48,6 +48,7 @@ EXPORTED = (
     "tw_layernorm_set_lds_pad", "tw_gemv_set_variant",
     "tw_gemm_f32", "tw_layernorm_f32", "tw_im2col_conv1_f32", "tw_im2col_conv2_f32", "tw_embed_decoder_f32",
     "tw_attn_encoder_f32", "tw_attn_decode_self_f32", "tw_attn_decode_cross_f32", "tw_gemm_set_epilogue",
+    "tw_gemm_set_persistent_grid",
 )
 
 
@@ -112,6 +113,7 @@ _SIGS = {
     "tw_gemm_bf16": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _P], _I),
     "tw_layernorm": ([_P, _P, _P, _I, _I, _F, _P, _P], _I),
     "tw_gemm_set_epilogue": ([_I], _I),
+    "tw_gemm_set_persistent_grid": ([_I], _I),
     "tw_gemm_f32": ([_P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _P], _I),
     "tw_layernorm_f32": ([_P, _P, _P, _I, _I, _F, _P, _P], _I),
     "tw_im2col_conv1_f32": ([_P, _I, _L, _P, _P, _P, _I, _I, _P, _P], _I),

@@ -612,13 +612,18 @@ class WhisperEngine:
     # next tile's first K-tile DMA'd under the epilogue: encoder layer 1404 -> 1332 us at 24 windows,
     # profiles/r05v_gemm_variant_ab.txt), 5 = k_gemm_8p (TW_GEMM_ALONE for A/B)
     gemm_alone = int(os.environ.get("TW_GEMM_ALONE", "6"))
+    # beside a decode: k_gemm_big (1: 184 VGPRs, so a decoder wave fits on every SIMD of every CU), or the persistent
+    # kernel on TW_GEMM_BESIDE_CUS CUs (6: the other CUs left to the decoder's kernels) — TW_GEMM_BESIDE for A/B
+    gemm_beside = int(os.environ.get("TW_GEMM_BESIDE", "1"))
+    gemm_beside_cus = int(os.environ.get("TW_GEMM_BESIDE_CUS", "224"))
 
     def _set_gemm_context(self, alone: bool) -> None:
         """Encoder kernels for the chunk about to be queued (see __init__): large-M GEMM gemm_alone alone, 1 beside a decode;
         the encoder attention capped at one workgroup per CU beside a decode (tw_attn_set_lds_pad: the decoder's
         kernels then find free wave slots; measured decoder GEMV 21.9 -> 5.6 us per launch beside it, bench step
         112.1 -> 108.5 ms), uncapped alone (the cap costs the attention itself 22 %)."""
-        _lib.call("tw_gemm_set_variant", self.gemm_alone if alone else 1)
+        _lib.call("tw_gemm_set_variant", self.gemm_alone if alone else self.gemm_beside)
+        _lib.call("tw_gemm_set_persistent_grid", 0 if alone else self.gemm_beside_cus)
         _lib.call("tw_attn_set_variant", self.attn_kernel[0 if alone else 1])
         _lib.call("tw_attn_set_lds_pad", self.attn_pad[0 if alone else 1])
         _lib.call("tw_layernorm_set_lds_pad", self.ln_pad[0 if alone else 1])
