@@ -78,7 +78,7 @@ def _wait(ev: "torch.cuda.Event") -> None:
 
 def _pad256(n: int) -> int:
     return (n + 255) // 256 * 256
-DEC_SPLITS = 4   # split-K factor of the decoder's d_model-wide projections (out_proj, fc2)
+DEC_SPLITS = 4   # split-K factor of the decoder's d_model-wide projections (out_proj, fc2); 2 or 8: bench 93.0-93.4 / 92.8-95.6 vs 90.4-90.5 ms (profiles/r05ag_dec_splits_ab.txt)
 # rows per decoder view: the packed GEMVs stream each weight byte once for up to 64 rows (four 16-row m-tiles; config
 # 5's 64 windows, beam-5 over 12 windows); more rows run as consecutive views
 VIEW_ROWS = 64
