@@ -1,7 +1,7 @@
 """Measurement (not a bench line): the MX fp8 GEMM kernels (tw_gemm_mx_set_variant 1 k_gemm_mx, 8 k_gemm_8p_mx) on the encoder shapes at 64 windows (M = 96000, BASELINE config 5) and 24 windows, interleaved,
 median of the per-rep means. One JSON line per case.
 
-    python scripts/gemm_mx_ab.py [--variants 1,8]
+    python scripts/gemm_mx_ab.py [--variants 1,8] [--lib path/to/libtwhip.so]
 """
 import argparse
 import json
@@ -23,9 +23,10 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--m", default="96000,36000")
+    ap.add_argument("--lib", default=None, help="another build of libtwhip.so (A/B across builds)")
     a = ap.parse_args()
     variants = [int(x) for x in a.variants.split(",")]
-    _lib.load()
+    _lib.load(a.lib) if a.lib else _lib.load()
     s = torch.cuda.current_stream().cuda_stream
     E = _lib
     shapes = [("qkv", 3840, 1280, E.TW_EPI_BF16), ("o_proj", 1280, 1280, E.TW_EPI_RESID_F32),

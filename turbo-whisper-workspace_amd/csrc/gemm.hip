@@ -2123,9 +2123,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
     voff[0][i] = (unsigned)(row * lda + ch * 16);
     voff[1][i] = (unsigned)(row * ldw + ch * 16);
   }
-  // scale DMA: wave w < 4 -> A scale dwords of rows 64w + lane, w >= 4 -> W rows 64(w-4) + lane
-  const uint8_t* gsc = wid < 4 ? Sa + (size_t)(m0 + 64 * wid + lane) * 4 : Sw + (size_t)(n0 + 64 * (wid - 4) + lane) * 4;
-  const size_t gsc_step = (size_t)(wid < 4 ? Mp : Np) * 4;
+  // scale DMA: wave w < 4 -> A scale dwords of rows 64w + lane, w >= 4 -> W rows 64(w-4) + lane, through one buffer
+  // descriptor per wave. (It was a global_load_lds: hipcc then drained vmcnt to 0 before every ds_read of the K loop —
+  // four full drains per K-tile, the next K-tile's DMA latency exposed in every phase — which it does not do for
+  // buffer_load ... lds.)
+  const int nk = K / MX_BK;
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+  const unsigned gsc_step = (unsigned)(wu < 4 ? Mp : Np) * 4u;
+  const __amdgpu_buffer_rsrc_t rsc = tw_uniform_rsrc(
+      wu < 4 ? Sa + (size_t)(m0 + 64 * wu) * 4 : Sw + (size_t)(n0 + 64 * (wu - 4)) * 4, (int)((nk - 1) * gsc_step + 256u));
   auto stage = [&](int buf, int h, int kt) {
     uint8_t* dst = smem + (buf * 4 + h) * HT;
 #pragma unroll
@@ -2134,16 +2140,21 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
                                                voff[h >> 1][i], (unsigned)(kt * MX_BK), 0, 0);
   };
   auto stage_sc = [&](int buf, int kt) {
-    __builtin_amdgcn_global_load_lds((const void*)(gsc + kt * gsc_step),
-                                     (lds_void_t*)(smem + MX8_SC + buf * 2048 + wid * 256), 4, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsc, (lds_void_t*)(smem + MX8_SC + buf * 2048 + wu * 256), 4,
+                                             (unsigned)lane * 4u, (unsigned)kt * gsc_step, 0, 0);
   };
 
   i32x8 af[4], bfr[2];
   int sap[2], sbp;
   auto frag = [&](const uint8_t* base, int row) {
     const uint8_t* p = base + row * MX_BK;
-    const int4 lo = *(const int4*)(p + ((fq ^ gb_swz(row)) << 4));
-    const int4 hi = *(const int4*)(p + (((fq + 4) ^ gb_swz(row)) << 4));
+    // (loaded as bf16x8 values, as k_gemm_8p's fragments, and only then bit-cast: with int4 loads — also what
+    // __builtin_bit_cast of the dereference itself emits — hipcc drained vmcnt to 0 before the fragment reads of every
+    // phase, exposing the next K-tile's DMA latency four times per K-tile; with bf16x8 loads it relies on the kernel's
+    // own counted waits, as in k_gemm_8p)
+    const bf16x8 lo8 = *(const bf16x8*)(p + ((fq ^ gb_swz(row)) << 4));
+    const bf16x8 hi8 = *(const bf16x8*)(p + (((fq + 4) ^ gb_swz(row)) << 4));
+    const int4 lo = __builtin_bit_cast(int4, lo8), hi = __builtin_bit_cast(int4, hi8);
     return (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
   };
   auto readA = [&](int buf, int mh) {
@@ -2198,7 +2209,6 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
 
-  const int nk = K / MX_BK;
 #pragma unroll
   for (int h = 0; h < 4; ++h) stage(0, h, 0);
   stage_sc(0, 0);
