@@ -49,9 +49,12 @@ extern "C" int tw_quant_mx(const bf16_t* src, int rows, int K, int ld, uint8_t* 
   return tw_check_launch("tw_quant_mx");
 }
 
-// LayerNorm as k_layernorm (one wave per row, the row kept in registers), storing MX fp8: lane l holds columns
-// 4(l + 64 i) .. +3, so the 8 consecutive lanes of a group cover one 32-column block.
+// LayerNorm as k_layernorm (one wave per row, the row kept in registers, sized to it by NC = ceil(D / 256) float4
+// chunks per lane; gamma / beta loaded with the row), storing MX fp8: lane l holds columns 4(l + 64 i) .. +3, so the 8
+// consecutive lanes of a group cover one 32-column block, whose absmax is three DPP lane moves on the VALU
+// (mx_group8_max_dpp) instead of three ds_bpermute round trips.
 #define LNQ_MAXC 16
+template <int NC>
 __global__ __launch_bounds__(256) void k_layernorm_mx(const float* __restrict__ x, const float* __restrict__ g,
                                                       const float* __restrict__ bta, int M, int D, float eps,
                                                       uint8_t* __restrict__ out, uint8_t* __restrict__ scales,
@@ -61,22 +64,25 @@ __global__ __launch_bounds__(256) void k_layernorm_mx(const float* __restrict__ 
   if (row >= M) return;  // wave-uniform
   const int nc = D >> 2;
   const float4* xr = (const float4*)(x + (size_t)row * D);
-  float4 v[LNQ_MAXC];
-  float s = 0.f;
+  float4 v[NC], gg[NC], bb[NC];
 #pragma unroll
-  for (int i = 0; i < LNQ_MAXC; ++i) {
-    const int c = lane + 64 * i;
-    if (64 * i < nc) {
-      v[i] = xr[min(c, nc - 1)];
-      if (c < nc) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  for (int i = 0; i < NC; ++i) {
+    if (64 * i < nc) {  // wave-uniform trip bound; the lane index is clamped, not branched on
+      const int cc = min(lane + 64 * i, nc - 1);
+      v[i] = xr[cc];
+      gg[i] = ((const float4*)g)[cc];
+      bb[i] = ((const float4*)bta)[cc];
     }
   }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+    if (64 * i < nc && lane + 64 * i < nc) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
   const float mean = wave_sum(s) / (float)D;
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < LNQ_MAXC; ++i) {
-    const int c = lane + 64 * i;
-    if (64 * i < nc && c < nc) {
+  for (int i = 0; i < NC; ++i) {
+    if (64 * i < nc && lane + 64 * i < nc) {
       const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, d = v[i].w - mean;
       q += (a * a + b * b) + (cc * cc + d * d);
     }
@@ -84,18 +90,18 @@ __global__ __launch_bounds__(256) void k_layernorm_mx(const float* __restrict__ 
   const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
   uint32_t* orow = (uint32_t*)(out + (size_t)row * D);
 #pragma unroll
-  for (int i = 0; i < LNQ_MAXC; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const int c = lane + 64 * i;
-    if (64 * i < nc) {  // wave-uniform: every lane of a group takes part in the shuffles (D % 32 == 0)
-      const int cc = min(c, nc - 1);
-      const float4 gg = ((const float4*)g)[cc], bb = ((const float4*)bta)[cc];
-      const float y0 = (v[i].x - mean) * rstd * gg.x + bb.x, y1 = (v[i].y - mean) * rstd * gg.y + bb.y;
-      const float y2 = (v[i].z - mean) * rstd * gg.z + bb.z, y3 = (v[i].w - mean) * rstd * gg.w + bb.w;
-      const uint32_t sb = mx_scale_byte(mx_group8_max(abs4max(y0, y1, y2, y3)));
+    if (64 * i < nc) {  // wave-uniform: every lane of a group takes part in the lane moves (D % 32 == 0)
+      const float y0 = (v[i].x - mean) * rstd * gg[i].x + bb[i].x, y1 = (v[i].y - mean) * rstd * gg[i].y + bb[i].y;
+      const float y2 = (v[i].z - mean) * rstd * gg[i].z + bb[i].z, y3 = (v[i].w - mean) * rstd * gg[i].w + bb[i].w;
+      const uint32_t sb = mx_scale_byte(mx_group8_max_dpp(abs4max(y0, y1, y2, y3)));
       const uint32_t w = mx_pack4(y0, y1, y2, y3, mx_inv_scale(sb));
       if (c < nc) {
         orow[c] = w;
+#ifndef TW_LNQ_PROBE_NOSCALE  // (probe build only: what the scattered scale-byte stores cost)
         if ((c & 7) == 0) scales[tw_mx_sidx(row, c >> 3, rows_pad)] = (uint8_t)sb;
+#endif
       }
     }
   }
@@ -107,7 +113,19 @@ extern "C" int tw_layernorm_mx(const float* x, const float* gamma, const float* 
   TW_REQUIRE(D % 128 == 0 && D <= 256 * LNQ_MAXC, "tw_layernorm_mx: D=%d must be a multiple of 128 and <= %d", D,
              256 * LNQ_MAXC);
   TW_REQUIRE(rows_pad >= M, "tw_layernorm_mx: rows_pad %d < M %d", rows_pad, M);
-  hipLaunchKernelGGL(k_layernorm_mx, dim3(tw_cdiv(M, 4)), dim3(256), 0, (hipStream_t)stream, x, gamma, beta, M, D,
-                     eps, out, scales, rows_pad);
+  const dim3 grid(tw_cdiv(M, 4)), blk(256);
+  hipStream_t st = (hipStream_t)stream;
+#define TW_LNQ(nc) hipLaunchKernelGGL(k_layernorm_mx<nc>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out, scales, rows_pad)
+  switch (tw_cdiv(D, 256)) {
+    case 1: TW_LNQ(1); break;
+    case 2: TW_LNQ(2); break;
+    case 3: TW_LNQ(3); break;
+    case 4: TW_LNQ(4); break;
+    case 5: TW_LNQ(5); break;
+    case 6: TW_LNQ(6); break;
+    case 7: case 8: TW_LNQ(8); break;
+    default: TW_LNQ(LNQ_MAXC); break;
+  }
+#undef TW_LNQ
   return tw_check_launch("tw_layernorm_mx");
 }

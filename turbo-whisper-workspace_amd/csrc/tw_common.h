@@ -128,6 +128,15 @@ __device__ inline float mx_group8_max(float v) {
   v = fmaxf(v, __shfl_xor(v, 4, 64));
   return v;
 }
+// the same by DPP lane moves (VALU instructions instead of ds_bpermute round trips on the LDS pipeline): xor 1 and
+// xor 2 as quad permutes, then the half-row mirror (lane i <-> 7 - i) once every quad holds its own maximum
+__device__ inline float mx_dpp_max(float v, int v2) { return fmaxf(v, __builtin_bit_cast(float, v2)); }
+__device__ inline float mx_group8_max_dpp(float v) {
+  v = mx_dpp_max(v, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+  v = mx_dpp_max(v, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+  v = mx_dpp_max(v, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));  // half mirror
+  return v;
+}
 __device__ inline float abs4max(float a, float b, float c, float d) {
   return fmaxf(fmaxf(fabsf(a), fabsf(b)), fmaxf(fabsf(c), fabsf(d)));
 }
