@@ -1,6 +1,6 @@
 """A/B timing of the encoder attention kernels at B=24 windows, S=1500, 20 heads (interleaved, one process), with
 the LDS cap the engine applies beside a running decode (pad 4) and without it (pad 0).
-    python scripts/attn_bench.py [variants...]"""
+    python scripts/attn_bench.py [--lib path/to/libtwhip.so] [variants...]"""
 import os
 import sys
 
@@ -10,10 +10,15 @@ import torch  # noqa: E402
 
 from twamd import _lib  # noqa: E402
 
-_lib.load()
+args = sys.argv[1:]
+if args[:1] == ["--lib"]:  # another build (A/B across builds)
+    _lib.load(args[1])
+    args = args[2:]
+else:
+    _lib.load()
 B, S, H = 24, 1500, 20
 D = H * 64
-VAR = [int(v) for v in sys.argv[1:]] or [16, 32, 8]
+VAR = [int(v) for v in args] or [16, 32, 8]
 qkv = (torch.randn(B * S, 3 * D, device="cuda")).to(torch.bfloat16)
 qkv[:, :D] = (qkv[:, :D].float() * 0.125).to(torch.bfloat16)
 out = torch.empty(B * S, D, dtype=torch.bfloat16, device="cuda")

@@ -2301,8 +2301,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
         v0 = gelu_erf4(v0);
         v1 = gelu_erf4(v1);
         float a = fmaxf(abs4max(v0.x, v0.y, v0.z, v0.w), abs4max(v1.x, v1.y, v1.z, v1.w));
-        a = fmaxf(a, __shfl_xor(a, 1, 64));
-        a = fmaxf(a, __shfl_xor(a, 2, 64));
+        a = mx_group4_max_dpp(a);  // (quad permutes on the VALU, not two ds_bpermute round trips)
         const uint32_t sbyte = mx_scale_byte(a);
         const float inv = mx_inv_scale(sbyte);
         uint2 w;

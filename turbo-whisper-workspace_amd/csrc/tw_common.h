@@ -131,6 +131,11 @@ __device__ inline float mx_group8_max(float v) {
 // the same by DPP lane moves (VALU instructions instead of ds_bpermute round trips on the LDS pipeline): xor 1 and
 // xor 2 as quad permutes, then the half-row mirror (lane i <-> 7 - i) once every quad holds its own maximum
 __device__ inline float mx_dpp_max(float v, int v2) { return fmaxf(v, __builtin_bit_cast(float, v2)); }
+__device__ inline float mx_group4_max_dpp(float v) {  // over the 4 lanes of a quad (xor 1, 2)
+  v = mx_dpp_max(v, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+  v = mx_dpp_max(v, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+  return v;
+}
 __device__ inline float mx_group8_max_dpp(float v) {
   v = mx_dpp_max(v, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
   v = mx_dpp_max(v, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
