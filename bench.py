@@ -179,12 +179,8 @@ def main():
         # next batch's encoder in slot k % 2, the last one alone in slot (n - 1) % 2. A warmup that did not meet every
         # (beside/alone, slot) the timed run meets leaves graph captures inside the timed region (~3.7 ms per step at
         # K = 20, W = 5; ~15 ms at the defaults: profiles/r05ai_bench_bisect.txt): up to 4 more untimed batches then.
-        def graph_keys(n):
-            return {("beside", k % 2) for k in range(n - 1)} | ({("alone", (n - 1) % 2)} if n else set())
-
-        need, have = graph_keys(a.steps), graph_keys(a.warmup)
-        if not need <= have:
-            extra_warm = next(n for n in range(1, 5) if need <= have | graph_keys(n))
+        extra_warm = warmup_completion(a.steps, a.warmup)
+        if extra_warm:
             run(extra_warm)
     torch.cuda.synchronize()
     if world > 1:
@@ -330,6 +326,24 @@ def parity_vs_golden(eng, B, T, model, fp8):
     return ok, {"tau": tp.TAU, "reference": "transformers fp32 CPU, tests/golden/turbo.npz + turbo_bench.npz",
                 "free_decode": det, "teacher_forced": forced, "positions_checked": forced["positions_checked"],
                 "worst_d_logit": forced["worst_d_logit"]}
+
+
+def decode_graph_keys(n: int) -> set:
+    """The captured decode graphs a run_batches call of n batches meets: batch k decodes beside the next batch's
+    encoder in pipeline slot k % 2, the last batch alone in slot (n - 1) % 2 (engine graph keys carry the slot and the
+    pass context)."""
+    return {("beside", k % 2) for k in range(n - 1)} | ({("alone", (n - 1) % 2)} if n else set())
+
+
+def warmup_completion(steps: int, warmup: int) -> int:
+    """Untimed batches to run after the warmup so that every decode graph the timed run of `steps` batches meets has
+    been captured (0 if the warmup already met them all, or when there is no warmup)."""
+    if warmup <= 0:
+        return 0
+    need, have = decode_graph_keys(steps), decode_graph_keys(warmup)
+    if need <= have:
+        return 0
+    return next(n for n in range(1, 5) if need <= have | decode_graph_keys(n))
 
 
 def profile_order(path: str):

@@ -61,3 +61,25 @@ def test_profile_order_is_by_round_then_tag_length():
     got = [os.path.basename(p) for p in sorted(names, key=bench.profile_order)]
     assert got == ["r04t_traffic.json", "r04ae_traffic.json", "r05b_traffic.json", "r05z_c5_traffic.json",
                    "r05ab_traffic.json", "r06a_traffic.json"]
+
+
+@pytest.mark.parametrize("steps,warmup,extra", [
+    (20, 5, 2),   # the driver's run: warmup ends alone in slot 0, the timed run alone in slot 1
+    (5, 2, 3),    # the default: warmup met beside-slot-0 only
+    (20, 4, 0),   # warmup already met every graph of the timed run
+    (4, 4, 0),
+    (1, 1, 0),
+    (2, 1, 2),
+    (3, 0, 0),    # no warmup: nothing to complete
+])
+def test_warmup_completion(steps, warmup, extra):
+    assert bench.warmup_completion(steps, warmup) == extra
+
+
+def test_warmup_completion_covers_every_timed_graph():
+    for steps in range(1, 12):
+        for warmup in range(1, 8):
+            extra = bench.warmup_completion(steps, warmup)
+            have = bench.decode_graph_keys(warmup) | bench.decode_graph_keys(extra)
+            assert bench.decode_graph_keys(steps) <= have, (steps, warmup, extra)
+            assert extra <= 4
