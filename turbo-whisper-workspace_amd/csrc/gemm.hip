@@ -1959,35 +1959,42 @@ __global__ __launch_bounds__(512, 1) void k_gemm_mx(const uint8_t* __restrict__ 
   tw_tile_grouped(wgid, ntm, ntn, ea.group_m, tm, tn);
   const int m0 = tm * GB_BM, n0 = tn * GB_BN;
 
-  const uint8_t* ga[4];
-  const uint8_t* gw[4];
+  // operands through one buffer descriptor per operand tile (32-bit per-lane offsets instead of eight 64-bit
+  // pointers: the registers that keep this kernel beside a decode; rows past M / N read as zeros, never stored)
+  const int rows_a = max(0, min(GB_BM, M - m0)), rows_w = max(0, min(GB_BN, N - n0));
+  const __amdgpu_buffer_rsrc_t ra = tw_uniform_rsrc(A + (size_t)m0 * lda, rows_a ? (rows_a - 1) * lda + K : 0);
+  const __amdgpu_buffer_rsrc_t rw = tw_uniform_rsrc(W + (size_t)n0 * ldw, rows_w ? (rows_w - 1) * ldw + K : 0);
+  unsigned va[4], vw[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = 8 * (4 * wid + i) + (lane >> 3);
     const int ch = (lane & 7) ^ gb_swz(row);
-    ga[i] = A + (size_t)min(m0 + row, M - 1) * lda + ch * 16;
-    gw[i] = W + (size_t)min(n0 + row, N - 1) * ldw + ch * 16;
+    va[i] = (unsigned)(row * lda + ch * 16);
+    vw[i] = (unsigned)(row * ldw + ch * 16);
   }
   // scales of K-step kt: rows m0..m0+255 of [K/128][Mp][4] are 1 KiB contiguous (Mp, Np: multiples of 256)
-  const uint8_t* gs = wid == 0 ? Sa + (size_t)m0 * 4 + lane * 16 : Sw + (size_t)n0 * 4 + lane * 16;
-  const size_t gs_step = (size_t)(wid == 0 ? Mp : Np) * 4;
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+  const unsigned gs_step = (unsigned)(wu == 0 ? Mp : Np) * 4u;
+  const __amdgpu_buffer_rsrc_t rsc =
+      tw_uniform_rsrc(wu == 0 ? Sa + (size_t)m0 * 4 : Sw + (size_t)n0 * 4, (int)((K / MX_BK - 1) * gs_step + 1024u));
   auto stage = [&](int buf, int kt) {
     uint8_t* As = smem + buf * MX_STAGE;
     uint8_t* Ws = As + MX_TILE;
-    const int k0 = kt * MX_BK;
+    const unsigned k0 = (unsigned)(kt * MX_BK);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int rb = 8 * (4 * wid + i) * MX_BK;
-      __builtin_amdgcn_global_load_lds((const void*)(ga[i] + k0), (lds_void_t*)(As + rb), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(gw[i] + k0), (lds_void_t*)(Ws + rb), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(As + rb), 16, va[i], k0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void_t*)(Ws + rb), 16, vw[i], k0, 0, 0);
     }
-    if (wid < 2)
-      __builtin_amdgcn_global_load_lds((const void*)(gs + kt * gs_step), (lds_void_t*)(As + 2 * MX_TILE + wid * 1024),
-                                       16, 0, 0);
+    if (wu < 2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsc, (lds_void_t*)(As + 2 * MX_TILE + wu * 1024), 16,
+                                               (unsigned)lane * 16u, (unsigned)kt * gs_step, 0, 0);
   };
 
   const int wr = wid >> 2, wc = wid & 3;
   const int fr = lane & 15, fq = lane >> 4;
+  const int lane_lo = fr * MX_BK + ((fq ^ ((fr >> 1) & 7)) << 4), lane_hi = fr * MX_BK + (((fq + 4) ^ ((fr >> 1) & 7)) << 4);
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -2004,29 +2011,44 @@ __global__ __launch_bounds__(512, 1) void k_gemm_mx(const uint8_t* __restrict__ 
     const uint8_t* Ws = As + MX_TILE;
     const uint8_t* SAs = As + 2 * MX_TILE;
     const uint8_t* SWs = SAs + 1024;
-    i32x8 bfr[4];
-    int sb[4];
+    // (fragments loaded as bf16x8 values and bit-cast, as k_gemm_8p_mx: int4 loads make hipcc drain vmcnt before
+    // them; the four W scale bytes packed into one register, picked by the MFMA's op_sel)
+    // (every fragment row of this lane is 16 k + fr: the chunk swizzle gb_swz(row) = (fr >> 1) & 7 is the same for
+    // all of them, so a fragment's address is one lane offset plus a compile-time row offset — no per-fragment
+    // address registers held across the loop)
+    auto frag = [&](const uint8_t* p, int r) {
+      (void)r;
+      const bf16x8 lo8 = *(const bf16x8*)(p + lane_lo);
+      const bf16x8 hi8 = *(const bf16x8*)(p + lane_hi);
+      const int4 lo = __builtin_bit_cast(int4, lo8), hi = __builtin_bit_cast(int4, hi8);
+      return (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    };
+    uint32_t sbp = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = wc * 64 + j * 16 + fr;
-      const uint8_t* p = Ws + col * MX_BK;
-      const int4 lo = *(const int4*)(p + ((fq ^ gb_swz(col)) << 4));
-      const int4 hi = *(const int4*)(p + (((fq + 4) ^ gb_swz(col)) << 4));
-      bfr[j] = (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      sb[j] = SWs[col * 4 + fq];
-    }
+    for (int j = 0; j < 4; ++j) sbp |= (uint32_t)SWs[(wc * 64 + j * 16 + fr) * 4 + fq] << (8 * j);
+    // two passes over the A fragments, two W fragments each: 16 instead of 32 W-fragment registers (the
+    // co-residency budget: <= 192 VGPRs leaves every SIMD a decoder wave of <= 128 beside two GEMM waves), at twice
+    // the A-fragment LDS reads (~60 % of the LDS bandwidth at full MFMA rate)
+    auto pass = [&](auto JH) {
+      constexpr int jh = decltype(JH)::value;
+      i32x8 bfr[2];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = wr * 128 + i * 16 + fr;
-      const uint8_t* p = As + row * MX_BK;
-      const int4 lo = *(const int4*)(p + ((fq ^ gb_swz(row)) << 4));
-      const int4 hi = *(const int4*)(p + (((fq + 4) ^ gb_swz(row)) << 4));
-      const i32x8 af = (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      const int sa = SAs[row * 4 + fq];
+      for (int jj = 0; jj < 2; ++jj) {
+        bfr[jj] = frag(Ws + (wc * 64 + (2 * jh + jj) * 16) * MX_BK, 0);
+      }
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[j], acc[i][j], 0, 0, 0, sa, 0, sb[j]);
-    }
+      for (int i = 0; i < 8; ++i) {
+        const i32x8 af = frag(As + (wr * 128 + i * 16) * MX_BK, 0);
+        const int sa = SAs[(wr * 128 + i * 16 + fr) * 4 + fq];
+        acc[i][2 * jh] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[0], acc[i][2 * jh], 0, 0, 0, sa,
+                                                                          2 * jh, (int)sbp);
+        acc[i][2 * jh + 1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[1], acc[i][2 * jh + 1], 0, 0, 0,
+                                                                              sa, 2 * jh + 1, (int)sbp);
+        __builtin_amdgcn_sched_barrier(0);  // (one A fragment live at a time)
+      }
+    };
+    pass(std::integral_constant<int, 0>{});
+    pass(std::integral_constant<int, 1>{});
     __syncthreads();
   }
 

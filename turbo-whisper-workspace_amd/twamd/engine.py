@@ -616,6 +616,10 @@ class WhisperEngine:
     # kernel on TW_GEMM_BESIDE_CUS CUs (6: the other CUs left to the decoder's kernels) — TW_GEMM_BESIDE for A/B
     gemm_beside = int(os.environ.get("TW_GEMM_BESIDE", "1"))
     gemm_beside_cus = int(os.environ.get("TW_GEMM_BESIDE_CUS", "224"))
+    # MX fp8 GEMM kernel (tw_gemm_mx_set_variant) of config 5's encoder chunks beside a decode: 8 = k_gemm_8p_mx (256
+    # VGPRs: no decoder wave fits beside its two waves per SIMD), 1 = k_gemm_mx (182 VGPRs, a decoder wave of <= 128
+    # on every SIMD beside it) — TW_MX_BESIDE for A/B; alone always the default (k_gemm_8p_mx)
+    mx_beside = int(os.environ.get("TW_MX_BESIDE", "8"))
 
     def _set_gemm_context(self, alone: bool) -> None:
         """Encoder kernels for the chunk about to be queued (see __init__): large-M GEMM gemm_alone alone, 1 beside a decode;
@@ -627,6 +631,8 @@ class WhisperEngine:
         _lib.call("tw_attn_set_variant", self.attn_kernel[0 if alone else 1])
         _lib.call("tw_attn_set_lds_pad", self.attn_pad[0 if alone else 1])
         _lib.call("tw_layernorm_set_lds_pad", self.ln_pad[0 if alone else 1])
+        if self.enc_fp8:
+            _lib.call("tw_gemm_mx_set_variant", 0 if alone else self.mx_beside)
 
     def _encode_steps(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True,
                       alone: bool = True):
