@@ -161,8 +161,9 @@ int tw_layernorm_set_lds_pad(int kib);
 int tw_gemm_mx(const uint8_t* A, const uint8_t* Sa, const uint8_t* W, const uint8_t* Sw, int M, int N, int K, int lda,
                int ldw, int Mp, int Np, int epi, void* out, int ldo, const float* bias, uint8_t* sout, int sout_rows,
                void* stream);
-/* Process-wide (returns 0): tw_gemm_mx's kernel, 0 = default (k_gemm_8p_mx), 1 = k_gemm_mx (2-stage),
- * 8 = k_gemm_8p_mx (8-phase ping-pong); the forced forms exist so that tests cover both kernels on every shape. */
+/* Process-wide (returns 0): tw_gemm_mx's kernel, 0 = default (by shape: k_gemm_mx for q/k/v, N = 3 K; k_gemm_8p_mx
+ * otherwise), 1 = k_gemm_mx (2-stage), 8 = k_gemm_8p_mx (8-phase ping-pong); the forced forms exist so that tests
+ * cover both kernels on every shape. */
 int tw_gemm_mx_set_variant(int v);
 /* bf16 src[rows][ld] -> MX fp8 dst[rows][K] + scales (K % 128 == 0). Encoder weights once at load; the
  * attention output before out_proj (modeling_whisper.py:350-356). */

@@ -2340,19 +2340,21 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p_mx(const uint8_t* __restrict
   }
 }
 
-// tw_gemm_mx kernel choice: 0 = default (k_gemm_8p_mx), 1 = k_gemm_mx, 8 = k_gemm_8p_mx (tw_gemm_mx_set_variant, A/B).
-// Round 4 picked by shape (k_gemm_mx on q/k/v and on o_proj at M = 36000). Since k_gemm_8p_mx packs its scale bytes
-// four to a register (op_sel) and streams through buffer descriptors, its spills went 136 -> 84 bytes (GELU_MX: 36 ->
-// 0) and it wins every encoder shape: q/k/v +3-4 %, o_proj +7-17 %, fc1 +19 %, fc2 +18 % at M = 96000 and 36000
-// (scripts/gemm_mx_ab.py, profiles/r05y_gemm_mx_ab.txt).
+// tw_gemm_mx kernel choice: 0 = default, by shape — k_gemm_mx for the q/k/v shape (N = 3 K), k_gemm_8p_mx for the
+// rest; 1 = k_gemm_mx, 8 = k_gemm_8p_mx (tw_gemm_mx_set_variant, forced forms for A/B and tests). Since k_gemm_8p_mx
+// packs its scale bytes four to a register (op_sel) and streams through buffer descriptors (spills 136 -> 84 bytes)
+// it won every encoder shape (profiles/r05y_gemm_mx_ab.txt); since k_gemm_mx did the same and took 182 VGPRs it wins
+// q/k/v again (573 vs 596 us at M = 96000, profiles/r05ba_mx_beside_ab.txt): config 5 183.2 -> 180.7 ms per step with
+// the shape rule (profiles/r05bb_mx_shape_rule_ab.txt).
 static int tw_gemm_mx_variant = 0;
 extern "C" int tw_gemm_mx_set_variant(int v) {
   tw_gemm_mx_variant = (v == 1 || v == 8) ? v : 0;
   return 0;
 }
 static inline bool mx_use_8p(int M, int N, int K) {
-  (void)M; (void)N; (void)K;
-  return tw_gemm_mx_variant != 1;
+  (void)M;
+  if (tw_gemm_mx_variant == 0) return N != 3 * K;
+  return tw_gemm_mx_variant == 8;
 }
 
 template <int EPI>

@@ -616,10 +616,13 @@ class WhisperEngine:
     # kernel on TW_GEMM_BESIDE_CUS CUs (6: the other CUs left to the decoder's kernels) — TW_GEMM_BESIDE for A/B
     gemm_beside = int(os.environ.get("TW_GEMM_BESIDE", "1"))
     gemm_beside_cus = int(os.environ.get("TW_GEMM_BESIDE_CUS", "224"))
-    # MX fp8 GEMM kernel (tw_gemm_mx_set_variant) of config 5's encoder chunks beside a decode: 8 = k_gemm_8p_mx (256
-    # VGPRs: no decoder wave fits beside its two waves per SIMD), 1 = k_gemm_mx (182 VGPRs, a decoder wave of <= 128
-    # on every SIMD beside it) — TW_MX_BESIDE for A/B; alone always the default (k_gemm_8p_mx)
-    mx_beside = int(os.environ.get("TW_MX_BESIDE", "8"))
+    # MX fp8 GEMM kernel (tw_gemm_mx_set_variant) of config 5's encoder chunks alone / beside a decode: 0 = the
+    # library's shape rule (k_gemm_mx for q/k/v, k_gemm_8p_mx for the rest: 180.7 vs 183.2 ms per step,
+    # profiles/r05bb_mx_shape_rule_ab.txt), 8 = k_gemm_8p_mx everywhere (256 VGPRs), 1 = k_gemm_mx everywhere (182
+    # VGPRs, so a decoder wave fits beside it — which does not pay: 188.6 vs 183.4 ms, profiles/r05ba_mx_beside_ab.txt)
+    # — TW_MX_ALONE / TW_MX_BESIDE for A/B
+    mx_alone = int(os.environ.get("TW_MX_ALONE", "0"))
+    mx_beside = int(os.environ.get("TW_MX_BESIDE", "0"))
 
     def _set_gemm_context(self, alone: bool) -> None:
         """Encoder kernels for the chunk about to be queued (see __init__): large-M GEMM gemm_alone alone, 1 beside a decode;
@@ -632,7 +635,7 @@ class WhisperEngine:
         _lib.call("tw_attn_set_lds_pad", self.attn_pad[0 if alone else 1])
         _lib.call("tw_layernorm_set_lds_pad", self.ln_pad[0 if alone else 1])
         if self.enc_fp8:
-            _lib.call("tw_gemm_mx_set_variant", 0 if alone else self.mx_beside)
+            _lib.call("tw_gemm_mx_set_variant", self.mx_alone if alone else self.mx_beside)
 
     def _encode_steps(self, R: int, row_map=True, seek=True, slot: Optional[int] = None, sync: bool = True,
                       alone: bool = True):
