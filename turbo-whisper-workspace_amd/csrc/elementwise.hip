@@ -61,6 +61,7 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, 
 // the LayerNorm's workgroups per CU so that their waves leave registers and LDS for a decoder wave on every SIMD
 // (uncapped, ~6 LayerNorm waves of 78 registers fill a SIMD) — the encoder attention's cap (tw_attn_set_lds_pad), here.
 static int tw_ln_lds_pad_kib = 0;
+size_t tw_layernorm_lds_pad_bytes() { return (size_t)tw_ln_lds_pad_kib * 1024; }  // (also tw_layernorm_mx's cap)
 extern "C" int tw_layernorm_set_lds_pad(int kib) {
   TW_REQUIRE(kib >= 0 && kib <= 64, "tw_layernorm_set_lds_pad: %d KiB (0..64)", kib);
   tw_ln_lds_pad_kib = kib;

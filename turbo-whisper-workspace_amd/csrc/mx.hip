@@ -107,6 +107,8 @@ __global__ __launch_bounds__(256) void k_layernorm_mx(const float* __restrict__ 
   }
 }
 
+size_t tw_layernorm_lds_pad_bytes();  // elementwise.hip: tw_layernorm_set_lds_pad's cap, beside a decode
+
 extern "C" int tw_layernorm_mx(const float* x, const float* gamma, const float* beta, int M, int D, float eps,
                                uint8_t* out, uint8_t* scales, int rows_pad, void* stream) {
   TW_REQUIRE(x && gamma && beta && out && scales && M > 0, "tw_layernorm_mx: bad args");
@@ -115,7 +117,8 @@ extern "C" int tw_layernorm_mx(const float* x, const float* gamma, const float* 
   TW_REQUIRE(rows_pad >= M, "tw_layernorm_mx: rows_pad %d < M %d", rows_pad, M);
   const dim3 grid(tw_cdiv(M, 4)), blk(256);
   hipStream_t st = (hipStream_t)stream;
-#define TW_LNQ(nc) hipLaunchKernelGGL(k_layernorm_mx<nc>, grid, blk, 0, st, x, gamma, beta, M, D, eps, out, scales, rows_pad)
+  const size_t lds = tw_layernorm_lds_pad_bytes();
+#define TW_LNQ(nc) hipLaunchKernelGGL(k_layernorm_mx<nc>, grid, blk, lds, st, x, gamma, beta, M, D, eps, out, scales, rows_pad)
   switch (tw_cdiv(D, 256)) {
     case 1: TW_LNQ(1); break;
     case 2: TW_LNQ(2); break;
