@@ -12,6 +12,8 @@
  *   tw_g711_decode                   G.711 mu-law / A-law expansion (WAV, AU, AIFF-C telephony codecs)
  *   tw_ima_adpcm_wav_decode          IMA ADPCM in WAV blocks
  *   tw_vorbis_probe / tw_vorbis_decode  Ogg Vorbis I (floor 1, residues 0/1/2, coupling, IMDCT, overlap-add)
+ *   tw_mp3_probe / tw_mp3_decode     MPEG-1 / MPEG-2 LSF / MPEG-2.5 Layer III (MP3), gapless-trimmed by the
+ *                                    LAME tag as ffmpeg's mp3 demuxer trims it
  *   tw_resample_pcm_i32 / _f32       downmix + polyphase resample on the GPU (DEVICE memory, `stream`), the
  *                                    libswresample default filter restated (Kaiser-windowed sinc, see
  *                                    twamd/audio.py: swr_filter_bank)
@@ -93,6 +95,34 @@ int tw_vorbis_decode(const uint8_t* data, int64_t size, float* out, int64_t out_
 /* The Vorbis inverse MDCT alone (for tests): y[i] = sum_{k < n/2} X[k] cos(2 pi / n (i + 1/2 + n/4)(k + 1/2)),
  * i < n, n a power of two >= 4. HOST memory. */
 int tw_vorbis_imdct(const float* X, int32_t n, float* y);
+
+typedef struct TwMp3Info {
+  int32_t sample_rate;       /* Hz (first audio frame; the stream may not change rate or channel count)      */
+  int32_t channels;          /* 1 or 2                                                                        */
+  int32_t version;           /* 1 (MPEG-1), 2 (MPEG-2 LSF) or 25 (MPEG-2.5)                                  */
+  int32_t bitrate_kbps;      /* of the first audio frame                                                      */
+  int64_t total_samples;     /* per channel, after the gapless trim (all decoded samples without a LAME tag)  */
+  int64_t n_frames;          /* audio frames (a Xing / Info / VBRI header frame is not counted)               */
+  int64_t skip_samples;      /* decoded samples dropped at the start (LAME delay + 529; 0 without the tag)    */
+  int32_t samples_per_frame; /* 1152 (MPEG-1) or 576                                                          */
+  int32_t enc_delay;         /* LAME / Lavc tag encoder delay and padding (-1: no such tag)                   */
+  int32_t enc_padding;
+  int32_t flags;             /* 1: Xing / Info frame, 2: LAME gapless fields, 4: VBRI frame                  */
+} TwMp3Info;
+
+/* MP3 (HOST memory): skip ID3v2 tags, find the first Layer III frame the next header confirms, walk the frames
+ * (resynchronising over junk, stopping at ID3v1 / APEv2 / trailing ID3 tags) and read the Xing / Info + LAME or VBRI
+ * header frame. Layer I / II and free-format streams are refused. Reference: the codec half of ffmpeg_read
+ * ($TF/pipelines/audio_utils.py:9-45) for the .mp3 uploads vocalis/api/main.py:67-75 stores. */
+int tw_mp3_probe(const uint8_t* data, int64_t size, TwMp3Info* info);
+
+/* Decode into out = f32[out_frames][channels] (interleaved, HOST, nominal full scale +-1). out_frames must be >=
+ * info.total_samples. Frame ranges decode on n_threads threads (<= 0: hardware concurrency), each primed by the
+ * frame before its range: the output does not depend on the thread count. A frame whose reservoir reaches before
+ * the first frame, or whose side information is reserved, decodes as silence. *frames_decoded receives the frames
+ * written (= info.total_samples). */
+int tw_mp3_decode(const uint8_t* data, int64_t size, float* out, int64_t out_frames, int32_t n_threads,
+                  int64_t* frames_decoded);
 
 #ifdef __cplusplus
 }

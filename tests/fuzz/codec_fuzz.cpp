@@ -1,4 +1,4 @@
-// Sanitizer driver for the host parsers of untrusted upload bytes (csrc/flac.cpp, vorbis.cpp, pcm_codecs.cpp): every
+// Sanitizer driver for the host parsers of untrusted upload bytes (csrc/flac.cpp, vorbis.cpp, pcm_codecs.cpp, mp3.cpp): every
 // input file, then `mutations` damaged copies of it (truncations, bit flips, byte overwrites, chunk duplications;
 // a fixed-seed PRNG), through probe + decode of every codec, single- and multi-threaded. Built with
 // -fsanitize=address,undefined and -fno-sanitize-recover (make -C turbo-whisper-workspace_amd/csrc sanitize): any
@@ -55,6 +55,16 @@ static void run_all(const std::vector<uint8_t>& buf) {
       int64_t got = 0;
       for (int th : {1, 4})
         if (tw_vorbis_decode(d, n, out.data(), info.total_samples, th, &got) == 0) ++g_ok;
+    }
+  }
+  {  // MP3 (Layer III)
+    TwMp3Info info;
+    if (tw_mp3_probe(d, n, &info) == 0 && info.channels > 0 && info.total_samples >= 0 &&
+        info.total_samples < (1 << 22)) {
+      std::vector<float> out((size_t)info.total_samples * info.channels + 1);
+      int64_t got = 0;
+      for (int th : {1, 3})
+        if (tw_mp3_decode(d, n, out.data(), info.total_samples, th, &got) == 0) ++g_ok;
     }
   }
   {  // G.711 (raw payload) and IMA ADPCM (Microsoft block layout) over the same bytes

@@ -6,6 +6,7 @@ mono) must decode to PCM whose MD5 equals its STREAMINFO MD5 (runs where /root/r
 the oracle's FLAC writer (oracle/audio_oracle.py) cover every subframe type, stereo mode, bit depth and blocking
 strategy and must round-trip exactly."""
 import os
+import re
 
 import numpy as np
 import pytest
@@ -181,14 +182,21 @@ def test_constant_subframe_stream_over_duration_cap(monkeypatch):
 
 
 def test_undecoded_containers_named_and_garbage_reported_as_reference():
-    """MP3 / Ogg / WebM / M4A uploads are refused by name; bytes no container matches get the reference's own
-    decode-failure message (transformers' ffmpeg_read), which its transcribe() returns as {"error": ...}."""
-    cases = {b"ID3\x04\x00" + bytes(64): "MP3", b"\xff\xfb\x90\x00" + bytes(64): "MP3", b"OggS\x00\x02" + bytes(64): "Ogg",
+    """MPEG Layer I / II, ADTS AAC, Ogg (not Vorbis) / WebM / M4A uploads are refused by name; bytes no container
+    matches get the reference's own decode-failure message (transformers' ffmpeg_read), which its transcribe()
+    returns as {"error": ...}. (MP3 is decoded: tests/test_audio_mp3.py.)"""
+    cases = {b"\xff\xfd\x90\x00" + bytes(64): "MPEG audio Layer II", b"\xff\xff\x90\x00" + bytes(64): "MPEG audio Layer I",
+             b"ID3\x04\x00\x00\x00\x00\x00\x04" + bytes(4) + b"\xff\xf1\x50\x80" + bytes(64): "AAC (ADTS)",
+             b"OggS\x00\x02" + bytes(64): "Ogg",
              b"\x1aE\xdf\xa3" + bytes(64): "Matroska/WebM", b"\x00\x00\x00\x20ftypM4A " + bytes(64): "MP4/M4A"}
     for data, name in cases.items():
         assert audio.container_name(data) == name
-        with pytest.raises(ValueError, match=f"^{name} audio is not decoded"):
+        with pytest.raises(ValueError, match=f"^{re.escape(name)} audio is not decoded"):
             audio.load_input(data)
+    # an ID3 tag over bytes holding no Layer III frame: named MP3, refused by the decoder's frame search
+    assert audio.container_name(b"ID3\x04\x00" + bytes(64)) == "MP3"
+    with pytest.raises(ValueError, match="no MPEG Layer III frame"):
+        audio.load_input(b"ID3\x04\x00" + bytes(64))
     with pytest.raises(ValueError) as e:
         audio.load_input(b"hello, not audio" * 8)
     assert str(e.value) == audio.MALFORMED and str(e.value).startswith("Soundfile is either not in the correct format")

@@ -2,12 +2,14 @@
 
 POST /api/transcribe stores any upload and the pipeline decodes it (/root/reference/vocalis/api/main.py:67-75;
 ffmpeg_read, $TF/pipelines/audio_utils.py:9-45); here the FLAC, Ogg Vorbis, G.711 and IMA ADPCM decoders do that in
-host C++ (csrc/flac.cpp, vorbis.cpp, pcm_codecs.cpp). `make sanitize` builds them with -fsanitize=address,undefined
+host C++ (csrc/flac.cpp, vorbis.cpp, pcm_codecs.cpp, mp3.cpp). `make sanitize` builds them with -fsanitize=address,undefined
 and -fno-sanitize-recover into tests/fuzz/codec_fuzz.cpp, which runs probe + decode over every corpus file and
 hundreds of damaged copies of each (truncations, bit flips, overwritten runs, duplicated chunks, random tails). Any
 out-of-bounds access, leak or undefined behaviour aborts the run. The corpus: the oracle's FLAC writer over every
 subframe kind / stereo mode / bit depth / blocking, its random-syntax Vorbis writer, the image's one libVorbis
-stream and the reference's example FLAC (first 256 KB, when present in this container)."""
+stream, the MP3 oracle's random-syntax Layer III writer (MPEG-1 / 2 / 2.5, every channel mode, Info + LAME frames,
+ID3v2 tags, junk between frames), the image's one real MP3 and the reference's example FLAC (first 256 KB, when
+present in this container)."""
 import os
 import subprocess
 
@@ -15,11 +17,13 @@ import numpy as np
 import pytest
 
 from oracle import audio_oracle as ao
+from oracle import mp3_oracle as mo
 from oracle import vorbis_oracle as vo
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "turbo-whisper-workspace_amd", "csrc")
 REAL_OGG = "/usr/local/lib/python3.10/dist-packages/kaleido/executable/etc/mathjax/extensions/a11y/invalid_keypress.ogg"
+REAL_MP3 = REAL_OGG[:-3] + "mp3"
 REF_FLAC = "/root/reference/examples/Test1/ChrisAndAlexDiTest.flac"
 
 
@@ -44,6 +48,11 @@ def _corpus(tmp_path):
         put(f"gen{seed}.ogg", vo.write_stream(np.random.default_rng(seed), channels=1 + seed % 3, n_packets=6))
     if os.path.exists(REAL_OGG):
         put("real.ogg", open(REAL_OGG, "rb").read())
+    for seed in range(6):
+        put(f"gen{seed}.mp3", mo.write_stream(np.random.default_rng(seed), version=(1, 2, 25)[seed % 3], nframes=5,
+                                              mode=seed % 4, xing=seed % 2 == 0, id3=seed == 1, junk=seed == 3))
+    if os.path.exists(REAL_MP3):
+        put("real.mp3", open(REAL_MP3, "rb").read())
     if os.path.exists(REF_FLAC):
         put("ref_prefix.flac", open(REF_FLAC, "rb").read()[: 256 * 1024])
     put("adpcm_like.bin", rng.integers(0, 256, size=4096, dtype=np.uint8))

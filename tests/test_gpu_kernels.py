@@ -587,6 +587,9 @@ GEMV_CASES = [  # M, N, K, epi, splits
     (64, 5120, 1280, _lib.TW_EPI_GELU_PACKED, 1), (33, 1536, 384, _lib.TW_EPI_GELU_PACKED, 1),
     (64, 1280, 5120, _lib.TW_EPI_PARTIAL_F32, 4), (60, 1296, 1280, _lib.TW_EPI_PARTIAL_F32, 4),
     (64, 51866, 1280, _lib.TW_EPI_F32, 1), (37, 51864, 384, _lib.TW_EPI_F32, 1),
+    # K / 32 not divisible by splits: slices of 10 and 11 steps, k_gemv_q's budget is the longest slice
+    (24, 1280, 1312, _lib.TW_EPI_PARTIAL_F32, 4), (20, 1280, 1344, _lib.TW_EPI_PARTIAL_F32, 3),
+    (24, 1296, 1312, _lib.TW_EPI_BF16, 1),
 ]
 
 

@@ -1729,14 +1729,17 @@ static void launch_gemv_q_kw(const bf16_t* A, int lda, const bf16_t* Wp, int M, 
 template <int EPI, bool APACK>
 static bool launch_gemv_q(const bf16_t* A, int lda, const bf16_t* Wp, int M, int N, int K, const EpiArgs& ea,
                           int splits, hipStream_t s) {
-  const int per = K / 32 / splits;  // steps per split-K slice
+  const int ns = K / 32;  // MFMA steps over K
   const int ngroups = tw_cdiv(N, 16);
+  // the longest wave slice at kw K-slices per block: the kernel cuts ns into kw * splits slices of floor / ceil size,
+  // and a wave holds at most U = 10 steps in flight (a longer slice would drop its tail)
+  auto longest = [&](int kw) { return tw_cdiv(ns, kw * splits); };
   // K-slices per block: the fewest that bring a wave to <= 10 steps; one more halving while the grid stays below
   // 256 workgroups and the waves keep >= 5 steps (o_proj: 80 groups x 4 splits of 10 steps -> KW = 2, 160 blocks)
   int kw = 1;
-  while (kw < 4 && (per + kw - 1) / kw > 10) kw *= 2;
-  if ((per + kw - 1) / kw > 10) return false;
-  while (kw < 4 && (long)tw_cdiv(ngroups, 4 / kw) * splits < 256 && (per + 2 * kw - 1) / (2 * kw) >= 5) kw *= 2;
+  while (kw < 4 && longest(kw) > 10) kw *= 2;
+  if (longest(kw) > 10) return false;
+  while (kw < 4 && (long)tw_cdiv(ngroups, 4 / kw) * splits < 256 && longest(2 * kw) >= 5) kw *= 2;
   if (kw == 1) launch_gemv_q_kw<EPI, APACK, 1>(A, lda, Wp, M, N, K, ea, splits, s);
   else if (kw == 2) launch_gemv_q_kw<EPI, APACK, 2>(A, lda, Wp, M, N, K, ea, splits, s);
   else launch_gemv_q_kw<EPI, APACK, 4>(A, lda, Wp, M, N, K, ea, splits, s);

@@ -7,7 +7,8 @@ which this image does not have), dicts carry {"raw"|"array", "sampling_rate"} an
 differs, multi-channel arrays are averaged to mono.
 
 Containers: FLAC (native multi-threaded decoder in libtwhip.so, include/tw_audio.h; bit-exact, verifiable
-against the stream's STREAMINFO MD5), Ogg Vorbis (native decoder, csrc/vorbis.cpp), RIFF/WAVE (PCM 8/16/24/32-bit, IEEE float 32/64, G.711 A-law / mu-law, IMA
+against the stream's STREAMINFO MD5), Ogg Vorbis (native decoder, csrc/vorbis.cpp), MP3 (MPEG-1 / 2 / 2.5 Layer III,
+native multi-threaded decoder csrc/mp3.cpp, gapless-trimmed by the LAME tag as ffmpeg trims it), RIFF/WAVE (PCM 8/16/24/32-bit, IEEE float 32/64, G.711 A-law / mu-law, IMA
 ADPCM), Sun AU and AIFF / AIFF-C (PCM, float, G.711) — the telephony codecs through native decoders
 (tw_g711_decode, tw_ima_adpcm_wav_decode), pinned to CPython's audioop / aifc / sunau / wave.
 Resampling runs on the GPU (tw_resample_pcm_*) with libswresample's default filter restated in
@@ -157,6 +158,32 @@ def decode_vorbis(data: bytes, threads: int = 0) -> Tuple[np.ndarray, int]:
     got = ctypes.c_int64()
     if lib.tw_vorbis_decode(ctypes.c_char_p(data), len(data), out.ctypes.data, total, int(threads),
                             ctypes.byref(got)) != 0:
+        raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    return out[: got.value], sr
+
+
+def mp3_probe(data: bytes):
+    _lib, lib = _flac_lib()
+    info = _lib.TwMp3Info()
+    if lib.tw_mp3_probe(ctypes.c_char_p(data), len(data), ctypes.byref(info)) != 0:
+        raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    return info
+
+
+def decode_mp3(data: bytes, threads: int = 0) -> Tuple[np.ndarray, int]:
+    """MP3 bytes -> f32 [frames, channels] through the native Layer III decoder (csrc/mp3.cpp; the Xing / Info frame
+    skipped, the LAME tag's delay + 529 samples dropped at the start and its padding - 529 at the end, as ffmpeg's mp3
+    demuxer does)."""
+    _lib, lib = _flac_lib()
+    info = mp3_probe(data)
+    total, ch, sr = int(info.total_samples), int(info.channels), int(info.sample_rate)
+    if total > max_audio_seconds() * sr:
+        raise ValueError(f"MP3 stream of {total} frames at {sr} Hz is longer than TW_MAX_AUDIO_S="
+                         f"{max_audio_seconds():g} s")
+    out = np.zeros((total, ch), np.float32)
+    got = ctypes.c_int64()
+    if lib.tw_mp3_decode(ctypes.c_char_p(data), len(data), out.ctypes.data, total, int(threads),
+                         ctypes.byref(got)) != 0:
         raise ValueError(lib.tw_last_error().decode(errors="replace"))
     return out[: got.value], sr
 
@@ -340,11 +367,34 @@ def max_audio_seconds() -> float:
     return float(os.environ.get("TW_MAX_AUDIO_S", "14400"))
 
 
-# Containers the engine recognises but does not decode (no MP3 / AAC / Opus decoder is built in): reported
-# by name, as a ValueError like the reference's own decode failure (ffmpeg_read, which its transcribe() turns into
-# its {"error": ...} result).
-_UNDECODED = ((b"ID3", "MP3"), (b"\xff\xfb", "MP3"), (b"\xff\xf3", "MP3"), (b"\xff\xf2", "MP3"), (b"OggS", "Ogg"),
-              (b"\x1aE\xdf\xa3", "Matroska/WebM"), (b"\xff\xf1", "AAC (ADTS)"), (b"\xff\xf9", "AAC (ADTS)"))
+# Containers the engine recognises but does not decode (no AAC / Opus decoder is built in): reported by name, as a
+# ValueError like the reference's own decode failure (ffmpeg_read, which its transcribe() turns into its
+# {"error": ...} result).
+_UNDECODED = ((b"OggS", "Ogg"), (b"\x1aE\xdf\xa3", "Matroska/WebM"))
+
+
+def _id3v2_end(data: bytes) -> int:
+    pos = 0
+    while data[pos: pos + 3] == b"ID3" and pos + 10 <= len(data):
+        flags, b = data[pos + 5], data[pos + 6: pos + 10]
+        pos += 10 + ((b[0] & 127) << 21 | (b[1] & 127) << 14 | (b[2] & 127) << 7 | (b[3] & 127))
+        pos += 10 if flags & 0x10 else 0  # (a footer)
+    return pos
+
+
+def _mpeg_audio_name(data: bytes) -> Optional[str]:
+    """MPEG audio frames (after any ID3v2 tags): Layer III is decoded; Layer I / II and ADTS AAC are named."""
+    pos = _id3v2_end(data)
+    h = data[pos: pos + 2]
+    if len(h) == 2 and h[0] == 0xFF and (h[1] & 0xE0) == 0xE0:
+        layer = (h[1] >> 1) & 3
+        if (h[1] & 0xF6) == 0xF0:  # 12-bit sync with layer 00: ADTS
+            return "AAC (ADTS)"
+        if (h[1] >> 3) & 3 != 1 and layer:
+            return {1: "MP3", 2: "MPEG audio Layer II", 3: "MPEG audio Layer I"}[layer]
+    if pos:  # an ID3v2 tag followed by something else: let the MP3 frame search decide
+        return "MP3"
+    return None
 # transformers' ffmpeg_read message for a payload ffmpeg cannot decode (pipelines/audio_utils.py)
 MALFORMED = ("Soundfile is either not in the correct format or is malformed. Ensure that the soundfile has a valid "
              "audio file extension (e.g. wav, flac or mp3) and is not corrupted. If reading from a remote URL, ensure "
@@ -370,11 +420,12 @@ def container_name(data: bytes) -> Optional[str]:
     for magic, name in _UNDECODED:
         if data.startswith(magic):
             return name
-    return None
+    return _mpeg_audio_name(data)
 
 
-_DECODERS = {"WAV": decode_wav, "AU": decode_au, "AIFF": decode_aiff, "Ogg Vorbis": decode_vorbis}
-DECODED = "FLAC, Ogg Vorbis, WAV (PCM, float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C"
+_DECODERS = {"WAV": decode_wav, "AU": decode_au, "AIFF": decode_aiff, "Ogg Vorbis": decode_vorbis, "MP3": decode_mp3}
+DECODED = "FLAC, Ogg Vorbis, MP3 (MPEG-1 / 2 / 2.5 Layer III), WAV (PCM, float, A-law, mu-law, IMA ADPCM), AU, " \
+          "AIFF / AIFF-C"
 
 
 def decode_bytes(data: bytes, sr_out: int = TARGET_SR, device=None) -> np.ndarray:
@@ -430,6 +481,9 @@ def duration_seconds(path: str) -> float:
     name = container_name(data)
     if name == "Ogg Vorbis":
         info = vorbis_probe(data)
+        return int(info.total_samples) / float(info.sample_rate)
+    if name == "MP3":
+        info = mp3_probe(data)
         return int(info.total_samples) / float(info.sample_rate)
     if name in _DECODERS:
         x, sr = _DECODERS[name](data)

@@ -62,18 +62,19 @@ def _capture(g: "torch.cuda.CUDAGraph", stream):
             gc.enable()
 
 
-# how the decode loop waits for a queued step: polling the event (default) or a blocking event synchronize, whose
+# how the decode loop waits for a queued step: polling the event rather than a blocking event synchronize, whose
 # wake-up latency depends on the runtime's scheduling mode (a process that has an RCCL communicator up paid ~10 ms per
-# bench step with the blocking wait: profiles/r05l_*). TW_WAIT=sync for A/B.
-_WAIT_POLL = os.environ.get("TW_WAIT", "poll") != "sync"
+# bench step with the blocking wait: profiles/r05l_*). The poll yields (sleep(0), which releases the GIL: the C4
+# diarizer thread keeps running) for the first _SPIN_POLLS checks — a decode step is ~0.4-0.7 ms — and then backs off
+# to 50 us sleeps, so a long wait does not hold a host core at 100 % beside other ranks' host work.
+_SPIN_POLLS = 2000
 
 
 def _wait(ev: "torch.cuda.Event") -> None:
-    if not _WAIT_POLL:
-        ev.synchronize()
-        return
+    n = 0
     while not ev.query():
-        time.sleep(0)  # (releases the GIL: the C4 diarizer thread keeps running)
+        time.sleep(0 if n < _SPIN_POLLS else 5e-5)
+        n += 1
 
 
 def _pad256(n: int) -> int:
@@ -197,8 +198,8 @@ class WhisperEngine:
                  enc_fp8: Optional[bool] = None):
         _lib.load()
         self.ops = _ops.load()  # torch.ops.tw (the encoder path's launches)
-        # (A/B: TW_ENC_OPS=0 issues the same encoder kernels through the C-ABI directly, without the dispatcher)
-        self.enc_via_ops = os.environ.get("TW_ENC_OPS", "1") != "0"
+        # (False: the same encoder kernels through the C-ABI directly, without the dispatcher; bench-equal, r05o)
+        self.enc_via_ops = True
         # Large-M GEMM kernel per encoder context (tw_gemm_set_variant): the 8-phase ping-pong k_gemm_8p (5) is 6-19 %
         # faster than k_gemm_big (1) on every encoder shape when it has the GPU to itself (scripts/gemm_bench.py), but
         # beside a running decode it slows the latency-bound decoder kernels more than it gains (bench step 117.1 vs
@@ -242,8 +243,8 @@ class WhisperEngine:
         # starting one row early (the t = 0 rows it then recomputes; the row in front only has to be readable)
         self._h1_rows = torch.zeros(M3 + 1, D, dtype=act, device=dev)
         self.h1 = self._h1_rows[1:]
-        # (A/B: TW_CONV2_IM2COL=1 materialises conv2's im2col operand, 276 MB at B = 24, as before round 4)
-        self._conv2_im2col = os.environ.get("TW_CONV2_IM2COL", "0") == "1"
+        # (True: materialise conv2's im2col operand, 276 MB at B = 24, as before round 4; the f32 path always does)
+        self._conv2_im2col = False
         self.a2 = torch.empty(M15, 3 * D, dtype=act, device=dev) if self._conv2_im2col or self.F32 else None
         self.x = torch.empty(M15, D, dtype=f32, device=dev)
         self.hln = torch.empty(M15, D, dtype=act, device=dev)
@@ -251,7 +252,7 @@ class WhisperEngine:
         self.att = torch.empty(M15, D, dtype=act, device=dev)
         self.ffn = torch.empty(M15, F, dtype=act, device=dev)
         # cross-attention K/V of the encoded windows, one buffer per pipeline slot
-        # BASELINE config 5: the encoder projections on MX fp8 operands (tw_gemm_mx); TW_ENC_FP8=1 turns it on
+        # BASELINE config 5: the encoder projections on MX fp8 operands (tw_gemm_mx); TW_ENC_FP8=1 (or enc_fp8=True)
         self.enc_fp8 = (os.environ.get("TW_ENC_FP8", "0") == "1") if enc_fp8 is None else bool(enc_fp8)
         if self.F32 and self.enc_fp8:
             raise ValueError("the fp32 path has no MX fp8 encoder")
@@ -318,25 +319,23 @@ class WhisperEngine:
         self._pump: Optional[_EncoderPump] = None  # paced next-batch encoder (run_batches)
         # decode steps queued ahead of the host before it pumps encoder chunks or waits, and encoder chunks pending
         # beside a decode: 1 and 2 (queue depths 1-3 re-measured within +-0.5 %)
-        self.dec_ahead = int(os.environ.get("TW_DEC_AHEAD", "1"))
-        self.pump_ahead = int(os.environ.get("TW_PUMP_AHEAD", "2"))
+        self.dec_ahead = 1
+        self.pump_ahead = 2
         # greedy steps end with the fused select + next-step embedding + first LayerNorm (tw_logits_select_embed):
         # 47 launches per token instead of 49 (False: the separate launches; the tests check both decode alike)
         self.fused_select = not self.F32
         # decoder steps per graph replay in the generation loop: alone (no encoder chunks pumped between steps) and
-        # beside run_batches' encoder pump (TW_GRAPH_STEPS_ALONE / _BESIDE for A/B)
-        self.graph_steps_alone = int(os.environ.get("TW_GRAPH_STEPS_ALONE", "1"))
-        self.graph_steps_beside = int(os.environ.get("TW_GRAPH_STEPS_BESIDE", "1"))
+        # beside run_batches' encoder pump
+        self.graph_steps_alone = 1
+        self.graph_steps_beside = 1
         # the prompt phase of a decode pass replayed as one captured graph (False: eager)
         self.prompt_graph = True
         # encoder attention kernel (tw_attn_set_variant) and its LDS cap in 16 KiB units (tw_attn_set_lds_pad) for an
         # encoder chunk alone / beside a running decode
         self.attn_kernel = (32, 32)  # k_attn_enc5 (round 4; 16 = k_attn_enc4, bit-identical to the enc2 form)
-        if os.environ.get("TW_ENC_ATTN"):
-            self.attn_kernel = (int(os.environ["TW_ENC_ATTN"]),) * 2
-        self.attn_pad = (0, int(os.environ.get("TW_ATTN_PAD_BESIDE", "4")))  # (A/B: TW_ATTN_PAD_BESIDE)
+        self.attn_pad = (0, 4)
         # the encoder LayerNorm's LDS request in KiB (tw_layernorm_set_lds_pad), alone / beside a decode
-        self.ln_pad = (0, int(os.environ.get("TW_LN_PAD_BESIDE", "0")))
+        self.ln_pad = (0, 0)
         # run_batches encodes batch k+1 beside the decode of batch k (sequential 138.6 vs overlapped 114.5 ms per
         # bench step, round 1); False: strictly in turn
         self.overlap = True
@@ -370,6 +369,7 @@ class WhisperEngine:
         self._pump = None
         self.step_hook = None
         self.pass_events = None
+        self.replay_host = None
         self.timers = None
         self._enc_ev = []
         self._chain_cache.clear()
@@ -610,19 +610,18 @@ class WhisperEngine:
 
     # large-M GEMM kernel of an encoder chunk that runs alone (tw_gemm_set_variant): 6 = the persistent k_gemm_8pp (the
     # next tile's first K-tile DMA'd under the epilogue: encoder layer 1404 -> 1332 us at 24 windows,
-    # profiles/r05v_gemm_variant_ab.txt), 5 = k_gemm_8p (TW_GEMM_ALONE for A/B)
-    gemm_alone = int(os.environ.get("TW_GEMM_ALONE", "6"))
+    # profiles/r05v_gemm_variant_ab.txt), 5 = k_gemm_8p
+    gemm_alone = 6
     # beside a decode: k_gemm_big (1: 184 VGPRs, so a decoder wave fits on every SIMD of every CU), or the persistent
-    # kernel on TW_GEMM_BESIDE_CUS CUs (6: the other CUs left to the decoder's kernels) — TW_GEMM_BESIDE for A/B
-    gemm_beside = int(os.environ.get("TW_GEMM_BESIDE", "1"))
-    gemm_beside_cus = int(os.environ.get("TW_GEMM_BESIDE_CUS", "224"))
+    # kernel on gemm_beside_cus CUs (6: the other CUs left to the decoder's kernels)
+    gemm_beside = 1
+    gemm_beside_cus = 224
     # MX fp8 GEMM kernel (tw_gemm_mx_set_variant) of config 5's encoder chunks alone / beside a decode: 0 = the
     # library's shape rule (k_gemm_mx for q/k/v, k_gemm_8p_mx for the rest: 180.7 vs 183.2 ms per step,
     # profiles/r05bb_mx_shape_rule_ab.txt), 8 = k_gemm_8p_mx everywhere (256 VGPRs), 1 = k_gemm_mx everywhere (182
     # VGPRs, so a decoder wave fits beside it — which does not pay: 188.6 vs 183.4 ms, profiles/r05ba_mx_beside_ab.txt)
-    # — TW_MX_ALONE / TW_MX_BESIDE for A/B
-    mx_alone = int(os.environ.get("TW_MX_ALONE", "0"))
-    mx_beside = int(os.environ.get("TW_MX_BESIDE", "0"))
+    mx_alone = 0
+    mx_beside = 0
 
     def _set_gemm_context(self, alone: bool) -> None:
         """Encoder kernels for the chunk about to be queued (see __init__): large-M GEMM gemm_alone alone, 1 beside a decode;
@@ -907,9 +906,11 @@ class WhisperEngine:
     # and re-run the head of the next step (embed_head) so the next replay of the captured step consumes the forced
     # token instead of the one the selection chose. None in normal decoding.
     step_hook = None
-    # measurement: a list to which decode_pass appends (start event, end event, steps) of its generation loop
+    # measurement: a list to which decode_pass appends (start event, end event, steps) of its generation loop, and the
+    # host seconds of each graph replay of the passes measured (an instance list, started with the first such pass;
+    # the caller clears it with pass_events)
     pass_events: Optional[list] = None
-    replay_host: list = []
+    replay_host: Optional[list] = None
 
     def embed_head(self, v: Optional[DecView] = None, R: Optional[int] = None) -> None:
         """The next step's head (embedding of ids at pos + layer 0's LayerNorm) for view v, or for rows [0, R) when
@@ -938,18 +939,18 @@ class WhisperEngine:
     # K-slices of the vocabulary-wide proj_out for a decode pass with no encoder beside it (the pipeline's last batch, a
     # single-batch call, beam passes of the as-shipped call, long-form). 1 by default: 4 slices make the launch itself
     # faster alone (22.7 vs 33 us) but the captured step slower (444.4 vs 439.6 us at 24 rows, bench 99.6 vs 98.9 ms,
-    # profiles/r04n_ab.txt). TW_DEC_ALONE_WIDE_KW overrides (1 / 2 / 4).
-    dec_alone_wide_kw = int(os.environ.get("TW_DEC_ALONE_WIDE_KW", "1"))
-    # (the same beside an encoder chunk: 1; TW_DEC_BESIDE_WIDE_KW for A/B)
-    dec_beside_wide_kw = int(os.environ.get("TW_DEC_BESIDE_WIDE_KW", "1"))
+    # profiles/r04n_ab.txt).
+    dec_alone_wide_kw = 1
+    # (the same beside an encoder chunk: 1)
+    dec_beside_wide_kw = 1
 
     # The layer GEMVs' kernel (tw_gemv_set_variant) for a decode pass alone: k_gemv_q (1: one column group per wave, the
     # whole K-slice in flight; the library keeps k_gemv_pc at <= 16 rows and above 32) — captured step 393.5 -> 384.8
     # us at 24 rows (profiles/r05i_decode_chain.txt; at 64 rows 682.6 -> 651.1 in the captured step, but config 5's
     # bench 201.7-202.5 vs 198.8-198.9 ms with k_gemv_pc, profiles/r05aa_c5_gemv_ab.txt); beside an encoder chunk
-    # k_gemv_pc (0): 87.86 vs 88.45 ms per bench step (profiles/r05i_gemv_ab.txt). TW_DEC_ALONE_GEMV / _BESIDE_GEMV.
-    dec_alone_gemv = int(os.environ.get("TW_DEC_ALONE_GEMV", "1"))
-    dec_beside_gemv = int(os.environ.get("TW_DEC_BESIDE_GEMV", "0"))
+    # k_gemv_pc (0): 87.86 vs 88.45 ms per bench step (profiles/r05i_gemv_ab.txt).
+    dec_alone_gemv = 1
+    dec_beside_gemv = 0
 
     @property
     def _wide_kw(self) -> int:
@@ -1126,6 +1127,8 @@ class WhisperEngine:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record(chains[0].stream)
             th0 = time.perf_counter()
+            if self.replay_host is None:
+                self.replay_host = []
         while steps < max_new:
             n = min(check_every if hook is None else 1, max_new - steps)
             done = 0
