@@ -419,6 +419,32 @@ def decode_cross_roofline(eng, B, traffic_lookup):
             "copy_peak": HBM_COPY_GBS, "frac_of_copy": round(gbs / HBM_COPY_GBS, 4)}
 
 
+def _cgroup_cpus():
+    """The CPU quota of this process's cgroup (cgroup v2 cpu.max: quota / period), or None without one."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(p)))
+    except (OSError, ValueError):
+        return None
+
+
+def host_threads() -> int:
+    """Threads for the CPU baseline: every CPU this process may run on (its affinity mask), bounded by the cgroup's
+    CPU quota and by OMP_NUM_THREADS when the box sets it (the GPU box's share is 16 of a larger machine: more
+    threads than the quota only time-slice)."""
+    n = len(os.sched_getaffinity(0))
+    for lim in (_cgroup_cpus(), os.environ.get("OMP_NUM_THREADS")):
+        if lim:
+            n = min(n, int(lim))
+    return max(1, n)
+
+
+def host_cpu_report() -> dict:
+    return {"affinity": len(os.sched_getaffinity(0)), "cgroup_quota": _cgroup_cpus(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "os_cpu_count": os.cpu_count()}
+
+
 def cpu_baseline(dims, gen, T, threads):
     """The reference's executed transcription path (transformers ASR pipeline, what
     vocalis/core/audio_pipeline.py:351-358 calls) on the host CPU, fp32, same seeded weights, with the reference's
@@ -432,7 +458,7 @@ def cpu_baseline(dims, gen, T, threads):
     from oracle import hf_baseline
     from twamd.synth_audio import speech_like
 
-    threads = threads or min(16, os.cpu_count() or 1)  # the GPU box grants 16 host cores
+    threads = threads or host_threads()
     g = copy.deepcopy(gen)
     g.suppress_tokens = list(gen.suppress_tokens) + [gen.special.eot]
     audio = speech_like(210.0, 1234)
@@ -454,7 +480,7 @@ def cpu_baseline(dims, gen, T, threads):
         pass
     r1, r5 = runs[1], runs[5]
     return {"value": round(r1["audio_s"] / r1["wall_s"], 3), "unit": "audio-s/wall-s", "cores": threads,
-            "kind": "reference", "cpu": cpu,
+            "kind": "reference", "cpu": cpu, "host_cpus": host_cpu_report(),
             "as_shipped_beam5": {"value": round(r5["audio_s"] / r5["wall_s"], 3), "wall_s": round(r5["wall_s"], 2)},
             "sample": f"transformers {__import__('transformers').__version__} ASR pipeline fp32 on CPU (the path the "
                       f"reference executes) with the reference kwargs (chunk_length_s=60, stride_length_s=5, "

@@ -1,4 +1,4 @@
-"""Chunk data parallelism (twamd.dist) on CPU: world_size-2 gloo process groups over 127.0.0.1.
+"""Chunk data parallelism (twamd.dist) on CPU: world_size-2 (and C3's 8-way) gloo process groups over 127.0.0.1.
 
 The engine itself needs the GPU, so the per-rank window work is a deterministic stand-in that turns each window's
 samples into a valid Whisper token sequence; what is under test is the sharding, the waveform broadcast, the
@@ -339,12 +339,14 @@ class _FakeEngine:
     load(k) filling wave[:n]); each window's tokens are fake_windows' function of the samples that load() put in
     wave, so the test sees exactly what the sharded upload delivered."""
 
-    def __init__(self, max_batch):
+    def __init__(self, max_batch, tokens=None):
+        self.tokens = tokens or (lambda wav, windows, idx: fake_windows(wav, windows))
         self.max_batch = max_batch
         self.wave = torch.zeros(max_batch, 480000)
         self.gen = GenerationSettings.default(PRESETS["large-v3-turbo"])
         self.device = torch.device("cpu")
         self.sizes = []
+        self.done = 0  # windows run so far (rank-local)
 
         class d:
             max_source_positions = 1500
@@ -357,7 +359,10 @@ class _FakeEngine:
         for k, n in enumerate(sizes):
             load(k)
             rows = self.wave[:n].numpy()
-            toks = fake_windows(rows.reshape(-1), [Window(j * 480000, 480000, 0, 0, False) for j in range(n)])
+            base = self.done
+            toks = self.tokens(rows.reshape(-1), [Window(j * 480000, 480000, 0, 0, False) for j in range(n)],
+                               [base + j for j in range(n)])
+            self.done += n
             out.append(toks)
             self.batch_langs.append([None] * n)
             self.batch_passes.append([[t] for t in toks])
@@ -407,6 +412,58 @@ def test_sharded_transcriber_call_equals_single_process():
     assert eng.sizes == [[8, 8, 8]]
     assert res[0][1] == ref and res[1][1] == ref  # every rank returns the stitched result
     assert res[0][2] == [[6, 6]] and res[1][2] == [[6, 6]]  # 12 windows per rank: two near-equal batches
+
+
+def fake_open_windows(wav, windows, idx):
+    """fake_windows whose closing timestamp is dropped (a segment left open into the next window) on every window
+    that ends a 15-window shard of C3's 8-way split and on the windows whose first text token is 0 mod 3; `idx` are
+    the global window indices of the batch."""
+    out = fake_windows(wav, windows)
+    for k, t in zip(idx, out):
+        if k % 15 == 14 or t[1] % 3 == 0:
+            t.pop()
+    return out
+
+
+def _c3_worker(rank, ws, port, n_samples, q):
+    from twamd.pipeline import TurboTranscriber
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        eng = _FakeEngine(24, tokens=lambda wav, w, idx: fake_open_windows(wav, w, [i + 15 * rank for i in idx]))
+        tr = TurboTranscriber(eng, WhisperVocab.synthetic(ST))
+        wav = np.random.default_rng(11).standard_normal(n_samples).astype(np.float32) if rank == 0 else None
+        out = tr(wav, **_call_kwargs())
+        q.put((rank, out, eng.sizes, twd.merge_pieces.last_restitched))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c3_eight_rank_split_equals_single_process():
+    """BASELINE config 3's exact partition, rehearsed on the CPU: one hour at 30-s windows (120 windows) over 8 gloo
+    ranks, 15 windows and one engine batch per rank, transcribe_sharded + stitch_sharded with timestamps, segments
+    left open across every rank boundary (the merge must re-stitch those shards). Every rank's result equals the
+    single-process call's."""
+    from twamd.pipeline import TurboTranscriber
+    n_samples, ws = 3600 * 16000, 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c3_worker, args=(r, ws, port, n_samples, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    eng = _FakeEngine(24, tokens=fake_open_windows)
+    tr = TurboTranscriber(eng, WhisperVocab.synthetic(ST))
+    ref = tr(np.random.default_rng(11).standard_normal(n_samples).astype(np.float32), **_call_kwargs())
+    assert eng.sizes == [[24] * 5] and len(ref["chunks"]) > 60
+    for r, out, sizes, restitched in res:
+        assert sizes == [[15]], (r, sizes)
+        assert out == ref, r
+        assert restitched >= 7  # every shard after the first opened with a segment in flight
 
 
 def test_batch_sizes_policy():

@@ -168,3 +168,46 @@ def test_engine_encoder_runs_through_the_ops(monkeypatch):
     assert calls["gemm_bf16_out"] == 1 + 4 * L + 1  # conv1, q/k/v + o + fc1 + fc2 per layer, cross-K/V
     assert calls["layernorm_out"] == 2 * L + 1
     eng.close()
+
+
+@pytest.mark.gpu
+def test_ops_refuse_bad_operands():
+    """a wrong-shaped call from Python is a TORCH_CHECK (RuntimeError naming the operand), never an
+    out-of-bounds device access: cache / output / bias lengths, dtypes, the bf16 epilogue's 16-byte row stride."""
+    tw = _ops.load()
+    bf = torch.bfloat16
+    B, H, T = 4, 2, 16
+    qkv = torch.zeros(B, 3 * H * 64, dtype=bf, device=DEV)
+    pos = torch.zeros(B, dtype=torch.int32, device=DEV)
+    kc = torch.zeros(B * H * T * 64, dtype=bf, device=DEV)
+    out = torch.zeros(B, H * 64, dtype=bf, device=DEV)
+    tw.attn_decode_self_(qkv, H, T, pos, kc, kc.clone(), out)
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="k_cache"):
+        tw.attn_decode_self_(qkv, H, T, pos, kc[:-64], kc.clone(), out)
+    with pytest.raises(RuntimeError, match="pos"):
+        tw.attn_decode_self_(qkv, H, T, pos.float(), kc, kc.clone(), out)
+    with pytest.raises(RuntimeError, match="out"):
+        tw.attn_decode_self_(qkv, H, T, pos, kc, kc.clone(), out[:2])
+    cross = torch.zeros(2 * B * H * 100 * 64, dtype=bf, device=DEV)
+    q = torch.zeros(B, H * 64, dtype=bf, device=DEV)
+    tw.attn_decode_cross_out(q, H, 100, B, None, cross, out)
+    with pytest.raises(RuntimeError, match="cross_kv"):
+        tw.attn_decode_cross_out(q, H, 101, B, None, cross, out)
+    A = torch.zeros(64, 64, dtype=bf, device=DEV)
+    W = torch.zeros(128, 64, dtype=bf, device=DEV)
+    with pytest.raises(RuntimeError, match="bias"):
+        tw.gemm_bf16_out(A, W, _lib.TW_EPI_BF16, torch.empty(64, 128, dtype=bf, device=DEV),
+                         torch.zeros(100, device=DEV))
+    wide = torch.empty(64, 132, dtype=bf, device=DEV)[:, :128]  # row stride 132: not 16-byte aligned rows
+    with pytest.raises(RuntimeError, match="multiple of 8"):
+        tw.gemm_bf16_out(A, W, _lib.TW_EPI_BF16, wide)
+    x = torch.zeros(24, 1280, device=DEV)
+    g = torch.ones(1280, device=DEV)
+    outp = torch.zeros(40 * 2 * 512, dtype=bf, device=DEV)
+    tw.resid_layernorm_packed_(x, None, 0, None, g, g, 1e-5, outp)
+    with pytest.raises(RuntimeError, match="gamma"):
+        tw.resid_layernorm_packed_(x, None, 0, None, g[:1000], g, 1e-5, outp)
+    with pytest.raises(RuntimeError, match="parts"):
+        tw.resid_layernorm_packed_(x, torch.zeros(24 * 1280, device=DEV), 4, None, g, g, 1e-5, outp)
+    torch.cuda.synchronize()

@@ -12,6 +12,7 @@
 // (twamd/_ops.py). SURVEY §8b; BASELINE north_star ("Python host code calling hand-written HIP through PyTorch-ROCm
 // custom ops").
 #include <ATen/ATen.h>
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
@@ -23,7 +24,12 @@ namespace {
 
 using at::Tensor;
 
-void* cur_stream() { return (void*)c10::hip::getCurrentHIPStream().stream(); }
+// Every op runs on the device of its first tensor: a device guard for the launch (TW_OP_DEVICE) and that device's
+// current stream (not the current device's, which may differ)
+#define TW_OP_DEVICE(t)                                                                                  \
+  c10::hip::OptionalHIPGuard tw_guard_((t).is_cuda() ? std::optional<c10::DeviceIndex>((t).device().index()) \
+                                                     : std::nullopt)
+void* cur_stream(const Tensor& t) { return (void*)c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
 
 void ok(int rc, const char* what) { TORCH_CHECK(rc == 0, "tw::", what, " failed (", rc, "): ", tw_last_error()); }
 
@@ -34,6 +40,22 @@ void dev(const Tensor& t, at::ScalarType st, const char* name) {
 
 void rows(const Tensor& t, const char* name) {  // 2-D, unit stride along the inner dimension
   TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, name, " must be 2-D with a contiguous inner dimension");
+}
+
+void same_device(const Tensor& a, const Tensor& b, const char* name) {
+  TORCH_CHECK(a.device() == b.device(), name, " is on ", b.device(), ", the op's operands on ", a.device());
+}
+
+// a contiguous device tensor of dtype st holding at least n elements, on the op's device
+void holds(const Tensor& first, const Tensor& t, at::ScalarType st, int64_t n, const char* name) {
+  dev(t, st, name);
+  same_device(first, t, name);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.numel() >= n, name, " holds ", t.numel(), " elements, the call needs ", n);
+}
+
+void opt_holds(const Tensor& first, const c10::optional<Tensor>& t, at::ScalarType st, int64_t n, const char* name) {
+  if (t.has_value() && t->defined()) holds(first, *t, st, n, name);
 }
 
 template <class T>
@@ -47,6 +69,7 @@ constexpr int64_t kFrames = 3000, kSamples = 480000;
 // ---- log-mel (WhisperFeatureExtractor._torch_extract_fbank_features, $TF/.../feature_extraction_whisper.py:135-168)
 void logmel_out(const Tensor& wave, const Tensor& basis_cos, const Tensor& basis_sin, const Tensor& mel_fb,
                 int64_t n_mels, Tensor& out, Tensor& maxkeys) {
+  TW_OP_DEVICE(wave);
   dev(wave, at::kFloat, "wave");
   TORCH_CHECK(wave.dim() == 2 && wave.size(1) == kSamples && wave.is_contiguous(), "wave must be [B][480000]");
   dev(out, at::kFloat, "out");
@@ -56,7 +79,7 @@ void logmel_out(const Tensor& wave, const Tensor& basis_cos, const Tensor& basis
   TORCH_CHECK(maxkeys.numel() >= B, "maxkeys must hold B entries");
   for (auto* t : {&basis_cos, &basis_sin, &mel_fb}) dev(*t, at::kFloat, "basis / filterbank");
   ok(tw_logmel(ptr<float>(wave), (int)B, ptr<float>(basis_cos), ptr<float>(basis_sin), ptr<float>(mel_fb),
-               (int)n_mels, ptr<float>(out), ptr<uint32_t>(maxkeys), cur_stream()),
+               (int)n_mels, ptr<float>(out), ptr<uint32_t>(maxkeys), cur_stream(wave)),
      "logmel");
 }
 
@@ -75,6 +98,7 @@ Tensor logmel_meta(const Tensor& wave, const Tensor&, const Tensor&, const Tenso
 // ---- large-M / skinny bf16 GEMM with the fused epilogues (modeling_whisper.py projections, FFN, conv stem) --------
 void gemm_bf16_out(const Tensor& A, const Tensor& W, int64_t epi, Tensor& out, const c10::optional<Tensor>& bias,
                    const c10::optional<Tensor>& aux, int64_t aux_rows, at::OptionalIntArrayRef kv_geom) {
+  TW_OP_DEVICE(A);
   dev(A, at::kBFloat16, "A");
   dev(W, at::kBFloat16, "W");
   rows(A, "A");
@@ -82,23 +106,35 @@ void gemm_bf16_out(const Tensor& A, const Tensor& W, int64_t epi, Tensor& out, c
   TORCH_CHECK(A.size(1) == W.size(1), "A and W disagree on K");
   const bool bf_out = epi == TW_EPI_BF16 || epi == TW_EPI_GELU_BF16 || epi == TW_EPI_CROSSKV;
   dev(out, bf_out ? at::kBFloat16 : at::kFloat, "out");
-  if (bias.has_value() && bias->defined()) dev(*bias, at::kFloat, "bias");
-  if (aux.has_value() && aux->defined()) dev(*aux, at::kFloat, "aux");
+  same_device(A, W, "W");
+  same_device(A, out, "out");
   const int M = (int)A.size(0), N = (int)W.size(0), K = (int)A.size(1);
+  opt_holds(A, bias, at::kFloat, N, "bias");
   int geom[4] = {0, 0, 0, 0};
   int ldo = N;
   if (epi == TW_EPI_CROSSKV) {
     TORCH_CHECK(kv_geom.has_value() && kv_geom->size() == 4, "CROSSKV needs kv_geom = [S, B, D, H]");
     for (int i = 0; i < 4; ++i) geom[i] = (int)(*kv_geom)[i];
     TORCH_CHECK(out.is_contiguous(), "CROSSKV out must be contiguous");
+    TORCH_CHECK(out.numel() >= (int64_t)M * N, "CROSSKV out too small");
   } else {
     rows(out, "out");
     TORCH_CHECK(out.size(0) >= M && out.size(1) >= N, "out too small");
     ldo = (int)out.stride(0);
+    // (the bf16 epilogues store 16-byte vectors: rows must start 16-byte aligned)
+    TORCH_CHECK(!bf_out || ldo % 8 == 0, "bf16 out needs a row stride that is a multiple of 8 elements");
+  }
+  if (epi == TW_EPI_GELU_POS_F32) {
+    TORCH_CHECK(aux.has_value() && aux->defined() && aux_rows > 0, "GELU_POS_F32 needs aux and aux_rows");
+    // aux[m % aux_rows][n] is indexed with the output's row stride
+    TORCH_CHECK(ldo == N, "GELU_POS_F32 needs out rows of exactly N (the aux stride)");
+    holds(A, *aux, at::kFloat, (int64_t)aux_rows * N, "aux");
+  } else {
+    opt_holds(A, aux, at::kFloat, 0, "aux");
   }
   ok(tw_gemm_bf16(ptr<uint16_t>(A), ptr<uint16_t>(W), M, N, K, (int)A.stride(0), (int)W.stride(0), (int)epi,
                   out.data_ptr(), ldo, optr<float>(bias), optr<float>(aux), (int)aux_rows,
-                  epi == TW_EPI_CROSSKV ? geom : nullptr, cur_stream()),
+                  epi == TW_EPI_CROSSKV ? geom : nullptr, cur_stream(A)),
      "gemm_bf16");
 }
 
@@ -120,14 +156,16 @@ Tensor gemm_bf16_meta(const Tensor& A, const Tensor& W, int64_t epi, const c10::
 
 // ---- encoder self-attention (WhisperSdpaAttention / eager attention, modeling_whisper.py:215-238) ----------------
 void attn_encoder_out(const Tensor& qkv, int64_t batch, int64_t heads, Tensor& out) {
+  TW_OP_DEVICE(qkv);
   dev(qkv, at::kBFloat16, "qkv");
   dev(out, at::kBFloat16, "out");
   TORCH_CHECK(qkv.is_contiguous() && out.is_contiguous(), "qkv / out must be contiguous");
   TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == 3 * heads * 64 && qkv.size(0) % batch == 0,
               "qkv must be [batch * S][3 * heads * 64]");
   TORCH_CHECK(out.numel() >= qkv.size(0) * heads * 64, "out too small");
+  same_device(qkv, out, "out");
   ok(tw_attn_encoder(ptr<uint16_t>(qkv), (int)batch, (int)(qkv.size(0) / batch), (int)heads, ptr<uint16_t>(out),
-                     cur_stream()),
+                     cur_stream(qkv)),
      "attn_encoder");
 }
 
@@ -143,13 +181,17 @@ Tensor attn_encoder_meta(const Tensor& qkv, int64_t, int64_t heads) {
 
 // ---- encoder LayerNorm ---------------------------------------------------------------------------------------------
 void layernorm_out(const Tensor& x, const Tensor& gamma, const Tensor& beta, double eps, Tensor& out) {
+  TW_OP_DEVICE(x);
   dev(x, at::kFloat, "x");
   dev(out, at::kBFloat16, "out");
   dev(gamma, at::kFloat, "gamma");
   dev(beta, at::kFloat, "beta");
   TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && x.dim() == 2 && out.numel() >= x.numel(), "x [M][D]");
+  holds(x, gamma, at::kFloat, x.size(1), "gamma");
+  holds(x, beta, at::kFloat, x.size(1), "beta");
+  same_device(x, out, "out");
   ok(tw_layernorm(ptr<float>(x), ptr<float>(gamma), ptr<float>(beta), (int)x.size(0), (int)x.size(1), (float)eps,
-                  ptr<uint16_t>(out), cur_stream()),
+                  ptr<uint16_t>(out), cur_stream(x)),
      "layernorm");
 }
 
@@ -166,45 +208,76 @@ Tensor layernorm_meta(const Tensor& x, const Tensor&, const Tensor&, double) {
 // ---- decoder step pieces (WhisperDecoderLayer.forward, modeling_whisper.py:448-505) ---------------------------------
 void gemv_packed_out(const Tensor& A, bool a_packed, const Tensor& Wp, int64_t M, int64_t N, int64_t K, int64_t epi,
                      Tensor& out, const c10::optional<Tensor>& bias, int64_t splits) {
+  TW_OP_DEVICE(A);
   dev(A, at::kBFloat16, "A");
   dev(Wp, at::kBFloat16, "Wp");
   TORCH_CHECK(Wp.numel() >= ((N + 15) / 16) * 16 * K, "Wp too small for [N][K] packed");
+  same_device(A, Wp, "Wp");
+  TORCH_CHECK(M >= 1 && M <= 64 && K % 32 == 0 && N >= 1, "gemv_packed: 1 <= M <= 64 rows, K % 32 == 0");
+  TORCH_CHECK(splits >= 1 && (splits == 1 || epi == TW_EPI_PARTIAL_F32), "splits > 1 only with PARTIAL_F32");
+  // a packed activation spans [K/32][M <= 32 ? 2 : 4][64][8]; a row-major one [M][lda]
+  TORCH_CHECK(A.numel() >= (a_packed ? (K / 32) * (M > 32 ? 4 : 2) * 512 : (M - 1) * A.stride(0) + K),
+              "A too small for ", M, " rows of K = ", K);
   const bool f32 = epi == TW_EPI_F32 || epi == TW_EPI_RESID_F32 || epi == TW_EPI_PARTIAL_F32;
-  dev(out, f32 ? at::kFloat : at::kBFloat16, "out");
   const int ldo = epi == TW_EPI_GELU_PACKED ? 0 : (int)N;
+  holds(A, out, f32 ? at::kFloat : at::kBFloat16,
+        epi == TW_EPI_GELU_PACKED ? (K > 0 ? ((N + 31) / 32) * (M > 32 ? 4 : 2) * 512 : 0)
+                                  : (epi == TW_EPI_PARTIAL_F32 ? splits : 1) * M * N,
+        "out");
+  opt_holds(A, bias, at::kFloat, N, "bias");
   ok(tw_gemv_packed(ptr<uint16_t>(A), a_packed ? 1 : 0, a_packed ? (int)K : (int)A.stride(0), ptr<uint16_t>(Wp),
                     (int)M, (int)N, (int)K, (int)epi, out.data_ptr(), ldo, optr<float>(bias), (int)splits,
-                    cur_stream()),
+                    cur_stream(A)),
      "gemv_packed");
 }
 
 void resid_layernorm_packed_(Tensor& x, const c10::optional<Tensor>& parts, int64_t nparts,
                              const c10::optional<Tensor>& bias, const Tensor& gamma, const Tensor& beta, double eps,
                              Tensor& out) {
+  TW_OP_DEVICE(x);
   dev(x, at::kFloat, "x");
   dev(out, at::kBFloat16, "out");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "x must be [M][D]");
+  const int64_t M = x.size(0), D = x.size(1);
+  TORCH_CHECK(M >= 1 && M <= 64 && D % 32 == 0, "resid_layernorm_packed: M <= 64, D % 32 == 0");
+  opt_holds(x, parts, at::kFloat, nparts * M * D, "parts");
+  opt_holds(x, bias, at::kFloat, D, "bias");
+  holds(x, gamma, at::kFloat, D, "gamma");
+  holds(x, beta, at::kFloat, D, "beta");
+  holds(x, out, at::kBFloat16, (D / 32) * (M > 32 ? 4 : 2) * 512, "out");
   ok(tw_resid_layernorm_packed(ptr<float>(x), optr<float>(parts), (int)nparts, optr<float>(bias), ptr<float>(gamma),
                                ptr<float>(beta), (int)x.size(0), (int)x.size(1), (float)eps, ptr<uint16_t>(out),
-                               cur_stream()),
+                               cur_stream(x)),
      "resid_layernorm_packed");
 }
 
 void attn_decode_self_(const Tensor& qkv, int64_t heads, int64_t max_pos, const Tensor& pos, Tensor& k_cache,
                        Tensor& v_cache, Tensor& out) {
+  TW_OP_DEVICE(qkv);
   dev(qkv, at::kBFloat16, "qkv");
-  dev(pos, at::kInt, "pos");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.is_contiguous() && qkv.size(1) == 3 * heads * 64, "qkv must be [B][3 H 64]");
+  const int64_t B = qkv.size(0);
+  holds(qkv, pos, at::kInt, B, "pos");
+  holds(qkv, k_cache, at::kBFloat16, B * heads * max_pos * 64, "k_cache");
+  holds(qkv, v_cache, at::kBFloat16, B * heads * max_pos * 64, "v_cache");
+  holds(qkv, out, at::kBFloat16, B * heads * 64, "out");
   ok(tw_attn_decode_self(ptr<uint16_t>(qkv), (int)qkv.size(0), (int)heads, (int)max_pos, ptr<int>(pos),
-                         ptr<uint16_t>(k_cache), ptr<uint16_t>(v_cache), ptr<uint16_t>(out), cur_stream()),
+                         ptr<uint16_t>(k_cache), ptr<uint16_t>(v_cache), ptr<uint16_t>(out), cur_stream(qkv)),
      "attn_decode_self");
 }
 
 void attn_decode_cross_out(const Tensor& q, int64_t heads, int64_t S, int64_t Bt, const c10::optional<Tensor>& row_map,
                            const Tensor& cross_kv, Tensor& out) {
+  TW_OP_DEVICE(q);
   dev(q, at::kBFloat16, "q");
-  dev(cross_kv, at::kBFloat16, "cross_kv");
+  TORCH_CHECK(q.dim() == 2 && q.is_contiguous() && q.size(1) == heads * 64, "q must be [B][H 64]");
+  const int64_t B = q.size(0);
+  TORCH_CHECK(row_map.has_value() && row_map->defined() ? true : B <= Bt, "without row_map B must be <= Bt");
+  holds(q, cross_kv, at::kBFloat16, 2 * Bt * heads * S * 64, "cross_kv");
+  opt_holds(q, row_map, at::kInt, B, "row_map");
+  holds(q, out, at::kBFloat16, B * heads * 64, "out");
   ok(tw_attn_decode_cross(ptr<uint16_t>(q), (int)q.size(0), (int)heads, (int)S, (int)Bt, optr<int>(row_map),
-                          ptr<uint16_t>(cross_kv), ptr<uint16_t>(out), cur_stream()),
+                          ptr<uint16_t>(cross_kv), ptr<uint16_t>(out), cur_stream(q)),
      "attn_decode_cross");
 }
 
@@ -213,9 +286,23 @@ void attn_decode_cross_out(const Tensor& q, int64_t heads, int64_t S, int64_t Bt
 // mode, lo, hi, n_begin_suppress, begin_suppress[8])
 void logits_select_(const Tensor& logits, const Tensor& suppress_bits, at::IntArrayRef params, Tensor& state,
                     const c10::optional<Tensor>& tokens, Tensor& ids, Tensor& pos, Tensor& workspace) {
+  TW_OP_DEVICE(logits);
   dev(logits, at::kFloat, "logits");
   rows(logits, "logits");
   TORCH_CHECK(params.size() == 20, "params: 20 ints (TwSelectParams)");
+  const int64_t B = logits.size(0), V = params[0];
+  TORCH_CHECK(logits.size(1) >= V, "logits narrower than V");
+  holds(logits, suppress_bits, at::kInt, (V + 31) / 32, "suppress_bits");
+  holds(logits, state, at::kInt, B * TW_STATE_STRIDE, "state");
+  holds(logits, ids, at::kInt, B, "ids");
+  holds(logits, pos, at::kInt, B, "pos");
+  holds(logits, workspace, at::kFloat, B * TW_SELECT_WS_PER_ROW, "workspace");
+  if (tokens.has_value() && tokens->defined()) {
+    dev(*tokens, at::kInt, "tokens");
+    same_device(logits, *tokens, "tokens");
+    rows(*tokens, "tokens");
+    TORCH_CHECK(tokens->size(0) >= B, "tokens must hold B rows");
+  }
   TwSelectParams p;
   int32_t* f = &p.V;
   for (int i = 0; i < 12; ++i) f[i] = (int32_t)params[i];
@@ -223,7 +310,7 @@ void logits_select_(const Tensor& logits, const Tensor& suppress_bits, at::IntAr
   const Tensor* tk = tokens.has_value() && tokens->defined() ? &*tokens : nullptr;
   ok(tw_logits_select(ptr<float>(logits), (int)logits.size(0), (int)logits.stride(0), ptr<uint32_t>(suppress_bits),
                       &p, ptr<int>(state), tk ? ptr<int>(*tk) : nullptr, tk ? (int)tk->stride(0) : 0, ptr<int>(ids),
-                      ptr<int>(pos), ptr<float>(workspace), cur_stream()),
+                      ptr<int>(pos), ptr<float>(workspace), cur_stream(logits)),
      "logits_select");
 }
 

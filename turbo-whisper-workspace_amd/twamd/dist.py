@@ -294,7 +294,9 @@ def stitch_sharded(vocab, outputs: Sequence[dict], group=None, force_collective:
     segment_size."""
     from .tokenizer import decode_asr
     rank, ws = world()
-    if not collective_path(force_collective):
+    # without timestamps no window closes its chunk (the text accumulates until the end), so every shard after the
+    # first would be re-stitched by the merge: the plain serial pass is less work (ADVICE r5)
+    if not collective_path(force_collective) or not kw.get("return_timestamps"):
         return decode_asr(vocab, outputs, **kw)
     bounds = [shard_range(len(outputs), ws, r) for r in range(ws)]
     piece = shard_piece(vocab, outputs, *bounds[rank], **kw)
