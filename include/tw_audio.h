@@ -14,6 +14,8 @@
  *   tw_vorbis_probe / tw_vorbis_decode  Ogg Vorbis I (floor 1, residues 0/1/2, coupling, IMDCT, overlap-add)
  *   tw_mp3_probe / tw_mp3_decode     MPEG-1 / MPEG-2 LSF / MPEG-2.5 Layer III (MP3), gapless-trimmed by the
  *                                    LAME tag as ffmpeg's mp3 demuxer trims it
+ *   tw_aac_*                         MPEG-4 AAC-LC: ADTS streams, and the raw access units of an MP4 / M4A track
+ *                                    (the container is demuxed by the caller, twamd/audio.py)
  *   tw_resample_pcm_i32 / _f32       downmix + polyphase resample on the GPU (DEVICE memory, `stream`), the
  *                                    libswresample default filter restated (Kaiser-windowed sinc, see
  *                                    twamd/audio.py: swr_filter_bank)
@@ -123,6 +125,35 @@ int tw_mp3_probe(const uint8_t* data, int64_t size, TwMp3Info* info);
  * written (= info.total_samples). */
 int tw_mp3_decode(const uint8_t* data, int64_t size, float* out, int64_t out_frames, int32_t n_threads,
                   int64_t* frames_decoded);
+
+typedef struct TwAacInfo {
+  int32_t sample_rate;   /* Hz                                                                          */
+  int32_t channels;      /* of the channel configuration (1..7 -> 1, 2, 3, 4, 5, 6, 8)                  */
+  int32_t object_type;   /* 2 (LC): every other object type is refused                                  */
+  int32_t frame_length;  /* 1024                                                                        */
+  int64_t n_frames;      /* ADTS: frames found (0 for tw_aac_parse_asc)                                 */
+  int64_t total_samples; /* n_frames * 1024 per channel (no trim)                                       */
+} TwAacInfo;
+
+/* The AudioSpecificConfig of an MP4 track (esds DecoderSpecificInfo). Refused: object types other than LC, HE-AAC
+ * (SBR / PS, explicit or backward-compatible signalling), 960-sample frames, channel configuration 0. */
+int tw_aac_parse_asc(const uint8_t* asc, int32_t asc_size, TwAacInfo* info);
+
+/* Decode n_au raw access units data[au_offset[i] .. + au_size[i]) (HOST) of the stream asc describes into
+ * out = f32[out_frames][channels] (interleaved, nominal full scale +-1), 1024 samples per unit, untrimmed (an MP4 edit
+ * list is applied by the caller). out_frames >= n_au * 1024. Units decode on n_threads threads (<= 0: hardware
+ * concurrency), each range primed by the unit before it: the output does not depend on the thread count. Every unit
+ * must parse to its END element (an error names the unit). Replaces ffmpeg_read's AAC decode
+ * ($TF/pipelines/audio_utils.py:9-45) for the .m4a uploads vocalis/security/security_monitor.py:353 lists. */
+int tw_aac_decode_raw(const uint8_t* asc, int32_t asc_size, const uint8_t* data, int64_t size, const int64_t* au_offset,
+                      const int64_t* au_size, int64_t n_au, float* out, int64_t out_frames, int32_t n_threads,
+                      int64_t* frames_decoded);
+
+/* ADTS (.aac): skip ID3v2 tags, find the first frame, walk the frames of the same stream (one raw_data_block per
+ * frame; CRC words skipped). */
+int tw_aac_adts_probe(const uint8_t* data, int64_t size, TwAacInfo* info);
+int tw_aac_adts_decode(const uint8_t* data, int64_t size, float* out, int64_t out_frames, int32_t n_threads,
+                       int64_t* frames_decoded);
 
 #ifdef __cplusplus
 }

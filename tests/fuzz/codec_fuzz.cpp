@@ -1,10 +1,12 @@
-// Sanitizer driver for the host parsers of untrusted upload bytes (csrc/flac.cpp, vorbis.cpp, pcm_codecs.cpp, mp3.cpp): every
+// Sanitizer driver for the host parsers of untrusted upload bytes (csrc/flac.cpp, vorbis.cpp, pcm_codecs.cpp, mp3.cpp,
+// aac.cpp): every
 // input file, then `mutations` damaged copies of it (truncations, bit flips, byte overwrites, chunk duplications;
 // a fixed-seed PRNG), through probe + decode of every codec, single- and multi-threaded. Built with
 // -fsanitize=address,undefined and -fno-sanitize-recover (make -C turbo-whisper-workspace_amd/csrc sanitize): any
 // out-of-bounds access, leak or undefined behaviour aborts the run. Test infrastructure (tests/test_codec_sanitize.py),
 // CPU only; the decoders' return codes are not judged here, only memory safety.
 //   codec_fuzz [-m mutations] [-s seed] file...
+#include <algorithm>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -66,6 +68,28 @@ static void run_all(const std::vector<uint8_t>& buf) {
       for (int th : {1, 3})
         if (tw_mp3_decode(d, n, out.data(), info.total_samples, th, &got) == 0) ++g_ok;
     }
+  }
+  {  // AAC: ADTS framing, and the same bytes as raw access units of 1..3 fixed sizes (the MP4 path) for two configs
+    TwAacInfo info;
+    if (tw_aac_adts_probe(d, n, &info) == 0 && info.channels > 0 && info.total_samples > 0 &&
+        info.total_samples < (1 << 22)) {
+      std::vector<float> out((size_t)info.total_samples * info.channels);
+      int64_t got = 0;
+      for (int th : {1, 3})
+        if (tw_aac_adts_decode(d, n, out.data(), info.total_samples, th, &got) == 0) ++g_ok;
+    }
+    const uint8_t ascs[2][2] = {{0x11, 0x88}, {0x12, 0x10}};  // 48 kHz mono, 44.1 kHz stereo
+    for (int a = 0; a < 2; a++)
+      for (int64_t unit : {(int64_t)37, (int64_t)200, (int64_t)700}) {
+        const int64_t nau = std::min<int64_t>(n / unit, 64);
+        if (nau <= 0) continue;
+        std::vector<int64_t> off(nau), sz(nau);
+        for (int64_t i = 0; i < nau; i++) off[i] = i * unit, sz[i] = unit;
+        std::vector<float> out((size_t)nau * 1024 * 2);
+        int64_t got = 0;
+        if (tw_aac_decode_raw(ascs[a], 2, d, n, off.data(), sz.data(), nau, out.data(), nau * 1024, 2, &got) == 0)
+          ++g_ok;
+      }
   }
   {  // G.711 (raw payload) and IMA ADPCM (Microsoft block layout) over the same bytes
     std::vector<int16_t> pcm(buf.size() + 1);

@@ -2,14 +2,15 @@
 
 POST /api/transcribe stores any upload and the pipeline decodes it (/root/reference/vocalis/api/main.py:67-75;
 ffmpeg_read, $TF/pipelines/audio_utils.py:9-45); here the FLAC, Ogg Vorbis, G.711 and IMA ADPCM decoders do that in
-host C++ (csrc/flac.cpp, vorbis.cpp, pcm_codecs.cpp, mp3.cpp). `make sanitize` builds them with -fsanitize=address,undefined
+host C++ (csrc/flac.cpp, vorbis.cpp, pcm_codecs.cpp, mp3.cpp, aac.cpp). `make sanitize` builds them with -fsanitize=address,undefined
 and -fno-sanitize-recover into tests/fuzz/codec_fuzz.cpp, which runs probe + decode over every corpus file and
 hundreds of damaged copies of each (truncations, bit flips, overwritten runs, duplicated chunks, random tails). Any
 out-of-bounds access, leak or undefined behaviour aborts the run. The corpus: the oracle's FLAC writer over every
 subframe kind / stereo mode / bit depth / blocking, its random-syntax Vorbis writer, the image's one libVorbis
 stream, the MP3 oracle's random-syntax Layer III writer (MPEG-1 / 2 / 2.5, every channel mode, Info + LAME frames,
-ID3v2 tags, junk between frames), the image's one real MP3 and the reference's example FLAC (first 256 KB, when
-present in this container)."""
+ID3v2 tags, junk between frames), the image's one real MP3, the AAC oracle's random-syntax ADTS streams, the access
+units of the image's one real AAC-LC track as ADTS, and the reference's example FLAC (first 256 KB, when present in
+this container)."""
 import os
 import subprocess
 
@@ -17,6 +18,7 @@ import numpy as np
 import pytest
 
 from oracle import audio_oracle as ao
+from oracle import aac_oracle as aao
 from oracle import mp3_oracle as mo
 from oracle import vorbis_oracle as vo
 
@@ -24,6 +26,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "turbo-whisper-workspace_amd", "csrc")
 REAL_OGG = "/usr/local/lib/python3.10/dist-packages/kaleido/executable/etc/mathjax/extensions/a11y/invalid_keypress.ogg"
 REAL_MP3 = REAL_OGG[:-3] + "mp3"
+REAL_AAC_MP4 = "/opt/conda/lib/python3.9/site-packages/imageio/resources/images/realshort.mp4"
 REF_FLAC = "/root/reference/examples/Test1/ChrisAndAlexDiTest.flac"
 
 
@@ -53,6 +56,19 @@ def _corpus(tmp_path):
                                               mode=seed % 4, xing=seed % 2 == 0, id3=seed == 1, junk=seed == 3))
     if os.path.exists(REAL_MP3):
         put("real.mp3", open(REAL_MP3, "rb").read())
+    for seed in range(6):
+        put(f"gen{seed}.aac", aao.write_adts(np.random.default_rng(seed), sri=(3, 4, 8, 11, 6, 0)[seed],
+                                             chan_config=(1, 2, 1, 2, 3, 6)[seed], nframes=4, crc=seed % 2 == 1))
+    if os.path.exists(REAL_AAC_MP4):
+        from twamd import audio
+        data = open(REAL_AAC_MP4, "rb").read()
+        tr = audio.mp4_audio_track(data)
+        adts = b""
+        for o, sz in zip(tr.offsets.tolist(), tr.sizes.tolist()):
+            fl = 7 + sz
+            adts += bytes([0xFF, 0xF1, 0x4C, 0x40 | (fl >> 11), (fl >> 3) & 0xFF, ((fl & 7) << 5) | 0x1F, 0xFC])
+            adts += data[o: o + sz]
+        put("real_aac.aac", adts)
     if os.path.exists(REF_FLAC):
         put("ref_prefix.flac", open(REF_FLAC, "rb").read()[: 256 * 1024])
     put("adpcm_like.bin", rng.integers(0, 256, size=4096, dtype=np.uint8))

@@ -1,5 +1,5 @@
 """Audio ingest on the MI355X: the GPU resampler (tw_resample_pcm_*) against the oracle's float64 restatement of
-libswresample's default filter, and FLAC / Ogg Vorbis / MP3 files through the full product path (host decode -> GPU resample ->
+libswresample's default filter, and FLAC / Ogg Vorbis / MP3 / AAC (M4A, ADTS) files through the full product path (host decode -> GPU resample ->
 transcription). Tolerance: 2e-6 absolute on [-1, 1] signals (float32 accumulation of <= 396 taps)."""
 import numpy as np
 import pytest
@@ -138,6 +138,65 @@ def test_mp3_file_through_process_audio(tmp_path):
     wav = audio.load_input(data)
     ref = tr(wav, **kw)
     assert res["text"] == ref["text"] == tr(path, **kw)["text"] == tr(data, **kw)["text"]
+
+
+def test_aac_bytes_through_load_input():
+    """Native AAC-LC decode (host; the MP4 demuxer or ADTS framing) -> GPU downmix + resample, against the oracle's
+    float64 decoder + resampler: the image's real AAC-LC track (realshort.mp4, 48 kHz mono) and a random-syntax
+    44.1 kHz stereo ADTS stream. Parity with ffmpeg is unpinned."""
+    import os
+
+    from oracle import aac_oracle as aao
+
+    real = "/opt/conda/lib/python3.9/site-packages/imageio/resources/images/realshort.mp4"
+    cases = []
+    if os.path.exists(real):
+        data = open(real, "rb").read()
+        tr = audio.mp4_audio_track(data)
+        units = [data[o: o + s] for o, s in zip(tr.offsets.tolist(), tr.sizes.tolist())]
+        cases.append((data, aao.decode_raw(tr.config, units)))
+    adts = aao.write_adts(np.random.default_rng(12), sri=4, chan_config=2, nframes=10)
+    cases.append((adts, aao.decode_adts(adts)))
+    for data, (x, sr, _) in cases:
+        got = audio.load_input(data)
+        ref = ao.swr_resample(x.astype(np.float64).mean(axis=1), sr, 16000)
+        scale = max(1.0, float(np.abs(ref).max()))
+        assert got.shape == ref.shape and np.abs(got - ref).max() < TOL * scale
+
+
+def test_m4a_file_through_process_audio(tmp_path):
+    """An .m4a upload (the image's real AAC-LC track when present, else a random-syntax MP4) through
+    AudioProcessingPipeline.process_audio and the drop-in callable on the tiny.en engine: the duration is the
+    track's decoded length, and the transcript equals the one of the same upload handed over as the ingest's 16 kHz
+    array."""
+    import os
+
+    from oracle import aac_oracle as aao
+    from twamd.audio_pipeline import AudioProcessingPipeline
+    from twamd.pipeline import TurboTranscriber
+
+    real = "/opt/conda/lib/python3.9/site-packages/imageio/resources/images/realshort.mp4"
+    data = open(real, "rb").read() if os.path.exists(real) else aao.write_mp4(np.random.default_rng(3))[0]
+    path = str(tmp_path / "upload.m4a")
+    with open(path, "wb") as f:
+        f.write(data)
+    tr = TurboTranscriber.from_pretrained("tiny.en", seed=1234, max_batch=4)
+    pipe = AudioProcessingPipeline(transcriber=tr)
+    orig = pipe.transcribe
+    kw = dict(chunk_length_s=60, stride_length_s=5, generate_kwargs={"max_new_tokens": 32}, return_timestamps=True)
+
+    def _tr(audio_path, task="transcribe", **_):  # tiny.en is English-only: the reference's task kwarg raises
+        return tr(audio_path, **kw)
+
+    pipe.transcribe = _tr
+    res = pipe.process_audio(path)
+    pipe.transcribe = orig
+    assert "error" not in res, res
+    x, sr = audio.decode_mp4(data)
+    assert abs(res["duration"] - len(x) / sr) < 1e-6
+    wav = audio.load_input(data)
+    ref = tr(wav, **kw)
+    assert res["text"] == ref["text"] == tr(path, **kw)["text"]
 
 
 def test_flac_file_through_process_audio(tmp_path):

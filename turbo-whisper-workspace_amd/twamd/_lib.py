@@ -48,7 +48,8 @@ EXPORTED = (
     "tw_layernorm_set_lds_pad", "tw_gemv_set_variant",
     "tw_gemm_f32", "tw_layernorm_f32", "tw_im2col_conv1_f32", "tw_im2col_conv2_f32", "tw_embed_decoder_f32",
     "tw_attn_encoder_f32", "tw_attn_decode_self_f32", "tw_attn_decode_cross_f32", "tw_gemm_set_epilogue",
-    "tw_gemm_set_persistent_grid", "tw_mp3_probe", "tw_mp3_decode",
+    "tw_gemm_set_persistent_grid", "tw_mp3_probe", "tw_mp3_decode", "tw_aac_parse_asc", "tw_aac_decode_raw",
+    "tw_aac_adts_probe", "tw_aac_adts_decode",
 )
 
 
@@ -94,6 +95,13 @@ class TwMp3Info(ctypes.Structure):
         ("bitrate_kbps", ctypes.c_int32), ("total_samples", ctypes.c_int64), ("n_frames", ctypes.c_int64),
         ("skip_samples", ctypes.c_int64), ("samples_per_frame", ctypes.c_int32), ("enc_delay", ctypes.c_int32),
         ("enc_padding", ctypes.c_int32), ("flags", ctypes.c_int32),
+    ]
+
+
+class TwAacInfo(ctypes.Structure):
+    _fields_ = [
+        ("sample_rate", ctypes.c_int32), ("channels", ctypes.c_int32), ("object_type", ctypes.c_int32),
+        ("frame_length", ctypes.c_int32), ("n_frames", ctypes.c_int64), ("total_samples", ctypes.c_int64),
     ]
 
 
@@ -178,6 +186,11 @@ _SIGS = {
     "tw_vorbis_imdct": ([_P, _I, _P], _I),
     "tw_mp3_probe": ([_P, ctypes.c_int64, ctypes.POINTER(TwMp3Info)], _I),
     "tw_mp3_decode": ([_P, ctypes.c_int64, _P, ctypes.c_int64, _I, ctypes.POINTER(ctypes.c_int64)], _I),
+    "tw_aac_parse_asc": ([_P, _I, ctypes.POINTER(TwAacInfo)], _I),
+    "tw_aac_decode_raw": ([_P, _I, _P, ctypes.c_int64, _P, _P, ctypes.c_int64, _P, ctypes.c_int64, _I,
+                           ctypes.POINTER(ctypes.c_int64)], _I),
+    "tw_aac_adts_probe": ([_P, ctypes.c_int64, ctypes.POINTER(TwAacInfo)], _I),
+    "tw_aac_adts_decode": ([_P, ctypes.c_int64, _P, ctypes.c_int64, _I, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_layernorm_set_lds_pad": ([_I], _I),
     "tw_ima_adpcm_wav_decode": ([_P, ctypes.c_int64, _I, _I, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_resample_pcm_i32": ([_P, ctypes.c_int64, _I, _F, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),

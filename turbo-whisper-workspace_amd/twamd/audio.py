@@ -8,7 +8,9 @@ differs, multi-channel arrays are averaged to mono.
 
 Containers: FLAC (native multi-threaded decoder in libtwhip.so, include/tw_audio.h; bit-exact, verifiable
 against the stream's STREAMINFO MD5), Ogg Vorbis (native decoder, csrc/vorbis.cpp), MP3 (MPEG-1 / 2 / 2.5 Layer III,
-native multi-threaded decoder csrc/mp3.cpp, gapless-trimmed by the LAME tag as ffmpeg trims it), RIFF/WAVE (PCM 8/16/24/32-bit, IEEE float 32/64, G.711 A-law / mu-law, IMA
+native multi-threaded decoder csrc/mp3.cpp, gapless-trimmed by the LAME tag as ffmpeg trims it), AAC-LC (native
+decoder csrc/aac.cpp) in ADTS or in an MP4 / M4A track (demuxed here: stsz / stsc / stco, trimmed by the edit list;
+an MP4's MP3 track goes to the MP3 decoder), RIFF/WAVE (PCM 8/16/24/32-bit, IEEE float 32/64, G.711 A-law / mu-law, IMA
 ADPCM), Sun AU and AIFF / AIFF-C (PCM, float, G.711) — the telephony codecs through native decoders
 (tw_g711_decode, tw_ima_adpcm_wav_decode), pinned to CPython's audioop / aifc / sunau / wave.
 Resampling runs on the GPU (tw_resample_pcm_*) with libswresample's default filter restated in
@@ -186,6 +188,215 @@ def decode_mp3(data: bytes, threads: int = 0) -> Tuple[np.ndarray, int]:
                          ctypes.byref(got)) != 0:
         raise ValueError(lib.tw_last_error().decode(errors="replace"))
     return out[: got.value], sr
+
+
+def aac_adts_probe(data: bytes):
+    _lib, lib = _flac_lib()
+    info = _lib.TwAacInfo()
+    if lib.tw_aac_adts_probe(ctypes.c_char_p(data), len(data), ctypes.byref(info)) != 0:
+        raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    return info
+
+
+def decode_aac_adts(data: bytes, threads: int = 0) -> Tuple[np.ndarray, int]:
+    """ADTS AAC-LC bytes (.aac) -> f32 [frames, channels] through the native decoder (csrc/aac.cpp): every frame's 1024
+    samples, untrimmed (ADTS carries no priming information; ffmpeg does not trim it either)."""
+    _lib, lib = _flac_lib()
+    info = aac_adts_probe(data)
+    total, ch, sr = int(info.total_samples), int(info.channels), int(info.sample_rate)
+    if total > max_audio_seconds() * sr:
+        raise ValueError(f"AAC stream longer than TW_MAX_AUDIO_S={max_audio_seconds():g} s")
+    out = np.zeros((total, ch), np.float32)
+    got = ctypes.c_int64()
+    if lib.tw_aac_adts_decode(ctypes.c_char_p(data), len(data), out.ctypes.data, total, int(threads),
+                              ctypes.byref(got)) != 0:
+        raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    return out[: got.value], sr
+
+
+class Mp4Track(NamedTuple):
+    codec: str               # "aac" or "mp3"
+    config: bytes            # AAC AudioSpecificConfig (b"" for MP3)
+    sample_rate: int
+    channels: int
+    offsets: np.ndarray      # int64 byte offset of each access unit in the file
+    sizes: np.ndarray        # int64 size of each access unit
+    timescale: int           # the track's (mdhd) time units per second
+    edit: Optional[Tuple[int, int]]  # first non-empty edit: (media_time, duration), both in the track's timescale
+    duration: int            # mdhd duration (track timescale)
+
+
+def _mp4_boxes(data: bytes, start: int, end: int):
+    pos = start
+    while pos + 8 <= end:
+        size, typ = struct.unpack(">I4s", data[pos: pos + 8])
+        hdr = 8
+        if size == 1:
+            if pos + 16 > end:
+                break
+            size, hdr = struct.unpack(">Q", data[pos + 8: pos + 16])[0], 16
+        elif size == 0:
+            size = end - pos
+        if size < hdr or pos + size > end:
+            raise ValueError(f"MP4: box {typ!r} at {pos} overruns its parent")
+        yield typ, pos + hdr, pos + size
+        pos += size
+
+
+def _desc(data: bytes, pos: int):
+    """An MPEG-4 descriptor at pos: (tag, body start, body end)."""
+    tag, pos, n = data[pos], pos + 1, 0
+    for _ in range(4):
+        b = data[pos]
+        pos += 1
+        n = (n << 7) | (b & 0x7F)
+        if not b & 0x80:
+            break
+    return tag, pos, pos + n
+
+
+def _esds_config(data: bytes, a: int, b: int) -> Tuple[int, bytes]:
+    """(objectTypeIndication, DecoderSpecificInfo) of an esds box body."""
+    tag, p, e = _desc(data, a + 4)  # (version / flags)
+    if tag != 3:
+        raise ValueError("MP4: esds without an ES_Descriptor")
+    flags = data[p + 2]
+    p += 3 + (2 if flags & 0x80 else 0)
+    if flags & 0x40:
+        p += 1 + data[p]
+    p += 2 if flags & 0x20 else 0
+    tag, q, qe = _desc(data, p)
+    if tag != 4:
+        raise ValueError("MP4: esds without a DecoderConfigDescriptor")
+    oti = data[q]
+    cfg = b""
+    if q + 13 < qe:
+        tag, r, re_ = _desc(data, q + 13)
+        if tag == 5:
+            cfg = data[r: re_]
+    return oti, cfg
+
+
+def mp4_audio_track(data: bytes) -> Mp4Track:
+    """The first sound track of an MP4 / M4A / MOV file: its codec configuration, the file offset and size of every
+    access unit (stsz, stsc, stco / co64) and its first edit (elst), as ffmpeg's mov demuxer reads them."""
+    moov = next(((a, b) for t, a, b in _mp4_boxes(data, 0, len(data)) if t == b"moov"), None)
+    if moov is None:
+        raise ValueError("MP4: no moov box" + (" (fragmented MP4 is not supported)" if b"moof" in data[:4096] else ""))
+    movie_ts = 1000
+    for t, a, b in _mp4_boxes(data, *moov):
+        if t == b"mvhd":
+            movie_ts = struct.unpack(">I", data[a + (20 if data[a] == 1 else 12): a + (24 if data[a] == 1 else 16)])[0]
+    for t, a, b in _mp4_boxes(data, *moov):
+        if t != b"trak":
+            continue
+        box = {}
+
+        def walk(lo, hi):
+            for tt, aa, bb in _mp4_boxes(data, lo, hi):
+                if tt in (b"mdia", b"minf", b"stbl", b"edts"):
+                    walk(aa, bb)
+                else:
+                    box.setdefault(tt, (aa, bb))
+        walk(a, b)
+        if b"hdlr" not in box or data[box[b"hdlr"][0] + 8: box[b"hdlr"][0] + 12] != b"soun":
+            continue
+        ha, _ = box[b"mdhd"]
+        if data[ha] == 1:
+            ts, dur = struct.unpack(">IQ", data[ha + 20: ha + 32])
+        else:
+            ts, dur = struct.unpack(">II", data[ha + 12: ha + 20])
+        sa, sb = box[b"stsd"]
+        ea = sa + 8  # (version / flags, entry count)
+        esize, etype = struct.unpack(">I4s", data[ea: ea + 8])
+        ver = struct.unpack(">H", data[ea + 16: ea + 18])[0]
+        channels = struct.unpack(">H", data[ea + 24: ea + 26])[0]
+        rate = struct.unpack(">I", data[ea + 32: ea + 36])[0] >> 16
+        child = ea + 36 + {0: 0, 1: 16, 2: 36}.get(ver, 0)
+        codec, cfg = None, b""
+        if etype in (b".mp3", b"mp3 "):
+            codec = "mp3"
+        elif etype == b"mp4a":
+            for tt, aa, bb in _mp4_boxes(data, child, ea + esize):
+                if tt == b"esds":
+                    oti, cfg = _esds_config(data, aa, bb)
+                    codec = {0x40: "aac", 0x66: "aac-main", 0x67: "aac", 0x68: "aac-ssr", 0x69: "mp3",
+                             0x6B: "mp3"}.get(oti, f"object type 0x{oti:02x}")
+                    if oti == 0x67:  # MPEG-2 AAC LC: no AudioSpecificConfig object type of its own
+                        cfg = cfg or bytes([0x10 | 0, 0])
+        if codec is None:
+            raise ValueError(f"MP4: sound track codec {etype.decode(errors='replace')!r} is not decoded")
+        # sample table
+        za, _ = box[b"stsz"]
+        fixed, count = struct.unpack(">II", data[za + 4: za + 12])
+        sizes = (np.full(count, fixed, np.int64) if fixed else
+                 np.frombuffer(data, ">u4", count, za + 12).astype(np.int64))
+        if b"co64" in box:
+            ca, _ = box[b"co64"]
+            chunks = np.frombuffer(data, ">u8", struct.unpack(">I", data[ca + 4: ca + 8])[0], ca + 8).astype(np.int64)
+        else:
+            ca, _ = box[b"stco"]
+            chunks = np.frombuffer(data, ">u4", struct.unpack(">I", data[ca + 4: ca + 8])[0], ca + 8).astype(np.int64)
+        qa, _ = box[b"stsc"]
+        runs = np.frombuffer(data, ">u4", 3 * struct.unpack(">I", data[qa + 4: qa + 8])[0], qa + 8).reshape(-1, 3)
+        per_chunk = np.zeros(len(chunks), np.int64)
+        for i, (first, spc, _) in enumerate(runs):
+            last = runs[i + 1][0] - 1 if i + 1 < len(runs) else len(chunks)
+            per_chunk[int(first) - 1: int(last)] = int(spc)
+        if int(per_chunk.sum()) < count:
+            raise ValueError("MP4: the sample-to-chunk table covers fewer samples than stsz")
+        chunk_of = np.repeat(np.arange(len(chunks)), per_chunk)[:count]
+        first_in_chunk = np.concatenate([[0], np.cumsum(per_chunk)[:-1]])[chunk_of]
+        csum = np.concatenate([[0], np.cumsum(sizes)])
+        offsets = chunks[chunk_of] + csum[np.arange(count)] - csum[first_in_chunk]
+        if count and int((offsets + sizes).max()) > len(data):
+            raise ValueError("MP4: an access unit lies beyond the end of the file (truncated upload)")
+        edit = None
+        if b"elst" in box:
+            la, _ = box[b"elst"]
+            v, n = data[la], struct.unpack(">I", data[la + 4: la + 8])[0]
+            fmt, w = (">Qq", 16) if v == 1 else (">Ii", 8)
+            for i in range(n):
+                sdur, mtime = struct.unpack(fmt, data[la + 8 + i * (w + 4): la + 8 + i * (w + 4) + w])
+                if mtime >= 0:
+                    edit = (int(mtime), int(round(sdur * ts / movie_ts)))
+                    break
+        return Mp4Track(codec, cfg, int(rate), int(channels), offsets, sizes, int(ts), edit, int(dur))
+    raise ValueError("MP4: no sound track")
+
+
+def decode_mp4(data: bytes, threads: int = 0) -> Tuple[np.ndarray, int]:
+    """MP4 / M4A bytes -> f32 [frames, channels]: the first sound track (AAC-LC through tw_aac_decode_raw, MP3 through
+    tw_mp3_decode), trimmed by its first edit (elst media_time skipped, the edit's duration kept), as ffmpeg's mov
+    demuxer presents it."""
+    _lib, lib = _flac_lib()
+    tr = mp4_audio_track(data)
+    n = len(tr.sizes)
+    if tr.codec == "mp3":
+        au = b"".join(data[o: o + s] for o, s in zip(tr.offsets.tolist(), tr.sizes.tolist()))
+        x, sr = decode_mp3(au, threads)
+    elif tr.codec == "aac":
+        info = _lib.TwAacInfo()
+        if lib.tw_aac_parse_asc(ctypes.c_char_p(tr.config), len(tr.config), ctypes.byref(info)) != 0:
+            raise ValueError(lib.tw_last_error().decode(errors="replace"))
+        sr, ch = int(info.sample_rate), int(info.channels)
+        if n * 1024 > max_audio_seconds() * sr:
+            raise ValueError(f"MP4 track longer than TW_MAX_AUDIO_S={max_audio_seconds():g} s")
+        x = np.zeros((n * 1024, ch), np.float32)
+        off = np.ascontiguousarray(tr.offsets, np.int64)
+        siz = np.ascontiguousarray(tr.sizes, np.int64)
+        got = ctypes.c_int64()
+        if lib.tw_aac_decode_raw(ctypes.c_char_p(tr.config), len(tr.config), ctypes.c_char_p(data), len(data),
+                                 off.ctypes.data, siz.ctypes.data, n, x.ctypes.data, len(x), int(threads),
+                                 ctypes.byref(got)) != 0:
+            raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    else:
+        raise ValueError(f"MP4 sound track codec {tr.codec} is not decoded (AAC-LC and MP3 are)")
+    if tr.edit is not None:
+        scale = sr / tr.timescale
+        skip, keep = int(round(tr.edit[0] * scale)), int(round(tr.edit[1] * scale))
+        x = x[skip: skip + keep]
+    return x, sr
 
 
 def g711_decode(codes: bytes, alaw: bool) -> np.ndarray:
@@ -423,9 +634,10 @@ def container_name(data: bytes) -> Optional[str]:
     return _mpeg_audio_name(data)
 
 
-_DECODERS = {"WAV": decode_wav, "AU": decode_au, "AIFF": decode_aiff, "Ogg Vorbis": decode_vorbis, "MP3": decode_mp3}
-DECODED = "FLAC, Ogg Vorbis, MP3 (MPEG-1 / 2 / 2.5 Layer III), WAV (PCM, float, A-law, mu-law, IMA ADPCM), AU, " \
-          "AIFF / AIFF-C"
+_DECODERS = {"WAV": decode_wav, "AU": decode_au, "AIFF": decode_aiff, "Ogg Vorbis": decode_vorbis, "MP3": decode_mp3,
+             "AAC (ADTS)": decode_aac_adts, "MP4/M4A": decode_mp4}
+DECODED = "FLAC, Ogg Vorbis, MP3 (MPEG-1 / 2 / 2.5 Layer III), AAC-LC (M4A / MP4, ADTS), WAV (PCM, float, A-law, " \
+          "mu-law, IMA ADPCM), AU, AIFF / AIFF-C"
 
 
 def decode_bytes(data: bytes, sr_out: int = TARGET_SR, device=None) -> np.ndarray:
@@ -484,6 +696,9 @@ def duration_seconds(path: str) -> float:
         return int(info.total_samples) / float(info.sample_rate)
     if name == "MP3":
         info = mp3_probe(data)
+        return int(info.total_samples) / float(info.sample_rate)
+    if name == "AAC (ADTS)":
+        info = aac_adts_probe(data)
         return int(info.total_samples) / float(info.sample_rate)
     if name in _DECODERS:
         x, sr = _DECODERS[name](data)
