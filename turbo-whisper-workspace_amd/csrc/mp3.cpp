@@ -265,10 +265,10 @@ struct Tables {
   float pow43[8207];
   float win[4][36];     // long block windows by block_type (2: the short window in [0, 12))
   float cos36[18][36];  // IMDCT-36: cos(pi/72 (2i + 19)(2k + 1)) x window, per block type below
-  float imdct_long[4][36][18];
-  float imdct_short[12][6];  // cos(pi/24 (2i + 7)(2k + 1)) x short window
+  float imdct_long[4][18][36];  // [block type][k][i]: the inner loops run over i (vectorised)
+  float imdct_short[6][12];     // [k][i]: cos(pi/24 (2i + 7)(2k + 1)) x short window
   float cs[8], ca[8];
-  float N[64][32];  // synthesis matrixing cos((16 + i)(2k + 1) pi / 64)
+  float N[32][64];  // synthesis matrixing cos((16 + i)(2k + 1) pi / 64), [k][i]
   float D[512];     // synthesis window
   float is_ratio[16][2];  // MPEG-1 intensity (left, right) by is_pos
   Tables() {
@@ -300,18 +300,18 @@ struct Tables {
     for (int bt = 0; bt < 4; bt++)
       for (int i = 0; i < 36; i++)
         for (int k = 0; k < 18; k++)
-          imdct_long[bt][i][k] =
+          imdct_long[bt][k][i] =
               (float)(cos(M_PI / 72 * (2 * i + 19) * (2 * k + 1)) * (bt == 2 ? 0.0 : (double)win[bt][i]));
     for (int i = 0; i < 12; i++)
       for (int k = 0; k < 6; k++)
-        imdct_short[i][k] = (float)(cos(M_PI / 24 * (2 * i + 7) * (2 * k + 1)) * sin(M_PI / 12 * (i + 0.5)));
+        imdct_short[k][i] = (float)(cos(M_PI / 24 * (2 * i + 7) * (2 * k + 1)) * sin(M_PI / 12 * (i + 0.5)));
     for (int i = 0; i < 8; i++) {
       const double c = kAliasC[i], r = sqrt(1.0 + c * c);
       cs[i] = (float)(1.0 / r);
       ca[i] = (float)(c / r);
     }
     for (int i = 0; i < 64; i++)
-      for (int k = 0; k < 32; k++) N[i][k] = (float)cos((16 + i) * (2 * k + 1) * M_PI / 64);
+      for (int k = 0; k < 32; k++) N[k][i] = (float)cos((16 + i) * (2 * k + 1) * M_PI / 64);
     for (int i = 0; i < 512; i++) {
       const int j = i <= 256 ? i : 512 - i;
       D[i] = (float)(kWin[j] * (((i >> 6) & 1) ? -1.0 : 1.0) / 65536.0);
@@ -707,20 +707,22 @@ struct Decoder {
         for (int i = 0; i < 36; i++) z[i] = 0.f;
       } else if (sb < long_end) {
         const int bt = shortb ? 0 : g.block_type;
-        for (int i = 0; i < 36; i++) {
-          float s = 0.f;
-          const float* c = T.imdct_long[bt][i];
-          for (int k = 0; k < 18; k++) s += c[k] * X[k];
-          z[i] = s;
+        for (int i = 0; i < 36; i++) z[i] = 0.f;
+        for (int k = 0; k < 18; k++) {
+          const float xk = X[k];
+          const float* c = T.imdct_long[bt][k];
+          for (int i = 0; i < 36; i++) z[i] += c[i] * xk;
         }
       } else {
         for (int i = 0; i < 36; i++) z[i] = 0.f;
-        for (int w = 0; w < 3; w++)
-          for (int i = 0; i < 12; i++) {
-            float s = 0.f;
-            for (int k = 0; k < 6; k++) s += T.imdct_short[i][k] * X[3 * k + w];
-            z[6 + 6 * w + i] += s;
+        for (int w = 0; w < 3; w++) {
+          float y[12] = {0.f};
+          for (int k = 0; k < 6; k++) {
+            const float xk = X[3 * k + w];
+            for (int i = 0; i < 12; i++) y[i] += T.imdct_short[k][i] * xk;
           }
+          for (int i = 0; i < 12; i++) z[6 + 6 * w + i] += y[i];
+        }
       }
       for (int i = 0; i < 18; i++) {
         float v = z[i] + ov[sb][i];
@@ -736,21 +738,24 @@ struct Decoder {
     for (int s = 0; s < 18; s++) {
       voff = (voff - 64) & 1023;
       const float* S = sbs[s];
-      float vv[64];
-      for (int i = 0; i < 64; i++) {
-        float a = 0.f;
-        for (int k = 0; k < 32; k++) a += T.N[i][k] * S[k];
-        vv[i] = a;
+      // matrixing into the newest 64-value block of V (voff is a multiple of 64, so every block is contiguous)
+      float* vv = V + voff;
+      for (int i = 0; i < 64; i++) vv[i] = 0.f;
+      for (int k = 0; k < 32; k++) {
+        const float sk = S[k];
+        if (sk == 0.f) continue;
+        const float* n = T.N[k];
+        for (int i = 0; i < 64; i++) vv[i] += n[i] * sk;
       }
-      for (int i = 0; i < 64; i++) V[(voff + i) & 1023] = vv[i];
-      for (int j = 0; j < 32; j++) {
-        float a = 0.f;
-        for (int i = 0; i < 8; i++) {
-          a += V[(voff + 128 * i + j) & 1023] * T.D[64 * i + j];
-          a += V[(voff + 128 * i + 96 + j) & 1023] * T.D[64 * i + 32 + j];
-        }
-        pcm[(size_t)(s * 32 + j) * stride] = a;
+      // windowing: out[j] = sum_i V[128 i + j] D[64 i + j] + V[128 i + 96 + j] D[64 i + 32 + j] over 32 contiguous j
+      float acc[32] = {0.f};
+      for (int i = 0; i < 8; i++) {
+        const float* v0 = V + ((voff + 128 * i) & 1023);
+        const float* v1 = V + ((voff + 128 * i + 96) & 1023);
+        const float* d0 = T.D + 64 * i;
+        for (int j = 0; j < 32; j++) acc[j] += v0[j] * d0[j] + v1[j] * d0[32 + j];
       }
+      for (int j = 0; j < 32; j++) pcm[(size_t)(s * 32 + j) * stride] = acc[j];
     }
   }
 
