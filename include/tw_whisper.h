@@ -269,6 +269,37 @@ int tw_gemm_set_epilogue(int tr);
 /* Workgroups of the persistent large-M GEMM (tw_gemm_set_variant(6)): 0 = one per CU, else n (a multiple of 8, one per
  * CU on n / 8 CUs of every XCD) — the rest of the CUs stay free for other queues' kernels. */
 int tw_gemm_set_persistent_grid(int n);
+/* ---- the decoder's layers as one persistent launch ------------------------------------------------- */
+/* One decoder layer's parameters (device memory, an array of n_layers): packed weights (tw_pack_weight of the
+ * [N][K] projections, q pre-scaled as for the launch chain), f32 biases and LayerNorm parameters. */
+typedef struct TwDecLayerW {
+  const uint16_t *wqkv, *wo, *wq_x, *wo_x, *w1, *w2;
+  const float *bqkv, *bo, *bq_x, *bo_x, *b1, *b2;
+  const float *ln1_g, *ln1_b, *ln2_g, *ln2_b, *ln3_g, *ln3_b;
+} TwDecLayerW;
+/* tw_dec_fused: WhisperDecoder's layers for one token of R <= 32 rows ($TF/models/whisper/modeling_whisper.py:
+ * 448-505 per layer, then the final layer_norm :682) — what the launch chain of residual + LayerNorm, q/k/v, self-
+ * attention, out_proj, cross-q, cross-attention, out_proj, fc1 and fc2 kernels computes — as ONE persistent launch
+ * of one workgroup per CU whose phases hand off through device-memory counters (d_model 1280, 20 heads, ffn 5120:
+ * tw_dec_fused_supported). In: x f32 [R][1280] = the token + position embedding (tw_embed_decoder); the self K/V
+ * caches kc / vc ([rows][20][max_pos][64] per layer, layer l at + l * kv_layer_stride elements) hold positions
+ * < pos[r]; the cross K/V of layer l at xkv + l * xkv_layer_stride (K) and + xkv_v_off (V), [rows][20][S][64].
+ * Out: x = the last layer's output, the caches appended at pos, hp = the final LayerNorm as a packed activation
+ * (proj_out's tw_gemv_packed operand). Scratch: qb, ab bf16 [R][1280], fb packed [32][5120], slab f32 [4][R][1280],
+ * sync: tw_dec_fused_sync_bytes() bytes, 16-byte aligned (zeroed by the call, on the stream). err: a sticky word the
+ * caller zeroes once; a phase wait that times out sets it (0x100 + phase) and the launch's outputs are void. The
+ * caller must not run other work on the device that waits for this launch's completion from inside a kernel. */
+size_t tw_dec_fused_sync_bytes(void);
+int tw_dec_fused_supported(int d_model, int heads, int ffn, int rows);
+/* Workgroups per launch (0 = the device's CU count, the default; n <= the CU count keeps every workgroup resident). */
+int tw_dec_fused_set_grid(int n);
+/* 1: an agent-scope acquire fence after every phase wait in addition to the sc1 (L1-bypassing) loads of every
+ * handed-off byte; 0 (default): the loads alone. The same results either way (A/B switch). Returns 0. */
+int tw_dec_fused_set_acquire(int on);
+int tw_dec_fused(const TwDecLayerW* layers, int n_layers, int R, const int* pos, float* x, uint16_t* kc,
+                 uint16_t* vc, long kv_layer_stride, int max_pos, const uint16_t* xkv, long xkv_layer_stride,
+                 long xkv_v_off, int S, uint16_t* qb, uint16_t* ab, uint16_t* fb, float* slab, const float* lnf_g,
+                 const float* lnf_b, uint16_t* hp, float eps, unsigned* sync, unsigned* err, void* stream);
 /* tw_resid_layernorm with the normalised rows written as a packed activation (M <= 64, D % 32 == 0). */
 int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
                               const float* beta, int M, int D, float eps, uint16_t* out, void* stream);

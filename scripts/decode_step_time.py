@@ -3,7 +3,10 @@ decoder step (47 launches per token), for several row counts. One pass = the pro
 detection, task token) + 128 generated tokens with EOS suppressed, i.e. 130 decoder steps; the encoder runs once
 before, untimed. Prints one JSON line per (rows, mode).
 
-    python scripts/decode_step_time.py [--rows 15 24 64] [--reps 3]
+    python scripts/decode_step_time.py [--rows 15 24 64] [--reps 3] [--fused 0 1]
+
+--fused 1: the decoder's layers as one persistent launch (WhisperEngine.dec_fused_alone, tw_dec_fused; rows <= 32),
+0: the launch chain; with both, each row count runs both and reports whether their tokens agree.
 """
 import argparse
 import json
@@ -27,6 +30,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--check-every", type=int, nargs="+", default=[8])
     ap.add_argument("--graph-steps", type=int, nargs="+", default=[1])
+    ap.add_argument("--fused", type=int, nargs="+", default=[0])
     ap.add_argument("--slope", type=int, default=0, help="also time 64-token passes: per-step slope without the "
                     "pass's fixed costs")
     a = ap.parse_args()
@@ -44,41 +48,45 @@ def main():
         eng.encode(R)
         torch.cuda.synchronize()
         ref = None
-        for ce in a.check_every:
-            for gs in a.graph_steps:
-                eng.graph_steps_alone = gs
-                eng._graphs.clear()
-                eng.decode_pass(R, tail, None, 128, check_every=ce)  # warm-up: graph captures
+        for fz, ce, gs in [(f, c, g) for f in a.fused for c in a.check_every for g in a.graph_steps]:
+            if fz and R > 32:
+                continue
+            eng.dec_fused_alone = bool(fz)
+            eng.graph_steps_alone = gs
+            eng._graphs.clear()
+            eng.decode_pass(R, tail, None, 128, check_every=ce)  # warm-up: graph captures
+            torch.cuda.synchronize()
+            best = 1e9
+            eng.pass_events = []
+            for _ in range(a.reps):
+                t0 = time.perf_counter()
+                res = eng.decode_pass(R, tail, None, 128, check_every=ce)
                 torch.cuda.synchronize()
-                best = 1e9
-                eng.pass_events = []
+                best = min(best, time.perf_counter() - t0)
+            loop_us = min(e0.elapsed_time(e1) * 1e3 / n for e0, e1, n, _ in eng.pass_events)
+            eng.pass_events = None
+            print(json.dumps({"rows": R, "fused": fz, "check_every": ce, "graph_steps": gs,
+                              "loop_us_per_step": round(loop_us, 1)}),
+                  flush=True)
+            assert all(len(t) == 128 for t in res.tokens)
+            ref = res.tokens if ref is None else ref
+            if a.slope:
+                eng.decode_pass(R, tail, None, 64, check_every=ce)
+                torch.cuda.synchronize()
+                b64 = 1e9
                 for _ in range(a.reps):
                     t0 = time.perf_counter()
-                    res = eng.decode_pass(R, tail, None, 128, check_every=ce)
-                    torch.cuda.synchronize()
-                    best = min(best, time.perf_counter() - t0)
-                loop_us = min(e0.elapsed_time(e1) * 1e3 / n for e0, e1, n, _ in eng.pass_events)
-                eng.pass_events = None
-                print(json.dumps({"rows": R, "check_every": ce, "graph_steps": gs, "loop_us_per_step": round(loop_us, 1)}),
-                      flush=True)
-                assert all(len(t) == 128 for t in res.tokens)
-                ref = res.tokens if ref is None else ref
-                if a.slope:
                     eng.decode_pass(R, tail, None, 64, check_every=ce)
                     torch.cuda.synchronize()
-                    b64 = 1e9
-                    for _ in range(a.reps):
-                        t0 = time.perf_counter()
-                        eng.decode_pass(R, tail, None, 64, check_every=ce)
-                        torch.cuda.synchronize()
-                        b64 = min(b64, time.perf_counter() - t0)
-                    print(json.dumps({"rows": R, "check_every": ce, "graph_steps": gs,
-                                      "pass64_ms": round(b64 * 1e3, 2),
-                                      "slope_us_per_step": round((best - b64) * 1e6 / 64, 1),
-                                      "fixed_ms": round((b64 - 66 * (best - b64) / 64) * 1e3, 2)}), flush=True)
-                print(json.dumps({"rows": R, "check_every": ce, "graph_steps": gs, "pass_ms": round(best * 1e3, 2),
-                                  "step_us": round(best * 1e6 / 130, 1), "tokens_equal": res.tokens == ref}),
-                      flush=True)
+                    b64 = min(b64, time.perf_counter() - t0)
+                print(json.dumps({"rows": R, "check_every": ce, "graph_steps": gs,
+                                  "pass64_ms": round(b64 * 1e3, 2),
+                                  "slope_us_per_step": round((best - b64) * 1e6 / 64, 1),
+                                  "fixed_ms": round((b64 - 66 * (best - b64) / 64) * 1e3, 2)}), flush=True)
+            print(json.dumps({"rows": R, "fused": fz, "check_every": ce, "graph_steps": gs,
+                              "pass_ms": round(best * 1e3, 2),
+                              "step_us": round(best * 1e6 / 130, 1), "tokens_equal": res.tokens == ref}),
+                  flush=True)
 
 
 if __name__ == "__main__":

@@ -129,6 +129,7 @@ class DecView:
     pos: torch.Tensor
     hp: torch.Tensor   # packed-activation LayerNorm output (tw_gemv_packed A operand), <= VIEW_ROWS rows
     fp: torch.Tensor   # packed-activation fc1 output (fc2's A operand)
+    fsync: Optional[torch.Tensor] = None  # tw_dec_fused's counter words for this view's launches
 
 
 class _EncoderPump:
@@ -301,7 +302,12 @@ class WhisperEngine:
         # prefix; while _masked, the self-attention masks those positions (tw_attn_decode_self_masked)
         self._kv_start = torch.zeros(self.max_rows, dtype=torch.int32, device=dev)
         self._masked = False
-        self._dec_ctx = (1, 0)  # the library's (tw_gemv_set_wide_slices, tw_gemv_set_variant) state (its defaults)
+        # the library's (tw_gemv_set_wide_slices, tw_gemv_set_variant) state (its defaults) and whether the decoder's
+        # layers run as one persistent launch (tw_dec_fused) in the current pass
+        self._dec_ctx = (1, 0, False)
+        self._fused_dims = (not self.F32 and bool(_lib.load().tw_dec_fused_supported(D, H, d.ffn, 1)))
+        self._fused_tab: Optional[torch.Tensor] = None  # device TwDecLayerW table (below, with the packed weights)
+        self._fused_err = torch.zeros(4, dtype=torch.int32, device=dev)  # sticky phase-timeout word
         self._beam: Optional[dict] = None  # beam-search buffers, allocated on first use
         self._align: Optional[dict] = None  # token-level timestamps: alignment-head attention recording
         self._align_buf: Optional[torch.Tensor] = None
@@ -348,6 +354,8 @@ class WhisperEngine:
                 self.dec_p = [{k: self._pack(getattr(L, k)) for k in ("wqkv", "wo", "wq_x", "wo_x", "w1", "w2")}
                               for L in weights.dec]
                 self.emb_p = self._pack(weights.emb)
+                if self._fused_dims:
+                    self._fused_tab = self._fused_table()
                 torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ lifetime
@@ -552,9 +560,11 @@ class WhisperEngine:
         adt = torch.float32 if self.F32 else torch.bfloat16
         hp = torch.zeros(VIEW_ROWS * self.d.d_model, dtype=adt, device=self.device)
         fp = torch.zeros(VIEW_ROWS * self.d.ffn, dtype=adt, device=self.device)
+        fsync = (torch.zeros(int(_lib.load().tw_dec_fused_sync_bytes()) // 4, dtype=torch.int32, device=self.device)
+                 if self._fused_dims else None)
         return DecView(r0, n, stream or self.stream, self.xd[sl], self.qkvd[sl], self.qd[sl], self.attd[sl],
                        self.logits[sl], self.parts if parts is None else parts, self.sel_ws[sl], self.state[sl],
-                       self.tokens[sl], self.ids[sl], self.pos[sl], hp, fp)
+                       self.tokens[sl], self.ids[sl], self.pos[sl], hp, fp, fsync)
 
     @on_engine_streams
     def set_long_input(self, wave: Optional[torch.Tensor]) -> int:
@@ -764,6 +774,11 @@ class WhisperEngine:
         if not pre_embedded:
             _lib.call("tw_embed_decoder", w.emb.data_ptr(), w.pos_dec.data_ptr(), v.ids.data_ptr(), v.pos.data_ptr(), R,
                       D, v.xd.data_ptr(), s)
+        if self._fused_ok(R):  # the layers as one persistent launch (it recomputes layer 0's LayerNorm itself)
+            self._fused_layers(R, r_enc, v)
+            if with_logits:
+                self._gemv(v.hp, True, self.emb_p, R, d.vocab, D, _lib.TW_EPI_F32, v.logits, v)
+            return
         xkv_stride = 2 * r_enc * H * S_ENC * 64
         nparts, pbias = 0, None
         PART, K4 = _lib.TW_EPI_PARTIAL_F32, DEC_SPLITS
@@ -952,6 +967,11 @@ class WhisperEngine:
     dec_alone_gemv = 1
     dec_beside_gemv = 0
 
+    # The decoder's layers for a decode pass alone as ONE persistent launch (tw_dec_fused, csrc/decfused.hip) instead
+    # of the 45-launch chain; rows <= 32, greedy / sampled passes without beams, prompt masks or alignment heads.
+    # Beside an encoder chunk the chain stays (a persistent grid would hold every CU the encoder GEMM needs).
+    dec_fused_alone = False
+
     @property
     def _wide_kw(self) -> int:
         return self._dec_ctx[0]
@@ -961,13 +981,52 @@ class WhisperEngine:
         kernel): alone unless run_batches' encoder pump is queued beside it. Graph keys carry the returned value (a
         captured step bakes the launches it recorded)."""
         beside = self._pump is not None
-        ctx = ((self.dec_beside_wide_kw, self.dec_beside_gemv) if beside
-               else (self.dec_alone_wide_kw, self.dec_alone_gemv))
-        if ctx != self._dec_ctx:
+        ctx = ((self.dec_beside_wide_kw, self.dec_beside_gemv, False) if beside
+               else (self.dec_alone_wide_kw, self.dec_alone_gemv, bool(self.dec_fused_alone and self._fused_dims)))
+        if ctx[:2] != self._dec_ctx[:2]:
             _lib.call("tw_gemv_set_wide_slices", ctx[0])
             _lib.call("tw_gemv_set_variant", ctx[1])
-            self._dec_ctx = ctx
+        self._dec_ctx = ctx
         return ctx
+
+    def _fused_ok(self, R: int) -> bool:
+        """The current step runs as tw_dec_fused (see dec_fused_alone)."""
+        return (self._dec_ctx[2] and R <= 32 and self._kv_tab is None and not self._masked and self._align is None
+                and not self._use_dec_row_map)
+
+    def _fused_layers(self, R: int, r_enc: int, v: DecView) -> None:
+        """tw_dec_fused for the view's rows: xd (the embedded token) -> the last layer's output, the self K/V caches
+        appended, hp = the final LayerNorm (proj_out's packed operand)."""
+        d, w = self.d, self.w
+        H, T = d.heads, d.max_target_positions
+        esz = self.cross_kv.element_size()
+        xkv = self.cross_kv.data_ptr() + v.r0 * H * S_ENC * 64 * esz
+        _lib.call("tw_dec_fused", self._fused_tab.data_ptr(), d.decoder_layers, R, v.pos.data_ptr(), v.xd.data_ptr(),
+                  self.kcache[0, v.r0].data_ptr(), self.vcache[0, v.r0].data_ptr(), self.kcache.stride(0), T, xkv,
+                  2 * r_enc * H * S_ENC * 64, r_enc * H * S_ENC * 64, S_ENC, v.qd.data_ptr(), v.attd.data_ptr(),
+                  v.fp.data_ptr(), v.parts.data_ptr(), w.dec_ln_g.data_ptr(), w.dec_ln_b.data_ptr(), v.hp.data_ptr(),
+                  LN_EPS, v.fsync.data_ptr(), self._fused_err.data_ptr(), v.stream.cuda_stream)
+
+    def _fused_table(self) -> torch.Tensor:
+        """tw_dec_fused's layer table: per decoder layer the TwDecLayerW pointers (packed weights, f32 biases and
+        LayerNorm parameters), int64 [layers][18] on the device."""
+        names_w = ("wqkv", "wo", "wq_x", "wo_x", "w1", "w2")
+        names_f = ("bqkv", "bo", "bq_x", "bo_x", "b1", "b2", "ln1_g", "ln1_b", "ln2_g", "ln2_b", "ln3_g", "ln3_b")
+        rows = []
+        for L, P in zip(self.w.dec, self.dec_p):
+            for k in names_f:
+                t = getattr(L, k)
+                if t.dtype != torch.float32 or not t.is_contiguous():
+                    raise ValueError(f"tw_dec_fused: decoder {k} must be contiguous f32")
+            rows.append([P[k].data_ptr() for k in names_w] + [getattr(L, k).data_ptr() for k in names_f])
+        return torch.tensor(rows, dtype=torch.int64, device=self.device)
+
+    def check_fused(self) -> None:
+        """Raise if a tw_dec_fused launch since the last check timed out in a phase wait (its outputs are void)."""
+        e = int(self._fused_err[0].item())
+        if e:
+            self._fused_err.zero_()
+            raise _lib.TwError(f"tw_dec_fused: a phase wait timed out (code {e:#x}); the decode pass is void")
 
     def _prompt_len(self, tail: Sequence[int], prefix=None) -> int:
         """decoder_input_ids' length: [prefix] + SOT (+ language) + tail (num_input_ids of the token timestamps)."""
@@ -1180,6 +1239,8 @@ class WhisperEngine:
             self.pass_events.append((ev0, ev1, steps - 1, time.perf_counter() - th0))
         ngen = self.state[:R, _lib.TW_ST_NGEN].tolist()
         toks = self.tokens[:R].tolist()
+        if self._dec_ctx[2]:
+            self.check_fused()
         detected = self.state[:R, _lib.TW_ST_LANG].tolist() if detect else None  # (mode-1 selection only writes it)
         return PassResult([toks[r][: ngen[r]] for r in range(R)], detected if lang_ids is None else list(lang_ids))
 
@@ -1268,6 +1329,8 @@ class WhisperEngine:
             self._row_group = 1
         ngen = stt[:, _lib.TW_ST_NGEN].tolist()
         toks = self.tokens[:R].tolist()
+        if self._dec_ctx[2]:
+            self.check_fused()
         f32 = stt.view(torch.float32)
         return PassResult([toks[r][: ngen[r]] for r in range(R)],
                           stt[:, _lib.TW_ST_LANG].tolist() if detect else list(lang_ids) if lang_ids is not None else None,
