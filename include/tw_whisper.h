@@ -285,7 +285,8 @@ typedef struct TwDecLayerW {
  * caches kc / vc ([rows][20][max_pos][64] per layer, layer l at + l * kv_layer_stride elements) hold positions
  * < pos[r]; the cross K/V of layer l at xkv + l * xkv_layer_stride (K) and + xkv_v_off (V), [rows][20][S][64].
  * Out: x = the last layer's output, the caches appended at pos, hp = the final LayerNorm as a packed activation
- * (proj_out's tw_gemv_packed operand). Scratch: qb, ab bf16 [R][1280], fb packed [32][5120], slab f32 [4][R][1280],
+ * (proj_out's tw_gemv_packed operand; also the launch's LayerNorm scratch). Scratch: qb, ab bf16 [R][1280], fb packed
+ * [32][5120], slab f32 [4][R][1280], xpart f32 tw_dec_fused_xpart_bytes(R),
  * sync: tw_dec_fused_sync_bytes() bytes, 16-byte aligned (zeroed by the call, on the stream). err: a sticky word the
  * caller zeroes once; a phase wait that times out sets it (0x100 + phase) and the launch's outputs are void. The
  * caller must not run other work on the device that waits for this launch's completion from inside a kernel. */
@@ -296,10 +297,19 @@ int tw_dec_fused_set_grid(int n);
 /* 1: an agent-scope acquire fence after every phase wait in addition to the sc1 (L1-bypassing) loads of every
  * handed-off byte; 0 (default): the loads alone. The same results either way (A/B switch). Returns 0. */
 int tw_dec_fused_set_acquire(int on);
+/* Measurement: buf (device, u64 [n_layers + 1][12][grid][2], zeroed by the caller) receives per (layer, phase,
+ * workgroup) the 100-MHz real-time clock at the start of the workgroup's first item of the phase (after its wait) and
+ * at the end of its last; slot (n_layers, 0) = each workgroup's start, (n_layers, 11) = the final LayerNorm. NULL (the
+ * default) turns it off. tw_dec_fused_grid: the grid of the last launch (0 before the first). */
+int tw_dec_fused_set_probe(void* buf);
+int tw_dec_fused_grid(void);
 int tw_dec_fused(const TwDecLayerW* layers, int n_layers, int R, const int* pos, float* x, uint16_t* kc,
                  uint16_t* vc, long kv_layer_stride, int max_pos, const uint16_t* xkv, long xkv_layer_stride,
-                 long xkv_v_off, int S, uint16_t* qb, uint16_t* ab, uint16_t* fb, float* slab, const float* lnf_g,
-                 const float* lnf_b, uint16_t* hp, float eps, unsigned* sync, unsigned* err, void* stream);
+                 long xkv_v_off, int S, uint16_t* qb, uint16_t* ab, uint16_t* fb, float* slab, float* xpart,
+                 const float* lnf_g, const float* lnf_b, uint16_t* hp, float eps, unsigned* sync, unsigned* err,
+                 void* stream);
+/* Bytes of tw_dec_fused's cross-attention slice scratch (xpart) for R rows. */
+size_t tw_dec_fused_xpart_bytes(int rows);
 /* tw_resid_layernorm with the normalised rows written as a packed activation (M <= 64, D % 32 == 0). */
 int tw_resid_layernorm_packed(float* x, const float* parts, int nparts, const float* bias, const float* gamma,
                               const float* beta, int M, int D, float eps, uint16_t* out, void* stream);

@@ -8,11 +8,11 @@ chain's):
   * one decoder step at R = 1 .. 32 rows from random caches (positions 0 .. 447, i.e. one and two key chunks of the
     self-attention) against a plain PyTorch fp32 restatement of the step from the same bf16 weights, caches and
     cross K/V (activations unrounded): the fused logits no further from it than REL_TO_CHAIN x the chain's distance +
-    ABS_SLACK, the K/V appended at pos within KV_ABS of the chain's (one bf16 ulp), every other cache position
-    untouched;
-  * bit-identical results from a second launch, from a 37-workgroup grid (items re-dealt over the workgroups) and
-    with an agent-scope acquire after every phase wait (tw_dec_fused_set_acquire): a stale read of a handed-off line
-    or a hand-off race would show as a difference here;
+    ABS_SLACK, the K/V appended at pos within KV_REL of the chain's (two bf16 ulps of the largest), every other cache
+    position untouched;
+  * bit-identical results from a second launch and with an agent-scope acquire after every phase wait
+    (tw_dec_fused_set_acquire): a stale read of a handed-off line or a hand-off race would show as a difference here;
+    a 37-workgroup grid (items re-dealt and re-sliced over fewer workgroups) within the chain tolerance;
   * a greedy pass over the bench workload (24 windows, 128 tokens, EOS suppressed) with the fused launch: windows
     0 and 23 against the fp32 goldens as the bench's parity leg checks them (exact or within tau), and the tokens of
     every window equal to the chain's up to near-ties;
@@ -35,7 +35,7 @@ pytestmark = pytest.mark.gpu
 LOGIT_ABS = 0.1     # fused vs chain logits, any step (random caches; the bench pass is judged against the goldens)
 REL_TO_CHAIN = 1.5  # fused distance to the fp32 step <= REL_TO_CHAIN x the chain's + ABS_SLACK
 ABS_SLACK = 0.01
-KV_ABS = 0.02
+KV_REL = 1.0 / 64  # appended K/V vs the chain's, relative to the largest appended value (two bf16 ulps)
 
 
 @pytest.fixture(scope="module")
@@ -129,17 +129,19 @@ def test_fused_step_matches_chain(turbo, R):
     xd = ((xf - xc).abs().max() / xc.abs().max()).item()
     ec, ef = (lc - ref).abs().max().item(), (lf - ref).abs().max().item()
     # the appended K/V at pos and nothing else
-    kd = vd = 0.0
+    kd = vd = kmax = vmax = 0.0
     for r in range(R):
         p = int(pos[r])
         kd = max(kd, (kf[:, r, :, p] - kc[:, r, :, p]).float().abs().max().item())
         vd = max(vd, (vf[:, r, :, p] - vc[:, r, :, p]).float().abs().max().item())
+        kmax = max(kmax, kc[:, r, :, p].float().abs().max().item())
+        vmax = max(vmax, vc[:, r, :, p].float().abs().max().item())
         kf[:, r, :, p] = kc[:, r, :, p]
         vf[:, r, :, p] = vc[:, r, :, p]
     print(f"R={R}: logits max|d| vs fp32 step: chain {ec:.2e}, fused {ef:.2e}; fused vs chain {d:.2e} (|logit| max "
           f"{scale:.1f}), residual rel {xd:.1e}, k {kd:.1e} v {vd:.1e}")
     assert ef <= REL_TO_CHAIN * ec + ABS_SLACK, (ef, ec)
-    assert d <= LOGIT_ABS and kd <= KV_ABS and vd <= KV_ABS
+    assert d <= LOGIT_ABS and kd <= KV_REL * kmax and vd <= KV_REL * vmax
     assert torch.equal(kf, kc) and torch.equal(vf, vc)  # no other cache position written
     # argmax agrees wherever the chain's top-2 margin is clear
     top2 = lc.topk(2, dim=1).values
@@ -149,9 +151,12 @@ def test_fused_step_matches_chain(turbo, R):
     lf2, kf2, vf2, xf2 = _step(eng, R, True)
     lg, kg, vg, xg = _step(eng, R, True, grid=37)
     la, ka, va, xa = _step(eng, R, True, acquire=1)
-    assert torch.equal(lf2, lf) and torch.equal(xf2, xf) and torch.equal(lg, lf) and torch.equal(xg, xf)
-    assert torch.equal(kg, kf2) and torch.equal(vg, vf2)
-    assert torch.equal(la, lf) and torch.equal(xa, xf) and torch.equal(ka, kf2) and torch.equal(va, vf2)
+    assert torch.equal(lf2, lf) and torch.equal(xf2, xf) and torch.equal(kf2, ka) and torch.equal(vf2, va)
+    assert torch.equal(la, lf) and torch.equal(xa, xf)
+    # (a 37-workgroup grid re-slices the attention items: the same sums in another order)
+    assert (lg - lf).abs().max().item() <= LOGIT_ABS and torch.isfinite(lg).all()
+    assert (kg.float() - ka.float()).abs().max().item() <= KV_REL * kmax
+    assert (vg.float() - va.float()).abs().max().item() <= KV_REL * vmax
     assert int(eng._fused_err[0].item()) == 0
 
 

@@ -50,7 +50,8 @@ EXPORTED = (
     "tw_attn_encoder_f32", "tw_attn_decode_self_f32", "tw_attn_decode_cross_f32", "tw_gemm_set_epilogue",
     "tw_gemm_set_persistent_grid", "tw_mp3_probe", "tw_mp3_decode", "tw_aac_parse_asc", "tw_aac_decode_raw",
     "tw_aac_adts_probe", "tw_aac_adts_decode", "tw_dec_fused", "tw_dec_fused_sync_bytes", "tw_dec_fused_supported",
-    "tw_dec_fused_set_grid", "tw_dec_fused_set_acquire",
+    "tw_dec_fused_set_grid", "tw_dec_fused_set_acquire", "tw_dec_fused_set_probe", "tw_dec_fused_grid",
+    "tw_dec_fused_xpart_bytes",
 )
 
 
@@ -196,12 +197,15 @@ _SIGS = {
     "tw_ima_adpcm_wav_decode": ([_P, ctypes.c_int64, _I, _I, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_resample_pcm_i32": ([_P, ctypes.c_int64, _I, _F, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),
     "tw_resample_pcm_f32": ([_P, ctypes.c_int64, _I, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),
-    "tw_dec_fused": ([_P, _I, _I, _P, _P, _P, _P, _L, _I, _P, _L, _L, _I, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P],
-                     _I),
+    "tw_dec_fused": ([_P, _I, _I, _P, _P, _P, _P, _L, _I, _P, _L, _L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P,
+                      _P], _I),
+    "tw_dec_fused_xpart_bytes": ([_I], ctypes.c_size_t),
     "tw_dec_fused_sync_bytes": ([], ctypes.c_size_t),
     "tw_dec_fused_supported": ([_I, _I, _I, _I], _I),
     "tw_dec_fused_set_grid": ([_I], _I),
     "tw_dec_fused_set_acquire": ([_I], _I),
+    "tw_dec_fused_set_probe": ([_P], _I),
+    "tw_dec_fused_grid": ([], _I),
 }
 
 _lib = None

@@ -308,6 +308,8 @@ class WhisperEngine:
         self._fused_dims = (not self.F32 and bool(_lib.load().tw_dec_fused_supported(D, H, d.ffn, 1)))
         self._fused_tab: Optional[torch.Tensor] = None  # device TwDecLayerW table (below, with the packed weights)
         self._fused_err = torch.zeros(4, dtype=torch.int32, device=dev)  # sticky phase-timeout word
+        self._fused_xpart = (torch.empty(int(_lib.load().tw_dec_fused_xpart_bytes(32)) // 4, dtype=torch.float32,
+                                         device=dev) if self._fused_dims else None)  # cross-attention slice states
         self._beam: Optional[dict] = None  # beam-search buffers, allocated on first use
         self._align: Optional[dict] = None  # token-level timestamps: alignment-head attention recording
         self._align_buf: Optional[torch.Tensor] = None
@@ -1004,7 +1006,8 @@ class WhisperEngine:
         _lib.call("tw_dec_fused", self._fused_tab.data_ptr(), d.decoder_layers, R, v.pos.data_ptr(), v.xd.data_ptr(),
                   self.kcache[0, v.r0].data_ptr(), self.vcache[0, v.r0].data_ptr(), self.kcache.stride(0), T, xkv,
                   2 * r_enc * H * S_ENC * 64, r_enc * H * S_ENC * 64, S_ENC, v.qd.data_ptr(), v.attd.data_ptr(),
-                  v.fp.data_ptr(), v.parts.data_ptr(), w.dec_ln_g.data_ptr(), w.dec_ln_b.data_ptr(), v.hp.data_ptr(),
+                  v.fp.data_ptr(), v.parts.data_ptr(), self._fused_xpart.data_ptr(), w.dec_ln_g.data_ptr(),
+                  w.dec_ln_b.data_ptr(), v.hp.data_ptr(),
                   LN_EPS, v.fsync.data_ptr(), self._fused_err.data_ptr(), v.stream.cuda_stream)
 
     def _fused_table(self) -> torch.Tensor:
