@@ -522,54 +522,80 @@ __global__ __launch_bounds__(NTHR, 1) void k_dec_fused(FusedArgs a) {
       wg_signal(a, K_QX);
       probe(a, l, K_QX, 1);
     }
-    // ---- CROSS: (row, head) over the encoder keys in XS key slices; a slice's unnormalised state goes to xpart and
-    //      the (row, head)'s last arrival (ticket) merges the XS states in slice order -> ab
+    // ---- CROSS: (row, head) over the encoder keys in XS key slices; a slice's unnormalised state goes to xpart. After
+    //      its last slice a workgroup drains once and takes one arrival ticket per slice (a lane each); the (row,
+    //      head)s its tickets complete it merges (XS states in slice order -> ab), eight at a time (32 lanes each)
     {
       const bf16_t* xk = a.xkv + (size_t)l * a.xkv_layer_stride;
-      for (int it = first_item(0, G); it < n_cross; it += G) {
-        if (it == first_item(0, G)) ok = wg_wait(a, K_QX, lp1 * G_D, flag) && ok;
-        if (it == first_item(0, G)) probe(a, l, K_CROSS, 0);
+      const int i0 = first_item(0, G);
+      for (int it = i0; it < n_cross; it += G) {
+        if (it == i0) ok = wg_wait(a, K_QX, lp1 * G_D, flag) && ok;
+        if (it == i0) probe(a, l, K_CROSS, 0);
         const int rh = it / XS, z = it - rh * XS, r = rh / FH, h = rh - r * FH;
         const int k0 = (int)((long)z * a.S / XS), k1 = (int)((long)(z + 1) * a.S / XS);
         const size_t off = ((size_t)r * FH + h) * a.S * 64, qo = (size_t)r * FD + h * 64;
-        bf16_t* o = a.ab + qo;
         if (XS == 1) {
-          attend<true, NWAVE, XUNR>(a.qb, qo, xk, xk + a.xkv_v_off, off, k0, k1, o, nullptr, wpart, wml);
+          attend<true, NWAVE, XUNR>(a.qb, qo, xk, xk + a.xkv_v_off, off, k0, k1, a.ab + qo, nullptr, wpart, wml);
           wg_signal(a, K_CROSS);
         } else {
-          float* st = a.xpart + ((size_t)rh * XS + z) * 66;
-          attend<true, NWAVE, XUNR>(a.qb, qo, xk, xk + a.xkv_v_off, off, k0, k1, nullptr, st, wpart, wml);
+          attend<true, NWAVE, XUNR>(a.qb, qo, xk, xk + a.xkv_v_off, off, k0, k1, nullptr,
+                                    a.xpart + ((size_t)rh * XS + z) * 66, wpart, wml);
+        }
+      }
+      if (XS > 1 && i0 < n_cross) {
+        const int nmine = (n_cross - i0 + G - 1) / G;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int done = 0;
+        for (int c0 = 0; c0 < nmine; c0 += 64) {  // this workgroup's slices, 64 tickets at a time
+          if (tid < 64) {
+            bool last = false;
+            if (c0 + tid < nmine) {
+              const int rh = (i0 + (c0 + tid) * G) / XS;
+              const unsigned old = __hip_atomic_fetch_add(a.sync + XTICKET_OFF + rh * TSTRIDE, 1u, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+              last = old % (unsigned)XS == (unsigned)XS - 1u;
+            }
+            const unsigned long long mk = __ballot(last);
+            if (tid == 0) {
+              flag[2] = (int)(unsigned)mk;
+              flag[3] = (int)(unsigned)(mk >> 32);
+              if (mk != 0ull && a.acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+          }
+          __syncthreads();
+          unsigned long long mk = (unsigned long long)(unsigned)flag[2] | ((unsigned long long)(unsigned)flag[3] << 32);
+          done += __popcll(mk);
+          for (int k = 0; mk != 0ull; ++k, mk &= mk - 1ull) {  // the completed (row, head)s, eight at a time
+            if ((k & 7) != (tid >> 5)) continue;
+            const int rh = (i0 + (c0 + __ffsll((long long)mk) - 1) * G) / XS, r = rh / FH, h = rh - r * FH;
+            const int lt = tid & 31;
+            const float* s0 = a.xpart + (size_t)rh * XS * 66;
+            float M = -INFINITY;
+            for (int zz = 0; zz < XS; ++zz) M = fmaxf(M, hld2(s0, (size_t)zz * 66 * 4)[0]);
+            float v0 = 0.f, v1 = 0.f, tot = 0.f;
+            for (int zz = 0; zz < XS; ++zz) {
+              const f32x2 ml = hld2(s0, (size_t)zz * 66 * 4);
+              const f32x2 vv = hld2(s0, ((size_t)zz * 66 + 2 + 2 * lt) * 4);
+              const float wt = ml[0] == -INFINITY ? 0.f : __expf(ml[0] - M);
+              tot += wt * ml[1];
+              v0 += wt * vv[0];
+              v1 += wt * vv[1];
+            }
+            st_sc1(a.ab + (size_t)r * FD + h * 64 + 2 * lt, pack_bf16x2(v0 / tot, v1 / tot));
+          }
+          __syncthreads();  // (flag words reused by the next chunk)
+        }
+        if (done > 0) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __syncthreads();
-          if (tid == 0) {
-            const unsigned old = __hip_atomic_fetch_add(a.sync + XTICKET_OFF + rh * TSTRIDE, 1u, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-            flag[1] = old % (unsigned)XS == (unsigned)XS - 1u;
-            if (flag[1] && a.acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-          __syncthreads();
-          if (flag[1]) {
-            if (tid < 32) {
-              const float* s0 = a.xpart + (size_t)rh * XS * 66;
-              float M = -INFINITY;
-              for (int zz = 0; zz < XS; ++zz) M = fmaxf(M, hld2(s0, (size_t)zz * 66 * 4)[0]);
-              float v0 = 0.f, v1 = 0.f, tot = 0.f;
-              for (int zz = 0; zz < XS; ++zz) {
-                const f32x2 ml = hld2(s0, (size_t)zz * 66 * 4);
-                const f32x2 vv = hld2(s0, ((size_t)zz * 66 + 2 + 2 * tid) * 4);
-                const float wt = ml[0] == -INFINITY ? 0.f : __expf(ml[0] - M);
-                tot += wt * ml[1];
-                v0 += wt * vv[0];
-                v1 += wt * vv[1];
-              }
-              st_sc1(o + 2 * tid, pack_bf16x2(v0 / tot, v1 / tot));
-            }
-            wg_signal(a, K_CROSS);
-          }
+          if (tid == 0)
+            __hip_atomic_fetch_add(ctr(a.sync, K_CROSS, blockIdx.x & 7), (unsigned)done, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
-        probe(a, l, K_CROSS, 1);
       }
+      if (i0 < n_cross) probe(a, l, K_CROSS, 1);
     }
     // ---- OX: x += ab . Wo_x + bo_x
     for (int it = first_item(0, G); it < G_D; it += G) {
