@@ -62,6 +62,26 @@ def main():
             per.append((t, ev0.elapsed_time(ev1) * 1e3))
     finally:
         _lib.call("tw_dec_fused_set_probe", None)
+    # the step's launches timed apart with HIP events on the engine stream: embedding, tw_dec_fused (memset node +
+    # kernel), proj_out
+    v = eng._view(0, R)
+    d = eng.d
+    parts = {"embed": [], "fused": [], "proj_out": []}
+    for _ in range(a.steps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        with torch.cuda.stream(eng.stream):
+            ev[0].record(eng.stream)
+            _lib.call("tw_embed_decoder", eng.w.emb.data_ptr(), eng.w.pos_dec.data_ptr(), v.ids.data_ptr(),
+                      v.pos.data_ptr(), R, d.d_model, v.xd.data_ptr(), eng.stream.cuda_stream)
+            ev[1].record(eng.stream)
+            eng._fused_layers(R, R, v)
+            ev[2].record(eng.stream)
+            eng._gemv(v.hp, True, eng.emb_p, R, d.vocab, d.d_model, _lib.TW_EPI_F32, v.logits, v)
+            ev[3].record(eng.stream)
+        torch.cuda.synchronize()
+        for k, (i, j) in zip(parts, ((0, 1), (1, 2), (2, 3))):
+            parts[k].append(ev[i].elapsed_time(ev[j]) * 1e3)
+    print(json.dumps({"launch_us_median": {k: round(float(np.median(x)), 1) for k, x in parts.items()}}), flush=True)
     eng.check_fused()
     # the median step by kernel span
     spans = []
