@@ -694,7 +694,28 @@ __global__ __launch_bounds__(NTHR, 1) void k_dec_fused(FusedArgs a) {
   (void)ok;
 }
 
-int g_fused_grid = 0;  // workgroups per launch: the device's CU count (one resident workgroup per CU)
+int g_fused_grid = 0;  // workgroups per launch (0: the resident maximum, g_fused_max)
+int g_fused_max = 0;   // the CU count x the workgroups the occupancy query admits per CU (at most 2)
+
+// Queries g_fused_max once. Every workgroup of a launch must be resident at the same time (static item assignment:
+// a workgroup never started would leave its items undone until the waits time out), so no grid may exceed it.
+int fused_max_grid() {
+  if (g_fused_max > 0) return TW_OK;
+  int dev = 0, cus = 0, occ1 = 0, occ2 = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+    tw_set_error("tw_dec_fused: cannot query the CU count");
+    return TW_ERR_LAUNCH;
+  }
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_dec_fused<1>, NTHR, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, k_dec_fused<2>, NTHR, 0) != hipSuccess ||
+      min(occ1, occ2) < 1) {
+    tw_set_error("tw_dec_fused: occupancy query failed (%d, %d)", occ1, occ2);
+    return TW_ERR_LAUNCH;
+  }
+  g_fused_max = cus * min(2, min(occ1, occ2));
+  return TW_OK;
+}
 int g_fused_acq = 0;   // FusedArgs::acq
 unsigned long long* g_fused_probe = nullptr;
 
@@ -707,7 +728,8 @@ extern "C" int tw_dec_fused_supported(int d_model, int heads, int ffn, int rows)
 }
 
 extern "C" int tw_dec_fused_set_grid(int n) {
-  TW_REQUIRE(n >= 0 && n <= 4096, "tw_dec_fused_set_grid: %d", n);
+  if (int rc = fused_max_grid()) return rc;
+  TW_REQUIRE(n >= 0 && n <= g_fused_max, "tw_dec_fused_set_grid: %d workgroups (0 .. %d resident)", n, g_fused_max);
   g_fused_grid = n;
   return TW_OK;
 }
@@ -757,24 +779,9 @@ extern "C" int tw_dec_fused(const TwDecLayerW* layers, int n_layers, int R, cons
              "tw_dec_fused: bad cache geometry");
   TW_REQUIRE(((uintptr_t)sync & 15) == 0, "tw_dec_fused: sync words not 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
-  if (g_fused_grid == 0) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
-      tw_set_error("tw_dec_fused: cannot query the CU count");
-      return TW_ERR_LAUNCH;
-    }
-    // every workgroup resident at once: the CU count times what the occupancy query admits per CU (at most 2)
-    int occ1 = 0, occ2 = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, k_dec_fused<1>, NTHR, 0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, k_dec_fused<2>, NTHR, 0) != hipSuccess ||
-        min(occ1, occ2) < 1) {
-      tw_set_error("tw_dec_fused: occupancy query failed (%d, %d)", occ1, occ2);
-      return TW_ERR_LAUNCH;
-    }
-    g_fused_grid = cus * min(2, min(occ1, occ2));
-  }
-  if (hipMemsetAsync(sync, 0, (size_t)SYNC_WORDS * 4, s) != hipSuccess) {
+  if (int rc = fused_max_grid()) return rc;
+  if (g_fused_grid == 0) g_fused_grid = g_fused_max;
+  if (hipMemsetAsync(sync, 0, (size_t)SYNC_WORDS * 4, s) != hipSuccess) {  // (a memset node when captured)
     tw_set_error("tw_dec_fused: memset of the sync words failed");
     return TW_ERR_LAUNCH;
   }
