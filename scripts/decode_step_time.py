@@ -5,8 +5,9 @@ before, untimed. Prints one JSON line per (rows, mode).
 
     python scripts/decode_step_time.py [--rows 15 24 64] [--reps 3] [--fused 0 1]
 
---fused 1: the decoder's layers as one persistent launch (WhisperEngine.dec_fused_alone, tw_dec_fused; rows <= 32),
-0: the launch chain; with both, each row count runs both and reports whether their tokens agree.
+--fused 1: the decoder's layers as one persistent launch (tw_dec_fused) at every row count <= 32, 0: the launch chain
+(WhisperEngine.dec_fused_alone / dec_fused_max_rows overridden); with both, each row count runs both and reports
+whether their tokens agree.
 """
 import argparse
 import json
@@ -52,6 +53,7 @@ def main():
             if fz and R > 32:
                 continue
             eng.dec_fused_alone = bool(fz)
+            eng.dec_fused_max_rows = 32 if fz else 0
             eng.graph_steps_alone = gs
             eng._graphs.clear()
             eng.decode_pass(R, tail, None, 128, check_every=ce)  # warm-up: graph captures

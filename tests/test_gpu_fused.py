@@ -42,7 +42,8 @@ KV_REL = 1.0 / 64  # appended K/V vs the chain's, relative to the largest append
 def turbo():
     tr = TurboTranscriber.from_pretrained("large-v3-turbo", seed=1234, max_batch=32, max_beams=1)
     yield tr
-    tr.engine.dec_fused_alone = False
+    tr.engine.dec_fused_alone = type(tr.engine).dec_fused_alone
+    tr.engine.dec_fused_max_rows = type(tr.engine).dec_fused_max_rows
     tr.engine._dec_context()
     del tr
     torch.cuda.empty_cache()
@@ -65,6 +66,7 @@ def _random_state(eng, R, seed):
 
 def _step(eng, R, fused, grid=0, acquire=0):
     eng.dec_fused_alone = fused
+    eng.dec_fused_max_rows = 32
     eng._dec_context()
     _lib.call("tw_dec_fused_set_grid", grid)
     _lib.call("tw_dec_fused_set_acquire", acquire)
@@ -188,6 +190,7 @@ def test_fused_bench_pass_vs_goldens(turbo):
     eng.set_suppress_tokens(list(gen.suppress_tokens) + [gen.special.eot])
     try:
         out = {}
+        eng.dec_fused_max_rows = 32
         for fused in (False, True):
             eng.dec_fused_alone = fused
             eng.wave[:B].copy_(torch.from_numpy(audio))
@@ -208,4 +211,5 @@ def test_fused_bench_pass_vs_goldens(turbo):
         eng.check_fused()
     finally:
         eng.set_suppress_tokens(list(gen.suppress_tokens))
-        eng.dec_fused_alone = False
+        eng.dec_fused_alone = type(eng).dec_fused_alone
+        eng.dec_fused_max_rows = type(eng).dec_fused_max_rows

@@ -970,9 +970,17 @@ class WhisperEngine:
     dec_beside_gemv = 0
 
     # The decoder's layers for a decode pass alone as ONE persistent launch (tw_dec_fused, csrc/decfused.hip) instead
-    # of the 45-launch chain; rows <= 32, greedy / sampled passes without beams, prompt masks or alignment heads.
-    # Beside an encoder chunk the chain stays (a persistent grid would hold every CU the encoder GEMM needs).
+    # of the 45-launch chain, for passes of at most dec_fused_max_rows rows (greedy / sampled, without beams, prompt
+    # masks or alignment heads). Measured per step alone (scripts/decode_step_time.py --fused 0 1,
+    # profiles/r06o_fused_small_rows.txt): 1 row 238 vs 276 us, 2: 243 vs 280, 4: 259 vs 283, 8: 303 vs 293,
+    # 15: 362 vs 324, 24: 407 vs 385 — the single-upload calls of the reference's API (a few windows) gain, the
+    # engine batches do not. Opt-in (False by default): its rows round differently from the chain's, so
+    # with it a call's transcript depends on how many windows share its decode pass, and a window-sharded call
+    # (twamd.dist: ranks of <= 4 windows) would no longer equal the single-process call bit for bit
+    # (tests/test_gpu_c3_c4.py). Beside an encoder chunk the chain stays (a persistent grid would hold every CU the
+    # encoder GEMM needs).
     dec_fused_alone = False
+    dec_fused_max_rows = 4
 
     @property
     def _wide_kw(self) -> int:
@@ -993,8 +1001,8 @@ class WhisperEngine:
 
     def _fused_ok(self, R: int) -> bool:
         """The current step runs as tw_dec_fused (see dec_fused_alone)."""
-        return (self._dec_ctx[2] and R <= 32 and self._kv_tab is None and not self._masked and self._align is None
-                and not self._use_dec_row_map)
+        return (self._dec_ctx[2] and R <= min(32, self.dec_fused_max_rows) and self._kv_tab is None
+                and not self._masked and self._align is None and not self._use_dec_row_map)
 
     def _fused_layers(self, R: int, r_enc: int, v: DecView) -> None:
         """tw_dec_fused for the view's rows: xd (the embedded token) -> the last layer's output, the self K/V caches
