@@ -8,7 +8,9 @@
 // 4-6 us for ~5 us of work; here one workgroup per CU walks the step's phases and hands each phase's
 // output to the next through write-through stores and per-XCD-sharded completion counters
 // (cdna_hip_programming.md §6 Guideline 16, recipe R1: sc1 payload stores, every storing wave drained, one counter
-// add behind a workgroup barrier; consumer: one relaxed poll, one agent-scope acquire, plain loads). A workgroup
+// add behind a workgroup barrier; consumer: one relaxed poll of the counter's eight shards, then sc1 loads of every
+// handed-off byte — the table row under which the agent-scope acquire may go; tw_dec_fused_set_acquire(1) keeps it
+// for an A/B, with bit-identical results). A workgroup
 // issues the weight loads of its next GEMV item BEFORE it waits for that phase's inputs, so the weight stream of a
 // phase overlaps the previous phase's tail and the hand-off itself.
 //
