@@ -216,5 +216,6 @@ def test_undecodable_upload_reaches_reference_error_convention(layout, tmp_path)
     got = p.transcribe(str(f), "transcribe")
     assert got == {"error": "Transcription error: MPEG audio Layer II audio is not decoded by this engine (decoded "
                             "containers: FLAC, Ogg Vorbis, MP3 (MPEG-1 / 2 / 2.5 Layer III), AAC-LC (M4A / MP4, ADTS), "
-                            "WAV (PCM, float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C); convert the upload to one of "
+                            "WAV / RIFX / RF64 (PCM, float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C); convert the "
+                            "upload to one of "
                             "them"}

@@ -430,8 +430,12 @@ def ima_adpcm_wav_decode(data: bytes, channels: int, block_align: int) -> np.nda
 
 
 def _pcm_to_float(raw: bytes, bits: int, big_endian: bool = False, unsigned8: bool = True) -> np.ndarray:
-    """Integer PCM -> float32 in [-1, 1) the way ffmpeg's s8/s16/s24/s32 -> flt conversion scales (2^-(bits-1))."""
+    """Integer PCM -> float32 in [-1, 1) the way ffmpeg's s8/s16/s24/s32/s64 -> flt conversion scales
+    (2^-(bits-1))."""
     e = ">" if big_endian else "<"
+    if bits == 64:
+        return (np.frombuffer(raw[: len(raw) // 8 * 8], e + "i8").astype(np.float64) / 9223372036854775808.0
+                ).astype(np.float32)
     if bits == 8:
         v = np.frombuffer(raw, np.uint8 if unsigned8 else np.int8).astype(np.float32)
         return (v - 128.0) / 128.0 if unsigned8 else v / 128.0
@@ -455,18 +459,33 @@ def _frames(x: np.ndarray, ch: int) -> np.ndarray:
 
 
 def decode_wav(data: bytes) -> Tuple[np.ndarray, int]:
-    """RIFF/WAVE bytes -> (float32 [frames, channels] in [-1, 1], sample_rate). Format tags: 1 PCM 8/16/24/32,
-    3 IEEE float 32/64, 6 A-law, 7 mu-law, 0x11 IMA ADPCM, and WAVE_FORMAT_EXTENSIBLE carrying any of them."""
-    if len(data) < 12 or data[:4] != b"RIFF" or data[8:12] != b"WAVE":
+    """RIFF/WAVE bytes -> (float32 [frames, channels] in [-1, 1], sample_rate), as ffmpeg's wav demuxer reads them
+    (libavformat/wavdec.c): "RIFF" little-endian, "RIFX" big-endian, "RF64" with its ds64 chunk's 64-bit data size.
+    Format tags: 1 PCM in 1 / 2 / 3 / 4 / 8-byte containers (bits per sample rounded up to whole bytes, as
+    ff_get_pcm_codec_id maps them: a 20-bit stream is s24, a 12-bit one s16, a 5-bit one u8; 5-7-byte containers are
+    refused, as ffmpeg refuses them), 3 IEEE float 32 / 64, 6 A-law, 7 mu-law, 0x11 IMA ADPCM, and
+    WAVE_FORMAT_EXTENSIBLE carrying any of them. A data chunk that runs past the end of the bytes is read up to it."""
+    if len(data) < 12 or data[:4] not in (b"RIFF", b"RIFX", b"RF64") or data[8:12] != b"WAVE":
         raise ValueError("not a RIFF/WAVE stream")
-    pos, fmt, pcm = 12, None, None
+    be = data[:4] == b"RIFX"
+    e = ">" if be else "<"
+    u16, u32 = e + "H", e + "I"
+    pos, fmt, pcm, ds64_data = 12, None, None, None
     while pos + 8 <= len(data):
-        cid, size = data[pos: pos + 4], struct.unpack("<I", data[pos + 4: pos + 8])[0]
+        cid, size = data[pos: pos + 4], struct.unpack(u32, data[pos + 4: pos + 8])[0]
+        if cid == b"ds64" and size >= 16:  # RF64: riff size, data size (64-bit each), sample count
+            ds64_data = struct.unpack("<Q", data[pos + 16: pos + 24])[0]
+        if cid == b"data" and size == 0xFFFFFFFF and ds64_data is not None:
+            size = ds64_data
         body = data[pos + 8: pos + 8 + size]
         if cid == b"fmt ":
-            tag, ch, sr, _, align, bits = struct.unpack("<HHIIHH", body[:16])
-            if tag == 0xFFFE and len(body) >= 26:  # WAVE_FORMAT_EXTENSIBLE: subformat GUID's first 2 bytes
-                tag = struct.unpack("<H", body[24:26])[0]
+            if len(body) < 16:
+                raise ValueError("WAVE fmt chunk too short")
+            tag, ch = struct.unpack(e + "HH", body[:4])
+            sr = struct.unpack(u32, body[4:8])[0]
+            align, bits = struct.unpack(e + "HH", body[12:16])
+            if tag == 0xFFFE and len(body) >= 28:  # WAVE_FORMAT_EXTENSIBLE: the subformat GUID's Data1 (its low 16
+                tag = struct.unpack(u32, body[24:28])[0] & 0xFFFF  # bits are the format tag), in the file's byte order
             fmt = (tag, ch, sr, bits, align)
         elif cid == b"data":
             pcm = body
@@ -477,9 +496,15 @@ def decode_wav(data: bytes) -> Tuple[np.ndarray, int]:
     if ch < 1:
         raise ValueError("WAVE stream with no channels")
     if tag == 1:
-        x = _pcm_to_float(pcm, bits)
+        width = (bits + 7) // 8
+        if bits < 1 or width not in (1, 2, 3, 4, 8):
+            raise ValueError(f"unsupported PCM width {bits}")
+        x = _pcm_to_float(pcm, 8 * width, big_endian=be)
     elif tag == 3:
-        x = np.frombuffer(pcm[: len(pcm) // (bits // 8) * (bits // 8)], "<f4" if bits == 32 else "<f8").astype(np.float32)
+        if bits not in (32, 64):
+            raise ValueError(f"unsupported IEEE float width {bits}")
+        w = bits // 8
+        x = np.frombuffer(pcm[: len(pcm) // w * w], e + ("f4" if w == 4 else "f8")).astype(np.float32)
     elif tag in (6, 7):
         x = g711_decode(pcm, alaw=tag == 6).astype(np.float32) / 32768.0
     elif tag == 0x11:
@@ -613,7 +638,7 @@ MALFORMED = ("Soundfile is either not in the correct format or is malformed. Ens
 
 
 def container_name(data: bytes) -> Optional[str]:
-    if data[:4] == b"RIFF":
+    if data[:4] in (b"RIFF", b"RIFX", b"RF64") and data[8:12] == b"WAVE":
         return "WAV"
     if data[:4] == b"fLaC":
         return "FLAC"
@@ -636,8 +661,8 @@ def container_name(data: bytes) -> Optional[str]:
 
 _DECODERS = {"WAV": decode_wav, "AU": decode_au, "AIFF": decode_aiff, "Ogg Vorbis": decode_vorbis, "MP3": decode_mp3,
              "AAC (ADTS)": decode_aac_adts, "MP4/M4A": decode_mp4}
-DECODED = "FLAC, Ogg Vorbis, MP3 (MPEG-1 / 2 / 2.5 Layer III), AAC-LC (M4A / MP4, ADTS), WAV (PCM, float, A-law, " \
-          "mu-law, IMA ADPCM), AU, AIFF / AIFF-C"
+DECODED = "FLAC, Ogg Vorbis, MP3 (MPEG-1 / 2 / 2.5 Layer III), AAC-LC (M4A / MP4, ADTS), WAV / RIFX / RF64 (PCM, " \
+          "float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C"
 
 
 def decode_bytes(data: bytes, sr_out: int = TARGET_SR, device=None) -> np.ndarray:
