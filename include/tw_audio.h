@@ -13,7 +13,7 @@
  *   tw_ima_adpcm_wav_decode          IMA ADPCM in WAV blocks
  *   tw_vorbis_probe / tw_vorbis_decode  Ogg Vorbis I (floor 1, residues 0/1/2, coupling, IMDCT, overlap-add)
  *   tw_mp3_probe / tw_mp3_decode     MPEG-1 / MPEG-2 LSF / MPEG-2.5 Layer III (MP3), gapless-trimmed by the
- *                                    LAME tag as ffmpeg's mp3 demuxer trims it
+ *                                    LAME tag as ffmpeg's mp3 demuxer trims it, and Layers I / II
  *   tw_aac_*                         MPEG-4 AAC-LC: ADTS streams, and the raw access units of an MP4 / M4A track
  *                                    (the container is demuxed by the caller, twamd/audio.py)
  *   tw_resample_pcm_i32 / _f32       downmix + polyphase resample on the GPU (DEVICE memory, `stream`), the
@@ -106,16 +106,18 @@ typedef struct TwMp3Info {
   int64_t total_samples;     /* per channel, after the gapless trim (all decoded samples without a LAME tag)  */
   int64_t n_frames;          /* audio frames (a Xing / Info / VBRI header frame is not counted)               */
   int64_t skip_samples;      /* decoded samples dropped at the start (LAME delay + 529; 0 without the tag)    */
-  int32_t samples_per_frame; /* 1152 (MPEG-1) or 576                                                          */
+  int32_t samples_per_frame; /* 1152 (Layer II, MPEG-1 Layer III), 576 (LSF Layer III) or 384 (Layer I)       */
   int32_t enc_delay;         /* LAME / Lavc tag encoder delay and padding (-1: no such tag)                   */
   int32_t enc_padding;
   int32_t flags;             /* 1: Xing / Info frame, 2: LAME gapless fields, 4: VBRI frame                  */
+  int32_t layer;             /* 1, 2 or 3 (a stream does not change layer)                                    */
 } TwMp3Info;
 
-/* MP3 (HOST memory): skip ID3v2 tags, find the first Layer III frame the next header confirms, walk the frames
- * (resynchronising over junk, stopping at ID3v1 / APEv2 / trailing ID3 tags) and read the Xing / Info + LAME or VBRI
- * header frame. Layer I / II and free-format streams are refused. Reference: the codec half of ffmpeg_read
- * ($TF/pipelines/audio_utils.py:9-45) for the .mp3 uploads vocalis/api/main.py:67-75 stores. */
+/* MP3 / MPEG audio (HOST memory): skip ID3v2 tags, find the first frame (Layer I, II or III) the next header
+ * confirms, walk the frames of that layer (resynchronising over junk, stopping at ID3v1 / APEv2 / trailing ID3 tags)
+ * and, for Layer III, read the Xing / Info + LAME or VBRI header frame. Free-format streams are refused.
+ * Reference: the codec half of ffmpeg_read ($TF/pipelines/audio_utils.py:9-45) for the .mp3 uploads
+ * vocalis/api/main.py:67-75 stores. */
 int tw_mp3_probe(const uint8_t* data, int64_t size, TwMp3Info* info);
 
 /* Decode into out = f32[out_frames][channels] (interleaved, HOST, nominal full scale +-1). out_frames must be >=

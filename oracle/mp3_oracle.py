@@ -1,4 +1,5 @@
-"""CPU oracle for MP3 (MPEG-1 / MPEG-2 LSF / MPEG-2.5 Layer III) ingest — TEST INFRASTRUCTURE ONLY.
+"""CPU oracle for MP3 (MPEG-1 / MPEG-2 LSF / MPEG-2.5 Layer III, and Layers I / II) ingest —
+TEST INFRASTRUCTURE ONLY.
 
 Only tests/ may import this module; the product (turbo-whisper-workspace_amd/twamd, csrc/mp3.cpp) never does.
 
@@ -18,6 +19,10 @@ prefix codes, band sums, a smooth window) and by the image's one real MP3, not b
   every Huffman table with linbits escapes, count1 tables A and B, MPEG-1 scfsi sharing and every LSF scalefactor
   partition (incl. the intensity right channel's), random scalefactors and gains; optionally an ID3v2 tag and a
   Xing / Info + LAME gapless header frame.
+* Layers I / II (11172-3 2.4.3.2-3; 13818-3's LSF Layer II table): `decode_frame_l12` reads allocation, scfsi,
+  scalefactors and (grouped) sample codes into subband samples with the standard's C (s'' + D) dequantiser;
+  `write_stream_l12(rng, layer, ...)` is the matching random-syntax writer. Their tables are restated here in the
+  standard's per-subband-range form and compared with the product's arrays (`l12_table_checks`).
 
 Pinning: the only real MP3 in this image is MathJax's a11y/invalid_keypress.mp3 (Lavf56 / libmp3lame, MPEG-1 128 kb/s
 44.1 kHz joint stereo, 21 audio frames + an Info frame whose LAME tag holds delay 576, padding 0). Against ffmpeg's own
@@ -102,6 +107,83 @@ def table_checks() -> Dict[str, object]:
     return res
 
 
+# ---- Layers I / II, restated in the standard's own form (a second transcription; the product's compact arrays in
+# mp3_tables.h are checked against these by l12_table_checks()) --------------------------------------------------------
+# bitrate (kbit/s) by bitrate_index, 11172-3 2.4.2.3 / 13818-3 2.4.2.3, keyed (layer, lsf)
+L12_BITRATE = {(1, 0): [0, 32, 64, 96, 128, 160, 192, 224, 256, 288, 320, 352, 384, 416, 448],
+               (2, 0): [0, 32, 48, 56, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384],
+               (1, 1): [0, 32, 48, 56, 64, 80, 96, 112, 128, 144, 160, 176, 192, 224, 256],
+               (2, 1): [0, 8, 16, 24, 32, 40, 48, 56, 64, 80, 96, 112, 128, 144, 160]}
+_FULL = [3, 7, 15, 31, 63, 127, 255, 511, 1023, 2047, 4095, 8191, 16383, 32767, 65535]
+_MID = [3, 5, 7, 9, 15, 31, 63, 127, 255, 511, 1023, 2047, 4095, 8191, 65535]
+_LOWR = [3, 5, 9, 15, 31, 63, 127, 255, 511, 1023, 2047, 4095, 8191, 16383, 32767]
+# Annex B Table B.2a-d and 13818-3 Table B.1: (first subband, last subband, steps of allocation codes 1..2^nbal - 1)
+L2_ALLOC = {
+    "a": [(0, 2, _FULL), (3, 10, _MID), (11, 22, [3, 5, 7, 9, 15, 31, 65535]), (23, 26, [3, 5, 65535])],
+    "b": [(0, 2, _FULL), (3, 10, _MID), (11, 22, [3, 5, 7, 9, 15, 31, 65535]), (23, 29, [3, 5, 65535])],
+    "c": [(0, 1, _LOWR), (2, 7, [3, 5, 9, 15, 31, 63, 127])],
+    "d": [(0, 1, _LOWR), (2, 11, [3, 5, 9, 15, 31, 63, 127])],
+    "lsf": [(0, 3, _LOWR), (4, 10, [3, 5, 9, 15, 31, 63, 127]), (11, 29, [3, 5, 9])],
+}
+
+
+def l2_codeword(steps: int) -> Tuple[int, bool]:
+    """(bits per codeword, grouped) of a Layer II quantisation class (Table B.4): 3, 5 and 9 steps code three samples
+    in one word of ceil(log2(steps^3)) bits, the others one sample in log2(steps + 1) bits."""
+    if steps in (3, 5, 9):
+        return int(math.ceil(math.log2(steps ** 3))), True
+    return int(round(math.log2(steps + 1))), False
+
+
+def l2_table_name(h) -> str:
+    """Table B.2's choice by sampling rate and bitrate per channel (LSF: Table B.1)."""
+    if h["lsf"]:
+        return "lsf"
+    chb = h["bitrate"] // h["channels"]
+    fs = h["sample_rate"]
+    if chb >= 96:  # 96..192 kbit/s per channel: a at 48 kHz, b at 44.1 / 32 kHz
+        return "a" if fs == 48000 else "b"
+    if chb >= 56:  # 56..80
+        return "a"
+    return "c" if fs != 32000 else "d"  # 32..48
+
+
+def l2_alloc(name: str):
+    """[(nbal, [steps of codes 1..]) per subband] of an allocation table."""
+    out = []
+    for a, b, steps in L2_ALLOC[name]:
+        nbal = int(math.log2(len(steps) + 1))
+        out += [(nbal, steps)] * (b - a + 1)
+    return out
+
+
+def l12_table_checks() -> Dict[str, bool]:
+    """The product's compact Layer I / II arrays against this module's transcription, plus structure."""
+    res = {}
+    res["bitrates"] = (TAB["kBitrateL12"][0].tolist() == L12_BITRATE[(1, 0)] and
+                       TAB["kBitrateL12"][1].tolist() == L12_BITRATE[(2, 0)] and
+                       TAB["kBitrateL12"][2].tolist() == L12_BITRATE[(1, 1)] and
+                       TAB["kBitrate"][1].tolist() == L12_BITRATE[(2, 1)])
+    steps, bits, grp = TAB["kL2Steps"], TAB["kL2Bits"], TAB["kL2Grouped"]
+    res["classes"] = all((int(b), bool(g)) == l2_codeword(int(st)) for st, b, g in zip(steps, bits, grp))
+    res["grouped_fit"] = all(int(st) ** 3 <= 2 ** int(b) for st, b, g in zip(steps, bits, grp) if g)
+    ok = True
+    for t, name in enumerate(("a", "b", "c", "d", "lsf")):
+        want = l2_alloc(name)
+        ok &= int(TAB["kL2Sblimit"][t]) == len(want)
+        for sb in range(30):
+            row = int(TAB["kL2SbRow"][t][sb])
+            if sb >= len(want):
+                ok &= row == -1
+                continue
+            nbal, st = want[sb]
+            got = [int(steps[c]) for c in TAB["kL2Row"][row] if c >= 0]
+            ok &= int(TAB["kL2RowBits"][row]) == nbal and got == st and len(got) == 2 ** nbal - 1
+            ok &= got == sorted(got)
+    res["alloc_tables"] = bool(ok)
+    return res
+
+
 # ---- frame header --------------------------------------------------------------------------------------------------
 def parse_header(b: bytes) -> Optional[dict]:
     if len(b) < 4:
@@ -110,17 +192,26 @@ def parse_header(b: bytes) -> Optional[dict]:
     if v >> 21 != 0x7FF:
         return None
     ver, layer, bri, sri = (v >> 19) & 3, (v >> 17) & 3, (v >> 12) & 15, (v >> 10) & 3
-    if ver == 1 or layer != 1 or bri in (0, 15) or sri == 3:
+    if ver == 1 or layer == 0 or bri in (0, 15) or sri == 3:
         return None
     lsf = int(ver != 3)
-    h = dict(lsf=lsf, version={3: 1, 2: 2, 0: 25}[ver], crc=int(not (v >> 16) & 1),
+    h = dict(layer=4 - layer, lsf=lsf, version={3: 1, 2: 2, 0: 25}[ver], crc=int(not (v >> 16) & 1),
              sr_index={3: 0, 2: 3, 0: 6}[ver] + sri, padding=(v >> 9) & 1, mode=(v >> 6) & 3, mode_ext=(v >> 4) & 3)
     h["sample_rate"] = int(TAB["kSampleRate"][h["sr_index"]])
-    h["bitrate"] = int(TAB["kBitrate"][lsf][bri])
     h["channels"] = 1 if h["mode"] == 3 else 2
+    if h["layer"] != 3:
+        h["bitrate"] = L12_BITRATE[(h["layer"], lsf)][bri]
+        if h["layer"] == 2:
+            h["frame_bytes"] = 144000 * h["bitrate"] // h["sample_rate"] + h["padding"]
+        else:
+            h["frame_bytes"] = (12000 * h["bitrate"] // h["sample_rate"] + h["padding"]) * 4
+        h["side_bytes"], h["granules"], h["spf"] = 0, 0, 1152 if h["layer"] == 2 else 384
+        return h
+    h["bitrate"] = int(TAB["kBitrate"][lsf][bri])
     h["frame_bytes"] = (72000 if lsf else 144000) * h["bitrate"] // h["sample_rate"] + h["padding"]
     h["side_bytes"] = (9 if h["channels"] == 1 else 17) if lsf else (17 if h["channels"] == 1 else 32)
     h["granules"] = 1 if lsf else 2
+    h["spf"] = 576 * h["granules"]
     return h
 
 
@@ -502,6 +593,8 @@ def scan(data: bytes):
     info = {"flags": 0, "enc_delay": -1, "enc_padding": -1, "tag_frames": -1}
     p0, h0 = frames[0]
     xo = p0 + 4 + h0["side_bytes"]
+    if h0["layer"] != 3:
+        return h0, frames, info
     if data[xo: xo + 4] in (b"Xing", b"Info"):
         info["flags"] |= 1
         fl = int.from_bytes(data[xo + 4: xo + 8], "big")
@@ -521,11 +614,115 @@ def scan(data: bytes):
     return h0, frames, info
 
 
+def _dequant(v: int, steps: int) -> float:
+    """11172-3 2.4.3.2.1 / 2.4.3.3.4: s''' = C (s'' + D), s'' the code as a two's-complement fraction with its MSB
+    inverted; for L = steps levels that is (2 v + 1 - L) / L."""
+    nb = int(math.ceil(math.log2(steps + 1)))
+    frac = v / 2 ** (nb - 1) - 1.0
+    c = 2 ** nb / steps if steps == 2 ** nb - 1 else {3: 4 / 3, 5: 8 / 5, 9: 16 / 9}[steps]
+    d = 2.0 ** (1 - nb) if steps == 2 ** nb - 1 else 0.5
+    return c * (frac + d)
+
+
+def _scalefactor(i: int) -> float:
+    return 2.0 ** (1 - i / 3)  # Table B.1: 2.0, 1.5874..., 1.2599..., ...
+
+
+def decode_frame_l12(fr: bytes, h) -> np.ndarray:
+    """One Layer I / II frame -> subband samples [channels][slots][32] (float64)."""
+    nch, layer = h["channels"], h["layer"]
+    br = Bits(fr)
+    br.pos = 32 + 16 * h["crc"]
+    bound = 4 * (h["mode_ext"] + 1) if h["mode"] == 1 else 32
+    S = np.zeros((nch, 12 if layer == 1 else 36, 32))
+    if layer == 1:
+        alloc = [[0] * 32 for _ in range(2)]
+        for sb in range(32):
+            for ch in (range(nch) if sb < bound else [0]):
+                alloc[ch][sb] = br.get(4)
+            if sb >= bound:
+                alloc[1][sb] = alloc[0][sb]
+        if any(alloc[ch][sb] == 15 for ch in range(nch) for sb in range(32)):
+            return S * 0
+        scf = [[br.get(6) if alloc[ch][sb] else 0 for ch in range(nch)] for sb in range(32)]
+        for s in range(12):
+            for sb in range(32):
+                if sb < bound:
+                    for ch in range(nch):
+                        n = alloc[ch][sb]
+                        if n:
+                            S[ch, s, sb] = _dequant(br.get(n + 1), 2 ** (n + 1) - 1) * _scalefactor(scf[sb][ch])
+                elif alloc[0][sb]:
+                    n = alloc[0][sb]
+                    q = _dequant(br.get(n + 1), 2 ** (n + 1) - 1)
+                    for ch in range(nch):
+                        S[ch, s, sb] = q * _scalefactor(scf[sb][ch])
+        return S
+    table = l2_alloc(l2_table_name(h))
+    sblimit = len(table)
+    bound = min(bound, sblimit)
+    steps = [[0] * 32 for _ in range(2)]  # 0: no allocation
+    for sb in range(sblimit):
+        nbal, st = table[sb]
+        codes = [br.get(nbal) for _ in range(nch)] if sb < bound else [br.get(nbal)] * 2
+        for ch in range(2 if sb >= bound else nch):
+            steps[ch][sb] = st[codes[ch] - 1] if codes[ch] else 0
+    scfsi = {(ch, sb): br.get(2) for sb in range(sblimit) for ch in range(nch) if steps[ch][sb]}
+    scf = {}
+    for sb in range(sblimit):
+        for ch in range(nch):
+            if not steps[ch][sb]:
+                continue
+            sel = scfsi[(ch, sb)]
+            if sel == 0:
+                scf[(ch, sb)] = [br.get(6), br.get(6), br.get(6)]
+            elif sel == 1:
+                a = br.get(6)
+                scf[(ch, sb)] = [a, a, br.get(6)]
+            elif sel == 2:
+                a = br.get(6)
+                scf[(ch, sb)] = [a, a, a]
+            else:
+                a, b = br.get(6), br.get(6)
+                scf[(ch, sb)] = [a, b, b]
+
+    def triple(L):
+        nb, grouped = l2_codeword(L)
+        if not grouped:
+            return [_dequant(br.get(nb), L) for _ in range(3)]
+        c = br.get(nb)
+        return [_dequant(c % L, L), _dequant((c // L) % L, L), _dequant(c // L // L, L)]
+
+    for gr in range(12):
+        for sb in range(sblimit):
+            if sb < bound:
+                for ch in range(nch):
+                    if steps[ch][sb]:
+                        S[ch, 3 * gr: 3 * gr + 3, sb] = np.array(triple(steps[ch][sb])) * _scalefactor(
+                            scf[(ch, sb)][gr // 4])
+            elif steps[0][sb]:
+                q = np.array(triple(steps[0][sb]))
+                for ch in range(nch):
+                    S[ch, 3 * gr: 3 * gr + 3, sb] = q * _scalefactor(scf[(ch, sb)][gr // 4])
+    return S
+
+
 def decode(data: bytes, stats: Optional[dict] = None):
     """MP3 bytes -> (f32 [frames, channels], sample_rate, info). stats (optional) collects per-granule bit accounting
     ('exact': Huffman data ended exactly at part2_3_length) and the Huffman tables used."""
     h0, frames, info = scan(data)
-    nch, spf = h0["channels"], 576 * h0["granules"]
+    nch, spf = h0["channels"], h0["spf"]
+    if h0["layer"] != 3:  # Layers I / II: self-contained frames into the synthesis bank, no trim
+        V = [np.zeros(1024) for _ in range(nch)]
+        pcm = np.zeros((len(frames) * spf, nch))
+        for k, (p, h) in enumerate(frames):
+            S = decode_frame_l12(data[p: p + h["frame_bytes"]], h)
+            if stats is not None:
+                stats.setdefault("l2_tables", set()).add(l2_table_name(h) if h["layer"] == 2 else "I")
+            for ch in range(nch):
+                pcm[k * spf: (k + 1) * spf, ch] = synthesize(S[ch], V[ch])
+        info.update(skip=0, total=len(pcm), n_frames=len(frames), sample_rate=h0["sample_rate"], channels=nch)
+        return pcm.astype(np.float32), h0["sample_rate"], info
     md, off = bytearray(), []
     for p, h in frames:
         off.append(len(md))
@@ -804,4 +1001,131 @@ def write_stream(rng, version: int = 1, sr_sub: Optional[int] = None, mode: Opti
         if use_crc:
             out += bytes(rng.integers(0, 256, 2, dtype=np.uint8))
         out += side + md_stream[off: off + cap]
+    return bytes(out)
+
+
+def _header_bytes_l12(layer, version, sr_sub, bri, crc, pad, mode, mode_ext) -> bytes:
+    v = (0x7FF << 21) | (_VER_BITS[version] << 19) | ((4 - layer) << 17) | ((0 if crc else 1) << 16) | (bri << 12)
+    v |= (sr_sub << 10) | (pad << 9) | (mode << 6) | (mode_ext << 4)
+    return v.to_bytes(4, "big")
+
+
+def write_stream_l12(rng, layer: int = 2, version: int = 1, sr_sub: Optional[int] = None, mode: Optional[int] = None,
+                     bri: Optional[int] = None, nframes: int = 6, crc: Optional[bool] = None, id3: bool = False,
+                     fill: float = 0.7, bad_groups: bool = True) -> bytes:
+    """A random-syntax Layer I or II stream: random bit allocations (every code of every row, dropped at random until
+    the frame's bits fit; `fill` the share of subbands allocated), scfsi patterns, scalefactors and sample codes —
+    grouped codewords past steps^3 included when bad_groups — with joint-stereo bounds, CRC words and padding;
+    ancillary bytes fill each frame."""
+    sr_sub = int(rng.integers(0, 3)) if sr_sub is None else sr_sub
+    mode = int(rng.integers(0, 4)) if mode is None else mode
+    if bri is None:
+        bri = int(rng.integers(6, 15))
+    out = bytearray()
+    if id3:
+        body = bytes(rng.integers(0, 128, 30, dtype=np.uint8))
+        out += b"ID3\x03\x00\x00" + bytes([0, 0, 0, len(body)]) + body
+    for _ in range(nframes):
+        pad = int(rng.integers(0, 2))
+        use_crc = bool(rng.integers(0, 2)) if crc is None else crc
+        mode_ext = int(rng.integers(0, 4)) if mode == 1 else 0
+        hdr = _header_bytes_l12(layer, version, sr_sub, bri, use_crc, pad, mode, mode_ext)
+        h = parse_header(hdr)
+        nch = h["channels"]
+        bound = 4 * (mode_ext + 1) if mode == 1 else 32
+        cap = 8 * h["frame_bytes"] - 32 - 16 * use_crc
+        if layer == 1:
+            rows = [(4, None)] * 32
+        else:
+            rows = l2_alloc(l2_table_name(h))
+        sblimit = len(rows)
+        bound = min(bound, sblimit)
+        # allocation codes [ch][sb]
+        codes = [[0] * 32 for _ in range(2)]
+        for sb in range(sblimit):
+            nbal = rows[sb][0]
+            top = 14 if layer == 1 else 2 ** nbal - 1
+            for ch in range(nch if sb < bound else 1):
+                if rng.random() < fill:
+                    codes[ch][sb] = int(rng.integers(1, top + 1))
+            if sb >= bound:
+                codes[1][sb] = codes[0][sb]
+        scfsi = [[int(x) for x in rng.integers(0, 4, 32)] for _ in range(2)]
+
+        def cost():
+            n = sum(rows[sb][0] * (nch if sb < bound else 1) for sb in range(sblimit))
+            for sb in range(sblimit):
+                for ch in range(nch):
+                    if codes[ch][sb]:
+                        if layer == 1:
+                            n += 6
+                        else:
+                            n += 2 + 6 * {0: 3, 1: 2, 2: 1, 3: 2}[scfsi[ch][sb]]
+            for sb in range(sblimit):
+                chans = range(nch) if sb < bound else [0]
+                for ch in chans:
+                    c = codes[ch][sb]
+                    if not c:
+                        continue
+                    if layer == 1:
+                        n += 12 * (c + 1)
+                    else:
+                        nb, grouped = l2_codeword(rows[sb][1][c - 1])
+                        n += 12 * (nb if grouped else 3 * nb)
+            return n
+
+        while cost() > cap:
+            live = [(ch, sb) for sb in range(sblimit) for ch in range(2) if codes[ch][sb]]
+            ch, sb = live[int(rng.integers(0, len(live)))]
+            if sb >= bound:
+                codes[0][sb] = codes[1][sb] = 0
+            else:
+                codes[ch][sb] = 0
+        w = BitWriter()
+        for sb in range(sblimit):
+            for ch in range(nch if sb < bound else 1):
+                w.put(codes[ch][sb], rows[sb][0])
+        if layer == 1:
+            for sb in range(32):
+                for ch in range(nch):
+                    if codes[ch][sb]:
+                        w.put(rng.integers(0, 63), 6)
+            for _s in range(12):
+                for sb in range(32):
+                    for ch in (range(nch) if sb < bound else [0]):
+                        c = codes[ch][sb]
+                        if c:
+                            w.put(rng.integers(0, 2 ** (c + 1) - 1), c + 1)  # (all-ones is forbidden)
+        else:
+            for sb in range(sblimit):
+                for ch in range(nch):
+                    if codes[ch][sb]:
+                        w.put(scfsi[ch][sb], 2)
+            for sb in range(sblimit):
+                for ch in range(nch):
+                    if codes[ch][sb]:
+                        for _k in range({0: 3, 1: 2, 2: 1, 3: 2}[scfsi[ch][sb]]):
+                            w.put(rng.integers(0, 63), 6)
+            for _gr in range(12):
+                for sb in range(sblimit):
+                    for ch in (range(nch) if sb < bound else [0]):
+                        c = codes[ch][sb]
+                        if not c:
+                            continue
+                        L = rows[sb][1][c - 1]
+                        nb, grouped = l2_codeword(L)
+                        if grouped:
+                            top = 2 ** nb if (bad_groups and rng.random() < 0.05) else L ** 3
+                            w.put(rng.integers(0, top), nb)
+                        else:
+                            for _k in range(3):
+                                w.put(rng.integers(0, L), nb)
+        assert w.n <= cap, (w.n, cap)
+        body = bytearray(_bytes(w.bits()))
+        nbody = h["frame_bytes"] - 4 - 2 * use_crc
+        body += bytes(rng.integers(0, 256, nbody - len(body), dtype=np.uint8))  # ancillary data
+        out += hdr
+        if use_crc:
+            out += bytes(rng.integers(0, 256, 2, dtype=np.uint8))
+        out += body
     return bytes(out)

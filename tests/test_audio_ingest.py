@@ -182,23 +182,30 @@ def test_constant_subframe_stream_over_duration_cap(monkeypatch):
 
 
 def test_undecoded_containers_named_and_garbage_reported_as_reference():
-    """MPEG Layer I / II, Ogg (not Vorbis: Opus) and WebM uploads are refused by name; bytes no container matches
-    get the reference's own decode-failure message (transformers' ffmpeg_read), which its transcribe() returns as
-    {"error": ...}. (MP3 and AAC / M4A are decoded: tests/test_audio_mp3.py, tests/test_audio_aac.py.)"""
-    cases = {b"\xff\xfd\x90\x00" + bytes(64): "MPEG audio Layer II", b"\xff\xff\x90\x00" + bytes(64): "MPEG audio Layer I",
-             b"OggS\x00\x02" + bytes(64): "Ogg", b"\x1aE\xdf\xa3" + bytes(64): "Matroska/WebM"}
+    """Ogg Opus (and Ogg of another codec) and WebM uploads are refused by name; bytes no container matches get the
+    reference's own decode-failure message (transformers' ffmpeg_read), which its transcribe() returns as
+    {"error": ...}. (MPEG audio of every layer and AAC / M4A are decoded: tests/test_audio_mp3.py,
+    tests/test_audio_mpeg_l12.py, tests/test_audio_aac.py.)"""
+    cases = {b"OggS\x00\x02" + bytes(22) + b"OpusHead" + bytes(32): "Ogg Opus", b"OggS\x00\x02" + bytes(64): "Ogg",
+             b"\x1aE\xdf\xa3" + bytes(64): "Matroska/WebM"}
     for data, name in cases.items():
         assert audio.container_name(data) == name
         with pytest.raises(ValueError, match=f"^{re.escape(name)} audio is not decoded"):
+            audio.load_input(data)
+    # a lone Layer I / II header (no frame the next header confirms): named, refused by the decoder's frame search
+    for data, name in ((b"\xff\xfd\x90\x00" + bytes(64), "MPEG audio Layer II"),
+                       (b"\xff\xff\x90\x00" + bytes(64), "MPEG audio Layer I")):
+        assert audio.container_name(data) == name
+        with pytest.raises(ValueError, match="no MPEG audio frame"):
             audio.load_input(data)
     # an ID3 tag before ADTS frames names AAC; an MP4 without a moov box is refused by the demuxer
     assert audio.container_name(b"ID3\x04\x00\x00\x00\x00\x00\x04" + bytes(4) + b"\xff\xf1\x50\x80" + bytes(64)) == \
         "AAC (ADTS)"
     with pytest.raises(ValueError, match="no moov"):
         audio.load_input(b"\x00\x00\x00\x20ftypM4A " + bytes(64))
-    # an ID3 tag over bytes holding no Layer III frame: named MP3, refused by the decoder's frame search
+    # an ID3 tag over bytes holding no MPEG audio frame: named MP3, refused by the decoder's frame search
     assert audio.container_name(b"ID3\x04\x00" + bytes(64)) == "MP3"
-    with pytest.raises(ValueError, match="no MPEG Layer III frame"):
+    with pytest.raises(ValueError, match="no MPEG audio frame"):
         audio.load_input(b"ID3\x04\x00" + bytes(64))
     with pytest.raises(ValueError) as e:
         audio.load_input(b"hello, not audio" * 8)

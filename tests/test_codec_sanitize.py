@@ -8,7 +8,7 @@ hundreds of damaged copies of each (truncations, bit flips, overwritten runs, du
 out-of-bounds access, leak or undefined behaviour aborts the run. The corpus: the oracle's FLAC writer over every
 subframe kind / stereo mode / bit depth / blocking, its random-syntax Vorbis writer, the image's one libVorbis
 stream, the MP3 oracle's random-syntax Layer III writer (MPEG-1 / 2 / 2.5, every channel mode, Info + LAME frames,
-ID3v2 tags, junk between frames), the image's one real MP3, the AAC oracle's random-syntax ADTS streams, the access
+ID3v2 tags, junk between frames) and its Layer I / II writer, the image's one real MP3, the AAC oracle's random-syntax ADTS streams, the access
 units of the image's one real AAC-LC track as ADTS, and the reference's example FLAC (first 256 KB, when present in
 this container)."""
 import os
@@ -54,6 +54,10 @@ def _corpus(tmp_path):
     for seed in range(6):
         put(f"gen{seed}.mp3", mo.write_stream(np.random.default_rng(seed), version=(1, 2, 25)[seed % 3], nframes=5,
                                               mode=seed % 4, xing=seed % 2 == 0, id3=seed == 1, junk=seed == 3))
+    for seed in range(6):
+        put(f"gen{seed}.mp2", mo.write_stream_l12(np.random.default_rng(seed), layer=1 + seed % 2,
+                                                  version=(1, 2, 25)[seed % 3], mode=seed % 4, nframes=4,
+                                                  id3=seed == 2))
     if os.path.exists(REAL_MP3):
         put("real.mp3", open(REAL_MP3, "rb").read())
     for seed in range(6):

@@ -206,16 +206,15 @@ def test_install_overlap_runs_diarizer_beside_transcription():
 
 @pytest.mark.parametrize("layout", ["vocalis", "root"])
 def test_undecodable_upload_reaches_reference_error_convention(layout, tmp_path):
-    """An upload the engine cannot decode (here MPEG audio Layer II) surfaces as the reference's transcribe() error result,
+    """An upload the engine cannot decode (here Ogg Opus) surfaces as the reference's transcribe() error result,
     {"error": "Transcription error: <message>"} (the "raises" fixture above), not as an exception."""
     cls = ap.AudioProcessingPipeline if layout == "vocalis" else ap.RootAudioProcessingPipeline
     p = cls()
     p.transcription_model = lambda inputs, **kw: tw_audio.load_input(inputs)
-    f = tmp_path / "upload.mp2"
-    f.write_bytes(b"\xff\xfd\x90\x00" + bytes(256))
+    f = tmp_path / "upload.ogg"
+    f.write_bytes(b"OggS\x00\x02" + bytes(22) + b"OpusHead" + bytes(256))
     got = p.transcribe(str(f), "transcribe")
-    assert got == {"error": "Transcription error: MPEG audio Layer II audio is not decoded by this engine (decoded "
-                            "containers: FLAC, Ogg Vorbis, MP3 (MPEG-1 / 2 / 2.5 Layer III), AAC-LC (M4A / MP4, ADTS), "
-                            "WAV / RIFX / RF64 (PCM, float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C); convert the "
-                            "upload to one of "
-                            "them"}
+    assert got == {"error": "Transcription error: Ogg Opus audio is not decoded by this engine (decoded containers: "
+                            "FLAC, Ogg Vorbis, MP3 / MPEG audio (MPEG-1 / 2 / 2.5 Layers I, II, III), AAC-LC (M4A / "
+                            "MP4, ADTS), WAV / RIFX / RF64 (PCM, float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C); "
+                            "convert the upload to one of them"}

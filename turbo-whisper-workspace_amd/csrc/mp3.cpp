@@ -1,24 +1,30 @@
-// Native MPEG-1 / MPEG-2 LSF / MPEG-2.5 Layer III ("MP3") decoder (host side of the audio ingest, include/tw_audio.h).
+// Native MPEG audio decoder: MPEG-1 / MPEG-2 LSF / MPEG-2.5 Layer III ("MP3"), and Layers I and II (host side of the
+// audio ingest, include/tw_audio.h).
 //
 // Replaces the codec half of the reference's ffmpeg_read ($TF/pipelines/audio_utils.py:9-45) for MP3 uploads: the
 // reference's POST /api/transcribe stores any upload under its own suffix (vocalis/api/main.py:67-75) and its own
-// callers list .mp3 (vocalis/security/security_monitor.py:353, scripts/normalize_audio.py:226). Written from ISO/IEC
-// 11172-3 and 13818-3: frame sync and header, side information, the bit reservoir (main_data_begin), scalefactors
+// callers list .mp3 (vocalis/security/security_monitor.py:353, scripts/normalize_audio.py:226); ffmpeg's mp3 demuxer
+// takes MPEG audio of any layer under that name (mp1 / mp2 / mp3float decoders). Written from ISO/IEC 11172-3 and
+// 13818-3: frame sync and header, side information, the bit reservoir (main_data_begin), scalefactors
 // (MPEG-1 scfsi sharing; the LSF scalefac_compress partitions incl. the intensity-stereo right channel), Huffman
 // big-values / count1 decoding with the standard's tables (mp3_tables.h), requantisation (|is|^(4/3), global gain,
 // subblock gain, scalefac_scale, pre-emphasis), short-block reordering, mid/side and intensity stereo (MPEG-1 tan
 // ratios, LSF intensity_scale powers), alias reduction, the IMDCT with the four window shapes and overlap-add,
 // frequency inversion and the 32-band polyphase synthesis filter bank. The Xing / Info / VBRI frame is skipped and
 // a LAME (or Lavf / Lavc) tag's encoder delay and padding trim the output to the encoded length, as ffmpeg's mp3
-// demuxer does (delay + 529 decoder-delay samples skipped at the start, padding - 529 at the end).
+// demuxer does (delay + 529 decoder-delay samples skipped at the start, padding - 529 at the end). Layers I / II:
+// bit allocation (Layer II's tables B.2a-d by rate and bitrate per channel, 13818-3's for LSF), scfsi, grouped
+// codewords, joint-stereo subband sharing above the bound, then the same filter bank; no tag, no trim.
 //
 // Parallel decode: a Layer III frame depends on earlier frames only through (a) reservoir bytes, read here from one
 // concatenated main-data buffer by offset, and (b) the IMDCT overlap and the synthesis buffer, which one decoded
-// frame (>= 18 subband slots >= the filter bank's 16) fully determines. Threads therefore decode frame ranges, each
-// starting one frame early with its output discarded: bit-identical to a serial decode for any thread count.
+// frame (>= 18 subband slots >= the filter bank's 16) fully determines; a Layer I / II frame only through the
+// synthesis buffer (36 slots a Layer II frame, 12 a Layer I frame: two frames prime it). Threads therefore decode
+// frame ranges, each starting one (Layer I: two) frames early with that output discarded: bit-identical to a serial
+// decode for any thread count.
 //
-// Output: f32 samples, interleaved [frames][channels], nominal full scale +-1 (what ffmpeg's mp3float decoder hands
-// to its resampler).
+// Output: f32 samples, interleaved [frames][channels], nominal full scale +-1 (what ffmpeg's float decoders hand to
+// its resampler).
 #include <math.h>
 #include <string.h>
 
@@ -38,37 +44,52 @@ using namespace mp3t;
 
 // ---- frame header ---------------------------------------------------------------------------------------------------
 struct Header {
-  int lsf = 0;  // 1: MPEG-2 / MPEG-2.5 (one granule per frame, LSF scalefactors)
+  int layer = 3;  // 1, 2 or 3
+  int lsf = 0;  // 1: MPEG-2 / MPEG-2.5 (Layer III: one granule per frame, LSF scalefactors)
   int version = 1;  // 1, 2 or 25
   int crc = 0;  // a 16-bit CRC follows the header
   int bitrate = 0, sr_index = 0, sample_rate = 0, padding = 0;
   int mode = 0, mode_ext = 0, channels = 0;
   int frame_bytes = 0, side_bytes = 0, granules = 0;
+  int spf = 0;  // samples per channel per frame: 384 (Layer I), 1152 (Layer II, MPEG-1 Layer III), 576 (LSF III)
 };
 
 bool parse_header(const uint8_t* p, Header& h) {
   const uint32_t v = (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
   if ((v >> 21) != 0x7ffu) return false;
-  const int ver = (v >> 19) & 3, layer = (v >> 17) & 3, bri = (v >> 12) & 15, sri = (v >> 10) & 3;
-  if (ver == 1 || layer != 1 || bri == 0 || bri == 15 || sri == 3) return false;  // reserved / not Layer III / free
+  const int ver = (v >> 19) & 3, lbits = (v >> 17) & 3, bri = (v >> 12) & 15, sri = (v >> 10) & 3;
+  if (ver == 1 || lbits == 0 || bri == 0 || bri == 15 || sri == 3) return false;  // reserved / free format
+  h.layer = 4 - lbits;
   h.lsf = ver != 3;
   h.version = ver == 3 ? 1 : ver == 2 ? 2 : 25;
   h.crc = !((v >> 16) & 1);
   h.sr_index = (ver == 3 ? 0 : ver == 2 ? 3 : 6) + sri;
   h.sample_rate = kSampleRate[h.sr_index];
-  h.bitrate = kBitrate[h.lsf][bri];
   h.padding = (v >> 9) & 1;
   h.mode = (v >> 6) & 3;
   h.mode_ext = (v >> 4) & 3;
   h.channels = h.mode == 3 ? 1 : 2;
-  h.frame_bytes = (h.lsf ? 72000 : 144000) * h.bitrate / h.sample_rate + h.padding;
-  h.side_bytes = h.lsf ? (h.channels == 1 ? 9 : 17) : (h.channels == 1 ? 17 : 32);
-  h.granules = h.lsf ? 1 : 2;
+  if (h.layer == 3) {
+    h.bitrate = kBitrate[h.lsf][bri];
+    h.frame_bytes = (h.lsf ? 72000 : 144000) * h.bitrate / h.sample_rate + h.padding;
+    h.side_bytes = h.lsf ? (h.channels == 1 ? 9 : 17) : (h.channels == 1 ? 17 : 32);
+    h.granules = h.lsf ? 1 : 2;
+    h.spf = 576 * h.granules;
+  } else if (h.layer == 2) {  // 1152 samples in every version; 144 bytes per kbit/s / kHz
+    h.bitrate = h.lsf ? kBitrate[1][bri] : kBitrateL12[1][bri];
+    h.frame_bytes = 144000 * h.bitrate / h.sample_rate + h.padding;
+    h.spf = 1152;
+  } else {  // Layer I: 384 samples in 4-byte slots
+    h.bitrate = kBitrateL12[h.lsf ? 2 : 0][bri];
+    h.frame_bytes = (12000 * h.bitrate / h.sample_rate + h.padding) * 4;
+    h.spf = 384;
+  }
   return h.frame_bytes >= 4 + 2 * h.crc + h.side_bytes;
 }
 
 bool same_stream(const Header& a, const Header& b) {
-  return a.lsf == b.lsf && a.version == b.version && a.sr_index == b.sr_index && a.channels == b.channels;
+  return a.layer == b.layer && a.lsf == b.lsf && a.version == b.version && a.sr_index == b.sr_index &&
+         a.channels == b.channels;
 }
 
 uint32_t be32(const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
@@ -108,7 +129,7 @@ bool scan(const uint8_t* d, int64_t n, Stream& s, const char** err) {
   Header h;
   while (pos + 4 <= n && !confirmed(d, n, pos, h)) pos++;
   if (pos + 4 > n) {
-    *err = "MP3: no MPEG Layer III frame found";
+    *err = "MP3: no MPEG audio frame found";
     return false;
   }
   s.first = h;
@@ -126,12 +147,14 @@ bool scan(const uint8_t* d, int64_t n, Stream& s, const char** err) {
     while (q + 4 <= n && !(parse_header(d + q, h) && same_stream(h, s.first) && q + h.frame_bytes <= n)) q++;
     pos = q;
   }
-  // the first frame may be a Xing / Info (LAME) or VBRI header frame instead of audio
+  // the first frame may be a Xing / Info (LAME) or VBRI header frame instead of audio (Layer III only: the tag
+  // sits after the Layer III side information)
   const int64_t p0 = s.pos[0];
   const Header& h0 = s.hdr[0];
   const int64_t fend = p0 + h0.frame_bytes;
   const int64_t xo = p0 + 4 + h0.side_bytes;  // (the offset ignores the CRC, as encoders and ffmpeg place it)
-  if (xo + 8 <= fend && (memcmp(d + xo, "Xing", 4) == 0 || memcmp(d + xo, "Info", 4) == 0)) {
+  const bool l3 = h0.layer == 3;
+  if (l3 && xo + 8 <= fend && (memcmp(d + xo, "Xing", 4) == 0 || memcmp(d + xo, "Info", 4) == 0)) {
     s.flags |= 1;
     const uint32_t fl = be32(d + xo + 4);
     int64_t q = xo + 8;
@@ -149,14 +172,14 @@ bool scan(const uint8_t* d, int64_t n, Stream& s, const char** err) {
       s.enc_padding = (g[1] & 15) << 8 | g[2];
       s.flags |= 2;
     }
-  } else if (p0 + 4 + 32 + 4 <= fend && memcmp(d + p0 + 4 + 32, "VBRI", 4) == 0) {
+  } else if (l3 && p0 + 4 + 32 + 4 <= fend && memcmp(d + p0 + 4 + 32, "VBRI", 4) == 0) {
     s.flags |= 4;
   }
   if (s.flags & 5) {
     s.pos.erase(s.pos.begin());
     s.hdr.erase(s.hdr.begin());
   }
-  const int64_t spf = s.first.granules * 576;
+  const int64_t spf = s.first.spf;
   const int64_t decoded = (int64_t)s.pos.size() * spf;
   if (s.flags & 2) {
     const int64_t frames = s.tag_frames >= 0 ? s.tag_frames : (int64_t)s.pos.size();
@@ -733,9 +756,9 @@ struct Decoder {
     }
   }
 
-  // polyphase synthesis of 18 slots of one channel: pcm[slot * 32 + j] (stride `stride` floats)
-  void synth(const float (*sbs)[32], float* V, int& voff, float* pcm, int stride) const {
-    for (int s = 0; s < 18; s++) {
+  // polyphase synthesis of `nslot` subband slots of one channel: pcm[slot * 32 + j] (stride `stride` floats)
+  void synth(const float (*sbs)[32], int nslot, float* V, int& voff, float* pcm, int stride) const {
+    for (int s = 0; s < nslot; s++) {
       voff = (voff - 64) & 1023;
       const float* S = sbs[s];
       // matrixing into the newest 64-value block of V (voff is a multiple of 64, so every block is contiguous)
@@ -759,9 +782,142 @@ struct Decoder {
     }
   }
 
+  // ---- Layers I and II (11172-3 2.4.3.2 / 2.4.3.3; 13818-3 2.4.3.2 for LSF Layer II's table) -----------------------
+  // A frame is self-contained: bit allocation, scalefactors and samples of the 32 subbands, then the same synthesis
+  // filter bank as Layer III. A sample code v of a class with L steps dequantises to (2 v + 1 - L) / L times the
+  // scalefactor 2^(1 - index / 3) (the standard's C (s'' + D) with s'' the code read as a two's-complement fraction,
+  // MSB inverted, written in closed form).
+  static float scale(int idx) { return (float)exp2(1.0 - idx / 3.0); }
+  static float dequant(int v, int steps) { return (float)((2.0 * v + 1.0 - steps) / steps); }
+
+  // Layer I: 12 slots; joint stereo shares the allocation and samples of subbands >= bound (each channel keeps its
+  // own scalefactor). An allocation of 15 (forbidden) makes the frame silent.
+  bool layer1(Bits& br, const Header& h, int bound, float (*sbs)[36][32]) const {
+    const int nch = h.channels;
+    int alloc[2][32], scf[2][32];
+    for (int sb = 0; sb < 32; sb++) {
+      if (sb < bound) {
+        for (int ch = 0; ch < nch; ch++) alloc[ch][sb] = br.get(4);
+      } else {
+        alloc[0][sb] = alloc[1][sb] = br.get(4);
+      }
+      for (int ch = 0; ch < nch; ch++)
+        if (alloc[ch][sb] == 15) return false;
+    }
+    for (int sb = 0; sb < 32; sb++)
+      for (int ch = 0; ch < nch; ch++) scf[ch][sb] = alloc[ch][sb] ? br.get(6) : 0;
+    for (int s = 0; s < 12; s++)
+      for (int sb = 0; sb < 32; sb++) {
+        if (sb < bound) {
+          for (int ch = 0; ch < nch; ch++)
+            if (const int n = alloc[ch][sb])
+              sbs[ch][s][sb] = dequant(br.get(n + 1), (2 << n) - 1) * scale(scf[ch][sb]);
+        } else if (const int n = alloc[0][sb]) {
+          const float q = dequant(br.get(n + 1), (2 << n) - 1);
+          for (int ch = 0; ch < nch; ch++) sbs[ch][s][sb] = q * scale(scf[ch][sb]);
+        }
+      }
+    return true;
+  }
+
+  // the Layer II allocation table (11172-3 Annex B Table B.2 by sampling rate and bitrate per channel; LSF: 13818-3
+  // Table B.1)
+  static int l2_table(const Header& h) {
+    if (h.lsf) return 4;
+    const int chb = h.bitrate / h.channels;
+    if ((h.sample_rate == 48000 && chb >= 56) || (chb >= 56 && chb <= 80)) return 0;
+    if (h.sample_rate != 48000 && chb >= 96) return 1;
+    if (h.sample_rate != 32000 && chb <= 48) return 2;
+    return 3;
+  }
+
+  // Layer II: 36 slots in 12 granules of 3; scfsi selects how the three scalefactors of a subband are shared across
+  // the frame's three parts of 12 slots
+  bool layer2(Bits& br, const Header& h, int bound, float (*sbs)[36][32]) const {
+    const int nch = h.channels, tab = l2_table(h), sblimit = kL2Sblimit[tab];
+    bound = std::min(bound, sblimit);
+    int cls[2][32], scf[2][32][3];
+    for (int sb = 0; sb < sblimit; sb++) {
+      const int row = kL2SbRow[tab][sb], nbal = kL2RowBits[row];
+      int a[2] = {0, 0};
+      if (sb < bound) {
+        for (int ch = 0; ch < nch; ch++) a[ch] = br.get(nbal);
+      } else {
+        a[0] = a[1] = br.get(nbal);
+      }
+      for (int ch = 0; ch < 2; ch++) cls[ch][sb] = a[ch] ? kL2Row[row][a[ch] - 1] : -1;
+    }
+    int scfsi[2][32];
+    for (int sb = 0; sb < sblimit; sb++)
+      for (int ch = 0; ch < nch; ch++) scfsi[ch][sb] = cls[ch][sb] >= 0 ? br.get(2) : 0;
+    for (int sb = 0; sb < sblimit; sb++)
+      for (int ch = 0; ch < nch; ch++) {
+        int* f = scf[ch][sb];
+        if (cls[ch][sb] < 0) {
+          f[0] = f[1] = f[2] = 0;
+          continue;
+        }
+        switch (scfsi[ch][sb]) {
+          case 0: f[0] = br.get(6), f[1] = br.get(6), f[2] = br.get(6); break;
+          case 1: f[0] = f[1] = br.get(6), f[2] = br.get(6); break;
+          case 2: f[0] = f[1] = f[2] = br.get(6); break;
+          default: f[0] = br.get(6), f[1] = f[2] = br.get(6); break;
+        }
+      }
+    // one triple of sample codes of class c (grouped: one codeword; the third value is the quotient left after two
+    // divisions, as ffmpeg's division tables hold it for codewords past steps^3)
+    auto triple = [&](int c, float* q) {
+      const int L = kL2Steps[c];
+      if (kL2Grouped[c]) {
+        int v = br.get(kL2Bits[c]);
+        const int a = v % L;
+        v /= L;
+        const int b = v % L;
+        q[0] = dequant(a, L), q[1] = dequant(b, L), q[2] = dequant(v / L, L);
+      } else {
+        for (int j = 0; j < 3; j++) q[j] = dequant(br.get(kL2Bits[c]), L);
+      }
+    };
+    for (int gr = 0; gr < 12; gr++)
+      for (int sb = 0; sb < sblimit; sb++) {
+        float q[3];
+        if (sb < bound) {
+          for (int ch = 0; ch < nch; ch++)
+            if (cls[ch][sb] >= 0) {
+              triple(cls[ch][sb], q);
+              const float f = scale(scf[ch][sb][gr >> 2]);
+              for (int j = 0; j < 3; j++) sbs[ch][3 * gr + j][sb] = q[j] * f;
+            }
+        } else if (cls[0][sb] >= 0) {
+          triple(cls[0][sb], q);
+          for (int ch = 0; ch < nch; ch++) {
+            const float f = scale(scf[ch][sb][gr >> 2]);
+            for (int j = 0; j < 3; j++) sbs[ch][3 * gr + j][sb] = q[j] * f;
+          }
+        }
+      }
+    return true;
+  }
+
+  void frame_l12(int64_t k, State& S, float* pcm) const {
+    const Header& h = st.hdr[k];
+    Bits br{data + st.pos[k], h.frame_bytes};
+    br.pos = 32 + 16 * h.crc;
+    const int nch = h.channels, nslot = h.spf / 32;
+    static thread_local float sbs[2][36][32];
+    memset(sbs, 0, sizeof(sbs));
+    const int bound = h.mode == 1 ? 4 * (h.mode_ext + 1) : 32;
+    if (!(h.layer == 1 ? layer1(br, h, bound, sbs) : layer2(br, h, bound, sbs))) memset(sbs, 0, sizeof(sbs));
+    for (int ch = 0; ch < nch; ch++) {
+      static thread_local float scratch[1152];
+      synth(sbs[ch], nslot, S.V[ch], S.voff[ch], pcm ? pcm + ch : scratch, pcm ? nch : 1);
+    }
+  }
+
   // decode frame k into pcm[spf][channels] (nullptr: state only)
   void frame(int64_t k, State& S, float* pcm) const {
     const Header& h = st.hdr[k];
+    if (h.layer != 3) return frame_l12(k, S, pcm);
     const int64_t p = st.pos[k];
     SideInfo si;
     parse_side(data + p + 4 + 2 * h.crc, h.side_bytes, h, si);
@@ -801,7 +957,7 @@ struct Decoder {
         imdct(g, xr[ch], S.overlap[ch], sbs);
         float scratch[576];
         float* out = pcm ? pcm + (size_t)gr * 576 * nch + ch : scratch;
-        synth(sbs, S.V[ch], S.voff[ch], out, pcm ? nch : 1);
+        synth(sbs, 18, S.V[ch], S.voff[ch], out, pcm ? nch : 1);
       }
     }
   }
@@ -812,8 +968,9 @@ bool build_main_data(const uint8_t* d, const Stream& s, std::vector<uint8_t>& md
   off.resize(s.pos.size());
   for (size_t k = 0; k < s.pos.size(); k++) {
     const Header& h = s.hdr[k];
-    const int64_t a = s.pos[k] + 4 + 2 * h.crc + h.side_bytes, b = s.pos[k] + h.frame_bytes;
     off[k] = (int64_t)md.size();
+    if (h.layer != 3) continue;  // (Layers I / II: no reservoir)
+    const int64_t a = s.pos[k] + 4 + 2 * h.crc + h.side_bytes, b = s.pos[k] + h.frame_bytes;
     md.insert(md.end(), d + a, d + b);
   }
   return true;
@@ -841,7 +998,8 @@ int tw_mp3_probe(const uint8_t* data, int64_t size, TwMp3Info* info) {
   info->bitrate_kbps = s.pos.empty() ? s.first.bitrate : s.hdr[0].bitrate;
   info->total_samples = s.total;
   info->n_frames = (int64_t)s.pos.size();
-  info->samples_per_frame = s.first.granules * 576;
+  info->samples_per_frame = s.first.spf;
+  info->layer = s.first.layer;
   info->enc_delay = s.enc_delay;
   info->enc_padding = s.enc_padding;
   info->flags = s.flags;
@@ -869,7 +1027,10 @@ int tw_mp3_decode(const uint8_t* data, int64_t size, float* out, int64_t out_fra
   std::vector<int64_t> off;
   build_main_data(data, s, md, off);
   const int nch = s.first.channels;
-  const int64_t spf = s.first.granules * 576, nf = (int64_t)s.pos.size();
+  const int64_t spf = s.first.spf, nf = (int64_t)s.pos.size();
+  // frames of priming before a thread's range: enough subband slots for the synthesis buffer's 16 (Layer I's 12 slots
+  // per frame need two frames)
+  const int64_t warm = s.first.layer == 1 ? 2 : 1;
   Decoder dec{data, s, md, off};
   int nt = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
   nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, nf / 8));
@@ -877,9 +1038,9 @@ int tw_mp3_decode(const uint8_t* data, int64_t size, float* out, int64_t out_fra
     State S;
     S.reset();
     std::vector<float> pcm((size_t)spf * nch);
-    for (int64_t k = std::max<int64_t>(0, a - 1); k < b; k++) {
+    for (int64_t k = std::max<int64_t>(0, a - warm); k < b; k++) {
       dec.frame(k, S, pcm.data());
-      if (k < a) continue;  // warm-up frame: primes the overlap and synthesis buffers only
+      if (k < a) continue;  // warm-up frames: prime the overlap and synthesis buffers only
       const int64_t g0 = k * spf - s.skip;
       for (int64_t i = 0; i < spf; i++) {
         const int64_t o = g0 + i;

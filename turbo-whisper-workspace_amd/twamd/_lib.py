@@ -96,7 +96,7 @@ class TwMp3Info(ctypes.Structure):
         ("sample_rate", ctypes.c_int32), ("channels", ctypes.c_int32), ("version", ctypes.c_int32),
         ("bitrate_kbps", ctypes.c_int32), ("total_samples", ctypes.c_int64), ("n_frames", ctypes.c_int64),
         ("skip_samples", ctypes.c_int64), ("samples_per_frame", ctypes.c_int32), ("enc_delay", ctypes.c_int32),
-        ("enc_padding", ctypes.c_int32), ("flags", ctypes.c_int32),
+        ("enc_padding", ctypes.c_int32), ("flags", ctypes.c_int32), ("layer", ctypes.c_int32),
     ]
 
 

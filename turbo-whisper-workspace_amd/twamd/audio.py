@@ -8,7 +8,7 @@ differs, multi-channel arrays are averaged to mono.
 
 Containers: FLAC (native multi-threaded decoder in libtwhip.so, include/tw_audio.h; bit-exact, verifiable
 against the stream's STREAMINFO MD5), Ogg Vorbis (native decoder, csrc/vorbis.cpp), MP3 (MPEG-1 / 2 / 2.5 Layer III,
-native multi-threaded decoder csrc/mp3.cpp, gapless-trimmed by the LAME tag as ffmpeg trims it), AAC-LC (native
+native multi-threaded decoder csrc/mp3.cpp, gapless-trimmed by the LAME tag as ffmpeg trims it; Layers I / II too), AAC-LC (native
 decoder csrc/aac.cpp) in ADTS or in an MP4 / M4A track (demuxed here: stsz / stsc / stco, trimmed by the edit list;
 an MP4's MP3 track goes to the MP3 decoder), RIFF/WAVE (PCM 8/16/24/32-bit, IEEE float 32/64, G.711 A-law / mu-law, IMA
 ADPCM), Sun AU and AIFF / AIFF-C (PCM, float, G.711) — the telephony codecs through native decoders
@@ -173,9 +173,9 @@ def mp3_probe(data: bytes):
 
 
 def decode_mp3(data: bytes, threads: int = 0) -> Tuple[np.ndarray, int]:
-    """MP3 bytes -> f32 [frames, channels] through the native Layer III decoder (csrc/mp3.cpp; the Xing / Info frame
-    skipped, the LAME tag's delay + 529 samples dropped at the start and its padding - 529 at the end, as ffmpeg's mp3
-    demuxer does)."""
+    """MP3 (or MPEG audio Layer I / II) bytes -> f32 [frames, channels] through the native decoder (csrc/mp3.cpp; for
+    Layer III the Xing / Info frame skipped, the LAME tag's delay + 529 samples dropped at the start and its
+    padding - 529 at the end, as ffmpeg's mp3 demuxer does)."""
     _lib, lib = _flac_lib()
     info = mp3_probe(data)
     total, ch, sr = int(info.total_samples), int(info.channels), int(info.sample_rate)
@@ -619,7 +619,8 @@ def _id3v2_end(data: bytes) -> int:
 
 
 def _mpeg_audio_name(data: bytes) -> Optional[str]:
-    """MPEG audio frames (after any ID3v2 tags): Layer III is decoded; Layer I / II and ADTS AAC are named."""
+    """MPEG audio frames (after any ID3v2 tags): Layers I, II and III (all decoded by csrc/mp3.cpp, as ffmpeg's mp3
+    demuxer takes every layer), or ADTS AAC."""
     pos = _id3v2_end(data)
     h = data[pos: pos + 2]
     if len(h) == 2 and h[0] == 0xFF and (h[1] & 0xE0) == 0xE0:
@@ -660,9 +661,10 @@ def container_name(data: bytes) -> Optional[str]:
 
 
 _DECODERS = {"WAV": decode_wav, "AU": decode_au, "AIFF": decode_aiff, "Ogg Vorbis": decode_vorbis, "MP3": decode_mp3,
-             "AAC (ADTS)": decode_aac_adts, "MP4/M4A": decode_mp4}
-DECODED = "FLAC, Ogg Vorbis, MP3 (MPEG-1 / 2 / 2.5 Layer III), AAC-LC (M4A / MP4, ADTS), WAV / RIFX / RF64 (PCM, " \
-          "float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C"
+             "MPEG audio Layer II": decode_mp3, "MPEG audio Layer I": decode_mp3, "AAC (ADTS)": decode_aac_adts,
+             "MP4/M4A": decode_mp4}
+DECODED = "FLAC, Ogg Vorbis, MP3 / MPEG audio (MPEG-1 / 2 / 2.5 Layers I, II, III), AAC-LC (M4A / MP4, ADTS), WAV / " \
+          "RIFX / RF64 (PCM, float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C"
 
 
 def decode_bytes(data: bytes, sr_out: int = TARGET_SR, device=None) -> np.ndarray:
