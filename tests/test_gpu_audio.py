@@ -1,6 +1,6 @@
 """Audio ingest on the MI355X: the GPU resampler (tw_resample_pcm_*) against the oracle's float64 restatement of
-libswresample's default filter, and FLAC / Ogg Vorbis / MP3 / AAC (M4A, ADTS) files through the full product path (host decode -> GPU resample ->
-transcription). Tolerance: 2e-6 absolute on [-1, 1] signals (float32 accumulation of <= 396 taps)."""
+libswresample's default filter, and FLAC / Ogg Vorbis / MP3 (and MPEG Layers I / II) / AAC (M4A, ADTS) files through
+the full product path (host decode -> GPU resample -> transcription). Tolerance: 2e-6 absolute on [-1, 1] signals (float32 accumulation of <= 396 taps)."""
 import numpy as np
 import pytest
 import torch
@@ -103,6 +103,35 @@ def test_mp3_bytes_through_load_input():
         c = float(m[:n] @ v / np.sqrt((m[:n] @ m[:n]) * (v @ v)))
         assert len(m) == -(-23087 * 16000 // 44100) and c >= 0.95, c
         print(f"mp3 vs vorbis at 16 kHz: correlation {c:.8f}")
+
+
+def test_mpeg_layer1_layer2_bytes_through_load_input():
+    """MPEG audio Layers I / II (host decode) -> GPU downmix + resample: random-syntax streams against the oracle's
+    float64 decoder + resampler, and the signal pin at 16 kHz — the test-side Annex C encoder's two-tone 48 kHz
+    signal (tests/test_audio_mpeg_l12.py) comes out of the ingest as the float64 resampling of that signal delayed by
+    the filter bank's 481 samples, to the bank's design error."""
+    from oracle import mp3_oracle as mo
+    from test_audio_mpeg_l12 import _encode
+
+    for layer, version, sr_sub in ((2, 1, 0), (1, 1, 1), (2, 2, 1)):
+        data = mo.write_stream_l12(np.random.default_rng(layer * 10 + version), layer=layer, version=version,
+                                   sr_sub=sr_sub, mode=1, bri=12, nframes=6)
+        x, sr, _ = mo.decode(data)
+        got = audio.load_input(data)
+        ref = ao.swr_resample(x.astype(np.float64).mean(axis=1), sr, 16000)
+        scale = max(1.0, float(np.abs(ref).max()))
+        assert got.shape == ref.shape and np.abs(got - ref).max() < TOL * scale
+    n = 48000 // 2
+    t = np.arange(n) / 48000.0
+    mono = 0.4 * np.sin(2 * np.pi * 440 * t) + 0.25 * np.sin(2 * np.pi * 2500 * t + 0.3)
+    for layer in (1, 2):
+        data = _encode(np.stack([mono, 0.5 * mono], axis=1), layer)
+        got = audio.load_input(data).astype(np.float64)
+        m = len(got) * 3
+        ref = ao.swr_resample(np.concatenate([np.zeros(481), 0.75 * mono])[:m], 48000, 16000)
+        mid = slice(1000, len(got) - 1000)
+        err = np.abs(got[mid] - ref[mid]).max()
+        assert got.shape == ref.shape and err < 3e-4 * np.abs(ref).max(), (layer, err)
 
 
 def test_mp3_file_through_process_audio(tmp_path):
