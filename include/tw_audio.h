@@ -11,6 +11,8 @@
  *                                    bit-exact PCM (checked against the stream's own STREAMINFO MD5)
  *   tw_g711_decode                   G.711 mu-law / A-law expansion (WAV, AU, AIFF-C telephony codecs)
  *   tw_ima_adpcm_wav_decode          IMA ADPCM in WAV blocks
+ *   tw_ms_adpcm_wav_decode           Microsoft ADPCM in WAV blocks
+ *   tw_ima_qt_decode                 Apple IMA4 (AIFF-C 'ima4')
  *   tw_vorbis_probe / tw_vorbis_decode  Ogg Vorbis I (floor 1, residues 0/1/2, coupling, IMDCT, overlap-add)
  *   tw_mp3_probe / tw_mp3_decode     MPEG-1 / MPEG-2 LSF / MPEG-2.5 Layer III (MP3), gapless-trimmed by the
  *                                    LAME tag as ffmpeg's mp3 demuxer trims it, and Layers I / II
@@ -73,6 +75,20 @@ int tw_g711_decode(const uint8_t* in, int64_t n, int32_t alaw, int16_t* out);
  * interleaved (HOST); *frames_decoded receives the frames written (1 + 8 * whole words per channel per block). */
 int tw_ima_adpcm_wav_decode(const uint8_t* data, int64_t size, int32_t channels, int32_t block_align, int16_t* out,
                             int64_t out_frames, int64_t* frames_decoded);
+
+/* Microsoft ADPCM in WAV blocks (format tag 2; ffmpeg's adpcm_ms), 1 or 2 channels: per block the channels'
+ * predictor indices (u8, the standard seven coefficient pairs), s16 deltas, s16 sample1 and s16 sample2, then two
+ * nibbles per byte, high first. A block of L bytes gives (L - 6 channels) * 2 / channels frames (the last may be
+ * shorter); a block naming a predictor index > 6 is dropped, as ffmpeg drops a packet it cannot decode. out =
+ * int16[out_frames][channels] interleaved (HOST). */
+int tw_ms_adpcm_wav_decode(const uint8_t* data, int64_t size, int32_t channels, int32_t block_align, int16_t* out,
+                           int64_t out_frames, int64_t* frames_decoded);
+
+/* Apple IMA4 (AIFF-C / QuickTime 'ima4'; ffmpeg's adpcm_ima_qt): packets of 34 bytes per channel, 64 frames each;
+ * a channel's IMA state carries over a packet boundary as ffmpeg carries it (same step index, predictor within
+ * 0x7f), otherwise the packet header resets it. out = int16[out_frames][channels] interleaved (HOST). */
+int tw_ima_qt_decode(const uint8_t* data, int64_t size, int32_t channels, int16_t* out, int64_t out_frames,
+                     int64_t* frames_decoded);
 
 typedef struct TwVorbisInfo {
   int32_t sample_rate;   /* Hz (identification header)                                            */

@@ -18,6 +18,13 @@ What it restates, and what pins it:
   decorrelation modes, CRC-8/CRC-16). It exists to produce streams that exercise every decoder path; the native
   decoder must return the encoder's input PCM exactly. Real-encoder parity is pinned separately by
   examples/Test1/ChrisAndAlexDiTest.flac (libFLAC 1.4.2): its STREAMINFO MD5 must match the decoded PCM.
+
+* `ms_adpcm_decode` / `ms_adpcm_encode` — Microsoft ADPCM (WAV format tag 2) as ffmpeg's adpcm_ms decodes it
+  (ffmpeg 6.x libavcodec/adpcm.c, absent from this image; restated from Microsoft's published algorithm and that
+  decoder's documented behaviour: the standard seven coefficient pairs, a predictor index > 6 drops the block), per
+  nibble in pure Python; and a greedy encoder whose streams exercise every nibble, the delta floor and the s16 clamp.
+  No MS ADPCM file or decoder exists in this image: parity against ffmpeg is UNPINNED; the encoder round trip pins
+  the semantics (a wrong sign, order or coefficient scale breaks the reconstruction of its input).
 """
 from __future__ import annotations
 
@@ -334,3 +341,87 @@ def flac_encode(pcm: np.ndarray, sample_rate: int, bps: int, blocksizes: Sequenc
     streaminfo = si.bytes() + md5.digest()
     meta = bytes([0x80 | 0]) + len(streaminfo).to_bytes(3, "big") + streaminfo
     return b"fLaC" + meta + b"".join(frames)
+
+
+# ---------------------------------------------------------------------------------------------- MS ADPCM
+MS_COEF = [(256, 0), (512, -256), (0, 0), (192, 64), (240, 0), (460, -208), (392, -232)]
+MS_ADAPT = [230, 230, 230, 230, 307, 409, 512, 614, 768, 614, 512, 409, 307, 230, 230, 230]
+
+
+def _c_div(a: int, b: int) -> int:
+    """C integer division (truncation toward zero)."""
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b >= 0) else -q
+
+
+def _ms_nibble(st: list, nib: int) -> int:
+    """st = [coef1, coef2, delta, sample1, sample2] updated in place; returns the new sample."""
+    c1, c2, delta, s1, s2 = st
+    pred = _c_div(s1 * c1 + s2 * c2, 256) + (nib - 16 if nib & 8 else nib) * delta
+    pred = max(-32768, min(32767, pred))
+    delta = max(16, (MS_ADAPT[nib] * delta) >> 8)
+    st[:] = [c1, c2, min(delta, 2147483647 // 768), pred, s1]
+    return pred
+
+
+def ms_adpcm_decode(payload: bytes, ch: int, align: int) -> np.ndarray:
+    """WAV MS ADPCM blocks -> int16 [frames, ch] (1 or 2 channels)."""
+    out = []
+    for pos in range(0, len(payload), align):
+        blk = payload[pos: pos + align]
+        if len(blk) < 7 * ch:
+            break
+        if any(blk[c] > 6 for c in range(ch)):
+            continue
+        nb = (len(blk) - 6 * ch) * 2 // ch
+        sts = []
+        for c in range(ch):
+            c1, c2 = MS_COEF[blk[c]]
+            delta = int.from_bytes(blk[ch + 2 * c: ch + 2 * c + 2], "little", signed=True)
+            s1 = int.from_bytes(blk[3 * ch + 2 * c: 3 * ch + 2 * c + 2], "little", signed=True)
+            s2 = int.from_bytes(blk[5 * ch + 2 * c: 5 * ch + 2 * c + 2], "little", signed=True)
+            sts.append([c1, c2, delta, s1, s2])
+        rows = [[st[4] for st in sts], [st[3] for st in sts]]
+        flat = []
+        nbytes = (nb - 2) // 2 if ch == 1 else nb - 2
+        for byte in blk[7 * ch: 7 * ch + nbytes]:
+            flat.append(_ms_nibble(sts[0], byte >> 4))
+            flat.append(_ms_nibble(sts[ch - 1], byte & 15))
+        rows += [flat[i: i + ch] for i in range(0, len(flat), ch)]
+        out += rows[:nb]
+    return np.array(out, np.int16).reshape(-1, ch)
+
+
+def ms_adpcm_encode(x: np.ndarray, ch: int, align: int, rng: np.random.Generator, predictors=None) -> bytes:
+    """int16 [frames, ch] -> MS ADPCM blocks: per block and channel a predictor index (given, or random), an initial
+    delta, the first two samples verbatim, then per sample the nibble whose decoded value is nearest the input
+    (searching all 16, so the decoder's own update is what follows)."""
+    per = (align - 6 * ch) * 2 // ch
+    out = bytearray()
+    for b0 in range(0, len(x), per):
+        seg = x[b0: b0 + per]
+        if len(seg) < 2:
+            break
+        pidx = [int(rng.integers(0, 7)) if predictors is None else predictors[c] for c in range(ch)]
+        sts = [[*MS_COEF[pidx[c]], int(rng.integers(16, 512)), int(seg[1, c]), int(seg[0, c])] for c in range(ch)]
+        hdr = bytes(pidx)
+        hdr += b"".join(int(sts[c][2]).to_bytes(2, "little", signed=True) for c in range(ch))
+        hdr += b"".join(int(seg[1, c]).to_bytes(2, "little", signed=True) for c in range(ch))
+        hdr += b"".join(int(seg[0, c]).to_bytes(2, "little", signed=True) for c in range(ch))
+        nibs = []
+        for i in range(2, len(seg)):
+            for c in range(ch):
+                best = None
+                for nib in range(16):
+                    trial = list(sts[c])
+                    v = _ms_nibble(trial, nib)
+                    e = abs(v - int(seg[i, c]))
+                    if best is None or e < best[0]:
+                        best = (e, nib, trial)
+                nibs.append(best[1])
+                sts[c] = best[2]
+        if len(nibs) % 2:
+            nibs.append(0)
+        body = bytes((nibs[i] << 4) | nibs[i + 1] for i in range(0, len(nibs), 2))
+        out += hdr + body
+    return bytes(out)

@@ -59,7 +59,7 @@ static void run_all(const std::vector<uint8_t>& buf) {
         if (tw_vorbis_decode(d, n, out.data(), info.total_samples, th, &got) == 0) ++g_ok;
     }
   }
-  {  // MP3 (Layer III)
+  {  // MP3 / MPEG audio (Layers I, II, III)
     TwMp3Info info;
     if (tw_mp3_probe(d, n, &info) == 0 && info.channels > 0 && info.total_samples >= 0 &&
         info.total_samples < (1 << 22)) {
@@ -101,7 +101,16 @@ static void run_all(const std::vector<uint8_t>& buf) {
         std::vector<int16_t> o((size_t)cap * ch);
         int64_t got = 0;
         if (tw_ima_adpcm_wav_decode(d, n, ch, ba, o.data(), cap, &got) == 0) ++g_ok;
+        const int64_t mcap = (n / ba + 1) * (int64_t)((ba - 6 * ch) * 2 / ch);  // MS ADPCM, as twamd sizes it
+        std::vector<int16_t> m((size_t)std::max<int64_t>(mcap, 1) * ch);
+        if (tw_ms_adpcm_wav_decode(d, n, ch, ba, m.data(), mcap, &got) == 0) ++g_ok;
       }
+    for (int ch : {1, 2, 5}) {  // Apple IMA4 packets
+      const int64_t cap = n / (34 * ch) * 64;
+      std::vector<int16_t> o((size_t)std::max<int64_t>(cap, 1) * ch);
+      int64_t got = 0;
+      if (tw_ima_qt_decode(d, n, ch, o.data(), cap, &got) == 0) ++g_ok;
+    }
   }
 }
 

@@ -2,8 +2,8 @@
 
 POST /api/transcribe stores any upload and the pipeline decodes it (/root/reference/vocalis/api/main.py:67-75;
 ffmpeg_read, $TF/pipelines/audio_utils.py:9-45); here the FLAC, Ogg Vorbis, G.711 and IMA ADPCM decoders do that in
-host C++ (csrc/flac.cpp, vorbis.cpp, pcm_codecs.cpp, mp3.cpp, aac.cpp). `make sanitize` builds them with -fsanitize=address,undefined
-and -fno-sanitize-recover into tests/fuzz/codec_fuzz.cpp, which runs probe + decode over every corpus file and
+host C++ (csrc/flac.cpp, vorbis.cpp, pcm_codecs.cpp incl. MS ADPCM and IMA4, mp3.cpp, aac.cpp). `make sanitize` builds
+them with -fsanitize=address,undefined and -fno-sanitize-recover into tests/fuzz/codec_fuzz.cpp, which runs probe + decode over every corpus file and
 hundreds of damaged copies of each (truncations, bit flips, overwritten runs, duplicated chunks, random tails). Any
 out-of-bounds access, leak or undefined behaviour aborts the run. The corpus: the oracle's FLAC writer over every
 subframe kind / stereo mode / bit depth / blocking, its random-syntax Vorbis writer, the image's one libVorbis
@@ -76,6 +76,8 @@ def _corpus(tmp_path):
     if os.path.exists(REF_FLAC):
         put("ref_prefix.flac", open(REF_FLAC, "rb").read()[: 256 * 1024])
     put("adpcm_like.bin", rng.integers(0, 256, size=4096, dtype=np.uint8))
+    tone = np.round(9000 * np.sin(np.arange(3000) / 7.0)).astype(np.int16)
+    put("ms_adpcm.bin", ao.ms_adpcm_encode(np.stack([tone, tone[::-1]], 1), 2, 256, np.random.default_rng(2)))
     return files
 
 

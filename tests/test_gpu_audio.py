@@ -294,10 +294,11 @@ def test_ogg_file_through_process_audio(tmp_path):
     assert res["text"] == ref["text"]
 
 
-@pytest.mark.parametrize("kind", ["wav_ulaw", "wav_ima", "au_alaw", "aifc_ulaw"])
+@pytest.mark.parametrize("kind", ["wav_ulaw", "wav_ima", "au_alaw", "aifc_ulaw", "wav_msadpcm", "aifc_ima4"])
 def test_telephony_files_through_load_input(kind):
-    """8 kHz call recordings (G.711 / IMA ADPCM) through the product path: native host decode, then the GPU resampler
-    to 16 kHz, against the oracle resampler applied to the stdlib (audioop) decode of the same bytes."""
+    """8 kHz call recordings (G.711 / IMA / MS ADPCM, Apple IMA4) through the product path: native host decode, then
+    the GPU resampler to 16 kHz, against the oracle resampler applied to the stdlib (audioop) decode of the same
+    bytes (MS ADPCM: the oracle's decode, tests/test_audio_adpcm_mpeg_wav.py)."""
     import audioop
     import struct
 
@@ -316,6 +317,30 @@ def test_telephony_files_through_load_input(kind):
         data = b"RIFF" + struct.pack("<I", 4 + 8 + len(fmt) + 8 + len(payload)) + b"WAVEfmt " + \
             struct.pack("<I", len(fmt)) + fmt + b"data" + struct.pack("<I", len(payload)) + bytes(payload)
         ref_lin = audio.decode_wav(data)[0][:, 0].astype(np.float64)  # checked against audioop in test_audio_codecs
+    elif kind == "wav_msadpcm":
+        s16 = np.frombuffer(lin, "<i2")[:, None]
+        payload = ao.ms_adpcm_encode(s16, 1, 256, np.random.default_rng(5), predictors=[0])
+        coefs = b"".join(struct.pack("<hh", a, b) for a, b in ao.MS_COEF)
+        fmt = struct.pack("<HHIIHH", 2, 1, 8000, 4096, 256, 4) + struct.pack("<HHH", 4 + len(coefs), 500, 7) + coefs
+        data = b"RIFF" + struct.pack("<I", 4 + 8 + len(fmt) + 8 + len(payload)) + b"WAVEfmt " + \
+            struct.pack("<I", len(fmt)) + fmt + b"data" + struct.pack("<I", len(payload)) + payload
+        ref_lin = ao.ms_adpcm_decode(payload, 1, 256)[:, 0] / 32768.0
+    elif kind == "aifc_ima4":
+        # an IMA4 encoder: audioop codes each 64-sample packet from the running state, which the packet header
+        # restates (so the decoder carries its exact state over, as ffmpeg's adpcm_ima_qt does)
+        s16 = np.frombuffer(lin, "<i2")
+        payload, state = bytearray(), (0, 0)
+        for i in range(0, len(s16) - 63, 64):
+            codes, nxt = audioop.lin2adpcm(s16[i: i + 64].tobytes(), 2, state)
+            payload += struct.pack(">h", (state[0] & ~0x7F) | state[1])
+            payload += bytes(((b & 0x0F) << 4) | (b >> 4) for b in codes)
+            state = nxt
+        comm = struct.pack(">hIh", 1, len(payload) // 34, 16) + struct.pack(">H", 16383 + 15) + \
+            struct.pack(">Q", 8000 << 48) + b"ima4\x00\x00"
+        body = b"COMM" + struct.pack(">I", len(comm)) + comm + b"SSND" + struct.pack(">I", 8 + len(payload)) + \
+            bytes(8) + bytes(payload)
+        data = b"FORM" + struct.pack(">I", 4 + len(body)) + b"AIFC" + body
+        ref_lin = audio.decode_aiff(data)[0][:, 0].astype(np.float64)  # checked against audioop on the CPU
     else:
         alaw = kind == "au_alaw"
         codes = audioop.lin2alaw(lin, 2) if alaw else audioop.lin2ulaw(lin, 2)

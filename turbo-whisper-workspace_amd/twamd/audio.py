@@ -429,6 +429,41 @@ def ima_adpcm_wav_decode(data: bytes, channels: int, block_align: int) -> np.nda
     return out[: got.value]
 
 
+def ms_adpcm_wav_decode(data: bytes, channels: int, block_align: int) -> np.ndarray:
+    """Microsoft ADPCM blocks (WAV format tag 2) -> int16 [frames, channels] (native tw_ms_adpcm_wav_decode;
+    ffmpeg's adpcm_ms)."""
+    _lib, lib = _flac_lib()
+    if channels not in (1, 2) or block_align < 7 * channels:
+        raise ValueError(f"MS ADPCM with {channels} channels, block_align {block_align} (1-2 channels, >= 7 each)")
+    cap = (len(data) // block_align + 1) * ((block_align - 6 * channels) * 2 // channels)
+    if cap > max_audio_seconds() * 192000:
+        raise ValueError("MS ADPCM stream longer than TW_MAX_AUDIO_S")
+    out = np.zeros((cap, channels), np.int16)
+    got = ctypes.c_int64()
+    src = np.frombuffer(data, np.uint8)
+    if lib.tw_ms_adpcm_wav_decode(src.ctypes.data, len(src), channels, block_align, out.ctypes.data, cap,
+                                  ctypes.byref(got)) != 0:
+        raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    return out[: got.value]
+
+
+def ima_qt_decode(data: bytes, channels: int) -> np.ndarray:
+    """Apple IMA4 packets (AIFF-C 'ima4') -> int16 [frames, channels] (native tw_ima_qt_decode; ffmpeg's
+    adpcm_ima_qt)."""
+    _lib, lib = _flac_lib()
+    if not 1 <= channels <= 8:
+        raise ValueError(f"IMA4 with {channels} channels (1-8 supported)")
+    cap = len(data) // (34 * channels) * 64
+    if cap > max_audio_seconds() * 192000:
+        raise ValueError("IMA4 stream longer than TW_MAX_AUDIO_S")
+    out = np.zeros((cap, channels), np.int16)
+    got = ctypes.c_int64()
+    src = np.frombuffer(data, np.uint8)
+    if lib.tw_ima_qt_decode(src.ctypes.data, len(src), channels, out.ctypes.data, cap, ctypes.byref(got)) != 0:
+        raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    return out[: got.value]
+
+
 def _pcm_to_float(raw: bytes, bits: int, big_endian: bool = False, unsigned8: bool = True) -> np.ndarray:
     """Integer PCM -> float32 in [-1, 1) the way ffmpeg's s8/s16/s24/s32/s64 -> flt conversion scales
     (2^-(bits-1))."""
@@ -463,8 +498,9 @@ def decode_wav(data: bytes) -> Tuple[np.ndarray, int]:
     (libavformat/wavdec.c): "RIFF" little-endian, "RIFX" big-endian, "RF64" with its ds64 chunk's 64-bit data size.
     Format tags: 1 PCM in 1 / 2 / 3 / 4 / 8-byte containers (bits per sample rounded up to whole bytes, as
     ff_get_pcm_codec_id maps them: a 20-bit stream is s24, a 12-bit one s16, a 5-bit one u8; 5-7-byte containers are
-    refused, as ffmpeg refuses them), 3 IEEE float 32 / 64, 6 A-law, 7 mu-law, 0x11 IMA ADPCM, and
-    WAVE_FORMAT_EXTENSIBLE carrying any of them. A data chunk that runs past the end of the bytes is read up to it."""
+    refused, as ffmpeg refuses them), 3 IEEE float 32 / 64, 6 A-law, 7 mu-law, 0x11 IMA ADPCM, 2 Microsoft ADPCM,
+    0x55 MP3 and 0x50 MPEG Layer I / II (the data chunk through the MPEG audio decoder), and WAVE_FORMAT_EXTENSIBLE
+    carrying any of them. A data chunk that runs past the end of the bytes is read up to it."""
     if len(data) < 12 or data[:4] not in (b"RIFF", b"RIFX", b"RF64") or data[8:12] != b"WAVE":
         raise ValueError("not a RIFF/WAVE stream")
     be = data[:4] == b"RIFX"
@@ -511,6 +547,10 @@ def decode_wav(data: bytes) -> Tuple[np.ndarray, int]:
         if bits != 4:
             raise ValueError(f"IMA ADPCM with {bits} bits per sample (4 supported)")
         return ima_adpcm_wav_decode(pcm, ch, align).astype(np.float32) / 32768.0, sr
+    elif tag == 2:
+        return ms_adpcm_wav_decode(pcm, ch, align).astype(np.float32) / 32768.0, sr
+    elif tag in (0x50, 0x55):  # MPEG audio in a WAV wrapper: the stream's own headers give rate and channels
+        return decode_mp3(bytes(pcm))
     else:
         raise ValueError(f"unsupported WAVE format tag {tag}")
     return _frames(x, ch), sr
@@ -551,7 +591,7 @@ def _ieee_extended(b: bytes) -> float:
 
 def decode_aiff(data: bytes) -> Tuple[np.ndarray, int]:
     """AIFF / AIFF-C bytes -> (float32 [frames, channels], sample_rate). Compression types: NONE / twos (big-endian
-    PCM), sowt (little-endian PCM), fl32 / fl64, ulaw, alaw (ffmpeg's aiff demuxer)."""
+    PCM), sowt (little-endian PCM), fl32 / fl64, ulaw, alaw, ima4 (Apple IMA ADPCM) (ffmpeg's aiff demuxer)."""
     if len(data) < 12 or data[:4] != b"FORM" or data[8:12] not in (b"AIFF", b"AIFC"):
         raise ValueError("not an AIFF stream")
     aifc = data[8:12] == b"AIFC"
@@ -583,6 +623,8 @@ def decode_aiff(data: bytes) -> Tuple[np.ndarray, int]:
         x = np.frombuffer(ssnd[: len(ssnd) // 8 * 8], ">f8").astype(np.float32)
     elif ctype in (b"ulaw", b"ULAW", b"alaw", b"ALAW"):
         x = g711_decode(ssnd, alaw=ctype.lower() == b"alaw").astype(np.float32) / 32768.0
+    elif ctype == b"ima4":  # every whole 34-byte-per-channel packet of SSND, as ffmpeg's demuxer hands them over
+        return ima_qt_decode(ssnd, ch).astype(np.float32) / 32768.0, int(round(sr))
     else:
         raise ValueError(f"unsupported AIFF-C compression {ctype!r}")
     fr = _frames(x, ch)
@@ -664,7 +706,7 @@ _DECODERS = {"WAV": decode_wav, "AU": decode_au, "AIFF": decode_aiff, "Ogg Vorbi
              "MPEG audio Layer II": decode_mp3, "MPEG audio Layer I": decode_mp3, "AAC (ADTS)": decode_aac_adts,
              "MP4/M4A": decode_mp4}
 DECODED = "FLAC, Ogg Vorbis, MP3 / MPEG audio (MPEG-1 / 2 / 2.5 Layers I, II, III), AAC-LC (M4A / MP4, ADTS), WAV / " \
-          "RIFX / RF64 (PCM, float, A-law, mu-law, IMA ADPCM), AU, AIFF / AIFF-C"
+          "RIFX / RF64 (PCM, float, A-law, mu-law, IMA / MS ADPCM, MPEG), AU, AIFF / AIFF-C"
 
 
 def decode_bytes(data: bytes, sr_out: int = TARGET_SR, device=None) -> np.ndarray:
