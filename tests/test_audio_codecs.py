@@ -256,8 +256,8 @@ def test_containers_are_recognised_and_dispatched():
     x = audio.decode_bytes(wav)
     mono = (_s16(audioop.ulaw2lin(bytes([0xFF, 0x7F]), 2)).astype(np.float32) / 32768.0).reshape(1, 2)
     np.testing.assert_array_equal(x, np.repeat(mono.mean(axis=1, dtype=np.float32), 10))
-    with pytest.raises(ValueError, match="unsupported WAVE format tag 85"):
-        audio.decode_wav(_wav_bytes(85, 1, 8000, 0, 1, bytes(8)))
+    with pytest.raises(ValueError, match="unsupported WAVE format tag 49"):  # GSM 6.10
+        audio.decode_wav(_wav_bytes(49, 1, 8000, 0, 65, bytes(65)))
 
 
 def test_duration_of_telephony_files(tmp_path):

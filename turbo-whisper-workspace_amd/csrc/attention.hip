@@ -1031,7 +1031,7 @@ static int tw_debug_tab_guard(const int* kv_tab, const int* pos, int row0, int B
   static int* d_bad = nullptr;
   static int cap = 0;
   if (cap < B) {
-    if (d_bad) hipFree(d_bad);
+    if (d_bad) (void)hipFree(d_bad);
     cap = 0;
     if (hipMalloc(&d_bad, sizeof(int) * B) != hipSuccess) {
       d_bad = nullptr;

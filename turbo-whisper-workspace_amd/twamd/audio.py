@@ -763,7 +763,7 @@ def duration_seconds(path: str) -> float:
     if name == "Ogg Vorbis":
         info = vorbis_probe(data)
         return int(info.total_samples) / float(info.sample_rate)
-    if name == "MP3":
+    if name in ("MP3", "MPEG audio Layer II", "MPEG audio Layer I"):
         info = mp3_probe(data)
         return int(info.total_samples) / float(info.sample_rate)
     if name == "AAC (ADTS)":
