@@ -17,6 +17,7 @@
  *   tw_mp3_probe / tw_mp3_decode     MPEG-1 / MPEG-2 LSF / MPEG-2.5 Layer III (MP3), gapless-trimmed by the
  *                                    LAME tag as ffmpeg's mp3 demuxer trims it, and Layers I / II
  *   tw_aac_*                         MPEG-4 AAC-LC: ADTS streams, and the raw access units of an MP4 / M4A track
+ *   tw_alac_*                        Apple Lossless access units of an MP4 / M4A track
  *                                    (the container is demuxed by the caller, twamd/audio.py)
  *   tw_resample_pcm_i32 / _f32       downmix + polyphase resample on the GPU (DEVICE memory, `stream`), the
  *                                    libswresample default filter restated (Kaiser-windowed sinc, see
@@ -89,6 +90,27 @@ int tw_ms_adpcm_wav_decode(const uint8_t* data, int64_t size, int32_t channels, 
  * 0x7f), otherwise the packet header resets it. out = int16[out_frames][channels] interleaved (HOST). */
 int tw_ima_qt_decode(const uint8_t* data, int64_t size, int32_t channels, int16_t* out, int64_t out_frames,
                      int64_t* frames_decoded);
+
+typedef struct TwAlacInfo {
+  int32_t sample_rate;   /* Hz (ALACSpecificConfig)                                                    */
+  int32_t channels;      /* 1 or 2 (other layouts are refused)                                          */
+  int32_t bit_depth;     /* 16, 20, 24 or 32                                                            */
+  int32_t frame_length;  /* samples per full frame (4096 from Apple's encoder)                          */
+  int32_t pb, mb, kb;    /* Rice history multiplier, initial history, parameter limit                   */
+} TwAlacInfo;
+
+/* Apple Lossless (ALAC) in an MP4 / M4A track (HOST memory; ffmpeg's alac decoder): `cookie` is the track's
+ * ALACSpecificConfig (24 bytes, or the 36-byte 'alac' atom holding it). */
+int tw_alac_parse_cookie(const uint8_t* cookie, int64_t size, TwAlacInfo* info);
+
+/* Decode the n_packets access units at data + offsets[k] (sizes[k] bytes each; the caller demuxes the container)
+ * into out = f32[out_frames][channels], interleaved, sample / 2^(bit_depth - 1). A packet whose first element
+ * header is invalid, or that the decoder refuses, contributes no samples (ffmpeg drops it). Packets decode on
+ * n_threads threads (<= 0: hardware concurrency); frames are independent, so the output does not depend on it.
+ * *frames_decoded receives the frames written. */
+int tw_alac_decode(const uint8_t* cookie, int64_t cookie_size, const uint8_t* data, int64_t size,
+                   const int64_t* offsets, const int64_t* sizes, int64_t n_packets, float* out, int64_t out_frames,
+                   int32_t n_threads, int64_t* frames_decoded);
 
 typedef struct TwVorbisInfo {
   int32_t sample_rate;   /* Hz (identification header)                                            */

@@ -91,6 +91,24 @@ static void run_all(const std::vector<uint8_t>& buf) {
           ++g_ok;
       }
   }
+  {  // ALAC: the bytes as access units of a few fixed sizes under mono / stereo, 16 / 24-bit configs
+    const uint8_t base[24] = {0, 0, 16, 0, 0, 16, 40, 10, 14, 1, 0, 255, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 172, 68};
+    for (int v = 0; v < 3; v++) {
+      uint8_t ck[24];
+      memcpy(ck, base, 24);
+      ck[2] = v == 2 ? 4 : 16;                // frame length 4096 or 1024 (big-endian u32 0x00001000 / 0x00000400)
+      ck[5] = v == 1 ? 24 : 16, ck[9] = (uint8_t)(1 + (v & 1));
+      for (int64_t unit : {(int64_t)64, (int64_t)900, (int64_t)3000}) {
+        const int64_t nau = std::min<int64_t>(n / unit, 32);
+        if (nau <= 0) continue;
+        std::vector<int64_t> off(nau), sz(nau);
+        for (int64_t i = 0; i < nau; i++) off[i] = i * unit, sz[i] = unit;
+        std::vector<float> out((size_t)nau * 4096 * 2);
+        int64_t got = 0;
+        if (tw_alac_decode(ck, 24, d, n, off.data(), sz.data(), nau, out.data(), nau * 4096, 1 + v, &got) == 0) ++g_ok;
+      }
+    }
+  }
   {  // G.711 (raw payload) and IMA ADPCM (Microsoft block layout) over the same bytes
     std::vector<int16_t> pcm(buf.size() + 1);
     if (tw_g711_decode(d, n, 0, pcm.data()) == 0) ++g_ok;

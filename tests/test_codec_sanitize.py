@@ -2,7 +2,7 @@
 
 POST /api/transcribe stores any upload and the pipeline decodes it (/root/reference/vocalis/api/main.py:67-75;
 ffmpeg_read, $TF/pipelines/audio_utils.py:9-45); here the FLAC, Ogg Vorbis, G.711 and IMA ADPCM decoders do that in
-host C++ (csrc/flac.cpp, vorbis.cpp, pcm_codecs.cpp incl. MS ADPCM and IMA4, mp3.cpp, aac.cpp). `make sanitize` builds
+host C++ (csrc/flac.cpp, vorbis.cpp, pcm_codecs.cpp incl. MS ADPCM and IMA4, mp3.cpp, aac.cpp, alac.cpp). `make sanitize` builds
 them with -fsanitize=address,undefined and -fno-sanitize-recover into tests/fuzz/codec_fuzz.cpp, which runs probe + decode over every corpus file and
 hundreds of damaged copies of each (truncations, bit flips, overwritten runs, duplicated chunks, random tails). Any
 out-of-bounds access, leak or undefined behaviour aborts the run. The corpus: the oracle's FLAC writer over every
@@ -19,6 +19,7 @@ import pytest
 
 from oracle import audio_oracle as ao
 from oracle import aac_oracle as aao
+from oracle import alac_oracle as alo
 from oracle import mp3_oracle as mo
 from oracle import vorbis_oracle as vo
 
@@ -78,6 +79,10 @@ def _corpus(tmp_path):
     put("adpcm_like.bin", rng.integers(0, 256, size=4096, dtype=np.uint8))
     tone = np.round(9000 * np.sin(np.arange(3000) / 7.0)).astype(np.int16)
     put("ms_adpcm.bin", ao.ms_adpcm_encode(np.stack([tone, tone[::-1]], 1), 2, 256, np.random.default_rng(2)))
+    for seed, (nch, depth) in enumerate(((1, 16), (2, 24))):  # ALAC packets back to back (the driver cuts them up)
+        ck, pk, _ = alo.write_stream(np.random.default_rng(seed), nch=nch, depth=depth, frames=2, frame_length=1024,
+                                     tail=200)
+        put(f"alac{seed}.bin", b"".join(pk))
     return files
 
 

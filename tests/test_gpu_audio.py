@@ -1,5 +1,5 @@
 """Audio ingest on the MI355X: the GPU resampler (tw_resample_pcm_*) against the oracle's float64 restatement of
-libswresample's default filter, and FLAC / Ogg Vorbis / MP3 (and MPEG Layers I / II) / AAC (M4A, ADTS) files through
+libswresample's default filter, and FLAC / Ogg Vorbis / MP3 (and MPEG Layers I / II) / AAC (M4A, ADTS) / ALAC files through
 the full product path (host decode -> GPU resample -> transcription). Tolerance: 2e-6 absolute on [-1, 1] signals (float32 accumulation of <= 396 taps)."""
 import numpy as np
 import pytest
@@ -132,6 +132,20 @@ def test_mpeg_layer1_layer2_bytes_through_load_input():
         mid = slice(1000, len(got) - 1000)
         err = np.abs(got[mid] - ref[mid]).max()
         assert got.shape == ref.shape and err < 3e-4 * np.abs(ref).max(), (layer, err)
+
+
+def test_alac_m4a_bytes_through_load_input():
+    """Apple Lossless in M4A (host decode behind the MP4 demuxer) -> GPU downmix + resample, against the oracle's
+    integer decode (lossless: the encoder's input) through the float64 resampler."""
+    from oracle import alac_oracle as al
+
+    for seed, (nch, depth) in enumerate(((2, 16), (1, 24))):
+        cookie, packets, x = al.write_stream(np.random.default_rng(seed), nch=nch, depth=depth, frames=3,
+                                             frame_length=4096, tail=1234)
+        data = al.write_m4a(cookie, packets, al.parse_cookie(cookie))
+        got = audio.load_input(data)
+        ref = ao.swr_resample(al.to_float(x, depth).astype(np.float64).mean(axis=1), 44100, 16000)
+        assert got.shape == ref.shape and np.abs(got - ref).max() < TOL
 
 
 def test_mp3_file_through_process_audio(tmp_path):

@@ -42,7 +42,7 @@ EXPORTED = (
     "tw_dtw", "tw_attn_decode_cross_probs", "tw_attn_decode_cross_grouped", "tw_attn_decode_cross_grouped_ws_bytes", "tw_attn_decode_self_tab", "tw_beam_workspace_bytes", "tw_beam_step", "tw_kv_reorder", "tw_pack_weight", "tw_gemv_packed", "tw_resid_layernorm_packed", "tw_flac_probe", "tw_flac_decode", "tw_resample_pcm_i32", "tw_resample_pcm_f32",
     "tw_gemm_mx", "tw_quant_mx", "tw_layernorm_mx", "tw_attn_encoder_mx", "tw_gemm_mx_set_variant", "tw_logits_select_embed",
     "tw_attn_set_lds_pad", "tw_logits_sample", "tw_token_prob", "tw_g711_decode", "tw_ima_adpcm_wav_decode",
-    "tw_ms_adpcm_wav_decode", "tw_ima_qt_decode",
+    "tw_ms_adpcm_wav_decode", "tw_ima_qt_decode", "tw_alac_parse_cookie", "tw_alac_decode",
     "tw_kv_tab_check", "tw_debug_build", "tw_resid_layernorm_packed_to", "tw_conv2_gemm",
     "tw_logmel_long", "tw_im2col_conv1_long", "tw_attn_decode_self_masked", "tw_attn_decode_self_tab_masked",
     "tw_gemv_set_wide_slices", "tw_vorbis_probe", "tw_vorbis_decode", "tw_vorbis_imdct",
@@ -98,6 +98,13 @@ class TwMp3Info(ctypes.Structure):
         ("bitrate_kbps", ctypes.c_int32), ("total_samples", ctypes.c_int64), ("n_frames", ctypes.c_int64),
         ("skip_samples", ctypes.c_int64), ("samples_per_frame", ctypes.c_int32), ("enc_delay", ctypes.c_int32),
         ("enc_padding", ctypes.c_int32), ("flags", ctypes.c_int32), ("layer", ctypes.c_int32),
+    ]
+
+
+class TwAlacInfo(ctypes.Structure):
+    _fields_ = [
+        ("sample_rate", ctypes.c_int32), ("channels", ctypes.c_int32), ("bit_depth", ctypes.c_int32),
+        ("frame_length", ctypes.c_int32), ("pb", ctypes.c_int32), ("mb", ctypes.c_int32), ("kb", ctypes.c_int32),
     ]
 
 
@@ -198,6 +205,9 @@ _SIGS = {
     "tw_ima_adpcm_wav_decode": ([_P, ctypes.c_int64, _I, _I, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_ms_adpcm_wav_decode": ([_P, ctypes.c_int64, _I, _I, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_ima_qt_decode": ([_P, ctypes.c_int64, _I, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)], _I),
+    "tw_alac_parse_cookie": ([_P, ctypes.c_int64, _P], _I),
+    "tw_alac_decode": ([_P, ctypes.c_int64, _P, ctypes.c_int64, _P, _P, ctypes.c_int64, _P, ctypes.c_int64, _I,
+                        ctypes.POINTER(ctypes.c_int64)], _I),
     "tw_resample_pcm_i32": ([_P, ctypes.c_int64, _I, _F, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),
     "tw_resample_pcm_f32": ([_P, ctypes.c_int64, _I, _I, _I, _P, _I, _P, ctypes.c_int64, _P], _I),
     "tw_dec_fused": ([_P, _I, _I, _P, _P, _P, _P, _L, _I, _P, _L, _L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _P, _P,

@@ -215,8 +215,8 @@ def decode_aac_adts(data: bytes, threads: int = 0) -> Tuple[np.ndarray, int]:
 
 
 class Mp4Track(NamedTuple):
-    codec: str               # "aac" or "mp3"
-    config: bytes            # AAC AudioSpecificConfig (b"" for MP3)
+    codec: str               # "aac", "mp3" or "alac"
+    config: bytes            # AAC AudioSpecificConfig / ALACSpecificConfig (b"" for MP3)
     sample_rate: int
     channels: int
     offsets: np.ndarray      # int64 byte offset of each access unit in the file
@@ -316,6 +316,10 @@ def mp4_audio_track(data: bytes) -> Mp4Track:
         codec, cfg = None, b""
         if etype in (b".mp3", b"mp3 "):
             codec = "mp3"
+        elif etype == b"alac":  # Apple Lossless: the ALACSpecificConfig in the entry's 'alac' child box
+            for tt, aa, bb in _mp4_boxes(data, child, ea + esize):
+                if tt == b"alac":
+                    codec, cfg = "alac", data[aa + 4: bb]
         elif etype == b"mp4a":
             for tt, aa, bb in _mp4_boxes(data, child, ea + esize):
                 if tt == b"esds":
@@ -367,7 +371,7 @@ def mp4_audio_track(data: bytes) -> Mp4Track:
 
 def decode_mp4(data: bytes, threads: int = 0) -> Tuple[np.ndarray, int]:
     """MP4 / M4A bytes -> f32 [frames, channels]: the first sound track (AAC-LC through tw_aac_decode_raw, MP3 through
-    tw_mp3_decode), trimmed by its first edit (elst media_time skipped, the edit's duration kept), as ffmpeg's mov
+    tw_mp3_decode, Apple Lossless through tw_alac_decode), trimmed by its first edit (elst media_time skipped, the edit's duration kept), as ffmpeg's mov
     demuxer presents it."""
     _lib, lib = _flac_lib()
     tr = mp4_audio_track(data)
@@ -390,8 +394,25 @@ def decode_mp4(data: bytes, threads: int = 0) -> Tuple[np.ndarray, int]:
                                  off.ctypes.data, siz.ctypes.data, n, x.ctypes.data, len(x), int(threads),
                                  ctypes.byref(got)) != 0:
             raise ValueError(lib.tw_last_error().decode(errors="replace"))
+    elif tr.codec == "alac":
+        info = _lib.TwAlacInfo()
+        if lib.tw_alac_parse_cookie(ctypes.c_char_p(tr.config), len(tr.config), ctypes.byref(info)) != 0:
+            raise ValueError(lib.tw_last_error().decode(errors="replace"))
+        sr, ch = int(info.sample_rate) or tr.sample_rate, int(info.channels)
+        cap = n * int(info.frame_length)
+        if cap > max_audio_seconds() * sr:
+            raise ValueError(f"MP4 track longer than TW_MAX_AUDIO_S={max_audio_seconds():g} s")
+        x = np.zeros((cap, ch), np.float32)
+        off = np.ascontiguousarray(tr.offsets, np.int64)
+        siz = np.ascontiguousarray(tr.sizes, np.int64)
+        got = ctypes.c_int64()
+        if lib.tw_alac_decode(ctypes.c_char_p(tr.config), len(tr.config), ctypes.c_char_p(data), len(data),
+                              off.ctypes.data, siz.ctypes.data, n, x.ctypes.data, cap, int(threads),
+                              ctypes.byref(got)) != 0:
+            raise ValueError(lib.tw_last_error().decode(errors="replace"))
+        x = x[: got.value]
     else:
-        raise ValueError(f"MP4 sound track codec {tr.codec} is not decoded (AAC-LC and MP3 are)")
+        raise ValueError(f"MP4 sound track codec {tr.codec} is not decoded (AAC-LC, MP3 and ALAC are)")
     if tr.edit is not None:
         scale = sr / tr.timescale
         skip, keep = int(round(tr.edit[0] * scale)), int(round(tr.edit[1] * scale))
@@ -705,7 +726,7 @@ def container_name(data: bytes) -> Optional[str]:
 _DECODERS = {"WAV": decode_wav, "AU": decode_au, "AIFF": decode_aiff, "Ogg Vorbis": decode_vorbis, "MP3": decode_mp3,
              "MPEG audio Layer II": decode_mp3, "MPEG audio Layer I": decode_mp3, "AAC (ADTS)": decode_aac_adts,
              "MP4/M4A": decode_mp4}
-DECODED = "FLAC, Ogg Vorbis, MP3 / MPEG audio (MPEG-1 / 2 / 2.5 Layers I, II, III), AAC-LC (M4A / MP4, ADTS), WAV / " \
+DECODED = "FLAC, Ogg Vorbis, MP3 / MPEG audio (MPEG-1 / 2 / 2.5 Layers I, II, III), AAC-LC / ALAC (M4A / MP4), AAC (ADTS), WAV / " \
           "RIFX / RF64 (PCM, float, A-law, mu-law, IMA / MS ADPCM, MPEG), AU, AIFF / AIFF-C"
 
 
