@@ -229,6 +229,22 @@ def test_aiff_matches_aifc(comptype, width, aifc_form, ch):
     np.testing.assert_array_equal(x, want.astype(np.float32).reshape(-1, ch))
 
 
+@pytest.mark.parametrize("ctype,width", [(b"in24", 3), (b"in32", 4), (b"raw ", 1)])
+def test_aifc_in24_in32_raw_equal_their_none_twins(ctype, width):
+    """in24 / in32 are big-endian s24 / s32 under their own compression types, 'raw ' is unsigned 8-bit (ffmpeg's
+    aiff tags): each decodes to the samples of the NONE file it was rewritten from."""
+    lin = RNG.integers(0, 256, 301 * 2 * width, dtype=np.uint8).tobytes()
+    none = _aiff(b"NONE", 2, width, lin)
+    data = none.replace(b"NONE", ctype, 1)
+    if ctype == b"raw ":
+        i = data.index(b"SSND") + 16
+        data = data[:i] + bytes(b ^ 0x80 for b in data[i: i + len(lin)]) + data[i + len(lin):]
+    x, sr = audio.decode_aiff(data)
+    y, _ = audio.decode_aiff(none)
+    assert x.shape == (301, 2)
+    np.testing.assert_array_equal(x, y)
+
+
 def test_aiff_float_and_extended_rates():
     for rate in (8000, 11025, 22050, 44100, 48000, 96000):
         ext = aifc._write_float  # noqa: SLF001 - the stdlib's own 80-bit writer pins the reader

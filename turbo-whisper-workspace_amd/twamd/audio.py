@@ -612,7 +612,8 @@ def _ieee_extended(b: bytes) -> float:
 
 def decode_aiff(data: bytes) -> Tuple[np.ndarray, int]:
     """AIFF / AIFF-C bytes -> (float32 [frames, channels], sample_rate). Compression types: NONE / twos (big-endian
-    PCM), sowt (little-endian PCM), fl32 / fl64, ulaw, alaw, ima4 (Apple IMA ADPCM) (ffmpeg's aiff demuxer)."""
+    PCM), sowt (little-endian PCM), in24 / in32, raw (unsigned 8-bit), fl32 / fl64, ulaw, alaw, ima4 (Apple IMA
+    ADPCM) (ffmpeg's aiff demuxer)."""
     if len(data) < 12 or data[:4] != b"FORM" or data[8:12] not in (b"AIFF", b"AIFC"):
         raise ValueError("not an AIFF stream")
     aifc = data[8:12] == b"AIFC"
@@ -638,6 +639,10 @@ def decode_aiff(data: bytes) -> Tuple[np.ndarray, int]:
         x = _pcm_to_float(ssnd, (bits + 7) // 8 * 8, big_endian=True, unsigned8=False)
     elif ctype == b"sowt":
         x = _pcm_to_float(ssnd, (bits + 7) // 8 * 8, big_endian=False, unsigned8=False)
+    elif ctype in (b"in24", b"in32"):  # big-endian s24 / s32 whatever COMM's depth says
+        x = _pcm_to_float(ssnd, 24 if ctype == b"in24" else 32, big_endian=True, unsigned8=False)
+    elif ctype == b"raw ":  # unsigned 8-bit
+        x = _pcm_to_float(ssnd, 8, unsigned8=True)
     elif ctype in (b"fl32", b"FL32"):
         x = np.frombuffer(ssnd[: len(ssnd) // 4 * 4], ">f4").astype(np.float32)
     elif ctype in (b"fl64", b"FL64"):
