@@ -39,13 +39,15 @@ typedef struct TwFlacInfo {
   int32_t bits_per_sample; /* 4..32                                                                    */
   int32_t min_blocksize;   /* samples per channel                                                      */
   int32_t max_blocksize;
-  int32_t reserved;
-  int64_t total_samples;   /* per channel; 0 = unknown (tw_flac_decode then refuses the stream)        */
+  int32_t total_from_frames; /* 1: STREAMINFO's total was 0 (unknown) and total_samples comes from the last frame */
+  int64_t total_samples;   /* per channel; 0 = unknown and no frame found (tw_flac_decode refuses the stream) */
   int64_t audio_offset;    /* byte offset of the first frame                                           */
   uint8_t md5[16];         /* MD5 of the unencoded PCM (interleaved, little-endian, ceil(bps/8) bytes) */
 } TwFlacInfo;
 
-/* Parse the "fLaC" marker and the metadata blocks (STREAMINFO required). HOST memory. */
+/* Parse the "fLaC" marker and the metadata blocks (STREAMINFO required). HOST memory. A STREAMINFO total of 0
+ * (unknown: a stream written to a pipe) is replaced by the last genuine frame's first sample + block size
+ * (total_from_frames = 1), as ffmpeg decodes such a stream to its end. */
 int tw_flac_probe(const uint8_t* data, int64_t size, TwFlacInfo* info);
 
 /* Decode every frame into out = int32[out_frames][channels] (interleaved, HOST memory, sample values as coded,

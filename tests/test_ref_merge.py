@@ -215,6 +215,6 @@ def test_undecodable_upload_reaches_reference_error_convention(layout, tmp_path)
     f.write_bytes(b"OggS\x00\x02" + bytes(22) + b"OpusHead" + bytes(256))
     got = p.transcribe(str(f), "transcribe")
     assert got == {"error": "Transcription error: Ogg Opus audio is not decoded by this engine (decoded containers: "
-                            "FLAC, Ogg Vorbis, MP3 / MPEG audio (MPEG-1 / 2 / 2.5 Layers I, II, III), AAC-LC / ALAC (M4A "
-                            "/ MP4), AAC (ADTS), WAV / RIFX / RF64 (PCM, float, A-law, mu-law, IMA / MS ADPCM, MPEG), AU, "
-                            "AIFF / AIFF-C); convert the upload to one of them"}
+                            "FLAC (native, Ogg), Ogg Vorbis, MP3 / MPEG audio (MPEG-1 / 2 / 2.5 Layers I, II, III), "
+                            "AAC-LC / ALAC (M4A / MP4), AAC (ADTS), WAV / RIFX / RF64 (PCM, float, A-law, mu-law, IMA / "
+                            "MS ADPCM, MPEG), AU, AIFF / AIFF-C); convert the upload to one of them"}

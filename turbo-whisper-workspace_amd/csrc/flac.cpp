@@ -361,6 +361,9 @@ size_t decode_frame(const uint8_t* d, size_t n, size_t pos, const TwFlacInfo& si
   size_t end = b.byte();
   if (end + 2 > n) return 0;
   if (crc16(d + pos, end - pos) != (uint16_t)((d[end] << 8) | d[end + 1])) return 0;
+  *first_sample = h.first_sample;
+  *blocksize = bs;
+  if (!out) return end + 2 - pos;  // (a validating pass: no output)
   int32_t* s0 = scratch.data();
   int32_t* s1 = nch > 1 ? scratch.data() + bs : nullptr;
   int32_t* o = out + h.first_sample * nch;
@@ -384,8 +387,6 @@ size_t decode_frame(const uint8_t* d, size_t n, size_t pos, const TwFlacInfo& si
       o[2 * i + 1] = (int32_t)((mid - s1[i]) >> 1);
     }
   }
-  *first_sample = h.first_sample;
-  *blocksize = bs;
   return end + 2 - pos;
 }
 
@@ -459,6 +460,21 @@ extern "C" int tw_flac_probe(const uint8_t* data, int64_t size, TwFlacInfo* info
     return 1;
   }
   info->audio_offset = (int64_t)pos;
+  if (info->total_samples == 0) {
+    // STREAMINFO leaves the length unknown (a stream written to a pipe): the last genuine frame (sync, CRC-8 and the
+    // CRC-16 of a full decode, searched back from the end) gives it, as its first sample + its block size
+    std::vector<int32_t> scratch;
+    for (size_t p = (size_t)size - 2; p + 1 > pos; p--) {
+      if (data[p] != 0xFF || (data[p + 1] & 0xFE) != 0xF8) continue;
+      int64_t fs;
+      int bsz;
+      if (decode_frame(data, (size_t)size, p, *info, nullptr, INT64_MAX, scratch, &fs, &bsz)) {
+        info->total_samples = fs + bsz;
+        info->total_from_frames = 1;
+        break;
+      }
+    }
+  }
   return 0;
 }
 
@@ -516,6 +532,7 @@ extern "C" int tw_flac_decode(const uint8_t* data, int64_t size, int32_t* out, i
         w[t].next = fs + bsz;
         w[t].decoded = std::max(w[t].decoded, fs + bsz);
         p += len;
+        if (fs + bsz >= total) break;  // the last frame: what follows (an ID3v1 / APE tag, padding) is not audio
       }
       if (p != stop && stop != n) {
         w[t].ok = false;

@@ -80,7 +80,7 @@ class TwBeamState(ctypes.Structure):
 class TwFlacInfo(ctypes.Structure):
     _fields_ = [
         ("sample_rate", ctypes.c_int32), ("channels", ctypes.c_int32), ("bits_per_sample", ctypes.c_int32),
-        ("min_blocksize", ctypes.c_int32), ("max_blocksize", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("min_blocksize", ctypes.c_int32), ("max_blocksize", ctypes.c_int32), ("total_from_frames", ctypes.c_int32),
         ("total_samples", ctypes.c_int64), ("audio_offset", ctypes.c_int64), ("md5", ctypes.c_uint8 * 16),
     ]
 

@@ -23,7 +23,7 @@ import io
 import math
 import os
 import struct
-from typing import NamedTuple, Optional, Tuple, Union
+from typing import List, NamedTuple, Optional, Tuple, Union
 
 import numpy as np
 
@@ -677,6 +677,41 @@ def max_audio_seconds() -> float:
 _UNDECODED = ((b"OggS", "Ogg"), (b"\x1aE\xdf\xa3", "Matroska/WebM"))
 
 
+def _ogg_packets(data: bytes) -> List[bytes]:
+    """The packets of an Ogg file's first logical stream (its pages' segments joined by lacing; other streams'
+    pages skipped), as ffmpeg's ogg demuxer hands them to a decoder."""
+    pos, serial, packets, cur = 0, None, [], b""
+    while pos + 27 <= len(data) and data[pos: pos + 4] == b"OggS":
+        nseg = data[pos + 26]
+        lacing = data[pos + 27: pos + 27 + nseg]
+        sn = struct.unpack("<I", data[pos + 14: pos + 18])[0]
+        serial = sn if serial is None else serial
+        off = pos + 27 + nseg
+        for n in lacing:
+            if sn == serial:
+                cur += data[off: off + n]
+                if n < 255:
+                    packets.append(cur)
+                    cur = b""
+            off += n
+        pos = off
+    return packets
+
+
+def ogg_flac_to_native(data: bytes) -> bytes:
+    """Ogg FLAC (the FLAC-to-Ogg mapping: a first packet "\x7fFLAC" + version + header count + "fLaC" + STREAMINFO,
+    then metadata-block packets, then one FLAC frame per packet) -> the native FLAC stream those bytes carry."""
+    packets = _ogg_packets(data)
+    if not packets or packets[0][:5] != b"\x7fFLAC" or packets[0][9:13] != b"fLaC" or len(packets[0]) < 13 + 38:
+        raise ValueError("Ogg FLAC: no FLAC mapping header")
+    si = bytearray(packets[0][13: 13 + 38])
+    si[0] |= 0x80  # STREAMINFO becomes the last metadata block
+    k = 1
+    while k < len(packets) and packets[k][:1] != b"\xff":  # the metadata-block packets (their count may be 0 = unknown)
+        k += 1
+    return b"fLaC" + bytes(si) + b"".join(packets[k:])
+
+
 def _id3v2_end(data: bytes) -> int:
     pos = 0
     while data[pos: pos + 3] == b"ID3" and pos + 10 <= len(data):
@@ -721,6 +756,8 @@ def container_name(data: bytes) -> Optional[str]:
         head = data[28: 28 + 8]  # the first packet of a one-segment first page (every Ogg codec's header packet)
         if head[:7] == b"\x01vorbis":
             return "Ogg Vorbis"
+        if head[:5] == b"\x7fFLAC":
+            return "Ogg FLAC"
         return "Ogg Opus" if head == b"OpusHead" else "Ogg"
     for magic, name in _UNDECODED:
         if data.startswith(magic):
@@ -731,7 +768,7 @@ def container_name(data: bytes) -> Optional[str]:
 _DECODERS = {"WAV": decode_wav, "AU": decode_au, "AIFF": decode_aiff, "Ogg Vorbis": decode_vorbis, "MP3": decode_mp3,
              "MPEG audio Layer II": decode_mp3, "MPEG audio Layer I": decode_mp3, "AAC (ADTS)": decode_aac_adts,
              "MP4/M4A": decode_mp4}
-DECODED = "FLAC, Ogg Vorbis, MP3 / MPEG audio (MPEG-1 / 2 / 2.5 Layers I, II, III), AAC-LC / ALAC (M4A / MP4), AAC (ADTS), WAV / " \
+DECODED = "FLAC (native, Ogg), Ogg Vorbis, MP3 / MPEG audio (MPEG-1 / 2 / 2.5 Layers I, II, III), AAC-LC / ALAC (M4A / MP4), AAC (ADTS), WAV / " \
           "RIFX / RF64 (PCM, float, A-law, mu-law, IMA / MS ADPCM, MPEG), AU, AIFF / AIFF-C"
 
 
@@ -740,8 +777,8 @@ def decode_bytes(data: bytes, sr_out: int = TARGET_SR, device=None) -> np.ndarra
     if name in _DECODERS:
         x, sr = _DECODERS[name](data)
         return resample(x.mean(axis=1) if x.shape[1] > 1 else x[:, 0], sr, sr_out, device)
-    if name == "FLAC":
-        fl = decode_flac(data)
+    if name in ("FLAC", "Ogg FLAC"):
+        fl = decode_flac(data if name == "FLAC" else ogg_flac_to_native(data))
         scale = 2.0 ** -(fl.bits_per_sample - 1)  # ffmpeg's s16/s32 -> flt conversion of the coded samples
         return resample_device(fl.pcm, fl.sample_rate, sr_out, scale=scale, device=device).cpu().numpy()
     if name is None:
@@ -798,8 +835,8 @@ def duration_seconds(path: str) -> float:
     if name in _DECODERS:
         x, sr = _DECODERS[name](data)
         return x.shape[0] / float(sr)
-    if name == "FLAC":
-        info = flac_probe(data)
+    if name in ("FLAC", "Ogg FLAC"):
+        info = flac_probe(data if name == "FLAC" else ogg_flac_to_native(data))
         return int(info.total_samples) / float(info.sample_rate)
     raise ValueError("duration: unsupported container")
 
