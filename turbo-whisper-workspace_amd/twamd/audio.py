@@ -277,12 +277,78 @@ def _esds_config(data: bytes, a: int, b: int) -> Tuple[int, bytes]:
     return oti, cfg
 
 
+def _fragment_samples(data: bytes, moov: Tuple[int, int], trak_a: int, trak_b: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Fragmented MP4 (what browsers' MediaRecorder and live writers produce): the byte offset and size of every sample
+    of this track in the file's moof / traf / trun boxes (ISO/IEC 14496-12 8.8, as ffmpeg's mov demuxer reads them):
+    sizes from trun, else tfhd's default, else the track's trex default; offsets from the base data offset (tfhd's
+    explicit one, the moof start under default-base-is-moof or for a moof's first traf, else where the previous
+    traf's data ended) plus trun's data offset, samples contiguous after it."""
+    tid = None
+    for t, a, b in _mp4_boxes(data, trak_a, trak_b):
+        if t == b"tkhd":
+            tid = struct.unpack(">I", data[a + (20 if data[a] == 1 else 12): a + (24 if data[a] == 1 else 16)])[0]
+    trex_size = 0
+    for t, a, b in _mp4_boxes(data, *moov):
+        if t == b"mvex":
+            for tt, aa, bb in _mp4_boxes(data, a, b):
+                if tt == b"trex" and struct.unpack(">I", data[aa + 4: aa + 8])[0] == tid:
+                    trex_size = struct.unpack(">I", data[aa + 16: aa + 20])[0]
+    offs: List[int] = []
+    sizes: List[int] = []
+    for t, ma, mb in _mp4_boxes(data, 0, len(data)):
+        if t != b"moof":
+            continue
+        moof_start, prev_end = ma - 8, None
+        for tt, ta, tb in _mp4_boxes(data, ma, mb):
+            if tt != b"traf":
+                continue
+            base, dflt_size, this_track = None, trex_size, False
+            for t3, a3, b3 in _mp4_boxes(data, ta, tb):
+                if t3 == b"tfhd":
+                    fl = int.from_bytes(data[a3 + 1: a3 + 4], "big")
+                    this_track = struct.unpack(">I", data[a3 + 4: a3 + 8])[0] == tid
+                    q = a3 + 8
+                    if fl & 0x01:
+                        base = struct.unpack(">Q", data[q: q + 8])[0]
+                        q += 8
+                    q += 4 * bool(fl & 0x02) + 4 * bool(fl & 0x08)
+                    if fl & 0x10:
+                        dflt_size = struct.unpack(">I", data[q: q + 4])[0]
+                    if base is None:
+                        base = moof_start if (fl & 0x20000 or prev_end is None) else prev_end
+                elif t3 == b"trun":
+                    fl = int.from_bytes(data[a3 + 1: a3 + 4], "big")
+                    n = struct.unpack(">I", data[a3 + 4: a3 + 8])[0]
+                    q = a3 + 8
+                    pos = base if base is not None else moof_start
+                    if fl & 0x01:
+                        pos = base + struct.unpack(">i", data[q: q + 4])[0]
+                        q += 4
+                    elif prev_end is not None:
+                        pos = prev_end
+                    q += 4 * bool(fl & 0x04)
+                    per = 4 * (bool(fl & 0x100) + bool(fl & 0x200) + bool(fl & 0x400) + bool(fl & 0x800))
+                    for i in range(n):
+                        rec = q + i * per
+                        sz = dflt_size
+                        if fl & 0x200:
+                            sz = struct.unpack(">I", data[rec + 4 * bool(fl & 0x100): rec + 4 * bool(fl & 0x100) + 4])[0]
+                        if this_track:
+                            offs.append(pos)
+                            sizes.append(sz)
+                        pos += sz
+                    prev_end = pos
+    return np.array(offs, np.int64), np.array(sizes, np.int64)
+
+
 def mp4_audio_track(data: bytes) -> Mp4Track:
     """The first sound track of an MP4 / M4A / MOV file: its codec configuration, the file offset and size of every
-    access unit (stsz, stsc, stco / co64) and its first edit (elst), as ffmpeg's mov demuxer reads them."""
+    access unit (stsz, stsc, stco / co64, then any moof fragments) and its first edit (elst), as ffmpeg's mov demuxer
+    reads them."""
     moov = next(((a, b) for t, a, b in _mp4_boxes(data, 0, len(data)) if t == b"moov"), None)
     if moov is None:
-        raise ValueError("MP4: no moov box" + (" (fragmented MP4 is not supported)" if b"moof" in data[:4096] else ""))
+        raise ValueError("MP4: no moov box" + (" (fragments without their initialization segment)" if b"moof" in
+                                               data[:4096] else ""))
     movie_ts = 1000
     for t, a, b in _mp4_boxes(data, *moov):
         if t == b"mvhd":
@@ -353,6 +419,11 @@ def mp4_audio_track(data: bytes) -> Mp4Track:
         first_in_chunk = np.concatenate([[0], np.cumsum(per_chunk)[:-1]])[chunk_of]
         csum = np.concatenate([[0], np.cumsum(sizes)])
         offsets = chunks[chunk_of] + csum[np.arange(count)] - csum[first_in_chunk]
+        if b"trex" in box or any(t == b"mvex" for t, _, _ in _mp4_boxes(data, *moov)):
+            extra_off, extra_siz = _fragment_samples(data, moov, a, b)
+            offsets = np.concatenate([offsets, extra_off])
+            sizes = np.concatenate([sizes, extra_siz])
+            count = len(sizes)
         if count and int((offsets + sizes).max()) > len(data):
             raise ValueError("MP4: an access unit lies beyond the end of the file (truncated upload)")
         edit = None
@@ -416,7 +487,7 @@ def decode_mp4(data: bytes, threads: int = 0) -> Tuple[np.ndarray, int]:
     if tr.edit is not None:
         scale = sr / tr.timescale
         skip, keep = int(round(tr.edit[0] * scale)), int(round(tr.edit[1] * scale))
-        x = x[skip: skip + keep]
+        x = x[skip: skip + keep] if keep else x[skip:]  # (a zero-length edit, as fragmented files write: to the end)
     return x, sr
 
 
