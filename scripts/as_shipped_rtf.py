@@ -22,12 +22,15 @@ ap.add_argument("--minutes", type=float, default=10.0)
 ap.add_argument("--model", default="large-v3-turbo", help="large-v3: the reference's own default model "
                 "(vocalis/core/audio_pipeline.py:171), the turbo encoder with a 32-layer decoder")
 ap.add_argument("--fused", type=int, default=0)
+ap.add_argument("--modes", default="as_shipped_beam5,greedy", help="which calls to time (comma-separated)")
 a = ap.parse_args()
 tr = TurboTranscriber.from_pretrained(a.model, seed=1234, fused_decode=bool(a.fused))
 audio = np.concatenate([speech_like(60.0, 500 + i) for i in range(int(a.minutes))]).astype(np.float32)
 kw = dict(chunk_length_s=60, stride_length_s=5, batch_size=32, return_timestamps=True)
 out = {}
 for name, gk in (("as_shipped_beam5", {"task": "transcribe"}), ("greedy", {"task": "transcribe", "num_beams": 1})):
+    if name not in a.modes.split(","):
+        continue
     tr(audio, generate_kwargs=dict(gk), **kw)  # warm-up (graph captures, buffers)
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -32,6 +32,17 @@ __device__ inline void lse_merge(float& m, float& s, float m2, float s2) {
   else s = s + s2 * __expf(m2 - m);
 }
 
+// lse_merge(m, s, x, 1) without branches (per logit in the beam partials): d = x - m; x above m rescales s by
+// exp(m - x) = exp(-|d|) and adds 1, otherwise s gains exp(d) = exp(-|d|) — the same exp argument and the same
+// arithmetic as lse_merge in every case (an -inf x adds exp(-inf) = 0; a first finite x over m = -inf gives
+// s * 0 + 1), so the result is bit-identical
+__device__ inline void lse_add1(float& m, float& s, float x) {
+  const float d = x - m;
+  const float e = (x == -INFINITY) ? 0.f : __expf(-fabsf(d));
+  s = (d > 0.f) ? s * e + 1.f : s + e;
+  m = fmaxf(m, x);
+}
+
 // Partial record of one vocab chunk of one row (8 words).
 struct SelPart {
   float bt_v; int bt_i;   // best text (or mode-1) candidate
@@ -555,7 +566,9 @@ struct Cand {
   float v;
   int i;
 };
-__device__ inline bool cand_better(float v, int i, const Cand& c) { return v > c.v || (v == c.v && i < c.i); }
+// (bitwise, not short-circuit: the || / && form compiled to exec-mask branches around every compare, which set the
+// beam kernels' time)
+__device__ inline bool cand_better(float v, int i, const Cand& c) { return (v > c.v) | ((v == c.v) & (i < c.i)); }
 
 // Sorted insert as a compare-swap chain: every index is static, so the list stays in VGPRs (the shifting form with
 // an early return was lowered to scratch: 80-272 B/lane, k_beam_partial 139 us per step at 60 rows).
@@ -572,22 +585,49 @@ __device__ inline void cand_insert(Cand (&L)[K], float v, int i) {
   }
 }
 
+// The wave's best (v, i, l) under the strict order "v higher, then i lower, then lane l lower", in every lane. DPP
+// within each 16-lane row (quad xor 1, xor 2, half-row mirror, row mirror: every lane of a row meets every other),
+// then the four rows' winners by readlane: ~4x shorter than a 6-level ds_bpermute butterfly (__shfl_xor), whose
+// latency chain set most of the beam kernels' time (K dependent rounds per list; k_beam_step 22 of 34 us). The order
+// is total, so the winner (and every later round) is the one the butterfly found.
+__device__ inline void wave_best(float& bv, int& bi, int& bl) {
+  auto step = [&](auto ctrl_tag) {
+    constexpr int ctrl = decltype(ctrl_tag)::value;
+    const float ov = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(bv), ctrl, 0xF, 0xF, false));
+    const int oi = __builtin_amdgcn_update_dpp(0, bi, ctrl, 0xF, 0xF, false);
+    const int ol = __builtin_amdgcn_update_dpp(0, bl, ctrl, 0xF, 0xF, false);
+    const bool b = (ov > bv) | ((ov == bv) & ((oi < bi) | ((oi == bi) & (ol < bl))));
+    bv = b ? ov : bv;
+    bi = b ? oi : bi;
+    bl = b ? ol : bl;
+  };
+  step(std::integral_constant<int, 0xB1>{});   // quad_perm [1, 0, 3, 2]
+  step(std::integral_constant<int, 0x4E>{});   // quad_perm [2, 3, 0, 1]
+  step(std::integral_constant<int, 0x141>{});  // row_half_mirror
+  step(std::integral_constant<int, 0x140>{});  // row_mirror
+  float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bv), 0));
+  int i = __builtin_amdgcn_readlane(bi, 0), l = __builtin_amdgcn_readlane(bl, 0);
+#pragma unroll
+  for (int r = 16; r < 64; r += 16) {
+    const float ov = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bv), r));
+    const int oi = __builtin_amdgcn_readlane(bi, r), ol = __builtin_amdgcn_readlane(bl, r);
+    const bool b = (ov > v) | ((ov == v) & ((oi < i) | ((oi == i) & (ol < l))));
+    v = b ? ov : v;
+    i = b ? oi : i;
+    l = b ? ol : l;
+  }
+  bv = v;
+  bi = i;
+  bl = l;
+}
+
 // K rounds of wave argmax over the lanes' sorted lists: out (LDS, K entries) = the wave's top-K, descending.
 template <int K>
 __device__ inline void wave_topk(Cand (&L)[K], Cand* out, int lane) {
   for (int r = 0; r < K; ++r) {
     float bv = L[0].v;
     int bi = L[0].i, bl = lane;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(bi, o, 64), ol = __shfl_xor(bl, o, 64);
-      if (ov > bv || (ov == bv && (oi < bi || (oi == bi && ol < bl)))) {
-        bv = ov;
-        bi = oi;
-        bl = ol;
-      }
-    }
+    wave_best(bv, bi, bl);
     if (lane == 0) out[r] = Cand{bv, bi};
     const bool pop = lane == bl;  // pop the head (selects, not a branch around register moves)
 #pragma unroll
@@ -604,12 +644,26 @@ struct BeamPart {
   float m_tx, s_tx;  // (renorm) log-sum-exp of the allowed text tokens
 };
 
+// -DTW_BEAM_PROBE (measurement builds only, never the product library): per-phase timestamps of block 0 of the two
+// beam kernels (100 MHz s_memrealtime, thread 0), read back with tw_beam_probe_read
+#ifdef TW_BEAM_PROBE
+__device__ unsigned long long tw_beam_probe_ts[2][16];
+#define BPROBE(k, slot) \
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) tw_beam_probe_ts[k][slot] = __builtin_amdgcn_s_memrealtime()
+extern "C" int tw_beam_probe_read(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(tw_beam_probe_ts), sizeof(tw_beam_probe_ts)) == hipSuccess ? 0 : 1;
+}
+#else
+#define BPROBE(k, slot)
+#endif
+
 template <int K>
 __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ logits, int ld_logits,
                                                       const uint32_t* __restrict__ suppress_bits, TwSelectParams p,
                                                       const int* __restrict__ state, BeamPart<K>* __restrict__ ws,
                                                       int renorm) {
   TW_DEC_PRIO();
+  BPROBE(0, 0);
   __shared__ Cand wl[2][4][K];
   __shared__ float wst[4][6];
   const int b = blockIdx.x, c = blockIdx.y, NC = gridDim.y;
@@ -627,7 +681,7 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
   for (int j = 0; j < K; ++j) T[j] = S[j] = Cand{-INFINITY, 0x7fffffff};
   float m_all = -INFINITY, s_all = 0.f, m_ts = -INFINITY, s_ts = 0.f, m_tx = -INFINITY, s_tx = 0.f;
   auto visit = [&](int v, float x, uint32_t sbw) {
-    lse_merge(m_all, s_all, x, 1.f);
+    lse_add1(m_all, s_all, x);
     bool masked = (sbw >> (v & 31)) & 1u;
     if (rm.init_step)
       for (int i = 0; i < p.n_begin_suppress; ++i) masked |= (v == p.begin_suppress[i]);
@@ -643,10 +697,10 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
     if (masked) return;
     if (v < tsb || !p.use_timestamps) {
       cand_insert<K>(T, x, v);
-      if (renorm) lse_merge(m_tx, s_tx, x, 1.f);
+      if (renorm) lse_add1(m_tx, s_tx, x);
     } else {
       cand_insert<K>(S, x, v);
-      lse_merge(m_ts, s_ts, x, 1.f);
+      lse_add1(m_ts, s_ts, x);
     }
   };
   // every logit (and suppress word) of this thread's share in flight at once: one load per loop trip serialised ~13
@@ -666,6 +720,7 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
     if (v < v1) visit(v, xs[u], sb[u]);
   }
   for (int v = v0 + tid + 256 * BP_MAXE; v < v1; v += 256) visit(v, row[v], suppress_bits ? suppress_bits[v >> 5] : 0u);
+  BPROBE(0, 1);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     float m2 = __shfl_xor(m_all, o, 64), s2 = __shfl_xor(s_all, o, 64);
@@ -683,8 +738,10 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
   // wholly inside them no text candidate: that list's K dependent argmax rounds (here and in the merge below) are
   // skipped, uniformly per block (each round is a 6-level shuffle chain: the reductions were ~20 us of 55)
   const bool any_ts = p.use_timestamps && v1 > tsb, any_tx = !p.use_timestamps || v0 < tsb;
+  BPROBE(0, 2);
   if (any_tx) wave_topk<K>(T, wl[0][wid], lane);
   if (any_ts) wave_topk<K>(S, wl[1][wid], lane);
+  BPROBE(0, 3);
   if (lane == 0) {
     wst[wid][0] = m_all;
     wst[wid][1] = s_all;
@@ -704,25 +761,19 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
       }
       continue;
     }
-    Cand mine = lane < 4 * K ? wl[l][lane / K][lane % K] : Cand{-INFINITY, 0x7fffffff};
-    bool used = false;
-    for (int r = 0; r < K; ++r) {
-      float bv = used ? -INFINITY : mine.v;
-      int bi = used ? 0x7fffffff : mine.i, bl = lane;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(bv, o, 64);
-        const int oi = __shfl_xor(bi, o, 64), ol = __shfl_xor(bl, o, 64);
-        if (ov > bv || (ov == bv && (oi < bi || (oi == bi && ol < bl)))) {
-          bv = ov;
-          bi = oi;
-          bl = ol;
-        }
+    // the block's top-K of the 4 waves' lists by rank (each of the 4K entries counts the entries ahead of it under
+    // the rounds' order, position breaking ties): one pass over 4K LDS broadcasts instead of K argmax rounds
+    if (lane < 4 * K) {
+      const Cand* all = &wl[l][0][0];
+      const Cand mine = all[lane];
+      int rank = 0;
+      for (int e = 0; e < 4 * K; ++e) {
+        const Cand o = all[e];
+        rank += (o.v > mine.v) | ((o.v == mine.v) & ((o.i < mine.i) | ((o.i == mine.i) & (e < lane))));
       }
-      if (lane == bl) used = true;
-      if (lane == 0) {
-        if (l == 0) out->t[r] = Cand{bv, bi};
-        else out->s[r] = Cand{bv, bi};
+      if (rank < K) {
+        if (l == 0) out->t[rank] = mine;
+        else out->s[rank] = mine;
       }
     }
   }
@@ -740,6 +791,7 @@ __global__ __launch_bounds__(256) void k_beam_partial(const float* __restrict__ 
     out->m_tx = mx;
     out->s_tx = sx;
   }
+  BPROBE(0, 4);
 }
 
 #define TW_BEAM_MAXNB 8
@@ -751,6 +803,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
                                                    int* __restrict__ tokens, int* __restrict__ ids,
                                                    int* __restrict__ pos) {
   TW_DEC_PRIO();
+  BPROBE(1, 0);
   __shared__ Cand rc[TW_BEAM_MAXNB][K];  // row candidates: accumulated log-prob, token
   __shared__ int old_tok[TW_BEAM_MAXNB][TW_BEAM_MAXT];
   __shared__ int old_fin[TW_BEAM_MAXNB][TW_BEAM_MAXT];
@@ -796,6 +849,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
   const int st_v = tid < nb * TW_STATE_STRIDE ? state[(w * nb) * TW_STATE_STRIDE + tid] : 0;
   const int fl_v = tid < nb ? bs.fin_len[w * nb + tid] : 0;
   const int ps_v = tid < nb ? pos[w * nb + tid] : 0;
+  BPROBE(1, 1);
 
   // 1. per row (one wave each): merge the chunk records, apply the timestamp rule, score the candidates
   if (wid < nb) {
@@ -820,9 +874,14 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
         lse_merge(m_tx, s_tx, m2, s2);
       }
     }
-    // top-K of the text list and of the timestamp list over the NC chunk lists (<= 4 entries per lane)
+    BPROBE(1, 8);
+    // top-K of the text list and of the timestamp list over the NC chunk lists (<= 4 entries per lane). With the
+    // timestamp split of k_beam_partial every timestamp candidate sits in the last chunk's (sorted) list and every
+    // other chunk's list is empty: that list is the merge's result as it stands
     Cand(*top)[K] = tops[wid];
-    for (int l = 0; l < 2; ++l) {
+    const bool split_ts = p.use_timestamps && p.ts_begin > 0 && p.ts_begin < p.V && NC > 1;
+    if (split_ts && lane < K) top[1][lane] = parts[NC - 1].s[lane];
+    for (int l = 0; l < (split_ts ? 1 : 2); ++l) {
       Cand mine[4];
       bool used[4];
 #pragma unroll
@@ -835,27 +894,19 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
         float bv = -INFINITY;
         int bi = 0x7fffffff, bq = -1;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (!used[q] && cand_better(mine[q].v, mine[q].i, Cand{bv, bi})) {
-            bv = mine[q].v;
-            bi = mine[q].i;
-            bq = q;
-          }
-        int bl = lane;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          const float ov = __shfl_xor(bv, o, 64);
-          const int oi = __shfl_xor(bi, o, 64), ol = __shfl_xor(bl, o, 64);
-          if (ov > bv || (ov == bv && (oi < bi || (oi == bi && ol < bl)))) {
-            bv = ov;
-            bi = oi;
-            bl = ol;
-          }
+        for (int q = 0; q < 4; ++q) {
+          const bool b = !used[q] & cand_better(mine[q].v, mine[q].i, Cand{bv, bi});
+          bv = b ? mine[q].v : bv;
+          bi = b ? mine[q].i : bi;
+          bq = b ? q : bq;
         }
+        int bl = lane;
+        wave_best(bv, bi, bl);
 #pragma unroll
         for (int q = 0; q < 4; ++q) used[q] = used[q] || (lane == bl && bq == q);
         if (lane == 0) top[l][r] = Cand{bv, bi};
       }
+      BPROBE(1, 9 + l);
     }
     if (lane == 0) {  // lane 0 wrote top
       const float lse_all = m_all + __logf(s_all);
@@ -886,6 +937,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
       }
     }
   }
+  BPROBE(1, 11);
   // stage the old running histories, finished histories and processor states of the window
 #pragma unroll
   for (int u = 0; u < STG; ++u) {
@@ -902,7 +954,9 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
     old_flen[tid] = fl_v;
     old_pos[tid] = ps_v;
   }
+  BPROBE(1, 2);
   __syncthreads();
+  BPROBE(1, 3);
 
   // 2. the window's beam bookkeeping. Each selection below is a stable top-n; it is computed as ranks, every
   // candidate counting the candidates ahead of it (LDS broadcast reads), instead of n sequential argmax rounds in
@@ -928,6 +982,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
     }
   }
   __syncthreads();
+  BPROBE(1, 4);
   const int unsat_prev = win[0];
   const float lp_div = __powf((float)(t + 1), bp.length_penalty);
   if (tid < K) {
@@ -990,6 +1045,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
     win[2] = t + 1;
   }
   __syncthreads();
+  BPROBE(1, 5);
 
   // 3. apply: running histories, state, ids, pos, the K/V source rows; finished histories
   for (int e = tid; e < nb * (t + 1); e += blockDim.x) {
@@ -1051,6 +1107,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
       bs.fin_lp[row] = f_lp[j];
     }
   }
+  BPROBE(1, 6);
 }
 
 template <int K>
