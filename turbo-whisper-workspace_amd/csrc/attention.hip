@@ -767,9 +767,7 @@ __device__ inline void dec_attend_off(const float* qf /*[64] f32 in LDS*/, const
       float d = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
-      d += __shfl_xor(d, 1, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 4, 64);
+      d = lane8_sum(d);
       const int key = (it0 + u) * 32 + g;
       if (gl == 0 && key < nkeys) sc[key] = d;
     }
@@ -932,9 +930,7 @@ __global__ TW_DEC_LB(256, 4) void k_attn_decode_self2(const bf16_t* __restrict__
     float d = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
-    d += __shfl_xor(d, 1, 64);
-    d += __shfl_xor(d, 2, 64);
-    d += __shfl_xor(d, 4, 64);
+    d = lane8_sum(d);
     p[u] = key <= t && key >= ks ? d : -INFINITY;
     mx = fmaxf(mx, p[u]);
   }
@@ -1183,9 +1179,7 @@ __global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_lean(const bf16_t* __re
       const bf16_t* ke = (const bf16_t*)&kk[u];
 #pragma unroll
       for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
-      d += __shfl_xor(d, 1, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 4, 64);
+      d = lane8_sum(d);
       sv[u] = (it0 + u) * NG + g < S ? d : -INFINITY;
       bm = fmaxf(bm, sv[u]);
     }
@@ -1309,9 +1303,7 @@ __global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_grp(const bf16_t* __res
         const bf16_t* ke = (const bf16_t*)&kk[u];
 #pragma unroll
         for (int e = 0; e < 8; ++e) d += qv[j][e] * bf16_to_f32(ke[e]);
-        d += __shfl_xor(d, 1, 64);
-        d += __shfl_xor(d, 2, 64);
-        d += __shfl_xor(d, 4, 64);
+        d = lane8_sum(d);
         sv[u] = k0 + (it0 + u) * NG + g < k1 ? d : -INFINITY;
         bm = fmaxf(bm, sv[u]);
       }

@@ -309,9 +309,7 @@ __device__ __forceinline__ void attend(const bf16_t* qb, size_t q_off, const bf1
       const bf16_t* ke = (const bf16_t*)&kk[u];
 #pragma unroll
       for (int e = 0; e < 8; ++e) d += qv[e] * bf16_to_f32(ke[e]);
-      d += __shfl_xor(d, 1, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 4, 64);
+      d = lane8_sum(d);
       sv[u] = (it0 + u) * NG + g < nk ? d : -INFINITY;
       bm = fmaxf(bm, sv[u]);
     }

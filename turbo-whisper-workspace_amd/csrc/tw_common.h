@@ -84,6 +84,17 @@ __device__ inline float4 gelu_erf4(float4 v) {
 }
 
 // ---- wave reductions (64 lanes) ----------------------------------------------------------------
+// Sum over each aligned group of 8 lanes, in every lane of the group: DPP quad_perm xor 1, xor 2, then the half-row
+// mirror (lane i with 7 - i, the other quad). Bit-identical to `d += __shfl_xor(d, 1); ... 2; ... 4` (after the two
+// quad steps every lane of a quad holds the same bits, and a + b == b + a), without the three ds_bpermute round trips
+// through the LDS crossbar per dot product (the decoder attentions' key loops issue one per key per row).
+__device__ __forceinline__ float lane8_sum(float d) {
+  d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0xB1, 0xF, 0xF, false));
+  d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x4E, 0xF, 0xF, false));
+  d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x141, 0xF, 0xF, false));
+  return d;
+}
+
 __device__ inline float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
