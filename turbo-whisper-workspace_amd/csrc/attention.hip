@@ -1237,7 +1237,8 @@ __global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_lean(const bf16_t* __re
 // k_attn_decode_cross_grp: the lean kernel for G rows that read the SAME encoder slot (the beams of one window): each
 // key/value row is loaded once for all G queries (num_beams x less cross K/V traffic: the beam-5 step's largest
 // kernel streamed 60 x 20 x 384 KB per layer for 12 distinct windows). One group per block would leave most CUs idle
-// (20 heads x 7 groups per 32-row view; measured slower than the lean kernel), so the keys are also split NSPLIT
+// (20 heads x 7 groups per 32-row view; measured slower than the lean kernel), so either the block is 512 threads
+// (NG = 64 key groups, NSPLIT = 1, the normalised output written here; <= 5 rows) or the keys are also split NSPLIT
 // ways (flash-decoding): grid (H, nblk, NSPLIT), each block writes its rows' unnormalised state (max, sum, 64 sums)
 // to ws and k_attn_cross_merge combines the NSPLIT states. Per row and key slice the arithmetic is the lean
 // kernel's (NG key groups, UNR blocks, the same merges).
@@ -1250,7 +1251,7 @@ template <int G, int NG = 32, int UNR = DA_UNR>
 __global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_grp(const bf16_t* __restrict__ q, int D, int S, int Bt, int R,
                                                                int first, const int* __restrict__ row_map,
                                                                const bf16_t* __restrict__ ckv,
-                                                               float* __restrict__ ws) {
+                                                               float* __restrict__ ws, bf16_t* __restrict__ out) {
   TW_DEC_PRIO();
   constexpr int NWV = NG / 8;
   __shared__ float wpart[NWV][G][64];
@@ -1359,6 +1360,10 @@ __global__ TW_DEC_LB(NG * 8, 1) void k_attn_decode_cross_grp(const bf16_t* __res
       tot += wt * wml[w][j][1];
       v += wt * wpart[w][j][c];
     }
+    if (NS == 1) {  // the whole key range in this block: the row's output directly (no merge launch)
+      out[(size_t)(r_lo + j) * D + h * 64 + c] = f32_to_bf16(v / tot);
+      continue;
+    }
     float* rec = ws + (((size_t)(r_lo + j) * H + h) * NS + z) * 66;
     rec[2 + c] = v;
     if (c == 0) {
@@ -1399,19 +1404,35 @@ extern "C" int tw_attn_decode_cross_grouped(const bf16_t* q, int B, int H, int S
              "tw_attn_decode_cross_grouped: group=%d first=%d (2 <= group <= 8, 0 <= first < group)", group, first);
   const int f = min(first, B);
   const int nblk = (f > 0 ? 1 : 0) + (B - f + group - 1) / group;
-  const dim3 grid(H, nblk, DA_XSPLIT), blk(256);
   hipStream_t s = (hipStream_t)stream;
   const int D = H * 64;
-  switch (group) {
-    case 2: hipLaunchKernelGGL((k_attn_decode_cross_grp<2>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
-    case 3: hipLaunchKernelGGL((k_attn_decode_cross_grp<3>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
-    case 4: hipLaunchKernelGGL((k_attn_decode_cross_grp<4>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
-    case 5: hipLaunchKernelGGL((k_attn_decode_cross_grp<5>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
-    case 6: hipLaunchKernelGGL((k_attn_decode_cross_grp<6>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
-    case 7: hipLaunchKernelGGL((k_attn_decode_cross_grp<7>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
-    default: hipLaunchKernelGGL((k_attn_decode_cross_grp<8>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, cross_kv, ws); break;
+  if (group <= 5) {
+    // up to 5 rows per group (the pipeline's beam-5): one 512-thread block per (head, group) over all keys writes the
+    // output itself — 240 blocks of 8 waves resident at once, no second round and no merge launch: the as-shipped
+    // beam-5 call 0.540 -> 0.519 s on one box (profiles/r06gd_cross_grp_direct_ab.txt). 6-8 rows would spill at
+    // 512 threads (256 VGPRs): they keep the 3-way key split + merge.
+    const dim3 grid(H, nblk, 1), blk(512);
+#define DA_GRP(GG) hipLaunchKernelGGL((k_attn_decode_cross_grp<GG, 64>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, \
+                                      cross_kv, ws, out)
+    switch (group) {
+      case 2: DA_GRP(2); break;
+      case 3: DA_GRP(3); break;
+      case 4: DA_GRP(4); break;
+      default: DA_GRP(5); break;
+    }
+#undef DA_GRP
+  } else {
+    const dim3 grid(H, nblk, DA_XSPLIT), blk(256);
+#define DA_GRP(GG) hipLaunchKernelGGL((k_attn_decode_cross_grp<GG>), grid, blk, 0, s, q, D, S, Bt, B, f, row_map, \
+                                      cross_kv, ws, out)
+    switch (group) {
+      case 6: DA_GRP(6); break;
+      case 7: DA_GRP(7); break;
+      default: DA_GRP(8); break;
+    }
+#undef DA_GRP
+    hipLaunchKernelGGL(k_attn_cross_merge, dim3(H, B), dim3(64), 0, s, ws, DA_XSPLIT, D, out);
   }
-  hipLaunchKernelGGL(k_attn_cross_merge, dim3(H, B), dim3(64), 0, s, ws, DA_XSPLIT, D, out);
   return tw_check_launch("tw_attn_decode_cross_grouped");
 }
 
