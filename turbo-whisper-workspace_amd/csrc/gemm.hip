@@ -1772,6 +1772,16 @@ static void launch_gemv_p2(const bf16_t* A, int lda, const bf16_t* Wp, int M, in
   // non-temporal weight loads (its MALL residency is what the decoder's layer weights would lose)
   const bool wide = N >= tw_gemv_nt_min_n;
   if (wide) {
+    if constexpr (EPI == TW_EPI_F32) {
+      // 33..64 rows (beam-5 passes, config 5's windows): two column groups per wave (k_gemv_pc) halve the activation
+      // fragments each weight byte costs — at four m-tiles k_gemv_p's waves read 4 KiB of L2-resident activations per
+      // 1 KiB weight fragment; one K-slice per group, the MFMA order per output unchanged (bit-identical logits).
+      // As-shipped beam-5 call 0.518 -> 0.513 s (profiles/r06pc_proj_out_pc_ab.txt)
+      if (M > 32 && tw_gemv_wide_kw == 1) {
+        launch_gemv_pc<EPI, 1, APACK, 5, true>(A, lda, Wp, M, N, K, ea, splits, s);
+        return;
+      }
+    }
     if (tw_gemv_wide_kw == 4 && steps >= 8 * 4) launch_gemv_p3<EPI, 4, 8, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
     else if (tw_gemv_wide_kw >= 2 && steps >= 8 * 2) launch_gemv_p3<EPI, 2, 8, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
     else launch_gemv_p3<EPI, 1, 16, APACK, true>(A, lda, Wp, M, N, K, ea, splits, s);
