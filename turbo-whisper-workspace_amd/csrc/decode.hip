@@ -972,7 +972,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
       const int j2 = e / K, k2 = e - j2 * K;
       const float v2 = rc[j2][k2].v;
       const long f2 = (long)j2 * p.V + rc[j2][k2].i;
-      rank += (v2 > v || (v2 == v && (f2 < f || (f2 == f && e < tid)))) ? 1 : 0;
+      rank += (v2 > v) | ((v2 == v) & ((f2 < f) | ((f2 == f) & (e < tid))));  // (bitwise: no branches)
     }
     if (rank < K) {
       c_beam[rank] = j;
@@ -1009,7 +1009,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
   if (tid < K) {
     const int c = tid;
     int rank = 0;
-    for (int c2 = 0; c2 < K; ++c2) rank += (rsc[c2] > rsc[c] || (rsc[c2] == rsc[c] && c2 < c)) ? 1 : 0;
+    for (int c2 = 0; c2 < K; ++c2) rank += (rsc[c2] > rsc[c]) | ((rsc[c2] == rsc[c]) & (c2 < c));
     if (rank < nb) {
       s_src[rank] = c_beam[c];
       s_tok[rank] = c_tok[c];
@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(512) void k_beam_step(const BeamPart<K>* __restrict
   if (tid >= 64 && tid < 64 + nb + K) {
     const int e = tid - 64;
     int rank = 0;
-    for (int e2 = 0; e2 < nb + K; ++e2) rank += (merged[e2] > merged[e] || (merged[e2] == merged[e] && e2 < e)) ? 1 : 0;
+    for (int e2 = 0; e2 < nb + K; ++e2) rank += (merged[e2] > merged[e]) | ((merged[e2] == merged[e]) & (e2 < e));
     if (rank < nb) {
       f_from[rank] = e;
       f_score[rank] = merged[e];
